@@ -1,0 +1,192 @@
+// ORACLE — test infrastructure only. This library is loaded by tests/, by
+// __graft_entry__.smoke() and by bench.py's cpu_baseline leg as the CHECKER /
+// CPU baseline; it is never part of the product path (kyverno_amd / libkpe).
+//
+// C ABI over the CPU restatement (oracle/*.hpp) of the reference's validate path.
+#include <atomic>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "engine.hpp"
+
+using namespace oracle;
+
+namespace {
+thread_local std::string g_err;
+
+std::vector<std::pair<const char*, size_t>> split_lines(const char* buf, size_t len) {
+  std::vector<std::pair<const char*, size_t>> out;
+  size_t i = 0;
+  while (i < len) {
+    size_t j = i;
+    while (j < len && buf[j] != '\n') ++j;
+    size_t a = i, b = j;
+    while (a < b && (buf[a] == ' ' || buf[a] == '\t' || buf[a] == '\r')) ++a;
+    while (b > a && (buf[b - 1] == ' ' || buf[b - 1] == '\t' || buf[b - 1] == '\r')) --b;
+    if (b > a) out.emplace_back(buf + a, b - a);
+    i = j + 1;
+  }
+  return out;
+}
+
+std::vector<Policy> load_policies(const char* json) {
+  JPtr arr = parse_json(json);
+  std::vector<Policy> ps;
+  if (arr->t == JT::Arr) {
+    for (auto& p : arr->a) ps.push_back(compile_policy(*p));
+  } else {
+    ps.push_back(compile_policy(*arr));
+  }
+  return ps;
+}
+}  // namespace
+
+extern "C" {
+
+const char* oracle_last_error() { return g_err.c_str(); }
+
+int oracle_wildcard_match(const char* pattern, const char* text) { return wildcard_match(pattern, text) ? 1 : 0; }
+
+// pkg/pss/evaluate_test.go:13-59 driver: decode pod + PodSecurity rule, ParseVersion, EvaluatePod.
+// Returns 1 allowed, 0 denied, -1 decode/version error.
+int oracle_pss_evaluate(const char* rule_json, const char* pod_json) {
+  try {
+    JPtr rule = parse_json(rule_json);
+    JPtr podj = parse_json(pod_json);
+    Pod pod = get_spec(*podj, "Pod");
+    Version v;
+    if (!parse_version(jstr(rule->get("version")), &v)) return -1;
+    std::string lvl = jstr(rule->get("level"));
+    LevelVersion lv{lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged),
+                    v};
+    std::vector<PSSExclude> ex;
+    const JVal* e = rule->get("exclude");
+    if (e && e->t == JT::Arr)
+      for (auto& x : e->a)
+        ex.push_back({jstr(x->get("controlName")), jstrlist(x->get("images")), jstr(x->get("restrictedField")),
+                      jstrlist(x->get("values"))});
+    return evaluate_pod(lv, ex, pod) ? 1 : 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  } catch (const DecodeError& de) {
+    g_err = de.msg;
+    return -1;
+  }
+}
+
+// Failing check IDs (comma separated, evaluation order) for one pod, no exclusions.
+int oracle_pss_failing_checks(const char* level, const char* version, const char* pod_json, char* buf, size_t cap) {
+  try {
+    JPtr podj = parse_json(pod_json);
+    Pod pod = get_spec(*podj, "Pod");
+    Version v;
+    if (!parse_version(version, &v)) return -1;
+    std::string lvl = level;
+    LevelVersion lv{lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged),
+                    v};
+    std::string s;
+    for (auto& r : evaluate_pss(lv, pod)) s += (s.empty() ? "" : ",") + r.id;
+    snprintf(buf, cap, "%s", s.c_str());
+    return 0;
+  } catch (...) {
+    return -1;
+  }
+}
+
+// Number of rules after autogen for a JSON array of policies; names written
+// newline-separated into buf as "<policy>/<rule>".
+int oracle_rule_names(const char* policies_json, char* buf, size_t cap) {
+  try {
+    auto ps = load_policies(policies_json);
+    std::string s;
+    int n = 0;
+    for (auto& p : ps)
+      for (auto& r : p.rules) {
+        s += p.name + "/" + r.name + "\n";
+        ++n;
+      }
+    if (buf && cap) snprintf(buf, cap, "%s", s.c_str());
+    return n;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// Verdict matrix for NDJSON resources x rules(after autogen) of all policies.
+//   ns_labels_json: {"<namespace>": {"k": "v"}, ...} or NULL.
+//   out: N x R bytes (row-major), values in oracle::Status.
+// Returns N (number of resources) or -1.
+long oracle_validate(const char* policies_json, const char* ndjson, size_t len, const char* ns_labels_json,
+                     uint8_t* out, size_t out_cap, int nthreads) {
+  try {
+    auto ps = load_policies(policies_json);
+    size_t R = 0;
+    for (auto& p : ps) R += p.rules.size();
+    std::vector<std::pair<std::string, Labels>> nsl;
+    if (ns_labels_json && *ns_labels_json) {
+      JPtr m = parse_json(ns_labels_json);
+      for (auto& kv : m->o) {
+        Labels l;
+        for (auto& x : kv.second->o) l.emplace_back(x.first, jstr(x.second.get()));
+        nsl.emplace_back(kv.first, l);
+      }
+    }
+    auto lines = split_lines(ndjson, len);
+    size_t N = lines.size();
+    if (N * R > out_cap) {
+      g_err = "output buffer too small";
+      return -1;
+    }
+    if (nthreads < 1) nthreads = 1;
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    std::string bad_msg;
+    static const Labels empty;
+    auto work = [&]() {
+      std::vector<uint8_t> row;
+      while (true) {
+        size_t i = next.fetch_add(64);
+        if (i >= N) break;
+        size_t e = std::min(N, i + 64);
+        for (; i < e; ++i) {
+          JPtr res;
+          try {
+            res = parse_json(std::string(lines[i].first, lines[i].second));
+          } catch (const std::exception& ex) {
+            bad = true;
+            continue;
+          }
+          Unstructured u{res.get()};
+          std::string ns = u.ns();
+          const Labels* l = &empty;
+          for (auto& kv : nsl)
+            if (kv.first == ns) l = &kv.second;
+          size_t col = 0;
+          for (auto& p : ps) {
+            validate(p, *res, *l, row);
+            memcpy(out + i * R + col, row.data(), row.size());
+            col += row.size();
+          }
+        }
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+    work();
+    for (auto& t : th) t.join();
+    if (bad) {
+      g_err = "malformed resource JSON";
+      return -1;
+    }
+    return (long)N;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,76 @@
+"""ctypes binding to oracle/build/liboracle.so — the CPU restatement used as the
+checker by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg only."""
+import ctypes
+import json
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "build", "liboracle.so")
+
+STATUS = {0: "na", 1: "pass", 2: "fail", 3: "warn", 4: "error", 5: "skip", 7: "unsupported"}
+
+
+class Oracle:
+    def __init__(self, path=LIB):
+        self.lib = L = ctypes.CDLL(path)
+        L.oracle_last_error.restype = ctypes.c_char_p
+        L.oracle_wildcard_match.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_pss_evaluate.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_pss_failing_checks.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                                ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_rule_names.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                                      ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.oracle_validate.restype = ctypes.c_long
+
+    def wildcard(self, pattern, text):
+        return bool(self.lib.oracle_wildcard_match(pattern.encode(), text.encode()))
+
+    def pss_evaluate(self, rule, pod):
+        return self.lib.oracle_pss_evaluate(json.dumps(rule).encode(), json.dumps(pod).encode())
+
+    def failing_checks(self, level, version, pod):
+        buf = ctypes.create_string_buffer(4096)
+        r = self.lib.oracle_pss_failing_checks(level.encode(), version.encode(), json.dumps(pod).encode(), buf, 4096)
+        if r < 0:
+            return None
+        s = buf.value.decode()
+        return s.split(",") if s else []
+
+    def rule_names(self, policies):
+        buf = ctypes.create_string_buffer(1 << 20)
+        n = self.lib.oracle_rule_names(json.dumps(policies).encode(), buf, 1 << 20)
+        if n < 0:
+            raise RuntimeError(self.lib.oracle_last_error().decode())
+        return buf.value.decode().splitlines()
+
+    def validate(self, policies, ndjson: bytes, ns_labels=None, nthreads=1):
+        """Verdict matrix (N x R uint8, oracle status codes) for NDJSON resources."""
+        R = len(self.rule_names(policies))
+        N = ndjson.count(b"\n") + 1
+        out = np.zeros(max(N * R, 1), dtype=np.uint8)
+        pj = json.dumps(policies).encode()
+        nl = json.dumps(ns_labels).encode() if ns_labels else None
+        n = self.lib.oracle_validate(pj, ndjson, len(ndjson), nl, out.ctypes.data, out.size, nthreads)
+        if n < 0:
+            raise RuntimeError(self.lib.oracle_last_error().decode())
+        return out[: n * R].reshape(n, R)
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle")])
+
+
+_inst = None
+
+
+def load():
+    global _inst
+    if _inst is None:
+        if not os.path.exists(LIB):
+            build()
+        _inst = Oracle()
+    return _inst
