@@ -1,0 +1,139 @@
+/*
+ * kpe — MI355X-native batch policy evaluation for Kyverno's validate path.
+ *
+ * C-ABI drop-in boundary (plain pointers and sizes; no C++/torch types).
+ * The reference has no FFI: these entry points are what a cgo shim behind
+ * Kyverno's engine interfaces binds:
+ *
+ *   engineapi.Engine.Validate(ctx, PolicyContext) EngineResponse
+ *       pkg/engine/api/engine.go:17-23, implemented by engine.Validate
+ *       pkg/engine/engine.go:87-101 (rule loop pkg/engine/validation.go:16-80)
+ *     -> kpe_evaluate() answers every (resource, rule) cell of a batch at once;
+ *        the Go shim slices one row per PolicyContext.
+ *   handlers.Handler.Process (validatePssHandler)
+ *       pkg/engine/handlers/handler.go:13-23,
+ *       pkg/engine/handlers/validation/validate_pss.go:31-112
+ *     -> PSS rules of the compiled program (kpe_check_masks gives the failing
+ *        PSA check IDs that become PodSecurityChecks / report "controls").
+ *   autogen.ComputeRules  pkg/autogen/autogen.go:236-270
+ *     -> kpe_program_compile() runs autogen once, at compile time.
+ *   callers: cmd/cli/kubectl-kyverno/processor/policy_processor.go:168-179
+ *            (kyverno apply loop) and pkg/controllers/report/utils/scanner.go:99-110
+ *            (background scan) build one PolicyContext per (resource, policy);
+ *            kpe_corpus_flatten() + kpe_evaluate() replace that loop for a batch.
+ *
+ * Verdict cell alphabet (engineapi.RuleStatus, pkg/engine/api/rulestatus.go:4-21;
+ * "no RuleResponse" = not applicable):
+ */
+#ifndef KPE_H_
+#define KPE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum kpe_verdict {
+  KPE_NA = 0,    /* rule did not match the resource: no RuleResponse      */
+  KPE_PASS = 1,  /* RuleStatusPass                                         */
+  KPE_FAIL = 2,  /* RuleStatusFail                                         */
+  KPE_WARN = 3,  /* RuleStatusWarn (reserved; never produced by validate)  */
+  KPE_ERROR = 4, /* RuleStatusError (e.g. typed decode failure in getSpec) */
+  KPE_SKIP = 5   /* RuleStatusSkip                                         */
+};
+
+/* Library status codes (0 = OK). Library-level failures set kpe_last_error(). */
+typedef int kpe_status;
+enum {
+  KPE_OK = 0,
+  KPE_E_INVALID = 1,     /* malformed input (policy / resource JSON)             */
+  KPE_E_UNSUPPORTED = 2, /* policy uses a construct this engine does not evaluate */
+  KPE_E_DEVICE = 3,      /* HIP runtime error / no device / kernel not loadable   */
+  KPE_E_LIMIT = 4,       /* a corpus exceeds a documented encoding limit          */
+  KPE_E_STATE = 5        /* wrong call order (e.g. corpus not uploaded)           */
+};
+
+typedef struct kpe_device kpe_device;   /* one HIP device + stream               */
+typedef struct kpe_program kpe_program; /* compiled policy set (after autogen)    */
+typedef struct kpe_corpus kpe_corpus;   /* flattened, string-interned resources   */
+
+/* Per-rule totals over a batch (pkg/engine/api/policyresponse.go:10-21 counting,
+ * cmd/cli/kubectl-kyverno/processor/result.go:34-68 summary line). */
+typedef struct kpe_counts {
+  uint64_t na, pass, fail, warn, error, skip;
+} kpe_counts;
+
+/* Thread-local message for the last failing call on this thread. */
+const char* kpe_last_error(void);
+const char* kpe_version(void);
+
+/* ---- device ------------------------------------------------------------ */
+kpe_status kpe_device_open(int ordinal, kpe_device** out);
+void kpe_device_close(kpe_device* dev);
+
+/* ---- policies ---------------------------------------------------------- */
+/* policies_json: one ClusterPolicy/Policy object or a JSON array of them
+ * (kyverno.io/v1 schema, api/kyverno/v1/spec_types.go:240-284). Autogen is
+ * applied (autogen.ComputeRules). Rules are laid out policy-major, in
+ * ComputeRules order: column r of the verdict matrix is rule r. */
+kpe_status kpe_program_compile(const char* policies_json, size_t len, kpe_program** out);
+int kpe_program_num_rules(const kpe_program* prog);
+/* "<policy-name>/<rule-name>" of rule r (owned by prog). */
+const char* kpe_program_rule_name(const kpe_program* prog, int r);
+/* 1 if rule r is a podSecurity rule (check masks are meaningful for it). */
+int kpe_program_rule_is_pss(const kpe_program* prog, int r);
+void kpe_program_free(kpe_program* prog);
+
+/* ---- resources --------------------------------------------------------- */
+/* ndjson: one resource JSON object per line. ns_labels_json: optional
+ * {"<namespace>": {"k": "v", ...}, ...} (the namespace label table the
+ * reference reads per resource: PolicyContext.NamespaceLabels). */
+kpe_status kpe_corpus_flatten(const char* ndjson, size_t len, const char* ns_labels_json, size_t ns_len,
+                              kpe_corpus** out);
+int64_t kpe_corpus_num_resources(const kpe_corpus* c);
+/* Host bytes of the columnar encoding (what one evaluation may read). */
+int64_t kpe_corpus_bytes(const kpe_corpus* c);
+/* Copy the columns to device memory (HBM). Evaluation requires this. */
+kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* c);
+void kpe_corpus_free(kpe_corpus* c);
+
+/* ---- evaluation -------------------------------------------------------- */
+/* Evaluate every (resource, rule) cell on the device and copy results back.
+ *   verdicts    : N x R bytes (row-major, kpe_verdict), may be NULL
+ *   check_masks : N x R uint32 (bit k = PSA check k failed, kpe_pss_check_id
+ *                 order; 0 for non-PSS rules), may be NULL
+ *   counts      : R entries, may be NULL
+ * Synchronous. Safe to call from several OS threads on distinct devices; calls
+ * on one device are serialised by a per-device mutex. */
+kpe_status kpe_evaluate(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
+                        uint32_t* check_masks, kpe_counts* counts);
+
+/* Asynchronous form for pipelines/benchmarks: enqueue one evaluation on the
+ * device stream; results stay in device buffers owned by the corpus. No host
+ * synchronisation. Use kpe_device_sync() and kpe_fetch() afterwards. */
+kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c);
+kpe_status kpe_device_sync(kpe_device* dev);
+kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
+                     uint32_t* check_masks, kpe_counts* counts);
+
+/* PSA check id k (bit k of a check mask), e.g. "capabilities_restricted". */
+const char* kpe_pss_check_id(int k);
+int kpe_pss_num_checks(void);
+
+/* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
+typedef struct kpe_kernel_stats {
+  uint64_t launches;        /* evaluations timed since the last reset           */
+  double pss_kernel_ms;     /* summed duration of the resource-scan kernel      */
+  double dict_kernel_ms;    /* summed duration of the dictionary predicate pass */
+  double scan_bytes;        /* algorithmic bytes one scan-kernel launch reads+writes */
+} kpe_kernel_stats;
+kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);
+kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c,
+                                   kpe_kernel_stats* out, int reset);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KPE_H_ */

@@ -1,0 +1,34 @@
+/*
+ * Synthetic corpus generator (benchmark / test utility, not part of the
+ * evaluation boundary). Produces NDJSON resources shaped like SURVEY.md §8(d):
+ *   C2: Pods with 1-4 containers (p=.7/.2/.07/.03), 0-1 initContainers (p=.8/.2),
+ *       ~60% restricted-compliant (docs/perf-testing/main.go:201-246 template),
+ *       ~40% with 1-3 violations drawn uniformly from the 17 PSA checks, fields
+ *       present or absent at p=0.5, namespaces ns-0000..ns-0999, images from
+ *       50 names x {latest, semver}.
+ * Deterministic in (seed, first_index): row i of a corpus depends only on
+ * (seed, first_index + i), so shards of one logical corpus can be generated
+ * independently per rank.
+ */
+#ifndef KPE_SYNTH_H_
+#define KPE_SYNTH_H_
+#include <stddef.h>
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum kpe_synth_mix {
+  KPE_SYNTH_PODS = 0,   /* C2: Pods only                                      */
+  KPE_SYNTH_MIXED = 1,  /* Pods, Deployments, DaemonSets, Jobs, CronJobs, Services, ConfigMaps */
+  KPE_SYNTH_EDGE = 2    /* MIXED + edge cases: nulls, windows pods, type errors, odd values */
+};
+
+/* Generate n resources as NDJSON into a malloc'd buffer (*out, *len). Free with kpe_synth_free. */
+int kpe_synth_resources(uint64_t seed, int64_t first_index, int64_t n, int mix, char** out, size_t* len);
+void kpe_synth_free(char* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

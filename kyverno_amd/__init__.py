@@ -1,0 +1,35 @@
+"""kyverno_amd — MI355X-native batch evaluation of Kyverno validate rules.
+
+The product path is libkpe.so (include/kpe.h): a C++ flattener/compiler plus
+CDNA4 HIP kernels. This package is the Python host binding over that C-ABI
+(ctypes) and a thin mirror of the reference's engine interface
+(pkg/engine/api/engine.go:17-56) for batch callers. There is no CPU fallback:
+evaluation without a working gfx950 device raises KpeError.
+"""
+from ._lib import KpeError, lib_path, load  # noqa: F401
+from .engine import (  # noqa: F401
+    Corpus,
+    Device,
+    Engine,
+    EngineResponse,
+    PolicyContext,
+    PolicySet,
+    RuleResponse,
+    RuleStatus,
+    synth_resources,
+)
+
+__all__ = [
+    "Corpus",
+    "Device",
+    "Engine",
+    "EngineResponse",
+    "KpeError",
+    "PolicyContext",
+    "PolicySet",
+    "RuleResponse",
+    "RuleStatus",
+    "synth_resources",
+    "load",
+    "lib_path",
+]

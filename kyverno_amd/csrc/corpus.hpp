@@ -1,0 +1,64 @@
+// Host-side columnar corpus: string dictionaries + SoA columns (see schema.h).
+#pragma once
+#include <cstdint>
+#include <string>
+#include <string_view>
+#include <unordered_map>
+#include <vector>
+
+#include "schema.h"
+
+namespace kpe {
+
+struct Dict {
+  std::unordered_map<std::string, uint32_t> map;
+  std::vector<char> bytes;
+  std::vector<uint32_t> off{0};
+  uint32_t intern(std::string_view s) {
+    auto it = map.find(std::string(s));
+    if (it != map.end()) return it->second;
+    uint32_t id = (uint32_t)(off.size() - 1);
+    map.emplace(std::string(s), id);
+    bytes.insert(bytes.end(), s.begin(), s.end());
+    off.push_back((uint32_t)bytes.size());
+    return id;
+  }
+  int64_t find(std::string_view s) const {
+    auto it = map.find(std::string(s));
+    return it == map.end() ? -1 : (int64_t)it->second;
+  }
+  uint32_t size() const { return (uint32_t)(off.size() - 1); }
+  std::string_view at(uint32_t i) const { return std::string_view(bytes.data() + off[i], off[i + 1] - off[i]); }
+};
+
+struct DeviceCorpus;  // defined in kpe_api.cpp
+
+struct Corpus {
+  int64_t n = 0;
+  Dict dict[KPE_NUM_DOMAINS];
+  // ---- resource rows (unstructured view, used by match/exclude) ----
+  std::vector<uint32_t> r_flags, r_gvk, r_name, r_mns, r_nsa, r_nsl;
+  std::vector<uint32_t> lab_off{0}, lab_k, lab_v;  // metadata.labels CSR
+  std::vector<uint32_t> ann_off{0}, ann_k, ann_v;  // metadata.annotations CSR
+  // ---- PSS pod view (typed decode of getSpec) ----
+  std::vector<uint32_t> p_sc;
+  std::vector<uint32_t> ctr_off{0};
+  std::vector<uint32_t> vol_off{0}, vol_src;
+  std::vector<uint32_t> sys_off{0}, sys_id;
+  std::vector<uint32_t> pann_off{0}, pann_k, pann_v;  // pod-template metadata annotations
+  // ---- containers (visit order: initContainers, containers, ephemeralContainers) ----
+  std::vector<uint32_t> c_sc;
+  std::vector<uint64_t> c_add, c_drop;
+  std::vector<uint32_t> c_name, c_image, c_sann;
+  std::vector<uint32_t> c_sec_str, c_pm_str, c_selt_str, c_selu_str, c_selr_str;  // cold (D_MISC)
+  std::vector<uint32_t> cport_off{0};
+  std::vector<int32_t> cport_host;  // cold: hostPort of every port
+  // ---- namespace label table (PolicyContext.NamespaceLabels) ----
+  std::vector<uint32_t> nsl_off{0}, nsl_k, nsl_v;
+  std::unordered_map<std::string, uint32_t> nsl_index;
+
+  DeviceCorpus* dev = nullptr;
+  int64_t bytes() const;
+};
+
+}  // namespace kpe

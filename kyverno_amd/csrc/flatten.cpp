@@ -1,0 +1,1098 @@
+// Corpus flattener: NDJSON resources -> columnar, string-interned tables.
+//
+// Two views of every resource are extracted in one walk:
+//  * the unstructured view the match path reads (unstructured.GetKind/GetName/
+//    GetNamespace/GetLabels/GetAnnotations; pkg/engine/utils/match.go:52-160);
+//  * the typed pod view the PSS handler reads after
+//    getSpec (pkg/engine/handlers/validation/validate_pss.go:137-188):
+//    encoding/json.Unmarshal into corev1.Pod / appsv1.Deployment / batchv1.CronJob.
+//    Keys match case-insensitively, null is a no-op, unknown keys are ignored and
+//    any type mismatch in a modelled field marks the row R_DECODE_ERR (=> the
+//    reference's RuleError). The modelled field set is listed in DESIGN.md.
+// The flattener only ENCODES (dictionary ids, enum codes, presence bits); every
+// predicate is evaluated on the device.
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "corpus.hpp"
+#include "jscan.hpp"
+
+namespace kpe {
+
+namespace {
+
+struct CtrView {
+  std::string name, image;
+  bool sc = false;
+  uint32_t priv = TRI_UNSET, ape = TRI_UNSET, rnr = TRI_UNSET, rau = RAU_UNSET, whp = TRI_UNSET;
+  bool caps = false;
+  std::vector<std::string> add, drop;
+  bool sec = false;
+  std::string sec_type;
+  bool pm = false;
+  std::string pm_val;
+  bool sel = false;
+  std::string sel_type, sel_user, sel_role;
+  std::vector<int32_t> hostports;
+  void reset() { *this = CtrView(); }
+};
+
+struct PodView {
+  bool hostnet = false, hostpid = false, hostipc = false;
+  bool sc = false;
+  uint32_t rnr = TRI_UNSET, rau = RAU_UNSET, whp = TRI_UNSET;
+  bool sec = false;
+  std::string sec_type;
+  bool sel = false;
+  std::string sel_type, sel_user, sel_role;
+  bool os = false;
+  std::string os_name;
+  std::vector<std::string> sysctls;
+  std::vector<uint32_t> vols;
+  std::vector<CtrView> ctr[3];  // init, containers, ephemeral
+  std::vector<std::pair<std::string, std::string>> ann;  // typed metadata annotations (map: unique keys)
+  void reset() {
+    hostnet = hostpid = hostipc = sc = sec = sel = os = false;
+    rnr = TRI_UNSET;
+    rau = RAU_UNSET;
+    whp = TRI_UNSET;
+    sec_type.clear();
+    sel_type.clear();
+    sel_user.clear();
+    sel_role.clear();
+    os_name.clear();
+    sysctls.clear();
+    vols.clear();
+    for (auto& c : ctr) c.clear();
+    ann.clear();
+  }
+};
+
+struct UView {  // unstructured metadata view
+  std::string kind, api_version, name, generate_name, ns;
+  bool labels_ok = true, ann_ok = true;
+  std::vector<std::pair<std::string, std::string>> labels, ann;
+  void reset() {
+    kind.clear();
+    api_version.clear();
+    name.clear();
+    generate_name.clear();
+    ns.clear();
+    labels_ok = ann_ok = true;
+    labels.clear();
+    ann.clear();
+  }
+};
+
+static const char* const kVolSrc[KPE_NUM_VOLUME_SOURCES] = {
+    "hostpath", "emptydir", "gcepersistentdisk", "awselasticblockstore", "gitrepo", "secret", "nfs",
+    "iscsi", "glusterfs", "persistentvolumeclaim", "rbd", "flexvolume", "cinder", "cephfs", "flocker",
+    "downwardapi", "fc", "azurefile", "configmap", "vspherevolume", "quobyte", "azuredisk",
+    "photonpersistentdisk", "projected", "portworxvolume", "scaleio", "storageos", "csi", "ephemeral"};
+
+// Typed decoder: walks a JSON value with the schema of a K8s Go type. `err` is
+// sticky (json.Unmarshal returns the first UnmarshalTypeError).
+class Typed {
+ public:
+  explicit Typed(JCur& c) : c_(c) {}
+  bool err = false;
+
+  // ---- leaves ----
+  void str(std::string* out) {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Str) {
+      bad();
+      return;
+    }
+    std::string_view v;
+    c_.str(&v, vs_);
+    if (out) out->assign(v.data(), v.size());
+  }
+  void strp(bool* set, std::string* out) {  // *string
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Str) {
+      bad();
+      return;
+    }
+    std::string_view v;
+    c_.str(&v, vs_);
+    if (set) *set = true;
+    if (out) out->assign(v.data(), v.size());
+  }
+  void boolean(bool* out) {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Bool) {
+      bad();
+      return;
+    }
+    bool b = false;
+    c_.boolean(&b);
+    if (out) *out = b;
+  }
+  void tri(uint32_t* out) {  // *bool
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Bool) {
+      bad();
+      return;
+    }
+    bool b = false;
+    c_.boolean(&b);
+    if (out) *out = b ? TRI_TRUE : TRI_FALSE;
+  }
+  bool integer(int64_t lo, int64_t hi, int64_t* out) {  // returns true if a value was set
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return false;
+    }
+    if (k != JK::Num) {
+      bad();
+      return false;
+    }
+    JNum n;
+    c_.number(&n);
+    int64_t x;
+    if (!n.integral(&x) || x < lo || x > hi) {
+      bad();
+      return false;
+    }
+    if (out) *out = x;
+    return true;
+  }
+  void i32() { integer(INT32_MIN, INT32_MAX, nullptr); }
+  void i64() { integer(INT64_MIN, INT64_MAX, nullptr); }
+  void strlist(std::vector<std::string>* out) {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      if (out) out->clear();
+      return;
+    }
+    if (k != JK::Arr) {
+      bad();
+      return;
+    }
+    if (out) out->clear();
+    c_.arr_begin();
+    bool f = true;
+    while (c_.arr_next(f)) {
+      std::string s;
+      str(out ? &s : nullptr);
+      if (out) out->push_back(std::move(s));
+    }
+  }
+  void i64list() {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Arr) {
+      bad();
+      return;
+    }
+    c_.arr_begin();
+    bool f = true;
+    while (c_.arr_next(f)) i64();
+  }
+  void strmap(std::vector<std::pair<std::string, std::string>>* out) {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      if (out) out->clear();
+      return;
+    }
+    if (k != JK::Obj) {
+      bad();
+      return;
+    }
+    if (out) out->clear();
+    c_.obj_begin();
+    bool f = true;
+    std::string_view key;
+    while (c_.obj_next(f, &key, ks_)) {
+      std::string kk(key);
+      std::string v;
+      str(out ? &v : nullptr);
+      if (out) {
+        bool rep = false;
+        for (auto& e : *out)
+          if (e.first == kk) {
+            e.second = v;
+            rep = true;
+          }
+        if (!rep) out->emplace_back(std::move(kk), std::move(v));
+      }
+    }
+  }
+  void timev() {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Str) {
+      bad();
+      return;
+    }
+    std::string_view v;
+    c_.str(&v, vs_);
+    if (!rfc3339(v)) err = true;
+  }
+  void anyobj() {  // an opaque struct: must be an object (or null)
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Obj) {
+      bad();
+      return;
+    }
+    c_.skip();
+  }
+
+  // Iterate an object's keys; fn(key) must consume the value (return false => skip it).
+  template <class F>
+  void obj(F fn) {
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (k != JK::Obj) {
+      bad();
+      return;
+    }
+    c_.obj_begin();
+    bool f = true;
+    std::string_view key;
+    std::string kscratch;
+    while (c_.obj_next(f, &key, kscratch)) {
+      std::string kk(key);  // stable copy (nested parsing reuses scratch buffers)
+      if (!fn(std::string_view(kk))) c_.skip();
+    }
+  }
+  template <class F>
+  bool arr(F fn) {  // returns false if null (caller clears)
+    JK k = c_.peek();
+    if (k == JK::Null) {
+      c_.null();
+      return false;
+    }
+    if (k != JK::Arr) {
+      bad();
+      return true;
+    }
+    c_.arr_begin();
+    bool f = true;
+    while (c_.arr_next(f)) fn();
+    return true;
+  }
+
+  // ---- K8s types ----
+  void object_meta(std::vector<std::pair<std::string, std::string>>* ann) {
+    obj([&](std::string_view k) {
+      if (keq(k, "name") || keq(k, "generatename") || keq(k, "namespace") || keq(k, "uid") ||
+          keq(k, "resourceversion") || keq(k, "selflink"))
+        str(nullptr);
+      else if (keq(k, "generation")) i64();
+      else if (keq(k, "creationtimestamp") || keq(k, "deletiontimestamp")) timev();
+      else if (keq(k, "labels")) strmap(nullptr);
+      else if (keq(k, "annotations")) strmap(ann);
+      else if (keq(k, "finalizers")) strlist(nullptr);
+      else return false;
+      return true;
+    });
+  }
+  void selinux(bool* set, std::string* type, std::string* user, std::string* role) {
+    if (c_.peek() == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (c_.peek() == JK::Obj) *set = true;
+    obj([&](std::string_view k) {
+      if (keq(k, "user")) str(user);
+      else if (keq(k, "role")) str(role);
+      else if (keq(k, "type")) str(type);
+      else if (keq(k, "level")) str(nullptr);
+      else return false;
+      return true;
+    });
+  }
+  void seccomp(bool* set, std::string* type) {
+    if (c_.peek() == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (c_.peek() == JK::Obj) *set = true;
+    obj([&](std::string_view k) {
+      if (keq(k, "type")) str(type);
+      else if (keq(k, "localhostprofile")) strp(nullptr, nullptr);
+      else return false;
+      return true;
+    });
+  }
+  void apparmor() {
+    obj([&](std::string_view k) {
+      if (keq(k, "type")) str(nullptr);
+      else if (keq(k, "localhostprofile")) strp(nullptr, nullptr);
+      else return false;
+      return true;
+    });
+  }
+  void winopts(uint32_t* hp) {
+    obj([&](std::string_view k) {
+      if (keq(k, "hostprocess")) tri(hp);
+      else if (keq(k, "gmsacredentialspecname") || keq(k, "gmsacredentialspec") || keq(k, "runasusername"))
+        strp(nullptr, nullptr);
+      else return false;
+      return true;
+    });
+  }
+  void security_context(CtrView& c) {
+    if (c_.peek() == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (c_.peek() == JK::Obj) c.sc = true;
+    obj([&](std::string_view k) {
+      if (keq(k, "capabilities")) {
+        if (c_.peek() == JK::Null) {
+          c_.null();
+          return true;
+        }
+        if (c_.peek() == JK::Obj) c.caps = true;
+        obj([&](std::string_view k2) {
+          if (keq(k2, "add")) strlist(&c.add);
+          else if (keq(k2, "drop")) strlist(&c.drop);
+          else return false;
+          return true;
+        });
+      } else if (keq(k, "privileged")) tri(&c.priv);
+      else if (keq(k, "selinuxoptions")) selinux(&c.sel, &c.sel_type, &c.sel_user, &c.sel_role);
+      else if (keq(k, "windowsoptions")) winopts(&c.whp);
+      else if (keq(k, "runasuser")) {
+        int64_t v;
+        if (integer(INT64_MIN, INT64_MAX, &v)) c.rau = v == 0 ? RAU_ZERO : RAU_NONZERO;
+      } else if (keq(k, "runasgroup")) i64();
+      else if (keq(k, "runasnonroot")) tri(&c.rnr);
+      else if (keq(k, "readonlyrootfilesystem")) tri(nullptr);
+      else if (keq(k, "allowprivilegeescalation")) tri(&c.ape);
+      else if (keq(k, "procmount")) strp(&c.pm, &c.pm_val);
+      else if (keq(k, "seccompprofile")) seccomp(&c.sec, &c.sec_type);
+      else if (keq(k, "apparmorprofile")) apparmor();
+      else return false;
+      return true;
+    });
+  }
+  void pod_security_context(PodView& p) {
+    if (c_.peek() == JK::Null) {
+      c_.null();
+      return;
+    }
+    if (c_.peek() == JK::Obj) p.sc = true;
+    obj([&](std::string_view k) {
+      if (keq(k, "selinuxoptions")) selinux(&p.sel, &p.sel_type, &p.sel_user, &p.sel_role);
+      else if (keq(k, "windowsoptions")) winopts(&p.whp);
+      else if (keq(k, "runasuser")) {
+        int64_t v;
+        if (integer(INT64_MIN, INT64_MAX, &v)) p.rau = v == 0 ? RAU_ZERO : RAU_NONZERO;
+      } else if (keq(k, "runasgroup") || keq(k, "fsgroup")) i64();
+      else if (keq(k, "runasnonroot")) tri(&p.rnr);
+      else if (keq(k, "supplementalgroups")) i64list();
+      else if (keq(k, "fsgroupchangepolicy")) strp(nullptr, nullptr);
+      else if (keq(k, "seccompprofile")) seccomp(&p.sec, &p.sec_type);
+      else if (keq(k, "apparmorprofile")) apparmor();
+      else if (keq(k, "sysctls")) {
+        std::vector<std::string> names;
+        bool notnull = arr([&]() {
+          std::string nm;
+          if (c_.peek() == JK::Null) c_.null();
+          else
+            obj([&](std::string_view k2) {
+              if (keq(k2, "name")) str(&nm);
+              else if (keq(k2, "value")) str(nullptr);
+              else return false;
+              return true;
+            });
+          names.push_back(nm);
+        });
+        p.sysctls = notnull ? names : std::vector<std::string>();
+      } else return false;
+      return true;
+    });
+  }
+  void container(CtrView& c) {
+    if (c_.peek() == JK::Null) {
+      c_.null();
+      return;
+    }
+    obj([&](std::string_view k) {
+      if (keq(k, "name")) str(&c.name);
+      else if (keq(k, "image")) str(&c.image);
+      else if (keq(k, "command") || keq(k, "args")) strlist(nullptr);
+      else if (keq(k, "workingdir") || keq(k, "imagepullpolicy") || keq(k, "terminationmessagepath") ||
+               keq(k, "terminationmessagepolicy") || keq(k, "targetcontainername"))
+        str(nullptr);
+      else if (keq(k, "stdin") || keq(k, "stdinonce") || keq(k, "tty")) boolean(nullptr);
+      else if (keq(k, "ports")) {
+        std::vector<int32_t> hp;
+        bool notnull = arr([&]() {
+          int64_t h = 0;
+          if (c_.peek() == JK::Null) c_.null();
+          else
+            obj([&](std::string_view k2) {
+              if (keq(k2, "hostport")) integer(INT32_MIN, INT32_MAX, &h);
+              else if (keq(k2, "containerport")) i32();
+              else if (keq(k2, "name") || keq(k2, "protocol") || keq(k2, "hostip")) str(nullptr);
+              else return false;
+              return true;
+            });
+          hp.push_back((int32_t)h);
+        });
+        c.hostports = notnull ? hp : std::vector<int32_t>();
+      } else if (keq(k, "env")) {
+        arr([&]() {
+          if (c_.peek() == JK::Null) {
+            c_.null();
+            return;
+          }
+          obj([&](std::string_view k2) {
+            if (keq(k2, "name") || keq(k2, "value")) str(nullptr);
+            else if (keq(k2, "valuefrom")) anyobj();
+            else return false;
+            return true;
+          });
+        });
+      } else if (keq(k, "resources")) anyobj();
+      else if (keq(k, "securitycontext")) security_context(c);
+      else return false;
+      return true;
+    });
+  }
+  void containers(std::vector<CtrView>& out) {
+    std::vector<CtrView> v;
+    bool notnull = arr([&]() {
+      CtrView c;
+      container(c);
+      v.push_back(std::move(c));
+    });
+    out = notnull ? std::move(v) : std::vector<CtrView>();
+  }
+  void volumes(std::vector<uint32_t>& out) {
+    std::vector<uint32_t> v;
+    bool notnull = arr([&]() {
+      uint32_t src = 0;
+      if (c_.peek() == JK::Null) c_.null();
+      else
+        obj([&](std::string_view k) {
+          if (keq(k, "name")) {
+            str(nullptr);
+            return true;
+          }
+          for (int i = 0; i < KPE_NUM_VOLUME_SOURCES; ++i) {
+            if (keq(k, kVolSrc[i])) {
+              JK t = c_.peek();
+              if (t == JK::Null) {
+                c_.null();
+                src &= ~(1u << i);
+                return true;
+              }
+              if (t != JK::Obj) {
+                bad();
+                return true;
+              }
+              src |= 1u << i;
+              obj([&](std::string_view k2) {
+                if (keq(k2, "path") || keq(k2, "secretname") || keq(k2, "claimname") || keq(k2, "medium") ||
+                    keq(k2, "server"))
+                  str(nullptr);
+                else if (keq(k2, "defaultmode")) i32();
+                else if (keq(k2, "readonly")) boolean(nullptr);
+                else return false;
+                return true;
+              });
+              return true;
+            }
+          }
+          return false;
+        });
+      v.push_back(src);
+    });
+    out = notnull ? std::move(v) : std::vector<uint32_t>();
+  }
+  void pod_spec(PodView& p) {
+    obj([&](std::string_view k) {
+      if (keq(k, "volumes")) volumes(p.vols);
+      else if (keq(k, "initcontainers")) containers(p.ctr[0]);
+      else if (keq(k, "containers")) containers(p.ctr[1]);
+      else if (keq(k, "ephemeralcontainers")) containers(p.ctr[2]);
+      else if (keq(k, "hostnetwork")) boolean(&p.hostnet);
+      else if (keq(k, "hostpid")) boolean(&p.hostpid);
+      else if (keq(k, "hostipc")) boolean(&p.hostipc);
+      else if (keq(k, "securitycontext")) pod_security_context(p);
+      else if (keq(k, "os")) {
+        if (c_.peek() == JK::Null) {
+          c_.null();
+          return true;
+        }
+        if (c_.peek() == JK::Obj) p.os = true;
+        obj([&](std::string_view k2) {
+          if (keq(k2, "name")) str(&p.os_name);
+          else return false;
+          return true;
+        });
+      } else if (keq(k, "restartpolicy") || keq(k, "dnspolicy") || keq(k, "serviceaccountname") ||
+                 keq(k, "serviceaccount") || keq(k, "nodename") || keq(k, "hostname") || keq(k, "subdomain") ||
+                 keq(k, "priorityclassname") || keq(k, "schedulername"))
+        str(nullptr);
+      else if (keq(k, "terminationgraceperiodseconds") || keq(k, "activedeadlineseconds")) i64();
+      else if (keq(k, "priority")) i32();
+      else if (keq(k, "automountserviceaccounttoken") || keq(k, "shareprocessnamespace") || keq(k, "hostusers") ||
+               keq(k, "enableservicelinks"))
+        tri(nullptr);
+      else if (keq(k, "runtimeclassname")) strp(nullptr, nullptr);
+      else if (keq(k, "nodeselector")) strmap(nullptr);
+      else return false;
+      return true;
+    });
+  }
+  void label_selector() {
+    obj([&](std::string_view k) {
+      if (keq(k, "matchlabels")) strmap(nullptr);
+      else if (keq(k, "matchexpressions")) {
+        arr([&]() {
+          if (c_.peek() == JK::Null) {
+            c_.null();
+            return;
+          }
+          obj([&](std::string_view k2) {
+            if (keq(k2, "key") || keq(k2, "operator")) str(nullptr);
+            else if (keq(k2, "values")) strlist(nullptr);
+            else return false;
+            return true;
+          });
+        });
+      } else return false;
+      return true;
+    });
+  }
+  // PodTemplateSpec; `meta_ann` receives template annotations when non-null.
+  void pod_template(PodView& p, bool take_meta) {
+    obj([&](std::string_view k) {
+      if (keq(k, "metadata")) object_meta(take_meta ? &p.ann : nullptr);
+      else if (keq(k, "spec")) pod_spec(p);
+      else return false;
+      return true;
+    });
+  }
+
+  static bool rfc3339(std::string_view s) {
+    auto d = [&](size_t i) { return i < s.size() && s[i] >= '0' && s[i] <= '9'; };
+    if (s.size() < 20) return false;
+    for (size_t i : {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18})
+      if (!d(i)) return false;
+    if (s[4] != '-' || s[7] != '-' || (s[10] != 'T' && s[10] != 't') || s[13] != ':' || s[16] != ':') return false;
+    size_t i = 19;
+    if (i < s.size() && s[i] == '.') {
+      ++i;
+      size_t st = i;
+      while (d(i)) ++i;
+      if (i == st) return false;
+    }
+    if (i < s.size() && (s[i] == 'Z' || s[i] == 'z')) return i + 1 == s.size();
+    if (i < s.size() && (s[i] == '+' || s[i] == '-'))
+      return i + 6 == s.size() && d(i + 1) && d(i + 2) && s[i + 3] == ':' && d(i + 4) && d(i + 5);
+    return false;
+  }
+
+ private:
+  JCur& c_;
+  std::string vs_, ks_;
+  void bad() {
+    err = true;
+    c_.skip();
+  }
+};
+
+uint32_t class_of(const std::string& kind) {
+  if (kind == "DaemonSet" || kind == "Deployment" || kind == "Job" || kind == "StatefulSet" ||
+      kind == "ReplicaSet" || kind == "ReplicationController")
+    return R_CLASS_CONTROLLER;
+  if (kind == "CronJob") return R_CLASS_CRONJOB;
+  if (kind == "Pod") return R_CLASS_POD;
+  return R_CLASS_OTHER;
+}
+
+// Pre-scan: top-level "kind" string (exact key, unstructured semantics).
+std::string top_kind(const char* p, const char* e) {
+  JCur c(p, e);
+  std::string out;
+  if (!c.obj_begin()) return out;
+  bool f = true;
+  std::string_view k;
+  std::string ks, vs;
+  while (c.obj_next(f, &k, ks)) {
+    if (k == "kind" && c.peek() == JK::Str) {
+      std::string_view v;
+      c.str(&v, vs);
+      out.assign(v);
+    } else {
+      c.skip();
+    }
+  }
+  return out;
+}
+
+uint32_t seccomp_code(bool set, const std::string& t) {
+  if (!set) return SECCOMP_NONE;
+  if (t == "RuntimeDefault") return SECCOMP_RUNTIMEDEFAULT;
+  if (t == "Localhost") return SECCOMP_LOCALHOST;
+  if (t == "Unconfined") return SECCOMP_UNCONFINED;
+  return SECCOMP_OTHER;
+}
+uint32_t sel_code(bool set, const std::string& t) {
+  if (!set) return SEL_NONE;
+  if (t.empty()) return SEL_EMPTY;
+  if (t == "container_t") return SEL_CONTAINER_T;
+  if (t == "container_init_t") return SEL_CONTAINER_INIT_T;
+  if (t == "container_kvm_t") return SEL_CONTAINER_KVM_T;
+  return SEL_OTHER;
+}
+
+struct LimitError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+class Flattener {
+ public:
+  explicit Flattener(Corpus& c) : C(c) {}
+
+  void add(const char* p, const char* e) {
+    u.reset();
+    pod.reset();
+    std::string kind = top_kind(p, e);
+    uint32_t cls = class_of(kind);
+    JCur cur(p, e);
+    Typed t(cur);
+    bool typed = cls != R_CLASS_OTHER;
+    // top-level walk: unstructured keys are exact; typed keys fold case
+    if (!cur.obj_begin()) throw std::invalid_argument("resource is not a JSON object");
+    bool f = true;
+    std::string_view key;
+    std::string ks;
+    while (cur.obj_next(f, &key, ks)) {
+      std::string k(key);
+      if (k == "kind" || k == "apiVersion") {
+        if (cur.peek() == JK::Str) {
+          std::string_view v;
+          std::string sc;
+          cur.str(&v, sc);
+          (k == "kind" ? u.kind : u.api_version).assign(v);
+        } else if (typed && cur.peek() != JK::Null) {
+          t.err = true;  // typed struct field is a string
+          cur.skip();
+        } else {
+          cur.skip();
+        }
+      } else if (keq(k, "kind") || keq(k, "apiversion")) {
+        if (typed) t.str(nullptr);
+        else cur.skip();
+      } else if (keq(k, "metadata")) {
+        meta(cur, t, k == "metadata", typed, cls == R_CLASS_POD);
+      } else if (keq(k, "spec") && typed) {
+        spec(t, cls);
+      } else {
+        cur.skip();
+      }
+    }
+    if (!cur.ok()) throw std::invalid_argument("malformed resource JSON");
+    emit(cls, typed && t.err);
+  }
+
+ private:
+  Corpus& C;
+  UView u;
+  PodView pod;
+
+  // metadata: unstructured (exact key "metadata") and/or typed ObjectMeta
+  void meta(JCur& cur, Typed& t, bool exact, bool typed, bool pod_meta) {
+    if (!exact) {  // only the typed decoder sees a case-variant key
+      if (typed) t.object_meta(pod_meta ? &pod.ann : nullptr);
+      else cur.skip();
+      return;
+    }
+    JK k0 = cur.peek();
+    if (k0 != JK::Obj) {
+      if (typed && k0 != JK::Null) t.err = true;
+      cur.skip();
+      return;
+    }
+    cur.obj_begin();
+    bool f = true;
+    std::string_view key;
+    std::string ks;
+    while (cur.obj_next(f, &key, ks)) {
+      std::string k(key);
+      // unstructured accessors
+      if (k == "name" || k == "generateName" || k == "namespace") {
+        if (cur.peek() == JK::Str) {
+          std::string_view v;
+          std::string sc;
+          cur.str(&v, sc);
+          std::string& dst = k == "name" ? u.name : (k == "namespace" ? u.ns : u.generate_name);
+          dst.assign(v);
+        } else {
+          if (typed && cur.peek() != JK::Null) t.err = true;
+          cur.skip();
+        }
+        continue;
+      }
+      if (k == "labels" || k == "annotations") {
+        bool is_lab = k == "labels";
+        auto& dst = is_lab ? u.labels : u.ann;
+        bool& ok = is_lab ? u.labels_ok : u.ann_ok;
+        dst.clear();
+        JK kk = cur.peek();
+        if (kk == JK::Null) {
+          cur.null();
+          ok = false;  // nil map
+          if (!is_lab && pod_meta) pod.ann.clear();
+          continue;
+        }
+        if (kk != JK::Obj) {
+          ok = false;
+          if (typed) t.err = true;
+          cur.skip();
+          continue;
+        }
+        cur.obj_begin();
+        bool f2 = true;
+        std::string_view k2;
+        std::string ks2;
+        std::vector<std::pair<std::string, std::string>> typed_ann;
+        while (cur.obj_next(f2, &k2, ks2)) {
+          std::string kk2(k2);
+          if (cur.peek() == JK::Str) {
+            std::string_view v;
+            std::string sc;
+            cur.str(&v, sc);
+            upsert(dst, kk2, std::string(v));
+            upsert(typed_ann, kk2, std::string(v));
+          } else if (cur.peek() == JK::Null) {
+            cur.null();
+            ok = false;  // NestedStringMap: non-string value => error => nil
+            upsert(typed_ann, kk2, std::string());
+          } else {
+            ok = false;
+            if (typed) t.err = true;
+            cur.skip();
+          }
+        }
+        if (!ok) dst.clear();
+        if (!is_lab && pod_meta) pod.ann = typed_ann;
+        continue;
+      }
+      // typed-only ObjectMeta fields (case-insensitive); unknown keys skipped
+      if (!typed) {
+        cur.skip();
+        continue;
+      }
+      if (keq(k, "name") || keq(k, "generatename") || keq(k, "namespace") || keq(k, "uid") ||
+          keq(k, "resourceversion") || keq(k, "selflink"))
+        t.str(nullptr);
+      else if (keq(k, "generation")) t.i64();
+      else if (keq(k, "creationtimestamp") || keq(k, "deletiontimestamp")) t.timev();
+      else if (keq(k, "labels")) t.strmap(nullptr);
+      else if (keq(k, "annotations")) t.strmap(pod_meta ? &pod.ann : nullptr);
+      else if (keq(k, "finalizers")) t.strlist(nullptr);
+      else cur.skip();
+    }
+  }
+  static void upsert(std::vector<std::pair<std::string, std::string>>& v, const std::string& k,
+                     const std::string& val) {
+    for (auto& e : v)
+      if (e.first == k) {
+        e.second = val;
+        return;
+      }
+    v.emplace_back(k, val);
+  }
+
+  void spec(Typed& t, uint32_t cls) {
+    if (cls == R_CLASS_POD) {
+      t.pod_spec(pod);
+    } else if (cls == R_CLASS_CONTROLLER) {
+      t.obj([&](std::string_view k) {
+        if (keq(k, "replicas") || keq(k, "revisionhistorylimit") || keq(k, "progressdeadlineseconds") ||
+            keq(k, "minreadyseconds"))
+          t.i32();
+        else if (keq(k, "paused")) t.boolean(nullptr);
+        else if (keq(k, "selector")) t.label_selector();
+        else if (keq(k, "template")) t.pod_template(pod, true);
+        else return false;
+        return true;
+      });
+    } else {  // CronJob
+      t.obj([&](std::string_view k) {
+        if (keq(k, "schedule") || keq(k, "concurrencypolicy")) t.str(nullptr);
+        else if (keq(k, "timezone")) t.strp(nullptr, nullptr);
+        else if (keq(k, "startingdeadlineseconds")) t.i64();
+        else if (keq(k, "suspend")) t.tri(nullptr);
+        else if (keq(k, "successfuljobshistorylimit") || keq(k, "failedjobshistorylimit")) t.i32();
+        else if (keq(k, "jobtemplate")) {
+          t.obj([&](std::string_view k3) {
+            // validate_pss.go:165-166: metadata from spec.jobTemplate.metadata
+            if (keq(k3, "metadata")) t.object_meta(&pod.ann);
+            else if (keq(k3, "spec")) {
+              t.obj([&](std::string_view k4) {
+                if (keq(k4, "parallelism") || keq(k4, "completions") || keq(k4, "backofflimit") ||
+                    keq(k4, "ttlsecondsafterfinished"))
+                  t.i32();
+                else if (keq(k4, "activedeadlineseconds")) t.i64();
+                else if (keq(k4, "selector")) t.label_selector();
+                else if (keq(k4, "manualselector") || keq(k4, "suspend")) t.tri(nullptr);
+                else if (keq(k4, "completionmode")) t.strp(nullptr, nullptr);
+                else if (keq(k4, "template")) {
+                  PodView tmp;
+                  t.pod_template(tmp, false);
+                  // only the spec is taken from the job's pod template
+                  for (int i = 0; i < 3; ++i) pod.ctr[i] = std::move(tmp.ctr[i]);
+                  pod.vols = std::move(tmp.vols);
+                  pod.sysctls = std::move(tmp.sysctls);
+                  pod.hostnet = tmp.hostnet;
+                  pod.hostpid = tmp.hostpid;
+                  pod.hostipc = tmp.hostipc;
+                  pod.sc = tmp.sc;
+                  pod.rnr = tmp.rnr;
+                  pod.rau = tmp.rau;
+                  pod.whp = tmp.whp;
+                  pod.sec = tmp.sec;
+                  pod.sec_type = tmp.sec_type;
+                  pod.sel = tmp.sel;
+                  pod.sel_type = tmp.sel_type;
+                  pod.sel_user = tmp.sel_user;
+                  pod.sel_role = tmp.sel_role;
+                  pod.os = tmp.os;
+                  pod.os_name = tmp.os_name;
+                } else return false;
+                return true;
+              });
+            } else return false;
+            return true;
+          });
+        } else return false;
+        return true;
+      });
+    }
+  }
+
+  uint32_t capmask(const std::vector<std::string>& l) {
+    uint64_t m = 0;
+    for (auto& s : l) {
+      uint32_t id = C.dict[D_CAP].intern(s);
+      if (id >= 64) throw LimitError("more than 64 distinct capability names in one corpus");
+      m |= 1ull << id;
+    }
+    last_mask_ = m;
+    return 0;
+  }
+  uint64_t last_mask_ = 0;
+
+  void emit(uint32_t cls, bool derr) {
+    // ---- resource row (unstructured view) ----
+    std::string group, version;
+    size_t sl = u.api_version.find('/');
+    if (sl == std::string::npos) version = u.api_version;
+    else {
+      group = u.api_version.substr(0, sl);
+      version = u.api_version.substr(sl + 1);
+    }
+    uint32_t kid = C.dict[D_KIND].intern(u.kind), vid = C.dict[D_VERSION].intern(version),
+             gid = C.dict[D_GROUP].intern(group);
+    if (kid >= 4096 || vid >= 1024 || gid >= 1024) throw LimitError("too many distinct kinds/versions/groups");
+    C.r_gvk.push_back(kid | (vid << 12) | (gid << 22));
+    bool is_ns = u.kind == "Namespace";
+    uint32_t flags = cls | (derr ? R_DECODE_ERR : 0u) | (is_ns ? R_IS_NAMESPACE : 0u) |
+                     (u.labels_ok ? 0u : R_LABELS_NIL) | (u.ann_ok ? 0u : R_ANNOT_NIL);
+    C.r_flags.push_back(flags);
+    C.r_name.push_back(C.dict[D_NAME].intern(u.name.empty() ? u.generate_name : u.name));
+    uint32_t nsa = C.dict[D_NS].intern(u.ns);
+    C.r_nsa.push_back(nsa);
+    C.r_mns.push_back(is_ns ? C.dict[D_NS].intern(u.name) : nsa);
+    auto it = C.nsl_index.find(u.ns);
+    C.r_nsl.push_back(it == C.nsl_index.end() ? KPE_NO_STR : it->second);
+    for (auto& kv : u.labels) {
+      C.lab_k.push_back(C.dict[D_LABK].intern(kv.first));
+      C.lab_v.push_back(C.dict[D_LABV].intern(kv.second));
+    }
+    C.lab_off.push_back((uint32_t)C.lab_k.size());
+    for (auto& kv : u.ann) {
+      C.ann_k.push_back(C.dict[D_ANNK].intern(kv.first));
+      C.ann_v.push_back(C.dict[D_ANNV].intern(kv.second));
+    }
+    C.ann_off.push_back((uint32_t)C.ann_k.size());
+
+    // ---- pod view ----
+    uint32_t p = 0;
+    if (pod.sc) p |= P_SC_PRESENT;
+    if (pod.hostnet) p |= P_HOSTNET;
+    if (pod.hostpid) p |= P_HOSTPID;
+    if (pod.hostipc) p |= P_HOSTIPC;
+    p |= pod.rnr << P_RNR_SH;
+    p |= pod.rau << P_RAU_SH;
+    p |= seccomp_code(pod.sec, pod.sec_type) << P_SECCOMP_SH;
+    p |= sel_code(pod.sel, pod.sel_type) << P_SEL_SH;
+    if (pod.sel && !pod.sel_user.empty()) p |= P_SEL_USER;
+    if (pod.sel && !pod.sel_role.empty()) p |= P_SEL_ROLE;
+    p |= pod.whp << P_WHP_SH;
+    p |= (pod.os ? (pod.os_name == "windows" ? OS_WINDOWS : OS_OTHER) : OS_NONE) << P_OS_SH;
+    C.p_sc.push_back(p);
+    for (uint32_t v : pod.vols) C.vol_src.push_back(v);
+    C.vol_off.push_back((uint32_t)C.vol_src.size());
+    for (auto& s : pod.sysctls) C.sys_id.push_back(C.dict[D_SYSCTL].intern(s));
+    C.sys_off.push_back((uint32_t)C.sys_id.size());
+    for (auto& kv : pod.ann) {
+      C.pann_k.push_back(C.dict[D_ANNK].intern(kv.first));
+      C.pann_v.push_back(C.dict[D_ANNV].intern(kv.second));
+    }
+    C.pann_off.push_back((uint32_t)C.pann_k.size());
+    static const std::string seccomp_ctr_prefix = "container.seccomp.security.alpha.kubernetes.io/";
+    for (uint32_t ct = 0; ct < 3; ++ct) {
+      for (auto& c : pod.ctr[ct]) {
+        uint32_t w = 0;
+        if (c.sc) w |= C_SC_PRESENT;
+        w |= c.priv << C_PRIV_SH;
+        w |= c.ape << C_APE_SH;
+        w |= c.rnr << C_RNR_SH;
+        w |= c.rau << C_RAU_SH;
+        w |= seccomp_code(c.sec, c.sec_type) << C_SECCOMP_SH;
+        w |= (c.pm ? (c.pm_val == "Default" ? PROCMOUNT_DEFAULT : PROCMOUNT_OTHER) : PROCMOUNT_UNSET)
+             << C_PROCMOUNT_SH;
+        w |= sel_code(c.sel, c.sel_type) << C_SEL_SH;
+        if (c.sel && !c.sel_user.empty()) w |= C_SEL_USER;
+        if (c.sel && !c.sel_role.empty()) w |= C_SEL_ROLE;
+        w |= c.whp << C_WHP_SH;
+        if (c.caps) w |= C_CAPS_PRESENT;
+        w |= ct << C_TYPE_SH;
+        uint32_t nz = 0;
+        for (int32_t h : c.hostports)
+          if (h != 0) ++nz;
+        w |= std::min(nz, 15u) << C_HOSTPORT_SH;
+        C.c_sc.push_back(w);
+        capmask(c.add);
+        C.c_add.push_back(last_mask_);
+        capmask(c.drop);
+        C.c_drop.push_back(last_mask_);
+        C.c_name.push_back(C.dict[D_CNAME].intern(c.name));
+        C.c_image.push_back(C.dict[D_IMAGE].intern(c.image));
+        uint32_t sann = KPE_NO_STR;  // join: pod annotation "container.seccomp...kubernetes.io/<name>"
+        if (!pod.ann.empty()) {
+          std::string key = seccomp_ctr_prefix + c.name;
+          for (auto& kv : pod.ann)
+            if (kv.first == key) sann = C.dict[D_ANNV].intern(kv.second);
+        }
+        C.c_sann.push_back(sann);
+        C.c_sec_str.push_back(c.sec ? C.dict[D_MISC].intern(c.sec_type) : KPE_NO_STR);
+        C.c_pm_str.push_back(c.pm ? C.dict[D_MISC].intern(c.pm_val) : KPE_NO_STR);
+        C.c_selt_str.push_back(c.sel ? C.dict[D_MISC].intern(c.sel_type) : KPE_NO_STR);
+        C.c_selu_str.push_back(c.sel ? C.dict[D_MISC].intern(c.sel_user) : KPE_NO_STR);
+        C.c_selr_str.push_back(c.sel ? C.dict[D_MISC].intern(c.sel_role) : KPE_NO_STR);
+        for (int32_t h : c.hostports) C.cport_host.push_back(h);
+        C.cport_off.push_back((uint32_t)C.cport_host.size());
+      }
+    }
+    C.ctr_off.push_back((uint32_t)C.c_sc.size());
+    C.n++;
+  }
+};
+
+void load_ns_labels(Corpus& C, const char* js, size_t len) {
+  if (!js || !len) return;
+  JCur c(js, js + len);
+  if (c.peek() == JK::Null) return;
+  if (!c.obj_begin()) throw std::invalid_argument("ns_labels_json must be an object");
+  bool f = true;
+  std::string_view k;
+  std::string ks, vs;
+  while (c.obj_next(f, &k, ks)) {
+    std::string ns(k);
+    uint32_t idx = (uint32_t)(C.nsl_off.size() - 1);
+    if (c.peek() == JK::Obj) {
+      c.obj_begin();
+      bool f2 = true;
+      std::string_view k2;
+      std::string ks2;
+      while (c.obj_next(f2, &k2, ks2)) {
+        std::string lk(k2);
+        if (c.peek() == JK::Str) {
+          std::string_view v;
+          c.str(&v, vs);
+          C.nsl_k.push_back(C.dict[D_LABK].intern(lk));
+          C.nsl_v.push_back(C.dict[D_LABV].intern(v));
+        } else {
+          c.skip();
+        }
+      }
+    } else {
+      c.skip();
+    }
+    C.nsl_off.push_back((uint32_t)C.nsl_k.size());
+    C.nsl_index[ns] = idx;
+  }
+  if (!c.ok()) throw std::invalid_argument("malformed ns_labels_json");
+}
+
+}  // namespace
+
+int64_t Corpus::bytes() const {
+  int64_t b = 0;
+  auto add = [&](const auto& v) { b += (int64_t)(v.size() * sizeof(v[0])); };
+  add(r_flags), add(r_gvk), add(r_name), add(r_mns), add(r_nsa), add(r_nsl);
+  add(lab_off), add(lab_k), add(lab_v), add(ann_off), add(ann_k), add(ann_v);
+  add(p_sc), add(ctr_off), add(vol_off), add(vol_src), add(sys_off), add(sys_id), add(pann_off), add(pann_k),
+      add(pann_v);
+  add(c_sc), add(c_add), add(c_drop), add(c_name), add(c_image), add(c_sann);
+  return b;
+}
+
+// Entry used by kpe_corpus_flatten. Throws std::invalid_argument / LimitError.
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len) {
+  load_ns_labels(C, nsl, nsl_len);
+  Flattener fl(C);
+  size_t i = 0;
+  while (i < len) {
+    size_t j = i;
+    while (j < len && buf[j] != '\n') ++j;
+    size_t a = i, b = j;
+    while (a < b && (buf[a] == ' ' || buf[a] == '\t' || buf[a] == '\r')) ++a;
+    while (b > a && (buf[b - 1] == ' ' || buf[b - 1] == '\t' || buf[b - 1] == '\r')) --b;
+    if (b > a) fl.add(buf + a, buf + b);
+    i = j + 1;
+  }
+}
+
+bool is_limit_error(const std::exception& e) { return dynamic_cast<const LimitError*>(&e) != nullptr; }
+
+}  // namespace kpe

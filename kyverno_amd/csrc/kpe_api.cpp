@@ -1,0 +1,566 @@
+// C-ABI implementation (include/kpe.h): device management, H2D upload of the
+// columnar corpus and compiled program, evaluation launches and result fetch.
+// There is no CPU evaluation path: without a usable HIP device every
+// evaluation call fails with KPE_E_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/kpe.h"
+#include "corpus.hpp"
+#include "program.hpp"
+
+namespace kpe {
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len);
+bool is_limit_error(const std::exception& e);
+}  // namespace kpe
+
+// ---- mirrors of kernels.hip argument structs (identical layout) ----
+struct PredJob {
+  uint32_t domain, pat0, npat, out_word, blk0;
+};
+struct PredArgs {
+  const uint8_t* dict_bytes[KPE_NUM_DOMAINS];
+  const uint32_t* dict_off[KPE_NUM_DOMAINS];
+  uint32_t dict_n[KPE_NUM_DOMAINS];
+  const uint8_t* pat_bytes;
+  const uint32_t* pat_off;
+  const PredJob* jobs;
+  uint32_t njobs;
+  uint32_t* out;
+};
+struct ScanArgs {
+  int64_t n;
+  const uint32_t *r_flags, *r_gvk, *r_name, *r_mns, *r_nsa, *ann_off, *ann_k, *ann_v;
+  const uint32_t *p_sc, *ctr_off, *vol_off, *vol_src, *sys_off, *sys_id, *pann_off, *pann_k, *pann_v;
+  const uint32_t* c_sc;
+  const uint64_t *c_add, *c_drop;
+  const uint32_t* c_sann;
+  const KpeRule* rules;
+  uint32_t nrules;
+  const KpeFilter* filters;
+  const KpeTerm* terms;
+  const KpeKindSel* kindsels;
+  const KpeAnnPair* annpairs;
+  const uint32_t* pred_bits;
+  const uint32_t* pred_word;
+  int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
+  int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
+  uint32_t cv_union;
+  uint32_t any_pss;
+  uint8_t* verdicts;
+  uint32_t* masks;
+  unsigned long long* counts;
+};
+extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s);
+
+namespace {
+thread_local std::string g_err;
+
+kpe_status fail(kpe_status s, const std::string& m) {
+  g_err = m;
+  return s;
+}
+#define HIPCHK(x)                                                                                  \
+  do {                                                                                             \
+    hipError_t e_ = (x);                                                                           \
+    if (e_ != hipSuccess) return fail(KPE_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  hipError_t ensure(size_t n) {
+    if (n <= bytes && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(n, 16));
+    if (e == hipSuccess) bytes = n;
+    return e;
+  }
+  template <class T>
+  T* as() const {
+    return static_cast<T*>(p);
+  }
+};
+
+template <class T>
+hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+  hipError_t e = b.ensure(v.size() * sizeof(T));
+  if (e != hipSuccess) return e;
+  if (!v.empty()) return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  return hipSuccess;
+}
+
+}  // namespace
+
+struct kpe_device {
+  int ordinal = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  bool timing = false;
+  struct EvPair {
+    hipEvent_t a, b, c;
+    double bytes;
+  };
+  std::vector<EvPair> pending;
+  std::vector<hipEvent_t> pool;
+  uint64_t launches = 0;
+  double pss_ms = 0, dict_ms = 0, last_bytes = 0;
+  hipEvent_t get_ev() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+};
+
+namespace kpe {
+struct DeviceProgram {
+  int ordinal = -1;
+  DevBuf rules, filters, terms, kindsels, annpairs, pat_bytes, pat_off;
+  std::vector<uint8_t> pat_bytes_h;
+  std::vector<uint32_t> pat_off_h;
+};
+
+struct Binding {  // program x corpus (dictionary sizes decide predicate layout)
+  const Program* prog = nullptr;
+  DevBuf jobs, pred_word, pred_bits, verdicts, masks, counts;
+  uint32_t nblocks = 0, njobs = 0;
+  size_t cells = 0;
+};
+
+struct DeviceCorpus {
+  int ordinal = -1;
+  DevBuf dict_bytes[KPE_NUM_DOMAINS], dict_off[KPE_NUM_DOMAINS];
+  DevBuf r_flags, r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
+  DevBuf p_sc, ctr_off, vol_off, vol_src, sys_off, sys_id, pann_off, pann_k, pann_v;
+  DevBuf c_sc, c_add, c_drop, c_sann;
+  Binding bind;
+  bool has_masks = false;
+};
+}  // namespace kpe
+
+struct kpe_program {
+  std::unique_ptr<kpe::Program> p;
+};
+struct kpe_corpus {
+  std::unique_ptr<kpe::Corpus> c;
+  std::unique_ptr<kpe::DeviceCorpus> d;
+};
+
+extern "C" {
+
+const char* kpe_last_error(void) { return g_err.c_str(); }
+const char* kpe_version(void) { return "kpe 0.1 (gfx950)"; }
+
+kpe_status kpe_device_open(int ordinal, kpe_device** out) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n == 0) return fail(KPE_E_DEVICE, "no HIP device available");
+  if (ordinal < 0 || ordinal >= n) return fail(KPE_E_DEVICE, "device ordinal out of range");
+  HIPCHK(hipSetDevice(ordinal));
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, ordinal));
+  if (std::string(prop.gcnArchName).find("gfx950") == std::string::npos)
+    return fail(KPE_E_DEVICE, std::string("kernels are built for gfx950, device is ") + prop.gcnArchName);
+  auto d = new (std::nothrow) kpe_device();
+  if (!d) return fail(KPE_E_DEVICE, "oom");
+  d->ordinal = ordinal;
+  e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    delete d;
+    return fail(KPE_E_DEVICE, hipGetErrorString(e));
+  }
+  *out = d;
+  return KPE_OK;
+}
+
+void kpe_device_close(kpe_device* d) {
+  if (!d) return;
+  (void)hipSetDevice(d->ordinal);
+  (void)hipStreamSynchronize(d->stream);
+  for (auto& p : d->pending) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+    (void)hipEventDestroy(p.c);
+  }
+  for (auto e : d->pool) (void)hipEventDestroy(e);
+  (void)hipStreamDestroy(d->stream);
+  delete d;
+}
+
+kpe_status kpe_program_compile(const char* json, size_t len, kpe_program** out) {
+  try {
+    auto p = kpe::compile_policies(json, len);
+    *out = new kpe_program{std::move(p)};
+    return KPE_OK;
+  } catch (const kpe::CompileError& e) {
+    return fail(KPE_E_UNSUPPORTED, e.what());
+  } catch (const std::exception& e) {
+    return fail(KPE_E_INVALID, e.what());
+  }
+}
+int kpe_program_num_rules(const kpe_program* p) { return p ? (int)p->p->rules.size() : 0; }
+const char* kpe_program_rule_name(const kpe_program* p, int r) {
+  if (!p || r < 0 || r >= (int)p->p->rule_names.size()) return nullptr;
+  return p->p->rule_names[r].c_str();
+}
+int kpe_program_rule_is_pss(const kpe_program* p, int r) {
+  if (!p || r < 0 || r >= (int)p->p->rules.size()) return 0;
+  return p->p->rules[r].handler == H_PSS ? 1 : 0;
+}
+void kpe_program_free(kpe_program* p) {
+  if (p) {
+    delete p->p->dev;
+    delete p;
+  }
+}
+
+kpe_status kpe_corpus_flatten(const char* ndjson, size_t len, const char* nsl, size_t nsl_len, kpe_corpus** out) {
+  auto c = std::make_unique<kpe::Corpus>();
+  try {
+    kpe::flatten_ndjson(*c, ndjson, len, nsl, nsl_len);
+  } catch (const std::exception& e) {
+    return fail(kpe::is_limit_error(e) ? KPE_E_LIMIT : KPE_E_INVALID, e.what());
+  }
+  *out = new kpe_corpus{std::move(c), nullptr};
+  return KPE_OK;
+}
+int64_t kpe_corpus_num_resources(const kpe_corpus* c) { return c ? c->c->n : 0; }
+int64_t kpe_corpus_bytes(const kpe_corpus* c) { return c ? c->c->bytes() : 0; }
+void kpe_corpus_free(kpe_corpus* c) {
+  if (!c) return;
+  if (c->d) (void)hipSetDevice(c->d->ordinal);
+  delete c;
+}
+
+kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
+  if (!dev || !cc) return fail(KPE_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& C = *cc->c;
+  cc->d = std::make_unique<kpe::DeviceCorpus>();
+  auto& D = *cc->d;
+  D.ordinal = dev->ordinal;
+  hipStream_t s = dev->stream;
+  for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
+    HIPCHK(upload(D.dict_bytes[i], C.dict[i].bytes, s));
+    HIPCHK(upload(D.dict_off[i], C.dict[i].off, s));
+  }
+  HIPCHK(upload(D.r_flags, C.r_flags, s));
+  HIPCHK(upload(D.r_gvk, C.r_gvk, s));
+  HIPCHK(upload(D.r_name, C.r_name, s));
+  HIPCHK(upload(D.r_mns, C.r_mns, s));
+  HIPCHK(upload(D.r_nsa, C.r_nsa, s));
+  HIPCHK(upload(D.ann_off, C.ann_off, s));
+  HIPCHK(upload(D.ann_k, C.ann_k, s));
+  HIPCHK(upload(D.ann_v, C.ann_v, s));
+  HIPCHK(upload(D.p_sc, C.p_sc, s));
+  HIPCHK(upload(D.ctr_off, C.ctr_off, s));
+  HIPCHK(upload(D.vol_off, C.vol_off, s));
+  HIPCHK(upload(D.vol_src, C.vol_src, s));
+  HIPCHK(upload(D.sys_off, C.sys_off, s));
+  HIPCHK(upload(D.sys_id, C.sys_id, s));
+  HIPCHK(upload(D.pann_off, C.pann_off, s));
+  HIPCHK(upload(D.pann_k, C.pann_k, s));
+  HIPCHK(upload(D.pann_v, C.pann_v, s));
+  HIPCHK(upload(D.c_sc, C.c_sc, s));
+  HIPCHK(upload(D.c_add, C.c_add, s));
+  HIPCHK(upload(D.c_drop, C.c_drop, s));
+  HIPCHK(upload(D.c_sann, C.c_sann, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return KPE_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
+  auto& P = *pp->p;
+  if (P.dev && P.dev->ordinal == dev->ordinal) return KPE_OK;
+  delete P.dev;
+  P.dev = new kpe::DeviceProgram();
+  auto& D = *P.dev;
+  D.ordinal = dev->ordinal;
+  hipStream_t s = dev->stream;
+  D.pat_off_h.assign(1, 0);
+  for (auto& pr : P.preds)
+    for (auto& g : pr.globs) {
+      D.pat_bytes_h.insert(D.pat_bytes_h.end(), g.begin(), g.end());
+      D.pat_off_h.push_back((uint32_t)D.pat_bytes_h.size());
+    }
+  HIPCHK(upload(D.rules, P.rules, s));
+  HIPCHK(upload(D.filters, P.filters, s));
+  HIPCHK(upload(D.terms, P.terms, s));
+  HIPCHK(upload(D.kindsels, P.kindsels, s));
+  HIPCHK(upload(D.annpairs, P.annpairs, s));
+  HIPCHK(upload(D.pat_bytes, D.pat_bytes_h, s));
+  HIPCHK(upload(D.pat_off, D.pat_off_h, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return KPE_OK;
+}
+
+kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool want_masks) {
+  auto& P = *pp->p;
+  auto& C = *cc->c;
+  auto& B = cc->d->bind;
+  size_t cells = (size_t)C.n * P.rules.size();
+  if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
+  hipStream_t s = dev->stream;
+  std::vector<PredJob> jobs;
+  std::vector<uint32_t> word;
+  uint32_t w = 0, blk = 0, pat = 0;
+  for (auto& pr : P.preds) {
+    uint32_t n = C.dict[pr.domain].size();
+    uint32_t nwords = ((n + 63) / 64) * 2 + 2;
+    jobs.push_back({pr.domain, pat, (uint32_t)pr.globs.size(), w, blk});
+    word.push_back(w);
+    w += nwords;
+    blk += (n + 255) / 256;
+    pat += (uint32_t)pr.globs.size();
+  }
+  B.njobs = (uint32_t)jobs.size();
+  B.nblocks = blk;
+  HIPCHK(upload(B.jobs, jobs, s));
+  HIPCHK(upload(B.pred_word, word, s));
+  HIPCHK(B.pred_bits.ensure(std::max<size_t>(w, 1) * 4));
+  HIPCHK(hipMemsetAsync(B.pred_bits.p, 0, std::max<size_t>(w, 1) * 4, s));
+  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 1)));
+  HIPCHK(B.counts.ensure(std::max<size_t>(P.rules.size(), 1) * 6 * 8));
+  if (want_masks) {
+    HIPCHK(B.masks.ensure(std::max<size_t>(cells, 1) * 4));
+    cc->d->has_masks = true;
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  B.prog = &P;
+  B.cells = cells;
+  return KPE_OK;
+}
+
+kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool masks) {
+  auto& P = *pp->p;
+  auto& C = *cc->c;
+  auto& D = *cc->d;
+  auto& PD = *P.dev;
+  auto& B = D.bind;
+  hipStream_t s = dev->stream;
+  kpe_device::EvPair ev{};
+  if (dev->timing) {
+    ev.a = dev->get_ev();
+    ev.b = dev->get_ev();
+    ev.c = dev->get_ev();
+    HIPCHK(hipEventRecord(ev.a, s));
+  }
+  PredArgs pa{};
+  for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
+    pa.dict_bytes[i] = D.dict_bytes[i].as<uint8_t>();
+    pa.dict_off[i] = D.dict_off[i].as<uint32_t>();
+    pa.dict_n[i] = C.dict[i].size();
+  }
+  pa.pat_bytes = PD.pat_bytes.as<uint8_t>();
+  pa.pat_off = PD.pat_off.as<uint32_t>();
+  pa.jobs = B.jobs.as<PredJob>();
+  pa.njobs = B.njobs;
+  pa.out = B.pred_bits.as<uint32_t>();
+  HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
+  HIPCHK(hipMemsetAsync(B.counts.p, 0, P.rules.size() * 6 * 8, s));
+  if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
+  ScanArgs sa{};
+  sa.n = C.n;
+  sa.r_flags = D.r_flags.as<uint32_t>();
+  sa.r_gvk = D.r_gvk.as<uint32_t>();
+  sa.r_name = D.r_name.as<uint32_t>();
+  sa.r_mns = D.r_mns.as<uint32_t>();
+  sa.r_nsa = D.r_nsa.as<uint32_t>();
+  sa.ann_off = D.ann_off.as<uint32_t>();
+  sa.ann_k = D.ann_k.as<uint32_t>();
+  sa.ann_v = D.ann_v.as<uint32_t>();
+  sa.p_sc = D.p_sc.as<uint32_t>();
+  sa.ctr_off = D.ctr_off.as<uint32_t>();
+  sa.vol_off = D.vol_off.as<uint32_t>();
+  sa.vol_src = D.vol_src.as<uint32_t>();
+  sa.sys_off = D.sys_off.as<uint32_t>();
+  sa.sys_id = D.sys_id.as<uint32_t>();
+  sa.pann_off = D.pann_off.as<uint32_t>();
+  sa.pann_k = D.pann_k.as<uint32_t>();
+  sa.pann_v = D.pann_v.as<uint32_t>();
+  sa.c_sc = D.c_sc.as<uint32_t>();
+  sa.c_add = D.c_add.as<uint64_t>();
+  sa.c_drop = D.c_drop.as<uint64_t>();
+  sa.c_sann = D.c_sann.as<uint32_t>();
+  sa.rules = PD.rules.as<KpeRule>();
+  sa.nrules = (uint32_t)P.rules.size();
+  sa.filters = PD.filters.as<KpeFilter>();
+  sa.terms = PD.terms.as<KpeTerm>();
+  sa.kindsels = PD.kindsels.as<KpeKindSel>();
+  sa.annpairs = PD.annpairs.as<KpeAnnPair>();
+  sa.pred_bits = B.pred_bits.as<uint32_t>();
+  sa.pred_word = B.pred_word.as<uint32_t>();
+  sa.pp_apparmor_key = P.pss.apparmor_key;
+  sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
+  sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;
+  sa.pp_seccomp_ann_ok = P.pss.seccomp_ann_ok;
+  sa.pp_caps_ok = P.pss.caps_baseline_ok;
+  sa.pp_cap_nbs = P.pss.cap_nbs;
+  sa.pp_cap_all = P.pss.cap_all;
+  sa.pp_sysctl0 = P.pss.sysctl[0];
+  sa.pp_sysctl1 = P.pss.sysctl[1];
+  sa.pp_sysctl2 = P.pss.sysctl[2];
+  sa.cv_union = P.cv_union;
+  sa.any_pss = P.any_pss ? 1u : 0u;
+  sa.verdicts = B.verdicts.as<uint8_t>();
+  sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
+  sa.counts = B.counts.as<unsigned long long>();
+  HIPCHK(kpe_launch_scan(&sa, s));
+  if (dev->timing) {
+    HIPCHK(hipEventRecord(ev.c, s));
+    // algorithmic bytes of one scan launch: every column the program reads + verdict cells written
+    double bytes = 0;
+    if (P.any_pss)
+      bytes += (double)(C.p_sc.size() + C.ctr_off.size() + C.vol_off.size() + C.sys_off.size() + C.pann_off.size() +
+                        C.vol_src.size() + C.sys_id.size() + 2 * C.pann_k.size()) * 4 +
+               (double)C.c_sc.size() * (4 + 8 + 8 + 4);
+    bytes += (double)(C.r_flags.size() + C.r_gvk.size() + C.r_nsa.size()) * 4;
+    bytes += (double)C.n * P.rules.size() * (masks ? 5 : 1);
+    ev.bytes = bytes;
+    dev->pending.push_back(ev);
+  }
+  return KPE_OK;
+}
+
+kpe_status prepare(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, bool masks) {
+  if (!dev || !prog || !c) return fail(KPE_E_INVALID, "null argument");
+  if (!c->d || c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
+  HIPCHK(hipSetDevice(dev->ordinal));
+  kpe_status st = ensure_program(dev, prog);
+  if (st) return st;
+  return ensure_binding(dev, prog, const_cast<kpe_corpus*>(c), masks);
+}
+
+}  // namespace
+
+extern "C" {
+
+kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c) {
+  if (!dev) return fail(KPE_E_INVALID, "null device");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  kpe_status st = prepare(dev, prog, c, false);
+  if (st) return st;
+  return launch(dev, prog, const_cast<kpe_corpus*>(c), false);
+}
+
+kpe_status kpe_device_sync(kpe_device* dev) {
+  if (!dev) return fail(KPE_E_INVALID, "null device");
+  HIPCHK(hipSetDevice(dev->ordinal));
+  HIPCHK(hipStreamSynchronize(dev->stream));
+  return KPE_OK;
+}
+
+kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
+                     uint32_t* masks, kpe_counts* counts) {
+  if (!dev || !prog || !c || !c->d) return fail(KPE_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& B = c->d->bind;
+  if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  size_t R = prog->p->rules.size(), cells = (size_t)c->c->n * R;
+  HIPCHK(hipStreamSynchronize(dev->stream));
+  if (verdicts && cells) HIPCHK(hipMemcpy(verdicts, B.verdicts.p, cells, hipMemcpyDeviceToHost));
+  if (masks && cells) {
+    if (!c->d->has_masks) return fail(KPE_E_STATE, "check masks were not computed");
+    HIPCHK(hipMemcpy(masks, B.masks.p, cells * 4, hipMemcpyDeviceToHost));
+  }
+  if (counts && R) {
+    std::vector<unsigned long long> h(R * 6);
+    HIPCHK(hipMemcpy(h.data(), B.counts.p, R * 6 * 8, hipMemcpyDeviceToHost));
+    for (size_t r = 0; r < R; ++r) {
+      uint64_t tot = 0;
+      for (int k = 1; k < 6; ++k) tot += h[r * 6 + k];
+      counts[r].na = (uint64_t)c->c->n - tot;
+      counts[r].pass = h[r * 6 + 1];
+      counts[r].fail = h[r * 6 + 2];
+      counts[r].warn = h[r * 6 + 3];
+      counts[r].error = h[r * 6 + 4];
+      counts[r].skip = h[r * 6 + 5];
+    }
+  }
+  return KPE_OK;
+}
+
+kpe_status kpe_evaluate(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
+                        uint32_t* masks, kpe_counts* counts) {
+  {
+    if (!dev) return fail(KPE_E_INVALID, "null device");
+    std::lock_guard<std::mutex> lk(dev->mu);
+    kpe_status st = prepare(dev, prog, c, masks != nullptr);
+    if (st) return st;
+    st = launch(dev, prog, const_cast<kpe_corpus*>(c), masks != nullptr);
+    if (st) return st;
+  }
+  return kpe_fetch(dev, prog, c, verdicts, masks, counts);
+}
+
+static const char* const kCheckIds[KPE_NUM_CHECKS] = {
+    "allowPrivilegeEscalation", "appArmorProfile", "capabilities_baseline", "capabilities_restricted",
+    "hostNamespaces", "hostPathVolumes", "hostPorts", "privileged", "procMount", "restrictedVolumes",
+    "runAsNonRoot", "runAsUser", "seLinuxOptions", "seccompProfile_baseline", "seccompProfile_restricted",
+    "sysctls", "windowsHostProcess"};
+const char* kpe_pss_check_id(int k) { return (k >= 0 && k < KPE_NUM_CHECKS) ? kCheckIds[k] : nullptr; }
+int kpe_pss_num_checks(void) { return KPE_NUM_CHECKS; }
+
+kpe_status kpe_device_set_timing(kpe_device* dev, int enabled) {
+  if (!dev) return fail(KPE_E_INVALID, "null device");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  dev->timing = enabled != 0;
+  return KPE_OK;
+}
+
+kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kpe_corpus*, kpe_kernel_stats* out,
+                                   int reset) {
+  if (!dev || !out) return fail(KPE_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  HIPCHK(hipStreamSynchronize(dev->stream));
+  for (auto& p : dev->pending) {
+    float d1 = 0, d2 = 0;
+    HIPCHK(hipEventElapsedTime(&d1, p.a, p.b));
+    HIPCHK(hipEventElapsedTime(&d2, p.b, p.c));
+    dev->dict_ms += d1;
+    dev->pss_ms += d2;
+    dev->last_bytes = p.bytes;
+    dev->launches++;
+    dev->pool.push_back(p.a);
+    dev->pool.push_back(p.b);
+    dev->pool.push_back(p.c);
+  }
+  dev->pending.clear();
+  out->launches = dev->launches;
+  out->pss_kernel_ms = dev->pss_ms;
+  out->dict_kernel_ms = dev->dict_ms;
+  out->scan_bytes = dev->last_bytes;
+  if (reset) {
+    dev->launches = 0;
+    dev->pss_ms = dev->dict_ms = 0;
+  }
+  return KPE_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,768 @@
+// Policy compiler: ClusterPolicy/Policy JSON -> autogen -> device rule program.
+//
+// Follows, in order:
+//   autogen.ComputeRules / CanAutoGen / generateRules   pkg/autogen/autogen.go:67-116,192-270
+//   generateRule / generateRuleForControllers / generateCronJobRule  pkg/autogen/rule.go:73-322
+//   rule handler precedence (manifest > PSS > CEL > resource) pkg/engine/validation.go:32-63
+//   match/exclude structure  pkg/engine/utils/match.go:168-300 (lowered to filter/term tables)
+//   kind selectors           pkg/utils/kube/kind.go:11-46
+//   PSS version selection    pkg/pss/evaluate.go:24-70 + ParseVersion :221-239 (folded into cv_mask)
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "jscan.hpp"
+#include "program.hpp"
+
+namespace kpe {
+
+// ---------------------------------------------------------------------------
+// Minimal JSON DOM for policies (small inputs; resources never use this).
+struct JV {
+  enum T { Null, Bool, Num, Str, Arr, Obj } t = Null;
+  bool b = false;
+  double n = 0;
+  bool is_int = false;
+  int64_t i = 0;
+  std::string s;
+  std::vector<JV> a;
+  std::vector<std::pair<std::string, JV>> o;
+  const JV* get(const char* k) const {
+    if (t != Obj) return nullptr;
+    const JV* r = nullptr;
+    for (auto& kv : o)
+      if (kv.first == k) r = &kv.second;
+    return r;
+  }
+  JV* getm(const char* k) {
+    if (t != Obj) return nullptr;
+    JV* r = nullptr;
+    for (auto& kv : o)
+      if (kv.first == k) r = &kv.second;
+    return r;
+  }
+  void set(const std::string& k, JV v) {
+    for (auto& kv : o)
+      if (kv.first == k) {
+        kv.second = std::move(v);
+        return;
+      }
+    o.emplace_back(k, std::move(v));
+  }
+  static JV str(const std::string& x) {
+    JV v;
+    v.t = Str;
+    v.s = x;
+    return v;
+  }
+  static JV obj() {
+    JV v;
+    v.t = Obj;
+    return v;
+  }
+  static JV strs(const std::vector<std::string>& l) {
+    JV v;
+    v.t = Arr;
+    for (auto& x : l) v.a.push_back(str(x));
+    return v;
+  }
+};
+
+namespace {
+
+JV parse_value(JCur& c) {
+  JV v;
+  std::string sc;
+  switch (c.peek()) {
+    case JK::Null: c.null(); break;
+    case JK::Bool:
+      v.t = JV::Bool;
+      c.boolean(&v.b);
+      break;
+    case JK::Num: {
+      JNum n;
+      c.number(&n);
+      v.t = JV::Num;
+      v.is_int = n.is_int;
+      v.i = n.i;
+      v.n = n.is_int ? (double)n.i : n.f;
+      break;
+    }
+    case JK::Str: {
+      std::string_view sv;
+      c.str(&sv, sc);
+      v.t = JV::Str;
+      v.s.assign(sv);
+      break;
+    }
+    case JK::Arr: {
+      v.t = JV::Arr;
+      c.arr_begin();
+      bool f = true;
+      while (c.arr_next(f)) v.a.push_back(parse_value(c));
+      break;
+    }
+    case JK::Obj: {
+      v.t = JV::Obj;
+      c.obj_begin();
+      bool f = true;
+      std::string_view k;
+      std::string ks;
+      while (c.obj_next(f, &k, ks)) {
+        std::string key(k);
+        JV child = parse_value(c);
+        v.set(key, std::move(child));  // duplicate keys: last wins
+      }
+      break;
+    }
+    default: c.fail();
+  }
+  return v;
+}
+
+void write(const JV& v, std::string& o) {
+  switch (v.t) {
+    case JV::Null: o += "null"; break;
+    case JV::Bool: o += v.b ? "true" : "false"; break;
+    case JV::Num: {
+      if (v.is_int) o += std::to_string(v.i);
+      else {
+        char b[64];
+        snprintf(b, sizeof b, "%.17g", v.n);
+        o += b;
+      }
+      break;
+    }
+    case JV::Str: {
+      o += '"';
+      for (unsigned char ch : v.s) {
+        if (ch == '"' || ch == '\\') {
+          o += '\\';
+          o += (char)ch;
+        } else if (ch < 0x20) {
+          char b[8];
+          snprintf(b, sizeof b, "\\u%04x", ch);
+          o += b;
+        } else {
+          o += (char)ch;
+        }
+      }
+      o += '"';
+      break;
+    }
+    case JV::Arr:
+      o += '[';
+      for (size_t k = 0; k < v.a.size(); ++k) {
+        if (k) o += ',';
+        write(v.a[k], o);
+      }
+      o += ']';
+      break;
+    case JV::Obj:
+      o += '{';
+      for (size_t k = 0; k < v.o.size(); ++k) {
+        if (k) o += ',';
+        write(JV::str(v.o[k].first), o);
+        o += ':';
+        write(v.o[k].second, o);
+      }
+      o += '}';
+      break;
+  }
+}
+
+JV parse_all(const char* p, size_t n) {
+  JCur c(p, p + n);
+  JV v = parse_value(c);
+  c.ws();
+  if (!c.ok() || c.pos() != p + n) throw std::invalid_argument("malformed policy JSON");
+  return v;
+}
+
+std::string sv(const JV* v) { return (v && v->t == JV::Str) ? v->s : std::string(); }
+std::vector<std::string> svl(const JV* v) {
+  std::vector<std::string> o;
+  if (v && v->t == JV::Arr)
+    for (auto& e : v->a)
+      if (e.t == JV::Str) o.push_back(e.s);
+  return o;
+}
+bool nonempty(const JV* v) {  // !DeepEqual(x, zero value)
+  if (!v) return false;
+  switch (v->t) {
+    case JV::Null: return false;
+    case JV::Bool: return v->b;
+    case JV::Num: return v->n != 0;
+    case JV::Str: return !v->s.empty();
+    case JV::Arr: return !v->a.empty();
+    case JV::Obj:
+      for (auto& kv : v->o)
+        if (nonempty(&kv.second)) return true;
+      return false;
+  }
+  return false;
+}
+
+std::vector<std::string> split(const std::string& s, char d) {
+  std::vector<std::string> o;
+  size_t i = 0;
+  while (true) {
+    size_t j = s.find(d, i);
+    if (j == std::string::npos) {
+      o.push_back(s.substr(i));
+      break;
+    }
+    o.push_back(s.substr(i, j - i));
+    i = j + 1;
+  }
+  return o;
+}
+
+// host glob (go-wildcard v1.0.3 semantics, runes) — only for compile-time constant folding
+bool glob_host(const std::string& pat, const std::string& s) {
+  if (pat.empty()) return s.empty();
+  if (pat == "*") return true;
+  auto runes = [](const std::string& x) {
+    std::vector<uint32_t> r;
+    for (size_t i = 0; i < x.size();) {
+      unsigned char ch = (unsigned char)x[i];
+      int n = ch < 0x80 ? 1 : (ch >> 5) == 6 ? 2 : (ch >> 4) == 14 ? 3 : (ch >> 3) == 30 ? 4 : 1;
+      uint32_t cp = 0;
+      for (int k = 0; k < n && i + k < x.size(); ++k) cp = (cp << 8) | (unsigned char)x[i + k];
+      r.push_back(cp);
+      i += n;
+    }
+    return r;
+  };
+  auto p = runes(pat), t = runes(s);
+  size_t pi = 0, si = 0, star = SIZE_MAX, mark = 0;
+  while (si < t.size()) {
+    if (pi < p.size() && (p[pi] == '?' || (p[pi] != '*' && p[pi] == t[si]))) {
+      ++pi;
+      ++si;
+    } else if (pi < p.size() && p[pi] == '*') {
+      star = pi++;
+      mark = si;
+    } else if (star != SIZE_MAX) {
+      pi = star + 1;
+      si = ++mark;
+    } else {
+      return false;
+    }
+  }
+  while (pi < p.size() && p[pi] == '*') ++pi;
+  return pi == p.size();
+}
+
+// ---- kind helpers (pkg/utils/kube/kind.go) ----
+bool version_regex(const std::string& s) {  // `^v\d((alpha|beta)\d)?|\*$`
+  if (s.size() >= 2 && s[0] == 'v' && s[1] >= '0' && s[1] <= '9') return true;
+  return !s.empty() && s.back() == '*';
+}
+struct KindSel {
+  std::string g, v, k, sub;
+};
+KindSel parse_kind_selector(const std::string& in) {
+  auto parts = split(in, '/');
+  auto last = split(parts.back(), '.');
+  parts.pop_back();
+  for (auto& x : last) parts.push_back(x);
+  auto lower = [](std::string x) {
+    for (auto& ch : x) ch = (char)tolower((unsigned char)ch);
+    return x;
+  };
+  switch (parts.size()) {
+    case 1: return {"*", "*", parts[0], ""};
+    case 2:
+      if (parts[0] == "*" && parts[1] == "*") return {"*", "*", "*", "*"};
+      if (parts[0] == "*" && lower(parts[1]) == parts[1]) return {"*", "*", parts[0], parts[1]};
+      if (version_regex(parts[0])) return {"*", parts[0], parts[1], ""};
+      return {"*", "*", parts[0], parts[1]};
+    case 3:
+      if (version_regex(parts[0])) return {"*", parts[0], parts[1], parts[2]};
+      return {parts[0], parts[1], parts[2], ""};
+    case 4: return {parts[0], parts[1], parts[2], parts[3]};
+    default: return {"", "", "", ""};
+  }
+}
+bool contains_kind(const std::vector<std::string>& list, const std::string& kind) {  // kube.ContainsKind
+  for (auto& e : list) {
+    auto parts = split(e, '/');
+    auto fmt = [](std::string s) {
+      size_t d = s.find('.');
+      if (d != std::string::npos) s[d] = '/';
+      return s;
+    };
+    std::string k;
+    switch (parts.size()) {
+      case 1: k = fmt(e); break;
+      case 2:
+        if (parts[0] == "*" && parts[1] == "*") k = "*/*";
+        else if (version_regex(parts[0])) k = fmt(parts[1]);
+        else k = parts[0] + "/" + parts[1];
+        break;
+      case 3: k = version_regex(parts[0]) ? parts[1] + "/" + parts[2] : fmt(parts[2]); break;
+      case 4: k = parts[2] + "/" + parts[3]; break;
+      default: k = "";
+    }
+    auto sp = split(k, '/');
+    if (sp.size() == 2) k = sp[0];
+    if (k == kind) return true;
+  }
+  return false;
+}
+
+// ---- autogen (pkg/autogen) ----
+const char* kPodControllers = "DaemonSet,Deployment,Job,StatefulSet,ReplicaSet,ReplicationController,CronJob";
+
+bool autogen_support(bool* needed, const JV* rd) {
+  if (!rd || rd->t != JV::Obj) return true;
+  static const std::set<std::string> pc = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet",
+                                           "ReplicationController", "CronJob", "Pod"};
+  auto kinds = svl(rd->get("kinds"));
+  const JV* ann = rd->get("annotations");
+  const JV* sel = rd->get("selector");
+  if (!sv(rd->get("name")).empty() || !svl(rd->get("names")).empty() || (sel && sel->t != JV::Null) ||
+      (ann && ann->t != JV::Null) || (kinds.size() > 1 && contains_kind(kinds, "Pod")))
+    return false;
+  for (auto& k : kinds)
+    if (pc.count(k)) *needed = true;
+  return true;
+}
+bool can_autogen(const JV& spec) {
+  bool needed = false;
+  const JV* rules = spec.get("rules");
+  if (!rules || rules->t != JV::Arr) return false;
+  for (auto& r : rules->a) {
+    const JV* mut = r.get("mutate");
+    if (mut && !sv(mut->get("patchesJson6902")).empty()) return false;
+    if (nonempty(r.get("generate"))) return false;
+    if (mut && mut->get("foreach") && mut->get("foreach")->t == JV::Arr)
+      for (auto& fe : mut->get("foreach")->a)
+        if (!sv(fe.get("patchesJson6902")).empty()) return false;
+    const JV* m = r.get("match");
+    const JV* x = r.get("exclude");
+    if (!autogen_support(&needed, m ? m->get("resources") : nullptr)) return false;
+    if (!autogen_support(&needed, x ? x->get("resources") : nullptr)) return false;
+    for (const JV* blk : {m, x}) {
+      if (!blk) continue;
+      for (const char* k : {"any", "all"}) {
+        const JV* l = blk->get(k);
+        if (l && l->t == JV::Arr)
+          for (auto& f : l->a)
+            if (!autogen_support(&needed, f.get("resources"))) return false;
+      }
+    }
+  }
+  return needed;
+}
+std::vector<std::string> block_kinds(const JV* blk) {  // MatchResources.GetKinds
+  std::vector<std::string> k;
+  if (!blk) return k;
+  if (const JV* rd = blk->get("resources"))
+    for (auto& s : svl(rd->get("kinds"))) k.push_back(s);
+  for (const char* key : {"all", "any"}) {
+    const JV* l = blk->get(key);
+    if (l && l->t == JV::Arr)
+      for (auto& f : l->a)
+        if (const JV* r = f.get("resources"))
+          for (auto& s : svl(r->get("kinds"))) k.push_back(s);
+  }
+  return k;
+}
+std::string autogen_name(const std::string& prefix, const std::string& name) {
+  std::string n = prefix + "-" + name;
+  return n.size() > 63 ? n.substr(0, 63) : n;
+}
+bool is_autogen_name(const std::string& n) { return n.compare(0, 8, "autogen-") == 0; }
+
+bool generate_rule(JV& out, const std::string& name, const JV& rule, const char* tpl,
+                   const std::vector<std::string>& kinds, bool all_filters) {
+  out = rule;
+  out.set("name", JV::str(name));
+  auto grf = [&](JV& list) {
+    for (auto& f : list.a) {
+      JV* rd = f.getm("resources");
+      if (!rd) continue;
+      if (all_filters || contains_kind(svl(rd->get("kinds")), "Pod")) rd->set("kinds", JV::strs(kinds));
+    }
+  };
+  for (const char* bk : {"match", "exclude"}) {
+    bool is_match = !strcmp(bk, "match");
+    JV* blk = out.getm(bk);
+    if (!blk || blk->t != JV::Obj) {
+      if (is_match) {
+        JV m = JV::obj(), rd = JV::obj();
+        rd.set("kinds", JV::strs(kinds));
+        m.set("resources", rd);
+        out.set(bk, m);
+      }
+      continue;
+    }
+    JV* any = blk->getm("any");
+    JV* all = blk->getm("all");
+    if (any && any->t == JV::Arr && !any->a.empty()) grf(*any);
+    else if (all && all->t == JV::Arr && !all->a.empty()) grf(*all);
+    else {
+      JV* rd = blk->getm("resources");
+      if (is_match) {
+        if (!rd) {
+          blk->set("resources", JV::obj());
+          rd = blk->getm("resources");
+        }
+        rd->set("kinds", JV::strs(kinds));
+      } else if (rd && !svl(rd->get("kinds")).empty()) {
+        rd->set("kinds", JV::strs(kinds));
+      }
+    }
+  }
+  const JV* val = rule.get("validate");
+  auto wrap = [&](const JV& target) {
+    JV inner = JV::obj(), outer = JV::obj();
+    inner.set(tpl, target);
+    outer.set("spec", inner);
+    return outer;
+  };
+  JV nv = JV::obj();
+  if (val && val->get("message")) nv.set("message", *val->get("message"));
+  auto present = [&](const char* k) { return val && val->get(k) && val->get(k)->t != JV::Null; };
+  if (present("pattern")) nv.set("pattern", wrap(*val->get("pattern")));
+  else if (present("deny")) nv.set("deny", *val->get("deny"));
+  else if (present("podSecurity")) nv.set("podSecurity", *val->get("podSecurity"));
+  else if (val && val->get("anyPattern") && val->get("anyPattern")->t == JV::Arr) {
+    JV arr;
+    arr.t = JV::Arr;
+    for (auto& p : val->get("anyPattern")->a) arr.a.push_back(wrap(p));
+    nv.set("anyPattern", arr);
+  } else if (val && val->get("foreach") && val->get("foreach")->t == JV::Arr && !val->get("foreach")->a.empty())
+    nv.set("foreach", *val->get("foreach"));
+  else
+    return false;
+  out.set("validate", nv);
+  return true;
+}
+bool gen_for_controllers(JV& out, const JV& rule, const std::string& controllers) {
+  std::string name = sv(rule.get("name"));
+  if (is_autogen_name(name) || controllers.empty()) return false;
+  auto mk = block_kinds(rule.get("match"));
+  auto xk = block_kinds(rule.get("exclude"));
+  if (!contains_kind(mk, "Pod") || (!xk.empty() && !contains_kind(xk, "Pod"))) return false;
+  static const std::set<std::string> valid = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet",
+                                              "ReplicationController"};
+  std::vector<std::string> kinds;
+  if (controllers == "all") kinds = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController"};
+  else {
+    for (auto& c : split(controllers, ','))
+      if (valid.count(c)) kinds.push_back(c);
+    if (kinds.empty()) kinds = split(controllers, ',');
+  }
+  return generate_rule(out, autogen_name("autogen", name), rule, "template", kinds, false);
+}
+std::string replace_all(std::string s, const std::string& a, const std::string& b) {
+  size_t p = 0;
+  while ((p = s.find(a, p)) != std::string::npos) {
+    s.replace(p, a.size(), b);
+    p += b.size();
+  }
+  return s;
+}
+JV convert_rule(const JV& r, bool cron) {  // autogen.go updateGenRuleByte
+  std::string s;
+  write(r, s);
+  std::string mid = cron ? "spec.jobTemplate.spec.template." : "spec.template.";
+  for (const char* o : {"request.object.", "request.oldObject."}) {
+    s = replace_all(s, std::string(o) + "spec", std::string(o) + mid + "spec");
+    s = replace_all(s, std::string(o) + "metadata", std::string(o) + mid + "metadata");
+  }
+  return parse_all(s.data(), s.size());
+}
+std::vector<JV> compute_rules(const JV& policy) {
+  const JV* spec = policy.get("spec");
+  std::vector<JV> orig;
+  if (spec && spec->get("rules") && spec->get("rules")->t == JV::Arr) orig = spec->get("rules")->a;
+  if (!spec) return orig;
+  bool apply = can_autogen(*spec);
+  std::string controllers = apply ? kPodControllers : "none";
+  const JV* meta = policy.get("metadata");
+  const JV* ann = meta ? meta->get("annotations") : nullptr;
+  const JV* ac = ann ? ann->get("pod-policies.kyverno.io/autogen-controllers") : nullptr;
+  if (ac && apply) controllers = sv(ac);
+  if (controllers == "none") return orig;
+  std::string nocron;
+  for (auto& c : split(controllers, ','))
+    if (c != "CronJob") nocron += (nocron.empty() ? "" : ",") + c;
+  std::vector<JV> gen;
+  for (auto& r : orig) {
+    JV g;
+    if (gen_for_controllers(g, r, nocron)) gen.push_back(convert_rule(g, false));
+    if (controllers.find("CronJob") != std::string::npos || controllers.find("all") != std::string::npos) {
+      JV inter;
+      if (gen_for_controllers(inter, r, controllers)) {
+        JV g2;
+        if (generate_rule(g2, autogen_name("autogen-cronjob", sv(r.get("name"))), inter, "jobTemplate",
+                          {"CronJob"}, true))
+          gen.push_back(convert_rule(g2, true));
+      }
+    }
+  }
+  if (gen.empty()) return orig;
+  std::vector<JV> out;
+  for (auto& r : orig)
+    if (!is_autogen_name(sv(r.get("name")))) out.push_back(r);
+  for (auto& g : gen) out.push_back(g);
+  return out;
+}
+
+// ---- lowering ----
+class Lowerer {
+ public:
+  explicit Lowerer(Program& p) : P(p) {}
+
+  int32_t pred(uint32_t domain, std::vector<std::string> globs) {
+    for (size_t i = 0; i < P.preds.size(); ++i)
+      if (P.preds[i].domain == domain && P.preds[i].globs == globs) return (int32_t)i;
+    P.preds.push_back({domain, std::move(globs)});
+    return (int32_t)P.preds.size() - 1;
+  }
+  static std::string glob_escape_check(const std::string& lit) {
+    if (lit.find('*') != std::string::npos || lit.find('?') != std::string::npos)
+      throw CompileError("literal namespace contains wildcard characters");
+    return lit;
+  }
+
+  void pss_preds() {
+    auto& s = P.pss;
+    if (s.apparmor_key >= 0) return;
+    s.apparmor_key = pred(D_ANNK, {"container.apparmor.security.beta.kubernetes.io/*"});
+    s.apparmor_val_ok = pred(D_ANNV, {"runtime/default", "localhost/*"});
+    s.seccomp_pod_key = pred(D_ANNK, {"seccomp.security.alpha.kubernetes.io/pod"});
+    s.seccomp_ann_ok = pred(D_ANNV, {"runtime/default", "docker/default", "localhost/*"});
+    s.caps_baseline_ok = pred(D_CAP, {"AUDIT_WRITE", "CHOWN", "DAC_OVERRIDE", "FOWNER", "FSETID", "KILL", "MKNOD",
+                                      "NET_BIND_SERVICE", "SETFCAP", "SETGID", "SETPCAP", "SETUID", "SYS_CHROOT"});
+    s.cap_nbs = pred(D_CAP, {"NET_BIND_SERVICE"});
+    s.cap_all = pred(D_CAP, {"ALL"});
+    std::vector<std::string> v10 = {"kernel.shm_rmid_forced", "net.ipv4.ip_local_port_range",
+                                    "net.ipv4.ip_unprivileged_port_start", "net.ipv4.tcp_syncookies",
+                                    "net.ipv4.ping_group_range"};
+    std::vector<std::string> v127 = v10;
+    v127.push_back("net.ipv4.ip_local_reserved_ports");
+    std::vector<std::string> v129 = v127;
+    for (auto n : {"net.ipv4.tcp_keepalive_time", "net.ipv4.tcp_fin_timeout", "net.ipv4.tcp_keepalive_intvl",
+                   "net.ipv4.tcp_keepalive_probes"})
+      v129.push_back(n);
+    s.sysctl[0] = pred(D_SYSCTL, v10);
+    s.sysctl[1] = pred(D_SYSCTL, v127);
+    s.sysctl[2] = pred(D_SYSCTL, v129);
+  }
+
+  // one filter block -> terms; returns filter index
+  uint32_t filter(const JV* rd, bool has_userinfo, bool is_exclude) {
+    KpeFilter f{(uint32_t)P.terms.size(), 0};
+    auto push = [&](KpeTerm t) {
+      P.terms.push_back(t);
+      f.nterms++;
+    };
+    bool rd_empty = !nonempty(rd);
+    if (!is_exclude) {
+      // userInfo is cleared for empty admission info (utils/match.go:263-265)
+      if (rd_empty) push({T_FALSE, 0, 0, 0});  // "match cannot be empty"
+    } else {
+      if (rd_empty && !has_userinfo) push({T_FALSE, 0, 0, 0});  // filter never excludes
+      if (has_userinfo) push({T_FALSE, 0, 0, 0});  // empty admission info never satisfies userInfo
+    }
+    if (!rd_empty) {
+      auto ops = svl(rd->get("operations"));
+      if (!ops.empty() && std::find(ops.begin(), ops.end(), "CREATE") == ops.end()) push({T_FALSE, 0, 0, 0});
+      auto kinds = svl(rd->get("kinds"));
+      if (!kinds.empty()) {
+        uint32_t k0 = (uint32_t)P.kindsels.size();
+        for (auto& k : kinds) {
+          KindSel s = parse_kind_selector(k);
+          KpeKindSel ks;
+          ks.pg = s.g == "*" ? -1 : pred(D_GROUP, {s.g});
+          ks.pv = s.v == "*" ? -1 : pred(D_VERSION, {s.v});
+          ks.pk = s.k == "*" ? -1 : pred(D_KIND, {s.k});
+          ks.sub_ok = glob_host(s.sub, "") ? 1u : 0u;
+          P.kindsels.push_back(ks);
+        }
+        push({T_KINDS, k0, (uint32_t)kinds.size(), 0});
+      }
+      std::string name = sv(rd->get("name"));
+      if (!name.empty()) push({T_PRED, (uint32_t)pred(D_NAME, {name}), COL_NAME, 0});
+      auto names = svl(rd->get("names"));
+      if (!names.empty()) push({T_PRED, (uint32_t)pred(D_NAME, names), COL_NAME, 0});
+      auto nss = svl(rd->get("namespaces"));
+      if (!nss.empty()) push({T_PRED, (uint32_t)pred(D_NS, nss), COL_MNS, 0});
+      const JV* ann = rd->get("annotations");
+      if (ann && ann->t == JV::Obj && !ann->o.empty()) {
+        uint32_t a0 = (uint32_t)P.annpairs.size();
+        for (auto& kv : ann->o) P.annpairs.push_back({pred(D_ANNK, {kv.first}), pred(D_ANNV, {sv(&kv.second)})});
+        push({T_ANNOTATIONS, a0, (uint32_t)ann->o.size(), 0});
+      }
+      const JV* sel = rd->get("selector");
+      if (sel && sel->t != JV::Null) throw CompileError("label selectors in match/exclude are not supported yet");
+      const JV* nsel = rd->get("namespaceSelector");
+      if (nsel && nsel->t != JV::Null)
+        throw CompileError("namespaceSelector in match/exclude is not supported yet");
+    }
+    P.filters.push_back(f);
+    return (uint32_t)P.filters.size() - 1;
+  }
+  static bool has_ui(const JV* f) {
+    if (!f) return false;
+    for (const char* k : {"roles", "clusterRoles", "subjects"})
+      if (nonempty(f->get(k))) return true;
+    return false;
+  }
+  void block(const JV* blk, bool is_exclude, uint32_t* mode, uint32_t* f0, uint32_t* nf) {
+    *f0 = (uint32_t)P.filters.size();
+    const JV* any = blk ? blk->get("any") : nullptr;
+    const JV* all = blk ? blk->get("all") : nullptr;
+    if (any && any->t == JV::Arr && !any->a.empty()) {
+      *mode = MODE_ANY;
+      for (auto& f : any->a) filter(f.get("resources"), has_ui(&f), is_exclude);
+    } else if (all && all->t == JV::Arr && !all->a.empty()) {
+      *mode = MODE_ALL;
+      for (auto& f : all->a) filter(f.get("resources"), has_ui(&f), is_exclude);
+    } else {
+      *mode = MODE_LEGACY;
+      filter(blk ? blk->get("resources") : nullptr, has_ui(blk), is_exclude);
+    }
+    *nf = (uint32_t)P.filters.size() - *f0;
+  }
+
+  static uint32_t cv_mask(const std::string& level, const std::string& version, bool* ok) {
+    // pss.ParseVersion + evaluatePSS version selection, folded at compile time.
+    bool latest = version.empty() || version == "latest";
+    int minor = 0;
+    *ok = true;
+    if (!latest) {
+      if (version.size() < 4 || version.compare(0, 3, "v1.") != 0) *ok = false;
+      std::string mi = *ok ? version.substr(3) : "";
+      if (mi.empty() || mi.size() > 9 || (mi.size() > 1 && mi[0] == '0')) *ok = false;
+      for (char ch : mi)
+        if (ch < '0' || ch > '9') *ok = false;
+      if (!*ok) return 0;
+      minor = atoi(mi.c_str());
+    }
+    bool baseline = level == "baseline";
+    struct VC {
+      int check;
+      bool restricted;
+      std::vector<std::pair<int, int>> versions;  // (minor, cv)
+    };
+    static const std::vector<VC> table = {
+        {CK_APE, true, {{8, CV_APE_1_8}, {25, CV_APE_1_25}}},
+        {CK_APPARMOR, false, {{0, CV_APPARMOR_1_0}}},
+        {CK_CAPS_BASELINE, false, {{0, CV_CAPS_BASELINE_1_0}}},
+        {CK_CAPS_RESTRICTED, true, {{22, CV_CAPS_RESTRICTED_1_22}, {25, CV_CAPS_RESTRICTED_1_25}}},
+        {CK_HOST_NS, false, {{0, CV_HOST_NS_1_0}}},
+        {CK_HOST_PATH, false, {{0, CV_HOST_PATH_1_0}}},
+        {CK_HOST_PORTS, false, {{0, CV_HOST_PORTS_1_0}}},
+        {CK_PRIVILEGED, false, {{0, CV_PRIVILEGED_1_0}}},
+        {CK_PROC_MOUNT, false, {{0, CV_PROC_MOUNT_1_0}}},
+        {CK_RESTRICTED_VOLUMES, true, {{0, CV_RESTRICTED_VOLUMES_1_0}}},
+        {CK_RUN_AS_NON_ROOT, true, {{0, CV_RUN_AS_NON_ROOT_1_0}}},
+        {CK_RUN_AS_USER, true, {{23, CV_RUN_AS_USER_1_23}}},
+        {CK_SELINUX, false, {{0, CV_SELINUX_1_0}}},
+        {CK_SECCOMP_BASELINE, false, {{0, CV_SECCOMP_BASELINE_1_0}, {19, CV_SECCOMP_BASELINE_1_19}}},
+        {CK_SECCOMP_RESTRICTED, true, {{19, CV_SECCOMP_RESTRICTED_1_19}, {25, CV_SECCOMP_RESTRICTED_1_25}}},
+        {CK_SYSCTLS, false, {{0, CV_SYSCTLS_1_0}, {27, CV_SYSCTLS_1_27}, {29, CV_SYSCTLS_1_29}}},
+        {CK_WIN_HOST_PROCESS, false, {{0, CV_WIN_HOST_PROCESS_1_0}}},
+    };
+    uint32_t m = 0;
+    for (auto& c : table) {
+      if (baseline && c.restricted) continue;  // level "privileged"/other: every check runs
+      if (latest) {
+        m |= 1u << c.versions.back().second;  // newest MinimumVersion
+      } else {
+        for (auto& v : c.versions)
+          if (v.first <= minor) m |= 1u << v.second;
+      }
+    }
+    return m;
+  }
+
+  void rule(const JV& r, uint32_t policy, bool apply_one, const std::string& pol_name, bool namespaced,
+            const std::string& pol_ns) {
+    KpeRule k{};
+    k.policy = policy;
+    k.apply_one = apply_one ? 1u : 0u;
+    k.pol_ns_pred = -1;
+    block(r.get("match"), false, &k.match_mode, &k.match_f0, &k.match_nf);
+    block(r.get("exclude"), true, &k.excl_mode, &k.excl_f0, &k.excl_nf);
+    if (namespaced || !pol_ns.empty()) {
+      if (namespaced && pol_ns.empty()) {  // checkNamespacedPolicy can never pass
+        k.match_f0 = (uint32_t)P.filters.size();
+        P.filters.push_back({(uint32_t)P.terms.size(), 1});
+        P.terms.push_back({T_FALSE, 0, 0, 0});
+        k.match_nf = 1;
+        k.match_mode = MODE_LEGACY;
+      } else {
+        k.pol_ns_pred = pred(D_NS, {glob_escape_check(pol_ns)});
+      }
+    }
+    const JV* v = r.get("validate");
+    bool has_validate = nonempty(v);
+    const JV* ps = v ? v->get("podSecurity") : nullptr;
+    std::string rname = sv(r.get("name"));
+    if (!has_validate) {
+      k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
+      if (nonempty(r.get("verifyImages"))) throw CompileError("rule '" + rname + "': verifyImages is not supported");
+    } else if (nonempty(v->get("manifests"))) {
+      throw CompileError("rule '" + rname + "': validate.manifests is not supported");
+    } else if (ps && ps->t == JV::Obj && nonempty(ps)) {
+      if (nonempty(r.get("preconditions")) || nonempty(r.get("context")))
+        throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
+      const JV* ex = ps->get("exclude");
+      if (ex && ex->t == JV::Arr && !ex->a.empty())
+        throw CompileError("rule '" + rname + "': podSecurity.exclude is not supported on the device yet");
+      bool ok;
+      k.cv_mask = cv_mask(sv(ps->get("level")), sv(ps->get("version")), &ok);
+      k.handler = ok ? H_PSS : H_ERROR;
+      pss_preds();
+      P.any_pss = true;
+      P.cv_union |= k.cv_mask;
+    } else {
+      throw CompileError("rule '" + rname + "': only podSecurity validate rules are supported on the device yet");
+    }
+    P.rules.push_back(k);
+    P.rule_names.push_back(pol_name + "/" + rname);
+  }
+
+ private:
+  Program& P;
+};
+
+}  // namespace
+
+Program::~Program() = default;
+
+std::unique_ptr<Program> compile_policies(const char* json, size_t len) {
+  JV root = parse_all(json, len);
+  std::vector<const JV*> pols;
+  if (root.t == JV::Arr)
+    for (auto& p : root.a) pols.push_back(&p);
+  else
+    pols.push_back(&root);
+  auto prog = std::make_unique<Program>();
+  Lowerer L(*prog);
+  for (size_t pi = 0; pi < pols.size(); ++pi) {
+    const JV& p = *pols[pi];
+    if (p.t != JV::Obj) throw std::invalid_argument("policy is not an object");
+    const JV* meta = p.get("metadata");
+    std::string name = meta ? sv(meta->get("name")) : "";
+    std::string ns = meta ? sv(meta->get("namespace")) : "";
+    bool namespaced = sv(p.get("kind")) == "Policy";
+    const JV* spec = p.get("spec");
+    bool apply_one = spec && sv(spec->get("applyRules")) == "One";
+    for (auto& r : compute_rules(p)) L.rule(r, (uint32_t)pi, apply_one, name, namespaced, ns);
+  }
+  return prog;
+}
+
+}  // namespace kpe

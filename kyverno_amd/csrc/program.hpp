@@ -1,0 +1,48 @@
+// Compiled policy set: rules after autogen, lowered to the device program
+// (schema.h KpeRule/KpeFilter/KpeTerm tables) plus the string predicates the
+// device evaluates over the corpus dictionaries.
+#pragma once
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "schema.h"
+
+namespace kpe {
+
+struct Pred {
+  uint32_t domain;
+  std::vector<std::string> globs;  // OR of go-wildcard patterns
+};
+
+// Fixed predicate slots used by the PSS kernel (indices into Program::preds).
+struct PssPreds {
+  int32_t apparmor_key = -1, apparmor_val_ok = -1, seccomp_pod_key = -1, seccomp_ann_ok = -1;
+  int32_t caps_baseline_ok = -1, cap_nbs = -1, cap_all = -1;
+  int32_t sysctl[3] = {-1, -1, -1};  // 1.0, 1.27, 1.29 allow-lists
+};
+
+struct DeviceProgram;  // kpe_api.cpp
+
+struct Program {
+  std::vector<std::string> rule_names;  // "<policy>/<rule>"
+  std::vector<KpeRule> rules;
+  std::vector<KpeFilter> filters;
+  std::vector<KpeTerm> terms;
+  std::vector<KpeKindSel> kindsels;
+  std::vector<KpeAnnPair> annpairs;
+  std::vector<Pred> preds;
+  PssPreds pss;
+  uint32_t cv_union = 0;  // union of cv_mask over rules
+  bool any_pss = false;
+  DeviceProgram* dev = nullptr;
+  ~Program();
+};
+
+// Throws CompileError (unsupported construct) or std::invalid_argument (bad JSON).
+struct CompileError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+std::unique_ptr<Program> compile_policies(const char* json, size_t len);
+
+}  // namespace kpe

@@ -1,0 +1,257 @@
+// Columnar encoding shared by the host flattener and the CDNA4 kernels.
+//
+// One resource = one row. String fields are dictionary-encoded per domain
+// (kpe::Dict); enum-typed K8s fields with a closed set of legal values are
+// stored as small codes (+ an OTHER code) in packed words; free-form strings a
+// rule may need verbatim stay as dictionary ids in "cold" columns that only the
+// exclusion/message paths read. All evaluation (which values are allowed, per
+// check and per PSS version, glob/prefix predicates, match/exclude) happens on
+// the device; the host only encodes.
+#pragma once
+#include <stdint.h>
+
+// ---- string domains ------------------------------------------------------------
+enum KpeDomain {
+  D_GROUP = 0,   // apiVersion group ("" for core)
+  D_VERSION,     // apiVersion version
+  D_KIND,        // kind
+  D_NAME,        // metadata.name, or metadata.generateName when name is empty (utils/match.go:78-81)
+  D_NS,          // metadata.namespace (and the name of Namespace objects, utils/match.go:18-22)
+  D_LABK,        // metadata.labels keys
+  D_LABV,        // metadata.labels values
+  D_ANNK,        // annotation keys (resource metadata and pod-template metadata)
+  D_ANNV,        // annotation values
+  D_CAP,         // capability names (<= 64 distinct per corpus: masks are u64)
+  D_SYSCTL,      // pod securityContext.sysctls[].name
+  D_IMAGE,       // container images
+  D_CNAME,       // container names
+  D_MISC,        // seccomp type / procMount / seLinux strings (cold, exclusions)
+  KPE_NUM_DOMAINS
+};
+
+#define KPE_NO_STR 0xFFFFFFFFu
+
+// ---- resource word r_flags -------------------------------------------------------
+#define R_CLASS_MASK 0x3u      // PSS spec class: validate_pss.go:137-188
+#define R_CLASS_POD 0u
+#define R_CLASS_CONTROLLER 1u  // DaemonSet, Deployment, Job, StatefulSet, ReplicaSet, ReplicationController
+#define R_CLASS_CRONJOB 2u
+#define R_CLASS_OTHER 3u       // "could not find correct resource type" => RuleError
+#define R_DECODE_ERR (1u << 2) // typed json.Unmarshal would fail => RuleError
+#define R_IS_NAMESPACE (1u << 3)
+#define R_LABELS_NIL (1u << 4)  // unstructured NestedStringMap failed => nil map
+#define R_ANNOT_NIL (1u << 5)
+
+// r_gvk = kind_id | version_id << 12 | group_id << 22
+#define GVK_KIND(x) ((x) & 0xFFFu)
+#define GVK_VER(x) (((x) >> 12) & 0x3FFu)
+#define GVK_GRP(x) ((x) >> 22)
+
+// ---- tri-state / enum codes ----------------------------------------------------
+#define TRI_UNSET 0u
+#define TRI_FALSE 1u
+#define TRI_TRUE 2u
+#define RAU_UNSET 0u
+#define RAU_NONZERO 1u
+#define RAU_ZERO 2u
+#define SECCOMP_NONE 0u        // seccompProfile == nil
+#define SECCOMP_RUNTIMEDEFAULT 1u
+#define SECCOMP_LOCALHOST 2u
+#define SECCOMP_UNCONFINED 3u
+#define SECCOMP_OTHER 4u       // any other type string (incl. "")
+#define PROCMOUNT_UNSET 0u
+#define PROCMOUNT_DEFAULT 1u
+#define PROCMOUNT_OTHER 2u
+#define SEL_NONE 0u            // seLinuxOptions == nil
+#define SEL_EMPTY 1u           // type ""
+#define SEL_CONTAINER_T 2u
+#define SEL_CONTAINER_INIT_T 3u
+#define SEL_CONTAINER_KVM_T 4u
+#define SEL_OTHER 5u
+#define OS_NONE 0u
+#define OS_WINDOWS 1u
+#define OS_OTHER 2u
+
+// ---- pod word p_sc (pod-level securityContext and spec flags) ---------------------
+#define P_SC_PRESENT (1u << 0)
+#define P_HOSTNET (1u << 1)
+#define P_HOSTPID (1u << 2)
+#define P_HOSTIPC (1u << 3)
+#define P_RNR_SH 4      // tri
+#define P_RAU_SH 6      // RAU_*
+#define P_SECCOMP_SH 8  // 3 bits
+#define P_SEL_SH 11     // 3 bits
+#define P_SEL_USER (1u << 14)
+#define P_SEL_ROLE (1u << 15)
+#define P_WHP_SH 16     // tri
+#define P_OS_SH 18      // OS_*
+#define FIELD(w, sh, bits) (((w) >> (sh)) & ((1u << (bits)) - 1u))
+
+// ---- container word c_sc -----------------------------------------------------------
+#define C_SC_PRESENT (1u << 0)
+#define C_PRIV_SH 1        // tri
+#define C_APE_SH 3         // tri
+#define C_RNR_SH 5         // tri
+#define C_RAU_SH 7         // RAU_*
+#define C_SECCOMP_SH 9     // 3 bits
+#define C_PROCMOUNT_SH 12  // 2 bits
+#define C_SEL_SH 14        // 3 bits
+#define C_SEL_USER (1u << 17)
+#define C_SEL_ROLE (1u << 18)
+#define C_WHP_SH 19        // tri
+#define C_CAPS_PRESENT (1u << 21)
+#define C_TYPE_SH 22       // 0 initContainers, 1 containers, 2 ephemeralContainers
+#define C_HOSTPORT_SH 24   // 4 bits: number of ports with hostPort != 0 (saturating at 15)
+
+// ---- volumes: vol_src bit i = corev1.VolumeSource field i present (declaration order) ----
+#define KPE_NUM_VOLUME_SOURCES 29
+#define VS_HOSTPATH 0
+#define VS_EMPTYDIR 1
+#define VS_GCEPD 2
+#define VS_AWSEBS 3
+#define VS_GITREPO 4
+#define VS_SECRET 5
+#define VS_NFS 6
+#define VS_ISCSI 7
+#define VS_GLUSTERFS 8
+#define VS_PVC 9
+#define VS_RBD 10
+#define VS_FLEXVOLUME 11
+#define VS_CINDER 12
+#define VS_CEPHFS 13
+#define VS_FLOCKER 14
+#define VS_DOWNWARDAPI 15
+#define VS_FC 16
+#define VS_AZUREFILE 17
+#define VS_CONFIGMAP 18
+#define VS_VSPHERE 19
+#define VS_QUOBYTE 20
+#define VS_AZUREDISK 21
+#define VS_PHOTONPD 22
+#define VS_PROJECTED 23
+#define VS_PORTWORX 24
+#define VS_SCALEIO 25
+#define VS_STORAGEOS 26
+#define VS_CSI 27
+#define VS_EPHEMERAL 28
+
+// ---- PSA checks (bit k of a check mask), policy.DefaultChecks() order ----------------------
+enum KpeCheck {
+  CK_APE = 0,            // allowPrivilegeEscalation
+  CK_APPARMOR,           // appArmorProfile
+  CK_CAPS_BASELINE,      // capabilities_baseline
+  CK_CAPS_RESTRICTED,    // capabilities_restricted
+  CK_HOST_NS,            // hostNamespaces
+  CK_HOST_PATH,          // hostPathVolumes
+  CK_HOST_PORTS,         // hostPorts
+  CK_PRIVILEGED,         // privileged
+  CK_PROC_MOUNT,         // procMount
+  CK_RESTRICTED_VOLUMES, // restrictedVolumes
+  CK_RUN_AS_NON_ROOT,    // runAsNonRoot
+  CK_RUN_AS_USER,        // runAsUser
+  CK_SELINUX,            // seLinuxOptions
+  CK_SECCOMP_BASELINE,   // seccompProfile_baseline
+  CK_SECCOMP_RESTRICTED, // seccompProfile_restricted
+  CK_SYSCTLS,            // sysctls
+  CK_WIN_HOST_PROCESS,   // windowsHostProcess
+  KPE_NUM_CHECKS
+};
+
+// ---- versioned check functions (bit v of a rule's cv_mask) --------------------------------
+enum KpeCheckVersion {
+  CV_APE_1_8 = 0,
+  CV_APE_1_25,
+  CV_APPARMOR_1_0,
+  CV_CAPS_BASELINE_1_0,
+  CV_CAPS_RESTRICTED_1_22,
+  CV_CAPS_RESTRICTED_1_25,
+  CV_HOST_NS_1_0,
+  CV_HOST_PATH_1_0,
+  CV_HOST_PORTS_1_0,
+  CV_PRIVILEGED_1_0,
+  CV_PROC_MOUNT_1_0,
+  CV_RESTRICTED_VOLUMES_1_0,
+  CV_RUN_AS_NON_ROOT_1_0,
+  CV_RUN_AS_USER_1_23,
+  CV_SELINUX_1_0,
+  CV_SECCOMP_BASELINE_1_0,
+  CV_SECCOMP_BASELINE_1_19,
+  CV_SECCOMP_RESTRICTED_1_19,
+  CV_SECCOMP_RESTRICTED_1_25,
+  CV_SYSCTLS_1_0,
+  CV_SYSCTLS_1_27,
+  CV_SYSCTLS_1_29,
+  CV_WIN_HOST_PROCESS_1_0,
+  KPE_NUM_CV
+};
+
+// ---- per-container derived violation bits (device-internal) ------------------------------------
+#define CB_APE (1u << 0)            // sc nil || ape nil || ape true
+#define CB_CAPS_BASE (1u << 1)      // caps present && add has a non-baseline capability
+#define CB_CAPS_DROP (1u << 2)      // caps nil || drop lacks "ALL"
+#define CB_CAPS_ADD (1u << 3)       // add has something other than NET_BIND_SERVICE
+#define CB_HOSTPORT (1u << 4)
+#define CB_PRIV (1u << 5)
+#define CB_PROCMOUNT (1u << 6)
+#define CB_RNR_FALSE (1u << 7)      // runAsNonRoot explicitly false
+#define CB_RNR_UNSET (1u << 8)
+#define CB_RAU_ZERO (1u << 9)
+#define CB_SELINUX (1u << 10)
+#define CB_SEC_BAD (1u << 11)       // seccomp set and not RuntimeDefault/Localhost
+#define CB_SEC_UNSET (1u << 12)
+#define CB_SEC_ANN (1u << 13)       // container seccomp annotation with a forbidden value (1.0)
+#define CB_WHP (1u << 14)
+
+// ---- verdict cells (same values as kpe.h enum kpe_verdict) ----
+#define KPE_NA_ 0
+#define KPE_PASS_ 1
+#define KPE_FAIL_ 2
+#define KPE_WARN_ 3
+#define KPE_ERROR_ 4
+#define KPE_SKIP_ 5
+
+// ---- policy program ------------------------------------------------------------------------------
+// Rule handlers
+#define H_NONE 0u  // no validate handler => no RuleResponse (NA even when matched)
+#define H_PSS 1u
+#define H_ERROR 2u  // every matching resource gets RuleStatusError (e.g. unparsable PSS version)
+
+// Match terms (AND inside a filter block)
+enum KpeTermType {
+  T_FALSE = 0,     // constant false ("match cannot be empty", operations w/o CREATE, user info on exclude)
+  T_KINDS = 1,     // OR over kind selectors [a, a+b) in the selector table
+  T_PRED = 2,      // bit lookup: predicate a over the resource column named by b (KpeCol)
+  T_ANNOTATIONS = 3,  // every pair [a, a+b) of the annotation-pair table must be matched by some annotation
+  T_SELECTOR = 4,     // label selector a (selector table) over resource labels
+  T_NSSELECTOR = 5    // label selector a over the namespace's labels (not for kind Namespace)
+};
+enum KpeCol { COL_NAME = 0, COL_MNS = 1, COL_NSA = 2 };
+
+typedef struct KpeTerm {
+  uint32_t type, a, b, pad;
+} KpeTerm;
+typedef struct KpeKindSel {
+  int32_t pg, pv, pk;  // predicate ids over D_GROUP/D_VERSION/D_KIND, -1 = always true ("*")
+  uint32_t sub_ok;     // wildcard.Match(sub, "") (no subresources in background/CLI scans)
+} KpeKindSel;
+typedef struct KpeAnnPair {
+  int32_t pk, pv;  // predicates over D_ANNK / D_ANNV
+} KpeAnnPair;
+typedef struct KpeFilter {
+  uint32_t term0, nterms;
+} KpeFilter;
+
+#define MODE_LEGACY 0u
+#define MODE_ANY 1u
+#define MODE_ALL 2u
+
+typedef struct KpeRule {
+  uint32_t handler;       // H_*
+  uint32_t cv_mask;       // PSS: versioned checks to run (version selection done at compile time)
+  uint32_t match_mode, match_f0, match_nf;    // filters [f0, f0+nf)
+  uint32_t excl_mode, excl_f0, excl_nf;
+  int32_t pol_ns_pred;    // -1 or predicate over D_NS (actual ns) that must hold (policy namespace)
+  uint32_t policy;        // policy index (ApplyOne grouping)
+  uint32_t apply_one;     // spec.applyRules == One
+  uint32_t pss_excl0, pss_nexcl;  // PSS exclusions (reserved)
+} KpeRule;

@@ -1,0 +1,250 @@
+"""Host-side mirror of the reference engine interface, backed by libkpe.
+
+Reference surface mirrored here (names and meaning kept):
+  engineapi.Engine.Validate(ctx, PolicyContext) EngineResponse   pkg/engine/api/engine.go:17-23
+  engineapi.EngineResponse / PolicyResponse.Rules                pkg/engine/api/engineresponse.go:14-60
+  engineapi.RuleResponse (name, type, status)                    pkg/engine/api/ruleresponse.go:25-60
+  engineapi.RuleStatus pass/fail/warning/error/skip              pkg/engine/api/rulestatus.go:4-21
+  engine.NewPolicyContext(..., Create, ...).WithNewResource(r).WithPolicy(p).WithNamespaceLabels(l)
+                                                                 pkg/controllers/report/utils/scanner.go:99-110
+Single-resource Validate() is served by the same batch kernels (a batch of one);
+batch callers (`kyverno apply`'s resource loop, the background scanner) use
+Engine.validate_batch()/evaluate(), which evaluate the whole resource x rule
+matrix on the GPU in one pass.
+"""
+import ctypes
+import enum
+import json
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from ._lib import Counts, KernelStats, KpeError, check, load
+
+
+class RuleStatus(str, enum.Enum):
+    PASS = "pass"
+    FAIL = "fail"
+    WARN = "warning"
+    ERROR = "error"
+    SKIP = "skip"
+
+
+# kpe_verdict cell codes -> RuleStatus (0 = no RuleResponse)
+VERDICT = {1: RuleStatus.PASS, 2: RuleStatus.FAIL, 3: RuleStatus.WARN, 4: RuleStatus.ERROR, 5: RuleStatus.SKIP}
+
+
+@dataclass
+class RuleResponse:
+    name: str
+    status: RuleStatus
+    rule_type: str = "Validation"
+    pod_security_checks: List[str] = field(default_factory=list)  # failing PSA check IDs (PSS rules)
+
+
+@dataclass
+class EngineResponse:
+    policy: str
+    resource: Optional[dict]
+    rules: List[RuleResponse]
+
+    def is_successful(self):  # engineresponse.go IsSuccessful: no fail/error rule
+        return not any(r.status in (RuleStatus.FAIL, RuleStatus.ERROR) for r in self.rules)
+
+
+@dataclass
+class PolicyContext:
+    """engine.NewPolicyContext(..., kyvernov1.Create, ...) for background/CLI scans."""
+    resource: dict
+    policy: dict
+    namespace_labels: Dict[str, str] = field(default_factory=dict)
+    operation: str = "CREATE"
+
+    def with_new_resource(self, r):
+        self.resource = r
+        return self
+
+    def with_policy(self, p):
+        self.policy = p
+        return self
+
+    def with_namespace_labels(self, l):
+        self.namespace_labels = dict(l or {})
+        return self
+
+
+class Device:
+    def __init__(self, ordinal: int = 0):
+        L = load()
+        h = ctypes.c_void_p()
+        check(L.kpe_device_open(int(ordinal), ctypes.byref(h)))
+        self.h, self.ordinal = h, ordinal
+
+    def close(self):
+        if self.h:
+            load().kpe_device_close(self.h)
+            self.h = None
+
+    def sync(self):
+        check(load().kpe_device_sync(self.h))
+
+    def set_timing(self, on: bool):
+        check(load().kpe_device_set_timing(self.h, 1 if on else 0))
+
+    def kernel_stats(self, reset=False):
+        st = KernelStats()
+        check(load().kpe_device_kernel_stats(self.h, None, None, ctypes.byref(st), 1 if reset else 0))
+        return st
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PolicySet:
+    """Compiled policies (autogen applied once, autogen.ComputeRules)."""
+
+    def __init__(self, policies):
+        L = load()
+        if isinstance(policies, (bytes, str)):
+            raw = policies if isinstance(policies, bytes) else policies.encode()
+            self.policies = None
+        else:
+            self.policies = list(policies) if isinstance(policies, (list, tuple)) else [policies]
+            raw = json.dumps(self.policies).encode()
+        h = ctypes.c_void_p()
+        check(L.kpe_program_compile(raw, len(raw), ctypes.byref(h)))
+        self.h = h
+        n = L.kpe_program_num_rules(h)
+        self.rule_names = [L.kpe_program_rule_name(h, i).decode() for i in range(n)]
+        self.is_pss = [bool(L.kpe_program_rule_is_pss(h, i)) for i in range(n)]
+
+    @property
+    def num_rules(self):
+        return len(self.rule_names)
+
+    def __del__(self):
+        try:
+            if self.h:
+                load().kpe_program_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class Corpus:
+    """Flattened, string-interned resources (host columns, optionally on a device)."""
+
+    def __init__(self, resources, namespace_labels: Optional[Dict[str, Dict[str, str]]] = None):
+        L = load()
+        if isinstance(resources, (bytes, bytearray)):
+            raw = bytes(resources)
+        elif isinstance(resources, str):
+            raw = resources.encode()
+        else:
+            raw = "\n".join(json.dumps(r, separators=(",", ":")) for r in resources).encode()
+        nsl = json.dumps(namespace_labels).encode() if namespace_labels else b""
+        h = ctypes.c_void_p()
+        check(L.kpe_corpus_flatten(raw, len(raw), nsl if nsl else None, len(nsl), ctypes.byref(h)))
+        self.h = h
+        self.n = int(L.kpe_corpus_num_resources(h))
+        self.nbytes = int(L.kpe_corpus_bytes(h))
+        self.device = None
+
+    def upload(self, dev: Device):
+        check(load().kpe_corpus_upload(dev.h, self.h))
+        self.device = dev
+        return self
+
+    def __del__(self):
+        try:
+            if self.h:
+                load().kpe_corpus_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def synth_resources(seed: int, n: int, mix: int = 0, first_index: int = 0) -> bytes:
+    """NDJSON from the synthetic generator (include/kpe_synth.h)."""
+    L = load()
+    p = ctypes.c_void_p()
+    ln = ctypes.c_size_t()
+    if L.kpe_synth_resources(seed, first_index, n, mix, ctypes.byref(p), ctypes.byref(ln)) != 0:
+        raise KpeError(-1, "synth failed")
+    try:
+        return ctypes.string_at(p, ln.value)
+    finally:
+        L.kpe_synth_free(p)
+
+
+class Engine:
+    """engineapi.Engine (validate path) on one MI355X."""
+
+    def __init__(self, device: Optional[Device] = None, ordinal: int = 0):
+        self.device = device or Device(ordinal)
+
+    # ---- columnar batch API ----
+    def evaluate(self, ps: PolicySet, corpus: Corpus, check_masks=False):
+        """Verdict matrix (N x R uint8, kpe_verdict), optional PSS check masks, per-rule counts."""
+        L = load()
+        if corpus.device is not self.device:
+            corpus.upload(self.device)
+        N, R = corpus.n, ps.num_rules
+        v = np.zeros((N, R), dtype=np.uint8)
+        m = np.zeros((N, R), dtype=np.uint32) if check_masks else None
+        counts = (Counts * max(R, 1))()
+        check(L.kpe_evaluate(self.device.h, ps.h, corpus.h, v.ctypes.data if N * R else None,
+                             m.ctypes.data if (m is not None and N * R) else None, counts))
+        cnt = [{"na": c.na, "pass": c.pass_, "fail": c.fail, "warn": c.warn, "error": c.error, "skip": c.skip}
+               for c in counts[:R]]
+        return v, m, cnt
+
+    def evaluate_async(self, ps: PolicySet, corpus: Corpus):
+        check(load().kpe_evaluate_async(self.device.h, ps.h, corpus.h))
+
+    # ---- reference-shaped API ----
+    def validate_batch(self, policies: Sequence[dict], resources: Sequence[dict],
+                       namespace_labels: Optional[Dict[str, Dict[str, str]]] = None) -> List[List[EngineResponse]]:
+        """EngineResponse per (resource, policy), rules in ComputeRules order, NA cells omitted."""
+        ps = PolicySet(list(policies))
+        corpus = Corpus(resources, namespace_labels)
+        v, m, _ = self.evaluate(ps, corpus, check_masks=True)
+        L = load()
+        check_ids = [L.kpe_pss_check_id(k).decode() for k in range(17)]
+        # policy boundaries by "<policy>/<rule>" prefix, in compile order
+        spans, start = [], 0
+        for p in policies:
+            cnt = 0
+            for x in ps.rule_names[start:]:
+                if x.split("/", 1)[0] != p["metadata"]["name"]:
+                    break
+                cnt += 1
+            spans.append((start, start + cnt))
+            start += cnt
+        out = []
+        for i, res in enumerate(resources):
+            row = []
+            for (a, b), p in zip(spans, policies):
+                rules = []
+                for r in range(a, b):
+                    cell = int(v[i, r])
+                    if cell == 0:
+                        continue
+                    checks = [check_ids[k] for k in range(17) if (int(m[i, r]) >> k) & 1] if ps.is_pss[r] else []
+                    rules.append(RuleResponse(ps.rule_names[r].split("/", 1)[1], VERDICT[cell],
+                                              pod_security_checks=checks))
+                row.append(EngineResponse(p["metadata"]["name"], res, rules))
+            out.append(row)
+        return out
+
+    def validate(self, policy_context: PolicyContext) -> EngineResponse:
+        """engineapi.Engine.Validate for one PolicyContext (a batch of one)."""
+        nsl = None
+        ns = (policy_context.resource.get("metadata") or {}).get("namespace")
+        if ns and policy_context.namespace_labels:
+            nsl = {ns: policy_context.namespace_labels}
+        return self.validate_batch([policy_context.policy], [policy_context.resource], nsl)[0][0]
