@@ -1,20 +1,29 @@
 // CDNA4 (gfx950) kernels for batch policy evaluation. wave64, HBM-bound scans.
 //
-//  kpe_pred_kernel  — dictionary pass: every string predicate of the compiled
-//                     program (OR of go-wildcard globs, ext/wildcard/match.go:7-9)
-//                     evaluated once per DISTINCT string of its domain; results
-//                     are bitsets (one bit per dictionary id) built with wave ballots.
-//  kpe_scan_kernel  — one resource per lane: match/exclude (pkg/engine/utils/match.go:
-//                     168-300) for every rule, PSS checks (PSA v0.29 policy checks via
-//                     pkg/pss/evaluate.go:24-70) and the verdict cell, with ApplyOne
-//                     (pkg/engine/validation.go:75-77). Containers of the block's
-//                     resources are streamed cooperatively (coalesced) through LDS,
-//                     so the irregular 1..64-container fan-out never diverges the
-//                     HBM loads; per-rule counters are reduced with wave ballots.
+//  kpe_pred_kernel   — dictionary pass for LARGE domains (names, namespaces, ...):
+//                      every string predicate of the compiled program (an OR of
+//                      go-wildcard globs, ext/wildcard/match.go:7-9) is evaluated
+//                      once per DISTINCT string of its domain into a bitset (wave
+//                      ballots, one bit per dictionary id).
+//  kpe_scan_kernel   — one resource per lane. Per block: (1) the compiled program
+//                      and the bitsets of predicates over SMALL domains (kinds,
+//                      capabilities, sysctls, annotation keys/values) are built
+//                      in LDS, so a step is a single launch when no large-domain
+//                      predicate exists; (2) the block's containers are streamed
+//                      coalesced through LDS and OR-reduced per resource (the
+//                      1..64-container fan-out never diverges the HBM loads);
+//                      (3) PSA versioned checks (pkg/pss/evaluate.go:24-70 over
+//                      PSA v0.29 policy/check_*.go); (4) match/exclude per rule
+//                      (pkg/engine/utils/match.go:168-300) with ApplyOne
+//                      (pkg/engine/validation.go:75-77); (5) verdict cells staged
+//                      in LDS and written as coalesced dwords; per-rule counters
+//                      by wave ballot into per-block partials (no atomics, no memset).
+//  kpe_count_reduce  — sums the per-block counter partials (fetch time only).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "schema.h"
+#include "kernels_abi.h"
 
 namespace {
 
@@ -55,179 +64,140 @@ __device__ bool glob(const uint8_t* p, int pn, const uint8_t* s, int sn) {
   return pi == pn;
 }
 
+__device__ __forceinline__ bool match_any(const uint8_t* pat_bytes, const uint32_t* pat_off, uint32_t pat0,
+                                          uint32_t npat, const uint8_t* s, int sn) {
+  for (uint32_t k = 0; k < npat; ++k) {
+    uint32_t p0 = pat_off[pat0 + k], p1 = pat_off[pat0 + k + 1];
+    if (glob(pat_bytes + p0, (int)(p1 - p0), s, sn)) return true;
+  }
+  return false;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------
-struct PredJob {
-  uint32_t domain;
-  uint32_t pat0, npat;      // patterns [pat0, pat0+npat) in the pattern table
-  uint32_t out_word;        // first output word
-  uint32_t blk0;            // first block of this job (exclusive prefix over jobs)
-};
-
-struct PredArgs {
-  const uint8_t* dict_bytes[KPE_NUM_DOMAINS];
-  const uint32_t* dict_off[KPE_NUM_DOMAINS];
-  uint32_t dict_n[KPE_NUM_DOMAINS];
-  const uint8_t* pat_bytes;
-  const uint32_t* pat_off;  // pattern k = pat_bytes[pat_off[k] .. pat_off[k+1])
-  const PredJob* jobs;
-  uint32_t njobs;
-  uint32_t* out;
-};
-
 __global__ void __launch_bounds__(256) kpe_pred_kernel(PredArgs a) {
-  // job lookup: blocks are laid out job-major (uniform per block)
   uint32_t b = blockIdx.x;
   uint32_t j = 0;
-  while (j + 1 < a.njobs && a.jobs[j + 1].blk0 <= b) ++j;
+  while (j + 1 < a.njobs && a.jobs[j + 1].blk0 <= b) ++j;  // uniform per block
   const PredJob job = a.jobs[j];
   uint32_t id = (b - job.blk0) * 256u + threadIdx.x;
   uint32_t n = a.dict_n[job.domain];
   bool hit = false;
   if (id < n) {
     const uint32_t* off = a.dict_off[job.domain];
-    const uint8_t* s = a.dict_bytes[job.domain] + off[id];
-    int sn = (int)(off[id + 1] - off[id]);
-    for (uint32_t k = 0; k < job.npat && !hit; ++k) {
-      uint32_t p0 = a.pat_off[job.pat0 + k], p1 = a.pat_off[job.pat0 + k + 1];
-      hit = glob(a.pat_bytes + p0, (int)(p1 - p0), s, sn);
-    }
+    hit = match_any(a.pat_bytes, a.pat_off, job.pat0, job.npat, a.dict_bytes[job.domain] + off[id],
+                    (int)(off[id + 1] - off[id]));
   }
   uint64_t m = __ballot(hit);
-  uint32_t lane = threadIdx.x & 63u;
   uint32_t wid = id >> 6;  // 64 strings per wave => two output words
-  if (lane == 0 && (uint64_t)wid * 64u < n) {
+  if ((threadIdx.x & 63u) == 0 && (uint64_t)wid * 64u < n) {
     a.out[job.out_word + 2 * wid] = (uint32_t)m;
     a.out[job.out_word + 2 * wid + 1] = (uint32_t)(m >> 32);
   }
 }
 
-// ---------------------------------------------------------------------------
-struct ScanArgs {
-  int64_t n;
-  // resource rows
-  const uint32_t* r_flags;
-  const uint32_t* r_gvk;
-  const uint32_t* r_name;
-  const uint32_t* r_mns;
-  const uint32_t* r_nsa;
-  const uint32_t* ann_off;
-  const uint32_t* ann_k;
-  const uint32_t* ann_v;
-  // pod view
-  const uint32_t* p_sc;
-  const uint32_t* ctr_off;
-  const uint32_t* vol_off;
-  const uint32_t* vol_src;
-  const uint32_t* sys_off;
-  const uint32_t* sys_id;
-  const uint32_t* pann_off;
-  const uint32_t* pann_k;
-  const uint32_t* pann_v;
-  // containers
-  const uint32_t* c_sc;
-  const uint64_t* c_add;
-  const uint64_t* c_drop;
-  const uint32_t* c_sann;
-  // program
-  const KpeRule* rules;
-  uint32_t nrules;
-  const KpeFilter* filters;
-  const KpeTerm* terms;
-  const KpeKindSel* kindsels;
-  const KpeAnnPair* annpairs;
-  const uint32_t* pred_bits;
-  const uint32_t* pred_word;  // first word of predicate p
-  int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
-  int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
-  uint32_t cv_union;
-  uint32_t any_pss;
-  // outputs
-  uint8_t* verdicts;   // n x nrules
-  uint32_t* masks;     // n x nrules or null
-  unsigned long long* counts;  // nrules x 6
-};
+__global__ void __launch_bounds__(256) kpe_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
+                                                        unsigned long long* out) {
+  uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (i >= width) return;
+  unsigned long long s = 0;
+  for (uint32_t b = 0; b < nblocks; ++b) s += part[(size_t)b * width + i];
+  out[i] = s;
+}
 
+// ---------------------------------------------------------------------------
 namespace {
 
-__device__ __forceinline__ bool pbit(const ScanArgs& a, int32_t p, uint32_t id) {
-  if (id == KPE_NO_STR) return false;
-  return (a.pred_bits[a.pred_word[p] + (id >> 5)] >> (id & 31u)) & 1u;
-}
-__device__ __forceinline__ uint64_t pmask64(const ScanArgs& a, int32_t p) {  // D_CAP predicates (<= 64 ids)
-  const uint32_t* w = a.pred_bits + a.pred_word[p];
-  return (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-}
+constexpr uint32_t kBlock = 256;
+constexpr uint32_t kChunk = 1024;      // containers staged per LDS pass
+constexpr uint32_t kStageV = 8192;     // verdict staging bytes (R <= 32)
+constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
+                                     (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
+                                     (1u << VS_PROJECTED) | (1u << VS_SECRET);
 
-__device__ bool eval_filter(const ScanArgs& a, uint32_t f, int64_t r, uint32_t gvk, uint32_t flags) {
-  KpeFilter fl = a.filters[f];
-  for (uint32_t t = 0; t < fl.nterms; ++t) {
-    KpeTerm tm = a.terms[fl.term0 + t];
-    bool ok;
-    switch (tm.type) {
-      case T_KINDS: {
-        ok = false;
-        for (uint32_t s = 0; s < tm.b && !ok; ++s) {
-          KpeKindSel ks = a.kindsels[tm.a + s];
-          ok = ks.sub_ok && (ks.pg < 0 || pbit(a, ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(a, ks.pv, GVK_VER(gvk))) &&
-               (ks.pk < 0 || pbit(a, ks.pk, GVK_KIND(gvk)));
-        }
-        break;
-      }
-      case T_PRED: {
-        uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : a.r_nsa[r]);
-        ok = pbit(a, (int32_t)tm.a, id);
-        break;
-      }
-      case T_ANNOTATIONS: {
-        ok = true;
-        uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
-        for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
-          KpeAnnPair pr = a.annpairs[tm.a + pi];
-          bool m = false;
-          for (uint32_t j = lo; j < hi && !m; ++j) m = pbit(a, pr.pk, a.ann_k[j]) && pbit(a, pr.pv, a.ann_v[j]);
-          ok = m;
-        }
-        break;
-      }
-      default: ok = false;
-    }
-    if (!ok) return false;
-  }
-  return true;
-}
-
-__device__ bool eval_block(const ScanArgs& a, uint32_t mode, uint32_t f0, uint32_t nf, int64_t r, uint32_t gvk,
-                           uint32_t flags) {
-  if (mode == MODE_ANY) {
-    for (uint32_t f = 0; f < nf; ++f)
-      if (eval_filter(a, f0 + f, r, gvk, flags)) return true;
-    return false;
-  }
-  if (mode == MODE_ALL) {
-    for (uint32_t f = 0; f < nf; ++f)
-      if (!eval_filter(a, f0 + f, r, gvk, flags)) return false;
-    return true;
-  }
-  return eval_filter(a, f0, r, gvk, flags);
-}
-
-// versioned check -> check bit
 __constant__ uint8_t kCvCheck[KPE_NUM_CV] = {
     CK_APE, CK_APE, CK_APPARMOR, CK_CAPS_BASELINE, CK_CAPS_RESTRICTED, CK_CAPS_RESTRICTED, CK_HOST_NS,
     CK_HOST_PATH, CK_HOST_PORTS, CK_PRIVILEGED, CK_PROC_MOUNT, CK_RESTRICTED_VOLUMES, CK_RUN_AS_NON_ROOT,
     CK_RUN_AS_USER, CK_SELINUX, CK_SECCOMP_BASELINE, CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED,
     CK_SECCOMP_RESTRICTED, CK_SYSCTLS, CK_SYSCTLS, CK_SYSCTLS, CK_WIN_HOST_PROCESS};
 
-constexpr uint32_t kBlock = 256;
-constexpr uint32_t kChunk = 2048;  // containers staged per LDS pass
-constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
-                                     (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
-                                     (1u << VS_PROJECTED) | (1u << VS_SECRET);
+struct Ctx {
+  const ScanArgs& a;
+  const uint32_t* lbits;       // LDS predicate bitsets (small domains)
+  const KpeRule* rules;        // LDS or global
+  const KpeFilter* filters;
+  const KpeTerm* terms;
+  const KpeKindSel* kindsels;
+  const KpeAnnPair* annpairs;
 
-__device__ __forceinline__ uint32_t container_bits(uint32_t w, uint64_t add, uint64_t drop, uint32_t sann,
-                                                   uint64_t caps_ok, uint64_t nbs, uint64_t all, const ScanArgs& a) {
+  __device__ __forceinline__ bool pbit(int32_t p, uint32_t id) const {
+    if (id == KPE_NO_STR) return false;
+    uint32_t w = a.pred_word[p];
+    if (w & PRED_LOCAL) return (lbits[(w & ~PRED_LOCAL) + (id >> 5)] >> (id & 31u)) & 1u;
+    return (a.pred_bits[w + (id >> 5)] >> (id & 31u)) & 1u;
+  }
+  __device__ __forceinline__ uint64_t pmask64(int32_t p) const {  // predicate over D_CAP (<= 64 ids)
+    if (p < 0) return 0;
+    uint32_t w = a.pred_word[p];
+    const uint32_t* b = (w & PRED_LOCAL) ? lbits + (w & ~PRED_LOCAL) : a.pred_bits + w;
+    return (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+  }
+
+  __device__ bool filter(uint32_t f, int64_t r, uint32_t gvk) const {
+    KpeFilter fl = filters[f];
+    for (uint32_t t = 0; t < fl.nterms; ++t) {
+      KpeTerm tm = terms[fl.term0 + t];
+      bool ok;
+      switch (tm.type) {
+        case T_KINDS: {
+          ok = false;
+          for (uint32_t s = 0; s < tm.b && !ok; ++s) {
+            KpeKindSel ks = kindsels[tm.a + s];
+            ok = ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) &&
+                 (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
+          }
+          break;
+        }
+        case T_PRED: {
+          uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : a.r_nsa[r]);
+          ok = pbit((int32_t)tm.a, id);
+          break;
+        }
+        case T_ANNOTATIONS: {
+          ok = true;
+          uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
+          for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
+            KpeAnnPair pr = annpairs[tm.a + pi];
+            bool m = false;
+            for (uint32_t j = lo; j < hi && !m; ++j) m = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
+            ok = m;
+          }
+          break;
+        }
+        default: ok = false;
+      }
+      if (!ok) return false;
+    }
+    return true;
+  }
+  __device__ bool block_any_all(uint32_t mode, uint32_t f0, uint32_t nf, int64_t r, uint32_t gvk) const {
+    if (mode == MODE_ANY) {
+      for (uint32_t f = 0; f < nf; ++f)
+        if (filter(f0 + f, r, gvk)) return true;
+      return false;
+    }
+    if (mode == MODE_ALL) {
+      for (uint32_t f = 0; f < nf; ++f)
+        if (!filter(f0 + f, r, gvk)) return false;
+      return true;
+    }
+    return filter(f0, r, gvk);
+  }
+};
+
+__device__ __forceinline__ uint32_t container_bits(const Ctx& x, uint32_t w, uint64_t add, uint64_t drop, uint32_t sann,
+                                                   uint64_t caps_ok, uint64_t nbs, uint64_t all) {
   uint32_t b = 0;
   bool caps = w & C_CAPS_PRESENT;
   if (FIELD(w, C_APE_SH, 2) != TRI_FALSE) b |= CB_APE;
@@ -246,20 +216,21 @@ __device__ __forceinline__ uint32_t container_bits(uint32_t w, uint64_t add, uin
   uint32_t sec = FIELD(w, C_SECCOMP_SH, 3);
   if (sec == SECCOMP_NONE) b |= CB_SEC_UNSET;
   else if (sec != SECCOMP_RUNTIMEDEFAULT && sec != SECCOMP_LOCALHOST) b |= CB_SEC_BAD;
-  if (sann != KPE_NO_STR && a.pp_seccomp_ann_ok >= 0 && !pbit(a, a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
+  if (sann != KPE_NO_STR && !x.pbit(x.a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
   if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
   return b;
 }
 
 // PSA versioned checks for one pod given the OR of its container bits.
-__device__ uint32_t cv_fails(const ScanArgs& a, uint32_t pw, uint32_t cb, bool vol_hostpath, bool vol_restricted,
-                             uint32_t sys_bad, bool apparmor_bad, bool sec_pod_ann_bad) {
+__device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_hostpath, bool vol_restricted,
+                                             uint32_t sys_bad, bool apparmor_bad, bool sec_pod_ann_bad) {
   uint32_t f = 0;
   bool win = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS;
   if (cb & CB_APE) f |= (1u << CV_APE_1_8) | (win ? 0u : (1u << CV_APE_1_25));
   if (apparmor_bad) f |= 1u << CV_APPARMOR_1_0;
   if (cb & CB_CAPS_BASE) f |= 1u << CV_CAPS_BASELINE_1_0;
-  if (cb & (CB_CAPS_DROP | CB_CAPS_ADD)) f |= (1u << CV_CAPS_RESTRICTED_1_22) | (win ? 0u : (1u << CV_CAPS_RESTRICTED_1_25));
+  if (cb & (CB_CAPS_DROP | CB_CAPS_ADD))
+    f |= (1u << CV_CAPS_RESTRICTED_1_22) | (win ? 0u : (1u << CV_CAPS_RESTRICTED_1_25));
   if (pw & (P_HOSTNET | P_HOSTPID | P_HOSTIPC)) f |= 1u << CV_HOST_NS_1_0;
   if (vol_hostpath) f |= 1u << CV_HOST_PATH_1_0;
   if (cb & CB_HOSTPORT) f |= 1u << CV_HOST_PORTS_1_0;
@@ -290,9 +261,11 @@ __device__ uint32_t cv_fails(const ScanArgs& a, uint32_t pw, uint32_t cb, bool v
 }  // namespace
 
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
+  extern __shared__ uint32_t dyn[];  // [program copy (a.prog_words)] [local predicate bits (a.lwords)]
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_cb[kChunk];
-  __shared__ unsigned long long s_cnt[6 * 64];
+  __shared__ uint32_t s_cnt[6 * KPE_SMALL_R];
+  __shared__ __attribute__((aligned(16))) uint8_t s_v[kStageV];
 
   const int64_t p0 = (int64_t)blockIdx.x * kBlock;
   const uint32_t t = threadIdx.x;
@@ -300,86 +273,113 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const bool live = r < a.n;
   const uint32_t np = (uint32_t)((a.n - p0) < (int64_t)kBlock ? (a.n - p0) : (int64_t)kBlock);
   const uint32_t R = a.nrules;
-  const bool small_r = R <= 64;
+  const bool small_r = R <= KPE_SMALL_R;
+  const bool stage_v = R * kBlock <= kStageV;
+
+  // ---- (1) program + small-domain predicate bitsets into LDS ----
+  uint32_t* lprog = dyn;
+  uint32_t* lbits = dyn + a.prog_words;
+  for (uint32_t i = t; i < a.prog_words; i += kBlock) lprog[i] = a.prog[i];
+  for (uint32_t i = t; i < a.lwords; i += kBlock) lbits[i] = 0;
   if (small_r)
     for (uint32_t i = t; i < 6 * R; i += kBlock) s_cnt[i] = 0;
   __syncthreads();
-
-  uint32_t fails = 0;  // versioned-check failures of this resource
-  if (a.any_pss) {
-    // ---- containers: coalesced stream through LDS, OR-reduced per resource ----
+  for (uint32_t i = t; i < a.lpairs; i += kBlock) {  // (predicate, string) pairs of small domains
+    uint32_t j = 0;
+    while (j + 1 < a.nlpreds && a.lpreds[j + 1].pair0 <= i) ++j;
+    const LocalPred lp = a.lpreds[j];
+    uint32_t id = i - lp.pair0;
+    const uint32_t* off = a.dict_off[lp.domain];
+    if (match_any(a.pat_bytes, a.pat_off, lp.pat0, lp.npat, a.dict_bytes[lp.domain] + off[id],
+                  (int)(off[id + 1] - off[id])))
+      atomicOr(&lbits[lp.word0 + (id >> 5)], 1u << (id & 31u));
+  }
+  const bool staged = a.prog_words != 0;
+  const Ctx x{a, lbits,
+              staged ? reinterpret_cast<const KpeRule*>(lprog + a.off_rules) : a.rules,
+              staged ? reinterpret_cast<const KpeFilter*>(lprog + a.off_filters) : a.filters,
+              staged ? reinterpret_cast<const KpeTerm*>(lprog + a.off_terms) : a.terms,
+              staged ? reinterpret_cast<const KpeKindSel*>(lprog + a.off_kindsels) : a.kindsels,
+              staged ? reinterpret_cast<const KpeAnnPair*>(lprog + a.off_annpairs) : a.annpairs};
+  if (a.any_pss)
     for (uint32_t i = t; i <= np; i += kBlock) s_off[i] = a.ctr_off[p0 + i];
-    __syncthreads();
+  __syncthreads();
+
+  // ---- (2)+(3) PSS: containers through LDS, pod-level lists, versioned checks ----
+  uint32_t fails = 0;
+  if (a.any_pss) {
     const uint32_t c_begin = s_off[0], c_end = s_off[np];
-    uint64_t caps_ok = a.pp_caps_ok >= 0 ? pmask64(a, a.pp_caps_ok) : 0, nbs = a.pp_cap_nbs >= 0 ? pmask64(a, a.pp_cap_nbs) : 0,
-             all = a.pp_cap_all >= 0 ? pmask64(a, a.pp_cap_all) : 0;
+    const uint64_t caps_ok = x.pmask64(a.pp_caps_ok), nbs = x.pmask64(a.pp_cap_nbs), all = x.pmask64(a.pp_cap_all);
+    const bool need_caps = a.need & NEED_CAPS, need_sann = a.need & NEED_SANN;
     uint32_t cb = 0;
     const uint32_t my_lo = live ? s_off[t] : 0, my_hi = live ? s_off[t + 1] : 0;
     for (uint32_t base = c_begin; base < c_end; base += kChunk) {
       const uint32_t lim = (c_end - base) < kChunk ? (c_end - base) : kChunk;
       for (uint32_t i = t; i < lim; i += kBlock) {
-        uint32_t c = base + i;
-        s_cb[i] = container_bits(a.c_sc[c], a.c_add[c], a.c_drop[c], a.c_sann[c], caps_ok, nbs, all, a);
+        const uint32_t c = base + i;
+        s_cb[i] = container_bits(x, a.c_sc[c], need_caps ? a.c_add[c] : 0ull, need_caps ? a.c_drop[c] : ~0ull,
+                                 need_sann ? a.c_sann[c] : KPE_NO_STR, caps_ok, nbs, all);
       }
       __syncthreads();
-      uint32_t lo = my_lo > base ? my_lo : base, hi = my_hi < base + lim ? my_hi : base + lim;
+      const uint32_t lo = my_lo > base ? my_lo : base, hi = my_hi < base + lim ? my_hi : base + lim;
       for (uint32_t c = lo; c < hi; ++c) cb |= s_cb[c - base];
       __syncthreads();
     }
     if (live) {
       const uint32_t pw = a.p_sc[r];
-      // volumes
       bool vol_hostpath = false, vol_restricted = false;
-      for (uint32_t j = a.vol_off[r], e = a.vol_off[r + 1]; j < e; ++j) {
-        uint32_t s = a.vol_src[j];
-        if (s & (1u << VS_HOSTPATH)) vol_hostpath = true;
-        if (!(s & kAllowedVolumes)) vol_restricted = true;
-      }
-      // sysctls (three allow-lists: 1.0, 1.27, 1.29)
+      if (a.need & NEED_VOL)
+        for (uint32_t j = a.vol_off[r], e = a.vol_off[r + 1]; j < e; ++j) {
+          const uint32_t s = a.vol_src[j];
+          vol_hostpath |= (s & (1u << VS_HOSTPATH)) != 0;
+          vol_restricted |= !(s & kAllowedVolumes);
+        }
       uint32_t sys_bad = 0;
-      for (uint32_t j = a.sys_off[r], e = a.sys_off[r + 1]; j < e; ++j) {
-        uint32_t id = a.sys_id[j];
-        if (!pbit(a, a.pp_sysctl0, id)) sys_bad |= 1u;
-        if (!pbit(a, a.pp_sysctl1, id)) sys_bad |= 2u;
-        if (!pbit(a, a.pp_sysctl2, id)) sys_bad |= 4u;
-      }
-      // pod-template annotations: AppArmor and the seccomp pod annotation
+      if (a.need & NEED_SYS)
+        for (uint32_t j = a.sys_off[r], e = a.sys_off[r + 1]; j < e; ++j) {
+          const uint32_t id = a.sys_id[j];
+          if (!x.pbit(a.pp_sysctl0, id)) sys_bad |= 1u;
+          if (!x.pbit(a.pp_sysctl1, id)) sys_bad |= 2u;
+          if (!x.pbit(a.pp_sysctl2, id)) sys_bad |= 4u;
+        }
       bool apparmor_bad = false, sec_pod_ann_bad = false;
-      for (uint32_t j = a.pann_off[r], e = a.pann_off[r + 1]; j < e; ++j) {
-        uint32_t k = a.pann_k[j], v = a.pann_v[j];
-        if (pbit(a, a.pp_apparmor_key, k) && !pbit(a, a.pp_apparmor_ok, v)) apparmor_bad = true;
-        if (pbit(a, a.pp_seccomp_pod_key, k) && !pbit(a, a.pp_seccomp_ann_ok, v)) sec_pod_ann_bad = true;
-      }
-      fails = cv_fails(a, pw, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
+      if (a.need & NEED_PANN)
+        for (uint32_t j = a.pann_off[r], e = a.pann_off[r + 1]; j < e; ++j) {
+          const uint32_t k = a.pann_k[j], v = a.pann_v[j];
+          apparmor_bad |= x.pbit(a.pp_apparmor_key, k) && !x.pbit(a.pp_apparmor_ok, v);
+          sec_pod_ann_bad |= x.pbit(a.pp_seccomp_pod_key, k) && !x.pbit(a.pp_seccomp_ann_ok, v);
+        }
+      fails = cv_fails(pw, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
     }
   }
 
-  // ---- rules: match/exclude, handler, ApplyOne, verdict cell ----
-  uint32_t flags = live ? a.r_flags[r] : 0, gvk = live ? a.r_gvk[r] : 0;
-  uint32_t nsa = live ? a.r_nsa[r] : KPE_NO_STR;
+  // ---- (4) rules: match/exclude, handler, ApplyOne, verdict cell ----
+  const uint32_t flags = (live && (a.need & NEED_FLAGS)) ? a.r_flags[r] : 0;
+  const uint32_t gvk = (live && (a.need & NEED_GVK)) ? a.r_gvk[r] : 0;
   bool applied = false;
   uint32_t cur_policy = 0xFFFFFFFFu;
+  const uint32_t lane = t & 63u;
   for (uint32_t ri = 0; ri < R; ++ri) {
-    KpeRule rule = a.rules[ri];
+    const KpeRule rule = x.rules[ri];
     if (rule.policy != cur_policy) {
       cur_policy = rule.policy;
       applied = false;
     }
-    uint8_t v = KPE_NA_;
+    uint32_t v = KPE_NA_;
     uint32_t cmask = 0;
     if (live && !(rule.apply_one && applied)) {
-      bool m = rule.pol_ns_pred < 0 || pbit(a, rule.pol_ns_pred, nsa);
-      m = m && eval_block(a, rule.match_mode, rule.match_f0, rule.match_nf, r, gvk, flags);
+      bool m = rule.pol_ns_pred < 0 || x.pbit(rule.pol_ns_pred, a.r_nsa[r]);
+      m = m && x.block_any_all(rule.match_mode, rule.match_f0, rule.match_nf, r, gvk);
       if (m) {
         bool ex;
         if (rule.excl_mode == MODE_ANY) {
           ex = false;
-          for (uint32_t f = 0; f < rule.excl_nf && !ex; ++f) ex = eval_filter(a, rule.excl_f0 + f, r, gvk, flags);
+          for (uint32_t f = 0; f < rule.excl_nf && !ex; ++f) ex = x.filter(rule.excl_f0 + f, r, gvk);
         } else if (rule.excl_mode == MODE_ALL) {
           ex = true;
-          for (uint32_t f = 0; f < rule.excl_nf && ex; ++f) ex = eval_filter(a, rule.excl_f0 + f, r, gvk, flags);
+          for (uint32_t f = 0; f < rule.excl_nf && ex; ++f) ex = x.filter(rule.excl_f0 + f, r, gvk);
         } else {
-          ex = eval_filter(a, rule.excl_f0, r, gvk, flags);
+          ex = x.filter(rule.excl_f0, r, gvk);
         }
         m = !ex;
       }
@@ -388,10 +388,11 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
           if ((flags & R_CLASS_MASK) == R_CLASS_OTHER || (flags & R_DECODE_ERR)) {
             v = KPE_ERROR_;
           } else {
-            uint32_t f = fails & rule.cv_mask;
+            const uint32_t f = fails & rule.cv_mask;
             v = f ? KPE_FAIL_ : KPE_PASS_;
-            for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
-              if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
+            if (a.masks)
+              for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
+                if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
           }
         } else if (rule.handler == H_ERROR) {
           v = KPE_ERROR_;
@@ -399,26 +400,30 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
       }
       if (v == KPE_PASS_ || v == KPE_FAIL_) applied = true;
     }
-    if (live) {
-      a.verdicts[r * R + ri] = v;
-      if (a.masks) a.masks[r * R + ri] = cmask;
-    }
+    if (stage_v) s_v[t * R + ri] = (uint8_t)v;
+    else if (live) a.verdicts[r * R + ri] = (uint8_t)v;
+    if (live && a.masks) a.masks[r * R + ri] = cmask;
     if (small_r) {
-      // wave-ballot histogram of this rule's verdicts
-      const uint32_t lane = t & 63u;
       for (uint32_t k = 1; k < 6; ++k) {
-        uint64_t b = __ballot(live && v == k);
-        if (lane == 0 && b) atomicAdd(&s_cnt[ri * 6 + k], (unsigned long long)__popcll(b));
+        const uint64_t b = __ballot(live && v == k);
+        if (lane == 0 && b) atomicAdd(&s_cnt[ri * 6 + k], (uint32_t)__popcll(b));
       }
     } else if (live && v != KPE_NA_) {
-      atomicAdd(&a.counts[ri * 6 + v], 1ull);
+      atomicAdd(&a.counts_global[ri * 6 + v], 1ull);
     }
   }
-  if (small_r) {
-    __syncthreads();
-    for (uint32_t i = t; i < 6 * R; i += kBlock)
-      if (i % 6 != 0 && s_cnt[i]) atomicAdd(&a.counts[i], s_cnt[i]);
+
+  // ---- (5) coalesced verdict store + counter partials ----
+  __syncthreads();
+  if (stage_v) {
+    const uint32_t bytes = np * R;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);  // p0*R*1 is 4-byte aligned
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(s_v);
+    for (uint32_t w = t; w < bytes / 4; w += kBlock) dst[w] = src[w];
+    if (t < (bytes & 3u)) a.verdicts[(size_t)p0 * R + (bytes & ~3u) + t] = s_v[(bytes & ~3u) + t];
   }
+  if (small_r)
+    for (uint32_t i = t; i < 6 * R; i += kBlock) a.counts_part[(size_t)blockIdx.x * 6 * R + i] = s_cnt[i];
 }
 
 // ---------------------------------------------------------------------------
@@ -428,9 +433,16 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipSt
   hipLaunchKernelGGL(kpe_pred_kernel, dim3(nblocks), dim3(256), 0, s, *a);
   return hipGetLastError();
 }
+extern "C" uint32_t kpe_scan_blocks(int64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s) {
   if (a->n == 0) return hipSuccess;
-  uint32_t blocks = (uint32_t)((a->n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(kpe_scan_kernel, dim3(blocks), dim3(kBlock), 0, s, *a);
+  size_t dyn = (size_t)(a->prog_words + a->lwords) * 4;
+  hipLaunchKernelGGL(kpe_scan_kernel, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
+  return hipGetLastError();
+}
+extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
+                                              unsigned long long* out, hipStream_t s) {
+  if (width == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_count_reduce, dim3((width + 255) / 256), dim3(256), 0, s, part, nblocks, width, out);
   return hipGetLastError();
 }

@@ -1,0 +1,79 @@
+// Kernel argument structs shared by kernels.hip (device) and kpe_api.cpp (host).
+#pragma once
+#include <stdint.h>
+
+#include "schema.h"
+
+#define PRED_LOCAL 0x80000000u  // pred_word flag: bitset lives in the scan block's LDS
+#define KPE_SMALL_R 64          // rules counted via LDS ballots + per-block partials
+
+// ScanArgs.need: which columns / lists the compiled program reads
+#define NEED_FLAGS (1u << 0)
+#define NEED_GVK (1u << 1)
+#define NEED_CAPS (1u << 2)
+#define NEED_SANN (1u << 3)
+#define NEED_VOL (1u << 4)
+#define NEED_SYS (1u << 5)
+#define NEED_PANN (1u << 6)
+#define NEED_NSA (1u << 7)
+
+struct PredJob {
+  uint32_t domain;
+  uint32_t pat0, npat;  // patterns [pat0, pat0+npat) of the pattern table
+  uint32_t out_word;    // first output word
+  uint32_t blk0;        // first block of this job
+};
+
+struct PredArgs {
+  const uint8_t* dict_bytes[KPE_NUM_DOMAINS];
+  const uint32_t* dict_off[KPE_NUM_DOMAINS];
+  uint32_t dict_n[KPE_NUM_DOMAINS];
+  const uint8_t* pat_bytes;
+  const uint32_t* pat_off;
+  const PredJob* jobs;
+  uint32_t njobs;
+  uint32_t* out;
+};
+
+struct LocalPred {  // predicate over a small domain, evaluated per scan block into LDS
+  uint32_t domain, pat0, npat, word0, pair0;
+};
+
+struct ScanArgs {
+  int64_t n;
+  // resource rows (unstructured view)
+  const uint32_t *r_flags, *r_gvk, *r_name, *r_mns, *r_nsa, *ann_off, *ann_k, *ann_v;
+  // pod view
+  const uint32_t *p_sc, *ctr_off, *vol_off, *vol_src, *sys_off, *sys_id, *pann_off, *pann_k, *pann_v;
+  // containers
+  const uint32_t* c_sc;
+  const uint64_t *c_add, *c_drop;
+  const uint32_t* c_sann;
+  // program (global copies)
+  const KpeRule* rules;
+  uint32_t nrules;
+  const KpeFilter* filters;
+  const KpeTerm* terms;
+  const KpeKindSel* kindsels;
+  const KpeAnnPair* annpairs;
+  // program image staged into LDS (prog_words == 0 => read the global copies)
+  const uint32_t* prog;
+  uint32_t prog_words, off_rules, off_filters, off_terms, off_kindsels, off_annpairs;
+  // predicates
+  const uint32_t* pred_bits;
+  const uint32_t* pred_word;  // per predicate: global word offset, or PRED_LOCAL | LDS word offset
+  const LocalPred* lpreds;
+  uint32_t nlpreds, lpairs, lwords;
+  const uint8_t* dict_bytes[KPE_NUM_DOMAINS];
+  const uint32_t* dict_off[KPE_NUM_DOMAINS];
+  const uint8_t* pat_bytes;
+  const uint32_t* pat_off;
+  int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
+  int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
+  uint32_t cv_union, any_pss, need;
+  // outputs
+  uint8_t* verdicts;                 // n x nrules
+  uint32_t* masks;                   // n x nrules or null
+  uint32_t* counts_part;             // blocks x nrules x 6 (nrules <= KPE_SMALL_R)
+  unsigned long long* counts_global; // nrules x 6 (nrules > KPE_SMALL_R)
+};

@@ -15,6 +15,7 @@
 
 #include "../../include/kpe.h"
 #include "corpus.hpp"
+#include "kernels_abi.h"
 #include "program.hpp"
 
 namespace kpe {
@@ -22,45 +23,11 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
 bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
-// ---- mirrors of kernels.hip argument structs (identical layout) ----
-struct PredJob {
-  uint32_t domain, pat0, npat, out_word, blk0;
-};
-struct PredArgs {
-  const uint8_t* dict_bytes[KPE_NUM_DOMAINS];
-  const uint32_t* dict_off[KPE_NUM_DOMAINS];
-  uint32_t dict_n[KPE_NUM_DOMAINS];
-  const uint8_t* pat_bytes;
-  const uint32_t* pat_off;
-  const PredJob* jobs;
-  uint32_t njobs;
-  uint32_t* out;
-};
-struct ScanArgs {
-  int64_t n;
-  const uint32_t *r_flags, *r_gvk, *r_name, *r_mns, *r_nsa, *ann_off, *ann_k, *ann_v;
-  const uint32_t *p_sc, *ctr_off, *vol_off, *vol_src, *sys_off, *sys_id, *pann_off, *pann_k, *pann_v;
-  const uint32_t* c_sc;
-  const uint64_t *c_add, *c_drop;
-  const uint32_t* c_sann;
-  const KpeRule* rules;
-  uint32_t nrules;
-  const KpeFilter* filters;
-  const KpeTerm* terms;
-  const KpeKindSel* kindsels;
-  const KpeAnnPair* annpairs;
-  const uint32_t* pred_bits;
-  const uint32_t* pred_word;
-  int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
-  int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
-  uint32_t cv_union;
-  uint32_t any_pss;
-  uint8_t* verdicts;
-  uint32_t* masks;
-  unsigned long long* counts;
-};
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s);
+extern "C" uint32_t kpe_scan_blocks(int64_t n);
+extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
+                                              unsigned long long* out, hipStream_t s);
 
 namespace {
 thread_local std::string g_err;
@@ -78,6 +45,9 @@ kpe_status fail(kpe_status s, const std::string& m) {
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
   ~DevBuf() {
     if (p) (void)hipFree(p);
   }
@@ -103,6 +73,11 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
   if (!v.empty()) return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
   return hipSuccess;
 }
+
+// LDS budgets of the scan kernel's dynamic region
+constexpr uint32_t kMaxProgWords = 4096;   // 16 KiB program image
+constexpr uint32_t kMaxLocalWords = 8192;  // 32 KiB of small-domain predicate bitsets
+constexpr uint32_t kMaxLocalPairs = 4096;  // (predicate, string) globs evaluated per block
 
 }  // namespace
 
@@ -134,15 +109,19 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
-  DevBuf rules, filters, terms, kindsels, annpairs, pat_bytes, pat_off;
+  DevBuf rules, filters, terms, kindsels, annpairs, pat_bytes, pat_off, image;
   std::vector<uint8_t> pat_bytes_h;
-  std::vector<uint32_t> pat_off_h;
+  std::vector<uint32_t> pat_off_h;  // pattern k of predicate p: pat0[p] + k
+  std::vector<uint32_t> pat0;
+  uint32_t image_words = 0, off_rules = 0, off_filters = 0, off_terms = 0, off_kindsels = 0, off_annpairs = 0;
 };
 
-struct Binding {  // program x corpus (dictionary sizes decide predicate layout)
+struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
   const Program* prog = nullptr;
-  DevBuf jobs, pred_word, pred_bits, verdicts, masks, counts;
-  uint32_t nblocks = 0, njobs = 0;
+  DevBuf jobs, pred_word, pred_bits, lpreds, verdicts, masks, counts_part, counts_global, counts_out;
+  uint32_t nblocks = 0, njobs = 0, nlpreds = 0, lpairs = 0, lwords = 0, scan_blocks = 0;
+  uint32_t need = 0;
+  double scan_bytes = 0;
   size_t cells = 0;
 };
 
@@ -168,7 +147,7 @@ struct kpe_corpus {
 extern "C" {
 
 const char* kpe_last_error(void) { return g_err.c_str(); }
-const char* kpe_version(void) { return "kpe 0.1 (gfx950)"; }
+const char* kpe_version(void) { return "kpe 0.2 (gfx950)"; }
 
 kpe_status kpe_device_open(int ordinal, kpe_device** out) {
   int n = 0;
@@ -293,6 +272,14 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
 
 namespace {
 
+template <class T>
+void append_words(std::vector<uint32_t>& img, const std::vector<T>& v, uint32_t* off) {
+  static_assert(sizeof(T) % 4 == 0, "program tables are word-sized");
+  *off = (uint32_t)img.size();
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(v.data());
+  img.insert(img.end(), w, w + v.size() * sizeof(T) / 4);
+}
+
 kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   auto& P = *pp->p;
   if (P.dev && P.dev->ordinal == dev->ordinal) return KPE_OK;
@@ -302,11 +289,20 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
   D.pat_off_h.assign(1, 0);
-  for (auto& pr : P.preds)
+  for (auto& pr : P.preds) {
+    D.pat0.push_back((uint32_t)D.pat_off_h.size() - 1);
     for (auto& g : pr.globs) {
       D.pat_bytes_h.insert(D.pat_bytes_h.end(), g.begin(), g.end());
       D.pat_off_h.push_back((uint32_t)D.pat_bytes_h.size());
     }
+  }
+  std::vector<uint32_t> img;
+  append_words(img, P.rules, &D.off_rules);
+  append_words(img, P.filters, &D.off_filters);
+  append_words(img, P.terms, &D.off_terms);
+  append_words(img, P.kindsels, &D.off_kindsels);
+  append_words(img, P.annpairs, &D.off_annpairs);
+  D.image_words = img.size() <= kMaxProgWords ? (uint32_t)img.size() : 0;
   HIPCHK(upload(D.rules, P.rules, s));
   HIPCHK(upload(D.filters, P.filters, s));
   HIPCHK(upload(D.terms, P.terms, s));
@@ -314,42 +310,110 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   HIPCHK(upload(D.annpairs, P.annpairs, s));
   HIPCHK(upload(D.pat_bytes, D.pat_bytes_h, s));
   HIPCHK(upload(D.pat_off, D.pat_off_h, s));
+  HIPCHK(upload(D.image, img, s));
   HIPCHK(hipStreamSynchronize(s));
   return KPE_OK;
+}
+
+// Columns the compiled program reads (kernel `need` flags) and their bytes.
+uint32_t need_flags(const kpe::Program& P) {
+  uint32_t need = 0;
+  if (P.any_pss) {
+    need |= NEED_FLAGS;
+    uint32_t u = P.cv_union;
+    if (u & ((1u << CV_CAPS_BASELINE_1_0) | (1u << CV_CAPS_RESTRICTED_1_22) | (1u << CV_CAPS_RESTRICTED_1_25)))
+      need |= NEED_CAPS;
+    if (u & (1u << CV_SECCOMP_BASELINE_1_0)) need |= NEED_SANN | NEED_PANN;
+    if (u & (1u << CV_APPARMOR_1_0)) need |= NEED_PANN;
+    if (u & ((1u << CV_HOST_PATH_1_0) | (1u << CV_RESTRICTED_VOLUMES_1_0))) need |= NEED_VOL;
+    if (u & ((1u << CV_SYSCTLS_1_0) | (1u << CV_SYSCTLS_1_27) | (1u << CV_SYSCTLS_1_29))) need |= NEED_SYS;
+  }
+  for (auto& r : P.rules)
+    if (r.handler != H_NONE && r.handler != H_PSS) need |= NEED_FLAGS;
+  for (auto& t : P.terms)
+    if (t.type == T_KINDS) need |= NEED_GVK;
+  for (auto& r : P.rules)
+    if (r.pol_ns_pred >= 0) need |= NEED_NSA;
+  return need;
+}
+double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
+  double b = 0;
+  const double n = (double)C.n;
+  if (need & NEED_FLAGS) b += 4 * n;
+  if (need & NEED_GVK) b += 4 * n;
+  if (need & NEED_NSA) b += 4 * n;
+  for (auto& t : P.terms)  // name / namespace columns read by predicate terms (once per resource)
+    if (t.type == T_PRED) {
+      b += 4 * n;
+      break;
+    }
+  if (P.any_pss) {
+    b += 4 * (n + 1) + 4 * n;                  // ctr_off, p_sc
+    b += 4.0 * C.c_sc.size();                 // container words
+    if (need & NEED_CAPS) b += 16.0 * C.c_sc.size();
+    if (need & NEED_SANN) b += 4.0 * C.c_sc.size();
+    if (need & NEED_VOL) b += 4 * (n + 1) + 4.0 * C.vol_src.size();
+    if (need & NEED_SYS) b += 4 * (n + 1) + 4.0 * C.sys_id.size();
+    if (need & NEED_PANN) b += 4 * (n + 1) + 8.0 * C.pann_k.size();
+  }
+  b += n * P.rules.size() * (masks ? 5.0 : 1.0);  // verdict cells (+ check masks)
+  if (P.rules.size() <= KPE_SMALL_R) b += 4.0 * kpe_scan_blocks(C.n) * 6 * P.rules.size();
+  return b;
 }
 
 kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool want_masks) {
   auto& P = *pp->p;
   auto& C = *cc->c;
   auto& B = cc->d->bind;
+  auto& PD = *P.dev;
   size_t cells = (size_t)C.n * P.rules.size();
   if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
   hipStream_t s = dev->stream;
+  // predicate placement: small domains are evaluated per scan block into LDS,
+  // large ones by the dictionary pass into a global bitset.
   std::vector<PredJob> jobs;
-  std::vector<uint32_t> word;
-  uint32_t w = 0, blk = 0, pat = 0;
-  for (auto& pr : P.preds) {
+  std::vector<LocalPred> lps;
+  std::vector<uint32_t> word(P.preds.size());
+  uint32_t gw = 0, blk = 0, lw = 0, lpairs = 0;
+  for (size_t p = 0; p < P.preds.size(); ++p) {
+    const auto& pr = P.preds[p];
     uint32_t n = C.dict[pr.domain].size();
     uint32_t nwords = ((n + 63) / 64) * 2 + 2;
-    jobs.push_back({pr.domain, pat, (uint32_t)pr.globs.size(), w, blk});
-    word.push_back(w);
-    w += nwords;
-    blk += (n + 255) / 256;
-    pat += (uint32_t)pr.globs.size();
+    uint32_t npat = (uint32_t)pr.globs.size();
+    if (lw + nwords <= kMaxLocalWords && lpairs + n <= kMaxLocalPairs) {
+      lps.push_back({pr.domain, PD.pat0[p], npat, lw, lpairs});
+      word[p] = PRED_LOCAL | lw;
+      lw += nwords;
+      lpairs += n;
+    } else {
+      jobs.push_back({pr.domain, PD.pat0[p], npat, gw, blk});
+      word[p] = gw;
+      gw += nwords;
+      blk += (n + 255) / 256;
+    }
   }
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
+  B.nlpreds = (uint32_t)lps.size();
+  B.lpairs = lpairs;
+  B.lwords = lw;
+  B.scan_blocks = kpe_scan_blocks(C.n);
   HIPCHK(upload(B.jobs, jobs, s));
+  HIPCHK(upload(B.lpreds, lps, s));
   HIPCHK(upload(B.pred_word, word, s));
-  HIPCHK(B.pred_bits.ensure(std::max<size_t>(w, 1) * 4));
-  HIPCHK(hipMemsetAsync(B.pred_bits.p, 0, std::max<size_t>(w, 1) * 4, s));
-  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 1)));
-  HIPCHK(B.counts.ensure(std::max<size_t>(P.rules.size(), 1) * 6 * 8));
+  HIPCHK(B.pred_bits.ensure(std::max<size_t>(gw, 1) * 4));
+  HIPCHK(hipMemsetAsync(B.pred_bits.p, 0, std::max<size_t>(gw, 1) * 4, s));
+  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
+  size_t width = P.rules.size() * 6;
+  HIPCHK(B.counts_part.ensure(std::max<size_t>((size_t)B.scan_blocks * width, 1) * 4));
+  HIPCHK(B.counts_global.ensure(std::max<size_t>(width, 1) * 8));
+  HIPCHK(B.counts_out.ensure(std::max<size_t>(width, 1) * 8));
   if (want_masks) {
     HIPCHK(B.masks.ensure(std::max<size_t>(cells, 1) * 4));
     cc->d->has_masks = true;
   }
   HIPCHK(hipStreamSynchronize(s));
+  B.need = need_flags(P);
   B.prog = &P;
   B.cells = cells;
   return KPE_OK;
@@ -369,19 +433,22 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     ev.c = dev->get_ev();
     HIPCHK(hipEventRecord(ev.a, s));
   }
-  PredArgs pa{};
-  for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
-    pa.dict_bytes[i] = D.dict_bytes[i].as<uint8_t>();
-    pa.dict_off[i] = D.dict_off[i].as<uint32_t>();
-    pa.dict_n[i] = C.dict[i].size();
+  const size_t R = P.rules.size();
+  if (B.nblocks) {  // dictionary pass for large-domain predicates
+    PredArgs pa{};
+    for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
+      pa.dict_bytes[i] = D.dict_bytes[i].as<uint8_t>();
+      pa.dict_off[i] = D.dict_off[i].as<uint32_t>();
+      pa.dict_n[i] = C.dict[i].size();
+    }
+    pa.pat_bytes = PD.pat_bytes.as<uint8_t>();
+    pa.pat_off = PD.pat_off.as<uint32_t>();
+    pa.jobs = B.jobs.as<PredJob>();
+    pa.njobs = B.njobs;
+    pa.out = B.pred_bits.as<uint32_t>();
+    HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
   }
-  pa.pat_bytes = PD.pat_bytes.as<uint8_t>();
-  pa.pat_off = PD.pat_off.as<uint32_t>();
-  pa.jobs = B.jobs.as<PredJob>();
-  pa.njobs = B.njobs;
-  pa.out = B.pred_bits.as<uint32_t>();
-  HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
-  HIPCHK(hipMemsetAsync(B.counts.p, 0, P.rules.size() * 6 * 8, s));
+  if (R > KPE_SMALL_R) HIPCHK(hipMemsetAsync(B.counts_global.p, 0, R * 6 * 8, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   ScanArgs sa{};
   sa.n = C.n;
@@ -407,13 +474,30 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.c_drop = D.c_drop.as<uint64_t>();
   sa.c_sann = D.c_sann.as<uint32_t>();
   sa.rules = PD.rules.as<KpeRule>();
-  sa.nrules = (uint32_t)P.rules.size();
+  sa.nrules = (uint32_t)R;
   sa.filters = PD.filters.as<KpeFilter>();
   sa.terms = PD.terms.as<KpeTerm>();
   sa.kindsels = PD.kindsels.as<KpeKindSel>();
   sa.annpairs = PD.annpairs.as<KpeAnnPair>();
+  sa.prog = PD.image.as<uint32_t>();
+  sa.prog_words = PD.image_words;
+  sa.off_rules = PD.off_rules;
+  sa.off_filters = PD.off_filters;
+  sa.off_terms = PD.off_terms;
+  sa.off_kindsels = PD.off_kindsels;
+  sa.off_annpairs = PD.off_annpairs;
   sa.pred_bits = B.pred_bits.as<uint32_t>();
   sa.pred_word = B.pred_word.as<uint32_t>();
+  sa.lpreds = B.lpreds.as<LocalPred>();
+  sa.nlpreds = B.nlpreds;
+  sa.lpairs = B.lpairs;
+  sa.lwords = B.lwords;
+  for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
+    sa.dict_bytes[i] = D.dict_bytes[i].as<uint8_t>();
+    sa.dict_off[i] = D.dict_off[i].as<uint32_t>();
+  }
+  sa.pat_bytes = PD.pat_bytes.as<uint8_t>();
+  sa.pat_off = PD.pat_off.as<uint32_t>();
   sa.pp_apparmor_key = P.pss.apparmor_key;
   sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
   sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;
@@ -426,21 +510,15 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pp_sysctl2 = P.pss.sysctl[2];
   sa.cv_union = P.cv_union;
   sa.any_pss = P.any_pss ? 1u : 0u;
+  sa.need = B.need;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
-  sa.counts = B.counts.as<unsigned long long>();
+  sa.counts_part = B.counts_part.as<uint32_t>();
+  sa.counts_global = B.counts_global.as<unsigned long long>();
   HIPCHK(kpe_launch_scan(&sa, s));
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.c, s));
-    // algorithmic bytes of one scan launch: every column the program reads + verdict cells written
-    double bytes = 0;
-    if (P.any_pss)
-      bytes += (double)(C.p_sc.size() + C.ctr_off.size() + C.vol_off.size() + C.sys_off.size() + C.pann_off.size() +
-                        C.vol_src.size() + C.sys_id.size() + 2 * C.pann_k.size()) * 4 +
-               (double)C.c_sc.size() * (4 + 8 + 8 + 4);
-    bytes += (double)(C.r_flags.size() + C.r_gvk.size() + C.r_nsa.size()) * 4;
-    bytes += (double)C.n * P.rules.size() * (masks ? 5 : 1);
-    ev.bytes = bytes;
+    ev.bytes = scan_bytes(P, C, B.need, masks);
     dev->pending.push_back(ev);
   }
   return KPE_OK;
@@ -482,15 +560,17 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
   auto& B = c->d->bind;
   if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
   size_t R = prog->p->rules.size(), cells = (size_t)c->c->n * R;
-  HIPCHK(hipStreamSynchronize(dev->stream));
-  if (verdicts && cells) HIPCHK(hipMemcpy(verdicts, B.verdicts.p, cells, hipMemcpyDeviceToHost));
-  if (masks && cells) {
-    if (!c->d->has_masks) return fail(KPE_E_STATE, "check masks were not computed");
-    HIPCHK(hipMemcpy(masks, B.masks.p, cells * 4, hipMemcpyDeviceToHost));
-  }
+  hipStream_t s = dev->stream;
   if (counts && R) {
+    const unsigned long long* src = B.counts_global.as<unsigned long long>();
+    if (R <= KPE_SMALL_R) {
+      HIPCHK(kpe_launch_count_reduce(B.counts_part.as<uint32_t>(), B.scan_blocks, (uint32_t)(R * 6),
+                                     B.counts_out.as<unsigned long long>(), s));
+      src = B.counts_out.as<unsigned long long>();
+    }
     std::vector<unsigned long long> h(R * 6);
-    HIPCHK(hipMemcpy(h.data(), B.counts.p, R * 6 * 8, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpyAsync(h.data(), src, R * 6 * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
     for (size_t r = 0; r < R; ++r) {
       uint64_t tot = 0;
       for (int k = 1; k < 6; ++k) tot += h[r * 6 + k];
@@ -501,6 +581,12 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
       counts[r].error = h[r * 6 + 4];
       counts[r].skip = h[r * 6 + 5];
     }
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  if (verdicts && cells) HIPCHK(hipMemcpy(verdicts, B.verdicts.p, cells, hipMemcpyDeviceToHost));
+  if (masks && cells) {
+    if (!c->d->has_masks) return fail(KPE_E_STATE, "check masks were not computed");
+    HIPCHK(hipMemcpy(masks, B.masks.p, cells * 4, hipMemcpyDeviceToHost));
   }
   return KPE_OK;
 }
