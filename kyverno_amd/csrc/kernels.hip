@@ -1,29 +1,29 @@
 // CDNA4 (gfx950) kernels for batch policy evaluation. wave64, HBM-bound scans.
 //
-//  kpe_pred_kernel   — dictionary pass for LARGE domains (names, namespaces, ...):
-//                      every string predicate of the compiled program (an OR of
-//                      go-wildcard globs, ext/wildcard/match.go:7-9) is evaluated
-//                      once per DISTINCT string of its domain into a bitset (wave
-//                      ballots, one bit per dictionary id).
-//  kpe_scan_kernel   — one resource per lane. Per block: (1) the compiled program
-//                      and the bitsets of predicates over SMALL domains (kinds,
-//                      capabilities, sysctls, annotation keys/values) are built
-//                      in LDS, so a step is a single launch when no large-domain
-//                      predicate exists; (2) the block's containers are streamed
+//  kpe_pred_kernel   — dictionary pass: every string predicate of the compiled
+//                      program (an OR of go-wildcard globs, ext/wildcard/match.go:7-9)
+//                      is evaluated once per DISTINCT string of its domain into a
+//                      bitset (one wave = 64 dictionary ids, built with a ballot).
+//                      Patterns are host-classified (exact / prefix / suffix /
+//                      contains / general glob) so the common cases are straight
+//                      byte compares without backtracking.
+//  kpe_scan_kernel   — one resource per lane. Per block: (1) the compiled program,
+//                      the predicate directory and the small-domain bitsets are
+//                      copied into LDS; (2) the block's containers are streamed
 //                      coalesced through LDS and OR-reduced per resource (the
 //                      1..64-container fan-out never diverges the HBM loads);
-//                      (3) PSA versioned checks (pkg/pss/evaluate.go:24-70 over
-//                      PSA v0.29 policy/check_*.go); (4) match/exclude per rule
-//                      (pkg/engine/utils/match.go:168-300) with ApplyOne
-//                      (pkg/engine/validation.go:75-77); (5) verdict cells staged
-//                      in LDS and written as coalesced dwords; per-rule counters
-//                      by wave ballot into per-block partials (no atomics, no memset).
+//                      (3) PSA versioned checks (pkg/pss/evaluate.go:24-70 over the
+//                      PSA v0.29 policy/check_*.go semantics); (4) match/exclude per
+//                      rule (pkg/engine/utils/match.go:168-300) with ApplyOne
+//                      (pkg/engine/validation.go:75-77); (5) verdict cells staged in
+//                      LDS and written as coalesced dwords; per-rule counters by
+//                      wave ballot into per-block partials (no atomics, no memset).
 //  kpe_count_reduce  — sums the per-block counter partials (fetch time only).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "schema.h"
 #include "kernels_abi.h"
+#include "schema.h"
 
 namespace {
 
@@ -40,7 +40,6 @@ __device__ __forceinline__ int rune_len(const uint8_t* s, int i, int n) {
 
 __device__ bool glob(const uint8_t* p, int pn, const uint8_t* s, int sn) {
   if (pn == 0) return sn == 0;
-  if (pn == 1 && p[0] == '*') return true;
   int pi = 0, si = 0, star = -1, mark = 0;
   while (si < sn) {
     if (pi < pn && p[pi] == '?') {
@@ -64,13 +63,26 @@ __device__ bool glob(const uint8_t* p, int pn, const uint8_t* s, int sn) {
   return pi == pn;
 }
 
-__device__ __forceinline__ bool match_any(const uint8_t* pat_bytes, const uint32_t* pat_off, uint32_t pat0,
-                                          uint32_t npat, const uint8_t* s, int sn) {
-  for (uint32_t k = 0; k < npat; ++k) {
-    uint32_t p0 = pat_off[pat0 + k], p1 = pat_off[pat0 + k + 1];
-    if (glob(pat_bytes + p0, (int)(p1 - p0), s, sn)) return true;
+__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int n) {
+  for (int i = 0; i < n; ++i)
+    if (a[i] != b[i]) return false;
+  return true;
+}
+
+__device__ bool pat_match(const KpePat& pt, const uint8_t* pb, const uint8_t* s, int sn) {
+  const uint8_t* lit = pb + pt.off;
+  const int ln = (int)pt.len;
+  switch (pt.kind) {
+    case PK_ANY: return true;
+    case PK_EXACT: return sn == ln && bytes_eq(lit, s, ln);
+    case PK_PREFIX: return sn >= ln && bytes_eq(lit, s, ln);
+    case PK_SUFFIX: return sn >= ln && bytes_eq(lit, s + sn - ln, ln);
+    case PK_CONTAINS:
+      for (int i = 0; i + ln <= sn; ++i)
+        if (bytes_eq(lit, s + i, ln)) return true;
+      return false;
+    default: return glob(lit, ln, s, sn);
   }
-  return false;
 }
 
 }  // namespace
@@ -81,37 +93,45 @@ __global__ void __launch_bounds__(256) kpe_pred_kernel(PredArgs a) {
   uint32_t j = 0;
   while (j + 1 < a.njobs && a.jobs[j + 1].blk0 <= b) ++j;  // uniform per block
   const PredJob job = a.jobs[j];
-  uint32_t id = (b - job.blk0) * 256u + threadIdx.x;
-  uint32_t n = a.dict_n[job.domain];
+  const uint32_t id = (b - job.blk0) * 256u + threadIdx.x;
+  const uint32_t n = a.dict_n[job.domain];
   bool hit = false;
   if (id < n) {
     const uint32_t* off = a.dict_off[job.domain];
-    hit = match_any(a.pat_bytes, a.pat_off, job.pat0, job.npat, a.dict_bytes[job.domain] + off[id],
-                    (int)(off[id + 1] - off[id]));
+    const uint8_t* s = a.dict_bytes[job.domain] + off[id];
+    const int sn = (int)(off[id + 1] - off[id]);
+    for (uint32_t k = 0; k < job.npat && !hit; ++k) hit = pat_match(a.pats[job.pat0 + k], a.pat_bytes, s, sn);
   }
-  uint64_t m = __ballot(hit);
-  uint32_t wid = id >> 6;  // 64 strings per wave => two output words
+  const uint64_t m = __ballot(hit);
+  const uint32_t wid = id >> 6;  // 64 strings per wave => two output words
   if ((threadIdx.x & 63u) == 0 && (uint64_t)wid * 64u < n) {
     a.out[job.out_word + 2 * wid] = (uint32_t)m;
     a.out[job.out_word + 2 * wid + 1] = (uint32_t)(m >> 32);
   }
 }
 
+// one block per counter column; coalesced over blocks-of-partials
 __global__ void __launch_bounds__(256) kpe_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
                                                         unsigned long long* out) {
-  uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i >= width) return;
+  __shared__ unsigned long long red[256];
+  const uint32_t col = blockIdx.x;
   unsigned long long s = 0;
-  for (uint32_t b = 0; b < nblocks; ++b) s += part[(size_t)b * width + i];
-  out[i] = s;
+  for (uint32_t b = threadIdx.x; b < nblocks; b += 256) s += part[(size_t)b * width + col];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[col] = red[0];
 }
 
 // ---------------------------------------------------------------------------
 namespace {
 
 constexpr uint32_t kBlock = 256;
-constexpr uint32_t kChunk = 1024;      // containers staged per LDS pass
-constexpr uint32_t kStageV = 8192;     // verdict staging bytes (R <= 32)
+constexpr uint32_t kChunk = 1024;   // containers staged per LDS pass
+constexpr uint32_t kStageV = 8192;  // verdict staging bytes (R <= 32)
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
@@ -122,110 +142,11 @@ __constant__ uint8_t kCvCheck[KPE_NUM_CV] = {
     CK_RUN_AS_USER, CK_SELINUX, CK_SECCOMP_BASELINE, CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED,
     CK_SECCOMP_RESTRICTED, CK_SYSCTLS, CK_SYSCTLS, CK_SYSCTLS, CK_WIN_HOST_PROCESS};
 
-struct Ctx {
-  const ScanArgs& a;
-  const uint32_t* lbits;       // LDS predicate bitsets (small domains)
-  const KpeRule* rules;        // LDS or global
-  const KpeFilter* filters;
-  const KpeTerm* terms;
-  const KpeKindSel* kindsels;
-  const KpeAnnPair* annpairs;
-
-  __device__ __forceinline__ bool pbit(int32_t p, uint32_t id) const {
-    if (id == KPE_NO_STR) return false;
-    uint32_t w = a.pred_word[p];
-    if (w & PRED_LOCAL) return (lbits[(w & ~PRED_LOCAL) + (id >> 5)] >> (id & 31u)) & 1u;
-    return (a.pred_bits[w + (id >> 5)] >> (id & 31u)) & 1u;
-  }
-  __device__ __forceinline__ uint64_t pmask64(int32_t p) const {  // predicate over D_CAP (<= 64 ids)
-    if (p < 0) return 0;
-    uint32_t w = a.pred_word[p];
-    const uint32_t* b = (w & PRED_LOCAL) ? lbits + (w & ~PRED_LOCAL) : a.pred_bits + w;
-    return (uint64_t)b[0] | ((uint64_t)b[1] << 32);
-  }
-
-  __device__ bool filter(uint32_t f, int64_t r, uint32_t gvk) const {
-    KpeFilter fl = filters[f];
-    for (uint32_t t = 0; t < fl.nterms; ++t) {
-      KpeTerm tm = terms[fl.term0 + t];
-      bool ok;
-      switch (tm.type) {
-        case T_KINDS: {
-          ok = false;
-          for (uint32_t s = 0; s < tm.b && !ok; ++s) {
-            KpeKindSel ks = kindsels[tm.a + s];
-            ok = ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) &&
-                 (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
-          }
-          break;
-        }
-        case T_PRED: {
-          uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : a.r_nsa[r]);
-          ok = pbit((int32_t)tm.a, id);
-          break;
-        }
-        case T_ANNOTATIONS: {
-          ok = true;
-          uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
-          for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
-            KpeAnnPair pr = annpairs[tm.a + pi];
-            bool m = false;
-            for (uint32_t j = lo; j < hi && !m; ++j) m = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
-            ok = m;
-          }
-          break;
-        }
-        default: ok = false;
-      }
-      if (!ok) return false;
-    }
-    return true;
-  }
-  __device__ bool block_any_all(uint32_t mode, uint32_t f0, uint32_t nf, int64_t r, uint32_t gvk) const {
-    if (mode == MODE_ANY) {
-      for (uint32_t f = 0; f < nf; ++f)
-        if (filter(f0 + f, r, gvk)) return true;
-      return false;
-    }
-    if (mode == MODE_ALL) {
-      for (uint32_t f = 0; f < nf; ++f)
-        if (!filter(f0 + f, r, gvk)) return false;
-      return true;
-    }
-    return filter(f0, r, gvk);
-  }
-};
-
-__device__ __forceinline__ uint32_t container_bits(const Ctx& x, uint32_t w, uint64_t add, uint64_t drop, uint32_t sann,
-                                                   uint64_t caps_ok, uint64_t nbs, uint64_t all) {
-  uint32_t b = 0;
-  bool caps = w & C_CAPS_PRESENT;
-  if (FIELD(w, C_APE_SH, 2) != TRI_FALSE) b |= CB_APE;
-  if (caps && (add & ~caps_ok)) b |= CB_CAPS_BASE;
-  if (!caps || !(drop & all)) b |= CB_CAPS_DROP;
-  if (caps && (add & ~nbs)) b |= CB_CAPS_ADD;
-  if (FIELD(w, C_HOSTPORT_SH, 4)) b |= CB_HOSTPORT;
-  if (FIELD(w, C_PRIV_SH, 2) == TRI_TRUE) b |= CB_PRIV;
-  if (FIELD(w, C_PROCMOUNT_SH, 2) == PROCMOUNT_OTHER) b |= CB_PROCMOUNT;
-  uint32_t rnr = FIELD(w, C_RNR_SH, 2);
-  if (rnr == TRI_FALSE) b |= CB_RNR_FALSE;
-  if (rnr == TRI_UNSET) b |= CB_RNR_UNSET;
-  if (FIELD(w, C_RAU_SH, 2) == RAU_ZERO) b |= CB_RAU_ZERO;
-  uint32_t sel = FIELD(w, C_SEL_SH, 3);
-  if (sel != SEL_NONE && (sel == SEL_OTHER || (w & (C_SEL_USER | C_SEL_ROLE)))) b |= CB_SELINUX;
-  uint32_t sec = FIELD(w, C_SECCOMP_SH, 3);
-  if (sec == SECCOMP_NONE) b |= CB_SEC_UNSET;
-  else if (sec != SECCOMP_RUNTIMEDEFAULT && sec != SECCOMP_LOCALHOST) b |= CB_SEC_BAD;
-  if (sann != KPE_NO_STR && !x.pbit(x.a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
-  if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
-  return b;
-}
-
 // PSA versioned checks for one pod given the OR of its container bits.
 __device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_hostpath, bool vol_restricted,
                                              uint32_t sys_bad, bool apparmor_bad, bool sec_pod_ann_bad) {
   uint32_t f = 0;
-  bool win = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS;
+  const bool win = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS;
   if (cb & CB_APE) f |= (1u << CV_APE_1_8) | (win ? 0u : (1u << CV_APE_1_25));
   if (apparmor_bad) f |= 1u << CV_APPARMOR_1_0;
   if (cb & CB_CAPS_BASE) f |= 1u << CV_CAPS_BASELINE_1_0;
@@ -237,17 +158,17 @@ __device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_
   if (cb & CB_PRIV) f |= 1u << CV_PRIVILEGED_1_0;
   if (cb & CB_PROCMOUNT) f |= 1u << CV_PROC_MOUNT_1_0;
   if (vol_restricted) f |= 1u << CV_RESTRICTED_VOLUMES_1_0;
-  uint32_t prnr = FIELD(pw, P_RNR_SH, 2);
+  const uint32_t prnr = FIELD(pw, P_RNR_SH, 2);
   if (prnr == TRI_FALSE || (cb & CB_RNR_FALSE) || (prnr != TRI_TRUE && (cb & CB_RNR_UNSET)))
     f |= 1u << CV_RUN_AS_NON_ROOT_1_0;
   if (FIELD(pw, P_RAU_SH, 2) == RAU_ZERO || (cb & CB_RAU_ZERO)) f |= 1u << CV_RUN_AS_USER_1_23;
-  uint32_t psel = FIELD(pw, P_SEL_SH, 3);
+  const uint32_t psel = FIELD(pw, P_SEL_SH, 3);
   if ((psel != SEL_NONE && (psel == SEL_OTHER || (pw & (P_SEL_USER | P_SEL_ROLE)))) || (cb & CB_SELINUX))
     f |= 1u << CV_SELINUX_1_0;
   if (sec_pod_ann_bad || (cb & CB_SEC_ANN)) f |= 1u << CV_SECCOMP_BASELINE_1_0;
-  uint32_t psec = FIELD(pw, P_SECCOMP_SH, 3);
-  bool psec_valid = psec == SECCOMP_RUNTIMEDEFAULT || psec == SECCOMP_LOCALHOST;
-  bool psec_bad = psec != SECCOMP_NONE && !psec_valid;
+  const uint32_t psec = FIELD(pw, P_SECCOMP_SH, 3);
+  const bool psec_valid = psec == SECCOMP_RUNTIMEDEFAULT || psec == SECCOMP_LOCALHOST;
+  const bool psec_bad = psec != SECCOMP_NONE && !psec_valid;
   if (psec_bad || (cb & CB_SEC_BAD)) f |= 1u << CV_SECCOMP_BASELINE_1_19;
   if (psec_bad || (cb & CB_SEC_BAD) || (!psec_valid && (cb & CB_SEC_UNSET)))
     f |= (1u << CV_SECCOMP_RESTRICTED_1_19) | (win ? 0u : (1u << CV_SECCOMP_RESTRICTED_1_25));
@@ -260,8 +181,10 @@ __device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_
 
 }  // namespace
 
+// STAGED: the program image fits the LDS budget (read from LDS); otherwise from global.
+template <bool STAGED>
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
-  extern __shared__ uint32_t dyn[];  // [program copy (a.prog_words)] [local predicate bits (a.lwords)]
+  extern __shared__ uint32_t dyn[];  // [program image][predicate directory][small-domain bitsets]
   __shared__ uint32_t s_off[kBlock + 1];
   __shared__ uint32_t s_cb[kChunk];
   __shared__ uint32_t s_cnt[6 * KPE_SMALL_R];
@@ -276,40 +199,48 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const bool small_r = R <= KPE_SMALL_R;
   const bool stage_v = R * kBlock <= kStageV;
 
-  // ---- (1) program + small-domain predicate bitsets into LDS ----
-  uint32_t* lprog = dyn;
-  uint32_t* lbits = dyn + a.prog_words;
-  for (uint32_t i = t; i < a.prog_words; i += kBlock) lprog[i] = a.prog[i];
-  for (uint32_t i = t; i < a.lwords; i += kBlock) lbits[i] = 0;
+  // ---- (1) program, predicate directory and small-domain bitsets into LDS ----
+  const uint32_t pw_off = STAGED ? a.prog_words : 0u;
+  uint32_t* s_pw = dyn + pw_off;
+  uint32_t* s_bits = s_pw + a.npreds;
+  if (STAGED)
+    for (uint32_t i = t; i < a.prog_words; i += kBlock) dyn[i] = a.prog[i];
+  for (uint32_t i = t; i < a.npreds; i += kBlock) s_pw[i] = a.pred_word[i];
+  for (uint32_t i = t; i < a.lwords; i += kBlock) s_bits[i] = a.pred_bits[i];
   if (small_r)
     for (uint32_t i = t; i < 6 * R; i += kBlock) s_cnt[i] = 0;
-  __syncthreads();
-  for (uint32_t i = t; i < a.lpairs; i += kBlock) {  // (predicate, string) pairs of small domains
-    uint32_t j = 0;
-    while (j + 1 < a.nlpreds && a.lpreds[j + 1].pair0 <= i) ++j;
-    const LocalPred lp = a.lpreds[j];
-    uint32_t id = i - lp.pair0;
-    const uint32_t* off = a.dict_off[lp.domain];
-    if (match_any(a.pat_bytes, a.pat_off, lp.pat0, lp.npat, a.dict_bytes[lp.domain] + off[id],
-                  (int)(off[id + 1] - off[id])))
-      atomicOr(&lbits[lp.word0 + (id >> 5)], 1u << (id & 31u));
-  }
-  const bool staged = a.prog_words != 0;
-  const Ctx x{a, lbits,
-              staged ? reinterpret_cast<const KpeRule*>(lprog + a.off_rules) : a.rules,
-              staged ? reinterpret_cast<const KpeFilter*>(lprog + a.off_filters) : a.filters,
-              staged ? reinterpret_cast<const KpeTerm*>(lprog + a.off_terms) : a.terms,
-              staged ? reinterpret_cast<const KpeKindSel*>(lprog + a.off_kindsels) : a.kindsels,
-              staged ? reinterpret_cast<const KpeAnnPair*>(lprog + a.off_annpairs) : a.annpairs};
   if (a.any_pss)
     for (uint32_t i = t; i <= np; i += kBlock) s_off[i] = a.ctr_off[p0 + i];
   __syncthreads();
+
+  const KpeRule* rules = STAGED ? reinterpret_cast<const KpeRule*>(dyn + a.off_rules) : a.rules;
+  const KpeFilter* filters = STAGED ? reinterpret_cast<const KpeFilter*>(dyn + a.off_filters) : a.filters;
+  const KpeTerm* terms = STAGED ? reinterpret_cast<const KpeTerm*>(dyn + a.off_terms) : a.terms;
+  const KpeKindSel* kindsels = STAGED ? reinterpret_cast<const KpeKindSel*>(dyn + a.off_kindsels) : a.kindsels;
+  const KpeAnnPair* annpairs = STAGED ? reinterpret_cast<const KpeAnnPair*>(dyn + a.off_annpairs) : a.annpairs;
+  const uint32_t* gbits = a.pred_bits;
+
+  auto pbit = [&](int32_t p, uint32_t id) -> bool {
+    if (id == KPE_NO_STR) return false;
+    const uint32_t w = s_pw[p];
+    const uint32_t word = (w & PRED_LOCAL) ? s_bits[(w & ~PRED_LOCAL) + (id >> 5)] : gbits[w + (id >> 5)];
+    return (word >> (id & 31u)) & 1u;
+  };
+  auto pmask64 = [&](int32_t p) -> uint64_t {  // predicate over D_CAP (<= 64 ids)
+    if (p < 0) return 0;
+    const uint32_t w = s_pw[p];
+    if (w & PRED_LOCAL) {
+      const uint32_t o = w & ~PRED_LOCAL;
+      return (uint64_t)s_bits[o] | ((uint64_t)s_bits[o + 1] << 32);
+    }
+    return (uint64_t)gbits[w] | ((uint64_t)gbits[w + 1] << 32);
+  };
 
   // ---- (2)+(3) PSS: containers through LDS, pod-level lists, versioned checks ----
   uint32_t fails = 0;
   if (a.any_pss) {
     const uint32_t c_begin = s_off[0], c_end = s_off[np];
-    const uint64_t caps_ok = x.pmask64(a.pp_caps_ok), nbs = x.pmask64(a.pp_cap_nbs), all = x.pmask64(a.pp_cap_all);
+    const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
     const bool need_caps = a.need & NEED_CAPS, need_sann = a.need & NEED_SANN;
     uint32_t cb = 0;
     const uint32_t my_lo = live ? s_off[t] : 0, my_hi = live ? s_off[t + 1] : 0;
@@ -317,8 +248,34 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
       const uint32_t lim = (c_end - base) < kChunk ? (c_end - base) : kChunk;
       for (uint32_t i = t; i < lim; i += kBlock) {
         const uint32_t c = base + i;
-        s_cb[i] = container_bits(x, a.c_sc[c], need_caps ? a.c_add[c] : 0ull, need_caps ? a.c_drop[c] : ~0ull,
-                                 need_sann ? a.c_sann[c] : KPE_NO_STR, caps_ok, nbs, all);
+        const uint32_t w = a.c_sc[c];
+        uint32_t b = 0;
+        const bool caps = w & C_CAPS_PRESENT;
+        if (need_caps) {
+          const uint64_t add = a.c_add[c], drop = a.c_drop[c];
+          if (caps && (add & ~caps_ok)) b |= CB_CAPS_BASE;
+          if (!caps || !(drop & all)) b |= CB_CAPS_DROP;
+          if (caps && (add & ~nbs)) b |= CB_CAPS_ADD;
+        }
+        if (FIELD(w, C_APE_SH, 2) != TRI_FALSE) b |= CB_APE;
+        if (FIELD(w, C_HOSTPORT_SH, 4)) b |= CB_HOSTPORT;
+        if (FIELD(w, C_PRIV_SH, 2) == TRI_TRUE) b |= CB_PRIV;
+        if (FIELD(w, C_PROCMOUNT_SH, 2) == PROCMOUNT_OTHER) b |= CB_PROCMOUNT;
+        const uint32_t rnr = FIELD(w, C_RNR_SH, 2);
+        if (rnr == TRI_FALSE) b |= CB_RNR_FALSE;
+        if (rnr == TRI_UNSET) b |= CB_RNR_UNSET;
+        if (FIELD(w, C_RAU_SH, 2) == RAU_ZERO) b |= CB_RAU_ZERO;
+        const uint32_t sel = FIELD(w, C_SEL_SH, 3);
+        if (sel != SEL_NONE && (sel == SEL_OTHER || (w & (C_SEL_USER | C_SEL_ROLE)))) b |= CB_SELINUX;
+        const uint32_t sec = FIELD(w, C_SECCOMP_SH, 3);
+        if (sec == SECCOMP_NONE) b |= CB_SEC_UNSET;
+        else if (sec != SECCOMP_RUNTIMEDEFAULT && sec != SECCOMP_LOCALHOST) b |= CB_SEC_BAD;
+        if (need_sann) {
+          const uint32_t sann = a.c_sann[c];
+          if (sann != KPE_NO_STR && !pbit(a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
+        }
+        if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
+        s_cb[i] = b;
       }
       __syncthreads();
       const uint32_t lo = my_lo > base ? my_lo : base, hi = my_hi < base + lim ? my_hi : base + lim;
@@ -338,16 +295,16 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
       if (a.need & NEED_SYS)
         for (uint32_t j = a.sys_off[r], e = a.sys_off[r + 1]; j < e; ++j) {
           const uint32_t id = a.sys_id[j];
-          if (!x.pbit(a.pp_sysctl0, id)) sys_bad |= 1u;
-          if (!x.pbit(a.pp_sysctl1, id)) sys_bad |= 2u;
-          if (!x.pbit(a.pp_sysctl2, id)) sys_bad |= 4u;
+          if (!pbit(a.pp_sysctl0, id)) sys_bad |= 1u;
+          if (!pbit(a.pp_sysctl1, id)) sys_bad |= 2u;
+          if (!pbit(a.pp_sysctl2, id)) sys_bad |= 4u;
         }
       bool apparmor_bad = false, sec_pod_ann_bad = false;
       if (a.need & NEED_PANN)
         for (uint32_t j = a.pann_off[r], e = a.pann_off[r + 1]; j < e; ++j) {
           const uint32_t k = a.pann_k[j], v = a.pann_v[j];
-          apparmor_bad |= x.pbit(a.pp_apparmor_key, k) && !x.pbit(a.pp_apparmor_ok, v);
-          sec_pod_ann_bad |= x.pbit(a.pp_seccomp_pod_key, k) && !x.pbit(a.pp_seccomp_ann_ok, v);
+          apparmor_bad |= pbit(a.pp_apparmor_key, k) && !pbit(a.pp_apparmor_ok, v);
+          sec_pod_ann_bad |= pbit(a.pp_seccomp_pod_key, k) && !pbit(a.pp_seccomp_ann_ok, v);
         }
       fails = cv_fails(pw, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
     }
@@ -356,11 +313,56 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   // ---- (4) rules: match/exclude, handler, ApplyOne, verdict cell ----
   const uint32_t flags = (live && (a.need & NEED_FLAGS)) ? a.r_flags[r] : 0;
   const uint32_t gvk = (live && (a.need & NEED_GVK)) ? a.r_gvk[r] : 0;
+  auto filter = [&](uint32_t f) -> bool {
+    const KpeFilter fl = filters[f];
+    for (uint32_t ti = 0; ti < fl.nterms; ++ti) {
+      const KpeTerm tm = terms[fl.term0 + ti];
+      bool ok;
+      if (tm.type == T_KINDS) {
+        ok = false;
+        for (uint32_t s = 0; s < tm.b && !ok; ++s) {
+          const KpeKindSel ks = kindsels[tm.a + s];
+          ok = ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) &&
+               (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
+        }
+      } else if (tm.type == T_PRED) {
+        const uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : a.r_nsa[r]);
+        ok = pbit((int32_t)tm.a, id);
+      } else if (tm.type == T_ANNOTATIONS) {
+        ok = true;
+        const uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
+        for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
+          const KpeAnnPair pr = annpairs[tm.a + pi];
+          bool m = false;
+          for (uint32_t j = lo; j < hi && !m; ++j) m = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
+          ok = m;
+        }
+      } else {
+        ok = false;
+      }
+      if (!ok) return false;
+    }
+    return true;
+  };
+  auto block_match = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> bool {
+    if (mode == MODE_ANY) {
+      for (uint32_t f = 0; f < nf; ++f)
+        if (filter(f0 + f)) return true;
+      return false;
+    }
+    if (mode == MODE_ALL) {
+      for (uint32_t f = 0; f < nf; ++f)
+        if (!filter(f0 + f)) return false;
+      return true;
+    }
+    return filter(f0);
+  };
+
   bool applied = false;
   uint32_t cur_policy = 0xFFFFFFFFu;
   const uint32_t lane = t & 63u;
   for (uint32_t ri = 0; ri < R; ++ri) {
-    const KpeRule rule = x.rules[ri];
+    const KpeRule rule = rules[ri];
     if (rule.policy != cur_policy) {
       cur_policy = rule.policy;
       applied = false;
@@ -368,18 +370,18 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     uint32_t v = KPE_NA_;
     uint32_t cmask = 0;
     if (live && !(rule.apply_one && applied)) {
-      bool m = rule.pol_ns_pred < 0 || x.pbit(rule.pol_ns_pred, a.r_nsa[r]);
-      m = m && x.block_any_all(rule.match_mode, rule.match_f0, rule.match_nf, r, gvk);
+      bool m = rule.pol_ns_pred < 0 || pbit(rule.pol_ns_pred, a.r_nsa[r]);
+      m = m && block_match(rule.match_mode, rule.match_f0, rule.match_nf);
       if (m) {
         bool ex;
         if (rule.excl_mode == MODE_ANY) {
           ex = false;
-          for (uint32_t f = 0; f < rule.excl_nf && !ex; ++f) ex = x.filter(rule.excl_f0 + f, r, gvk);
+          for (uint32_t f = 0; f < rule.excl_nf && !ex; ++f) ex = filter(rule.excl_f0 + f);
         } else if (rule.excl_mode == MODE_ALL) {
           ex = true;
-          for (uint32_t f = 0; f < rule.excl_nf && ex; ++f) ex = x.filter(rule.excl_f0 + f, r, gvk);
+          for (uint32_t f = 0; f < rule.excl_nf && ex; ++f) ex = filter(rule.excl_f0 + f);
         } else {
-          ex = x.filter(rule.excl_f0, r, gvk);
+          ex = filter(rule.excl_f0);
         }
         m = !ex;
       }
@@ -417,7 +419,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   __syncthreads();
   if (stage_v) {
     const uint32_t bytes = np * R;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);  // p0*R*1 is 4-byte aligned
+    uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);  // p0*R is a multiple of 4
     const uint32_t* src = reinterpret_cast<const uint32_t*>(s_v);
     for (uint32_t w = t; w < bytes / 4; w += kBlock) dst[w] = src[w];
     if (t < (bytes & 3u)) a.verdicts[(size_t)p0 * R + (bytes & ~3u) + t] = s_v[(bytes & ~3u) + t];
@@ -436,13 +438,16 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipSt
 extern "C" uint32_t kpe_scan_blocks(int64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s) {
   if (a->n == 0) return hipSuccess;
-  size_t dyn = (size_t)(a->prog_words + a->lwords) * 4;
-  hipLaunchKernelGGL(kpe_scan_kernel, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
+  const size_t dyn = (size_t)(a->prog_words + a->npreds + a->lwords) * 4;
+  if (a->prog_words)
+    hipLaunchKernelGGL(kpe_scan_kernel<true>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
+  else
+    hipLaunchKernelGGL(kpe_scan_kernel<false>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
   return hipGetLastError();
 }
 extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
                                               unsigned long long* out, hipStream_t s) {
   if (width == 0) return hipSuccess;
-  hipLaunchKernelGGL(kpe_count_reduce, dim3((width + 255) / 256), dim3(256), 0, s, part, nblocks, width, out);
+  hipLaunchKernelGGL(kpe_count_reduce, dim3(width), dim3(256), 0, s, part, nblocks, width, out);
   return hipGetLastError();
 }

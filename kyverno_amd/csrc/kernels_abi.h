@@ -17,6 +17,17 @@
 #define NEED_PANN (1u << 6)
 #define NEED_NSA (1u << 7)
 
+// Pattern classes (host-classified go-wildcard patterns; '?' or an inner '*' => PK_GLOB)
+#define PK_ANY 0u       // "*"
+#define PK_EXACT 1u     // no wildcard
+#define PK_PREFIX 2u    // "lit*"
+#define PK_SUFFIX 3u    // "*lit"
+#define PK_CONTAINS 4u  // "*lit*"
+#define PK_GLOB 5u      // general: full pattern text
+struct KpePat {
+  uint32_t kind, off, len, pad;  // literal (or full pattern for PK_GLOB) = pat_bytes[off, off+len)
+};
+
 struct PredJob {
   uint32_t domain;
   uint32_t pat0, npat;  // patterns [pat0, pat0+npat) of the pattern table
@@ -29,15 +40,12 @@ struct PredArgs {
   const uint32_t* dict_off[KPE_NUM_DOMAINS];
   uint32_t dict_n[KPE_NUM_DOMAINS];
   const uint8_t* pat_bytes;
-  const uint32_t* pat_off;
+  const KpePat* pats;
   const PredJob* jobs;
   uint32_t njobs;
   uint32_t* out;
 };
 
-struct LocalPred {  // predicate over a small domain, evaluated per scan block into LDS
-  uint32_t domain, pat0, npat, word0, pair0;
-};
 
 struct ScanArgs {
   int64_t n;
@@ -60,14 +68,10 @@ struct ScanArgs {
   const uint32_t* prog;
   uint32_t prog_words, off_rules, off_filters, off_terms, off_kindsels, off_annpairs;
   // predicates
-  const uint32_t* pred_bits;
-  const uint32_t* pred_word;  // per predicate: global word offset, or PRED_LOCAL | LDS word offset
-  const LocalPred* lpreds;
-  uint32_t nlpreds, lpairs, lwords;
-  const uint8_t* dict_bytes[KPE_NUM_DOMAINS];
-  const uint32_t* dict_off[KPE_NUM_DOMAINS];
-  const uint8_t* pat_bytes;
-  const uint32_t* pat_off;
+  const uint32_t* pred_bits;   // all predicate bitsets (dictionary pass output)
+  const uint32_t* pred_word;   // per predicate: global word offset, or PRED_LOCAL | LDS word offset
+  uint32_t npreds;
+  uint32_t lwords;             // pred_bits[0, lwords) = small-domain bitsets, copied into LDS per block
   int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, any_pss, need;

@@ -77,7 +77,7 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 // LDS budgets of the scan kernel's dynamic region
 constexpr uint32_t kMaxProgWords = 4096;   // 16 KiB program image
 constexpr uint32_t kMaxLocalWords = 8192;  // 32 KiB of small-domain predicate bitsets
-constexpr uint32_t kMaxLocalPairs = 4096;  // (predicate, string) globs evaluated per block
+constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
 
 }  // namespace
 
@@ -109,17 +109,17 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
-  DevBuf rules, filters, terms, kindsels, annpairs, pat_bytes, pat_off, image;
+  DevBuf rules, filters, terms, kindsels, annpairs, pat_bytes, pats, image;
   std::vector<uint8_t> pat_bytes_h;
-  std::vector<uint32_t> pat_off_h;  // pattern k of predicate p: pat0[p] + k
+  std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
   uint32_t image_words = 0, off_rules = 0, off_filters = 0, off_terms = 0, off_kindsels = 0, off_annpairs = 0;
 };
 
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
   const Program* prog = nullptr;
-  DevBuf jobs, pred_word, pred_bits, lpreds, verdicts, masks, counts_part, counts_global, counts_out;
-  uint32_t nblocks = 0, njobs = 0, nlpreds = 0, lpairs = 0, lwords = 0, scan_blocks = 0;
+  DevBuf jobs, pred_word, pred_bits, verdicts, masks, counts_part, counts_global, counts_out;
+  uint32_t nblocks = 0, njobs = 0, lwords = 0, scan_blocks = 0;
   uint32_t need = 0;
   double scan_bytes = 0;
   size_t cells = 0;
@@ -272,6 +272,33 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
 
 namespace {
 
+// go-wildcard pattern -> device pattern class (the literal is stored; only a
+// '?' or an inner '*' needs the general backtracking matcher).
+KpePat classify_pattern(const std::string& g, std::vector<uint8_t>& bytes) {
+  KpePat p{PK_GLOB, (uint32_t)bytes.size(), 0, 0};
+  auto put = [&](const std::string& lit) {
+    p.off = (uint32_t)bytes.size();
+    p.len = (uint32_t)lit.size();
+    bytes.insert(bytes.end(), lit.begin(), lit.end());
+  };
+  size_t stars = std::count(g.begin(), g.end(), '*');
+  bool q = g.find('?') != std::string::npos;
+  if (g == "*") p.kind = PK_ANY;
+  else if (!q && stars == 0) p.kind = PK_EXACT;
+  else if (!q && stars == 1 && g.back() == '*') p.kind = PK_PREFIX;
+  else if (!q && stars == 1 && g.front() == '*') p.kind = PK_SUFFIX;
+  else if (!q && stars == 2 && g.size() >= 2 && g.front() == '*' && g.back() == '*') p.kind = PK_CONTAINS;
+  switch (p.kind) {
+    case PK_ANY: put(""); break;
+    case PK_EXACT: put(g); break;
+    case PK_PREFIX: put(g.substr(0, g.size() - 1)); break;
+    case PK_SUFFIX: put(g.substr(1)); break;
+    case PK_CONTAINS: put(g.substr(1, g.size() - 2)); break;
+    default: put(g);
+  }
+  return p;
+}
+
 template <class T>
 void append_words(std::vector<uint32_t>& img, const std::vector<T>& v, uint32_t* off) {
   static_assert(sizeof(T) % 4 == 0, "program tables are word-sized");
@@ -288,13 +315,9 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   auto& D = *P.dev;
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
-  D.pat_off_h.assign(1, 0);
   for (auto& pr : P.preds) {
-    D.pat0.push_back((uint32_t)D.pat_off_h.size() - 1);
-    for (auto& g : pr.globs) {
-      D.pat_bytes_h.insert(D.pat_bytes_h.end(), g.begin(), g.end());
-      D.pat_off_h.push_back((uint32_t)D.pat_bytes_h.size());
-    }
+    D.pat0.push_back((uint32_t)D.pats_h.size());
+    for (auto& g : pr.globs) D.pats_h.push_back(classify_pattern(g, D.pat_bytes_h));
   }
   std::vector<uint32_t> img;
   append_words(img, P.rules, &D.off_rules);
@@ -309,7 +332,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   HIPCHK(upload(D.kindsels, P.kindsels, s));
   HIPCHK(upload(D.annpairs, P.annpairs, s));
   HIPCHK(upload(D.pat_bytes, D.pat_bytes_h, s));
-  HIPCHK(upload(D.pat_off, D.pat_off_h, s));
+  HIPCHK(upload(D.pats, D.pats_h, s));
   HIPCHK(upload(D.image, img, s));
   HIPCHK(hipStreamSynchronize(s));
   return KPE_OK;
@@ -369,37 +392,45 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   size_t cells = (size_t)C.n * P.rules.size();
   if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
   hipStream_t s = dev->stream;
-  // predicate placement: small domains are evaluated per scan block into LDS,
-  // large ones by the dictionary pass into a global bitset.
+  // predicate placement: every predicate is evaluated by the dictionary pass;
+  // small-domain bitsets are laid out first ([0, lwords)) so each scan block
+  // copies them into LDS with one loop, large ones stay in global memory.
   std::vector<PredJob> jobs;
-  std::vector<LocalPred> lps;
   std::vector<uint32_t> word(P.preds.size());
-  uint32_t gw = 0, blk = 0, lw = 0, lpairs = 0;
-  for (size_t p = 0; p < P.preds.size(); ++p) {
+  std::vector<uint32_t> order;
+  uint32_t lw = 0;
+  for (int pass = 0; pass < 2; ++pass)
+    for (size_t p = 0; p < P.preds.size(); ++p) {
+      uint32_t n = C.dict[P.preds[p].domain].size();
+      uint32_t nwords = ((n + 63) / 64) * 2 + 2;
+      bool small = lw + nwords <= kMaxLocalWords && n <= kMaxLocalPairs;
+      if (pass == 0 && small) {
+        order.push_back((uint32_t)p);
+        lw += nwords;
+      } else if (pass == 1 && std::find(order.begin(), order.end(), (uint32_t)p) == order.end()) {
+        order.push_back((uint32_t)p);
+      }
+    }
+  uint32_t gw = 0, blk = 0, nlocal = 0;
+  for (size_t i = 0; i < order.size(); ++i) {
+    uint32_t p = order[i];
     const auto& pr = P.preds[p];
     uint32_t n = C.dict[pr.domain].size();
     uint32_t nwords = ((n + 63) / 64) * 2 + 2;
-    uint32_t npat = (uint32_t)pr.globs.size();
-    if (lw + nwords <= kMaxLocalWords && lpairs + n <= kMaxLocalPairs) {
-      lps.push_back({pr.domain, PD.pat0[p], npat, lw, lpairs});
-      word[p] = PRED_LOCAL | lw;
-      lw += nwords;
-      lpairs += n;
-    } else {
-      jobs.push_back({pr.domain, PD.pat0[p], npat, gw, blk});
-      word[p] = gw;
-      gw += nwords;
+    bool local = gw + nwords <= lw;
+    word[p] = local ? (PRED_LOCAL | gw) : gw;
+    nlocal += local;
+    if (n) {
+      jobs.push_back({pr.domain, PD.pat0[p], (uint32_t)pr.globs.size(), gw, blk});
       blk += (n + 255) / 256;
     }
+    gw += nwords;
   }
+  B.lwords = lw;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  B.nlpreds = (uint32_t)lps.size();
-  B.lpairs = lpairs;
-  B.lwords = lw;
   B.scan_blocks = kpe_scan_blocks(C.n);
   HIPCHK(upload(B.jobs, jobs, s));
-  HIPCHK(upload(B.lpreds, lps, s));
   HIPCHK(upload(B.pred_word, word, s));
   HIPCHK(B.pred_bits.ensure(std::max<size_t>(gw, 1) * 4));
   HIPCHK(hipMemsetAsync(B.pred_bits.p, 0, std::max<size_t>(gw, 1) * 4, s));
@@ -442,7 +473,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.dict_n[i] = C.dict[i].size();
     }
     pa.pat_bytes = PD.pat_bytes.as<uint8_t>();
-    pa.pat_off = PD.pat_off.as<uint32_t>();
+    pa.pats = PD.pats.as<KpePat>();
     pa.jobs = B.jobs.as<PredJob>();
     pa.njobs = B.njobs;
     pa.out = B.pred_bits.as<uint32_t>();
@@ -488,16 +519,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.off_annpairs = PD.off_annpairs;
   sa.pred_bits = B.pred_bits.as<uint32_t>();
   sa.pred_word = B.pred_word.as<uint32_t>();
-  sa.lpreds = B.lpreds.as<LocalPred>();
-  sa.nlpreds = B.nlpreds;
-  sa.lpairs = B.lpairs;
+  sa.npreds = (uint32_t)P.preds.size();
   sa.lwords = B.lwords;
-  for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
-    sa.dict_bytes[i] = D.dict_bytes[i].as<uint8_t>();
-    sa.dict_off[i] = D.dict_off[i].as<uint32_t>();
-  }
-  sa.pat_bytes = PD.pat_bytes.as<uint8_t>();
-  sa.pat_off = PD.pat_off.as<uint32_t>();
   sa.pp_apparmor_key = P.pss.apparmor_key;
   sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
   sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;
