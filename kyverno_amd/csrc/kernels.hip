@@ -132,6 +132,7 @@ namespace {
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kChunk = 1024;   // containers staged per LDS pass
 constexpr uint32_t kStageV = 8192;  // verdict staging bytes (R <= 32)
+constexpr uint32_t kListChunk = 1024;  // volumes / sysctls / pod annotations staged per LDS pass
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
@@ -182,11 +183,20 @@ __device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_
 }  // namespace
 
 // STAGED: the program image fits the LDS budget (read from LDS); otherwise from global.
+//
+// Phases (one global round trip each, so a wave's lifetime is ~2 memory latencies):
+//  A  block offsets of every list (containers, volumes, sysctls, pod annotations),
+//     this lane's pod word / flags / gvk, program + predicate bitsets -> LDS/regs
+//  B  every list item of the block streamed coalesced (thread i takes items i, i+256, ...)
+//     and reduced to a few violation bits per item in LDS
+//  C  per-lane OR over its item ranges (LDS only), PSA versioned checks, rule loop,
+//     verdict cells into LDS; then one coalesced store.
 template <bool STAGED>
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   extern __shared__ uint32_t dyn[];  // [program image][predicate directory][small-domain bitsets]
-  __shared__ uint32_t s_off[kBlock + 1];
+  __shared__ uint32_t s_coff[kBlock + 1], s_voff[kBlock + 1], s_soff[kBlock + 1], s_aoff[kBlock + 1];
   __shared__ uint32_t s_cb[kChunk];
+  __shared__ uint8_t s_vb[kListChunk], s_sb[kListChunk], s_ab[kListChunk];
   __shared__ uint32_t s_cnt[6 * KPE_SMALL_R];
   __shared__ __attribute__((aligned(16))) uint8_t s_v[kStageV];
 
@@ -198,8 +208,13 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const uint32_t R = a.nrules;
   const bool small_r = R <= KPE_SMALL_R;
   const bool stage_v = R * kBlock <= kStageV;
+  const uint32_t need = a.need;
+  const bool pss = a.any_pss;
 
-  // ---- (1) program, predicate directory and small-domain bitsets into LDS ----
+  // ---- phase A ----
+  const uint32_t flags = (live && (need & NEED_FLAGS)) ? a.r_flags[r] : 0;
+  const uint32_t gvk = (live && (need & NEED_GVK)) ? a.r_gvk[r] : 0;
+  const uint32_t pw = (live && pss) ? a.p_sc[r] : 0;
   const uint32_t pw_off = STAGED ? a.prog_words : 0u;
   uint32_t* s_pw = dyn + pw_off;
   uint32_t* s_bits = s_pw + a.npreds;
@@ -209,8 +224,14 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   for (uint32_t i = t; i < a.lwords; i += kBlock) s_bits[i] = a.pred_bits[i];
   if (small_r)
     for (uint32_t i = t; i < 6 * R; i += kBlock) s_cnt[i] = 0;
-  if (a.any_pss)
-    for (uint32_t i = t; i <= np; i += kBlock) s_off[i] = a.ctr_off[p0 + i];
+  if (pss) {
+    for (uint32_t i = t; i <= np; i += kBlock) {
+      s_coff[i] = a.ctr_off[p0 + i];
+      if (need & NEED_VOL) s_voff[i] = a.vol_off[p0 + i];
+      if (need & NEED_SYS) s_soff[i] = a.sys_off[p0 + i];
+      if (need & NEED_PANN) s_aoff[i] = a.pann_off[p0 + i];
+    }
+  }
   __syncthreads();
 
   const KpeRule* rules = STAGED ? reinterpret_cast<const KpeRule*>(dyn + a.off_rules) : a.rules;
@@ -236,18 +257,30 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     return (uint64_t)gbits[w] | ((uint64_t)gbits[w + 1] << 32);
   };
 
-  // ---- (2)+(3) PSS: containers through LDS, pod-level lists, versioned checks ----
+  // ---- phases B + C for the PSS pod view ----
   uint32_t fails = 0;
-  if (a.any_pss) {
-    const uint32_t c_begin = s_off[0], c_end = s_off[np];
+  if (pss) {
+    const uint32_t c_begin = s_coff[0], c_end = s_coff[np];
+    const uint32_t v_begin = (need & NEED_VOL) ? s_voff[0] : 0, v_end = (need & NEED_VOL) ? s_voff[np] : 0;
+    const uint32_t s_begin = (need & NEED_SYS) ? s_soff[0] : 0, s_end = (need & NEED_SYS) ? s_soff[np] : 0;
+    const uint32_t a_begin = (need & NEED_PANN) ? s_aoff[0] : 0, a_end = (need & NEED_PANN) ? s_aoff[np] : 0;
     const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
-    const bool need_caps = a.need & NEED_CAPS, need_sann = a.need & NEED_SANN;
+    const bool need_caps = need & NEED_CAPS, need_sann = need & NEED_SANN;
     uint32_t cb = 0;
-    const uint32_t my_lo = live ? s_off[t] : 0, my_hi = live ? s_off[t + 1] : 0;
-    for (uint32_t base = c_begin; base < c_end; base += kChunk) {
-      const uint32_t lim = (c_end - base) < kChunk ? (c_end - base) : kChunk;
-      for (uint32_t i = t; i < lim; i += kBlock) {
-        const uint32_t c = base + i;
+    bool vol_hostpath = false, vol_restricted = false, apparmor_bad = false, sec_pod_ann_bad = false;
+    uint32_t sys_bad = 0;
+    const uint32_t my_c0 = live ? s_coff[t] : 0, my_c1 = live ? s_coff[t + 1] : 0;
+    const uint32_t my_v0 = (live && (need & NEED_VOL)) ? s_voff[t] : 0, my_v1 = (live && (need & NEED_VOL)) ? s_voff[t + 1] : 0;
+    const uint32_t my_s0 = (live && (need & NEED_SYS)) ? s_soff[t] : 0, my_s1 = (live && (need & NEED_SYS)) ? s_soff[t + 1] : 0;
+    const uint32_t my_a0 = (live && (need & NEED_PANN)) ? s_aoff[t] : 0, my_a1 = (live && (need & NEED_PANN)) ? s_aoff[t + 1] : 0;
+    // one pass per chunk window; in the common case every list fits its window in one pass
+    for (uint32_t pass = 0;; ++pass) {
+      const uint32_t cb0 = c_begin + pass * kChunk, vb0 = v_begin + pass * kListChunk,
+                     sb0 = s_begin + pass * kListChunk, ab0 = a_begin + pass * kListChunk;
+      if (cb0 >= c_end && vb0 >= v_end && sb0 >= s_end && ab0 >= a_end) break;
+      // phase B: all item loads of this window are independent
+      for (uint32_t i = t; i < kChunk && cb0 + i < c_end; i += kBlock) {
+        const uint32_t c = cb0 + i;
         const uint32_t w = a.c_sc[c];
         uint32_t b = 0;
         const bool caps = w & C_CAPS_PRESENT;
@@ -277,42 +310,50 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
         if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
         s_cb[i] = b;
       }
+      for (uint32_t i = t; i < kListChunk && vb0 + i < v_end; i += kBlock) {
+        const uint32_t sv = a.vol_src[vb0 + i];
+        s_vb[i] = (uint8_t)(((sv & (1u << VS_HOSTPATH)) ? 1u : 0u) | ((sv & kAllowedVolumes) ? 0u : 2u));
+      }
+      for (uint32_t i = t; i < kListChunk && sb0 + i < s_end; i += kBlock) {
+        const uint32_t id = a.sys_id[sb0 + i];
+        s_sb[i] = (uint8_t)((pbit(a.pp_sysctl0, id) ? 0u : 1u) | (pbit(a.pp_sysctl1, id) ? 0u : 2u) |
+                            (pbit(a.pp_sysctl2, id) ? 0u : 4u));
+      }
+      for (uint32_t i = t; i < kListChunk && ab0 + i < a_end; i += kBlock) {
+        const uint32_t k = a.pann_k[ab0 + i], v = a.pann_v[ab0 + i];
+        s_ab[i] = (uint8_t)((pbit(a.pp_apparmor_key, k) && !pbit(a.pp_apparmor_ok, v) ? 1u : 0u) |
+                            (pbit(a.pp_seccomp_pod_key, k) && !pbit(a.pp_seccomp_ann_ok, v) ? 2u : 0u));
+      }
       __syncthreads();
-      const uint32_t lo = my_lo > base ? my_lo : base, hi = my_hi < base + lim ? my_hi : base + lim;
-      for (uint32_t c = lo; c < hi; ++c) cb |= s_cb[c - base];
+      // phase C (reduce): this lane's ranges intersected with the window
+      {
+        const uint32_t lo = my_c0 > cb0 ? my_c0 : cb0, hi = my_c1 < cb0 + kChunk ? my_c1 : cb0 + kChunk;
+        for (uint32_t c = lo; c < hi; ++c) cb |= s_cb[c - cb0];
+      }
+      {
+        const uint32_t lo = my_v0 > vb0 ? my_v0 : vb0, hi = my_v1 < vb0 + kListChunk ? my_v1 : vb0 + kListChunk;
+        for (uint32_t j = lo; j < hi; ++j) {
+          vol_hostpath |= s_vb[j - vb0] & 1u;
+          vol_restricted |= (s_vb[j - vb0] >> 1) & 1u;
+        }
+      }
+      {
+        const uint32_t lo = my_s0 > sb0 ? my_s0 : sb0, hi = my_s1 < sb0 + kListChunk ? my_s1 : sb0 + kListChunk;
+        for (uint32_t j = lo; j < hi; ++j) sys_bad |= s_sb[j - sb0];
+      }
+      {
+        const uint32_t lo = my_a0 > ab0 ? my_a0 : ab0, hi = my_a1 < ab0 + kListChunk ? my_a1 : ab0 + kListChunk;
+        for (uint32_t j = lo; j < hi; ++j) {
+          apparmor_bad |= s_ab[j - ab0] & 1u;
+          sec_pod_ann_bad |= (s_ab[j - ab0] >> 1) & 1u;
+        }
+      }
       __syncthreads();
     }
-    if (live) {
-      const uint32_t pw = a.p_sc[r];
-      bool vol_hostpath = false, vol_restricted = false;
-      if (a.need & NEED_VOL)
-        for (uint32_t j = a.vol_off[r], e = a.vol_off[r + 1]; j < e; ++j) {
-          const uint32_t s = a.vol_src[j];
-          vol_hostpath |= (s & (1u << VS_HOSTPATH)) != 0;
-          vol_restricted |= !(s & kAllowedVolumes);
-        }
-      uint32_t sys_bad = 0;
-      if (a.need & NEED_SYS)
-        for (uint32_t j = a.sys_off[r], e = a.sys_off[r + 1]; j < e; ++j) {
-          const uint32_t id = a.sys_id[j];
-          if (!pbit(a.pp_sysctl0, id)) sys_bad |= 1u;
-          if (!pbit(a.pp_sysctl1, id)) sys_bad |= 2u;
-          if (!pbit(a.pp_sysctl2, id)) sys_bad |= 4u;
-        }
-      bool apparmor_bad = false, sec_pod_ann_bad = false;
-      if (a.need & NEED_PANN)
-        for (uint32_t j = a.pann_off[r], e = a.pann_off[r + 1]; j < e; ++j) {
-          const uint32_t k = a.pann_k[j], v = a.pann_v[j];
-          apparmor_bad |= pbit(a.pp_apparmor_key, k) && !pbit(a.pp_apparmor_ok, v);
-          sec_pod_ann_bad |= pbit(a.pp_seccomp_pod_key, k) && !pbit(a.pp_seccomp_ann_ok, v);
-        }
-      fails = cv_fails(pw, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
-    }
+    if (live) fails = cv_fails(pw, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
   }
 
-  // ---- (4) rules: match/exclude, handler, ApplyOne, verdict cell ----
-  const uint32_t flags = (live && (a.need & NEED_FLAGS)) ? a.r_flags[r] : 0;
-  const uint32_t gvk = (live && (a.need & NEED_GVK)) ? a.r_gvk[r] : 0;
+  // ---- phase C: rules (match/exclude, handler, ApplyOne, verdict cell) ----
   auto filter = [&](uint32_t f) -> bool {
     const KpeFilter fl = filters[f];
     for (uint32_t ti = 0; ti < fl.nterms; ++ti) {
@@ -415,7 +456,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     }
   }
 
-  // ---- (5) coalesced verdict store + counter partials ----
+  // ---- coalesced verdict store + counter partials ----
   __syncthreads();
   if (stage_v) {
     const uint32_t bytes = np * R;
