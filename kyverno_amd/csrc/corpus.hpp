@@ -53,6 +53,13 @@ struct Corpus {
   std::vector<uint32_t> c_sec_str, c_pm_str, c_selt_str, c_selu_str, c_selr_str;  // cold (D_MISC)
   std::vector<uint32_t> cport_off{0};
   std::vector<int32_t> cport_host;  // cold: hostPort of every port
+  // ---- packed hot records for the PSS scan (schema.h) ----
+  std::vector<uint32_t> rec;   // 4 words per pod
+  std::vector<uint32_t> hdr;   // 4 words per 64 pods
+  std::vector<uint32_t> crec;  // 2 words per container
+  std::vector<uint32_t> pann_kv;  // (key, value) pairs of pod-template annotations
+  std::vector<uint64_t> capset_add, capset_drop;
+  std::unordered_map<std::string, uint32_t> capset_index;
   // ---- namespace label table (PolicyContext.NamespaceLabels) ----
   std::vector<uint32_t> nsl_off{0}, nsl_k, nsl_v;
   std::unordered_map<std::string, uint32_t> nsl_index;

@@ -955,6 +955,16 @@ class Flattener {
     C.ann_off.push_back((uint32_t)C.ann_k.size());
 
     // ---- pod view ----
+    if (C.n % 64 == 0) {  // wave header: list bases of the next 64 pods
+      C.hdr.push_back((uint32_t)C.c_sc.size());
+      C.hdr.push_back((uint32_t)C.vol_src.size());
+      C.hdr.push_back((uint32_t)C.sys_id.size());
+      C.hdr.push_back((uint32_t)(C.pann_kv.size() / 2));
+    }
+    size_t nctr = pod.ctr[0].size() + pod.ctr[1].size() + pod.ctr[2].size();
+    if (nctr > KPE_MAX_LIST || pod.vols.size() > KPE_MAX_LIST || pod.sysctls.size() > KPE_MAX_LIST ||
+        pod.ann.size() > KPE_MAX_LIST)
+      throw LimitError("a pod has more than 255 containers, volumes, sysctls or annotations");
     uint32_t p = 0;
     if (pod.sc) p |= P_SC_PRESENT;
     if (pod.hostnet) p |= P_HOSTNET;
@@ -976,6 +986,8 @@ class Flattener {
     for (auto& kv : pod.ann) {
       C.pann_k.push_back(C.dict[D_ANNK].intern(kv.first));
       C.pann_v.push_back(C.dict[D_ANNV].intern(kv.second));
+      C.pann_kv.push_back(C.pann_k.back());
+      C.pann_kv.push_back(C.pann_v.back());
     }
     C.pann_off.push_back((uint32_t)C.pann_k.size());
     static const std::string seccomp_ctr_prefix = "container.seccomp.security.alpha.kubernetes.io/";
@@ -1005,6 +1017,24 @@ class Flattener {
         C.c_add.push_back(last_mask_);
         capmask(c.drop);
         C.c_drop.push_back(last_mask_);
+        {  // capability-set dictionary: distinct (add, drop) mask pairs
+          std::string key(16, '\0');
+          memcpy(&key[0], &C.c_add.back(), 8);
+          memcpy(&key[8], &C.c_drop.back(), 8);
+          auto it = C.capset_index.find(key);
+          uint32_t cs;
+          if (it == C.capset_index.end()) {
+            cs = (uint32_t)C.capset_add.size();
+            if (cs >= KPE_MAX_CAPSETS) throw LimitError("more than 2048 distinct capability (add, drop) sets");
+            C.capset_index.emplace(key, cs);
+            C.capset_add.push_back(C.c_add.back());
+            C.capset_drop.push_back(C.c_drop.back());
+          } else {
+            cs = it->second;
+          }
+          C.crec.push_back(w);
+          C.crec.push_back(cs);
+        }
         C.c_name.push_back(C.dict[D_CNAME].intern(c.name));
         C.c_image.push_back(C.dict[D_IMAGE].intern(c.image));
         uint32_t sann = KPE_NO_STR;  // join: pod annotation "container.seccomp...kubernetes.io/<name>"
@@ -1024,6 +1054,11 @@ class Flattener {
       }
     }
     C.ctr_off.push_back((uint32_t)C.c_sc.size());
+    C.rec.push_back(p | ((flags & R_CLASS_MASK) << PR_CLASS_SH) | (derr ? PR_DECODE_ERR : 0u));
+    C.rec.push_back(C.r_gvk.back());
+    C.rec.push_back((uint32_t)nctr | ((uint32_t)pod.vols.size() << 8) | ((uint32_t)pod.sysctls.size() << 16) |
+                    ((uint32_t)pod.ann.size() << 24));
+    C.rec.push_back(nsa);
     C.n++;
   }
 };
@@ -1071,9 +1106,8 @@ int64_t Corpus::bytes() const {
   auto add = [&](const auto& v) { b += (int64_t)(v.size() * sizeof(v[0])); };
   add(r_flags), add(r_gvk), add(r_name), add(r_mns), add(r_nsa), add(r_nsl);
   add(lab_off), add(lab_k), add(lab_v), add(ann_off), add(ann_k), add(ann_v);
-  add(p_sc), add(ctr_off), add(vol_off), add(vol_src), add(sys_off), add(sys_id), add(pann_off), add(pann_k),
-      add(pann_v);
-  add(c_sc), add(c_add), add(c_drop), add(c_name), add(c_image), add(c_sann);
+  add(rec), add(hdr), add(crec), add(vol_src), add(sys_id), add(pann_kv), add(capset_add), add(capset_drop);
+  add(c_sann);
   return b;
 }
 

@@ -182,21 +182,56 @@ __device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_
 
 }  // namespace
 
+// Capability-set violation bits (computed per block into LDS from the capset dictionary)
+#define CS_BASE 1u  // add has a capability outside the baseline allow-list
+#define CS_DROP 2u  // drop lacks "ALL"
+#define CS_ADD 4u   // add has anything but NET_BIND_SERVICE
+
+__device__ __forceinline__ uint32_t ctr_bits(uint32_t w, uint32_t csb) {
+  uint32_t b = 0;
+  const bool caps = w & C_CAPS_PRESENT;
+  if (caps && (csb & CS_BASE)) b |= CB_CAPS_BASE;
+  if (!caps || (csb & CS_DROP)) b |= CB_CAPS_DROP;
+  if (caps && (csb & CS_ADD)) b |= CB_CAPS_ADD;
+  if (FIELD(w, C_APE_SH, 2) != TRI_FALSE) b |= CB_APE;
+  if (FIELD(w, C_HOSTPORT_SH, 4)) b |= CB_HOSTPORT;
+  if (FIELD(w, C_PRIV_SH, 2) == TRI_TRUE) b |= CB_PRIV;
+  if (FIELD(w, C_PROCMOUNT_SH, 2) == PROCMOUNT_OTHER) b |= CB_PROCMOUNT;
+  const uint32_t rnr = FIELD(w, C_RNR_SH, 2);
+  if (rnr == TRI_FALSE) b |= CB_RNR_FALSE;
+  if (rnr == TRI_UNSET) b |= CB_RNR_UNSET;
+  if (FIELD(w, C_RAU_SH, 2) == RAU_ZERO) b |= CB_RAU_ZERO;
+  const uint32_t sel = FIELD(w, C_SEL_SH, 3);
+  if (sel != SEL_NONE && (sel == SEL_OTHER || (w & (C_SEL_USER | C_SEL_ROLE)))) b |= CB_SELINUX;
+  const uint32_t sec = FIELD(w, C_SECCOMP_SH, 3);
+  if (sec == SECCOMP_NONE) b |= CB_SEC_UNSET;
+  else if (sec != SECCOMP_RUNTIMEDEFAULT && sec != SECCOMP_LOCALHOST) b |= CB_SEC_BAD;
+  if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
+  return b;
+}
+
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
 // STAGED: the program image fits the LDS budget (read from LDS); otherwise from global.
 //
-// Phases (one global round trip each, so a wave's lifetime is ~2 memory latencies):
-//  A  block offsets of every list (containers, volumes, sysctls, pod annotations),
-//     this lane's pod word / flags / gvk, program + predicate bitsets -> LDS/regs
-//  B  every list item of the block streamed coalesced (thread i takes items i, i+256, ...)
-//     and reduced to a few violation bits per item in LDS
-//  C  per-lane OR over its item ranges (LDS only), PSA versioned checks, rule loop,
-//     verdict cells into LDS; then one coalesced store.
+// One resource per lane, two global round trips per wave:
+//  1  the lane's 16-byte pod record (dwordx4), the wave header, the program, the
+//     predicate directory / small-domain bitsets and the capability-set table;
+//  2  the lane's list items at (header + exclusive wave scan of the counts):
+//     up to 4 containers, 2 volumes, 2 annotations and 1 sysctl are loaded
+//     before any is used (longer lists continue in a loop).
 template <bool STAGED>
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   extern __shared__ uint32_t dyn[];  // [program image][predicate directory][small-domain bitsets]
-  __shared__ uint32_t s_coff[kBlock + 1], s_voff[kBlock + 1], s_soff[kBlock + 1], s_aoff[kBlock + 1];
-  __shared__ uint32_t s_cb[kChunk];
-  __shared__ uint8_t s_vb[kListChunk], s_sb[kListChunk], s_ab[kListChunk];
+  __shared__ uint8_t s_capb[KPE_MAX_CAPSETS];
   __shared__ uint32_t s_cnt[6 * KPE_SMALL_R];
   __shared__ __attribute__((aligned(16))) uint8_t s_v[kStageV];
 
@@ -211,10 +246,20 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const uint32_t need = a.need;
   const bool pss = a.any_pss;
 
-  // ---- phase A ----
-  const uint32_t flags = (live && (need & NEED_FLAGS)) ? a.r_flags[r] : 0;
-  const uint32_t gvk = (live && (need & NEED_GVK)) ? a.r_gvk[r] : 0;
-  const uint32_t pw = (live && pss) ? a.p_sc[r] : 0;
+  // ---- round 1 ----
+  uint4 rec = make_uint4(0, 0, 0, 0);
+  if (live && pss) rec = reinterpret_cast<const uint4*>(a.rec)[r];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)(r >> 6));
+  uint4 hdr = make_uint4(0, 0, 0, 0);
+  if (pss && (int64_t)wave * 64 < a.n) hdr = reinterpret_cast<const uint4*>(a.hdr)[wave];
+  const uint32_t gvk = pss ? rec.y : ((live && (need & NEED_GVK)) ? a.r_gvk[r] : 0u);
+  const uint32_t nsa = pss ? rec.w : ((live && (need & NEED_NSA)) ? a.r_nsa[r] : KPE_NO_STR);
+  const bool need_caps = pss && (need & NEED_CAPS);
+  uint64_t cs_add = 0, cs_drop = 0;
+  if (need_caps && t < a.ncapsets) {
+    cs_add = a.capset_add[t];
+    cs_drop = a.capset_drop[t];
+  }
   const uint32_t pw_off = STAGED ? a.prog_words : 0u;
   uint32_t* s_pw = dyn + pw_off;
   uint32_t* s_bits = s_pw + a.npreds;
@@ -224,14 +269,6 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   for (uint32_t i = t; i < a.lwords; i += kBlock) s_bits[i] = a.pred_bits[i];
   if (small_r)
     for (uint32_t i = t; i < 6 * R; i += kBlock) s_cnt[i] = 0;
-  if (pss) {
-    for (uint32_t i = t; i <= np; i += kBlock) {
-      s_coff[i] = a.ctr_off[p0 + i];
-      if (need & NEED_VOL) s_voff[i] = a.vol_off[p0 + i];
-      if (need & NEED_SYS) s_soff[i] = a.sys_off[p0 + i];
-      if (need & NEED_PANN) s_aoff[i] = a.pann_off[p0 + i];
-    }
-  }
   __syncthreads();
 
   const KpeRule* rules = STAGED ? reinterpret_cast<const KpeRule*>(dyn + a.off_rules) : a.rules;
@@ -257,109 +294,104 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     return (uint64_t)gbits[w] | ((uint64_t)gbits[w + 1] << 32);
   };
 
-  // ---- phases B + C for the PSS pod view ----
   uint32_t fails = 0;
   if (pss) {
-    const uint32_t c_begin = s_coff[0], c_end = s_coff[np];
-    const uint32_t v_begin = (need & NEED_VOL) ? s_voff[0] : 0, v_end = (need & NEED_VOL) ? s_voff[np] : 0;
-    const uint32_t s_begin = (need & NEED_SYS) ? s_soff[0] : 0, s_end = (need & NEED_SYS) ? s_soff[np] : 0;
-    const uint32_t a_begin = (need & NEED_PANN) ? s_aoff[0] : 0, a_end = (need & NEED_PANN) ? s_aoff[np] : 0;
-    const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
-    const bool need_caps = need & NEED_CAPS, need_sann = need & NEED_SANN;
-    uint32_t cb = 0;
-    bool vol_hostpath = false, vol_restricted = false, apparmor_bad = false, sec_pod_ann_bad = false;
-    uint32_t sys_bad = 0;
-    const uint32_t my_c0 = live ? s_coff[t] : 0, my_c1 = live ? s_coff[t + 1] : 0;
-    const uint32_t my_v0 = (live && (need & NEED_VOL)) ? s_voff[t] : 0, my_v1 = (live && (need & NEED_VOL)) ? s_voff[t + 1] : 0;
-    const uint32_t my_s0 = (live && (need & NEED_SYS)) ? s_soff[t] : 0, my_s1 = (live && (need & NEED_SYS)) ? s_soff[t + 1] : 0;
-    const uint32_t my_a0 = (live && (need & NEED_PANN)) ? s_aoff[t] : 0, my_a1 = (live && (need & NEED_PANN)) ? s_aoff[t + 1] : 0;
-    // one pass per chunk window; in the common case every list fits its window in one pass
-    for (uint32_t pass = 0;; ++pass) {
-      const uint32_t cb0 = c_begin + pass * kChunk, vb0 = v_begin + pass * kListChunk,
-                     sb0 = s_begin + pass * kListChunk, ab0 = a_begin + pass * kListChunk;
-      if (cb0 >= c_end && vb0 >= v_end && sb0 >= s_end && ab0 >= a_end) break;
-      // phase B: all item loads of this window are independent
-      for (uint32_t i = t; i < kChunk && cb0 + i < c_end; i += kBlock) {
-        const uint32_t c = cb0 + i;
-        const uint32_t w = a.c_sc[c];
-        uint32_t b = 0;
-        const bool caps = w & C_CAPS_PRESENT;
-        if (need_caps) {
-          const uint64_t add = a.c_add[c], drop = a.c_drop[c];
-          if (caps && (add & ~caps_ok)) b |= CB_CAPS_BASE;
-          if (!caps || !(drop & all)) b |= CB_CAPS_DROP;
-          if (caps && (add & ~nbs)) b |= CB_CAPS_ADD;
-        }
-        if (FIELD(w, C_APE_SH, 2) != TRI_FALSE) b |= CB_APE;
-        if (FIELD(w, C_HOSTPORT_SH, 4)) b |= CB_HOSTPORT;
-        if (FIELD(w, C_PRIV_SH, 2) == TRI_TRUE) b |= CB_PRIV;
-        if (FIELD(w, C_PROCMOUNT_SH, 2) == PROCMOUNT_OTHER) b |= CB_PROCMOUNT;
-        const uint32_t rnr = FIELD(w, C_RNR_SH, 2);
-        if (rnr == TRI_FALSE) b |= CB_RNR_FALSE;
-        if (rnr == TRI_UNSET) b |= CB_RNR_UNSET;
-        if (FIELD(w, C_RAU_SH, 2) == RAU_ZERO) b |= CB_RAU_ZERO;
-        const uint32_t sel = FIELD(w, C_SEL_SH, 3);
-        if (sel != SEL_NONE && (sel == SEL_OTHER || (w & (C_SEL_USER | C_SEL_ROLE)))) b |= CB_SELINUX;
-        const uint32_t sec = FIELD(w, C_SECCOMP_SH, 3);
-        if (sec == SECCOMP_NONE) b |= CB_SEC_UNSET;
-        else if (sec != SECCOMP_RUNTIMEDEFAULT && sec != SECCOMP_LOCALHOST) b |= CB_SEC_BAD;
-        if (need_sann) {
-          const uint32_t sann = a.c_sann[c];
-          if (sann != KPE_NO_STR && !pbit(a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
-        }
-        if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
-        s_cb[i] = b;
-      }
-      for (uint32_t i = t; i < kListChunk && vb0 + i < v_end; i += kBlock) {
-        const uint32_t sv = a.vol_src[vb0 + i];
-        s_vb[i] = (uint8_t)(((sv & (1u << VS_HOSTPATH)) ? 1u : 0u) | ((sv & kAllowedVolumes) ? 0u : 2u));
-      }
-      for (uint32_t i = t; i < kListChunk && sb0 + i < s_end; i += kBlock) {
-        const uint32_t id = a.sys_id[sb0 + i];
-        s_sb[i] = (uint8_t)((pbit(a.pp_sysctl0, id) ? 0u : 1u) | (pbit(a.pp_sysctl1, id) ? 0u : 2u) |
-                            (pbit(a.pp_sysctl2, id) ? 0u : 4u));
-      }
-      for (uint32_t i = t; i < kListChunk && ab0 + i < a_end; i += kBlock) {
-        const uint32_t k = a.pann_k[ab0 + i], v = a.pann_v[ab0 + i];
-        s_ab[i] = (uint8_t)((pbit(a.pp_apparmor_key, k) && !pbit(a.pp_apparmor_ok, v) ? 1u : 0u) |
-                            (pbit(a.pp_seccomp_pod_key, k) && !pbit(a.pp_seccomp_ann_ok, v) ? 2u : 0u));
-      }
-      __syncthreads();
-      // phase C (reduce): this lane's ranges intersected with the window
-      {
-        const uint32_t lo = my_c0 > cb0 ? my_c0 : cb0, hi = my_c1 < cb0 + kChunk ? my_c1 : cb0 + kChunk;
-        for (uint32_t c = lo; c < hi; ++c) cb |= s_cb[c - cb0];
-      }
-      {
-        const uint32_t lo = my_v0 > vb0 ? my_v0 : vb0, hi = my_v1 < vb0 + kListChunk ? my_v1 : vb0 + kListChunk;
-        for (uint32_t j = lo; j < hi; ++j) {
-          vol_hostpath |= s_vb[j - vb0] & 1u;
-          vol_restricted |= (s_vb[j - vb0] >> 1) & 1u;
-        }
-      }
-      {
-        const uint32_t lo = my_s0 > sb0 ? my_s0 : sb0, hi = my_s1 < sb0 + kListChunk ? my_s1 : sb0 + kListChunk;
-        for (uint32_t j = lo; j < hi; ++j) sys_bad |= s_sb[j - sb0];
-      }
-      {
-        const uint32_t lo = my_a0 > ab0 ? my_a0 : ab0, hi = my_a1 < ab0 + kListChunk ? my_a1 : ab0 + kListChunk;
-        for (uint32_t j = lo; j < hi; ++j) {
-          apparmor_bad |= s_ab[j - ab0] & 1u;
-          sec_pod_ann_bad |= (s_ab[j - ab0] >> 1) & 1u;
-        }
+    if (need_caps) {
+      const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
+      for (uint32_t i = t; i < a.ncapsets; i += kBlock) {
+        const uint64_t ad = i == t ? cs_add : a.capset_add[i], dr = i == t ? cs_drop : a.capset_drop[i];
+        s_capb[i] = (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
       }
       __syncthreads();
     }
-    if (live) fails = cv_fails(pw, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
+    // ---- list offsets: header + exclusive wave scan of the packed counts ----
+    const uint32_t z = rec.z;
+    const uint32_t c01 = (z & 0xFFu) | ((z & 0xFF00u) << 8), c23 = ((z >> 16) & 0xFFu) | ((z >> 24) << 16);
+    const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
+    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+    const uint32_t oc = hdr.x + (e01 & 0xFFFFu), ov = hdr.y + (e01 >> 16), os = hdr.z + (e23 & 0xFFFFu),
+                   oa = hdr.w + (e23 >> 16);
+    // ---- round 2: issue every first-wave load before using any ----
+    const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
+    const uint2* pkv = reinterpret_cast<const uint2*>(a.pann_kv);
+    const bool nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN, nsann = need & NEED_SANN;
+    uint2 k0 = make_uint2(0, 0), k1 = k0, k2 = k0, k3 = k0;
+    if (nc > 0) k0 = crec[oc];
+    if (nc > 1) k1 = crec[oc + 1];
+    if (nc > 2) k2 = crec[oc + 2];
+    if (nc > 3) k3 = crec[oc + 3];
+    uint32_t v0 = 0, v1 = 0, sy0 = 0;
+    if (nvol && nv > 0) v0 = a.vol_src[ov];
+    if (nvol && nv > 1) v1 = a.vol_src[ov + 1];
+    if (nsys && ns > 0) sy0 = a.sys_id[os];
+    uint2 q0 = make_uint2(0, 0), q1 = q0;
+    if (npann && na > 0) q0 = pkv[oa];
+    if (npann && na > 1) q1 = pkv[oa + 1];
+    uint32_t sa0 = KPE_NO_STR, sa1 = KPE_NO_STR, sa2 = KPE_NO_STR, sa3 = KPE_NO_STR;
+    if (nsann) {
+      if (nc > 0) sa0 = a.c_sann[oc];
+      if (nc > 1) sa1 = a.c_sann[oc + 1];
+      if (nc > 2) sa2 = a.c_sann[oc + 2];
+      if (nc > 3) sa3 = a.c_sann[oc + 3];
+    }
+    // ---- containers ----
+    auto sec_ann = [&](uint32_t sann) -> uint32_t {
+      return (sann != KPE_NO_STR && !pbit(a.pp_seccomp_ann_ok, sann)) ? CB_SEC_ANN : 0u;
+    };
+    uint32_t cb = 0;
+    if (nc > 0) cb |= ctr_bits(k0.x, need_caps ? s_capb[k0.y] : 0u) | sec_ann(sa0);
+    if (nc > 1) cb |= ctr_bits(k1.x, need_caps ? s_capb[k1.y] : 0u) | sec_ann(sa1);
+    if (nc > 2) cb |= ctr_bits(k2.x, need_caps ? s_capb[k2.y] : 0u) | sec_ann(sa2);
+    if (nc > 3) cb |= ctr_bits(k3.x, need_caps ? s_capb[k3.y] : 0u) | sec_ann(sa3);
+    for (uint32_t k = 4; k < nc; ++k) {
+      const uint2 kk = crec[oc + k];
+      cb |= ctr_bits(kk.x, need_caps ? s_capb[kk.y] : 0u) | sec_ann(nsann ? a.c_sann[oc + k] : KPE_NO_STR);
+    }
+    // ---- volumes ----
+    bool vol_hostpath = false, vol_restricted = false;
+    if (nvol) {
+      auto vol = [&](uint32_t sv) {
+        vol_hostpath |= (sv & (1u << VS_HOSTPATH)) != 0;
+        vol_restricted |= !(sv & kAllowedVolumes);
+      };
+      if (nv > 0) vol(v0);
+      if (nv > 1) vol(v1);
+      for (uint32_t k = 2; k < nv; ++k) vol(a.vol_src[ov + k]);
+    }
+    // ---- sysctls (allow-lists 1.0 / 1.27 / 1.29) ----
+    uint32_t sys_bad = 0;
+    if (nsys) {
+      auto sysf = [&](uint32_t id) {
+        if (!pbit(a.pp_sysctl0, id)) sys_bad |= 1u;
+        if (!pbit(a.pp_sysctl1, id)) sys_bad |= 2u;
+        if (!pbit(a.pp_sysctl2, id)) sys_bad |= 4u;
+      };
+      if (ns > 0) sysf(sy0);
+      for (uint32_t k = 1; k < ns; ++k) sysf(a.sys_id[os + k]);
+    }
+    // ---- pod-template annotations: AppArmor, seccomp pod annotation ----
+    bool apparmor_bad = false, sec_pod_ann_bad = false;
+    if (npann) {
+      auto ann = [&](uint2 kv) {
+        apparmor_bad |= pbit(a.pp_apparmor_key, kv.x) && !pbit(a.pp_apparmor_ok, kv.y);
+        sec_pod_ann_bad |= pbit(a.pp_seccomp_pod_key, kv.x) && !pbit(a.pp_seccomp_ann_ok, kv.y);
+      };
+      if (na > 0) ann(q0);
+      if (na > 1) ann(q1);
+      for (uint32_t k = 2; k < na; ++k) ann(pkv[oa + k]);
+    }
+    if (live) fails = cv_fails(rec.x, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
   }
 
-  // ---- phase C: rules (match/exclude, handler, ApplyOne, verdict cell) ----
+  // ---- rules: match/exclude, handler, ApplyOne, verdict cell ----
   auto filter = [&](uint32_t f) -> bool {
     const KpeFilter fl = filters[f];
     for (uint32_t ti = 0; ti < fl.nterms; ++ti) {
       const KpeTerm tm = terms[fl.term0 + ti];
       bool ok;
-      if (tm.type == T_KINDS) {
+      if (tm.type == T_KIND_PRED) {
+        ok = pbit((int32_t)tm.a, GVK_KIND(gvk));
+      } else if (tm.type == T_KINDS) {
         ok = false;
         for (uint32_t s = 0; s < tm.b && !ok; ++s) {
           const KpeKindSel ks = kindsels[tm.a + s];
@@ -367,7 +399,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
                (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
         }
       } else if (tm.type == T_PRED) {
-        const uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : a.r_nsa[r]);
+        const uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : nsa);
         ok = pbit((int32_t)tm.a, id);
       } else if (tm.type == T_ANNOTATIONS) {
         ok = true;
@@ -399,6 +431,8 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     return filter(f0);
   };
 
+  const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
+  const bool pss_err = cls == R_CLASS_OTHER || (rec.x & PR_DECODE_ERR);
   bool applied = false;
   uint32_t cur_policy = 0xFFFFFFFFu;
   const uint32_t lane = t & 63u;
@@ -411,7 +445,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     uint32_t v = KPE_NA_;
     uint32_t cmask = 0;
     if (live && !(rule.apply_one && applied)) {
-      bool m = rule.pol_ns_pred < 0 || pbit(rule.pol_ns_pred, a.r_nsa[r]);
+      bool m = rule.pol_ns_pred < 0 || pbit(rule.pol_ns_pred, nsa);
       m = m && block_match(rule.match_mode, rule.match_f0, rule.match_nf);
       if (m) {
         bool ex;
@@ -428,7 +462,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
       }
       if (m) {
         if (rule.handler == H_PSS) {
-          if ((flags & R_CLASS_MASK) == R_CLASS_OTHER || (flags & R_DECODE_ERR)) {
+          if (pss_err) {
             v = KPE_ERROR_;
           } else {
             const uint32_t f = fails & rule.cv_mask;
@@ -447,9 +481,11 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     else if (live) a.verdicts[r * R + ri] = (uint8_t)v;
     if (live && a.masks) a.masks[r * R + ri] = cmask;
     if (small_r) {
-      for (uint32_t k = 1; k < 6; ++k) {
-        const uint64_t b = __ballot(live && v == k);
-        if (lane == 0 && b) atomicAdd(&s_cnt[ri * 6 + k], (uint32_t)__popcll(b));
+      if (__ballot(v != KPE_NA_)) {  // wave-uniform skip of all-NA columns
+        for (uint32_t k = 1; k < 6; ++k) {
+          const uint64_t b = __ballot(v == k);
+          if (lane == 0 && b) atomicAdd(&s_cnt[ri * 6 + k], (uint32_t)__popcll(b));
+        }
       }
     } else if (live && v != KPE_NA_) {
       atomicAdd(&a.counts_global[ri * 6 + v], 1ull);

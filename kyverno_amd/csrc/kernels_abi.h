@@ -49,14 +49,19 @@ struct PredArgs {
 
 struct ScanArgs {
   int64_t n;
-  // resource rows (unstructured view)
-  const uint32_t *r_flags, *r_gvk, *r_name, *r_mns, *r_nsa, *ann_off, *ann_k, *ann_v;
-  // pod view
-  const uint32_t *p_sc, *ctr_off, *vol_off, *vol_src, *sys_off, *sys_id, *pann_off, *pann_k, *pann_v;
-  // containers
-  const uint32_t* c_sc;
-  const uint64_t *c_add, *c_drop;
-  const uint32_t* c_sann;
+  // resource rows (unstructured view) — read by match terms
+  const uint32_t *r_gvk, *r_name, *r_mns, *r_nsa, *ann_off, *ann_k, *ann_v;
+  // PSS hot records (schema.h): pod records, wave headers, container records
+  const uint32_t* rec;        // 4 words per pod
+  const uint32_t* hdr;        // 4 words per 64 pods
+  const uint32_t* crec;       // 2 words per container
+  const uint32_t* vol_src;    // per volume: VolumeSource presence mask
+  const uint32_t* sys_id;     // per sysctl: D_SYSCTL id
+  const uint32_t* pann_kv;    // per pod-template annotation: (D_ANNK id, D_ANNV id)
+  const uint32_t* c_sann;     // per container: value id of its seccomp annotation (cold)
+  const uint64_t* capset_add; // capability-set dictionary
+  const uint64_t* capset_drop;
+  uint32_t ncapsets;
   // program (global copies)
   const KpeRule* rules;
   uint32_t nrules;

@@ -128,9 +128,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
 struct DeviceCorpus {
   int ordinal = -1;
   DevBuf dict_bytes[KPE_NUM_DOMAINS], dict_off[KPE_NUM_DOMAINS];
-  DevBuf r_flags, r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
-  DevBuf p_sc, ctr_off, vol_off, vol_src, sys_off, sys_id, pann_off, pann_k, pann_v;
-  DevBuf c_sc, c_add, c_drop, c_sann;
+  DevBuf r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
+  DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capset_add, capset_drop;
   Binding bind;
   bool has_masks = false;
 };
@@ -243,7 +242,6 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
     HIPCHK(upload(D.dict_bytes[i], C.dict[i].bytes, s));
     HIPCHK(upload(D.dict_off[i], C.dict[i].off, s));
   }
-  HIPCHK(upload(D.r_flags, C.r_flags, s));
   HIPCHK(upload(D.r_gvk, C.r_gvk, s));
   HIPCHK(upload(D.r_name, C.r_name, s));
   HIPCHK(upload(D.r_mns, C.r_mns, s));
@@ -251,19 +249,15 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   HIPCHK(upload(D.ann_off, C.ann_off, s));
   HIPCHK(upload(D.ann_k, C.ann_k, s));
   HIPCHK(upload(D.ann_v, C.ann_v, s));
-  HIPCHK(upload(D.p_sc, C.p_sc, s));
-  HIPCHK(upload(D.ctr_off, C.ctr_off, s));
-  HIPCHK(upload(D.vol_off, C.vol_off, s));
+  HIPCHK(upload(D.rec, C.rec, s));
+  HIPCHK(upload(D.hdr, C.hdr, s));
+  HIPCHK(upload(D.crec, C.crec, s));
   HIPCHK(upload(D.vol_src, C.vol_src, s));
-  HIPCHK(upload(D.sys_off, C.sys_off, s));
   HIPCHK(upload(D.sys_id, C.sys_id, s));
-  HIPCHK(upload(D.pann_off, C.pann_off, s));
-  HIPCHK(upload(D.pann_k, C.pann_k, s));
-  HIPCHK(upload(D.pann_v, C.pann_v, s));
-  HIPCHK(upload(D.c_sc, C.c_sc, s));
-  HIPCHK(upload(D.c_add, C.c_add, s));
-  HIPCHK(upload(D.c_drop, C.c_drop, s));
+  HIPCHK(upload(D.pann_kv, C.pann_kv, s));
   HIPCHK(upload(D.c_sann, C.c_sann, s));
+  HIPCHK(upload(D.capset_add, C.capset_add, s));
+  HIPCHK(upload(D.capset_drop, C.capset_drop, s));
   HIPCHK(hipStreamSynchronize(s));
   return KPE_OK;
 }
@@ -354,7 +348,7 @@ uint32_t need_flags(const kpe::Program& P) {
   for (auto& r : P.rules)
     if (r.handler != H_NONE && r.handler != H_PSS) need |= NEED_FLAGS;
   for (auto& t : P.terms)
-    if (t.type == T_KINDS) need |= NEED_GVK;
+    if (t.type == T_KINDS || t.type == T_KIND_PRED) need |= NEED_GVK;
   for (auto& r : P.rules)
     if (r.pol_ns_pred >= 0) need |= NEED_NSA;
   return need;
@@ -362,23 +356,23 @@ uint32_t need_flags(const kpe::Program& P) {
 double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
   double b = 0;
   const double n = (double)C.n;
-  if (need & NEED_FLAGS) b += 4 * n;
-  if (need & NEED_GVK) b += 4 * n;
-  if (need & NEED_NSA) b += 4 * n;
+  if (P.any_pss) {
+    b += 16 * n + 16.0 * ((C.n + 63) / 64);  // pod records + wave headers
+    b += 8.0 * C.c_sc.size();               // container records
+    if (need & NEED_CAPS) b += 16.0 * C.capset_add.size();
+    if (need & NEED_SANN) b += 4.0 * C.c_sc.size();
+    if (need & NEED_VOL) b += 4.0 * C.vol_src.size();
+    if (need & NEED_SYS) b += 4.0 * C.sys_id.size();
+    if (need & NEED_PANN) b += 8.0 * C.pann_kv.size() / 2;
+  } else {
+    if (need & NEED_GVK) b += 4 * n;
+    if (need & NEED_NSA) b += 4 * n;
+  }
   for (auto& t : P.terms)  // name / namespace columns read by predicate terms (once per resource)
     if (t.type == T_PRED) {
       b += 4 * n;
       break;
     }
-  if (P.any_pss) {
-    b += 4 * (n + 1) + 4 * n;                  // ctr_off, p_sc
-    b += 4.0 * C.c_sc.size();                 // container words
-    if (need & NEED_CAPS) b += 16.0 * C.c_sc.size();
-    if (need & NEED_SANN) b += 4.0 * C.c_sc.size();
-    if (need & NEED_VOL) b += 4 * (n + 1) + 4.0 * C.vol_src.size();
-    if (need & NEED_SYS) b += 4 * (n + 1) + 4.0 * C.sys_id.size();
-    if (need & NEED_PANN) b += 4 * (n + 1) + 8.0 * C.pann_k.size();
-  }
   b += n * P.rules.size() * (masks ? 5.0 : 1.0);  // verdict cells (+ check masks)
   if (P.rules.size() <= KPE_SMALL_R) b += 4.0 * kpe_scan_blocks(C.n) * 6 * P.rules.size();
   return b;
@@ -483,7 +477,6 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   ScanArgs sa{};
   sa.n = C.n;
-  sa.r_flags = D.r_flags.as<uint32_t>();
   sa.r_gvk = D.r_gvk.as<uint32_t>();
   sa.r_name = D.r_name.as<uint32_t>();
   sa.r_mns = D.r_mns.as<uint32_t>();
@@ -491,19 +484,16 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.ann_off = D.ann_off.as<uint32_t>();
   sa.ann_k = D.ann_k.as<uint32_t>();
   sa.ann_v = D.ann_v.as<uint32_t>();
-  sa.p_sc = D.p_sc.as<uint32_t>();
-  sa.ctr_off = D.ctr_off.as<uint32_t>();
-  sa.vol_off = D.vol_off.as<uint32_t>();
+  sa.rec = D.rec.as<uint32_t>();
+  sa.hdr = D.hdr.as<uint32_t>();
+  sa.crec = D.crec.as<uint32_t>();
   sa.vol_src = D.vol_src.as<uint32_t>();
-  sa.sys_off = D.sys_off.as<uint32_t>();
   sa.sys_id = D.sys_id.as<uint32_t>();
-  sa.pann_off = D.pann_off.as<uint32_t>();
-  sa.pann_k = D.pann_k.as<uint32_t>();
-  sa.pann_v = D.pann_v.as<uint32_t>();
-  sa.c_sc = D.c_sc.as<uint32_t>();
-  sa.c_add = D.c_add.as<uint64_t>();
-  sa.c_drop = D.c_drop.as<uint64_t>();
+  sa.pann_kv = D.pann_kv.as<uint32_t>();
   sa.c_sann = D.c_sann.as<uint32_t>();
+  sa.capset_add = D.capset_add.as<uint64_t>();
+  sa.capset_drop = D.capset_drop.as<uint64_t>();
+  sa.ncapsets = (uint32_t)C.capset_add.size();
   sa.rules = PD.rules.as<KpeRule>();
   sa.nrules = (uint32_t)R;
   sa.filters = PD.filters.as<KpeFilter>();

@@ -579,17 +579,34 @@ class Lowerer {
       if (!ops.empty() && std::find(ops.begin(), ops.end(), "CREATE") == ops.end()) push({T_FALSE, 0, 0, 0});
       auto kinds = svl(rd->get("kinds"));
       if (!kinds.empty()) {
-        uint32_t k0 = (uint32_t)P.kindsels.size();
-        for (auto& k : kinds) {
-          KindSel s = parse_kind_selector(k);
-          KpeKindSel ks;
-          ks.pg = s.g == "*" ? -1 : pred(D_GROUP, {s.g});
-          ks.pv = s.v == "*" ? -1 : pred(D_VERSION, {s.v});
-          ks.pk = s.k == "*" ? -1 : pred(D_KIND, {s.k});
-          ks.sub_ok = glob_host(s.sub, "") ? 1u : 0u;
-          P.kindsels.push_back(ks);
+        // CheckKind (pkg/utils/match/kind.go:14-26): OR over selectors of
+        // glob(g)&&glob(v)&&glob(k)&&glob(sub,""). Selectors whose group and
+        // version are "*" fold into one predicate over the kind dictionary.
+        std::vector<KindSel> sels;
+        for (auto& k : kinds) sels.push_back(parse_kind_selector(k));
+        bool kind_only = true;
+        std::vector<std::string> kpats;
+        for (auto& s : sels) {
+          if (!glob_host(s.sub, "")) continue;  // never matches a scan (no subresource)
+          if (s.g != "*" || s.v != "*") kind_only = false;
+          kpats.push_back(s.k);
         }
-        push({T_KINDS, k0, (uint32_t)kinds.size(), 0});
+        if (kpats.empty()) {
+          push({T_FALSE, 0, 0, 0});
+        } else if (kind_only) {
+          push({T_KIND_PRED, (uint32_t)pred(D_KIND, kpats), 0, 0});
+        } else {
+          uint32_t k0 = (uint32_t)P.kindsels.size();
+          for (auto& s : sels) {
+            KpeKindSel ks;
+            ks.pg = s.g == "*" ? -1 : pred(D_GROUP, {s.g});
+            ks.pv = s.v == "*" ? -1 : pred(D_VERSION, {s.v});
+            ks.pk = s.k == "*" ? -1 : pred(D_KIND, {s.k});
+            ks.sub_ok = glob_host(s.sub, "") ? 1u : 0u;
+            P.kindsels.push_back(ks);
+          }
+          push({T_KINDS, k0, (uint32_t)kinds.size(), 0});
+        }
       }
       std::string name = sv(rd->get("name"));
       if (!name.empty()) push({T_PRED, (uint32_t)pred(D_NAME, {name}), COL_NAME, 0});

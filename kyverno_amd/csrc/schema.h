@@ -87,6 +87,24 @@ enum KpeDomain {
 #define P_OS_SH 18      // OS_*
 #define FIELD(w, sh, bits) (((w) >> (sh)) & ((1u << (bits)) - 1u))
 
+// ---- packed hot records of the PSS scan ------------------------------------------------
+// Pod record (uint4, one dwordx4 per lane):
+//   x = pod word p_sc (bits 0..19) | R_CLASS << PR_CLASS_SH | PR_DECODE_ERR
+//   y = r_gvk, z = list counts (PRC_*), w = r_nsa (namespace id)
+// Wave header (uint4 per 64 pods): first container / volume / sysctl / pod-annotation
+//   index of the wave; a lane's own offsets are the header plus an exclusive wave scan
+//   of the counts.
+// Container record (uint2): x = c_sc, y = capability-set id (dictionary of distinct
+//   (add, drop) capability masks).
+#define PR_CLASS_SH 20
+#define PR_DECODE_ERR (1u << 22)
+#define PRC_CTR(z) ((z) & 0xFFu)
+#define PRC_VOL(z) (((z) >> 8) & 0xFFu)
+#define PRC_SYS(z) (((z) >> 16) & 0xFFu)
+#define PRC_PANN(z) ((z) >> 24)
+#define KPE_MAX_LIST 255u  // per-pod containers / volumes / sysctls / annotations (KPE_E_LIMIT beyond)
+#define KPE_MAX_CAPSETS 2048u
+
 // ---- container word c_sc -----------------------------------------------------------
 #define C_SC_PRESENT (1u << 0)
 #define C_PRIV_SH 1        // tri
@@ -223,7 +241,8 @@ enum KpeTermType {
   T_PRED = 2,      // bit lookup: predicate a over the resource column named by b (KpeCol)
   T_ANNOTATIONS = 3,  // every pair [a, a+b) of the annotation-pair table must be matched by some annotation
   T_SELECTOR = 4,     // label selector a (selector table) over resource labels
-  T_NSSELECTOR = 5    // label selector a over the namespace's labels (not for kind Namespace)
+  T_NSSELECTOR = 5,   // label selector a over the namespace's labels (not for kind Namespace)
+  T_KIND_PRED = 6     // kind-only selectors folded into one predicate a over D_KIND
 };
 enum KpeCol { COL_NAME = 0, COL_MNS = 1, COL_NSA = 2 };
 
