@@ -220,19 +220,21 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
-// STAGED: the program image fits the LDS budget (read from LDS); otherwise from global.
+// STAGED: the program image is part of the LDS preamble; otherwise rules/filters/terms
+// are read from their global copies.
 //
 // One resource per lane, two global round trips per wave:
-//  1  the lane's 16-byte pod record (dwordx4), the wave header, the program, the
-//     predicate directory / small-domain bitsets and the capability-set table;
+//  1  pod record (dwordx4), wave header, the preamble (program image, predicate
+//     directory, small-domain bitsets: one dwordx4 per thread) and the
+//     capability-set table — all issued before the first wait;
 //  2  the lane's list items at (header + exclusive wave scan of the counts):
-//     up to 4 containers, 2 volumes, 2 annotations and 1 sysctl are loaded
-//     before any is used (longer lists continue in a loop).
+//     up to 4 containers, 2 volumes, 2 annotations and 1 sysctl are loaded before
+//     any is used (longer lists continue in a loop).
 template <bool STAGED>
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
-  extern __shared__ uint32_t dyn[];  // [program image][predicate directory][small-domain bitsets]
-  __shared__ uint8_t s_capb[KPE_MAX_CAPSETS];
-  __shared__ uint32_t s_cnt[6 * KPE_SMALL_R];
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // preamble copy
+  __shared__ __attribute__((aligned(16))) uint8_t s_capb[KPE_MAX_CAPSETS];
+  __shared__ __attribute__((aligned(16))) uint32_t s_cnt[6 * KPE_SMALL_R];
   __shared__ __attribute__((aligned(16))) uint8_t s_v[kStageV];
 
   const int64_t p0 = (int64_t)blockIdx.x * kBlock;
@@ -245,63 +247,75 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const bool stage_v = R * kBlock <= kStageV;
   const uint32_t need = a.need;
   const bool pss = a.any_pss;
-
-  // ---- round 1 ----
-  uint4 rec = make_uint4(0, 0, 0, 0);
-  if (live && pss) rec = reinterpret_cast<const uint4*>(a.rec)[r];
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)(r >> 6));
-  uint4 hdr = make_uint4(0, 0, 0, 0);
-  if (pss && (int64_t)wave * 64 < a.n) hdr = reinterpret_cast<const uint4*>(a.hdr)[wave];
-  const uint32_t gvk = pss ? rec.y : ((live && (need & NEED_GVK)) ? a.r_gvk[r] : 0u);
-  const uint32_t nsa = pss ? rec.w : ((live && (need & NEED_NSA)) ? a.r_nsa[r] : KPE_NO_STR);
   const bool need_caps = pss && (need & NEED_CAPS);
-  uint64_t cs_add = 0, cs_drop = 0;
-  if (need_caps && t < a.ncapsets) {
-    cs_add = a.capset_add[t];
-    cs_drop = a.capset_drop[t];
+
+  // ---- round 1: every load issued before the first use ----
+  // Loads are unconditional at clamped (always valid) addresses and the value is
+  // selected afterwards, so no exec-mask branch splits the issue sequence.
+  const uint4 z4 = make_uint4(0, 0, 0, 0);
+  const int64_t rc = live ? r : a.n - 1;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)(r >> 6));
+  const uint32_t wave_c = __builtin_amdgcn_readfirstlane((uint32_t)(rc >> 6));
+  uint4 rec_raw = z4, hdr_raw = z4;
+  uint32_t gvk_raw = 0, nsa_raw = KPE_NO_STR;
+  if (pss) {
+    rec_raw = reinterpret_cast<const uint4*>(a.rec)[rc];
+    // vector load of the wave header: a scalar load here would be waited on
+    // before the preamble loads issue
+    uint32_t hv = (uint32_t)(rc >> 6);
+    asm volatile("" : "+v"(hv));
+    hdr_raw = reinterpret_cast<const uint4*>(a.hdr)[hv];
+  } else {
+    if (need & NEED_GVK) gvk_raw = a.r_gvk[rc];
+    if (need & NEED_NSA) nsa_raw = a.r_nsa[rc];
   }
-  const uint32_t pw_off = STAGED ? a.prog_words : 0u;
-  uint32_t* s_pw = dyn + pw_off;
-  uint32_t* s_bits = s_pw + a.npreds;
-  if (STAGED)
-    for (uint32_t i = t; i < a.prog_words; i += kBlock) dyn[i] = a.prog[i];
-  for (uint32_t i = t; i < a.npreds; i += kBlock) s_pw[i] = a.pred_word[i];
-  for (uint32_t i = t; i < a.lwords; i += kBlock) s_bits[i] = a.pred_bits[i];
+  const uint32_t nb4 = a.blob_words >> 2;  // >= 1
+  const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
+  const uint4 b0 = blob[t < nb4 ? t : nb4 - 1];
+  const uint4 b1 = blob[t + kBlock < nb4 ? t + kBlock : nb4 - 1];
+  uint4 cs = z4;
+  if (need_caps && a.ncapsets) cs = reinterpret_cast<const uint4*>(a.capsets)[t < a.ncapsets ? t : a.ncapsets - 1];
+  uint4* d4 = reinterpret_cast<uint4*>(dyn);
+  if (t < nb4) d4[t] = b0;
+  if (t + kBlock < nb4) d4[t + kBlock] = b1;
+#pragma unroll 1
+  for (uint32_t i = t + 2 * kBlock; i < nb4; i += kBlock) d4[i] = blob[i];
   if (small_r)
+#pragma unroll 1
     for (uint32_t i = t; i < 6 * R; i += kBlock) s_cnt[i] = 0;
   __syncthreads();
 
-  const KpeRule* rules = STAGED ? reinterpret_cast<const KpeRule*>(dyn + a.off_rules) : a.rules;
-  const KpeFilter* filters = STAGED ? reinterpret_cast<const KpeFilter*>(dyn + a.off_filters) : a.filters;
-  const KpeTerm* terms = STAGED ? reinterpret_cast<const KpeTerm*>(dyn + a.off_terms) : a.terms;
-  const KpeKindSel* kindsels = STAGED ? reinterpret_cast<const KpeKindSel*>(dyn + a.off_kindsels) : a.kindsels;
-  const KpeAnnPair* annpairs = STAGED ? reinterpret_cast<const KpeAnnPair*>(dyn + a.off_annpairs) : a.annpairs;
-  const uint32_t* gbits = a.pred_bits;
-
+  // results of round 1 are consumed only after the barrier
+  const uint4 rec = live ? rec_raw : z4;
+  const uint4 hdr = (int64_t)wave * 64 < a.n ? hdr_raw : z4;
+  const uint32_t gvk_col = live ? gvk_raw : 0u, nsa_col = live ? nsa_raw : KPE_NO_STR;
+  const uint32_t* dir = dyn + a.img_words;
+  const uint32_t* pbuf = a.pbuf;
+  auto pword = [&](int32_t p, uint32_t wi) -> uint32_t {  // word wi of predicate p's bitset
+    const uint32_t w = dir[p];
+    return (w & PRED_LOCAL) ? dyn[(w & ~PRED_LOCAL) + wi] : pbuf[w + wi];
+  };
   auto pbit = [&](int32_t p, uint32_t id) -> bool {
     if (id == KPE_NO_STR) return false;
-    const uint32_t w = s_pw[p];
-    const uint32_t word = (w & PRED_LOCAL) ? s_bits[(w & ~PRED_LOCAL) + (id >> 5)] : gbits[w + (id >> 5)];
-    return (word >> (id & 31u)) & 1u;
+    return (pword(p, id >> 5) >> (id & 31u)) & 1u;
   };
   auto pmask64 = [&](int32_t p) -> uint64_t {  // predicate over D_CAP (<= 64 ids)
     if (p < 0) return 0;
-    const uint32_t w = s_pw[p];
-    if (w & PRED_LOCAL) {
-      const uint32_t o = w & ~PRED_LOCAL;
-      return (uint64_t)s_bits[o] | ((uint64_t)s_bits[o + 1] << 32);
-    }
-    return (uint64_t)gbits[w] | ((uint64_t)gbits[w + 1] << 32);
+    return (uint64_t)pword(p, 0) | ((uint64_t)pword(p, 1) << 32);
   };
 
   uint32_t fails = 0;
   if (pss) {
     if (need_caps) {
       const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
-      for (uint32_t i = t; i < a.ncapsets; i += kBlock) {
-        const uint64_t ad = i == t ? cs_add : a.capset_add[i], dr = i == t ? cs_drop : a.capset_drop[i];
-        s_capb[i] = (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
-      }
+      auto capbits = [&](uint4 c) -> uint8_t {
+        const uint64_t ad = (uint64_t)c.x | ((uint64_t)c.y << 32), dr = (uint64_t)c.z | ((uint64_t)c.w << 32);
+        return (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+      };
+      if (t < a.ncapsets) s_capb[t] = capbits(cs);
+#pragma unroll 1
+      for (uint32_t i = t + kBlock; i < a.ncapsets; i += kBlock)
+        s_capb[i] = capbits(reinterpret_cast<const uint4*>(a.capsets)[i]);
       __syncthreads();
     }
     // ---- list offsets: header + exclusive wave scan of the packed counts ----
@@ -311,131 +325,105 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
     const uint32_t oc = hdr.x + (e01 & 0xFFFFu), ov = hdr.y + (e01 >> 16), os = hdr.z + (e23 & 0xFFFFu),
                    oa = hdr.w + (e23 >> 16);
-    // ---- round 2: issue every first-wave load before using any ----
+    // ---- round 2: issue every first-pass list load before using any ----
+    // (clamped unconditional loads; totals > 0 are wave-uniform guards)
     const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
     const uint2* pkv = reinterpret_cast<const uint2*>(a.pann_kv);
-    const bool nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN, nsann = need & NEED_SANN;
-    uint2 k0 = make_uint2(0, 0), k1 = k0, k2 = k0, k3 = k0;
-    if (nc > 0) k0 = crec[oc];
-    if (nc > 1) k1 = crec[oc + 1];
-    if (nc > 2) k2 = crec[oc + 2];
-    if (nc > 3) k3 = crec[oc + 3];
+    const bool nvol = (need & NEED_VOL) && a.nvol_total, nsys = (need & NEED_SYS) && a.nsys_total,
+               npann = (need & NEED_PANN) && a.npann_total, nsann = (need & NEED_SANN) && a.nctr_total;
+    const uint2 z2 = make_uint2(0, 0);
+    uint2 k0 = z2, k1 = z2, k2 = z2, k3 = z2;
+    if (a.nctr_total) {
+      const uint32_t lim = a.nctr_total - 1;
+      k0 = crec[min(oc, lim)];
+      k1 = crec[min(oc + 1, lim)];
+      k2 = crec[min(oc + 2, lim)];
+      k3 = crec[min(oc + 3, lim)];
+    }
     uint32_t v0 = 0, v1 = 0, sy0 = 0;
-    if (nvol && nv > 0) v0 = a.vol_src[ov];
-    if (nvol && nv > 1) v1 = a.vol_src[ov + 1];
-    if (nsys && ns > 0) sy0 = a.sys_id[os];
-    uint2 q0 = make_uint2(0, 0), q1 = q0;
-    if (npann && na > 0) q0 = pkv[oa];
-    if (npann && na > 1) q1 = pkv[oa + 1];
-    uint32_t sa0 = KPE_NO_STR, sa1 = KPE_NO_STR, sa2 = KPE_NO_STR, sa3 = KPE_NO_STR;
+    if (nvol) {
+      v0 = a.vol_src[min(ov, a.nvol_total - 1)];
+      v1 = a.vol_src[min(ov + 1, a.nvol_total - 1)];
+    }
+    if (nsys) sy0 = a.sys_id[min(os, a.nsys_total - 1)];
+    uint2 q0 = z2, q1 = z2;
+    if (npann) {
+      q0 = pkv[min(oa, a.npann_total - 1)];
+      q1 = pkv[min(oa + 1, a.npann_total - 1)];
+    }
+    uint32_t sa[4] = {KPE_NO_STR, KPE_NO_STR, KPE_NO_STR, KPE_NO_STR};
     if (nsann) {
-      if (nc > 0) sa0 = a.c_sann[oc];
-      if (nc > 1) sa1 = a.c_sann[oc + 1];
-      if (nc > 2) sa2 = a.c_sann[oc + 2];
-      if (nc > 3) sa3 = a.c_sann[oc + 3];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t x = a.c_sann[min(oc + k, a.nctr_total - 1)];
+        sa[k] = nc > k ? x : KPE_NO_STR;
+      }
     }
     // ---- containers ----
-    auto sec_ann = [&](uint32_t sann) -> uint32_t {
-      return (sann != KPE_NO_STR && !pbit(a.pp_seccomp_ann_ok, sann)) ? CB_SEC_ANN : 0u;
+    auto one = [&](uint2 kk, uint32_t sann) -> uint32_t {
+      uint32_t b = ctr_bits(kk.x, need_caps ? s_capb[kk.y] : 0u);
+      if (sann != KPE_NO_STR && !pbit(a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
+      return b;
     };
     uint32_t cb = 0;
-    if (nc > 0) cb |= ctr_bits(k0.x, need_caps ? s_capb[k0.y] : 0u) | sec_ann(sa0);
-    if (nc > 1) cb |= ctr_bits(k1.x, need_caps ? s_capb[k1.y] : 0u) | sec_ann(sa1);
-    if (nc > 2) cb |= ctr_bits(k2.x, need_caps ? s_capb[k2.y] : 0u) | sec_ann(sa2);
-    if (nc > 3) cb |= ctr_bits(k3.x, need_caps ? s_capb[k3.y] : 0u) | sec_ann(sa3);
-    for (uint32_t k = 4; k < nc; ++k) {
-      const uint2 kk = crec[oc + k];
-      cb |= ctr_bits(kk.x, need_caps ? s_capb[kk.y] : 0u) | sec_ann(nsann ? a.c_sann[oc + k] : KPE_NO_STR);
-    }
+    if (nc > 0) cb |= one(k0, sa[0]);
+    if (nc > 1) cb |= one(k1, sa[1]);
+    if (nc > 2) cb |= one(k2, sa[2]);
+    if (nc > 3) cb |= one(k3, sa[3]);
+#pragma unroll 1
+    for (uint32_t k = 4; k < nc; ++k) cb |= one(crec[oc + k], nsann ? a.c_sann[oc + k] : KPE_NO_STR);
     // ---- volumes ----
     bool vol_hostpath = false, vol_restricted = false;
+    auto vol = [&](uint32_t sv) {
+      vol_hostpath |= (sv & (1u << VS_HOSTPATH)) != 0;
+      vol_restricted |= !(sv & kAllowedVolumes);
+    };
     if (nvol) {
-      auto vol = [&](uint32_t sv) {
-        vol_hostpath |= (sv & (1u << VS_HOSTPATH)) != 0;
-        vol_restricted |= !(sv & kAllowedVolumes);
-      };
       if (nv > 0) vol(v0);
       if (nv > 1) vol(v1);
+#pragma unroll 1
       for (uint32_t k = 2; k < nv; ++k) vol(a.vol_src[ov + k]);
     }
     // ---- sysctls (allow-lists 1.0 / 1.27 / 1.29) ----
     uint32_t sys_bad = 0;
+    auto sysf = [&](uint32_t id) {
+      sys_bad |= (pbit(a.pp_sysctl0, id) ? 0u : 1u) | (pbit(a.pp_sysctl1, id) ? 0u : 2u) |
+                 (pbit(a.pp_sysctl2, id) ? 0u : 4u);
+    };
     if (nsys) {
-      auto sysf = [&](uint32_t id) {
-        if (!pbit(a.pp_sysctl0, id)) sys_bad |= 1u;
-        if (!pbit(a.pp_sysctl1, id)) sys_bad |= 2u;
-        if (!pbit(a.pp_sysctl2, id)) sys_bad |= 4u;
-      };
       if (ns > 0) sysf(sy0);
+#pragma unroll 1
       for (uint32_t k = 1; k < ns; ++k) sysf(a.sys_id[os + k]);
     }
     // ---- pod-template annotations: AppArmor, seccomp pod annotation ----
     bool apparmor_bad = false, sec_pod_ann_bad = false;
+    auto ann = [&](uint2 kv) {
+      apparmor_bad |= pbit(a.pp_apparmor_key, kv.x) && !pbit(a.pp_apparmor_ok, kv.y);
+      sec_pod_ann_bad |= pbit(a.pp_seccomp_pod_key, kv.x) && !pbit(a.pp_seccomp_ann_ok, kv.y);
+    };
     if (npann) {
-      auto ann = [&](uint2 kv) {
-        apparmor_bad |= pbit(a.pp_apparmor_key, kv.x) && !pbit(a.pp_apparmor_ok, kv.y);
-        sec_pod_ann_bad |= pbit(a.pp_seccomp_pod_key, kv.x) && !pbit(a.pp_seccomp_ann_ok, kv.y);
-      };
       if (na > 0) ann(q0);
       if (na > 1) ann(q1);
+#pragma unroll 1
       for (uint32_t k = 2; k < na; ++k) ann(pkv[oa + k]);
     }
     if (live) fails = cv_fails(rec.x, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
   }
 
   // ---- rules: match/exclude, handler, ApplyOne, verdict cell ----
-  auto filter = [&](uint32_t f) -> bool {
-    const KpeFilter fl = filters[f];
-    for (uint32_t ti = 0; ti < fl.nterms; ++ti) {
-      const KpeTerm tm = terms[fl.term0 + ti];
-      bool ok;
-      if (tm.type == T_KIND_PRED) {
-        ok = pbit((int32_t)tm.a, GVK_KIND(gvk));
-      } else if (tm.type == T_KINDS) {
-        ok = false;
-        for (uint32_t s = 0; s < tm.b && !ok; ++s) {
-          const KpeKindSel ks = kindsels[tm.a + s];
-          ok = ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) &&
-               (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
-        }
-      } else if (tm.type == T_PRED) {
-        const uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : nsa);
-        ok = pbit((int32_t)tm.a, id);
-      } else if (tm.type == T_ANNOTATIONS) {
-        ok = true;
-        const uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
-        for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
-          const KpeAnnPair pr = annpairs[tm.a + pi];
-          bool m = false;
-          for (uint32_t j = lo; j < hi && !m; ++j) m = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
-          ok = m;
-        }
-      } else {
-        ok = false;
-      }
-      if (!ok) return false;
-    }
-    return true;
-  };
-  auto block_match = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> bool {
-    if (mode == MODE_ANY) {
-      for (uint32_t f = 0; f < nf; ++f)
-        if (filter(f0 + f)) return true;
-      return false;
-    }
-    if (mode == MODE_ALL) {
-      for (uint32_t f = 0; f < nf; ++f)
-        if (!filter(f0 + f)) return false;
-      return true;
-    }
-    return filter(f0);
-  };
-
+  const KpeRule* rules = STAGED ? reinterpret_cast<const KpeRule*>(dyn + a.off_rules) : a.rules;
+  const KpeFilter* filters = STAGED ? reinterpret_cast<const KpeFilter*>(dyn + a.off_filters) : a.filters;
+  const KpeTerm* terms = STAGED ? reinterpret_cast<const KpeTerm*>(dyn + a.off_terms) : a.terms;
+  const KpeKindSel* kindsels = STAGED ? reinterpret_cast<const KpeKindSel*>(dyn + a.off_kindsels) : a.kindsels;
+  const KpeAnnPair* annpairs = STAGED ? reinterpret_cast<const KpeAnnPair*>(dyn + a.off_annpairs) : a.annpairs;
+  const uint32_t gvk = pss ? rec.y : gvk_col;
+  const uint32_t nsa = pss ? rec.w : nsa_col;
   const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
   const bool pss_err = cls == R_CLASS_OTHER || (rec.x & PR_DECODE_ERR);
   bool applied = false;
   uint32_t cur_policy = 0xFFFFFFFFu;
   const uint32_t lane = t & 63u;
+#pragma unroll 1
   for (uint32_t ri = 0; ri < R; ++ri) {
     const KpeRule rule = rules[ri];
     if (rule.policy != cur_policy) {
@@ -446,19 +434,57 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     uint32_t cmask = 0;
     if (live && !(rule.apply_one && applied)) {
       bool m = rule.pol_ns_pred < 0 || pbit(rule.pol_ns_pred, nsa);
-      m = m && block_match(rule.match_mode, rule.match_f0, rule.match_nf);
-      if (m) {
-        bool ex;
-        if (rule.excl_mode == MODE_ANY) {
-          ex = false;
-          for (uint32_t f = 0; f < rule.excl_nf && !ex; ++f) ex = filter(rule.excl_f0 + f);
-        } else if (rule.excl_mode == MODE_ALL) {
-          ex = true;
-          for (uint32_t f = 0; f < rule.excl_nf && ex; ++f) ex = filter(rule.excl_f0 + f);
-        } else {
-          ex = filter(rule.excl_f0);
+      // phase 0 = match block, phase 1 = exclude block; one filter evaluation site
+#pragma unroll 1
+      for (uint32_t phase = 0; phase < 2 && m; ++phase) {
+        const uint32_t mode = phase ? rule.excl_mode : rule.match_mode;
+        const uint32_t f0 = phase ? rule.excl_f0 : rule.match_f0;
+        const uint32_t nf = mode == MODE_LEGACY ? 1u : (phase ? rule.excl_nf : rule.match_nf);
+        const bool all_mode = mode == MODE_ALL;
+        bool acc = all_mode;
+#pragma unroll 1
+        for (uint32_t f = 0; f < nf; ++f) {
+          const KpeFilter fl = filters[f0 + f];
+          bool ok = true;
+#pragma unroll 1
+          for (uint32_t ti = 0; ti < fl.nterms && ok; ++ti) {
+            const KpeTerm tm = terms[fl.term0 + ti];
+            if (tm.type == T_KIND_PRED) {
+              ok = pbit((int32_t)tm.a, GVK_KIND(gvk));
+            } else if (tm.type == T_KINDS) {
+              ok = false;
+#pragma unroll 1
+              for (uint32_t s = 0; s < tm.b && !ok; ++s) {
+                const KpeKindSel ks = kindsels[tm.a + s];
+                ok = ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) &&
+                     (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) && (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
+              }
+            } else if (tm.type == T_PRED) {
+              const uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : nsa);
+              ok = pbit((int32_t)tm.a, id);
+            } else if (tm.type == T_ANNOTATIONS) {
+              const uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
+#pragma unroll 1
+              for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
+                const KpeAnnPair pr = annpairs[tm.a + pi];
+                bool hit = false;
+#pragma unroll 1
+                for (uint32_t j = lo; j < hi && !hit; ++j) hit = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
+                ok = hit;
+              }
+            } else {
+              ok = false;
+            }
+          }
+          if (all_mode) {
+            acc = acc && ok;
+            if (!acc) break;
+          } else {
+            acc = acc || ok;
+            if (acc) break;
+          }
         }
-        m = !ex;
+        m = phase ? !acc : acc;
       }
       if (m) {
         if (rule.handler == H_PSS) {
@@ -467,9 +493,11 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
           } else {
             const uint32_t f = fails & rule.cv_mask;
             v = f ? KPE_FAIL_ : KPE_PASS_;
-            if (a.masks)
+            if (a.masks) {
+#pragma unroll 1
               for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
                 if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
+            }
           }
         } else if (rule.handler == H_ERROR) {
           v = KPE_ERROR_;
@@ -498,10 +526,12 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     const uint32_t bytes = np * R;
     uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);  // p0*R is a multiple of 4
     const uint32_t* src = reinterpret_cast<const uint32_t*>(s_v);
+#pragma unroll 1
     for (uint32_t w = t; w < bytes / 4; w += kBlock) dst[w] = src[w];
     if (t < (bytes & 3u)) a.verdicts[(size_t)p0 * R + (bytes & ~3u) + t] = s_v[(bytes & ~3u) + t];
   }
   if (small_r)
+#pragma unroll 1
     for (uint32_t i = t; i < 6 * R; i += kBlock) a.counts_part[(size_t)blockIdx.x * 6 * R + i] = s_cnt[i];
 }
 
@@ -515,8 +545,8 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipSt
 extern "C" uint32_t kpe_scan_blocks(int64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s) {
   if (a->n == 0) return hipSuccess;
-  const size_t dyn = (size_t)(a->prog_words + a->npreds + a->lwords) * 4;
-  if (a->prog_words)
+  const size_t dyn = (size_t)a->blob_words * 4;
+  if (a->img_words)
     hipLaunchKernelGGL(kpe_scan_kernel<true>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
   else
     hipLaunchKernelGGL(kpe_scan_kernel<false>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);

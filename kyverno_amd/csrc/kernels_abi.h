@@ -59,24 +59,22 @@ struct ScanArgs {
   const uint32_t* sys_id;     // per sysctl: D_SYSCTL id
   const uint32_t* pann_kv;    // per pod-template annotation: (D_ANNK id, D_ANNV id)
   const uint32_t* c_sann;     // per container: value id of its seccomp annotation (cold)
-  const uint64_t* capset_add; // capability-set dictionary
-  const uint64_t* capset_drop;
+  const uint32_t* capsets;    // capability-set dictionary: 4 words (add lo/hi, drop lo/hi) per set
   uint32_t ncapsets;
-  // program (global copies)
+  uint32_t nctr_total, nvol_total, nsys_total, npann_total;  // list lengths (load clamping)
+  // program (global copies, used when the image does not fit LDS)
   const KpeRule* rules;
   uint32_t nrules;
   const KpeFilter* filters;
   const KpeTerm* terms;
   const KpeKindSel* kindsels;
   const KpeAnnPair* annpairs;
-  // program image staged into LDS (prog_words == 0 => read the global copies)
-  const uint32_t* prog;
-  uint32_t prog_words, off_rules, off_filters, off_terms, off_kindsels, off_annpairs;
-  // predicates
-  const uint32_t* pred_bits;   // all predicate bitsets (dictionary pass output)
-  const uint32_t* pred_word;   // per predicate: global word offset, or PRED_LOCAL | LDS word offset
-  uint32_t npreds;
-  uint32_t lwords;             // pred_bits[0, lwords) = small-domain bitsets, copied into LDS per block
+  // preamble: pbuf[0, blob_words) = [program image (img_words)][predicate directory (npreds)]
+  // [small-domain bitsets], copied into LDS by every block; pbuf[blob_words, ...) = large-domain
+  // bitsets. Directory entry: PRED_LOCAL | LDS word index, or absolute pbuf word index.
+  const uint32_t* pbuf;
+  uint32_t blob_words, img_words, npreds;
+  uint32_t off_rules, off_filters, off_terms, off_kindsels, off_annpairs;
   int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, any_pss, need;

@@ -118,8 +118,8 @@ struct DeviceProgram {
 
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
   const Program* prog = nullptr;
-  DevBuf jobs, pred_word, pred_bits, verdicts, masks, counts_part, counts_global, counts_out;
-  uint32_t nblocks = 0, njobs = 0, lwords = 0, scan_blocks = 0;
+  DevBuf jobs, pbuf, verdicts, masks, counts_part, counts_global, counts_out;
+  uint32_t nblocks = 0, njobs = 0, blob_words = 0, img_words = 0, scan_blocks = 0;
   uint32_t need = 0;
   double scan_bytes = 0;
   size_t cells = 0;
@@ -129,7 +129,7 @@ struct DeviceCorpus {
   int ordinal = -1;
   DevBuf dict_bytes[KPE_NUM_DOMAINS], dict_off[KPE_NUM_DOMAINS];
   DevBuf r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
-  DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capset_add, capset_drop;
+  DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
   Binding bind;
   bool has_masks = false;
 };
@@ -256,8 +256,16 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   HIPCHK(upload(D.sys_id, C.sys_id, s));
   HIPCHK(upload(D.pann_kv, C.pann_kv, s));
   HIPCHK(upload(D.c_sann, C.c_sann, s));
-  HIPCHK(upload(D.capset_add, C.capset_add, s));
-  HIPCHK(upload(D.capset_drop, C.capset_drop, s));
+  {
+    std::vector<uint32_t> cs;
+    for (size_t i = 0; i < C.capset_add.size(); ++i) {
+      cs.push_back((uint32_t)C.capset_add[i]);
+      cs.push_back((uint32_t)(C.capset_add[i] >> 32));
+      cs.push_back((uint32_t)C.capset_drop[i]);
+      cs.push_back((uint32_t)(C.capset_drop[i] >> 32));
+    }
+    HIPCHK(upload(D.capsets, cs, s));
+  }
   HIPCHK(hipStreamSynchronize(s));
   return KPE_OK;
 }
@@ -386,48 +394,54 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   size_t cells = (size_t)C.n * P.rules.size();
   if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
   hipStream_t s = dev->stream;
-  // predicate placement: every predicate is evaluated by the dictionary pass;
-  // small-domain bitsets are laid out first ([0, lwords)) so each scan block
-  // copies them into LDS with one loop, large ones stay in global memory.
-  std::vector<PredJob> jobs;
-  std::vector<uint32_t> word(P.preds.size());
-  std::vector<uint32_t> order;
+  // Preamble layout (pbuf): [program image][predicate directory][small-domain bitsets]
+  // (padded to 16 B; copied into LDS by every scan block) followed by the large-domain
+  // bitsets. Every predicate is evaluated by the dictionary pass straight into pbuf.
+  const uint32_t img = PD.image_words;  // 0 when the program does not fit the LDS budget
+  const uint32_t npreds = (uint32_t)P.preds.size();
+  std::vector<uint32_t> nwords(npreds);
+  std::vector<char> local(npreds, 0);
   uint32_t lw = 0;
-  for (int pass = 0; pass < 2; ++pass)
-    for (size_t p = 0; p < P.preds.size(); ++p) {
-      uint32_t n = C.dict[P.preds[p].domain].size();
-      uint32_t nwords = ((n + 63) / 64) * 2 + 2;
-      bool small = lw + nwords <= kMaxLocalWords && n <= kMaxLocalPairs;
-      if (pass == 0 && small) {
-        order.push_back((uint32_t)p);
-        lw += nwords;
-      } else if (pass == 1 && std::find(order.begin(), order.end(), (uint32_t)p) == order.end()) {
-        order.push_back((uint32_t)p);
-      }
+  for (uint32_t p = 0; p < npreds; ++p) {
+    uint32_t n = C.dict[P.preds[p].domain].size();
+    nwords[p] = ((n + 63) / 64) * 2 + 2;
+    if (lw + nwords[p] <= kMaxLocalWords && n <= kMaxLocalPairs) {
+      local[p] = 1;
+      lw += nwords[p];
     }
-  uint32_t gw = 0, blk = 0, nlocal = 0;
-  for (size_t i = 0; i < order.size(); ++i) {
-    uint32_t p = order[i];
-    const auto& pr = P.preds[p];
-    uint32_t n = C.dict[pr.domain].size();
-    uint32_t nwords = ((n + 63) / 64) * 2 + 2;
-    bool local = gw + nwords <= lw;
-    word[p] = local ? (PRED_LOCAL | gw) : gw;
-    nlocal += local;
+  }
+  const uint32_t blob = std::max(4u, (img + npreds + lw + 3) & ~3u);
+  std::vector<uint32_t> dir(npreds);
+  std::vector<PredJob> jobs;
+  uint32_t lo = img + npreds, go = blob, blk = 0;
+  for (uint32_t p = 0; p < npreds; ++p) {
+    uint32_t at;
+    if (local[p]) {
+      at = lo;
+      lo += nwords[p];
+      dir[p] = PRED_LOCAL | at;  // LDS word index (== pbuf index inside the preamble)
+    } else {
+      at = go;
+      go += nwords[p];
+      dir[p] = at;
+    }
+    uint32_t n = C.dict[P.preds[p].domain].size();
     if (n) {
-      jobs.push_back({pr.domain, PD.pat0[p], (uint32_t)pr.globs.size(), gw, blk});
+      jobs.push_back({P.preds[p].domain, PD.pat0[p], (uint32_t)P.preds[p].globs.size(), at, blk});
       blk += (n + 255) / 256;
     }
-    gw += nwords;
   }
-  B.lwords = lw;
+  HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
+  HIPCHK(hipMemsetAsync(B.pbuf.p, 0, (size_t)go * 4 + 16, s));
+  if (img) HIPCHK(hipMemcpyAsync(B.pbuf.p, PD.image.p, (size_t)img * 4, hipMemcpyDeviceToDevice, s));
+  if (npreds)
+    HIPCHK(hipMemcpyAsync(B.pbuf.as<uint32_t>() + img, dir.data(), (size_t)npreds * 4, hipMemcpyHostToDevice, s));
+  B.blob_words = blob;
+  B.img_words = img;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
   B.scan_blocks = kpe_scan_blocks(C.n);
   HIPCHK(upload(B.jobs, jobs, s));
-  HIPCHK(upload(B.pred_word, word, s));
-  HIPCHK(B.pred_bits.ensure(std::max<size_t>(gw, 1) * 4));
-  HIPCHK(hipMemsetAsync(B.pred_bits.p, 0, std::max<size_t>(gw, 1) * 4, s));
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
   size_t width = P.rules.size() * 6;
   HIPCHK(B.counts_part.ensure(std::max<size_t>((size_t)B.scan_blocks * width, 1) * 4));
@@ -470,7 +484,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     pa.pats = PD.pats.as<KpePat>();
     pa.jobs = B.jobs.as<PredJob>();
     pa.njobs = B.njobs;
-    pa.out = B.pred_bits.as<uint32_t>();
+    pa.out = B.pbuf.as<uint32_t>();
     HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
   }
   if (R > KPE_SMALL_R) HIPCHK(hipMemsetAsync(B.counts_global.p, 0, R * 6 * 8, s));
@@ -491,26 +505,27 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.sys_id = D.sys_id.as<uint32_t>();
   sa.pann_kv = D.pann_kv.as<uint32_t>();
   sa.c_sann = D.c_sann.as<uint32_t>();
-  sa.capset_add = D.capset_add.as<uint64_t>();
-  sa.capset_drop = D.capset_drop.as<uint64_t>();
+  sa.capsets = D.capsets.as<uint32_t>();
   sa.ncapsets = (uint32_t)C.capset_add.size();
+  sa.nctr_total = (uint32_t)C.c_sc.size();
+  sa.nvol_total = (uint32_t)C.vol_src.size();
+  sa.nsys_total = (uint32_t)C.sys_id.size();
+  sa.npann_total = (uint32_t)(C.pann_kv.size() / 2);
   sa.rules = PD.rules.as<KpeRule>();
   sa.nrules = (uint32_t)R;
   sa.filters = PD.filters.as<KpeFilter>();
   sa.terms = PD.terms.as<KpeTerm>();
   sa.kindsels = PD.kindsels.as<KpeKindSel>();
   sa.annpairs = PD.annpairs.as<KpeAnnPair>();
-  sa.prog = PD.image.as<uint32_t>();
-  sa.prog_words = PD.image_words;
+  sa.pbuf = B.pbuf.as<uint32_t>();
+  sa.blob_words = B.blob_words;
+  sa.img_words = B.img_words;
+  sa.npreds = (uint32_t)P.preds.size();
   sa.off_rules = PD.off_rules;
   sa.off_filters = PD.off_filters;
   sa.off_terms = PD.off_terms;
   sa.off_kindsels = PD.off_kindsels;
   sa.off_annpairs = PD.off_annpairs;
-  sa.pred_bits = B.pred_bits.as<uint32_t>();
-  sa.pred_word = B.pred_word.as<uint32_t>();
-  sa.npreds = (uint32_t)P.preds.size();
-  sa.lwords = B.lwords;
   sa.pp_apparmor_key = P.pss.apparmor_key;
   sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
   sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;
