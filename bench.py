@@ -38,6 +38,7 @@ def main():
     import torch.distributed as dist
 
     import kyverno_amd as K
+    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, max_over_ranks
     from tests.policies import restricted_latest
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -68,10 +69,12 @@ def main():
         corpora.append(c)
     t_setup = time.time() - t_setup
     # correctness touch + counters from one synchronous evaluation per replica
-    total_fail = 0
+    totals = [dict.fromkeys(COUNT_FIELDS, 0) for _ in range(R)]
     for c in corpora:
-        v, _, cnt = eng.evaluate(ps, c)
-        total_fail += cnt[0]["fail"]
+        _, _, cnt = eng.evaluate(ps, c)
+        for r in range(R):
+            for f in COUNT_FIELDS:
+                totals[r][f] += cnt[r][f]
 
     for i in range(args.warmup):
         eng.evaluate_async(ps, corpora[i % len(corpora)])
@@ -90,13 +93,10 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        cnt_t = torch.tensor([total_fail], dtype=torch.int64, device="cuda")
-        dist.all_reduce(cnt_t)  # the one real exchange: per-rule totals (RCCL over xGMI)
-        total_fail = int(cnt_t.item())
+    elapsed = max_over_ranks(elapsed, device="cuda")
+    # the one real exchange: per-rule totals (R x 6 u64, RCCL over xGMI)
+    totals = allreduce_counts(totals, device="cuda")
+    total_fail = totals[0]["fail"]
 
     # ---- per-kernel timing pass (HIP events on the evaluation stream) ----
     eng.device.set_timing(True)
@@ -150,7 +150,8 @@ def main():
             "config": {"workload": "C2: 1M synthetic Pods x PSS restricted:latest per GPU (R=3 rules after autogen)",
                        "resources_per_gpu": n, "rules": R, "global_resources": n * world,
                        "replicas_rotated": args.replicas, "parallelism": f"resource-sharded x{world}",
-                       "fail_fraction": total_fail / float(n * args.replicas * world)},
+                       "fail_fraction": total_fail / float(n * args.replicas * world),
+                       "counts_rule0": totals[0]},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "kpe_scan_kernel", "kernel_ms": scan_ms, "dict_kernel_ms": dict_ms,

@@ -100,6 +100,11 @@ def test_c2_scale_properties(engine, oracle):
     # idempotence: a second evaluation gives the identical matrix
     v2, _, _ = engine.evaluate(ps, c)
     assert np.array_equal(v, v2)
+    # batch-position independence: a separately flattened shard gives the same rows
+    first = 500_000
+    shard = K.Corpus(K.synth_resources(0xC2, 1000, mix=0, first_index=first))
+    vs, _, _ = engine.evaluate(ps, shard)
+    assert np.array_equal(vs, v[first:first + 1000])
     lines = nd.split(b"\n")
     idx = list(range(0, n, 997))
     sub = b"\n".join(lines[i] for i in idx)
