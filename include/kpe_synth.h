@@ -21,12 +21,17 @@ extern "C" {
 enum kpe_synth_mix {
   KPE_SYNTH_PODS = 0,   /* C2: Pods only                                      */
   KPE_SYNTH_MIXED = 1,  /* Pods, Deployments, DaemonSets, Jobs, CronJobs, Services, ConfigMaps */
-  KPE_SYNTH_EDGE = 2    /* MIXED + edge cases: nulls, windows pods, type errors, odd values */
+  KPE_SYNTH_EDGE = 2,   /* MIXED + edge cases: nulls, windows pods, type errors, odd values */
+  KPE_SYNTH_SELECTORS = 3 /* C4: Deployments + Services, 8 labels from a 64-key vocabulary,
+                             namespaces ns-00000..ns-09999 */
 };
 
 /* Generate n resources as NDJSON into a malloc'd buffer (*out, *len). Free with kpe_synth_free. */
 int kpe_synth_resources(uint64_t seed, int64_t first_index, int64_t n, int mix, char** out, size_t* len);
 void kpe_synth_free(char* p);
+/* Namespace label table {"ns-…": {"k": "v"}} for namespaces 0..n-1 of the given mix
+ * (ns-%04d, or ns-%05d for KPE_SYNTH_SELECTORS). Free with kpe_synth_free. */
+int kpe_synth_ns_labels(uint64_t seed, int64_t n_namespaces, int mix, char** out, size_t* len);
 
 #ifdef __cplusplus
 }

@@ -16,6 +16,7 @@ from .engine import (  # noqa: F401
     PolicySet,
     RuleResponse,
     RuleStatus,
+    synth_ns_labels,
     synth_resources,
 )
 
@@ -29,6 +30,7 @@ __all__ = [
     "PolicySet",
     "RuleResponse",
     "RuleStatus",
+    "synth_ns_labels",
     "synth_resources",
     "load",
     "lib_path",

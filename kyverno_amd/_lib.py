@@ -65,6 +65,8 @@ def load():
     L.kpe_synth_resources.argtypes = [ctypes.c_uint64, i64, i64, i32, ctypes.POINTER(ctypes.c_void_p),
                                       ctypes.POINTER(sz)]
     L.kpe_synth_free.argtypes = [vp]
+    L.kpe_synth_ns_labels.argtypes = [ctypes.c_uint64, i64, i32, ctypes.POINTER(ctypes.c_void_p),
+                                      ctypes.POINTER(ctypes.c_size_t)]
     _LIB = L
     return L
 

@@ -69,6 +69,42 @@ __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int
   return true;
 }
 
+// k8s.io/apimachinery v0.29.1 util/validation (IsQualifiedName / IsValidLabelValue)
+__device__ __forceinline__ bool qn_char(uint8_t c) {
+  return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9');
+}
+__device__ bool name_part_ok(const uint8_t* s, int n) {
+  if (n == 0 || n > 63 || !qn_char(s[0]) || !qn_char(s[n - 1])) return false;
+  for (int i = 0; i < n; ++i)
+    if (!(qn_char(s[i]) || s[i] == '-' || s[i] == '_' || s[i] == '.')) return false;
+  return true;
+}
+__device__ bool dns1123_subdomain_ok(const uint8_t* s, int n) {
+  if (n == 0 || n > 253) return false;
+  int start = 0;
+  for (int i = 0; i <= n; ++i) {
+    if (i == n || s[i] == '.') {
+      if (i == start) return false;
+      start = i + 1;
+      continue;
+    }
+    const uint8_t c = s[i];
+    const bool an = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9');
+    if (!(an || (c == '-' && i != start && i + 1 < n && s[i + 1] != '.'))) return false;
+  }
+  return true;
+}
+__device__ bool qualified_name_ok(const uint8_t* s, int n) {
+  int slash = -1;
+  for (int i = 0; i < n; ++i)
+    if (s[i] == '/') {
+      if (slash >= 0) return false;
+      slash = i;
+    }
+  if (slash < 0) return name_part_ok(s, n);
+  return dns1123_subdomain_ok(s, slash) && name_part_ok(s + slash + 1, n - slash - 1);
+}
+
 __device__ bool pat_match(const KpePat& pt, const uint8_t* pb, const uint8_t* s, int sn) {
   const uint8_t* lit = pb + pt.off;
   const int ln = (int)pt.len;
@@ -81,6 +117,8 @@ __device__ bool pat_match(const KpePat& pt, const uint8_t* pb, const uint8_t* s,
       for (int i = 0; i + ln <= sn; ++i)
         if (bytes_eq(lit, s + i, ln)) return true;
       return false;
+    case PK_QNAME: return qualified_name_ok(s, sn);
+    case PK_LABVAL: return sn == 0 || name_part_ok(s, sn);
     default: return glob(lit, ln, s, sn);
   }
 }
@@ -416,6 +454,8 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const KpeTerm* terms = STAGED ? reinterpret_cast<const KpeTerm*>(dyn + a.off_terms) : a.terms;
   const KpeKindSel* kindsels = STAGED ? reinterpret_cast<const KpeKindSel*>(dyn + a.off_kindsels) : a.kindsels;
   const KpeAnnPair* annpairs = STAGED ? reinterpret_cast<const KpeAnnPair*>(dyn + a.off_annpairs) : a.annpairs;
+  const KpeSelector* selectors = STAGED ? reinterpret_cast<const KpeSelector*>(dyn + a.off_selectors) : a.selectors;
+  const KpeSelReq* selreqs = STAGED ? reinterpret_cast<const KpeSelReq*>(dyn + a.off_selreqs) : a.selreqs;
   const uint32_t gvk = pss ? rec.y : gvk_col;
   const uint32_t nsa = pss ? rec.w : nsa_col;
   const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
@@ -471,6 +511,51 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
 #pragma unroll 1
                 for (uint32_t j = lo; j < hi && !hit; ++j) hit = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
                 ok = hit;
+              }
+            } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
+              const KpeSelector S = selectors[tm.a];
+              uint32_t lo = 0, hi = 0;
+              const uint32_t *K, *V;
+              bool eval = true;
+              if (tm.type == T_SELECTOR) {
+                lo = a.lab_off[r], hi = a.lab_off[r + 1];
+                K = a.lab_k, V = a.lab_v;
+              } else {
+                // namespaceSelector: never for kind Namespace; skipped for an empty kind
+                // unless the block's kinds hold "*" (pkg/engine/utils/match.go:125-138)
+                const uint32_t kid = GVK_KIND(gvk);
+                const uint32_t row = a.r_nsl[r];
+                if (row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
+                K = a.nsl_k, V = a.nsl_v;
+                if (pbit(S.p_kind_ns, kid)) {
+                  ok = false, eval = false;
+                } else if (pbit(S.p_kind_empty, kid) && !S.star_kind) {
+                  ok = true, eval = false;
+                } else if (S.invalid) {
+                  ok = false, eval = false;
+                }
+              }
+              if (eval) {
+                ok = true;
+#pragma unroll 1
+                for (uint32_t qi = 0; qi < S.nreq && ok; ++qi) {
+                  const KpeSelReq q = selreqs[S.req0 + qi];
+                  const bool wild = q.op == SR_WILD;
+                  uint32_t j = lo;
+#pragma unroll 1
+                  for (; j < hi; ++j)
+                    if (pbit(q.pk, K[j]) && (!wild || pbit(q.pv, V[j]))) break;
+                  const bool found = j < hi;
+                  const uint32_t vid = found ? V[j] : KPE_NO_STR;
+                  switch (q.op) {
+                    case SR_EQ:
+                    case SR_IN: ok = found && pbit(q.pv, vid); break;
+                    case SR_WILD: ok = found && pbit(q.pk_ok, K[j]) && pbit(q.pv_ok, vid); break;
+                    case SR_NOTIN: ok = !found || !pbit(q.pv, vid); break;
+                    case SR_EXISTS: ok = found; break;
+                    default: ok = !found; break;
+                  }
+                }
               }
             } else {
               ok = false;

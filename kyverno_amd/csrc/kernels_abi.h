@@ -16,6 +16,8 @@
 #define NEED_SYS (1u << 5)
 #define NEED_PANN (1u << 6)
 #define NEED_NSA (1u << 7)
+#define NEED_LAB (1u << 8)   // resource labels (CSR) for label selectors
+#define NEED_NSL (1u << 9)   // namespace label table for namespaceSelector
 
 // Pattern classes (host-classified go-wildcard patterns; '?' or an inner '*' => PK_GLOB)
 #define PK_ANY 0u       // "*"
@@ -24,6 +26,8 @@
 #define PK_SUFFIX 3u    // "*lit"
 #define PK_CONTAINS 4u  // "*lit*"
 #define PK_GLOB 5u      // general: full pattern text
+#define PK_QNAME 6u     // validation.IsQualifiedName (apimachinery v0.29.1, label keys)
+#define PK_LABVAL 7u    // validation.IsValidLabelValue
 struct KpePat {
   uint32_t kind, off, len, pad;  // literal (or full pattern for PK_GLOB) = pat_bytes[off, off+len)
 };
@@ -51,6 +55,8 @@ struct ScanArgs {
   int64_t n;
   // resource rows (unstructured view) — read by match terms
   const uint32_t *r_gvk, *r_name, *r_mns, *r_nsa, *ann_off, *ann_k, *ann_v;
+  const uint32_t *lab_off, *lab_k, *lab_v;           // metadata.labels CSR
+  const uint32_t *r_nsl, *nsl_off, *nsl_k, *nsl_v;   // namespace label table row per resource
   // PSS hot records (schema.h): pod records, wave headers, container records
   const uint32_t* rec;        // 4 words per pod
   const uint32_t* hdr;        // 4 words per 64 pods
@@ -69,12 +75,14 @@ struct ScanArgs {
   const KpeTerm* terms;
   const KpeKindSel* kindsels;
   const KpeAnnPair* annpairs;
+  const KpeSelector* selectors;
+  const KpeSelReq* selreqs;
   // preamble: pbuf[0, blob_words) = [program image (img_words)][predicate directory (npreds)]
   // [small-domain bitsets], copied into LDS by every block; pbuf[blob_words, ...) = large-domain
   // bitsets. Directory entry: PRED_LOCAL | LDS word index, or absolute pbuf word index.
   const uint32_t* pbuf;
   uint32_t blob_words, img_words, npreds;
-  uint32_t off_rules, off_filters, off_terms, off_kindsels, off_annpairs;
+  uint32_t off_rules, off_filters, off_terms, off_kindsels, off_annpairs, off_selectors, off_selreqs;
   int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, any_pss, need;

@@ -109,11 +109,12 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
-  DevBuf rules, filters, terms, kindsels, annpairs, pat_bytes, pats, image;
+  DevBuf rules, filters, terms, kindsels, annpairs, selectors, selreqs, pat_bytes, pats, image;
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
   uint32_t image_words = 0, off_rules = 0, off_filters = 0, off_terms = 0, off_kindsels = 0, off_annpairs = 0;
+  uint32_t off_selectors = 0, off_selreqs = 0;
 };
 
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
@@ -129,6 +130,7 @@ struct DeviceCorpus {
   int ordinal = -1;
   DevBuf dict_bytes[KPE_NUM_DOMAINS], dict_off[KPE_NUM_DOMAINS];
   DevBuf r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
+  DevBuf lab_off, lab_k, lab_v, r_nsl, nsl_off, nsl_k, nsl_v;
   DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
   Binding bind;
   bool has_masks = false;
@@ -249,6 +251,13 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   HIPCHK(upload(D.ann_off, C.ann_off, s));
   HIPCHK(upload(D.ann_k, C.ann_k, s));
   HIPCHK(upload(D.ann_v, C.ann_v, s));
+  HIPCHK(upload(D.lab_off, C.lab_off, s));
+  HIPCHK(upload(D.lab_k, C.lab_k, s));
+  HIPCHK(upload(D.lab_v, C.lab_v, s));
+  HIPCHK(upload(D.r_nsl, C.r_nsl, s));
+  HIPCHK(upload(D.nsl_off, C.nsl_off, s));
+  HIPCHK(upload(D.nsl_k, C.nsl_k, s));
+  HIPCHK(upload(D.nsl_v, C.nsl_v, s));
   HIPCHK(upload(D.rec, C.rec, s));
   HIPCHK(upload(D.hdr, C.hdr, s));
   HIPCHK(upload(D.crec, C.crec, s));
@@ -319,6 +328,10 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   hipStream_t s = dev->stream;
   for (auto& pr : P.preds) {
     D.pat0.push_back((uint32_t)D.pats_h.size());
+    if (pr.special == PRED_SPECIAL_QNAME)
+      D.pats_h.push_back({PK_QNAME, 0, 0, 0});
+    else if (pr.special == PRED_SPECIAL_LABVAL)
+      D.pats_h.push_back({PK_LABVAL, 0, 0, 0});
     for (auto& g : pr.globs) D.pats_h.push_back(classify_pattern(g, D.pat_bytes_h));
   }
   std::vector<uint32_t> img;
@@ -327,12 +340,16 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   append_words(img, P.terms, &D.off_terms);
   append_words(img, P.kindsels, &D.off_kindsels);
   append_words(img, P.annpairs, &D.off_annpairs);
+  append_words(img, P.selectors, &D.off_selectors);
+  append_words(img, P.selreqs, &D.off_selreqs);
   D.image_words = img.size() <= kMaxProgWords ? (uint32_t)img.size() : 0;
   HIPCHK(upload(D.rules, P.rules, s));
   HIPCHK(upload(D.filters, P.filters, s));
   HIPCHK(upload(D.terms, P.terms, s));
   HIPCHK(upload(D.kindsels, P.kindsels, s));
   HIPCHK(upload(D.annpairs, P.annpairs, s));
+  HIPCHK(upload(D.selectors, P.selectors, s));
+  HIPCHK(upload(D.selreqs, P.selreqs, s));
   HIPCHK(upload(D.pat_bytes, D.pat_bytes_h, s));
   HIPCHK(upload(D.pats, D.pats_h, s));
   HIPCHK(upload(D.image, img, s));
@@ -356,7 +373,11 @@ uint32_t need_flags(const kpe::Program& P) {
   for (auto& r : P.rules)
     if (r.handler != H_NONE && r.handler != H_PSS) need |= NEED_FLAGS;
   for (auto& t : P.terms)
-    if (t.type == T_KINDS || t.type == T_KIND_PRED) need |= NEED_GVK;
+    if (t.type == T_KINDS || t.type == T_KIND_PRED || t.type == T_NSSELECTOR) need |= NEED_GVK;
+  for (auto& t : P.terms) {
+    if (t.type == T_SELECTOR) need |= NEED_LAB;
+    if (t.type == T_NSSELECTOR) need |= NEED_NSL;
+  }
   for (auto& r : P.rules)
     if (r.pol_ns_pred >= 0) need |= NEED_NSA;
   return need;
@@ -381,6 +402,9 @@ double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bo
       b += 4 * n;
       break;
     }
+  // label CSR / namespace-label rows read by selector terms (once per resource)
+  if (need & NEED_LAB) b += 4.0 * n + 8.0 * C.lab_k.size();
+  if (need & NEED_NSL) b += 4.0 * n;  // r_nsl; the namespace table itself is cache-resident
   b += n * P.rules.size() * (masks ? 5.0 : 1.0);  // verdict cells (+ check masks)
   if (P.rules.size() <= KPE_SMALL_R) b += 4.0 * kpe_scan_blocks(C.n) * 6 * P.rules.size();
   return b;
@@ -427,7 +451,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     }
     uint32_t n = C.dict[P.preds[p].domain].size();
     if (n) {
-      jobs.push_back({P.preds[p].domain, PD.pat0[p], (uint32_t)P.preds[p].globs.size(), at, blk});
+      const uint32_t pend = p + 1 < PD.pat0.size() ? PD.pat0[p + 1] : (uint32_t)PD.pats_h.size();
+      jobs.push_back({P.preds[p].domain, PD.pat0[p], pend - PD.pat0[p], at, blk});
       blk += (n + 255) / 256;
     }
   }
@@ -498,6 +523,13 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.ann_off = D.ann_off.as<uint32_t>();
   sa.ann_k = D.ann_k.as<uint32_t>();
   sa.ann_v = D.ann_v.as<uint32_t>();
+  sa.lab_off = D.lab_off.as<uint32_t>();
+  sa.lab_k = D.lab_k.as<uint32_t>();
+  sa.lab_v = D.lab_v.as<uint32_t>();
+  sa.r_nsl = D.r_nsl.as<uint32_t>();
+  sa.nsl_off = D.nsl_off.as<uint32_t>();
+  sa.nsl_k = D.nsl_k.as<uint32_t>();
+  sa.nsl_v = D.nsl_v.as<uint32_t>();
   sa.rec = D.rec.as<uint32_t>();
   sa.hdr = D.hdr.as<uint32_t>();
   sa.crec = D.crec.as<uint32_t>();
@@ -517,6 +549,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.terms = PD.terms.as<KpeTerm>();
   sa.kindsels = PD.kindsels.as<KpeKindSel>();
   sa.annpairs = PD.annpairs.as<KpeAnnPair>();
+  sa.selectors = PD.selectors.as<KpeSelector>();
+  sa.selreqs = PD.selreqs.as<KpeSelReq>();
   sa.pbuf = B.pbuf.as<uint32_t>();
   sa.blob_words = B.blob_words;
   sa.img_words = B.img_words;
@@ -526,6 +560,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.off_terms = PD.off_terms;
   sa.off_kindsels = PD.off_kindsels;
   sa.off_annpairs = PD.off_annpairs;
+  sa.off_selectors = PD.off_selectors;
+  sa.off_selreqs = PD.off_selreqs;
   sa.pp_apparmor_key = P.pss.apparmor_key;
   sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
   sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;

@@ -259,6 +259,42 @@ bool glob_host(const std::string& pat, const std::string& s) {
 }
 
 // ---- kind helpers (pkg/utils/kube/kind.go) ----
+// k8s.io/apimachinery v0.29.1 util/validation, restated (third-party; pinned by
+// pkg/utils/match/labels_test.go and the selector cases of tests/golden).
+bool qname_char(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
+bool name_part_ok(const std::string& s) {  // qualifiedNameFmt, <= 63 bytes
+  if (s.empty() || s.size() > 63 || !qname_char(s.front()) || !qname_char(s.back())) return false;
+  for (char c : s)
+    if (!(qname_char(c) || c == '-' || c == '_' || c == '.')) return false;
+  return true;
+}
+bool dns1123_subdomain_ok(const std::string& s) {  // dns1123SubdomainFmt, <= 253 bytes
+  if (s.empty() || s.size() > 253) return false;
+  size_t i = 0;
+  while (true) {
+    size_t j = s.find('.', i);
+    if (j == std::string::npos) j = s.size();
+    if (j == i) return false;
+    for (size_t k = i; k < j; ++k) {
+      char c = s[k];
+      bool an = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9');
+      if (!(an || (c == '-' && k != i && k + 1 != j))) return false;
+    }
+    if (j == s.size()) return true;
+    i = j + 1;
+  }
+}
+bool qualified_name_ok(const std::string& s) {  // IsQualifiedName
+  size_t p = s.find('/');
+  if (p == std::string::npos) return name_part_ok(s);
+  if (s.find('/', p + 1) != std::string::npos) return false;
+  return dns1123_subdomain_ok(s.substr(0, p)) && name_part_ok(s.substr(p + 1));
+}
+bool label_value_ok(const std::string& s) { return s.empty() || name_part_ok(s); }  // IsValidLabelValue
+bool has_wildcard(const std::string& s) {  // wildcard.ContainsWildcard
+  return s.find('*') != std::string::npos || s.find('?') != std::string::npos;
+}
+
 bool version_regex(const std::string& s) {  // `^v\d((alpha|beta)\d)?|\*$`
   if (s.size() >= 2 && s[0] == 'v' && s[1] >= '0' && s[1] <= '9') return true;
   return !s.empty() && s.back() == '*';
@@ -566,7 +602,12 @@ class Lowerer {
       P.terms.push_back(t);
       f.nterms++;
     };
-    bool rd_empty = !nonempty(rd);
+    // ResourceDescription{} DeepEqual: a present selector pointer is never zero, even `{}`
+    auto sel_obj = [&](const char* k) {
+      const JV* x = rd ? rd->get(k) : nullptr;
+      return x && x->t == JV::Obj;
+    };
+    bool rd_empty = !nonempty(rd) && !sel_obj("selector") && !sel_obj("namespaceSelector");
     if (!is_exclude) {
       // userInfo is cleared for empty admission info (utils/match.go:263-265)
       if (rd_empty) push({T_FALSE, 0, 0, 0});  // "match cannot be empty"
@@ -621,14 +662,118 @@ class Lowerer {
         push({T_ANNOTATIONS, a0, (uint32_t)ann->o.size(), 0});
       }
       const JV* sel = rd->get("selector");
-      if (sel && sel->t != JV::Null) throw CompileError("label selectors in match/exclude are not supported yet");
+      if (sel && sel->t != JV::Null) selector(sel, false, false, push);
       const JV* nsel = rd->get("namespaceSelector");
-      if (nsel && nsel->t != JV::Null)
-        throw CompileError("namespaceSelector in match/exclude is not supported yet");
+      if (nsel && nsel->t != JV::Null) {
+        bool star = std::find(kinds.begin(), kinds.end(), "*") != kinds.end();
+        selector(nsel, true, star, push);
+      }
     }
     P.filters.push_back(f);
     return (uint32_t)P.filters.size() - 1;
   }
+  int32_t special_pred(uint32_t domain, uint32_t special) {
+    for (size_t i = 0; i < P.preds.size(); ++i)
+      if (P.preds[i].domain == domain && P.preds[i].special == special) return (int32_t)i;
+    P.preds.push_back({domain, {}, special});
+    return (int32_t)P.preds.size() - 1;
+  }
+  // CheckSelector (pkg/utils/match/labels.go:9-24): ReplaceInSelector then
+  // metav1.LabelSelectorAsSelector + Matches. A selector that fails to build is a
+  // non-match ("failed to parse selector", pkg/engine/utils/match.go:114-123).
+  template <class Push>
+  void selector(const JV* sel, bool ns_sel, bool star_kind, Push&& push) {
+    if (sel->t != JV::Obj) throw std::invalid_argument("label selector must be an object");
+    const JV* ml = sel->get("matchLabels");
+    const JV* me = sel->get("matchExpressions");
+    if (ml && ml->t != JV::Null && ml->t != JV::Obj) throw std::invalid_argument("matchLabels must be an object");
+    if (me && me->t != JV::Null && me->t != JV::Arr) throw std::invalid_argument("matchExpressions must be a list");
+    const size_t nml = ml && ml->t == JV::Obj ? ml->o.size() : 0, nme = me && me->t == JV::Arr ? me->a.size() : 0;
+    KpeSelector S{};
+    S.req0 = (uint32_t)P.selreqs.size();
+    S.p_kind_ns = S.p_kind_empty = -1;
+    if (ns_sel) {
+      S.p_kind_ns = pred(D_KIND, {"Namespace"});
+      S.p_kind_empty = pred(D_KIND, {""});
+      S.star_kind = star_kind ? 1u : 0u;
+    }
+    bool invalid = false;
+    std::vector<KpeSelReq> reqs;
+    if (nml) {
+      // Wildcard keys can make two entries resolve to the same key; the result
+      // then depends on Go map iteration order in the reference. Refuse those.
+      std::vector<std::string> keys;
+      for (auto& kv : ml->o) keys.push_back(kv.first);
+      for (size_t i = 0; i < keys.size(); ++i) {
+        if (!has_wildcard(keys[i])) continue;
+        std::string rk = keys[i];
+        for (auto& c : rk)
+          if (c == '*' || c == '?') c = '0';
+        for (size_t j = 0; j < keys.size(); ++j)
+          if (j != i && (has_wildcard(keys[j]) || glob_host(keys[i], keys[j]) || rk == keys[j]))
+            throw CompileError("label selector with colliding wildcard keys (order-dependent in the reference)");
+      }
+      for (auto& kv : ml->o) {
+        if (kv.second.t != JV::Str) throw std::invalid_argument("matchLabels values must be strings");
+        const std::string& k = kv.first;
+        const std::string& v = kv.second.s;
+        KpeSelReq q{};
+        q.pk_ok = q.pv_ok = -1;
+        if (has_wildcard(k) || has_wildcard(v)) {
+          q.op = SR_WILD;
+          q.pk = pred(D_LABK, {k});
+          q.pv = pred(D_LABV, {v});
+          q.pk_ok = special_pred(D_LABK, PRED_SPECIAL_QNAME);
+          q.pv_ok = special_pred(D_LABV, PRED_SPECIAL_LABVAL);
+        } else {
+          if (!qualified_name_ok(k) || !label_value_ok(v)) invalid = true;
+          q.op = SR_EQ;
+          q.pk = pred(D_LABK, {k});
+          q.pv = pred(D_LABV, {v});
+        }
+        reqs.push_back(q);
+      }
+    }
+    for (size_t i = 0; i < nme; ++i) {
+      const JV& e = me->a[i];
+      std::string key = sv(e.get("key")), op = sv(e.get("operator"));
+      auto vals = svl(e.get("values"));
+      KpeSelReq q{};
+      q.pk_ok = q.pv_ok = -1;
+      if (!qualified_name_ok(key)) invalid = true;
+      if (op == "In" || op == "NotIn") {
+        if (vals.empty()) invalid = true;
+        q.op = op == "In" ? SR_IN : SR_NOTIN;
+      } else if (op == "Exists" || op == "DoesNotExist") {
+        if (!vals.empty()) invalid = true;
+        q.op = op == "Exists" ? SR_EXISTS : SR_NOTEXIST;
+      } else {
+        invalid = true;
+      }
+      for (auto& v : vals)
+        if (!label_value_ok(v)) invalid = true;
+      if (invalid) break;
+      q.pk = pred(D_LABK, {key});
+      q.pv = vals.empty() ? -1 : pred(D_LABV, vals);  // valid values hold no '*'/'?': exact patterns
+      reqs.push_back(q);
+    }
+    if (invalid) {
+      // A label selector that never builds is constant false. A namespaceSelector
+      // is still skipped for an empty kind without "*" kinds (match.go:125-138).
+      if (!ns_sel) {
+        push({T_FALSE, 0, 0, 0});
+        return;
+      }
+      S.invalid = 1;
+      reqs.clear();
+    }
+    if (reqs.empty() && !ns_sel && !S.invalid) return;  // labels.Everything()
+    S.nreq = (uint32_t)reqs.size();
+    P.selreqs.insert(P.selreqs.end(), reqs.begin(), reqs.end());
+    P.selectors.push_back(S);
+    push({ns_sel ? T_NSSELECTOR : T_SELECTOR, (uint32_t)P.selectors.size() - 1, 0, 0});
+  }
+
   static bool has_ui(const JV* f) {
     if (!f) return false;
     for (const char* k : {"roles", "clusterRoles", "subjects"})

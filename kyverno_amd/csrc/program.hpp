@@ -13,7 +13,11 @@ namespace kpe {
 struct Pred {
   uint32_t domain;
   std::vector<std::string> globs;  // OR of go-wildcard patterns
+  uint32_t special = 0;            // PRED_SPECIAL_*: a validity test instead of globs
 };
+#define PRED_SPECIAL_NONE 0u
+#define PRED_SPECIAL_QNAME 1u   // validation.IsQualifiedName (label keys)
+#define PRED_SPECIAL_LABVAL 2u  // validation.IsValidLabelValue
 
 // Fixed predicate slots used by the PSS kernel (indices into Program::preds).
 struct PssPreds {
@@ -31,6 +35,8 @@ struct Program {
   std::vector<KpeTerm> terms;
   std::vector<KpeKindSel> kindsels;
   std::vector<KpeAnnPair> annpairs;
+  std::vector<KpeSelector> selectors;
+  std::vector<KpeSelReq> selreqs;
   std::vector<Pred> preds;
   PssPreds pss;
   uint32_t cv_union = 0;  // union of cv_mask over rules

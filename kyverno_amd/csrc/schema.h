@@ -256,6 +256,31 @@ typedef struct KpeKindSel {
 typedef struct KpeAnnPair {
   int32_t pk, pv;  // predicates over D_ANNK / D_ANNV
 } KpeAnnPair;
+// Label selector (CheckSelector, pkg/utils/match/labels.go:9-24, after
+// wildcards.ReplaceInSelector, pkg/engine/wildcards/wildcards.go:13-58): an AND of
+// requirements [req0, req0+nreq). Statically invalid selectors and selectors
+// that are always true are folded at compile time (T_FALSE / no term).
+typedef struct KpeSelector {
+  uint32_t req0, nreq;
+  int32_t p_kind_ns;     // namespaceSelector: D_KIND predicate "Namespace" (never applies)
+  int32_t p_kind_empty;  // namespaceSelector: D_KIND predicate "" (skipped unless kinds has "*")
+  uint32_t star_kind;    // namespaceSelector: the block's kinds contain "*"
+  uint32_t invalid;      // namespaceSelector that fails to build (false wherever it is evaluated)
+  uint32_t pad[2];
+} KpeSelector;
+#define SR_EQ 0u        // matchLabels k: v (no wildcards): first label with key k has value v
+#define SR_WILD 1u      // matchLabels with wildcards: first label matching both globs, and that
+                        // label is a valid key/value (else LabelSelectorAsSelector fails)
+#define SR_IN 2u        // matchExpressions In:     key present and value in set
+#define SR_NOTIN 3u     // matchExpressions NotIn:  key absent or value not in set
+#define SR_EXISTS 4u    // matchExpressions Exists
+#define SR_NOTEXIST 5u  // matchExpressions DoesNotExist
+typedef struct KpeSelReq {
+  uint32_t op;
+  int32_t pk, pv;       // predicates over D_LABK / D_LABV (pv unused for EXISTS / NOTEXIST)
+  int32_t pk_ok, pv_ok; // SR_WILD: validity predicates (qualified name / label value)
+  uint32_t pad[3];
+} KpeSelReq;
 typedef struct KpeFilter {
   uint32_t term0, nterms;
 } KpeFilter;

@@ -98,22 +98,51 @@ void emit_ctr(std::string& o, const Ctr& c) {
   o += "}}";
 }
 
+// C4 label sets: 8 distinct keys from a 64-key vocabulary (some prefixed), values
+// from small per-key vocabularies; ~1% carry a key or value that is not a valid
+// label (selector parse errors when a wildcard resolves to it).
+std::string label_key(int k) {
+  static const char* kPre[4] = {"", "app.kubernetes.io/", "example.com/", "team.io/"};
+  return std::string(kPre[k & 3]) + "k" + std::to_string(k);
+}
+std::string selector_labels(Rng& r) {
+  uint64_t used = 0;
+  std::string l = "{";
+  for (int i = 0; i < 8; ++i) {
+    int k;
+    do k = r.below(64);
+    while (used >> k & 1);
+    used |= 1ull << k;
+    std::string v = "v" + std::to_string(r.below(k < 8 ? 4 : 16));
+    std::string key = label_key(k);
+    if (r.p(0.005)) v = "bad value";
+    if (r.p(0.005)) key = "Bad_/key/x";
+    l += (i ? ",\"" : "\"") + key + "\":\"" + v + "\"";
+  }
+  return l + "}";
+}
+
 void gen_one(std::string& o, uint64_t seed, int64_t idx, int mix) {
   Rng r(seed ^ ((uint64_t)idx * 0xD1B54A32D192ED03ull));
   // ---- kind ----
   int kind = 0;  // 0 Pod, 1 Deployment, 2 DaemonSet, 3 Job, 4 CronJob, 5 Service, 6 ConfigMap, 7 StatefulSet
-  if (mix >= KPE_SYNTH_MIXED) {
+  const bool sel_mix = mix == KPE_SYNTH_SELECTORS;
+  if (sel_mix) {
+    kind = r.p(0.5) ? 1 : 5;
+  } else if (mix >= KPE_SYNTH_MIXED) {
     double u = r.u();
     kind = u < 0.40 ? 0 : u < 0.60 ? 1 : u < 0.64 ? 2 : u < 0.67 ? 3 : u < 0.70 ? 4 : u < 0.85 ? 5 : u < 0.97 ? 6 : 7;
   }
   bool edge = mix == KPE_SYNTH_EDGE;
   char nsbuf[16];
-  snprintf(nsbuf, sizeof nsbuf, "ns-%04d", r.below(1000));
+  if (sel_mix) snprintf(nsbuf, sizeof nsbuf, "ns-%05d", r.below(10000));
+  else snprintf(nsbuf, sizeof nsbuf, "ns-%04d", r.below(1000));
   std::string ns = nsbuf;
   std::string name = "res-" + std::to_string(idx);
   static const char* kKinds[] = {"Pod", "Deployment", "DaemonSet", "Job", "CronJob", "Service", "ConfigMap", "StatefulSet"};
   static const char* kApi[] = {"v1", "apps/v1", "apps/v1", "batch/v1", "batch/v1", "v1", "v1", "apps/v1"};
   auto labels = [&]() {
+    if (sel_mix) return selector_labels(r);
     std::string l = "{\"app\":\"app-" + std::to_string(r.below(200)) + "\",\"tier\":\"" +
                     (r.p(0.5) ? "frontend" : "backend") + "\"";
     if (r.p(0.3)) l += ",\"team\":\"team-" + std::to_string(r.below(20)) + "\"";
@@ -292,3 +321,28 @@ extern "C" int kpe_synth_resources(uint64_t seed, int64_t first, int64_t n, int 
 }
 
 extern "C" void kpe_synth_free(char* p) { free(p); }
+
+extern "C" int kpe_synth_ns_labels(uint64_t seed, int64_t n_namespaces, int mix, char** out, size_t* len) {
+  if (n_namespaces < 0 || !out || !len) return 1;
+  std::string s = "{";
+  static const char* kEnv[3] = {"prod", "staging", "dev"};
+  for (int64_t i = 0; i < n_namespaces; ++i) {
+    Rng r(seed ^ 0x5EEDull ^ ((uint64_t)i * 0xA24BAED4963EE407ull));
+    char nsbuf[16];
+    if (mix == KPE_SYNTH_SELECTORS) snprintf(nsbuf, sizeof nsbuf, "ns-%05d", (int)i);
+    else snprintf(nsbuf, sizeof nsbuf, "ns-%04d", (int)i);
+    if (i) s += ",";
+    s += "\"" + std::string(nsbuf) + "\":{\"kubernetes.io/metadata.name\":\"" + nsbuf + "\",\"env\":\"" +
+         kEnv[r.below(3)] + "\",\"team\":\"team-" + std::to_string(r.below(50)) + "\"";
+    if (r.p(0.5)) s += ",\"pss\":\"" + std::string(r.p(0.5) ? "restricted" : "baseline") + "\"";
+    if (r.p(0.1)) s += ",\"region\":\"r" + std::to_string(r.below(6)) + "\"";
+    s += "}";
+  }
+  s += "}";
+  char* buf = (char*)malloc(s.size() + 1);
+  if (!buf) return 2;
+  memcpy(buf, s.data(), s.size() + 1);
+  *out = buf;
+  *len = s.size();
+  return 0;
+}

@@ -146,7 +146,10 @@ class Corpus:
             raw = resources.encode()
         else:
             raw = "\n".join(json.dumps(r, separators=(",", ":")) for r in resources).encode()
-        nsl = json.dumps(namespace_labels).encode() if namespace_labels else b""
+        if isinstance(namespace_labels, (bytes, bytearray)):
+            nsl = bytes(namespace_labels)
+        else:
+            nsl = json.dumps(namespace_labels).encode() if namespace_labels else b""
         h = ctypes.c_void_p()
         check(L.kpe_corpus_flatten(raw, len(raw), nsl if nsl else None, len(nsl), ctypes.byref(h)))
         self.h = h
@@ -174,6 +177,19 @@ def synth_resources(seed: int, n: int, mix: int = 0, first_index: int = 0) -> by
     p = ctypes.c_void_p()
     ln = ctypes.c_size_t()
     if L.kpe_synth_resources(seed, first_index, n, mix, ctypes.byref(p), ctypes.byref(ln)) != 0:
+        raise KpeError(-1, "synth failed")
+    try:
+        return ctypes.string_at(p, ln.value)
+    finally:
+        L.kpe_synth_free(p)
+
+
+def synth_ns_labels(seed: int, n_namespaces: int, mix: int = 0) -> bytes:
+    """Namespace label table JSON from the synthetic generator (include/kpe_synth.h)."""
+    L = load()
+    p = ctypes.c_void_p()
+    ln = ctypes.c_size_t()
+    if L.kpe_synth_ns_labels(seed, n_namespaces, mix, ctypes.byref(p), ctypes.byref(ln)) != 0:
         raise KpeError(-1, "synth failed")
     try:
         return ctypes.string_at(p, ln.value)

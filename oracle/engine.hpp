@@ -172,7 +172,7 @@ inline bool is_dns1123_subdomain(const std::string& s) {
     size_t j = s.find('.', i);
     if (j == std::string::npos) j = s.size();
     std::string lab = s.substr(i, j - i);
-    if (lab.empty() || lab.size() > 63) return false;
+    if (lab.empty()) return false;  // dns1123SubdomainFmt has no per-label length limit
     for (size_t k = 0; k < lab.size(); ++k) {
       char c = lab[k];
       bool alnum = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9');
@@ -435,7 +435,12 @@ struct Policy {
 inline ResourceDescription parse_rd(const JVal* v) {
   ResourceDescription r;
   if (!v || v->t != JT::Obj) return r;
-  r.empty = !jnonempty(v);
+  // DeepEqual(rd, ResourceDescription{}): a present selector pointer is non-zero even for `{}`
+  auto sel_obj = [&](const char* k) {
+    const JVal* x = v->get(k);
+    return x && x->t == JT::Obj;
+  };
+  r.empty = !jnonempty(v) && !sel_obj("selector") && !sel_obj("namespaceSelector");
   r.kinds = jstrlist(v->get("kinds"));
   r.names = jstrlist(v->get("names"));
   r.namespaces = jstrlist(v->get("namespaces"));

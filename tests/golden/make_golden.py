@@ -14,6 +14,11 @@ outputs) lifted from the reference's tests:
                               `($error != null): true` => fail, otherwise pass)
   background_report.json   <- test/conformance/chainsaw/reports/background/test-report-background-mode
                               (restricted:latest policy, badpod01, expected report result)
+  check_selector.json      <- pkg/utils/match/labels_test.go (TestCheckSelector table:
+                              expected LabelSelector.MatchLabels, actual labels, want, wantErr)
+  match_rd_cases.json      <- pkg/engine/utils/utils_test.go:1828-2460, hand-transcribed below
+                              (Go struct literals): MatchesResourceDescription on the nginx
+                              Deployment with kinds/name/generateName/selector/exclude blocks
 
 Usage:  python tests/golden/make_golden.py [/root/reference]
 """
@@ -152,8 +157,76 @@ def background_report():
     return {"src": base, "policy": policy, "resource": pod, "results": rep["results"], "summary": rep["summary"]}
 
 
+def _go_string_map(body):
+    return {k: v for k, v in re.findall(r'"((?:[^"\\]|\\.)*)"\s*:\s*"((?:[^"\\]|\\.)*)"', body)}
+
+
+def check_selector():
+    rel = "pkg/utils/match/labels_test.go"
+    text = open(os.path.join(REF, rel)).read()
+    table = text[text.index("tests := []struct"):text.index("for _, tt := range tests")]
+    out = []
+    for i, case in enumerate(re.split(r"\n\t\}, \{", table)):
+        if "args: args{" not in case:
+            continue
+        line = text[:text.index(table)].count("\n") + table[:table.index(case)].count("\n") + 1
+        exp = re.search(r"expected: &metav1\.LabelSelector\{(.*?)\n\t\t\t\},?", case, re.S)
+        ml = re.search(r"MatchLabels: map\[string\]string\{(.*?)\}", exp.group(1), re.S) if exp else None
+        act = re.search(r"actual: +map\[string\]string\{(.*?)\}", case, re.S)
+        want = re.search(r"want: +(true|false)", case)
+        werr = re.search(r"wantErr: +(true|false)", case)
+        out.append({
+            "name": f"{rel}:{line}",
+            "selector": {"matchLabels": _go_string_map(ml.group(1))} if ml else {},
+            "actual": _go_string_map(act.group(1)) if act else {},
+            "want": bool(want and want.group(1) == "true"),
+            "wantErr": bool(werr and werr.group(1) == "true"),
+        })
+    return out
+
+
+def match_rd_cases():
+    rel = "pkg/engine/utils/utils_test.go"
+
+    def deploy(meta):
+        return {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": meta,
+                "spec": {"replicas": 3, "selector": {"matchLabels": {"app": "nginx"}},
+                         "template": {"metadata": {"labels": {"app": "nginx"}},
+                                      "spec": {"containers": [{"name": "nginx", "image": "nginx:1.7.9",
+                                                               "ports": [{"containerPort": 80}]}]}}}}
+
+    named = {"name": "nginx-deployment", "labels": {"app": "nginx"}}
+    gen = {"generateName": "nginx-deployment", "labels": {"app": "nginx"}}
+    empty_sel = {"matchLabels": None, "matchExpressions": None}
+    cases = [
+        (1828, named, {"kinds": ["Deployment", "Pods"], "selector": empty_sel}, None, True),
+        (2023, named, {"kinds": ["Deployment"], "name": "nginx-deployment", "selector": empty_sel}, None, True),
+        (2081, gen, {"kinds": ["Deployment"], "name": "nginx-deployment", "selector": empty_sel}, None, True),
+        (2140, named, {"kinds": ["Deployment"], "name": "nginx-*", "selector": empty_sel}, None, True),
+        (2198, gen, {"kinds": ["Deployment"], "name": "nginx-*", "selector": empty_sel}, None, True),
+        (2257, named, {"kinds": ["Deployment"], "name": "nginx-*", "selector": {
+            "matchLabels": None, "matchExpressions": [{"key": "label2", "operator": "NotIn", "values": ["sometest1"]}]}},
+         None, True),
+        (2324, named, {"kinds": ["Deployment"], "name": "nginx-*", "selector": {
+            "matchLabels": None,
+            "matchExpressions": [{"key": "app", "operator": "NotIn", "values": ["nginx1", "nginx2"]}]}}, None, True),
+        (2392, {"name": "nginx-deployment", "labels": {"app": "nginx", "block": "true"}},
+         {"kinds": ["Deployment"], "name": "nginx-*", "selector": {
+             "matchLabels": None,
+             "matchExpressions": [{"key": "app", "operator": "NotIn", "values": ["nginx1", "nginx2"]}]}},
+         {"selector": {"matchLabels": {"block": "true"}}}, False),
+    ]
+    out = []
+    for line, meta, match, exclude, matched in cases:
+        out.append({"name": f"{rel}:{line}", "resource": deploy(meta), "match": {"resources": match},
+                    "exclude": {"resources": exclude} if exclude else None, "matched": matched})
+    return out
+
+
 if __name__ == "__main__":
     _dump("pss_evaluate_cases.json", pss_cases())
     _dump("wildcard_match.json", wildcard_cases())
     _dump("chainsaw_psa.json", chainsaw_psa())
     _dump("background_report.json", background_report())
+    _dump("check_selector.json", check_selector())
+    _dump("match_rd_cases.json", match_rd_cases())

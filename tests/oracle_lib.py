@@ -53,7 +53,10 @@ class Oracle:
         N = ndjson.count(b"\n") + 1
         out = np.zeros(max(N * R, 1), dtype=np.uint8)
         pj = json.dumps(policies).encode()
-        nl = json.dumps(ns_labels).encode() if ns_labels else None
+        if isinstance(ns_labels, (bytes, bytearray)):
+            nl = bytes(ns_labels)
+        else:
+            nl = json.dumps(ns_labels).encode() if ns_labels else None
         n = self.lib.oracle_validate(pj, ndjson, len(ndjson), nl, out.ctypes.data, out.size, nthreads)
         if n < 0:
             raise RuntimeError(self.lib.oracle_last_error().decode())

@@ -57,4 +57,75 @@ def parity_policy_set():
     pols.append(p)
     p = pss_policy("ann", "restricted", "latest", extra_match={"annotations": {"owner": "team-1*"}})
     pols.append(p)
+    pols.append(pss_policy("sel", "baseline", "latest", kinds=("Pod", "Deployment"),
+                           extra_match={"selector": {"matchLabels": {"tier": "front*"},
+                                                     "matchExpressions": [{"key": "team", "operator": "Exists"}]}}))
+    pols.append(pss_policy("nssel", "baseline", "latest", kinds=("*",),
+                           extra_match={"namespaceSelector": {"matchExpressions": [
+                               {"key": "env", "operator": "NotIn", "values": ["prod"]}]}}))
     return pols
+
+
+def selector_policy(name, level="baseline", kinds=("Deployment",), selector=None, ns_selector=None, exclude=None,
+                    any_filters=None, all_filters=None):
+    """A podSecurity rule whose match block uses label selectors (C4 shape)."""
+    if any_filters is not None:
+        match = {"any": any_filters}
+    elif all_filters is not None:
+        match = {"all": all_filters}
+    else:
+        res = {"kinds": list(kinds)}
+        if selector is not None:
+            res["selector"] = selector
+        if ns_selector is not None:
+            res["namespaceSelector"] = ns_selector
+        match = {"any": [{"resources": res}]}
+    rule = {"name": name, "match": match, "validate": {"podSecurity": {"level": level, "version": "latest"}}}
+    if exclude is not None:
+        rule["exclude"] = exclude
+    return {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": f"sel-{name}"},
+            "spec": {"background": True, "validationFailureAction": "Audit", "rules": [rule]}}
+
+
+def c4_policy_set():
+    """C4: matchLabels incl. wildcard keys/values, matchExpressions
+    In/NotIn/Exists/DoesNotExist, namespaceSelector over the namespace label table,
+    selector excludes, invalid selectors, any/all blocks."""
+    P = selector_policy
+    return [
+        P("eq", selector={"matchLabels": {"k12": "v1"}}),
+        P("eq-prefixed", selector={"matchLabels": {"app.kubernetes.io/k13": "v3", "k16": "v0"}}),
+        P("wild-value", selector={"matchLabels": {"example.com/k14": "v1*"}}),
+        P("wild-key", selector={"matchLabels": {"team.io/*": "v?"}}),
+        P("wild-both", selector={"matchLabels": {"*": "*"}}),
+        P("wild-miss", selector={"matchLabels": {"nope/*": "*"}}),
+        P("in", selector={"matchExpressions": [{"key": "k20", "operator": "In", "values": ["v1", "v2", "v3"]}]}),
+        P("notin", selector={"matchExpressions": [{"key": "k24", "operator": "NotIn", "values": ["v0", "v5"]}]}),
+        P("exists", selector={"matchExpressions": [{"key": "example.com/k30", "operator": "Exists"}]}),
+        P("notexist", selector={"matchExpressions": [{"key": "k32", "operator": "DoesNotExist"}]}),
+        P("mixed", kinds=("Deployment", "Service"), selector={
+            "matchLabels": {"k36": "v*"},
+            "matchExpressions": [{"key": "app.kubernetes.io/k37", "operator": "NotIn", "values": ["v1"]},
+                                 {"key": "k40", "operator": "Exists"}]}),
+        P("empty-sel", selector={}),
+        P("bad-op", selector={"matchExpressions": [{"key": "k1", "operator": "Foo"}]}),
+        P("bad-in", selector={"matchExpressions": [{"key": "k1", "operator": "In", "values": []}]}),
+        P("bad-key", selector={"matchLabels": {"Bad_/key/x": "v1"}}),
+        P("ns-env", ns_selector={"matchLabels": {"env": "prod"}}),
+        P("ns-pss", level="restricted", ns_selector={"matchExpressions": [
+            {"key": "pss", "operator": "In", "values": ["restricted"]}]}),
+        P("ns-wild", kinds=("*",), ns_selector={"matchLabels": {"team": "team-1*"}}),
+        P("ns-notexist", kinds=("Service",), ns_selector={"matchExpressions": [
+            {"key": "region", "operator": "DoesNotExist"}]}),
+        P("ns-bad", ns_selector={"matchExpressions": [{"key": "env", "operator": "Exists", "values": ["x"]}]}),
+        P("sel-and-ns", selector={"matchLabels": {"k8": "v2"}}, ns_selector={"matchLabels": {"env": "dev"}}),
+        P("excl", selector={"matchLabels": {"k4": "*"}},
+          exclude={"any": [{"resources": {"selector": {"matchLabels": {"app.kubernetes.io/k5": "v1"}}}},
+                           {"resources": {"namespaceSelector": {"matchLabels": {"env": "staging"}}}}]}),
+        P("any-two", any_filters=[{"resources": {"kinds": ["Deployment"], "selector": {"matchLabels": {"example.com/k2": "v0"}}}},
+                                  {"resources": {"kinds": ["Deployment"],
+                                                 "namespaceSelector": {"matchLabels": {"team": "team-7"}}}}]),
+        P("all-two", all_filters=[{"resources": {"kinds": ["Deployment"], "selector": {"matchLabels": {"team.io/k3": "v*"}}}},
+                                  {"resources": {"namespaceSelector": {"matchExpressions": [
+                                      {"key": "env", "operator": "NotIn", "values": ["dev"]}]}}}]),
+    ]

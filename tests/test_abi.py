@@ -59,6 +59,23 @@ def test_compile_unsupported_is_loud():
     assert e.value.status == 2  # KPE_E_UNSUPPORTED
 
 
+def test_compile_selectors():
+    from tests.policies import c4_policy_set, selector_policy
+
+    ps = K.PolicySet(c4_policy_set())
+    assert ps.num_rules == len(c4_policy_set())  # selectors disable autogen
+    # two wildcard keys can resolve to one label key: Go map order decides => refused
+    with pytest.raises(KpeError) as e:
+        K.PolicySet([selector_policy("c", selector={"matchLabels": {"a*": "x", "ab": "y"}})])
+    assert e.value.status == 2
+    with pytest.raises(KpeError) as e:
+        K.PolicySet([selector_policy("c", selector={"matchLabels": {"a*": "x", "b*": "y"}})])
+    assert e.value.status == 2
+    with pytest.raises(KpeError) as e:  # malformed (not an object)
+        K.PolicySet([selector_policy("c", selector="app=x")])
+    assert e.value.status == 1
+
+
 def test_flatten_synth_counts():
     nd = K.synth_resources(1, 5000, mix=2)
     assert nd.count(b"\n") == 5000

@@ -110,3 +110,32 @@ def test_c2_scale_properties(engine, oracle):
     sub = b"\n".join(lines[i] for i in idx)
     ref = oracle.validate([restricted_latest()], sub, nthreads=8)
     assert np.array_equal(v[idx], ref)
+
+
+def test_selector_golden(engine):
+    """pkg/utils/match/labels_test.go and utils_test.go selector/name cases through the GPU."""
+    from tests.test_oracle_golden import MRD, SEL, match_rd_inputs, selector_case_inputs
+
+    for case in SEL:
+        pol, pod = selector_case_inputs(case)
+        v, _, _ = _gpu(engine, [pol], json.dumps(pod).encode())
+        assert (v[0, 0] != 0) == (case["want"] and not case["wantErr"]), case["name"]
+    for case in MRD:
+        pol, res = match_rd_inputs(case)
+        v, _, _ = _gpu(engine, [pol], json.dumps(res).encode())
+        assert (v[0, 0] != 0) == case["matched"], case["name"]
+
+
+@pytest.mark.parametrize("n,seed", [(20000, 0xC4), (50000, 41)])
+def test_c4_selectors_bit_exact(engine, oracle, n, seed):
+    from tests.policies import c4_policy_set
+
+    pols = c4_policy_set()
+    nd = K.synth_resources(seed, n, mix=3)
+    nsl = K.synth_ns_labels(seed, 10000, mix=3)
+    v, _, cnt = _gpu(engine, pols, nd, nsl)
+    ref = oracle.validate(pols, nd, ns_labels=nsl, nthreads=8)
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()}"
+    for r in range(v.shape[1]):
+        assert cnt[r]["pass"] == int((v[:, r] == 1).sum()) and cnt[r]["na"] == int((v[:, r] == 0).sum())

@@ -6,6 +6,8 @@ the reference's test sources (text only):
   * ext/wildcard/{match,utils}_test.go  -> wildcard_match.json (52 + 6 + 7)
   * chainsaw validate/.../standard/psa  -> chainsaw_psa.json (51 admissions)
   * chainsaw reports/background/test-report-background-mode -> background_report.json
+  * pkg/utils/match/labels_test.go      -> check_selector.json (12)
+  * pkg/engine/utils/utils_test.go:1828-2460 -> match_rd_cases.json (8, hand-transcribed)
 """
 import json
 import os
@@ -24,12 +26,52 @@ PSS = _load("pss_evaluate_cases.json")
 WILD = _load("wildcard_match.json")
 CHAINSAW = _load("chainsaw_psa.json")
 BG = _load("background_report.json")
+SEL = _load("check_selector.json")
+MRD = _load("match_rd_cases.json")
+
+COMPLIANT_POD_SPEC = {"containers": [{"name": "c", "image": "nginx"}]}
+
+
+def selector_case_inputs(case):
+    """CheckSelector vector -> (policy, pod): the pod carries `actual` as labels and the
+    rule matches Pods by the selector; matched <=> want && !wantErr."""
+    from tests.policies import selector_policy
+
+    pol = selector_policy("golden", kinds=("Pod",), selector=case["selector"])
+    pod = {"apiVersion": "v1", "kind": "Pod",
+           "metadata": {"name": "p", "namespace": "default", "labels": case["actual"]},
+           "spec": COMPLIANT_POD_SPEC}
+    return pol, pod
+
+
+def match_rd_inputs(case):
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "mrd"},
+           "spec": {"rules": [{"name": "r", "match": case["match"],
+                               "validate": {"podSecurity": {"level": "baseline", "version": "latest"}}}]}}
+    if case["exclude"]:
+        pol["spec"]["rules"][0]["exclude"] = case["exclude"]
+    return pol, case["resource"]
 
 
 def test_fixture_counts():
     assert len(PSS) == 227
     assert len(WILD["match"]) == 52
     assert len(CHAINSAW) == 51
+    assert len(SEL) == 12 and len(MRD) == 8
+
+
+@pytest.mark.parametrize("case", SEL, ids=[c["name"] for c in SEL])
+def test_check_selector_golden(oracle, case):
+    pol, pod = selector_case_inputs(case)
+    v = oracle.validate([pol], json.dumps(pod).encode())
+    assert (v[0, 0] != 0) == (case["want"] and not case["wantErr"])
+
+
+@pytest.mark.parametrize("case", MRD, ids=[c["name"] for c in MRD])
+def test_match_resource_description_golden(oracle, case):
+    pol, res = match_rd_inputs(case)
+    v = oracle.validate([pol], json.dumps(res).encode())
+    assert (v[0, 0] != 0) == case["matched"]
 
 
 @pytest.mark.parametrize("case", PSS, ids=[c["name"] for c in PSS])
