@@ -169,7 +169,8 @@ namespace {
 
 constexpr uint32_t kBlock = 256;
 constexpr uint32_t kChunk = 1024;   // containers staged per LDS pass
-constexpr uint32_t kStageV = 8192;  // verdict staging bytes (R <= 32)
+constexpr uint32_t kStageCols = 32;                // verdict columns staged per pass
+constexpr uint32_t kStageV = kBlock * kStageCols;  // verdict staging bytes
 constexpr uint32_t kListChunk = 1024;  // volumes / sysctls / pod annotations staged per LDS pass
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
@@ -258,45 +259,68 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
   return x;
 }
 
-// STAGED: the program image is part of the LDS preamble; otherwise rules/filters/terms
-// are read from their global copies.
+// Wave-uniform table read: the address is uniform, so this is a scalar (SMEM) load
+// through the constant cache — no LDS round trip and no readfirstlane to branch on it.
+template <class T>
+__device__ __forceinline__ T sld(const T* p, uint32_t i) {
+  static_assert(sizeof(T) % 4 == 0, "word-sized tables");
+  typedef __attribute__((address_space(4))) const uint32_t* cptr;
+  const cptr src = (cptr)(p + i);
+  T out;
+  uint32_t* d = reinterpret_cast<uint32_t*>(&out);
+#pragma unroll
+  for (uint32_t k = 0; k < sizeof(T) / 4; ++k) d[k] = src[k];
+  return out;
+}
+__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// One resource per lane; rules are evaluated bit-sliced per wave.
 //
-// One resource per lane, two global round trips per wave:
-//  1  pod record (dwordx4), wave header, the preamble (program image, predicate
-//     directory, small-domain bitsets: one dwordx4 per thread) and the
-//     capability-set table — all issued before the first wait;
-//  2  the lane's list items at (header + exclusive wave scan of the counts):
-//     up to 4 containers, 2 volumes, 2 annotations and 1 sysctl are loaded before
-//     any is used (longer lists continue in a loop).
-template <bool STAGED>
+//  round 1  pod record (dwordx4) + wave header (PSS programs) or the gvk / namespace
+//           columns, the name columns the terms read, the LDS preamble (predicate
+//           directory + small-domain bitsets) and the capability-set table: every
+//           load is issued before the first wait;
+//  round 2  (PSS) the lane's list items at header + exclusive wave scan of the
+//           counts: up to 4 containers, 2 volumes, 2 annotations, 1 sysctl, issued
+//           together; the PSA versioned checks give a per-lane failure bitmask;
+//  terms    each DISTINCT match term of the program is evaluated once per resource
+//           and ballot-ed into a 64-bit wave mask (LDS, per wave);
+//  rules    wave-uniform loop on the scalar unit: match/exclude blocks are AND/OR of
+//           term masks (pkg/engine/utils/match.go:168-300), ApplyOne
+//           (pkg/engine/validation.go:75-77) is a mask, the PSS handler's pass /
+//           fail / error cells are masks, per-rule counts are popcounts. Each lane
+//           only extracts its verdict byte.
+template <bool PSS>
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // preamble copy
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // [preamble copy][term masks]
   __shared__ __attribute__((aligned(16))) uint8_t s_capb[KPE_MAX_CAPSETS];
   __shared__ __attribute__((aligned(16))) uint32_t s_cnt[6 * KPE_SMALL_R];
   __shared__ __attribute__((aligned(16))) uint8_t s_v[kStageV];
 
   const int64_t p0 = (int64_t)blockIdx.x * kBlock;
   const uint32_t t = threadIdx.x;
+  const uint32_t lane = t & 63u, wv = t >> 6;
   const int64_t r = p0 + t;
   const bool live = r < a.n;
   const uint32_t np = (uint32_t)((a.n - p0) < (int64_t)kBlock ? (a.n - p0) : (int64_t)kBlock);
   const uint32_t R = a.nrules;
   const bool small_r = R <= KPE_SMALL_R;
-  const bool stage_v = R * kBlock <= kStageV;
   const uint32_t need = a.need;
-  const bool pss = a.any_pss;
-  const bool need_caps = pss && (need & NEED_CAPS);
+  const bool need_caps = PSS && (need & NEED_CAPS);
 
   // ---- round 1: every load issued before the first use ----
   // Loads are unconditional at clamped (always valid) addresses and the value is
-  // selected afterwards, so no exec-mask branch splits the issue sequence.
+  // selected after the barrier, so no exec-mask branch splits the issue sequence.
   const uint4 z4 = make_uint4(0, 0, 0, 0);
   const int64_t rc = live ? r : a.n - 1;
   const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)(r >> 6));
-  const uint32_t wave_c = __builtin_amdgcn_readfirstlane((uint32_t)(rc >> 6));
   uint4 rec_raw = z4, hdr_raw = z4;
-  uint32_t gvk_raw = 0, nsa_raw = KPE_NO_STR;
-  if (pss) {
+  uint32_t gvk_raw = 0, nsa_raw = KPE_NO_STR, name_raw = KPE_NO_STR, mns_raw = KPE_NO_STR;
+  if (PSS) {
     rec_raw = reinterpret_cast<const uint4*>(a.rec)[rc];
     // vector load of the wave header: a scalar load here would be waited on
     // before the preamble loads issue
@@ -307,6 +331,8 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     if (need & NEED_GVK) gvk_raw = a.r_gvk[rc];
     if (need & NEED_NSA) nsa_raw = a.r_nsa[rc];
   }
+  if (need & NEED_NAME) name_raw = a.r_name[rc];
+  if (need & NEED_MNS) mns_raw = a.r_mns[rc];
   const uint32_t nb4 = a.blob_words >> 2;  // >= 1
   const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
   const uint4 b0 = blob[t < nb4 ? t : nb4 - 1];
@@ -327,10 +353,10 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   const uint4 rec = live ? rec_raw : z4;
   const uint4 hdr = (int64_t)wave * 64 < a.n ? hdr_raw : z4;
   const uint32_t gvk_col = live ? gvk_raw : 0u, nsa_col = live ? nsa_raw : KPE_NO_STR;
-  const uint32_t* dir = dyn + a.img_words;
+  const uint32_t name_col = live ? name_raw : KPE_NO_STR, mns_col = live ? mns_raw : KPE_NO_STR;
   const uint32_t* pbuf = a.pbuf;
   auto pword = [&](int32_t p, uint32_t wi) -> uint32_t {  // word wi of predicate p's bitset
-    const uint32_t w = dir[p];
+    const uint32_t w = sld(pbuf, (uint32_t)p);            // directory entry (uniform)
     return (w & PRED_LOCAL) ? dyn[(w & ~PRED_LOCAL) + wi] : pbuf[w + wi];
   };
   auto pbit = [&](int32_t p, uint32_t id) -> bool {
@@ -343,7 +369,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
   };
 
   uint32_t fails = 0;
-  if (pss) {
+  if (PSS) {
     if (need_caps) {
       const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
       auto capbits = [&](uint4 c) -> uint8_t {
@@ -448,177 +474,195 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
     if (live) fails = cv_fails(rec.x, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
   }
 
-  // ---- rules: match/exclude, handler, ApplyOne, verdict cell ----
-  const KpeRule* rules = STAGED ? reinterpret_cast<const KpeRule*>(dyn + a.off_rules) : a.rules;
-  const KpeFilter* filters = STAGED ? reinterpret_cast<const KpeFilter*>(dyn + a.off_filters) : a.filters;
-  const KpeTerm* terms = STAGED ? reinterpret_cast<const KpeTerm*>(dyn + a.off_terms) : a.terms;
-  const KpeKindSel* kindsels = STAGED ? reinterpret_cast<const KpeKindSel*>(dyn + a.off_kindsels) : a.kindsels;
-  const KpeAnnPair* annpairs = STAGED ? reinterpret_cast<const KpeAnnPair*>(dyn + a.off_annpairs) : a.annpairs;
-  const KpeSelector* selectors = STAGED ? reinterpret_cast<const KpeSelector*>(dyn + a.off_selectors) : a.selectors;
-  const KpeSelReq* selreqs = STAGED ? reinterpret_cast<const KpeSelReq*>(dyn + a.off_selreqs) : a.selreqs;
-  const uint32_t gvk = pss ? rec.y : gvk_col;
-  const uint32_t nsa = pss ? rec.w : nsa_col;
+
+  // ---- terms: one ballot per distinct term per wave ----
+  const uint32_t gvk = PSS ? rec.y : gvk_col;
+  const uint32_t nsa = PSS ? rec.w : nsa_col;
+  uint64_t* tmask = reinterpret_cast<uint64_t*>(dyn + a.tm_lds) + (size_t)wv * a.nterms;
+#pragma unroll 1
+  for (uint32_t ti = 0; ti < a.nterms; ++ti) {
+    const KpeTerm tm = sld(a.terms, ti);
+    bool ok = true;
+    if (tm.type == T_KIND_PRED) {
+      ok = pbit((int32_t)tm.a, GVK_KIND(gvk));
+    } else if (tm.type == T_KINDS) {  // CheckKind: OR over kind selectors
+      ok = false;
+#pragma unroll 1
+      for (uint32_t k = 0; k < tm.b; ++k) {
+        const KpeKindSel ks = sld(a.kindsels, tm.a + k);
+        ok |= ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) &&
+              (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
+      }
+    } else if (tm.type == T_PRED) {
+      const uint32_t id = tm.b == COL_NAME ? name_col : (tm.b == COL_MNS ? mns_col : nsa);
+      ok = pbit((int32_t)tm.a, id);
+    } else if (tm.type == T_ANNOTATIONS) {  // CheckAnnotations: every pair matched by some annotation
+      const uint32_t lo = a.ann_off[rc], hi = live ? a.ann_off[rc + 1] : lo;
+#pragma unroll 1
+      for (uint32_t k = 0; k < tm.b; ++k) {
+        const KpeAnnPair pr = sld(a.annpairs, tm.a + k);
+        bool hit = false;
+#pragma unroll 1
+        for (uint32_t j = lo; j < hi && !hit; ++j) hit = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
+        ok &= hit;
+      }
+    } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
+      // CheckSelector (pkg/utils/match/labels.go:9-24) over the resource's labels or,
+      // for namespaceSelector, its namespace's labels (utils/match.go:114-138)
+      const KpeSelector S = sld(a.selectors, tm.a);
+      uint32_t lo = 0, hi = 0;
+      const uint32_t *K = a.lab_k, *V = a.lab_v;
+      bool eval = true;
+      if (tm.type == T_SELECTOR) {
+        lo = a.lab_off[rc];
+        hi = live ? a.lab_off[rc + 1] : lo;
+      } else {
+        // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
+        const uint32_t kid = GVK_KIND(gvk);
+        const uint32_t row = a.r_nsl[rc];
+        if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
+        K = a.nsl_k, V = a.nsl_v;
+        if (pbit(S.p_kind_ns, kid)) {
+          ok = false, eval = false;
+        } else if (pbit(S.p_kind_empty, kid) && !S.star_kind) {
+          ok = true, eval = false;
+        } else if (S.invalid) {
+          ok = false, eval = false;
+        }
+      }
+      if (eval) {
+#pragma unroll 1
+        for (uint32_t qi = 0; qi < S.nreq; ++qi) {
+          const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
+          const bool wild = q.op == SR_WILD;
+          uint32_t j = lo;
+#pragma unroll 1
+          for (; j < hi; ++j)  // first label with a matching key (and value, for wildcards)
+            if (pbit(q.pk, K[j]) && (!wild || pbit(q.pv, V[j]))) break;
+          const bool found = j < hi;
+          const uint32_t kid = found ? K[j] : KPE_NO_STR, vid = found ? V[j] : KPE_NO_STR;
+          bool qok;
+          switch (q.op) {
+            case SR_EQ:
+            case SR_IN: qok = found && pbit(q.pv, vid); break;
+            case SR_WILD: qok = found && pbit(q.pk_ok, kid) && pbit(q.pv_ok, vid); break;
+            case SR_NOTIN: qok = !found || !pbit(q.pv, vid); break;
+            case SR_EXISTS: qok = found; break;
+            default: qok = !found; break;
+          }
+          ok &= qok;
+        }
+      }
+    } else {  // T_FALSE
+      ok = false;
+    }
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) tmask[ti] = m;
+  }
+  auto term_mask = [&](uint32_t ti) -> uint64_t { return uniform64(tmask[ti]); };
+  // match / exclude block: any => OR of filters, all => AND, legacy => its one filter;
+  // a filter is the AND of its terms
+  auto block_mask = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> uint64_t {
+    const bool all = mode == MODE_ALL;
+    uint64_t acc = all ? ~0ull : 0ull;
+#pragma unroll 1
+    for (uint32_t f = 0; f < nf; ++f) {
+      const KpeFilter fl = sld(a.filters, f0 + f);
+      uint64_t fm = ~0ull;
+#pragma unroll 1
+      for (uint32_t k = 0; k < fl.nt && fm; ++k) fm &= term_mask(sld(a.fterms, fl.t0 + k));
+      acc = all ? (acc & fm) : (acc | fm);
+    }
+    return acc;
+  };
+
+  // ---- rules (wave-uniform) ----
   const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
   const bool pss_err = cls == R_CLASS_OTHER || (rec.x & PR_DECODE_ERR);
-  bool applied = false;
+  const uint64_t live_m = __ballot(live);
+  const uint64_t err_m = PSS ? __ballot(pss_err) : 0ull;
+  const uint32_t cw = R < kStageCols ? R : kStageCols;  // verdict columns staged per pass
+  uint64_t applied = 0;
   uint32_t cur_policy = 0xFFFFFFFFu;
-  const uint32_t lane = t & 63u;
 #pragma unroll 1
   for (uint32_t ri = 0; ri < R; ++ri) {
-    const KpeRule rule = rules[ri];
+    const KpeRule rule = sld(a.rules, ri);
     if (rule.policy != cur_policy) {
       cur_policy = rule.policy;
-      applied = false;
+      applied = 0;
     }
-    uint32_t v = KPE_NA_;
-    uint32_t cmask = 0;
-    if (live && !(rule.apply_one && applied)) {
-      bool m = rule.pol_ns_pred < 0 || pbit(rule.pol_ns_pred, nsa);
-      // phase 0 = match block, phase 1 = exclude block; one filter evaluation site
+    uint64_t m = live_m;
+    if (rule.pol_term >= 0) m &= term_mask((uint32_t)rule.pol_term);
+    if (m) m &= block_mask(rule.match_mode, rule.match_f0, rule.match_nf);
+    if (m) m &= ~block_mask(rule.excl_mode, rule.excl_f0, rule.excl_nf);
+    if (rule.apply_one) m &= ~applied;
+    uint64_t pm = 0, fm = 0, em = 0;
+    if (rule.handler == H_PSS) {
+      em = m & err_m;
+      fm = m & ~em & __ballot((fails & rule.cv_mask) != 0u);
+      pm = m & ~em & ~fm;
+    } else if (rule.handler == H_ERROR) {
+      em = m;
+    }
+    applied |= pm | fm;
+    const uint32_t v = ((pm >> lane) & 1u) ? KPE_PASS_ : ((fm >> lane) & 1u) ? KPE_FAIL_
+                                                          : ((em >> lane) & 1u) ? KPE_ERROR_ : KPE_NA_;
+    if (a.masks && live) {
+      uint32_t cmask = 0;
+      if ((fm >> lane) & 1u) {
+        const uint32_t f = fails & rule.cv_mask;
 #pragma unroll 1
-      for (uint32_t phase = 0; phase < 2 && m; ++phase) {
-        const uint32_t mode = phase ? rule.excl_mode : rule.match_mode;
-        const uint32_t f0 = phase ? rule.excl_f0 : rule.match_f0;
-        const uint32_t nf = mode == MODE_LEGACY ? 1u : (phase ? rule.excl_nf : rule.match_nf);
-        const bool all_mode = mode == MODE_ALL;
-        bool acc = all_mode;
-#pragma unroll 1
-        for (uint32_t f = 0; f < nf; ++f) {
-          const KpeFilter fl = filters[f0 + f];
-          bool ok = true;
-#pragma unroll 1
-          for (uint32_t ti = 0; ti < fl.nterms && ok; ++ti) {
-            const KpeTerm tm = terms[fl.term0 + ti];
-            if (tm.type == T_KIND_PRED) {
-              ok = pbit((int32_t)tm.a, GVK_KIND(gvk));
-            } else if (tm.type == T_KINDS) {
-              ok = false;
-#pragma unroll 1
-              for (uint32_t s = 0; s < tm.b && !ok; ++s) {
-                const KpeKindSel ks = kindsels[tm.a + s];
-                ok = ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) &&
-                     (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) && (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
-              }
-            } else if (tm.type == T_PRED) {
-              const uint32_t id = tm.b == COL_NAME ? a.r_name[r] : (tm.b == COL_MNS ? a.r_mns[r] : nsa);
-              ok = pbit((int32_t)tm.a, id);
-            } else if (tm.type == T_ANNOTATIONS) {
-              const uint32_t lo = a.ann_off[r], hi = a.ann_off[r + 1];
-#pragma unroll 1
-              for (uint32_t pi = 0; pi < tm.b && ok; ++pi) {
-                const KpeAnnPair pr = annpairs[tm.a + pi];
-                bool hit = false;
-#pragma unroll 1
-                for (uint32_t j = lo; j < hi && !hit; ++j) hit = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
-                ok = hit;
-              }
-            } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
-              const KpeSelector S = selectors[tm.a];
-              uint32_t lo = 0, hi = 0;
-              const uint32_t *K, *V;
-              bool eval = true;
-              if (tm.type == T_SELECTOR) {
-                lo = a.lab_off[r], hi = a.lab_off[r + 1];
-                K = a.lab_k, V = a.lab_v;
-              } else {
-                // namespaceSelector: never for kind Namespace; skipped for an empty kind
-                // unless the block's kinds hold "*" (pkg/engine/utils/match.go:125-138)
-                const uint32_t kid = GVK_KIND(gvk);
-                const uint32_t row = a.r_nsl[r];
-                if (row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
-                K = a.nsl_k, V = a.nsl_v;
-                if (pbit(S.p_kind_ns, kid)) {
-                  ok = false, eval = false;
-                } else if (pbit(S.p_kind_empty, kid) && !S.star_kind) {
-                  ok = true, eval = false;
-                } else if (S.invalid) {
-                  ok = false, eval = false;
-                }
-              }
-              if (eval) {
-                ok = true;
-#pragma unroll 1
-                for (uint32_t qi = 0; qi < S.nreq && ok; ++qi) {
-                  const KpeSelReq q = selreqs[S.req0 + qi];
-                  const bool wild = q.op == SR_WILD;
-                  uint32_t j = lo;
-#pragma unroll 1
-                  for (; j < hi; ++j)
-                    if (pbit(q.pk, K[j]) && (!wild || pbit(q.pv, V[j]))) break;
-                  const bool found = j < hi;
-                  const uint32_t vid = found ? V[j] : KPE_NO_STR;
-                  switch (q.op) {
-                    case SR_EQ:
-                    case SR_IN: ok = found && pbit(q.pv, vid); break;
-                    case SR_WILD: ok = found && pbit(q.pk_ok, K[j]) && pbit(q.pv_ok, vid); break;
-                    case SR_NOTIN: ok = !found || !pbit(q.pv, vid); break;
-                    case SR_EXISTS: ok = found; break;
-                    default: ok = !found; break;
-                  }
-                }
-              }
-            } else {
-              ok = false;
-            }
-          }
-          if (all_mode) {
-            acc = acc && ok;
-            if (!acc) break;
-          } else {
-            acc = acc || ok;
-            if (acc) break;
-          }
-        }
-        m = phase ? !acc : acc;
+        for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
+          if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
       }
-      if (m) {
-        if (rule.handler == H_PSS) {
-          if (pss_err) {
-            v = KPE_ERROR_;
-          } else {
-            const uint32_t f = fails & rule.cv_mask;
-            v = f ? KPE_FAIL_ : KPE_PASS_;
-            if (a.masks) {
+      a.masks[r * R + ri] = cmask;
+    }
+    // counters: popcounts of the cell masks, one LDS/global atomic per wave and status
+    if (lane == 0) {
+      const uint32_t cp = (uint32_t)__popcll(pm), cf = (uint32_t)__popcll(fm), ce = (uint32_t)__popcll(em);
+      if (small_r) {
+        if (cp) atomicAdd(&s_cnt[ri * 6 + KPE_PASS_], cp);
+        if (cf) atomicAdd(&s_cnt[ri * 6 + KPE_FAIL_], cf);
+        if (ce) atomicAdd(&s_cnt[ri * 6 + KPE_ERROR_], ce);
+      } else {
+        if (cp) atomicAdd(&a.counts_global[ri * 6 + KPE_PASS_], (unsigned long long)cp);
+        if (cf) atomicAdd(&a.counts_global[ri * 6 + KPE_FAIL_], (unsigned long long)cf);
+        if (ce) atomicAdd(&a.counts_global[ri * 6 + KPE_ERROR_], (unsigned long long)ce);
+      }
+    }
+    // verdict bytes: staged per block in column chunks of <= kStageCols, then stored
+    // as contiguous row segments
+    const uint32_t c0 = ri - ri % kStageCols;
+    s_v[t * cw + (ri - c0)] = (uint8_t)v;
+    const bool chunk_end = ri + 1 == R || ri + 1 - c0 == kStageCols;
+    if (chunk_end) {
+      __syncthreads();
+      const uint32_t w = ri + 1 - c0;  // columns in this chunk
+      if (w == R && (R & 3u) == 0u) {
+        // whole rows, 4-byte aligned: coalesced dword copy of the block's np x R bytes
+        uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(s_v);
 #pragma unroll 1
-              for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
-                if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
-            }
-          }
-        } else if (rule.handler == H_ERROR) {
-          v = KPE_ERROR_;
+        for (uint32_t i = t; i < np * R / 4; i += kBlock) dst[i] = src[i];
+      } else if (w == R) {
+        uint8_t* dst = a.verdicts + (size_t)p0 * R;
+#pragma unroll 1
+        for (uint32_t i = t; i < np * R; i += kBlock) dst[i] = s_v[i];
+      } else {
+#pragma unroll 1
+        for (uint32_t i = t; i < np * w; i += kBlock) {
+          const uint32_t row = i / w, col = i - row * w;
+          a.verdicts[(size_t)(p0 + row) * R + c0 + col] = s_v[row * cw + col];
         }
       }
-      if (v == KPE_PASS_ || v == KPE_FAIL_) applied = true;
+      __syncthreads();
     }
-    if (stage_v) s_v[t * R + ri] = (uint8_t)v;
-    else if (live) a.verdicts[r * R + ri] = (uint8_t)v;
-    if (live && a.masks) a.masks[r * R + ri] = cmask;
-    if (small_r) {
-      if (__ballot(v != KPE_NA_)) {  // wave-uniform skip of all-NA columns
-        for (uint32_t k = 1; k < 6; ++k) {
-          const uint64_t b = __ballot(v == k);
-          if (lane == 0 && b) atomicAdd(&s_cnt[ri * 6 + k], (uint32_t)__popcll(b));
-        }
-      }
-    } else if (live && v != KPE_NA_) {
-      atomicAdd(&a.counts_global[ri * 6 + v], 1ull);
-    }
-  }
-
-  // ---- coalesced verdict store + counter partials ----
-  __syncthreads();
-  if (stage_v) {
-    const uint32_t bytes = np * R;
-    uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);  // p0*R is a multiple of 4
-    const uint32_t* src = reinterpret_cast<const uint32_t*>(s_v);
-#pragma unroll 1
-    for (uint32_t w = t; w < bytes / 4; w += kBlock) dst[w] = src[w];
-    if (t < (bytes & 3u)) a.verdicts[(size_t)p0 * R + (bytes & ~3u) + t] = s_v[(bytes & ~3u) + t];
   }
   if (small_r)
 #pragma unroll 1
     for (uint32_t i = t; i < 6 * R; i += kBlock) a.counts_part[(size_t)blockIdx.x * 6 * R + i] = s_cnt[i];
 }
+
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers (called from kpe_api.cpp).
@@ -628,10 +672,13 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipSt
   return hipGetLastError();
 }
 extern "C" uint32_t kpe_scan_blocks(int64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s) {
+extern "C" size_t kpe_scan_lds_bytes(uint32_t blob_words, uint32_t nterms) {
+  return (size_t)(((blob_words + 1u) & ~1u) + 2u * (kBlock / 64u) * nterms) * 4u;
+}
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, hipStream_t s) {
   if (a->n == 0) return hipSuccess;
-  const size_t dyn = (size_t)a->blob_words * 4;
-  if (a->img_words)
+  const size_t dyn = kpe_scan_lds_bytes(a->blob_words, a->nterms);
+  if (pss)
     hipLaunchKernelGGL(kpe_scan_kernel<true>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
   else
     hipLaunchKernelGGL(kpe_scan_kernel<false>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);

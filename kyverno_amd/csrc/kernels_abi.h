@@ -18,6 +18,8 @@
 #define NEED_NSA (1u << 7)
 #define NEED_LAB (1u << 8)   // resource labels (CSR) for label selectors
 #define NEED_NSL (1u << 9)   // namespace label table for namespaceSelector
+#define NEED_NAME (1u << 10) // r_name (name / names terms)
+#define NEED_MNS (1u << 11)  // r_mns (namespaces terms)
 
 // Pattern classes (host-classified go-wildcard patterns; '?' or an inner '*' => PK_GLOB)
 #define PK_ANY 0u       // "*"
@@ -68,24 +70,25 @@ struct ScanArgs {
   const uint32_t* capsets;    // capability-set dictionary: 4 words (add lo/hi, drop lo/hi) per set
   uint32_t ncapsets;
   uint32_t nctr_total, nvol_total, nsys_total, npann_total;  // list lengths (load clamping)
-  // program (global copies, used when the image does not fit LDS)
+  // program tables (wave-uniform: read with scalar loads)
   const KpeRule* rules;
-  uint32_t nrules;
   const KpeFilter* filters;
+  const uint32_t* fterms;
   const KpeTerm* terms;
   const KpeKindSel* kindsels;
   const KpeAnnPair* annpairs;
   const KpeSelector* selectors;
   const KpeSelReq* selreqs;
-  // preamble: pbuf[0, blob_words) = [program image (img_words)][predicate directory (npreds)]
-  // [small-domain bitsets], copied into LDS by every block; pbuf[blob_words, ...) = large-domain
-  // bitsets. Directory entry: PRED_LOCAL | LDS word index, or absolute pbuf word index.
+  uint32_t nrules, nterms;
+  // predicate bitsets: pbuf[0, npreds) = directory (PRED_LOCAL | LDS word index, or pbuf
+  // word index); pbuf[npreds, blob_words) = small-domain bitsets, copied into LDS by every
+  // block (same word indices); the rest = large-domain bitsets read from HBM/L2.
   const uint32_t* pbuf;
-  uint32_t blob_words, img_words, npreds;
-  uint32_t off_rules, off_filters, off_terms, off_kindsels, off_annpairs, off_selectors, off_selreqs;
+  uint32_t blob_words, npreds;
+  uint32_t tm_lds;  // LDS word offset of the per-wave term-mask table (nterms x u64 per wave)
   int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
-  uint32_t cv_union, any_pss, need;
+  uint32_t cv_union, need;
   // outputs
   uint8_t* verdicts;                 // n x nrules
   uint32_t* masks;                   // n x nrules or null

@@ -24,7 +24,9 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, hipStream_t s);
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, hipStream_t s);
+extern "C" size_t kpe_scan_lds_bytes(uint32_t blob_words, uint32_t nterms);
+static inline uint32_t kpe_scan_block_threads() { return 256; }
 extern "C" uint32_t kpe_scan_blocks(int64_t n);
 extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
                                               unsigned long long* out, hipStream_t s);
@@ -75,8 +77,9 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 }
 
 // LDS budgets of the scan kernel's dynamic region
-constexpr uint32_t kMaxProgWords = 4096;   // 16 KiB program image
 constexpr uint32_t kMaxLocalWords = 8192;  // 32 KiB of small-domain predicate bitsets
+constexpr uint32_t kMaxDynWords = 13312;   // dynamic LDS per scan block (52 KiB)
+constexpr uint32_t kMaxTerms = 1024;       // distinct match terms (term masks: 8 B x 4 waves each)
 constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
 
 }  // namespace
@@ -109,12 +112,10 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
-  DevBuf rules, filters, terms, kindsels, annpairs, selectors, selreqs, pat_bytes, pats, image;
+  DevBuf rules, filters, fterms, terms, kindsels, annpairs, selectors, selreqs, pat_bytes, pats;
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
-  uint32_t image_words = 0, off_rules = 0, off_filters = 0, off_terms = 0, off_kindsels = 0, off_annpairs = 0;
-  uint32_t off_selectors = 0, off_selreqs = 0;
 };
 
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
@@ -334,17 +335,9 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
       D.pats_h.push_back({PK_LABVAL, 0, 0, 0});
     for (auto& g : pr.globs) D.pats_h.push_back(classify_pattern(g, D.pat_bytes_h));
   }
-  std::vector<uint32_t> img;
-  append_words(img, P.rules, &D.off_rules);
-  append_words(img, P.filters, &D.off_filters);
-  append_words(img, P.terms, &D.off_terms);
-  append_words(img, P.kindsels, &D.off_kindsels);
-  append_words(img, P.annpairs, &D.off_annpairs);
-  append_words(img, P.selectors, &D.off_selectors);
-  append_words(img, P.selreqs, &D.off_selreqs);
-  D.image_words = img.size() <= kMaxProgWords ? (uint32_t)img.size() : 0;
   HIPCHK(upload(D.rules, P.rules, s));
   HIPCHK(upload(D.filters, P.filters, s));
+  HIPCHK(upload(D.fterms, P.fterms, s));
   HIPCHK(upload(D.terms, P.terms, s));
   HIPCHK(upload(D.kindsels, P.kindsels, s));
   HIPCHK(upload(D.annpairs, P.annpairs, s));
@@ -352,7 +345,6 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   HIPCHK(upload(D.selreqs, P.selreqs, s));
   HIPCHK(upload(D.pat_bytes, D.pat_bytes_h, s));
   HIPCHK(upload(D.pats, D.pats_h, s));
-  HIPCHK(upload(D.image, img, s));
   HIPCHK(hipStreamSynchronize(s));
   return KPE_OK;
 }
@@ -372,14 +364,14 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   for (auto& r : P.rules)
     if (r.handler != H_NONE && r.handler != H_PSS) need |= NEED_FLAGS;
-  for (auto& t : P.terms)
+  for (auto& t : P.terms) {
     if (t.type == T_KINDS || t.type == T_KIND_PRED || t.type == T_NSSELECTOR) need |= NEED_GVK;
+    if (t.type == T_PRED) need |= t.b == COL_NAME ? NEED_NAME : t.b == COL_MNS ? NEED_MNS : NEED_NSA;
+  }
   for (auto& t : P.terms) {
     if (t.type == T_SELECTOR) need |= NEED_LAB;
     if (t.type == T_NSSELECTOR) need |= NEED_NSL;
   }
-  for (auto& r : P.rules)
-    if (r.pol_ns_pred >= 0) need |= NEED_NSA;
   return need;
 }
 double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
@@ -397,11 +389,8 @@ double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bo
     if (need & NEED_GVK) b += 4 * n;
     if (need & NEED_NSA) b += 4 * n;
   }
-  for (auto& t : P.terms)  // name / namespace columns read by predicate terms (once per resource)
-    if (t.type == T_PRED) {
-      b += 4 * n;
-      break;
-    }
+  if (need & NEED_NAME) b += 4 * n;  // name / namespace columns read by predicate terms
+  if (need & NEED_MNS) b += 4 * n;
   // label CSR / namespace-label rows read by selector terms (once per resource)
   if (need & NEED_LAB) b += 4.0 * n + 8.0 * C.lab_k.size();
   if (need & NEED_NSL) b += 4.0 * n;  // r_nsl; the namespace table itself is cache-resident
@@ -421,15 +410,19 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   // Preamble layout (pbuf): [program image][predicate directory][small-domain bitsets]
   // (padded to 16 B; copied into LDS by every scan block) followed by the large-domain
   // bitsets. Every predicate is evaluated by the dictionary pass straight into pbuf.
-  const uint32_t img = PD.image_words;  // 0 when the program does not fit the LDS budget
+  const uint32_t img = 0;  // program tables are read with scalar loads, not staged
   const uint32_t npreds = (uint32_t)P.preds.size();
+  const uint32_t nterms = (uint32_t)P.terms.size();
+  if (nterms > kMaxTerms) return fail(KPE_E_LIMIT, "program has more than 1024 distinct match terms");
+  const int64_t budget = (int64_t)kMaxDynWords - 2 * (kpe_scan_block_threads() / 64) * nterms - npreds - 8;
+  const uint32_t local_budget = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kMaxLocalWords, budget));
   std::vector<uint32_t> nwords(npreds);
   std::vector<char> local(npreds, 0);
   uint32_t lw = 0;
   for (uint32_t p = 0; p < npreds; ++p) {
     uint32_t n = C.dict[P.preds[p].domain].size();
     nwords[p] = ((n + 63) / 64) * 2 + 2;
-    if (lw + nwords[p] <= kMaxLocalWords && n <= kMaxLocalPairs) {
+    if (lw + nwords[p] <= local_budget && n <= kMaxLocalPairs) {
       local[p] = 1;
       lw += nwords[p];
     }
@@ -458,7 +451,6 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   }
   HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
   HIPCHK(hipMemsetAsync(B.pbuf.p, 0, (size_t)go * 4 + 16, s));
-  if (img) HIPCHK(hipMemcpyAsync(B.pbuf.p, PD.image.p, (size_t)img * 4, hipMemcpyDeviceToDevice, s));
   if (npreds)
     HIPCHK(hipMemcpyAsync(B.pbuf.as<uint32_t>() + img, dir.data(), (size_t)npreds * 4, hipMemcpyHostToDevice, s));
   B.blob_words = blob;
@@ -553,15 +545,10 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.selreqs = PD.selreqs.as<KpeSelReq>();
   sa.pbuf = B.pbuf.as<uint32_t>();
   sa.blob_words = B.blob_words;
-  sa.img_words = B.img_words;
   sa.npreds = (uint32_t)P.preds.size();
-  sa.off_rules = PD.off_rules;
-  sa.off_filters = PD.off_filters;
-  sa.off_terms = PD.off_terms;
-  sa.off_kindsels = PD.off_kindsels;
-  sa.off_annpairs = PD.off_annpairs;
-  sa.off_selectors = PD.off_selectors;
-  sa.off_selreqs = PD.off_selreqs;
+  sa.fterms = PD.fterms.as<uint32_t>();
+  sa.nterms = (uint32_t)P.terms.size();
+  sa.tm_lds = (B.blob_words + 1u) & ~1u;
   sa.pp_apparmor_key = P.pss.apparmor_key;
   sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
   sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;
@@ -573,13 +560,12 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pp_sysctl1 = P.pss.sysctl[1];
   sa.pp_sysctl2 = P.pss.sysctl[2];
   sa.cv_union = P.cv_union;
-  sa.any_pss = P.any_pss ? 1u : 0u;
   sa.need = B.need;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   sa.counts_part = B.counts_part.as<uint32_t>();
   sa.counts_global = B.counts_global.as<unsigned long long>();
-  HIPCHK(kpe_launch_scan(&sa, s));
+  HIPCHK(kpe_launch_scan(&sa, P.any_pss ? 1 : 0, s));
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.c, s));
     ev.bytes = scan_bytes(P, C, B.need, masks);

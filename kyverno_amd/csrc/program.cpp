@@ -595,12 +595,21 @@ class Lowerer {
     s.sysctl[2] = pred(D_SYSCTL, v129);
   }
 
+  uint32_t term(const KpeTerm& t) {  // distinct terms are evaluated once per resource
+    for (size_t i = 0; i < P.terms.size(); ++i) {
+      const KpeTerm& u = P.terms[i];
+      if (u.type == t.type && u.a == t.a && u.b == t.b && u.pad == t.pad) return (uint32_t)i;
+    }
+    P.terms.push_back(t);
+    return (uint32_t)P.terms.size() - 1;
+  }
+
   // one filter block -> terms; returns filter index
   uint32_t filter(const JV* rd, bool has_userinfo, bool is_exclude) {
-    KpeFilter f{(uint32_t)P.terms.size(), 0};
+    KpeFilter f{(uint32_t)P.fterms.size(), 0};
     auto push = [&](KpeTerm t) {
-      P.terms.push_back(t);
-      f.nterms++;
+      P.fterms.push_back(term(t));
+      f.nt++;
     };
     // ResourceDescription{} DeepEqual: a present selector pointer is never zero, even `{}`
     auto sel_obj = [&](const char* k) {
@@ -854,18 +863,18 @@ class Lowerer {
     KpeRule k{};
     k.policy = policy;
     k.apply_one = apply_one ? 1u : 0u;
-    k.pol_ns_pred = -1;
+    k.pol_term = -1;
     block(r.get("match"), false, &k.match_mode, &k.match_f0, &k.match_nf);
     block(r.get("exclude"), true, &k.excl_mode, &k.excl_f0, &k.excl_nf);
     if (namespaced || !pol_ns.empty()) {
       if (namespaced && pol_ns.empty()) {  // checkNamespacedPolicy can never pass
         k.match_f0 = (uint32_t)P.filters.size();
-        P.filters.push_back({(uint32_t)P.terms.size(), 1});
-        P.terms.push_back({T_FALSE, 0, 0, 0});
+        P.filters.push_back({(uint32_t)P.fterms.size(), 1});
+        P.fterms.push_back(term({T_FALSE, 0, 0, 0}));
         k.match_nf = 1;
         k.match_mode = MODE_LEGACY;
       } else {
-        k.pol_ns_pred = pred(D_NS, {glob_escape_check(pol_ns)});
+        k.pol_term = (int32_t)term({T_PRED, (uint32_t)pred(D_NS, {glob_escape_check(pol_ns)}), COL_NSA, 0});
       }
     }
     const JV* v = r.get("validate");

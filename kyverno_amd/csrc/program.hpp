@@ -32,7 +32,8 @@ struct Program {
   std::vector<std::string> rule_names;  // "<policy>/<rule>"
   std::vector<KpeRule> rules;
   std::vector<KpeFilter> filters;
-  std::vector<KpeTerm> terms;
+  std::vector<uint32_t> fterms;  // term indices of the filters
+  std::vector<KpeTerm> terms;    // distinct terms (each evaluated once per resource)
   std::vector<KpeKindSel> kindsels;
   std::vector<KpeAnnPair> annpairs;
   std::vector<KpeSelector> selectors;

@@ -281,8 +281,10 @@ typedef struct KpeSelReq {
   int32_t pk_ok, pv_ok; // SR_WILD: validity predicates (qualified name / label value)
   uint32_t pad[3];
 } KpeSelReq;
+// A filter (one ResourceFilter / ResourceDescription block) is the AND of the
+// distinct terms fterms[t0, t0+nt) (indices into the term table).
 typedef struct KpeFilter {
-  uint32_t term0, nterms;
+  uint32_t t0, nt;
 } KpeFilter;
 
 #define MODE_LEGACY 0u
@@ -294,8 +296,9 @@ typedef struct KpeRule {
   uint32_t cv_mask;       // PSS: versioned checks to run (version selection done at compile time)
   uint32_t match_mode, match_f0, match_nf;    // filters [f0, f0+nf)
   uint32_t excl_mode, excl_f0, excl_nf;
-  int32_t pol_ns_pred;    // -1 or predicate over D_NS (actual ns) that must hold (policy namespace)
+  int32_t pol_term;       // -1 or term that must hold (namespaced policy: resource ns == policy ns)
   uint32_t policy;        // policy index (ApplyOne grouping)
   uint32_t apply_one;     // spec.applyRules == One
   uint32_t pss_excl0, pss_nexcl;  // PSS exclusions (reserved)
+  uint32_t pad[3];        // 16 words: one scalar dwordx16 load per rule
 } KpeRule;
