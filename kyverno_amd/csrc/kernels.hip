@@ -168,10 +168,6 @@ __global__ void __launch_bounds__(256) kpe_count_reduce(const uint32_t* part, ui
 namespace {
 
 constexpr uint32_t kBlock = 256;
-constexpr uint32_t kChunk = 1024;   // containers staged per LDS pass
-constexpr uint32_t kStageCols = 32;                // verdict columns staged per pass
-constexpr uint32_t kStageV = kBlock * kStageCols;  // verdict staging bytes
-constexpr uint32_t kListChunk = 1024;  // volumes / sysctls / pod annotations staged per LDS pass
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
@@ -278,389 +274,453 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t x) {
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 
-// One resource per lane; rules are evaluated bit-sliced per wave.
+// Bitset word of a resolved predicate location (PRED_LOCAL | LDS index, or pbuf index).
+struct Bits {
+  const uint32_t* lds;
+  const uint32_t* pbuf;
+  __device__ __forceinline__ uint32_t word(uint32_t loc, uint32_t wi) const {
+    return (loc & PRED_LOCAL) ? lds[(loc & ~PRED_LOCAL) + wi] : pbuf[loc + wi];
+  }
+  __device__ __forceinline__ bool bit(uint32_t loc, uint32_t id) const {
+    if (id == KPE_NO_STR) return false;
+    return (word(loc, id >> 5) >> (id & 31u)) & 1u;
+  }
+  __device__ __forceinline__ uint64_t mask64(uint32_t loc) const {  // predicate over D_CAP (<= 64 ids)
+    return loc == PRED_NONE ? 0ull : ((uint64_t)word(loc, 0) | ((uint64_t)word(loc, 1) << 32));
+  }
+};
+
+// Round-1 data of one 64-resource tile.
+struct Tile1 {
+  uint4 rec, hdr;
+  uint32_t gvk, nsa, name, mns;
+};
+
+template <bool PSS>
+__device__ __forceinline__ Tile1 load_tile1(const ScanArgs& a, int64_t tile, uint32_t lane) {
+  Tile1 d;
+  d.rec = d.hdr = make_uint4(0, 0, 0, 0);
+  d.gvk = 0;
+  d.nsa = d.name = d.mns = KPE_NO_STR;
+  const int64_t r = tile * 64 + lane;
+  const int64_t rc = r < a.n ? r : a.n - 1;  // clamped: loads are unconditional
+  if (PSS) {
+    d.rec = reinterpret_cast<const uint4*>(a.rec)[rc];
+    // the wave header as a vector load (a scalar load would be waited on at once)
+    uint32_t hv = (uint32_t)tile;
+    asm volatile("" : "+v"(hv));
+    d.hdr = reinterpret_cast<const uint4*>(a.hdr)[hv];
+  } else {
+    if (a.need & NEED_GVK) d.gvk = a.r_gvk[rc];
+    if (a.need & NEED_NSA) d.nsa = a.r_nsa[rc];
+  }
+  if (a.need & NEED_NAME) d.name = a.r_name[rc];
+  if (a.need & NEED_MNS) d.mns = a.r_mns[rc];
+  return d;
+}
+
+// Persistent, wave-autonomous scan. Every wave walks 64-resource tiles
+// (tile = global wave id, + total waves, ...) with the next tile's round-1 loads in
+// flight while the current tile is evaluated:
 //
-//  round 1  pod record (dwordx4) + wave header (PSS programs) or the gvk / namespace
-//           columns, the name columns the terms read, the LDS preamble (predicate
-//           directory + small-domain bitsets) and the capability-set table: every
-//           load is issued before the first wait;
+//  round 1  pod record (dwordx4) + wave header (PSS programs) or the gvk /
+//           namespace columns, plus the name columns the terms read — prefetched
+//           one tile ahead;
 //  round 2  (PSS) the lane's list items at header + exclusive wave scan of the
-//           counts: up to 4 containers, 2 volumes, 2 annotations, 1 sysctl, issued
-//           together; the PSA versioned checks give a per-lane failure bitmask;
-//  terms    each DISTINCT match term of the program is evaluated once per resource
-//           and ballot-ed into a 64-bit wave mask (LDS, per wave);
-//  rules    wave-uniform loop on the scalar unit: match/exclude blocks are AND/OR of
-//           term masks (pkg/engine/utils/match.go:168-300), ApplyOne
-//           (pkg/engine/validation.go:75-77) is a mask, the PSS handler's pass /
-//           fail / error cells are masks, per-rule counts are popcounts. Each lane
-//           only extracts its verdict byte.
+//           counts: up to 4 containers, 2 volumes, 2 annotations, 1 sysctl issued
+//           together; the PSA versioned checks give a per-lane failure bitmask
+//           (pkg/pss/evaluate.go:24-70 over the PSA v0.29 check semantics);
+//  terms    every DISTINCT match term is evaluated once per resource and ballot-ed
+//           into a 64-bit mask (LDS, per wave); so is every distinct PSS version set;
+//  rules    transposed: lane j evaluates rule c0+j for all 64 resources at once with
+//           64-bit mask algebra (match/exclude: pkg/engine/utils/match.go:168-300;
+//           ApplyOne: pkg/engine/validation.go:75-77), then each resource lane
+//           extracts its verdict bytes; cells are staged per wave and stored as
+//           contiguous row segments; counts are popcounts (LDS per block).
 template <bool PSS>
 __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];  // [preamble copy][term masks]
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ __attribute__((aligned(16))) uint8_t s_capb[KPE_MAX_CAPSETS];
-  __shared__ __attribute__((aligned(16))) uint32_t s_cnt[6 * KPE_SMALL_R];
-  __shared__ __attribute__((aligned(16))) uint8_t s_v[kStageV];
+  __shared__ __attribute__((aligned(16))) uint32_t s_cnt[3 * KPE_LDS_R];
 
-  const int64_t p0 = (int64_t)blockIdx.x * kBlock;
-  const uint32_t t = threadIdx.x;
-  const uint32_t lane = t & 63u, wv = t >> 6;
-  const int64_t r = p0 + t;
-  const bool live = r < a.n;
-  const uint32_t np = (uint32_t)((a.n - p0) < (int64_t)kBlock ? (a.n - p0) : (int64_t)kBlock);
-  const uint32_t R = a.nrules;
-  const bool small_r = R <= KPE_SMALL_R;
-  const uint32_t need = a.need;
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t R = a.nrules, need = a.need;
+  const bool lds_cnt = R <= KPE_LDS_R;
   const bool need_caps = PSS && (need & NEED_CAPS);
+  const int64_t ntiles = (a.n + 63) >> 6;
+  const uint32_t W = gridDim.x * (kBlock / 64u);
+  int64_t tile = (int64_t)blockIdx.x * (kBlock / 64u) + wv;
 
-  // ---- round 1: every load issued before the first use ----
-  // Loads are unconditional at clamped (always valid) addresses and the value is
-  // selected after the barrier, so no exec-mask branch splits the issue sequence.
-  const uint4 z4 = make_uint4(0, 0, 0, 0);
-  const int64_t rc = live ? r : a.n - 1;
-  const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)(r >> 6));
-  uint4 rec_raw = z4, hdr_raw = z4;
-  uint32_t gvk_raw = 0, nsa_raw = KPE_NO_STR, name_raw = KPE_NO_STR, mns_raw = KPE_NO_STR;
-  if (PSS) {
-    rec_raw = reinterpret_cast<const uint4*>(a.rec)[rc];
-    // vector load of the wave header: a scalar load here would be waited on
-    // before the preamble loads issue
-    uint32_t hv = (uint32_t)(rc >> 6);
-    asm volatile("" : "+v"(hv));
-    hdr_raw = reinterpret_cast<const uint4*>(a.hdr)[hv];
-  } else {
-    if (need & NEED_GVK) gvk_raw = a.r_gvk[rc];
-    if (need & NEED_NSA) nsa_raw = a.r_nsa[rc];
+  // ---- block prologue (overlapped with the first tile's round-1 loads) ----
+  Tile1 nx{};
+  if (tile < ntiles) nx = load_tile1<PSS>(a, tile, lane);
+  {
+    const uint32_t nb4 = a.blob_words >> 2;  // >= 1
+    const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
+    uint4* d4 = reinterpret_cast<uint4*>(dyn);
+#pragma unroll 1
+    for (uint32_t i = t; i < nb4; i += kBlock) d4[i] = blob[i];
+    if (a.filt_lds != PRED_NONE) {  // program filters + filter terms for the rule lanes
+      const uint32_t nw = a.fterm_lds + a.nfterms - a.filt_lds;
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(a.filters);
+#pragma unroll 1
+      for (uint32_t i = t; i < nw; i += kBlock)
+        dyn[a.filt_lds + i] = i < a.fterm_lds - a.filt_lds ? src[i] : a.fterms[i - (a.fterm_lds - a.filt_lds)];
+    }
+#pragma unroll 1
+    for (uint32_t i = t; i < 3 * R && lds_cnt; i += kBlock) s_cnt[i] = 0;
   }
-  if (need & NEED_NAME) name_raw = a.r_name[rc];
-  if (need & NEED_MNS) mns_raw = a.r_mns[rc];
-  const uint32_t nb4 = a.blob_words >> 2;  // >= 1
-  const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
-  const uint4 b0 = blob[t < nb4 ? t : nb4 - 1];
-  const uint4 b1 = blob[t + kBlock < nb4 ? t + kBlock : nb4 - 1];
-  uint4 cs = z4;
-  if (need_caps && a.ncapsets) cs = reinterpret_cast<const uint4*>(a.capsets)[t < a.ncapsets ? t : a.ncapsets - 1];
-  uint4* d4 = reinterpret_cast<uint4*>(dyn);
-  if (t < nb4) d4[t] = b0;
-  if (t + kBlock < nb4) d4[t + kBlock] = b1;
-#pragma unroll 1
-  for (uint32_t i = t + 2 * kBlock; i < nb4; i += kBlock) d4[i] = blob[i];
-  if (small_r)
-#pragma unroll 1
-    for (uint32_t i = t; i < 6 * R; i += kBlock) s_cnt[i] = 0;
   __syncthreads();
+  const Bits B{dyn, a.pbuf};
+  if (need_caps) {  // capability-set violation bits (add/drop masks vs the fixed allow-lists)
+    const uint64_t caps_ok = B.mask64(a.pp_caps_ok), nbs = B.mask64(a.pp_cap_nbs), all = B.mask64(a.pp_cap_all);
+#pragma unroll 1
+    for (uint32_t i = t; i < a.ncapsets; i += kBlock) {
+      const uint4 c = reinterpret_cast<const uint4*>(a.capsets)[i];
+      const uint64_t ad = (uint64_t)c.x | ((uint64_t)c.y << 32), dr = (uint64_t)c.z | ((uint64_t)c.w << 32);
+      s_capb[i] = (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+    }
+    __syncthreads();
+  }
+  const KpeFilter* filt =
+      a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
+  const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
 
-  // results of round 1 are consumed only after the barrier
-  const uint4 rec = live ? rec_raw : z4;
-  const uint4 hdr = (int64_t)wave * 64 < a.n ? hdr_raw : z4;
-  const uint32_t gvk_col = live ? gvk_raw : 0u, nsa_col = live ? nsa_raw : KPE_NO_STR;
-  const uint32_t name_col = live ? name_raw : KPE_NO_STR, mns_col = live ? mns_raw : KPE_NO_STR;
-  const uint32_t* pbuf = a.pbuf;
-  auto pword = [&](int32_t p, uint32_t wi) -> uint32_t {  // word wi of predicate p's bitset
-    const uint32_t w = sld(pbuf, (uint32_t)p);            // directory entry (uniform)
-    return (w & PRED_LOCAL) ? dyn[(w & ~PRED_LOCAL) + wi] : pbuf[w + wi];
-  };
-  auto pbit = [&](int32_t p, uint32_t id) -> bool {
-    if (id == KPE_NO_STR) return false;
-    return (pword(p, id >> 5) >> (id & 31u)) & 1u;
-  };
-  auto pmask64 = [&](int32_t p) -> uint64_t {  // predicate over D_CAP (<= 64 ids)
-    if (p < 0) return 0;
-    return (uint64_t)pword(p, 0) | ((uint64_t)pword(p, 1) << 32);
-  };
+  // per-wave LDS: term masks, PSS version-set masks, rule cell masks, verdict staging
+  uint64_t* tmk = reinterpret_cast<uint64_t*>(dyn + a.wave_lds + wv * a.wave_words);
+  uint64_t* cvm = tmk + a.nterms;
+  uint64_t* rmk = cvm + a.ncv;                                       // kRC x (P, F, E)
+  uint8_t* sv = reinterpret_cast<uint8_t*>(rmk + 3 * KPE_RULE_CHUNK);  // 64 x kRC bytes
 
-  uint32_t fails = 0;
-  if (PSS) {
-    if (need_caps) {
-      const uint64_t caps_ok = pmask64(a.pp_caps_ok), nbs = pmask64(a.pp_cap_nbs), all = pmask64(a.pp_cap_all);
-      auto capbits = [&](uint4 c) -> uint8_t {
-        const uint64_t ad = (uint64_t)c.x | ((uint64_t)c.y << 32), dr = (uint64_t)c.z | ((uint64_t)c.w << 32);
-        return (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+  // single-chunk programs keep lane j's packed rule in registers for every tile
+  uint4 myrule = make_uint4(0, 0, 0, 0);
+  if (R <= KPE_RULE_CHUNK && lane < R) myrule = reinterpret_cast<const uint4*>(a.rule_lanes)[lane];
+
+#pragma unroll 1
+  for (; tile < ntiles; tile += W) {
+    const Tile1 cur = nx;
+    if (tile + W < ntiles) nx = load_tile1<PSS>(a, tile + W, lane);
+    const int64_t r = tile * 64 + lane;
+    const bool live = r < a.n;
+    const int64_t rc = live ? r : a.n - 1;
+    const uint4 rec = live ? cur.rec : make_uint4(0, 0, 0, 0);
+    const uint4 hdr = cur.hdr;
+
+    uint32_t fails = 0;
+    if (PSS) {
+      // ---- list offsets: header + exclusive wave scan of the packed counts ----
+      const uint32_t z = rec.z;
+      const uint32_t c01 = (z & 0xFFu) | ((z & 0xFF00u) << 8), c23 = ((z >> 16) & 0xFFu) | ((z >> 24) << 16);
+      const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
+      const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+      const uint32_t oc = hdr.x + (e01 & 0xFFFFu), ov = hdr.y + (e01 >> 16), os = hdr.z + (e23 & 0xFFFFu),
+                     oa = hdr.w + (e23 >> 16);
+      // ---- round 2: every first-pass list load issued before any is used ----
+      const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
+      const uint2* pkv = reinterpret_cast<const uint2*>(a.pann_kv);
+      const bool nvol = (need & NEED_VOL) && a.nvol_total, nsys = (need & NEED_SYS) && a.nsys_total,
+                 npann = (need & NEED_PANN) && a.npann_total, nsann = (need & NEED_SANN) && a.nctr_total;
+      const uint2 z2 = make_uint2(0, 0);
+      uint2 k0 = z2, k1 = z2, k2 = z2, k3 = z2;
+      if (a.nctr_total) {
+        const uint32_t lim = a.nctr_total - 1;
+        k0 = crec[min(oc, lim)];
+        k1 = crec[min(oc + 1, lim)];
+        k2 = crec[min(oc + 2, lim)];
+        k3 = crec[min(oc + 3, lim)];
+      }
+      uint32_t v0 = 0, v1 = 0, sy0 = 0;
+      if (nvol) {
+        v0 = a.vol_src[min(ov, a.nvol_total - 1)];
+        v1 = a.vol_src[min(ov + 1, a.nvol_total - 1)];
+      }
+      if (nsys) sy0 = a.sys_id[min(os, a.nsys_total - 1)];
+      uint2 q0 = z2, q1 = z2;
+      if (npann) {
+        q0 = pkv[min(oa, a.npann_total - 1)];
+        q1 = pkv[min(oa + 1, a.npann_total - 1)];
+      }
+      uint32_t sa0 = KPE_NO_STR, sa1 = KPE_NO_STR, sa2 = KPE_NO_STR, sa3 = KPE_NO_STR;
+      if (nsann) {
+        const uint32_t lim = a.nctr_total - 1;
+        sa0 = a.c_sann[min(oc, lim)];
+        sa1 = a.c_sann[min(oc + 1, lim)];
+        sa2 = a.c_sann[min(oc + 2, lim)];
+        sa3 = a.c_sann[min(oc + 3, lim)];
+      }
+      // ---- containers: violation bits OR-ed over the pod's containers ----
+      auto one = [&](uint2 kk, uint32_t sann) -> uint32_t {
+        uint32_t b = ctr_bits(kk.x, need_caps ? s_capb[kk.y] : 0u);
+        if (nsann && sann != KPE_NO_STR && !B.bit(a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
+        return b;
       };
-      if (t < a.ncapsets) s_capb[t] = capbits(cs);
+      uint32_t cb = (nc > 0 ? one(k0, sa0) : 0u) | (nc > 1 ? one(k1, sa1) : 0u) | (nc > 2 ? one(k2, sa2) : 0u) |
+                    (nc > 3 ? one(k3, sa3) : 0u);
 #pragma unroll 1
-      for (uint32_t i = t + kBlock; i < a.ncapsets; i += kBlock)
-        s_capb[i] = capbits(reinterpret_cast<const uint4*>(a.capsets)[i]);
-      __syncthreads();
-    }
-    // ---- list offsets: header + exclusive wave scan of the packed counts ----
-    const uint32_t z = rec.z;
-    const uint32_t c01 = (z & 0xFFu) | ((z & 0xFF00u) << 8), c23 = ((z >> 16) & 0xFFu) | ((z >> 24) << 16);
-    const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
-    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
-    const uint32_t oc = hdr.x + (e01 & 0xFFFFu), ov = hdr.y + (e01 >> 16), os = hdr.z + (e23 & 0xFFFFu),
-                   oa = hdr.w + (e23 >> 16);
-    // ---- round 2: issue every first-pass list load before using any ----
-    // (clamped unconditional loads; totals > 0 are wave-uniform guards)
-    const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
-    const uint2* pkv = reinterpret_cast<const uint2*>(a.pann_kv);
-    const bool nvol = (need & NEED_VOL) && a.nvol_total, nsys = (need & NEED_SYS) && a.nsys_total,
-               npann = (need & NEED_PANN) && a.npann_total, nsann = (need & NEED_SANN) && a.nctr_total;
-    const uint2 z2 = make_uint2(0, 0);
-    uint2 k0 = z2, k1 = z2, k2 = z2, k3 = z2;
-    if (a.nctr_total) {
-      const uint32_t lim = a.nctr_total - 1;
-      k0 = crec[min(oc, lim)];
-      k1 = crec[min(oc + 1, lim)];
-      k2 = crec[min(oc + 2, lim)];
-      k3 = crec[min(oc + 3, lim)];
-    }
-    uint32_t v0 = 0, v1 = 0, sy0 = 0;
-    if (nvol) {
-      v0 = a.vol_src[min(ov, a.nvol_total - 1)];
-      v1 = a.vol_src[min(ov + 1, a.nvol_total - 1)];
-    }
-    if (nsys) sy0 = a.sys_id[min(os, a.nsys_total - 1)];
-    uint2 q0 = z2, q1 = z2;
-    if (npann) {
-      q0 = pkv[min(oa, a.npann_total - 1)];
-      q1 = pkv[min(oa + 1, a.npann_total - 1)];
-    }
-    uint32_t sa[4] = {KPE_NO_STR, KPE_NO_STR, KPE_NO_STR, KPE_NO_STR};
-    if (nsann) {
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t x = a.c_sann[min(oc + k, a.nctr_total - 1)];
-        sa[k] = nc > k ? x : KPE_NO_STR;
+      for (uint32_t k = 4; k < nc; ++k) cb |= one(crec[oc + k], nsann ? a.c_sann[oc + k] : KPE_NO_STR);
+      // ---- volumes ----
+      uint32_t vor = 0, vand = ~0u;  // hostPath present anywhere / some volume outside the allow-list
+      auto vol = [&](uint32_t sv_) {
+        vor |= sv_;
+        vand &= (sv_ & kAllowedVolumes) ? ~0u : 0u;
+      };
+      if (nvol) {
+        if (nv > 0) vol(v0);
+        if (nv > 1) vol(v1);
+#pragma unroll 1
+        for (uint32_t k = 2; k < nv; ++k) vol(a.vol_src[ov + k]);
       }
-    }
-    // ---- containers ----
-    auto one = [&](uint2 kk, uint32_t sann) -> uint32_t {
-      uint32_t b = ctr_bits(kk.x, need_caps ? s_capb[kk.y] : 0u);
-      if (sann != KPE_NO_STR && !pbit(a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
-      return b;
-    };
-    uint32_t cb = 0;
-    if (nc > 0) cb |= one(k0, sa[0]);
-    if (nc > 1) cb |= one(k1, sa[1]);
-    if (nc > 2) cb |= one(k2, sa[2]);
-    if (nc > 3) cb |= one(k3, sa[3]);
+      const bool vol_hostpath = (vor >> VS_HOSTPATH) & 1u, vol_restricted = vand == 0u;
+      // ---- sysctls (allow-lists 1.0 / 1.27 / 1.29) ----
+      uint32_t sys_bad = 0;
+      auto sysf = [&](uint32_t id) {
+        sys_bad |= (B.bit(a.pp_sysctl0, id) ? 0u : 1u) | (B.bit(a.pp_sysctl1, id) ? 0u : 2u) |
+                   (B.bit(a.pp_sysctl2, id) ? 0u : 4u);
+      };
+      if (nsys) {
+        if (ns > 0) sysf(sy0);
 #pragma unroll 1
-    for (uint32_t k = 4; k < nc; ++k) cb |= one(crec[oc + k], nsann ? a.c_sann[oc + k] : KPE_NO_STR);
-    // ---- volumes ----
-    bool vol_hostpath = false, vol_restricted = false;
-    auto vol = [&](uint32_t sv) {
-      vol_hostpath |= (sv & (1u << VS_HOSTPATH)) != 0;
-      vol_restricted |= !(sv & kAllowedVolumes);
-    };
-    if (nvol) {
-      if (nv > 0) vol(v0);
-      if (nv > 1) vol(v1);
+        for (uint32_t k = 1; k < ns; ++k) sysf(a.sys_id[os + k]);
+      }
+      // ---- pod-template annotations: AppArmor, seccomp pod annotation ----
+      bool apparmor_bad = false, sec_pod_ann_bad = false;
+      auto ann = [&](uint2 kv) {
+        apparmor_bad |= B.bit(a.pp_apparmor_key, kv.x) && !B.bit(a.pp_apparmor_ok, kv.y);
+        sec_pod_ann_bad |= B.bit(a.pp_seccomp_pod_key, kv.x) && !B.bit(a.pp_seccomp_ann_ok, kv.y);
+      };
+      if (npann) {
+        if (na > 0) ann(q0);
+        if (na > 1) ann(q1);
 #pragma unroll 1
-      for (uint32_t k = 2; k < nv; ++k) vol(a.vol_src[ov + k]);
+        for (uint32_t k = 2; k < na; ++k) ann(pkv[oa + k]);
+      }
+      if (live) fails = cv_fails(rec.x, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
     }
-    // ---- sysctls (allow-lists 1.0 / 1.27 / 1.29) ----
-    uint32_t sys_bad = 0;
-    auto sysf = [&](uint32_t id) {
-      sys_bad |= (pbit(a.pp_sysctl0, id) ? 0u : 1u) | (pbit(a.pp_sysctl1, id) ? 0u : 2u) |
-                 (pbit(a.pp_sysctl2, id) ? 0u : 4u);
-    };
-    if (nsys) {
-      if (ns > 0) sysf(sy0);
-#pragma unroll 1
-      for (uint32_t k = 1; k < ns; ++k) sysf(a.sys_id[os + k]);
-    }
-    // ---- pod-template annotations: AppArmor, seccomp pod annotation ----
-    bool apparmor_bad = false, sec_pod_ann_bad = false;
-    auto ann = [&](uint2 kv) {
-      apparmor_bad |= pbit(a.pp_apparmor_key, kv.x) && !pbit(a.pp_apparmor_ok, kv.y);
-      sec_pod_ann_bad |= pbit(a.pp_seccomp_pod_key, kv.x) && !pbit(a.pp_seccomp_ann_ok, kv.y);
-    };
-    if (npann) {
-      if (na > 0) ann(q0);
-      if (na > 1) ann(q1);
-#pragma unroll 1
-      for (uint32_t k = 2; k < na; ++k) ann(pkv[oa + k]);
-    }
-    if (live) fails = cv_fails(rec.x, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
-  }
 
-
-  // ---- terms: one ballot per distinct term per wave ----
-  const uint32_t gvk = PSS ? rec.y : gvk_col;
-  const uint32_t nsa = PSS ? rec.w : nsa_col;
-  uint64_t* tmask = reinterpret_cast<uint64_t*>(dyn + a.tm_lds) + (size_t)wv * a.nterms;
+    // ---- terms: one ballot per distinct term ----
+    const uint32_t gvk = PSS ? rec.y : (live ? cur.gvk : 0u);
+    const uint32_t nsa = PSS ? rec.w : (live ? cur.nsa : KPE_NO_STR);
+    const uint32_t name_col = live ? cur.name : KPE_NO_STR, mns_col = live ? cur.mns : KPE_NO_STR;
 #pragma unroll 1
-  for (uint32_t ti = 0; ti < a.nterms; ++ti) {
-    const KpeTerm tm = sld(a.terms, ti);
-    bool ok = true;
-    if (tm.type == T_KIND_PRED) {
-      ok = pbit((int32_t)tm.a, GVK_KIND(gvk));
-    } else if (tm.type == T_KINDS) {  // CheckKind: OR over kind selectors
-      ok = false;
+    for (uint32_t ti = 0; ti < a.nterms; ++ti) {
+      const KpeTerm tm = sld(a.terms, ti);
+      bool ok = true;
+      if (tm.type == T_KIND_PRED) {
+        ok = B.bit(tm.a, GVK_KIND(gvk));
+      } else if (tm.type == T_KINDS) {  // CheckKind: OR over kind selectors
+        ok = false;
 #pragma unroll 1
-      for (uint32_t k = 0; k < tm.b; ++k) {
-        const KpeKindSel ks = sld(a.kindsels, tm.a + k);
-        ok |= ks.sub_ok && (ks.pg < 0 || pbit(ks.pg, GVK_GRP(gvk))) && (ks.pv < 0 || pbit(ks.pv, GVK_VER(gvk))) &&
-              (ks.pk < 0 || pbit(ks.pk, GVK_KIND(gvk)));
-      }
-    } else if (tm.type == T_PRED) {
-      const uint32_t id = tm.b == COL_NAME ? name_col : (tm.b == COL_MNS ? mns_col : nsa);
-      ok = pbit((int32_t)tm.a, id);
-    } else if (tm.type == T_ANNOTATIONS) {  // CheckAnnotations: every pair matched by some annotation
-      const uint32_t lo = a.ann_off[rc], hi = live ? a.ann_off[rc + 1] : lo;
-#pragma unroll 1
-      for (uint32_t k = 0; k < tm.b; ++k) {
-        const KpeAnnPair pr = sld(a.annpairs, tm.a + k);
-        bool hit = false;
-#pragma unroll 1
-        for (uint32_t j = lo; j < hi && !hit; ++j) hit = pbit(pr.pk, a.ann_k[j]) && pbit(pr.pv, a.ann_v[j]);
-        ok &= hit;
-      }
-    } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
-      // CheckSelector (pkg/utils/match/labels.go:9-24) over the resource's labels or,
-      // for namespaceSelector, its namespace's labels (utils/match.go:114-138)
-      const KpeSelector S = sld(a.selectors, tm.a);
-      uint32_t lo = 0, hi = 0;
-      const uint32_t *K = a.lab_k, *V = a.lab_v;
-      bool eval = true;
-      if (tm.type == T_SELECTOR) {
-        lo = a.lab_off[rc];
-        hi = live ? a.lab_off[rc + 1] : lo;
-      } else {
-        // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
-        const uint32_t kid = GVK_KIND(gvk);
-        const uint32_t row = a.r_nsl[rc];
-        if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
-        K = a.nsl_k, V = a.nsl_v;
-        if (pbit(S.p_kind_ns, kid)) {
-          ok = false, eval = false;
-        } else if (pbit(S.p_kind_empty, kid) && !S.star_kind) {
-          ok = true, eval = false;
-        } else if (S.invalid) {
-          ok = false, eval = false;
+        for (uint32_t k = 0; k < tm.b; ++k) {
+          const KpeKindSel ks = sld(a.kindsels, tm.a + k);
+          ok |= ks.sub_ok && (ks.pg == PRED_NONE || B.bit(ks.pg, GVK_GRP(gvk))) &&
+                (ks.pv == PRED_NONE || B.bit(ks.pv, GVK_VER(gvk))) && (ks.pk == PRED_NONE || B.bit(ks.pk, GVK_KIND(gvk)));
         }
-      }
-      if (eval) {
+      } else if (tm.type == T_PRED) {
+        const uint32_t id = tm.b == COL_NAME ? name_col : (tm.b == COL_MNS ? mns_col : nsa);
+        ok = B.bit(tm.a, id);
+      } else if (tm.type == T_ANNOTATIONS) {  // CheckAnnotations: every pair matched by some annotation
+        const uint32_t lo = a.ann_off[rc], hi = live ? a.ann_off[rc + 1] : lo;
 #pragma unroll 1
-        for (uint32_t qi = 0; qi < S.nreq; ++qi) {
-          const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
-          const bool wild = q.op == SR_WILD;
-          uint32_t j = lo;
+        for (uint32_t k = 0; k < tm.b; ++k) {
+          const KpeAnnPair pr = sld(a.annpairs, tm.a + k);
+          bool hit = false;
 #pragma unroll 1
-          for (; j < hi; ++j)  // first label with a matching key (and value, for wildcards)
-            if (pbit(q.pk, K[j]) && (!wild || pbit(q.pv, V[j]))) break;
-          const bool found = j < hi;
-          const uint32_t kid = found ? K[j] : KPE_NO_STR, vid = found ? V[j] : KPE_NO_STR;
-          bool qok;
-          switch (q.op) {
-            case SR_EQ:
-            case SR_IN: qok = found && pbit(q.pv, vid); break;
-            case SR_WILD: qok = found && pbit(q.pk_ok, kid) && pbit(q.pv_ok, vid); break;
-            case SR_NOTIN: qok = !found || !pbit(q.pv, vid); break;
-            case SR_EXISTS: qok = found; break;
-            default: qok = !found; break;
+          for (uint32_t j = lo; j < hi && !hit; ++j) hit = B.bit(pr.pk, a.ann_k[j]) && B.bit(pr.pv, a.ann_v[j]);
+          ok &= hit;
+        }
+      } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
+        // CheckSelector (pkg/utils/match/labels.go:9-24) over the resource's labels or,
+        // for namespaceSelector, its namespace's labels (utils/match.go:114-138)
+        const KpeSelector S = sld(a.selectors, tm.a);
+        uint32_t lo = 0, hi = 0;
+        const uint32_t *K = a.lab_k, *V = a.lab_v;
+        bool eval = true;
+        if (tm.type == T_SELECTOR) {
+          lo = a.lab_off[rc];
+          hi = live ? a.lab_off[rc + 1] : lo;
+        } else {
+          // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
+          const uint32_t kid = GVK_KIND(gvk);
+          const uint32_t row = a.r_nsl[rc];
+          if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
+          K = a.nsl_k, V = a.nsl_v;
+          if (B.bit(S.p_kind_ns, kid)) {
+            ok = false, eval = false;
+          } else if (B.bit(S.p_kind_empty, kid) && !S.star_kind) {
+            ok = true, eval = false;
+          } else if (S.invalid) {
+            ok = false, eval = false;
           }
-          ok &= qok;
         }
+        if (eval) {
+#pragma unroll 1
+          for (uint32_t qi = 0; qi < S.nreq; ++qi) {
+            const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
+            const bool wild = q.op == SR_WILD;
+            uint32_t j = lo;
+#pragma unroll 1
+            for (; j < hi; ++j)  // first label with a matching key (and value, for wildcards)
+              if (B.bit(q.pk, K[j]) && (!wild || B.bit(q.pv, V[j]))) break;
+            const bool found = j < hi;
+            const uint32_t kid = found ? K[j] : KPE_NO_STR, vid = found ? V[j] : KPE_NO_STR;
+            bool qok;
+            switch (q.op) {
+              case SR_EQ:
+              case SR_IN: qok = found && B.bit(q.pv, vid); break;
+              case SR_WILD: qok = found && B.bit(q.pk_ok, kid) && B.bit(q.pv_ok, vid); break;
+              case SR_NOTIN: qok = !found || !B.bit(q.pv, vid); break;
+              case SR_EXISTS: qok = found; break;
+              default: qok = !found; break;
+            }
+            ok &= qok;
+          }
+        }
+      } else {  // T_FALSE
+        ok = false;
       }
-    } else {  // T_FALSE
-      ok = false;
+      const uint64_t m = __ballot(ok);
+      if (lane == 0) tmk[ti] = m;
     }
-    const uint64_t m = __ballot(ok);
-    if (lane == 0) tmask[ti] = m;
-  }
-  auto term_mask = [&](uint32_t ti) -> uint64_t { return uniform64(tmask[ti]); };
-  // match / exclude block: any => OR of filters, all => AND, legacy => its one filter;
-  // a filter is the AND of its terms
-  auto block_mask = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> uint64_t {
-    const bool all = mode == MODE_ALL;
-    uint64_t acc = all ? ~0ull : 0ull;
+    // PSS version sets: resources failing some check of each distinct cv_mask
 #pragma unroll 1
-    for (uint32_t f = 0; f < nf; ++f) {
-      const KpeFilter fl = sld(a.filters, f0 + f);
-      uint64_t fm = ~0ull;
-#pragma unroll 1
-      for (uint32_t k = 0; k < fl.nt && fm; ++k) fm &= term_mask(sld(a.fterms, fl.t0 + k));
-      acc = all ? (acc & fm) : (acc | fm);
+    for (uint32_t c = 0; c < a.ncv; ++c) {
+      const uint64_t m = __ballot((fails & sld(a.cv_classes, c)) != 0u);
+      if (lane == 0) cvm[c] = m;
     }
-    return acc;
-  };
+    const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
+    const uint64_t live_m = __ballot(live);
+    const uint64_t err_m = PSS ? __ballot(live && (cls == R_CLASS_OTHER || (rec.x & PR_DECODE_ERR))) : 0ull;
+    const uint32_t nrows = (uint32_t)min((int64_t)64, a.n - tile * 64);
+    __builtin_amdgcn_wave_barrier();
 
-  // ---- rules (wave-uniform) ----
-  const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
-  const bool pss_err = cls == R_CLASS_OTHER || (rec.x & PR_DECODE_ERR);
-  const uint64_t live_m = __ballot(live);
-  const uint64_t err_m = PSS ? __ballot(pss_err) : 0ull;
-  const uint32_t cw = R < kStageCols ? R : kStageCols;  // verdict columns staged per pass
-  uint64_t applied = 0;
-  uint32_t cur_policy = 0xFFFFFFFFu;
+    // ---- rules, KPE_RULE_CHUNK at a time ----
+    uint64_t applied = 0;  // ApplyOne state (lane 0, rule order)
+    uint32_t cur_policy = 0xFFFFFFFFu;
 #pragma unroll 1
-  for (uint32_t ri = 0; ri < R; ++ri) {
-    const KpeRule rule = sld(a.rules, ri);
-    if (rule.policy != cur_policy) {
-      cur_policy = rule.policy;
-      applied = 0;
-    }
-    uint64_t m = live_m;
-    if (rule.pol_term >= 0) m &= term_mask((uint32_t)rule.pol_term);
-    if (m) m &= block_mask(rule.match_mode, rule.match_f0, rule.match_nf);
-    if (m) m &= ~block_mask(rule.excl_mode, rule.excl_f0, rule.excl_nf);
-    if (rule.apply_one) m &= ~applied;
-    uint64_t pm = 0, fm = 0, em = 0;
-    if (rule.handler == H_PSS) {
-      em = m & err_m;
-      fm = m & ~em & __ballot((fails & rule.cv_mask) != 0u);
-      pm = m & ~em & ~fm;
-    } else if (rule.handler == H_ERROR) {
-      em = m;
-    }
-    applied |= pm | fm;
-    const uint32_t v = ((pm >> lane) & 1u) ? KPE_PASS_ : ((fm >> lane) & 1u) ? KPE_FAIL_
-                                                          : ((em >> lane) & 1u) ? KPE_ERROR_ : KPE_NA_;
-    if (a.masks && live) {
-      uint32_t cmask = 0;
-      if ((fm >> lane) & 1u) {
-        const uint32_t f = fails & rule.cv_mask;
+    for (uint32_t c0 = 0; c0 < R; c0 += KPE_RULE_CHUNK) {
+      const uint32_t nc = min((uint32_t)KPE_RULE_CHUNK, R - c0);
+      // (a) transposed: lane j evaluates rule c0 + j over the whole tile
+      if (lane < nc) {
+        const uint4 rl = R <= KPE_RULE_CHUNK ? myrule : reinterpret_cast<const uint4*>(a.rule_lanes)[c0 + lane];
+        auto block_mask = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> uint64_t {
+          const bool all = mode == MODE_ALL;  // any => OR of filters, all => AND, legacy => its filter
+          uint64_t acc = all ? ~0ull : 0ull;
 #pragma unroll 1
-        for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
-          if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
+          for (uint32_t f = 0; f < nf; ++f) {
+            const KpeFilter fl = filt[f0 + f];
+            uint64_t fm = ~0ull;  // a filter is the AND of its terms
+#pragma unroll 1
+            for (uint32_t k = 0; k < fl.nt; ++k) fm &= tmk[fterm[fl.t0 + k]];
+            acc = all ? (acc & fm) : (acc | fm);
+          }
+          return acc;
+        };
+        const uint32_t handler = RL_HANDLER(rl.x);
+        uint64_t m = live_m;
+        if (rl.w != PRED_NONE) m &= tmk[rl.w];
+        if (m) m &= block_mask(RL_MATCH_MODE(rl.x), RL_F0(rl.y), RL_NF(rl.y));
+        if (m) m &= ~block_mask(RL_EXCL_MODE(rl.x), RL_F0(rl.z), RL_NF(rl.z));
+        uint64_t pm = 0, fm = 0, em = 0;
+        if (handler == H_PSS) {
+          em = m & err_m;
+          fm = m & ~em & cvm[RL_CV(rl.x)];
+          pm = m & ~em & ~fm;
+        } else if (handler == H_ERROR) {
+          em = m;
+        }
+        rmk[lane * 3 + 0] = pm;
+        rmk[lane * 3 + 1] = fm;
+        rmk[lane * 3 + 2] = em;
       }
-      a.masks[r * R + ri] = cmask;
-    }
-    // counters: popcounts of the cell masks, one LDS/global atomic per wave and status
-    if (lane == 0) {
-      const uint32_t cp = (uint32_t)__popcll(pm), cf = (uint32_t)__popcll(fm), ce = (uint32_t)__popcll(em);
-      if (small_r) {
-        if (cp) atomicAdd(&s_cnt[ri * 6 + KPE_PASS_], cp);
-        if (cf) atomicAdd(&s_cnt[ri * 6 + KPE_FAIL_], cf);
-        if (ce) atomicAdd(&s_cnt[ri * 6 + KPE_ERROR_], ce);
-      } else {
-        if (cp) atomicAdd(&a.counts_global[ri * 6 + KPE_PASS_], (unsigned long long)cp);
-        if (cf) atomicAdd(&a.counts_global[ri * 6 + KPE_FAIL_], (unsigned long long)cf);
-        if (ce) atomicAdd(&a.counts_global[ri * 6 + KPE_ERROR_], (unsigned long long)ce);
+      __builtin_amdgcn_wave_barrier();
+      if (a.any_apply_one) {  // ApplyOne: later rules of a policy skip resources already applied
+        if (lane == 0) {
+#pragma unroll 1
+          for (uint32_t j = 0; j < nc; ++j) {
+            const KpeRule rule = a.rules[c0 + j];
+            if (rule.policy != cur_policy) {
+              cur_policy = rule.policy;
+              applied = 0;
+            }
+            uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
+            if (rule.apply_one) {
+              pm &= ~applied, fm &= ~applied, em &= ~applied;
+              rmk[j * 3] = pm, rmk[j * 3 + 1] = fm, rmk[j * 3 + 2] = em;
+            }
+            applied |= pm | fm;
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
       }
-    }
-    // verdict bytes: staged per block in column chunks of <= kStageCols, then stored
-    // as contiguous row segments
-    const uint32_t c0 = ri - ri % kStageCols;
-    s_v[t * cw + (ri - c0)] = (uint8_t)v;
-    const bool chunk_end = ri + 1 == R || ri + 1 - c0 == kStageCols;
-    if (chunk_end) {
-      __syncthreads();
-      const uint32_t w = ri + 1 - c0;  // columns in this chunk
-      if (w == R && (R & 3u) == 0u) {
-        // whole rows, 4-byte aligned: coalesced dword copy of the block's np x R bytes
-        uint32_t* dst = reinterpret_cast<uint32_t*>(a.verdicts + (size_t)p0 * R);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(s_v);
-#pragma unroll 1
-        for (uint32_t i = t; i < np * R / 4; i += kBlock) dst[i] = src[i];
-      } else if (w == R) {
-        uint8_t* dst = a.verdicts + (size_t)p0 * R;
-#pragma unroll 1
-        for (uint32_t i = t; i < np * R; i += kBlock) dst[i] = s_v[i];
-      } else {
-#pragma unroll 1
-        for (uint32_t i = t; i < np * w; i += kBlock) {
-          const uint32_t row = i / w, col = i - row * w;
-          a.verdicts[(size_t)(p0 + row) * R + c0 + col] = s_v[row * cw + col];
+      // (b) counts: popcounts of the cell masks (rule lanes)
+      if (lane < nc) {
+        const uint32_t cp = (uint32_t)__popcll(rmk[lane * 3]), cf = (uint32_t)__popcll(rmk[lane * 3 + 1]),
+                       ce = (uint32_t)__popcll(rmk[lane * 3 + 2]);
+        const uint32_t ri = c0 + lane;
+        if (lds_cnt) {
+          if (cp) atomicAdd(&s_cnt[ri * 3 + 0], cp);
+          if (cf) atomicAdd(&s_cnt[ri * 3 + 1], cf);
+          if (ce) atomicAdd(&s_cnt[ri * 3 + 2], ce);
+        } else {
+          if (cp) atomicAdd(&a.counts_global[ri * 6 + KPE_PASS_], (unsigned long long)cp);
+          if (cf) atomicAdd(&a.counts_global[ri * 6 + KPE_FAIL_], (unsigned long long)cf);
+          if (ce) atomicAdd(&a.counts_global[ri * 6 + KPE_ERROR_], (unsigned long long)ce);
         }
       }
-      __syncthreads();
+      // (c) verdict bytes (resource lanes)
+#pragma unroll 4
+      for (uint32_t j = 0; j < nc; ++j) {
+        const uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
+        const uint32_t v = ((pm >> lane) & 1u) ? KPE_PASS_ : ((fm >> lane) & 1u) ? KPE_FAIL_
+                                                               : ((em >> lane) & 1u) ? KPE_ERROR_ : KPE_NA_;
+        sv[lane * nc + j] = (uint8_t)v;
+      }
+      if (a.masks && live) {
+#pragma unroll 1
+        for (uint32_t j = 0; j < nc; ++j) {
+          uint32_t cmask = 0;
+          if ((rmk[j * 3 + 1] >> lane) & 1u) {
+            const uint32_t f = fails & sld(a.rules, c0 + j).cv_mask;
+#pragma unroll 1
+            for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
+              if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
+          }
+          a.masks[r * R + c0 + j] = cmask;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+      // (d) store the tile's row segments [c0, c0 + nc)
+      uint8_t* base = a.verdicts + (size_t)tile * 64 * R + c0;
+      if (nc == R && (R & 3u) == 0u) {  // whole rows, dword aligned: contiguous nrows x R bytes
+        uint32_t* dst = reinterpret_cast<uint32_t*>(base);
+        const uint32_t* src = reinterpret_cast<const uint32_t*>(sv);
+#pragma unroll 1
+        for (uint32_t i = lane; i < nrows * R / 4; i += 64) dst[i] = src[i];
+      } else if (nc == R) {
+#pragma unroll 1
+        for (uint32_t i = lane; i < nrows * R; i += 64) base[i] = sv[i];
+      } else {
+#pragma clang loop vectorize(disable) unroll(disable)
+        for (uint32_t i = lane; i < nrows * nc; i += 64) {
+          const uint32_t row = i / nc, col = i - row * nc;
+          base[(size_t)row * R + col] = sv[i];
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
     }
   }
-  if (small_r)
+
+  // ---- epilogue: per-block count partials ----
+  if (lds_cnt) {
+    __syncthreads();
 #pragma unroll 1
-    for (uint32_t i = t; i < 6 * R; i += kBlock) a.counts_part[(size_t)blockIdx.x * 6 * R + i] = s_cnt[i];
+    for (uint32_t i = t; i < 6 * R; i += kBlock) {
+      const uint32_t ri = i / 6, k = i - ri * 6;
+      const uint32_t v = k == KPE_PASS_ ? s_cnt[ri * 3] : k == KPE_FAIL_ ? s_cnt[ri * 3 + 1]
+                                                          : k == KPE_ERROR_ ? s_cnt[ri * 3 + 2] : 0u;
+      a.counts_part[(size_t)blockIdx.x * 6 * R + i] = v;
+    }
+  }
 }
 
 
@@ -671,17 +731,32 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipSt
   hipLaunchKernelGGL(kpe_pred_kernel, dim3(nblocks), dim3(256), 0, s, *a);
   return hipGetLastError();
 }
-extern "C" uint32_t kpe_scan_blocks(int64_t n) { return (uint32_t)((n + kBlock - 1) / kBlock); }
-extern "C" size_t kpe_scan_lds_bytes(uint32_t blob_words, uint32_t nterms) {
-  return (size_t)(((blob_words + 1u) & ~1u) + 2u * (kBlock / 64u) * nterms) * 4u;
+// Persistent grid: as many blocks as can be resident at once (occupancy x CUs),
+// capped by the number of 256-resource tiles.
+extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, size_t dyn_bytes) {
+  if (n <= 0) return 0;
+  static thread_local int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  int per_cu = 0;
+  if (pss) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kpe_scan_kernel<true>, kBlock, dyn_bytes) != hipSuccess) per_cu = 1;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kpe_scan_kernel<false>, kBlock, dyn_bytes) != hipSuccess) per_cu = 1;
+  }
+  const int64_t tiles = (n + kBlock - 1) / kBlock;
+  const int64_t g = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
+  return (uint32_t)(g < tiles ? g : tiles);
 }
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, hipStream_t s) {
-  if (a->n == 0) return hipSuccess;
-  const size_t dyn = kpe_scan_lds_bytes(a->blob_words, a->nterms);
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, uint32_t grid, size_t dyn_bytes, hipStream_t s) {
+  if (a->n == 0 || grid == 0) return hipSuccess;
   if (pss)
-    hipLaunchKernelGGL(kpe_scan_kernel<true>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
+    hipLaunchKernelGGL(kpe_scan_kernel<true>, dim3(grid), dim3(kBlock), dyn_bytes, s, *a);
   else
-    hipLaunchKernelGGL(kpe_scan_kernel<false>, dim3(kpe_scan_blocks(a->n)), dim3(kBlock), dyn, s, *a);
+    hipLaunchKernelGGL(kpe_scan_kernel<false>, dim3(grid), dim3(kBlock), dyn_bytes, s, *a);
   return hipGetLastError();
 }
 extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,

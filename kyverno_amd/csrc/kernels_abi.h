@@ -5,7 +5,6 @@
 #include "schema.h"
 
 #define PRED_LOCAL 0x80000000u  // pred_word flag: bitset lives in the scan block's LDS
-#define KPE_SMALL_R 64          // rules counted via LDS ballots + per-block partials
 
 // ScanArgs.need: which columns / lists the compiled program reads
 #define NEED_FLAGS (1u << 0)
@@ -53,6 +52,22 @@ struct PredArgs {
 };
 
 
+// Predicate references in the scan kernel's tables are resolved per binding to
+// bitset locations: PRED_LOCAL | LDS word index, or a pbuf word index; PRED_NONE = absent.
+#define PRED_NONE 0xFFFFFFFFu
+#define KPE_RULE_CHUNK 32  // rules evaluated per transposed pass (one rule per lane)
+#define KPE_LDS_R 256      // rules counted in LDS per block (more: global atomics)
+
+// Rule lane record (uint4, one per rule, evaluated by one lane in the transposed pass):
+//   x = handler | cv_class << 4 | match_mode << 16 | excl_mode << 18
+//   y = match_f0 | match_nf << 24, z = excl_f0 | excl_nf << 24, w = pol_term (PRED_NONE: none)
+#define RL_HANDLER(x) ((x) & 0xFu)
+#define RL_CV(x) (((x) >> 4) & 0xFFFu)
+#define RL_MATCH_MODE(x) (((x) >> 16) & 3u)
+#define RL_EXCL_MODE(x) (((x) >> 18) & 3u)
+#define RL_F0(y) ((y) & 0xFFFFFFu)
+#define RL_NF(y) ((y) >> 24)
+
 struct ScanArgs {
   int64_t n;
   // resource rows (unstructured view) — read by match terms
@@ -70,8 +85,9 @@ struct ScanArgs {
   const uint32_t* capsets;    // capability-set dictionary: 4 words (add lo/hi, drop lo/hi) per set
   uint32_t ncapsets;
   uint32_t nctr_total, nvol_total, nsys_total, npann_total;  // list lengths (load clamping)
-  // program tables (wave-uniform: read with scalar loads)
+  // program tables; predicate fields resolved to bitset locations (binding copies)
   const KpeRule* rules;
+  const uint32_t* rule_lanes;  // packed rule lane records (RL_*)
   const KpeFilter* filters;
   const uint32_t* fterms;
   const KpeTerm* terms;
@@ -79,19 +95,22 @@ struct ScanArgs {
   const KpeAnnPair* annpairs;
   const KpeSelector* selectors;
   const KpeSelReq* selreqs;
-  uint32_t nrules, nterms;
-  // predicate bitsets: pbuf[0, npreds) = directory (PRED_LOCAL | LDS word index, or pbuf
-  // word index); pbuf[npreds, blob_words) = small-domain bitsets, copied into LDS by every
-  // block (same word indices); the rest = large-domain bitsets read from HBM/L2.
+  const uint32_t* cv_classes;  // distinct PSS cv_masks (rule.cv_class indexes them)
+  uint32_t filt_lds, fterm_lds, nfterms;  // filters / filter terms staged in LDS at these word
+                                          // offsets (filt_lds == PRED_NONE: read from HBM)
+  uint32_t nrules, nterms, ncv, any_apply_one;
+  // predicate bitsets: pbuf[0, blob_words) = small-domain bitsets, copied into LDS by
+  // every block (same word indices); the rest = large-domain bitsets (HBM/L2)
   const uint32_t* pbuf;
-  uint32_t blob_words, npreds;
-  uint32_t tm_lds;  // LDS word offset of the per-wave term-mask table (nterms x u64 per wave)
-  int32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
-  int32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
+  uint32_t blob_words;
+  uint32_t wave_lds, wave_words;  // per-wave LDS regions: dyn[wave_lds + wv * wave_words ...]
+  // fixed PSS predicates (resolved locations)
+  uint32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
+  uint32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, need;
   // outputs
   uint8_t* verdicts;                 // n x nrules
   uint32_t* masks;                   // n x nrules or null
-  uint32_t* counts_part;             // blocks x nrules x 6 (nrules <= KPE_SMALL_R)
-  unsigned long long* counts_global; // nrules x 6 (nrules > KPE_SMALL_R)
+  uint32_t* counts_part;             // gridDim x nrules x 6 (nrules <= KPE_LDS_R)
+  unsigned long long* counts_global; // nrules x 6 (nrules > KPE_LDS_R)
 };

@@ -24,10 +24,8 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, hipStream_t s);
-extern "C" size_t kpe_scan_lds_bytes(uint32_t blob_words, uint32_t nterms);
-static inline uint32_t kpe_scan_block_threads() { return 256; }
-extern "C" uint32_t kpe_scan_blocks(int64_t n);
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, uint32_t grid, size_t dyn_bytes, hipStream_t s);
+extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, size_t dyn_bytes);
 extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
                                               unsigned long long* out, hipStream_t s);
 
@@ -80,6 +78,7 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 constexpr uint32_t kMaxLocalWords = 8192;  // 32 KiB of small-domain predicate bitsets
 constexpr uint32_t kMaxDynWords = 13312;   // dynamic LDS per scan block (52 KiB)
 constexpr uint32_t kMaxTerms = 1024;       // distinct match terms (term masks: 8 B x 4 waves each)
+constexpr uint32_t kMaxProgLds = 4096;     // filters + filter terms staged in LDS
 constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
 
 }  // namespace
@@ -112,7 +111,7 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
-  DevBuf rules, filters, fterms, terms, kindsels, annpairs, selectors, selreqs, pat_bytes, pats;
+  DevBuf rules, rule_lanes, filters, fterms, terms, kindsels, annpairs, selectors, selreqs, pat_bytes, pats;
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
@@ -121,7 +120,11 @@ struct DeviceProgram {
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
   const Program* prog = nullptr;
   DevBuf jobs, pbuf, verdicts, masks, counts_part, counts_global, counts_out;
-  uint32_t nblocks = 0, njobs = 0, blob_words = 0, img_words = 0, scan_blocks = 0;
+  DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
+  uint32_t pp[10] = {};  // fixed PSS predicate locations
+  uint32_t wave_lds = 0, wave_words = 0, filt_lds = PRED_NONE, fterm_lds = 0;
+  size_t dyn_bytes = 0;
+  uint32_t nblocks = 0, njobs = 0, blob_words = 0, scan_blocks = 0;
   uint32_t need = 0;
   double scan_bytes = 0;
   size_t cells = 0;
@@ -322,6 +325,15 @@ void append_words(std::vector<uint32_t>& img, const std::vector<T>& v, uint32_t*
 kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   auto& P = *pp->p;
   if (P.dev && P.dev->ordinal == dev->ordinal) return KPE_OK;
+  std::vector<uint32_t> lanes;  // rule lane records (kernels_abi.h RL_*)
+  for (auto& r : P.rules) {
+    if (r.match_nf > 255 || r.excl_nf > 255 || r.match_f0 > 0xFFFFFF || r.excl_f0 > 0xFFFFFF || r.cv_class > 0xFFF)
+      return fail(KPE_E_LIMIT, "rule exceeds the device rule encoding (filters per block <= 255)");
+    lanes.push_back(r.handler | r.cv_class << 4 | r.match_mode << 16 | r.excl_mode << 18);
+    lanes.push_back(r.match_f0 | r.match_nf << 24);
+    lanes.push_back(r.excl_f0 | r.excl_nf << 24);
+    lanes.push_back(r.pol_term < 0 ? PRED_NONE : (uint32_t)r.pol_term);
+  }
   delete P.dev;
   P.dev = new kpe::DeviceProgram();
   auto& D = *P.dev;
@@ -336,6 +348,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     for (auto& g : pr.globs) D.pats_h.push_back(classify_pattern(g, D.pat_bytes_h));
   }
   HIPCHK(upload(D.rules, P.rules, s));
+  HIPCHK(upload(D.rule_lanes, lanes, s));
   HIPCHK(upload(D.filters, P.filters, s));
   HIPCHK(upload(D.fterms, P.fterms, s));
   HIPCHK(upload(D.terms, P.terms, s));
@@ -374,7 +387,7 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   return need;
 }
-double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
+double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks, uint32_t grid_blocks) {
   double b = 0;
   const double n = (double)C.n;
   if (P.any_pss) {
@@ -395,7 +408,7 @@ double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bo
   if (need & NEED_LAB) b += 4.0 * n + 8.0 * C.lab_k.size();
   if (need & NEED_NSL) b += 4.0 * n;  // r_nsl; the namespace table itself is cache-resident
   b += n * P.rules.size() * (masks ? 5.0 : 1.0);  // verdict cells (+ check masks)
-  if (P.rules.size() <= KPE_SMALL_R) b += 4.0 * kpe_scan_blocks(C.n) * 6 * P.rules.size();
+  if (P.rules.size() <= KPE_LDS_R) b += 4.0 * grid_blocks * 6 * P.rules.size();  // count partials
   return b;
 }
 
@@ -410,12 +423,19 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   // Preamble layout (pbuf): [program image][predicate directory][small-domain bitsets]
   // (padded to 16 B; copied into LDS by every scan block) followed by the large-domain
   // bitsets. Every predicate is evaluated by the dictionary pass straight into pbuf.
-  const uint32_t img = 0;  // program tables are read with scalar loads, not staged
+  // pbuf: [small-domain bitsets (copied into LDS by every scan block)][large-domain
+  // bitsets]. Predicate references in the scan tables are resolved to these locations.
+  // Dynamic LDS per scan block: [bitsets][filters + filter terms][4 per-wave regions].
   const uint32_t npreds = (uint32_t)P.preds.size();
-  const uint32_t nterms = (uint32_t)P.terms.size();
+  const uint32_t nterms = (uint32_t)P.terms.size(), ncv = (uint32_t)P.cv_classes.size();
   if (nterms > kMaxTerms) return fail(KPE_E_LIMIT, "program has more than 1024 distinct match terms");
-  const int64_t budget = (int64_t)kMaxDynWords - 2 * (kpe_scan_block_threads() / 64) * nterms - npreds - 8;
-  const uint32_t local_budget = (uint32_t)std::max<int64_t>(0, std::min<int64_t>(kMaxLocalWords, budget));
+  const uint32_t wave_words = 2 * nterms + 2 * ncv + 2 * 3 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4;
+  const uint32_t prog_words = 2 * (uint32_t)P.filters.size() + (uint32_t)P.fterms.size();
+  const bool stage_prog = prog_words <= kMaxProgLds;
+  const int64_t budget =
+      (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8;
+  if (budget < 0) return fail(KPE_E_LIMIT, "program does not fit the scan kernel's LDS budget");
+  const uint32_t local_budget = (uint32_t)std::min<int64_t>(kMaxLocalWords, budget);
   std::vector<uint32_t> nwords(npreds);
   std::vector<char> local(npreds, 0);
   uint32_t lw = 0;
@@ -427,10 +447,10 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
       lw += nwords[p];
     }
   }
-  const uint32_t blob = std::max(4u, (img + npreds + lw + 3) & ~3u);
+  const uint32_t blob = std::max(4u, (lw + 3) & ~3u);
   std::vector<uint32_t> dir(npreds);
   std::vector<PredJob> jobs;
-  uint32_t lo = img + npreds, go = blob, blk = 0;
+  uint32_t lo = 0, go = blob, blk = 0;
   for (uint32_t p = 0; p < npreds; ++p) {
     uint32_t at;
     if (local[p]) {
@@ -449,15 +469,44 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
       blk += (n + 255) / 256;
     }
   }
+  auto loc = [&](int32_t p) -> uint32_t { return p < 0 ? PRED_NONE : dir[(size_t)p]; };
+  std::vector<KpeTerm> terms = P.terms;
+  for (auto& t : terms)
+    if (t.type == T_KIND_PRED || t.type == T_PRED) t.a = loc((int32_t)t.a);
+  std::vector<KpeKindSel> kindsels = P.kindsels;
+  for (auto& k : kindsels) {
+    k.pg = (int32_t)loc(k.pg);
+    k.pv = (int32_t)loc(k.pv);
+    k.pk = (int32_t)loc(k.pk);
+  }
+  std::vector<KpeAnnPair> annpairs = P.annpairs;
+  for (auto& x : annpairs) x.pk = (int32_t)loc(x.pk), x.pv = (int32_t)loc(x.pv);
+  std::vector<KpeSelector> selectors = P.selectors;
+  for (auto& x : selectors) x.p_kind_ns = (int32_t)loc(x.p_kind_ns), x.p_kind_empty = (int32_t)loc(x.p_kind_empty);
+  std::vector<KpeSelReq> selreqs = P.selreqs;
+  for (auto& x : selreqs)
+    x.pk = (int32_t)loc(x.pk), x.pv = (int32_t)loc(x.pv), x.pk_ok = (int32_t)loc(x.pk_ok), x.pv_ok = (int32_t)loc(x.pv_ok);
+  HIPCHK(upload(B.terms_r, terms, s));
+  HIPCHK(upload(B.kindsels_r, kindsels, s));
+  HIPCHK(upload(B.annpairs_r, annpairs, s));
+  HIPCHK(upload(B.selectors_r, selectors, s));
+  HIPCHK(upload(B.selreqs_r, selreqs, s));
+  HIPCHK(upload(B.cv_classes, P.cv_classes, s));
+  const auto& ps = P.pss;
+  const int32_t fixed[10] = {ps.apparmor_key, ps.apparmor_val_ok, ps.seccomp_pod_key, ps.seccomp_ann_ok,
+                             ps.caps_baseline_ok, ps.cap_nbs, ps.cap_all, ps.sysctl[0], ps.sysctl[1], ps.sysctl[2]};
+  for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
+  B.filt_lds = stage_prog ? blob : PRED_NONE;
+  B.fterm_lds = blob + 2 * (uint32_t)P.filters.size();
+  B.wave_lds = (blob + (stage_prog ? prog_words : 0) + 1) & ~1u;
+  B.wave_words = wave_words;
+  B.dyn_bytes = (size_t)(B.wave_lds + 4 * wave_words) * 4;
   HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
   HIPCHK(hipMemsetAsync(B.pbuf.p, 0, (size_t)go * 4 + 16, s));
-  if (npreds)
-    HIPCHK(hipMemcpyAsync(B.pbuf.as<uint32_t>() + img, dir.data(), (size_t)npreds * 4, hipMemcpyHostToDevice, s));
   B.blob_words = blob;
-  B.img_words = img;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  B.scan_blocks = kpe_scan_blocks(C.n);
+  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
   size_t width = P.rules.size() * 6;
@@ -504,7 +553,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     pa.out = B.pbuf.as<uint32_t>();
     HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
   }
-  if (R > KPE_SMALL_R) HIPCHK(hipMemsetAsync(B.counts_global.p, 0, R * 6 * 8, s));
+  if (R > KPE_LDS_R) HIPCHK(hipMemsetAsync(B.counts_global.p, 0, R * 6 * 8, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   ScanArgs sa{};
   sa.n = C.n;
@@ -536,39 +585,46 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.nsys_total = (uint32_t)C.sys_id.size();
   sa.npann_total = (uint32_t)(C.pann_kv.size() / 2);
   sa.rules = PD.rules.as<KpeRule>();
+  sa.rule_lanes = PD.rule_lanes.as<uint32_t>();
   sa.nrules = (uint32_t)R;
   sa.filters = PD.filters.as<KpeFilter>();
-  sa.terms = PD.terms.as<KpeTerm>();
-  sa.kindsels = PD.kindsels.as<KpeKindSel>();
-  sa.annpairs = PD.annpairs.as<KpeAnnPair>();
-  sa.selectors = PD.selectors.as<KpeSelector>();
-  sa.selreqs = PD.selreqs.as<KpeSelReq>();
+  sa.fterms = PD.fterms.as<uint32_t>();
+  sa.terms = B.terms_r.as<KpeTerm>();
+  sa.kindsels = B.kindsels_r.as<KpeKindSel>();
+  sa.annpairs = B.annpairs_r.as<KpeAnnPair>();
+  sa.selectors = B.selectors_r.as<KpeSelector>();
+  sa.selreqs = B.selreqs_r.as<KpeSelReq>();
+  sa.cv_classes = B.cv_classes.as<uint32_t>();
+  sa.nterms = (uint32_t)P.terms.size();
+  sa.ncv = (uint32_t)P.cv_classes.size();
+  sa.any_apply_one = P.any_apply_one ? 1u : 0u;
+  sa.filt_lds = B.filt_lds;
+  sa.fterm_lds = B.fterm_lds;
+  sa.nfterms = (uint32_t)P.fterms.size();
   sa.pbuf = B.pbuf.as<uint32_t>();
   sa.blob_words = B.blob_words;
-  sa.npreds = (uint32_t)P.preds.size();
-  sa.fterms = PD.fterms.as<uint32_t>();
-  sa.nterms = (uint32_t)P.terms.size();
-  sa.tm_lds = (B.blob_words + 1u) & ~1u;
-  sa.pp_apparmor_key = P.pss.apparmor_key;
-  sa.pp_apparmor_ok = P.pss.apparmor_val_ok;
-  sa.pp_seccomp_pod_key = P.pss.seccomp_pod_key;
-  sa.pp_seccomp_ann_ok = P.pss.seccomp_ann_ok;
-  sa.pp_caps_ok = P.pss.caps_baseline_ok;
-  sa.pp_cap_nbs = P.pss.cap_nbs;
-  sa.pp_cap_all = P.pss.cap_all;
-  sa.pp_sysctl0 = P.pss.sysctl[0];
-  sa.pp_sysctl1 = P.pss.sysctl[1];
-  sa.pp_sysctl2 = P.pss.sysctl[2];
+  sa.wave_lds = B.wave_lds;
+  sa.wave_words = B.wave_words;
+  sa.pp_apparmor_key = B.pp[0];
+  sa.pp_apparmor_ok = B.pp[1];
+  sa.pp_seccomp_pod_key = B.pp[2];
+  sa.pp_seccomp_ann_ok = B.pp[3];
+  sa.pp_caps_ok = B.pp[4];
+  sa.pp_cap_nbs = B.pp[5];
+  sa.pp_cap_all = B.pp[6];
+  sa.pp_sysctl0 = B.pp[7];
+  sa.pp_sysctl1 = B.pp[8];
+  sa.pp_sysctl2 = B.pp[9];
   sa.cv_union = P.cv_union;
   sa.need = B.need;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   sa.counts_part = B.counts_part.as<uint32_t>();
   sa.counts_global = B.counts_global.as<unsigned long long>();
-  HIPCHK(kpe_launch_scan(&sa, P.any_pss ? 1 : 0, s));
+  HIPCHK(kpe_launch_scan(&sa, P.any_pss ? 1 : 0, B.scan_blocks, B.dyn_bytes, s));
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.c, s));
-    ev.bytes = scan_bytes(P, C, B.need, masks);
+    ev.bytes = scan_bytes(P, C, B.need, masks, B.scan_blocks);
     dev->pending.push_back(ev);
   }
   return KPE_OK;
@@ -613,7 +669,7 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
   hipStream_t s = dev->stream;
   if (counts && R) {
     const unsigned long long* src = B.counts_global.as<unsigned long long>();
-    if (R <= KPE_SMALL_R) {
+    if (R <= KPE_LDS_R) {
       HIPCHK(kpe_launch_count_reduce(B.counts_part.as<uint32_t>(), B.scan_blocks, (uint32_t)(R * 6),
                                      B.counts_out.as<unsigned long long>(), s));
       src = B.counts_out.as<unsigned long long>();

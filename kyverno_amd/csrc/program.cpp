@@ -898,9 +898,13 @@ class Lowerer {
       pss_preds();
       P.any_pss = true;
       P.cv_union |= k.cv_mask;
+      auto it = std::find(P.cv_classes.begin(), P.cv_classes.end(), k.cv_mask);
+      k.cv_class = (uint32_t)(it - P.cv_classes.begin());
+      if (it == P.cv_classes.end()) P.cv_classes.push_back(k.cv_mask);
     } else {
       throw CompileError("rule '" + rname + "': only podSecurity validate rules are supported on the device yet");
     }
+    if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
     P.rule_names.push_back(pol_name + "/" + rname);
   }

@@ -41,6 +41,8 @@ struct Program {
   std::vector<Pred> preds;
   PssPreds pss;
   uint32_t cv_union = 0;  // union of cv_mask over rules
+  std::vector<uint32_t> cv_classes;  // distinct cv_masks of PSS rules
+  bool any_apply_one = false;
   bool any_pss = false;
   DeviceProgram* dev = nullptr;
   ~Program();

@@ -300,5 +300,6 @@ typedef struct KpeRule {
   uint32_t policy;        // policy index (ApplyOne grouping)
   uint32_t apply_one;     // spec.applyRules == One
   uint32_t pss_excl0, pss_nexcl;  // PSS exclusions (reserved)
-  uint32_t pad[3];        // 16 words: one scalar dwordx16 load per rule
+  uint32_t cv_class;      // PSS: index of cv_mask among the program's distinct cv_masks
+  uint32_t pad[2];        // 16 words
 } KpeRule;
