@@ -25,6 +25,31 @@ namespace kpe {
 
 namespace {
 
+// c_sc enum word -> state bitmap (schema.h CX_*): one bit per state of each field.
+uint32_t state_bitmap(uint32_t w) {
+  auto tri = [&](uint32_t sh, uint32_t t, uint32_t f, uint32_t u) {
+    const uint32_t v = FIELD(w, sh, 2);
+    return v == TRI_TRUE ? t : v == TRI_FALSE ? f : u;
+  };
+  uint32_t x = tri(C_PRIV_SH, CX_PRIV_T, CX_PRIV_F, CX_PRIV_U) | tri(C_APE_SH, CX_APE_T, CX_APE_F, CX_APE_U) |
+               tri(C_RNR_SH, CX_RNR_T, CX_RNR_F, CX_RNR_U);
+  const uint32_t rau = FIELD(w, C_RAU_SH, 2);
+  x |= rau == RAU_ZERO ? CX_RAU_Z : rau == RAU_NONZERO ? CX_RAU_NZ : CX_RAU_U;
+  static const uint32_t sec[5] = {CX_SEC_NONE, CX_SEC_RD, CX_SEC_LH, CX_SEC_UNC, CX_SEC_OTHER};
+  x |= sec[std::min(FIELD(w, C_SECCOMP_SH, 3), 4u)];
+  const uint32_t pm = FIELD(w, C_PROCMOUNT_SH, 2);
+  x |= pm == PROCMOUNT_OTHER ? CX_PM_OTHER : pm == PROCMOUNT_DEFAULT ? CX_PM_DEFAULT : CX_PM_U;
+  const uint32_t sel = FIELD(w, C_SEL_SH, 3);
+  x |= sel == SEL_NONE ? CX_SEL_NONE : sel == SEL_OTHER ? CX_SEL_OTHER : CX_SEL_OK;
+  if (w & C_SEL_USER) x |= CX_SEL_USER;
+  if (w & C_SEL_ROLE) x |= CX_SEL_ROLE;
+  x |= FIELD(w, C_WHP_SH, 2) == TRI_TRUE ? CX_WHP_T : CX_WHP_NT;
+  x |= (w & C_CAPS_PRESENT) ? CX_CAPS : CX_NOCAPS;
+  x |= FIELD(w, C_HOSTPORT_SH, 4) ? CX_HOSTPORT : CX_NOHOSTPORT;
+  if (w & C_SC_PRESENT) x |= CX_SC;
+  return x;
+}
+
 struct CtrView {
   std::string name, image;
   bool sc = false;
@@ -921,6 +946,7 @@ class Flattener {
   uint64_t last_mask_ = 0;
 
   void emit(uint32_t cls, bool derr) {
+    if (C.n >= 0x7FFFFFC0) throw LimitError("more than 2^31 - 64 resources in one corpus (32-bit row ids)");
     // ---- resource row (unstructured view) ----
     std::string group, version;
     size_t sl = u.api_version.find('/');
@@ -1032,8 +1058,8 @@ class Flattener {
           } else {
             cs = it->second;
           }
-          C.crec.push_back(w);
-          C.crec.push_back(cs);
+          C.crec.push_back(state_bitmap(w));
+          C.crec.push_back(cs | (ct << 16));
         }
         C.c_name.push_back(C.dict[D_CNAME].intern(c.name));
         C.c_image.push_back(C.dict[D_IMAGE].intern(c.image));
@@ -1125,6 +1151,11 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
     if (b > a) fl.add(buf + a, buf + b);
     i = j + 1;
   }
+  // sentinel wave header: list ends of the last tile (tile t's lists are [hdr[t], hdr[t+1]))
+  C.hdr.push_back((uint32_t)C.c_sc.size());
+  C.hdr.push_back((uint32_t)C.vol_src.size());
+  C.hdr.push_back((uint32_t)C.sys_id.size());
+  C.hdr.push_back((uint32_t)(C.pann_kv.size() / 2));
 }
 
 bool is_limit_error(const std::exception& e) { return dynamic_cast<const LimitError*>(&e) != nullptr; }

@@ -4,23 +4,25 @@
 //                      program (an OR of go-wildcard globs, ext/wildcard/match.go:7-9)
 //                      is evaluated once per DISTINCT string of its domain into a
 //                      bitset (one wave = 64 dictionary ids, built with a ballot).
-//                      Patterns are host-classified (exact / prefix / suffix /
-//                      contains / general glob) so the common cases are straight
-//                      byte compares without backtracking.
-//  kpe_scan_kernel   — one resource per lane. Per block: (1) the compiled program,
-//                      the predicate directory and the small-domain bitsets are
-//                      copied into LDS; (2) the block's containers are streamed
-//                      coalesced through LDS and OR-reduced per resource (the
-//                      1..64-container fan-out never diverges the HBM loads);
-//                      (3) PSA versioned checks (pkg/pss/evaluate.go:24-70 over the
-//                      PSA v0.29 policy/check_*.go semantics); (4) match/exclude per
-//                      rule (pkg/engine/utils/match.go:168-300) with ApplyOne
-//                      (pkg/engine/validation.go:75-77); (5) verdict cells staged in
-//                      LDS and written as coalesced dwords; per-rule counters by
-//                      wave ballot into per-block partials (no atomics, no memset).
-//  kpe_count_reduce  — sums the per-block counter partials (fetch time only).
+//                      Each block stages its 256 strings and the pattern bytes in
+//                      LDS first, so the byte-serial compares never wait on HBM/L2.
+//  kpe_scan_kernel   — one resource per lane, persistent wave-autonomous 64-row
+//                      tiles: (1) PSS: list offsets from a DPP wave scan, the pod's
+//                      container state bitmaps OR-ed (schema.h CX_*), the PSA
+//                      versioned checks decided once per pod (pkg/pss/evaluate.go:24-70
+//                      over the PSA v0.29 check semantics); (2) distinct match terms once
+//                      per resource; (3) rules: NARROW programs (<= 32 terms and rules)
+//                      run a per-lane rule loop over term bits, WIDE programs a
+//                      transposed pass (one rule per lane, 64-bit cell masks); match /
+//                      exclude pkg/engine/utils/match.go:168-300, ApplyOne
+//                      pkg/engine/validation.go:75-77; (4) verdict cells staged per wave
+//                      in LDS and stored as contiguous row segments.
+//  kpe_count_kernel  — per-rule status histogram of a verdict matrix (the CLI totals
+//                      of cmd/cli/kubectl-kyverno/processor/result.go:34-68); fetch time.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <algorithm>
 
 #include "kernels_abi.h"
 #include "schema.h"
@@ -64,9 +66,16 @@ __device__ bool glob(const uint8_t* p, int pn, const uint8_t* s, int sn) {
 }
 
 __device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int n) {
-  for (int i = 0; i < n; ++i)
-    if (a[i] != b[i]) return false;
-  return true;
+  int i = 0;
+  for (; i + 8 <= n; i += 8) {  // 8 independent byte loads per step: short dependence chains
+    uint32_t d = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d |= (uint32_t)(a[i + k] ^ b[i + k]);
+    if (d) return false;
+  }
+  uint32_t d = 0;
+  for (; i < n; ++i) d |= (uint32_t)(a[i] ^ b[i]);
+  return d == 0;
 }
 
 // k8s.io/apimachinery v0.29.1 util/validation (IsQualifiedName / IsValidLabelValue)
@@ -123,138 +132,6 @@ __device__ bool pat_match(const KpePat& pt, const uint8_t* pb, const uint8_t* s,
   }
 }
 
-}  // namespace
-
-// ---------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) kpe_pred_kernel(PredArgs a) {
-  uint32_t b = blockIdx.x;
-  uint32_t j = 0;
-  while (j + 1 < a.njobs && a.jobs[j + 1].blk0 <= b) ++j;  // uniform per block
-  const PredJob job = a.jobs[j];
-  const uint32_t id = (b - job.blk0) * 256u + threadIdx.x;
-  const uint32_t n = a.dict_n[job.domain];
-  bool hit = false;
-  if (id < n) {
-    const uint32_t* off = a.dict_off[job.domain];
-    const uint8_t* s = a.dict_bytes[job.domain] + off[id];
-    const int sn = (int)(off[id + 1] - off[id]);
-    for (uint32_t k = 0; k < job.npat && !hit; ++k) hit = pat_match(a.pats[job.pat0 + k], a.pat_bytes, s, sn);
-  }
-  const uint64_t m = __ballot(hit);
-  const uint32_t wid = id >> 6;  // 64 strings per wave => two output words
-  if ((threadIdx.x & 63u) == 0 && (uint64_t)wid * 64u < n) {
-    a.out[job.out_word + 2 * wid] = (uint32_t)m;
-    a.out[job.out_word + 2 * wid + 1] = (uint32_t)(m >> 32);
-  }
-}
-
-// one block per counter column; coalesced over blocks-of-partials
-__global__ void __launch_bounds__(256) kpe_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
-                                                        unsigned long long* out) {
-  __shared__ unsigned long long red[256];
-  const uint32_t col = blockIdx.x;
-  unsigned long long s = 0;
-  for (uint32_t b = threadIdx.x; b < nblocks; b += 256) s += part[(size_t)b * width + col];
-  red[threadIdx.x] = s;
-  __syncthreads();
-  for (uint32_t k = 128; k > 0; k >>= 1) {
-    if (threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) out[col] = red[0];
-}
-
-// ---------------------------------------------------------------------------
-namespace {
-
-constexpr uint32_t kBlock = 256;
-constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
-                                     (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
-                                     (1u << VS_PROJECTED) | (1u << VS_SECRET);
-
-__constant__ uint8_t kCvCheck[KPE_NUM_CV] = {
-    CK_APE, CK_APE, CK_APPARMOR, CK_CAPS_BASELINE, CK_CAPS_RESTRICTED, CK_CAPS_RESTRICTED, CK_HOST_NS,
-    CK_HOST_PATH, CK_HOST_PORTS, CK_PRIVILEGED, CK_PROC_MOUNT, CK_RESTRICTED_VOLUMES, CK_RUN_AS_NON_ROOT,
-    CK_RUN_AS_USER, CK_SELINUX, CK_SECCOMP_BASELINE, CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED,
-    CK_SECCOMP_RESTRICTED, CK_SYSCTLS, CK_SYSCTLS, CK_SYSCTLS, CK_WIN_HOST_PROCESS};
-
-// PSA versioned checks for one pod given the OR of its container bits.
-__device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t cb, bool vol_hostpath, bool vol_restricted,
-                                             uint32_t sys_bad, bool apparmor_bad, bool sec_pod_ann_bad) {
-  uint32_t f = 0;
-  const bool win = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS;
-  if (cb & CB_APE) f |= (1u << CV_APE_1_8) | (win ? 0u : (1u << CV_APE_1_25));
-  if (apparmor_bad) f |= 1u << CV_APPARMOR_1_0;
-  if (cb & CB_CAPS_BASE) f |= 1u << CV_CAPS_BASELINE_1_0;
-  if (cb & (CB_CAPS_DROP | CB_CAPS_ADD))
-    f |= (1u << CV_CAPS_RESTRICTED_1_22) | (win ? 0u : (1u << CV_CAPS_RESTRICTED_1_25));
-  if (pw & (P_HOSTNET | P_HOSTPID | P_HOSTIPC)) f |= 1u << CV_HOST_NS_1_0;
-  if (vol_hostpath) f |= 1u << CV_HOST_PATH_1_0;
-  if (cb & CB_HOSTPORT) f |= 1u << CV_HOST_PORTS_1_0;
-  if (cb & CB_PRIV) f |= 1u << CV_PRIVILEGED_1_0;
-  if (cb & CB_PROCMOUNT) f |= 1u << CV_PROC_MOUNT_1_0;
-  if (vol_restricted) f |= 1u << CV_RESTRICTED_VOLUMES_1_0;
-  const uint32_t prnr = FIELD(pw, P_RNR_SH, 2);
-  if (prnr == TRI_FALSE || (cb & CB_RNR_FALSE) || (prnr != TRI_TRUE && (cb & CB_RNR_UNSET)))
-    f |= 1u << CV_RUN_AS_NON_ROOT_1_0;
-  if (FIELD(pw, P_RAU_SH, 2) == RAU_ZERO || (cb & CB_RAU_ZERO)) f |= 1u << CV_RUN_AS_USER_1_23;
-  const uint32_t psel = FIELD(pw, P_SEL_SH, 3);
-  if ((psel != SEL_NONE && (psel == SEL_OTHER || (pw & (P_SEL_USER | P_SEL_ROLE)))) || (cb & CB_SELINUX))
-    f |= 1u << CV_SELINUX_1_0;
-  if (sec_pod_ann_bad || (cb & CB_SEC_ANN)) f |= 1u << CV_SECCOMP_BASELINE_1_0;
-  const uint32_t psec = FIELD(pw, P_SECCOMP_SH, 3);
-  const bool psec_valid = psec == SECCOMP_RUNTIMEDEFAULT || psec == SECCOMP_LOCALHOST;
-  const bool psec_bad = psec != SECCOMP_NONE && !psec_valid;
-  if (psec_bad || (cb & CB_SEC_BAD)) f |= 1u << CV_SECCOMP_BASELINE_1_19;
-  if (psec_bad || (cb & CB_SEC_BAD) || (!psec_valid && (cb & CB_SEC_UNSET)))
-    f |= (1u << CV_SECCOMP_RESTRICTED_1_19) | (win ? 0u : (1u << CV_SECCOMP_RESTRICTED_1_25));
-  if (sys_bad & 1u) f |= 1u << CV_SYSCTLS_1_0;
-  if (sys_bad & 2u) f |= 1u << CV_SYSCTLS_1_27;
-  if (sys_bad & 4u) f |= 1u << CV_SYSCTLS_1_29;
-  if (FIELD(pw, P_WHP_SH, 2) == TRI_TRUE || (cb & CB_WHP)) f |= 1u << CV_WIN_HOST_PROCESS_1_0;
-  return f;
-}
-
-}  // namespace
-
-// Capability-set violation bits (computed per block into LDS from the capset dictionary)
-#define CS_BASE 1u  // add has a capability outside the baseline allow-list
-#define CS_DROP 2u  // drop lacks "ALL"
-#define CS_ADD 4u   // add has anything but NET_BIND_SERVICE
-
-__device__ __forceinline__ uint32_t ctr_bits(uint32_t w, uint32_t csb) {
-  uint32_t b = 0;
-  const bool caps = w & C_CAPS_PRESENT;
-  if (caps && (csb & CS_BASE)) b |= CB_CAPS_BASE;
-  if (!caps || (csb & CS_DROP)) b |= CB_CAPS_DROP;
-  if (caps && (csb & CS_ADD)) b |= CB_CAPS_ADD;
-  if (FIELD(w, C_APE_SH, 2) != TRI_FALSE) b |= CB_APE;
-  if (FIELD(w, C_HOSTPORT_SH, 4)) b |= CB_HOSTPORT;
-  if (FIELD(w, C_PRIV_SH, 2) == TRI_TRUE) b |= CB_PRIV;
-  if (FIELD(w, C_PROCMOUNT_SH, 2) == PROCMOUNT_OTHER) b |= CB_PROCMOUNT;
-  const uint32_t rnr = FIELD(w, C_RNR_SH, 2);
-  if (rnr == TRI_FALSE) b |= CB_RNR_FALSE;
-  if (rnr == TRI_UNSET) b |= CB_RNR_UNSET;
-  if (FIELD(w, C_RAU_SH, 2) == RAU_ZERO) b |= CB_RAU_ZERO;
-  const uint32_t sel = FIELD(w, C_SEL_SH, 3);
-  if (sel != SEL_NONE && (sel == SEL_OTHER || (w & (C_SEL_USER | C_SEL_ROLE)))) b |= CB_SELINUX;
-  const uint32_t sec = FIELD(w, C_SECCOMP_SH, 3);
-  if (sec == SECCOMP_NONE) b |= CB_SEC_UNSET;
-  else if (sec != SECCOMP_RUNTIMEDEFAULT && sec != SECCOMP_LOCALHOST) b |= CB_SEC_BAD;
-  if (FIELD(w, C_WHP_SH, 2) == TRI_TRUE) b |= CB_WHP;
-  return b;
-}
-
-__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
-  const uint32_t lane = threadIdx.x & 63u;
-#pragma unroll
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    if (lane >= d) x += y;
-  }
-  return x;
-}
-
 // Wave-uniform table read: the address is uniform, so this is a scalar (SMEM) load
 // through the constant cache — no LDS round trip and no readfirstlane to branch on it.
 template <class T>
@@ -268,18 +145,197 @@ __device__ __forceinline__ T sld(const T* p, uint32_t i) {
   for (uint32_t k = 0; k < sizeof(T) / 4; ++k) d[k] = src[k];
   return out;
 }
-__device__ __forceinline__ uint64_t uniform64(uint64_t x) {
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)x);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32));
-  return (uint64_t)lo | ((uint64_t)hi << 32);
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+constexpr uint32_t kPredStrLds = 16384;  // staged dictionary bytes per block
+constexpr uint32_t kPredPatLds = 4096;   // staged pattern bytes
+constexpr uint32_t kPredPats = 64;       // staged pattern records per job
+
+// Grid (x, y): job y (one predicate over one domain), strings [256 x, 256 x + 256).
+// Every input of the block's compares is staged in LDS in one round (the job's
+// pattern records and bytes, the block's strings), so no compare waits on HBM/L2.
+__global__ void __launch_bounds__(256) kpe_pred_kernel(PredArgs a) {
+  __shared__ __attribute__((aligned(16))) uint8_t s_str[kPredStrLds];
+  __shared__ __attribute__((aligned(16))) uint8_t s_pat[kPredPatLds];
+  __shared__ KpePat s_pats[kPredPats];
+  const uint32_t t = threadIdx.x;
+  const PredJob job = sld(a.jobs, blockIdx.y);
+  const uint32_t n = a.dict_n[job.domain];
+  const uint32_t id0 = blockIdx.x * 256u;
+  if (id0 >= n) return;  // uniform: this job has fewer blocks than the grid's x extent
+  const uint32_t* off = a.dict_off[job.domain];
+  const uint8_t* bytes = a.dict_bytes[job.domain];
+  const uint32_t idh = min(id0 + 256u, n);
+  const uint32_t lo = off[id0], hi = off[idh];
+  const uint32_t id = id0 + t;
+  const uint32_t o0 = id < n ? off[id] : 0u, o1 = id < n ? off[id + 1] : 0u;
+  const bool str_lds = hi - lo <= kPredStrLds;
+  const bool pat_lds = a.pat_len <= kPredPatLds && job.npat <= kPredPats;
+  if (str_lds)
+    for (uint32_t i = t; i < hi - lo; i += 256) s_str[i] = bytes[lo + i];
+  if (pat_lds) {
+    for (uint32_t i = t; i < a.pat_len; i += 256) s_pat[i] = a.pat_bytes[i];
+    if (t < job.npat) s_pats[t] = a.pats[job.pat0 + t];
+  }
+  __syncthreads();
+  bool hit = false;
+  if (id < n) {
+    const uint8_t* s = str_lds ? s_str + (o0 - lo) : bytes + o0;
+    const int sn = (int)(o1 - o0);
+    if (pat_lds) {
+      for (uint32_t k = 0; k < job.npat && !hit; ++k) hit = pat_match(s_pats[k], s_pat, s, sn);
+    } else {
+      for (uint32_t k = 0; k < job.npat && !hit; ++k) hit = pat_match(a.pats[job.pat0 + k], a.pat_bytes, s, sn);
+    }
+  }
+  const uint64_t m = __ballot(hit);
+  const uint32_t wid = id >> 6;  // 64 strings per wave => two output words
+  if ((t & 63u) == 0 && (uint64_t)wid * 64u < n) {
+    a.out[job.out_word + 2 * wid] = (uint32_t)m;
+    a.out[job.out_word + 2 * wid + 1] = (uint32_t)(m >> 32);
+  }
+}
+
+// Per-rule status histogram of a row-major N x R verdict matrix. Each wave takes
+// 64 rows at a time; per rule, one ballot per status, lane 0 accumulates in LDS;
+// one 64-bit global add per (rule, status) and block at the end.
+__global__ void __launch_bounds__(256) kpe_count_kernel(const uint8_t* v, int64_t n, uint32_t R, uint32_t r0,
+                                                        uint32_t rn, unsigned long long* out) {
+  extern __shared__ uint32_t hist[];  // rules [r0, r0 + rn) x 6
+  const uint32_t t = threadIdx.x, lane = t & 63u;
+  for (uint32_t i = t; i < rn * 6; i += 256) hist[i] = 0;
+  __syncthreads();
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t tile = (int64_t)blockIdx.x * 4 + (t >> 6); tile * 64 < n; tile += nw) {
+    const int64_t row = tile * 64 + lane;
+    const bool live = row < n;
+    for (uint32_t r = 0; r < rn; ++r) {
+      const uint32_t c = live ? v[row * R + r0 + r] : 0u;
+#pragma unroll
+      for (uint32_t s = 1; s < 6; ++s) {
+        const uint32_t k = (uint32_t)__popcll(__ballot(c == s));
+        if (lane == 0 && k) atomicAdd(&hist[r * 6 + s], k);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t i = t; i < rn * 6; i += 256)
+    if (hist[i]) atomicAdd(&out[(size_t)r0 * 6 + i], (unsigned long long)hist[i]);
+}
+
+// ---------------------------------------------------------------------------
+namespace {
+
+constexpr uint32_t kBlock = 256;
+// Diagnostic builds only (scripts/diag_variants.sh): phases skipped to time the others.
+#ifndef KPE_DIAG
+#define KPE_DIAG 0
+#endif
+#define DIAG_NOPRO 1u    // no fused dictionary pass / capability bits in the prologue
+#define DIAG_NOPSS 2u    // PSS lists loaded but not evaluated
+#define DIAG_NORULES 4u  // no terms / rules: a verdict derived from the PSS bits
+#define DIAG_NOLOOP 8u   // no tiles: launch + prologue only
+constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
+                                     (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
+                                     (1u << VS_PROJECTED) | (1u << VS_SECRET);
+
+__constant__ uint8_t kCvCheck[KPE_NUM_CV] = {
+    CK_APE, CK_APE, CK_APPARMOR, CK_CAPS_BASELINE, CK_CAPS_RESTRICTED, CK_CAPS_RESTRICTED, CK_HOST_NS,
+    CK_HOST_PATH, CK_HOST_PORTS, CK_PRIVILEGED, CK_PROC_MOUNT, CK_RESTRICTED_VOLUMES, CK_RUN_AS_NON_ROOT,
+    CK_RUN_AS_USER, CK_SELINUX, CK_SECCOMP_BASELINE, CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED,
+    CK_SECCOMP_RESTRICTED, CK_SYSCTLS, CK_SYSCTLS, CK_SYSCTLS, CK_WIN_HOST_PROCESS};
+
+// Capability-set violation bits (computed per block into LDS from the capset dictionary)
+#define CS_BASE 1u  // add has a capability outside the baseline allow-list
+#define CS_DROP 2u  // drop lacks "ALL" (also: no capabilities at all)
+#define CS_ADD 4u   // add has anything but NET_BIND_SERVICE
+
+// PSA versioned checks for one pod (PSA v0.29 policy/check_*.go, restated in
+// oracle/pss.hpp) from the pod word and the OR of its containers' state bitmaps.
+// "Containers" = initContainers + containers + ephemeralContainers.
+__device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t xo, uint32_t co, bool sec_ann_bad,
+                                             bool vol_hostpath, bool vol_restricted, uint32_t sys_bad,
+                                             bool apparmor_bad, bool sec_pod_ann_bad) {
+  uint32_t f = 0;
+  const bool win = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS;
+  const uint32_t nwin = win ? 0u : ~0u;
+  // allowPrivilegeEscalation: some container whose APE is unset (or SC nil) or true
+  if (xo & (CX_APE_T | CX_APE_U)) f |= (1u << CV_APE_1_8) | ((1u << CV_APE_1_25) & nwin);
+  if (apparmor_bad) f |= 1u << CV_APPARMOR_1_0;
+  if (co & CS_BASE) f |= 1u << CV_CAPS_BASELINE_1_0;
+  if (co & (CS_DROP | CS_ADD)) f |= (1u << CV_CAPS_RESTRICTED_1_22) | ((1u << CV_CAPS_RESTRICTED_1_25) & nwin);
+  if (pw & (P_HOSTNET | P_HOSTPID | P_HOSTIPC)) f |= 1u << CV_HOST_NS_1_0;
+  if (vol_hostpath) f |= 1u << CV_HOST_PATH_1_0;
+  if (xo & CX_HOSTPORT) f |= 1u << CV_HOST_PORTS_1_0;
+  if (xo & CX_PRIV_T) f |= 1u << CV_PRIVILEGED_1_0;
+  if (xo & CX_PM_OTHER) f |= 1u << CV_PROC_MOUNT_1_0;
+  if (vol_restricted) f |= 1u << CV_RESTRICTED_VOLUMES_1_0;
+  const uint32_t prnr = FIELD(pw, P_RNR_SH, 2);
+  if (prnr == TRI_FALSE || (xo & CX_RNR_F) || (prnr != TRI_TRUE && (xo & CX_RNR_U)))
+    f |= 1u << CV_RUN_AS_NON_ROOT_1_0;
+  if (FIELD(pw, P_RAU_SH, 2) == RAU_ZERO || (xo & CX_RAU_Z)) f |= 1u << CV_RUN_AS_USER_1_23;
+  const uint32_t psel = FIELD(pw, P_SEL_SH, 3);
+  if ((psel != SEL_NONE && (psel == SEL_OTHER || (pw & (P_SEL_USER | P_SEL_ROLE)))) ||
+      (xo & (CX_SEL_OTHER | CX_SEL_USER | CX_SEL_ROLE)))
+    f |= 1u << CV_SELINUX_1_0;
+  if (sec_pod_ann_bad || sec_ann_bad) f |= 1u << CV_SECCOMP_BASELINE_1_0;
+  const uint32_t psec = FIELD(pw, P_SECCOMP_SH, 3);
+  const bool psec_valid = psec == SECCOMP_RUNTIMEDEFAULT || psec == SECCOMP_LOCALHOST;
+  const bool psec_bad = psec != SECCOMP_NONE && !psec_valid;
+  const bool csec_bad = xo & (CX_SEC_UNC | CX_SEC_OTHER);
+  if (psec_bad || csec_bad) f |= 1u << CV_SECCOMP_BASELINE_1_19;
+  if (psec_bad || csec_bad || (!psec_valid && (xo & CX_SEC_NONE)))
+    f |= (1u << CV_SECCOMP_RESTRICTED_1_19) | ((1u << CV_SECCOMP_RESTRICTED_1_25) & nwin);
+  if (sys_bad & 1u) f |= 1u << CV_SYSCTLS_1_0;
+  if (sys_bad & 2u) f |= 1u << CV_SYSCTLS_1_27;
+  if (sys_bad & 4u) f |= 1u << CV_SYSCTLS_1_29;
+  if (FIELD(pw, P_WHP_SH, 2) == TRI_TRUE || (xo & CX_WHP_T)) f |= 1u << CV_WIN_HOST_PROCESS_1_0;
+  return f;
+}
+
+// Inclusive wave64 prefix sum: 4 row_shr steps inside each 16-lane row, then
+// row_bcast:15 / row_bcast:31 across rows (6 DPP adds, no LDS).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xf, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xa, 0xf, false);
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xc, 0xf, false);
+  return x;
+}
+
+// The scan's arguments live in device memory (one copy per program x corpus
+// binding) and are read through the constant address space with scalar loads. The
+// pointer is laundered once per tile so the loads are re-issued near their uses
+// instead of being hoisted out of the tile loop (hoisted, ~60 fields exceed the
+// SGPR file and spill to VGPR lanes).
+typedef const __attribute__((address_space(4))) ScanArgs CArgs;
+__device__ __forceinline__ CArgs* launder(const ScanArgs* p) {
+  uint64_t v = (uint64_t)p;
+  asm volatile("" : "+s"(v));
+  return (CArgs*)v;
 }
 
 // Bitset word of a resolved predicate location (PRED_LOCAL | LDS index, or pbuf index).
+typedef __attribute__((address_space(3))) const uint32_t* LdsPtr;
+typedef __attribute__((address_space(1))) const uint32_t* GblPtr;
+// Large-domain bitset words (HBM/L2): out of line, so the wait for this load sits in
+// the callee and never at the join with the LDS path (where it would also wait for
+// the next tile's prefetch on every call).
+__device__ __noinline__ uint32_t gbl_word(GblPtr p, uint32_t i) { return p[i]; }
 struct Bits {
-  const uint32_t* lds;
-  const uint32_t* pbuf;
+  LdsPtr lds;
+  GblPtr pbuf;
+  __device__ Bits(const uint32_t* l, const uint32_t* g) : lds((LdsPtr)l), pbuf((GblPtr)g) {}
+  // `loc` is wave-uniform: the branch is uniform and the reads are typed LDS / global
+  // pointers, so they stay distinct instructions (a pointer select would become a flat
+  // load whose wait also covers every global load in flight: the next tile's prefetch).
   __device__ __forceinline__ uint32_t word(uint32_t loc, uint32_t wi) const {
-    return (loc & PRED_LOCAL) ? lds[(loc & ~PRED_LOCAL) + wi] : pbuf[loc + wi];
+    if (loc & PRED_LOCAL) return lds[(loc & ~PRED_LOCAL) + wi];
+    return gbl_word(pbuf, loc + wi);
   }
   __device__ __forceinline__ bool bit(uint32_t loc, uint32_t id) const {
     if (id == KPE_NO_STR) return false;
@@ -290,295 +346,556 @@ struct Bits {
   }
 };
 
-// Round-1 data of one 64-resource tile.
-struct Tile1 {
-  uint4 rec, hdr;
+// Data of one 64-resource tile, loaded one tile ahead of its evaluation. PSS programs
+// read the pod record per lane and the tile's list items COOPERATIVELY: the tile's
+// containers are crec[C0, C1) with C0/C1 from its header and the next one, so lane i
+// loads items C0 + i and C0 + 64 + i (coalesced) in the same round as the pod records.
+// Items past the preloaded slots (rare: > 128 containers or > 64 other items per tile)
+// are loaded when the tile is evaluated.
+template <bool PSS>
+struct Tile;
+template <>
+struct Tile<true> {
+  uint32_t C0, V0, S0, A0, nct, nvt, nst, nat;  // the tile's list ranges (wave-uniform)
+  uint4 rec;
+  uint2 c0, c1;   // containers C0 + lane, C0 + 64 + lane
+  uint32_t v0, s0;  // volume / sysctl V0 + lane, S0 + lane
+  uint2 q0;       // pod annotation A0 + lane
+  uint32_t sa0, sa1;  // container seccomp annotations (NEED_SANN)
+  uint32_t name, mns;
+};
+template <>
+struct Tile<false> {
   uint32_t gvk, nsa, name, mns;
 };
 
+// Tile header words: lane k (< 8) holds word k of hdr[tile], hdr[tile + 1]
+// (C0 V0 S0 A0 C1 V1 S1 A1); read back with v_readlane into scalars.
+__device__ __forceinline__ uint32_t load_hdr(CArgs& a, uint32_t tile, uint32_t lane) {
+  return a.hdr[tile * 4 + (lane & 7u)];
+}
+__device__ __forceinline__ uint32_t hw(uint32_t h, uint32_t k) { return __builtin_amdgcn_readlane(h, k); }
+
 template <bool PSS>
-__device__ __forceinline__ Tile1 load_tile1(const ScanArgs& a, int64_t tile, uint32_t lane) {
-  Tile1 d;
-  d.rec = d.hdr = make_uint4(0, 0, 0, 0);
-  d.gvk = 0;
-  d.nsa = d.name = d.mns = KPE_NO_STR;
-  const int64_t r = tile * 64 + lane;
-  const int64_t rc = r < a.n ? r : a.n - 1;  // clamped: loads are unconditional
-  if (PSS) {
-    d.rec = reinterpret_cast<const uint4*>(a.rec)[rc];
-    // the wave header as a vector load (a scalar load would be waited on at once)
-    uint32_t hv = (uint32_t)tile;
-    asm volatile("" : "+v"(hv));
-    d.hdr = reinterpret_cast<const uint4*>(a.hdr)[hv];
-  } else {
-    if (a.need & NEED_GVK) d.gvk = a.r_gvk[rc];
-    if (a.need & NEED_NSA) d.nsa = a.r_nsa[rc];
-  }
-  if (a.need & NEED_NAME) d.name = a.r_name[rc];
-  if (a.need & NEED_MNS) d.mns = a.r_mns[rc];
+__device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane);
+
+// Every load of a tile is issued on every path (an unneeded column is read from the
+// binding's zero page instead: one broadcast cache line), so the number of loads a
+// prefetch puts in flight is static and the compiler can wait for an older tile with
+// a counted vmcnt instead of draining the prefetch with vmcnt(0).
+template <class T>
+__device__ __forceinline__ const T* col(bool on, const void* p, const uint32_t* zero) {
+  return reinterpret_cast<const T*>(on ? p : (const void*)zero);
+}
+template <>
+__device__ __forceinline__ Tile<true> load_tile<true>(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane) {
+  Tile<true> d;
+  const uint32_t n = (uint32_t)a.n, need = a.need;
+  const uint32_t r = tile * 64 + lane;
+  const uint32_t rc = r < n ? r : n - 1;  // clamped: loads are unconditional
+  const uint32_t* zp = a.zero_page;
+  d.C0 = hw(h, 0), d.V0 = hw(h, 1), d.S0 = hw(h, 2), d.A0 = hw(h, 3);
+  d.nct = hw(h, 4) - d.C0, d.nvt = hw(h, 5) - d.V0, d.nst = hw(h, 6) - d.S0, d.nat = hw(h, 7) - d.A0;
+  // item index clamped into the tile's range [b0, b0 + cnt) and the column (index 0 of
+  // an empty column / of the zero page reads in-bounds garbage that is never used)
+  auto at = [&](uint32_t b0, uint32_t cnt, uint32_t k, uint32_t total) {
+    const uint32_t i = b0 + min(k, cnt ? cnt - 1 : 0u);
+    return total ? min(i, total - 1) : 0u;
+  };
+  const bool on_c = a.nctr_total, on_sa = on_c && (need & NEED_SANN);
+  const bool on_v = (need & NEED_VOL) && a.nvol_total, on_s = (need & NEED_SYS) && a.nsys_total;
+  const bool on_q = (need & NEED_PANN) && a.npann_total;
+  const uint32_t i0 = on_c ? at(d.C0, d.nct, lane, a.nctr_total) : 0u;
+  const uint32_t i1 = on_c ? at(d.C0, d.nct, lane + 64, a.nctr_total) : 0u;
+  d.rec = reinterpret_cast<const uint4*>(a.rec)[rc];
+  d.c0 = col<uint2>(on_c, a.crec, zp)[i0];
+  d.c1 = col<uint2>(on_c, a.crec, zp)[i1];
+  d.sa0 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i0 : 0u];
+  d.sa1 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i1 : 0u];
+  d.v0 = col<uint32_t>(on_v, a.vol_src, zp)[on_v ? at(d.V0, d.nvt, lane, a.nvol_total) : 0u];
+  d.s0 = col<uint32_t>(on_s, a.sys_id, zp)[on_s ? at(d.S0, d.nst, lane, a.nsys_total) : 0u];
+  d.q0 = col<uint2>(on_q, a.pann_kv, zp)[on_q ? at(d.A0, d.nat, lane, a.npann_total) : 0u];
+  const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
+  d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
+  d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+  if (!on_sa) d.sa0 = d.sa1 = KPE_NO_STR;
+  if (!on_n) d.name = KPE_NO_STR;
+  if (!on_m) d.mns = KPE_NO_STR;
   return d;
 }
 
-// Persistent, wave-autonomous scan. Every wave walks 64-resource tiles
-// (tile = global wave id, + total waves, ...) with the next tile's round-1 loads in
-// flight while the current tile is evaluated:
-//
-//  round 1  pod record (dwordx4) + wave header (PSS programs) or the gvk /
-//           namespace columns, plus the name columns the terms read — prefetched
-//           one tile ahead;
-//  round 2  (PSS) the lane's list items at header + exclusive wave scan of the
-//           counts: up to 4 containers, 2 volumes, 2 annotations, 1 sysctl issued
-//           together; the PSA versioned checks give a per-lane failure bitmask
-//           (pkg/pss/evaluate.go:24-70 over the PSA v0.29 check semantics);
-//  terms    every DISTINCT match term is evaluated once per resource and ballot-ed
-//           into a 64-bit mask (LDS, per wave); so is every distinct PSS version set;
-//  rules    transposed: lane j evaluates rule c0+j for all 64 resources at once with
-//           64-bit mask algebra (match/exclude: pkg/engine/utils/match.go:168-300;
-//           ApplyOne: pkg/engine/validation.go:75-77), then each resource lane
-//           extracts its verdict bytes; cells are staged per wave and stored as
-//           contiguous row segments; counts are popcounts (LDS per block).
-template <bool PSS>
-__global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-  __shared__ __attribute__((aligned(16))) uint8_t s_capb[KPE_MAX_CAPSETS];
-  __shared__ __attribute__((aligned(16))) uint32_t s_cnt[3 * KPE_LDS_R];
+template <>
+__device__ __forceinline__ Tile<false> load_tile<false>(CArgs& a, uint32_t tile, uint32_t, uint32_t lane) {
+  Tile<false> d;
+  const uint32_t n = (uint32_t)a.n, need = a.need;
+  const uint32_t r = tile * 64 + lane;
+  const uint32_t rc = r < n ? r : n - 1;
+  const uint32_t* zp = a.zero_page;
+  const bool on_g = need & NEED_GVK, on_a = need & NEED_NSA, on_n = need & NEED_NAME, on_m = need & NEED_MNS;
+  d.gvk = col<uint32_t>(on_g, a.r_gvk, zp)[on_g ? rc : 0u];
+  d.nsa = col<uint32_t>(on_a, a.r_nsa, zp)[on_a ? rc : 0u];
+  d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
+  d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+  if (!on_g) d.gvk = 0;
+  if (!on_a) d.nsa = KPE_NO_STR;
+  if (!on_n) d.name = KPE_NO_STR;
+  if (!on_m) d.mns = KPE_NO_STR;
+  return d;
+}
 
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t R = a.nrules, need = a.need;
-  const bool lds_cnt = R <= KPE_LDS_R;
-  const bool need_caps = PSS && (need & NEED_CAPS);
-  const int64_t ntiles = (a.n + 63) >> 6;
-  const uint32_t W = gridDim.x * (kBlock / 64u);
-  int64_t tile = (int64_t)blockIdx.x * (kBlock / 64u) + wv;
-
-  // ---- block prologue (overlapped with the first tile's round-1 loads) ----
-  Tile1 nx{};
-  if (tile < ntiles) nx = load_tile1<PSS>(a, tile, lane);
+// PSS part of one tile: the lane's failing versioned checks (0 for dead lanes).
+// Segmented OR of the tile's list items into their pods: every list item is turned
+// into its violation code by an "item lane" (item j on lane j % 64, from the tile's
+// preloaded slots) and staged in the wave's LDS area; after one wave barrier each pod
+// lane ORs the codes of its own items [o, o + cnt). The common path issues no memory
+// operation at all (the next tile's loads stay in flight); items past the staged
+// chunk (> 128 containers or > 64 other items per tile) take a rare direct-load path.
+__device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint8_t* s_capb, const Tile<true>& d,
+                                             bool live, uint32_t* stage, uint32_t lane) {
+  const uint32_t need = a.need;
+  const uint32_t C0 = d.C0, V0 = d.V0, S0 = d.S0, A0 = d.A0;
+  const uint32_t nct = d.nct, nvt = d.nvt, nst = d.nst, nat = d.nat;
+  const bool nsann = need & NEED_SANN;
+  const bool nvol = (need & NEED_VOL) && nvt, nsys = (need & NEED_SYS) && nst, npann = (need & NEED_PANN) && nat;
+  // ---- the pod's own item offsets: exclusive wave scans of its packed counts ----
+  const uint32_t z = live ? d.rec.z : 0u;
+  const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+  const uint32_t c01 = nc | (nv << 16);
+  const uint32_t e01 = wave_incl_scan(c01) - c01;
+  uint32_t e23 = 0;
+  if (nsys || npann) {
+    const uint32_t c23 = ns | (na << 16);
+    e23 = wave_incl_scan(c23) - c23;
+  }
+  const uint32_t oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
+  uint2* sc = reinterpret_cast<uint2*>(stage);
+  uint8_t* sbv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_CTR * 2);
+  uint8_t* sbs = sbv + KPE_STAGE_SMALL;
+  uint8_t* sba = sbs + KPE_STAGE_SMALL;
+  // item codes
+  auto ctr_code = [&](uint2 e, uint32_t sa) -> uint2 {  // (state bitmap, capset bits | seccomp-annotation bit)
+    uint32_t ex = s_capb[CY_CAPSET(e.y)];
+    if (nsann && sa != KPE_NO_STR && !B.bit(a.pp_seccomp_ann_ok, sa)) ex |= 8u;
+    return make_uint2(e.x, ex);
+  };
+  auto vol_code = [&](uint32_t sv) -> uint32_t {  // bit 0 hostPath, bit 1 outside the restricted allow-list
+    return ((sv >> VS_HOSTPATH) & 1u) | ((sv & kAllowedVolumes) ? 0u : 2u);
+  };
+  auto sys_code = [&](uint32_t id) -> uint32_t {  // bit k: outside the 1.0 / 1.27 / 1.29 allow-list
+    return (B.bit(a.pp_sysctl0, id) ? 0u : 1u) | (B.bit(a.pp_sysctl1, id) ? 0u : 2u) | (B.bit(a.pp_sysctl2, id) ? 0u : 4u);
+  };
+  auto ann_code = [&](uint2 kv) -> uint32_t {  // bit 0 AppArmor profile, bit 1 seccomp pod annotation
+    return (B.bit(a.pp_apparmor_key, kv.x) && !B.bit(a.pp_apparmor_ok, kv.y) ? 1u : 0u) |
+           (B.bit(a.pp_seccomp_pod_key, kv.x) && !B.bit(a.pp_seccomp_ann_ok, kv.y) ? 2u : 0u);
+  };
+  // ---- stage the first chunk of every list from the preloaded slots ----
+  if (lane < nct) sc[lane] = ctr_code(d.c0, d.sa0);
+  if (lane + 64 < nct) sc[lane + 64] = ctr_code(d.c1, d.sa1);
+  if (nvol && lane < nvt) sbv[lane] = (uint8_t)vol_code(d.v0);
+  if (nsys && lane < nst) sbs[lane] = (uint8_t)sys_code(d.s0);
+  if (npann && lane < nat) sba[lane] = (uint8_t)ann_code(d.q0);
+  __builtin_amdgcn_wave_barrier();
+  uint32_t xo = 0, co = 0, vcode = 0, scode = 0, acode = 0;
   {
-    const uint32_t nb4 = a.blob_words >> 2;  // >= 1
+    const uint32_t hi = min(oc + nc, (uint32_t)KPE_STAGE_CTR);
+#pragma unroll 2
+    for (uint32_t k = oc; k < hi; ++k) {
+      const uint2 e = sc[k];
+      xo |= e.x;
+      co |= e.y;
+    }
+  }
+  if (nvol) {
+    const uint32_t hi = min(ov + nv, (uint32_t)KPE_STAGE_SMALL);
+    for (uint32_t k = ov; k < hi; ++k) vcode |= sbv[k];
+  }
+  if (nsys) {
+    const uint32_t hi = min(os + ns, (uint32_t)KPE_STAGE_SMALL);
+    for (uint32_t k = os; k < hi; ++k) scode |= sbs[k];
+  }
+  if (npann) {
+    const uint32_t hi = min(oa + na, (uint32_t)KPE_STAGE_SMALL);
+    for (uint32_t k = oa; k < hi; ++k) acode |= sba[k];
+  }
+  __builtin_amdgcn_wave_barrier();
+  // ---- rare: items beyond the staged chunk, loaded directly by their pod lane ----
+  if (nct > KPE_STAGE_CTR || (nvol && nvt > KPE_STAGE_SMALL) || (nsys && nst > KPE_STAGE_SMALL) ||
+      (npann && nat > KPE_STAGE_SMALL)) {
+    const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
+    for (uint32_t k = max(oc, (uint32_t)KPE_STAGE_CTR); k < oc + nc; ++k) {
+      const uint2 e = ctr_code(crec[C0 + k], nsann ? a.c_sann[C0 + k] : KPE_NO_STR);
+      xo |= e.x;
+      co |= e.y;
+    }
+    if (nvol)
+      for (uint32_t k = max(ov, (uint32_t)KPE_STAGE_SMALL); k < ov + nv; ++k) vcode |= vol_code(a.vol_src[V0 + k]);
+    if (nsys)
+      for (uint32_t k = max(os, (uint32_t)KPE_STAGE_SMALL); k < os + ns; ++k) scode |= sys_code(a.sys_id[S0 + k]);
+    if (npann)
+      for (uint32_t k = max(oa, (uint32_t)KPE_STAGE_SMALL); k < oa + na; ++k)
+        acode |= ann_code(reinterpret_cast<const uint2*>(a.pann_kv)[A0 + k]);
+  }
+  if (!live) return 0u;
+  return cv_fails(d.rec.x, xo, co & 7u, co & 8u, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & a.cv_union;
+}
+
+// One match term for this lane's resource (utils/match.go:52-160 attributes).
+__device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm& tm, uint32_t gvk,
+                                          uint32_t nsa, uint32_t name_col, uint32_t mns_col, uint32_t rc,
+                                          bool live) {
+  bool ok = true;
+  if (tm.type == T_KIND_PRED) {
+    ok = B.bit(tm.a, GVK_KIND(gvk));
+  } else if (tm.type == T_KINDS) {  // CheckKind: OR over kind selectors
+    ok = false;
+#pragma unroll 1
+    for (uint32_t k = 0; k < tm.b; ++k) {
+      const KpeKindSel ks = sld(a.kindsels, tm.a + k);
+      ok |= ks.sub_ok && (ks.pg == PRED_NONE || B.bit(ks.pg, GVK_GRP(gvk))) &&
+            (ks.pv == PRED_NONE || B.bit(ks.pv, GVK_VER(gvk))) && (ks.pk == PRED_NONE || B.bit(ks.pk, GVK_KIND(gvk)));
+    }
+  } else if (tm.type == T_PRED) {
+    const uint32_t id = tm.b == COL_NAME ? name_col : (tm.b == COL_MNS ? mns_col : nsa);
+    ok = B.bit(tm.a, id);
+  } else if (tm.type == T_ANNOTATIONS) {  // CheckAnnotations: every pair matched by some annotation
+    const uint32_t lo = a.ann_off[rc], hi = live ? a.ann_off[rc + 1] : lo;
+#pragma unroll 1
+    for (uint32_t k = 0; k < tm.b; ++k) {
+      const KpeAnnPair pr = sld(a.annpairs, tm.a + k);
+      bool hit = false;
+#pragma unroll 1
+      for (uint32_t j = lo; j < hi && !hit; ++j) hit = B.bit(pr.pk, a.ann_k[j]) && B.bit(pr.pv, a.ann_v[j]);
+      ok &= hit;
+    }
+  } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
+    // CheckSelector (pkg/utils/match/labels.go:9-24) over the resource's labels or,
+    // for namespaceSelector, its namespace's labels (utils/match.go:114-138)
+    const KpeSelector S = sld(a.selectors, tm.a);
+    uint32_t lo = 0, hi = 0;
+    const uint32_t *K = a.lab_k, *V = a.lab_v;
+    bool eval = true;
+    if (tm.type == T_SELECTOR) {
+      lo = a.lab_off[rc];
+      hi = live ? a.lab_off[rc + 1] : lo;
+    } else {
+      // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
+      const uint32_t kid = GVK_KIND(gvk);
+      const uint32_t row = a.r_nsl[rc];
+      if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
+      K = a.nsl_k, V = a.nsl_v;
+      if (B.bit(S.p_kind_ns, kid)) {
+        ok = false, eval = false;
+      } else if (B.bit(S.p_kind_empty, kid) && !S.star_kind) {
+        ok = true, eval = false;
+      } else if (S.invalid) {
+        ok = false, eval = false;
+      }
+    }
+    if (eval) {
+#pragma unroll 1
+      for (uint32_t qi = 0; qi < S.nreq; ++qi) {
+        const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
+        const bool wild = q.op == SR_WILD;
+        uint32_t j = lo;
+#pragma unroll 1
+        for (; j < hi; ++j)  // first label with a matching key (and value, for wildcards)
+          if (B.bit(q.pk, K[j]) && (!wild || B.bit(q.pv, V[j]))) break;
+        const bool found = j < hi;
+        const uint32_t kid = found ? K[j] : KPE_NO_STR, vid = found ? V[j] : KPE_NO_STR;
+        bool qok;
+        switch (q.op) {
+          case SR_EQ:
+          case SR_IN: qok = found && B.bit(q.pv, vid); break;
+          case SR_WILD: qok = found && B.bit(q.pk_ok, kid) && B.bit(q.pv_ok, vid); break;
+          case SR_NOTIN: qok = !found || !B.bit(q.pv, vid); break;
+          case SR_EXISTS: qok = found; break;
+          default: qok = !found; break;
+        }
+        ok &= qok;
+      }
+    }
+  } else {  // T_FALSE
+    ok = false;
+  }
+  return ok;
+}
+
+__device__ __forceinline__ uint32_t check_mask(uint32_t f) {  // versioned checks -> PSA check ids
+  uint32_t cmask = 0;
+#pragma unroll 1
+  for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
+    if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
+  return cmask;
+}
+
+// Store a tile's staged row segments [c0, c0 + nc) of R-byte rows.
+__device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv, uint32_t tile, uint32_t R,
+                                           uint32_t c0, uint32_t nc, uint32_t nrows, uint32_t lane) {
+  uint8_t* base = verdicts + (size_t)tile * (64 * R) + c0;
+  if (nc == R) {  // whole rows: contiguous nrows x R bytes, dword aligned (64 R % 4 == 0)
+    const uint32_t nb = nrows * R, nw = nb >> 2;
+    uint32_t* dst = reinterpret_cast<uint32_t*>(base);
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(sv);
+#pragma unroll 1
+    for (uint32_t i = lane; i < nw; i += 64) dst[i] = src[i];
+    if (lane < (nb & 3u)) base[(nw << 2) + lane] = sv[(nw << 2) + lane];
+  } else {
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (uint32_t i = lane; i < nrows * nc; i += 64) {
+      const uint32_t row = i / nc, col = i - row * nc;
+      base[(size_t)row * R + col] = sv[i];
+    }
+  }
+}
+
+}  // namespace
+
+// Persistent, wave-autonomous scan. Every wave walks 64-resource tiles
+// (tile = global wave id, + total waves, ...); the next tile's data (pod records +
+// cooperative list loads, or the match columns) is in flight while the current tile
+// is evaluated, and the tile header one step further ahead.
+// NARROW: terms become a per-lane bit vector and each lane runs the rule loop for
+// its resource (rule records and filter masks are wave-uniform scalar loads).
+// WIDE: terms are ballot-ed into per-wave 64-bit masks in LDS and lane j evaluates
+// rule c0 + j for all 64 resources with 64-bit mask algebra.
+template <bool PSS, bool NARROW>
+__global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  __shared__ __attribute__((aligned(16))) uint8_t s_capb[PSS ? KPE_MAX_CAPSETS : 4];
+
+  CArgs& a0 = *launder(ap);
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t ntiles = a0.ntiles;
+  const uint32_t W = gridDim.x * (kBlock / 64u);
+  uint32_t tile = blockIdx.x * (kBlock / 64u) + wv;
+
+  // ---- first tile's loads, then the block prologue while they are in flight ----
+  uint32_t h = 0;  // header words of the tile whose data is loaded next
+  Tile<PSS> ta{};
+  if (tile < ntiles) {
+    if (PSS) h = load_hdr(a0, tile, lane);
+    ta = load_tile<PSS>(a0, tile, h, lane);
+    if (PSS && tile + W < ntiles) h = load_hdr(a0, tile + W, lane);
+  }
+  // capability sets: the block's first 256 prefetched alongside (tiny dictionary)
+  uint4 cs0 = make_uint4(0, 0, 0, 0);
+  if (PSS && (a0.need & NEED_CAPS) && t < a0.ncapsets) cs0 = reinterpret_cast<const uint4*>(a0.capsets)[t];
+  {
+    CArgs& a = a0;
+    // small-domain predicate bitsets (kpe_pred_kernel output) into LDS
     const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
     uint4* d4 = reinterpret_cast<uint4*>(dyn);
 #pragma unroll 1
-    for (uint32_t i = t; i < nb4; i += kBlock) d4[i] = blob[i];
-    if (a.filt_lds != PRED_NONE) {  // program filters + filter terms for the rule lanes
+    for (uint32_t i = t; i < (a.blob_words >> 2); i += kBlock) d4[i] = blob[i];
+    if (!NARROW && a.filt_lds != PRED_NONE) {  // program filters + filter terms for the rule lanes
       const uint32_t nw = a.fterm_lds + a.nfterms - a.filt_lds;
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.filters);
 #pragma unroll 1
       for (uint32_t i = t; i < nw; i += kBlock)
         dyn[a.filt_lds + i] = i < a.fterm_lds - a.filt_lds ? src[i] : a.fterms[i - (a.fterm_lds - a.filt_lds)];
     }
-#pragma unroll 1
-    for (uint32_t i = t; i < 3 * R && lds_cnt; i += kBlock) s_cnt[i] = 0;
   }
   __syncthreads();
-  const Bits B{dyn, a.pbuf};
-  if (need_caps) {  // capability-set violation bits (add/drop masks vs the fixed allow-lists)
-    const uint64_t caps_ok = B.mask64(a.pp_caps_ok), nbs = B.mask64(a.pp_cap_nbs), all = B.mask64(a.pp_cap_all);
+  if (PSS && !(KPE_DIAG & DIAG_NOPRO)) {
+    CArgs& a = a0;
+    const Bits B{dyn, a.pbuf};
+    if (a.need & NEED_CAPS) {  // capability-set violation bits (add/drop masks vs the fixed allow-lists)
+      const uint64_t caps_ok = B.mask64(a.pp_caps_ok), nbs = B.mask64(a.pp_cap_nbs), all = B.mask64(a.pp_cap_all);
+      auto capb = [&](uint4 c) -> uint8_t {
+        const uint64_t ad = (uint64_t)c.x | ((uint64_t)c.y << 32), dr = (uint64_t)c.z | ((uint64_t)c.w << 32);
+        return (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+      };
+      if (t < a.ncapsets) s_capb[t] = capb(cs0);
 #pragma unroll 1
-    for (uint32_t i = t; i < a.ncapsets; i += kBlock) {
-      const uint4 c = reinterpret_cast<const uint4*>(a.capsets)[i];
-      const uint64_t ad = (uint64_t)c.x | ((uint64_t)c.y << 32), dr = (uint64_t)c.z | ((uint64_t)c.w << 32);
-      s_capb[i] = (uint8_t)(((ad & ~caps_ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+      for (uint32_t i = t + kBlock; i < a.ncapsets; i += kBlock) s_capb[i] = capb(reinterpret_cast<const uint4*>(a.capsets)[i]);
+    } else {
+#pragma unroll 1
+      for (uint32_t i = t; i < a.ncapsets; i += kBlock) s_capb[i] = 0;
     }
     __syncthreads();
   }
-  const KpeFilter* filt =
-      a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
-  const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
 
-  // per-wave LDS: term masks, PSS version-set masks, rule cell masks, verdict staging
-  uint64_t* tmk = reinterpret_cast<uint64_t*>(dyn + a.wave_lds + wv * a.wave_words);
-  uint64_t* cvm = tmk + a.nterms;
-  uint64_t* rmk = cvm + a.ncv;                                       // kRC x (P, F, E)
-  uint8_t* sv = reinterpret_cast<uint8_t*>(rmk + 3 * KPE_RULE_CHUNK);  // 64 x kRC bytes
-
-  // single-chunk programs keep lane j's packed rule in registers for every tile
+  // Program tables held in lanes for the whole kernel (read back with v_readlane:
+  // no memory access inside the tile loop). WIDE single-chunk programs: lane j's
+  // packed rule. NARROW: lane j holds rule j's record, lane f filter f's term mask,
+  // lane t term t.
   uint4 myrule = make_uint4(0, 0, 0, 0);
-  if (R <= KPE_RULE_CHUNK && lane < R) myrule = reinterpret_cast<const uint4*>(a.rule_lanes)[lane];
+  uint32_t fm_lane = 0, tm_type = 0, tm_a = 0, tm_b = 0;
+  if (NARROW) {
+    if (lane < a0.nrules) myrule = reinterpret_cast<const uint4*>(a0.narrow_rules)[lane];
+    if (lane < a0.nfilters) fm_lane = a0.fmask[lane];
+    if (lane < a0.nterms) {
+      const KpeTerm tm = a0.terms[lane];
+      tm_type = tm.type, tm_a = tm.a, tm_b = tm.b;
+    }
+  } else if (a0.nrules <= KPE_RULE_CHUNK && lane < a0.nrules) {
+    myrule = reinterpret_cast<const uint4*>(a0.rule_lanes)[lane];
+  }
+  // NARROW truth table: tt[v] = rules whose match / exclude / namespaced-policy term
+  // conditions hold for term vector v (pkg/engine/utils/match.go:168-300 over filters)
+  uint32_t cls_cv = 0, cls_rm = 0;
+  if (NARROW && a0.tt_lds != PRED_NONE) {
+    if (lane < a0.ncls) {
+      const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
+      cls_cv = c.x, cls_rm = c.y;
+    }
+    const uint32_t R = a0.nrules, nv = 1u << a0.nterms;
+    for (uint32_t tb = t; tb < nv; tb += kBlock) {
+      uint32_t mm = 0;
+      for (uint32_t ri = 0; ri < R; ++ri) {
+        const uint32_t x = hw(myrule.x, ri), z = hw(myrule.z, ri), w = hw(myrule.w, ri);
+        auto block = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> bool {
+          const bool all = mode == MODE_ALL;
+          bool acc = all;
+          for (uint32_t f = 0; f < nf; ++f) {
+            const uint32_t fm = hw(fm_lane, f0 + f);
+            const bool hit = (tb & fm) == fm;
+            acc = all ? (acc && hit) : (acc || hit);
+          }
+          return acc;
+        };
+        const uint32_t pol = NR_POLTERM(x);
+        bool m = pol == 0u || ((tb >> (pol - 1u)) & 1u);
+        m = m && block(NR_MATCH_MODE(x), RL_F0(z), RL_NF(z));
+        m = m && !block(NR_EXCL_MODE(x), RL_F0(w), RL_NF(w));
+        if (m) mm |= 1u << ri;
+      }
+      dyn[a0.tt_lds + tb] = mm;
+    }
+    __syncthreads();
+  }
+  // NARROW verdict rows are stored one tile late (double-buffered in LDS), after the
+  // next tile's loads are issued, so no wait for those loads ever covers a store.
+  uint32_t prev_tile = 0xFFFFFFFFu, prev_rows = 0, buf = 0;
 
-#pragma unroll 1
-  for (; tile < ntiles; tile += W) {
-    const Tile1 cur = nx;
-    if (tile + W < ntiles) nx = load_tile1<PSS>(a, tile + W, lane);
-    const int64_t r = tile * 64 + lane;
-    const bool live = r < a.n;
-    const int64_t rc = live ? r : a.n - 1;
-    const uint4 rec = live ? cur.rec : make_uint4(0, 0, 0, 0);
-    const uint4 hdr = cur.hdr;
-
-    uint32_t fails = 0;
-    if (PSS) {
-      // ---- list offsets: header + exclusive wave scan of the packed counts ----
-      const uint32_t z = rec.z;
-      const uint32_t c01 = (z & 0xFFu) | ((z & 0xFF00u) << 8), c23 = ((z >> 16) & 0xFFu) | ((z >> 24) << 16);
-      const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
-      const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
-      const uint32_t oc = hdr.x + (e01 & 0xFFFFu), ov = hdr.y + (e01 >> 16), os = hdr.z + (e23 & 0xFFFFu),
-                     oa = hdr.w + (e23 >> 16);
-      // ---- round 2: every first-pass list load issued before any is used ----
-      const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
-      const uint2* pkv = reinterpret_cast<const uint2*>(a.pann_kv);
-      const bool nvol = (need & NEED_VOL) && a.nvol_total, nsys = (need & NEED_SYS) && a.nsys_total,
-                 npann = (need & NEED_PANN) && a.npann_total, nsann = (need & NEED_SANN) && a.nctr_total;
-      const uint2 z2 = make_uint2(0, 0);
-      uint2 k0 = z2, k1 = z2, k2 = z2, k3 = z2;
-      if (a.nctr_total) {
-        const uint32_t lim = a.nctr_total - 1;
-        k0 = crec[min(oc, lim)];
-        k1 = crec[min(oc + 1, lim)];
-        k2 = crec[min(oc + 2, lim)];
-        k3 = crec[min(oc + 3, lim)];
-      }
-      uint32_t v0 = 0, v1 = 0, sy0 = 0;
-      if (nvol) {
-        v0 = a.vol_src[min(ov, a.nvol_total - 1)];
-        v1 = a.vol_src[min(ov + 1, a.nvol_total - 1)];
-      }
-      if (nsys) sy0 = a.sys_id[min(os, a.nsys_total - 1)];
-      uint2 q0 = z2, q1 = z2;
-      if (npann) {
-        q0 = pkv[min(oa, a.npann_total - 1)];
-        q1 = pkv[min(oa + 1, a.npann_total - 1)];
-      }
-      uint32_t sa0 = KPE_NO_STR, sa1 = KPE_NO_STR, sa2 = KPE_NO_STR, sa3 = KPE_NO_STR;
-      if (nsann) {
-        const uint32_t lim = a.nctr_total - 1;
-        sa0 = a.c_sann[min(oc, lim)];
-        sa1 = a.c_sann[min(oc + 1, lim)];
-        sa2 = a.c_sann[min(oc + 2, lim)];
-        sa3 = a.c_sann[min(oc + 3, lim)];
-      }
-      // ---- containers: violation bits OR-ed over the pod's containers ----
-      auto one = [&](uint2 kk, uint32_t sann) -> uint32_t {
-        uint32_t b = ctr_bits(kk.x, need_caps ? s_capb[kk.y] : 0u);
-        if (nsann && sann != KPE_NO_STR && !B.bit(a.pp_seccomp_ann_ok, sann)) b |= CB_SEC_ANN;
-        return b;
-      };
-      uint32_t cb = (nc > 0 ? one(k0, sa0) : 0u) | (nc > 1 ? one(k1, sa1) : 0u) | (nc > 2 ? one(k2, sa2) : 0u) |
-                    (nc > 3 ? one(k3, sa3) : 0u);
-#pragma unroll 1
-      for (uint32_t k = 4; k < nc; ++k) cb |= one(crec[oc + k], nsann ? a.c_sann[oc + k] : KPE_NO_STR);
-      // ---- volumes ----
-      uint32_t vor = 0, vand = ~0u;  // hostPath present anywhere / some volume outside the allow-list
-      auto vol = [&](uint32_t sv_) {
-        vor |= sv_;
-        vand &= (sv_ & kAllowedVolumes) ? ~0u : 0u;
-      };
-      if (nvol) {
-        if (nv > 0) vol(v0);
-        if (nv > 1) vol(v1);
-#pragma unroll 1
-        for (uint32_t k = 2; k < nv; ++k) vol(a.vol_src[ov + k]);
-      }
-      const bool vol_hostpath = (vor >> VS_HOSTPATH) & 1u, vol_restricted = vand == 0u;
-      // ---- sysctls (allow-lists 1.0 / 1.27 / 1.29) ----
-      uint32_t sys_bad = 0;
-      auto sysf = [&](uint32_t id) {
-        sys_bad |= (B.bit(a.pp_sysctl0, id) ? 0u : 1u) | (B.bit(a.pp_sysctl1, id) ? 0u : 2u) |
-                   (B.bit(a.pp_sysctl2, id) ? 0u : 4u);
-      };
-      if (nsys) {
-        if (ns > 0) sysf(sy0);
-#pragma unroll 1
-        for (uint32_t k = 1; k < ns; ++k) sysf(a.sys_id[os + k]);
-      }
-      // ---- pod-template annotations: AppArmor, seccomp pod annotation ----
-      bool apparmor_bad = false, sec_pod_ann_bad = false;
-      auto ann = [&](uint2 kv) {
-        apparmor_bad |= B.bit(a.pp_apparmor_key, kv.x) && !B.bit(a.pp_apparmor_ok, kv.y);
-        sec_pod_ann_bad |= B.bit(a.pp_seccomp_pod_key, kv.x) && !B.bit(a.pp_seccomp_ann_ok, kv.y);
-      };
-      if (npann) {
-        if (na > 0) ann(q0);
-        if (na > 1) ann(q1);
-#pragma unroll 1
-        for (uint32_t k = 2; k < na; ++k) ann(pkv[oa + k]);
-      }
-      if (live) fails = cv_fails(rec.x, cb, vol_hostpath, vol_restricted, sys_bad, apparmor_bad, sec_pod_ann_bad) & a.cv_union;
+  if (KPE_DIAG & DIAG_NOLOOP) {
+    if (tile < ntiles && lane == 0) a0.verdicts[tile] = (uint8_t)(dyn[0] + s_capb[0]);
+    return;
+  }
+  // Ping-pong tile buffers: the tile evaluated in one step was loaded into its own
+  // registers during the previous step, and the next tile is loaded into the other
+  // buffer, so no register holding an in-flight load is ever copied (a loop-carried
+  // copy of a prefetched register makes the compiler wait for the prefetch at once).
+  auto step = [&](const Tile<PSS>& cur, Tile<PSS>& nxt) {
+    CArgs& a = *launder(ap);
+    const uint32_t R = a.nrules, n = (uint32_t)a.n;
+    const Bits B{dyn, a.pbuf};
+    // per-wave LDS: PSS list staging, then NARROW: verdict staging (64 x R bytes);
+    // WIDE: term masks, PSS version-set masks, rule cell masks, verdict staging.
+    uint32_t* wbase = dyn + a.wave_lds + wv * a.wave_words;
+    uint32_t* stage = wbase;
+    uint32_t* wrest = wbase + (PSS ? KPE_STAGE_WORDS : 0u);
+    uint64_t* tmk = reinterpret_cast<uint64_t*>(wrest);
+    uint64_t* cvm = tmk + a.nterms;
+    uint64_t* rmk = cvm + a.ncv;  // kRC x (P, F, E)
+    uint8_t* sv = NARROW ? reinterpret_cast<uint8_t*>(wrest) + buf * 64 * R
+                         : reinterpret_cast<uint8_t*>(rmk + 3 * KPE_RULE_CHUNK);
+    // ---- prefetch the next tile into the other buffer, then evaluate `cur` ----
+    // (unconditional, clamped: past the end it re-reads the last tile, never used)
+    nxt = load_tile<PSS>(a, min(tile + W, ntiles - 1), h, lane);
+    if (PSS) h = load_hdr(a, min(tile + 2 * W, ntiles - 1), lane);
+    const uint32_t r = tile * 64 + lane;
+    const bool live = r < n;
+    const uint32_t rc = live ? r : n - 1;
+    uint32_t fails = 0, gvk, nsa, name_col, mns_col;
+    bool err = false;
+    if constexpr (PSS) {
+      if (KPE_DIAG & DIAG_NOPSS)
+        fails = cur.rec.x ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.s0 ^ cur.q0.x ^ cur.q0.y ^ cur.C0;
+      else
+        fails = pss_tile(a, B, s_capb, cur, live, stage, lane);
+      const uint32_t cls = (cur.rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
+      err = live && (cls == R_CLASS_OTHER || (cur.rec.x & PR_DECODE_ERR));
+      gvk = live ? cur.rec.y : 0u;
+      nsa = live ? cur.rec.w : KPE_NO_STR;
+    } else {
+      gvk = live ? cur.gvk : 0u;
+      nsa = live ? cur.nsa : KPE_NO_STR;
+    }
+    name_col = live ? cur.name : KPE_NO_STR;
+    mns_col = live ? cur.mns : KPE_NO_STR;
+    const uint32_t nrows = min(64u, n - tile * 64);
+    if (NARROW && prev_tile != 0xFFFFFFFFu) {  // the previous tile's rows (other LDS buffer)
+      store_rows(a.verdicts, reinterpret_cast<uint8_t*>(wrest) + (buf ^ 1u) * 64 * R, prev_tile, R, 0, R, prev_rows,
+                 lane);
+      prev_tile = 0xFFFFFFFFu;
     }
 
-    // ---- terms: one ballot per distinct term ----
-    const uint32_t gvk = PSS ? rec.y : (live ? cur.gvk : 0u);
-    const uint32_t nsa = PSS ? rec.w : (live ? cur.nsa : KPE_NO_STR);
-    const uint32_t name_col = live ? cur.name : KPE_NO_STR, mns_col = live ? cur.mns : KPE_NO_STR;
+    if (KPE_DIAG & DIAG_NORULES) {
+      sv[lane * R] = (uint8_t)(fails ^ (err ? 1u : 0u) ^ gvk);
+      __builtin_amdgcn_wave_barrier();
+      store_rows(a.verdicts, sv, tile, R, 0, R, nrows, lane);
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
+    if (NARROW) {
+      // ---- terms -> bit vector ----
+      uint32_t tb = 0;
+#pragma unroll 1
+      for (uint32_t ti = 0; ti < a.nterms; ++ti) {
+        const KpeTerm tm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u};
+        tb |= eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live) ? (1u << ti) : 0u;
+      }
+      if (a.tt_lds != PRED_NONE && !a.masks) {  // truth-table fast path
+        const uint32_t matched = live ? dyn[a.tt_lds + tb] : 0u;
+        uint32_t failr = 0;
+#pragma unroll 1
+        for (uint32_t c = 0; c < a.ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+        const uint32_t E = matched & ((err ? a.pss_rules : 0u) | a.err_rules);
+        const uint32_t F = matched & a.pss_rules & failr & ~E;
+        const uint32_t P = matched & a.pss_rules & ~failr & ~E;
+#pragma unroll 1
+        for (uint32_t ri = 0; ri < R; ++ri)
+          sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+        __builtin_amdgcn_wave_barrier();
+        prev_tile = tile, prev_rows = nrows, buf ^= 1u;
+        return;
+      }
+      // ---- rules, in program order, for this lane's resource ----
+      bool applied = false;
+#pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri) {
+        const uint4 nr = make_uint4(hw(myrule.x, ri), hw(myrule.y, ri), hw(myrule.z, ri), hw(myrule.w, ri));
+        const uint32_t x = nr.x;
+        // a block is an OR (any / legacy) or AND (all) of filters; a filter holds when
+        // all of its terms hold: (tb & mask) == mask
+        auto block = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> bool {
+          const bool all = mode == MODE_ALL;
+          bool acc = all;
+#pragma unroll 1
+          for (uint32_t f = 0; f < nf; ++f) {
+            const uint32_t fm = hw(fm_lane, f0 + f);
+            const bool h = (tb & fm) == fm;
+            acc = all ? (acc && h) : (acc || h);
+          }
+          return acc;
+        };
+        const uint32_t pol = NR_POLTERM(x);
+        bool m = live && (pol == 0u || ((tb >> (pol - 1u)) & 1u));
+        m = m && block(NR_MATCH_MODE(x), RL_F0(nr.z), RL_NF(nr.z));
+        m = m && !block(NR_EXCL_MODE(x), RL_F0(nr.w), RL_NF(nr.w));
+        const uint32_t hd = NR_HANDLER(x);
+        uint32_t v = KPE_NA_;
+        if (m && hd == H_PSS) v = err ? KPE_ERROR_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
+        else if (m && hd == H_ERROR) v = KPE_ERROR_;
+        if (x & NR_NEW_POLICY) applied = false;
+        if ((x & NR_APPLY_ONE) && applied) v = KPE_NA_;
+        applied |= v == KPE_PASS_ || v == KPE_FAIL_;
+        sv[lane * R + ri] = (uint8_t)v;
+        if (a.masks && live) a.masks[(size_t)r * R + ri] = v == KPE_FAIL_ ? check_mask(fails & nr.y) : 0u;
+      }
+      __builtin_amdgcn_wave_barrier();
+      prev_tile = tile, prev_rows = nrows, buf ^= 1u;
+      return;
+    }
+
+    // ---- WIDE: terms, one ballot per distinct term ----
+    const KpeFilter* filt =
+        a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
+    const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
 #pragma unroll 1
     for (uint32_t ti = 0; ti < a.nterms; ++ti) {
-      const KpeTerm tm = sld(a.terms, ti);
-      bool ok = true;
-      if (tm.type == T_KIND_PRED) {
-        ok = B.bit(tm.a, GVK_KIND(gvk));
-      } else if (tm.type == T_KINDS) {  // CheckKind: OR over kind selectors
-        ok = false;
-#pragma unroll 1
-        for (uint32_t k = 0; k < tm.b; ++k) {
-          const KpeKindSel ks = sld(a.kindsels, tm.a + k);
-          ok |= ks.sub_ok && (ks.pg == PRED_NONE || B.bit(ks.pg, GVK_GRP(gvk))) &&
-                (ks.pv == PRED_NONE || B.bit(ks.pv, GVK_VER(gvk))) && (ks.pk == PRED_NONE || B.bit(ks.pk, GVK_KIND(gvk)));
-        }
-      } else if (tm.type == T_PRED) {
-        const uint32_t id = tm.b == COL_NAME ? name_col : (tm.b == COL_MNS ? mns_col : nsa);
-        ok = B.bit(tm.a, id);
-      } else if (tm.type == T_ANNOTATIONS) {  // CheckAnnotations: every pair matched by some annotation
-        const uint32_t lo = a.ann_off[rc], hi = live ? a.ann_off[rc + 1] : lo;
-#pragma unroll 1
-        for (uint32_t k = 0; k < tm.b; ++k) {
-          const KpeAnnPair pr = sld(a.annpairs, tm.a + k);
-          bool hit = false;
-#pragma unroll 1
-          for (uint32_t j = lo; j < hi && !hit; ++j) hit = B.bit(pr.pk, a.ann_k[j]) && B.bit(pr.pv, a.ann_v[j]);
-          ok &= hit;
-        }
-      } else if (tm.type == T_SELECTOR || tm.type == T_NSSELECTOR) {
-        // CheckSelector (pkg/utils/match/labels.go:9-24) over the resource's labels or,
-        // for namespaceSelector, its namespace's labels (utils/match.go:114-138)
-        const KpeSelector S = sld(a.selectors, tm.a);
-        uint32_t lo = 0, hi = 0;
-        const uint32_t *K = a.lab_k, *V = a.lab_v;
-        bool eval = true;
-        if (tm.type == T_SELECTOR) {
-          lo = a.lab_off[rc];
-          hi = live ? a.lab_off[rc + 1] : lo;
-        } else {
-          // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
-          const uint32_t kid = GVK_KIND(gvk);
-          const uint32_t row = a.r_nsl[rc];
-          if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
-          K = a.nsl_k, V = a.nsl_v;
-          if (B.bit(S.p_kind_ns, kid)) {
-            ok = false, eval = false;
-          } else if (B.bit(S.p_kind_empty, kid) && !S.star_kind) {
-            ok = true, eval = false;
-          } else if (S.invalid) {
-            ok = false, eval = false;
-          }
-        }
-        if (eval) {
-#pragma unroll 1
-          for (uint32_t qi = 0; qi < S.nreq; ++qi) {
-            const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
-            const bool wild = q.op == SR_WILD;
-            uint32_t j = lo;
-#pragma unroll 1
-            for (; j < hi; ++j)  // first label with a matching key (and value, for wildcards)
-              if (B.bit(q.pk, K[j]) && (!wild || B.bit(q.pv, V[j]))) break;
-            const bool found = j < hi;
-            const uint32_t kid = found ? K[j] : KPE_NO_STR, vid = found ? V[j] : KPE_NO_STR;
-            bool qok;
-            switch (q.op) {
-              case SR_EQ:
-              case SR_IN: qok = found && B.bit(q.pv, vid); break;
-              case SR_WILD: qok = found && B.bit(q.pk_ok, kid) && B.bit(q.pv_ok, vid); break;
-              case SR_NOTIN: qok = !found || !B.bit(q.pv, vid); break;
-              case SR_EXISTS: qok = found; break;
-              default: qok = !found; break;
-            }
-            ok &= qok;
-          }
-        }
-      } else {  // T_FALSE
-        ok = false;
-      }
-      const uint64_t m = __ballot(ok);
+      const uint64_t m = __ballot(eval_term(a, B, sld(a.terms, ti), gvk, nsa, name_col, mns_col, rc, live));
       if (lane == 0) tmk[ti] = m;
     }
     // PSS version sets: resources failing some check of each distinct cv_mask
@@ -587,10 +904,8 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
       const uint64_t m = __ballot((fails & sld(a.cv_classes, c)) != 0u);
       if (lane == 0) cvm[c] = m;
     }
-    const uint32_t cls = (rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
     const uint64_t live_m = __ballot(live);
-    const uint64_t err_m = PSS ? __ballot(live && (cls == R_CLASS_OTHER || (rec.x & PR_DECODE_ERR))) : 0ull;
-    const uint32_t nrows = (uint32_t)min((int64_t)64, a.n - tile * 64);
+    const uint64_t err_m = __ballot(err);
     __builtin_amdgcn_wave_barrier();
 
     // ---- rules, KPE_RULE_CHUNK at a time ----
@@ -652,22 +967,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
         }
         __builtin_amdgcn_wave_barrier();
       }
-      // (b) counts: popcounts of the cell masks (rule lanes)
-      if (lane < nc) {
-        const uint32_t cp = (uint32_t)__popcll(rmk[lane * 3]), cf = (uint32_t)__popcll(rmk[lane * 3 + 1]),
-                       ce = (uint32_t)__popcll(rmk[lane * 3 + 2]);
-        const uint32_t ri = c0 + lane;
-        if (lds_cnt) {
-          if (cp) atomicAdd(&s_cnt[ri * 3 + 0], cp);
-          if (cf) atomicAdd(&s_cnt[ri * 3 + 1], cf);
-          if (ce) atomicAdd(&s_cnt[ri * 3 + 2], ce);
-        } else {
-          if (cp) atomicAdd(&a.counts_global[ri * 6 + KPE_PASS_], (unsigned long long)cp);
-          if (cf) atomicAdd(&a.counts_global[ri * 6 + KPE_FAIL_], (unsigned long long)cf);
-          if (ce) atomicAdd(&a.counts_global[ri * 6 + KPE_ERROR_], (unsigned long long)ce);
-        }
-      }
-      // (c) verdict bytes (resource lanes)
+      // (b) verdict bytes (resource lanes)
 #pragma unroll 4
       for (uint32_t j = 0; j < nc; ++j) {
         const uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
@@ -678,62 +978,54 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(ScanArgs a) {
       if (a.masks && live) {
 #pragma unroll 1
         for (uint32_t j = 0; j < nc; ++j) {
-          uint32_t cmask = 0;
-          if ((rmk[j * 3 + 1] >> lane) & 1u) {
-            const uint32_t f = fails & sld(a.rules, c0 + j).cv_mask;
-#pragma unroll 1
-            for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
-              if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
-          }
-          a.masks[r * R + c0 + j] = cmask;
+          const uint32_t cm = ((rmk[j * 3 + 1] >> lane) & 1u) ? check_mask(fails & sld(a.rules, c0 + j).cv_mask) : 0u;
+          a.masks[(size_t)r * R + c0 + j] = cm;
         }
       }
       __builtin_amdgcn_wave_barrier();
-      // (d) store the tile's row segments [c0, c0 + nc)
-      uint8_t* base = a.verdicts + (size_t)tile * 64 * R + c0;
-      if (nc == R && (R & 3u) == 0u) {  // whole rows, dword aligned: contiguous nrows x R bytes
-        uint32_t* dst = reinterpret_cast<uint32_t*>(base);
-        const uint32_t* src = reinterpret_cast<const uint32_t*>(sv);
-#pragma unroll 1
-        for (uint32_t i = lane; i < nrows * R / 4; i += 64) dst[i] = src[i];
-      } else if (nc == R) {
-#pragma unroll 1
-        for (uint32_t i = lane; i < nrows * R; i += 64) base[i] = sv[i];
-      } else {
-#pragma clang loop vectorize(disable) unroll(disable)
-        for (uint32_t i = lane; i < nrows * nc; i += 64) {
-          const uint32_t row = i / nc, col = i - row * nc;
-          base[(size_t)row * R + col] = sv[i];
-        }
-      }
+      store_rows(a.verdicts, sv, tile, R, c0, nc, nrows, lane);
       __builtin_amdgcn_wave_barrier();
     }
+    };
+  Tile<PSS> tb{};
+  while (tile < ntiles) {
+    step(ta, tb);
+    tile += W;
+    if (tile >= ntiles) break;
+    step(tb, ta);
+    tile += W;
   }
 
-  // ---- epilogue: per-block count partials ----
-  if (lds_cnt) {
-    __syncthreads();
-#pragma unroll 1
-    for (uint32_t i = t; i < 6 * R; i += kBlock) {
-      const uint32_t ri = i / 6, k = i - ri * 6;
-      const uint32_t v = k == KPE_PASS_ ? s_cnt[ri * 3] : k == KPE_FAIL_ ? s_cnt[ri * 3 + 1]
-                                                          : k == KPE_ERROR_ ? s_cnt[ri * 3 + 2] : 0u;
-      a.counts_part[(size_t)blockIdx.x * 6 * R + i] = v;
-    }
+  if (NARROW && prev_tile != 0xFFFFFFFFu) {
+    CArgs& a = *launder(ap);
+    const uint32_t R = a.nrules;
+    const uint8_t* last = reinterpret_cast<const uint8_t*>(dyn + a.wave_lds + wv * a.wave_words +
+                                                          (PSS ? KPE_STAGE_WORDS : 0u)) + (buf ^ 1u) * 64 * R;
+    store_rows(a.verdicts, last, prev_tile, R, 0, R, prev_rows, lane);
   }
 }
 
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers (called from kpe_api.cpp).
-extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s) {
-  if (nblocks == 0) return hipSuccess;
-  hipLaunchKernelGGL(kpe_pred_kernel, dim3(nblocks), dim3(256), 0, s, *a);
+// grid: x = blocks of the largest job, y = jobs
+extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipStream_t s) {
+  if (xblocks == 0 || a->njobs == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_pred_kernel, dim3(xblocks, a->njobs), dim3(256), 0, s, *a);
   return hipGetLastError();
 }
+
+namespace {
+typedef void (*ScanFn)(const ScanArgs*);
+ScanFn scan_fn(int pss, int narrow) {
+  if (pss) return narrow ? kpe_scan_kernel<true, true> : kpe_scan_kernel<true, false>;
+  return narrow ? kpe_scan_kernel<false, true> : kpe_scan_kernel<false, false>;
+}
+}  // namespace
+
 // Persistent grid: as many blocks as can be resident at once (occupancy x CUs),
 // capped by the number of 256-resource tiles.
-extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, size_t dyn_bytes) {
+extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes) {
   if (n <= 0) return 0;
   static thread_local int cus = 0;
   if (!cus) {
@@ -742,26 +1034,31 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, size_t dyn_bytes) {
       cus = 256;
   }
   int per_cu = 0;
-  if (pss) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kpe_scan_kernel<true>, kBlock, dyn_bytes) != hipSuccess) per_cu = 1;
-  } else {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kpe_scan_kernel<false>, kBlock, dyn_bytes) != hipSuccess) per_cu = 1;
-  }
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn(pss, narrow), kBlock, dyn_bytes) != hipSuccess)
+    per_cu = 1;
   const int64_t tiles = (n + kBlock - 1) / kBlock;
   const int64_t g = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
   return (uint32_t)(g < tiles ? g : tiles);
 }
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, uint32_t grid, size_t dyn_bytes, hipStream_t s) {
-  if (a->n == 0 || grid == 0) return hipSuccess;
-  if (pss)
-    hipLaunchKernelGGL(kpe_scan_kernel<true>, dim3(grid), dim3(kBlock), dyn_bytes, s, *a);
-  else
-    hipLaunchKernelGGL(kpe_scan_kernel<false>, dim3(grid), dim3(kBlock), dyn_bytes, s, *a);
+// `dargs` is the device copy of the arguments; `n` its row count.
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
+                                      size_t dyn_bytes, hipStream_t s) {
+  if (n == 0 || grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
   return hipGetLastError();
 }
-extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
-                                              unsigned long long* out, hipStream_t s) {
-  if (width == 0) return hipSuccess;
-  hipLaunchKernelGGL(kpe_count_reduce, dim3(width), dim3(256), 0, s, part, nblocks, width, out);
-  return hipGetLastError();
+extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
+                                       hipStream_t s) {
+  if (R == 0) return hipSuccess;
+  hipError_t e = hipMemsetAsync(out, 0, (size_t)R * 6 * 8, s);
+  if (e != hipSuccess || n == 0) return e;
+  const int64_t waves = (n + 63) / 64;
+  const uint32_t grid = (uint32_t)std::min<int64_t>((waves + 3) / 4, 1024);
+  for (uint32_t r0 = 0; r0 < R; r0 += 2048) {  // <= 48 KiB of LDS histogram per launch
+    const uint32_t rn = std::min<uint32_t>(2048, R - r0);
+    hipLaunchKernelGGL(kpe_count_kernel, dim3(grid), dim3(256), (size_t)rn * 6 * 4, s, verdicts, n, R, r0, rn, out);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }

@@ -45,7 +45,8 @@ struct PredArgs {
   const uint32_t* dict_off[KPE_NUM_DOMAINS];
   uint32_t dict_n[KPE_NUM_DOMAINS];
   const uint8_t* pat_bytes;
-  const KpePat* pats;
+  uint32_t pat_len;
+  const KpePat* pats;  // pattern records
   const PredJob* jobs;
   uint32_t njobs;
   uint32_t* out;
@@ -56,7 +57,6 @@ struct PredArgs {
 // bitset locations: PRED_LOCAL | LDS word index, or a pbuf word index; PRED_NONE = absent.
 #define PRED_NONE 0xFFFFFFFFu
 #define KPE_RULE_CHUNK 32  // rules evaluated per transposed pass (one rule per lane)
-#define KPE_LDS_R 256      // rules counted in LDS per block (more: global atomics)
 
 // Rule lane record (uint4, one per rule, evaluated by one lane in the transposed pass):
 //   x = handler | cv_class << 4 | match_mode << 16 | excl_mode << 18
@@ -67,6 +67,29 @@ struct PredArgs {
 #define RL_EXCL_MODE(x) (((x) >> 18) & 3u)
 #define RL_F0(y) ((y) & 0xFFFFFFu)
 #define RL_NF(y) ((y) >> 24)
+
+// NARROW programs (<= KPE_NARROW_TERMS distinct terms, <= KPE_NARROW_R rules): each
+// lane evaluates every rule for its own resource from a term bit vector.
+// Narrow rule record (uint4): x = handler | match_mode << 4 | excl_mode << 6 |
+//   NR_APPLY_ONE | NR_NEW_POLICY | (pol_term + 1) << 16 (0: no namespaced-policy term),
+//   y = cv_mask, z = match filters (RL_F0 / RL_NF), w = exclude filters;
+//   fmask[f] = bit mask of the terms filter f ANDs.
+#define KPE_NARROW_TERMS 32
+#define KPE_NARROW_R 32
+#define KPE_NARROW_FILTERS 64
+#define KPE_TT_TERMS 8
+#define NR_HANDLER(x) ((x) & 0xFu)
+#define NR_MATCH_MODE(x) (((x) >> 4) & 3u)
+#define NR_EXCL_MODE(x) (((x) >> 6) & 3u)
+#define NR_APPLY_ONE (1u << 8)
+#define NR_NEW_POLICY (1u << 9)
+#define NR_POLTERM(x) ((x) >> 16)
+
+// Per-wave PSS list staging (LDS): 128 container entries (uint2) + 64 one-byte codes
+// each for volumes, sysctls and pod annotations.
+#define KPE_STAGE_CTR 128
+#define KPE_STAGE_SMALL 64
+#define KPE_STAGE_WORDS ((KPE_STAGE_CTR * 8 + 3 * KPE_STAGE_SMALL) / 4)
 
 struct ScanArgs {
   int64_t n;
@@ -82,12 +105,22 @@ struct ScanArgs {
   const uint32_t* sys_id;     // per sysctl: D_SYSCTL id
   const uint32_t* pann_kv;    // per pod-template annotation: (D_ANNK id, D_ANNV id)
   const uint32_t* c_sann;     // per container: value id of its seccomp annotation (cold)
+  uint32_t ntiles;            // ceil(n / 64); hdr has ntiles + 1 entries
+  const uint32_t* zero_page;  // >= 64 zero bytes: source of the loads of unneeded columns
   const uint32_t* capsets;    // capability-set dictionary: 4 words (add lo/hi, drop lo/hi) per set
   uint32_t ncapsets;
   uint32_t nctr_total, nvol_total, nsys_total, npann_total;  // list lengths (load clamping)
   // program tables; predicate fields resolved to bitset locations (binding copies)
   const KpeRule* rules;
   const uint32_t* rule_lanes;  // packed rule lane records (RL_*)
+  const uint32_t* narrow_rules;  // NARROW: 4 words per rule (NR_*)
+  const uint32_t* fmask;         // NARROW: term mask per filter
+  uint32_t nfilters;
+  // NARROW truth-table fast path (tt_lds != PRED_NONE: <= KPE_TT_TERMS terms, no ApplyOne):
+  // every block tabulates matched-rule masks for all 2^nterms term vectors in LDS at
+  // tt_lds; narrow_cls holds (cv_mask, rule mask) per distinct PSS version set.
+  uint32_t tt_lds, ncls, pss_rules, err_rules;
+  const uint32_t* narrow_cls;
   const KpeFilter* filters;
   const uint32_t* fterms;
   const KpeTerm* terms;
@@ -103,14 +136,19 @@ struct ScanArgs {
   // every block (same word indices); the rest = large-domain bitsets (HBM/L2)
   const uint32_t* pbuf;
   uint32_t blob_words;
+  // fused dictionary pass (fuse_words == 0: the bitsets come from pbuf's blob instead)
+  // fuse image (all LDS-resident after one copy): [FuseJob table][KpePat table]
+  // [pattern bytes][per small domain: offsets, bytes]
+  const uint32_t* fuse;
+  uint32_t fuse_words, fuse_lds;  // image size and its LDS word offset
+  uint32_t nfjobs, npairs;        // jobs, total (job, dictionary string) pairs
+  uint32_t fuse_pats, fuse_patb;  // LDS word index of the pattern table / pattern bytes
   uint32_t wave_lds, wave_words;  // per-wave LDS regions: dyn[wave_lds + wv * wave_words ...]
   // fixed PSS predicates (resolved locations)
   uint32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   uint32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, need;
   // outputs
-  uint8_t* verdicts;                 // n x nrules
-  uint32_t* masks;                   // n x nrules or null
-  uint32_t* counts_part;             // gridDim x nrules x 6 (nrules <= KPE_LDS_R)
-  unsigned long long* counts_global; // nrules x 6 (nrules > KPE_LDS_R)
+  uint8_t* verdicts;  // n x nrules
+  uint32_t* masks;    // n x nrules or null
 };

@@ -5,6 +5,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -24,10 +26,11 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* a, int pss, uint32_t grid, size_t dyn_bytes, hipStream_t s);
-extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, size_t dyn_bytes);
-extern "C" hipError_t kpe_launch_count_reduce(const uint32_t* part, uint32_t nblocks, uint32_t width,
-                                              unsigned long long* out, hipStream_t s);
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
+                                      size_t dyn_bytes, hipStream_t s);
+extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
+extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
+                                       hipStream_t s);
 
 namespace {
 thread_local std::string g_err;
@@ -111,7 +114,11 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
-  DevBuf rules, rule_lanes, filters, fterms, terms, kindsels, annpairs, selectors, selreqs, pat_bytes, pats;
+  DevBuf rules, rule_lanes, narrow_rules, fmask, narrow_cls, filters, fterms, terms, kindsels, annpairs, selectors, selreqs,
+      pat_bytes, pats;
+  bool narrow = false;  // per-lane rule loop (kernels_abi.h NR_*)
+  bool tt = false;      // + truth-table fast path
+  uint32_t ncls = 0, pss_rules = 0, err_rules = 0;
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
@@ -119,10 +126,14 @@ struct DeviceProgram {
 
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
   const Program* prog = nullptr;
-  DevBuf jobs, pbuf, verdicts, masks, counts_part, counts_global, counts_out;
+  DevBuf jobs, pbuf, verdicts, masks, counts_out;
+  DevBuf dargs;        // device copy of the scan arguments (kernel reads them with scalar loads)
+  DevBuf zero_page;    // 256 zero bytes (loads of columns a program does not read)
+  ScanArgs hargs{};    // what dargs holds
+  bool args_valid = false;
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
   uint32_t pp[10] = {};  // fixed PSS predicate locations
-  uint32_t wave_lds = 0, wave_words = 0, filt_lds = PRED_NONE, fterm_lds = 0;
+  uint32_t wave_lds = 0, wave_words = 0, filt_lds = PRED_NONE, fterm_lds = 0, tt_lds = PRED_NONE;
   size_t dyn_bytes = 0;
   uint32_t nblocks = 0, njobs = 0, blob_words = 0, scan_blocks = 0;
   uint32_t need = 0;
@@ -334,9 +345,55 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     lanes.push_back(r.excl_f0 | r.excl_nf << 24);
     lanes.push_back(r.pol_term < 0 ? PRED_NONE : (uint32_t)r.pol_term);
   }
+  // NARROW programs: per-rule records + per-filter term masks (kernels_abi.h NR_*)
+  const bool narrow = !P.rules.empty() && P.rules.size() <= KPE_NARROW_R && P.terms.size() <= KPE_NARROW_TERMS &&
+                      P.filters.size() <= KPE_NARROW_FILTERS;
+  std::vector<uint32_t> nrules, fmask;
+  if (narrow) {
+    for (auto& f : P.filters) {
+      uint32_t m = 0;
+      for (uint32_t k = 0; k < f.nt; ++k) m |= 1u << P.fterms[f.t0 + k];
+      fmask.push_back(m);
+    }
+    uint32_t prev_policy = 0xFFFFFFFFu;
+    for (auto& r : P.rules) {
+      uint32_t x = r.handler | r.match_mode << 4 | r.excl_mode << 6;
+      if (r.apply_one) x |= NR_APPLY_ONE;
+      if (r.policy != prev_policy) x |= NR_NEW_POLICY;
+      prev_policy = r.policy;
+      if (r.pol_term >= 0) x |= ((uint32_t)r.pol_term + 1u) << 16;
+      nrules.push_back(x);
+      nrules.push_back(r.cv_mask);
+      nrules.push_back(r.match_f0 | r.match_nf << 24);
+      nrules.push_back(r.excl_f0 | r.excl_nf << 24);
+    }
+  }
+  // truth-table fast path: few terms, no ApplyOne; per PSS version set its rule mask
+  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_apply_one;
+  std::vector<uint32_t> cls;  // (cv_mask, rule mask) pairs
+  uint32_t pss_rules = 0, err_rules = 0;
+  if (tt) {
+    for (size_t r = 0; r < P.rules.size(); ++r) {
+      const auto& k = P.rules[r];
+      if (k.handler == H_PSS) {
+        pss_rules |= 1u << r;
+        size_t c = 0;
+        while (c < cls.size() && cls[c] != k.cv_mask) c += 2;
+        if (c == cls.size()) cls.push_back(k.cv_mask), cls.push_back(0);
+        cls[c + 1] |= 1u << r;
+      } else if (k.handler == H_ERROR) {
+        err_rules |= 1u << r;
+      }
+    }
+  }
   delete P.dev;
   P.dev = new kpe::DeviceProgram();
   auto& D = *P.dev;
+  D.narrow = narrow;
+  D.tt = tt;
+  D.ncls = (uint32_t)cls.size() / 2;
+  D.pss_rules = pss_rules;
+  D.err_rules = err_rules;
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
   for (auto& pr : P.preds) {
@@ -349,6 +406,9 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   }
   HIPCHK(upload(D.rules, P.rules, s));
   HIPCHK(upload(D.rule_lanes, lanes, s));
+  HIPCHK(upload(D.narrow_rules, nrules, s));
+  HIPCHK(upload(D.fmask, fmask, s));
+  HIPCHK(upload(D.narrow_cls, cls, s));
   HIPCHK(upload(D.filters, P.filters, s));
   HIPCHK(upload(D.fterms, P.fterms, s));
   HIPCHK(upload(D.terms, P.terms, s));
@@ -387,7 +447,7 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   return need;
 }
-double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks, uint32_t grid_blocks) {
+double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
   double b = 0;
   const double n = (double)C.n;
   if (P.any_pss) {
@@ -408,7 +468,6 @@ double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bo
   if (need & NEED_LAB) b += 4.0 * n + 8.0 * C.lab_k.size();
   if (need & NEED_NSL) b += 4.0 * n;  // r_nsl; the namespace table itself is cache-resident
   b += n * P.rules.size() * (masks ? 5.0 : 1.0);  // verdict cells (+ check masks)
-  if (P.rules.size() <= KPE_LDS_R) b += 4.0 * grid_blocks * 6 * P.rules.size();  // count partials
   return b;
 }
 
@@ -420,20 +479,23 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   size_t cells = (size_t)C.n * P.rules.size();
   if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
   hipStream_t s = dev->stream;
-  // Preamble layout (pbuf): [program image][predicate directory][small-domain bitsets]
-  // (padded to 16 B; copied into LDS by every scan block) followed by the large-domain
-  // bitsets. Every predicate is evaluated by the dictionary pass straight into pbuf.
-  // pbuf: [small-domain bitsets (copied into LDS by every scan block)][large-domain
-  // bitsets]. Predicate references in the scan tables are resolved to these locations.
-  // Dynamic LDS per scan block: [bitsets][filters + filter terms][4 per-wave regions].
+  // Predicates over small dictionaries get LDS-resident bitsets ("local": every scan
+  // block copies them from pbuf's blob), the rest are read from pbuf (HBM/L2). All are
+  // evaluated per evaluation by kpe_pred_kernel (grid x = strings / 256, y = predicate).
+  // pbuf: [local bitsets (blob)][large-domain bitsets].
+  // Dynamic LDS per scan block: [local bitsets][filters + filter terms][4 per-wave regions].
   const uint32_t npreds = (uint32_t)P.preds.size();
   const uint32_t nterms = (uint32_t)P.terms.size(), ncv = (uint32_t)P.cv_classes.size();
   if (nterms > kMaxTerms) return fail(KPE_E_LIMIT, "program has more than 1024 distinct match terms");
-  const uint32_t wave_words = 2 * nterms + 2 * ncv + 2 * 3 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4;
+  const bool narrow = PD.narrow;
+  const uint32_t wave_words = (P.any_pss ? KPE_STAGE_WORDS : 0u) +
+                              (narrow ? 2 * 64 * (uint32_t)P.rules.size() / 4  // double-buffered rows
+                                      : 2 * nterms + 2 * ncv + 2 * 3 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4);
   const uint32_t prog_words = 2 * (uint32_t)P.filters.size() + (uint32_t)P.fterms.size();
-  const bool stage_prog = prog_words <= kMaxProgLds;
+  const bool stage_prog = !narrow && prog_words <= kMaxProgLds;
   const int64_t budget =
-      (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8;
+      (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 -
+      (PD.tt ? (1 << KPE_TT_TERMS) : 0);
   if (budget < 0) return fail(KPE_E_LIMIT, "program does not fit the scan kernel's LDS budget");
   const uint32_t local_budget = (uint32_t)std::min<int64_t>(kMaxLocalWords, budget);
   std::vector<uint32_t> nwords(npreds);
@@ -462,11 +524,11 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
       go += nwords[p];
       dir[p] = at;
     }
-    uint32_t n = C.dict[P.preds[p].domain].size();
+    const uint32_t d = P.preds[p].domain, n = C.dict[d].size();
     if (n) {
       const uint32_t pend = p + 1 < PD.pat0.size() ? PD.pat0[p + 1] : (uint32_t)PD.pats_h.size();
-      jobs.push_back({P.preds[p].domain, PD.pat0[p], pend - PD.pat0[p], at, blk});
-      blk += (n + 255) / 256;
+      jobs.push_back({d, PD.pat0[p], pend - PD.pat0[p], at, 0});
+      blk = std::max(blk, (n + 255) / 256);  // grid x extent (grid y = jobs)
     }
   }
   auto loc = [&](int32_t p) -> uint32_t { return p < 0 ? PRED_NONE : dir[(size_t)p]; };
@@ -496,9 +558,14 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const int32_t fixed[10] = {ps.apparmor_key, ps.apparmor_val_ok, ps.seccomp_pod_key, ps.seccomp_ann_ok,
                              ps.caps_baseline_ok, ps.cap_nbs, ps.cap_all, ps.sysctl[0], ps.sysctl[1], ps.sysctl[2]};
   for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
-  B.filt_lds = stage_prog ? blob : PRED_NONE;
-  B.fterm_lds = blob + 2 * (uint32_t)P.filters.size();
-  B.wave_lds = (blob + (stage_prog ? prog_words : 0) + 1) & ~1u;
+  const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
+  const uint32_t tt_at = blob;
+  const uint32_t prog_at = blob + ((tt_words + 3) & ~3u);
+  B.tt_lds = PD.tt ? tt_at : PRED_NONE;
+  B.filt_lds = stage_prog ? prog_at : PRED_NONE;
+  B.fterm_lds = prog_at + 2 * (uint32_t)P.filters.size();
+  B.wave_lds = (prog_at + (stage_prog ? prog_words : 0) + 1) & ~1u;
+
   B.wave_words = wave_words;
   B.dyn_bytes = (size_t)(B.wave_lds + 4 * wave_words) * 4;
   HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
@@ -506,19 +573,26 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.blob_words = blob;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, B.dyn_bytes);
+  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
-  size_t width = P.rules.size() * 6;
-  HIPCHK(B.counts_part.ensure(std::max<size_t>((size_t)B.scan_blocks * width, 1) * 4));
-  HIPCHK(B.counts_global.ensure(std::max<size_t>(width, 1) * 8));
-  HIPCHK(B.counts_out.ensure(std::max<size_t>(width, 1) * 8));
+  HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 6, 1) * 8));
+  if (!B.zero_page.p) {
+    HIPCHK(B.zero_page.ensure(256));
+    HIPCHK(hipMemsetAsync(B.zero_page.p, 0, 256, s));
+  }
   if (want_masks) {
     HIPCHK(B.masks.ensure(std::max<size_t>(cells, 1) * 4));
     cc->d->has_masks = true;
   }
+  if (getenv("KPE_DEBUG")) {
+    fprintf(stderr, "kpe bind: n=%lld R=%zu narrow=%d blob=%u pred_jobs=%u pred_xblocks=%u scan_blocks=%u dyn=%zu "
+            "wave_words=%u\n", (long long)C.n, P.rules.size(), (int)narrow, blob, (unsigned)jobs.size(), blk,
+            B.scan_blocks, B.dyn_bytes, wave_words);
+  }
   HIPCHK(hipStreamSynchronize(s));
   B.need = need_flags(P);
+  B.args_valid = false;
   B.prog = &P;
   B.cells = cells;
   return KPE_OK;
@@ -547,15 +621,16 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.dict_n[i] = C.dict[i].size();
     }
     pa.pat_bytes = PD.pat_bytes.as<uint8_t>();
+    pa.pat_len = (uint32_t)PD.pat_bytes_h.size();
     pa.pats = PD.pats.as<KpePat>();
     pa.jobs = B.jobs.as<PredJob>();
     pa.njobs = B.njobs;
     pa.out = B.pbuf.as<uint32_t>();
     HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
   }
-  if (R > KPE_LDS_R) HIPCHK(hipMemsetAsync(B.counts_global.p, 0, R * 6 * 8, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
-  ScanArgs sa{};
+  ScanArgs sa;
+  memset(&sa, 0, sizeof(sa));  // padding too: compared bytewise
   sa.n = C.n;
   sa.r_gvk = D.r_gvk.as<uint32_t>();
   sa.r_name = D.r_name.as<uint32_t>();
@@ -578,6 +653,9 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.sys_id = D.sys_id.as<uint32_t>();
   sa.pann_kv = D.pann_kv.as<uint32_t>();
   sa.c_sann = D.c_sann.as<uint32_t>();
+  sa.ntiles = (uint32_t)((C.n + 63) / 64);
+  sa.zero_page = B.zero_page.as<uint32_t>();
+
   sa.capsets = D.capsets.as<uint32_t>();
   sa.ncapsets = (uint32_t)C.capset_add.size();
   sa.nctr_total = (uint32_t)C.c_sc.size();
@@ -586,6 +664,14 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.npann_total = (uint32_t)(C.pann_kv.size() / 2);
   sa.rules = PD.rules.as<KpeRule>();
   sa.rule_lanes = PD.rule_lanes.as<uint32_t>();
+  sa.narrow_rules = PD.narrow_rules.as<uint32_t>();
+  sa.fmask = PD.fmask.as<uint32_t>();
+  sa.nfilters = (uint32_t)P.filters.size();
+  sa.tt_lds = B.tt_lds;
+  sa.ncls = PD.ncls;
+  sa.pss_rules = PD.pss_rules;
+  sa.err_rules = PD.err_rules;
+  sa.narrow_cls = PD.narrow_cls.as<uint32_t>();
   sa.nrules = (uint32_t)R;
   sa.filters = PD.filters.as<KpeFilter>();
   sa.fterms = PD.fterms.as<uint32_t>();
@@ -619,12 +705,18 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.need = B.need;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
-  sa.counts_part = B.counts_part.as<uint32_t>();
-  sa.counts_global = B.counts_global.as<unsigned long long>();
-  HIPCHK(kpe_launch_scan(&sa, P.any_pss ? 1 : 0, B.scan_blocks, B.dyn_bytes, s));
+  if (!B.args_valid || memcmp(&sa, &B.hargs, sizeof(ScanArgs)) != 0) {  // once per binding / masks mode
+    HIPCHK(B.dargs.ensure(sizeof(ScanArgs)));
+    B.hargs = sa;
+    HIPCHK(hipMemcpyAsync(B.dargs.p, &B.hargs, sizeof(ScanArgs), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    B.args_valid = true;
+  }
+  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.scan_blocks,
+                         B.dyn_bytes, s));
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.c, s));
-    ev.bytes = scan_bytes(P, C, B.need, masks, B.scan_blocks);
+    ev.bytes = scan_bytes(P, C, B.need, masks);
     dev->pending.push_back(ev);
   }
   return KPE_OK;
@@ -668,12 +760,9 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
   size_t R = prog->p->rules.size(), cells = (size_t)c->c->n * R;
   hipStream_t s = dev->stream;
   if (counts && R) {
-    const unsigned long long* src = B.counts_global.as<unsigned long long>();
-    if (R <= KPE_LDS_R) {
-      HIPCHK(kpe_launch_count_reduce(B.counts_part.as<uint32_t>(), B.scan_blocks, (uint32_t)(R * 6),
-                                     B.counts_out.as<unsigned long long>(), s));
-      src = B.counts_out.as<unsigned long long>();
-    }
+    // per-rule totals from the verdict matrix (processor/result.go:34-68 counting)
+    HIPCHK(kpe_launch_count(B.verdicts.as<uint8_t>(), c->c->n, (uint32_t)R, B.counts_out.as<unsigned long long>(), s));
+    const unsigned long long* src = B.counts_out.as<unsigned long long>();
     std::vector<unsigned long long> h(R * 6);
     HIPCHK(hipMemcpyAsync(h.data(), src, R * 6 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));

@@ -91,11 +91,11 @@ enum KpeDomain {
 // Pod record (uint4, one dwordx4 per lane):
 //   x = pod word p_sc (bits 0..19) | R_CLASS << PR_CLASS_SH | PR_DECODE_ERR
 //   y = r_gvk, z = list counts (PRC_*), w = r_nsa (namespace id)
-// Wave header (uint4 per 64 pods): first container / volume / sysctl / pod-annotation
-//   index of the wave; a lane's own offsets are the header plus an exclusive wave scan
-//   of the counts.
-// Container record (uint2): x = c_sc, y = capability-set id (dictionary of distinct
-//   (add, drop) capability masks).
+// Wave header (uint4 per 64 pods, plus one sentinel): first container / volume / sysctl /
+//   pod-annotation index of the tile; tile t's lists are [hdr[t], hdr[t+1]) and a lane's
+//   own offsets are the exclusive wave scan of the counts.
+// Container record (uint2): x = container state bitmap (CX_*), y = capability-set id
+//   (dictionary of distinct (add, drop) capability masks) | type << 16.
 #define PR_CLASS_SH 20
 #define PR_DECODE_ERR (1u << 22)
 #define PRC_CTR(z) ((z) & 0xFFu)
@@ -120,6 +120,46 @@ enum KpeDomain {
 #define C_CAPS_PRESENT (1u << 21)
 #define C_TYPE_SH 22       // 0 initContainers, 1 containers, 2 ephemeralContainers
 #define C_HOSTPORT_SH 24   // 4 bits: number of ports with hostPort != 0 (saturating at 15)
+
+// ---- container state bitmap (crec.x of the scan's container record) ------------------
+// One bit per STATE of each securityContext field the PSA checks read (a bitmap
+// index of c_sc: exactly one bit of every group is set). The PSA container checks are
+// all "some container is in state s", so a pod's OR of its containers' bitmaps is a
+// sufficient statistic: the scan ORs 1..255 records and decides the checks once per pod.
+#define CX_PRIV_T (1u << 0)
+#define CX_PRIV_F (1u << 1)
+#define CX_PRIV_U (1u << 2)
+#define CX_APE_T (1u << 3)
+#define CX_APE_F (1u << 4)
+#define CX_APE_U (1u << 5)
+#define CX_RNR_T (1u << 6)
+#define CX_RNR_F (1u << 7)
+#define CX_RNR_U (1u << 8)
+#define CX_RAU_NZ (1u << 9)
+#define CX_RAU_Z (1u << 10)
+#define CX_RAU_U (1u << 11)
+#define CX_SEC_NONE (1u << 12)    // seccompProfile == nil
+#define CX_SEC_RD (1u << 13)      // RuntimeDefault
+#define CX_SEC_LH (1u << 14)      // Localhost
+#define CX_SEC_UNC (1u << 15)     // Unconfined
+#define CX_SEC_OTHER (1u << 16)   // any other type string
+#define CX_PM_U (1u << 17)        // procMount unset
+#define CX_PM_DEFAULT (1u << 18)
+#define CX_PM_OTHER (1u << 19)
+#define CX_SEL_NONE (1u << 20)    // seLinuxOptions == nil
+#define CX_SEL_OK (1u << 21)      // type "", container_t, container_init_t, container_kvm_t
+#define CX_SEL_OTHER (1u << 22)   // any other type
+#define CX_SEL_USER (1u << 23)    // user != "" (only with seLinuxOptions set)
+#define CX_SEL_ROLE (1u << 24)    // role != ""
+#define CX_WHP_T (1u << 25)       // windowsOptions.hostProcess == true
+#define CX_WHP_NT (1u << 26)      // hostProcess unset or false
+#define CX_CAPS (1u << 27)        // capabilities present
+#define CX_NOCAPS (1u << 28)
+#define CX_HOSTPORT (1u << 29)    // some port with hostPort != 0
+#define CX_NOHOSTPORT (1u << 30)
+#define CX_SC (1u << 31)          // securityContext present
+// crec.y = capability-set id (bits 0..15) | container type (C_TYPE) << 16
+#define CY_CAPSET(y) ((y) & 0xFFFFu)
 
 // ---- volumes: vol_src bit i = corev1.VolumeSource field i present (declaration order) ----
 #define KPE_NUM_VOLUME_SOURCES 29

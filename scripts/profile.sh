@@ -10,7 +10,7 @@ run() {  # run <name> <timeout> <rocprof args...>
   echo "== $name"
   timeout -k 10 "$to" rocprofv3 "$@" -d gpurun_out/prof_$name -o $name --output-format csv -- python3 bench.py $ARGS > gpurun_out/prof_$name.log 2>&1
   local rc=$?
-  echo "== $name rc=$rc"; tail -n 3 gpurun_out/prof_$name.log
+  echo "== $name rc=$rc"; tail -n 2 gpurun_out/prof_$name.log
   if [ $rc -ge 124 ]; then exit $rc; fi
 }
 run trace 300 --kernel-trace --stats
@@ -18,5 +18,4 @@ run pmc_sq 300 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_IN
 [ -n "$QUICK" ] || run pmc_fetch 300 --pmc FETCH_SIZE
 [ -n "$QUICK" ] || run pmc_write 300 --pmc WRITE_SIZE
 run pmc_busy 300 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY
-run pmc_lds 300 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR SQ_WAVES
-find gpurun_out -name "*stats*.csv" -o -name "*counter_collection*.csv" | head -20
+run pmc_lds 300 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH SQ_INSTS_VMEM_WR SQ_WAVES SQ_INSTS_SMEM SQ_INST_CYCLES_SALU
