@@ -682,11 +682,19 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
   if (PSS && (a0.need & NEED_CAPS) && t < a0.ncapsets) cs0 = reinterpret_cast<const uint4*>(a0.capsets)[t];
   {
     CArgs& a = a0;
-    // small-domain predicate bitsets (kpe_pred_kernel output) into LDS
-    const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
-    uint4* d4 = reinterpret_cast<uint4*>(dyn);
+    if (a.npairs) {  // fused dictionary pass: stage the fuse image, clear the local bitsets
+      const uint4* src = reinterpret_cast<const uint4*>(a.fuse);
+      uint4* f4 = reinterpret_cast<uint4*>(dyn + a.fuse_lds);
 #pragma unroll 1
-    for (uint32_t i = t; i < (a.blob_words >> 2); i += kBlock) d4[i] = blob[i];
+      for (uint32_t i = t; i < (a.fuse_words >> 2); i += kBlock) f4[i] = src[i];
+#pragma unroll 1
+      for (uint32_t i = t; i < a.blob_words; i += kBlock) dyn[i] = 0;
+    } else {  // small-domain predicate bitsets (kpe_pred_kernel output) into LDS
+      const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
+      uint4* d4 = reinterpret_cast<uint4*>(dyn);
+#pragma unroll 1
+      for (uint32_t i = t; i < (a.blob_words >> 2); i += kBlock) d4[i] = blob[i];
+    }
     if (!NARROW && a.filt_lds != PRED_NONE) {  // program filters + filter terms for the rule lanes
       const uint32_t nw = a.fterm_lds + a.nfterms - a.filt_lds;
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.filters);
@@ -696,6 +704,20 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
     }
   }
   __syncthreads();
+  if (a0.npairs && !(KPE_DIAG & DIAG_NOPRO)) {  // one short LDS compare per (string, pattern)
+    CArgs& a = a0;
+    const uint2* pairs = reinterpret_cast<const uint2*>(dyn + a.fuse_lds);
+    const KpePat* pats = reinterpret_cast<const KpePat*>(dyn + a.fuse_pats);
+    const uint8_t* lb = reinterpret_cast<const uint8_t*>(dyn);
+    const uint8_t* pb = lb + a.fuse_patb * 4;
+#pragma unroll 1
+    for (uint32_t i = t; i < a.npairs; i += kBlock) {
+      const uint2 e = pairs[i];
+      if (pat_match(pats[e.y & 0xFFFu], pb, lb + (e.x & 0xFFFFFu), (int)(e.x >> 20)))
+        atomicOr(&dyn[(e.y >> 12) & 0x7FFFu], 1u << (e.y >> 27));
+    }
+    __syncthreads();
+  }
   if (PSS && !(KPE_DIAG & DIAG_NOPRO)) {
     CArgs& a = a0;
     const Bits B{dyn, a.pbuf};

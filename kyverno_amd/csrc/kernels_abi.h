@@ -136,12 +136,13 @@ struct ScanArgs {
   // every block (same word indices); the rest = large-domain bitsets (HBM/L2)
   const uint32_t* pbuf;
   uint32_t blob_words;
-  // fused dictionary pass (fuse_words == 0: the bitsets come from pbuf's blob instead)
-  // fuse image (all LDS-resident after one copy): [FuseJob table][KpePat table]
-  // [pattern bytes][per small domain: offsets, bytes]
+  // Fused dictionary pass (npairs > 0): every block evaluates the small-domain
+  // predicates itself from the binding's fuse image, copied into LDS at fuse_lds:
+  // [pair table (uint2 per (string, pattern))][KpePat table][pattern bytes][strings].
+  // Pair: x = string LDS byte address | length << 20; y = pattern index |
+  // bitset word << 12 | bit << 27 (OR-ed in with an LDS atomic).
   const uint32_t* fuse;
-  uint32_t fuse_words, fuse_lds;  // image size and its LDS word offset
-  uint32_t nfjobs, npairs;        // jobs, total (job, dictionary string) pairs
+  uint32_t fuse_words, fuse_lds, npairs;
   uint32_t fuse_pats, fuse_patb;  // LDS word index of the pattern table / pattern bytes
   uint32_t wave_lds, wave_words;  // per-wave LDS regions: dyn[wave_lds + wv * wave_words ...]
   // fixed PSS predicates (resolved locations)

@@ -83,6 +83,8 @@ constexpr uint32_t kMaxDynWords = 13312;   // dynamic LDS per scan block (52 KiB
 constexpr uint32_t kMaxTerms = 1024;       // distinct match terms (term masks: 8 B x 4 waves each)
 constexpr uint32_t kMaxProgLds = 4096;     // filters + filter terms staged in LDS
 constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
+constexpr uint32_t kMaxFuseWords = 4096;   // fuse image <= 16 KiB of LDS
+constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated per block
 
 }  // namespace
 
@@ -129,6 +131,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf jobs, pbuf, verdicts, masks, counts_out;
   DevBuf dargs;        // device copy of the scan arguments (kernel reads them with scalar loads)
   DevBuf zero_page;    // 256 zero bytes (loads of columns a program does not read)
+  DevBuf fuse;         // fused dictionary pass image (pairs, patterns, small dictionaries)
+  uint32_t fuse_lds = 0, fuse_words = 0, npairs = 0, fuse_pats = 0, fuse_patb = 0;
   ScanArgs hargs{};    // what dargs holds
   bool args_valid = false;
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
@@ -510,8 +514,51 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     }
   }
   const uint32_t blob = std::max(4u, (lw + 3) & ~3u);
+  // Fused dictionary pass: when every small-domain (local) predicate's strings and the
+  // pattern bytes fit the fuse budget, the scan blocks evaluate them in their prologue
+  // from a pair table; the dictionary kernel then only runs for large domains.
+  size_t fuse_strings = 0, fuse_pairs = 0;
+  bool fusable = lw > 0 && PD.pats_h.size() <= 4096;
+  for (uint32_t p = 0; p < npreds && fusable; ++p) {
+    if (!local[p]) continue;
+    const auto& D0 = C.dict[P.preds[p].domain];
+    const uint32_t pend = p + 1 < PD.pat0.size() ? PD.pat0[p + 1] : (uint32_t)PD.pats_h.size();
+    fuse_pairs += (size_t)D0.size() * (pend - PD.pat0[p]);
+    for (uint32_t i = 0; i < D0.size(); ++i)
+      if (D0.off[i + 1] - D0.off[i] > 4095) fusable = false;
+  }
+  std::vector<bool> dom_seen(KPE_NUM_DOMAINS, false);
+  for (uint32_t p = 0; p < npreds; ++p)
+    if (local[p] && !dom_seen[P.preds[p].domain]) {
+      dom_seen[P.preds[p].domain] = true;
+      fuse_strings += C.dict[P.preds[p].domain].bytes.size();
+    }
+  const size_t fuse_est = 2 * fuse_pairs + 4 * PD.pats_h.size() + (PD.pat_bytes_h.size() + fuse_strings) / 4 + 16;
+  const bool fused = fusable && fuse_pairs <= kMaxFusePairs && fuse_est <= kMaxFuseWords &&
+                     budget - (int64_t)blob - (int64_t)fuse_est >= 0;
   std::vector<uint32_t> dir(npreds);
   std::vector<PredJob> jobs;
+  std::vector<uint32_t> fimg;  // fuse image (words)
+  std::vector<uint32_t> pairs;
+  std::vector<int64_t> dom_byte(KPE_NUM_DOMAINS, -1);  // byte offset of a domain's strings in the image
+  uint32_t fpats_at = 0, fpatb_at = 0, fstr_at = 0;
+  if (fused) {
+    fpats_at = (uint32_t)((2 * fuse_pairs + 3) & ~(size_t)3);  // 16 B aligned pattern records
+    fpatb_at = fpats_at + (uint32_t)PD.pats_h.size() * 4;
+    fstr_at = fpatb_at + (uint32_t)(PD.pat_bytes_h.size() + 3) / 4;
+    std::vector<uint8_t> strbytes;
+    for (uint32_t p = 0; p < npreds; ++p) {
+      const uint32_t d = P.preds[p].domain;
+      if (!local[p] || dom_byte[d] >= 0) continue;
+      dom_byte[d] = (int64_t)strbytes.size();
+      strbytes.insert(strbytes.end(), C.dict[d].bytes.begin(), C.dict[d].bytes.end());
+    }
+    fimg.assign(fstr_at + (strbytes.size() + 3) / 4, 0);
+    memcpy(fimg.data() + fpats_at, PD.pats_h.data(), PD.pats_h.size() * sizeof(KpePat));
+    if (!PD.pat_bytes_h.empty()) memcpy(fimg.data() + fpatb_at, PD.pat_bytes_h.data(), PD.pat_bytes_h.size());
+    if (!strbytes.empty()) memcpy(fimg.data() + fstr_at, strbytes.data(), strbytes.size());
+    fimg.resize((fimg.size() + 3) & ~(size_t)3, 0);
+  }
   uint32_t lo = 0, go = blob, blk = 0;
   for (uint32_t p = 0; p < npreds; ++p) {
     uint32_t at;
@@ -527,8 +574,18 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     const uint32_t d = P.preds[p].domain, n = C.dict[d].size();
     if (n) {
       const uint32_t pend = p + 1 < PD.pat0.size() ? PD.pat0[p + 1] : (uint32_t)PD.pats_h.size();
-      jobs.push_back({d, PD.pat0[p], pend - PD.pat0[p], at, 0});
-      blk = std::max(blk, (n + 255) / 256);  // grid x extent (grid y = jobs)
+      if (fused && local[p]) {
+        const uint32_t str0 = (blob + fstr_at) * 4 + (uint32_t)dom_byte[d];  // LDS byte address
+        for (uint32_t i = 0; i < n; ++i)
+          for (uint32_t k = PD.pat0[p]; k < pend; ++k) {
+            const uint32_t w = at + (i >> 5);
+            pairs.push_back((str0 + C.dict[d].off[i]) | ((C.dict[d].off[i + 1] - C.dict[d].off[i]) << 20));
+            pairs.push_back(k | (w << 12) | ((i & 31u) << 27));
+          }
+      } else {
+        jobs.push_back({d, PD.pat0[p], pend - PD.pat0[p], at, 0});
+        blk = std::max(blk, (n + 255) / 256);  // grid x extent (grid y = jobs)
+      }
     }
   }
   auto loc = [&](int32_t p) -> uint32_t { return p < 0 ? PRED_NONE : dir[(size_t)p]; };
@@ -558,10 +615,18 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const int32_t fixed[10] = {ps.apparmor_key, ps.apparmor_val_ok, ps.seccomp_pod_key, ps.seccomp_ann_ok,
                              ps.caps_baseline_ok, ps.cap_nbs, ps.cap_all, ps.sysctl[0], ps.sysctl[1], ps.sysctl[2]};
   for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
+  if (fused) memcpy(fimg.data(), pairs.data(), pairs.size() * 4);
+  const uint32_t fuse_words = fused ? (uint32_t)fimg.size() : 0u;
   const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
-  const uint32_t tt_at = blob;
-  const uint32_t prog_at = blob + ((tt_words + 3) & ~3u);
+  const uint32_t tt_at = blob + fuse_words;
+  const uint32_t prog_at = tt_at + ((tt_words + 3) & ~3u);
   B.tt_lds = PD.tt ? tt_at : PRED_NONE;
+  B.fuse_lds = blob;
+  B.fuse_words = fuse_words;
+  B.npairs = fused ? (uint32_t)(pairs.size() / 2) : 0u;
+  B.fuse_pats = blob + fpats_at;
+  B.fuse_patb = blob + fpatb_at;
+  if (fused) HIPCHK(upload(B.fuse, fimg, s));
   B.filt_lds = stage_prog ? prog_at : PRED_NONE;
   B.fterm_lds = prog_at + 2 * (uint32_t)P.filters.size();
   B.wave_lds = (prog_at + (stage_prog ? prog_words : 0) + 1) & ~1u;
@@ -655,6 +720,12 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.c_sann = D.c_sann.as<uint32_t>();
   sa.ntiles = (uint32_t)((C.n + 63) / 64);
   sa.zero_page = B.zero_page.as<uint32_t>();
+  sa.fuse = B.fuse.as<uint32_t>();
+  sa.fuse_words = B.fuse_words;
+  sa.fuse_lds = B.fuse_lds;
+  sa.npairs = B.npairs;
+  sa.fuse_pats = B.fuse_pats;
+  sa.fuse_patb = B.fuse_patb;
 
   sa.capsets = D.capsets.as<uint32_t>();
   sa.ncapsets = (uint32_t)C.capset_add.size();
