@@ -189,4 +189,103 @@ long oracle_validate(const char* policies_json, const char* ndjson, size_t len, 
   }
 }
 
+// ---- pattern path (pkg/engine/{pattern,validate}) ----------------------------------
+// Values are JSON texts; numbers keep their literal type (integer literal -> int, else
+// float), so Go literals such as `7`, `7.0`, `nil`, `"x"` map 1:1. all_float=1 decodes
+// every number as float64 (encoding/json into interface{}, as the Go tests do).
+static JPtr pjson(const char* s, int all_float) {
+  JPtr v = parse_json(s);
+  if (all_float) pat::numbers_to_float(*v);
+  return v;
+}
+
+// pattern.Validate(value, pattern)
+int oracle_pattern_validate(const char* value_json, const char* pattern_json) {
+  try {
+    JPtr v = pjson(value_json, 0), p = pjson(pattern_json, 0);
+    return pat::validate_leaf(v.get(), *p) ? 1 : 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// validateString(value, pattern, op) with op one of "", ">=", "<=", "!", ">", "<"
+int oracle_validate_string(const char* value_json, const char* pattern, const char* op) {
+  try {
+    JPtr v = pjson(value_json, 0);
+    std::string o = op;
+    pat::Op k = o == ">=" ? pat::OP_GE
+              : o == "<=" ? pat::OP_LE
+              : o == "!"  ? pat::OP_NE
+              : o == ">"  ? pat::OP_GT
+              : o == "<"  ? pat::OP_LT
+                          : pat::OP_EQ;
+    return pat::validate_string(v.get(), pattern, k) ? 1 : 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// which = 0: validateStringPattern, 1: validateStringPatterns, 2: compareString(op "" / "!")
+int oracle_string_pattern(const char* value_json, const char* pattern, int which, const char* op) {
+  try {
+    JPtr v = pjson(value_json, 0);
+    if (which == 0) return pat::validate_string_pattern(v.get(), pattern) ? 1 : 0;
+    if (which == 1) return pat::validate_string_patterns(v.get(), pattern) ? 1 : 0;
+    return pat::compare_string(v.get(), pattern, std::string(op) == "!" ? pat::OP_NE : pat::OP_EQ) ? 1 : 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// operator.GetOperatorFromStringPattern -> index into {"", ">=", "<=", "!", ">", "<", "-", "!-"}
+int oracle_get_operator(const char* pattern) { return (int)pat::get_operator(pattern); }
+
+// convertNumberToString: 0 ok (text in buf), 1 error
+int oracle_number_to_string(const char* value_json, char* buf, size_t cap) {
+  try {
+    JPtr v = pjson(value_json, 0);
+    std::string s;
+    if (!pat::number_to_string(v.get(), &s)) return 1;
+    snprintf(buf, cap, "%s", s.c_str());
+    return 0;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// validateResourceElement(resource, pattern, "/") (mode 0) or validateMap (mode 1).
+// Returns the error kind (0 none, 1 conditional, 2 global, 3 negation, 4 other,
+// 5 skip aggregate) and writes the returned path into buf.
+int oracle_validate_element(const char* resource_json, const char* pattern_json, int mode, int all_float, char* buf,
+                            size_t cap) {
+  try {
+    JPtr r = pjson(resource_json, all_float), p = pjson(pattern_json, all_float);
+    pat::Walker w;
+    pat::Err e = mode == 1 ? w.map(*r, *p, "/") : w.element(r.get(), *p, "/");
+    snprintf(buf, cap, "%s", e.path.c_str());
+    return (int)e.k;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
+// validate.MatchPattern: 0 pass, 1 skip, 2 fail (path in buf; empty path => rule error)
+int oracle_match_pattern(const char* resource_json, const char* pattern_json, int all_float, char* buf, size_t cap) {
+  try {
+    JPtr r = pjson(resource_json, all_float), p = pjson(pattern_json, all_float);
+    pat::MatchResult m = pat::match_pattern(*r, *p);
+    snprintf(buf, cap, "%s", m.path.c_str());
+    return (int)m.k;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 }  // extern "C"

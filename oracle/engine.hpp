@@ -24,6 +24,7 @@
 
 #include "json_dom.hpp"
 #include "k8s_typed.hpp"
+#include "pattern.hpp"
 #include "pss.hpp"
 #include "wildcard.hpp"
 
@@ -41,6 +42,7 @@ inline void json_write(const JVal& v, std::string& o) {
       char b[64];
       snprintf(b, sizeof b, "%.17g", v.f);
       o += b;
+      if (!strpbrk(b, ".eEni")) o += ".0";  // keep the float64 type through a re-parse
       break;
     }
     case JT::Str: {
@@ -422,6 +424,7 @@ struct Rule {
   JPtr raw;
   MatchRes match, exclude;
   bool has_validate = false, has_pss = false, unsupported = false;
+  JPtr pattern, any_pattern;  // validate.pattern / validate.anyPattern (validate_resource.go:316-398)
   std::string pss_level, pss_version;
   std::vector<PSSExclude> pss_excludes;
 };
@@ -603,7 +606,9 @@ inline JPtr generate_rule(const std::string& name, const JVal* rule, const char*
   const JVal* val = rule->get("validate");
   auto wrap = [&](const JVal* target) {
     auto inner = jobj();
-    jset(*inner, tpl_key, deep_copy(*target));
+    JPtr c = deep_copy(*target);
+    pat::marshal_roundtrip(*c);
+    jset(*inner, tpl_key, c);
     auto outer = jobj();
     jset(*outer, "spec", inner);
     return outer;
@@ -728,7 +733,22 @@ inline Rule compile_rule(const JPtr& raw) {
         r.pss_excludes.push_back({jstr(e->get("controlName")), jstrlist(e->get("images")),
                                   jstr(e->get("restrictedField")), jstrlist(e->get("values"))});
   } else if (r.has_validate) {
-    r.unsupported = true;  // pattern/anyPattern/deny/foreach/cel: not restated in this round
+    // validate_resource.go:121-170: deny, then pattern/anyPattern, then foreach
+    const JVal* deny = v->get("deny");
+    const JVal* pt = v->get("pattern");
+    const JVal* ap = v->get("anyPattern");
+    if (deny && !deny->is_null()) {
+      r.unsupported = true;  // deny conditions (JMESPath) are not restated yet
+    } else if (pt && !pt->is_null()) {
+      r.pattern = deep_copy(*pt);
+      if (pat::has_variables(*r.pattern)) r.unsupported = true;
+    } else if (ap && !ap->is_null()) {
+      r.any_pattern = deep_copy(*ap);
+      pat::numbers_to_float(*r.any_pattern);  // encoding/json round trip (validate_resource.go:400-416)
+      if (pat::has_variables(*r.any_pattern)) r.unsupported = true;
+    } else if (jnonempty(v->get("foreach")) || jnonempty(v->get("cel"))) {
+      r.unsupported = true;
+    }
   }
   if (jnonempty(raw->get("preconditions")) || jnonempty(raw->get("context"))) r.unsupported = r.has_validate;
   return r;
@@ -855,6 +875,27 @@ inline bool matches_resource_description(const Rule& r, const Policy& p, const M
   return fails == 0;
 }
 
+// validate_resource.go:316-398 validatePatterns (no exceptions, CREATE operation)
+inline Status pattern_handler(const Rule& r, const JVal& res) {
+  if (r.pattern) {
+    pat::MatchResult m = pat::match_pattern(res, *r.pattern);
+    if (m.k == pat::M_PASS) return PASS;
+    if (m.k == pat::M_SKIP) return SKIP;
+    return m.path.empty() ? ERROR : FAIL;
+  }
+  if (r.any_pattern->t != JT::Arr) return ERROR;  // deserializeAnyPattern failure
+  int fails = 0, skips = 0;
+  for (auto& p : r.any_pattern->a) {
+    pat::MatchResult m = pat::match_pattern(res, *p);
+    if (m.k == pat::M_PASS) return PASS;
+    if (m.k == pat::M_SKIP) ++skips;
+    else ++fails;  // an empty-path PatternError counts as a failure here
+  }
+  if (skips > 0 && fails == 0) return SKIP;
+  if (fails > 0) return FAIL;
+  return PASS;
+}
+
 // validate_pss.go:31-112 (no exceptions, CREATE operation)
 inline Status pss_handler(const Rule& r, const JVal& res, const std::string& kind) {
   Pod pod;
@@ -892,6 +933,7 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
     Status s;
     if (r.unsupported) s = UNSUPPORTED;
     else if (r.has_pss) s = pss_handler(r, res, u.kind());
+    else if (r.pattern || r.any_pattern) s = pattern_handler(r, res);
     else s = NA;
     out[i] = s;
     if (s == PASS || s == FAIL) ++applied;

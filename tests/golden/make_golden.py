@@ -16,6 +16,16 @@ outputs) lifted from the reference's tests:
                               (restricted:latest policy, badpod01, expected report result)
   check_selector.json      <- pkg/utils/match/labels_test.go (TestCheckSelector table:
                               expected LabelSelector.MatchLabels, actual labels, want, wantErr)
+  pattern_leaf_cases.json  <- pkg/engine/pattern/pattern_test.go (Validate / validateNilPattern /
+                              validateMapPattern / convertNumberToString / validateStringPatterns /
+                              compareString tables and the assert one-liners)
+  pattern_tree_cases.json  <- pkg/engine/validate/validate_test.go (validateMap /
+                              validateResourceElement path+error cases, testValidationPattern
+                              calls, MatchPattern status tables)
+  cli_cases.json           <- test/cli/test/*/kyverno-test.yaml (policies, resources and expected
+                              per-rule results of `kyverno test`; YAML decoded like
+                              sigs.k8s.io/yaml: no timestamp resolution, whole floats -> ints;
+                              empty namespaces set to "default" as resource.go:56-58 does)
   match_rd_cases.json      <- pkg/engine/utils/utils_test.go:1828-2460, hand-transcribed below
                               (Go struct literals): MatchesResourceDescription on the nginx
                               Deployment with kinds/name/generateName/selector/exclude blocks
@@ -28,6 +38,9 @@ import re
 import sys
 
 import yaml
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from golit import Reader, Unsupported, table, to_json  # noqa: E402
 
 REF = sys.argv[1] if len(sys.argv) > 1 else "/root/reference"
 OUT = os.path.dirname(os.path.abspath(__file__))
@@ -223,7 +236,175 @@ def match_rd_cases():
     return out
 
 
+_OPS = {"operator.Equal": "", "operator.MoreEqual": ">=", "operator.LessEqual": "<=", "operator.NotEqual": "!",
+        "operator.More": ">", "operator.Less": "<", "operator.InRange": "-", "operator.NotInRange": "!-"}
+
+
+def _line(text, pos):
+    return text.count("\n", 0, pos) + 1
+
+
+def pattern_leaf_cases():
+    rel = "pkg/engine/pattern/pattern_test.go"
+    text = open(os.path.join(REF, rel)).read()
+    out = []
+
+    def add(func, case, **kw):
+        kw.update({"fn": func, "name": f"{rel}:{case}"})
+        out.append(kw)
+
+    for func, fixed_pattern in (("TestValidate", None), ("Test_validateNilPattern", "null"),
+                                ("Test_validateMapPattern", "{}")):
+        for n, c in enumerate(table(text, func)):
+            a = c[1]["args"][1]
+            try:
+                v = to_json(a["value"])
+                p = fixed_pattern if fixed_pattern else to_json(a["pattern"])
+            except Unsupported:
+                continue
+            add("validate", f"{func}[{n}]", value=v, pattern=p, want=c[1]["want"][1])
+    for n, c in enumerate(table(text, "Test_convertNumberToString")):
+        a = c[1]["args"][1]
+        try:
+            v = to_json(a["value"])
+        except Unsupported:
+            continue
+        we = c[1].get("wantErr", ("bool", False))[1]
+        add("n2s", f"Test_convertNumberToString[{n}]", value=v, want=c[1].get("want", ("str", ""))[1], wantErr=we)
+    for n, c in enumerate(table(text, "Test_validateStringPatterns")):
+        a = c[1]["args"][1]
+        add("patterns", f"Test_validateStringPatterns[{n}]", value=to_json(a["value"]), pattern=a["pattern"][1],
+            want=c[1]["want"][1])
+    for n, c in enumerate(table(text, "Test_compareString")):
+        a = c[1]["args"][1]
+        add("compare", f"Test_compareString[{n}]", value=to_json(a["value"]), pattern=a["pattern"][1],
+            op=_OPS[a["operatorVariable"][1]], want=c[1]["want"][1])
+    # one-line asserts
+    for m in re.finditer(r"assert\.Assert\(t, (!?)(validateFloatPattern|validateStringPattern|validateString)\("
+                         r"logr\.Discard\(\), ", text):
+        r = Reader(text, m.end())
+        v = r.value()
+        r.eat(",")
+        p = r.value()
+        op = None
+        if m.group(2) == "validateString":
+            r.eat(",")
+            op = _OPS[r.value()[1]]
+        want = m.group(1) != "!"
+        name = f"{rel}:{_line(text, m.start())}"
+        if m.group(2) == "validateFloatPattern":
+            if p[0] == "int":
+                p = ("float", p[1] + ".0")
+            out.append({"fn": "validate", "name": name, "value": to_json(v), "pattern": to_json(p), "want": want})
+        elif m.group(2) == "validateStringPattern":
+            out.append({"fn": "pattern", "name": name, "value": to_json(v), "pattern": p[1], "want": want})
+        else:
+            out.append({"fn": "string", "name": name, "value": to_json(v), "pattern": p[1], "op": op, "want": want})
+    for m in re.finditer(r"assert\.Equal\(t, operator\.GetOperatorFromStringPattern\((\"[^\"]*\")\), "
+                         r"(operator\.\w+)\)", text):
+        out.append({"fn": "operator", "name": f"{rel}:{_line(text, m.start())}", "pattern": json.loads(m.group(1)),
+                    "want": _OPS[m.group(2)]})
+    return out
+
+
+def pattern_tree_cases():
+    rel = "pkg/engine/validate/validate_test.go"
+    text = open(os.path.join(REF, rel)).read()
+    out = []
+    funcs = [(m.group(1), m.start()) for m in re.finditer(r"^func (\w+)\(t \*testing\.T\) \{", text, re.M)]
+    for idx, (name, start) in enumerate(funcs):
+        end = funcs[idx + 1][1] if idx + 1 < len(funcs) else len(text)
+        body = text[start:end]
+        if "variables." in body:
+            continue  # $(...) reference substitution: not part of the restated subset
+        mp = re.search(r"rawPattern := \[\]byte\(`(.*?)`\)", body, re.S)
+        mr = re.search(r"rawMap := \[\]byte\(`(.*?)`\)", body, re.S)
+        mc = re.search(r"path, err := (validateMap|validateResourceElement)\(", body)
+        if mp and mr and mc:
+            after = body[mc.end():]
+            mpath = re.search(r'assert\.Equal\(t, path, "([^"]*)"\)', after)
+            nil_err = bool(re.search(r"assert\.NilError\(t, err\)|assert\.Assert\(t, err == nil\)", after))
+            out.append({"name": f"{rel}:{name}", "kind": "element", "mode": 1 if mc.group(1) == "validateMap" else 0,
+                        "pattern": mp.group(1), "resource": mr.group(1),
+                        "path": mpath.group(1) if mpath else None, "nil_err": nil_err})
+    # testValidationPattern(t, num, pattern, resource, path, nilErr) with the preceding assignments
+    for m in re.finditer(r'pattern :?= \[\]byte\(`(.*?)`\)\s*resource :?= \[\]byte\(`(.*?)`\)\s*'
+                         r'testValidationPattern\(t, "(\w+)", pattern, resource, "([^"]*)", (true|false)\)', text, re.S):
+        out.append({"name": f"{rel}:TestValidateMapWildcardKeys/{m.group(3)}", "kind": "element", "mode": 0,
+                    "pattern": m.group(1), "resource": m.group(2), "path": m.group(4),
+                    "nil_err": m.group(5) == "true"})
+    st = {"engineapi.RuleStatusPass": "pass", "engineapi.RuleStatusSkip": "skip",
+          "engineapi.RuleStatusFail": "fail", "engineapi.RuleStatusError": "error"}
+    for func in ("TestConditionalAnchorWithMultiplePatterns", "Test_global_anchor"):
+        for c in table(text, func):
+            f = c[1]
+            out.append({"name": f"{rel}:{func}/{f['name'][1]}", "kind": "match", "pattern": f["pattern"][1],
+                        "resource": f["resource"][1], "status": st[f["status"][1]]})
+    return out
+
+
+class _GoYamlLoader(yaml.SafeLoader):
+    pass
+
+
+# go-yaml into interface{} keeps timestamps as strings
+_GoYamlLoader.yaml_implicit_resolvers = {
+    k: [(tag, rx) for tag, rx in v if tag != "tag:yaml.org,2002:timestamp"]
+    for k, v in yaml.SafeLoader.yaml_implicit_resolvers.items()}
+
+
+def _go_json(v):
+    """YAML value -> JSON-compatible value as YAMLToJSON (json.Marshal of float64) emits it."""
+    if isinstance(v, dict):
+        return {str(k): _go_json(x) for k, x in v.items()}
+    if isinstance(v, list):
+        return [_go_json(x) for x in v]
+    if isinstance(v, float) and v == int(v) and abs(v) < 1e21:
+        return int(v)
+    return v
+
+
+def _yaml_docs(path):
+    with open(path) as f:
+        return [_go_json(d) for d in yaml.load_all(f, Loader=_GoYamlLoader) if d]
+
+
+def cli_cases():
+    base = "test/cli/test"
+    out = []
+    for d in sorted(os.listdir(os.path.join(REF, base))):
+        tf = os.path.join(REF, base, d, "kyverno-test.yaml")
+        if not os.path.exists(tf):
+            continue
+        t = _yaml_docs(tf)[0]
+        if t.get("variables") or t.get("userinfo"):
+            continue  # values / admission user info: variables are outside the restated subset
+        try:
+            pols, ress = [], []
+            for f in t.get("policies", []):
+                pols += [p for p in _yaml_docs(os.path.join(REF, base, d, f)) if p.get("kind") in
+                         ("ClusterPolicy", "Policy")]
+            for f in t.get("resources", []):
+                ress += _yaml_docs(os.path.join(REF, base, d, f))
+        except (OSError, yaml.YAMLError):
+            continue
+        for r in ress:
+            md = r.setdefault("metadata", {})
+            if not md.get("namespace"):
+                md["namespace"] = "default"
+        results = []
+        for r in t.get("results", []):
+            names = r.get("resources") or ([r["resource"]] if r.get("resource") else [])
+            results.append({"policy": r.get("policy"), "rule": r.get("rule"), "resources": names,
+                            "kind": r.get("kind"), "namespace": r.get("namespace"), "result": r.get("result")})
+        out.append({"name": f"{base}/{d}", "policies": pols, "resources": ress, "results": results})
+    return out
+
+
 if __name__ == "__main__":
+    _dump("cli_cases.json", cli_cases())
+    _dump("pattern_leaf_cases.json", pattern_leaf_cases())
+    _dump("pattern_tree_cases.json", pattern_tree_cases())
     _dump("pss_evaluate_cases.json", pss_cases())
     _dump("wildcard_match.json", wildcard_cases())
     _dump("chainsaw_psa.json", chainsaw_psa())

@@ -25,6 +25,14 @@ class Oracle:
         L.oracle_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.oracle_validate.restype = ctypes.c_long
+        cp = ctypes.c_char_p
+        L.oracle_pattern_validate.argtypes = [cp, cp]
+        L.oracle_validate_string.argtypes = [cp, cp, cp]
+        L.oracle_string_pattern.argtypes = [cp, cp, ctypes.c_int, cp]
+        L.oracle_get_operator.argtypes = [cp]
+        L.oracle_number_to_string.argtypes = [cp, cp, ctypes.c_size_t]
+        L.oracle_validate_element.argtypes = [cp, cp, ctypes.c_int, ctypes.c_int, cp, ctypes.c_size_t]
+        L.oracle_match_pattern.argtypes = [cp, cp, ctypes.c_int, cp, ctypes.c_size_t]
 
     def wildcard(self, pattern, text):
         return bool(self.lib.oracle_wildcard_match(pattern.encode(), text.encode()))
@@ -61,6 +69,48 @@ class Oracle:
         if n < 0:
             raise RuntimeError(self.lib.oracle_last_error().decode())
         return out[: n * R].reshape(n, R)
+
+
+    # ---- pattern path (values are JSON texts; integer literals stay int64) ----
+    def _chk(self, r):
+        if r < 0:
+            raise RuntimeError(self.lib.oracle_last_error().decode())
+        return r
+
+    def pattern_validate(self, value_json, pattern_json):
+        return bool(self._chk(self.lib.oracle_pattern_validate(value_json.encode(), pattern_json.encode())))
+
+    def validate_string(self, value_json, pattern, op):
+        return bool(self._chk(self.lib.oracle_validate_string(value_json.encode(), pattern.encode(), op.encode())))
+
+    def string_pattern(self, value_json, pattern, which, op=""):
+        return bool(self._chk(self.lib.oracle_string_pattern(value_json.encode(), pattern.encode(), which,
+                                                             op.encode())))
+
+    OPS = ["", ">=", "<=", "!", ">", "<", "-", "!-"]
+
+    def get_operator(self, pattern):
+        return self.OPS[self.lib.oracle_get_operator(pattern.encode())]
+
+    def number_to_string(self, value_json):
+        buf = ctypes.create_string_buffer(512)
+        r = self._chk(self.lib.oracle_number_to_string(value_json.encode(), buf, 512))
+        return (None, True) if r == 1 else (buf.value.decode(), False)
+
+    ERR_KINDS = ["none", "conditional", "global", "negation", "other", "skip"]
+
+    def validate_element(self, resource_json, pattern_json, mode=0, all_float=True):
+        buf = ctypes.create_string_buffer(4096)
+        k = self._chk(self.lib.oracle_validate_element(resource_json.encode(), pattern_json.encode(), mode,
+                                                       int(all_float), buf, 4096))
+        return self.ERR_KINDS[k], buf.value.decode()
+
+    def match_pattern(self, resource_json, pattern_json, all_float=True):
+        """validate.MatchPattern -> ('pass'|'skip'|'fail', path)."""
+        buf = ctypes.create_string_buffer(4096)
+        k = self._chk(self.lib.oracle_match_pattern(resource_json.encode(), pattern_json.encode(), int(all_float),
+                                                    buf, 4096))
+        return ["pass", "skip", "fail"][k], buf.value.decode()
 
 
 def build():

@@ -8,6 +8,9 @@ the reference's test sources (text only):
   * chainsaw reports/background/test-report-background-mode -> background_report.json
   * pkg/utils/match/labels_test.go      -> check_selector.json (12)
   * pkg/engine/utils/utils_test.go:1828-2460 -> match_rd_cases.json (8, hand-transcribed)
+  * pkg/engine/pattern/pattern_test.go  -> pattern_leaf_cases.json (leaf validators)
+  * pkg/engine/validate/validate_test.go -> pattern_tree_cases.json (tree walk + MatchPattern)
+  * test/cli/test/*/kyverno-test.yaml     -> cli_cases.json (end-to-end `kyverno test` results)
 """
 import json
 import os
@@ -28,6 +31,9 @@ CHAINSAW = _load("chainsaw_psa.json")
 BG = _load("background_report.json")
 SEL = _load("check_selector.json")
 MRD = _load("match_rd_cases.json")
+PLEAF = _load("pattern_leaf_cases.json")
+PTREE = _load("pattern_tree_cases.json")
+CLI = _load("cli_cases.json")
 
 COMPLIANT_POD_SPEC = {"containers": [{"name": "c", "image": "nginx"}]}
 
@@ -140,3 +146,100 @@ def test_background_report_restricted_latest(oracle):
     v = oracle.validate([BG["policy"]], json.dumps(pod).encode())
     assert list(v[0]) == [2, 0, 0]
     assert BG["results"][0]["result"] == "fail" and BG["summary"]["fail"] == 1
+
+
+# ---- pattern path --------------------------------------------------
+@pytest.mark.parametrize("case", PLEAF, ids=[c["name"] for c in PLEAF])
+def test_pattern_leaf_golden(oracle, case):
+    fn = case["fn"]
+    if fn == "validate":
+        got = oracle.pattern_validate(case["value"], case["pattern"])
+    elif fn == "pattern":
+        got = oracle.string_pattern(case["value"], case["pattern"], 0)
+    elif fn == "patterns":
+        got = oracle.string_pattern(case["value"], case["pattern"], 1)
+    elif fn == "compare":
+        got = oracle.string_pattern(case["value"], case["pattern"], 2, case["op"])
+    elif fn == "string":
+        got = oracle.validate_string(case["value"], case["pattern"], case["op"])
+    elif fn == "operator":
+        got = oracle.get_operator(case["pattern"])
+    elif fn == "n2s":
+        text, err = oracle.number_to_string(case["value"])
+        assert err == case["wantErr"]
+        got = case["want"] if err else text
+    else:
+        raise AssertionError(fn)
+    assert got == case["want"]
+
+
+@pytest.mark.parametrize("case", PTREE, ids=[c["name"] for c in PTREE])
+def test_pattern_tree_golden(oracle, case):
+    if case["kind"] == "element":
+        kind, path = oracle.validate_element(case["resource"], case["pattern"], case["mode"])
+        assert (kind == "none") == case["nil_err"]
+        if case["path"] is not None:
+            assert path == case["path"]
+    else:
+        status, path = oracle.match_pattern(case["resource"], case["pattern"])
+        want = case["status"]
+        if want == "fail":
+            # validate_test.go:1663-1691 testMatchPattern asserts nothing for RuleStatusFail
+            # (several of those table rows actually skip in the reference); not a pin.
+            return
+        if status == "fail" and path == "":
+            status = "error"
+        assert status == want
+
+
+def cli_expectations(oracle, case):
+    """(row, [columns], expected, unscored) of a `kyverno test` scenario, with the oracle's
+    verdict matrix. A result names rule R and matches responses of R, autogen-R and
+    autogen-cronjob-R (commands/test/command.go:206-221)."""
+    names = oracle.rule_names(case["policies"])
+    nd = b"\n".join(json.dumps(r).encode() for r in case["resources"])
+    M = oracle.validate(case["policies"], nd)
+    unscored = {p["metadata"]["name"] for p in case["policies"]
+                if (p["metadata"].get("annotations") or {}).get("policies.kyverno.io/scored") == "false"}
+    out = []
+    for res in case["results"]:
+        pol = res["policy"].split("/")[-1]
+        cols = [names.index(f"{pol}/{p}{res['rule']}") for p in ("", "autogen-", "autogen-cronjob-")
+                if f"{pol}/{p}{res['rule']}" in names]
+        if not cols:
+            continue
+        for nm in res["resources"]:
+            ns, _, name = nm.rpartition("/")
+            for i, r in enumerate(case["resources"]):
+                md = r.get("metadata", {})
+                if md.get("name") != name or (res["kind"] and r.get("kind") != res["kind"]):
+                    continue
+                if (ns or res["namespace"]) and md.get("namespace") != (ns or res["namespace"]):
+                    continue
+                out.append((i, cols, res["result"], pol in unscored, pol, res["rule"]))
+    return M, out
+
+
+@pytest.mark.parametrize("case", CLI, ids=[c["name"] for c in CLI])
+def test_cli_golden(oracle, case):
+    """Stricter than `kyverno test` itself, which counts every expected `fail` and every
+    resource without a rule response as a success (commands/test/output.go:193-236): here a
+    response must equal the expectation, and "no response" is accepted only for an expected
+    `skip` (excluded resource) or a rule without a validate handler (mutate / verifyImages)."""
+    from tests.oracle_lib import STATUS
+
+    pols = {p["metadata"]["name"]: p for p in case["policies"]}
+    M, exp = cli_expectations(oracle, case)
+    for i, cols, want, unscored, pol, rule in exp:
+        got = [STATUS[int(M[i, c])] for c in cols]
+        got = next((g for g in got if g != "na"), "na")
+        if got == "unsupported":
+            continue
+        if got == "fail" and unscored:
+            got = "warn"
+        if got == "na":
+            rules = [r for r in pols.get(pol, {}).get("spec", {}).get("rules", []) if r.get("name") == rule]
+            validating = any(r.get("validate") for r in rules)
+            assert want in ("skip", "fail") or not validating, (case["resources"][i]["metadata"]["name"], want)
+            continue
+        assert got == want, (case["resources"][i]["metadata"]["name"], cols, got, want)
