@@ -92,6 +92,13 @@ void kpe_program_free(kpe_program* prog);
  * reference reads per resource: PolicyContext.NamespaceLabels). */
 kpe_status kpe_corpus_flatten(const char* ndjson, size_t len, const char* ns_labels_json, size_t ns_len,
                               kpe_corpus** out);
+/* Same with flags. KPE_CORPUS_DOCS keeps every resource's document tape (its JSON as the
+ * reference's unstructured map, pkg/engine/validate/validate.go:31 walks it) for
+ * pattern / anyPattern rules; kpe_corpus_flatten sets it. Without it the corpus only
+ * serves podSecurity and match-only programs (KPE_E_STATE otherwise). */
+#define KPE_CORPUS_DOCS 1u
+kpe_status kpe_corpus_flatten_ex(const char* ndjson, size_t len, const char* ns_labels_json, size_t ns_len,
+                                 uint32_t flags, kpe_corpus** out);
 int64_t kpe_corpus_num_resources(const kpe_corpus* c);
 /* Host bytes of the columnar encoding (what one evaluation may read). */
 int64_t kpe_corpus_bytes(const kpe_corpus* c);

@@ -48,6 +48,7 @@ def load():
     L.kpe_program_rule_is_pss.argtypes = [vp, i32]
     L.kpe_program_free.argtypes = [vp]
     L.kpe_corpus_flatten.argtypes = [cp, sz, cp, sz, ctypes.POINTER(vp)]
+    L.kpe_corpus_flatten_ex.argtypes = [cp, sz, cp, sz, ctypes.c_uint32, ctypes.POINTER(vp)]
     L.kpe_corpus_num_resources.argtypes = [vp]
     L.kpe_corpus_num_resources.restype = i64
     L.kpe_corpus_bytes.argtypes = [vp]

@@ -64,6 +64,16 @@ struct Corpus {
   std::vector<uint32_t> nsl_off{0}, nsl_k, nsl_v;
   std::unordered_map<std::string, uint32_t> nsl_index;
 
+  // ---- generic document tape + scalar table (pattern rules; schema.h DN_* / KpeScalar) ----
+  bool has_docs = false;
+  std::vector<uint32_t> doc;          // 2 words per node
+  std::vector<uint64_t> doc_off{0};   // node offset of each resource
+  std::vector<KpeScalar> scal;        // scalar table (ids 0/1/2 = null/false/true)
+  std::vector<char> scal_text;        // compareString texts
+  std::unordered_map<std::string, uint32_t> scal_str;
+  std::unordered_map<int64_t, uint32_t> scal_int;
+  std::unordered_map<uint64_t, uint32_t> scal_float;
+
   DeviceCorpus* dev = nullptr;
   int64_t bytes() const;
 };

@@ -12,6 +12,7 @@
 // The flattener only ENCODES (dictionary ids, enum codes, presence bits); every
 // predicate is evaluated on the device.
 #include <algorithm>
+#include <memory>
 #include <cstring>
 #include <stdexcept>
 #include <string>
@@ -19,6 +20,7 @@
 #include <vector>
 
 #include "corpus.hpp"
+#include "goval.hpp"
 #include "jscan.hpp"
 
 namespace kpe {
@@ -1089,6 +1091,146 @@ class Flattener {
   }
 };
 
+// ---- generic document tape (pattern rules) --------------------------------------------
+// Scalar attributes (schema.h KpeScalar) from the value's text forms; see goval.hpp.
+void scalar_attrs(KpeScalar& e, std::string_view numstr) {
+  int64_t d;
+  if (goval::parse_duration(numstr, &d)) e.flags |= SC_DUR, e.dur = d;
+  goval::Quantity q;
+  if (goval::parse_quantity(numstr, &q)) {
+    e.flags |= SC_QTY | (q.neg ? SC_QNEG : 0u);
+    e.qlo = (uint64_t)q.m, e.qhi = (uint64_t)(q.m >> 64), e.qexp = q.e;
+  }
+}
+
+class DocBuilder {
+ public:
+  explicit DocBuilder(Corpus& c) : C(c) {
+    if (C.scal.empty()) {  // fixed entries: null, false, true
+      KpeScalar n{}, f{}, t{};
+      n.flags = SC_T_NULL;
+      scalar_attrs(n, "0");  // convertNumberToString(nil) == "0"
+      f.flags = SC_T_BOOL | SC_TEXT;
+      t.flags = SC_T_BOOL | SC_TEXT | SC_BTRUE;
+      f.text_off = text("false"), f.text_len = 5;
+      t.text_off = text("true"), t.text_len = 4;
+      C.scal = {n, f, t};
+    }
+  }
+  void add(const char* b, const char* e) {
+    JCur c(b, e);
+    value(c, 0, 0);
+    if (!c.ok()) throw std::invalid_argument("malformed resource JSON");
+    C.doc_off.push_back(C.doc.size() / 2);
+  }
+
+ private:
+  Corpus& C;
+  std::string scratch;
+  uint32_t text(std::string_view t) {
+    const size_t off = C.scal_text.size();
+    if (off + t.size() > 0xFFFFFFFFull) throw LimitError("scalar text pool exceeds 4 GiB");
+    C.scal_text.insert(C.scal_text.end(), t.begin(), t.end());
+    return (uint32_t)off;
+  }
+  uint32_t push_scalar(KpeScalar e) {
+    if (C.scal.size() >= 0xFFFFFFFFull) throw LimitError("too many distinct scalars");
+    C.scal.push_back(e);
+    return (uint32_t)(C.scal.size() - 1);
+  }
+  uint32_t int_id(int64_t v) {
+    auto it = C.scal_int.find(v);
+    if (it != C.scal_int.end()) return it->second;
+    KpeScalar e{};
+    e.flags = SC_T_INT | SC_TEXT;
+    e.ival = v;
+    const std::string t = std::to_string(v);
+    e.text_off = text(t), e.text_len = (uint32_t)t.size();
+    scalar_attrs(e, t);
+    return C.scal_int[v] = push_scalar(e);
+  }
+  uint32_t float_id(double v) {
+    uint64_t bits;
+    memcpy(&bits, &v, 8);
+    auto it = C.scal_float.find(bits);
+    if (it != C.scal_float.end()) return it->second;
+    KpeScalar e{};
+    e.flags = SC_T_FLOAT | SC_TEXT;
+    e.fval = v;
+    const std::string t = goval::fmt_E(v);
+    e.text_off = text(t), e.text_len = (uint32_t)t.size();
+    scalar_attrs(e, goval::fmt_f(v));
+    return C.scal_float[bits] = push_scalar(e);
+  }
+  uint32_t str_id(std::string_view v) {
+    std::string k(v);
+    auto it = C.scal_str.find(k);
+    if (it != C.scal_str.end()) return it->second;
+    KpeScalar e{};
+    e.flags = SC_T_STR | SC_TEXT;
+    e.text_off = text(v), e.text_len = (uint32_t)v.size();
+    int64_t i;
+    double f;
+    if (goval::parse_int(v, &i)) e.flags |= SC_PINT, e.ival = i;
+    if (goval::parse_float(v, &f)) e.flags |= SC_PFLOAT, e.fval = f;
+    scalar_attrs(e, v);
+    return C.scal_str[k] = push_scalar(e);
+  }
+  void node(uint32_t kind, uint32_t key1, uint32_t y) {
+    C.doc.push_back(kind | (key1 << 2));
+    C.doc.push_back(y);
+  }
+  void value(JCur& c, uint32_t key1, int depth) {
+    if (depth > 256) throw LimitError("document nesting deeper than 256");
+    const size_t at = C.doc.size() / 2;
+    switch (c.peek()) {
+      case JK::Null: c.null(), node(DN_SCALAR, key1, SC_NULL_ID); break;
+      case JK::Bool: {
+        bool b = false;
+        c.boolean(&b);
+        node(DN_SCALAR, key1, b ? SC_TRUE_ID : SC_FALSE_ID);
+        break;
+      }
+      case JK::Num: {
+        JNum n;
+        c.number(&n);
+        node(DN_SCALAR, key1, n.is_int ? int_id(n.i) : float_id(n.f));
+        break;
+      }
+      case JK::Str: {
+        std::string_view v;
+        c.str(&v, scratch);
+        node(DN_SCALAR, key1, str_id(v));
+        break;
+      }
+      case JK::Obj: {
+        node(DN_MAP, key1, 0);
+        c.obj_begin();
+        bool f = true;
+        std::string_view k;
+        std::string ks;
+        while (c.obj_next(f, &k, ks)) {
+          const uint32_t kid = C.dict[D_KEY].intern(k);
+          if (kid >= DN_MAX_KEYS) throw LimitError("too many distinct member names");
+          value(c, kid + 1, depth + 1);
+        }
+        C.doc[2 * at + 1] = (uint32_t)(C.doc.size() / 2 - at - 1);
+        break;
+      }
+      case JK::Arr: {
+        node(DN_ARR, key1, 0);
+        c.arr_begin();
+        bool f = true;
+        while (c.arr_next(f)) value(c, 0, depth + 1);
+        C.doc[2 * at + 1] = (uint32_t)(C.doc.size() / 2 - at - 1);
+        break;
+      }
+      default: throw std::invalid_argument("malformed resource JSON");
+    }
+    if (C.doc.size() / 2 - at > 0xFFFFFFFFull) throw LimitError("document too large");
+  }
+};
+
 void load_ns_labels(Corpus& C, const char* js, size_t len) {
   if (!js || !len) return;
   JCur c(js, js + len);
@@ -1134,13 +1276,16 @@ int64_t Corpus::bytes() const {
   add(lab_off), add(lab_k), add(lab_v), add(ann_off), add(ann_k), add(ann_v);
   add(rec), add(hdr), add(crec), add(vol_src), add(sys_id), add(pann_kv), add(capset_add), add(capset_drop);
   add(c_sann);
+  add(doc), add(doc_off), add(scal), add(scal_text);
   return b;
 }
 
 // Entry used by kpe_corpus_flatten. Throws std::invalid_argument / LimitError.
-void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len) {
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs) {
   load_ns_labels(C, nsl, nsl_len);
   Flattener fl(C);
+  std::unique_ptr<DocBuilder> db;
+  if (docs) db = std::make_unique<DocBuilder>(C), C.has_docs = true;
   size_t i = 0;
   while (i < len) {
     size_t j = i;
@@ -1148,7 +1293,10 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
     size_t a = i, b = j;
     while (a < b && (buf[a] == ' ' || buf[a] == '\t' || buf[a] == '\r')) ++a;
     while (b > a && (buf[b - 1] == ' ' || buf[b - 1] == '\t' || buf[b - 1] == '\r')) --b;
-    if (b > a) fl.add(buf + a, buf + b);
+    if (b > a) {
+      fl.add(buf + a, buf + b);
+      if (db) db->add(buf + a, buf + b);
+    }
     i = j + 1;
   }
   // sentinel wave header: list ends of the last tile (tile t's lists are [hdr[t], hdr[t+1]))

@@ -119,7 +119,7 @@ struct ScanArgs {
   // NARROW truth-table fast path (tt_lds != PRED_NONE: <= KPE_TT_TERMS terms, no ApplyOne):
   // every block tabulates matched-rule masks for all 2^nterms term vectors in LDS at
   // tt_lds; narrow_cls holds (cv_mask, rule mask) per distinct PSS version set.
-  uint32_t tt_lds, ncls, pss_rules, err_rules;
+  uint32_t tt_lds, ncls, pss_rules, err_rules, pat_rules;
   const uint32_t* narrow_cls;
   const KpeFilter* filters;
   const uint32_t* fterms;
@@ -152,4 +152,25 @@ struct ScanArgs {
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules or null
+};
+
+// kpe_pattern_kernel arguments (device-resident, one copy per binding)
+struct PatArgs {
+  int64_t n;
+  uint32_t R, npr;                 // rules per row, pattern rules
+  const uint32_t* doc;             // document tape (2 words per node)
+  const uint64_t* doc_off;         // first node of each resource
+  const KpeScalar* scal;
+  const uint8_t* scal_text;
+  const KpePNode* nodes;
+  const uint4* members;            // resolved per binding (names -> D_KEY ids + 1)
+  const uint32_t* lists;
+  const KpeLeaf* leaves;
+  const KpeCond* conds;
+  const KpePat* pats;              // operand records
+  const uint8_t* pat_bytes;
+  const uint32_t* roots;           // (node, anchor slots) pairs
+  const KpePatRule* rules;
+  const uint32_t* pbuf;            // glob member-name bitsets (HBM)
+  uint8_t* verdicts;
 };

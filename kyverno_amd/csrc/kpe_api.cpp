@@ -21,11 +21,12 @@
 #include "program.hpp"
 
 namespace kpe {
-void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len);
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs);
 bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
@@ -120,7 +121,9 @@ struct DeviceProgram {
       pat_bytes, pats;
   bool narrow = false;  // per-lane rule loop (kernels_abi.h NR_*)
   bool tt = false;      // + truth-table fast path
-  uint32_t ncls = 0, pss_rules = 0, err_rules = 0;
+  uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
+  // pattern rules: compiled trees + operand records (program.hpp PatProgram)
+  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
@@ -133,6 +136,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf zero_page;    // 256 zero bytes (loads of columns a program does not read)
   DevBuf fuse;         // fused dictionary pass image (pairs, patterns, small dictionaries)
   uint32_t fuse_lds = 0, fuse_words = 0, npairs = 0, fuse_pats = 0, fuse_patb = 0;
+  DevBuf pmembers, pargs;  // pattern rules: resolved members, device copy of PatArgs
+  bool pargs_valid = false;
   ScanArgs hargs{};    // what dargs holds
   bool args_valid = false;
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
@@ -151,6 +156,7 @@ struct DeviceCorpus {
   DevBuf r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
   DevBuf lab_off, lab_k, lab_v, r_nsl, nsl_off, nsl_k, nsl_v;
   DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
+  DevBuf doc, doc_off, scal, scal_text;  // document tape + scalar table (pattern rules)
   Binding bind;
   bool has_masks = false;
 };
@@ -233,9 +239,13 @@ void kpe_program_free(kpe_program* p) {
 }
 
 kpe_status kpe_corpus_flatten(const char* ndjson, size_t len, const char* nsl, size_t nsl_len, kpe_corpus** out) {
+  return kpe_corpus_flatten_ex(ndjson, len, nsl, nsl_len, KPE_CORPUS_DOCS, out);
+}
+kpe_status kpe_corpus_flatten_ex(const char* ndjson, size_t len, const char* nsl, size_t nsl_len, uint32_t flags,
+                                 kpe_corpus** out) {
   auto c = std::make_unique<kpe::Corpus>();
   try {
-    kpe::flatten_ndjson(*c, ndjson, len, nsl, nsl_len);
+    kpe::flatten_ndjson(*c, ndjson, len, nsl, nsl_len, (flags & KPE_CORPUS_DOCS) != 0);
   } catch (const std::exception& e) {
     return fail(kpe::is_limit_error(e) ? KPE_E_LIMIT : KPE_E_INVALID, e.what());
   }
@@ -284,6 +294,12 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   HIPCHK(upload(D.sys_id, C.sys_id, s));
   HIPCHK(upload(D.pann_kv, C.pann_kv, s));
   HIPCHK(upload(D.c_sann, C.c_sann, s));
+  if (C.has_docs) {
+    HIPCHK(upload(D.doc, C.doc, s));
+    HIPCHK(upload(D.doc_off, C.doc_off, s));
+    HIPCHK(upload(D.scal, C.scal, s));
+    HIPCHK(upload(D.scal_text, C.scal_text, s));
+  }
   {
     std::vector<uint32_t> cs;
     for (size_t i = 0; i < C.capset_add.size(); ++i) {
@@ -375,7 +391,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   // truth-table fast path: few terms, no ApplyOne; per PSS version set its rule mask
   const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_apply_one;
   std::vector<uint32_t> cls;  // (cv_mask, rule mask) pairs
-  uint32_t pss_rules = 0, err_rules = 0;
+  uint32_t pss_rules = 0, err_rules = 0, pat_rules = 0;
   if (tt) {
     for (size_t r = 0; r < P.rules.size(); ++r) {
       const auto& k = P.rules[r];
@@ -387,6 +403,8 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
         cls[c + 1] |= 1u << r;
       } else if (k.handler == H_ERROR) {
         err_rules |= 1u << r;
+      } else if (k.handler == H_PATTERN) {
+        pat_rules |= 1u << r;
       }
     }
   }
@@ -398,6 +416,29 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   D.ncls = (uint32_t)cls.size() / 2;
   D.pss_rules = pss_rules;
   D.err_rules = err_rules;
+  D.pat_rules = pat_rules;
+  {  // pattern rules: operand records (a verbatim operand is an exact compare)
+    const auto& PP = P.pat;
+    std::vector<uint8_t> pb;
+    std::vector<KpePat> pp;
+    for (size_t i = 0; i < PP.operands.size(); ++i) {
+      if (PP.operand_exact[i]) {
+        pp.push_back({PK_EXACT, (uint32_t)pb.size(), (uint32_t)PP.operands[i].size(), 0});
+        pb.insert(pb.end(), PP.operands[i].begin(), PP.operands[i].end());
+      } else {
+        pp.push_back(classify_pattern(PP.operands[i], pb));
+      }
+    }
+    hipStream_t s0 = dev->stream;
+    HIPCHK(upload(D.pnodes, PP.nodes, s0));
+    HIPCHK(upload(D.plists, PP.lists, s0));
+    HIPCHK(upload(D.pleaves, PP.leaves, s0));
+    HIPCHK(upload(D.pconds, PP.conds, s0));
+    HIPCHK(upload(D.ppats, pp, s0));
+    HIPCHK(upload(D.pbytes, pb, s0));
+    HIPCHK(upload(D.proots, PP.roots, s0));
+    HIPCHK(upload(D.prules, PP.rules, s0));
+  }
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
   for (auto& pr : P.preds) {
@@ -508,7 +549,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   for (uint32_t p = 0; p < npreds; ++p) {
     uint32_t n = C.dict[P.preds[p].domain].size();
     nwords[p] = ((n + 63) / 64) * 2 + 2;
-    if (lw + nwords[p] <= local_budget && n <= kMaxLocalPairs) {
+    if (!P.preds[p].global_only && lw + nwords[p] <= local_budget && n <= kMaxLocalPairs) {
       local[p] = 1;
       lw += nwords[p];
     }
@@ -615,6 +656,19 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const int32_t fixed[10] = {ps.apparmor_key, ps.apparmor_val_ok, ps.seccomp_pod_key, ps.seccomp_ann_ok,
                              ps.caps_baseline_ok, ps.cap_nbs, ps.cap_all, ps.sysctl[0], ps.sysctl[1], ps.sysctl[2]};
   for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
+  if (!P.pat.rules.empty()) {  // pattern members: names -> D_KEY ids + 1, glob names -> bitsets
+    if (!C.has_docs) return fail(KPE_E_STATE, "pattern rules need a corpus flattened with KPE_CORPUS_DOCS");
+    const auto& PP = P.pat;
+    std::vector<int64_t> kid(PP.keys.size());
+    for (size_t i = 0; i < PP.keys.size(); ++i) kid[i] = C.dict[D_KEY].find(PP.keys[i]);
+    std::vector<uint32_t> mem(PP.members);
+    for (size_t i = 0; i < mem.size(); i += 4) {
+      mem[i + 1] = kid[mem[i + 1]] < 0 ? 0u : (uint32_t)kid[mem[i + 1]] + 1u;
+      if (mem[i] & PMF_GLOB) mem[i + 3] = loc((int32_t)mem[i + 3]);
+    }
+    HIPCHK(upload(B.pmembers, mem, s));
+    B.pargs_valid = false;
+  }
   if (fused) memcpy(fimg.data(), pairs.data(), pairs.size() * 4);
   const uint32_t fuse_words = fused ? (uint32_t)fimg.size() : 0u;
   const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
@@ -742,6 +796,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.ncls = PD.ncls;
   sa.pss_rules = PD.pss_rules;
   sa.err_rules = PD.err_rules;
+  sa.pat_rules = PD.pat_rules;
   sa.narrow_cls = PD.narrow_cls.as<uint32_t>();
   sa.nrules = (uint32_t)R;
   sa.filters = PD.filters.as<KpeFilter>();
@@ -785,6 +840,34 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.scan_blocks,
                          B.dyn_bytes, s));
+  if (!P.pat.rules.empty()) {
+    if (!B.pargs_valid) {
+      PatArgs pa{};
+      pa.n = C.n;
+      pa.R = (uint32_t)R;
+      pa.npr = (uint32_t)P.pat.rules.size();
+      pa.doc = D.doc.as<uint32_t>();
+      pa.doc_off = D.doc_off.as<uint64_t>();
+      pa.scal = D.scal.as<KpeScalar>();
+      pa.scal_text = D.scal_text.as<uint8_t>();
+      pa.nodes = PD.pnodes.as<KpePNode>();
+      pa.members = B.pmembers.as<uint4>();
+      pa.lists = PD.plists.as<uint32_t>();
+      pa.leaves = PD.pleaves.as<KpeLeaf>();
+      pa.conds = PD.pconds.as<KpeCond>();
+      pa.pats = PD.ppats.as<KpePat>();
+      pa.pat_bytes = PD.pbytes.as<uint8_t>();
+      pa.roots = PD.proots.as<uint32_t>();
+      pa.rules = PD.prules.as<KpePatRule>();
+      pa.pbuf = B.pbuf.as<uint32_t>();
+      pa.verdicts = B.verdicts.as<uint8_t>();
+      HIPCHK(B.pargs.ensure(sizeof(PatArgs)));
+      HIPCHK(hipMemcpyAsync(B.pargs.p, &pa, sizeof(PatArgs), hipMemcpyHostToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+      B.pargs_valid = true;
+    }
+    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, s));
+  }
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.c, s));
     ev.bytes = scan_bytes(P, C, B.need, masks);

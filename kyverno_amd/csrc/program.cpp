@@ -8,13 +8,16 @@
 //   kind selectors           pkg/utils/kube/kind.go:11-46
 //   PSS version selection    pkg/pss/evaluate.go:24-70 + ParseVersion :221-239 (folded into cv_mask)
 #include <algorithm>
+#include <cmath>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <set>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
+#include "goval.hpp"
 #include "jscan.hpp"
 #include "program.hpp"
 
@@ -134,6 +137,7 @@ void write(const JV& v, std::string& o) {
         char b[64];
         snprintf(b, sizeof b, "%.17g", v.n);
         o += b;
+        if (!strpbrk(b, ".eEni")) o += ".0";  // stays a float64 through a re-parse
       }
       break;
     }
@@ -457,7 +461,18 @@ bool generate_rule(JV& out, const std::string& name, const JV& rule, const char*
     }
   }
   const JV* val = rule.get("validate");
-  auto wrap = [&](const JV& target) {
+  // SetPattern(ToJSON(...)) (autogen rule.go:130-183): json.Marshal writes a whole float64
+  // below 1e21 as an integer literal, which decodes back as int64 when it fits.
+  std::function<void(JV&)> marshal = [&](JV& x) {
+    if (x.t == JV::Num && !x.is_int && std::isfinite(x.n) && x.n == std::trunc(x.n) && std::fabs(x.n) < 1e21 &&
+        x.n >= -9223372036854775808.0 && x.n < 9223372036854775808.0)
+      x.is_int = true, x.i = (int64_t)x.n;
+    for (auto& y : x.a) marshal(y);
+    for (auto& kv : x.o) marshal(kv.second);
+  };
+  auto wrap = [&](const JV& target0) {
+    JV target = target0;
+    marshal(target);
     JV inner = JV::obj(), outer = JV::obj();
     inner.set(tpl, target);
     outer.set("spec", inner);
@@ -553,11 +568,327 @@ std::vector<JV> compute_rules(const JV& policy) {
   return out;
 }
 
+// ---- pattern compilation (validate.pattern / anyPattern) ----------------------------------
+// Restates, at compile time, every decision of the reference's tree walk that depends only
+// on the pattern: anchor parsing (anchor/anchor.go:8-123), the anchor / non-anchor split and
+// evaluation order of validateMap (validate/validate.go:118-175, validate/utils.go:11-69),
+// array shapes (validate.go:177-261), the string-pattern grammar (pattern.go:152-215,
+// operator/operator.go:7-61) and the ExpandInMetadata targets (wildcards/wildcards.go:83-162).
+// Everything that depends on the resource is left to kpe_pattern_kernel.
+namespace pc {
+
+enum AK { AK_NONE, AK_COND, AK_GLOBAL, AK_NEG, AK_ADD, AK_EQ, AK_EXIST };
+struct Anc {
+  AK k = AK_NONE;
+  std::string key;
+};
+inline bool ws_ascii(char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\v' || c == '\f' || c == '\r'; }
+std::string trim_ws(const std::string& s) {
+  size_t a = 0, b = s.size();
+  while (a < b && ws_ascii(s[a])) ++a;
+  while (b > a && ws_ascii(s[b - 1])) --b;
+  return s.substr(a, b - a);
+}
+std::string trim_sp(const std::string& s) {
+  size_t a = s.find_first_not_of(' ');
+  if (a == std::string::npos) return "";
+  return s.substr(a, s.find_last_not_of(' ') - a + 1);
+}
+// ^([+<=X^])?\((.+)\)$ on the TrimSpace-d key
+Anc anchor_of(const std::string& raw) {
+  Anc r;
+  const std::string t = trim_ws(raw);
+  if (t.size() < 3 || t.back() != ')') return r;
+  static const char mods[] = "+<=X^";
+  static const AK kinds[] = {AK_ADD, AK_GLOBAL, AK_EQ, AK_NEG, AK_EXIST};
+  size_t open = 0;
+  AK k = AK_COND;
+  if (const char* m = strchr(mods, t[0]); m && t[0]) k = kinds[m - mods], open = 1;
+  if (t[open] != '(') return r;
+  std::string inner = t.substr(open + 1, t.size() - open - 2);
+  if (inner.empty() || inner.find('\n') != std::string::npos) return r;
+  r.k = k;
+  r.key = std::move(inner);
+  return r;
+}
+bool phase1(AK k) { return k == AK_COND || k == AK_EXIST || k == AK_EQ || k == AK_NEG; }
+bool nested_anchor(const JV& v) {
+  if (v.t == JV::Obj) {
+    for (auto& kv : v.o) {
+      const AK k = anchor_of(kv.first).k;
+      if (phase1(k) || k == AK_GLOBAL) return true;
+    }
+    for (auto& kv : v.o)
+      if (nested_anchor(kv.second)) return true;
+  } else if (v.t == JV::Arr) {
+    for (auto& x : v.a)
+      if (nested_anchor(x)) return true;
+  }
+  return false;
+}
+bool has_glob(const std::string& s) { return s.find_first_of("*?") != std::string::npos; }
+bool has_vars(const JV& v) {
+  auto bad = [](const std::string& x) { return x.find("{{") != std::string::npos || x.find("$(") != std::string::npos; };
+  if (v.t == JV::Str) return bad(v.s);
+  for (auto& x : v.a)
+    if (has_vars(x)) return true;
+  for (auto& kv : v.o)
+    if (bad(kv.first) || has_vars(kv.second)) return true;
+  return false;
+}
+// one range endpoint, anchored: [-|+]?\d+(\.\d+)?[A-Za-z]*
+bool endpoint(const std::string& x) {
+  size_t i = 0;
+  auto dg = [&](size_t j) { return j < x.size() && x[j] >= '0' && x[j] <= '9'; };
+  if (i < x.size() && (x[i] == '-' || x[i] == '|' || x[i] == '+')) ++i;
+  if (!dg(i)) return false;
+  while (dg(i)) ++i;
+  if (i < x.size() && x[i] == '.') {
+    if (!dg(i + 1)) return false;
+    ++i;
+    while (dg(i)) ++i;
+  }
+  while (i < x.size() && isalpha((unsigned char)x[i])) ++i;
+  return i == x.size();
+}
+bool split_range(const std::string& t, const char* sep, std::string* l, std::string* r) {
+  const size_t n = strlen(sep);
+  for (size_t k = 1; k + n <= t.size(); ++k)
+    if (!t.compare(k, n, sep) && endpoint(t.substr(0, k)) && endpoint(t.substr(k + n))) {
+      *l = t.substr(0, k), *r = t.substr(k + n);
+      return true;
+    }
+  return false;
+}
+
+class PatCompiler {
+ public:
+  PatCompiler(PatProgram& pp, std::function<int32_t(const std::string&)> key_pred) : PP(pp), key_pred_(key_pred) {}
+
+  // one root (validate.MatchPattern call); returns the root table index
+  uint32_t root(const JV& pattern) {
+    slots_.clear();
+    expand_.clear();
+    const uint32_t n = node(pattern, 0, false);
+    PP.roots.push_back(n);
+    PP.roots.push_back((uint32_t)slots_.size());
+    return (uint32_t)(PP.roots.size() / 2 - 1);
+  }
+
+ private:
+  static constexpr int kMaxDepth = 12;  // kernels.hip PatEval depth
+  PatProgram& PP;
+  std::function<int32_t(const std::string&)> key_pred_;
+  std::map<std::string, uint32_t> slots_;  // AnchorMap key -> slot
+  std::set<const JV*> expand_;             // labels/annotations maps ExpandInMetadata rewrites
+
+  uint32_t push_node(KpePNode n) {
+    PP.nodes.push_back(n);
+    return (uint32_t)PP.nodes.size() - 1;
+  }
+  uint32_t operand(const std::string& text, bool exact) {
+    PP.operands.push_back(text);
+    PP.operand_exact.push_back(exact ? 1 : 0);
+    return (uint32_t)PP.operands.size() - 1;
+  }
+  void cond(uint32_t op, const std::string& operand_text, uint32_t flags) {
+    KpeCond c{};
+    c.op = op | flags;
+    c.pat = operand(operand_text, false);
+    int64_t d;
+    if (goval::parse_duration(operand_text, &d)) c.op |= PC_DUR, c.dur = d;
+    goval::Quantity q;
+    if (goval::parse_quantity(operand_text, &q)) {
+      c.op |= PC_QTY | (q.neg ? PC_QNEG : 0u);
+      c.qlo = (uint64_t)q.m, c.qhi = (uint64_t)(q.m >> 64), c.qexp = q.e;
+    }
+    PP.conds.push_back(c);
+  }
+  uint32_t leaf(const JV& v) {
+    KpeLeaf l{};
+    switch (v.t) {
+      case JV::Bool: l.type = PL_BOOL, l.bval = v.b ? 1u : 0u; break;
+      case JV::Num:
+        if (v.is_int) l.type = PL_INT, l.ival = v.i;
+        else l.type = PL_FLOAT, l.fval = v.n;
+        break;
+      case JV::Null: l.type = PL_NIL; break;
+      case JV::Str: {
+        l.type = PL_STR;
+        l.exact = operand(v.s, true);
+        l.c0 = (uint32_t)PP.conds.size();
+        size_t a = 0;
+        const std::string& pat = v.s;
+        for (size_t i = 0; i <= pat.size(); ++i) {  // strings.Split(pattern, "|")
+          if (i < pat.size() && pat[i] != '|') continue;
+          const std::string alt = trim_sp(pat.substr(a, i - a));
+          a = i + 1;
+          uint32_t group = PC_NEWGROUP;
+          size_t b = 0;
+          for (size_t j = 0; j <= alt.size(); ++j) {  // strings.Split(alternative, "&")
+            if (j < alt.size() && alt[j] != '&') continue;
+            const std::string t = trim_sp(alt.substr(b, j - b));
+            b = j + 1;
+            std::string lo, hi;
+            // operator.GetOperatorFromStringPattern
+            uint32_t op = PC_EQ;
+            size_t oplen = 0;
+            if (t.size() >= 2) {
+              if (!t.compare(0, 2, ">=")) op = PC_GE, oplen = 2;
+              else if (!t.compare(0, 2, "<=")) op = PC_LE, oplen = 2;
+              else if (t[0] == '>') op = PC_GT, oplen = 1;
+              else if (t[0] == '<') op = PC_LT, oplen = 1;
+              else if (t[0] == '!') op = PC_NE, oplen = 1;
+              else if (split_range(t, "!-", &lo, &hi)) {  // NotInRange: < lo | > hi
+                cond(PC_LT, lo, group | PC_OR2);
+                cond(PC_GT, hi, 0);
+                group = 0;
+                continue;
+              } else if (split_range(t, "-", &lo, &hi)) {  // InRange: >= lo & <= hi
+                cond(PC_GE, lo, group);
+                cond(PC_LE, hi, 0);
+                group = 0;
+                continue;
+              }
+            }
+            cond(op, trim_ws(t.substr(oplen)), group);
+            group = 0;
+          }
+        }
+        l.nc = (uint32_t)PP.conds.size() - l.c0;
+        break;
+      }
+      default: l.type = PL_NEVER; break;
+    }
+    PP.leaves.push_back(l);
+    return (uint32_t)PP.leaves.size() - 1;
+  }
+
+  uint32_t node(const JV& v, int depth, bool repeated) {
+    if (depth > kMaxDepth) throw CompileError("pattern nested deeper than 12 levels");
+    if (v.t == JV::Obj) return map(v, depth, repeated);
+    if (v.t == JV::Arr) {
+      if (v.a.empty()) return push_node({PN_ARR_EMPTY, 0, 0, 0});
+      const JV& e0 = v.a[0];
+      if (e0.t == JV::Obj) {
+        const uint32_t n = node(e0, depth + 1, true);
+        return push_node({PN_ARR_MAPS, n, 0, 0});
+      }
+      if (e0.t != JV::Arr) return push_node({PN_ARR_LEAF, leaf(e0), 0, 0});
+      std::vector<uint32_t> kids;
+      for (auto& e : v.a) kids.push_back(node(e, depth + 1, true));
+      const uint32_t at = (uint32_t)PP.lists.size();
+      PP.lists.insert(PP.lists.end(), kids.begin(), kids.end());
+      return push_node({PN_ARR_POS, at, (uint32_t)kids.size(), 0});
+    }
+    return push_node({PN_LEAF, leaf(v), 0, 0});
+  }
+
+  uint32_t map(const JV& v, int depth, bool repeated) {
+    // ExpandInMetadata targets below this map (getPatternValue: plain or anchored key)
+    const JV* meta = nullptr;
+    for (auto& kv : v.o)
+      if (kv.first == "metadata" || anchor_of(kv.first).key == "metadata") {
+        meta = &kv.second;
+        break;
+      }
+    if (meta && meta->t == JV::Obj)
+      for (const char* tag : {"labels", "annotations"})
+        for (auto& kv : meta->o)
+          if (kv.first == tag || anchor_of(kv.first).key == tag) {
+            if (kv.second.t == JV::Obj) expand_.insert(&kv.second);
+            break;
+          }
+    const bool expanding = expand_.count(&v) > 0;
+    std::vector<std::string> first, front, back;
+    for (auto& kv : v.o) {
+      const Anc a = anchor_of(kv.first);
+      if (expanding && has_glob(kv.first)) {
+        if (repeated) throw CompileError("wildcard metadata keys under an array pattern are not supported");
+        if (a.k != AK_NONE && a.k != AK_EQ && a.k != AK_ADD)
+          throw CompileError("wildcard condition/negation/existence/global anchors in metadata are not supported");
+      }
+      if (phase1(a.k)) first.push_back(kv.first);
+    }
+    std::sort(first.begin(), first.end());
+    std::vector<std::string> rest;
+    for (auto& kv : v.o)
+      if (!phase1(anchor_of(kv.first).k)) rest.push_back(kv.first);
+    std::sort(rest.begin(), rest.end());
+    for (auto& k : rest) {
+      if (anchor_of(k).k == AK_GLOBAL || nested_anchor(*v.get(k.c_str()))) front.insert(front.begin(), k);
+      else back.push_back(k);
+    }
+    std::vector<std::string> order = first;
+    order.insert(order.end(), front.begin(), front.end());
+    order.insert(order.end(), back.begin(), back.end());
+    // members are written after the values are compiled (values append members too)
+    std::vector<uint32_t> mem;
+    for (auto& k : order) {
+      const JV& val = *v.get(k.c_str());
+      const Anc a = anchor_of(k);
+      uint32_t h = PM_DEFAULT, flags = 0, slot = 0, w = 0xFFFFFFFFu, vn = 0xFFFFFFFFu;  // w: PRED_NONE
+      std::string name = k;
+      switch (a.k) {
+        case AK_COND: h = PM_COND; break;
+        case AK_GLOBAL: h = PM_GLOBAL; break;
+        case AK_EXIST: h = PM_EXIST; break;
+        case AK_EQ: h = PM_EQ; break;
+        case AK_NEG: h = PM_NEG; break;
+        default: break;  // plain keys and "+(...)" keys are looked up verbatim
+      }
+      if (h != PM_DEFAULT) name = a.key;
+      if (h == PM_COND || h == PM_EXIST) {
+        auto it = slots_.find(k);
+        if (it == slots_.end()) {
+          if (slots_.size() >= 32) throw CompileError("more than 32 condition/existence anchors in one pattern");
+          it = slots_.emplace(k, (uint32_t)slots_.size()).first;
+        }
+        flags |= PMF_SLOT, slot = it->second;
+      }
+      if (h == PM_DEFAULT && val.t == JV::Str && val.s == "*") flags |= PMF_STAR;
+      if (expanding && has_glob(k) && a.k != AK_ADD) {  // "+(...)" keys stay verbatim
+        flags |= PMF_GLOB;
+        w = (uint32_t)key_pred_(name);
+      }
+      if (h == PM_EXIST) {
+        if (val.t != JV::Arr) {
+          vn = push_node({PN_BAD, 0, 0, 0});
+        } else {
+          std::vector<uint32_t> kids;
+          for (auto& e : val.a)
+            kids.push_back(e.t == JV::Obj ? node(e, depth + 1, true) : push_node({PN_BAD, 0, 0, 0}));
+          const uint32_t at = (uint32_t)PP.lists.size();
+          PP.lists.insert(PP.lists.end(), kids.begin(), kids.end());
+          vn = push_node({PN_EXLIST, at, (uint32_t)kids.size(), 0});
+        }
+      } else if (h != PM_NEG && !(flags & PMF_STAR)) {
+        vn = node(val, depth + 1, repeated);
+      }
+      uint32_t ki = 0;
+      for (; ki < PP.keys.size() && PP.keys[ki] != name; ++ki) {
+      }
+      if (ki == PP.keys.size()) PP.keys.push_back(name);
+      mem.insert(mem.end(), {h | flags | (slot << 8), ki, vn, w});
+    }
+    const uint32_t m0 = (uint32_t)(PP.members.size() / 4);
+    PP.members.insert(PP.members.end(), mem.begin(), mem.end());
+    return push_node({PN_MAP, m0, (uint32_t)first.size() | ((uint32_t)order.size() << 16), 0});
+  }
+};
+
+}  // namespace pc
+
 // ---- lowering ----
 class Lowerer {
  public:
   explicit Lowerer(Program& p) : P(p) {}
 
+  static void to_float(JV& v) {
+    if (v.t == JV::Num && v.is_int) v.is_int = false, v.n = (double)v.i;
+    for (auto& x : v.a) to_float(x);
+    for (auto& kv : v.o) to_float(kv.second);
+  }
   int32_t pred(uint32_t domain, std::vector<std::string> globs) {
     for (size_t i = 0; i < P.preds.size(); ++i)
       if (P.preds[i].domain == domain && P.preds[i].globs == globs) return (int32_t)i;
@@ -902,7 +1233,46 @@ class Lowerer {
       k.cv_class = (uint32_t)(it - P.cv_classes.begin());
       if (it == P.cv_classes.end()) P.cv_classes.push_back(k.cv_mask);
     } else {
-      throw CompileError("rule '" + rname + "': only podSecurity validate rules are supported on the device yet");
+      // validate_resource.go:121-170: deny, then pattern / anyPattern, then foreach
+      auto present = [&](const char* key) { return v->get(key) && v->get(key)->t != JV::Null; };
+      if (present("deny")) throw CompileError("rule '" + rname + "': validate.deny is not supported on the device yet");
+      if (present("pattern") || present("anyPattern")) {
+        if (nonempty(r.get("preconditions")) || nonempty(r.get("context")))
+          throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
+        if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with pattern rules is not supported");
+        pc::PatCompiler pcomp(P.pat, [&](const std::string& g) {
+          const int32_t id = pred(D_KEY, {g});
+          P.preds[id].global_only = true;
+          return id;
+        });
+        KpePatRule pr{(uint32_t)P.rules.size(), 0, (uint32_t)(P.pat.roots.size() / 2), 0};
+        if (present("pattern")) {
+          const JV& pt = *v->get("pattern");
+          if (pc::has_vars(pt)) throw CompileError("rule '" + rname + "': pattern variables are not supported yet");
+          pcomp.root(pt);
+          pr.nr = 1;
+        } else {
+          const JV& ap = *v->get("anyPattern");
+          pr.flags = PR_ANY;
+          if (ap.t != JV::Arr) {
+            pr.flags |= PR_ANY_BAD;  // deserializeAnyPattern fails: RuleStatusError
+          } else {
+            if (pc::has_vars(ap)) throw CompileError("rule '" + rname + "': pattern variables are not supported yet");
+            for (auto& e : ap.a) {
+              JV f = e;
+              to_float(f);  // encoding/json round trip (validate_resource.go:400-416)
+              pcomp.root(f);
+              ++pr.nr;
+            }
+          }
+        }
+        P.pat.rules.push_back(pr);
+        k.handler = H_PATTERN;
+      } else if (nonempty(v->get("foreach")) || nonempty(v->get("cel"))) {
+        throw CompileError("rule '" + rname + "': validate.foreach/cel are not supported on the device yet");
+      } else {
+        k.handler = H_NONE;  // no podSecurity/cel/pattern/deny/foreach: the validator returns nil
+      }
     }
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);

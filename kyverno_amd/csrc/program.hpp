@@ -14,6 +14,23 @@ struct Pred {
   uint32_t domain;
   std::vector<std::string> globs;  // OR of go-wildcard patterns
   uint32_t special = 0;            // PRED_SPECIAL_*: a validity test instead of globs
+  bool global_only = false;        // read outside the scan kernel (kept in HBM, never LDS-only)
+};
+
+// Compiled validate.pattern / anyPattern trees (schema.h PN_* / PM_* / PL_* / PC_*).
+// Member names and string operands are kept as text: a binding resolves names to corpus
+// D_KEY ids and the device program turns operands into pattern records.
+struct PatProgram {
+  std::vector<KpePNode> nodes;
+  std::vector<uint32_t> members;       // 4 words per member; y = index into keys
+  std::vector<std::string> keys;       // member names
+  std::vector<uint32_t> lists;         // node lists (PN_ARR_POS / PN_EXLIST)
+  std::vector<KpeLeaf> leaves;
+  std::vector<KpeCond> conds;          // KpeCond.pat / KpeLeaf.exact index operands
+  std::vector<std::string> operands;   // glob operand text
+  std::vector<uint8_t> operand_exact;  // 1: compare verbatim (the `value == pattern` check)
+  std::vector<uint32_t> roots;         // 2 words per root: node, anchor slots used
+  std::vector<KpePatRule> rules;
 };
 #define PRED_SPECIAL_NONE 0u
 #define PRED_SPECIAL_QNAME 1u   // validation.IsQualifiedName (label keys)
@@ -44,6 +61,7 @@ struct Program {
   std::vector<uint32_t> cv_classes;  // distinct cv_masks of PSS rules
   bool any_apply_one = false;
   bool any_pss = false;
+  PatProgram pat;  // pattern rules (H_PATTERN)
   DeviceProgram* dev = nullptr;
   ~Program();
 };

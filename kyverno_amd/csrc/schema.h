@@ -26,6 +26,7 @@ enum KpeDomain {
   D_IMAGE,       // container images
   D_CNAME,       // container names
   D_MISC,        // seccomp type / procMount / seLinux strings (cold, exclusions)
+  D_KEY,         // object member names of the generic document tape (pattern rules)
   KPE_NUM_DOMAINS
 };
 
@@ -267,12 +268,14 @@ enum KpeCheckVersion {
 #define KPE_WARN_ 3
 #define KPE_ERROR_ 4
 #define KPE_SKIP_ 5
+#define KPE_PENDING_ 6  // device-internal: matched pattern rule, resolved by kpe_pattern_kernel
 
 // ---- policy program ------------------------------------------------------------------------------
 // Rule handlers
 #define H_NONE 0u  // no validate handler => no RuleResponse (NA even when matched)
 #define H_PSS 1u
 #define H_ERROR 2u  // every matching resource gets RuleStatusError (e.g. unparsable PSS version)
+#define H_PATTERN 3u  // validate.pattern / validate.anyPattern (validate_resource.go:316-398)
 
 // Match terms (AND inside a filter block)
 enum KpeTermType {
@@ -343,3 +346,109 @@ typedef struct KpeRule {
   uint32_t cv_class;      // PSS: index of cv_mask among the program's distinct cv_masks
   uint32_t pad[2];        // 16 words
 } KpeRule;
+
+// ---- generic document tape (pattern rules) ---------------------------------------------
+// Every resource is also kept as a pre-order node array (its JSON document as the
+// reference's unstructured map sees it). Node (uint2):
+//   x = kind | (member-name id + 1) << 2   (D_KEY id; 0 = array element / root)
+//   y = scalar id (DN_SCALAR) or number of nodes in the subtree below (DN_MAP / DN_ARR),
+//       so the next sibling of node i is i + 1 + (container ? y : 0).
+#define DN_SCALAR 0u
+#define DN_MAP 1u
+#define DN_ARR 2u
+#define DN_KIND(x) ((x) & 3u)
+#define DN_KEY(x) ((x) >> 2)
+#define DN_MAX_KEYS 0x3FFFFFFEu
+
+// Scalar table: one entry per distinct (type, value) of the corpus; ids 0/1/2 are null,
+// false, true. Attributes are what pattern.go derives from a value (goval.hpp).
+#define SC_NULL_ID 0u
+#define SC_FALSE_ID 1u
+#define SC_TRUE_ID 2u
+#define SC_T_NULL 0u
+#define SC_T_BOOL 1u
+#define SC_T_INT 2u
+#define SC_T_FLOAT 3u
+#define SC_T_STR 4u
+#define SC_TYPE(f) ((f) & 7u)
+#define SC_PINT (1u << 3)    // string: strconv.ParseInt ok -> ival
+#define SC_PFLOAT (1u << 4)  // string: strconv.ParseFloat ok -> fval
+#define SC_DUR (1u << 5)     // convertNumberToString(v) parses as a duration -> dur
+#define SC_QTY (1u << 6)     // ... as a quantity -> (qneg, qlo/qhi, qexp)
+#define SC_QNEG (1u << 7)
+#define SC_TEXT (1u << 8)    // compareString text valid: text pool [text_off, +text_len)
+#define SC_BTRUE (1u << 9)
+typedef struct KpeScalar {
+  uint32_t flags, text_off, text_len, pad;
+  int64_t ival;
+  double fval;
+  int64_t dur;
+  int64_t qexp;
+  uint64_t qlo, qhi;
+} KpeScalar;  // 64 bytes
+
+// ---- compiled patterns -------------------------------------------------------------------
+// Pattern node
+#define PN_LEAF 0u       // y = leaf index
+#define PN_MAP 1u        // y = first member, z = number of anchor-phase members | total << 16
+#define PN_ARR_EMPTY 2u  // []: "pattern Array empty"
+#define PN_ARR_MAPS 3u   // [map, ...]: y = node of element 0 (validateArrayOfMaps)
+#define PN_ARR_LEAF 4u   // [scalar, ...]: y = leaf of element 0 (every element must match)
+#define PN_ARR_POS 5u    // [[...], ...]: y = first entry of the node list, z = count (positional)
+#define PN_EXLIST 6u     // existence-anchor value: y = node list entry, z = count (PN_BAD entries allowed)
+#define PN_BAD 7u        // existence element that is not a map / pattern that is not a list
+typedef struct KpePNode {
+  uint32_t kind, y, z, w;
+} KpePNode;
+// Pattern member (uint4): x = handler | PMF_* | slot << 8, y = member-name id + 1 (per
+// binding; 0 = name absent from the corpus), z = value node, w = glob-key predicate
+// location (PMF_GLOB) or PRED_NONE
+#define PM_DEFAULT 0u
+#define PM_COND 1u
+#define PM_GLOBAL 2u
+#define PM_EXIST 3u
+#define PM_EQ 4u
+#define PM_NEG 5u
+#define PM_HANDLER(x) ((x) & 7u)
+#define PMF_STAR (1u << 3)   // default handler whose value is the string "*" (presence check)
+#define PMF_GLOB (1u << 4)   // ExpandInMetadata: first resource member matching the glob (string values)
+#define PMF_SLOT (1u << 5)   // condition / existence anchor tracked in the AnchorMap
+#define PM_SLOT(x) (((x) >> 8) & 31u)
+// Leaf
+#define PL_BOOL 0u
+#define PL_INT 1u
+#define PL_FLOAT 2u
+#define PL_NIL 3u
+#define PL_STR 4u
+#define PL_NEVER 5u  // array pattern in leaf position: always false
+typedef struct KpeLeaf {
+  uint32_t type, bval, c0, nc;  // PL_STR: conditions [c0, c0 + nc)
+  int64_t ival;
+  double fval;
+  uint32_t exact;               // PL_STR: pattern-operand record of the whole pattern (value == pattern)
+  uint32_t pad[3];
+} KpeLeaf;  // 40 -> 48 bytes
+// String-pattern condition (one `&`-term of one `|`-alternative)
+#define PC_OP(x) ((x) & 7u)
+#define PC_EQ 0u
+#define PC_GE 1u
+#define PC_LE 2u
+#define PC_NE 3u
+#define PC_GT 4u
+#define PC_LT 5u
+#define PC_NEWGROUP (1u << 3)  // first condition of a `|` alternative
+#define PC_OR2 (1u << 4)       // NotInRange: this condition OR the next one (one term)
+#define PC_DUR (1u << 5)       // operand parses as a duration
+#define PC_QTY (1u << 6)       // operand parses as a quantity
+#define PC_QNEG (1u << 7)
+typedef struct KpeCond {
+  uint32_t op, pat, pad0, pad1;  // pat: operand record (compareString glob)
+  int64_t dur, qexp;
+  uint64_t qlo, qhi;
+} KpeCond;  // 48 bytes
+// Pattern rule: roots [r0, r0 + nr) of the root table (uint2: node, anchor slots)
+#define PR_ANY 1u        // anyPattern
+#define PR_ANY_BAD 2u    // anyPattern that is not a list: RuleStatusError
+typedef struct KpePatRule {
+  uint32_t col, flags, r0, nr;
+} KpePatRule;

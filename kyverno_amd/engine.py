@@ -138,7 +138,9 @@ class PolicySet:
 class Corpus:
     """Flattened, string-interned resources (host columns, optionally on a device)."""
 
-    def __init__(self, resources, namespace_labels: Optional[Dict[str, Dict[str, str]]] = None):
+    DOCS = 1  # KPE_CORPUS_DOCS: keep document tapes (pattern / anyPattern rules)
+
+    def __init__(self, resources, namespace_labels: Optional[Dict[str, Dict[str, str]]] = None, docs: bool = True):
         L = load()
         if isinstance(resources, (bytes, bytearray)):
             raw = bytes(resources)
@@ -151,7 +153,8 @@ class Corpus:
         else:
             nsl = json.dumps(namespace_labels).encode() if namespace_labels else b""
         h = ctypes.c_void_p()
-        check(L.kpe_corpus_flatten(raw, len(raw), nsl if nsl else None, len(nsl), ctypes.byref(h)))
+        check(L.kpe_corpus_flatten_ex(raw, len(raw), nsl if nsl else None, len(nsl), self.DOCS if docs else 0,
+                                      ctypes.byref(h)))
         self.h = h
         self.n = int(L.kpe_corpus_num_resources(h))
         self.nbytes = int(L.kpe_corpus_bytes(h))

@@ -26,6 +26,10 @@ outputs) lifted from the reference's tests:
                               per-rule results of `kyverno test`; YAML decoded like
                               sigs.k8s.io/yaml: no timestamp resolution, whole floats -> ints;
                               empty namespaces set to "default" as resource.go:56-58 does)
+  chart_policies.json      <- charts/kyverno-policies/templates/{baseline,restricted}/*.yaml rendered
+                              with the chart defaults (ClusterPolicy, Audit, background, every
+                              `if`/`with` false except the file guard, `else` branches taken,
+                              backtick-escaped JMESPath kept verbatim)
   match_rd_cases.json      <- pkg/engine/utils/utils_test.go:1828-2460, hand-transcribed below
                               (Go struct literals): MatchesResourceDescription on the nginx
                               Deployment with kinds/name/generateName/selector/exclude blocks
@@ -401,7 +405,45 @@ def cli_cases():
     return out
 
 
+def _render_chart_template(text):
+    name = re.search(r'\$name := "([^"]+)"', text).group(1)
+    out, stack = [], []  # stack of "branch active" flags
+    for line in text.splitlines():
+        ctl = re.match(r"\s*\{\{-?\s*(if|with|else|end)\b(.*?)-?\}\}\s*$", line)
+        if ctl:
+            kw, arg = ctl.group(1), ctl.group(2)
+            if kw in ("if", "with"):
+                stack.append("include \"kyverno-policies.podSecurity" in arg)  # the file guard only
+            elif kw == "else":
+                stack[-1] = not stack[-1]
+            else:
+                stack.pop()
+            continue
+        if not all(stack):
+            continue
+        if line.strip().startswith("{{"):
+            continue  # `{{- $x := ... }}`, `{{- include ... }}`
+        line = re.sub(r"\{\{`(.*?)`\}\}", lambda m: m.group(1), line)
+        line = line.replace("{{ .Values.policyKind }}", "ClusterPolicy").replace("{{ $name }}", name)
+        line = line.replace("{{ .Values.validationFailureAction }}", "Audit")
+        line = line.replace("{{ .Values.background }}", "true").replace("{{ .Values.failurePolicy }}", "Fail")
+        if "{{" in line:
+            continue  # labels / severity includes: metadata only
+        out.append(line)
+    return yaml.load("\n".join(out), Loader=_GoYamlLoader)
+
+
+def chart_policies():
+    base = "charts/kyverno-policies/templates"
+    out = {}
+    for level in ("baseline", "restricted"):
+        for f in sorted(os.listdir(os.path.join(REF, base, level))):
+            out.setdefault(level, []).append(_go_json(_render_chart_template(open(os.path.join(REF, base, level, f)).read())))
+    return out
+
+
 if __name__ == "__main__":
+    _dump("chart_policies.json", chart_policies())
     _dump("cli_cases.json", cli_cases())
     _dump("pattern_leaf_cases.json", pattern_leaf_cases())
     _dump("pattern_tree_cases.json", pattern_tree_cases())

@@ -53,10 +53,19 @@ def test_compile_matches_oracle_rule_names(oracle):
 
 def test_compile_unsupported_is_loud():
     pol = pss_policy("x", "baseline")
-    pol["spec"]["rules"][0]["validate"] = {"pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}
+    pol["spec"]["rules"][0]["validate"] = {"deny": {"conditions": {"any": [{"key": "a", "operator": "Equals",
+                                                                            "value": "a"}]}}}
     with pytest.raises(KpeError) as e:
         K.PolicySet([pol])
     assert e.value.status == 2  # KPE_E_UNSUPPORTED
+    # pattern variables need JMESPath substitution: refused too
+    pol["spec"]["rules"][0]["validate"] = {"pattern": {"metadata": {"name": "{{ request.object.kind }}"}}}
+    with pytest.raises(KpeError) as e:
+        K.PolicySet([pol])
+    assert e.value.status == 2
+    # plain patterns compile (H_PATTERN)
+    pol["spec"]["rules"][0]["validate"] = {"pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}
+    assert K.PolicySet([pol]).num_rules == 3
 
 
 def test_compile_selectors():
