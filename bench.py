@@ -63,7 +63,7 @@ def main():
         # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus (seed 0xC2)
         first = (rank * args.replicas + k) * n
         nd = K.synth_resources(0xC2, n, mix=0, first_index=first)
-        c = K.Corpus(nd)
+        c = K.Corpus(nd, docs=False)  # PSS only: no document tapes
         del nd
         c.upload(eng.device)
         corpora.append(c)

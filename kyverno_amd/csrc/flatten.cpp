@@ -1099,7 +1099,7 @@ void scalar_attrs(KpeScalar& e, std::string_view numstr) {
   goval::Quantity q;
   if (goval::parse_quantity(numstr, &q)) {
     e.flags |= SC_QTY | (q.neg ? SC_QNEG : 0u);
-    e.qlo = (uint64_t)q.m, e.qhi = (uint64_t)(q.m >> 64), e.qexp = q.e;
+    goval::qty_key(q, &e.qexp, &e.qlo, &e.qhi);
   }
 }
 
@@ -1180,6 +1180,26 @@ class DocBuilder {
     C.doc.push_back(kind | (key1 << 2));
     C.doc.push_back(y);
   }
+  // rewrite the members of the map at node `at` (the tape's last subtree) keeping only the
+  // last member of each name
+  void drop_duplicates(size_t at) {
+    const size_t end = C.doc.size() / 2;
+    std::vector<std::pair<size_t, size_t>> kids;  // (first node, node count)
+    for (size_t i = at + 1; i < end;) {
+      const uint32_t x = C.doc[2 * i];
+      const size_t len = 1 + (DN_KIND(x) != DN_SCALAR ? C.doc[2 * i + 1] : 0u);
+      kids.emplace_back(i, len);
+      i += len;
+    }
+    std::unordered_map<uint32_t, size_t> last;
+    for (size_t j = 0; j < kids.size(); ++j) last[DN_KEY(C.doc[2 * kids[j].first])] = j;
+    std::vector<uint32_t> out;
+    for (size_t j = 0; j < kids.size(); ++j)
+      if (last[DN_KEY(C.doc[2 * kids[j].first])] == j)
+        out.insert(out.end(), C.doc.begin() + 2 * kids[j].first, C.doc.begin() + 2 * (kids[j].first + kids[j].second));
+    C.doc.resize(2 * (at + 1));
+    C.doc.insert(C.doc.end(), out.begin(), out.end());
+  }
   void value(JCur& c, uint32_t key1, int depth) {
     if (depth > 256) throw LimitError("document nesting deeper than 256");
     const size_t at = C.doc.size() / 2;
@@ -1209,10 +1229,17 @@ class DocBuilder {
         bool f = true;
         std::string_view k;
         std::string ks;
+        std::vector<uint32_t> names;
         while (c.obj_next(f, &k, ks)) {
           const uint32_t kid = C.dict[D_KEY].intern(k);
           if (kid >= DN_MAX_KEYS) throw LimitError("too many distinct member names");
+          names.push_back(kid);
           value(c, kid + 1, depth + 1);
+        }
+        if (names.size() > 1) {  // duplicate names: a Go map decode keeps the last one
+          std::vector<uint32_t> sorted(names);
+          std::sort(sorted.begin(), sorted.end());
+          if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) drop_duplicates(at);
         }
         C.doc[2 * at + 1] = (uint32_t)(C.doc.size() / 2 - at - 1);
         break;

@@ -355,6 +355,22 @@ inline bool parse_quantity(std::string_view str, Quantity* out) {
   return true;
 }
 
+// Comparison key of a quantity: order = number of digits of m + e, and m left-aligned to
+// 38 digits (m * 10^(38 - digits) < 10^38 < 2^127). Two non-zero values of one sign then
+// compare by (order, aligned m) with plain integer compares on the device.
+inline void qty_key(const Quantity& q, int64_t* order, uint64_t* lo, uint64_t* hi) {
+  if (q.m == 0) {
+    *order = 0, *lo = 0, *hi = 0;
+    return;
+  }
+  int d = 0;
+  for (u128 t = q.m; t; t /= 10) ++d;
+  u128 x = q.m;
+  for (int k = d; k < 38; ++k) x *= 10;
+  *order = (int64_t)d + q.e;
+  *lo = (uint64_t)x, *hi = (uint64_t)(x >> 64);
+}
+
 // fmt.Sprintf("%f", v)
 inline std::string fmt_f(double v) {
   char b[400];

@@ -28,109 +28,7 @@
 #include "schema.h"
 
 namespace {
-
-// ---------------------------------------------------------------------------
-// go-wildcard v1.0.3 over UTF-8: '*' any rune sequence, '?' exactly one rune.
-__device__ __forceinline__ int rune_len(const uint8_t* s, int i, int n) {
-  uint8_t c = s[i];
-  int l = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 1;
-  if (i + l > n) return 1;
-  for (int k = 1; k < l; ++k)
-    if ((s[i + k] >> 6) != 2) return 1;  // invalid sequence: one byte = one (U+FFFD) rune
-  return l;
-}
-
-__device__ bool glob(const uint8_t* p, int pn, const uint8_t* s, int sn) {
-  if (pn == 0) return sn == 0;
-  int pi = 0, si = 0, star = -1, mark = 0;
-  while (si < sn) {
-    if (pi < pn && p[pi] == '?') {
-      ++pi;
-      si += rune_len(s, si, sn);
-    } else if (pi < pn && p[pi] == '*') {
-      star = pi++;
-      mark = si;
-    } else if (pi < pn && p[pi] == s[si]) {
-      ++pi;
-      ++si;
-    } else if (star >= 0) {
-      pi = star + 1;
-      mark += rune_len(s, mark, sn);
-      si = mark;
-    } else {
-      return false;
-    }
-  }
-  while (pi < pn && p[pi] == '*') ++pi;
-  return pi == pn;
-}
-
-__device__ __forceinline__ bool bytes_eq(const uint8_t* a, const uint8_t* b, int n) {
-  int i = 0;
-  for (; i + 8 <= n; i += 8) {  // 8 independent byte loads per step: short dependence chains
-    uint32_t d = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d |= (uint32_t)(a[i + k] ^ b[i + k]);
-    if (d) return false;
-  }
-  uint32_t d = 0;
-  for (; i < n; ++i) d |= (uint32_t)(a[i] ^ b[i]);
-  return d == 0;
-}
-
-// k8s.io/apimachinery v0.29.1 util/validation (IsQualifiedName / IsValidLabelValue)
-__device__ __forceinline__ bool qn_char(uint8_t c) {
-  return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9');
-}
-__device__ bool name_part_ok(const uint8_t* s, int n) {
-  if (n == 0 || n > 63 || !qn_char(s[0]) || !qn_char(s[n - 1])) return false;
-  for (int i = 0; i < n; ++i)
-    if (!(qn_char(s[i]) || s[i] == '-' || s[i] == '_' || s[i] == '.')) return false;
-  return true;
-}
-__device__ bool dns1123_subdomain_ok(const uint8_t* s, int n) {
-  if (n == 0 || n > 253) return false;
-  int start = 0;
-  for (int i = 0; i <= n; ++i) {
-    if (i == n || s[i] == '.') {
-      if (i == start) return false;
-      start = i + 1;
-      continue;
-    }
-    const uint8_t c = s[i];
-    const bool an = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9');
-    if (!(an || (c == '-' && i != start && i + 1 < n && s[i + 1] != '.'))) return false;
-  }
-  return true;
-}
-__device__ bool qualified_name_ok(const uint8_t* s, int n) {
-  int slash = -1;
-  for (int i = 0; i < n; ++i)
-    if (s[i] == '/') {
-      if (slash >= 0) return false;
-      slash = i;
-    }
-  if (slash < 0) return name_part_ok(s, n);
-  return dns1123_subdomain_ok(s, slash) && name_part_ok(s + slash + 1, n - slash - 1);
-}
-
-__device__ bool pat_match(const KpePat& pt, const uint8_t* pb, const uint8_t* s, int sn) {
-  const uint8_t* lit = pb + pt.off;
-  const int ln = (int)pt.len;
-  switch (pt.kind) {
-    case PK_ANY: return true;
-    case PK_EXACT: return sn == ln && bytes_eq(lit, s, ln);
-    case PK_PREFIX: return sn >= ln && bytes_eq(lit, s, ln);
-    case PK_SUFFIX: return sn >= ln && bytes_eq(lit, s + sn - ln, ln);
-    case PK_CONTAINS:
-      for (int i = 0; i + ln <= sn; ++i)
-        if (bytes_eq(lit, s + i, ln)) return true;
-      return false;
-    case PK_QNAME: return qualified_name_ok(s, sn);
-    case PK_LABVAL: return sn == 0 || name_part_ok(s, sn);
-    default: return glob(lit, ln, s, sn);
-  }
-}
+#include "strmatch.inl"
 
 // Wave-uniform table read: the address is uniform, so this is a scalar (SMEM) load
 // through the constant cache — no LDS round trip and no readfirstlane to branch on it.
@@ -1038,320 +936,21 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
 // ===========================================================================
 // Pattern rules: validate.MatchPattern over the document tape
 // (pkg/engine/validate/validate.go:15-261, anchor/handlers.go:31-275, pattern/pattern.go).
-// One lane per resource walks the compiled pattern (program.cpp pc::PatCompiler) against
+// One lane per resource runs the compiled pattern (program.cpp pc::PatCompiler) against
 // its document nodes; cells the scan kernel marked KPE_PENDING_ (rule matched) are
 // resolved to pass / fail / error / skip. Only the class of the error a subtree returns
-// and whether its path is empty matter for the verdict, so that is all a call returns.
+// and whether its path is empty decide the verdict, so that is all a subtree reports.
+// The reference's recursion is an explicit per-lane frame stack (no calls, so no spilled
+// call frames and no callee register budget): a frame is a map validated member by
+// member, or an array validated element by element; scalar leaves resolve in place.
 // ===========================================================================
 namespace {
-constexpr uint32_t PE_OK = 0, PE_SKIP = 1, PE_NEG = 2, PE_OTHER = 3, PE_OTHER_NOPATH = 4;
-constexpr uint32_t kNoNode = 0xFFFFFFFFu;
-constexpr int kPatDepth = 13;  // program.cpp kMaxDepth + 1
-
-struct PatLane {
-  const uint2* doc;   // this resource's nodes (root = 0)
-  uint32_t reg, val;  // AnchorMap: slots registered / found in the resource
-};
-
-__device__ __forceinline__ uint32_t nd_skip(uint2 n) { return 1u + (DN_KIND(n.x) != DN_SCALAR ? n.y : 0u); }
-
-// last member named key1 (Go map decode keeps the last duplicate); kNoNode if absent
-__device__ uint32_t pat_lookup(const uint2* doc, uint32_t m, uint32_t key1) {
-  uint32_t found = kNoNode;
-  if (key1 == 0u) return found;
-  const uint32_t end = m + 1u + doc[m].y;
-  for (uint32_t c = m + 1u; c < end;) {
-    const uint2 n = doc[c];
-    if (DN_KEY(n.x) == key1) found = c;
-    c += nd_skip(n);
-  }
-  return found;
-}
-// ExpandInMetadata: first string member whose name matches the glob (bitset over D_KEY)
-__device__ uint32_t pat_lookup_glob(const PatArgs& a, const uint2* doc, uint32_t m, uint32_t loc) {
-  const uint32_t end = m + 1u + doc[m].y;
-  for (uint32_t c = m + 1u; c < end;) {
-    const uint2 n = doc[c];
-    const uint32_t k1 = DN_KEY(n.x);
-    if (k1 && DN_KIND(n.x) == DN_SCALAR && SC_TYPE(a.scal[n.y].flags) == SC_T_STR &&
-        ((a.pbuf[loc + ((k1 - 1u) >> 5)] >> ((k1 - 1u) & 31u)) & 1u))
-      return c;
-    c += nd_skip(n);
-  }
-  return kNoNode;
-}
-
-__device__ __forceinline__ int qcmp(uint32_t vneg, uint64_t vlo, uint64_t vhi, int64_t ve, uint32_t pneg,
-                                    uint64_t plo, uint64_t phi, int64_t pe) {
-  typedef unsigned __int128 u128;
-  const u128 vm = ((u128)vhi << 64) | vlo, pm = ((u128)phi << 64) | plo;
-  const int sv = vm == 0 ? 0 : (vneg ? -1 : 1), sp = pm == 0 ? 0 : (pneg ? -1 : 1);
-  if (sv != sp) return sv < sp ? -1 : 1;
-  if (sv == 0) return 0;
-  int dv = 0, dp = 0;
-  for (u128 t = vm; t; t /= 10) ++dv;
-  for (u128 t = pm; t; t /= 10) ++dp;
-  int mag;
-  if ((int64_t)dv + ve != (int64_t)dp + pe) {
-    mag = (int64_t)dv + ve < (int64_t)dp + pe ? -1 : 1;
-  } else {
-    u128 x = vm, y = pm;
-    for (; dv < dp; ++dv) x *= 10;
-    for (; dp < dv; ++dp) y *= 10;
-    mag = x == y ? 0 : (x < y ? -1 : 1);
-  }
-  return sv > 0 ? mag : -mag;
-}
-__device__ __forceinline__ bool op_holds(uint32_t op, int c) {
-  switch (op) {
-    case PC_EQ: return c == 0;
-    case PC_NE: return c != 0;
-    case PC_GT: return c > 0;
-    case PC_LT: return c < 0;
-    case PC_GE: return c >= 0;
-    default: return c <= 0;  // PC_LE
-  }
-}
-// validateString (pattern.go:201-305): duration, then quantity, then wildcard string compare
-__device__ bool pat_cond(const PatArgs& a, const KpeScalar& v, const KpeCond& cd) {
-  const uint32_t op = PC_OP(cd.op);
-  if ((cd.op & PC_DUR) && (v.flags & SC_DUR)) return op_holds(op, v.dur < cd.dur ? -1 : (v.dur > cd.dur ? 1 : 0));
-  if ((cd.op & PC_QTY) && (v.flags & SC_QTY))
-    return op_holds(op, qcmp(v.flags & SC_QNEG, v.qlo, v.qhi, v.qexp, cd.op & PC_QNEG, cd.qlo, cd.qhi, cd.qexp));
-  if (op != PC_EQ && op != PC_NE) return false;
-  if (!(v.flags & SC_TEXT)) return false;
-  const bool m = pat_match(a.pats[cd.pat], a.pat_bytes, a.scal_text + v.text_off, (int)v.text_len);
-  return op == PC_NE ? !m : m;
-}
-__device__ __forceinline__ int64_t go_f2i(double f) {
-  return (f >= -9223372036854775808.0 && f < 9223372036854775808.0) ? (int64_t)f : INT64_MIN;
-}
-// pattern.Validate (pattern.go:26-50) of scalar `sid` (or of a map / array when sid is kNoNode)
-__device__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li) {
-  const KpeLeaf L = a.leaves[li];
-  if (sid == kNoNode) return false;  // map / array value: no scalar validator accepts it
-  const KpeScalar v = a.scal[sid];
-  const uint32_t t = SC_TYPE(v.flags);
-  switch (L.type) {
-    case PL_BOOL: return t == SC_T_BOOL && ((v.flags & SC_BTRUE) != 0u) == (L.bval != 0u);
-    case PL_INT:
-      if (t == SC_T_INT) return v.ival == L.ival;
-      if (t == SC_T_FLOAT) return v.fval == trunc(v.fval) && go_f2i(v.fval) == L.ival;
-      if (t == SC_T_STR) return (v.flags & SC_PINT) && v.ival == L.ival;
-      return false;
-    case PL_FLOAT:
-      if (t == SC_T_INT) return L.fval == trunc(L.fval) && go_f2i(L.fval) == v.ival;
-      if (t == SC_T_FLOAT) return v.fval == L.fval;
-      if (t == SC_T_STR) return (v.flags & SC_PFLOAT) && v.fval == L.fval;
-      return false;
-    case PL_NIL:
-      switch (t) {
-        case SC_T_NULL: return true;
-        case SC_T_BOOL: return !(v.flags & SC_BTRUE);
-        case SC_T_INT: return v.ival == 0;
-        case SC_T_FLOAT: return v.fval == 0.0;
-        default: return v.text_len == 0u;
-      }
-    case PL_STR: {
-      if (t == SC_T_STR && pat_match(a.pats[L.exact], a.pat_bytes, a.scal_text + v.text_off, (int)v.text_len))
-        return true;  // value == pattern
-      bool group = true;  // OR over `|` alternatives of AND over `&` terms
-      for (uint32_t i = L.c0, e = L.c0 + L.nc; i < e; ++i) {
-        const KpeCond cd = a.conds[i];
-        if ((cd.op & PC_NEWGROUP) && i != L.c0) {
-          if (group) return true;
-          group = true;
-        }
-        bool r = group && pat_cond(a, v, cd);
-        if (cd.op & PC_OR2) {  // NotInRange: `< lo` OR `> hi`
-          ++i;
-          r = group && (r || pat_cond(a, v, a.conds[i]));
-        }
-        group = group && r;
-      }
-      return group;
-    }
-    default: return false;
-  }
-}
-// scalar id of node c (kNoNode for maps / arrays); an absent member is null
-__device__ __forceinline__ uint32_t node_sid(const uint2* doc, uint32_t c) {
-  if (c == kNoNode) return SC_NULL_ID;
-  const uint2 n = doc[c];
-  return DN_KIND(n.x) == DN_SCALAR ? n.y : kNoNode;
-}
-
-template <int D>
-__device__ __noinline__ uint32_t pat_element(const PatArgs& a, PatLane& L, uint32_t r, uint32_t pn);
-
-template <>
-__device__ __noinline__ uint32_t pat_element<0>(const PatArgs&, PatLane&, uint32_t, uint32_t) {
-  return PE_OTHER;  // unreachable: the compiler bounds pattern depth
-}
-
-// validateResourceElement (validate.go:71-114) + validateMap / validateArray
-template <int D>
-__device__ __noinline__ uint32_t pat_element(const PatArgs& a, PatLane& L, uint32_t r, uint32_t pi) {
-  const uint2* doc = L.doc;
-  const KpePNode pn = a.nodes[pi];
-  const uint32_t rk = r == kNoNode ? 0xFFu : DN_KIND(doc[r].x);
-  if (pn.kind == PN_LEAF) {
-    if (rk == DN_ARR) {  // a scalar pattern against a list: every element must match
-      const uint32_t end = r + 1u + doc[r].y;
-      for (uint32_t c = r + 1u; c < end; c += nd_skip(doc[c]))
-        if (!pat_leaf(a, node_sid(doc, c), pn.y)) return PE_OTHER;
-      return PE_OK;
-    }
-    return pat_leaf(a, node_sid(doc, r), pn.y) ? PE_OK : PE_OTHER;
-  }
-  if (pn.kind == PN_MAP) {
-    if (rk != DN_MAP) return PE_OTHER;
-    const uint32_t m0 = pn.y, nanch = pn.z & 0xFFFFu, nmem = pn.z >> 16;
-    // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
-    for (uint32_t k = 0; k < nmem; ++k) {
-      const uint4 m = a.members[m0 + k];
-      if (m.x & PMF_SLOT) {
-        const uint32_t bit = 1u << PM_SLOT(m.x);
-        L.reg |= bit;
-        if (pat_lookup(doc, r, m.y) != kNoNode) L.val |= bit;
-      }
-    }
-    uint32_t applied = 0, skips = 0;
-    for (uint32_t k = 0; k < nmem; ++k) {
-      if (k == nanch && applied == 0 && skips > 0) return PE_SKIP;  // every anchor skipped
-      const uint4 m = a.members[m0 + k];
-      const uint32_t c = (m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, r, m.w) : pat_lookup(doc, r, m.y);
-      uint32_t e = PE_OK;
-      switch (PM_HANDLER(m.x)) {
-        case PM_COND:
-          e = c == kNoNode ? PE_SKIP : (pat_element<D - 1>(a, L, c, m.z) != PE_OK ? PE_SKIP : PE_OK);
-          break;
-        case PM_GLOBAL:
-          e = c == kNoNode ? PE_OK : (pat_element<D - 1>(a, L, c, m.z) != PE_OK ? PE_SKIP : PE_OK);
-          break;
-        case PM_EQ: e = c == kNoNode ? PE_OK : pat_element<D - 1>(a, L, c, m.z); break;
-        case PM_NEG: e = c == kNoNode ? PE_OK : PE_NEG; break;
-        case PM_EXIST: {
-          if (c == kNoNode) break;
-          if (DN_KIND(doc[c].x) != DN_ARR) {
-            e = PE_OTHER;
-            break;
-          }
-          const KpePNode xl = a.nodes[m.z];
-          if (xl.kind != PN_EXLIST) {
-            e = PE_OTHER;
-            break;
-          }
-          const uint32_t end = c + 1u + doc[c].y;
-          for (uint32_t j = 0; j < xl.z && e == PE_OK; ++j) {  // each pattern map needs one element
-            const uint32_t pj = a.lists[xl.y + j];
-            if (a.nodes[pj].kind == PN_BAD) {
-              e = PE_OTHER;
-              break;
-            }
-            bool found = false;
-            for (uint32_t q = c + 1u; q < end && !found; q += nd_skip(doc[q]))
-              found = pat_element<D - 1>(a, L, q, pj) == PE_OK;
-            if (!found) e = PE_OTHER;
-          }
-          break;
-        }
-        default:  // defaultHandler
-          if (m.x & PMF_STAR) e = (c != kNoNode && node_sid(doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
-          else e = pat_element<D - 1>(a, L, c, m.z);
-          break;
-      }
-      if (k < nanch) {  // anchors: skips are counted, other errors end the map
-        if (e == PE_SKIP) {
-          ++skips;
-          continue;
-        }
-        if (e != PE_OK) return e;
-        ++applied;
-      } else if (e != PE_OK) {
-        return e;
-      }
-    }
-    if (nmem == nanch && applied == 0 && skips > 0) return PE_SKIP;
-    return PE_OK;
-  }
-  // arrays
-  if (rk != DN_ARR) return PE_OTHER;
-  const uint32_t end = r + 1u + doc[r].y;
-  switch (pn.kind) {
-    case PN_ARR_EMPTY: return PE_OTHER;
-    case PN_ARR_LEAF:
-      for (uint32_t c = r + 1u; c < end; c += nd_skip(doc[c]))
-        if (!pat_leaf(a, node_sid(doc, c), pn.y)) return PE_OTHER;
-      return PE_OK;
-    case PN_ARR_MAPS: {
-      uint32_t applied = 0, skips = 0;
-      for (uint32_t c = r + 1u; c < end; c += nd_skip(doc[c])) {
-        const uint32_t e = pat_element<D - 1>(a, L, c, pn.y);
-        if (e == PE_SKIP) ++skips;
-        else if (e != PE_OK) return e;
-        else ++applied;
-      }
-      return (applied == 0 && skips > 0) ? PE_SKIP : PE_OK;
-    }
-    default: {  // PN_ARR_POS: positional, after a length check whose error has an empty path
-      uint32_t len = 0;
-      for (uint32_t c = r + 1u; c < end; c += nd_skip(doc[c])) ++len;
-      if (len < pn.z) return PE_OTHER_NOPATH;
-      uint32_t applied = 0, skips = 0, c = r + 1u;
-      for (uint32_t j = 0; j < pn.z; ++j, c += nd_skip(doc[c])) {
-        const uint32_t e = pat_element<D - 1>(a, L, c, a.lists[pn.y + j]);
-        if (e == PE_SKIP) ++skips;
-        else if (e != PE_OK) return e;
-        else ++applied;
-      }
-      return (applied == 0 && skips > 0) ? PE_SKIP : PE_OK;
-    }
-  }
-}
-
-// validate.MatchPattern (validate.go:31-56) -> verdict of a single pattern:
-// pass / skip / fail (error when the PatternError path is empty)
-__device__ uint32_t pat_match_root(const PatArgs& a, const uint2* doc, uint32_t root) {
-  PatLane L{doc, 0u, 0u};
-  const uint32_t e = pat_element<kPatDepth>(a, L, 0u, a.roots[2 * root]);
-  if (e == PE_OK) return KPE_PASS_;
-  if (e == PE_SKIP) return KPE_SKIP_;
-  if (e == PE_NEG) return KPE_FAIL_;
-  if (e == PE_OTHER_NOPATH || (L.reg & ~L.val)) return KPE_ERROR_;  // AnchorMap.KeysAreMissing
-  return KPE_FAIL_;
-}
+#include "patvm.inl"
 }  // namespace
 
 __global__ void __launch_bounds__(256) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
-  const PatArgs& a = *ap;
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= a.n) return;
-  const uint2* doc = reinterpret_cast<const uint2*>(a.doc) + a.doc_off[r];
-  uint8_t* row = a.verdicts + (size_t)r * a.R;
-  for (uint32_t i = 0; i < a.npr; ++i) {
-    const KpePatRule pr = a.rules[i];
-    if (row[pr.col] != KPE_PENDING_) continue;
-    uint32_t v;
-    if (!(pr.flags & PR_ANY)) {
-      v = pat_match_root(a, doc, pr.r0);
-      if (v == KPE_ERROR_) v = KPE_ERROR_;
-    } else if (pr.flags & PR_ANY_BAD) {
-      v = KPE_ERROR_;
-    } else {  // validatePatterns anyPattern (validate_resource.go:339-398)
-      uint32_t fails = 0, skips = 0;
-      v = KPE_PASS_;
-      bool passed = false;
-      for (uint32_t k = 0; k < pr.nr && !passed; ++k) {
-        const uint32_t x = pat_match_root(a, doc, pr.r0 + k);
-        if (x == KPE_PASS_) passed = true;
-        else if (x == KPE_SKIP_) ++skips;
-        else ++fails;  // an empty-path error counts as a failure here
-      }
-      if (!passed) v = fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_);
-    }
-    row[pr.col] = (uint8_t)v;
-  }
+  if (r < ap->n) pat_eval_row(*ap, r);
 }
 
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s) {

@@ -173,4 +173,8 @@ struct PatArgs {
   const KpePatRule* rules;
   const uint32_t* pbuf;            // glob member-name bitsets (HBM)
   uint8_t* verdicts;
+  // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)
+  uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
+  uint64_t nscal, ndoc;
+  uint32_t* err;
 };

@@ -18,6 +18,7 @@
 #include "../../include/kpe.h"
 #include "corpus.hpp"
 #include "kernels_abi.h"
+#include "patclass.hpp"
 #include "program.hpp"
 
 namespace kpe {
@@ -95,13 +96,13 @@ struct kpe_device {
   std::mutex mu;
   bool timing = false;
   struct EvPair {
-    hipEvent_t a, b, c;
+    hipEvent_t a, b, c, d;
     double bytes;
   };
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
   uint64_t launches = 0;
-  double pss_ms = 0, dict_ms = 0, last_bytes = 0;
+  double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0;
   hipEvent_t get_ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -136,7 +137,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf zero_page;    // 256 zero bytes (loads of columns a program does not read)
   DevBuf fuse;         // fused dictionary pass image (pairs, patterns, small dictionaries)
   uint32_t fuse_lds = 0, fuse_words = 0, npairs = 0, fuse_pats = 0, fuse_patb = 0;
-  DevBuf pmembers, pargs;  // pattern rules: resolved members, device copy of PatArgs
+  DevBuf pmembers, pargs, perr;  // pattern rules: resolved members, PatArgs copy, check flags
   bool pargs_valid = false;
   ScanArgs hargs{};    // what dargs holds
   bool args_valid = false;
@@ -205,6 +206,7 @@ void kpe_device_close(kpe_device* d) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
     (void)hipEventDestroy(p.c);
+    (void)hipEventDestroy(p.d);
   }
   for (auto e : d->pool) (void)hipEventDestroy(e);
   (void)hipStreamDestroy(d->stream);
@@ -320,30 +322,6 @@ namespace {
 
 // go-wildcard pattern -> device pattern class (the literal is stored; only a
 // '?' or an inner '*' needs the general backtracking matcher).
-KpePat classify_pattern(const std::string& g, std::vector<uint8_t>& bytes) {
-  KpePat p{PK_GLOB, (uint32_t)bytes.size(), 0, 0};
-  auto put = [&](const std::string& lit) {
-    p.off = (uint32_t)bytes.size();
-    p.len = (uint32_t)lit.size();
-    bytes.insert(bytes.end(), lit.begin(), lit.end());
-  };
-  size_t stars = std::count(g.begin(), g.end(), '*');
-  bool q = g.find('?') != std::string::npos;
-  if (g == "*") p.kind = PK_ANY;
-  else if (!q && stars == 0) p.kind = PK_EXACT;
-  else if (!q && stars == 1 && g.back() == '*') p.kind = PK_PREFIX;
-  else if (!q && stars == 1 && g.front() == '*') p.kind = PK_SUFFIX;
-  else if (!q && stars == 2 && g.size() >= 2 && g.front() == '*' && g.back() == '*') p.kind = PK_CONTAINS;
-  switch (p.kind) {
-    case PK_ANY: put(""); break;
-    case PK_EXACT: put(g); break;
-    case PK_PREFIX: put(g.substr(0, g.size() - 1)); break;
-    case PK_SUFFIX: put(g.substr(1)); break;
-    case PK_CONTAINS: put(g.substr(1, g.size() - 2)); break;
-    default: put(g);
-  }
-  return p;
-}
 
 template <class T>
 void append_words(std::vector<uint32_t>& img, const std::vector<T>& v, uint32_t* off) {
@@ -426,7 +404,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
         pp.push_back({PK_EXACT, (uint32_t)pb.size(), (uint32_t)PP.operands[i].size(), 0});
         pb.insert(pb.end(), PP.operands[i].begin(), PP.operands[i].end());
       } else {
-        pp.push_back(classify_pattern(PP.operands[i], pb));
+        pp.push_back(kpe::classify_pattern(PP.operands[i], pb));
       }
     }
     hipStream_t s0 = dev->stream;
@@ -447,7 +425,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
       D.pats_h.push_back({PK_QNAME, 0, 0, 0});
     else if (pr.special == PRED_SPECIAL_LABVAL)
       D.pats_h.push_back({PK_LABVAL, 0, 0, 0});
-    for (auto& g : pr.globs) D.pats_h.push_back(classify_pattern(g, D.pat_bytes_h));
+    for (auto& g : pr.globs) D.pats_h.push_back(kpe::classify_pattern(g, D.pat_bytes_h));
   }
   HIPCHK(upload(D.rules, P.rules, s));
   HIPCHK(upload(D.rule_lanes, lanes, s));
@@ -729,6 +707,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     ev.a = dev->get_ev();
     ev.b = dev->get_ev();
     ev.c = dev->get_ev();
+    ev.d = dev->get_ev();
     HIPCHK(hipEventRecord(ev.a, s));
   }
   const size_t R = P.rules.size();
@@ -840,6 +819,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.scan_blocks,
                          B.dyn_bytes, s));
+  if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
   if (!P.pat.rules.empty()) {
     if (!B.pargs_valid) {
       PatArgs pa{};
@@ -861,15 +841,29 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.rules = PD.prules.as<KpePatRule>();
       pa.pbuf = B.pbuf.as<uint32_t>();
       pa.verdicts = B.verdicts.as<uint8_t>();
+      pa.nnodes = (uint32_t)P.pat.nodes.size(), pa.nmembers = (uint32_t)(P.pat.members.size() / 4);
+      pa.nlists = (uint32_t)P.pat.lists.size(), pa.nleaves = (uint32_t)P.pat.leaves.size();
+      pa.nconds = (uint32_t)P.pat.conds.size(), pa.npats = (uint32_t)P.pat.operands.size();
+      pa.nroots = (uint32_t)P.pat.roots.size(), pa.npbuf = (uint32_t)(B.pbuf.bytes / 4);
+      pa.nscal = C.scal.size(), pa.ndoc = C.doc.size() / 2;
+      HIPCHK(B.perr.ensure(4));
+      HIPCHK(hipMemsetAsync(B.perr.p, 0, 4, s));
+      pa.err = B.perr.as<uint32_t>();
       HIPCHK(B.pargs.ensure(sizeof(PatArgs)));
       HIPCHK(hipMemcpyAsync(B.pargs.p, &pa, sizeof(PatArgs), hipMemcpyHostToDevice, s));
       HIPCHK(hipStreamSynchronize(s));
       B.pargs_valid = true;
     }
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, s));
+    if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
+      uint32_t e = 0;
+      HIPCHK(hipMemcpyAsync(&e, B.perr.p, 4, hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      fprintf(stderr, "kpe patvm err=0x%x\n", e);
+    }
   }
   if (dev->timing) {
-    HIPCHK(hipEventRecord(ev.c, s));
+    HIPCHK(hipEventRecord(ev.d, s));
     ev.bytes = scan_bytes(P, C, B.need, masks);
     dev->pending.push_back(ev);
   }
@@ -975,25 +969,29 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
   HIPCHK(hipSetDevice(dev->ordinal));
   HIPCHK(hipStreamSynchronize(dev->stream));
   for (auto& p : dev->pending) {
-    float d1 = 0, d2 = 0;
+    float d1 = 0, d2 = 0, d3 = 0;
     HIPCHK(hipEventElapsedTime(&d1, p.a, p.b));
     HIPCHK(hipEventElapsedTime(&d2, p.b, p.c));
+    HIPCHK(hipEventElapsedTime(&d3, p.c, p.d));
     dev->dict_ms += d1;
     dev->pss_ms += d2;
+    dev->pat_ms += d3;
     dev->last_bytes = p.bytes;
     dev->launches++;
     dev->pool.push_back(p.a);
     dev->pool.push_back(p.b);
     dev->pool.push_back(p.c);
+    dev->pool.push_back(p.d);
   }
   dev->pending.clear();
   out->launches = dev->launches;
   out->pss_kernel_ms = dev->pss_ms;
   out->dict_kernel_ms = dev->dict_ms;
   out->scan_bytes = dev->last_bytes;
+  out->pattern_kernel_ms = dev->pat_ms;
   if (reset) {
     dev->launches = 0;
-    dev->pss_ms = dev->dict_ms = 0;
+    dev->pss_ms = dev->dict_ms = dev->pat_ms = 0;
   }
   return KPE_OK;
 }

@@ -700,7 +700,7 @@ class PatCompiler {
     goval::Quantity q;
     if (goval::parse_quantity(operand_text, &q)) {
       c.op |= PC_QTY | (q.neg ? PC_QNEG : 0u);
-      c.qlo = (uint64_t)q.m, c.qhi = (uint64_t)(q.m >> 64), c.qexp = q.e;
+      goval::qty_key(q, &c.qexp, &c.qlo, &c.qhi);
     }
     PP.conds.push_back(c);
   }

@@ -374,7 +374,7 @@ typedef struct KpeRule {
 #define SC_PINT (1u << 3)    // string: strconv.ParseInt ok -> ival
 #define SC_PFLOAT (1u << 4)  // string: strconv.ParseFloat ok -> fval
 #define SC_DUR (1u << 5)     // convertNumberToString(v) parses as a duration -> dur
-#define SC_QTY (1u << 6)     // ... as a quantity -> (qneg, qlo/qhi, qexp)
+#define SC_QTY (1u << 6)     // ... as a quantity -> comparison key (QNEG, qexp = order, qlo/qhi)
 #define SC_QNEG (1u << 7)
 #define SC_TEXT (1u << 8)    // compareString text valid: text pool [text_off, +text_len)
 #define SC_BTRUE (1u << 9)
@@ -383,8 +383,8 @@ typedef struct KpeScalar {
   int64_t ival;
   double fval;
   int64_t dur;
-  int64_t qexp;
-  uint64_t qlo, qhi;
+  int64_t qexp;       // quantity comparison key (goval::qty_key): order (digits + exponent)
+  uint64_t qlo, qhi;  // ... and the mantissa left-aligned to 38 digits
 } KpeScalar;  // 64 bytes
 
 // ---- compiled patterns -------------------------------------------------------------------

@@ -18,7 +18,7 @@ def main():
     eng = K.Engine(ordinal=0)
     corpora = []
     for k in range(4):
-        c = K.Corpus(K.synth_resources(0xC2, n, mix=0, first_index=k * n))
+        c = K.Corpus(K.synth_resources(0xC2, n, mix=0, first_index=k * n), docs=False)
         c.upload(eng.device)
         corpora.append(c)
     ps = K.PolicySet([restricted_latest()])

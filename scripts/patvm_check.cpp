@@ -1,0 +1,136 @@
+// Host build of the pattern VM (kyverno_amd/csrc/patvm.inl + strmatch.inl, the exact text
+// kpe_pattern_kernel runs) for sanitizer runs without a GPU:
+//   make -C scripts patvm_check && scripts/build/patvm_check policies.json resources.ndjson out.bin
+// Flattens the resources with document tapes, compiles the policies, binds the pattern
+// program the way kpe_api.cpp does (member names -> D_KEY ids, glob names -> bitsets,
+// operand records) and evaluates every pattern cell as if the rule matched. Writes the
+// N x R verdict bytes (non-pattern columns 0) to out.bin.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#define __device__
+#define __forceinline__ inline
+#define KPE_PATVM_CHECK 1
+struct uint2 {
+  uint32_t x, y;
+};
+struct uint4 {
+  uint32_t x, y, z, w;
+};
+using std::trunc;
+
+#include "../kyverno_amd/csrc/corpus.hpp"
+#include "../kyverno_amd/csrc/kernels_abi.h"
+#include "../kyverno_amd/csrc/patclass.hpp"
+#include "../kyverno_amd/csrc/program.hpp"
+#include "../kyverno_amd/csrc/schema.h"
+
+namespace kpe {
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs);
+}
+
+namespace {
+#include "../kyverno_amd/csrc/strmatch.inl"
+#include "../kyverno_amd/csrc/patvm.inl"
+}  // namespace
+
+static std::string slurp(const char* p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) throw std::runtime_error(std::string("cannot read ") + p);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    fprintf(stderr, "usage: %s policies.json resources.ndjson out.bin\n", argv[0]);
+    return 2;
+  }
+  const std::string pj = slurp(argv[1]), nd = slurp(argv[2]);
+  kpe::Corpus C;
+  kpe::flatten_ndjson(C, nd.data(), nd.size(), nullptr, 0, true);
+  auto P = kpe::compile_policies(pj.data(), pj.size());
+  const auto& PP = P->pat;
+  // tape invariants: every subtree inside its resource, scalar ids in range, names valid
+  for (int64_t r = 0; r < C.n; ++r) {
+    const uint64_t b = C.doc_off[r], e = C.doc_off[r + 1];
+    for (uint64_t i = b; i < e; ++i) {
+      const uint32_t x = C.doc[2 * i], y = C.doc[2 * i + 1];
+      if (DN_KIND(x) == DN_SCALAR ? y >= C.scal.size() : i + 1 + y > e) {
+        fprintf(stderr, "bad node %llu of resource %lld\n", (unsigned long long)i, (long long)r);
+        return 1;
+      }
+      if (DN_KEY(x) > C.dict[D_KEY].size()) {
+        fprintf(stderr, "bad member name at node %llu\n", (unsigned long long)i);
+        return 1;
+      }
+    }
+  }
+  // bind: operand records, member names, glob bitsets (host copies of the device tables)
+  std::vector<uint8_t> pb;
+  std::vector<KpePat> pats;
+  for (size_t i = 0; i < PP.operands.size(); ++i) {
+    if (PP.operand_exact[i]) {
+      pats.push_back({PK_EXACT, (uint32_t)pb.size(), (uint32_t)PP.operands[i].size(), 0});
+      pb.insert(pb.end(), PP.operands[i].begin(), PP.operands[i].end());
+    } else {
+      pats.push_back(kpe::classify_pattern(PP.operands[i], pb));
+    }
+  }
+  pb.push_back(0);
+  std::vector<uint32_t> pbuf;
+  std::vector<uint4> mem(PP.members.size() / 4);
+  const auto& K = C.dict[D_KEY];
+  for (size_t i = 0; i < mem.size(); ++i) {
+    uint4 m{PP.members[4 * i], PP.members[4 * i + 1], PP.members[4 * i + 2], PP.members[4 * i + 3]};
+    const int64_t id = K.find(PP.keys[m.y]);
+    m.y = id < 0 ? 0u : (uint32_t)id + 1u;
+    if (m.x & PMF_GLOB) {
+      const auto& pr = P->preds[m.w];
+      m.w = (uint32_t)pbuf.size();
+      pbuf.resize(pbuf.size() + (K.size() + 31) / 32 + 1, 0u);
+      for (uint32_t s = 0; s < K.size(); ++s) {
+        const auto str = K.at(s);
+        bool hit = false;
+        for (auto& g : pr.globs)
+          hit = hit || glob(reinterpret_cast<const uint8_t*>(g.data()), (int)g.size(),
+                            reinterpret_cast<const uint8_t*>(str.data()), (int)str.size());
+        if (hit) pbuf[m.w + (s >> 5)] |= 1u << (s & 31u);
+      }
+    }
+    mem[i] = m;
+  }
+  const uint32_t R = (uint32_t)P->rules.size();
+  std::vector<uint8_t> verdicts((size_t)C.n * R, 0);
+  for (int64_t r = 0; r < C.n; ++r)
+    for (auto& pr : PP.rules) verdicts[(size_t)r * R + pr.col] = KPE_PENDING_;
+  std::vector<KpeScalar> scal(C.scal);
+  std::vector<uint8_t> text(C.scal_text.begin(), C.scal_text.end());
+  text.push_back(0);
+  PatArgs a{};
+  a.n = C.n, a.R = R, a.npr = (uint32_t)PP.rules.size();
+  a.doc = C.doc.data(), a.doc_off = C.doc_off.data(), a.scal = scal.data(), a.scal_text = text.data();
+  a.nodes = PP.nodes.data(), a.members = mem.data(), a.lists = PP.lists.data(), a.leaves = PP.leaves.data();
+  a.conds = PP.conds.data(), a.pats = pats.data(), a.pat_bytes = pb.data(), a.roots = PP.roots.data();
+  a.rules = PP.rules.data(), a.pbuf = pbuf.data(), a.verdicts = verdicts.data();
+  uint32_t err = 0;
+  a.nnodes = (uint32_t)PP.nodes.size(), a.nmembers = (uint32_t)mem.size(), a.nlists = (uint32_t)PP.lists.size();
+  a.nleaves = (uint32_t)PP.leaves.size(), a.nconds = (uint32_t)PP.conds.size(), a.npats = (uint32_t)pats.size();
+  a.nroots = (uint32_t)PP.roots.size(), a.npbuf = (uint32_t)pbuf.size(), a.nscal = scal.size();
+  a.ndoc = C.doc.size() / 2, a.err = &err;
+  for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r);  // kpe_pattern_kernel's lane body
+  FILE* f = fopen(argv[3], "wb");
+  fwrite(verdicts.data(), 1, verdicts.size(), f);
+  fclose(f);
+  printf("%lld %u err=0x%x\n", (long long)C.n, R, err);
+  if (err) return 1;
+  return 0;
+}
