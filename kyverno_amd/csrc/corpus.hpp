@@ -66,8 +66,8 @@ struct Corpus {
 
   // ---- generic document tape + scalar table (pattern rules; schema.h DN_* / KpeScalar) ----
   bool has_docs = false;
-  std::vector<uint32_t> doc;          // 2 words per node
-  std::vector<uint64_t> doc_off{0};   // node offset of each resource
+  std::vector<uint32_t> doc;          // 2 words per entry (schema.h DN_*)
+  std::vector<uint64_t> doc_off;      // root entry (absolute tape index) of each resource
   std::vector<KpeScalar> scal;        // scalar table (ids 0/1/2 = null/false/true)
   std::vector<char> scal_text;        // compareString texts
   std::unordered_map<std::string, uint32_t> scal_str;

@@ -1119,9 +1119,10 @@ class DocBuilder {
   }
   void add(const char* b, const char* e) {
     JCur c(b, e);
-    value(c, 0, 0);
+    const uint64_t root = value(c, 0, 0);
     if (!c.ok()) throw std::invalid_argument("malformed resource JSON");
-    C.doc_off.push_back(C.doc.size() / 2);
+    put(root);
+    C.doc_off.push_back(C.doc.size() / 2 - 1);  // the resource's root entry
   }
 
  private:
@@ -1176,85 +1177,81 @@ class DocBuilder {
     scalar_attrs(e, v);
     return C.scal_str[k] = push_scalar(e);
   }
-  void node(uint32_t kind, uint32_t key1, uint32_t y) {
-    C.doc.push_back(kind | (key1 << 2));
-    C.doc.push_back(y);
+  static uint64_t entry(uint32_t kind, uint32_t key1, uint32_t y) {
+    return (uint64_t)(kind | (key1 << 2)) | ((uint64_t)y << 32);
   }
-  // rewrite the members of the map at node `at` (the tape's last subtree) keeping only the
-  // last member of each name
-  void drop_duplicates(size_t at) {
-    const size_t end = C.doc.size() / 2;
-    std::vector<std::pair<size_t, size_t>> kids;  // (first node, node count)
-    for (size_t i = at + 1; i < end;) {
-      const uint32_t x = C.doc[2 * i];
-      const size_t len = 1 + (DN_KIND(x) != DN_SCALAR ? C.doc[2 * i + 1] : 0u);
-      kids.emplace_back(i, len);
-      i += len;
-    }
-    std::unordered_map<uint32_t, size_t> last;
-    for (size_t j = 0; j < kids.size(); ++j) last[DN_KEY(C.doc[2 * kids[j].first])] = j;
-    std::vector<uint32_t> out;
-    for (size_t j = 0; j < kids.size(); ++j)
-      if (last[DN_KEY(C.doc[2 * kids[j].first])] == j)
-        out.insert(out.end(), C.doc.begin() + 2 * kids[j].first, C.doc.begin() + 2 * (kids[j].first + kids[j].second));
-    C.doc.resize(2 * (at + 1));
-    C.doc.insert(C.doc.end(), out.begin(), out.end());
+  void put(uint64_t en) {
+    C.doc.push_back((uint32_t)en);
+    C.doc.push_back((uint32_t)(en >> 32));
   }
-  void value(JCur& c, uint32_t key1, int depth) {
-    if (depth > 256) throw LimitError("document nesting deeper than 256");
+  // A container's body: {count, 0} then its member / element entries, contiguous, so a
+  // member lookup reads one short run of independent entries (schema.h DN_*).
+  uint32_t body(std::vector<uint64_t>& kids) {
     const size_t at = C.doc.size() / 2;
+    if (at + 1 + kids.size() > 0xFFFFFFFFull) throw LimitError("document tape exceeds 2^32 entries");
+    put((uint64_t)kids.size());
+    for (uint64_t en : kids) put(en);
+    return (uint32_t)at;
+  }
+  uint64_t value(JCur& c, uint32_t key1, int depth) {
+    if (depth > 256) throw LimitError("document nesting deeper than 256");
     switch (c.peek()) {
-      case JK::Null: c.null(), node(DN_SCALAR, key1, SC_NULL_ID); break;
+      case JK::Null: c.null(); return entry(DN_SCALAR, key1, SC_NULL_ID);
       case JK::Bool: {
         bool b = false;
         c.boolean(&b);
-        node(DN_SCALAR, key1, b ? SC_TRUE_ID : SC_FALSE_ID);
-        break;
+        return entry(DN_SCALAR, key1, b ? SC_TRUE_ID : SC_FALSE_ID);
       }
       case JK::Num: {
         JNum n;
         c.number(&n);
-        node(DN_SCALAR, key1, n.is_int ? int_id(n.i) : float_id(n.f));
-        break;
+        return entry(DN_SCALAR, key1, n.is_int ? int_id(n.i) : float_id(n.f));
       }
       case JK::Str: {
         std::string_view v;
         c.str(&v, scratch);
-        node(DN_SCALAR, key1, str_id(v));
-        break;
+        return entry(DN_SCALAR, key1, str_id(v));
       }
       case JK::Obj: {
-        node(DN_MAP, key1, 0);
         c.obj_begin();
         bool f = true;
         std::string_view k;
         std::string ks;
-        std::vector<uint32_t> names;
+        std::vector<uint64_t> kids;
+        bool dup = false;
         while (c.obj_next(f, &k, ks)) {
           const uint32_t kid = C.dict[D_KEY].intern(k);
           if (kid >= DN_MAX_KEYS) throw LimitError("too many distinct member names");
-          names.push_back(kid);
-          value(c, kid + 1, depth + 1);
+          const uint64_t en = value(c, kid + 1, depth + 1);
+          for (size_t q = 0; q < kids.size() && !dup && kids.size() < 64; ++q)
+            dup = DN_KEY((uint32_t)kids[q]) == kid + 1;
+          kids.push_back(en);
         }
-        if (names.size() > 1) {  // duplicate names: a Go map decode keeps the last one
-          std::vector<uint32_t> sorted(names);
-          std::sort(sorted.begin(), sorted.end());
-          if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end()) drop_duplicates(at);
+        if (kids.size() >= 64 && !dup) {
+          std::vector<uint32_t> names;
+          for (uint64_t en : kids) names.push_back(DN_KEY((uint32_t)en));
+          std::sort(names.begin(), names.end());
+          dup = std::adjacent_find(names.begin(), names.end()) != names.end();
         }
-        C.doc[2 * at + 1] = (uint32_t)(C.doc.size() / 2 - at - 1);
-        break;
+        if (dup) {  // duplicate names: a Go map decode keeps the last one
+          std::unordered_map<uint32_t, size_t> last;
+          for (size_t q = 0; q < kids.size(); ++q) last[DN_KEY((uint32_t)kids[q])] = q;
+          std::vector<uint64_t> kept;
+          for (size_t q = 0; q < kids.size(); ++q)
+            if (last[DN_KEY((uint32_t)kids[q])] == q) kept.push_back(kids[q]);
+          kids.swap(kept);
+        }
+        return entry(DN_MAP, key1, body(kids));
       }
       case JK::Arr: {
-        node(DN_ARR, key1, 0);
         c.arr_begin();
         bool f = true;
-        while (c.arr_next(f)) value(c, 0, depth + 1);
-        C.doc[2 * at + 1] = (uint32_t)(C.doc.size() / 2 - at - 1);
-        break;
+        std::vector<uint64_t> kids;
+        while (c.arr_next(f)) kids.push_back(value(c, 0, depth + 1));
+        return entry(DN_ARR, key1, body(kids));
       }
       default: throw std::invalid_argument("malformed resource JSON");
     }
-    if (C.doc.size() / 2 - at > 0xFFFFFFFFull) throw LimitError("document too large");
   }
 };
 

@@ -4,7 +4,10 @@
 constexpr uint32_t PE_OK = 0, PE_SKIP = 1, PE_NEG = 2, PE_OTHER = 3, PE_OTHER_NOPATH = 4, PE_PUSHED = 8,
                    PE_NONE = 9;
 constexpr uint32_t kNoNode = 0xFFFFFFFFu;
-constexpr int kPatStack = 14;  // program.cpp kMaxDepth (12) + root + 1
+#ifndef KPE_PAT_STACK
+#define KPE_PAT_STACK 14
+#endif
+constexpr int kPatStack = KPE_PAT_STACK;  // program.cpp kMaxDepth (12) + root + 1
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
 
 // Bounds-checked table reads in KPE_PATVM_CHECK builds (scripts/patvm_check.cpp, the
@@ -20,38 +23,59 @@ __device__ __forceinline__ uint32_t pv_fail(const PatArgs& a, uint32_t code) {
   return 0u;
 }
 #define PV(i, n, code) ((uint64_t)(i) < (uint64_t)(n) ? (i) : pv_fail(a, code))
-#define PVD(i) ((uint64_t)(doc - reinterpret_cast<const uint2*>(a.doc)) + (uint64_t)(i) < a.ndoc ? (i) : pv_fail(a, 9))
+#define PVD(i) ((uint64_t)(i) < a.ndoc ? (i) : pv_fail(a, 9))
 #else
 #define PV(i, n, code) (i)
 #define PVD(i) (i)
 #endif
 
-__device__ __forceinline__ uint32_t nd_skip(uint2 n) { return 1u + (DN_KIND(n.x) != DN_SCALAR ? n.y : 0u); }
+// children of container entry e: entries [first, end) of its body
+#define PV_KIDS(e, first, end)                   \
+  const uint32_t first##_b = doc[PVD(e)].y;      \
+  const uint32_t first = first##_b + 1u;         \
+  const uint32_t end = first + doc[PVD(first##_b)].x
 
 // member named key1 (the flattener keeps only the last of duplicate names, as a Go map
 // decode does); kNoNode if absent
 __device__ __forceinline__ uint32_t pat_lookup(const PatArgs& a, const uint2* doc, uint32_t m, uint32_t key1) {
   if (key1 == 0u) return kNoNode;
-  const uint32_t end = m + 1u + doc[PVD(m)].y;
-  for (uint32_t c = m + 1u; c < end;) {
-    const uint2 n = doc[PVD(c)];
-    if (DN_KEY(n.x) == key1) return c;
-    c += nd_skip(n);
+  PV_KIDS(m, c, end);
+  uint32_t i = c;
+  for (; i + 4u <= end; i += 4u) {  // four independent entry loads per step
+    const uint2 n0 = doc[PVD(i)], n1 = doc[PVD(i + 1u)], n2 = doc[PVD(i + 2u)], n3 = doc[PVD(i + 3u)];
+    if (DN_KEY(n0.x) == key1) return i;
+    if (DN_KEY(n1.x) == key1) return i + 1u;
+    if (DN_KEY(n2.x) == key1) return i + 2u;
+    if (DN_KEY(n3.x) == key1) return i + 3u;
   }
+  for (; i < end; ++i)
+    if (DN_KEY(doc[PVD(i)].x) == key1) return i;
   return kNoNode;
 }
 // ExpandInMetadata: first string member whose name matches the glob (bitset over D_KEY)
 __device__ __forceinline__ uint32_t pat_lookup_glob(const PatArgs& a, const uint2* doc, uint32_t m, uint32_t loc) {
-  const uint32_t end = m + 1u + doc[PVD(m)].y;
-  for (uint32_t c = m + 1u; c < end;) {
+  PV_KIDS(m, c0, end);
+  for (uint32_t c = c0; c < end; ++c) {
     const uint2 n = doc[PVD(c)];
     const uint32_t k1 = DN_KEY(n.x);
     if (k1 && DN_KIND(n.x) == DN_SCALAR && SC_TYPE(a.scal[PV(n.y, a.nscal, 7)].flags) == SC_T_STR &&
         ((a.pbuf[PV(loc + ((k1 - 1u) >> 5), a.npbuf, 10)] >> ((k1 - 1u) & 31u)) & 1u))
       return c;
-    c += nd_skip(n);
   }
   return kNoNode;
+}
+
+// compareString / exact-equality match: literal classes inline, contains / glob out of line
+__device__ __forceinline__ bool pv_match(const KpePat pt, const uint8_t* pb, const uint8_t* s, int sn) {
+  const uint8_t* lit = pb + pt.off;
+  const int ln = (int)pt.len;
+  switch (pt.kind) {
+    case PK_ANY: return true;
+    case PK_EXACT: return sn == ln && bytes_eq(lit, s, ln);
+    case PK_PREFIX: return sn >= ln && bytes_eq(lit, s, ln);
+    case PK_SUFFIX: return sn >= ln && bytes_eq(lit, s + sn - ln, ln);
+    default: return pat_match(pt, pb, s, sn);
+  }
 }
 
 // Quantity.Cmp on comparison keys (goval::qty_key): sign, order, 38-digit aligned mantissa
@@ -87,7 +111,7 @@ __device__ __forceinline__ bool pat_cond(const PatArgs& a, const KpeScalar* v, u
     return op_holds(op, qcmp(vf & SC_QNEG, v->qexp, v->qlo, v->qhi, cop & PC_QNEG, cd->qexp, cd->qlo, cd->qhi));
   if (op != PC_EQ && op != PC_NE) return false;
   if (!(vf & SC_TEXT)) return false;
-  const bool m = pat_match(a.pats[PV(cd->pat, a.npats, 6)], a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len);
+  const bool m = pv_match(a.pats[PV(cd->pat, a.npats, 6)], a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len);
   return op == PC_NE ? !m : m;
 }
 __device__ __forceinline__ int64_t go_f2i(double f) {
@@ -120,7 +144,7 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
         default: return v->text_len == 0u;
       }
     case PL_STR: {
-      if (t == SC_T_STR && pat_match(a.pats[PV(L->exact, a.npats, 6)], a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len))
+      if (t == SC_T_STR && pv_match(a.pats[PV(L->exact, a.npats, 6)], a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len))
         return true;  // value == pattern
       bool group = true;  // OR over `|` alternatives of an AND over their `&` terms
       const uint32_t c0 = L->c0, ce = c0 + L->nc;
@@ -159,180 +183,190 @@ struct PFrame {
   uint32_t c;       // MAP existence search: the resource list node
 };
 
-// Every VM member is inlined: a call would receive the lane's private frame stack through a
-// generic pointer, and a flat access into the private aperture from a callee faults.
+// The VM is one loop over three states, so every piece of the walk exists once in the
+// kernel: BEGIN evaluates an element against a pattern node (a leaf resolves at once, a
+// map / array pushes a frame), STEP advances the top frame (it either asks for a BEGIN of
+// the next child or completes), RET hands a completed verdict to the frame below. Lanes of
+// a wave in different states then run each state's code once per iteration instead of
+// every inlined copy. Nothing is called: a callee would reach the lane's private frame
+// stack through a generic pointer, and flat accesses into the private aperture fault.
+constexpr uint32_t VM_BEGIN = 0, VM_STEP = 1, VM_RET = 2;
+
 struct PatVM {
   const PatArgs& a;
-  const uint2* doc;
+  const uint2* doc;   // the whole tape (absolute entry indices)
+  uint32_t root;      // this resource's root entry
   uint32_t reg, val;  // AnchorMap: slots registered / present in the resource
   int sp;
   PFrame st[kPatStack];
 
-  __device__ __forceinline__ uint32_t leaf_all(uint32_t r, uint32_t li) {  // a scalar pattern vs a list
-    const uint32_t end = r + 1u + doc[PVD(r)].y;
-    for (uint32_t c = r + 1u; c < end; c += nd_skip(doc[PVD(c)]))
-      if (!pat_leaf(a, node_sid(a, doc, c), li)) return PE_OTHER;
-    return PE_OK;
+  // validate.MatchPattern (validate.go:31-56) of pattern root node `root_pi`
+  __device__ __forceinline__ uint32_t run(uint32_t root_pi) {
+    sp = -1, reg = 0u, val = 0u;
+    uint32_t state = VM_BEGIN, br = root, bpi = root_pi, v = PE_NONE;
+    for (;;) {
+      if (state == VM_BEGIN) {
+        // ---- validateResourceElement (validate.go:71-114) ----
+        const KpePNode pn = a.nodes[PV(bpi, a.nnodes, 1)];
+        const uint32_t rk = br == kNoNode ? 0xFFu : DN_KIND(doc[PVD(br)].x);
+        state = VM_RET;
+        if (pn.kind == PN_LEAF && rk != DN_ARR) {
+          v = pat_leaf(a, node_sid(a, doc, br), pn.y) ? PE_OK : PE_OTHER;
+        } else if (pn.kind == PN_LEAF || pn.kind == PN_ARR_LEAF) {  // scalar pattern vs a list
+          if (rk != DN_ARR) {
+            v = PE_OTHER;
+          } else {
+            PV_KIDS(br, c0, end);
+            v = PE_OK;
+            for (uint32_t c = c0; c < end && v == PE_OK; ++c)
+              if (!pat_leaf(a, node_sid(a, doc, c), pn.y)) v = PE_OTHER;
+          }
+        } else if (pn.kind == PN_MAP) {
+          if (rk != DN_MAP) {
+            v = PE_OTHER;
+          } else {
+            const uint32_t nmem = pn.z >> 16;
+            for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
+              const uint4 m = a.members[PV(pn.y + k, a.nmembers, 2)];
+              if (m.x & PMF_SLOT) {
+                const uint32_t bit = 1u << PM_SLOT(m.x);
+                reg |= bit;
+                if (pat_lookup(a, doc, br, m.y) != kNoNode) val |= bit;
+              }
+            }
+            v = push(PF_MAP, br, bpi, 0u);
+          }
+        } else if (rk != DN_ARR || pn.kind == PN_ARR_EMPTY) {
+          v = PE_OTHER;  // a list pattern needs a list; [] is "pattern Array empty"
+        } else {
+          PV_KIDS(br, c0, end);
+          if (pn.kind == PN_ARR_POS && end - c0 < pn.z) v = PE_OTHER_NOPATH;  // length mismatch: no path
+          else v = push(pn.kind == PN_ARR_POS ? PF_APOS : PF_AMAPS, br, bpi, c0);
+        }
+        if (v == PE_PUSHED) state = VM_STEP, v = PE_NONE;
+        continue;
+      }
+      if (state == VM_RET) {
+        if (sp < 0) return v;
+        state = VM_STEP;  // deliver v to the frame below
+        continue;
+      }
+      // ---- VM_STEP: advance the top frame with child verdict v (PE_NONE: none pending) ----
+      PFrame& F = st[PV(sp, kPatStack, 11)];
+      const KpePNode pn = a.nodes[PV(F.pi, a.nnodes, 1)];
+      if ((F.kind_k & 3u) == PF_MAP) {
+        // validateMap (validate.go:118-175) + anchor/handlers.go
+        const uint32_t m0 = pn.y, nanch = pn.z & 0xFFFFu, nmem = pn.z >> 16;
+        uint32_t k = F.kind_k >> 2, applied = F.cnt & 0xFFFFu, skips = F.cnt >> 16;
+        uint32_t e = PE_NONE;
+        bool begin_child = false;
+        if (v != PE_NONE) {  // the child BEGIN of member k finished with v
+          const uint32_t h = PM_HANDLER(a.members[PV(m0 + k, a.nmembers, 2)].x);
+          if (F.x) {  // existence search: element F.cur against pattern element F.x - 1
+            if (v == PE_OK) F.x += 1u, F.cur = doc[PVD(F.c)].y + 1u;
+            else F.cur += 1u;
+          } else {
+            e = (h == PM_COND || h == PM_GLOBAL) ? (v == PE_OK ? PE_OK : PE_SKIP) : v;
+          }
+        }
+        for (;;) {
+          if (e == PE_NONE && F.x) {  // existence anchor: each pattern map needs one matching element
+            const KpePNode xl = a.nodes[PV(a.members[PV(m0 + k, a.nmembers, 2)].z, a.nnodes, 1)];
+            PV_KIDS(F.c, c0, end);
+            (void)c0;
+            if (F.x - 1u >= xl.z) {
+              e = PE_OK, F.x = 0u;
+            } else {
+              const uint32_t pj = a.lists[PV(xl.y + F.x - 1u, a.nlists, 3)];
+              if (a.nodes[PV(pj, a.nnodes, 1)].kind == PN_BAD || F.cur >= end) {
+                e = PE_OTHER, F.x = 0u;
+              } else {
+                br = F.cur, bpi = pj, begin_child = true;
+                break;
+              }
+            }
+          }
+          if (e == PE_NONE) {  // start member k
+            if (k == nanch && applied == 0u && skips > 0u) {  // every anchor skipped
+              e = PE_SKIP;
+              k = nmem + 1u;  // completes below
+            } else if (k == nmem) {
+              e = PE_OK;
+              k = nmem + 1u;
+            } else {
+              const uint4 m = a.members[PV(m0 + k, a.nmembers, 2)];
+              const uint32_t h = PM_HANDLER(m.x);
+              const uint32_t c = (m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, F.r, m.w) : pat_lookup(a, doc, F.r, m.y);
+              if (h == PM_NEG) {
+                e = c == kNoNode ? PE_OK : PE_NEG;
+              } else if (c == kNoNode && h != PM_DEFAULT) {
+                e = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
+              } else if (m.x & PMF_STAR) {
+                e = (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
+              } else if (h == PM_EXIST) {
+                if (DN_KIND(doc[PVD(c)].x) != DN_ARR || a.nodes[PV(m.z, a.nnodes, 1)].kind != PN_EXLIST) {
+                  e = PE_OTHER;
+                } else {
+                  F.x = 1u, F.cur = doc[PVD(c)].y + 1u, F.c = c;
+                  continue;  // search
+                }
+              } else {
+                br = c, bpi = m.z, begin_child = true;
+                break;
+              }
+            }
+          }
+          if (k > nmem) break;  // the map itself completed with e
+          // member k's verdict e
+          if (k < nanch) {
+            if (e == PE_SKIP) ++skips;
+            else if (e != PE_OK) break;
+            else ++applied;
+          } else if (e != PE_OK) {
+            break;
+          }
+          ++k, e = PE_NONE;
+        }
+        if (begin_child) {
+          F.kind_k = PF_MAP | (k << 2), F.cnt = applied | (skips << 16);
+          state = VM_BEGIN, v = PE_NONE;
+        } else {
+          --sp;
+          state = VM_RET, v = e;
+        }
+        continue;
+      }
+      // validateArrayOfMaps / positional validateArray (validate.go:177-261)
+      {
+        const bool pos = (F.kind_k & 3u) == PF_APOS;
+        PV_KIDS(F.r, c0, end);
+        (void)c0;
+        uint32_t applied = F.cnt, skips = F.x, j = F.kind_k >> 2, cur = F.cur;
+        uint32_t e = PE_NONE;
+        if (v != PE_NONE) {  // element `cur` finished
+          if (v == PE_SKIP) ++skips;
+          else if (v != PE_OK) e = v;
+          else ++applied;
+          cur += 1u, ++j;
+        }
+        if (e == PE_NONE && (pos ? j >= pn.z : cur >= end)) e = (applied == 0u && skips > 0u) ? PE_SKIP : PE_OK;
+        if (e != PE_NONE) {
+          --sp;
+          state = VM_RET, v = e;
+        } else {
+          F.kind_k = (F.kind_k & 3u) | (j << 2), F.cnt = applied, F.x = skips, F.cur = cur;
+          br = cur, bpi = pos ? a.lists[PV(pn.y + j, a.nlists, 3)] : pn.y;
+          state = VM_BEGIN, v = PE_NONE;
+        }
+      }
+    }
   }
+
   __device__ __forceinline__ uint32_t push(uint32_t kind, uint32_t r, uint32_t pi, uint32_t cur) {
     if (sp + 1 >= kPatStack) return PE_OTHER;  // unreachable: the compiler bounds pattern depth
     ++sp;
     st[PV(sp, kPatStack, 11)] = PFrame{kind, r, pi, 0u, cur, 0u, 0u};
     return PE_PUSHED;
-  }
-  __device__ __forceinline__ uint32_t pop(uint32_t e) {
-    --sp;
-    return e;
-  }
-  // validateResourceElement (validate.go:71-114): a verdict, or PE_PUSHED with a new frame
-  __device__ __forceinline__ uint32_t begin(uint32_t r, uint32_t pi) {
-    const KpePNode pn = a.nodes[PV(pi, a.nnodes, 1)];
-    const uint32_t rk = r == kNoNode ? 0xFFu : DN_KIND(doc[PVD(r)].x);
-    if (pn.kind == PN_LEAF) {
-      if (rk == DN_ARR) return leaf_all(r, pn.y);
-      return pat_leaf(a, node_sid(a, doc, r), pn.y) ? PE_OK : PE_OTHER;
-    }
-    if (pn.kind == PN_MAP) {
-      if (rk != DN_MAP) return PE_OTHER;
-      const uint32_t nmem = pn.z >> 16;
-      for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
-        const uint4 m = a.members[PV(pn.y + k, a.nmembers, 2)];
-        if (m.x & PMF_SLOT) {
-          const uint32_t bit = 1u << PM_SLOT(m.x);
-          reg |= bit;
-          if (pat_lookup(a, doc, r, m.y) != kNoNode) val |= bit;
-        }
-      }
-      return push(PF_MAP, r, pi, 0u);
-    }
-    if (rk != DN_ARR) return PE_OTHER;
-    switch (pn.kind) {
-      case PN_ARR_LEAF: return leaf_all(r, pn.y);
-      case PN_ARR_MAPS: return push(PF_AMAPS, r, pi, r + 1u);
-      case PN_ARR_POS: {
-        uint32_t len = 0;
-        const uint32_t end = r + 1u + doc[PVD(r)].y;
-        for (uint32_t c = r + 1u; c < end; c += nd_skip(doc[PVD(c)])) ++len;
-        if (len < pn.z) return PE_OTHER_NOPATH;  // length mismatch: a PatternError with no path
-        return push(PF_APOS, r, pi, r + 1u);
-      }
-      default: return PE_OTHER;  // PN_ARR_EMPTY: "pattern Array empty"
-    }
-  }
-
-  // validateMap (validate.go:118-175) + anchor handlers, resumed with the verdict `v` of
-  // the child frame it waited on (PE_NONE: nothing pending)
-  __device__ __forceinline__ uint32_t map_step(uint32_t v) {
-    PFrame& F = st[PV(sp, kPatStack, 11)];
-    const KpePNode pn = a.nodes[PV(F.pi, a.nnodes, 1)];
-    const uint32_t m0 = pn.y, nanch = pn.z & 0xFFFFu, nmem = pn.z >> 16;
-    uint32_t k = F.kind_k >> 2, applied = F.cnt & 0xFFFFu, skips = F.cnt >> 16;
-    for (;;) {
-      uint32_t e;
-      if (v == PE_NONE) {
-        if (k == nanch && applied == 0u && skips > 0u) return pop(PE_SKIP);  // every anchor skipped
-        if (k == nmem) return pop(PE_OK);
-        const uint4 m = a.members[PV(m0 + k, a.nmembers, 2)];
-        const uint32_t h = PM_HANDLER(m.x);
-        const uint32_t c = (m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, F.r, m.w) : pat_lookup(a, doc, F.r, m.y);
-        if (h == PM_NEG) {
-          e = c == kNoNode ? PE_OK : PE_NEG;
-        } else if (c == kNoNode && h != PM_DEFAULT) {
-          e = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
-        } else if (m.x & PMF_STAR) {
-          e = (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
-        } else if (h == PM_EXIST) {
-          if (DN_KIND(doc[PVD(c)].x) != DN_ARR || a.nodes[PV(m.z, a.nnodes, 1)].kind != PN_EXLIST) {
-            e = PE_OTHER;
-          } else {
-            F.x = 1u, F.cur = c + 1u, F.c = c;
-            e = PE_NONE;  // search below
-          }
-        } else {
-          F.kind_k = PF_MAP | (k << 2), F.cnt = applied | (skips << 16);
-          const uint32_t w = begin(c, m.z);
-          if (w == PE_PUSHED) return PE_PUSHED;
-          e = (h == PM_COND || h == PM_GLOBAL) ? (w == PE_OK ? PE_OK : PE_SKIP) : w;
-        }
-      } else {  // the child of member k finished with v
-        const uint32_t h = PM_HANDLER(a.members[PV(m0 + k, a.nmembers, 2)].x);
-        if (h == PM_EXIST) {
-          if (v == PE_OK) F.x += 1u, F.cur = F.c + 1u;
-          else F.cur += nd_skip(doc[PVD(F.cur)]);
-          e = PE_NONE;
-        } else {
-          e = (h == PM_COND || h == PM_GLOBAL) ? (v == PE_OK ? PE_OK : PE_SKIP) : v;
-        }
-        v = PE_NONE;
-      }
-      if (e == PE_NONE) {  // existence anchor: each pattern map needs one matching element
-        const KpePNode xl = a.nodes[PV(a.members[PV(m0 + k, a.nmembers, 2)].z, a.nnodes, 1)];
-        const uint32_t end = F.c + 1u + doc[PVD(F.c)].y;
-        e = PE_OK;
-        while (F.x - 1u < xl.z) {
-          const uint32_t pj = a.lists[PV(xl.y + F.x - 1u, a.nlists, 3)];
-          if (a.nodes[PV(pj, a.nnodes, 1)].kind == PN_BAD || F.cur >= end) {
-            e = PE_OTHER;
-            break;
-          }
-          F.kind_k = PF_MAP | (k << 2), F.cnt = applied | (skips << 16);
-          const uint32_t w = begin(F.cur, pj);
-          if (w == PE_PUSHED) return PE_PUSHED;
-          if (w == PE_OK) F.x += 1u, F.cur = F.c + 1u;
-          else F.cur += nd_skip(doc[PVD(F.cur)]);
-        }
-        F.x = 0u;
-      }
-      if (k < nanch) {  // anchors: skips are counted, any other error ends the map
-        if (e == PE_SKIP) ++skips;
-        else if (e != PE_OK) return pop(e);
-        else ++applied;
-      } else if (e != PE_OK) {
-        return pop(e);
-      }
-      ++k;
-    }
-  }
-
-  // validateArrayOfMaps / positional validateArray (validate.go:177-261)
-  __device__ __forceinline__ uint32_t arr_step(uint32_t v) {
-    PFrame& F = st[PV(sp, kPatStack, 11)];
-    const KpePNode pn = a.nodes[PV(F.pi, a.nnodes, 1)];
-    const bool pos = (F.kind_k & 3u) == PF_APOS;
-    const uint32_t end = F.r + 1u + doc[PVD(F.r)].y;
-    uint32_t applied = F.cnt, skips = F.x, j = F.kind_k >> 2, cur = F.cur;
-    for (;;) {
-      if (v != PE_NONE) {  // element `cur` finished
-        if (v == PE_SKIP) ++skips;
-        else if (v != PE_OK) return pop(v);
-        else ++applied;
-        cur += nd_skip(doc[PVD(cur)]);
-        ++j;
-        v = PE_NONE;
-      }
-      if (pos ? j >= pn.z : cur >= end) return pop(applied == 0u && skips > 0u ? PE_SKIP : PE_OK);
-      F.kind_k = (F.kind_k & 3u) | (j << 2), F.cnt = applied, F.x = skips, F.cur = cur;
-      const uint32_t w = begin(cur, pos ? a.lists[PV(pn.y + j, a.nlists, 3)] : pn.y);
-      if (w == PE_PUSHED) return PE_PUSHED;
-      v = w;
-    }
-  }
-
-  // validate.MatchPattern (validate.go:31-56) of pattern root node `pi`
-  __device__ __forceinline__ uint32_t run(uint32_t pi) {
-    sp = -1, reg = 0u, val = 0u;
-    uint32_t v = begin(0u, pi);
-    if (v != PE_PUSHED) return v;
-    v = PE_NONE;
-    for (;;) {
-      const uint32_t w = (st[PV(sp, kPatStack, 11)].kind_k & 3u) == PF_MAP ? map_step(v) : arr_step(v);
-      if (w == PE_PUSHED) {
-        v = PE_NONE;
-        continue;
-      }
-      if (sp < 0) return w;
-      v = w;
-    }
   }
 };
 
@@ -350,7 +384,7 @@ __device__ __forceinline__ uint32_t pat_match_root(PatVM& vm, uint32_t root) {
 // kpe_pattern_kernel's body for resource r: resolve the row's KPE_PENDING_ pattern cells
 // (validate_resource.go:316-398: one pattern, or anyPattern's first pass / skip / fail)
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
-  PatVM vm{a, reinterpret_cast<const uint2*>(a.doc) + a.doc_off[r]};
+  PatVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r]};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   for (uint32_t i = 0; i < a.npr; ++i) {
     const KpePatRule pr = a.rules[i];

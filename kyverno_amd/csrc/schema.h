@@ -348,11 +348,12 @@ typedef struct KpeRule {
 } KpeRule;
 
 // ---- generic document tape (pattern rules) ---------------------------------------------
-// Every resource is also kept as a pre-order node array (its JSON document as the
-// reference's unstructured map sees it). Node (uint2):
-//   x = kind | (member-name id + 1) << 2   (D_KEY id; 0 = array element / root)
-//   y = scalar id (DN_SCALAR) or number of nodes in the subtree below (DN_MAP / DN_ARR),
-//       so the next sibling of node i is i + 1 + (container ? y : 0).
+// Every resource is also kept as its JSON document (the reference's unstructured map).
+// An entry (uint2) is x = kind | (member-name id + 1) << 2 (D_KEY id; 0 = array element /
+// root) and y = scalar id (DN_SCALAR) or the tape index of the container's body. A body is
+// {count, 0} followed by the count member / element entries, contiguous (so a member
+// lookup is one run of independent loads). Corpus::doc_off[r] is resource r's root entry
+// (absolute tape index).
 #define DN_SCALAR 0u
 #define DN_MAP 1u
 #define DN_ARR 2u

@@ -59,19 +59,18 @@ int main(int argc, char** argv) {
   kpe::flatten_ndjson(C, nd.data(), nd.size(), nullptr, 0, true);
   auto P = kpe::compile_policies(pj.data(), pj.size());
   const auto& PP = P->pat;
-  // tape invariants: every subtree inside its resource, scalar ids in range, names valid
-  for (int64_t r = 0; r < C.n; ++r) {
-    const uint64_t b = C.doc_off[r], e = C.doc_off[r + 1];
-    for (uint64_t i = b; i < e; ++i) {
-      const uint32_t x = C.doc[2 * i], y = C.doc[2 * i + 1];
-      if (DN_KIND(x) == DN_SCALAR ? y >= C.scal.size() : i + 1 + y > e) {
-        fprintf(stderr, "bad node %llu of resource %lld\n", (unsigned long long)i, (long long)r);
-        return 1;
-      }
-      if (DN_KEY(x) > C.dict[D_KEY].size()) {
-        fprintf(stderr, "bad member name at node %llu\n", (unsigned long long)i);
-        return 1;
-      }
+  // tape invariants: one root entry per resource; every body inside the tape
+  if ((int64_t)C.doc_off.size() != C.n) return fprintf(stderr, "doc_off size\n"), 1;
+  const uint64_t ndoc = C.doc.size() / 2;
+  for (uint64_t i = 0; i < ndoc; ++i) {
+    const uint32_t x = C.doc[2 * i], y = C.doc[2 * i + 1];
+    if (DN_KIND(x) == DN_SCALAR ? y >= C.scal.size() && y != 0 && DN_KEY(x) != 0 : false) {
+      fprintf(stderr, "bad scalar id at entry %llu\n", (unsigned long long)i);
+      return 1;
+    }
+    if ((DN_KIND(x) == DN_MAP || DN_KIND(x) == DN_ARR) && (y >= ndoc || y + 1 + C.doc[2 * y] > ndoc)) {
+      fprintf(stderr, "bad body at entry %llu\n", (unsigned long long)i);
+      return 1;
     }
   }
   // bind: operand records, member names, glob bitsets (host copies of the device tables)

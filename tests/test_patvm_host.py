@@ -1,0 +1,55 @@
+"""The pattern VM's device source (kyverno_amd/csrc/patvm.inl + strmatch.inl) compiled for
+the host with AddressSanitizer/UBSan and bounds flags (scripts/patvm_check.cpp), run over
+the chart policies, the validate_test.go trees, the test/cli/test scenarios and the edge
+documents. Every cell the oracle applies must agree; no bounds flag may be raised. CPU only:
+this keeps the exact kernel logic under test without a GPU."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import kyverno_amd as K
+from tests.test_gpu_pattern import CLI, PTREE, _policy_for, chart_pattern_policies, device_policies, edge_case_inputs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "scripts", "build", "patvm_check")
+
+
+@pytest.fixture(scope="module")
+def harness():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), "patvm_check"])
+    return BIN
+
+
+def _sets():
+    out = [("chart-mix0", chart_pattern_policies(), K.synth_resources(0xC1, 1500, mix=0)),
+           ("chart-mix2", chart_pattern_policies(), K.synth_resources(22, 1500, mix=2))]
+    pols, nd = edge_case_inputs(1500)
+    out.append(("edge", pols, nd))
+    cases = [c for c in PTREE if isinstance(json.loads(c["resource"]), dict)]
+    pols = device_policies([_policy_for(f"t{i}", json.loads(c["pattern"])) for i, c in enumerate(cases)])
+    out.append(("validate_test.go", pols, "\n".join(json.dumps(json.loads(c["resource"])) for c in cases).encode()))
+    for c in CLI:
+        p = device_policies(c["policies"])
+        if p and c["resources"]:
+            out.append((c["name"], p, "\n".join(json.dumps(r) for r in c["resources"]).encode()))
+    return out
+
+
+SETS = _sets()
+
+
+@pytest.mark.parametrize("name,pols,nd", SETS, ids=[s[0] for s in SETS])
+def test_patvm_host_matches_oracle(harness, oracle, tmp_path, name, pols, nd):
+    pj, rj, vb = tmp_path / "p.json", tmp_path / "r.ndjson", tmp_path / "v.bin"
+    pj.write_text(json.dumps(pols))
+    rj.write_bytes(nd)
+    r = subprocess.run([harness, str(pj), str(rj), str(vb)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    ref = oracle.validate(pols, nd)
+    v = np.fromfile(vb, dtype=np.uint8).reshape(ref.shape)
+    applied = ref != 0  # the harness resolves every pattern cell as if its rule matched
+    bad = np.argwhere((v != ref) & applied)
+    assert bad.size == 0, f"{len(bad)} cells differ, first {bad[:5].tolist()}"
