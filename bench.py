@@ -27,7 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--resources", type=int, default=1_000_000, help="Pods per GPU")
-    ap.add_argument("--replicas", type=int, default=4)
+    ap.add_argument("--replicas", type=int, default=8)
     ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="Pods in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
