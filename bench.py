@@ -155,6 +155,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "kernel": "kpe_scan_kernel", "kernel_ms": scan_ms, "dict_kernel_ms": dict_ms,
+                         # the same bytes over the timed region's step time (launches of
+                         # different shards overlap on two streams there)
+                         "achieved_per_step": st.scan_bytes / (ms_per_step * 1e-3) / 1e9,
                          "alg_bytes_per_launch": st.scan_bytes},
             "cpu_baseline": cpu,
             "setup_s": t_setup,

@@ -131,10 +131,16 @@ constexpr uint32_t kBlock = 256;
 #ifndef KPE_DIAG
 #define KPE_DIAG 0
 #endif
+// Minimum waves per SIMD the scan kernel is compiled for (register budget).
+#ifndef KPE_SCAN_WAVES
+#define KPE_SCAN_WAVES 6
+#endif
 #define DIAG_NOPRO 1u    // no fused dictionary pass / capability bits in the prologue
 #define DIAG_NOPSS 2u    // PSS lists loaded but not evaluated
 #define DIAG_NORULES 4u  // no terms / rules: a verdict derived from the PSS bits
 #define DIAG_NOLOOP 8u   // no tiles: launch + prologue only
+#define DIAG_EMPTY 16u   // return at entry: launch cost only
+#define DIAG_NOTT 32u    // no truth table in the prologue
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
@@ -277,6 +283,17 @@ __device__ __forceinline__ uint32_t hw(uint32_t h, uint32_t k) { return __builti
 template <bool PSS>
 __device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane);
 
+// Pin a tile's registers here: code that uses them cannot be hoisted above this point
+// (the compiler would otherwise move ALU work on a tile's loaded values above the next
+// tile's load issue, or into the block prologue, and wait for the loads there).
+__device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)::"memory"); }
+__device__ __forceinline__ void pin(uint2& x) { pin(x.x), pin(x.y); }
+__device__ __forceinline__ void pin(uint4& x) { pin(x.x), pin(x.y), pin(x.z), pin(x.w); }
+__device__ __forceinline__ void pin_tile(Tile<true>& d) {
+  pin(d.rec), pin(d.c0), pin(d.c1), pin(d.v0), pin(d.s0), pin(d.q0), pin(d.sa0), pin(d.sa1), pin(d.name), pin(d.mns);
+}
+__device__ __forceinline__ void pin_tile(Tile<false>& d) { pin(d.gvk), pin(d.nsa), pin(d.name), pin(d.mns); }
+
 // Every load of a tile is issued on every path (an unneeded column is read from the
 // binding's zero page instead: one broadcast cache line), so the number of loads a
 // prefetch puts in flight is static and the compiler can wait for an older tile with
@@ -316,9 +333,8 @@ __device__ __forceinline__ Tile<true> load_tile<true>(CArgs& a, uint32_t tile, u
   const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
   d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
   d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
-  if (!on_sa) d.sa0 = d.sa1 = KPE_NO_STR;
-  if (!on_n) d.name = KPE_NO_STR;
-  if (!on_m) d.mns = KPE_NO_STR;
+  // no fix-ups of loaded values here (a select on a loaded register waits for the load):
+  // columns that are off are masked where they are used (tile_cols, pss_tile's `nsann`)
   return d;
 }
 
@@ -334,10 +350,6 @@ __device__ __forceinline__ Tile<false> load_tile<false>(CArgs& a, uint32_t tile,
   d.nsa = col<uint32_t>(on_a, a.r_nsa, zp)[on_a ? rc : 0u];
   d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
   d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
-  if (!on_g) d.gvk = 0;
-  if (!on_a) d.nsa = KPE_NO_STR;
-  if (!on_n) d.name = KPE_NO_STR;
-  if (!on_m) d.mns = KPE_NO_STR;
   return d;
 }
 
@@ -393,28 +405,30 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
   if (nsys && lane < nst) sbs[lane] = (uint8_t)sys_code(d.s0);
   if (npann && lane < nat) sba[lane] = (uint8_t)ann_code(d.q0);
   __builtin_amdgcn_wave_barrier();
+  // Each pod ORs its own staged items, four independent LDS reads per round (indices
+  // clamped to the pod's last item: a repeated item does not change an OR), so a pod
+  // with <= 4 items of a list pays one LDS round trip for it, not one per item.
   uint32_t xo = 0, co = 0, vcode = 0, scode = 0, acode = 0;
   {
     const uint32_t hi = min(oc + nc, (uint32_t)KPE_STAGE_CTR);
-#pragma unroll 2
-    for (uint32_t k = oc; k < hi; ++k) {
-      const uint2 e = sc[k];
-      xo |= e.x;
-      co |= e.y;
+#pragma unroll 1
+    for (uint32_t k = oc; k < hi; k += 4) {
+      const uint2 e0 = sc[k], e1 = sc[min(k + 1, hi - 1)], e2 = sc[min(k + 2, hi - 1)], e3 = sc[min(k + 3, hi - 1)];
+      xo |= e0.x | e1.x | e2.x | e3.x;
+      co |= e0.y | e1.y | e2.y | e3.y;
     }
   }
-  if (nvol) {
-    const uint32_t hi = min(ov + nv, (uint32_t)KPE_STAGE_SMALL);
-    for (uint32_t k = ov; k < hi; ++k) vcode |= sbv[k];
-  }
-  if (nsys) {
-    const uint32_t hi = min(os + ns, (uint32_t)KPE_STAGE_SMALL);
-    for (uint32_t k = os; k < hi; ++k) scode |= sbs[k];
-  }
-  if (npann) {
-    const uint32_t hi = min(oa + na, (uint32_t)KPE_STAGE_SMALL);
-    for (uint32_t k = oa; k < hi; ++k) acode |= sba[k];
-  }
+  auto or_bytes = [](const uint8_t* b, uint32_t o, uint32_t cnt) -> uint32_t {
+    const uint32_t hi = min(o + cnt, (uint32_t)KPE_STAGE_SMALL);
+    uint32_t x = 0;
+#pragma unroll 1
+    for (uint32_t k = o; k < hi; k += 4)
+      x |= (uint32_t)b[k] | b[min(k + 1, hi - 1)] | b[min(k + 2, hi - 1)] | b[min(k + 3, hi - 1)];
+    return x;
+  };
+  if (nvol) vcode = or_bytes(sbv, ov, nv);
+  if (nsys) scode = or_bytes(sbs, os, ns);
+  if (npann) acode = or_bytes(sba, oa, na);
   __builtin_amdgcn_wave_barrier();
   // ---- rare: items beyond the staged chunk, loaded directly by their pod lane ----
   if (nct > KPE_STAGE_CTR || (nvol && nvt > KPE_STAGE_SMALL) || (nsys && nst > KPE_STAGE_SMALL) ||
@@ -557,41 +571,68 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
 // WIDE: terms are ballot-ed into per-wave 64-bit masks in LDS and lane j evaluates
 // rule c0 + j for all 64 resources with 64-bit mask algebra.
 template <bool PSS, bool NARROW>
-__global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
+__global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ __attribute__((aligned(16))) uint8_t s_capb[PSS ? KPE_MAX_CAPSETS : 4];
 
+  if (KPE_DIAG & DIAG_EMPTY) return;
   CArgs& a0 = *launder(ap);
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t ntiles = a0.ntiles;
   const uint32_t W = gridDim.x * (kBlock / 64u);
   uint32_t tile = blockIdx.x * (kBlock / 64u) + wv;
 
-  // ---- first tile's loads, then the block prologue while they are in flight ----
+  // ---- first tile's header, the prologue's own loads, then the first tile's data; the
+  // block prologue runs while the tile loads are in flight. No loaded value is touched
+  // before the header is needed, so nothing waits for more than the load it uses. ----
   uint32_t h = 0;  // header words of the tile whose data is loaded next
-  Tile<PSS> ta{};
-  if (tile < ntiles) {
-    if (PSS) h = load_hdr(a0, tile, lane);
-    ta = load_tile<PSS>(a0, tile, h, lane);
-    if (PSS && tile + W < ntiles) h = load_hdr(a0, tile + W, lane);
+  // unconditional, clamped (a wave without a tile re-reads the last one and never uses
+  // it): the number of loads in flight is the same on every path, so waits are counted
+  const uint32_t tile0 = min(tile, ntiles - 1u);
+  if (PSS) h = load_hdr(a0, tile0, lane);
+  // capability sets (tiny dictionary) and the first slice of the LDS image, clamped and
+  // unconditional (a zero page stands in for an absent table)
+  const uint32_t ncs = a0.ncapsets;
+  const bool capl = PSS && (a0.need & NEED_CAPS) && ncs;
+  const uint4 cs0 = reinterpret_cast<const uint4*>(capl ? a0.capsets : a0.zero_page)[capl ? min(t, ncs - 1u) : 0u];
+  const bool fused = a0.npairs != 0;
+  const uint32_t img_n4 = (fused ? a0.fuse_words : a0.blob_words) >> 2;
+  const uint4* img = reinterpret_cast<const uint4*>(img_n4 ? (fused ? a0.fuse : a0.pbuf) : a0.zero_page);
+  const uint4 img0 = img[img_n4 ? min(t, img_n4 - 1u) : 0u];
+  // Program tables held in lanes for the whole kernel (read back with v_readlane:
+  // no memory access inside the tile loop). WIDE single-chunk programs: lane j's
+  // packed rule. NARROW: lane j holds rule j's record, lane f filter f's term mask,
+  // lane t term t.
+  uint4 myrule = make_uint4(0, 0, 0, 0);
+  uint32_t fm_lane = 0, tm_type = 0, tm_a = 0, tm_b = 0;
+  if (NARROW) {
+    if (lane < a0.nrules) myrule = reinterpret_cast<const uint4*>(a0.narrow_rules)[lane];
+    if (lane < a0.nfilters) fm_lane = a0.fmask[lane];
+    if (lane < a0.nterms) {
+      const KpeTerm tm = a0.terms[lane];
+      tm_type = tm.type, tm_a = tm.a, tm_b = tm.b;
+    }
+  } else if (a0.nrules <= KPE_RULE_CHUNK && lane < a0.nrules) {
+    myrule = reinterpret_cast<const uint4*>(a0.rule_lanes)[lane];
   }
-  // capability sets: the block's first 256 prefetched alongside (tiny dictionary)
-  uint4 cs0 = make_uint4(0, 0, 0, 0);
-  if (PSS && (a0.need & NEED_CAPS) && t < a0.ncapsets) cs0 = reinterpret_cast<const uint4*>(a0.capsets)[t];
+  uint32_t cls_cv = 0, cls_rm = 0;  // NARROW PSS classes: (check set, rules failing on it)
+  if (NARROW && a0.tt_lds != PRED_NONE && lane < a0.ncls) {
+    const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
+    cls_cv = c.x, cls_rm = c.y;
+  }
+  Tile<PSS> ta = load_tile<PSS>(a0, tile0, h, lane);
+  if (PSS) h = load_hdr(a0, min(tile + W, ntiles - 1u), lane);
   {
     CArgs& a = a0;
-    if (a.npairs) {  // fused dictionary pass: stage the fuse image, clear the local bitsets
-      const uint4* src = reinterpret_cast<const uint4*>(a.fuse);
-      uint4* f4 = reinterpret_cast<uint4*>(dyn + a.fuse_lds);
+    // fused dictionary pass: the fuse image, and the local bitsets cleared; otherwise the
+    // small-domain predicate bitsets (kpe_pred_kernel output)
+    uint4* d4 = reinterpret_cast<uint4*>(dyn + (fused ? a.fuse_lds : 0u));
+    if (t < img_n4) d4[t] = img0;
 #pragma unroll 1
-      for (uint32_t i = t; i < (a.fuse_words >> 2); i += kBlock) f4[i] = src[i];
+    for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
+    if (fused) {
 #pragma unroll 1
       for (uint32_t i = t; i < a.blob_words; i += kBlock) dyn[i] = 0;
-    } else {  // small-domain predicate bitsets (kpe_pred_kernel output) into LDS
-      const uint4* blob = reinterpret_cast<const uint4*>(a.pbuf);
-      uint4* d4 = reinterpret_cast<uint4*>(dyn);
-#pragma unroll 1
-      for (uint32_t i = t; i < (a.blob_words >> 2); i += kBlock) d4[i] = blob[i];
     }
     if (!NARROW && a.filt_lds != PRED_NONE) {  // program filters + filter terms for the rule lanes
       const uint32_t nw = a.fterm_lds + a.nfterms - a.filt_lds;
@@ -635,30 +676,9 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
     __syncthreads();
   }
 
-  // Program tables held in lanes for the whole kernel (read back with v_readlane:
-  // no memory access inside the tile loop). WIDE single-chunk programs: lane j's
-  // packed rule. NARROW: lane j holds rule j's record, lane f filter f's term mask,
-  // lane t term t.
-  uint4 myrule = make_uint4(0, 0, 0, 0);
-  uint32_t fm_lane = 0, tm_type = 0, tm_a = 0, tm_b = 0;
-  if (NARROW) {
-    if (lane < a0.nrules) myrule = reinterpret_cast<const uint4*>(a0.narrow_rules)[lane];
-    if (lane < a0.nfilters) fm_lane = a0.fmask[lane];
-    if (lane < a0.nterms) {
-      const KpeTerm tm = a0.terms[lane];
-      tm_type = tm.type, tm_a = tm.a, tm_b = tm.b;
-    }
-  } else if (a0.nrules <= KPE_RULE_CHUNK && lane < a0.nrules) {
-    myrule = reinterpret_cast<const uint4*>(a0.rule_lanes)[lane];
-  }
   // NARROW truth table: tt[v] = rules whose match / exclude / namespaced-policy term
   // conditions hold for term vector v (pkg/engine/utils/match.go:168-300 over filters)
-  uint32_t cls_cv = 0, cls_rm = 0;
-  if (NARROW && a0.tt_lds != PRED_NONE) {
-    if (lane < a0.ncls) {
-      const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
-      cls_cv = c.x, cls_rm = c.y;
-    }
+  if (NARROW && a0.tt_lds != PRED_NONE && !(KPE_DIAG & DIAG_NOTT)) {
     const uint32_t R = a0.nrules, nv = 1u << a0.nterms;
     for (uint32_t tb = t; tb < nv; tb += kBlock) {
       uint32_t mm = 0;
@@ -696,7 +716,7 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
   // registers during the previous step, and the next tile is loaded into the other
   // buffer, so no register holding an in-flight load is ever copied (a loop-carried
   // copy of a prefetched register makes the compiler wait for the prefetch at once).
-  auto step = [&](const Tile<PSS>& cur, Tile<PSS>& nxt) {
+  auto step = [&](Tile<PSS>& cur, Tile<PSS>& nxt) {
     CArgs& a = *launder(ap);
     const uint32_t R = a.nrules, n = (uint32_t)a.n;
     const Bits B{dyn, a.pbuf};
@@ -714,11 +734,13 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
     // (unconditional, clamped: past the end it re-reads the last tile, never used)
     nxt = load_tile<PSS>(a, min(tile + W, ntiles - 1), h, lane);
     if (PSS) h = load_hdr(a, min(tile + 2 * W, ntiles - 1), lane);
+    pin_tile(cur);
     const uint32_t r = tile * 64 + lane;
     const bool live = r < n;
     const uint32_t rc = live ? r : n - 1;
     uint32_t fails = 0, gvk, nsa, name_col, mns_col;
     bool err = false;
+    const uint32_t need = a.need;
     if constexpr (PSS) {
       if (KPE_DIAG & DIAG_NOPSS)
         fails = cur.rec.x ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.s0 ^ cur.q0.x ^ cur.q0.y ^ cur.C0;
@@ -729,11 +751,11 @@ __global__ void __launch_bounds__(kBlock) kpe_scan_kernel(const ScanArgs* __rest
       gvk = live ? cur.rec.y : 0u;
       nsa = live ? cur.rec.w : KPE_NO_STR;
     } else {
-      gvk = live ? cur.gvk : 0u;
-      nsa = live ? cur.nsa : KPE_NO_STR;
+      gvk = live && (need & NEED_GVK) ? cur.gvk : 0u;
+      nsa = live && (need & NEED_NSA) ? cur.nsa : KPE_NO_STR;
     }
-    name_col = live ? cur.name : KPE_NO_STR;
-    mns_col = live ? cur.mns : KPE_NO_STR;
+    name_col = live && (need & NEED_NAME) ? cur.name : KPE_NO_STR;
+    mns_col = live && (need & NEED_MNS) ? cur.mns : KPE_NO_STR;
     const uint32_t nrows = min(64u, n - tile * 64);
     if (NARROW && prev_tile != 0xFFFFFFFFu) {  // the previous tile's rows (other LDS buffer)
       store_rows(a.verdicts, reinterpret_cast<uint8_t*>(wrest) + (buf ^ 1u) * 64 * R, prev_tile, R, 0, R, prev_rows,

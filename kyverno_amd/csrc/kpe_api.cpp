@@ -90,9 +90,17 @@ constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated 
 
 }  // namespace
 
+// Evaluation streams per device: a corpus binding is pinned to one of them, so the
+// evaluations of independent corpora (shards, rotated batches) run concurrently and one
+// launch's prologue overlaps another's tail. Setup (uploads, binds) and timed launches
+// use stream 0.
+constexpr int kMaxLanes = 4;
 struct kpe_device {
   int ordinal = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;  // == lanes[0]
+  hipStream_t lanes[kMaxLanes] = {};
+  int nlanes = 2;  // KPE_LANES (1..4) overrides
+  uint32_t next_lane = 0;
   std::mutex mu;
   bool timing = false;
   struct EvPair {
@@ -149,6 +157,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t need = 0;
   double scan_bytes = 0;
   size_t cells = 0;
+  int lane = -1;                  // evaluation stream (kpe_device::lanes) of this corpus
+  hipStream_t last = nullptr;     // stream of the last launch (fetch orders after it)
 };
 
 struct DeviceCorpus {
@@ -189,11 +199,16 @@ kpe_status kpe_device_open(int ordinal, kpe_device** out) {
   auto d = new (std::nothrow) kpe_device();
   if (!d) return fail(KPE_E_DEVICE, "oom");
   d->ordinal = ordinal;
-  e = hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    delete d;
-    return fail(KPE_E_DEVICE, hipGetErrorString(e));
+  if (const char* ev = getenv("KPE_LANES")) d->nlanes = std::max(1, std::min(kMaxLanes, atoi(ev)));
+  for (int k = 0; k < d->nlanes; ++k) {
+    e = hipStreamCreateWithFlags(&d->lanes[k], hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      for (int j = 0; j < k; ++j) (void)hipStreamDestroy(d->lanes[j]);
+      delete d;
+      return fail(KPE_E_DEVICE, hipGetErrorString(e));
+    }
   }
+  d->stream = d->lanes[0];
   *out = d;
   return KPE_OK;
 }
@@ -201,7 +216,7 @@ kpe_status kpe_device_open(int ordinal, kpe_device** out) {
 void kpe_device_close(kpe_device* d) {
   if (!d) return;
   (void)hipSetDevice(d->ordinal);
-  (void)hipStreamSynchronize(d->stream);
+  for (int k = 0; k < d->nlanes; ++k) (void)hipStreamSynchronize(d->lanes[k]);
   for (auto& p : d->pending) {
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
@@ -209,7 +224,7 @@ void kpe_device_close(kpe_device* d) {
     (void)hipEventDestroy(p.d);
   }
   for (auto e : d->pool) (void)hipEventDestroy(e);
-  (void)hipStreamDestroy(d->stream);
+  for (int k = 0; k < d->nlanes; ++k) (void)hipStreamDestroy(d->lanes[k]);
   delete d;
 }
 
@@ -501,6 +516,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   auto& PD = *P.dev;
   size_t cells = (size_t)C.n * P.rules.size();
   if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
+  if (B.last) HIPCHK(hipStreamSynchronize(B.last));  // no launch may still read what is rebuilt
+  if (B.lane < 0) B.lane = (int)(dev->next_lane++ % (uint32_t)dev->nlanes);
   hipStream_t s = dev->stream;
   // Predicates over small dictionaries get LDS-resident bitsets ("local": every scan
   // block copies them from pbuf's blob), the rest are read from pbuf (HBM/L2). All are
@@ -684,8 +701,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   }
   if (getenv("KPE_DEBUG")) {
     fprintf(stderr, "kpe bind: n=%lld R=%zu narrow=%d blob=%u pred_jobs=%u pred_xblocks=%u scan_blocks=%u dyn=%zu "
-            "wave_words=%u\n", (long long)C.n, P.rules.size(), (int)narrow, blob, (unsigned)jobs.size(), blk,
-            B.scan_blocks, B.dyn_bytes, wave_words);
+            "wave_words=%u npairs=%u fuse_words=%u ncapsets=%zu\n", (long long)C.n, P.rules.size(), (int)narrow, blob,
+            (unsigned)jobs.size(), blk, B.scan_blocks, B.dyn_bytes, wave_words, B.npairs, fuse_words, C.capset_add.size());
   }
   HIPCHK(hipStreamSynchronize(s));
   B.need = need_flags(P);
@@ -701,7 +718,10 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   auto& D = *cc->d;
   auto& PD = *P.dev;
   auto& B = D.bind;
-  hipStream_t s = dev->stream;
+  // timed launches are serialised on stream 0 so each kernel's events measure it alone
+  hipStream_t s = dev->timing || B.lane < 0 ? dev->stream : dev->lanes[B.lane];
+  if (B.last && B.last != s) HIPCHK(hipStreamSynchronize(B.last));  // keep this corpus's launches ordered
+  B.last = s;
   kpe_device::EvPair ev{};
   if (dev->timing) {
     ev.a = dev->get_ev();
@@ -894,7 +914,7 @@ kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kp
 kpe_status kpe_device_sync(kpe_device* dev) {
   if (!dev) return fail(KPE_E_INVALID, "null device");
   HIPCHK(hipSetDevice(dev->ordinal));
-  HIPCHK(hipStreamSynchronize(dev->stream));
+  for (int k = 0; k < dev->nlanes; ++k) HIPCHK(hipStreamSynchronize(dev->lanes[k]));
   return KPE_OK;
 }
 
@@ -906,7 +926,7 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
   auto& B = c->d->bind;
   if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
   size_t R = prog->p->rules.size(), cells = (size_t)c->c->n * R;
-  hipStream_t s = dev->stream;
+  hipStream_t s = B.last ? B.last : dev->stream;
   if (counts && R) {
     // per-rule totals from the verdict matrix (processor/result.go:34-68 counting)
     HIPCHK(kpe_launch_count(B.verdicts.as<uint8_t>(), c->c->n, (uint32_t)R, B.counts_out.as<unsigned long long>(), s));
@@ -967,7 +987,7 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
   if (!dev || !out) return fail(KPE_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(dev->mu);
   HIPCHK(hipSetDevice(dev->ordinal));
-  HIPCHK(hipStreamSynchronize(dev->stream));
+  for (int k = 0; k < dev->nlanes; ++k) HIPCHK(hipStreamSynchronize(dev->lanes[k]));
   for (auto& p : dev->pending) {
     float d1 = 0, d2 = 0, d3 = 0;
     HIPCHK(hipEventElapsedTime(&d1, p.a, p.b));
