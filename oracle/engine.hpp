@@ -22,6 +22,7 @@
 #include <string>
 #include <vector>
 
+#include "conditions.hpp"
 #include "json_dom.hpp"
 #include "k8s_typed.hpp"
 #include "pattern.hpp"
@@ -427,6 +428,15 @@ struct Rule {
   JPtr pattern, any_pattern;  // validate.pattern / validate.anyPattern (validate_resource.go:316-398)
   std::string pss_level, pss_version;
   std::vector<PSSExclude> pss_excludes;
+  cond::Conditions pre;   // rule.preconditions (engine.go:278-286)
+  cond::Conditions deny;  // validate.deny.conditions (validate_resource.go:268-279)
+  bool has_deny = false;
+  struct ForEach {        // validate.foreach entry with a deny (validate_resource.go:186-254)
+    cond::Query list;
+    cond::Conditions pre, deny;
+    int scope = -1;       // elementScope: -1 unset, 0 false, 1 true
+  };
+  std::vector<ForEach> foreach;
 };
 struct Policy {
   std::string name, ns;
@@ -737,8 +747,15 @@ inline Rule compile_rule(const JPtr& raw) {
     const JVal* deny = v->get("deny");
     const JVal* pt = v->get("pattern");
     const JVal* ap = v->get("anyPattern");
+    const JVal* fe = v->get("foreach");
     if (deny && !deny->is_null()) {
-      r.unsupported = true;  // deny conditions (JMESPath) are not restated yet
+      try {
+        r.deny = cond::parse_conditions(deny->get("conditions"));
+        r.has_deny = true;
+        cond::precompile(r.deny);
+      } catch (const cond::Unsupported&) {
+        r.unsupported = true;
+      }
     } else if (pt && !pt->is_null()) {
       r.pattern = deep_copy(*pt);
       if (pat::has_variables(*r.pattern)) r.unsupported = true;
@@ -746,11 +763,41 @@ inline Rule compile_rule(const JPtr& raw) {
       r.any_pattern = deep_copy(*ap);
       pat::numbers_to_float(*r.any_pattern);  // encoding/json round trip (validate_resource.go:400-416)
       if (pat::has_variables(*r.any_pattern)) r.unsupported = true;
-    } else if (jnonempty(v->get("foreach")) || jnonempty(v->get("cel"))) {
+    } else if (fe && fe->t == JT::Arr && !fe->a.empty()) {
+      try {
+        for (auto& e : fe->a) {
+          // only deny foreach entries (no nested foreach, patterns or context) are restated
+          if (e->t != JT::Obj || !e->get("deny") || jnonempty(e->get("pattern")) || jnonempty(e->get("anyPattern")) ||
+              jnonempty(e->get("foreach")) || jnonempty(e->get("context")))
+            throw cond::Unsupported("foreach entry");
+          Rule::ForEach f;
+          f.list = cond::compile_query(jstr(e->get("list")));
+          f.pre = cond::parse_conditions(e->get("preconditions"));
+          f.deny = cond::parse_conditions(e->get("deny")->get("conditions"));
+          cond::precompile(f.pre);
+          cond::precompile(f.deny);
+          const JVal* sc = e->get("elementScope");
+          if (sc && sc->t == JT::Bool) f.scope = sc->b ? 1 : 0;
+          r.foreach.push_back(std::move(f));
+        }
+      } catch (const cond::Unsupported&) {
+        r.unsupported = true;
+      } catch (const cond::EvalError&) {
+        r.unsupported = true;  // an unparsable list expression: not restated
+      }
+    } else if (jnonempty(v->get("cel"))) {
       r.unsupported = true;
     }
   }
-  if (jnonempty(raw->get("preconditions")) || jnonempty(raw->get("context"))) r.unsupported = r.has_validate;
+  if (jnonempty(raw->get("context"))) r.unsupported = r.has_validate;
+  if (jnonempty(raw->get("preconditions"))) {
+    try {
+      r.pre = cond::parse_conditions(raw->get("preconditions"));
+      cond::precompile(r.pre);
+    } catch (const cond::Unsupported&) {
+      r.unsupported = r.has_validate;
+    }
+  }
   return r;
 }
 inline Policy compile_policy(const JVal& p) {
@@ -896,6 +943,61 @@ inline Status pattern_handler(const Rule& r, const JVal& res) {
   return PASS;
 }
 
+// validate_resource.go:268-279 validateDeny: conditions true => FAIL, false => PASS, error => ERROR
+inline Status deny_handler(const Rule& r, const cond::Ctx& cx) {
+  try {
+    return cond::eval_conditions(r.deny, cx) ? FAIL : PASS;
+  } catch (const cond::EvalError&) {
+    return ERROR;
+  } catch (const cond::Unsupported&) {
+    return UNSUPPORTED;
+  }
+}
+// validate_resource.go:186-254 validateForEach / validateElements (deny entries), utils/foreach.go
+inline Status foreach_handler(const Rule& r, const cond::Ctx& cx) {
+  int apply_count = 0;
+  try {
+    for (auto& f : r.foreach) {
+      JPtr lst;
+      try {
+        lst = cond::run_query(f.list, cx.root);  // EvaluateList
+      } catch (const cond::NotFound&) {
+        continue;  // "failed to evaluate list": the entry is skipped
+      } catch (const cond::EvalError&) {
+        continue;
+      }
+      std::vector<JPtr> elems;
+      if (!cond::is_null(lst) && lst->t == JT::Arr) elems = lst->a;
+      else elems = {lst};
+      int count = 0;
+      for (size_t idx = 0; idx < elems.size(); ++idx) {
+        const JPtr& el = elems[idx];
+        if (cond::is_null(el)) continue;
+        if (f.scope == 1 && el->t != JT::Obj) return ERROR;  // AddElementToContext error
+        cond::Ctx ex{cond::with_element(cx.root, el, (int64_t)idx)};
+        Status st;
+        try {
+          if (f.pre.present && !cond::eval_conditions(f.pre, ex)) st = SKIP;
+          else st = cond::eval_conditions(f.deny, ex) ? FAIL : PASS;
+        } catch (const cond::EvalError&) {
+          st = f.pre.present ? ERROR : ERROR;
+        }
+        if (st == SKIP) continue;
+        if (st == ERROR) {
+          if (idx + 1 < elems.size()) continue;
+          return ERROR;
+        }
+        if (st == FAIL) return FAIL;
+        ++count;
+      }
+      apply_count += count;
+    }
+  } catch (const cond::Unsupported&) {
+    return UNSUPPORTED;
+  }
+  return apply_count == 0 ? NA : PASS;
+}
+
 // validate_pss.go:31-112 (no exceptions, CREATE operation)
 inline Status pss_handler(const Rule& r, const JVal& res, const std::string& kind) {
   Pod pod;
@@ -926,15 +1028,34 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
   }
   MatchCtx c{u, gvk_of(u), ns_labels};
   int applied = 0;
+  cond::Ctx cx;  // JSON context, built on first use
   for (size_t i = 0; i < p.rules.size(); ++i) {
     const Rule& r = p.rules[i];
     if (!matches_resource_description(r, p, c)) continue;
     if (!r.has_validate) continue;  // handler factory returns nil => no response
     Status s;
-    if (r.unsupported) s = UNSUPPORTED;
-    else if (r.has_pss) s = pss_handler(r, res, u.kind());
-    else if (r.pattern || r.any_pattern) s = pattern_handler(r, res);
-    else s = NA;
+    if (r.unsupported) {
+      s = UNSUPPORTED;
+    } else {
+      if ((r.pre.present || r.has_deny || !r.foreach.empty()) && !cx.root) cx.root = cond::request_context(res);
+      s = NA;
+      bool done = false;
+      if (r.pre.present) {  // engine.go:278-286: error => ERROR, false => SKIP
+        try {
+          if (!cond::eval_conditions(r.pre, cx)) s = SKIP, done = true;
+        } catch (const cond::EvalError&) {
+          s = ERROR, done = true;
+        } catch (const cond::Unsupported&) {
+          s = UNSUPPORTED, done = true;
+        }
+      }
+      if (!done) {
+        if (r.has_pss) s = pss_handler(r, res, u.kind());
+        else if (r.has_deny) s = deny_handler(r, cx);
+        else if (r.pattern || r.any_pattern) s = pattern_handler(r, res);
+        else if (!r.foreach.empty()) s = foreach_handler(r, cx);
+      }
+    }
     out[i] = s;
     if (s == PASS || s == FAIL) ++applied;
     if (p.apply_one && applied > 0) break;

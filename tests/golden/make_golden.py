@@ -405,6 +405,49 @@ def cli_cases():
     return out
 
 
+def engine_validate_cases():
+    """pkg/engine/validation_test.go: every test whose policy / resource are raw JSON
+    literals and whose expectation is a rule status (testForEach, :3170-3185), the
+    success of the whole response (er.IsSuccessful()) or a status table (Flux, :1997-2054)."""
+    path = os.path.join(REF, "pkg/engine/validation_test.go")
+    src = open(path).read()
+    out = []
+    funcs = [(m.start(), m.group(1)) for m in re.finditer(r"^func (Test\w+)\(t \*testing\.T\)", src, re.M)]
+    funcs.append((len(src), None))
+    for (a, name), (b, _) in zip(funcs, funcs[1:]):
+        body = src[a:b]
+        line = src.count("\n", 0, a) + 1
+        if "kyvernov1.Create" not in body and "testForEach" not in body:
+            continue
+        raws = {}
+        for m in re.finditer(r"(\w+)\s*:?=\s*\[\]byte\(`(.*?)`\)", body, re.S):
+            raws[m.group(1).lower()] = m.group(2)
+        def load(txt):
+            try:
+                return json.loads(txt)
+            except ValueError:
+                return None
+        if "expectedResults" in body and "policyRaw:" in body:  # status table
+            for i, m in enumerate(re.finditer(r"policyRaw:\s*\[\]byte\(`(.*?)`\),.*?resourceRaw:\s*\[\]byte\(`(.*?)`\),"
+                                              r".*?expectedResults:\s*\[\]engineapi\.RuleStatus\{(.*?)\}", body, re.S)):
+                pol, res = load(m.group(1)), load(m.group(2))
+                st = [x.strip().replace("engineapi.RuleStatus", "").lower() for x in m.group(3).split(",") if x.strip()]
+                if pol and res:
+                    out.append({"name": f"{name}[{i}]", "line": line, "policy": pol, "resource": res, "statuses": st})
+            continue
+        pol, res = load(raws.get("policyraw", "")), load(raws.get("resourceraw", ""))
+        if not pol or not res:
+            continue
+        m = re.search(r"testForEach\(t, policyraw, resourceRaw, \"[^\"]*\", engineapi\.RuleStatus(\w+)", body)
+        if m:
+            out.append({"name": name, "line": line, "policy": pol, "resource": res, "first": m.group(1).lower()})
+        elif "assert.Assert(t, !er.IsSuccessful())" in body:
+            out.append({"name": name, "line": line, "policy": pol, "resource": res, "successful": False})
+        elif "assert.Assert(t, er.IsSuccessful())" in body:
+            out.append({"name": name, "line": line, "policy": pol, "resource": res, "successful": True})
+    return out
+
+
 def _render_chart_template(text):
     name = re.search(r'\$name := "([^"]+)"', text).group(1)
     out, stack = [], []  # stack of "branch active" flags
@@ -423,12 +466,13 @@ def _render_chart_template(text):
             continue
         if line.strip().startswith("{{"):
             continue  # `{{- $x := ... }}`, `{{- include ... }}`
-        line = re.sub(r"\{\{`(.*?)`\}\}", lambda m: m.group(1), line)
         line = line.replace("{{ .Values.policyKind }}", "ClusterPolicy").replace("{{ $name }}", name)
         line = line.replace("{{ .Values.validationFailureAction }}", "Audit")
         line = line.replace("{{ .Values.background }}", "true").replace("{{ .Values.failurePolicy }}", "Fail")
-        if "{{" in line:
+        if "{{" in re.sub(r"\{\{`(.*?)`\}\}", "", line):
             continue  # labels / severity includes: metadata only
+        # {{`...`}} is helm's escape for a literal kyverno variable: keep the inside
+        line = re.sub(r"\{\{`(.*?)`\}\}", lambda m: m.group(1), line)
         out.append(line)
     return yaml.load("\n".join(out), Loader=_GoYamlLoader)
 
@@ -444,6 +488,7 @@ def chart_policies():
 
 if __name__ == "__main__":
     _dump("chart_policies.json", chart_policies())
+    _dump("engine_validate_cases.json", engine_validate_cases())
     _dump("cli_cases.json", cli_cases())
     _dump("pattern_leaf_cases.json", pattern_leaf_cases())
     _dump("pattern_tree_cases.json", pattern_tree_cases())

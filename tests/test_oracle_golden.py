@@ -243,3 +243,27 @@ def test_cli_golden(oracle, case):
             assert want in ("skip", "fail") or not validating, (case["resources"][i]["metadata"]["name"], want)
             continue
         assert got == want, (case["resources"][i]["metadata"]["name"], cols, got, want)
+
+
+ENGINE = _load("engine_validate_cases.json")
+
+
+@pytest.mark.parametrize("case", ENGINE, ids=[c["name"] for c in ENGINE])
+def test_engine_validate_golden(oracle, case):
+    """pkg/engine/validation_test.go deny / foreach / precondition cases (extracted by
+    make_golden.engine_validate_cases): the response's rule statuses, its first rule's
+    status (testForEach) or IsSuccessful(). Cases needing constructs outside the restated
+    subset (custom JMESPath functions, context entries) answer `unsupported` and are skipped."""
+    from tests.oracle_lib import STATUS
+
+    nd = (json.dumps(case["resource"]) + "\n").encode()
+    M = oracle.validate([case["policy"]], nd)
+    got = [STATUS[int(x)] for x in M[0] if STATUS[int(x)] != "na"]
+    if "unsupported" in got:
+        pytest.skip("outside the restated subset")
+    if "statuses" in case:
+        assert got == case["statuses"]
+    elif "first" in case:
+        assert got and got[0] == case["first"]
+    else:
+        assert (not any(g in ("fail", "error") for g in got)) == case["successful"]
