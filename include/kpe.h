@@ -129,6 +129,28 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
 const char* kpe_pss_check_id(int k);
 int kpe_pss_num_checks(void);
 
+/* Versioned-check form of the check masks (after kpe_evaluate / kpe_evaluate_async with
+ * masks): N x R uint32, bit v = PSA versioned check v failed (0 unless the cell is FAIL).
+ * A rule pinned to a version runs every version of a check up to it
+ * (pkg/pss/evaluate.go:51-66, evaluatePSS), so one check id can fail more than once;
+ * kpe_pss_cv_check(v) is the check id index of versioned check v. */
+kpe_status kpe_fetch_cv_masks(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint32_t* cv_masks);
+int kpe_pss_num_cv(void);
+int kpe_pss_cv_check(int v);
+
+/* PolicyReport results of one resource (pkg/utils/report/results.go:89-156,
+ * EngineResponseToReportResults), as the JSON array encoding/json writes for
+ * []PolicyReportResult: one object per rule with a response, in rule order, with
+ * source, policy (cache.MetaNamespaceKeyFunc key), rule, result (unscored fail => warn),
+ * scored, properties {controls, standard, version} for failing podSecurity rules,
+ * category and severity. message and timestamp are not produced.
+ *   verdict_row : R verdict cells of the resource (kpe_evaluate row)
+ *   cv_mask_row : R cells of kpe_fetch_cv_masks, or NULL (then no controls)
+ * Writes at most cap-1 bytes plus NUL; returns the full length (call again with a larger
+ * buffer when it is >= cap), or a negative kpe_status. Host only; no device call. */
+long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row, char* buf,
+                        size_t cap);
+
 /* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
 typedef struct kpe_kernel_stats {
   uint64_t launches;        /* evaluations timed since the last reset           */

@@ -16,6 +16,7 @@ from .engine import (  # noqa: F401
     PolicySet,
     RuleResponse,
     RuleStatus,
+    report_results,
     synth_ns_labels,
     synth_resources,
 )
@@ -30,6 +31,7 @@ __all__ = [
     "PolicySet",
     "RuleResponse",
     "RuleStatus",
+    "report_results",
     "synth_ns_labels",
     "synth_resources",
     "load",

@@ -62,6 +62,10 @@ def load():
     L.kpe_fetch.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_pss_check_id.argtypes = [i32]
     L.kpe_pss_check_id.restype = cp
+    L.kpe_fetch_cv_masks.argtypes = [vp, vp, vp, vp]
+    L.kpe_pss_cv_check.argtypes = [i32]
+    L.kpe_report_results.argtypes = [vp, vp, vp, ctypes.c_char_p, sz]
+    L.kpe_report_results.restype = ctypes.c_long
     L.kpe_device_set_timing.argtypes = [vp, i32]
     L.kpe_device_kernel_stats.argtypes = [vp, vp, vp, ctypes.POINTER(KernelStats), i32]
     L.kpe_synth_resources.argtypes = [ctypes.c_uint64, i64, i64, i32, ctypes.POINTER(ctypes.c_void_p),

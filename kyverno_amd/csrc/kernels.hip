@@ -145,11 +145,6 @@ constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
 
-__constant__ uint8_t kCvCheck[KPE_NUM_CV] = {
-    CK_APE, CK_APE, CK_APPARMOR, CK_CAPS_BASELINE, CK_CAPS_RESTRICTED, CK_CAPS_RESTRICTED, CK_HOST_NS,
-    CK_HOST_PATH, CK_HOST_PORTS, CK_PRIVILEGED, CK_PROC_MOUNT, CK_RESTRICTED_VOLUMES, CK_RUN_AS_NON_ROOT,
-    CK_RUN_AS_USER, CK_SELINUX, CK_SECCOMP_BASELINE, CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED,
-    CK_SECCOMP_RESTRICTED, CK_SYSCTLS, CK_SYSCTLS, CK_SYSCTLS, CK_WIN_HOST_PROCESS};
 
 // Capability-set violation bits (computed per block into LDS from the capset dictionary)
 #define CS_BASE 1u  // add has a capability outside the baseline allow-list
@@ -532,13 +527,6 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
   return ok;
 }
 
-__device__ __forceinline__ uint32_t check_mask(uint32_t f) {  // versioned checks -> PSA check ids
-  uint32_t cmask = 0;
-#pragma unroll 1
-  for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv)
-    if (f & (1u << cv)) cmask |= 1u << kCvCheck[cv];
-  return cmask;
-}
 
 // Store a tile's staged row segments [c0, c0 + nc) of R-byte rows.
 __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv, uint32_t tile, uint32_t R,
@@ -825,7 +813,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
         if ((x & NR_APPLY_ONE) && applied) v = KPE_NA_;
         applied |= v == KPE_PASS_ || v == KPE_FAIL_;
         sv[lane * R + ri] = (uint8_t)v;
-        if (a.masks && live) a.masks[(size_t)r * R + ri] = v == KPE_FAIL_ ? check_mask(fails & nr.y) : 0u;
+        if (a.masks && live) a.masks[(size_t)r * R + ri] = v == KPE_FAIL_ ? (fails & nr.y) : 0u;
       }
       __builtin_amdgcn_wave_barrier();
       prev_tile = tile, prev_rows = nrows, buf ^= 1u;
@@ -924,7 +912,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
       if (a.masks && live) {
 #pragma unroll 1
         for (uint32_t j = 0; j < nc; ++j) {
-          const uint32_t cm = ((rmk[j * 3 + 1] >> lane) & 1u) ? check_mask(fails & sld(a.rules, c0 + j).cv_mask) : 0u;
+          const uint32_t cm = ((rmk[j * 3 + 1] >> lane) & 1u) ? (fails & sld(a.rules, c0 + j).cv_mask) : 0u;
           a.masks[(size_t)r * R + c0 + j] = cm;
         }
       }

@@ -151,7 +151,7 @@ struct ScanArgs {
   uint32_t cv_union, need;
   // outputs
   uint8_t* verdicts;  // n x nrules
-  uint32_t* masks;    // n x nrules or null
+  uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null
 };
 
 // kpe_pattern_kernel arguments (device-resident, one copy per binding)

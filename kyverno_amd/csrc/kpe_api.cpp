@@ -918,8 +918,22 @@ kpe_status kpe_device_sync(kpe_device* dev) {
   return KPE_OK;
 }
 
-kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
-                     uint32_t* masks, kpe_counts* counts) {
+static const uint8_t kCvCheck[KPE_NUM_CV] = KPE_CV_CHECK_TABLE;
+
+// The scan kernel stores failing versioned checks; the public masks are per PSA check id.
+static void cv_to_check_masks(uint32_t* m, size_t cells) {
+  for (size_t i = 0; i < cells; ++i) {
+    uint32_t f = m[i], c = 0;
+    while (f) {
+      c |= 1u << kCvCheck[__builtin_ctz(f)];
+      f &= f - 1;
+    }
+    m[i] = c;
+  }
+}
+
+static kpe_status fetch_impl(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
+                             uint32_t* masks, kpe_counts* counts, bool raw_cv) {
   if (!dev || !prog || !c || !c->d) return fail(KPE_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(dev->mu);
   HIPCHK(hipSetDevice(dev->ordinal));
@@ -950,8 +964,19 @@ kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus*
   if (masks && cells) {
     if (!c->d->has_masks) return fail(KPE_E_STATE, "check masks were not computed");
     HIPCHK(hipMemcpy(masks, B.masks.p, cells * 4, hipMemcpyDeviceToHost));
+    if (!raw_cv) cv_to_check_masks(masks, cells);
   }
   return KPE_OK;
+}
+
+kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
+                     uint32_t* masks, kpe_counts* counts) {
+  return fetch_impl(dev, prog, c, verdicts, masks, counts, false);
+}
+
+kpe_status kpe_fetch_cv_masks(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint32_t* cv_masks) {
+  if (!cv_masks) return fail(KPE_E_INVALID, "null cv_masks");
+  return fetch_impl(dev, prog, c, nullptr, cv_masks, nullptr, true);
 }
 
 kpe_status kpe_evaluate(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
@@ -974,6 +999,97 @@ static const char* const kCheckIds[KPE_NUM_CHECKS] = {
     "sysctls", "windowsHostProcess"};
 const char* kpe_pss_check_id(int k) { return (k >= 0 && k < KPE_NUM_CHECKS) ? kCheckIds[k] : nullptr; }
 int kpe_pss_num_checks(void) { return KPE_NUM_CHECKS; }
+int kpe_pss_num_cv(void) { return KPE_NUM_CV; }
+int kpe_pss_cv_check(int v) { return (v >= 0 && v < KPE_NUM_CV) ? (int)kCvCheck[v] : -1; }
+
+static void json_str(std::string& o, const std::string& s) {  // encoding/json string escaping
+  static const char* hx = "0123456789abcdef";
+  o += '"';
+  for (unsigned char ch : s) {
+    if (ch == '"' || ch == '\\') {
+      o += '\\';
+      o += (char)ch;
+    } else if (ch == '\n') {
+      o += "\\n";
+    } else if (ch == '\r') {
+      o += "\\r";
+    } else if (ch == '\t') {
+      o += "\\t";
+    } else if (ch < 0x20 || ch == '<' || ch == '>' || ch == '&') {
+      o += "\\u00";
+      o += hx[ch >> 4];
+      o += hx[ch & 15];
+    } else {
+      o += (char)ch;
+    }
+  }
+  o += '"';
+}
+
+// pkg/utils/report/results.go:89-156 (EngineResponseToReportResults) for one resource row,
+// over every policy of the program; toPolicyResult results.go:56-71.
+long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row, char* buf,
+                        size_t cap) {
+  if (!prog || !verdict_row) {
+    fail(KPE_E_INVALID, "null argument");
+    return -KPE_E_INVALID;
+  }
+  static const char* const kResult[6] = {nullptr, "pass", "fail", "warn", "error", "skip"};
+  const kpe::Program& P = *prog->p;
+  std::string o = "[";
+  bool first = true;
+  for (size_t r = 0; r < P.rules.size(); ++r) {
+    const uint8_t v = verdict_row[r];
+    if (v == KPE_NA || v > KPE_SKIP) continue;  // no RuleResponse
+    const kpe::RuleReport& rr = P.reports[r];
+    const char* res = kResult[v];
+    if (v == KPE_FAIL && !rr.scored) res = "warn";  // results.go:131-133
+    o += first ? "{" : ",{";
+    first = false;
+    o += "\"source\":\"kyverno\",\"policy\":";
+    json_str(o, rr.policy_key);
+    if (!rr.rule.empty()) {
+      o += ",\"rule\":";
+      json_str(o, rr.rule);
+    }
+    o += ",\"result\":\"";
+    o += res;
+    o += '"';
+    if (rr.scored) o += ",\"scored\":true";
+    // results.go:114-129: failing check ids (one per failing versioned check), sorted
+    const uint32_t f = (rr.pss && v == KPE_FAIL && cv_mask_row) ? cv_mask_row[r] : 0u;
+    if (f) {
+      std::vector<std::string> ids;
+      for (uint32_t b = f; b; b &= b - 1) ids.push_back(kCheckIds[kCvCheck[__builtin_ctz(b)]]);
+      std::sort(ids.begin(), ids.end());
+      std::string ctl;
+      for (auto& id : ids) ctl += (ctl.empty() ? "" : ",") + id;
+      o += ",\"properties\":{\"controls\":";
+      json_str(o, ctl);
+      o += ",\"standard\":";
+      json_str(o, rr.pss_level);
+      o += ",\"version\":";
+      json_str(o, rr.pss_version);
+      o += '}';
+    }
+    if (!rr.category.empty()) {
+      o += ",\"category\":";
+      json_str(o, rr.category);
+    }
+    if (!rr.severity.empty()) {
+      o += ",\"severity\":";
+      json_str(o, rr.severity);
+    }
+    o += '}';
+  }
+  o += ']';
+  if (buf && cap > 0) {
+    const size_t n = std::min(o.size(), cap - 1);
+    memcpy(buf, o.data(), n);
+    buf[n] = 0;
+  }
+  return (long)o.size();
+}
 
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled) {
   if (!dev) return fail(KPE_E_INVALID, "null device");

@@ -1277,6 +1277,14 @@ class Lowerer {
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
     P.rule_names.push_back(pol_name + "/" + rname);
+    RuleReport rr;
+    rr.rule = rname;
+    if (ps && ps->t == JV::Obj && nonempty(ps)) {
+      rr.pss = true;
+      rr.pss_level = sv(ps->get("level"));
+      rr.pss_version = sv(ps->get("version"));
+    }
+    P.reports.push_back(std::move(rr));
   }
 
  private:
@@ -1305,7 +1313,20 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len) {
     bool namespaced = sv(p.get("kind")) == "Policy";
     const JV* spec = p.get("spec");
     bool apply_one = spec && sv(spec->get("applyRules")) == "One";
+    const size_t r0 = prog->reports.size();
     for (auto& r : compute_rules(p)) L.rule(r, (uint32_t)pi, apply_one, name, namespaced, ns);
+    // results.go:94-108: policy key, scored / category / severity annotations
+    const JV* ann = meta ? meta->get("annotations") : nullptr;
+    auto annv = [&](const char* k) { return ann ? sv(ann->get(k)) : std::string(); };
+    std::string sev = annv("policies.kyverno.io/severity");
+    if (sev != "critical" && sev != "high" && sev != "medium" && sev != "low" && sev != "info") sev.clear();
+    for (size_t i = r0; i < prog->reports.size(); ++i) {
+      RuleReport& rr = prog->reports[i];
+      rr.policy_key = ns.empty() ? name : ns + "/" + name;
+      rr.scored = annv("policies.kyverno.io/scored") != "false";
+      rr.category = annv("policies.kyverno.io/category");
+      rr.severity = sev;
+    }
   }
   return prog;
 }

@@ -45,8 +45,21 @@ struct PssPreds {
 
 struct DeviceProgram;  // kpe_api.cpp
 
+// What a PolicyReportResult carries for rule r besides its verdict
+// (pkg/utils/report/results.go:89-156, EngineResponseToReportResults).
+struct RuleReport {
+  std::string policy_key;  // cache.MetaNamespaceKeyFunc: "<ns>/<name>" or "<name>"
+  std::string rule;        // rule name after autogen
+  std::string category;    // policies.kyverno.io/category
+  std::string severity;    // SeverityFromString(policies.kyverno.io/severity)
+  std::string pss_level, pss_version;  // podSecurity rules: PodSecurityChecks.Level / Version
+  bool scored = true;      // policies.kyverno.io/scored != "false"
+  bool pss = false;
+};
+
 struct Program {
   std::vector<std::string> rule_names;  // "<policy>/<rule>"
+  std::vector<RuleReport> reports;      // per rule, same order
   std::vector<KpeRule> rules;
   std::vector<KpeFilter> filters;
   std::vector<uint32_t> fterms;  // term indices of the filters

@@ -244,6 +244,15 @@ enum KpeCheckVersion {
   KPE_NUM_CV
 };
 
+// PSA check of each versioned check (KpeCheckVersion -> KpeCheck); shared by the device
+// (per-ID check masks) and the host (report `controls`, one entry per failing versioned check).
+#define KPE_CV_CHECK_TABLE                                                                              \
+  {CK_APE,           CK_APE,           CK_APPARMOR,          CK_CAPS_BASELINE,      CK_CAPS_RESTRICTED, \
+   CK_CAPS_RESTRICTED, CK_HOST_NS,     CK_HOST_PATH,         CK_HOST_PORTS,         CK_PRIVILEGED,      \
+   CK_PROC_MOUNT,    CK_RESTRICTED_VOLUMES, CK_RUN_AS_NON_ROOT, CK_RUN_AS_USER,     CK_SELINUX,         \
+   CK_SECCOMP_BASELINE, CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED, CK_SECCOMP_RESTRICTED, CK_SYSCTLS,    \
+   CK_SYSCTLS,       CK_SYSCTLS,       CK_WIN_HOST_PROCESS}
+
 // ---- per-container derived violation bits (device-internal) ------------------------------------
 #define CB_APE (1u << 0)            // sc nil || ape nil || ape true
 #define CB_CAPS_BASE (1u << 1)      // caps present && add has a non-baseline capability

@@ -222,6 +222,14 @@ class Engine:
                for c in counts[:R]]
         return v, m, cnt
 
+    def cv_masks(self, ps: PolicySet, corpus: Corpus):
+        """Failing versioned PSS checks (N x R uint32, bit v = kpe_pss_cv_check(v)) of the last
+        evaluation with check_masks=True (kpe_fetch_cv_masks)."""
+        m = np.zeros((corpus.n, ps.num_rules), dtype=np.uint32)
+        if m.size:
+            check(load().kpe_fetch_cv_masks(self.device.h, ps.h, corpus.h, m.ctypes.data))
+        return m
+
     def evaluate_async(self, ps: PolicySet, corpus: Corpus):
         check(load().kpe_evaluate_async(self.device.h, ps.h, corpus.h))
 
@@ -267,3 +275,22 @@ class Engine:
         if ns and policy_context.namespace_labels:
             nsl = {ns: policy_context.namespace_labels}
         return self.validate_batch([policy_context.policy], [policy_context.resource], nsl)[0][0]
+
+
+def report_results(ps: PolicySet, verdict_row, cv_mask_row=None) -> List[dict]:
+    """EngineResponseToReportResults (pkg/utils/report/results.go:89-156) for one resource row,
+    through kpe_report_results (message and timestamp are not produced)."""
+    L = load()
+    v = np.ascontiguousarray(verdict_row, dtype=np.uint8)
+    m = None if cv_mask_row is None else np.ascontiguousarray(cv_mask_row, dtype=np.uint32)
+    if v.size != ps.num_rules or (m is not None and m.size != ps.num_rules):
+        raise ValueError("row length != number of rules")
+    cap = 4096
+    while True:
+        buf = ctypes.create_string_buffer(cap)
+        n = L.kpe_report_results(ps.h, v.ctypes.data, None if m is None else m.ctypes.data, buf, cap)
+        if n < 0:
+            check(-n)
+        if n < cap:
+            return json.loads(buf.value.decode())
+        cap = n + 1

@@ -1,0 +1,90 @@
+"""Oracle (TEST INFRASTRUCTURE ONLY — imported by tests/, never by the product path):
+PolicyReport results of one resource, a pure-Python restatement of
+EngineResponseToReportResults (pkg/utils/report/results.go:89-156) over the oracle's
+verdict cells and its failing PSA check list (oracle/pss.hpp evaluate_pss, which keeps one
+entry per failing versioned check, pkg/pss/evaluate.go:24-70).
+
+Restated:
+  - policy key: cache.MetaNamespaceKeyFunc -> "<ns>/<name>" or "<name>" (results.go:93)
+  - scored: annotation policies.kyverno.io/scored != "false"; category / severity from
+    policies.kyverno.io/{category,severity}, SeverityFromString (results.go:73-87, 96-107)
+  - toPolicyResult (results.go:56-71); unscored fail => warn (results.go:131-133)
+  - properties {standard, version, controls}: failing check ids sorted and comma-joined,
+    only when at least one check failed (results.go:114-129); PodSecurityChecks.Level /
+    Version are the rule's raw podSecurity strings (validate_pss.go:79-82)
+  - JSON omitempty of PolicyReportResult (api/policyreport/v1alpha2/common.go:93-137)
+Not restated: message and timestamp (message text is SURVEY.md 8(f) rank 1), exception
+and ValidatingAdmissionPolicy branches (out of the path's scope).
+Autogen rules are mapped back to their source rule by the "autogen-" / "autogen-cronjob-"
+prefix (pkg/autogen/autogen.go:213-222); names truncated to 63 characters are not mapped
+(the fixtures used have short names).
+"""
+from typing import Callable, Dict, List, Optional
+
+RESULT = {1: "pass", 2: "fail", 3: "warn", 4: "error", 5: "skip"}
+SEVERITIES = ("critical", "high", "medium", "low", "info")
+_POD_PATH = {  # validate_pss.go:137-188 getSpec
+    "Pod": (),
+    "CronJob": ("spec", "jobTemplate", "spec", "template"),
+}
+_TEMPLATE_KINDS = ("DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController")
+
+
+def pod_of(resource: dict) -> Optional[dict]:
+    """The Pod (metadata + spec) a podSecurity rule evaluates for this resource."""
+    kind = resource.get("kind")
+    path = _POD_PATH.get(kind, ("spec", "template") if kind in _TEMPLATE_KINDS else None)
+    if path is None:
+        return None
+    node = resource
+    for k in path:
+        node = (node or {}).get(k)
+    node = node or {}
+    return {"kind": "Pod", "metadata": node.get("metadata") or {}, "spec": node.get("spec") or {}}
+
+
+def _source_rule(policy: dict, rule_name: str) -> dict:
+    rules = {r.get("name"): r for r in (policy.get("spec") or {}).get("rules") or []}
+    for prefix in ("autogen-cronjob-", "autogen-", ""):
+        if rule_name.startswith(prefix) and rule_name[len(prefix):] in rules:
+            return rules[rule_name[len(prefix):]]
+    return {}
+
+
+def report_results(policies: List[dict], rule_names: List[str], verdict_row, resource: dict,
+                   failing_checks: Callable[[str, str, dict], List[str]]) -> List[Dict]:
+    """[]PolicyReportResult for one resource over all policies (rules in rule_names order)."""
+    by_name = {p["metadata"]["name"]: p for p in policies}
+    out = []
+    for r, full in enumerate(rule_names):
+        cell = int(verdict_row[r])
+        if cell not in RESULT:
+            continue  # no RuleResponse
+        pname, rname = full.split("/", 1)
+        pol = by_name[pname]
+        meta = pol.get("metadata") or {}
+        ann = meta.get("annotations") or {}
+        ns = meta.get("namespace") or ""
+        scored = ann.get("policies.kyverno.io/scored") != "false"
+        res = RESULT[cell]
+        if res == "fail" and not scored:
+            res = "warn"
+        item = {"source": "kyverno", "policy": f"{ns}/{pname}" if ns else pname}
+        if rname:
+            item["rule"] = rname
+        item["result"] = res
+        if scored:
+            item["scored"] = True
+        ps = ((_source_rule(pol, rname).get("validate") or {}).get("podSecurity"))
+        if ps and cell == 2:
+            controls = sorted(failing_checks(ps.get("level", ""), ps.get("version", ""), pod_of(resource)))
+            if controls:
+                item["properties"] = {"controls": ",".join(controls), "standard": ps.get("level", ""),
+                                      "version": ps.get("version", "")}
+        if ann.get("policies.kyverno.io/category"):
+            item["category"] = ann["policies.kyverno.io/category"]
+        sev = ann.get("policies.kyverno.io/severity", "")
+        if sev in SEVERITIES:
+            item["severity"] = sev
+        out.append(item)
+    return out

@@ -1,0 +1,134 @@
+"""PolicyReport results (pkg/utils/report/results.go:89-156).
+
+CPU: the oracle restatement (oracle/report.py) is pinned by the chainsaw background-report
+fixture; kpe_report_results (host formatting over a verdict row) is checked against it
+with oracle verdict rows. GPU: verdicts and versioned check masks from the scan kernel,
+formatted by kpe_report_results, equal the oracle's results field for field."""
+import copy
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import kyverno_amd as K
+from tests.policies import parity_policy_set
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(__file__)), "oracle"))
+import report as oracle_report  # noqa: E402  (test infrastructure)
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _no_message(results):
+    return [{k: v for k, v in r.items() if k not in ("message", "timestamp")} for r in results]
+
+
+def report_policy_set():
+    """parity_policy_set with report annotations: scored=false (fail => warn), category,
+    valid and invalid severities."""
+    pols = copy.deepcopy(parity_policy_set())
+    for i, p in enumerate(pols):
+        ann = {}
+        if i % 3 == 0:
+            ann["policies.kyverno.io/category"] = "Pod Security <Standards> & \"more\""
+        if i % 4 == 1:
+            ann["policies.kyverno.io/severity"] = ("high", "medium", "low", "critical", "info", "bogus")[i % 6]
+        if i % 5 == 2:
+            ann["policies.kyverno.io/scored"] = "false"
+        if ann:
+            p["metadata"]["annotations"] = ann
+    return pols
+
+
+def test_oracle_pinned_by_background_report(oracle):
+    bg = json.load(open(os.path.join(GOLD, "background_report.json")))
+    names = oracle.rule_names([bg["policy"]])
+    v = oracle.validate([bg["policy"]], json.dumps(bg["resource"]).encode())
+    got = oracle_report.report_results([bg["policy"]], names, v[0], bg["resource"], oracle.failing_checks)
+    assert got == _no_message(bg["results"])  # report-assert.yaml, message aside
+
+
+def test_host_report_matches_oracle_without_controls(oracle):
+    pols = report_policy_set()
+    ps = K.PolicySet(pols)
+    names = oracle.rule_names(pols)
+    assert names == ps.rule_names
+    nd = K.synth_resources(7, 400, mix=2)
+    docs = [json.loads(x) for x in nd.split(b"\n") if x.strip()]
+    v = oracle.validate(pols, nd, nthreads=4)
+    seen = set()
+    for i, doc in enumerate(docs):
+        want = oracle_report.report_results(pols, names, v[i], doc, lambda *a: [])
+        got = K.report_results(ps, v[i])
+        assert got == want, i
+        seen.update(r["result"] for r in got)
+    assert {"pass", "fail", "warn", "error"} <= seen
+
+
+def test_host_report_versioned_controls():
+    """A baseline:v1.19 rule runs seccompProfile_baseline at 1.0 (annotations) and 1.19
+    (fields); both failing lists the id twice (pkg/pss/evaluate.go:51-66)."""
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "Policy",
+           "metadata": {"name": "p", "namespace": "team-a"},
+           "spec": {"rules": [{"name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                               "validate": {"podSecurity": {"level": "baseline", "version": "v1.19"}}}]}}
+    ps = K.PolicySet([pol])
+    L = K.load()
+    ids = [L.kpe_pss_check_id(L.kpe_pss_cv_check(c)).decode() for c in range(L.kpe_pss_num_cv())]
+    bits = [c for c, x in enumerate(ids) if x == "seccompProfile_baseline"]
+    hp = ids.index("hostPorts")
+    assert len(bits) == 2
+    row_v = np.array([2] + [0] * (ps.num_rules - 1), dtype=np.uint8)
+    row_m = np.zeros(ps.num_rules, dtype=np.uint32)
+    row_m[0] = (1 << bits[0]) | (1 << bits[1]) | (1 << hp)
+    got = K.report_results(ps, row_v, row_m)
+    assert got == [{"source": "kyverno", "policy": "team-a/p", "rule": "r", "result": "fail", "scored": True,
+                    "properties": {"controls": "hostPorts,seccompProfile_baseline,seccompProfile_baseline",
+                                   "standard": "baseline", "version": "v1.19"}}]
+    # no response => no result; masks ignored for non-fail cells
+    assert K.report_results(ps, np.zeros(ps.num_rules, np.uint8), row_m) == []
+    row_v[0] = 1
+    assert "properties" not in K.report_results(ps, row_v, row_m)[0]
+
+
+@pytest.mark.gpu
+def test_gpu_report_background_fixture():
+    bg = json.load(open(os.path.join(GOLD, "background_report.json")))
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet([bg["policy"]])
+    c = K.Corpus(json.dumps(bg["resource"]).encode())
+    v, _, _ = eng.evaluate(ps, c, check_masks=True)
+    m = eng.cv_masks(ps, c)
+    assert K.report_results(ps, v[0], m[0]) == _no_message(bg["results"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix,n,seed", [(0, 3000, 0xC2), (2, 3000, 21)])
+def test_gpu_report_matches_oracle(oracle, mix, n, seed):
+    pols = report_policy_set()
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(seed, n, mix=mix)
+    c = K.Corpus(nd)
+    v, masks, _ = eng.evaluate(ps, c, check_masks=True)
+    cv = eng.cv_masks(ps, c)
+    L = K.load()
+    cv_check = [L.kpe_pss_cv_check(b) for b in range(L.kpe_pss_num_cv())]
+    folded = np.zeros_like(cv)
+    for b, k in enumerate(cv_check):  # the per-id masks are the OR of the versioned ones
+        folded |= ((cv >> np.uint32(b)) & np.uint32(1)) << np.uint32(k)
+    assert (folded == masks).all()
+    names = oracle.rule_names(pols)
+    docs = [json.loads(x) for x in nd.split(b"\n") if x.strip()]
+    ref = oracle.validate(pols, nd, nthreads=8)
+    assert (v == ref).all()
+    dup = 0
+    for i in range(0, n, 3):
+        want = oracle_report.report_results(pols, names, ref[i], docs[i], oracle.failing_checks)
+        got = K.report_results(ps, v[i], cv[i])
+        assert got == want, (i, got, want)
+        dup += sum(1 for r in got if "properties" in r and len(set(r["properties"]["controls"].split(","))) <
+                   len(r["properties"]["controls"].split(",")))
+    assert dup > 0  # some pinned-version rule lists a check id twice
