@@ -809,6 +809,9 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
         if (m && hd == H_PSS) v = err ? KPE_ERROR_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
         else if (m && hd == H_ERROR) v = KPE_ERROR_;
         else if (m && hd == H_PATTERN) v = KPE_PENDING_;
+        else if (m && hd == H_CONST_SKIP) v = KPE_SKIP_;
+        else if (m && hd == H_CONST_FAIL) v = KPE_FAIL_;
+        else if (m && hd == H_CONST_PASS) v = KPE_PASS_;
         if (x & NR_NEW_POLICY) applied = false;
         if ((x & NR_APPLY_ONE) && applied) v = KPE_NA_;
         applied |= v == KPE_PASS_ || v == KPE_FAIL_;
@@ -875,6 +878,12 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
           em = m;
         } else if (handler == H_PATTERN) {
           fm = em = m;  // both bits: KPE_PENDING_
+        } else if (handler == H_CONST_SKIP) {
+          pm = em = m;  // both bits: KPE_SKIP_ (no ApplyOne with constant handlers)
+        } else if (handler == H_CONST_FAIL) {
+          fm = m;
+        } else if (handler == H_CONST_PASS) {
+          pm = m;
         }
         rmk[lane * 3 + 0] = pm;
         rmk[lane * 3 + 1] = fm;
@@ -905,8 +914,9 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
       for (uint32_t j = 0; j < nc; ++j) {
         const uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
         const uint32_t f = (fm >> lane) & 1u, e = (em >> lane) & 1u;
-        const uint32_t v = ((pm >> lane) & 1u) ? KPE_PASS_ : (f && e) ? KPE_PENDING_ : f ? KPE_FAIL_
-                                                               : e ? KPE_ERROR_ : KPE_NA_;
+        const uint32_t p = (pm >> lane) & 1u;
+        const uint32_t v = p ? (e ? KPE_SKIP_ : KPE_PASS_) : (f && e) ? KPE_PENDING_ : f ? KPE_FAIL_
+                                                                   : e ? KPE_ERROR_ : KPE_NA_;
         sv[lane * nc + j] = (uint8_t)v;
       }
       if (a.masks && live) {

@@ -382,7 +382,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     }
   }
   // truth-table fast path: few terms, no ApplyOne; per PSS version set its rule mask
-  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_apply_one;
+  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_apply_one && !P.any_const;
   std::vector<uint32_t> cls;  // (cv_mask, rule mask) pairs
   uint32_t pss_rules = 0, err_rules = 0, pat_rules = 0;
   if (tt) {

@@ -880,6 +880,98 @@ class PatCompiler {
 }  // namespace pc
 
 // ---- lowering ----
+// ---- compile-time condition folding ---------------------------------------------------
+// Preconditions and deny conditions whose keys and values are letter-only literals or the
+// whole-string variable {{request.operation}} are decided here: the CLI and background scans
+// evaluate with request.operation = CREATE (policy_processor.go / scanner.go build CREATE
+// contexts). Letter-only strings are never durations, quantities, JSON or globs, so every
+// operator (variables/operator/{equal,notequal,anyin,allin,anynotin,allnotin,in,notin}.go)
+// reduces to string equality / membership. Anything else is not folded (nullopt => refuse).
+enum Fold { F_NO = 0, F_FALSE = 1, F_TRUE = 2 };
+
+bool fold_scalar(const JV& v, std::string* out) {
+  if (v.t != JV::Str) return false;
+  std::string t = v.s;
+  if (t.find("{{") != std::string::npos) {
+    // replaceBracesAndTrimSpaces (variables/vars.go:422-427) on a whole-string reference
+    if (t.size() < 4 || t.compare(0, 2, "{{") != 0 || t.compare(t.size() - 2, 2, "}}") != 0) return false;
+    std::string in = t.substr(2, t.size() - 4);
+    size_t a = in.find_first_not_of(" \t"), b = in.find_last_not_of(" \t");
+    if (a == std::string::npos || in.substr(a, b - a + 1) != "request.operation") return false;
+    *out = "CREATE";
+    return true;
+  }
+  if (t.empty()) return false;
+  for (char c : t)
+    if (!((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'))) return false;
+  *out = t;
+  return true;
+}
+
+Fold fold_condition(const JV& c) {
+  if (c.t != JV::Obj) return F_NO;
+  const JV* k = c.get("key");
+  const JV* v = c.get("value");
+  std::string key, op;
+  if (!k || !fold_scalar(*k, &key)) return F_NO;
+  for (char ch : sv(c.get("operator"))) op += (char)tolower((unsigned char)ch);
+  std::vector<std::string> vals;
+  bool list = false;
+  if (!v) return F_NO;
+  if (v->t == JV::Arr) {
+    list = true;
+    for (auto& e : v->a) {
+      std::string x;
+      if (!fold_scalar(e, &x)) return F_NO;
+      vals.push_back(x);
+    }
+  } else {
+    std::string x;
+    if (!fold_scalar(*v, &x)) return F_NO;
+    vals.push_back(x);
+  }
+  const bool in = std::find(vals.begin(), vals.end(), key) != vals.end();
+  bool r;
+  if (op == "equal" || op == "equals") r = !list && in;          // equal.go: string key vs string value
+  else if (op == "notequal" || op == "notequals") r = list || !in;  // notequal.go: other value types => true
+  else if (op == "anyin" || op == "allin" || op == "in") r = in;    // a single key against the value set
+  else if (op == "anynotin" || op == "allnotin" || op == "notin") r = !in;
+  else return F_NO;
+  return r ? F_TRUE : F_FALSE;
+}
+
+// variables/evaluate.go:29-125 (EvaluateConditions / evaluateAnyAllConditions); null or absent
+// conditions are true.
+Fold fold_conditions(const JV* j) {
+  if (!j || j->t == JV::Null) return F_TRUE;
+  auto all_of = [](const JV& arr) {
+    Fold out = F_TRUE;
+    for (auto& e : arr.a) {
+      Fold f = fold_condition(e);
+      if (f == F_NO) return F_NO;
+      if (f == F_FALSE) out = F_FALSE;
+    }
+    return out;
+  };
+  if (j->t == JV::Arr) return all_of(*j);
+  if (j->t != JV::Obj) return F_NO;
+  const JV* any = j->get("any");
+  const JV* all = j->get("all");
+  if ((any && any->t != JV::Arr && any->t != JV::Null) || (all && all->t != JV::Arr && all->t != JV::Null)) return F_NO;
+  Fold any_ok = F_TRUE, all_ok = F_TRUE;
+  if (any && any->t == JV::Arr) {
+    any_ok = F_FALSE;
+    for (auto& e : any->a) {
+      Fold f = fold_condition(e);
+      if (f == F_NO) return F_NO;
+      if (f == F_TRUE) any_ok = F_TRUE;
+    }
+  }
+  if (all && all->t == JV::Arr) all_ok = all_of(*all);
+  if (all_ok == F_NO) return F_NO;
+  return (any_ok == F_TRUE && all_ok == F_TRUE) ? F_TRUE : F_FALSE;
+}
+
 class Lowerer {
  public:
   explicit Lowerer(Program& p) : P(p) {}
@@ -1212,13 +1304,21 @@ class Lowerer {
     bool has_validate = nonempty(v);
     const JV* ps = v ? v->get("podSecurity") : nullptr;
     std::string rname = sv(r.get("name"));
+    // preconditions (validate_resource.go:121-132): folded at compile time or refused
+    Fold pre = F_TRUE;
+    if (has_validate && nonempty(r.get("preconditions"))) {
+      if (nonempty(r.get("context")))
+        throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
+      pre = fold_conditions(r.get("preconditions"));
+      if (pre == F_NO) throw CompileError("rule '" + rname + "': preconditions are not supported yet");
+    }
     if (!has_validate) {
       k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
       if (nonempty(r.get("verifyImages"))) throw CompileError("rule '" + rname + "': verifyImages is not supported");
     } else if (nonempty(v->get("manifests"))) {
       throw CompileError("rule '" + rname + "': validate.manifests is not supported");
     } else if (ps && ps->t == JV::Obj && nonempty(ps)) {
-      if (nonempty(r.get("preconditions")) || nonempty(r.get("context")))
+      if (nonempty(r.get("context")))
         throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
       const JV* ex = ps->get("exclude");
       if (ex && ex->t == JV::Arr && !ex->a.empty())
@@ -1235,9 +1335,20 @@ class Lowerer {
     } else {
       // validate_resource.go:121-170: deny, then pattern / anyPattern, then foreach
       auto present = [&](const char* key) { return v->get(key) && v->get(key)->t != JV::Null; };
-      if (present("deny")) throw CompileError("rule '" + rname + "': validate.deny is not supported on the device yet");
-      if (present("pattern") || present("anyPattern")) {
-        if (nonempty(r.get("preconditions")) || nonempty(r.get("context")))
+      if (present("deny")) {
+        // validateDeny (validate_resource.go:268-279): conditions true => fail, else pass
+        if (nonempty(r.get("context")))
+          throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
+        const JV* d = v->get("deny");
+        const Fold f = d->t == JV::Obj ? fold_conditions(d->get("conditions")) : F_NO;
+        if (f == F_NO) throw CompileError("rule '" + rname + "': validate.deny is not supported on the device yet");
+        k.handler = f == F_TRUE ? H_CONST_FAIL : H_CONST_PASS;
+      } else if (pre == F_FALSE && (present("pattern") || present("anyPattern"))) {
+        if (nonempty(r.get("context")))
+          throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
+        k.handler = H_CONST_SKIP;  // patterns are never evaluated
+      } else if (present("pattern") || present("anyPattern")) {
+        if (nonempty(r.get("context")))
           throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
         if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with pattern rules is not supported");
         pc::PatCompiler pcomp(P.pat, [&](const std::string& g) {
@@ -1273,6 +1384,11 @@ class Lowerer {
       } else {
         k.handler = H_NONE;  // no podSecurity/cel/pattern/deny/foreach: the validator returns nil
       }
+    }
+    if (pre == F_FALSE && k.handler != H_NONE) k.handler = H_CONST_SKIP;  // before every handler
+    if (k.handler >= H_CONST_SKIP) {
+      if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with folded conditions is not supported");
+      P.any_const = true;
     }
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);

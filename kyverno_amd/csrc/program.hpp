@@ -73,6 +73,7 @@ struct Program {
   uint32_t cv_union = 0;  // union of cv_mask over rules
   std::vector<uint32_t> cv_classes;  // distinct cv_masks of PSS rules
   bool any_apply_one = false;
+  bool any_const = false;  // some rule has a constant handler (H_CONST_*)
   bool any_pss = false;
   PatProgram pat;  // pattern rules (H_PATTERN)
   DeviceProgram* dev = nullptr;

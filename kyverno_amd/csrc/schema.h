@@ -285,6 +285,11 @@ enum KpeCheckVersion {
 #define H_PSS 1u
 #define H_ERROR 2u  // every matching resource gets RuleStatusError (e.g. unparsable PSS version)
 #define H_PATTERN 3u  // validate.pattern / validate.anyPattern (validate_resource.go:316-398)
+// constant verdicts of rules whose preconditions / deny conditions fold at compile time
+// (they read only request.operation, CREATE in the CLI and background scans)
+#define H_CONST_SKIP 4u  // preconditions false: RuleSkip (validate_resource.go:125-132)
+#define H_CONST_FAIL 5u  // deny conditions true: RuleFail (validate_resource.go:268-279)
+#define H_CONST_PASS 6u  // deny conditions false: RulePass
 
 // Match terms (AND inside a filter block)
 enum KpeTermType {

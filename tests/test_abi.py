@@ -53,8 +53,8 @@ def test_compile_matches_oracle_rule_names(oracle):
 
 def test_compile_unsupported_is_loud():
     pol = pss_policy("x", "baseline")
-    pol["spec"]["rules"][0]["validate"] = {"deny": {"conditions": {"any": [{"key": "a", "operator": "Equals",
-                                                                            "value": "a"}]}}}
+    pol["spec"]["rules"][0]["validate"] = {"deny": {"conditions": {"any": [{"key": "{{ request.object.kind }}",
+                                                                            "operator": "Equals", "value": "a"}]}}}
     with pytest.raises(KpeError) as e:
         K.PolicySet([pol])
     assert e.value.status == 2  # KPE_E_UNSUPPORTED

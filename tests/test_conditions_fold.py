@@ -1,0 +1,125 @@
+"""Preconditions and deny conditions folded at compile time (request.operation = CREATE and
+letter-only literals; validate_resource.go:121-132, 268-279, variables/evaluate.go).
+
+CPU: which conditions kpe_program_compile folds and which it refuses (KPE_E_UNSUPPORTED).
+GPU: the constant verdicts (skip / fail / pass) land in the matrix bit-exact against the
+oracle's condition engine (oracle/conditions.hpp) on synthetic corpora."""
+import copy
+
+import numpy as np
+import pytest
+
+import kyverno_amd as K
+from tests.policies import pss_policy
+
+OP = "{{ request.operation }}"
+
+
+def _rule(name, pre=None, validate=None, kinds=("Pod",)):
+    r = {"name": name, "match": {"any": [{"resources": {"kinds": list(kinds)}}]},
+         "validate": validate or {"message": "m", "deny": {}}}
+    if pre is not None:
+        r["preconditions"] = pre
+    return r
+
+
+def _policy(name, rules):
+    return {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": name},
+            "spec": {"validationFailureAction": "Audit", "background": True, "rules": rules}}
+
+
+PATTERN = {"message": "m", "pattern": {"spec": {"containers": [{"image": "!*:latest"}]}}}
+
+
+def folded_policy_set():
+    rules = [
+        _rule("deny-empty"),  # deny {} => fail
+        _rule("deny-op-true", validate={"deny": {"conditions": {"any": [{"key": OP, "operator": "Equals",
+                                                                           "value": "CREATE"}]}}}),
+        _rule("deny-op-false", validate={"deny": {"conditions": {"all": [{"key": OP, "operator": "AnyIn",
+                                                                           "value": ["DELETE", "CONNECT"]}]}}}),
+        _rule("deny-list-form", validate={"deny": {"conditions": [{"key": OP, "operator": "NotEquals",
+                                                                    "value": "UPDATE"}]}}),
+        _rule("pre-true-pattern", pre={"all": [{"key": OP, "operator": "AllIn", "value": ["CREATE", "UPDATE"]}]},
+              validate=PATTERN),
+        _rule("pre-false-pattern", pre={"any": [{"key": OP, "operator": "Equals", "value": "DELETE"}]},
+              validate=PATTERN),
+        _rule("pre-false-deny", pre=[{"key": OP, "operator": "In", "value": ["UPDATE"]}]),
+        _rule("pre-notin", pre={"all": [{"key": OP, "operator": "NotIn", "value": ["DELETE"]}]}),
+        _rule("deny-ctrl", kinds=("Deployment", "CronJob"),
+              validate={"deny": {"conditions": {"any": [{"key": OP, "operator": "anynotin", "value": ["CREATE"]}]}}}),
+    ]
+    pols = [_policy("folded", rules)]
+    p = pss_policy("pre-pss", "restricted", "latest", kinds=("Pod",))
+    p["spec"]["rules"][0]["preconditions"] = {"all": [{"key": OP, "operator": "Equals", "value": "DELETE"}]}
+    pols.append(p)
+    p = pss_policy("pre-pss-true", "baseline", "v1.24", kinds=("Pod", "Deployment"))
+    p["spec"]["rules"][0]["preconditions"] = {"any": [{"key": OP, "operator": "Equals", "value": "CREATE"}]}
+    pols.append(p)
+    # autogen: a Pod rule with folded preconditions expands to Deployment/CronJob rules
+    pols.append(_policy("autogen", [_rule("deny-pod", pre={"all": [{"key": OP, "operator": "Equals",
+                                                                       "value": "CREATE"}]})]))
+    return pols
+
+
+def test_fold_compiles():
+    ps = K.PolicySet(folded_policy_set())
+    assert ps.num_rules >= 14
+    assert any(n.startswith("autogen/autogen-") for n in ps.rule_names)
+
+
+@pytest.mark.parametrize("cond", [
+    {"all": [{"key": "{{ request.object.metadata.name }}", "operator": "Equals", "value": "x"}]},
+    {"all": [{"key": OP, "operator": "Equals", "value": "CRE*"}]},          # glob: not folded
+    {"all": [{"key": OP, "operator": "GreaterThan", "value": "A"}]},          # operator outside the set
+    {"all": [{"key": "1Gi", "operator": "Equals", "value": "1024Mi"}]},       # quantities: not folded
+    {"all": [{"key": OP, "operator": "Equals", "value": "{{ request.operation }}-x"}]},
+])
+def test_unfoldable_refused(cond):
+    for pol in (_policy("p", [_rule("r", pre=cond, validate=PATTERN)]),
+                _policy("p", [_rule("r", validate={"deny": {"conditions": cond}})])):
+        with pytest.raises(K.KpeError):
+            K.PolicySet([pol])
+
+
+def test_apply_one_with_folded_refused():
+    pol = _policy("p", [_rule("a"), _rule("b")])
+    pol["spec"]["applyRules"] = "One"
+    with pytest.raises(K.KpeError):
+        K.PolicySet([pol])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix,n,seed", [(0, 4000, 0xC2), (2, 4000, 31)])
+def test_folded_conditions_bit_exact(oracle, mix, n, seed):
+    pols = folded_policy_set()
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(seed, n, mix=mix)
+    v, _, cnt = eng.evaluate(ps, K.Corpus(nd))
+    ref = oracle.validate(pols, nd, nthreads=8)
+    assert v.shape == ref.shape
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()} {v[tuple(bad[0])]} {ref[tuple(bad[0])]}"
+    assert {1, 2, 5} <= set(np.unique(v).tolist())  # pass, fail and skip all occur
+    for r in range(v.shape[1]):
+        assert cnt[r]["skip"] == int((v[:, r] == 5).sum())
+
+
+@pytest.mark.gpu
+def test_folded_with_wide_program(oracle):
+    """Many distinct match terms push the program off the narrow / truth-table paths."""
+    pols = folded_policy_set()
+    for i in range(40):
+        p = copy.deepcopy(pols[0])
+        p["metadata"]["name"] = f"folded-{i}"
+        for r in p["spec"]["rules"]:
+            r["match"]["any"][0]["resources"]["names"] = [f"res-{i}*"]
+        pols.append(p)
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(5, 3000, mix=2)
+    v, _, _ = eng.evaluate(ps, K.Corpus(nd))
+    ref = oracle.validate(pols, nd, nthreads=8)
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()}"

@@ -31,8 +31,12 @@ def _sets():
     cases = [c for c in PTREE if isinstance(json.loads(c["resource"]), dict)]
     pols = device_policies([_policy_for(f"t{i}", json.loads(c["pattern"])) for i, c in enumerate(cases)])
     out.append(("validate_test.go", pols, "\n".join(json.dumps(json.loads(c["resource"])) for c in cases).encode()))
+    def pattern_only(pols):  # the harness runs the pattern VM alone (no folded deny / preconditions)
+        return [q for q in pols if not any((r.get("validate") or {}).get("deny") is not None or r.get("preconditions")
+                                          for r in q["spec"]["rules"])]
+
     for c in CLI:
-        p = device_policies(c["policies"])
+        p = pattern_only(device_policies(c["policies"]))
         if p and c["resources"]:
             out.append((c["name"], p, "\n".join(json.dumps(r) for r in c["resources"]).encode()))
     return out
