@@ -1306,7 +1306,8 @@ class Lowerer {
     std::string rname = sv(r.get("name"));
     // preconditions (validate_resource.go:121-132): folded at compile time or refused
     Fold pre = F_TRUE;
-    if (has_validate && nonempty(r.get("preconditions"))) {
+    const JV* pre_raw = r.get("preconditions");  // any non-null block is evaluated (utils.go:78-95)
+    if (has_validate && pre_raw && pre_raw->t != JV::Null) {
       if (nonempty(r.get("context")))
         throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
       pre = fold_conditions(r.get("preconditions"));

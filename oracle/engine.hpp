@@ -790,7 +790,9 @@ inline Rule compile_rule(const JPtr& raw) {
     }
   }
   if (jnonempty(raw->get("context"))) r.unsupported = r.has_validate;
-  if (jnonempty(raw->get("preconditions"))) {
+  // any non-null block is evaluated: TransformConditions (engine/utils/utils.go:78-95) decodes
+  // `any: []` to a non-nil empty list, which evaluateAnyAllConditions reads as false
+  if (raw->get("preconditions") && !raw->get("preconditions")->is_null()) {
     try {
       r.pre = cond::parse_conditions(raw->get("preconditions"));
       cond::precompile(r.pre);

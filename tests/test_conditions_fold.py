@@ -45,6 +45,8 @@ def folded_policy_set():
         _rule("pre-false-pattern", pre={"any": [{"key": OP, "operator": "Equals", "value": "DELETE"}]},
               validate=PATTERN),
         _rule("pre-false-deny", pre=[{"key": OP, "operator": "In", "value": ["UPDATE"]}]),
+        _rule("pre-empty-any", pre={"any": []}, validate=PATTERN),  # non-nil empty any => false => skip
+        _rule("pre-empty-block", pre={}, validate=PATTERN),  # no any / all => true
         _rule("pre-notin", pre={"all": [{"key": OP, "operator": "NotIn", "value": ["DELETE"]}]}),
         _rule("deny-ctrl", kinds=("Deployment", "CronJob"),
               validate={"deny": {"conditions": {"any": [{"key": OP, "operator": "anynotin", "value": ["CREATE"]}]}}}),
