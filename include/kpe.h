@@ -138,6 +138,17 @@ kpe_status kpe_fetch_cv_masks(kpe_device* dev, const kpe_program* prog, const kp
 int kpe_pss_num_cv(void);
 int kpe_pss_cv_check(int v);
 
+/* `kyverno apply` summary line (cmd/cli/kubectl-kyverno/processor/result.go:34-68) from the
+ * per-rule counts of kpe_evaluate / kpe_fetch: unscored fails (policies.kyverno.io/scored:
+ * "false") and, with audit_warn (--audit-warn), fails of Audit policies count as warn; a
+ * response is counted once per validate rule of its policy with the same name (the
+ * reference matches by name). KPE_E_UNSUPPORTED when audit_warn meets
+ * validationFailureActionOverrides (the action then depends on each resource's namespace). */
+typedef struct kpe_cli_totals {
+  uint64_t pass, fail, warn, error, skip;
+} kpe_cli_totals;
+kpe_status kpe_cli_summary(const kpe_program* prog, const kpe_counts* counts, int audit_warn, kpe_cli_totals* out);
+
 /* PolicyReport results of one resource (pkg/utils/report/results.go:89-156,
  * EngineResponseToReportResults), as the JSON array encoding/json writes for
  * []PolicyReportResult: one object per rule with a response, in rule order, with

@@ -16,6 +16,7 @@ from .engine import (  # noqa: F401
     PolicySet,
     RuleResponse,
     RuleStatus,
+    cli_summary,
     report_results,
     synth_ns_labels,
     synth_resources,
@@ -32,6 +33,7 @@ __all__ = [
     "RuleResponse",
     "RuleStatus",
     "report_results",
+    "cli_summary",
     "synth_ns_labels",
     "synth_resources",
     "load",

@@ -14,6 +14,11 @@ class KpeError(RuntimeError):
         self.status = status
 
 
+class CliTotals(ctypes.Structure):
+    _fields_ = [("pass_", ctypes.c_uint64), ("fail", ctypes.c_uint64), ("warn", ctypes.c_uint64),
+                ("error", ctypes.c_uint64), ("skip", ctypes.c_uint64)]
+
+
 class Counts(ctypes.Structure):
     _fields_ = [(k, ctypes.c_uint64) for k in ("na", "pass_", "fail", "warn", "error", "skip")]
 
@@ -66,6 +71,7 @@ def load():
     L.kpe_pss_cv_check.argtypes = [i32]
     L.kpe_report_results.argtypes = [vp, vp, vp, ctypes.c_char_p, sz]
     L.kpe_report_results.restype = ctypes.c_long
+    L.kpe_cli_summary.argtypes = [vp, ctypes.POINTER(Counts), i32, ctypes.POINTER(CliTotals)]
     L.kpe_device_set_timing.argtypes = [vp, i32]
     L.kpe_device_kernel_stats.argtypes = [vp, vp, vp, ctypes.POINTER(KernelStats), i32]
     L.kpe_synth_resources.argtypes = [ctypes.c_uint64, i64, i64, i32, ctypes.POINTER(ctypes.c_void_p),

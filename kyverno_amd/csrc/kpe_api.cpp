@@ -1026,6 +1026,29 @@ static void json_str(std::string& o, const std::string& s) {  // encoding/json s
   o += '"';
 }
 
+// cmd/cli/kubectl-kyverno/processor/result.go:34-68 (ResultCounts.addEngineResponse): every
+// response rule is counted once per validate rule of its policy with the same name; a fail is
+// a warn when the policy is unscored, or with --audit-warn when its action is Audit.
+kpe_status kpe_cli_summary(const kpe_program* prog, const kpe_counts* counts, int audit_warn, kpe_cli_totals* out) {
+  if (!prog || !counts || !out) return fail(KPE_E_INVALID, "null argument");
+  const kpe::Program& P = *prog->p;
+  *out = kpe_cli_totals{};
+  for (size_t r = 0; r < P.rules.size(); ++r) {
+    const kpe::RuleReport& rr = P.reports[r];
+    const uint64_t m = rr.name_mult;
+    if (!m) continue;
+    if (audit_warn && rr.overrides && rr.scored && counts[r].fail)
+      return fail(KPE_E_UNSUPPORTED, "validationFailureActionOverrides with --audit-warn (per-namespace action)");
+    out->pass += m * counts[r].pass;
+    out->error += m * counts[r].error;
+    out->skip += m * counts[r].skip;
+    out->warn += m * counts[r].warn;
+    if (!rr.scored || (audit_warn && rr.audit)) out->warn += m * counts[r].fail;
+    else out->fail += m * counts[r].fail;
+  }
+  return KPE_OK;
+}
+
 // pkg/utils/report/results.go:89-156 (EngineResponseToReportResults) for one resource row,
 // over every policy of the program; toPolicyResult results.go:56-71.
 long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row, char* buf,

@@ -1396,6 +1396,7 @@ class Lowerer {
     P.rule_names.push_back(pol_name + "/" + rname);
     RuleReport rr;
     rr.rule = rname;
+    rr.has_validate = has_validate;
     if (ps && ps->t == JV::Obj && nonempty(ps)) {
       rr.pss = true;
       rr.pss_level = sv(ps->get("level"));
@@ -1437,8 +1438,15 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len) {
     auto annv = [&](const char* k) { return ann ? sv(ann->get(k)) : std::string(); };
     std::string sev = annv("policies.kyverno.io/severity");
     if (sev != "critical" && sev != "high" && sev != "medium" && sev != "low" && sev != "info") sev.clear();
+    const std::string vfa = spec ? sv(spec->get("validationFailureAction")) : std::string();
+    const JV* ovr = spec ? spec->get("validationFailureActionOverrides") : nullptr;
     for (size_t i = r0; i < prog->reports.size(); ++i) {
       RuleReport& rr = prog->reports[i];
+      rr.audit = !(vfa == "Enforce" || vfa == "enforce");
+      rr.overrides = ovr && ovr->t == JV::Arr && !ovr->a.empty();
+      rr.name_mult = 0;
+      for (size_t j = r0; j < prog->reports.size(); ++j)
+        if (prog->reports[j].has_validate && prog->reports[j].rule == rr.rule) ++rr.name_mult;
       rr.policy_key = ns.empty() ? name : ns + "/" + name;
       rr.scored = annv("policies.kyverno.io/scored") != "false";
       rr.category = annv("policies.kyverno.io/category");

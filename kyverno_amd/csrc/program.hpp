@@ -54,6 +54,10 @@ struct RuleReport {
   std::string severity;    // SeverityFromString(policies.kyverno.io/severity)
   std::string pss_level, pss_version;  // podSecurity rules: PodSecurityChecks.Level / Version
   bool scored = true;      // policies.kyverno.io/scored != "false"
+  bool has_validate = false;  // rule.HasValidate() (processor/result.go:42)
+  bool audit = true;          // spec.validationFailureAction.Audit() (!Enforce, spec_types.go:31-37)
+  bool overrides = false;     // spec.validationFailureActionOverrides non-empty (per-namespace action)
+  uint32_t name_mult = 1;     // validate rules of the policy with this name (result.go:44 name match)
   bool pss = false;
 };
 

@@ -20,7 +20,7 @@ from typing import Dict, List, Optional, Sequence
 
 import numpy as np
 
-from ._lib import Counts, KernelStats, KpeError, check, load
+from ._lib import CliTotals, Counts, KernelStats, KpeError, check, load
 
 
 class RuleStatus(str, enum.Enum):
@@ -294,3 +294,15 @@ def report_results(ps: PolicySet, verdict_row, cv_mask_row=None) -> List[dict]:
         if n < cap:
             return json.loads(buf.value.decode())
         cap = n + 1
+
+
+def cli_summary(ps: PolicySet, counts: List[dict], audit_warn: bool = False) -> Dict[str, int]:
+    """`kyverno apply` pass/fail/warn/error/skip totals (processor/result.go:34-68) from the
+    per-rule counts Engine.evaluate returns, through kpe_cli_summary."""
+    arr = (Counts * max(len(counts), 1))()
+    for i, c in enumerate(counts):
+        arr[i].na, arr[i].pass_, arr[i].fail = c["na"], c["pass"], c["fail"]
+        arr[i].warn, arr[i].error, arr[i].skip = c["warn"], c["error"], c["skip"]
+    out = CliTotals()
+    check(load().kpe_cli_summary(ps.h, arr, 1 if audit_warn else 0, ctypes.byref(out)))
+    return {"pass": out.pass_, "fail": out.fail, "warn": out.warn, "error": out.error, "skip": out.skip}

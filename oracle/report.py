@@ -88,3 +88,38 @@ def report_results(policies: List[dict], rule_names: List[str], verdict_row, res
             item["severity"] = sev
         out.append(item)
     return out
+
+
+def cli_summary(policies: List[dict], rule_names: List[str], verdicts, audit_warn: bool = False) -> Dict[str, int]:
+    """`kyverno apply` totals, ResultCounts.addEngineResponse
+    (cmd/cli/kubectl-kyverno/processor/result.go:34-68), over an N x R verdict matrix:
+    per resource and policy, every computed validate rule is matched by name against the
+    response rules (so duplicate names count twice); unscored fail => warn; with
+    --audit-warn a fail of an Audit policy (spec_types.go:31-37) => warn."""
+    by_name = {p["metadata"]["name"]: p for p in policies}
+    cols: Dict[str, List[int]] = {}
+    for r, full in enumerate(rule_names):
+        cols.setdefault(full.split("/", 1)[0], []).append(r)
+    tot = {"pass": 0, "fail": 0, "warn": 0, "error": 0, "skip": 0}
+    for row in verdicts:
+        for pname, rs in cols.items():
+            pol = by_name[pname]
+            responses = [(rule_names[r].split("/", 1)[1], int(row[r])) for r in rs if int(row[r]) in RESULT]
+            if not responses:
+                continue  # response.IsEmpty()
+            ann = (pol.get("metadata") or {}).get("annotations") or {}
+            scored = ann.get("policies.kyverno.io/scored") != "false"
+            action = (pol.get("spec") or {}).get("validationFailureAction", "")
+            audit = action not in ("Enforce", "enforce")
+            for r in rs:
+                rname = rule_names[r].split("/", 1)[1]
+                if not (_source_rule(pol, rname).get("validate")):
+                    continue  # rule.HasValidate()
+                for name, cell in responses:
+                    if name != rname:
+                        continue
+                    st = RESULT[cell]
+                    if st == "fail" and (not scored or (audit_warn and audit)):
+                        st = "warn"
+                    tot[st] += 1
+    return tot

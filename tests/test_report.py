@@ -132,3 +132,58 @@ def test_gpu_report_matches_oracle(oracle, mix, n, seed):
         dup += sum(1 for r in got if "properties" in r and len(set(r["properties"]["controls"].split(","))) <
                    len(r["properties"]["controls"].split(",")))
     assert dup > 0  # some pinned-version rule lists a check id twice
+
+
+def _counts(v):
+    return [{"na": int((v[:, r] == 0).sum()), "pass": int((v[:, r] == 1).sum()), "fail": int((v[:, r] == 2).sum()),
+             "warn": int((v[:, r] == 3).sum()), "error": int((v[:, r] == 4).sum()), "skip": int((v[:, r] == 5).sum())}
+            for r in range(v.shape[1])]
+
+
+def test_cli_summary_pinned_by_background_report(oracle):
+    bg = json.load(open(os.path.join(GOLD, "background_report.json")))
+    names = oracle.rule_names([bg["policy"]])
+    v = oracle.validate([bg["policy"]], json.dumps(bg["resource"]).encode())
+    assert oracle_report.cli_summary([bg["policy"]], names, v) == bg["summary"]
+    assert K.cli_summary(K.PolicySet([bg["policy"]]), _counts(v)) == bg["summary"]
+
+
+@pytest.mark.parametrize("audit_warn", [False, True])
+def test_cli_summary_matches_oracle(oracle, audit_warn):
+    pols = report_policy_set()
+    enf = copy.deepcopy(pols[1])
+    enf["metadata"]["name"] = "enforced"
+    enf["spec"]["validationFailureAction"] = "Enforce"
+    dup = copy.deepcopy(pols[2])  # two rules with one name: each response counts twice
+    dup["metadata"]["name"] = "dup-names"
+    dup["spec"]["rules"].append(copy.deepcopy(dup["spec"]["rules"][0]))
+    pols += [enf, dup]
+    ps = K.PolicySet(pols)
+    names = oracle.rule_names(pols)
+    nd = K.synth_resources(9, 600, mix=2)
+    v = oracle.validate(pols, nd, nthreads=4)
+    want = oracle_report.cli_summary(pols, names, v, audit_warn)
+    assert K.cli_summary(ps, _counts(v), audit_warn) == want
+    assert want["warn"] > 0 and want["fail"] > 0
+
+
+def test_cli_summary_overrides_with_audit_warn_refused():
+    pol = copy.deepcopy(report_policy_set()[1])
+    pol["spec"]["validationFailureActionOverrides"] = [{"action": "Enforce", "namespaces": ["prod-*"]}]
+    ps = K.PolicySet([pol])
+    cnt = [{"na": 0, "pass": 0, "fail": 1, "warn": 0, "error": 0, "skip": 0}] * ps.num_rules
+    assert K.cli_summary(ps, cnt)["fail"] + K.cli_summary(ps, cnt)["warn"] == ps.num_rules
+    with pytest.raises(K.KpeError):
+        K.cli_summary(ps, cnt, audit_warn=True)
+
+
+@pytest.mark.gpu
+def test_gpu_cli_summary_matches_oracle(oracle):
+    pols = report_policy_set()
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(13, 5000, mix=2)
+    _, _, cnt = eng.evaluate(ps, K.Corpus(nd))
+    ref = oracle.validate(pols, nd, nthreads=8)
+    for aw in (False, True):
+        assert K.cli_summary(ps, cnt, aw) == oracle_report.cli_summary(pols, oracle.rule_names(pols), ref, aw)
