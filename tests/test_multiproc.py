@@ -3,7 +3,9 @@
 totals, as bench.py does over RCCL. The shard evaluation here is the oracle
 (this is a test of sharding + the exchange, not of the kernels, which
 tests/test_gpu_parity.py covers)."""
+import json
 import os
+import sys
 import socket
 
 import numpy as np
@@ -55,6 +57,10 @@ def _worker(rank, world, port, outdir):
     if rank == 0:
         np.save(os.path.join(outdir, "counts.npy"), np.array(shard.counts_to_rows(total), dtype=np.int64))
         np.save(os.path.join(outdir, "slowest.npy"), np.array([slowest]))
+        # `kyverno apply` summary of the whole job from the all-reduced per-rule counts
+        summ = K.cli_summary(K.PolicySet(parity_policy_set()), total)
+        with open(os.path.join(outdir, "summary.json"), "w") as f:
+            json.dump(summ, f)
     np.save(os.path.join(outdir, f"verdicts{rank}.npy"), v)
     dist.barrier()
     dist.destroy_process_group()
@@ -99,3 +105,9 @@ def test_gloo_two_ranks_counts(tmp_path):
     stacked = np.concatenate([np.load(tmp_path / f"verdicts{r}.npy") for r in range(world)])
     assert np.array_equal(stacked, ref_v)
     assert float(np.load(tmp_path / "slowest.npy")[0]) == 2.0
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
+    import report as oracle_report
+
+    pols = parity_policy_set()
+    want_summary = oracle_report.cli_summary(pols, load_oracle().rule_names(pols), ref_v)
+    assert json.load(open(tmp_path / "summary.json")) == want_summary
