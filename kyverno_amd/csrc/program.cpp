@@ -882,14 +882,14 @@ class PatCompiler {
 // ---- lowering ----
 // ---- compile-time condition folding ---------------------------------------------------
 // Preconditions and deny conditions whose keys and values are letter-only literals or the
-// whole-string variable {{request.operation}} are decided here: the CLI and background scans
+// whole-string variable {{request.operation}} (values may add * and ? globs) are decided here: the CLI and background scans
 // evaluate with request.operation = CREATE (policy_processor.go / scanner.go build CREATE
 // contexts). Letter-only strings are never durations, quantities, JSON or globs, so every
 // operator (variables/operator/{equal,notequal,anyin,allin,anynotin,allnotin,in,notin}.go)
-// reduces to string equality / membership. Anything else is not folded (nullopt => refuse).
+// reduces to glob membership of the key in the values. Anything else is refused.
 enum Fold { F_NO = 0, F_FALSE = 1, F_TRUE = 2 };
 
-bool fold_scalar(const JV& v, std::string* out) {
+bool fold_scalar(const JV& v, std::string* out, bool glob = false) {
   if (v.t != JV::Str) return false;
   std::string t = v.s;
   if (t.find("{{") != std::string::npos) {
@@ -903,7 +903,7 @@ bool fold_scalar(const JV& v, std::string* out) {
   }
   if (t.empty()) return false;
   for (char c : t)
-    if (!((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'))) return false;
+    if (!((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z') || (glob && (c == '*' || c == '?')))) return false;
   *out = t;
   return true;
 }
@@ -922,15 +922,18 @@ Fold fold_condition(const JV& c) {
     list = true;
     for (auto& e : v->a) {
       std::string x;
-      if (!fold_scalar(e, &x)) return F_NO;
+      if (!fold_scalar(e, &x, true)) return F_NO;
       vals.push_back(x);
     }
   } else {
     std::string x;
-    if (!fold_scalar(*v, &x)) return F_NO;
+    if (!fold_scalar(*v, &x, true)) return F_NO;
     vals.push_back(x);
   }
-  const bool in = std::find(vals.begin(), vals.end(), key) != vals.end();
+  // values may be go-wildcard globs; the key never is, so the two-way wildcard.Match of the
+  // set operators (anyin.go etc.) reduces to value-as-pattern
+  bool in = false;
+  for (auto& x : vals) in = in || glob_host(x, key);
   bool r;
   if (op == "equal" || op == "equals") r = !list && in;          // equal.go: string key vs string value
   else if (op == "notequal" || op == "notequals") r = list || !in;  // notequal.go: other value types => true

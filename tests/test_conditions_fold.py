@@ -47,6 +47,12 @@ def folded_policy_set():
         _rule("pre-false-deny", pre=[{"key": OP, "operator": "In", "value": ["UPDATE"]}]),
         _rule("pre-empty-any", pre={"any": []}, validate=PATTERN),  # non-nil empty any => false => skip
         _rule("pre-empty-block", pre={}, validate=PATTERN),  # no any / all => true
+        _rule("pre-glob-eq", pre={"all": [{"key": OP, "operator": "Equals", "value": "CRE*"}]}),
+        _rule("pre-glob-miss", pre={"all": [{"key": OP, "operator": "Equals", "value": "UPD?TE"}]}),
+        _rule("deny-glob-in", validate={"deny": {"conditions": {"any": [{"key": OP, "operator": "AnyIn",
+                                                                           "value": ["DEL*", "C?EATE"]}]}}}),
+        _rule("deny-glob-notin", validate={"deny": {"conditions": {"all": [{"key": OP, "operator": "NotIn",
+                                                                             "value": "*"}]}}}),
         _rule("pre-notin", pre={"all": [{"key": OP, "operator": "NotIn", "value": ["DELETE"]}]}),
         _rule("deny-ctrl", kinds=("Deployment", "CronJob"),
               validate={"deny": {"conditions": {"any": [{"key": OP, "operator": "anynotin", "value": ["CREATE"]}]}}}),
@@ -72,7 +78,8 @@ def test_fold_compiles():
 
 @pytest.mark.parametrize("cond", [
     {"all": [{"key": "{{ request.object.metadata.name }}", "operator": "Equals", "value": "x"}]},
-    {"all": [{"key": OP, "operator": "Equals", "value": "CRE*"}]},          # glob: not folded
+    {"all": [{"key": "CRE*", "operator": "Equals", "value": OP}]},          # glob key: not folded
+    {"all": [{"key": OP, "operator": "AnyIn", "value": ["a-b"]}]},          # range form: not folded
     {"all": [{"key": OP, "operator": "GreaterThan", "value": "A"}]},          # operator outside the set
     {"all": [{"key": "1Gi", "operator": "Equals", "value": "1024Mi"}]},       # quantities: not folded
     {"all": [{"key": OP, "operator": "Equals", "value": "{{ request.operation }}-x"}]},
