@@ -187,3 +187,29 @@ def test_gpu_cli_summary_matches_oracle(oracle):
     ref = oracle.validate(pols, nd, nthreads=8)
     for aw in (False, True):
         assert K.cli_summary(ps, cnt, aw) == oracle_report.cli_summary(pols, oracle.rule_names(pols), ref, aw)
+
+
+@pytest.mark.gpu
+def test_gpu_report_chart_policies(oracle):
+    """The rendered kyverno-policies chart (device-supported policies: PSS-style pattern rules
+    with their category annotations) on mixed kinds: report results and the CLI
+    summary from the device equal the oracle's."""
+    from tests.test_gpu_pattern import chart_pattern_policies
+
+    pols = chart_pattern_policies()
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(0xC1, 3000, mix=2)
+    docs = [json.loads(x) for x in nd.split(b"\n") if x.strip()]
+    v, _, cnt = eng.evaluate(ps, K.Corpus(nd), check_masks=True)
+    names = oracle.rule_names(pols)
+    ref = oracle.validate(pols, nd, nthreads=8)
+    assert (v == ref).all()
+    seen = set()
+    for i in range(0, len(docs), 5):
+        want = oracle_report.report_results(pols, names, ref[i], docs[i], oracle.failing_checks)
+        got = K.report_results(ps, v[i])  # pattern rules: no PSS controls
+        assert got == want, (i, got, want)
+        seen.update((r["result"], "category" in r) for r in got)
+    assert ("fail", True) in seen and ("pass", True) in seen
+    assert K.cli_summary(ps, cnt) == oracle_report.cli_summary(pols, names, ref)
