@@ -881,12 +881,18 @@ class PatCompiler {
 
 // ---- lowering ----
 // ---- compile-time condition folding ---------------------------------------------------
-// Preconditions and deny conditions whose keys and values are letter-only literals or the
-// whole-string variable {{request.operation}} (values may add * and ? globs) are decided here: the CLI and background scans
-// evaluate with request.operation = CREATE (policy_processor.go / scanner.go build CREATE
-// contexts). Letter-only strings are never durations, quantities, JSON or globs, so every
-// operator (variables/operator/{equal,notequal,anyin,allin,anynotin,allnotin,in,notin}.go)
-// reduces to glob membership of the key in the values. Anything else is refused.
+// Preconditions and deny conditions whose keys are letter-only literals or the whole-string
+// variable {{request.operation}}, and whose values are letter-only literals that may add `*`
+// and `?` globs, are decided here: the CLI and background scans evaluate with
+// request.operation = CREATE (policy_processor.go / scanner.go build CREATE contexts).
+// Letter-only strings are never durations, quantities or InRange patterns, and the key is
+// never a glob, so the two-way wildcard.Match of the operators reduces to value-as-pattern:
+// equal.go / notequal.go wildcard.Match(value, key), anyin.go:65 / allin.go:60 / in.go:64
+// Match(sprint(v), k) || Match(k, sprint(v)). A scalar string value that does not match is
+// then decoded as a JSON []string: "null" is a valid empty list, "true" / "false" fail to
+// decode (invalid type => the operator is false), and any other letter-only text is not JSON,
+// which anyin.go:81-88 (and allin / anynotin / allnotin) reads as a one-element list but
+// in.go:74-78 / notin.go (keyExistsInArray) reads as an invalid type. Anything else is refused.
 enum Fold { F_NO = 0, F_FALSE = 1, F_TRUE = 2 };
 
 bool fold_scalar(const JV& v, std::string* out, bool glob = false) {
@@ -930,15 +936,21 @@ Fold fold_condition(const JV& c) {
     if (!fold_scalar(*v, &x, true)) return F_NO;
     vals.push_back(x);
   }
-  // values may be go-wildcard globs; the key never is, so the two-way wildcard.Match of the
-  // set operators (anyin.go etc.) reduces to value-as-pattern
+  // values may be go-wildcard globs; the key never is (see above)
   bool in = false;
   for (auto& x : vals) in = in || glob_host(x, key);
+  const bool legacy = op == "in" || op == "notin";
+  bool invalid = false;  // the value fails to decode as a []string: every such operator is false
+  if (!list && !in) {
+    const std::string& x = vals[0];
+    if (x == "true" || x == "false") invalid = true;   // valid JSON, not a []string
+    else if (x != "null" && legacy) invalid = true;    // not JSON: keyExistsInArray's Unmarshal error
+  }
   bool r;
   if (op == "equal" || op == "equals") r = !list && in;          // equal.go: string key vs string value
   else if (op == "notequal" || op == "notequals") r = list || !in;  // notequal.go: other value types => true
-  else if (op == "anyin" || op == "allin" || op == "in") r = in;    // a single key against the value set
-  else if (op == "anynotin" || op == "allnotin" || op == "notin") r = !in;
+  else if (op == "anyin" || op == "allin" || op == "in") r = !invalid && in;  // a single key against the value set
+  else if (op == "anynotin" || op == "allnotin" || op == "notin") r = !invalid && !in;
   else return F_NO;
   return r ? F_TRUE : F_FALSE;
 }
@@ -1389,7 +1401,10 @@ class Lowerer {
         k.handler = H_NONE;  // no podSecurity/cel/pattern/deny/foreach: the validator returns nil
       }
     }
-    if (pre == F_FALSE && k.handler != H_NONE) k.handler = H_CONST_SKIP;  // before every handler
+    // invokeRuleHandler (engine.go:278-285) checks preconditions before any handler runs, and
+    // every validate rule has one (validation.go:37-53: at least NewValidateResourceHandler,
+    // even when its validator then returns nil)
+    if (pre == F_FALSE && (k.handler != H_NONE || has_validate)) k.handler = H_CONST_SKIP;
     if (k.handler >= H_CONST_SKIP) {
       if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with folded conditions is not supported");
       P.any_const = true;

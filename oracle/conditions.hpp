@@ -981,7 +981,8 @@ inline bool json_string_array(const std::string& s, std::vector<std::string>* ou
   } catch (const std::exception&) {
     return false;  // not valid JSON: the string itself
   }
-  if (!v || v->t != JT::Arr) {
+  if (!v || v->t == JT::Null) return true;  // json.Unmarshal("null", &[]string) leaves a nil slice, no error
+  if (v->t != JT::Arr) {
     *invalid = true;  // valid JSON but not a string array: Unmarshal error
     return true;
   }
@@ -1087,19 +1088,23 @@ inline OpKind parse_op(const std::string& o) {
 // in.go / notin.go (deprecated): key in value list / string
 inline bool op_in(const JPtr& key, const JPtr& value, bool notin) {
   if (is_null(key)) return false;
-  auto key_in = [&](const std::string& k) -> int {  // 1 in, 0 not in, -1 invalid
+  // keyExistsInArray (in.go:60-92): 1 in, 0 not in, -1 invalid type (both operators false)
+  auto key_in = [&](const std::string& k) -> int {
     if (is_null(value)) return -1;
     if (value->t == JT::Arr) {
-      for (auto& e : value->a)
-        if (wmatch(go_sprint(e), k)) return 1;
+      for (auto& e : value->a) {
+        const std::string s = go_sprint(e);
+        if (wmatch(s, k) || wmatch(k, s)) return 1;
+      }
       return 0;
     }
     if (value->t == JT::Str) {
       if (wmatch(value->s, k)) return 1;
       std::vector<std::string> arr;
       bool invalid;
-      if (!json_string_array(value->s, &arr, &invalid)) arr = {value->s};
-      else if (invalid) return -1;
+      // json.Unmarshal straight away (no json.Valid fallback as in anyin.go): text that is not
+      // JSON is an Unmarshal error
+      if (!json_string_array(value->s, &arr, &invalid) || invalid) return -1;
       for (auto& a : arr)
         if (a == k) return 1;
       return 0;
@@ -1115,29 +1120,39 @@ inline bool op_in(const JPtr& key, const JPtr& value, bool notin) {
       return (r == 1) != notin;
     }
     case JT::Arr: {
+      // in.go:35-40: every key element is asserted to be a string (the reference panics
+      // otherwise; restated as an evaluation error, PARITY UNPINNED)
+      std::vector<std::string> keys;
+      for (auto& e : key->a) {
+        if (is_null(e) || e->t != JT::Str) throw EvalError{"In/NotIn key list element is not a string"};
+        keys.push_back(e->s);
+      }
       if (is_null(value)) return false;
       std::vector<std::string> vals;
-      if (value->t == JT::Arr) {
-        for (auto& e : value->a) vals.push_back(go_sprint(e));
+      if (value->t == JT::Arr) {  // setExistsInArray (in.go:108-123): string elements only
+        for (auto& e : value->a) {
+          if (is_null(e) || e->t != JT::Str) return false;
+          vals.push_back(e->s);
+        }
       } else if (value->t == JT::Str) {
-        if (key->a.size() == 1 && go_sprint(key->a[0]) == value->s) return !notin;
+        // in.go:126-128: a one-element key equal to the value reports keyExists for both
+        // operators, so NotIn is true there as well
+        if (keys.size() == 1 && keys[0] == value->s) return true;
         bool invalid;
-        if (!json_string_array(value->s, &vals, &invalid)) vals = {value->s};
-        else if (invalid) return false;
+        if (!json_string_array(value->s, &vals, &invalid) || invalid) return false;
       } else {
         return false;
       }
-      // isIn: every key is in the value set (exact); notIn: no key is (exact)
-      bool all = true, none = true;
-      for (auto& e : key->a) {
-        const std::string k = go_sprint(e);
+      // isIn: every key is in the value set; isNotIn: some key is not (exact set lookups)
+      bool all = true, any_missing = false;
+      for (auto& k : keys) {
         bool f = false;
         for (auto& v : vals)
-          if (wmatch(v, k)) f = true;
+          if (v == k) f = true;
         all = all && f;
-        none = none && !f;
+        any_missing = any_missing || !f;
       }
-      return notin ? none : all;
+      return notin ? any_missing : all;
     }
     default: return false;
   }

@@ -56,6 +56,16 @@ def folded_policy_set():
         _rule("pre-notin", pre={"all": [{"key": OP, "operator": "NotIn", "value": ["DELETE"]}]}),
         _rule("deny-ctrl", kinds=("Deployment", "CronJob"),
               validate={"deny": {"conditions": {"any": [{"key": OP, "operator": "anynotin", "value": ["CREATE"]}]}}}),
+        # scalar string values that are not JSON: in.go / notin.go report an invalid type
+        # (both false), anyin.go & co. read them as a one-element list
+        _rule("pre-notin-scalar", pre={"all": [{"key": OP, "operator": "NotIn", "value": "DELETE"}]}),
+        _rule("pre-in-scalar", pre={"all": [{"key": OP, "operator": "In", "value": "DELETE"}]}),
+        _rule("pre-anynotin-scalar", pre={"all": [{"key": OP, "operator": "AnyNotIn", "value": "DELETE"}]}),
+        _rule("pre-notin-null", pre={"all": [{"key": OP, "operator": "NotIn", "value": "null"}]}),
+        _rule("pre-allnotin-true", pre={"all": [{"key": OP, "operator": "AllNotIn", "value": "true"}]}),
+        # a validate block with no handler still skips on false preconditions (validation.go:52)
+        _rule("pre-false-message-only", pre={"all": [{"key": OP, "operator": "Equals", "value": "DELETE"}]},
+              validate={"message": "m"}),
     ]
     pols = [_policy("folded", rules)]
     p = pss_policy("pre-pss", "restricted", "latest", kinds=("Pod",))
@@ -74,6 +84,38 @@ def test_fold_compiles():
     ps = K.PolicySet(folded_policy_set())
     assert ps.num_rules >= 14
     assert any(n.startswith("autogen/autogen-") for n in ps.rule_names)
+
+
+# Expected verdicts restated from the reference operators on key "CREATE" (CPU, oracle only):
+# in.go:60-92 keyExistsInArray, notin.go:45-53, anyin.go:61-101, allnotin.go:43-50.
+# 1 = pass (deny false), 2 = fail (deny true), 5 = skip (preconditions false).
+@pytest.mark.parametrize("op,value,want", [
+    ("NotIn", "DELETE", 5),          # not JSON => invalid type => NotIn false => preconditions skip
+    ("In", "DELETE", 5),
+    ("AnyNotIn", "DELETE", 2),       # json.Valid fails => ["DELETE"] => CREATE not in => true
+    ("NotIn", "null", 2),            # null decodes to an empty list => NotIn true
+    ("AllNotIn", "true", 5),         # valid JSON, not a []string => invalid => false
+    ("NotIn", ["DELETE"], 2),
+    ("In", ["CRE*"], 2),
+    ("In", ["*EATE", "x"], 2),
+])
+def test_oracle_in_notin_semantics(oracle, op, value, want):
+    pol = _policy("p", [_rule("r", pre={"all": [{"key": OP, "operator": op, "value": value}]})])
+    nd = b'{"apiVersion":"v1","kind":"Pod","metadata":{"name":"a","namespace":"d"},"spec":{}}'
+    assert int(oracle.validate([pol], nd)[0, 0]) == want
+
+
+def test_oracle_in_list_key_semantics(oracle):
+    """in.go:35-40 / setExistsInArray :108-140: a one-element key list equal to a string value
+    reports keyExists, so NotIn is true there (notin.go:55-63); list values match exactly."""
+    def deny(op, key, value):
+        return _rule("r", validate={"deny": {"conditions": {"all": [{"key": key, "operator": op, "value": value}]}}})
+    nd = b'{"apiVersion":"v1","kind":"Pod","metadata":{"name":"web","namespace":"d"},"spec":{}}'
+    name = "{{ request.object.metadata.name }}"
+    cases = [("NotIn", [name], "web", 2), ("In", [name], "web", 2), ("In", [name], ["we*"], 1),
+             ("NotIn", [name], ["we*"], 2), ("In", [name], ["web", "x"], 2), ("NotIn", [name], "[1]", 1)]
+    for op, key, value, want in cases:
+        assert int(oracle.validate([_policy("p", [deny(op, key, value)])], nd)[0, 0]) == want, (op, key, value)
 
 
 @pytest.mark.parametrize("cond", [
