@@ -1,13 +1,20 @@
 #!/usr/bin/env python3
-"""Headline benchmark: resource-rule evals/s, 1M synthetic Pods x PSS restricted
-(BASELINE.json metric/configs[1]) per GPU, weak-scaled over N GPUs (one process
-per GPU, resources sharded, no data-path collective; the per-rule counters are
-all-reduced once over RCCL after the timed region).
+"""Headline benchmark: resource-rule evals/s (BASELINE.json metric) per GPU, weak-scaled over N
+GPUs (one process per GPU, resources sharded, no data-path collective; the per-rule counters
+are all-reduced once over RCCL after the timed region).
 
-One step = one evaluation pass of the compiled program over one 1M-Pod shard
-resident in HBM (dictionary predicate pass + resource-scan kernel + counters).
-`--replicas` distinct shards are rotated so consecutive steps do not re-read a
-corpus out of the 256 MiB Infinity Cache.
+--config c2 (default, the metric's configuration, BASELINE.json configs[1]): 1M synthetic Pods
+    x the PSS restricted:latest policy (R = 3 rules after autogen) per GPU.
+--config c3: a 1/8 shard (1.25M rows) of 10M mixed resources x 200 wildcard ClusterPolicies
+    per GPU (configs[2]; the full 10M is the 8-GPU job).
+--config c5: 1M Pods / Deployments with 1-64 containers x the require-requests-limits /
+    disallow-latest-tag / host-ports / anchor pattern set per GPU (configs[4]).
+
+One step = one evaluation pass of the compiled program over one resident shard
+(kpe_evaluate_async: dictionary predicate pass, resource-scan kernel, pattern kernel when the
+program has pattern rules). `--replicas` distinct shards are rotated so consecutive C2 steps do
+not re-read a corpus out of the 256 MiB Infinity Cache. Per-rule counters are built once, after
+the timed region (kpe_fetch), not per step.
 """
 import argparse
 import json
@@ -21,25 +28,50 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--resources", type=int, default=1_000_000, help="Pods per GPU")
-    ap.add_argument("--replicas", type=int, default=8)
-    ap.add_argument("--cpu-sample", type=int, default=1_000_000, help="Pods in the CPU-baseline sample (0 = skip)")
+    ap.add_argument("--config", choices=("c2", "c3", "c5"), default="c2")
+    ap.add_argument("--resources", type=int, default=0, help="rows per GPU (0 = the config's size)")
+    ap.add_argument("--replicas", type=int, default=0, help="distinct shards rotated (0 = the config's default)")
+    ap.add_argument("--cpu-sample", type=int, default=-1, help="rows in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default="")
     args = ap.parse_args()
 
-    import numpy as np
+    import numpy as np  # noqa: F401
     import torch
     import torch.distributed as dist
 
     import kyverno_amd as K
     from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, max_over_ranks
-    from tests.policies import restricted_latest
+    from tests.policies import c3_policy_set, c5_policy_set, restricted_latest
+
+    cfg = args.config
+    if cfg == "c2":
+        policies, mix, seed, n_def, rep_def, docs = [restricted_latest()], K.SYNTH_PODS, 0xC2, 1_000_000, 8, False
+        workload = "C2: 1M synthetic Pods x PSS restricted:latest per GPU (R=3 rules after autogen)"
+    elif cfg == "c3":
+        policies, mix, seed, n_def, rep_def, docs = c3_policy_set(), K.SYNTH_C3, 0xC3, 1_250_000, 1, True
+        workload = ("C3: 1/8 shard (1.25M rows) of 10M mixed resources x 200 wildcard ClusterPolicies per GPU")
+    else:
+        policies, mix, seed, n_def, rep_def, docs = c5_policy_set(), K.SYNTH_FANOUT, 0xC5, 1_000_000, 1, True
+        workload = "C5: 1M Pods/Deployments with 1-64 containers x requests-limits/latest-tag/host-ports/anchor patterns"
+    n = args.resources or n_def
+    replicas = args.replicas or rep_def
+    traffic_json = args.traffic_json or os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -53,21 +85,27 @@ def main():
             dist.barrier()
 
     eng = K.Engine(ordinal=local)
-    policy = restricted_latest()
-    ps = K.PolicySet([policy])
+    ps = K.PolicySet(policies)
     R = ps.num_rules
-    n = args.resources
     corpora = []
-    t_setup = time.time()
-    for k in range(args.replicas):
-        # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus (seed 0xC2)
-        first = (rank * args.replicas + k) * n
-        nd = K.synth_resources(0xC2, n, mix=0, first_index=first)
-        c = K.Corpus(nd, docs=False)  # PSS only: no document tapes
+    t_flatten = t_upload = 0.0
+    for k in range(replicas):
+        # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus
+        first = (rank * replicas + k) * n
+        nd = K.synth_resources(seed, n, mix=mix, first_index=first)
+        t0 = time.perf_counter()
+        c = K.Corpus(nd, docs=docs)
+        t1 = time.perf_counter()
         del nd
         c.upload(eng.device)
+        t_flatten += t1 - t0
+        t_upload += time.perf_counter() - t1
         corpora.append(c)
-    t_setup = time.time() - t_setup
+    # end-to-end leg for one shard: flatten + H2D (measured above) + one synchronous evaluation
+    t0 = time.perf_counter()
+    eng.evaluate_async(ps, corpora[0])
+    eng.device.sync()
+    t_eval1 = time.perf_counter() - t0
     # correctness touch + counters from one synchronous evaluation per replica
     totals = [dict.fromkeys(COUNT_FIELDS, 0) for _ in range(R)]
     for c in corpora:
@@ -79,9 +117,6 @@ def main():
     for i in range(args.warmup):
         eng.evaluate_async(ps, corpora[i % len(corpora)])
     eng.device.sync()
-    eng.device.set_timing(True)
-    eng.device.kernel_stats(reset=True)
-    eng.device.set_timing(False)
 
     # ---- timed region: exactly K steps ----
     barrier()
@@ -96,44 +131,66 @@ def main():
     elapsed = max_over_ranks(elapsed, device="cuda")
     # the one real exchange: per-rule totals (R x 6 u64, RCCL over xGMI)
     totals = allreduce_counts(totals, device="cuda")
-    total_fail = totals[0]["fail"]
 
-    # ---- per-kernel timing pass (HIP events on the evaluation stream) ----
+    # ---- per-kernel timing pass: HIP events on the library's stream, launches serialised on
+    # one stream so each kernel's duration is its own (isolated, single-stream figure) ----
     eng.device.set_timing(True)
+    eng.device.kernel_stats(reset=True)
+    t1 = time.perf_counter()
     for i in range(args.steps):
         eng.evaluate_async(ps, corpora[i % len(corpora)])
     st = eng.device.kernel_stats(reset=True)
+    single_stream_ms = (time.perf_counter() - t1) / args.steps * 1e3
     eng.device.set_timing(False)
-    scan_ms = st.pss_kernel_ms / max(st.launches, 1)
-    dict_ms = st.dict_kernel_ms / max(st.launches, 1)
-    achieved = st.scan_bytes / (scan_ms * 1e-3) / 1e9
+    L = max(st.launches, 1)
+    scan_ms = st.pss_kernel_ms / L
+    dict_ms = st.dict_kernel_ms / L
+    pat_ms = st.pattern_kernel_ms / L
+    scan_achieved = st.scan_bytes / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else 0.0
 
     ms_per_step = elapsed / args.steps * 1e3
     evals = float(n) * R * world * args.steps
     value = evals / elapsed
 
     traffic = None
-    if os.path.exists(args.traffic_json):
+    if os.path.exists(traffic_json):
         try:
-            traffic = json.load(open(args.traffic_json)).get("scan_bytes_per_launch")
+            traffic = json.load(open(traffic_json)).get("scan_bytes_per_launch")
         except Exception:
             traffic = None
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
+    sample = args.cpu_sample if args.cpu_sample >= 0 else {"c2": 1_000_000, "c3": 200_000, "c5": 100_000}[cfg]
+    if rank == 0 and world == 1 and sample > 0:
         from tests.oracle_lib import load as load_oracle
 
         orc = load_oracle()
-        nd = K.synth_resources(0xC2, args.cpu_sample, mix=0)
+        nd = K.synth_resources(seed, sample, mix=mix)
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         t1 = time.perf_counter()
-        ref = orc.validate([policy], nd, nthreads=thr)
+        ref = orc.validate(policies, nd, nthreads=thr)
         dt = time.perf_counter() - t1
+        # single-thread leg on a 1/8 sub-sample (bounded run time)
+        sub = b"\n".join(nd.split(b"\n")[: max(1, sample // 8)])
+        t1 = time.perf_counter()
+        ref1 = orc.validate(policies, sub, nthreads=1)
+        dt1 = time.perf_counter() - t1
         cpu = {"value": ref.size / dt, "unit": "resource-rule evals/s", "cores": thr, "kind": "port",
-               "sample": f"{args.cpu_sample} C2 Pods x {R} rules (NDJSON parse + typed decode + evaluate), "
-                         f"oracle/ CPU restatement, {thr} threads, {dt:.2f}s"}
+               "single_thread_value": ref1.size / dt1, "cpu_model": cpu_model(),
+               "sample": f"{sample} {cfg.upper()} rows x {R} rules (NDJSON parse + typed decode + evaluate), "
+                         f"oracle/ CPU restatement, {thr} threads {dt:.2f}s; single-thread leg "
+                         f"{max(1, sample // 8)} rows {dt1:.2f}s"}
 
     if rank == 0:
+        scan_roof = {"bound": "hbm", "achieved": scan_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": scan_achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "kpe_scan_kernel",
+                     "kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes, "dict_kernel_ms": dict_ms,
+                     "pattern_kernel_ms": pat_ms,
+                     # the same bytes over the timed region's step time (launches of different
+                     # shards overlap on two streams there) and the isolated single-stream step
+                     "achieved_per_step": st.scan_bytes / (ms_per_step * 1e-3) / 1e9,
+                     "single_stream_step_ms": single_stream_ms}
+        e2e_s = t_flatten / replicas + t_upload / replicas + t_eval1
         line = {
             "metric": "resource-rule evals/sec, 1M Pods × PSS restricted, 1/8 GPU; % HBM BW",
             "value": value,
@@ -146,21 +203,18 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
-            "data": "synthetic (kpe_synth C2 generator, seed 0xC2)",
-            "config": {"workload": "C2: 1M synthetic Pods x PSS restricted:latest per GPU (R=3 rules after autogen)",
-                       "resources_per_gpu": n, "rules": R, "global_resources": n * world,
-                       "replicas_rotated": args.replicas, "parallelism": f"resource-sharded x{world}",
-                       "fail_fraction": total_fail / float(n * args.replicas * world),
+            "data": f"synthetic (kpe_synth {cfg.upper()} generator, seed {seed:#x})",
+            "config": {"workload": workload, "resources_per_gpu": n, "rules": R, "global_resources": n * world,
+                       "replicas_rotated": replicas, "parallelism": f"resource-sharded x{world}",
+                       # cells where the rule matched the resource (a RuleResponse exists), per s
+                       "matched_cell_evals_per_s": value * sum(n * replicas * world - totals[r]["na"]
+                                                               for r in range(R)) / float(n * replicas * world * R),
                        "counts_rule0": totals[0]},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "kernel": "kpe_scan_kernel", "kernel_ms": scan_ms, "dict_kernel_ms": dict_ms,
-                         # the same bytes over the timed region's step time (launches of
-                         # different shards overlap on two streams there)
-                         "achieved_per_step": st.scan_bytes / (ms_per_step * 1e-3) / 1e9,
-                         "alg_bytes_per_launch": st.scan_bytes},
+            "roofline": scan_roof,
             "cpu_baseline": cpu,
-            "setup_s": t_setup,
+            "e2e": {"e2e_evals_per_s": float(n) * R / e2e_s, "flatten_s": t_flatten / replicas,
+                    "upload_s": t_upload / replicas, "first_eval_s": t_eval1,
+                    "note": "one shard: host flatten (NDJSON -> columns) + H2D + one evaluation, not in value"},
         }
         print(json.dumps(line))
     if world > 1:

@@ -22,8 +22,16 @@ enum kpe_synth_mix {
   KPE_SYNTH_PODS = 0,   /* C2: Pods only                                      */
   KPE_SYNTH_MIXED = 1,  /* Pods, Deployments, DaemonSets, Jobs, CronJobs, Services, ConfigMaps */
   KPE_SYNTH_EDGE = 2,   /* MIXED + edge cases: nulls, windows pods, type errors, odd values */
-  KPE_SYNTH_SELECTORS = 3 /* C4: Deployments + Services, 8 labels from a 64-key vocabulary,
+  KPE_SYNTH_SELECTORS = 3, /* C4: Deployments + Services, 8 labels from a 64-key vocabulary,
                              namespaces ns-00000..ns-09999 */
+  KPE_SYNTH_FANOUT = 4,   /* C5: Pods (85%) and Deployments with 1-64 containers (truncated
+                             geometric, mean ~6) + 0-3 initContainers; images with / without
+                             tags, digests, registries; resources.requests/limits present,
+                             partial, empty or absent; ports with / without hostPort */
+  KPE_SYNTH_C3 = 5        /* C3: Pod 40%, Deployment 20%, Service 15%, ConfigMap 15%,
+                             Job / CronJob / StatefulSet 10%; names app-<word>-<c>, web-*,
+                             *-canary, *-db-*; namespaces team-<k>[-prod|-dev], *-prod,
+                             kube-system, default */
 };
 
 /* Generate n resources as NDJSON into a malloc'd buffer (*out, *len). Free with kpe_synth_free. */

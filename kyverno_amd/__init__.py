@@ -8,6 +8,12 @@ evaluation without a working gfx950 device raises KpeError.
 """
 from ._lib import KpeError, lib_path, load  # noqa: F401
 from .engine import (  # noqa: F401
+    SYNTH_C3,
+    SYNTH_EDGE,
+    SYNTH_FANOUT,
+    SYNTH_MIXED,
+    SYNTH_PODS,
+    SYNTH_SELECTORS,
     Corpus,
     Device,
     Engine,

@@ -1,5 +1,7 @@
 // Synthetic corpus generator (see include/kpe_synth.h). Benchmark/test utility.
+#include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -122,23 +124,127 @@ std::string selector_labels(Rng& r) {
   return l + "}";
 }
 
+// C5: irregular fan-out pods for the require-pod-requests-limits /
+// disallow-latest-tag / disallow-host-ports pattern set. Container counts follow a geometric
+// law of mean ~6 truncated to [1, 64] (redrawn above 64).
+void gen_fanout(std::string& o, Rng& r, int64_t idx) {
+  auto count = [&]() {
+    for (;;) {
+      const double u = r.u();
+      const int k = 1 + (int)std::floor(std::log(1.0 - u) / std::log(1.0 - 1.0 / 6.0));
+      if (k <= 64) return k;
+    }
+  };
+  const int nc = count();
+  const int ni = r.p(0.7) ? 0 : 1 + r.below(3);
+  auto ctr = [&](std::string& s, const std::string& name) {
+    s += "{\"name\":\"" + name + "\",\"image\":\"";
+    const std::string img = kImages[r.below(50)];
+    const double t = r.u();
+    if (t < 0.45) s += img + ":1." + std::to_string(r.below(30)) + "." + std::to_string(r.below(10));
+    else if (t < 0.65) s += img + ":latest";
+    else if (t < 0.80) s += img;  // no tag
+    else if (t < 0.90) s += img + "@sha256:" + std::to_string(1000000 + r.below(1000000));
+    else s += "ghcr.io/org-" + std::to_string(r.below(9)) + "/" + img + (r.p(0.5) ? ":2.0" : ":latest");
+    s += "\"";
+    const double pp = r.u();
+    if (pp < 0.4) s += ",\"imagePullPolicy\":\"Always\"";
+    else if (pp < 0.7) s += ",\"imagePullPolicy\":\"IfNotPresent\"";
+    const double q = r.u();
+    if (q < 0.75) {
+      s += ",\"resources\":{\"limits\":{\"memory\":\"" + std::to_string(64 << r.below(5)) + "Mi\",\"cpu\":\"" +
+           std::to_string(100 * (1 + r.below(8))) + "m\"},\"requests\":{\"cpu\":\"" +
+           std::to_string(50 * (1 + r.below(8))) + "m\",\"memory\":\"" + std::to_string(32 << r.below(5)) + "Mi\"}}";
+    } else if (q < 0.85) {
+      s += ",\"resources\":{\"limits\":{\"memory\":\"256Mi\"},\"requests\":{\"memory\":\"128Mi\"}}";  // no cpu request
+    } else if (q < 0.90) {
+      s += ",\"resources\":{\"limits\":{\"memory\":\"\"},\"requests\":{\"cpu\":\"1\",\"memory\":\"1Gi\"}}";
+    } else if (q < 0.95) {
+      s += ",\"resources\":{\"requests\":{}}";
+    }
+    const double pt = r.u();
+    if (pt < 0.30) s += ",\"ports\":[{\"containerPort\":8080}]";
+    else if (pt < 0.33) s += ",\"ports\":[{\"containerPort\":80,\"hostPort\":0},{\"containerPort\":443}]";
+    else if (pt < 0.36) s += ",\"ports\":[{\"containerPort\":9090,\"hostPort\":" + std::to_string(9000 + r.below(99)) + "}]";
+    s += "}";
+  };
+  std::string spec = "{";
+  if (ni) {
+    spec += "\"initContainers\":[";
+    for (int i = 0; i < ni; ++i) {
+      if (i) spec += ",";
+      ctr(spec, "init-" + std::to_string(i));
+    }
+    spec += "],";
+  }
+  spec += "\"containers\":[";
+  for (int i = 0; i < nc; ++i) {
+    if (i) spec += ",";
+    ctr(spec, "c-" + std::to_string(i));
+  }
+  spec += "]";
+  if (r.p(0.1)) spec += ",\"volumes\":[{\"name\":\"data\",\"hostPath\":{\"path\":\"/data\"}}]";
+  spec += "}";
+  char nsbuf[16];
+  snprintf(nsbuf, sizeof nsbuf, "ns-%04d", r.below(1000));
+  const std::string name = "res-" + std::to_string(idx);
+  const std::string labels = "{\"app\":\"app-" + std::to_string(r.below(200)) + "\"}";
+  if (r.p(0.85)) {
+    o += "{\"apiVersion\":\"v1\",\"kind\":\"Pod\",\"metadata\":{\"name\":\"" + name + "\",\"namespace\":\"" + nsbuf +
+         "\",\"labels\":" + labels + "},\"spec\":" + spec + "}";
+  } else {
+    o += "{\"apiVersion\":\"apps/v1\",\"kind\":\"Deployment\",\"metadata\":{\"name\":\"" + name + "\",\"namespace\":\"" +
+         nsbuf + "\",\"labels\":" + labels + "},\"spec\":{\"replicas\":2,\"selector\":{\"matchLabels\":" + labels +
+         "},\"template\":{\"metadata\":{\"labels\":" + labels + "},\"spec\":" + spec + "}}}";
+  }
+}
+
 void gen_one(std::string& o, uint64_t seed, int64_t idx, int mix) {
   Rng r(seed ^ ((uint64_t)idx * 0xD1B54A32D192ED03ull));
+  if (mix == KPE_SYNTH_FANOUT) {
+    gen_fanout(o, r, idx);
+    return;
+  }
   // ---- kind ----
   int kind = 0;  // 0 Pod, 1 Deployment, 2 DaemonSet, 3 Job, 4 CronJob, 5 Service, 6 ConfigMap, 7 StatefulSet
   const bool sel_mix = mix == KPE_SYNTH_SELECTORS;
+  const bool c3 = mix == KPE_SYNTH_C3;
   if (sel_mix) {
     kind = r.p(0.5) ? 1 : 5;
+  } else if (c3) {  // SURVEY.md 8(d) C3 ratios
+    double u = r.u();
+    kind = u < 0.40 ? 0 : u < 0.60 ? 1 : u < 0.75 ? 5 : u < 0.90 ? 6 : u < 0.9333 ? 3 : u < 0.9667 ? 4 : 7;
   } else if (mix >= KPE_SYNTH_MIXED) {
     double u = r.u();
     kind = u < 0.40 ? 0 : u < 0.60 ? 1 : u < 0.64 ? 2 : u < 0.67 ? 3 : u < 0.70 ? 4 : u < 0.85 ? 5 : u < 0.97 ? 6 : 7;
   }
   bool edge = mix == KPE_SYNTH_EDGE;
-  char nsbuf[16];
+  char nsbuf[32];
   if (sel_mix) snprintf(nsbuf, sizeof nsbuf, "ns-%05d", r.below(10000));
-  else snprintf(nsbuf, sizeof nsbuf, "ns-%04d", r.below(1000));
+  else if (c3) {
+    const double u = r.u();
+    const int t = r.below(40);
+    if (u < 0.35) snprintf(nsbuf, sizeof nsbuf, "team-%d-prod", t);
+    else if (u < 0.60) snprintf(nsbuf, sizeof nsbuf, "team-%d-dev", t);
+    else if (u < 0.75) snprintf(nsbuf, sizeof nsbuf, "team-%d", t);
+    else if (u < 0.85) snprintf(nsbuf, sizeof nsbuf, "shop-%d-prod", t % 7);
+    else if (u < 0.92) snprintf(nsbuf, sizeof nsbuf, "kube-system");
+    else snprintf(nsbuf, sizeof nsbuf, "default");
+  } else snprintf(nsbuf, sizeof nsbuf, "ns-%04d", r.below(1000));
   std::string ns = nsbuf;
   std::string name = "res-" + std::to_string(idx);
+  if (c3) {
+    static const char* kWords[12] = {"api", "web", "cart", "auth", "db", "cache", "queue", "search", "pay", "mail",
+                                     "log", "ui"};
+    const double u = r.u();
+    const std::string w = kWords[r.below(12)];
+    if (u < 0.40) name = "app-" + w + "-" + std::string(1, (char)('a' + r.below(26)));  // app-*-?
+    else if (u < 0.55) name = "app-" + w + "-" + std::to_string(idx % 1000);
+    else if (u < 0.70) name = "web-" + w + "-" + std::to_string(idx % 97);
+    else if (u < 0.80) name = w + "-db-" + std::to_string(idx % 13);
+    else if (u < 0.88) name = w + "-canary";
+    else name = "res-" + std::to_string(idx);
+  }
   static const char* kKinds[] = {"Pod", "Deployment", "DaemonSet", "Job", "CronJob", "Service", "ConfigMap", "StatefulSet"};
   static const char* kApi[] = {"v1", "apps/v1", "apps/v1", "batch/v1", "batch/v1", "v1", "v1", "apps/v1"};
   auto labels = [&]() {

@@ -174,6 +174,10 @@ class Corpus:
             pass
 
 
+# kpe_synth_mix (include/kpe_synth.h)
+SYNTH_PODS, SYNTH_MIXED, SYNTH_EDGE, SYNTH_SELECTORS, SYNTH_FANOUT, SYNTH_C3 = range(6)
+
+
 def synth_resources(seed: int, n: int, mix: int = 0, first_index: int = 0) -> bytes:
     """NDJSON from the synthetic generator (include/kpe_synth.h)."""
     L = load()

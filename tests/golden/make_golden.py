@@ -486,7 +486,19 @@ def chart_policies():
     return out
 
 
+def best_practices():
+    """test/best_practices/*.yaml (the policies commands/apply/command_test.go:17-230 applies;
+    C5 uses require_pod_requests_limits.yaml and disallow_latest_tag.yaml), keyed by file name."""
+    base = "test/best_practices"
+    out = {}
+    for f in sorted(os.listdir(os.path.join(REF, base))):
+        if f.endswith(".yaml"):
+            out[f] = [p for p in _yaml_docs(os.path.join(REF, base, f)) if p.get("kind") in ("ClusterPolicy", "Policy")]
+    return out
+
+
 if __name__ == "__main__":
+    _dump("best_practices.json", best_practices())
     _dump("chart_policies.json", chart_policies())
     _dump("engine_validate_cases.json", engine_validate_cases())
     _dump("cli_cases.json", cli_cases())

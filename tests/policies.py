@@ -129,3 +129,114 @@ def c4_policy_set():
                                   {"resources": {"namespaceSelector": {"matchExpressions": [
                                       {"key": "env", "operator": "NotIn", "values": ["dev"]}]}}}]),
     ]
+
+
+def _golden(name):
+    import json
+    import os
+    return json.load(open(os.path.join(os.path.dirname(__file__), "golden", name)))
+
+
+def _pattern_policy(name, pattern=None, any_pattern=None, kinds=("Pod",), annotations=None):
+    v = {"message": f"{name} failed"}
+    if pattern is not None:
+        v["pattern"] = pattern
+    else:
+        v["anyPattern"] = any_pattern
+    pol = {"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": name},
+           "spec": {"background": True, "validationFailureAction": "Audit",
+                    "rules": [{"name": name, "match": {"any": [{"resources": {"kinds": list(kinds)}}]},
+                               "validate": v}]}}
+    if annotations:
+        pol["metadata"]["annotations"] = dict(annotations)
+    return pol
+
+
+def c5_policy_set():
+    """C5: test/best_practices/require_pod_requests_limits.yaml and
+    disallow_latest_tag.yaml, chart baseline disallow-host-ports (nested =() arrays), and
+    conditional / existence / negation / equality-anchor variants shaped like the
+    pkg/engine/validation_test.go patterns (:111 conditional image, :1227 ^(containers),
+    :1375 X(hostPath)) and pkg/engine/validate/validate_test.go:1368 (`|` with `!`)."""
+    bp = _golden("best_practices.json")
+    chart = _golden("chart_policies.json")
+    pols = list(bp["require_pod_requests_limits.yaml"]) + list(bp["disallow_latest_tag.yaml"])
+    pols += [p for p in chart["baseline"] if p["metadata"]["name"] == "disallow-host-ports"]
+    pols.append(_pattern_policy("latest-needs-always", {"spec": {"containers": [
+        {"(image)": "*:latest", "imagePullPolicy": "Always"}]}}))
+    pols.append(_pattern_policy("untagged-not-always", {"spec": {"containers": [
+        {"name": "*", "(image)": "*:latest | !*:*", "imagePullPolicy": "!Always"}]}}))
+    pols.append(_pattern_policy("has-nginx", {"spec": {"^(containers)": [{"image": "nginx*"}]}}))
+    pols.append(_pattern_policy("no-hostpath", {"spec": {"=(volumes)": [{"name": "*", "X(hostPath)": "null"}]}}))
+    pols.append(_pattern_policy("memory-cap", {"spec": {"=(initContainers)": [
+        {"=(resources)": {"=(limits)": {"=(memory)": "<=1Gi"}}}], "containers": [
+        {"=(resources)": {"=(limits)": {"=(memory)": "<=512Mi", "=(cpu)": "<=2"}}}]}}))
+    pols.append(_pattern_policy("pinned-image", any_pattern=[
+        {"spec": {"containers": [{"image": "*@sha256:*"}]}},
+        {"spec": {"containers": [{"image": "*:?*.*"}]}}]))
+    return pols
+
+
+def c3_policy_set(n=200, seed=0xC3):
+    """C3: `n` ClusterPolicies whose match / exclude blocks use wildcard kinds
+    (`*`, `Deploy*`, `apps/v1/*`, `batch/v1/*`, `*Job`), names (`app-*-?`, `web-*`, `*-db-*`) and
+    namespaces (`team-*`, `*-prod`, `team-?-prod`) in any / all / legacy form, with
+    podSecurity (Pod-like kinds) or pattern handlers. Deterministic in `seed`."""
+    import random
+    rng = random.Random(seed)
+    kinds_pool = [["*"], ["Deploy*"], ["apps/v1/*"], ["Pod"], ["Pod", "Deployment"], ["batch/v1/*"], ["Service"],
+                  ["ConfigMap"], ["StatefulSet", "DaemonSet"], ["*Job"], ["v1/Pod"], ["Pod", "Deploy*"],
+                  ["Service", "ConfigMap"], ["apps/*/Deployment"], ["*/*"]]
+    podlike = {"Pod", "Deploy*", "apps/v1/*", "v1/Pod", "StatefulSet", "DaemonSet", "Deployment", "*Job",
+               "batch/v1/*", "apps/*/Deployment"}
+    names_pool = [None, None, ["app-*-?"], ["app-*"], ["web-*"], ["*-db-*"], ["app-api-?", "web-ui-*"]]
+    ns_pool = [None, None, ["team-*"], ["*-prod"], ["team-?-prod"], ["team-1*", "shop-*"], ["default"]]
+    excl_pool = [None, None, None, {"namespaces": ["kube-*"]}, {"names": ["*-canary"]}, {"kinds": ["ConfigMap"]},
+                 {"namespaces": ["*-dev"], "names": ["app-*"]}]
+    patterns = [
+        {"metadata": {"labels": {"app": "?*"}}},
+        {"metadata": {"labels": {"tier": "front* | back*"}}},
+        {"metadata": {"=(annotations)": {"=(owner)": "team-*"}}},
+        {"metadata": {"name": "!*-canary"}},
+        {"spec": {"=(replicas)": "<5"}},
+    ]
+    pod_patterns = [
+        {"spec": {"containers": [{"image": "!*:latest"}]}},
+        {"spec": {"=(hostNetwork)": False}},
+        {"spec": {"containers": [{"=(securityContext)": {"=(privileged)": False}}]}},
+    ]
+    pols = []
+    for i in range(n):
+        def resdesc():
+            rd = {"kinds": list(rng.choice(kinds_pool))}
+            nm = rng.choice(names_pool)
+            if nm:
+                rd["names"] = list(nm)
+            ns = rng.choice(ns_pool)
+            if ns:
+                rd["namespaces"] = list(ns)
+            return rd
+        rd = resdesc()
+        mode = rng.random()
+        if mode < 0.6:
+            match = {"any": [{"resources": rd}] + ([{"resources": resdesc()}] if rng.random() < 0.3 else [])}
+        elif mode < 0.8:
+            match = {"all": [{"resources": rd}, {"resources": {"namespaces": list(rng.choice(ns_pool[2:]))}}]}
+        else:
+            match = {"resources": rd}
+        rule = {"name": f"r{i}", "match": match}
+        ex = rng.choice(excl_pool)
+        if ex:
+            rule["exclude"] = {"any": [{"resources": dict(ex)}]}
+        is_pod = all(k in podlike for k in rd["kinds"])
+        h = rng.random()
+        if is_pod and h < 0.45:
+            rule["validate"] = {"podSecurity": {"level": rng.choice(["baseline", "restricted"]),
+                                                "version": rng.choice(["latest", "v1.24", "v1.29"])}}
+        elif is_pod and h < 0.75:
+            rule["validate"] = {"message": "m", "pattern": rng.choice(pod_patterns)}
+        else:
+            rule["validate"] = {"message": "m", "pattern": rng.choice(patterns)}
+        pols.append({"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": f"c3-{i:03d}"},
+                     "spec": {"background": True, "validationFailureAction": "Audit", "rules": [rule]}})
+    return pols
