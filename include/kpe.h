@@ -41,7 +41,11 @@ enum kpe_verdict {
   KPE_FAIL = 2,  /* RuleStatusFail                                         */
   KPE_WARN = 3,  /* RuleStatusWarn (reserved; never produced by validate)  */
   KPE_ERROR = 4, /* RuleStatusError (e.g. typed decode failure in getSpec) */
-  KPE_SKIP = 5   /* RuleStatusSkip                                         */
+  KPE_SKIP = 5,  /* RuleStatusSkip                                         */
+  KPE_UNDECIDED = 7 /* the device could not decide this cell (a documented device limit,
+                       e.g. a condition list longer than the VM's list capacity, a resource
+                       string that may be JSON where an operator would decode it): the
+                       caller evaluates this (resource, rule) with the reference engine */
 };
 
 /* Library status codes (0 = OK). Library-level failures set kpe_last_error(). */
@@ -62,7 +66,7 @@ typedef struct kpe_corpus kpe_corpus;   /* flattened, string-interned resources 
 /* Per-rule totals over a batch (pkg/engine/api/policyresponse.go:10-21 counting,
  * cmd/cli/kubectl-kyverno/processor/result.go:34-68 summary line). */
 typedef struct kpe_counts {
-  uint64_t na, pass, fail, warn, error, skip;
+  uint64_t na, pass, fail, warn, error, skip, undecided;
 } kpe_counts;
 
 /* Thread-local message for the last failing call on this thread. */

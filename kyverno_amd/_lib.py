@@ -20,7 +20,7 @@ class CliTotals(ctypes.Structure):
 
 
 class Counts(ctypes.Structure):
-    _fields_ = [(k, ctypes.c_uint64) for k in ("na", "pass_", "fail", "warn", "error", "skip")]
+    _fields_ = [(k, ctypes.c_uint64) for k in ("na", "pass_", "fail", "warn", "error", "skip", "undecided")]
 
 
 class KernelStats(ctypes.Structure):

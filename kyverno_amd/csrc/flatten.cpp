@@ -1147,6 +1147,8 @@ class DocBuilder {
     e.ival = v;
     const std::string t = std::to_string(v);
     e.text_off = text(t), e.text_len = (uint32_t)t.size();
+    const std::string sp = goval::sprint_float((double)v);  // condition context numbers are float64
+    text(sp), e.sp_len = (uint32_t)sp.size();
     scalar_attrs(e, t);
     return C.scal_int[v] = push_scalar(e);
   }
@@ -1160,6 +1162,8 @@ class DocBuilder {
     e.fval = v;
     const std::string t = goval::fmt_E(v);
     e.text_off = text(t), e.text_len = (uint32_t)t.size();
+    const std::string sp = goval::sprint_float(v);
+    text(sp), e.sp_len = (uint32_t)sp.size();
     scalar_attrs(e, goval::fmt_f(v));
     return C.scal_float[bits] = push_scalar(e);
   }

@@ -390,5 +390,32 @@ inline std::string fmt_E(double v) {
   return b;
 }
 
+// fmt.Sprint(float64) = strconv.AppendFloat(v, 'g', -1, 64): the shortest round-trip digits,
+// in %e form when the decimal exponent is < -4 or >= 6 (ftoa.go: "if precision was the
+// shortest possible, use precision 6 for this decision"), e.g. 1e+06, 123456, 1.5e-05. The
+// variables/operator set operators compare fmt.Sprint of JSON numbers (always float64 there).
+inline std::string sprint_float(double v) {
+  if (std::isnan(v)) return "NaN";
+  if (std::isinf(v)) return v > 0 ? "+Inf" : "-Inf";
+  if (v == 0) return std::signbit(v) ? "-0" : "0";
+  const std::string e = fmt_E(std::fabs(v));
+  const size_t E = e.find('E');
+  std::string d;
+  for (size_t i = 0; i < E; ++i)
+    if (dig(e[i])) d += e[i];
+  const int ex = atoi(e.c_str() + E + 1), nd = (int)d.size(), dp = ex + 1;
+  const std::string sign = v < 0 ? "-" : "";
+  if (ex < -4 || ex >= 6) {
+    std::string o = sign + d.substr(0, 1);
+    if (nd > 1) o += "." + d.substr(1);
+    char buf[16];
+    snprintf(buf, sizeof buf, "e%c%02d", ex < 0 ? '-' : '+', ex < 0 ? -ex : ex);
+    return o + buf;
+  }
+  if (dp <= 0) return sign + "0." + std::string(-dp, '0') + d;
+  if (dp >= nd) return sign + d + std::string(dp - nd, '0');
+  return sign + d.substr(0, dp) + "." + d.substr(dp);
+}
+
 }  // namespace goval
 }  // namespace kpe

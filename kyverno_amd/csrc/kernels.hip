@@ -96,14 +96,14 @@ __global__ void __launch_bounds__(256) kpe_pred_kernel(PredArgs a) {
   }
 }
 
-// Per-rule status histogram of a row-major N x R verdict matrix. Each wave takes
-// 64 rows at a time; per rule, one ballot per status, lane 0 accumulates in LDS;
-// one 64-bit global add per (rule, status) and block at the end.
+// Per-rule status histogram of a row-major N x R verdict matrix (8 slots per rule: the
+// kpe_verdict codes). Each wave takes 64 rows at a time; per rule, one ballot per status,
+// lane 0 accumulates in LDS; one 64-bit global add per (rule, status) and block at the end.
 __global__ void __launch_bounds__(256) kpe_count_kernel(const uint8_t* v, int64_t n, uint32_t R, uint32_t r0,
                                                         uint32_t rn, unsigned long long* out) {
-  extern __shared__ uint32_t hist[];  // rules [r0, r0 + rn) x 6
+  extern __shared__ uint32_t hist[];  // rules [r0, r0 + rn) x 8
   const uint32_t t = threadIdx.x, lane = t & 63u;
-  for (uint32_t i = t; i < rn * 6; i += 256) hist[i] = 0;
+  for (uint32_t i = t; i < rn * 8; i += 256) hist[i] = 0;
   __syncthreads();
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t tile = (int64_t)blockIdx.x * 4 + (t >> 6); tile * 64 < n; tile += nw) {
@@ -112,15 +112,15 @@ __global__ void __launch_bounds__(256) kpe_count_kernel(const uint8_t* v, int64_
     for (uint32_t r = 0; r < rn; ++r) {
       const uint32_t c = live ? v[row * R + r0 + r] : 0u;
 #pragma unroll
-      for (uint32_t s = 1; s < 6; ++s) {
+      for (uint32_t s = 1; s < 8; ++s) {
         const uint32_t k = (uint32_t)__popcll(__ballot(c == s));
-        if (lane == 0 && k) atomicAdd(&hist[r * 6 + s], k);
+        if (lane == 0 && k) atomicAdd(&hist[r * 8 + s], k);
       }
     }
   }
   __syncthreads();
-  for (uint32_t i = t; i < rn * 6; i += 256)
-    if (hist[i]) atomicAdd(&out[(size_t)r0 * 6 + i], (unsigned long long)hist[i]);
+  for (uint32_t i = t; i < rn * 8; i += 256)
+    if (hist[i]) atomicAdd(&out[(size_t)r0 * 8 + i], (unsigned long long)hist[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -808,7 +808,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
         uint32_t v = KPE_NA_;
         if (m && hd == H_PSS) v = err ? KPE_ERROR_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
         else if (m && hd == H_ERROR) v = KPE_ERROR_;
-        else if (m && hd == H_PATTERN) v = KPE_PENDING_;
+        else if (m && (hd == H_PATTERN || hd == H_COND)) v = KPE_PENDING_;
         else if (m && hd == H_CONST_SKIP) v = KPE_SKIP_;
         else if (m && hd == H_CONST_FAIL) v = KPE_FAIL_;
         else if (m && hd == H_CONST_PASS) v = KPE_PASS_;
@@ -876,7 +876,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
           pm = m & ~em & ~fm;
         } else if (handler == H_ERROR) {
           em = m;
-        } else if (handler == H_PATTERN) {
+        } else if (handler == H_PATTERN || handler == H_COND) {
           fm = em = m;  // both bits: KPE_PENDING_
         } else if (handler == H_CONST_SKIP) {
           pm = em = m;  // both bits: KPE_SKIP_ (no ApplyOne with constant handlers)
@@ -973,6 +973,27 @@ __global__ void __launch_bounds__(256) kpe_pattern_kernel(const PatArgs* __restr
   if (r < ap->n) pat_eval_row(*ap, r);
 }
 
+// ===========================================================================
+// Preconditions / deny / foreach-deny conditions (condvm.inl): one lane per resource resolves
+// the cells of the rules whose conditions read the resource. Runs after the scan kernel (which
+// marks H_COND cells pending and writes every other handler's verdict) and before the pattern
+// kernel (a pattern cell whose preconditions hold stays pending).
+// ===========================================================================
+namespace {
+#include "condvm.inl"
+}  // namespace
+
+__global__ void __launch_bounds__(128) kpe_cond_kernel(const CondArgs* __restrict__ ap) {
+  const int64_t r = (int64_t)blockIdx.x * 128 + threadIdx.x;
+  if (r < ap->n) cond_eval_row(*ap, r);
+}
+
+extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_cond_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dargs);
@@ -1020,13 +1041,13 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss,
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
                                        hipStream_t s) {
   if (R == 0) return hipSuccess;
-  hipError_t e = hipMemsetAsync(out, 0, (size_t)R * 6 * 8, s);
+  hipError_t e = hipMemsetAsync(out, 0, (size_t)R * 8 * 8, s);
   if (e != hipSuccess || n == 0) return e;
   const int64_t waves = (n + 63) / 64;
   const uint32_t grid = (uint32_t)std::min<int64_t>((waves + 3) / 4, 1024);
-  for (uint32_t r0 = 0; r0 < R; r0 += 2048) {  // <= 48 KiB of LDS histogram per launch
-    const uint32_t rn = std::min<uint32_t>(2048, R - r0);
-    hipLaunchKernelGGL(kpe_count_kernel, dim3(grid), dim3(256), (size_t)rn * 6 * 4, s, verdicts, n, R, r0, rn, out);
+  for (uint32_t r0 = 0; r0 < R; r0 += 1536) {  // <= 48 KiB of LDS histogram per launch
+    const uint32_t rn = std::min<uint32_t>(1536, R - r0);
+    hipLaunchKernelGGL(kpe_count_kernel, dim3(grid), dim3(256), (size_t)rn * 8 * 4, s, verdicts, n, R, r0, rn, out);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
   }

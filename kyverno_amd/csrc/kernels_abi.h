@@ -178,3 +178,27 @@ struct PatArgs {
   uint64_t nscal, ndoc;
   uint32_t* err;
 };
+
+// kpe_cond_kernel arguments (device-resident, one copy per binding)
+struct CondArgs {
+  int64_t n;
+  uint32_t R, ncr;                 // rules per row, condition rules
+  const uint32_t* doc;             // document tape (2 words per entry)
+  const uint64_t* doc_off;         // root entry of each resource
+  const KpeScalar* scal;
+  const uint8_t* scal_text;
+  const uint8_t* key_bytes;        // D_KEY dictionary (keys(@) results)
+  const uint32_t* key_off;
+  const uint2* ops;                // condition program (program.hpp CondProgram)
+  const KpeCExpr* exprs;
+  const KpeVTmpl* tmpls;
+  const KpeCCond* conds;
+  const KpeCBlock* blocks;
+  const KpeCForeach* fes;
+  const KpeCRule* rules;
+  const KpeScalar* ctab;           // constants
+  const uint8_t* ctext;
+  const uint32_t* clist;
+  const uint32_t* fkeys;           // field index -> D_KEY id + 1 (0: absent from the corpus)
+  uint8_t* verdicts;
+};

@@ -28,6 +28,7 @@ bool is_limit_error(const std::exception& e);
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
@@ -133,6 +134,8 @@ struct DeviceProgram {
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
   DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
+  // condition rules: compiled programs (program.hpp CondProgram)
+  DevBuf cops, cexprs, ctmpls, cconds, cblocks, cfes, crules, cconsts, ctext, cclist;
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
@@ -147,6 +150,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t fuse_lds = 0, fuse_words = 0, npairs = 0, fuse_pats = 0, fuse_patb = 0;
   DevBuf pmembers, pargs, perr;  // pattern rules: resolved members, PatArgs copy, check flags
   bool pargs_valid = false;
+  DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
+  bool cargs_valid = false;
   ScanArgs hargs{};    // what dargs holds
   bool args_valid = false;
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
@@ -431,6 +436,17 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.pbytes, pb, s0));
     HIPCHK(upload(D.proots, PP.roots, s0));
     HIPCHK(upload(D.prules, PP.rules, s0));
+    const auto& CP = P.cond;
+    HIPCHK(upload(D.cops, CP.ops, s0));
+    HIPCHK(upload(D.cexprs, CP.exprs, s0));
+    HIPCHK(upload(D.ctmpls, CP.tmpls, s0));
+    HIPCHK(upload(D.cconds, CP.conds, s0));
+    HIPCHK(upload(D.cblocks, CP.blocks, s0));
+    HIPCHK(upload(D.cfes, CP.fes, s0));
+    HIPCHK(upload(D.crules, CP.rules, s0));
+    HIPCHK(upload(D.cconsts, CP.consts, s0));
+    HIPCHK(upload(D.ctext, CP.ctext, s0));
+    HIPCHK(upload(D.cclist, CP.clist, s0));
   }
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
@@ -664,6 +680,16 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     HIPCHK(upload(B.pmembers, mem, s));
     B.pargs_valid = false;
   }
+  if (!P.cond.rules.empty()) {  // condition field names -> D_KEY ids + 1
+    if (!C.has_docs) return fail(KPE_E_STATE, "condition rules need a corpus flattened with KPE_CORPUS_DOCS");
+    std::vector<uint32_t> fk(P.cond.fields.size());
+    for (size_t i = 0; i < fk.size(); ++i) {
+      const int64_t id = C.dict[D_KEY].find(P.cond.fields[i]);
+      fk[i] = id < 0 ? 0u : (uint32_t)id + 1u;
+    }
+    HIPCHK(upload(B.cfkeys, fk, s));
+    B.cargs_valid = false;
+  }
   if (fused) memcpy(fimg.data(), pairs.data(), pairs.size() * 4);
   const uint32_t fuse_words = fused ? (uint32_t)fimg.size() : 0u;
   const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
@@ -690,7 +716,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
-  HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 6, 1) * 8));
+  HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 8, 1) * 8));
   if (!B.zero_page.p) {
     HIPCHK(B.zero_page.ensure(256));
     HIPCHK(hipMemsetAsync(B.zero_page.p, 0, 256, s));
@@ -840,6 +866,37 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
+  if (!P.cond.rules.empty()) {
+    if (!B.cargs_valid) {
+      CondArgs ca{};
+      ca.n = C.n;
+      ca.R = (uint32_t)R;
+      ca.ncr = (uint32_t)P.cond.rules.size();
+      ca.doc = D.doc.as<uint32_t>();
+      ca.doc_off = D.doc_off.as<uint64_t>();
+      ca.scal = D.scal.as<KpeScalar>();
+      ca.scal_text = D.scal_text.as<uint8_t>();
+      ca.key_bytes = D.dict_bytes[D_KEY].as<uint8_t>();
+      ca.key_off = D.dict_off[D_KEY].as<uint32_t>();
+      ca.ops = PD.cops.as<uint2>();
+      ca.exprs = PD.cexprs.as<KpeCExpr>();
+      ca.tmpls = PD.ctmpls.as<KpeVTmpl>();
+      ca.conds = PD.cconds.as<KpeCCond>();
+      ca.blocks = PD.cblocks.as<KpeCBlock>();
+      ca.fes = PD.cfes.as<KpeCForeach>();
+      ca.rules = PD.crules.as<KpeCRule>();
+      ca.ctab = PD.cconsts.as<KpeScalar>();
+      ca.ctext = PD.ctext.as<uint8_t>();
+      ca.clist = PD.cclist.as<uint32_t>();
+      ca.fkeys = B.cfkeys.as<uint32_t>();
+      ca.verdicts = B.verdicts.as<uint8_t>();
+      HIPCHK(B.cargs.ensure(sizeof(CondArgs)));
+      HIPCHK(hipMemcpyAsync(B.cargs.p, &ca, sizeof(CondArgs), hipMemcpyHostToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+      B.cargs_valid = true;
+    }
+    HIPCHK(kpe_launch_cond(B.cargs.as<CondArgs>(), C.n, s));
+  }
   if (!P.pat.rules.empty()) {
     if (!B.pargs_valid) {
       PatArgs pa{};
@@ -945,18 +1002,19 @@ static kpe_status fetch_impl(kpe_device* dev, const kpe_program* prog, const kpe
     // per-rule totals from the verdict matrix (processor/result.go:34-68 counting)
     HIPCHK(kpe_launch_count(B.verdicts.as<uint8_t>(), c->c->n, (uint32_t)R, B.counts_out.as<unsigned long long>(), s));
     const unsigned long long* src = B.counts_out.as<unsigned long long>();
-    std::vector<unsigned long long> h(R * 6);
-    HIPCHK(hipMemcpyAsync(h.data(), src, R * 6 * 8, hipMemcpyDeviceToHost, s));
+    std::vector<unsigned long long> h(R * 8);
+    HIPCHK(hipMemcpyAsync(h.data(), src, R * 8 * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     for (size_t r = 0; r < R; ++r) {
       uint64_t tot = 0;
-      for (int k = 1; k < 6; ++k) tot += h[r * 6 + k];
+      for (int k = 1; k < 8; ++k) tot += h[r * 8 + k];
       counts[r].na = (uint64_t)c->c->n - tot;
-      counts[r].pass = h[r * 6 + 1];
-      counts[r].fail = h[r * 6 + 2];
-      counts[r].warn = h[r * 6 + 3];
-      counts[r].error = h[r * 6 + 4];
-      counts[r].skip = h[r * 6 + 5];
+      counts[r].pass = h[r * 8 + 1];
+      counts[r].fail = h[r * 8 + 2];
+      counts[r].warn = h[r * 8 + 3];
+      counts[r].error = h[r * 8 + 4];
+      counts[r].skip = h[r * 8 + 5];
+      counts[r].undecided = h[r * 8 + 7];
     }
   }
   HIPCHK(hipStreamSynchronize(s));
@@ -1063,7 +1121,7 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
   bool first = true;
   for (size_t r = 0; r < P.rules.size(); ++r) {
     const uint8_t v = verdict_row[r];
-    if (v == KPE_NA || v > KPE_SKIP) continue;  // no RuleResponse
+    if (v == KPE_NA || v > KPE_SKIP) continue;  // no RuleResponse (KPE_UNDECIDED: the caller's)
     const kpe::RuleReport& rr = P.reports[r];
     const char* res = kResult[v];
     if (v == KPE_FAIL && !rr.scored) res = "warn";  // results.go:131-133

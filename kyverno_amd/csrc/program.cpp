@@ -903,7 +903,19 @@ bool fold_scalar(const JV& v, std::string* out, bool glob = false) {
     if (t.size() < 4 || t.compare(0, 2, "{{") != 0 || t.compare(t.size() - 2, 2, "}}") != 0) return false;
     std::string in = t.substr(2, t.size() - 4);
     size_t a = in.find_first_not_of(" \t"), b = in.find_last_not_of(" \t");
-    if (a == std::string::npos || in.substr(a, b - a + 1) != "request.operation") return false;
+    if (a == std::string::npos) return false;
+    in = in.substr(a, b - a + 1);
+    if (in != "request.operation") {
+      // `request.operation || '<raw string>'` (the chart idiom): CREATE is truthy, so `||`
+      // returns it; the right operand only has to parse
+      if (in.compare(0, 17, "request.operation") != 0) return false;
+      size_t i = in.find_first_not_of(" \t", 17);
+      if (i == std::string::npos || in.compare(i, 2, "||") != 0) return false;
+      i = in.find_first_not_of(" \t", i + 2);
+      if (i == std::string::npos || in[i] != '\'' || in.back() != '\'' || i + 1 >= in.size()) return false;
+      for (size_t k = i + 1; k + 1 < in.size(); ++k)
+        if (in[k] == '\'' || in[k] == '\\') return false;
+    }
     *out = "CREATE";
     return true;
   }
@@ -987,9 +999,562 @@ Fold fold_conditions(const JV* j) {
   return (any_ok == F_TRUE && all_ok == F_TRUE) ? F_TRUE : F_FALSE;
 }
 
+// ---- condition programs evaluated per resource (kpe_cond_kernel) -------------------------
+// Conditions that read the resource (or a foreach element) are compiled to the device program
+// of schema.h QO_* / KpeC*. The restated subset, with everything else refused (CompileError):
+//   * substitution (variables/vars.go:311-389): a key / value is a constant, a string that is
+//     exactly one {{ }} variable (which keeps its JSON type), or a list of those; `$(...)`,
+//     partial-string and nested variables are refused;
+//   * JMESPath (github.com/kyverno/go-jmespath, go.mod:33) over request.object,
+//     request.operation ("CREATE"), element / elementIndex: fields, quoted fields, [n], `[]`,
+//     `[*]`, `.[a, b]` multi-select of relative field chains, keys(@), `||` with a literal or
+//     another chain, raw-string and JSON literals. Parse errors of an empty expression are
+//     run-time errors; anything outside the subset is refused;
+//   * operators Equals / NotEquals / AnyIn / AllIn / AnyNotIn / AllNotIn / In / NotIn
+//     (variables/operator/*.go); InRange values of set operators are refused (as the oracle).
+namespace cq {
+
+enum Tok { T_EOF, T_ID, T_QID, T_NUM, T_DOT, T_STAR, T_FLAT, T_LBRACK, T_RBRACK, T_COMMA, T_LPAREN, T_RPAREN,
+           T_CUR, T_OR, T_LIT, T_RAW, T_OTHER };
+struct Token {
+  Tok t;
+  std::string s;
+  long n = 0;
+  JV lit;
+};
+// go-jmespath lexer.go, the token subset above (anything else is T_OTHER => refused)
+std::vector<Token> lex(const std::string& q) {
+  std::vector<Token> out;
+  size_t i = 0;
+  while (i < q.size()) {
+    const char c = q[i];
+    if (c == ' ' || c == '\t' || c == '\n' || c == '\r') {
+      ++i;
+      continue;
+    }
+    if (isalpha((unsigned char)c) || c == '_') {
+      size_t j = i;
+      while (j < q.size() && (isalnum((unsigned char)q[j]) || q[j] == '_')) ++j;
+      out.push_back({T_ID, q.substr(i, j - i)});
+      i = j;
+      continue;
+    }
+    if (isdigit((unsigned char)c) || (c == '-' && i + 1 < q.size() && isdigit((unsigned char)q[i + 1]))) {
+      size_t j = i + 1;
+      while (j < q.size() && isdigit((unsigned char)q[j])) ++j;
+      Token t{T_NUM, q.substr(i, j - i)};
+      t.n = atol(t.s.c_str());
+      out.push_back(t);
+      i = j;
+      continue;
+    }
+    if (c == '"') {  // quoted identifier (a JSON string)
+      size_t j = i + 1;
+      while (j < q.size() && q[j] != '"') j += q[j] == '\\' ? 2 : 1;
+      if (j >= q.size()) throw CompileError("JMESPath: unclosed quoted identifier");
+      const std::string body = q.substr(i, j + 1 - i);
+      JCur jc(body.data(), body.data() + body.size());
+      JV v = parse_value(jc);
+      if (!jc.ok() || v.t != JV::Str) throw CompileError("JMESPath: bad quoted identifier");
+      out.push_back({T_QID, v.s});
+      i = j + 1;
+      continue;
+    }
+    if (c == '\'') {  // raw string literal
+      std::string s;
+      size_t j = i + 1;
+      while (j < q.size() && q[j] != '\'') {
+        if (q[j] == '\\' && j + 1 < q.size() && q[j + 1] == '\'') {
+          s += '\'';
+          j += 2;
+        } else {
+          s += q[j++];
+        }
+      }
+      if (j >= q.size()) throw CompileError("JMESPath: unclosed raw string");
+      Token t{T_RAW, s};
+      t.lit = JV::str(s);
+      out.push_back(t);
+      i = j + 1;
+      continue;
+    }
+    if (c == '`') {  // JSON literal (an invalid one is a deprecated string literal)
+      std::string s;
+      size_t j = i + 1;
+      while (j < q.size() && q[j] != '`') {
+        if (q[j] == '\\' && j + 1 < q.size() && q[j + 1] == '`') {
+          s += '`';
+          j += 2;
+        } else {
+          s += q[j++];
+        }
+      }
+      if (j >= q.size()) throw CompileError("JMESPath: unclosed JSON literal");
+      Token t{T_LIT, s};
+      JCur jc(s.data(), s.data() + s.size());
+      JV v = parse_value(jc);
+      jc.ws();
+      if (jc.ok() && jc.pos() == s.data() + s.size()) t.lit = v;
+      else t.lit = JV::str(s);
+      out.push_back(t);
+      i = j + 1;
+      continue;
+    }
+    auto two = [&](char a, char b) { return c == a && i + 1 < q.size() && q[i + 1] == b; };
+    if (two('[', ']')) {
+      out.push_back({T_FLAT});
+      i += 2;
+      continue;
+    }
+    if (two('|', '|')) {
+      out.push_back({T_OR});
+      i += 2;
+      continue;
+    }
+    Tok t = T_OTHER;
+    switch (c) {
+      case '.': t = T_DOT; break;
+      case '*': t = T_STAR; break;
+      case '[': t = (i + 1 < q.size() && q[i + 1] == '?') ? T_OTHER : T_LBRACK; break;
+      case ']': t = T_RBRACK; break;
+      case ',': t = T_COMMA; break;
+      case '(': t = T_LPAREN; break;
+      case ')': t = T_RPAREN; break;
+      case '@': t = T_CUR; break;
+      default: break;
+    }
+    if (t == T_OTHER) throw CompileError(std::string("JMESPath construct '") + c + "' is not supported on the device");
+    out.push_back({t});
+    ++i;
+  }
+  out.push_back({T_EOF});
+  return out;
+}
+
+// Constant table shared by the policy's literals, JSON literals and request.operation.
+class Consts {
+ public:
+  explicit Consts(CondProgram& cp) : CP(cp) {}
+  uint32_t scalar(const JV& v) {
+    KpeScalar e{};
+    switch (v.t) {
+      case JV::Null: e.flags = SC_T_NULL; break;
+      case JV::Bool:
+        e.flags = SC_T_BOOL | SC_TEXT | (v.b ? SC_BTRUE : 0u);
+        text(e, v.b ? "true" : "false");
+        break;
+      case JV::Num: {  // the JSON context holds float64 numbers (encoding/json into interface{})
+        const double f = v.is_int ? (double)v.i : v.n;
+        e.flags = SC_T_FLOAT | SC_TEXT;
+        e.fval = f;
+        text(e, goval::fmt_E(f));
+        const std::string sp = goval::sprint_float(f);
+        CP.ctext.insert(CP.ctext.end(), sp.begin(), sp.end());
+        e.sp_len = (uint32_t)sp.size();
+        break;
+      }
+      case JV::Str: {
+        e.flags = SC_T_STR | SC_TEXT;
+        text(e, v.s);
+        int64_t i;
+        double f;
+        if (goval::parse_int(v.s, &i)) e.flags |= SC_PINT, e.ival = i;
+        if (goval::parse_float(v.s, &f)) e.flags |= SC_PFLOAT, e.fval = f;
+        int64_t d;
+        if (goval::parse_duration(v.s, &d)) e.flags |= SC_DUR, e.dur = d;
+        goval::Quantity q;
+        if (goval::parse_quantity(v.s, &q)) {
+          e.flags |= SC_QTY | (q.neg ? SC_QNEG : 0u);
+          goval::qty_key(q, &e.qexp, &e.qlo, &e.qhi);
+        }
+        json_list(e, v.s);
+        break;
+      }
+      default: throw CompileError("condition constant: objects are not supported on the device");
+    }
+    CP.consts.push_back(e);
+    return (uint32_t)CP.consts.size() - 1;
+  }
+  // a list of constants (SC_T_ARR)
+  uint32_t list(const std::vector<uint32_t>& items) {
+    KpeScalar e{};
+    e.flags = SC_T_ARR;
+    e.text_off = (uint32_t)CP.clist.size();
+    e.text_len = (uint32_t)items.size();
+    CP.clist.insert(CP.clist.end(), items.begin(), items.end());
+    CP.consts.push_back(e);
+    return (uint32_t)CP.consts.size() - 1;
+  }
+  uint32_t value(const JV& v) {
+    if (v.t == JV::Arr) {
+      std::vector<uint32_t> items;
+      for (auto& x : v.a) {
+        if (x.t == JV::Arr || x.t == JV::Obj) throw CompileError("condition constant: nested lists are not supported");
+        items.push_back(scalar(x));
+      }
+      return list(items);
+    }
+    return scalar(v);
+  }
+
+ private:
+  CondProgram& CP;
+  void text(KpeScalar& e, const std::string& s) {
+    e.text_off = (uint32_t)CP.ctext.size();
+    e.text_len = (uint32_t)s.size();
+    CP.ctext.insert(CP.ctext.end(), s.begin(), s.end());
+  }
+  // A string value of a set / In operator is decoded as a JSON []string when json.Valid
+  // (anyin.go:81-88; in.go:74-78 decodes it straight away): SC_JVALID marks valid JSON, SC_JLIST
+  // a successful []string decode whose elements are the constant list packed in ival.
+  void json_list(KpeScalar& e, const std::string& s) {
+    JCur c(s.data(), s.data() + s.size());
+    c.ws();
+    if (c.pos() == s.data() + s.size()) return;  // empty / blank: not JSON
+    JV v = parse_value(c);
+    c.ws();
+    if (!c.ok() || c.pos() != s.data() + s.size()) return;
+    e.flags |= SC_JVALID;
+    if (v.t == JV::Null) {  // null decodes to a nil slice
+      e.flags |= SC_JLIST;
+      e.ival = (int64_t)CP.clist.size();  // count 0
+      return;
+    }
+    if (v.t != JV::Arr) return;
+    std::vector<uint32_t> items;
+    for (auto& x : v.a) {
+      if (x.t == JV::Null) items.push_back(scalar(JV::str("")));  // null => "" in a []string
+      else if (x.t == JV::Str) items.push_back(scalar(x));
+      else return;                                                 // Unmarshal type error
+    }
+    e.flags |= SC_JLIST;
+    e.ival = (int64_t)CP.clist.size() | ((int64_t)items.size() << 32);
+    CP.clist.insert(CP.clist.end(), items.begin(), items.end());
+  }
+};
+
+// Parser of the restated JMESPath subset into schema.h QO_* ops.
+class QueryParser {
+ public:
+  QueryParser(CondProgram& cp, Consts& k) : CP(cp), K(k) {}
+
+  // a whole query (a {{ }} variable text or a foreach list); returns the expression index
+  uint32_t compile(const std::string& q0) {
+    std::string q = q0;
+    while (!q.empty() && isspace((unsigned char)q.back())) q.pop_back();
+    size_t b = 0;
+    while (b < q.size() && isspace((unsigned char)q[b])) ++b;
+    q = q.substr(b);
+    if (q.empty()) {  // "invalid query (nil)": an evaluation error at run time
+      KpeCExpr e{(uint32_t)CP.ops.size() / 2, 1, 0, CE_NONE};
+      CP.ops.insert(CP.ops.end(), {QO_ERROR, 0u});
+      CP.exprs.push_back(e);
+      return (uint32_t)CP.exprs.size() - 1;
+    }
+    t_ = lex(q);
+    i_ = 0;
+    std::vector<std::vector<uint32_t>> chains;
+    std::vector<bool> plain;
+    for (;;) {
+      bool pl = true;
+      chains.push_back(chain(&pl));
+      plain.push_back(pl);
+      if (cur().t == T_OR) {
+        ++i_;
+        continue;
+      }
+      break;
+    }
+    if (cur().t != T_EOF) throw CompileError("JMESPath expression outside the device subset: " + q);
+    // `a || b || c`: left-associative N_OR nodes; the first truthy operand wins, else the last
+    uint32_t next = CE_NONE;
+    for (size_t k = chains.size(); k-- > 0;) {
+      KpeCExpr e{(uint32_t)CP.ops.size() / 2, (uint32_t)chains[k].size() / 2, 0, next};
+      // strict (NotFoundError on a missing member) only for a query that is one plain chain
+      if (chains.size() == 1 && plain[k]) e.flags |= CE_STRICT;
+      CP.ops.insert(CP.ops.end(), chains[k].begin(), chains[k].end());
+      CP.exprs.push_back(e);
+      next = (uint32_t)CP.exprs.size() - 1;
+    }
+    return next;
+  }
+
+ private:
+  CondProgram& CP;
+  Consts& K;
+  std::vector<Token> t_;
+  size_t i_ = 0;
+  const Token& cur() const { return t_[i_]; }
+  const Token& peek(size_t k = 1) const { return t_[std::min(i_ + k, t_.size() - 1)]; }
+  static void op(std::vector<uint32_t>& o, uint32_t x, uint32_t y = 0) { o.push_back(x), o.push_back(y); }
+  uint32_t field(const std::string& name) {
+    for (size_t k = 0; k < CP.fields.size(); ++k)
+      if (CP.fields[k] == name) return (uint32_t)k;
+    CP.fields.push_back(name);
+    return (uint32_t)CP.fields.size() - 1;
+  }
+  bool name_tok() const { return cur().t == T_ID || cur().t == T_QID; }
+  // relative chain inside a multi-select list: fields and indexes only
+  std::vector<uint32_t> rel_chain() {
+    std::vector<uint32_t> o;
+    if (!name_tok()) throw CompileError("JMESPath multi-select item outside the device subset");
+    op(o, QO_FIELD, field(cur().s));
+    ++i_;
+    for (;;) {
+      if (cur().t == T_DOT && (peek().t == T_ID || peek().t == T_QID)) {
+        op(o, QO_FIELD, field(peek().s));
+        i_ += 2;
+      } else if (cur().t == T_LBRACK && peek().t == T_NUM && peek(2).t == T_RBRACK) {
+        op(o, QO_INDEX, (uint32_t)(int32_t)peek().n);
+        i_ += 3;
+      } else {
+        return o;
+      }
+    }
+  }
+  std::vector<uint32_t> chain(bool* plain) {
+    std::vector<uint32_t> o;
+    // ---- root ----
+    if (cur().t == T_RAW || cur().t == T_LIT) {
+      op(o, QO_CONST, K.value(cur().lit));
+      ++i_;
+      *plain = false;
+      if (cur().t != T_OR && cur().t != T_EOF) throw CompileError("JMESPath: steps after a literal are not supported");
+      return o;
+    }
+    if (cur().t != T_ID) throw CompileError("JMESPath root outside the device subset");
+    const std::string r = cur().s;
+    ++i_;
+    if (r == "request") {
+      if (cur().t != T_DOT || peek().t != T_ID || (peek().s != "object" && peek().s != "operation"))
+        throw CompileError("context value request." + (peek().t == T_ID ? peek().s : std::string("?")) +
+                           " is not available to device conditions");
+      if (peek().s == "object") op(o, QO_OBJ);
+      else op(o, QO_CONST, K.scalar(JV::str("CREATE")));  // background scans / CLI: CREATE
+      i_ += 2;
+    } else if (r == "element" || r == "element0") {
+      op(o, QO_EL);
+    } else if (r == "elementIndex" || r == "elementIndex0") {
+      op(o, QO_IDX);
+    } else {
+      throw CompileError("context value " + r + " is not available to device conditions");
+    }
+    // ---- steps ----
+    bool proj = false;  // inside a projection (steps apply per element)
+    bool keys_open = false;
+    for (;;) {
+      const Token& t = cur();
+      if (keys_open && t.t != T_FLAT) throw CompileError("keys(@) inside a projection must be flattened");
+      if (t.t == T_DOT && (peek().t == T_ID || peek().t == T_QID)) {
+        if (peek().t == T_ID && peek().s == "keys" && peek(2).t == T_LPAREN) {
+          if (peek(3).t != T_CUR || peek(4).t != T_RPAREN) throw CompileError("keys() argument other than @");
+          op(o, QO_KEYS);
+          *plain = false;
+          keys_open = proj;
+          i_ += 5;
+          continue;
+        }
+        op(o, QO_FIELD, field(peek().s));
+        i_ += 2;
+      } else if (t.t == T_LBRACK && peek().t == T_NUM && peek(2).t == T_RBRACK) {
+        op(o, QO_INDEX, (uint32_t)(int32_t)peek().n);
+        i_ += 3;
+      } else if (t.t == T_FLAT) {
+        op(o, QO_FLAT);
+        *plain = false;
+        proj = true, keys_open = false;
+        ++i_;
+      } else if (t.t == T_LBRACK && peek().t == T_STAR && peek(2).t == T_RBRACK) {
+        op(o, QO_STAR);
+        *plain = false;
+        proj = true;
+        i_ += 3;
+      } else if (t.t == T_DOT && peek().t == T_LBRACK) {
+        if (proj) throw CompileError("multi-select inside a projection is not supported on the device");
+        i_ += 2;
+        std::vector<std::vector<uint32_t>> items;
+        for (;;) {
+          items.push_back(rel_chain());
+          if (cur().t == T_RBRACK) break;
+          if (cur().t != T_COMMA) throw CompileError("JMESPath multi-select outside the device subset");
+          ++i_;
+        }
+        ++i_;
+        op(o, QO_MSL | (uint32_t)items.size() << 8);
+        for (auto& it : items) {
+          op(o, QO_ITEM | (uint32_t)(it.size() / 2) << 8);
+          o.insert(o.end(), it.begin(), it.end());
+        }
+        *plain = false;
+      } else {
+        break;
+      }
+    }
+    if (keys_open) throw CompileError("keys(@) inside a projection must be flattened");
+    return o;
+  }
+};
+
+// variables.replaceBracesAndTrimSpaces on the text of one {{ }} match
+std::string var_text(const std::string& v) {
+  std::string s;
+  for (size_t i = 0; i < v.size(); ++i) {
+    if ((v[i] == '{' || v[i] == '}') && i + 1 < v.size() && v[i + 1] == v[i]) {
+      ++i;
+      continue;
+    }
+    s += v[i];
+  }
+  return pc::trim_ws(s);
+}
+// regex.RegexVariables `(^|[^\\])(\{\{(?:\{[^{}]*\}|[^{}])*\}\})`: the first match at or after from
+bool next_var(const std::string& s, size_t from, size_t* st, size_t* en) {
+  for (size_t i = from; i + 1 < s.size(); ++i) {
+    if (s[i] != '{' || s[i + 1] != '{') continue;
+    if (i > 0 && s[i - 1] == '\\') continue;
+    size_t j = i + 2;
+    bool ok = false;
+    while (j < s.size()) {
+      if (s[j] == '}' && j + 1 < s.size() && s[j + 1] == '}') {
+        ok = true;
+        break;
+      }
+      if (s[j] == '{') {
+        size_t k = j + 1;
+        while (k < s.size() && s[k] != '{' && s[k] != '}') ++k;
+        if (k >= s.size() || s[k] != '}') break;
+        j = k + 1;
+        continue;
+      }
+      if (s[j] == '}') break;
+      ++j;
+    }
+    if (ok) {
+      *st = i, *en = j + 2;
+      return true;
+    }
+  }
+  return false;
+}
+
+class CondCompiler {
+ public:
+  explicit CondCompiler(CondProgram& cp) : CP(cp), K(cp), Q(cp, K) {}
+
+  // a condition key / value after substitution
+  uint32_t tmpl(const JV& v, int depth = 0) {
+    KpeVTmpl t{};
+    if (v.t == JV::Str) {
+      if (v.s.find("$(") != std::string::npos) throw CompileError("$(...) references in conditions are not supported");
+      size_t st, en;
+      if (!next_var(v.s, 0, &st, &en)) {
+        if (v.s.find("\\{{") != std::string::npos) throw CompileError("escaped variables in conditions");
+        t.kind = VT_CONST, t.a = K.scalar(v);
+      } else {
+        if (st != 0 || en != v.s.size()) throw CompileError("partial-string variables in conditions are not supported");
+        const std::string q = var_text(v.s);
+        if (q == "@" || q.find("{{") != std::string::npos) throw CompileError("{{@}} / nested variables");
+        t.kind = VT_QUERY, t.a = Q.compile(q);
+      }
+    } else if (v.t == JV::Arr && depth == 0 && has_var(v)) {
+      std::vector<uint32_t> el;
+      for (auto& x : v.a) {
+        if (x.t == JV::Arr || x.t == JV::Obj) throw CompileError("nested lists with variables");
+        el.push_back(tmpl(x, 1));
+      }
+      t.kind = VT_ARRAY, t.a = el.empty() ? 0u : el[0], t.b = (uint32_t)el.size();
+      // element templates are contiguous: re-emit them in order
+      const uint32_t base = (uint32_t)CP.tmpls.size();
+      for (uint32_t k : el) CP.tmpls.push_back(CP.tmpls[k]);
+      t.a = base;
+    } else if (v.t == JV::Obj) {
+      throw CompileError("object condition keys / values are not supported on the device");
+    } else {
+      t.kind = VT_CONST, t.a = K.value(v);
+    }
+    CP.tmpls.push_back(t);
+    return (uint32_t)CP.tmpls.size() - 1;
+  }
+  uint32_t condition(const JV& c) {
+    if (c.t != JV::Obj) throw CompileError("condition is not an object");
+    std::string op;
+    for (char ch : sv(c.get("operator"))) op += (char)tolower((unsigned char)ch);
+    uint32_t o;
+    if (op == "equal" || op == "equals") o = CO_EQ;
+    else if (op == "notequal" || op == "notequals") o = CO_NE;
+    else if (op == "anyin") o = CO_ANYIN;
+    else if (op == "allin") o = CO_ALLIN;
+    else if (op == "anynotin") o = CO_ANYNOTIN;
+    else if (op == "allnotin") o = CO_ALLNOTIN;
+    else if (op == "in") o = CO_IN;
+    else if (op == "notin") o = CO_NOTIN;
+    else throw CompileError("condition operator '" + sv(c.get("operator")) + "' is not supported on the device");
+    static const JV null_v;
+    const JV* k = c.get("key");
+    const JV* v = c.get("value");
+    const JV& vv = v ? *v : null_v;
+    if (vv.t == JV::Str && o >= CO_ANYIN && o <= CO_ALLNOTIN) {
+      size_t st, en;
+      if (!next_var(vv.s, 0, &st, &en) && in_range(vv.s)) throw CompileError("InRange values of set operators");
+    }
+    KpeCCond cc{o, tmpl(k ? *k : null_v), tmpl(vv), 0};
+    CP.conds.push_back(cc);
+    return (uint32_t)CP.conds.size() - 1;
+  }
+  // utils.TransformConditions: a list => the deprecated form; a map => any / all
+  uint32_t block(const JV* j) {
+    KpeCBlock b{};
+    std::vector<KpeCCond> any, all;
+    auto collect = [&](const JV& arr, std::vector<KpeCCond>& dst) {
+      for (auto& e : arr.a) dst.push_back(CP.conds[condition(e)]);
+    };
+    if (j && j->t == JV::Arr) {
+      collect(*j, all);
+    } else if (j && j->t == JV::Obj) {
+      const JV* a = j->get("any");
+      const JV* l = j->get("all");
+      if (a && a->t == JV::Arr) b.flags |= CB_HAS_ANY, collect(*a, any);
+      else if (a && a->t != JV::Null) throw CompileError("condition block 'any' is not a list");
+      if (l && l->t == JV::Arr) collect(*l, all);
+      else if (l && l->t != JV::Null) throw CompileError("condition block 'all' is not a list");
+    } else if (j && j->t != JV::Null) {
+      throw CompileError("condition block");
+    }
+    b.c0 = (uint32_t)CP.conds.size();
+    b.nany = (uint32_t)any.size(), b.nall = (uint32_t)all.size();
+    CP.conds.insert(CP.conds.end(), any.begin(), any.end());
+    CP.conds.insert(CP.conds.end(), all.begin(), all.end());
+    CP.blocks.push_back(b);
+    return (uint32_t)CP.blocks.size() - 1;
+  }
+  uint32_t list_query(const std::string& q) { return Q.compile(q); }
+
+ private:
+  CondProgram& CP;
+  Consts K;
+  QueryParser Q;
+  static bool has_var(const JV& v) {
+    size_t a, b;
+    if (v.t == JV::Str) return next_var(v.s, 0, &a, &b);
+    for (auto& x : v.a)
+      if (has_var(x)) return true;
+    return false;
+  }
+  // operator.GetOperatorFromStringPattern == InRange (operator/operator.go:7-61)
+  static bool in_range(const std::string& s) {
+    for (const char* p : {">=", "<=", ">", "<", "!"})
+      if (!s.compare(0, strlen(p), p)) return false;
+    std::string l, r;
+    if (pc::split_range(s, "!-", &l, &r)) return false;
+    return pc::split_range(s, "-", &l, &r);
+  }
+};
+
+}  // namespace cq
+
 class Lowerer {
  public:
-  explicit Lowerer(Program& p) : P(p) {}
+  explicit Lowerer(Program& p) : P(p), CC(p.cond) {}
 
   static void to_float(JV& v) {
     if (v.t == JV::Num && v.is_int) v.is_int = false, v.n = (double)v.i;
@@ -1319,23 +1884,30 @@ class Lowerer {
     bool has_validate = nonempty(v);
     const JV* ps = v ? v->get("podSecurity") : nullptr;
     std::string rname = sv(r.get("name"));
-    // preconditions (validate_resource.go:121-132): folded at compile time or refused
+    // preconditions (engine.go:278-285): folded at compile time, else evaluated per resource by
+    // kpe_cond_kernel
     Fold pre = F_TRUE;
+    uint32_t pre_block = CE_NONE;
     const JV* pre_raw = r.get("preconditions");  // any non-null block is evaluated (utils.go:78-95)
+    if (has_validate && nonempty(r.get("context")))
+      throw CompileError("rule '" + rname + "': context entries are not supported on the device");
     if (has_validate && pre_raw && pre_raw->t != JV::Null) {
-      if (nonempty(r.get("context")))
-        throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
-      pre = fold_conditions(r.get("preconditions"));
-      if (pre == F_NO) throw CompileError("rule '" + rname + "': preconditions are not supported yet");
+      pre = fold_conditions(pre_raw);
+      if (pre == F_NO) {
+        try {
+          pre_block = CC.block(pre_raw);
+        } catch (const CompileError& e) {
+          throw CompileError("rule '" + rname + "': preconditions: " + e.what());
+        }
+      }
     }
+    KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0};
     if (!has_validate) {
       k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
       if (nonempty(r.get("verifyImages"))) throw CompileError("rule '" + rname + "': verifyImages is not supported");
     } else if (nonempty(v->get("manifests"))) {
       throw CompileError("rule '" + rname + "': validate.manifests is not supported");
     } else if (ps && ps->t == JV::Obj && nonempty(ps)) {
-      if (nonempty(r.get("context")))
-        throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
       const JV* ex = ps->get("exclude");
       if (ex && ex->t == JV::Arr && !ex->a.empty())
         throw CompileError("rule '" + rname + "': podSecurity.exclude is not supported on the device yet");
@@ -1353,19 +1925,23 @@ class Lowerer {
       auto present = [&](const char* key) { return v->get(key) && v->get(key)->t != JV::Null; };
       if (present("deny")) {
         // validateDeny (validate_resource.go:268-279): conditions true => fail, else pass
-        if (nonempty(r.get("context")))
-          throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
         const JV* d = v->get("deny");
-        const Fold f = d->t == JV::Obj ? fold_conditions(d->get("conditions")) : F_NO;
-        if (f == F_NO) throw CompileError("rule '" + rname + "': validate.deny is not supported on the device yet");
-        k.handler = f == F_TRUE ? H_CONST_FAIL : H_CONST_PASS;
+        if (d->t != JV::Obj) throw CompileError("rule '" + rname + "': validate.deny is not an object");
+        const Fold f = fold_conditions(d->get("conditions"));
+        if (f != F_NO) {
+          k.handler = f == F_TRUE ? H_CONST_FAIL : H_CONST_PASS;
+        } else {
+          try {
+            crule.deny = CC.block(d->get("conditions"));
+          } catch (const CompileError& e) {
+            throw CompileError("rule '" + rname + "': validate.deny: " + e.what());
+          }
+          crule.kind = CR_DENY;
+          k.handler = H_COND;
+        }
       } else if (pre == F_FALSE && (present("pattern") || present("anyPattern"))) {
-        if (nonempty(r.get("context")))
-          throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
         k.handler = H_CONST_SKIP;  // patterns are never evaluated
       } else if (present("pattern") || present("anyPattern")) {
-        if (nonempty(r.get("context")))
-          throw CompileError("rule '" + rname + "': preconditions/context are not supported yet");
         if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with pattern rules is not supported");
         pc::PatCompiler pcomp(P.pat, [&](const std::string& g) {
           const int32_t id = pred(D_KEY, {g});
@@ -1395,6 +1971,32 @@ class Lowerer {
         }
         P.pat.rules.push_back(pr);
         k.handler = H_PATTERN;
+      } else if (v->get("foreach") && v->get("foreach")->t == JV::Arr && !v->get("foreach")->a.empty()) {
+        // validateForEach (validate_resource.go:186-254): entries with a deny only
+        crule.kind = CR_FOREACH;
+        crule.fe0 = (uint32_t)P.cond.fes.size();
+        std::vector<KpeCForeach> fes;
+        try {
+          for (auto& e : v->get("foreach")->a) {
+            if (e.t != JV::Obj || !e.get("deny") || nonempty(e.get("pattern")) || nonempty(e.get("anyPattern")) ||
+                nonempty(e.get("foreach")) || nonempty(e.get("context")))
+              throw CompileError("foreach entries other than deny are not supported on the device");
+            KpeCForeach f{};
+            f.list = CC.list_query(sv(e.get("list")));
+            const JV* fp = e.get("preconditions");
+            f.pre = (fp && fp->t != JV::Null) ? CC.block(fp) : CE_NONE;
+            const JV* dn = e.get("deny");
+            f.deny = CC.block(dn->t == JV::Obj ? dn->get("conditions") : nullptr);
+            const JV* sc = e.get("elementScope");
+            f.scope = (sc && sc->t == JV::Bool) ? (sc->b ? 2u : 1u) : 0u;
+            fes.push_back(f);
+          }
+        } catch (const CompileError& e) {
+          throw CompileError("rule '" + rname + "': validate.foreach: " + e.what());
+        }
+        P.cond.fes.insert(P.cond.fes.end(), fes.begin(), fes.end());
+        crule.nfe = (uint32_t)fes.size();
+        k.handler = H_COND;
       } else if (nonempty(v->get("foreach")) || nonempty(v->get("cel"))) {
         throw CompileError("rule '" + rname + "': validate.foreach/cel are not supported on the device yet");
       } else {
@@ -1405,10 +2007,15 @@ class Lowerer {
     // every validate rule has one (validation.go:37-53: at least NewValidateResourceHandler,
     // even when its validator then returns nil)
     if (pre == F_FALSE && (k.handler != H_NONE || has_validate)) k.handler = H_CONST_SKIP;
-    if (k.handler >= H_CONST_SKIP) {
-      if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with folded conditions is not supported");
+    if (pre_block != CE_NONE && k.handler == H_NONE && has_validate) {
+      k.handler = H_COND;  // matched cells need the preconditions' skip / error
+      crule.kind = CR_NONE;
+    }
+    if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) {
+      if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with conditions is not supported");
       P.any_const = true;
     }
+    if (pre_block != CE_NONE || k.handler == H_COND) P.cond.rules.push_back(crule);
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
     P.rule_names.push_back(pol_name + "/" + rname);
@@ -1425,6 +2032,7 @@ class Lowerer {
 
  private:
   Program& P;
+  cq::CondCompiler CC;
 };
 
 }  // namespace

@@ -32,6 +32,22 @@ struct PatProgram {
   std::vector<uint32_t> roots;         // 2 words per root: node, anchor slots used
   std::vector<KpePatRule> rules;
 };
+// Compiled preconditions / deny / foreach-deny programs (schema.h QO_* / KpeC*), evaluated per
+// resource by kpe_cond_kernel. Field names are kept as text: a binding resolves them to corpus
+// D_KEY ids.
+struct CondProgram {
+  std::vector<uint32_t> ops;  // 2 words per op
+  std::vector<KpeCExpr> exprs;
+  std::vector<KpeVTmpl> tmpls;
+  std::vector<KpeCCond> conds;
+  std::vector<KpeCBlock> blocks;
+  std::vector<KpeCForeach> fes;
+  std::vector<KpeCRule> rules;
+  std::vector<KpeScalar> consts;  // constant table (SC_T_* types, SC_T_ARR lists in clist)
+  std::vector<char> ctext;        // constant texts
+  std::vector<uint32_t> clist;    // elements of constant lists
+  std::vector<std::string> fields;
+};
 #define PRED_SPECIAL_NONE 0u
 #define PRED_SPECIAL_QNAME 1u   // validation.IsQualifiedName (label keys)
 #define PRED_SPECIAL_LABVAL 2u  // validation.IsValidLabelValue
@@ -80,6 +96,7 @@ struct Program {
   bool any_const = false;  // some rule has a constant handler (H_CONST_*)
   bool any_pss = false;
   PatProgram pat;  // pattern rules (H_PATTERN)
+  CondProgram cond;  // rules with preconditions / deny / foreach evaluated per resource
   DeviceProgram* dev = nullptr;
   ~Program();
 };

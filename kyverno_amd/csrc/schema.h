@@ -277,7 +277,9 @@ enum KpeCheckVersion {
 #define KPE_WARN_ 3
 #define KPE_ERROR_ 4
 #define KPE_SKIP_ 5
-#define KPE_PENDING_ 6  // device-internal: matched pattern rule, resolved by kpe_pattern_kernel
+#define KPE_PENDING_ 6  // device-internal: matched pattern / condition rule, resolved by a later kernel
+#define KPE_UNDECIDED_ 7  // the device cannot decide this cell (a documented device limit, e.g. a
+                          // condition list longer than CV_LIST_CAP): the caller evaluates it
 
 // ---- policy program ------------------------------------------------------------------------------
 // Rule handlers
@@ -290,6 +292,7 @@ enum KpeCheckVersion {
 #define H_CONST_SKIP 4u  // preconditions false: RuleSkip (validate_resource.go:125-132)
 #define H_CONST_FAIL 5u  // deny conditions true: RuleFail (validate_resource.go:268-279)
 #define H_CONST_PASS 6u  // deny conditions false: RulePass
+#define H_COND 7u        // deny / foreach-deny evaluated per resource by kpe_cond_kernel (cell PENDING)
 
 // Match terms (AND inside a filter block)
 enum KpeTermType {
@@ -393,8 +396,13 @@ typedef struct KpeRule {
 #define SC_QNEG (1u << 7)
 #define SC_TEXT (1u << 8)    // compareString text valid: text pool [text_off, +text_len)
 #define SC_BTRUE (1u << 9)
+#define SC_JVALID (1u << 10)  // condition constant string: json.Valid
+#define SC_JLIST (1u << 11)   // ... and decodes as a []string (or null): elements = constant list
+                              // [ival & 0xFFFFFFFF, + ival >> 32) of the constant-list table
+#define SC_T_ARR 5          // condition constants only: text_off = first element (constant list), text_len = count
 typedef struct KpeScalar {
-  uint32_t flags, text_off, text_len, pad;
+  uint32_t flags, text_off, text_len;
+  uint32_t sp_len;    // numbers: fmt.Sprint text (%v of the float64) follows the text: [text_off + text_len, +sp_len)
   int64_t ival;
   double fval;
   int64_t dur;
@@ -467,3 +475,71 @@ typedef struct KpeCond {
 typedef struct KpePatRule {
   uint32_t col, flags, r0, nr;
 } KpePatRule;
+
+// ---- condition programs (preconditions / deny / foreach-deny; kpe_cond_kernel) -------------
+// A query is the JMESPath expression of a whole-string {{ }} variable (or a foreach `list`),
+// compiled to a linear op list (program.cpp cq::QueryParser): a root, then steps. After `[]`
+// or `[*]` the following steps apply to every element of the projected list; the nulls they
+// produce are dropped when the projection ends (go-jmespath projection semantics).
+#define QO_OBJ 0u     // request.object: the resource's document root
+#define QO_EL 1u      // element / element0 (foreach)
+#define QO_IDX 2u     // elementIndex / elementIndex0 (a float64)
+#define QO_CONST 3u   // y = constant (request.operation = "CREATE", raw-string / JSON literals)
+#define QO_FIELD 4u   // y = field-name index (a binding resolves it to D_KEY id + 1; 0 = absent)
+#define QO_INDEX 5u   // y = index (int32; negative counts from the end)
+#define QO_FLAT 6u    // `[]`
+#define QO_STAR 7u    // `[*]`
+#define QO_KEYS 8u    // keys(@) of the current value
+#define QO_MSL 9u     // `[a, b, ...]` over the current value; QO_ARG = number of items, each a
+                      // QO_ITEM (QO_ARG = its op count) followed by a relative field / index chain
+#define QO_ITEM 10u
+#define QO_ERROR 11u  // the expression is empty: every evaluation is an error (RuleError)
+#define QO_OP(x) ((x) & 0xFFu)
+#define QO_ARG(x) ((x) >> 8)
+typedef struct KpeCExpr {
+  uint32_t op0, nops;  // ops [op0, op0 + nops) (uint2 each)
+  uint32_t flags;      // CE_STRICT: a plain field / index chain: a missing member is a NotFoundError
+  uint32_t alt;        // `||` right operand (an expression index) or 0xFFFFFFFF
+} KpeCExpr;
+#define CE_STRICT 1u
+#define CE_NONE 0xFFFFFFFFu
+// Value template: a condition key / value after variable substitution
+#define VT_CONST 0u  // a = constant
+#define VT_QUERY 1u  // a = expression
+#define VT_ARRAY 2u  // a = first element template, b = count (a list with variables inside)
+typedef struct KpeVTmpl {
+  uint32_t kind, a, b, pad;
+} KpeVTmpl;
+// Condition operators (variables/operator/operator.go:27-67)
+#define CO_EQ 0u
+#define CO_NE 1u
+#define CO_ANYIN 2u
+#define CO_ALLIN 3u
+#define CO_ANYNOTIN 4u
+#define CO_ALLNOTIN 5u
+#define CO_IN 6u
+#define CO_NOTIN 7u
+typedef struct KpeCCond {
+  uint32_t op, key, value, pad;  // key / value: template indices
+} KpeCCond;
+// Condition block: AnyAllConditions (any = conds [c0, c0 + nany), all = the next nall), or the
+// deprecated list form (nany = 0, all = the list)
+#define CB_HAS_ANY 1u
+typedef struct KpeCBlock {
+  uint32_t c0, nany, nall, flags;
+} KpeCBlock;
+typedef struct KpeCForeach {
+  uint32_t list;   // expression
+  uint32_t pre;    // block or CE_NONE
+  uint32_t deny;   // block
+  uint32_t scope;  // elementScope: 0 unset, 1 false, 2 true
+} KpeCForeach;
+#define CR_PRE_ONLY 0u  // only the rule's preconditions are evaluated here (other handler)
+#define CR_DENY 1u      // H_COND: validate.deny
+#define CR_FOREACH 2u   // H_COND: validate.foreach (deny entries)
+#define CR_NONE 3u      // H_COND: a validate block without handler (validation.go:52: the
+                        // resource validator returns nil) behind per-resource preconditions
+typedef struct KpeCRule {
+  uint32_t col, pre, kind, deny;  // pre / deny: block or CE_NONE
+  uint32_t fe0, nfe, pad0, pad1;
+} KpeCRule;

@@ -33,6 +33,7 @@ class RuleStatus(str, enum.Enum):
 
 # kpe_verdict cell codes -> RuleStatus (0 = no RuleResponse)
 VERDICT = {1: RuleStatus.PASS, 2: RuleStatus.FAIL, 3: RuleStatus.WARN, 4: RuleStatus.ERROR, 5: RuleStatus.SKIP}
+UNDECIDED = 7  # kpe_verdict KPE_UNDECIDED: a cell the device leaves to the reference engine
 
 
 @dataclass
@@ -222,8 +223,8 @@ class Engine:
         counts = (Counts * max(R, 1))()
         check(L.kpe_evaluate(self.device.h, ps.h, corpus.h, v.ctypes.data if N * R else None,
                              m.ctypes.data if (m is not None and N * R) else None, counts))
-        cnt = [{"na": c.na, "pass": c.pass_, "fail": c.fail, "warn": c.warn, "error": c.error, "skip": c.skip}
-               for c in counts[:R]]
+        cnt = [{"na": c.na, "pass": c.pass_, "fail": c.fail, "warn": c.warn, "error": c.error, "skip": c.skip,
+                "undecided": c.undecided} for c in counts[:R]]
         return v, m, cnt
 
     def cv_masks(self, ps: PolicySet, corpus: Corpus):
@@ -265,6 +266,9 @@ class Engine:
                     cell = int(v[i, r])
                     if cell == 0:
                         continue
+                    if cell == UNDECIDED:
+                        raise KpeError(-1, f"cell ({i}, {ps.rule_names[r]}) is beyond the device's documented "
+                                           "limits (KPE_UNDECIDED): evaluate it with the reference engine")
                     checks = [check_ids[k] for k in range(17) if (int(m[i, r]) >> k) & 1] if ps.is_pss[r] else []
                     rules.append(RuleResponse(ps.rule_names[r].split("/", 1)[1], VERDICT[cell],
                                               pod_security_checks=checks))
@@ -307,6 +311,7 @@ def cli_summary(ps: PolicySet, counts: List[dict], audit_warn: bool = False) -> 
     for i, c in enumerate(counts):
         arr[i].na, arr[i].pass_, arr[i].fail = c["na"], c["pass"], c["fail"]
         arr[i].warn, arr[i].error, arr[i].skip = c["warn"], c["error"], c["skip"]
+        arr[i].undecided = c.get("undecided", 0)
     out = CliTotals()
     check(load().kpe_cli_summary(ps.h, arr, 1 if audit_warn else 0, ctypes.byref(out)))
     return {"pass": out.pass_, "fail": out.fail, "warn": out.warn, "error": out.error, "skip": out.skip}

@@ -11,7 +11,7 @@ stay on the rank that produced them.
 """
 from typing import Dict, List, Sequence, Tuple
 
-COUNT_FIELDS = ("na", "pass", "fail", "warn", "error", "skip")
+COUNT_FIELDS = ("na", "pass", "fail", "warn", "error", "skip", "undecided")
 
 
 def shard_range(total: int, rank: int, world: int) -> Tuple[int, int]:

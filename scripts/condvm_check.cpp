@@ -1,0 +1,89 @@
+// Host build of the condition VM (kyverno_amd/csrc/condvm.inl, the exact text kpe_cond_kernel
+// runs) for sanitizer runs and parity checks without a GPU:
+//   scripts/build/condvm_check policies.json resources.ndjson seed.bin out.bin
+// Flattens the resources with document tapes, compiles the policies, binds the condition
+// program the way kpe_api.cpp does (field names -> D_KEY ids) and runs cond_eval_row over a
+// verdict matrix seeded from seed.bin (N x R bytes: what the scan kernel would have written,
+// i.e. KPE_PENDING_ for matched H_COND cells, the handler verdict for other matched cells,
+// KPE_NA_ for unmatched ones). Writes the resulting N x R verdict bytes to out.bin.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#define __device__
+#define __forceinline__ inline
+struct uint2 {
+  uint32_t x, y;
+};
+struct uint4 {
+  uint32_t x, y, z, w;
+};
+using std::trunc;
+
+#include "../kyverno_amd/csrc/corpus.hpp"
+#include "../kyverno_amd/csrc/kernels_abi.h"
+#include "../kyverno_amd/csrc/program.hpp"
+#include "../kyverno_amd/csrc/schema.h"
+
+namespace kpe {
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs);
+}
+
+namespace {
+#include "../kyverno_amd/csrc/strmatch.inl"
+#include "../kyverno_amd/csrc/patvm.inl"
+#include "../kyverno_amd/csrc/condvm.inl"
+}  // namespace
+
+static std::string slurp(const char* p) {
+  std::ifstream f(p, std::ios::binary);
+  if (!f) throw std::runtime_error(std::string("cannot read ") + p);
+  std::stringstream ss;
+  ss << f.rdbuf();
+  return ss.str();
+}
+
+int main(int argc, char** argv) {
+  if (argc < 5) {
+    fprintf(stderr, "usage: %s policies.json resources.ndjson seed.bin out.bin\n", argv[0]);
+    return 2;
+  }
+  const std::string pj = slurp(argv[1]), nd = slurp(argv[2]), seed = slurp(argv[3]);
+  kpe::Corpus C;
+  kpe::flatten_ndjson(C, nd.data(), nd.size(), nullptr, 0, true);
+  auto P = kpe::compile_policies(pj.data(), pj.size());
+  const auto& CP = P->cond;
+  const uint32_t R = (uint32_t)P->rules.size();
+  if (seed.size() != (size_t)C.n * R) return fprintf(stderr, "seed size %zu != %lld x %u\n", seed.size(), (long long)C.n, R), 1;
+  std::vector<uint8_t> verdicts(seed.begin(), seed.end());
+  std::vector<uint32_t> fk(CP.fields.size());
+  for (size_t i = 0; i < fk.size(); ++i) {
+    const int64_t id = C.dict[D_KEY].find(CP.fields[i]);
+    fk[i] = id < 0 ? 0u : (uint32_t)id + 1u;
+  }
+  std::vector<uint8_t> text(C.scal_text.begin(), C.scal_text.end()), ctext(CP.ctext.begin(), CP.ctext.end()),
+      kb(C.dict[D_KEY].bytes.begin(), C.dict[D_KEY].bytes.end());
+  text.push_back(0), ctext.push_back(0), kb.push_back(0);
+  std::vector<uint2> ops(CP.ops.size() / 2);
+  for (size_t i = 0; i < ops.size(); ++i) ops[i] = uint2{CP.ops[2 * i], CP.ops[2 * i + 1]};
+  CondArgs a{};
+  a.n = C.n, a.R = R, a.ncr = (uint32_t)CP.rules.size();
+  a.doc = C.doc.data(), a.doc_off = C.doc_off.data(), a.scal = C.scal.data(), a.scal_text = text.data();
+  a.key_bytes = kb.data(), a.key_off = C.dict[D_KEY].off.data();
+  a.ops = ops.data(), a.exprs = CP.exprs.data(), a.tmpls = CP.tmpls.data(), a.conds = CP.conds.data();
+  a.blocks = CP.blocks.data(), a.fes = CP.fes.data(), a.rules = CP.rules.data();
+  a.ctab = CP.consts.data(), a.ctext = ctext.data(), a.clist = CP.clist.data(), a.fkeys = fk.data();
+  a.verdicts = verdicts.data();
+  for (int64_t r = 0; r < a.n; ++r) cond_eval_row(a, r);  // kpe_cond_kernel's lane body
+  FILE* f = fopen(argv[4], "wb");
+  fwrite(verdicts.data(), 1, verdicts.size(), f);
+  fclose(f);
+  printf("%lld %u\n", (long long)C.n, R);
+  return 0;
+}

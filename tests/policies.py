@@ -240,3 +240,79 @@ def c3_policy_set(n=200, seed=0xC3):
         pols.append({"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": f"c3-{i:03d}"},
                      "spec": {"background": True, "validationFailureAction": "Audit", "rules": [rule]}})
     return pols
+
+
+def cond_policy_set():
+    """Preconditions / deny / foreach-deny rules whose conditions read the resource (evaluated
+    per resource by kpe_cond_kernel): every operator family (variables/operator/*.go) over
+    strings, numbers, lists and missing values, the JMESPath forms the device restates
+    (fields, [n], [], [*], multi-select, keys(@), `||` defaults) and foreach with element
+    preconditions, elementScope and elementIndex (validate_resource.go:186-254)."""
+    def rule(name, validate, pre=None, kinds=("Pod", "Deployment", "Service", "ConfigMap")):
+        r = {"name": name, "match": {"any": [{"resources": {"kinds": list(kinds)}}]}, "validate": validate}
+        if pre is not None:
+            r["preconditions"] = pre
+        return r
+
+    def deny(*conds, any_block=False):
+        return {"message": "m", "deny": {"conditions": {("any" if any_block else "all"): list(conds)}}}
+
+    def c(key, op, value):
+        return {"key": key, "operator": op, "value": value}
+
+    obj = "request.object"
+    spec_ctrs = "{{ " + obj + ".spec.[initContainers, containers][] }}"
+    rules = [
+        rule("app-anyin", deny(c("{{ " + obj + ".metadata.labels.app }}", "AnyIn", ["app-1*", "app-2?"]))),
+        rule("team-strict", deny(c("{{ " + obj + ".metadata.labels.team }}", "Equals", "team-1"))),  # missing => error
+        rule("team-default", deny(c("{{ " + obj + ".metadata.labels.team || 'none' }}", "NotEquals", "none"))),
+        rule("tier-notin", deny(c("{{ " + obj + ".metadata.labels.tier }}", "NotIn", ["frontend"]))),
+        rule("tier-in-scalar", deny(c("{{ " + obj + ".metadata.labels.tier }}", "In", "back*"))),
+        rule("images-allnotin", deny(c("{{ " + obj + ".spec.containers[].image }}", "AllNotIn", ["*:latest"]))),
+        rule("images-anyin", deny(c("{{ " + obj + ".spec.[initContainers, containers][].image }}", "AnyIn",
+                                    ["nginx:*", "redis:*"]))),
+        rule("names-any-or", deny(c("{{ " + obj + ".spec.[initContainers, containers][].name }}", "AnyIn",
+                                    ["init-*"]),
+                                  c("{{ " + obj + ".metadata.name }}", "Equals", "res-1?"), any_block=True)),
+        rule("replicas-eq", deny(c("{{ " + obj + ".spec.replicas || `1` }}", "Equals", 3)), kinds=("Deployment",)),
+        rule("replicas-anyin", deny(c("{{ " + obj + ".spec.replicas }}", "AnyIn", ["2", "4"])), kinds=("Deployment",)),
+        rule("ports-first", deny(c("{{ " + obj + ".spec.containers[0].ports[0].containerPort || `0` }}", "Equals",
+                                   "8080"))),
+        rule("ns-list-key", deny(c(["{{ " + obj + ".metadata.namespace }}"], "NotIn", ["ns-0001", "ns-0002"]))),
+        rule("vol-keys", deny(c("{{ " + obj + ".spec.volumes[].keys(@)[] || '' }}", "AnyNotIn",
+                                ["name", "configMap", "emptyDir", ""]))),
+        rule("caps-add", deny(c("{{ " + obj + ".spec.[ephemeralContainers, initContainers, containers][]."
+                                "securityContext.capabilities.add[] }}", "AnyNotIn", ["CHOWN", "NET_BIND_SERVICE"]))),
+        rule("star-proj", deny(c("{{ " + obj + ".spec.containers[*].name }}", "AllIn", ["c-*", "init-*"]))),
+        rule("missing-default", deny(c("{{ " + obj + ".spec.nothing || `[]` }}", "Equals", []))),
+        rule("pre-ns", {"message": "m", "pattern": {"metadata": {"name": "res-*"}}},
+             pre={"all": [c("{{ " + obj + ".metadata.namespace }}", "NotEquals", "ns-00*")]}),
+        rule("pre-kind-pss", {"podSecurity": {"level": "baseline", "version": "latest"}},
+             pre={"any": [c("{{ " + obj + ".metadata.labels.tier }}", "Equals", "frontend")]}, kinds=("Pod",)),
+        rule("pre-only", {"message": "m"}, pre=[c("{{ " + obj + ".kind }}", "Equals", "Service")]),
+        rule("foreach-image", {"message": "m", "foreach": [{
+            "list": obj + ".spec.containers",
+            "preconditions": {"all": [c("{{ element.name }}", "NotEquals", "c-0")]},
+            "deny": {"conditions": {"any": [c("{{ element.image }}", "Equals", "*:latest")]}}}]}),
+        rule("foreach-strings", {"message": "m", "foreach": [{
+            "list": obj + ".spec.containers[].image",
+            "deny": {"conditions": {"all": [c("{{ element }}", "NotEquals", "nginx*")]}}}]}),
+        rule("foreach-scope", {"message": "m", "foreach": [{
+            "list": obj + ".spec.containers[].image", "elementScope": True,
+            "deny": {"conditions": {"all": [c("{{ element }}", "Equals", "x")]}}}]}),
+        rule("foreach-index", {"message": "m", "foreach": [{
+            "list": obj + ".spec.[initContainers, containers][]",
+            "deny": {"conditions": {"all": [c("{{ elementIndex }}", "Equals", 2),
+                                            c("{{ element.securityContext.privileged || `false` }}", "Equals",
+                                              False)]}}}]}),
+        rule("foreach-drop-all", {"message": "m", "foreach": [{
+            "list": obj + ".spec.[ephemeralContainers, initContainers, containers][]",
+            "deny": {"conditions": {"all": [c("ALL", "AnyNotIn",
+                                              "{{ element.securityContext.capabilities.drop[] || `[]` }}")]}}}]}),
+        rule("foreach-none", {"message": "m", "foreach": [{
+            "list": obj + ".spec.missing[]",
+            "deny": {"conditions": {"all": [c("{{ element }}", "Equals", "x")]}}}]}),
+        rule("spec-ctrs-count", deny(c(spec_ctrs, "Equals", []))),
+    ]
+    return [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "cond"},
+             "spec": {"background": True, "validationFailureAction": "Audit", "rules": rules}}]

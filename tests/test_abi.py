@@ -53,7 +53,8 @@ def test_compile_matches_oracle_rule_names(oracle):
 
 def test_compile_unsupported_is_loud():
     pol = pss_policy("x", "baseline")
-    pol["spec"]["rules"][0]["validate"] = {"deny": {"conditions": {"any": [{"key": "{{ request.object.kind }}",
+    # a condition outside the device's JMESPath subset (a function call) is refused
+    pol["spec"]["rules"][0]["validate"] = {"deny": {"conditions": {"any": [{"key": "{{ to_upper(request.object.kind) }}",
                                                                             "operator": "Equals", "value": "a"}]}}}
     with pytest.raises(KpeError) as e:
         K.PolicySet([pol])

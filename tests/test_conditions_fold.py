@@ -119,18 +119,28 @@ def test_oracle_in_list_key_semantics(oracle):
 
 
 @pytest.mark.parametrize("cond", [
-    {"all": [{"key": "{{ request.object.metadata.name }}", "operator": "Equals", "value": "x"}]},
-    {"all": [{"key": "CRE*", "operator": "Equals", "value": OP}]},          # glob key: not folded
-    {"all": [{"key": OP, "operator": "AnyIn", "value": ["a-b"]}]},          # range form: not folded
     {"all": [{"key": OP, "operator": "GreaterThan", "value": "A"}]},          # operator outside the set
-    {"all": [{"key": "1Gi", "operator": "Equals", "value": "1024Mi"}]},       # quantities: not folded
-    {"all": [{"key": OP, "operator": "Equals", "value": "{{ request.operation }}-x"}]},
+    {"all": [{"key": OP, "operator": "Equals", "value": "{{ request.operation }}-x"}]},  # partial variable
 ])
 def test_unfoldable_refused(cond):
     for pol in (_policy("p", [_rule("r", pre=cond, validate=PATTERN)]),
                 _policy("p", [_rule("r", validate={"deny": {"conditions": cond}})])):
         with pytest.raises(K.KpeError):
             K.PolicySet([pol])
+
+
+@pytest.mark.parametrize("cond", [
+    {"all": [{"key": "{{ request.object.metadata.name }}", "operator": "Equals", "value": "x"}]},
+    {"all": [{"key": "CRE*", "operator": "Equals", "value": OP}]},          # glob key
+    {"all": [{"key": OP, "operator": "AnyIn", "value": ["a-b"]}]},          # range text inside a list
+    {"all": [{"key": "1Gi", "operator": "Equals", "value": "1024Mi"}]},       # quantities
+    {"all": [{"key": "{{ request.operation || 'BACKGROUND' }}", "operator": "NotEquals", "value": "DELETE"}]},
+])
+def test_unfoldable_compiled_per_resource(cond):
+    """Not folded at compile time: evaluated per resource by kpe_cond_kernel instead."""
+    for pol in (_policy("p", [_rule("r", pre=cond, validate=PATTERN)]),
+                _policy("p", [_rule("r", validate={"deny": {"conditions": cond}})])):
+        K.PolicySet([pol])
 
 
 def test_apply_one_with_folded_refused():

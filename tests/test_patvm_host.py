@@ -23,17 +23,19 @@ def harness():
     return BIN
 
 
+def pattern_only(pols):  # the harness runs the pattern VM alone (no deny / foreach / preconditions)
+    return [q for q in pols if not any((r.get("validate") or {}).get("deny") is not None or r.get("preconditions")
+                                      or (r.get("validate") or {}).get("foreach") for r in q["spec"]["rules"])]
+
+
 def _sets():
-    out = [("chart-mix0", chart_pattern_policies(), K.synth_resources(0xC1, 1500, mix=0)),
-           ("chart-mix2", chart_pattern_policies(), K.synth_resources(22, 1500, mix=2))]
+    out = [("chart-mix0", pattern_only(chart_pattern_policies()), K.synth_resources(0xC1, 1500, mix=0)),
+           ("chart-mix2", pattern_only(chart_pattern_policies()), K.synth_resources(22, 1500, mix=2))]
     pols, nd = edge_case_inputs(1500)
     out.append(("edge", pols, nd))
     cases = [c for c in PTREE if isinstance(json.loads(c["resource"]), dict)]
-    pols = device_policies([_policy_for(f"t{i}", json.loads(c["pattern"])) for i, c in enumerate(cases)])
+    pols = pattern_only(device_policies([_policy_for(f"t{i}", json.loads(c["pattern"])) for i, c in enumerate(cases)]))
     out.append(("validate_test.go", pols, "\n".join(json.dumps(json.loads(c["resource"])) for c in cases).encode()))
-    def pattern_only(pols):  # the harness runs the pattern VM alone (no folded deny / preconditions)
-        return [q for q in pols if not any((r.get("validate") or {}).get("deny") is not None or r.get("preconditions")
-                                          for r in q["spec"]["rules"])]
 
     for c in CLI:
         p = pattern_only(device_policies(c["policies"]))
