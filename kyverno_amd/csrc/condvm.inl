@@ -9,6 +9,9 @@
 //   engine.go:278-285 (preconditions), validate_resource.go:186-279 (foreach, deny),
 //   utils/foreach.go:12-63 (EvaluateList, AddElementToContext)
 //   go-jmespath (go.mod:33) field / index / flatten / projection / multi-select / keys / `||`
+// Every function is forced inline and each heavy one has a single call site (cond_eval_row is a
+// state machine around one block() call): a call would receive the lane's private list buffers
+// through a generic `this` pointer (the same constraint as patvm.inl). Nothing recurses.
 // Values a restated operator cannot decide on the device (a map or list printed by
 // fmt.Sprint, a resource string that may be JSON, lists longer than CV_LIST_CAP) make the
 // cell KPE_UNDECIDED_ instead of guessing.
@@ -39,15 +42,16 @@ struct CondVM {
   uint32_t root;
   CV buf[kCvBufs][CV_LIST_CAP];
   uint32_t blen[kCvBufs];
-  char nb[2][16];  // fmt.Sprint of an elementIndex
+  char (*nb)[16];  // 2 x 16 bytes for fmt.Sprint of an elementIndex: LDS on the device, so that
+                   // no generic pointer ever reaches the lane's private memory
 
   // ---- value access ----------------------------------------------------------------------
-  __device__ CV node(uint32_t e) const {  // a tape entry; a null scalar is the null value
+  __device__ __forceinline__ CV node(uint32_t e) const {  // a tape entry; a null scalar is the null value
     const uint2 n = doc[e];
     if (DN_KIND(n.x) == DN_SCALAR && SC_TYPE(a.scal[n.y].flags) == SC_T_NULL) return cv(VK_NULL, 0);
     return cv(VK_NODE, e);
   }
-  __device__ const KpeScalar* scalar(CV v, const uint8_t** text) const {
+  __device__ __forceinline__ const KpeScalar* scalar(CV v, const uint8_t** text) const {
     if (v.k == VK_NODE) {
       *text = a.scal_text;
       return a.scal + doc[v.p].y;
@@ -55,7 +59,7 @@ struct CondVM {
     *text = a.ctext;
     return a.ctab + v.p;
   }
-  __device__ uint32_t type(CV v) const {
+  __device__ __forceinline__ uint32_t type(CV v) const {
     switch (v.k) {
       case VK_NODE: {
         const uint2 n = doc[v.p];
@@ -75,12 +79,12 @@ struct CondVM {
       default: return JT_NULL;
     }
   }
-  __device__ uint32_t alen(CV v) const {
+  __device__ __forceinline__ uint32_t alen(CV v) const {
     if (v.k == VK_NODE) return doc[doc[v.p].y].x;
     if (v.k == VK_CONST) return a.ctab[v.p].text_len;
     return blen[v.p];
   }
-  __device__ CV aget(CV v, uint32_t i) const {
+  __device__ __forceinline__ CV aget(CV v, uint32_t i) const {
     if (v.k == VK_NODE) return node(doc[v.p].y + 1u + i);
     if (v.k == VK_CONST) {
       const uint32_t c = a.clist[a.ctab[v.p].text_off + i];
@@ -88,24 +92,24 @@ struct CondVM {
     }
     return buf[v.p][i];
   }
-  __device__ SView str(CV v) const {  // a JT_STR value's text
+  __device__ __forceinline__ SView str(CV v) const {  // a JT_STR value's text
     if (v.k == VK_KEY) return SView{a.key_bytes + a.key_off[v.p], (int)(a.key_off[v.p + 1] - a.key_off[v.p])};
     const uint8_t* t;
     const KpeScalar* s = scalar(v, &t);
     return SView{t + s->text_off, (int)s->text_len};
   }
-  __device__ double num(CV v) const {
+  __device__ __forceinline__ double num(CV v) const {
     if (v.k == VK_NUM) return (double)v.p;
     const uint8_t* t;
     const KpeScalar* s = scalar(v, &t);
     return SC_TYPE(s->flags) == SC_T_INT ? (double)s->ival : s->fval;
   }
-  __device__ bool btrue(CV v) const {
+  __device__ __forceinline__ bool btrue(CV v) const {
     const uint8_t* t;
     return (scalar(v, &t)->flags & SC_BTRUE) != 0u;
   }
   // fmt.Sprint of a scalar (false: a map or list, which the device does not print)
-  __device__ bool sprint(CV v, int slot, SView* out) {
+  __device__ __forceinline__ bool sprint(CV v, int slot, SView* out) {
     switch (type(v)) {
       case JT_NULL: *out = SView{reinterpret_cast<const uint8_t*>("<nil>"), 5}; return true;
       case JT_BOOL:
@@ -133,7 +137,7 @@ struct CondVM {
       default: return false;
     }
   }
-  __device__ bool is_false(CV v) const {  // JMESPath false-like values
+  __device__ __forceinline__ bool is_false(CV v) const {  // JMESPath false-like values
     switch (type(v)) {
       case JT_NULL: return true;
       case JT_BOOL: return !btrue(v);
@@ -143,17 +147,17 @@ struct CondVM {
       default: return false;
     }
   }
-  static __device__ bool seq(SView x, SView y) { return x.n == y.n && bytes_eq(x.s, y.s, x.n); }
-  static __device__ bool wm(SView pat, SView s) { return glob(pat.s, pat.n, s.s, s.n); }
+  __device__ __forceinline__ static bool seq(SView x, SView y) { return x.n == y.n && bytes_eq(x.s, y.s, x.n); }
+  __device__ __forceinline__ static bool wm(SView pat, SView s) { return glob(pat.s, pat.n, s.s, s.n); }
 
   // ---- JMESPath subset ------------------------------------------------------------------
-  __device__ int push(uint32_t b, CV x) {
+  __device__ __forceinline__ int push(uint32_t b, CV x) {
     if (blen[b] >= (uint32_t)CV_LIST_CAP) return CS_UNDEC;
     buf[b][blen[b]++] = x;
     return CS_OK;
   }
   // member named key1 of map entry m (the flattener keeps the last of duplicate names)
-  __device__ uint32_t lookup(uint32_t m, uint32_t key1) const {
+  __device__ __forceinline__ uint32_t lookup(uint32_t m, uint32_t key1) const {
     if (key1 == 0u) return kNoNode;
     const uint32_t b = doc[m].y, c0 = b + 1u, end = c0 + doc[b].x;
     uint32_t i = c0;
@@ -168,7 +172,7 @@ struct CondVM {
       if (DN_KEY(doc[i].x) == key1) return i;
     return kNoNode;
   }
-  __device__ CV field(CV v, uint32_t fi, bool strict, int* st) {
+  __device__ __forceinline__ CV field(CV v, uint32_t fi, bool strict, int* st) {
     if (type(v) != JT_OBJ) return cv(VK_NULL, 0);
     const uint32_t m = lookup(v.p, a.fkeys[fi]);
     if (m == kNoNode) {
@@ -177,7 +181,7 @@ struct CondVM {
     }
     return node(m);
   }
-  __device__ CV index(CV v, int32_t i) const {
+  __device__ __forceinline__ CV index(CV v, int32_t i) const {
     if (type(v) != JT_ARR) return cv(VK_NULL, 0);
     const int32_t n = (int32_t)alen(v);
     if (i < 0) i += n;
@@ -185,7 +189,7 @@ struct CondVM {
     return aget(v, (uint32_t)i);
   }
   // splice arrays, keep everything else (nulls too): N_FLATTEN
-  __device__ int flatten_into(CV v, uint32_t out) {
+  __device__ __forceinline__ int flatten_into(CV v, uint32_t out) {
     blen[out] = 0;
     const uint32_t n = alen(v);
     for (uint32_t i = 0; i < n; ++i) {
@@ -200,13 +204,13 @@ struct CondVM {
     }
     return CS_OK;
   }
-  __device__ void drop_nulls(uint32_t b) {
+  __device__ __forceinline__ void drop_nulls(uint32_t b) {
     uint32_t k = 0;
     for (uint32_t i = 0; i < blen[b]; ++i)
       if (type(buf[b][i]) != JT_NULL) buf[b][k++] = buf[b][i];
     blen[b] = k;
   }
-  __device__ int keys_into(CV v, uint32_t out, bool append) {  // keys(@) of an object
+  __device__ __forceinline__ int keys_into(CV v, uint32_t out, bool append) {  // keys(@) of an object
     if (!append) blen[out] = 0;
     const uint32_t b = doc[v.p].y, c0 = b + 1u, end = c0 + doc[b].x;
     for (uint32_t c = c0; c < end; ++c)
@@ -215,7 +219,7 @@ struct CondVM {
   }
 
   // One expression (no `||`): the result may be a list in buffer b0 or b1.
-  __device__ int run_ops(const KpeCExpr& e, CV el, uint32_t eli, uint32_t b0, uint32_t b1, CV* out) {
+  __device__ __forceinline__ int run_ops(const KpeCExpr& e, CV el, uint32_t eli, uint32_t b0, uint32_t b1, CV* out) {
     const bool strict = e.flags & CE_STRICT;
     uint32_t mode = 0;  // 0 single value, 1 projection over list `lb`, 2 dead projection (null)
     CV cur = cv(VK_NULL, 0);
@@ -337,7 +341,7 @@ struct CondVM {
     return CS_OK;
   }
   // A query with its `||` operands: the first truthy one, else the last one's value.
-  __device__ int query(uint32_t ei, CV el, uint32_t eli, uint32_t b0, uint32_t b1, CV* out) {
+  __device__ __forceinline__ int query(uint32_t ei, CV el, uint32_t eli, uint32_t b0, uint32_t b1, CV* out) {
     for (;;) {
       const KpeCExpr e = a.exprs[ei];
       CV r;
@@ -351,19 +355,26 @@ struct CondVM {
       ei = e.alt;
     }
   }
-  // A condition key / value after substitution (template `ti`); lists go to buffer bl.
-  __device__ int value(uint32_t ti, CV el, uint32_t eli, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
+  // A condition key / value after substitution (template `ti`); lists go to buffer bl. One
+  // query() call site: a single query is a one-element template walk that returns its value.
+  __device__ __forceinline__ int value(uint32_t ti, CV el, uint32_t eli, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
     const KpeVTmpl t = a.tmpls[ti];
-    if (t.kind == VT_CONST) {
-      *out = SC_TYPE(a.ctab[t.a].flags) == SC_T_NULL ? cv(VK_NULL, 0) : cv(VK_CONST, t.a);
-      return CS_OK;
-    }
-    if (t.kind == VT_QUERY) return query(t.a, el, eli, b0, b1, out);
+    const bool arr = t.kind == VT_ARRAY;
+    const uint32_t n = arr ? t.b : 1u;
     blen[bl] = 0;
-    for (uint32_t k = 0; k < t.b; ++k) {
+    for (uint32_t k = 0; k < n; ++k) {  // list elements: constants or queries (no nested lists)
+      const KpeVTmpl te = arr ? a.tmpls[t.a + k] : t;
       CV x;
-      const int st = value(t.a + k, el, eli, b0, b1, bl, &x);
-      if (st != CS_OK) return st;
+      if (te.kind == VT_CONST) {
+        x = SC_TYPE(a.ctab[te.a].flags) == SC_T_NULL ? cv(VK_NULL, 0) : cv(VK_CONST, te.a);
+      } else {
+        const int st = query(te.a, el, eli, b0, b1, &x);
+        if (st != CS_OK) return st;
+      }
+      if (!arr) {
+        *out = x;
+        return CS_OK;
+      }
       if (x.k == VK_LIST) return CS_UNDEC;  // a list inside a list
       if (push(bl, x)) return CS_UNDEC;
     }
@@ -374,7 +385,7 @@ struct CondVM {
   // ---- operators --------------------------------------------------------------------------
   // operator.go:79-138 parseDuration: a string (other than "0") that parses as a duration, or a
   // number of seconds beside one; -1 when neither side is a duration string
-  __device__ int duration2(CV k, CV v, double* ks, double* vs) const {
+  __device__ __forceinline__ int duration2(CV k, CV v, double* ks, double* vs) const {
     auto dstr = [&](CV x, int64_t* d) -> bool {
       if (type(x) != JT_STR || x.k == VK_KEY) return false;
       const uint8_t* t;
@@ -403,7 +414,7 @@ struct CondVM {
   // A member name (VK_KEY) carries no parsed attributes: undecided where it could parse as a
   // number, duration or quantity.
   // (durations and quantities start with [-+.0-9]; strconv.ParseFloat also takes inf / nan)
-  __device__ bool numeric_looking(CV x, bool floats) const {
+  __device__ __forceinline__ bool numeric_looking(CV x, bool floats) const {
     if (x.k != VK_KEY) return false;
     const SView s = str(x);
     if (s.n == 0) return false;
@@ -412,7 +423,7 @@ struct CondVM {
     return floats && (c == 'I' || c == 'i' || c == 'N' || c == 'n');
   }
   // equal.go / notequal.go
-  __device__ int op_equals(CV k, CV v, bool neg) {
+  __device__ __forceinline__ int op_equals(CV k, CV v, bool neg) {
     const uint32_t kt = type(k), vt = type(v);
     switch (kt) {
       case JT_NULL: return 0;
@@ -452,7 +463,7 @@ struct CondVM {
       default: return vt != JT_OBJ ? neg : -1;  // map equality: undecided
     }
   }
-  __device__ int deep_equal_list(CV x, CV y) {  // reflect.DeepEqual of two lists of scalars
+  __device__ __forceinline__ int deep_equal_list(CV x, CV y) {  // reflect.DeepEqual of two lists of scalars
     const uint32_t n = alen(x);
     if (alen(y) != n) return 0;
     for (uint32_t i = 0; i < n; ++i) {
@@ -469,7 +480,7 @@ struct CondVM {
   // A string value of a set / In operator decoded as a JSON []string: 1 decoded (*c0, *cn list
   // of constants), 0 not JSON, 2 valid JSON that is not a []string, -1 undecided (a resource
   // string that may be JSON).
-  __device__ int json_list(CV v, uint32_t* c0, uint32_t* cn) const {
+  __device__ __forceinline__ int json_list(CV v, uint32_t* c0, uint32_t* cn) const {
     if (v.k == VK_CONST) {
       const KpeScalar& s = a.ctab[v.p];
       if (!(s.flags & SC_JVALID)) return 0;
@@ -487,7 +498,7 @@ struct CondVM {
     return 0;
   }
   // anyin.go / allin.go / anynotin.go / allnotin.go
-  __device__ int op_set(uint32_t op, CV k, CV v) {
+  __device__ __forceinline__ int op_set(uint32_t op, CV k, CV v) {
     const uint32_t kt = type(k), vt = type(v);
     if (kt == JT_NULL || kt == JT_OBJ) return 0;
     const bool notin = op == CO_ANYNOTIN || op == CO_ALLNOTIN;
@@ -562,7 +573,7 @@ struct CondVM {
     return (op == CO_ALLIN || op == CO_ALLNOTIN) ? 1 : 0;
   }
   // in.go / notin.go (deprecated): keyExistsInArray / setExistsInArray
-  __device__ int op_in(CV k, CV v, bool notin) {
+  __device__ __forceinline__ int op_in(CV k, CV v, bool notin) {
     const uint32_t kt = type(k), vt = type(v);
     if (kt == JT_NULL || kt == JT_OBJ) return 0;
     if (kt != JT_ARR) {
@@ -631,124 +642,164 @@ struct CondVM {
   }
 
   // ---- conditions ---------------------------------------------------------------------------
-  __device__ int condition(uint32_t ci, CV el, uint32_t eli) {
+  __device__ __forceinline__ int condition(uint32_t ci, CV el, uint32_t eli) {
     const KpeCCond c = a.conds[ci];
-    CV k, v;
-    int st = value(c.key, el, eli, 0, 1, 2, &k);
-    if (st == CS_UNDEC) return CB_UNDEC;
-    if (st != CS_OK) return CB_ERROR;
-    st = value(c.value, el, eli, 3, 4, 5, &v);
-    if (st == CS_UNDEC) return CB_UNDEC;
-    if (st != CS_OK) return CB_ERROR;
-    int r;
-    switch (c.op) {
-      case CO_EQ: r = op_equals(k, v, false); break;
-      case CO_NE: r = op_equals(k, v, true); break;
-      case CO_IN: r = op_in(k, v, false); break;
-      case CO_NOTIN: r = op_in(k, v, true); break;
-      default: r = op_set(c.op, k, v); break;
+    CV kv[2];
+    for (int side = 0; side < 2; ++side) {  // key (buffers 0, 1, 2), then value (3, 4, 5)
+      const uint32_t b = side ? 3u : 0u;
+      const int st = value(side ? c.value : c.key, el, eli, b, b + 1u, b + 2u, &kv[side]);
+      if (st == CS_UNDEC) return CB_UNDEC;
+      if (st != CS_OK) return CB_ERROR;
     }
+    const CV k = kv[0], v = kv[1];
+    int r;
+    if (c.op <= CO_NE) r = op_equals(k, v, c.op == CO_NE);
+    else if (c.op >= CO_IN) r = op_in(k, v, c.op == CO_NOTIN);
+    else r = op_set(c.op, k, v);
     if (r == -2) return CB_ERROR;
     if (r < 0) return CB_UNDEC;
     return r ? CB_TRUE : CB_FALSE;
   }
   // evaluateAnyAllConditions: any (when present) then all, each short-circuiting
-  __device__ int block(uint32_t bi, CV el, uint32_t eli) {
+  __device__ __forceinline__ int block(uint32_t bi, CV el, uint32_t eli) {
     const KpeCBlock b = a.blocks[bi];
-    bool any_ok = true;
-    if (b.flags & CB_HAS_ANY) {
-      any_ok = false;
-      for (uint32_t i = 0; i < b.nany; ++i) {
-        const int r = condition(b.c0 + i, el, eli);
-        if (r >= CB_ERROR) return r;
-        if (r == CB_TRUE) {
-          any_ok = true;
-          break;
-        }
-      }
-    }
-    for (uint32_t i = 0; i < b.nall; ++i) {
-      const int r = condition(b.c0 + b.nany + i, el, eli);
+    const bool has_any = b.flags & CB_HAS_ANY;
+    bool any_ok = !has_any;
+    const uint32_t n = b.nany + b.nall;
+    for (uint32_t i = has_any ? 0u : b.nany; i < n; ++i) {  // any (when present), then all
+      const int r = condition(b.c0 + i, el, eli);
       if (r >= CB_ERROR) return r;
-      if (r == CB_FALSE) return CB_FALSE;
+      if (i < b.nany) {
+        if (r == CB_TRUE) {  // the first true `any` condition ends the any loop
+          any_ok = true;
+          i = b.nany - 1u;
+        }
+      } else if (r == CB_FALSE) {
+        return CB_FALSE;
+      }
     }
     return any_ok ? CB_TRUE : CB_FALSE;
   }
-  // validateForEach / validateElements (validate_resource.go:186-254) over deny entries
-  __device__ uint32_t foreach_rule(const KpeCRule& r) {
-    uint32_t applied = 0;
-    for (uint32_t f = 0; f < r.nfe; ++f) {
-      const KpeCForeach fe = a.fes[r.fe0 + f];
-      CV lst;
-      const int st = query(fe.list, cv(VK_NULL, 0), 0, 0, 1, &lst);
-      if (st == CS_UNDEC) return KPE_UNDECIDED_;
-      if (st != CS_OK) continue;  // "failed to evaluate list": the entry is skipped
-      // EvaluateList: a non-list result is a one-element list; a computed list moves to buffer 6
-      CV list = lst;
-      bool one = type(lst) != JT_ARR;
-      if (!one && lst.k == VK_LIST) {
-        blen[6] = blen[lst.p];
-        for (uint32_t i = 0; i < blen[6]; ++i) buf[6][i] = buf[lst.p][i];
-        list = cv(VK_LIST, 6);
-      }
-      const uint32_t n = one ? 1u : alen(list);
-      uint32_t count = 0;
-      for (uint32_t idx = 0; idx < n; ++idx) {
-        const CV el = one ? lst : aget(list, idx);
-        if (type(el) == JT_NULL) continue;
-        if (fe.scope == 2u && type(el) != JT_OBJ) return KPE_ERROR_;  // AddElementToContext
-        int res;  // element verdict
-        int p = CB_TRUE;
-        if (fe.pre != CE_NONE) p = block(fe.pre, el, idx);
-        if (p == CB_UNDEC) return KPE_UNDECIDED_;
-        if (p == CB_ERROR) {
-          res = KPE_ERROR_;
-        } else if (p == CB_FALSE) {
-          res = KPE_SKIP_;
-        } else {
-          const int d = block(fe.deny, el, idx);
-          if (d == CB_UNDEC) return KPE_UNDECIDED_;
-          res = d == CB_ERROR ? KPE_ERROR_ : d == CB_TRUE ? KPE_FAIL_ : KPE_PASS_;
-        }
-        if (res == KPE_SKIP_) continue;
-        if (res == KPE_ERROR_) {
-          if (idx + 1u < n) continue;
-          return KPE_ERROR_;
-        }
-        if (res == KPE_FAIL_) return KPE_FAIL_;
-        ++count;
-      }
-      applied += count;
-    }
-    return applied ? KPE_PASS_ : KPE_NA_;
-  }
 };
 
-// kpe_cond_kernel's body for resource r: every condition rule whose cell the scan matched
-__device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r) {
-  CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r]};
+// kpe_cond_kernel's body for resource r: every condition rule whose cell the scan matched.
+// A small state machine so that block() (and the foreach list's value()) are each called
+// from one place: everything is inlined, and every extra call site would be another copy.
+constexpr uint32_t PH_PRE = 0, PH_HANDLER = 1, PH_DENY = 2, PH_FE_LIST = 3, PH_FE_EL = 4, PH_FE_PRE = 5,
+                   PH_FE_DENY = 6, PH_DONE = 7;
+__device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16]) {
+  CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], {}, {}, nb};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   for (uint32_t i = 0; i < a.ncr; ++i) {
     const KpeCRule cr = a.rules[i];
     const uint8_t cell = row[cr.col];
     if (cell == KPE_NA_) continue;  // the rule did not match
     uint32_t v = cell;
-    bool done = false;
-    if (cr.pre != CE_NONE) {  // engine.go:278-285
-      const int p = vm.block(cr.pre, cv(VK_NULL, 0), 0);
-      if (p != CB_TRUE) {
-        v = p == CB_FALSE ? KPE_SKIP_ : p == CB_ERROR ? KPE_ERROR_ : KPE_UNDECIDED_;
-        done = true;
+    uint32_t ph = cr.pre != CE_NONE ? PH_PRE : PH_HANDLER;
+    // foreach state (validateForEach / validateElements, validate_resource.go:186-254)
+    uint32_t f = 0, idx = 0, n = 0, count = 0, applied = 0;
+    KpeCForeach fe{};
+    CV lst = cv(VK_NULL, 0), el = cv(VK_NULL, 0);
+    bool one = false;
+    while (ph != PH_DONE) {
+      uint32_t bi = CE_NONE;
+      if (ph == PH_HANDLER) {
+        if (cr.kind == CR_DENY) {
+          ph = PH_DENY;
+        } else if (cr.kind == CR_FOREACH) {
+          ph = PH_FE_LIST;
+        } else {
+          if (cr.kind == CR_NONE) v = KPE_NA_;  // no handler: no response
+          ph = PH_DONE;
+        }
+        continue;
       }
-    }
-    if (!done) {
-      if (cr.kind == CR_DENY) {  // validateDeny (validate_resource.go:268-279)
-        const int d = vm.block(cr.deny, cv(VK_NULL, 0), 0);
-        v = d == CB_TRUE ? KPE_FAIL_ : d == CB_FALSE ? KPE_PASS_ : d == CB_ERROR ? KPE_ERROR_ : KPE_UNDECIDED_;
-      } else if (cr.kind == CR_FOREACH) {
-        v = vm.foreach_rule(cr);
-      } else if (cr.kind == CR_NONE) {
-        v = KPE_NA_;  // no handler: no response
+      if (ph == PH_FE_LIST) {  // next entry: EvaluateList (utils/foreach.go:12-24)
+        if (f >= cr.nfe) {
+          v = applied ? KPE_PASS_ : KPE_NA_;
+          ph = PH_DONE;
+          continue;
+        }
+        fe = a.fes[cr.fe0 + f];
+        const int st = vm.value(fe.list, cv(VK_NULL, 0), 0, 0, 1, 2, &lst);
+        if (st == CS_UNDEC) {
+          v = KPE_UNDECIDED_;
+          ph = PH_DONE;
+          continue;
+        }
+        if (st != CS_OK) {  // "failed to evaluate list": the entry is skipped
+          ++f;
+          continue;
+        }
+        one = vm.type(lst) != JT_ARR;  // a non-list result is a one-element list
+        if (!one && lst.k == VK_LIST) {  // keep a computed list out of the key / value buffers
+          vm.blen[6] = vm.blen[lst.p];
+          for (uint32_t k = 0; k < vm.blen[6]; ++k) vm.buf[6][k] = vm.buf[lst.p][k];
+          lst = cv(VK_LIST, 6);
+        }
+        n = one ? 1u : vm.alen(lst);
+        idx = 0, count = 0;
+        ph = PH_FE_EL;
+        continue;
+      }
+      if (ph == PH_FE_EL) {
+        if (idx >= n) {
+          applied += count;
+          ++f;
+          ph = PH_FE_LIST;
+          continue;
+        }
+        el = one ? lst : vm.aget(lst, idx);
+        if (vm.type(el) == JT_NULL) {
+          ++idx;
+          continue;
+        }
+        if (fe.scope == 2u && vm.type(el) != JT_OBJ) {  // AddElementToContext: elementScope needs a map
+          v = KPE_ERROR_;
+          ph = PH_DONE;
+          continue;
+        }
+        ph = fe.pre != CE_NONE ? PH_FE_PRE : PH_FE_DENY;
+        continue;
+      }
+      const bool elem = ph == PH_FE_PRE || ph == PH_FE_DENY;
+      bi = ph == PH_PRE ? cr.pre : ph == PH_DENY ? cr.deny : ph == PH_FE_PRE ? fe.pre : fe.deny;
+      const int res = vm.block(bi, elem ? el : cv(VK_NULL, 0), elem ? idx : 0u);  // the one call site
+      if (res == CB_UNDEC) {
+        v = KPE_UNDECIDED_;
+        ph = PH_DONE;
+        continue;
+      }
+      if (ph == PH_PRE) {  // engine.go:278-285: false => skip, error => error
+        if (res == CB_TRUE) {
+          ph = PH_HANDLER;
+        } else {
+          v = res == CB_FALSE ? KPE_SKIP_ : KPE_ERROR_;
+          ph = PH_DONE;
+        }
+      } else if (ph == PH_DENY) {  // validateDeny (validate_resource.go:268-279)
+        v = res == CB_TRUE ? KPE_FAIL_ : res == CB_FALSE ? KPE_PASS_ : KPE_ERROR_;
+        ph = PH_DONE;
+      } else {  // an element's preconditions (false => skip) or deny (true => fail)
+        uint32_t ev;
+        if (res == CB_ERROR) ev = KPE_ERROR_;
+        else if (ph == PH_FE_PRE) ev = res == CB_FALSE ? KPE_SKIP_ : 0u;
+        else ev = res == CB_TRUE ? KPE_FAIL_ : KPE_PASS_;
+        if (ev == 0u) {  // preconditions hold: evaluate the deny conditions
+          ph = PH_FE_DENY;
+          continue;
+        }
+        ph = PH_FE_EL;
+        ++idx;
+        if (ev == KPE_PASS_) {
+          ++count;
+        } else if (ev == KPE_FAIL_) {
+          v = KPE_FAIL_;
+          ph = PH_DONE;
+        } else if (ev == KPE_ERROR_ && idx >= n) {  // an error counts only on the last element
+          v = KPE_ERROR_;
+          ph = PH_DONE;
+        }
       }
     }
     row[cr.col] = (uint8_t)v;

@@ -984,8 +984,9 @@ namespace {
 }  // namespace
 
 __global__ void __launch_bounds__(128) kpe_cond_kernel(const CondArgs* __restrict__ ap) {
+  __shared__ char nb[128][2][16];
   const int64_t r = (int64_t)blockIdx.x * 128 + threadIdx.x;
-  if (r < ap->n) cond_eval_row(*ap, r);
+  if (r < ap->n) cond_eval_row(*ap, r, nb[threadIdx.x]);
 }
 
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s) {

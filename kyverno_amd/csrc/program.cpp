@@ -1527,7 +1527,13 @@ class CondCompiler {
     CP.blocks.push_back(b);
     return (uint32_t)CP.blocks.size() - 1;
   }
-  uint32_t list_query(const std::string& q) { return Q.compile(q); }
+  // a foreach list: a query template (the device evaluates it through the condition-value path)
+  uint32_t list_query(const std::string& q) {
+    KpeVTmpl t{};
+    t.kind = VT_QUERY, t.a = Q.compile(q);
+    CP.tmpls.push_back(t);
+    return (uint32_t)CP.tmpls.size() - 1;
+  }
 
  private:
   CondProgram& CP;

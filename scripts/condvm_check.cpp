@@ -80,7 +80,8 @@ int main(int argc, char** argv) {
   a.blocks = CP.blocks.data(), a.fes = CP.fes.data(), a.rules = CP.rules.data();
   a.ctab = CP.consts.data(), a.ctext = ctext.data(), a.clist = CP.clist.data(), a.fkeys = fk.data();
   a.verdicts = verdicts.data();
-  for (int64_t r = 0; r < a.n; ++r) cond_eval_row(a, r);  // kpe_cond_kernel's lane body
+  char nb[2][16];
+  for (int64_t r = 0; r < a.n; ++r) cond_eval_row(a, r, nb);  // kpe_cond_kernel's lane body
   FILE* f = fopen(argv[4], "wb");
   fwrite(verdicts.data(), 1, verdicts.size(), f);
   fclose(f);
