@@ -46,13 +46,16 @@ struct Corpus {
   std::vector<uint32_t> vol_off{0}, vol_src;
   std::vector<uint32_t> sys_off{0}, sys_id;
   std::vector<uint32_t> pann_off{0}, pann_k, pann_v;  // pod-template metadata annotations
+  std::vector<uint32_t> p_cold;  // cold (D_MISC), 4 per pod: seccomp type, seLinux type / user / role
   // ---- containers (visit order: initContainers, containers, ephemeralContainers) ----
   std::vector<uint32_t> c_sc;
   std::vector<uint64_t> c_add, c_drop;
   std::vector<uint32_t> c_name, c_image, c_sann;
+  std::vector<uint32_t> c_sann_key;  // cold: D_ANNK id of the container's seccomp annotation key
   std::vector<uint32_t> c_sec_str, c_pm_str, c_selt_str, c_selu_str, c_selr_str;  // cold (D_MISC)
   std::vector<uint32_t> cport_off{0};
   std::vector<int32_t> cport_host;  // cold: hostPort of every port
+  std::vector<uint32_t> cport_str;  // cold: D_MISC id of strconv.Itoa(hostPort), KPE_NO_STR for 0
   // ---- packed hot records for the PSS scan (schema.h) ----
   std::vector<uint32_t> rec;   // 4 words per pod
   std::vector<uint32_t> hdr;   // 4 words per 64 pods

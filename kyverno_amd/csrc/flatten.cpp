@@ -1007,6 +1007,10 @@ class Flattener {
     p |= pod.whp << P_WHP_SH;
     p |= (pod.os ? (pod.os_name == "windows" ? OS_WINDOWS : OS_OTHER) : OS_NONE) << P_OS_SH;
     C.p_sc.push_back(p);
+    C.p_cold.push_back(pod.sec ? C.dict[D_MISC].intern(pod.sec_type) : KPE_NO_STR);
+    C.p_cold.push_back(pod.sel ? C.dict[D_MISC].intern(pod.sel_type) : KPE_NO_STR);
+    C.p_cold.push_back(pod.sel ? C.dict[D_MISC].intern(pod.sel_user) : KPE_NO_STR);
+    C.p_cold.push_back(pod.sel ? C.dict[D_MISC].intern(pod.sel_role) : KPE_NO_STR);
     for (uint32_t v : pod.vols) C.vol_src.push_back(v);
     C.vol_off.push_back((uint32_t)C.vol_src.size());
     for (auto& s : pod.sysctls) C.sys_id.push_back(C.dict[D_SYSCTL].intern(s));
@@ -1065,19 +1069,23 @@ class Flattener {
         }
         C.c_name.push_back(C.dict[D_CNAME].intern(c.name));
         C.c_image.push_back(C.dict[D_IMAGE].intern(c.image));
-        uint32_t sann = KPE_NO_STR;  // join: pod annotation "container.seccomp...kubernetes.io/<name>"
+        uint32_t sann = KPE_NO_STR, sann_key = KPE_NO_STR;  // join: "container.seccomp...kubernetes.io/<name>"
         if (!pod.ann.empty()) {
           std::string key = seccomp_ctr_prefix + c.name;
           for (auto& kv : pod.ann)
-            if (kv.first == key) sann = C.dict[D_ANNV].intern(kv.second);
+            if (kv.first == key) sann = C.dict[D_ANNV].intern(kv.second), sann_key = C.dict[D_ANNK].intern(kv.first);
         }
         C.c_sann.push_back(sann);
+        C.c_sann_key.push_back(sann_key);
         C.c_sec_str.push_back(c.sec ? C.dict[D_MISC].intern(c.sec_type) : KPE_NO_STR);
         C.c_pm_str.push_back(c.pm ? C.dict[D_MISC].intern(c.pm_val) : KPE_NO_STR);
         C.c_selt_str.push_back(c.sel ? C.dict[D_MISC].intern(c.sel_type) : KPE_NO_STR);
         C.c_selu_str.push_back(c.sel ? C.dict[D_MISC].intern(c.sel_user) : KPE_NO_STR);
         C.c_selr_str.push_back(c.sel ? C.dict[D_MISC].intern(c.sel_role) : KPE_NO_STR);
-        for (int32_t h : c.hostports) C.cport_host.push_back(h);
+        for (int32_t h : c.hostports) {
+          C.cport_host.push_back(h);
+          C.cport_str.push_back(h ? C.dict[D_MISC].intern(std::to_string(h)) : KPE_NO_STR);
+        }
         C.cport_off.push_back((uint32_t)C.cport_host.size());
       }
     }

@@ -995,6 +995,26 @@ extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStrea
   return hipGetLastError();
 }
 
+// ===========================================================================
+// podSecurity.exclude (pssx.inl): one lane per pod re-evaluates the failing cells of the
+// rules with exclusions. Runs after the condition kernel (preconditions may have skipped a
+// cell); reads the corpus's pod columns and the predicate bitsets in pbuf.
+// ===========================================================================
+namespace {
+#include "pssx.inl"
+}  // namespace
+
+__global__ void __launch_bounds__(128) kpe_pssx_kernel(const PssxArgs* __restrict__ ap) {
+  const int64_t r = (int64_t)blockIdx.x * 128 + threadIdx.x;
+  if (r < ap->n) pssx_eval_row(*ap, r);
+}
+
+extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_pssx_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s) {
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dargs);

@@ -202,3 +202,30 @@ struct CondArgs {
   const uint32_t* fkeys;           // field index -> D_KEY id + 1 (0: absent from the corpus)
   uint8_t* verdicts;
 };
+
+// kpe_pssx_kernel arguments (device-resident, one copy per binding): podSecurity rules with
+// exclusions, after the scan wrote their plain PSS verdicts.
+struct PssxArgs {
+  int64_t n;
+  uint32_t R, nxr;
+  const KpeXRule* rules;
+  const KpeXExcl* excl;            // predicate fields resolved to pbuf word indices
+  const uint32_t* rec;             // pod records (x = pod word)
+  const uint32_t *ctr_off, *vol_off, *sys_off, *pann_off;  // per-pod list offsets (n + 1)
+  const uint32_t* crec;            // container records (state bitmap, capset | type << 16)
+  const uint32_t* capsets;         // 4 words per capability set
+  const uint32_t *c_name, *c_image, *c_sann, *c_sann_key;
+  const uint32_t *c_sec_str, *c_pm_str, *c_selt_str, *c_selu_str, *c_selr_str;
+  const uint32_t *cport_off, *cport_str;
+  const uint32_t *vol_src, *sys_id, *pann_k, *pann_v;
+  const uint32_t* p_cold;          // 4 words per pod (D_MISC ids)
+  const uint32_t *misc_off, *annv_off, *sysd_off;  // dictionary offsets (empty-string tests)
+  const uint32_t* ann_norm;        // D_ANNK id -> normalised-key id
+  const uint32_t* rf_ann;          // XRF_ANN text index -> normalised-key id (KPE_NO_STR: none)
+  uint32_t key_pod_sec, key_fake_sec;  // D_ANNK ids of the pod / "fake" container seccomp keys
+  const uint32_t* pbuf;            // predicate bitsets (global locations)
+  uint32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_ok, pp_caps_ok, pp_nbs, pp_all;
+  uint32_t pp_sysctl[3];
+  uint8_t* verdicts;
+  uint32_t* masks;                 // n x R failing versioned checks, or null
+};

@@ -29,6 +29,7 @@ bool is_limit_error(const std::exception& e);
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
@@ -136,6 +137,7 @@ struct DeviceProgram {
   DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
   // condition rules: compiled programs (program.hpp CondProgram)
   DevBuf cops, cexprs, ctmpls, cconds, cblocks, cfes, crules, cconsts, ctext, cclist;
+  DevBuf xrules;  // podSecurity rules with exclusions (program.hpp PssxProgram)
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
   std::vector<uint32_t> pat0;
@@ -152,6 +154,10 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   bool pargs_valid = false;
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
+  DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
+  bool xargs_valid = false;
+  void* xmasks = nullptr;  // the masks buffer xargs points at (null: no masks)
+  uint32_t xpp[9] = {}, key_pod_sec = KPE_NO_STR, key_fake_sec = KPE_NO_STR;
   ScanArgs hargs{};    // what dargs holds
   bool args_valid = false;
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
@@ -173,6 +179,10 @@ struct DeviceCorpus {
   DevBuf lab_off, lab_k, lab_v, r_nsl, nsl_off, nsl_k, nsl_v;
   DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
   DevBuf doc, doc_off, scal, scal_text;  // document tape + scalar table (pattern rules)
+  // cold pod columns, uploaded on the first binding of a program with podSecurity exclusions
+  DevBuf ctr_off, vol_off, sys_off, pann_off, c_name, c_image, c_sann_key, c_sec_str, c_pm_str, c_selt_str, c_selu_str,
+      c_selr_str, cport_off, cport_str, pann_k, pann_v, p_cold;
+  bool cold = false;
   Binding bind;
   bool has_masks = false;
 };
@@ -447,6 +457,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.cconsts, CP.consts, s0));
     HIPCHK(upload(D.ctext, CP.ctext, s0));
     HIPCHK(upload(D.cclist, CP.clist, s0));
+    HIPCHK(upload(D.xrules, P.pssx.rules, s0));
   }
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
@@ -690,6 +701,66 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     HIPCHK(upload(B.cfkeys, fk, s));
     B.cargs_valid = false;
   }
+  if (!P.pssx.rules.empty()) {  // podSecurity exclusions: cold pod columns, key tables, resolved excludes
+    auto& D = *cc->d;
+    if (!D.cold) {
+      HIPCHK(upload(D.ctr_off, C.ctr_off, s));
+      HIPCHK(upload(D.vol_off, C.vol_off, s));
+      HIPCHK(upload(D.sys_off, C.sys_off, s));
+      HIPCHK(upload(D.pann_off, C.pann_off, s));
+      HIPCHK(upload(D.c_name, C.c_name, s));
+      HIPCHK(upload(D.c_image, C.c_image, s));
+      HIPCHK(upload(D.c_sann_key, C.c_sann_key, s));
+      HIPCHK(upload(D.c_sec_str, C.c_sec_str, s));
+      HIPCHK(upload(D.c_pm_str, C.c_pm_str, s));
+      HIPCHK(upload(D.c_selt_str, C.c_selt_str, s));
+      HIPCHK(upload(D.c_selu_str, C.c_selu_str, s));
+      HIPCHK(upload(D.c_selr_str, C.c_selr_str, s));
+      HIPCHK(upload(D.cport_off, C.cport_off, s));
+      HIPCHK(upload(D.cport_str, C.cport_str, s));
+      HIPCHK(upload(D.pann_k, C.pann_k, s));
+      HIPCHK(upload(D.pann_v, C.pann_v, s));
+      HIPCHK(upload(D.p_cold, C.p_cold, s));
+      D.cold = true;
+    }
+    // annotation keys with digit runs replaced by "*" (parseField's regexIndex), numbered
+    const kpe::Dict& AK = C.dict[D_ANNK];
+    std::unordered_map<std::string, uint32_t> nid;
+    auto normalise = [](std::string_view k) {
+      std::string o;
+      for (size_t i = 0; i < k.size();) {
+        if (k[i] >= '0' && k[i] <= '9') {
+          while (i < k.size() && k[i] >= '0' && k[i] <= '9') ++i;
+          o += '*';
+        } else {
+          o += k[i++];
+        }
+      }
+      return o;
+    };
+    std::vector<uint32_t> norm(std::max<uint32_t>(AK.size(), 1u), KPE_NO_STR);
+    for (uint32_t i = 0; i < AK.size(); ++i) norm[i] = nid.emplace(normalise(AK.at(i)), (uint32_t)nid.size()).first->second;
+    std::vector<uint32_t> rf(std::max<size_t>(P.pssx.rf_ann.size(), 1), KPE_NO_STR);
+    for (size_t i = 0; i < P.pssx.rf_ann.size(); ++i) {
+      auto it = nid.find(P.pssx.rf_ann[i]);
+      if (it != nid.end()) rf[i] = it->second;
+    }
+    HIPCHK(upload(B.ann_norm, norm, s));
+    HIPCHK(upload(B.rf_ann, rf, s));
+    std::vector<KpeXExcl> xe = P.pssx.excl;
+    for (auto& x : xe) {
+      x.img = (int32_t)loc(x.img);
+      x.pv_misc = (int32_t)loc(x.pv_misc), x.pv_annv = (int32_t)loc(x.pv_annv);
+      x.pv_sys = (int32_t)loc(x.pv_sys), x.pv_cap = (int32_t)loc(x.pv_cap);
+    }
+    HIPCHK(upload(B.xexcl, xe, s));
+    for (int k = 0; k < 9; ++k) B.xpp[k] = loc(P.pssx_preds[k]);
+    const int64_t kp = AK.find("seccomp.security.alpha.kubernetes.io/pod");
+    const int64_t kf = AK.find("container.seccomp.security.alpha.kubernetes.io/fake");
+    B.key_pod_sec = kp < 0 ? KPE_NO_STR : (uint32_t)kp;
+    B.key_fake_sec = kf < 0 ? KPE_NO_STR : (uint32_t)kf;
+    B.xargs_valid = false;
+  }
   if (fused) memcpy(fimg.data(), pairs.data(), pairs.size() * 4);
   const uint32_t fuse_words = fused ? (uint32_t)fimg.size() : 0u;
   const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
@@ -896,6 +967,58 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       B.cargs_valid = true;
     }
     HIPCHK(kpe_launch_cond(B.cargs.as<CondArgs>(), C.n, s));
+  }
+  if (!P.pssx.rules.empty()) {
+    if (!B.xargs_valid || (masks ? B.masks.p : nullptr) != B.xmasks) {
+      PssxArgs xa{};
+      xa.n = C.n;
+      xa.R = (uint32_t)R;
+      xa.nxr = (uint32_t)P.pssx.rules.size();
+      xa.rules = PD.xrules.as<KpeXRule>();
+      xa.excl = B.xexcl.as<KpeXExcl>();
+      xa.rec = D.rec.as<uint32_t>();
+      xa.ctr_off = D.ctr_off.as<uint32_t>();
+      xa.vol_off = D.vol_off.as<uint32_t>();
+      xa.sys_off = D.sys_off.as<uint32_t>();
+      xa.pann_off = D.pann_off.as<uint32_t>();
+      xa.crec = D.crec.as<uint32_t>();
+      xa.capsets = D.capsets.as<uint32_t>();
+      xa.c_name = D.c_name.as<uint32_t>();
+      xa.c_image = D.c_image.as<uint32_t>();
+      xa.c_sann = D.c_sann.as<uint32_t>();
+      xa.c_sann_key = D.c_sann_key.as<uint32_t>();
+      xa.c_sec_str = D.c_sec_str.as<uint32_t>();
+      xa.c_pm_str = D.c_pm_str.as<uint32_t>();
+      xa.c_selt_str = D.c_selt_str.as<uint32_t>();
+      xa.c_selu_str = D.c_selu_str.as<uint32_t>();
+      xa.c_selr_str = D.c_selr_str.as<uint32_t>();
+      xa.cport_off = D.cport_off.as<uint32_t>();
+      xa.cport_str = D.cport_str.as<uint32_t>();
+      xa.vol_src = D.vol_src.as<uint32_t>();
+      xa.sys_id = D.sys_id.as<uint32_t>();
+      xa.pann_k = D.pann_k.as<uint32_t>();
+      xa.pann_v = D.pann_v.as<uint32_t>();
+      xa.p_cold = D.p_cold.as<uint32_t>();
+      xa.misc_off = D.dict_off[D_MISC].as<uint32_t>();
+      xa.annv_off = D.dict_off[D_ANNV].as<uint32_t>();
+      xa.sysd_off = D.dict_off[D_SYSCTL].as<uint32_t>();
+      xa.ann_norm = B.ann_norm.as<uint32_t>();
+      xa.rf_ann = B.rf_ann.as<uint32_t>();
+      xa.key_pod_sec = B.key_pod_sec;
+      xa.key_fake_sec = B.key_fake_sec;
+      xa.pbuf = B.pbuf.as<uint32_t>();
+      xa.pp_apparmor_key = B.xpp[0], xa.pp_apparmor_ok = B.xpp[1], xa.pp_seccomp_ok = B.xpp[2];
+      xa.pp_caps_ok = B.xpp[3], xa.pp_nbs = B.xpp[4], xa.pp_all = B.xpp[5];
+      for (int v = 0; v < 3; ++v) xa.pp_sysctl[v] = B.xpp[6 + v];
+      xa.verdicts = B.verdicts.as<uint8_t>();
+      xa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
+      HIPCHK(B.xargs.ensure(sizeof(PssxArgs)));
+      HIPCHK(hipMemcpyAsync(B.xargs.p, &xa, sizeof(PssxArgs), hipMemcpyHostToDevice, s));
+      HIPCHK(hipStreamSynchronize(s));
+      B.xmasks = masks ? B.masks.p : nullptr;
+      B.xargs_valid = true;
+    }
+    HIPCHK(kpe_launch_pssx(B.xargs.as<PssxArgs>(), C.n, s));
   }
   if (!P.pat.rules.empty()) {
     if (!B.pargs_valid) {

@@ -1604,6 +1604,140 @@ class Lowerer {
     s.sysctl[2] = pred(D_SYSCTL, v129);
   }
 
+  // a predicate read only by a kernel after the scan: its bitset is always written to pbuf
+  int32_t gpred(uint32_t domain, std::vector<std::string> globs) {
+    for (size_t i = 0; i < P.preds.size(); ++i)
+      if (P.preds[i].global_only && P.preds[i].domain == domain && P.preds[i].globs == globs) return (int32_t)i;
+    P.preds.push_back({domain, std::move(globs)});
+    P.preds.back().global_only = true;
+    return (int32_t)P.preds.size() - 1;
+  }
+
+  // restrictedField -> XRF_* (the field paths the PSA checks report, digit runs as "*")
+  static void restricted_field(const std::string& f, KpeXExcl* x, std::vector<std::string>& ann) {
+    static const char* sfx[] = {"securityContext.allowPrivilegeEscalation", "securityContext.capabilities.add",
+                                "securityContext.capabilities.drop", "ports[*].hostPort",
+                                "securityContext.privileged", "securityContext.procMount",
+                                "securityContext.runAsNonRoot", "securityContext.runAsUser",
+                                "securityContext.seLinuxOptions.type", "securityContext.seLinuxOptions.user",
+                                "securityContext.seLinuxOptions.role", "securityContext.seccompProfile.type",
+                                "securityContext.windowsOptions.hostProcess"};
+    static const char* ctn[] = {"initContainers", "containers", "ephemeralContainers"};
+    // corev1.VolumeSource JSON names by VS_* index
+    static const char* vs[] = {"hostPath", "emptyDir", "gcePersistentDisk", "awsElasticBlockStore", "gitRepo",
+                               "secret", "nfs", "iscsi", "glusterfs", "persistentVolumeClaim", "rbd",
+                               "flexVolume", "cinder", "cephfs", "flocker", "downwardAPI", "fc", "azureFile",
+                               "configMap", "vsphereVolume", "quobyte", "azureDisk", "photonPersistentDisk",
+                               "projected", "portworxVolume", "scaleIO", "storageos", "csi", "ephemeral"};
+    static_assert(sizeof(vs) / sizeof(vs[0]) == KPE_NUM_VOLUME_SOURCES, "volume sources");
+    x->rf_kind = XRF_NEVER;
+    if (f.empty()) {
+      x->rf_kind = XRF_ANY;
+      return;
+    }
+    auto set = [&](uint32_t fc, uint32_t ct) { x->rf_kind = XRF_FIELD, x->rf_key = XKEY(fc, ct); };
+    for (uint32_t c = 0; c < 3; ++c)
+      for (uint32_t k = 0; k <= XF_WHP; ++k)
+        if (f == std::string("spec.") + ctn[c] + "[*]." + sfx[k]) set(k, c);
+    for (uint32_t k : {XF_RNR, XF_RAU, XF_SEL_TYPE, XF_SEL_USER, XF_SEL_ROLE, XF_SECCOMP, XF_WHP})
+      if (f == std::string("spec.") + sfx[k]) set(k, XT_POD);
+    if (f == "spec.hostNetwork") set(XF_HOSTNET, XT_POD);
+    if (f == "spec.hostPID") set(XF_HOSTPID, XT_POD);
+    if (f == "spec.hostIPC") set(XF_HOSTIPC, XT_POD);
+    if (f == "spec.securityContext.sysctls[*].name") set(XF_SYSCTL, XT_POD);
+    for (uint32_t v = 0; v < KPE_NUM_VOLUME_SOURCES; ++v)
+      if (f == std::string("spec.volumes[*].") + vs[v]) set(XF_VOL + v, XT_POD);
+    if (f == "spec.volumes[*].unknown") set(XF_VOL + 31, XT_POD);
+    const std::string pre = "metadata.annotations[";
+    if (f.size() > pre.size() + 1 && f.compare(0, pre.size(), pre) == 0 && f.back() == ']') {
+      x->rf_kind = XRF_ANN;
+      x->rf_key = (uint32_t)ann.size();
+      ann.push_back(f.substr(pre.size(), f.size() - pre.size() - 1));
+    }
+  }
+
+  // podSecurity.exclude (pkg/pss/evaluate.go:72-317; exclude.Validate, common_types.go:472-478)
+  void pss_exclusions(const JV& ex, uint32_t col, uint32_t cvm, const std::string& rname) {
+    static const std::map<std::string, uint32_t> controls = {  // pkg/pss/utils/mapping.go:45-107
+        {"Capabilities", (1u << CK_CAPS_BASELINE) | (1u << CK_CAPS_RESTRICTED)},
+        {"Seccomp", (1u << CK_SECCOMP_BASELINE) | (1u << CK_SECCOMP_RESTRICTED)},
+        {"Privileged Containers", 1u << CK_PRIVILEGED},
+        {"Host Ports", 1u << CK_HOST_PORTS},
+        {"/proc Mount Type", 1u << CK_PROC_MOUNT},
+        {"HostProcess", 1u << CK_WIN_HOST_PROCESS},
+        {"SELinux", 1u << CK_SELINUX},
+        {"Host Namespaces", 1u << CK_HOST_NS},
+        {"HostPath Volumes", 1u << CK_HOST_PATH},
+        {"Sysctls", 1u << CK_SYSCTLS},
+        {"AppArmor", 1u << CK_APPARMOR},
+        {"Privilege Escalation", 1u << CK_APE},
+        {"Running as Non-root", 1u << CK_RUN_AS_NON_ROOT},
+        {"Running as Non-root user", 1u << CK_RUN_AS_USER},
+        {"Volume Types", 1u << CK_RESTRICTED_VOLUMES},
+    };
+    auto strs = [&](const JV* j, const char* what) {
+      std::vector<std::string> out;
+      if (!j || j->t == JV::Null) return out;
+      if (j->t != JV::Arr) throw CompileError("rule '" + rname + "': podSecurity.exclude " + what + " is not a list");
+      for (auto& e : j->a) {
+        if (e.t != JV::Str) throw CompileError("rule '" + rname + "': podSecurity.exclude " + what + " entry");
+        out.push_back(e.s);
+      }
+      return out;
+    };
+    auto str = [&](const JV* j, const char* what) {
+      if (!j || j->t == JV::Null) return std::string();
+      if (j->t != JV::Str) throw CompileError("rule '" + rname + "': podSecurity.exclude " + what + " is not a string");
+      return j->s;
+    };
+    KpeXRule xr{};
+    xr.col = col, xr.cv_mask = cvm, xr.excl0 = (uint32_t)P.pssx.excl.size(), xr.nexcl = (uint32_t)ex.a.size();
+    int64_t last_invalid = -1;
+    for (size_t i = 0; i < ex.a.size(); ++i) {
+      const JV& e = ex.a[i];
+      if (e.t != JV::Obj) throw CompileError("rule '" + rname + "': podSecurity.exclude entry is not an object");
+      const std::string cn = str(e.get("controlName"), "controlName");
+      const std::vector<std::string> images = strs(e.get("images"), "images");
+      const std::string rf = str(e.get("restrictedField"), "restrictedField");
+      const std::vector<std::string> values = strs(e.get("values"), "values");
+      if ((!rf.empty() && values.empty()) || (rf.empty() && !values.empty())) last_invalid = (int64_t)i;
+      KpeXExcl x{};
+      auto it = controls.find(cn);
+      x.checks = it == controls.end() ? 0u : it->second;
+      x.img = images.empty() ? -1 : gpred(D_IMAGE, images);
+      restricted_field(rf, &x, P.pssx.rf_ann);
+      x.has_values = values.empty() ? 0u : 1u;
+      x.pv_misc = x.pv_annv = x.pv_sys = x.pv_cap = -1;
+      if (!values.empty()) {
+        auto any = [&](const char* s) {
+          for (auto& v : values)
+            if (glob_host(v, s)) return true;
+          return false;
+        };
+        x.vconst = (any("true") ? XV_TRUE : 0u) | (any("false") ? XV_FALSE : 0u) | (any("0") ? XV_ZERO : 0u);
+        x.pv_misc = gpred(D_MISC, values);
+        x.pv_annv = gpred(D_ANNV, values);
+        x.pv_sys = gpred(D_SYSCTL, values);
+        x.pv_cap = gpred(D_CAP, values);
+      }
+      xr.kx |= x.checks;
+      P.pssx.excl.push_back(x);
+    }
+    if (last_invalid >= 0)
+      xr.force = last_invalid == (int64_t)ex.a.size() - 1 ? XR_FORCE_FAIL : XR_FORCE_PASS;
+    if (P.pssx.rules.empty()) {  // fixed PSA predicates, read from pbuf by kpe_pssx_kernel
+      auto& g = P.pssx_preds;
+      g[0] = gpred(D_ANNK, {"container.apparmor.security.beta.kubernetes.io/*"});
+      g[1] = gpred(D_ANNV, {"runtime/default", "localhost/*"});
+      g[2] = gpred(D_ANNV, {"runtime/default", "docker/default", "localhost/*"});
+      g[3] = gpred(D_CAP, P.preds[P.pss.caps_baseline_ok].globs);
+      g[4] = gpred(D_CAP, {"NET_BIND_SERVICE"});
+      g[5] = gpred(D_CAP, {"ALL"});
+      for (int v = 0; v < 3; ++v) g[6 + v] = gpred(D_SYSCTL, P.preds[P.pss.sysctl[v]].globs);
+    }
+    P.pssx.rules.push_back(xr);
+  }
+
   uint32_t term(const KpeTerm& t) {  // distinct terms are evaluated once per resource
     for (size_t i = 0; i < P.terms.size(); ++i) {
       const KpeTerm& u = P.terms[i];
@@ -1914,13 +2048,19 @@ class Lowerer {
     } else if (nonempty(v->get("manifests"))) {
       throw CompileError("rule '" + rname + "': validate.manifests is not supported");
     } else if (ps && ps->t == JV::Obj && nonempty(ps)) {
-      const JV* ex = ps->get("exclude");
-      if (ex && ex->t == JV::Arr && !ex->a.empty())
-        throw CompileError("rule '" + rname + "': podSecurity.exclude is not supported on the device yet");
       bool ok;
       k.cv_mask = cv_mask(sv(ps->get("level")), sv(ps->get("version")), &ok);
       k.handler = ok ? H_PSS : H_ERROR;
       pss_preds();
+      const JV* ex = ps->get("exclude");
+      if (ok && ex && ex->t != JV::Null) {
+        if (ex->t != JV::Arr) throw CompileError("rule '" + rname + "': podSecurity.exclude is not a list");
+        if (!ex->a.empty()) {
+          if (apply_one)
+            throw CompileError("rule '" + rname + "': applyRules=One with podSecurity.exclude is not supported");
+          pss_exclusions(*ex, (uint32_t)P.rules.size(), k.cv_mask, rname);
+        }
+      }
       P.any_pss = true;
       P.cv_union |= k.cv_mask;
       auto it = std::find(P.cv_classes.begin(), P.cv_classes.end(), k.cv_mask);

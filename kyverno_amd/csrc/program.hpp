@@ -48,6 +48,13 @@ struct CondProgram {
   std::vector<uint32_t> clist;    // elements of constant lists
   std::vector<std::string> fields;
 };
+// podSecurity rules with exclusions (schema.h KpeXRule / KpeXExcl), evaluated per pod by
+// kpe_pssx_kernel after the scan. Predicate fields hold predicate ids (resolved per binding).
+struct PssxProgram {
+  std::vector<KpeXRule> rules;
+  std::vector<KpeXExcl> excl;
+  std::vector<std::string> rf_ann;  // XRF_ANN annotation keys K of restrictedField "metadata.annotations[K]"
+};
 #define PRED_SPECIAL_NONE 0u
 #define PRED_SPECIAL_QNAME 1u   // validation.IsQualifiedName (label keys)
 #define PRED_SPECIAL_LABVAL 2u  // validation.IsValidLabelValue
@@ -97,6 +104,8 @@ struct Program {
   bool any_pss = false;
   PatProgram pat;  // pattern rules (H_PATTERN)
   CondProgram cond;  // rules with preconditions / deny / foreach evaluated per resource
+  PssxProgram pssx;  // podSecurity.exclude
+  int32_t pssx_preds[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // PSA predicates of kpe_pssx_kernel
   DeviceProgram* dev = nullptr;
   ~Program();
 };

@@ -364,6 +364,59 @@ typedef struct KpeRule {
   uint32_t pad[2];        // 16 words
 } KpeRule;
 
+// ---- podSecurity.exclude (pkg/pss/evaluate.go:72-317), evaluated by kpe_pssx_kernel ----------
+// A PSA field error is keyed by its field path with digit runs replaced by "*": a suffix
+// code (XF_*) and the container list it names (XT_*, XT_POD for pod-level fields).
+// Annotation fields carry the normalised annotation key; container fields the container name.
+#define XF_APE 0u         // securityContext.allowPrivilegeEscalation
+#define XF_CAPS_ADD 1u    // securityContext.capabilities.add
+#define XF_CAPS_DROP 2u   // securityContext.capabilities.drop
+#define XF_HOSTPORT 3u    // ports[*].hostPort
+#define XF_PRIV 4u        // securityContext.privileged
+#define XF_PROCMOUNT 5u   // securityContext.procMount
+#define XF_RNR 6u         // securityContext.runAsNonRoot
+#define XF_RAU 7u         // securityContext.runAsUser
+#define XF_SEL_TYPE 8u    // securityContext.seLinuxOptions.type
+#define XF_SEL_USER 9u    // securityContext.seLinuxOptions.user
+#define XF_SEL_ROLE 10u   // securityContext.seLinuxOptions.role
+#define XF_SECCOMP 11u    // securityContext.seccompProfile.type
+#define XF_WHP 12u        // securityContext.windowsOptions.hostProcess
+#define XF_HOSTNET 13u    // spec.hostNetwork
+#define XF_HOSTPID 14u    // spec.hostPID
+#define XF_HOSTIPC 15u    // spec.hostIPC
+#define XF_SYSCTL 16u     // spec.securityContext.sysctls[*].name
+#define XF_ANN 17u        // metadata.annotations[<key>]
+#define XF_VOL 32u        // spec.volumes[*].<source>: XF_VOL + VS_* (XF_VOL + 31: "unknown")
+#define XT_POD 3u         // 0 initContainers, 1 containers, 2 ephemeralContainers
+#define XKEY(fc, ct) ((fc) | ((ct) << 8))
+// restrictedField forms
+#define XRF_ANY 0u    // restrictedField "" (with no values)
+#define XRF_FIELD 1u  // a fixed field path: key XKEY(fc, ct)
+#define XRF_ANN 2u    // metadata.annotations[K]: K against normalised annotation keys
+#define XRF_NEVER 3u  // a path no PSA check reports
+// constant bad-value matches of an exclude (extractBadValues of bools and the int 0)
+#define XV_TRUE 1u
+#define XV_FALSE 2u
+#define XV_ZERO 4u
+typedef struct KpeXExcl {
+  uint32_t checks;         // PSA check ids of controlName (pkg/pss/utils/mapping.go), bit per KpeCheck
+  int32_t img;             // predicate over D_IMAGE (images); -1: pod-level exclusion
+  uint32_t rf_kind, rf_key;  // XRF_*; XRF_FIELD: XKEY; XRF_ANN: index of K in the program's text table
+  uint32_t has_values, vconst;  // values non-empty; XV_* bits
+  int32_t pv_misc, pv_annv, pv_sys, pv_cap;  // predicates (values) over D_MISC / D_ANNV / D_SYSCTL / D_CAP
+  uint32_t pad[2];
+} KpeXExcl;  // 16 words
+// force: the exclusion list fails Validate (common_types.go:472-478): the last exclude's error
+// makes every evaluated pod fail; an earlier one empties the results (every pod passes)
+#define XR_FORCE_NONE 0u
+#define XR_FORCE_PASS 1u
+#define XR_FORCE_FAIL 2u
+typedef struct KpeXRule {
+  uint32_t col, cv_mask, excl0, nexcl;
+  uint32_t force, kx;  // kx: check ids some exclude names
+  uint32_t pad[2];
+} KpeXRule;
+
 // ---- generic document tape (pattern rules) ---------------------------------------------
 // Every resource is also kept as its JSON document (the reference's unstructured map).
 // An entry (uint2) is x = kind | (member-name id + 1) << 2 (D_KEY id; 0 = array element /

@@ -1,0 +1,134 @@
+"""podSecurity.exclude on the device (kpe_pssx_kernel, kyverno_amd/csrc/pssx.inl) against the
+oracle's restatement of pkg/pss/evaluate.go:72-317, which the reference's own cases pin
+(pkg/pss/evaluate_test.go: 222 cases with exclusions; chainsaw psa exclusion fixtures).
+
+CPU: the exclusion pass compiled for the host under ASan/UBSan (scripts/pssx_check.cpp),
+seeded with the plain PSS verdicts. GPU: the whole device path through the C-ABI."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import kyverno_amd as K
+from tests.policies import pss_policy
+from tests.pss_fuzz import fuzz_case, strip_exclusions
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+BIN = os.path.join(ROOT, "scripts", "build", "pssx_check")
+
+
+def golden_cases():
+    cases = [c for c in json.load(open(os.path.join(GOLD, "pss_evaluate_cases.json"))) if c["rule"].get("exclude")]
+    pols = [pss_policy(f"g{i}", c["rule"]["level"], c["rule"].get("version", "latest"), exclude=c["rule"]["exclude"])
+            for i, c in enumerate(cases)]
+    return cases, pols
+
+
+def chainsaw_cases():
+    """Chainsaw admissions with exclusions, minus test-exclusion-procmount/good-pod.yaml: its
+    expectation depends on the API server's ProcMountType gate (tests/test_oracle_golden.py);
+    the engine-level verdict is fail."""
+    cs = [c for c in json.load(open(os.path.join(GOLD, "chainsaw_psa.json")))
+          if c["policy"]["spec"]["rules"][0]["validate"]["podSecurity"].get("exclude")
+          and not c["file"].endswith("test-exclusion-procmount/good-pod.yaml")]
+    return cs
+
+
+@pytest.fixture(scope="module")
+def pssx_bin():
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), "pssx_check"])
+    return BIN
+
+
+def _host(pssx_bin, tmp_path, pols, nd, seed):
+    (tmp_path / "p.json").write_text(json.dumps(pols))
+    (tmp_path / "r.ndjson").write_bytes(nd)
+    (tmp_path / "seed.bin").write_bytes(np.ascontiguousarray(seed, dtype=np.uint8).tobytes())
+    subprocess.check_call([pssx_bin, str(tmp_path / "p.json"), str(tmp_path / "r.ndjson"),
+                           str(tmp_path / "seed.bin"), str(tmp_path / "out.bin")], stdout=subprocess.DEVNULL)
+    return np.frombuffer((tmp_path / "out.bin").read_bytes(), dtype=np.uint8).reshape(seed.shape)
+
+
+def test_compile_exclusions():
+    cases, pols = golden_cases()
+    ps = K.PolicySet(pols)
+    assert ps.num_rules == 3 * len(pols)  # + the two autogen rules of each
+    bad = pss_policy("b", "baseline", exclude={"controlName": "x"})
+    with pytest.raises(K.KpeError):
+        K.PolicySet([bad])
+
+
+def test_golden_evaluate_cases_host(pssx_bin, oracle, tmp_path):
+    """Every evaluate_test.go case with exclusions: one rule per case, all pods against all rules."""
+    cases, pols = golden_cases()
+    nd = "\n".join(json.dumps(c["pod"]) for c in cases).encode()
+    ref = oracle.validate(pols, nd, nthreads=8)
+    # the reference's own expectations sit on the diagonal (rule g<i> is column 3i)
+    assert [int(ref[i, 3 * i]) for i in range(len(cases))] == [1 if c["allowed"] else 2 for c in cases]
+    seed = oracle.validate(strip_exclusions(pols), nd, nthreads=8)
+    out = _host(pssx_bin, tmp_path, pols, nd, seed)
+    bad = np.argwhere(out != ref)
+    assert bad.size == 0, [(cases[j // 3]["name"], i, int(out[i, j]), int(ref[i, j])) for i, j in bad[:5]]
+
+
+def test_chainsaw_exclusions_host(pssx_bin, oracle, tmp_path):
+    cs = chainsaw_cases()
+    assert len(cs) >= 40
+    for c in cs:
+        nd = json.dumps(c["resource"]).encode()
+        ref = oracle.validate([c["policy"]], nd)
+        seed = oracle.validate(strip_exclusions([c["policy"]]), nd)
+        out = _host(pssx_bin, tmp_path, [c["policy"]], nd, seed)
+        assert (out == ref).all(), c["file"]
+        applied = [x for x in out[0] if x]
+        assert len(applied) == 1 and {1: "pass", 2: "fail"}[int(applied[0])] == c["expect"], c["file"]
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3, 4, 5, 6])
+def test_fuzz_exclusions_host(pssx_bin, oracle, tmp_path, seed):
+    pols, nd = fuzz_case(seed)
+    ref = oracle.validate(pols, nd, nthreads=8)
+    base = oracle.validate(strip_exclusions(pols), nd, nthreads=8)
+    out = _host(pssx_bin, tmp_path, pols, nd, base)
+    assert (out == 7).sum() == 0
+    bad = np.argwhere(out != ref)
+    assert bad.size == 0, [(int(i), int(j), int(out[i, j]), int(ref[i, j])) for i, j in bad[:8]]
+    # the exclusions change verdicts (the test exercises them)
+    assert ((base == 2) & (ref == 1)).sum() > 20
+
+
+# ---- GPU: the device path through the C-ABI ------------------------------------------------
+@pytest.mark.gpu
+def test_golden_evaluate_cases_gpu(oracle):
+    cases, pols = golden_cases()
+    nd = "\n".join(json.dumps(c["pod"]) for c in cases).encode()
+    eng = K.Engine(ordinal=0)
+    v, _, _ = eng.evaluate(K.PolicySet(pols), K.Corpus(nd))
+    ref = oracle.validate(pols, nd, nthreads=8)
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, [(cases[j // 3]["name"], i, int(v[i, j]), int(ref[i, j])) for i, j in bad[:5]]
+    assert [int(v[i, 3 * i]) for i in range(len(cases))] == [1 if c["allowed"] else 2 for c in cases]
+
+
+@pytest.mark.gpu
+def test_chainsaw_exclusions_gpu():
+    eng = K.Engine(ordinal=0)
+    for c in chainsaw_cases():
+        v, _, _ = eng.evaluate(K.PolicySet([c["policy"]]), K.Corpus(json.dumps(c["resource"]).encode()))
+        applied = [x for x in v[0] if x]
+        assert len(applied) == 1 and {1: "pass", 2: "fail"}[int(applied[0])] == c["expect"], c["file"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [11, 12])
+def test_fuzz_exclusions_gpu(oracle, seed):
+    pols, nd = fuzz_case(seed, npods=4000, nrules=32)
+    eng = K.Engine(ordinal=0)
+    v, masks, _ = eng.evaluate(K.PolicySet(pols), K.Corpus(nd), check_masks=True)
+    ref = oracle.validate(pols, nd, nthreads=8)
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, [(int(i), int(j), int(v[i, j]), int(ref[i, j])) for i, j in bad[:8]]
+    assert (masks[v != 2] == 0).all()  # masks: the checks still failing after the exclusions
