@@ -9,6 +9,18 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+def build_host_tool(target):
+    """make a scripts/ host harness under an exclusive lock: parallel test workers must not
+    run a binary another worker is relinking."""
+    import fcntl
+
+    os.makedirs(os.path.join(ROOT, "scripts", "build"), exist_ok=True)
+    with open(os.path.join(ROOT, "scripts", "build", ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), target])
+    return os.path.join(ROOT, "scripts", "build", target)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs the HIP kernels through the C-ABI)")
 

@@ -18,7 +18,9 @@ PRE_ONLY = {"pre-ns", "pre-kind-pss"}  # other handlers behind per-resource prec
 
 @pytest.fixture(scope="module")
 def condvm_bin():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), "condvm_check"])
+    from tests.conftest import build_host_tool
+
+    build_host_tool("condvm_check")
     return BIN
 
 

@@ -19,7 +19,9 @@ BIN = os.path.join(ROOT, "scripts", "build", "patvm_check")
 
 @pytest.fixture(scope="module")
 def harness():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), "patvm_check"])
+    from tests.conftest import build_host_tool
+
+    build_host_tool("patvm_check")
     return BIN
 
 

@@ -39,7 +39,9 @@ def chainsaw_cases():
 
 @pytest.fixture(scope="module")
 def pssx_bin():
-    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), "pssx_check"])
+    from tests.conftest import build_host_tool
+
+    build_host_tool("pssx_check")
     return BIN
 
 
