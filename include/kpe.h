@@ -106,6 +106,9 @@ kpe_status kpe_corpus_flatten_ex(const char* ndjson, size_t len, const char* ns_
 int64_t kpe_corpus_num_resources(const kpe_corpus* c);
 /* Host bytes of the columnar encoding (what one evaluation may read). */
 int64_t kpe_corpus_bytes(const kpe_corpus* c);
+/* 64-bit digest of every column and dictionary of the encoding (identity of two flattens of
+ * the same input, e.g. the parallel flattener against a one-thread flatten). */
+uint64_t kpe_corpus_digest(const kpe_corpus* c);
 /* Copy the columns to device memory (HBM). Evaluation requires this. */
 kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* c);
 void kpe_corpus_free(kpe_corpus* c);

@@ -15,10 +15,9 @@ struct Dict {
   std::vector<char> bytes;
   std::vector<uint32_t> off{0};
   uint32_t intern(std::string_view s) {
-    auto it = map.find(std::string(s));
-    if (it != map.end()) return it->second;
-    uint32_t id = (uint32_t)(off.size() - 1);
-    map.emplace(std::string(s), id);
+    const uint32_t id = (uint32_t)(off.size() - 1);
+    auto r = map.try_emplace(std::string(s), id);
+    if (!r.second) return r.first->second;
     bytes.insert(bytes.end(), s.begin(), s.end());
     off.push_back((uint32_t)bytes.size());
     return id;

@@ -12,6 +12,8 @@
 // The flattener only ENCODES (dictionary ids, enum codes, presence bits); every
 // predicate is evaluated on the device.
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <memory>
 #include <cstring>
 #include <stdexcept>
@@ -983,12 +985,6 @@ class Flattener {
     C.ann_off.push_back((uint32_t)C.ann_k.size());
 
     // ---- pod view ----
-    if (C.n % 64 == 0) {  // wave header: list bases of the next 64 pods
-      C.hdr.push_back((uint32_t)C.c_sc.size());
-      C.hdr.push_back((uint32_t)C.vol_src.size());
-      C.hdr.push_back((uint32_t)C.sys_id.size());
-      C.hdr.push_back((uint32_t)(C.pann_kv.size() / 2));
-    }
     size_t nctr = pod.ctr[0].size() + pod.ctr[1].size() + pod.ctr[2].size();
     if (nctr > KPE_MAX_LIST || pod.vols.size() > KPE_MAX_LIST || pod.sysctls.size() > KPE_MAX_LIST ||
         pod.ann.size() > KPE_MAX_LIST)
@@ -1316,13 +1312,12 @@ int64_t Corpus::bytes() const {
   return b;
 }
 
-// Entry used by kpe_corpus_flatten. Throws std::invalid_argument / LimitError.
-void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs) {
-  load_ns_labels(C, nsl, nsl_len);
+namespace {
+
+void flatten_range(Corpus& C, const char* buf, size_t i, size_t len, bool docs) {
   Flattener fl(C);
   std::unique_ptr<DocBuilder> db;
   if (docs) db = std::make_unique<DocBuilder>(C), C.has_docs = true;
-  size_t i = 0;
   while (i < len) {
     size_t j = i;
     while (j < len && buf[j] != '\n') ++j;
@@ -1335,11 +1330,298 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
     }
     i = j + 1;
   }
-  // sentinel wave header: list ends of the last tile (tile t's lists are [hdr[t], hdr[t+1]))
+}
+
+// wave headers (schema.h): list bases of every 64-row tile, plus the sentinel
+void rebuild_headers(Corpus& C) {
+  C.hdr.clear();
+  for (int64_t r = 0; r < C.n; r += 64) {
+    C.hdr.push_back(C.ctr_off[r]), C.hdr.push_back(C.vol_off[r]);
+    C.hdr.push_back(C.sys_off[r]), C.hdr.push_back(C.pann_off[r]);
+  }
   C.hdr.push_back((uint32_t)C.c_sc.size());
   C.hdr.push_back((uint32_t)C.vol_src.size());
   C.hdr.push_back((uint32_t)C.sys_id.size());
   C.hdr.push_back((uint32_t)(C.pann_kv.size() / 2));
+}
+
+template <class T>
+void grow(std::vector<T>& v, size_t n) {
+  v.resize(v.size() + n);
+}
+
+// Concatenate per-chunk corpora (flattened in parallel, each with its own dictionaries) into
+// C. Parts are merged in document order, so every dictionary, scalar and capability-set id
+// is the one a sequential flatten assigns (first occurrence order).
+void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthreads) {
+  const size_t T = parts.size();
+  // ---- id maps (sequential, document order) ----
+  std::vector<std::vector<std::vector<uint32_t>>> dmap(T, std::vector<std::vector<uint32_t>>(KPE_NUM_DOMAINS));
+  std::vector<std::vector<uint32_t>> capmap(T), scmap(T);
+  auto merge_scalars = [&] {  // scalar tables (document tapes), parts in document order
+    for (size_t t = 0; t < T; ++t) {
+      const Corpus& P = parts[t];
+      if (C.scal.empty()) C.scal.assign(P.scal.begin(), P.scal.begin() + 3), C.scal_text.assign(P.scal_text.begin(), P.scal_text.begin() + 9);
+      auto& sm = scmap[t];
+      sm.resize(P.scal.size());
+      for (uint32_t k = 0; k < 3 && k < P.scal.size(); ++k) sm[k] = k;  // null, false, true
+      for (size_t k = 3; k < P.scal.size(); ++k) {
+        const KpeScalar& e = P.scal[k];
+        const uint32_t ty = SC_TYPE(e.flags);
+        uint32_t* slot = nullptr;
+        if (ty == SC_T_INT) {
+          slot = &C.scal_int.emplace(e.ival, 0xFFFFFFFFu).first->second;
+        } else if (ty == SC_T_FLOAT) {
+          uint64_t bits;
+          memcpy(&bits, &e.fval, 8);
+          slot = &C.scal_float.emplace(bits, 0xFFFFFFFFu).first->second;
+        } else {
+          slot = &C.scal_str.emplace(std::string(P.scal_text.data() + e.text_off, e.text_len), 0xFFFFFFFFu).first->second;
+        }
+        if (*slot == 0xFFFFFFFFu) {
+          KpeScalar g = e;
+          const size_t nb = (size_t)e.text_len + e.sp_len;
+          if (C.scal_text.size() + nb > 0xFFFFFFFFull) throw LimitError("scalar text pool exceeds 4 GiB");
+          g.text_off = (uint32_t)C.scal_text.size();
+          C.scal_text.insert(C.scal_text.end(), P.scal_text.begin() + e.text_off, P.scal_text.begin() + e.text_off + nb);
+          *slot = (uint32_t)C.scal.size();
+          C.scal.push_back(g);
+        }
+        sm[k] = *slot;
+      }
+  
+    }
+  };
+  {  // one thread per domain and one for the scalars (all independent); parts in document order
+    std::vector<std::thread> th;
+    std::exception_ptr serr;
+    if (docs)
+      th.emplace_back([&] {
+        try {
+          merge_scalars();
+        } catch (...) {
+          serr = std::current_exception();
+        }
+      });
+    for (int d = 0; d < KPE_NUM_DOMAINS; ++d)
+      th.emplace_back([&, d] {
+        size_t tot = C.dict[d].size();
+        for (size_t t = 0; t < T; ++t) tot += parts[t].dict[d].size();
+        C.dict[d].map.reserve(tot);
+        for (size_t t = 0; t < T; ++t) {
+          const Dict& D = parts[t].dict[d];
+          auto& m = dmap[t][d];
+          m.resize(D.size());
+          for (uint32_t i = 0; i < D.size(); ++i) m[i] = C.dict[d].intern(D.at(i));
+        }
+      });
+    for (auto& x : th) x.join();
+    if (serr) std::rethrow_exception(serr);
+  }
+  if (C.dict[D_CAP].size() > 64) throw LimitError("more than 64 distinct capability names in one corpus");
+  if (C.dict[D_KIND].size() > 4096 || C.dict[D_VERSION].size() > 1024 || C.dict[D_GROUP].size() > 1024)
+    throw LimitError("too many distinct kinds/versions/groups");
+  if (docs && C.dict[D_KEY].size() >= DN_MAX_KEYS) throw LimitError("too many distinct member names");
+  auto capbits = [](uint64_t m, const std::vector<uint32_t>& cm) {
+    uint64_t o = 0;
+    for (; m; m &= m - 1) o |= 1ull << cm[__builtin_ctzll(m)];
+    return o;
+  };
+  for (size_t t = 0; t < T; ++t) {
+    const Corpus& P = parts[t];
+    for (size_t j = 0; j < P.capset_add.size(); ++j) {
+      const uint64_t ad = capbits(P.capset_add[j], dmap[t][D_CAP]), dr = capbits(P.capset_drop[j], dmap[t][D_CAP]);
+      std::string key(16, '\0');
+      memcpy(&key[0], &ad, 8);
+      memcpy(&key[8], &dr, 8);
+      auto it = C.capset_index.find(key);
+      uint32_t cs;
+      if (it == C.capset_index.end()) {
+        cs = (uint32_t)C.capset_add.size();
+        if (cs >= KPE_MAX_CAPSETS) throw LimitError("more than 2048 distinct capability (add, drop) sets");
+        C.capset_index.emplace(key, cs);
+        C.capset_add.push_back(ad), C.capset_drop.push_back(dr);
+      } else {
+        cs = it->second;
+      }
+      capmap[t].push_back(cs);
+    }
+  }
+  // ---- bases of every part in the merged columns ----
+  struct Base {
+    size_t n, lab, ann, ctr, vol, sys, pann, port, doc;
+  };
+  std::vector<Base> base(T + 1);
+  base[0] = Base{(size_t)C.n, C.lab_k.size(), C.ann_k.size(), C.c_sc.size(), C.vol_src.size(), C.sys_id.size(),
+                 C.pann_k.size(), C.cport_host.size(), C.doc.size() / 2};
+  for (size_t t = 0; t < T; ++t) {
+    const Corpus& P = parts[t];
+    base[t + 1] = Base{base[t].n + (size_t)P.n, base[t].lab + P.lab_k.size(), base[t].ann + P.ann_k.size(),
+                       base[t].ctr + P.c_sc.size(), base[t].vol + P.vol_src.size(), base[t].sys + P.sys_id.size(),
+                       base[t].pann + P.pann_k.size(), base[t].port + P.cport_host.size(),
+                       base[t].doc + P.doc.size() / 2};
+  }
+  const Base& e = base[T];
+  if (e.n >= 0x7FFFFFC0ull) throw LimitError("more than 2^31 - 64 resources in one corpus (32-bit row ids)");
+  if (e.doc > 0xFFFFFFFFull) throw LimitError("document tape exceeds 2^32 entries");
+  const size_t n0 = C.n;
+  for (auto* v : {&C.r_flags, &C.r_gvk, &C.r_name, &C.r_mns, &C.r_nsa, &C.r_nsl, &C.p_sc}) v->resize(e.n);
+  C.p_cold.resize(e.n * 4), C.rec.resize(e.n * 4);
+  for (auto* v : {&C.lab_off, &C.ann_off, &C.ctr_off, &C.vol_off, &C.sys_off, &C.pann_off}) v->resize(e.n + 1);
+  C.lab_k.resize(e.lab), C.lab_v.resize(e.lab), C.ann_k.resize(e.ann), C.ann_v.resize(e.ann);
+  C.vol_src.resize(e.vol), C.sys_id.resize(e.sys), C.pann_k.resize(e.pann), C.pann_v.resize(e.pann);
+  C.pann_kv.resize(e.pann * 2);
+  for (auto* v : {&C.c_sc, &C.c_name, &C.c_image, &C.c_sann, &C.c_sann_key, &C.c_sec_str, &C.c_pm_str, &C.c_selt_str,
+                  &C.c_selu_str, &C.c_selr_str})
+    v->resize(e.ctr);
+  C.c_add.resize(e.ctr), C.c_drop.resize(e.ctr), C.crec.resize(e.ctr * 2), C.cport_off.resize(e.ctr + 1);
+  C.cport_host.resize(e.port), C.cport_str.resize(e.port);
+  if (docs) C.doc.resize(e.doc * 2), C.doc_off.resize(e.n), C.has_docs = true;
+  // ---- remap and place every part (parallel) ----
+  auto place = [&](size_t t) {
+    const Corpus& P = parts[t];
+    const Base& b = base[t];
+    const auto& M = dmap[t];
+    auto id = [&](int d, uint32_t x) { return x == KPE_NO_STR ? x : M[d][x]; };
+    for (size_t r = 0; r < (size_t)P.n; ++r) {
+      const size_t g = b.n + r;
+      const uint32_t gv = P.r_gvk[r];
+      const uint32_t gvk = M[D_KIND][GVK_KIND(gv)] | (M[D_VERSION][GVK_VER(gv)] << 12) | (M[D_GROUP][GVK_GRP(gv)] << 22);
+      C.r_flags[g] = P.r_flags[r], C.r_gvk[g] = gvk, C.r_name[g] = id(D_NAME, P.r_name[r]);
+      C.r_mns[g] = id(D_NS, P.r_mns[r]), C.r_nsa[g] = id(D_NS, P.r_nsa[r]), C.r_nsl[g] = P.r_nsl[r];
+      C.p_sc[g] = P.p_sc[r];
+      for (int k = 0; k < 4; ++k) C.p_cold[g * 4 + k] = id(D_MISC, P.p_cold[r * 4 + k]);
+      C.rec[g * 4] = P.rec[r * 4], C.rec[g * 4 + 1] = gvk, C.rec[g * 4 + 2] = P.rec[r * 4 + 2];
+      C.rec[g * 4 + 3] = id(D_NS, P.rec[r * 4 + 3]);
+      C.lab_off[g + 1] = (uint32_t)(b.lab + P.lab_off[r + 1]), C.ann_off[g + 1] = (uint32_t)(b.ann + P.ann_off[r + 1]);
+      C.ctr_off[g + 1] = (uint32_t)(b.ctr + P.ctr_off[r + 1]), C.vol_off[g + 1] = (uint32_t)(b.vol + P.vol_off[r + 1]);
+      C.sys_off[g + 1] = (uint32_t)(b.sys + P.sys_off[r + 1]);
+      C.pann_off[g + 1] = (uint32_t)(b.pann + P.pann_off[r + 1]);
+    }
+    for (size_t k = 0; k < P.lab_k.size(); ++k)
+      C.lab_k[b.lab + k] = id(D_LABK, P.lab_k[k]), C.lab_v[b.lab + k] = id(D_LABV, P.lab_v[k]);
+    for (size_t k = 0; k < P.ann_k.size(); ++k)
+      C.ann_k[b.ann + k] = id(D_ANNK, P.ann_k[k]), C.ann_v[b.ann + k] = id(D_ANNV, P.ann_v[k]);
+    for (size_t k = 0; k < P.vol_src.size(); ++k) C.vol_src[b.vol + k] = P.vol_src[k];
+    for (size_t k = 0; k < P.sys_id.size(); ++k) C.sys_id[b.sys + k] = id(D_SYSCTL, P.sys_id[k]);
+    for (size_t k = 0; k < P.pann_k.size(); ++k) {
+      const uint32_t ak = id(D_ANNK, P.pann_k[k]), av = id(D_ANNV, P.pann_v[k]);
+      C.pann_k[b.pann + k] = ak, C.pann_v[b.pann + k] = av;
+      C.pann_kv[(b.pann + k) * 2] = ak, C.pann_kv[(b.pann + k) * 2 + 1] = av;
+    }
+    for (size_t k = 0; k < P.c_sc.size(); ++k) {
+      const size_t g = b.ctr + k;
+      C.c_sc[g] = P.c_sc[k];
+      C.c_add[g] = capbits(P.c_add[k], M[D_CAP]), C.c_drop[g] = capbits(P.c_drop[k], M[D_CAP]);
+      C.c_name[g] = id(D_CNAME, P.c_name[k]), C.c_image[g] = id(D_IMAGE, P.c_image[k]);
+      C.c_sann[g] = id(D_ANNV, P.c_sann[k]), C.c_sann_key[g] = id(D_ANNK, P.c_sann_key[k]);
+      C.c_sec_str[g] = id(D_MISC, P.c_sec_str[k]), C.c_pm_str[g] = id(D_MISC, P.c_pm_str[k]);
+      C.c_selt_str[g] = id(D_MISC, P.c_selt_str[k]), C.c_selu_str[g] = id(D_MISC, P.c_selu_str[k]);
+      C.c_selr_str[g] = id(D_MISC, P.c_selr_str[k]);
+      const uint32_t y = P.crec[k * 2 + 1];
+      C.crec[g * 2] = P.crec[k * 2], C.crec[g * 2 + 1] = capmap[t][CY_CAPSET(y)] | (y & 0xFFFF0000u);
+      C.cport_off[g + 1] = (uint32_t)(b.port + P.cport_off[k + 1]);
+    }
+    for (size_t k = 0; k < P.cport_host.size(); ++k)
+      C.cport_host[b.port + k] = P.cport_host[k], C.cport_str[b.port + k] = id(D_MISC, P.cport_str[k]);
+    if (!docs) return;
+    const auto& sm = scmap[t];
+    const uint32_t tb = (uint32_t)b.doc;
+    auto remap = [&](uint32_t x, uint32_t y, uint32_t* ox, uint32_t* oy) {
+      const uint32_t key1 = DN_KEY(x);
+      *ox = DN_KIND(x) | ((key1 ? M[D_KEY][key1 - 1] + 1u : 0u) << 2);
+      *oy = DN_KIND(x) == DN_SCALAR ? sm[y] : y + tb;
+    };
+    std::vector<uint32_t> stack;
+    for (size_t r = 0; r < (size_t)P.n; ++r) {  // walk every document from its root entry
+      const uint32_t root = (uint32_t)P.doc_off[r];
+      C.doc_off[b.n + r] = tb + root;
+      stack.assign(1, root);
+      while (!stack.empty()) {
+        const uint32_t en = stack.back();
+        stack.pop_back();
+        const uint32_t x = P.doc[en * 2], y = P.doc[en * 2 + 1];
+        remap(x, y, &C.doc[(size_t)(tb + en) * 2], &C.doc[(size_t)(tb + en) * 2 + 1]);
+        if (DN_KIND(x) != DN_SCALAR) {
+          const uint32_t cnt = P.doc[y * 2];
+          C.doc[(size_t)(tb + y) * 2] = cnt, C.doc[(size_t)(tb + y) * 2 + 1] = 0;
+          for (uint32_t q = 0; q < cnt; ++q) stack.push_back(y + 1 + q);
+        }
+      }
+    }
+  };
+  auto place_and_free = [&](size_t t) {
+    place(t);
+    parts[t] = Corpus();  // release the part's columns on this thread
+  };
+  if (T > 0) {
+    C.lab_off[n0] = (uint32_t)base[0].lab, C.ann_off[n0] = (uint32_t)base[0].ann;
+    C.ctr_off[n0] = (uint32_t)base[0].ctr, C.vol_off[n0] = (uint32_t)base[0].vol;
+    C.sys_off[n0] = (uint32_t)base[0].sys, C.pann_off[n0] = (uint32_t)base[0].pann;
+  }
+  if (base[0].ctr < C.cport_off.size()) C.cport_off[base[0].ctr] = (uint32_t)base[0].port;
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < T; ++t) {
+    if (th.size() >= nthreads) th.front().join(), th.erase(th.begin());
+    th.emplace_back(place_and_free, t);
+  }
+  for (auto& x : th) x.join();
+  C.n = (int64_t)e.n;
+}
+
+unsigned flatten_threads() {
+  if (const char* ev = getenv("KPE_FLATTEN_THREADS")) return std::max(1, std::min(64, atoi(ev)));
+  const unsigned hw = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(16u, hw ? hw : 1u));  // the GPU box's CPU share is 16
+}
+
+}  // namespace
+
+// Entry used by kpe_corpus_flatten. Throws std::invalid_argument / LimitError. Large inputs are
+// cut at line boundaries and flattened by up to flatten_threads() threads into per-chunk
+// corpora, then merged in document order (ids equal to a sequential flatten). The first error
+// in document order is the one thrown; corpus-wide limits are checked at the merge.
+void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs) {
+  load_ns_labels(C, nsl, nsl_len);
+  const unsigned T = std::min<unsigned>(flatten_threads(), (unsigned)(len / (1u << 20)));
+  if (T <= 1 || C.n != 0) {
+    flatten_range(C, buf, 0, len, docs);
+    rebuild_headers(C);
+    return;
+  }
+  std::vector<size_t> cut(T + 1, len);
+  cut[0] = 0;
+  for (unsigned t = 1; t < T; ++t) {
+    size_t p = std::max(cut[t - 1], len * t / T);
+    while (p < len && buf[p] != '\n') ++p;
+    cut[t] = p < len ? p + 1 : len;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  std::vector<Corpus> parts(T);
+  std::vector<std::exception_ptr> errs(T);
+  for (auto& P : parts) P.nsl_index = C.nsl_index;
+  {
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < T; ++t)
+      th.emplace_back([&, t] {
+        try {
+          flatten_range(parts[t], buf + cut[t], 0, cut[t + 1] - cut[t], docs);
+        } catch (...) {
+          errs[t] = std::current_exception();
+        }
+      });
+    for (auto& x : th) x.join();
+  }
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+  const auto t1 = std::chrono::steady_clock::now();
+  merge_parts(C, parts, docs, T);
+  rebuild_headers(C);
+  if (getenv("KPE_DEBUG")) {
+    const auto t2 = std::chrono::steady_clock::now();
+    fprintf(stderr, "kpe flatten: %u threads, chunks %.3f s, merge %.3f s\n", T,
+            std::chrono::duration<double>(t1 - t0).count(), std::chrono::duration<double>(t2 - t1).count());
+  }
 }
 
 bool is_limit_error(const std::exception& e) { return dynamic_cast<const LimitError*>(&e) != nullptr; }

@@ -558,7 +558,10 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
 // its resource (rule records and filter masks are wave-uniform scalar loads).
 // WIDE: terms are ballot-ed into per-wave 64-bit masks in LDS and lane j evaluates
 // rule c0 + j for all 64 resources with 64-bit mask algebra.
-template <bool PSS, bool NARROW>
+// PREP (one block per evaluation): run the block prologue once and store its LDS products
+// (predicate bitsets, truth table, capability-set bits) as ScanArgs::pimg; the scan blocks
+// of that evaluation then copy the image instead of recomputing it.
+template <bool PSS, bool NARROW, bool PREP>
 __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ __attribute__((aligned(16))) uint8_t s_capb[PSS ? KPE_MAX_CAPSETS : 4];
@@ -577,15 +580,17 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
   // unconditional, clamped (a wave without a tile re-reads the last one and never uses
   // it): the number of loads in flight is the same on every path, so waits are counted
   const uint32_t tile0 = min(tile, ntiles - 1u);
-  if (PSS) h = load_hdr(a0, tile0, lane);
+  if (PSS && !PREP) h = load_hdr(a0, tile0, lane);
   // capability sets (tiny dictionary) and the first slice of the LDS image, clamped and
   // unconditional (a zero page stands in for an absent table)
+  const bool prepped = !PREP && a0.pimg != nullptr;  // the prologue image is ready in HBM
   const uint32_t ncs = a0.ncapsets;
-  const bool capl = PSS && (a0.need & NEED_CAPS) && ncs;
+  const bool capl = PSS && !prepped && (a0.need & NEED_CAPS) && ncs;
   const uint4 cs0 = reinterpret_cast<const uint4*>(capl ? a0.capsets : a0.zero_page)[capl ? min(t, ncs - 1u) : 0u];
-  const bool fused = a0.npairs != 0;
-  const uint32_t img_n4 = (fused ? a0.fuse_words : a0.blob_words) >> 2;
-  const uint4* img = reinterpret_cast<const uint4*>(img_n4 ? (fused ? a0.fuse : a0.pbuf) : a0.zero_page);
+  const bool fused = !prepped && a0.npairs != 0;
+  const uint32_t img_n4 = (prepped ? a0.pimg_words : fused ? a0.fuse_words : a0.blob_words) >> 2;
+  const uint4* img = reinterpret_cast<const uint4*>(img_n4 ? (prepped ? a0.pimg : fused ? a0.fuse : a0.pbuf)
+                                                          : a0.zero_page);
   const uint4 img0 = img[img_n4 ? min(t, img_n4 - 1u) : 0u];
   // Program tables held in lanes for the whole kernel (read back with v_readlane:
   // no memory access inside the tile loop). WIDE single-chunk programs: lane j's
@@ -608,16 +613,41 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
     const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
     cls_cv = c.x, cls_rm = c.y;
   }
-  Tile<PSS> ta = load_tile<PSS>(a0, tile0, h, lane);
-  if (PSS) h = load_hdr(a0, min(tile + W, ntiles - 1u), lane);
+  Tile<PSS> ta{};
+  if constexpr (!PREP) {
+    ta = load_tile<PSS>(a0, tile0, h, lane);
+    if (PSS) h = load_hdr(a0, min(tile + W, ntiles - 1u), lane);
+  }
   {
     CArgs& a = a0;
+    // prepped: the prologue image, scattered to the bitsets / truth table / capability bits;
     // fused dictionary pass: the fuse image, and the local bitsets cleared; otherwise the
     // small-domain predicate bitsets (kpe_pred_kernel output)
-    uint4* d4 = reinterpret_cast<uint4*>(dyn + (fused ? a.fuse_lds : 0u));
-    if (t < img_n4) d4[t] = img0;
+    if (prepped) {
+      const uint32_t* iw = reinterpret_cast<const uint32_t*>(&img0);
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) {
+        const uint32_t i = t * 4 + k;
+        if (t < img_n4) {
+          if (i < a.blob_words) dyn[i] = iw[k];
+          else if (i >= a.pimg_tt && i < a.pimg_capb) dyn[a.tt_lds + i - a.pimg_tt] = iw[k];
+          else if (i >= a.pimg_capb) reinterpret_cast<uint32_t*>(s_capb)[i - a.pimg_capb] = iw[k];
+        }
+      }
 #pragma unroll 1
-    for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
+      for (uint32_t i = t * 4 + kBlock * 4; i < img_n4 * 4; ++i) {  // (images past 4 KiB: rare)
+        const uint32_t w = reinterpret_cast<const uint32_t*>(img)[i];
+        if (i < a.blob_words) dyn[i] = w;
+        else if (i >= a.pimg_tt && i < a.pimg_capb) dyn[a.tt_lds + i - a.pimg_tt] = w;
+        else if (i >= a.pimg_capb) reinterpret_cast<uint32_t*>(s_capb)[i - a.pimg_capb] = w;
+        if ((i & 3u) == 3u) i += (kBlock - 1) * 4;
+      }
+    } else {
+      uint4* d4 = reinterpret_cast<uint4*>(dyn + (fused ? a.fuse_lds : 0u));
+      if (t < img_n4) d4[t] = img0;
+#pragma unroll 1
+      for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
+    }
     if (fused) {
 #pragma unroll 1
       for (uint32_t i = t; i < a.blob_words; i += kBlock) dyn[i] = 0;
@@ -631,7 +661,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
     }
   }
   __syncthreads();
-  if (a0.npairs && !(KPE_DIAG & DIAG_NOPRO)) {  // one short LDS compare per (string, pattern)
+  if (fused && !(KPE_DIAG & DIAG_NOPRO)) {  // one short LDS compare per (string, pattern)
     CArgs& a = a0;
     const uint2* pairs = reinterpret_cast<const uint2*>(dyn + a.fuse_lds);
     const KpePat* pats = reinterpret_cast<const KpePat*>(dyn + a.fuse_pats);
@@ -645,7 +675,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
     }
     __syncthreads();
   }
-  if (PSS && !(KPE_DIAG & DIAG_NOPRO)) {
+  if (PSS && !prepped && !(KPE_DIAG & DIAG_NOPRO)) {
     CArgs& a = a0;
     const Bits B{dyn, a.pbuf};
     if (a.need & NEED_CAPS) {  // capability-set violation bits (add/drop masks vs the fixed allow-lists)
@@ -666,7 +696,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
 
   // NARROW truth table: tt[v] = rules whose match / exclude / namespaced-policy term
   // conditions hold for term vector v (pkg/engine/utils/match.go:168-300 over filters)
-  if (NARROW && a0.tt_lds != PRED_NONE && !(KPE_DIAG & DIAG_NOTT)) {
+  if (NARROW && !prepped && a0.tt_lds != PRED_NONE && !(KPE_DIAG & DIAG_NOTT)) {
     const uint32_t R = a0.nrules, nv = 1u << a0.nterms;
     for (uint32_t tb = t; tb < nv; tb += kBlock) {
       uint32_t mm = 0;
@@ -691,6 +721,21 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
       dyn[a0.tt_lds + tb] = mm;
     }
     __syncthreads();
+  }
+  if constexpr (PREP) {  // store the prologue's products: bitsets, truth table, capability bits
+    CArgs& a = a0;
+    const uint32_t ntt = a.pimg_capb - a.pimg_tt;
+#pragma unroll 1
+    for (uint32_t i = t; i < a.pimg_words; i += kBlock) {
+      uint32_t w = 0;
+      if (i < a.blob_words) w = dyn[i];
+      else if (i >= a.pimg_tt && i < a.pimg_capb) w = a.tt_lds != PRED_NONE ? dyn[a.tt_lds + i - a.pimg_tt] : 0u;
+      else if (i >= a.pimg_capb && (i - a.pimg_capb) * 4 < (PSS ? (uint32_t)KPE_MAX_CAPSETS : 4u))
+        w = reinterpret_cast<const uint32_t*>(s_capb)[i - a.pimg_capb];
+      a.pimg[i] = w;
+    }
+    (void)ntt;
+    return;
   }
   // NARROW verdict rows are stored one tile late (double-buffered in LDS), after the
   // next tile's loads are issued, so no wait for those loads ever covers a store.
@@ -1030,8 +1075,12 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipSt
 namespace {
 typedef void (*ScanFn)(const ScanArgs*);
 ScanFn scan_fn(int pss, int narrow) {
-  if (pss) return narrow ? kpe_scan_kernel<true, true> : kpe_scan_kernel<true, false>;
-  return narrow ? kpe_scan_kernel<false, true> : kpe_scan_kernel<false, false>;
+  if (pss) return narrow ? kpe_scan_kernel<true, true, false> : kpe_scan_kernel<true, false, false>;
+  return narrow ? kpe_scan_kernel<false, true, false> : kpe_scan_kernel<false, false, false>;
+}
+ScanFn prep_fn(int pss, int narrow) {
+  if (pss) return narrow ? kpe_scan_kernel<true, true, true> : kpe_scan_kernel<true, false, true>;
+  return narrow ? kpe_scan_kernel<false, true, true> : kpe_scan_kernel<false, false, true>;
 }
 }  // namespace
 
@@ -1057,6 +1106,11 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss,
                                       size_t dyn_bytes, hipStream_t s) {
   if (n == 0 || grid == 0) return hipSuccess;
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
+  return hipGetLastError();
+}
+// One block: the evaluation's prologue image (ScanArgs::pimg).
+extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s) {
+  hipLaunchKernelGGL(prep_fn(pss, narrow), dim3(1), dim3(kBlock), dyn_bytes, s, dargs);
   return hipGetLastError();
 }
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,

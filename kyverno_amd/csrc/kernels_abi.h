@@ -149,6 +149,11 @@ struct ScanArgs {
   uint32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   uint32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, need;
+  // Per-evaluation prologue image (kpe_scan_kernel<..., PREP = true>, one block, writes it):
+  // [0, blob_words) predicate bitsets, [pimg_tt, + 2^nterms) truth table, [pimg_capb, ...)
+  // capability-set bits (bytes). Null: every scan block computes its own prologue.
+  uint32_t* pimg;
+  uint32_t pimg_tt, pimg_capb, pimg_words, pad_pimg;
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null

@@ -29,6 +29,7 @@ bool is_limit_error(const std::exception& e);
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
 extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
@@ -154,6 +155,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   bool pargs_valid = false;
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
+  DevBuf pimg;  // per-evaluation prologue image (kpe_launch_prep)
+  uint32_t pimg_tt = 0, pimg_capb = 0, pimg_words = 0;
   DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
   bool xargs_valid = false;
   void* xmasks = nullptr;  // the masks buffer xargs points at (null: no masks)
@@ -286,6 +289,34 @@ kpe_status kpe_corpus_flatten_ex(const char* ndjson, size_t len, const char* nsl
 }
 int64_t kpe_corpus_num_resources(const kpe_corpus* c) { return c ? c->c->n : 0; }
 int64_t kpe_corpus_bytes(const kpe_corpus* c) { return c ? c->c->bytes() : 0; }
+uint64_t kpe_corpus_digest(const kpe_corpus* c) {
+  if (!c) return 0;
+  const kpe::Corpus& C = *c->c;
+  uint64_t h = 0xcbf29ce484222325ull;
+  auto mix = [&](const void* p, size_t n) {  // FNV-1a over 8-byte words, then the tail
+    const uint8_t* b = static_cast<const uint8_t*>(p);
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      uint64_t w;
+      memcpy(&w, b + i, 8);
+      h = (h ^ w) * 0x100000001b3ull;
+    }
+    for (; i < n; ++i) h = (h ^ b[i]) * 0x100000001b3ull;
+    h = (h ^ n) * 0x100000001b3ull;
+  };
+  auto v = [&](const auto& x) { mix(x.data(), x.size() * sizeof(x[0])); };
+  mix(&C.n, sizeof(C.n));
+  for (int d = 0; d < KPE_NUM_DOMAINS; ++d) v(C.dict[d].bytes), v(C.dict[d].off);
+  v(C.r_flags), v(C.r_gvk), v(C.r_name), v(C.r_mns), v(C.r_nsa), v(C.r_nsl);
+  v(C.lab_off), v(C.lab_k), v(C.lab_v), v(C.ann_off), v(C.ann_k), v(C.ann_v);
+  v(C.p_sc), v(C.p_cold), v(C.ctr_off), v(C.vol_off), v(C.vol_src), v(C.sys_off), v(C.sys_id);
+  v(C.pann_off), v(C.pann_k), v(C.pann_v), v(C.c_sc), v(C.c_add), v(C.c_drop), v(C.c_name), v(C.c_image);
+  v(C.c_sann), v(C.c_sann_key), v(C.c_sec_str), v(C.c_pm_str), v(C.c_selt_str), v(C.c_selu_str), v(C.c_selr_str);
+  v(C.cport_off), v(C.cport_host), v(C.cport_str), v(C.rec), v(C.hdr), v(C.crec), v(C.pann_kv);
+  v(C.capset_add), v(C.capset_drop), v(C.doc), v(C.doc_off), v(C.scal_text);
+  for (const KpeScalar& e : C.scal) mix(&e, sizeof(e));
+  return h;
+}
 void kpe_corpus_free(kpe_corpus* c) {
   if (!c) return;
   if (c->d) (void)hipSetDevice(c->d->ordinal);
@@ -779,6 +810,14 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
 
   B.wave_words = wave_words;
   B.dyn_bytes = (size_t)(B.wave_lds + 4 * wave_words) * 4;
+  if (!getenv("KPE_NO_PREP")) {  // prologue image: [bitsets][truth table][capability-set bits]
+    B.pimg_tt = blob;
+    B.pimg_capb = B.pimg_tt + tt_words;
+    B.pimg_words = (B.pimg_capb + (P.any_pss ? (uint32_t)(C.capset_add.size() + 3) / 4 : 0u) + 3) & ~3u;
+    HIPCHK(B.pimg.ensure((size_t)B.pimg_words * 4 + 16));
+  } else {
+    B.pimg_words = 0;
+  }
   HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
   HIPCHK(hipMemsetAsync(B.pbuf.p, 0, (size_t)go * 4 + 16, s));
   B.blob_words = blob;
@@ -843,7 +882,6 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     pa.out = B.pbuf.as<uint32_t>();
     HIPCHK(kpe_launch_pred(&pa, B.nblocks, s));
   }
-  if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   ScanArgs sa;
   memset(&sa, 0, sizeof(sa));  // padding too: compared bytewise
   sa.n = C.n;
@@ -925,6 +963,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pp_sysctl2 = B.pp[9];
   sa.cv_union = P.cv_union;
   sa.need = B.need;
+  sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
+  sa.pimg_tt = B.pimg_tt, sa.pimg_capb = B.pimg_capb, sa.pimg_words = B.pimg_words;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   if (!B.args_valid || memcmp(&sa, &B.hargs, sizeof(ScanArgs)) != 0) {  // once per binding / masks mode
@@ -934,6 +974,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(hipStreamSynchronize(s));
     B.args_valid = true;
   }
+  if (sa.pimg) HIPCHK(kpe_launch_prep(B.dargs.as<ScanArgs>(), P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.dyn_bytes, s));
+  if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));

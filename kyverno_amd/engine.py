@@ -161,6 +161,10 @@ class Corpus:
         self.nbytes = int(L.kpe_corpus_bytes(h))
         self.device = None
 
+    def digest(self) -> int:
+        """64-bit digest of the columnar encoding (kpe_corpus_digest)."""
+        return int(load().kpe_corpus_digest(self.h))
+
     def upload(self, dev: Device):
         check(load().kpe_corpus_upload(dev.h, self.h))
         self.device = dev
