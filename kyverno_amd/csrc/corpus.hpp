@@ -37,6 +37,7 @@ struct Corpus {
   Dict dict[KPE_NUM_DOMAINS];
   // ---- resource rows (unstructured view, used by match/exclude) ----
   std::vector<uint32_t> r_flags, r_gvk, r_name, r_mns, r_nsa, r_nsl;
+  std::vector<uint32_t> limit_rows;  // rows past a per-resource limit (R_LIMIT): all cells undecided
   std::vector<uint32_t> lab_off{0}, lab_k, lab_v;  // metadata.labels CSR
   std::vector<uint32_t> ann_off{0}, ann_k, ann_v;  // metadata.annotations CSR
   // ---- PSS pod view (typed decode of getSpec) ----

@@ -713,6 +713,10 @@ uint32_t sel_code(bool set, const std::string& t) {
 struct LimitError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
+struct DepthError : LimitError {  // per resource (DocBuilder)
+  using LimitError::LimitError;
+};
+struct NeedSequential {};  // a corpus-wide dictionary limit was crossed by the merge of parallel parts
 
 class Flattener {
  public:
@@ -937,15 +941,34 @@ class Flattener {
     }
   }
 
-  uint32_t capmask(const std::vector<std::string>& l) {
+  uint32_t capmask(const std::vector<std::string>& l) {  // names are interned (limits checked first)
     uint64_t m = 0;
-    for (auto& s : l) {
-      uint32_t id = C.dict[D_CAP].intern(s);
-      if (id >= 64) throw LimitError("more than 64 distinct capability names in one corpus");
-      m |= 1ull << id;
-    }
+    for (auto& s : l) m |= 1ull << C.dict[D_CAP].intern(s);
     last_mask_ = m;
     return 0;
+  }
+  // Per-resource limits of the encoding: would this pod's containers push the capability
+  // dictionary past 64 names or the capability-set dictionary past KPE_MAX_CAPSETS?
+  bool caps_over_limit() {
+    std::vector<std::string> fresh;
+    for (auto& ct : pod.ctr)
+      for (auto& c : ct)
+        for (auto* l : {&c.add, &c.drop})
+          for (auto& n : *l)
+            if (C.dict[D_CAP].find(n) < 0 && std::find(fresh.begin(), fresh.end(), n) == fresh.end()) fresh.push_back(n);
+    if (C.dict[D_CAP].size() + fresh.size() > 64) return true;
+    std::vector<std::string> keys;
+    for (auto& ct : pod.ctr)
+      for (auto& c : ct) {
+        uint64_t ad = 0, dr = 0;
+        for (auto& n : c.add) ad |= 1ull << C.dict[D_CAP].intern(n);
+        for (auto& n : c.drop) dr |= 1ull << C.dict[D_CAP].intern(n);
+        std::string key(16, '\0');
+        memcpy(&key[0], &ad, 8);
+        memcpy(&key[8], &dr, 8);
+        if (!C.capset_index.count(key) && std::find(keys.begin(), keys.end(), key) == keys.end()) keys.push_back(key);
+      }
+    return C.capset_add.size() + keys.size() > KPE_MAX_CAPSETS;
   }
   uint64_t last_mask_ = 0;
 
@@ -959,13 +982,27 @@ class Flattener {
       group = u.api_version.substr(0, sl);
       version = u.api_version.substr(sl + 1);
     }
-    uint32_t kid = C.dict[D_KIND].intern(u.kind), vid = C.dict[D_VERSION].intern(version),
-             gid = C.dict[D_GROUP].intern(group);
-    if (kid >= 4096 || vid >= 1024 || gid >= 1024) throw LimitError("too many distinct kinds/versions/groups");
+    bool limit = false;  // a per-resource limit: the row is kept, its cells are undecided
+    auto small_id = [&](int d, const std::string& v, uint32_t cap) -> uint32_t {
+      const int64_t id = C.dict[d].find(v);
+      if (id >= 0) return (uint32_t)id;
+      if (C.dict[d].size() >= cap) return limit = true, 0u;
+      return C.dict[d].intern(v);
+    };
+    const uint32_t kid = small_id(D_KIND, u.kind, 4096), vid = small_id(D_VERSION, version, 1024),
+                   gid = small_id(D_GROUP, group, 1024);
     C.r_gvk.push_back(kid | (vid << 12) | (gid << 22));
     bool is_ns = u.kind == "Namespace";
+    // ---- per-resource limits of the pod view ----
+    const size_t nctr0 = pod.ctr[0].size() + pod.ctr[1].size() + pod.ctr[2].size();
+    if (nctr0 > KPE_MAX_LIST || pod.vols.size() > KPE_MAX_LIST || pod.sysctls.size() > KPE_MAX_LIST ||
+        pod.ann.size() > KPE_MAX_LIST || caps_over_limit()) {
+      limit = true;
+      pod.reset();
+    }
     uint32_t flags = cls | (derr ? R_DECODE_ERR : 0u) | (is_ns ? R_IS_NAMESPACE : 0u) |
-                     (u.labels_ok ? 0u : R_LABELS_NIL) | (u.ann_ok ? 0u : R_ANNOT_NIL);
+                     (u.labels_ok ? 0u : R_LABELS_NIL) | (u.ann_ok ? 0u : R_ANNOT_NIL) | (limit ? R_LIMIT : 0u);
+    if (limit) C.limit_rows.push_back((uint32_t)C.n);
     C.r_flags.push_back(flags);
     C.r_name.push_back(C.dict[D_NAME].intern(u.name.empty() ? u.generate_name : u.name));
     uint32_t nsa = C.dict[D_NS].intern(u.ns);
@@ -985,10 +1022,7 @@ class Flattener {
     C.ann_off.push_back((uint32_t)C.ann_k.size());
 
     // ---- pod view ----
-    size_t nctr = pod.ctr[0].size() + pod.ctr[1].size() + pod.ctr[2].size();
-    if (nctr > KPE_MAX_LIST || pod.vols.size() > KPE_MAX_LIST || pod.sysctls.size() > KPE_MAX_LIST ||
-        pod.ann.size() > KPE_MAX_LIST)
-      throw LimitError("a pod has more than 255 containers, volumes, sysctls or annotations");
+    const size_t nctr = pod.ctr[0].size() + pod.ctr[1].size() + pod.ctr[2].size();
     uint32_t p = 0;
     if (pod.sc) p |= P_SC_PRESENT;
     if (pod.hostnet) p |= P_HOSTNET;
@@ -1052,8 +1086,7 @@ class Flattener {
           auto it = C.capset_index.find(key);
           uint32_t cs;
           if (it == C.capset_index.end()) {
-            cs = (uint32_t)C.capset_add.size();
-            if (cs >= KPE_MAX_CAPSETS) throw LimitError("more than 2048 distinct capability (add, drop) sets");
+            cs = (uint32_t)C.capset_add.size();  // < KPE_MAX_CAPSETS (caps_over_limit)
             C.capset_index.emplace(key, cs);
             C.capset_add.push_back(C.c_add.back());
             C.capset_drop.push_back(C.c_drop.back());
@@ -1123,8 +1156,18 @@ class DocBuilder {
   }
   void add(const char* b, const char* e) {
     JCur c(b, e);
-    const uint64_t root = value(c, 0, 0);
-    if (!c.ok()) throw std::invalid_argument("malformed resource JSON");
+    uint64_t root;
+    const size_t at = C.doc.size();
+    try {
+      root = value(c, 0, 0);
+      if (!c.ok()) throw std::invalid_argument("malformed resource JSON");
+    } catch (const DepthError&) {  // a per-resource limit: null document, the row's cells undecided
+      C.doc.resize(at);  // drop the bodies of the partial walk
+      root = entry(DN_SCALAR, 0, SC_NULL_ID);
+      const uint32_t row = (uint32_t)(C.n - 1);
+      C.r_flags[row] |= R_LIMIT;
+      if (C.limit_rows.empty() || C.limit_rows.back() != row) C.limit_rows.push_back(row);
+    }
     put(root);
     C.doc_off.push_back(C.doc.size() / 2 - 1);  // the resource's root entry
   }
@@ -1202,7 +1245,7 @@ class DocBuilder {
     return (uint32_t)at;
   }
   uint64_t value(JCur& c, uint32_t key1, int depth) {
-    if (depth > 256) throw LimitError("document nesting deeper than 256");
+    if (depth > 256) throw DepthError("document nesting deeper than 256");
     switch (c.peek()) {
       case JK::Null: c.null(); return entry(DN_SCALAR, key1, SC_NULL_ID);
       case JK::Bool: {
@@ -1418,9 +1461,11 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
     for (auto& x : th) x.join();
     if (serr) std::rethrow_exception(serr);
   }
-  if (C.dict[D_CAP].size() > 64) throw LimitError("more than 64 distinct capability names in one corpus");
-  if (C.dict[D_KIND].size() > 4096 || C.dict[D_VERSION].size() > 1024 || C.dict[D_GROUP].size() > 1024)
-    throw LimitError("too many distinct kinds/versions/groups");
+  // per-resource limits decided against one part's dictionaries may differ from the merged
+  // ones: such a corpus is flattened again on one thread
+  if (C.dict[D_CAP].size() > 64 || C.dict[D_KIND].size() > 4096 || C.dict[D_VERSION].size() > 1024 ||
+      C.dict[D_GROUP].size() > 1024)
+    throw NeedSequential();
   if (docs && C.dict[D_KEY].size() >= DN_MAX_KEYS) throw LimitError("too many distinct member names");
   auto capbits = [](uint64_t m, const std::vector<uint32_t>& cm) {
     uint64_t o = 0;
@@ -1438,7 +1483,7 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
       uint32_t cs;
       if (it == C.capset_index.end()) {
         cs = (uint32_t)C.capset_add.size();
-        if (cs >= KPE_MAX_CAPSETS) throw LimitError("more than 2048 distinct capability (add, drop) sets");
+        if (cs >= KPE_MAX_CAPSETS) throw NeedSequential();
         C.capset_index.emplace(key, cs);
         C.capset_add.push_back(ad), C.capset_drop.push_back(dr);
       } else {
@@ -1560,6 +1605,8 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
     C.sys_off[n0] = (uint32_t)base[0].sys, C.pann_off[n0] = (uint32_t)base[0].pann;
   }
   if (base[0].ctr < C.cport_off.size()) C.cport_off[base[0].ctr] = (uint32_t)base[0].port;
+  for (size_t t = 0; t < T; ++t)
+    for (uint32_t row : parts[t].limit_rows) C.limit_rows.push_back((uint32_t)(base[t].n + row));
   std::vector<std::thread> th;
   for (size_t t = 0; t < T; ++t) {
     if (th.size() >= nthreads) th.front().join(), th.erase(th.begin());
@@ -1615,7 +1662,14 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
   for (auto& e : errs)
     if (e) std::rethrow_exception(e);
   const auto t1 = std::chrono::steady_clock::now();
-  merge_parts(C, parts, docs, T);
+  try {
+    merge_parts(C, parts, docs, T);
+  } catch (const NeedSequential&) {
+    parts.clear();
+    C = Corpus();
+    load_ns_labels(C, nsl, nsl_len);
+    flatten_range(C, buf, 0, len, docs);
+  }
   rebuild_headers(C);
   if (getenv("KPE_DEBUG")) {
     const auto t2 = std::chrono::steady_clock::now();

@@ -1113,6 +1113,20 @@ extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow
   hipLaunchKernelGGL(prep_fn(pss, narrow), dim3(1), dim3(kBlock), dyn_bytes, s, dargs);
   return hipGetLastError();
 }
+// Rows past a per-resource encoding limit (Corpus::limit_rows): every cell undecided.
+__global__ void __launch_bounds__(256) kpe_fill_rows_kernel(uint8_t* verdicts, uint32_t R, const uint32_t* rows,
+                                                            uint32_t nrows, uint8_t value) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i < (uint64_t)nrows * R) verdicts[(size_t)rows[i / R] * R + i % R] = value;
+}
+extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
+                                           uint8_t value, hipStream_t s) {
+  const uint64_t cells = (uint64_t)nrows * R;
+  if (cells == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_fill_rows_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, verdicts, R, rows,
+                     nrows, value);
+  return hipGetLastError();
+}
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
                                        hipStream_t s) {
   if (R == 0) return hipSuccess;

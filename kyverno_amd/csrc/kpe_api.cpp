@@ -29,6 +29,8 @@ bool is_limit_error(const std::exception& e);
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
+                                           uint8_t value, hipStream_t s);
 extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
 extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
@@ -182,6 +184,7 @@ struct DeviceCorpus {
   DevBuf lab_off, lab_k, lab_v, r_nsl, nsl_off, nsl_k, nsl_v;
   DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
   DevBuf doc, doc_off, scal, scal_text;  // document tape + scalar table (pattern rules)
+  DevBuf limit_rows;                     // rows past a per-resource limit
   // cold pod columns, uploaded on the first binding of a program with podSecurity exclusions
   DevBuf ctr_off, vol_off, sys_off, pann_off, c_name, c_image, c_sann_key, c_sec_str, c_pm_str, c_selt_str, c_selu_str,
       c_selr_str, cport_off, cport_str, pann_k, pann_v, p_cold;
@@ -313,7 +316,7 @@ uint64_t kpe_corpus_digest(const kpe_corpus* c) {
   v(C.pann_off), v(C.pann_k), v(C.pann_v), v(C.c_sc), v(C.c_add), v(C.c_drop), v(C.c_name), v(C.c_image);
   v(C.c_sann), v(C.c_sann_key), v(C.c_sec_str), v(C.c_pm_str), v(C.c_selt_str), v(C.c_selu_str), v(C.c_selr_str);
   v(C.cport_off), v(C.cport_host), v(C.cport_str), v(C.rec), v(C.hdr), v(C.crec), v(C.pann_kv);
-  v(C.capset_add), v(C.capset_drop), v(C.doc), v(C.doc_off), v(C.scal_text);
+  v(C.capset_add), v(C.capset_drop), v(C.doc), v(C.doc_off), v(C.scal_text), v(C.limit_rows);
   for (const KpeScalar& e : C.scal) mix(&e, sizeof(e));
   return h;
 }
@@ -357,6 +360,7 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   HIPCHK(upload(D.sys_id, C.sys_id, s));
   HIPCHK(upload(D.pann_kv, C.pann_kv, s));
   HIPCHK(upload(D.c_sann, C.c_sann, s));
+  HIPCHK(upload(D.limit_rows, C.limit_rows, s));
   if (C.has_docs) {
     HIPCHK(upload(D.doc, C.doc, s));
     HIPCHK(upload(D.doc_off, C.doc_off, s));
@@ -1104,6 +1108,9 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       fprintf(stderr, "kpe patvm err=0x%x\n", e);
     }
   }
+  if (!C.limit_rows.empty())  // last: no later kernel may resolve these cells
+    HIPCHK(kpe_launch_fill_rows(B.verdicts.as<uint8_t>(), (uint32_t)R, D.limit_rows.as<uint32_t>(),
+                                (uint32_t)C.limit_rows.size(), KPE_UNDECIDED_, s));
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.bytes = scan_bytes(P, C, B.need, masks);

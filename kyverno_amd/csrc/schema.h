@@ -42,6 +42,8 @@ enum KpeDomain {
 #define R_IS_NAMESPACE (1u << 3)
 #define R_LABELS_NIL (1u << 4)  // unstructured NestedStringMap failed => nil map
 #define R_ANNOT_NIL (1u << 5)
+#define R_LIMIT (1u << 6)       // a per-resource encoding limit (e.g. > 255 containers): every cell of
+                                // the row is KPE_UNDECIDED_ (Corpus::limit_rows)
 
 // r_gvk = kind_id | version_id << 12 | group_id << 22
 #define GVK_KIND(x) ((x) & 0xFFFu)

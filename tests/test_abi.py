@@ -103,13 +103,13 @@ def test_flatten_rejects_malformed():
     assert e.value.status == 1
 
 
-def test_cap_dictionary_limit():
+def test_cap_dictionary_limit_is_per_row():
+    """A pod past the 64-name capability dictionary is kept (its cells come back undecided,
+    tests/test_limits.py); the batch is not refused."""
     res = [{"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "p"},
             "spec": {"containers": [{"name": "c", "image": "x",
                                      "securityContext": {"capabilities": {"add": [f"CAP{i}" for i in range(70)]}}}]}}]
-    with pytest.raises(KpeError) as e:
-        K.Corpus(res)
-    assert e.value.status == 4  # KPE_E_LIMIT
+    assert K.Corpus(res).n == 1
 
 
 def test_no_gpu_means_loud_device_error():
