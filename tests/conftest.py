@@ -17,7 +17,7 @@ def build_host_tool(target):
     os.makedirs(os.path.join(ROOT, "scripts", "build"), exist_ok=True)
     with open(os.path.join(ROOT, "scripts", "build", ".lock"), "w") as lk:
         fcntl.flock(lk, fcntl.LOCK_EX)
-        subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "scripts"), target])
+        subprocess.check_call(["make", "-s", "-j4", "-C", os.path.join(ROOT, "scripts"), target])
     return os.path.join(ROOT, "scripts", "build", target)
 
 
