@@ -258,7 +258,7 @@ struct Tile<true> {
   uint32_t C0, V0, S0, A0, nct, nvt, nst, nat;  // the tile's list ranges (wave-uniform)
   uint4 rec;
   uint2 c0, c1;   // containers C0 + lane, C0 + 64 + lane
-  uint32_t v0, s0;  // volume / sysctl V0 + lane, S0 + lane
+  uint32_t v0, v1, s0;  // volumes V0 + lane, V0 + 64 + lane; sysctl S0 + lane
   uint2 q0;       // pod annotation A0 + lane
   uint32_t sa0, sa1;  // container seccomp annotations (NEED_SANN)
   uint32_t name, mns;
@@ -285,7 +285,8 @@ __device__ __forceinline__ void pin(uint32_t& x) { asm volatile("" : "+v"(x)::"m
 __device__ __forceinline__ void pin(uint2& x) { pin(x.x), pin(x.y); }
 __device__ __forceinline__ void pin(uint4& x) { pin(x.x), pin(x.y), pin(x.z), pin(x.w); }
 __device__ __forceinline__ void pin_tile(Tile<true>& d) {
-  pin(d.rec), pin(d.c0), pin(d.c1), pin(d.v0), pin(d.s0), pin(d.q0), pin(d.sa0), pin(d.sa1), pin(d.name), pin(d.mns);
+  pin(d.rec), pin(d.c0), pin(d.c1), pin(d.v0), pin(d.v1), pin(d.s0), pin(d.q0), pin(d.sa0), pin(d.sa1), pin(d.name),
+      pin(d.mns);
 }
 __device__ __forceinline__ void pin_tile(Tile<false>& d) { pin(d.gvk), pin(d.nsa), pin(d.name), pin(d.mns); }
 
@@ -323,6 +324,7 @@ __device__ __forceinline__ Tile<true> load_tile<true>(CArgs& a, uint32_t tile, u
   d.sa0 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i0 : 0u];
   d.sa1 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i1 : 0u];
   d.v0 = col<uint32_t>(on_v, a.vol_src, zp)[on_v ? at(d.V0, d.nvt, lane, a.nvol_total) : 0u];
+  d.v1 = col<uint32_t>(on_v, a.vol_src, zp)[on_v ? at(d.V0, d.nvt, lane + 64, a.nvol_total) : 0u];
   d.s0 = col<uint32_t>(on_s, a.sys_id, zp)[on_s ? at(d.S0, d.nst, lane, a.nsys_total) : 0u];
   d.q0 = col<uint2>(on_q, a.pann_kv, zp)[on_q ? at(d.A0, d.nat, lane, a.npann_total) : 0u];
   const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
@@ -355,9 +357,27 @@ __device__ __forceinline__ Tile<false> load_tile<false>(CArgs& a, uint32_t tile,
 // lane ORs the codes of its own items [o, o + cnt). The common path issues no memory
 // operation at all (the next tile's loads stay in flight); items past the staged
 // chunk (> 128 containers or > 64 other items per tile) take a rare direct-load path.
+// Fixed PSA predicate locations of a LEAN scan, read once per kernel (all LDS-resident).
+struct LeanPP {
+  uint32_t sann_ok, aa_key, aa_ok, sp_key, sys0, sys1, sys2;
+};
+template <bool LEAN>
 __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint8_t* s_capb, const Tile<true>& d,
-                                             bool live, uint32_t* stage, uint32_t lane) {
+                                             bool live, uint32_t* stage, uint32_t lane, const LeanPP& lp) {
   const uint32_t need = a.need;
+  // LEAN: every predicate here is LDS-resident (checked by the host), no location branch
+  auto pbit = [&](uint32_t loc, uint32_t id) -> bool {
+    if constexpr (LEAN) {
+      if (id == KPE_NO_STR) return false;
+      return (B.lds[(loc & ~PRED_LOCAL) + (id >> 5)] >> (id & 31u)) & 1u;
+    } else {
+      return B.bit(loc, id);
+    }
+  };
+  const uint32_t p_sann = LEAN ? lp.sann_ok : a.pp_seccomp_ann_ok, p_s0 = LEAN ? lp.sys0 : a.pp_sysctl0,
+                 p_s1 = LEAN ? lp.sys1 : a.pp_sysctl1, p_s2 = LEAN ? lp.sys2 : a.pp_sysctl2,
+                 p_aak = LEAN ? lp.aa_key : a.pp_apparmor_key, p_aao = LEAN ? lp.aa_ok : a.pp_apparmor_ok,
+                 p_spk = LEAN ? lp.sp_key : a.pp_seccomp_pod_key;
   const uint32_t C0 = d.C0, V0 = d.V0, S0 = d.S0, A0 = d.A0;
   const uint32_t nct = d.nct, nvt = d.nvt, nst = d.nst, nat = d.nat;
   const bool nsann = need & NEED_SANN;
@@ -375,28 +395,28 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
   const uint32_t oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
   uint2* sc = reinterpret_cast<uint2*>(stage);
   uint8_t* sbv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_CTR * 2);
-  uint8_t* sbs = sbv + KPE_STAGE_SMALL;
+  uint8_t* sbs = sbv + KPE_STAGE_VOL;
   uint8_t* sba = sbs + KPE_STAGE_SMALL;
   // item codes
   auto ctr_code = [&](uint2 e, uint32_t sa) -> uint2 {  // (state bitmap, capset bits | seccomp-annotation bit)
     uint32_t ex = s_capb[CY_CAPSET(e.y)];
-    if (nsann && sa != KPE_NO_STR && !B.bit(a.pp_seccomp_ann_ok, sa)) ex |= 8u;
+    if (nsann && sa != KPE_NO_STR && !pbit(p_sann, sa)) ex |= 8u;
     return make_uint2(e.x, ex);
   };
   auto vol_code = [&](uint32_t sv) -> uint32_t {  // bit 0 hostPath, bit 1 outside the restricted allow-list
     return ((sv >> VS_HOSTPATH) & 1u) | ((sv & kAllowedVolumes) ? 0u : 2u);
   };
   auto sys_code = [&](uint32_t id) -> uint32_t {  // bit k: outside the 1.0 / 1.27 / 1.29 allow-list
-    return (B.bit(a.pp_sysctl0, id) ? 0u : 1u) | (B.bit(a.pp_sysctl1, id) ? 0u : 2u) | (B.bit(a.pp_sysctl2, id) ? 0u : 4u);
+    return (pbit(p_s0, id) ? 0u : 1u) | (pbit(p_s1, id) ? 0u : 2u) | (pbit(p_s2, id) ? 0u : 4u);
   };
   auto ann_code = [&](uint2 kv) -> uint32_t {  // bit 0 AppArmor profile, bit 1 seccomp pod annotation
-    return (B.bit(a.pp_apparmor_key, kv.x) && !B.bit(a.pp_apparmor_ok, kv.y) ? 1u : 0u) |
-           (B.bit(a.pp_seccomp_pod_key, kv.x) && !B.bit(a.pp_seccomp_ann_ok, kv.y) ? 2u : 0u);
+    return (pbit(p_aak, kv.x) && !pbit(p_aao, kv.y) ? 1u : 0u) | (pbit(p_spk, kv.x) && !pbit(p_sann, kv.y) ? 2u : 0u);
   };
   // ---- stage the first chunk of every list from the preloaded slots ----
   if (lane < nct) sc[lane] = ctr_code(d.c0, d.sa0);
   if (lane + 64 < nct) sc[lane + 64] = ctr_code(d.c1, d.sa1);
   if (nvol && lane < nvt) sbv[lane] = (uint8_t)vol_code(d.v0);
+  if (nvol && lane + 64 < nvt) sbv[lane + 64] = (uint8_t)vol_code(d.v1);
   if (nsys && lane < nst) sbs[lane] = (uint8_t)sys_code(d.s0);
   if (npann && lane < nat) sba[lane] = (uint8_t)ann_code(d.q0);
   __builtin_amdgcn_wave_barrier();
@@ -413,20 +433,20 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
       co |= e0.y | e1.y | e2.y | e3.y;
     }
   }
-  auto or_bytes = [](const uint8_t* b, uint32_t o, uint32_t cnt) -> uint32_t {
-    const uint32_t hi = min(o + cnt, (uint32_t)KPE_STAGE_SMALL);
+  auto or_bytes = [](const uint8_t* b, uint32_t o, uint32_t cnt, uint32_t cap) -> uint32_t {
+    const uint32_t hi = min(o + cnt, cap);
     uint32_t x = 0;
 #pragma unroll 1
     for (uint32_t k = o; k < hi; k += 4)
       x |= (uint32_t)b[k] | b[min(k + 1, hi - 1)] | b[min(k + 2, hi - 1)] | b[min(k + 3, hi - 1)];
     return x;
   };
-  if (nvol) vcode = or_bytes(sbv, ov, nv);
-  if (nsys) scode = or_bytes(sbs, os, ns);
-  if (npann) acode = or_bytes(sba, oa, na);
+  if (nvol) vcode = or_bytes(sbv, ov, nv, KPE_STAGE_VOL);
+  if (nsys) scode = or_bytes(sbs, os, ns, KPE_STAGE_SMALL);
+  if (npann) acode = or_bytes(sba, oa, na, KPE_STAGE_SMALL);
   __builtin_amdgcn_wave_barrier();
   // ---- rare: items beyond the staged chunk, loaded directly by their pod lane ----
-  if (nct > KPE_STAGE_CTR || (nvol && nvt > KPE_STAGE_SMALL) || (nsys && nst > KPE_STAGE_SMALL) ||
+  if (nct > KPE_STAGE_CTR || (nvol && nvt > KPE_STAGE_VOL) || (nsys && nst > KPE_STAGE_SMALL) ||
       (npann && nat > KPE_STAGE_SMALL)) {
     const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
     for (uint32_t k = max(oc, (uint32_t)KPE_STAGE_CTR); k < oc + nc; ++k) {
@@ -435,7 +455,7 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
       co |= e.y;
     }
     if (nvol)
-      for (uint32_t k = max(ov, (uint32_t)KPE_STAGE_SMALL); k < ov + nv; ++k) vcode |= vol_code(a.vol_src[V0 + k]);
+      for (uint32_t k = max(ov, (uint32_t)KPE_STAGE_VOL); k < ov + nv; ++k) vcode |= vol_code(a.vol_src[V0 + k]);
     if (nsys)
       for (uint32_t k = max(os, (uint32_t)KPE_STAGE_SMALL); k < os + ns; ++k) scode |= sys_code(a.sys_id[S0 + k]);
     if (npann)
@@ -561,7 +581,9 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
 // PREP (one block per evaluation): run the block prologue once and store its LDS products
 // (predicate bitsets, truth table, capability-set bits) as ScanArgs::pimg; the scan blocks
 // of that evaluation then copy the image instead of recomputing it.
-template <bool PSS, bool NARROW, bool PREP>
+// LEAN (PSS, NARROW, prepped, kind-only match terms, every fixed PSA predicate in LDS, no
+// check masks): the rule match is one kind-table read, the PSS predicates direct LDS reads.
+template <bool PSS, bool NARROW, bool PREP, bool LEAN = false>
 __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ __attribute__((aligned(16))) uint8_t s_capb[PSS ? KPE_MAX_CAPSETS : 4];
@@ -631,6 +653,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
         if (t < img_n4) {
           if (i < a.blob_words) dyn[i] = iw[k];
           else if (i >= a.pimg_tt && i < a.pimg_capb) dyn[a.tt_lds + i - a.pimg_tt] = iw[k];
+          else if (i >= a.pimg_kt && a.kt_lds != PRED_NONE) dyn[a.kt_lds + i - a.pimg_kt] = iw[k];
           else if (i >= a.pimg_capb) reinterpret_cast<uint32_t*>(s_capb)[i - a.pimg_capb] = iw[k];
         }
       }
@@ -639,6 +662,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
         const uint32_t w = reinterpret_cast<const uint32_t*>(img)[i];
         if (i < a.blob_words) dyn[i] = w;
         else if (i >= a.pimg_tt && i < a.pimg_capb) dyn[a.tt_lds + i - a.pimg_tt] = w;
+        else if (i >= a.pimg_kt && a.kt_lds != PRED_NONE) dyn[a.kt_lds + i - a.pimg_kt] = w;
         else if (i >= a.pimg_capb) reinterpret_cast<uint32_t*>(s_capb)[i - a.pimg_capb] = w;
         if ((i & 3u) == 3u) i += (kBlock - 1) * 4;
       }
@@ -722,20 +746,36 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
     }
     __syncthreads();
   }
-  if constexpr (PREP) {  // store the prologue's products: bitsets, truth table, capability bits
+  if constexpr (PREP) {  // store the prologue's products: bitsets, truth table, capability bits, kind table
     CArgs& a = a0;
-    const uint32_t ntt = a.pimg_capb - a.pimg_tt;
+    const Bits B{dyn, a.pbuf};
 #pragma unroll 1
     for (uint32_t i = t; i < a.pimg_words; i += kBlock) {
       uint32_t w = 0;
-      if (i < a.blob_words) w = dyn[i];
-      else if (i >= a.pimg_tt && i < a.pimg_capb) w = a.tt_lds != PRED_NONE ? dyn[a.tt_lds + i - a.pimg_tt] : 0u;
-      else if (i >= a.pimg_capb && (i - a.pimg_capb) * 4 < (PSS ? (uint32_t)KPE_MAX_CAPSETS : 4u))
+      if (i < a.blob_words) {
+        w = dyn[i];
+      } else if (i >= a.pimg_tt && i < a.pimg_capb) {
+        w = a.tt_lds != PRED_NONE ? dyn[a.tt_lds + i - a.pimg_tt] : 0u;
+      } else if (i >= a.pimg_kt && a.kt_lds != PRED_NONE) {  // kt[k]: the truth table at kind k's term vector (kind-only terms)
+        const uint32_t k = i - a.pimg_kt;
+        uint32_t tv = 0;
+        if (NARROW && k < a.nkinds)
+          for (uint32_t ti = 0; ti < a.nterms; ++ti)  // T_KIND_PRED terms (T_FALSE: never)
+            tv |= hw(tm_type, ti) == T_KIND_PRED && B.bit(hw(tm_a, ti), k) ? (1u << ti) : 0u;
+        w = k < a.nkinds && a.tt_lds != PRED_NONE ? dyn[a.tt_lds + tv] : 0u;
+      } else if (i >= a.pimg_capb && (i - a.pimg_capb) * 4 < (PSS ? (uint32_t)KPE_MAX_CAPSETS : 4u)) {
         w = reinterpret_cast<const uint32_t*>(s_capb)[i - a.pimg_capb];
+      }
       a.pimg[i] = w;
     }
-    (void)ntt;
     return;
+  }
+  LeanPP lp{};
+  uint32_t kt_lds = 0;
+  if constexpr (LEAN) {
+    lp = LeanPP{a0.pp_seccomp_ann_ok, a0.pp_apparmor_key, a0.pp_apparmor_ok, a0.pp_seccomp_pod_key,
+                a0.pp_sysctl0, a0.pp_sysctl1, a0.pp_sysctl2};
+    kt_lds = a0.kt_lds;
   }
   // NARROW verdict rows are stored one tile late (double-buffered in LDS), after the
   // next tile's loads are issued, so no wait for those loads ever covers a store.
@@ -776,9 +816,9 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
     const uint32_t need = a.need;
     if constexpr (PSS) {
       if (KPE_DIAG & DIAG_NOPSS)
-        fails = cur.rec.x ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.s0 ^ cur.q0.x ^ cur.q0.y ^ cur.C0;
+        fails = cur.rec.x ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.v1 ^ cur.s0 ^ cur.q0.x ^ cur.q0.y ^ cur.C0;
       else
-        fails = pss_tile(a, B, s_capb, cur, live, stage, lane);
+        fails = pss_tile<LEAN>(a, B, s_capb, cur, live, stage, lane, lp);
       const uint32_t cls = (cur.rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
       err = live && (cls == R_CLASS_OTHER || (cur.rec.x & PR_DECODE_ERR));
       gvk = live ? cur.rec.y : 0u;
@@ -806,13 +846,15 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
     if (NARROW) {
       // ---- terms -> bit vector ----
       uint32_t tb = 0;
+      if constexpr (!LEAN) {
 #pragma unroll 1
-      for (uint32_t ti = 0; ti < a.nterms; ++ti) {
-        const KpeTerm tm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u};
-        tb |= eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live) ? (1u << ti) : 0u;
+        for (uint32_t ti = 0; ti < a.nterms; ++ti) {
+          const KpeTerm tm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u};
+          tb |= eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live) ? (1u << ti) : 0u;
+        }
       }
-      if (a.tt_lds != PRED_NONE && !a.masks) {  // truth-table fast path
-        const uint32_t matched = live ? dyn[a.tt_lds + tb] : 0u;
+      if (LEAN || (a.tt_lds != PRED_NONE && !a.masks)) {  // truth-table fast path (LEAN: the kind table)
+        const uint32_t matched = !live ? 0u : LEAN ? dyn[kt_lds + GVK_KIND(gvk)] : dyn[a.tt_lds + tb];
         uint32_t failr = 0;
 #pragma unroll 1
         for (uint32_t c = 0; c < a.ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
@@ -1075,6 +1117,7 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipSt
 namespace {
 typedef void (*ScanFn)(const ScanArgs*);
 ScanFn scan_fn(int pss, int narrow) {
+  if (pss && narrow == 2) return kpe_scan_kernel<true, true, false, true>;
   if (pss) return narrow ? kpe_scan_kernel<true, true, false> : kpe_scan_kernel<true, false, false>;
   return narrow ? kpe_scan_kernel<false, true, false> : kpe_scan_kernel<false, false, false>;
 }

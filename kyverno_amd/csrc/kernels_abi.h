@@ -85,11 +85,12 @@ struct PredArgs {
 #define NR_NEW_POLICY (1u << 9)
 #define NR_POLTERM(x) ((x) >> 16)
 
-// Per-wave PSS list staging (LDS): 128 container entries (uint2) + 64 one-byte codes
-// each for volumes, sysctls and pod annotations.
+// Per-wave PSS list staging (LDS): 128 container entries (uint2), 128 one-byte volume codes,
+// 64 one-byte codes each for sysctls and pod annotations.
 #define KPE_STAGE_CTR 128
+#define KPE_STAGE_VOL 128  // pods average > 1 volume (C2: 1.4): two preloaded slots per lane
 #define KPE_STAGE_SMALL 64
-#define KPE_STAGE_WORDS ((KPE_STAGE_CTR * 8 + 3 * KPE_STAGE_SMALL) / 4)
+#define KPE_STAGE_WORDS ((KPE_STAGE_CTR * 8 + KPE_STAGE_VOL + 2 * KPE_STAGE_SMALL) / 4)
 
 struct ScanArgs {
   int64_t n;
@@ -153,7 +154,10 @@ struct ScanArgs {
   // [0, blob_words) predicate bitsets, [pimg_tt, + 2^nterms) truth table, [pimg_capb, ...)
   // capability-set bits (bytes). Null: every scan block computes its own prologue.
   uint32_t* pimg;
-  uint32_t pimg_tt, pimg_capb, pimg_words, pad_pimg;
+  uint32_t pimg_tt, pimg_capb, pimg_words, pimg_kt;
+  // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask, computed by the
+  // prep kernel into the image at pimg_kt and copied to LDS at kt_lds (PRED_NONE: no table)
+  uint32_t kt_lds, nkinds;
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null

@@ -158,7 +158,9 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
   DevBuf pimg;  // per-evaluation prologue image (kpe_launch_prep)
-  uint32_t pimg_tt = 0, pimg_capb = 0, pimg_words = 0;
+  uint32_t pimg_tt = 0, pimg_capb = 0, pimg_words = 0, pimg_kt = 0;
+  bool lean = false;  // LEAN scan instantiation (kind table; no check masks)
+  uint32_t kt_lds = PRED_NONE, nkinds = 0;
   DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
   bool xargs_valid = false;
   void* xmasks = nullptr;  // the masks buffer xargs points at (null: no masks)
@@ -595,9 +597,15 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
                                       : 2 * nterms + 2 * ncv + 2 * 3 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4);
   const uint32_t prog_words = 2 * (uint32_t)P.filters.size() + (uint32_t)P.fterms.size();
   const bool stage_prog = !narrow && prog_words <= kMaxProgLds;
+  // LEAN scan candidate: prepped, NARROW truth-table program of kind-only terms (a kind table
+  // replaces the per-resource term loop); confirmed below once predicate placement is known
+  bool lean = !getenv("KPE_NO_PREP") && !getenv("KPE_NO_LEAN") && narrow && PD.tt && P.any_pss &&
+              C.dict[D_KIND].size() <= 4096;
+  for (const auto& tm : P.terms) lean = lean && (tm.type == T_KIND_PRED || tm.type == T_FALSE);
+  const uint32_t kt_words = lean ? (C.dict[D_KIND].size() + 3) & ~3u : 0u;
   const int64_t budget =
       (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 -
-      (PD.tt ? (1 << KPE_TT_TERMS) : 0);
+      (PD.tt ? (1 << KPE_TT_TERMS) : 0) - kt_words;
   if (budget < 0) return fail(KPE_E_LIMIT, "program does not fit the scan kernel's LDS budget");
   const uint32_t local_budget = (uint32_t)std::min<int64_t>(kMaxLocalWords, budget);
   std::vector<uint32_t> nwords(npreds);
@@ -713,6 +721,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const int32_t fixed[10] = {ps.apparmor_key, ps.apparmor_val_ok, ps.seccomp_pod_key, ps.seccomp_ann_ok,
                              ps.caps_baseline_ok, ps.cap_nbs, ps.cap_all, ps.sysctl[0], ps.sysctl[1], ps.sysctl[2]};
   for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
+  for (int k : {0, 1, 2, 3, 7, 8, 9}) lean = lean && (B.pp[k] & PRED_LOCAL) && B.pp[k] != PRED_NONE;
+  for (const auto& tm : terms) lean = lean && (tm.type != T_KIND_PRED || ((tm.a & PRED_LOCAL) && tm.a != PRED_NONE));
   if (!P.pat.rules.empty()) {  // pattern members: names -> D_KEY ids + 1, glob names -> bitsets
     if (!C.has_docs) return fail(KPE_E_STATE, "pattern rules need a corpus flattened with KPE_CORPUS_DOCS");
     const auto& PP = P.pat;
@@ -800,8 +810,12 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const uint32_t fuse_words = fused ? (uint32_t)fimg.size() : 0u;
   const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
   const uint32_t tt_at = blob + fuse_words;
-  const uint32_t prog_at = tt_at + ((tt_words + 3) & ~3u);
+  const uint32_t kt_at = tt_at + ((tt_words + 3) & ~3u);
+  const uint32_t prog_at = kt_at + (lean ? kt_words : 0u);
   B.tt_lds = PD.tt ? tt_at : PRED_NONE;
+  B.lean = lean;
+  B.kt_lds = lean ? kt_at : PRED_NONE;
+  B.nkinds = lean ? C.dict[D_KIND].size() : 0u;
   B.fuse_lds = blob;
   B.fuse_words = fuse_words;
   B.npairs = fused ? (uint32_t)(pairs.size() / 2) : 0u;
@@ -817,7 +831,9 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   if (!getenv("KPE_NO_PREP")) {  // prologue image: [bitsets][truth table][capability-set bits]
     B.pimg_tt = blob;
     B.pimg_capb = B.pimg_tt + tt_words;
-    B.pimg_words = (B.pimg_capb + (P.any_pss ? (uint32_t)(C.capset_add.size() + 3) / 4 : 0u) + 3) & ~3u;
+    const uint32_t kt0 = B.pimg_capb + (P.any_pss ? (uint32_t)(C.capset_add.size() + 3) / 4 : 0u);
+    B.pimg_words = (kt0 + (lean ? kt_words : 0u) + 3) & ~3u;
+    B.pimg_kt = lean ? kt0 : B.pimg_words;  // no kind table: an empty range
     HIPCHK(B.pimg.ensure((size_t)B.pimg_words * 4 + 16));
   } else {
     B.pimg_words = 0;
@@ -827,7 +843,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.blob_words = blob;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, narrow ? 1 : 0, B.dyn_bytes);
+  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? 2 : narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
   HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 8, 1) * 8));
@@ -968,7 +984,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.cv_union = P.cv_union;
   sa.need = B.need;
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
-  sa.pimg_tt = B.pimg_tt, sa.pimg_capb = B.pimg_capb, sa.pimg_words = B.pimg_words;
+  sa.pimg_tt = B.pimg_tt, sa.pimg_capb = B.pimg_capb, sa.pimg_words = B.pimg_words, sa.pimg_kt = B.pimg_kt;
+  sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   if (!B.args_valid || memcmp(&sa, &B.hargs, sizeof(ScanArgs)) != 0) {  // once per binding / masks mode
@@ -979,8 +996,19 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     B.args_valid = true;
   }
   if (sa.pimg) HIPCHK(kpe_launch_prep(B.dargs.as<ScanArgs>(), P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.dyn_bytes, s));
+  if (sa.pimg && getenv("KPE_DEBUG_PIMG")) {
+    std::vector<uint32_t> img(B.pimg_words);
+    HIPCHK(hipMemcpyAsync(img.data(), B.pimg.p, img.size() * 4, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    fprintf(stderr, "pimg: words=%u blob=%u tt@%u capb@%u kt@%u kt_lds=%u tt_lds=%u nkinds=%u lean=%d nterms=%u\n",
+            B.pimg_words, B.blob_words, B.pimg_tt, B.pimg_capb, B.pimg_kt, B.kt_lds, B.tt_lds, B.nkinds, (int)B.lean,
+            (unsigned)P.terms.size());
+    for (uint32_t i = 0; i < B.pimg_words; ++i) fprintf(stderr, "%s%08x", i % 8 ? " " : "\n  ", img[i]);
+    fprintf(stderr, "\n");
+  }
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
-  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.scan_blocks,
+  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, B.lean && !masks ? 2 : PD.narrow ? 1 : 0,
+                         B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
   if (!P.cond.rules.empty()) {
