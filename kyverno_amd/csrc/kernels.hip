@@ -275,7 +275,7 @@ __device__ __forceinline__ uint32_t load_hdr(CArgs& a, uint32_t tile, uint32_t l
 }
 __device__ __forceinline__ uint32_t hw(uint32_t h, uint32_t k) { return __builtin_amdgcn_readlane(h, k); }
 
-template <bool PSS>
+template <bool PSS, bool LEAN = false>
 __device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane);
 
 // Pin a tile's registers here: code that uses them cannot be hoisted above this point
@@ -298,8 +298,10 @@ template <class T>
 __device__ __forceinline__ const T* col(bool on, const void* p, const uint32_t* zero) {
   return reinterpret_cast<const T*>(on ? p : (const void*)zero);
 }
-template <>
-__device__ __forceinline__ Tile<true> load_tile<true>(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane) {
+// PSS tile. LEAN (no container seccomp annotations, names or match namespaces read): only
+// the pod records and the list slots are loaded.
+template <bool LEAN>
+__device__ __forceinline__ Tile<true> load_pss_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane) {
   Tile<true> d;
   const uint32_t n = (uint32_t)a.n, need = a.need;
   const uint32_t r = tile * 64 + lane;
@@ -321,22 +323,29 @@ __device__ __forceinline__ Tile<true> load_tile<true>(CArgs& a, uint32_t tile, u
   d.rec = reinterpret_cast<const uint4*>(a.rec)[rc];
   d.c0 = col<uint2>(on_c, a.crec, zp)[i0];
   d.c1 = col<uint2>(on_c, a.crec, zp)[i1];
-  d.sa0 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i0 : 0u];
-  d.sa1 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i1 : 0u];
+  if constexpr (!LEAN) {
+    d.sa0 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i0 : 0u];
+    d.sa1 = col<uint32_t>(on_sa, a.c_sann, zp)[on_sa ? i1 : 0u];
+  } else {
+    d.sa0 = d.sa1 = KPE_NO_STR;
+  }
   d.v0 = col<uint32_t>(on_v, a.vol_src, zp)[on_v ? at(d.V0, d.nvt, lane, a.nvol_total) : 0u];
   d.v1 = col<uint32_t>(on_v, a.vol_src, zp)[on_v ? at(d.V0, d.nvt, lane + 64, a.nvol_total) : 0u];
   d.s0 = col<uint32_t>(on_s, a.sys_id, zp)[on_s ? at(d.S0, d.nst, lane, a.nsys_total) : 0u];
   d.q0 = col<uint2>(on_q, a.pann_kv, zp)[on_q ? at(d.A0, d.nat, lane, a.npann_total) : 0u];
-  const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
-  d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
-  d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+  if constexpr (!LEAN) {
+    const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
+    d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
+    d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+  } else {
+    d.name = d.mns = KPE_NO_STR;
+  }
   // no fix-ups of loaded values here (a select on a loaded register waits for the load):
   // columns that are off are masked where they are used (tile_cols, pss_tile's `nsann`)
   return d;
 }
 
-template <>
-__device__ __forceinline__ Tile<false> load_tile<false>(CArgs& a, uint32_t tile, uint32_t, uint32_t lane) {
+__device__ __forceinline__ Tile<false> load_match_tile(CArgs& a, uint32_t tile, uint32_t lane) {
   Tile<false> d;
   const uint32_t n = (uint32_t)a.n, need = a.need;
   const uint32_t r = tile * 64 + lane;
@@ -348,6 +357,12 @@ __device__ __forceinline__ Tile<false> load_tile<false>(CArgs& a, uint32_t tile,
   d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
   d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
   return d;
+}
+
+template <bool PSS, bool LEAN>
+__device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane) {
+  if constexpr (PSS) return load_pss_tile<LEAN>(a, tile, h, lane);
+  else return load_match_tile(a, tile, lane);
 }
 
 // PSS part of one tile: the lane's failing versioned checks (0 for dead lanes).
@@ -380,7 +395,7 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
                  p_spk = LEAN ? lp.sp_key : a.pp_seccomp_pod_key;
   const uint32_t C0 = d.C0, V0 = d.V0, S0 = d.S0, A0 = d.A0;
   const uint32_t nct = d.nct, nvt = d.nvt, nst = d.nst, nat = d.nat;
-  const bool nsann = need & NEED_SANN;
+  const bool nsann = !LEAN && (need & NEED_SANN);
   const bool nvol = (need & NEED_VOL) && nvt, nsys = (need & NEED_SYS) && nst, npann = (need & NEED_PANN) && nat;
   // ---- the pod's own item offsets: exclusive wave scans of its packed counts ----
   const uint32_t z = live ? d.rec.z : 0u;
@@ -637,7 +652,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
   }
   Tile<PSS> ta{};
   if constexpr (!PREP) {
-    ta = load_tile<PSS>(a0, tile0, h, lane);
+    ta = load_tile<PSS, LEAN>(a0, tile0, h, lane);
     if (PSS) h = load_hdr(a0, min(tile + W, ntiles - 1u), lane);
   }
   {
@@ -805,7 +820,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
                          : reinterpret_cast<uint8_t*>(rmk + 3 * KPE_RULE_CHUNK);
     // ---- prefetch the next tile into the other buffer, then evaluate `cur` ----
     // (unconditional, clamped: past the end it re-reads the last tile, never used)
-    nxt = load_tile<PSS>(a, min(tile + W, ntiles - 1), h, lane);
+    nxt = load_tile<PSS, LEAN>(a, min(tile + W, ntiles - 1), h, lane);
     if (PSS) h = load_hdr(a, min(tile + 2 * W, ntiles - 1), lane);
     pin_tile(cur);
     const uint32_t r = tile * 64 + lane;

@@ -602,6 +602,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   bool lean = !getenv("KPE_NO_PREP") && !getenv("KPE_NO_LEAN") && narrow && PD.tt && P.any_pss &&
               C.dict[D_KIND].size() <= 4096;
   for (const auto& tm : P.terms) lean = lean && (tm.type == T_KIND_PRED || tm.type == T_FALSE);
+  lean = lean && !(need_flags(P) & (NEED_SANN | NEED_NAME | NEED_MNS));  // columns a LEAN tile never loads
   const uint32_t kt_words = lean ? (C.dict[D_KIND].size() + 3) & ~3u : 0u;
   const int64_t budget =
       (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 -
