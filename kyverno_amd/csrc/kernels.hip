@@ -380,13 +380,13 @@ template <bool LEAN>
 __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint8_t* s_capb, const Tile<true>& d,
                                              bool live, uint32_t* stage, uint32_t lane, const LeanPP& lp) {
   const uint32_t need = a.need;
-  // LEAN: every predicate here is LDS-resident (checked by the host), no location branch
-  auto pbit = [&](uint32_t loc, uint32_t id) -> bool {
+  // LEAN: every predicate here is LDS-resident (checked by the host) and every id a real
+  // dictionary id (sysctl names, annotation keys / values): a branch-free bit read
+  auto pbit = [&](uint32_t loc, uint32_t id) -> uint32_t {
     if constexpr (LEAN) {
-      if (id == KPE_NO_STR) return false;
       return (B.lds[(loc & ~PRED_LOCAL) + (id >> 5)] >> (id & 31u)) & 1u;
     } else {
-      return B.bit(loc, id);
+      return B.bit(loc, id) ? 1u : 0u;
     }
   };
   const uint32_t p_sann = LEAN ? lp.sann_ok : a.pp_seccomp_ann_ok, p_s0 = LEAN ? lp.sys0 : a.pp_sysctl0,
@@ -422,10 +422,10 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
     return ((sv >> VS_HOSTPATH) & 1u) | ((sv & kAllowedVolumes) ? 0u : 2u);
   };
   auto sys_code = [&](uint32_t id) -> uint32_t {  // bit k: outside the 1.0 / 1.27 / 1.29 allow-list
-    return (pbit(p_s0, id) ? 0u : 1u) | (pbit(p_s1, id) ? 0u : 2u) | (pbit(p_s2, id) ? 0u : 4u);
+    return (pbit(p_s0, id) ^ 1u) | ((pbit(p_s1, id) ^ 1u) << 1) | ((pbit(p_s2, id) ^ 1u) << 2);
   };
   auto ann_code = [&](uint2 kv) -> uint32_t {  // bit 0 AppArmor profile, bit 1 seccomp pod annotation
-    return (pbit(p_aak, kv.x) && !pbit(p_aao, kv.y) ? 1u : 0u) | (pbit(p_spk, kv.x) && !pbit(p_sann, kv.y) ? 2u : 0u);
+    return (pbit(p_aak, kv.x) & (pbit(p_aao, kv.y) ^ 1u)) | ((pbit(p_spk, kv.x) & (pbit(p_sann, kv.y) ^ 1u)) << 1);
   };
   // ---- stage the first chunk of every list from the preloaded slots ----
   if (lane < nct) sc[lane] = ctr_code(d.c0, d.sa0);
@@ -598,8 +598,12 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
 // of that evaluation then copy the image instead of recomputing it.
 // LEAN (PSS, NARROW, prepped, kind-only match terms, every fixed PSA predicate in LDS, no
 // check masks): the rule match is one kind-table read, the PSS predicates direct LDS reads.
+#ifndef KPE_LEAN_WAVES
+#define KPE_LEAN_WAVES 5
+#endif
 template <bool PSS, bool NARROW, bool PREP, bool LEAN = false>
-__global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
+__global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES)
+    kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   __shared__ __attribute__((aligned(16))) uint8_t s_capb[PSS ? KPE_MAX_CAPSETS : 4];
 
@@ -620,7 +624,7 @@ __global__ void __launch_bounds__(kBlock, KPE_SCAN_WAVES) kpe_scan_kernel(const 
   if (PSS && !PREP) h = load_hdr(a0, tile0, lane);
   // capability sets (tiny dictionary) and the first slice of the LDS image, clamped and
   // unconditional (a zero page stands in for an absent table)
-  const bool prepped = !PREP && a0.pimg != nullptr;  // the prologue image is ready in HBM
+  const bool prepped = LEAN || (!PREP && a0.pimg != nullptr);  // the prologue image is ready in HBM
   const uint32_t ncs = a0.ncapsets;
   const bool capl = PSS && !prepped && (a0.need & NEED_CAPS) && ncs;
   const uint4 cs0 = reinterpret_cast<const uint4*>(capl ? a0.capsets : a0.zero_page)[capl ? min(t, ncs - 1u) : 0u];
