@@ -56,7 +56,7 @@ def main():
     import torch.distributed as dist
 
     import kyverno_amd as K
-    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, max_over_ranks
+    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, gather_rows, max_over_ranks
     from tests.policies import c3_policy_set, c5_policy_set, restricted_latest
 
     cfg = args.config
@@ -129,8 +129,18 @@ def main():
     elapsed = time.perf_counter() - t0
     barrier()
     elapsed = max_over_ranks(elapsed, device="cuda")
-    # the one real exchange: per-rule totals (R x 6 u64, RCCL over xGMI)
+    # the exchanges, after the timed region: per-rule totals (R x 7 u64, one RCCL all-reduce over
+    # xGMI) and the verdict rows of each rank's first shard gathered to rank 0 (grouped RCCL
+    # point-to-point: one send per rank, all receives posted together on rank 0)
     totals = allreduce_counts(totals, device="cuda")
+    v0, _, _ = eng.evaluate(ps, corpora[0])
+    barrier()
+    t1 = time.perf_counter()
+    full = gather_rows(v0, n * world, dst=0, device=torch.device("cuda", local))
+    torch.cuda.synchronize()
+    gather_s = max_over_ranks(time.perf_counter() - t1, device="cuda")
+    gather = {"rows": n * world, "bytes": n * world * R, "seconds": gather_s,
+              "rows_ok": bool(rank != 0 or (full is not None and full.shape == (n * world, R)))}
 
     # ---- per-kernel timing pass: HIP events on the library's stream, launches serialised on
     # one stream so each kernel's duration is its own (isolated, single-stream figure) ----
@@ -212,6 +222,7 @@ def main():
                        "counts_rule0": totals[0]},
             "roofline": scan_roof,
             "cpu_baseline": cpu,
+            "gather": gather,
             "e2e": {"e2e_evals_per_s": float(n) * R / e2e_s, "flatten_s": t_flatten / replicas,
                     "upload_s": t_upload / replicas, "first_eval_s": t_eval1,
                     "note": "one shard: host flatten (NDJSON -> columns) + H2D + one evaluation, not in value"},

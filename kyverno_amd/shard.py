@@ -4,12 +4,14 @@ Every (resource, rule) cell is independent given the replicated program and
 namespace-label table (MatchesResourceDescription reads only the resource, its
 namespace labels and the rule: pkg/engine/utils/match.go:168), so ranks take
 contiguous row ranges of one logical corpus and evaluate them with no data-path
-collective. The only exchange is the per-rule totals (kpe_counts, R x 6 u64)
-that `kyverno apply` prints (cmd/cli/kubectl-kyverno/processor/result.go:34-68),
-summed with one all-reduce; PolicyReports are per resource, so verdict bytes
-stay on the rank that produced them.
+collective. After the evaluation two exchanges exist: the per-rule totals
+(kpe_counts, R x 7 u64) that `kyverno apply` prints
+(cmd/cli/kubectl-kyverno/processor/result.go:34-68), summed with one all-reduce, and,
+for a caller that reports from one process (the CLI's table of results), the
+verdict rows gathered to one rank with grouped point-to-point transfers
+(gather_rows: one send per rank, all receives posted together on the root).
 """
-from typing import Dict, List, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence, Tuple
 
 COUNT_FIELDS = ("na", "pass", "fail", "warn", "error", "skip", "undecided")
 
@@ -55,3 +57,41 @@ def max_over_ranks(seconds: float, device=None) -> float:
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def gather_rows(local, total: int, dst: int = 0, device=None):
+    """Gather every rank's contiguous verdict rows (shard_range order) of an N x R uint8
+    matrix to rank `dst`: each rank posts one send, the root posts all receives in one
+    batch_isend_irecv group (RCCL point-to-point over xGMI on GPU ranks, gloo on CPU).
+    Returns the total x R matrix on `dst`, None elsewhere; the local rows when not
+    initialised or world_size == 1."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    local = np.ascontiguousarray(local, dtype=np.uint8)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return local
+    world, rank = dist.get_world_size(), dist.get_rank()
+    R = local.shape[1] if local.ndim == 2 else 0
+    first, n = shard_range(total, rank, world)
+    if local.shape[0] != n:
+        raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard has {n}")
+    ops = []
+    out: Optional["torch.Tensor"] = None
+    if rank == dst:
+        out = torch.empty((total, R), dtype=torch.uint8, device=device)
+        if n:
+            out[first:first + n] = torch.from_numpy(local).to(device)
+        for r in range(world):
+            f, m = shard_range(total, r, world)
+            if r != dst and m and R:
+                ops.append(dist.P2POp(dist.irecv, out[f:f + m], r))
+    elif n and R:
+        ops.append(dist.P2POp(dist.isend, torch.from_numpy(local).to(device), dst))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+    if rank != dst:
+        return None
+    return out.cpu().numpy()

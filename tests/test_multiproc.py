@@ -62,6 +62,11 @@ def _worker(rank, world, port, outdir):
         with open(os.path.join(outdir, "summary.json"), "w") as f:
             json.dump(summ, f)
     np.save(os.path.join(outdir, f"verdicts{rank}.npy"), v)
+    full = shard.gather_rows(v, TOTAL, dst=0)  # grouped point-to-point gather to rank 0
+    if rank == 0:
+        np.save(os.path.join(outdir, "gathered.npy"), full)
+    else:
+        assert full is None
     dist.barrier()
     dist.destroy_process_group()
 
@@ -87,13 +92,13 @@ def test_synth_shards_concatenate():
     assert a + b == full
 
 
-def test_gloo_two_ranks_counts(tmp_path):
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_ranks_counts_and_gather(tmp_path, world):
     from tests.oracle_lib import load as load_oracle
     from tests.policies import parity_policy_set
 
     import kyverno_amd as K
 
-    world = 2
     mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
                        start_method="spawn")
     got = np.load(tmp_path / "counts.npy")
@@ -104,7 +109,9 @@ def test_gloo_two_ranks_counts(tmp_path):
     # verdict rows stay on their rank; stacked in rank order they are the full matrix
     stacked = np.concatenate([np.load(tmp_path / f"verdicts{r}.npy") for r in range(world)])
     assert np.array_equal(stacked, ref_v)
-    assert float(np.load(tmp_path / "slowest.npy")[0]) == 2.0
+    # ... and the gathered matrix on rank 0 is the oracle's matrix of the whole corpus
+    assert np.array_equal(np.load(tmp_path / "gathered.npy"), ref_v)
+    assert float(np.load(tmp_path / "slowest.npy")[0]) == float(world)
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oracle"))
     import report as oracle_report
 
