@@ -7,6 +7,9 @@ are all-reduced once over RCCL after the timed region).
     x the PSS restricted:latest policy (R = 3 rules after autogen) per GPU.
 --config c3: a 1/8 shard (1.25M rows) of 10M mixed resources x 200 wildcard ClusterPolicies
     per GPU (configs[2]; the full 10M is the 8-GPU job).
+--config c4: a 1/8 shard (625k rows) of 5M Deployments + Services x the selector policy set
+    (matchLabels with wildcards, matchExpressions, namespaceSelector over a 10k-namespace
+    label table) per GPU (configs[3]).
 --config c5: 1M Pods / Deployments with 1-64 containers x the require-requests-limits /
     disallow-latest-tag / host-ports / anchor pattern set per GPU (configs[4]).
 
@@ -43,7 +46,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--config", choices=("c2", "c3", "c5"), default="c2")
+    ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2")
     ap.add_argument("--resources", type=int, default=0, help="rows per GPU (0 = the config's size)")
     ap.add_argument("--replicas", type=int, default=0, help="distinct shards rotated (0 = the config's default)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="rows in the CPU-baseline sample (0 = skip)")
@@ -57,7 +60,7 @@ def main():
 
     import kyverno_amd as K
     from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, gather_rows, max_over_ranks
-    from tests.policies import c3_policy_set, c5_policy_set, restricted_latest
+    from tests.policies import c3_policy_set, c4_policy_set, c5_policy_set, restricted_latest
 
     cfg = args.config
     if cfg == "c2":
@@ -66,6 +69,10 @@ def main():
     elif cfg == "c3":
         policies, mix, seed, n_def, rep_def, docs = c3_policy_set(), K.SYNTH_C3, 0xC3, 1_250_000, 1, True
         workload = ("C3: 1/8 shard (1.25M rows) of 10M mixed resources x 200 wildcard ClusterPolicies per GPU")
+    elif cfg == "c4":
+        policies, mix, seed, n_def, rep_def, docs = c4_policy_set(), K.SYNTH_SELECTORS, 0xC4, 625_000, 1, False
+        workload = ("C4: 1/8 shard (625k rows) of 5M Deployments + Services x selector policies "
+                    "(namespaceSelector over 10k namespaces) per GPU")
     else:
         policies, mix, seed, n_def, rep_def, docs = c5_policy_set(), K.SYNTH_FANOUT, 0xC5, 1_000_000, 1, True
         workload = "C5: 1M Pods/Deployments with 1-64 containers x requests-limits/latest-tag/host-ports/anchor patterns"
@@ -93,8 +100,9 @@ def main():
         # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus
         first = (rank * replicas + k) * n
         nd = K.synth_resources(seed, n, mix=mix, first_index=first)
+        nsl = K.synth_ns_labels(seed, 10000, mix=mix) if cfg == "c4" else None
         t0 = time.perf_counter()
-        c = K.Corpus(nd, docs=docs)
+        c = K.Corpus(nd, namespace_labels=nsl, docs=docs)
         t1 = time.perf_counter()
         del nd
         c.upload(eng.device)
@@ -170,20 +178,22 @@ def main():
             traffic = None
 
     cpu = None
-    sample = args.cpu_sample if args.cpu_sample >= 0 else {"c2": 1_000_000, "c3": 200_000, "c5": 100_000}[cfg]
+    sample = args.cpu_sample if args.cpu_sample >= 0 else {"c2": 1_000_000, "c3": 200_000, "c4": 200_000,
+                                                           "c5": 100_000}[cfg]
     if rank == 0 and world == 1 and sample > 0:
         from tests.oracle_lib import load as load_oracle
 
         orc = load_oracle()
         nd = K.synth_resources(seed, sample, mix=mix)
+        nsl_s = K.synth_ns_labels(seed, 10000, mix=mix) if cfg == "c4" else None
         thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
         t1 = time.perf_counter()
-        ref = orc.validate(policies, nd, nthreads=thr)
+        ref = orc.validate(policies, nd, ns_labels=nsl_s, nthreads=thr)
         dt = time.perf_counter() - t1
         # single-thread leg on a 1/8 sub-sample (bounded run time)
         sub = b"\n".join(nd.split(b"\n")[: max(1, sample // 8)])
         t1 = time.perf_counter()
-        ref1 = orc.validate(policies, sub, nthreads=1)
+        ref1 = orc.validate(policies, sub, ns_labels=nsl_s, nthreads=1)
         dt1 = time.perf_counter() - t1
         cpu = {"value": ref.size / dt, "unit": "resource-rule evals/s", "cores": thr, "kind": "port",
                "single_thread_value": ref1.size / dt1, "cpu_model": cpu_model(),
