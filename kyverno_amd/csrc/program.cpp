@@ -2115,6 +2115,7 @@ class Lowerer {
             }
           }
         }
+        if (P.pat.rules.size() >= 65535) throw CompileError("more than 65535 pattern rules in one program");
         P.pat.rules.push_back(pr);
         k.handler = H_PATTERN;
       } else if (v->get("foreach") && v->get("foreach")->t == JV::Arr && !v->get("foreach")->a.empty()) {
