@@ -109,6 +109,16 @@ int64_t kpe_corpus_bytes(const kpe_corpus* c);
 /* 64-bit digest of every column and dictionary of the encoding (identity of two flattens of
  * the same input, e.g. the parallel flattener against a one-thread flatten). */
 uint64_t kpe_corpus_digest(const kpe_corpus* c);
+/* Per-row status of the flatten (host only, no device call): out[i] for each of the
+ * kpe_corpus_num_resources rows. KPE_ROW_DECODE_ERROR: the typed decode of getSpec
+ * (validate_pss.go:137-188, encoding/json into corev1.Pod / appsv1.Deployment /
+ * batchv1.CronJob) would fail, so every podSecurity cell of the row is a RuleError.
+ * KPE_ROW_LIMIT: past a per-resource encoding limit, every cell is KPE_UNDECIDED.
+ * KPE_ROW_NO_SPEC: a kind getSpec does not decode ("could not find correct resource type"). */
+#define KPE_ROW_DECODE_ERROR 1u
+#define KPE_ROW_LIMIT 2u
+#define KPE_ROW_NO_SPEC 4u
+kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out);
 /* Copy the columns to device memory (HBM). Evaluation requires this. */
 kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* c);
 void kpe_corpus_free(kpe_corpus* c);

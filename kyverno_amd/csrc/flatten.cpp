@@ -24,6 +24,7 @@
 #include "corpus.hpp"
 #include "goval.hpp"
 #include "jscan.hpp"
+#include "k8s_schema.hpp"
 
 namespace kpe {
 
@@ -202,7 +203,7 @@ class Typed {
     c_.number(&n);
     int64_t x;
     if (!n.integral(&x) || x < lo || x > hi) {
-      bad();
+      err = true;  // the number is consumed already
       return false;
     }
     if (out) *out = x;
@@ -288,22 +289,94 @@ class Typed {
     c_.str(&v, vs_);
     if (!rfc3339(v)) err = true;
   }
-  void anyobj() {  // an opaque struct: must be an object (or null)
-    JK k = c_.peek();
-    if (k == JK::Null) {
+  // struct id of a k8s type (k8s_schema.hpp), looked up once per call site
+#define sid(name) ([] { static const uint16_t id_ = k8s::schema().struct_id(name); return id_; }())
+  // The value of member `key` of struct `s`: type-checked against the schema, or skipped when
+  // `key` is not a member (encoding/json ignores unknown fields).
+  void member(uint16_t s, std::string_view key) {
+    const auto& S = k8s::schema();
+    const int f = S.field(s, key);
+    if (f < 0) {
+      c_.skip();
+      return;
+    }
+    check(S.structs[s].fields[f].type);
+  }
+  // Consume one value of schema type `ty` (encoding/json Unmarshal semantics; a mismatch is
+  // sticky in `err`, decoding goes on).
+  void check(uint16_t ty) {
+    const auto& S = k8s::schema();
+    const k8s::Type T = S.types[ty];
+    const JK k = c_.peek();
+    if (k == JK::Null) {  // null leaves any field unset
       c_.null();
       return;
     }
-    if (k != JK::Obj) {
-      bad();
-      return;
+    switch (T.kind) {
+      case k8s::K_STR:
+        if (k == JK::Str) c_.skip();
+        else bad();
+        return;
+      case k8s::K_BOOL:
+        if (k == JK::Bool) c_.skip();
+        else bad();
+        return;
+      case k8s::K_I32: i32(); return;
+      case k8s::K_I64: i64(); return;
+      case k8s::K_QTY: {  // resource.Quantity.UnmarshalJSON: a number, or a ParseQuantity string
+        if (k == JK::Num) {
+          c_.skip();
+        } else if (k == JK::Str) {
+          std::string_view v;
+          c_.str(&v, vs_);
+          std::string t(v);
+          size_t a = t.find_first_not_of(" \t\n\r"), b = t.find_last_not_of(" \t\n\r");
+          goval::Quantity q;
+          if (a == std::string::npos || !goval::parse_quantity(std::string_view(t).substr(a, b - a + 1), &q))
+            err = true;
+        } else {
+          bad();
+        }
+        return;
+      }
+      case k8s::K_IOS:  // intstr.IntOrString: a string, or an int32
+        if (k == JK::Str) c_.skip();
+        else if (k == JK::Num) i32();
+        else bad();
+        return;
+      case k8s::K_TIME: timev(); return;
+      case k8s::K_RAW: c_.skip(); return;
+      case k8s::K_STRUCT: obj(T.sub, [](std::string_view) { return false; }); return;
+      case k8s::K_LIST:
+        if (k != JK::Arr) {
+          bad();
+          return;
+        }
+        {
+          c_.arr_begin();
+          bool f = true;
+          while (c_.arr_next(f)) check(T.sub);
+        }
+        return;
+      case k8s::K_MAP:
+        if (k != JK::Obj) {
+          bad();
+          return;
+        }
+        {
+          c_.obj_begin();
+          bool f = true;
+          std::string_view key;
+          while (c_.obj_next(f, &key, ks_)) check(T.sub);
+        }
+        return;
     }
-    c_.skip();
   }
 
-  // Iterate an object's keys; fn(key) must consume the value (return false => skip it).
+  // Iterate the keys of an object of struct `s`; fn(key) consumes a modelled member's value
+  // (return false: the member is type-checked against the schema instead).
   template <class F>
-  void obj(F fn) {
+  void obj(uint16_t s, F fn) {
     JK k = c_.peek();
     if (k == JK::Null) {
       c_.null();
@@ -319,7 +392,7 @@ class Typed {
     std::string kscratch;
     while (c_.obj_next(f, &key, kscratch)) {
       std::string kk(key);  // stable copy (nested parsing reuses scratch buffers)
-      if (!fn(std::string_view(kk))) c_.skip();
+      if (!fn(std::string_view(kk))) member(s, kk);
     }
   }
   template <class F>
@@ -341,7 +414,7 @@ class Typed {
 
   // ---- K8s types ----
   void object_meta(std::vector<std::pair<std::string, std::string>>* ann) {
-    obj([&](std::string_view k) {
+    obj(sid("ObjectMeta"), [&](std::string_view k) {
       if (keq(k, "name") || keq(k, "generatename") || keq(k, "namespace") || keq(k, "uid") ||
           keq(k, "resourceversion") || keq(k, "selflink"))
         str(nullptr);
@@ -360,7 +433,7 @@ class Typed {
       return;
     }
     if (c_.peek() == JK::Obj) *set = true;
-    obj([&](std::string_view k) {
+    obj(sid("SELinuxOptions"), [&](std::string_view k) {
       if (keq(k, "user")) str(user);
       else if (keq(k, "role")) str(role);
       else if (keq(k, "type")) str(type);
@@ -375,23 +448,15 @@ class Typed {
       return;
     }
     if (c_.peek() == JK::Obj) *set = true;
-    obj([&](std::string_view k) {
+    obj(sid("SeccompProfile"), [&](std::string_view k) {
       if (keq(k, "type")) str(type);
       else if (keq(k, "localhostprofile")) strp(nullptr, nullptr);
       else return false;
       return true;
     });
   }
-  void apparmor() {
-    obj([&](std::string_view k) {
-      if (keq(k, "type")) str(nullptr);
-      else if (keq(k, "localhostprofile")) strp(nullptr, nullptr);
-      else return false;
-      return true;
-    });
-  }
   void winopts(uint32_t* hp) {
-    obj([&](std::string_view k) {
+    obj(sid("WindowsSecurityContextOptions"), [&](std::string_view k) {
       if (keq(k, "hostprocess")) tri(hp);
       else if (keq(k, "gmsacredentialspecname") || keq(k, "gmsacredentialspec") || keq(k, "runasusername"))
         strp(nullptr, nullptr);
@@ -405,14 +470,14 @@ class Typed {
       return;
     }
     if (c_.peek() == JK::Obj) c.sc = true;
-    obj([&](std::string_view k) {
+    obj(sid("SecurityContext"), [&](std::string_view k) {
       if (keq(k, "capabilities")) {
         if (c_.peek() == JK::Null) {
           c_.null();
           return true;
         }
         if (c_.peek() == JK::Obj) c.caps = true;
-        obj([&](std::string_view k2) {
+        obj(sid("Capabilities"), [&](std::string_view k2) {
           if (keq(k2, "add")) strlist(&c.add);
           else if (keq(k2, "drop")) strlist(&c.drop);
           else return false;
@@ -430,7 +495,6 @@ class Typed {
       else if (keq(k, "allowprivilegeescalation")) tri(&c.ape);
       else if (keq(k, "procmount")) strp(&c.pm, &c.pm_val);
       else if (keq(k, "seccompprofile")) seccomp(&c.sec, &c.sec_type);
-      else if (keq(k, "apparmorprofile")) apparmor();
       else return false;
       return true;
     });
@@ -441,7 +505,7 @@ class Typed {
       return;
     }
     if (c_.peek() == JK::Obj) p.sc = true;
-    obj([&](std::string_view k) {
+    obj(sid("PodSecurityContext"), [&](std::string_view k) {
       if (keq(k, "selinuxoptions")) selinux(&p.sel, &p.sel_type, &p.sel_user, &p.sel_role);
       else if (keq(k, "windowsoptions")) winopts(&p.whp);
       else if (keq(k, "runasuser")) {
@@ -452,14 +516,13 @@ class Typed {
       else if (keq(k, "supplementalgroups")) i64list();
       else if (keq(k, "fsgroupchangepolicy")) strp(nullptr, nullptr);
       else if (keq(k, "seccompprofile")) seccomp(&p.sec, &p.sec_type);
-      else if (keq(k, "apparmorprofile")) apparmor();
       else if (keq(k, "sysctls")) {
         std::vector<std::string> names;
         bool notnull = arr([&]() {
           std::string nm;
           if (c_.peek() == JK::Null) c_.null();
           else
-            obj([&](std::string_view k2) {
+            obj(sid("Sysctl"), [&](std::string_view k2) {
               if (keq(k2, "name")) str(&nm);
               else if (keq(k2, "value")) str(nullptr);
               else return false;
@@ -472,12 +535,12 @@ class Typed {
       return true;
     });
   }
-  void container(CtrView& c) {
+  void container(CtrView& c, uint16_t s) {
     if (c_.peek() == JK::Null) {
       c_.null();
       return;
     }
-    obj([&](std::string_view k) {
+    obj(s, [&](std::string_view k) {
       if (keq(k, "name")) str(&c.name);
       else if (keq(k, "image")) str(&c.image);
       else if (keq(k, "command") || keq(k, "args")) strlist(nullptr);
@@ -491,7 +554,7 @@ class Typed {
           int64_t h = 0;
           if (c_.peek() == JK::Null) c_.null();
           else
-            obj([&](std::string_view k2) {
+            obj(sid("ContainerPort"), [&](std::string_view k2) {
               if (keq(k2, "hostport")) integer(INT32_MIN, INT32_MAX, &h);
               else if (keq(k2, "containerport")) i32();
               else if (keq(k2, "name") || keq(k2, "protocol") || keq(k2, "hostip")) str(nullptr);
@@ -507,35 +570,35 @@ class Typed {
             c_.null();
             return;
           }
-          obj([&](std::string_view k2) {
+          obj(sid("EnvVar"), [&](std::string_view k2) {
             if (keq(k2, "name") || keq(k2, "value")) str(nullptr);
-            else if (keq(k2, "valuefrom")) anyobj();
             else return false;
             return true;
           });
         });
-      } else if (keq(k, "resources")) anyobj();
-      else if (keq(k, "securitycontext")) security_context(c);
+      } else if (keq(k, "securitycontext")) security_context(c);
       else return false;
       return true;
     });
   }
-  void containers(std::vector<CtrView>& out) {
+  void containers(std::vector<CtrView>& out, const char* type) {
+    const uint16_t s = k8s::schema().struct_id(type);
     std::vector<CtrView> v;
     bool notnull = arr([&]() {
       CtrView c;
-      container(c);
+      container(c, s);
       v.push_back(std::move(c));
     });
     out = notnull ? std::move(v) : std::vector<CtrView>();
   }
   void volumes(std::vector<uint32_t>& out) {
     std::vector<uint32_t> v;
+    const uint16_t vsid = sid("Volume");
     bool notnull = arr([&]() {
       uint32_t src = 0;
       if (c_.peek() == JK::Null) c_.null();
       else
-        obj([&](std::string_view k) {
+        obj(vsid, [&](std::string_view k) {
           if (keq(k, "name")) {
             str(nullptr);
             return true;
@@ -553,15 +616,7 @@ class Typed {
                 return true;
               }
               src |= 1u << i;
-              obj([&](std::string_view k2) {
-                if (keq(k2, "path") || keq(k2, "secretname") || keq(k2, "claimname") || keq(k2, "medium") ||
-                    keq(k2, "server"))
-                  str(nullptr);
-                else if (keq(k2, "defaultmode")) i32();
-                else if (keq(k2, "readonly")) boolean(nullptr);
-                else return false;
-                return true;
-              });
+              member(vsid, k);  // the source struct, type-checked against the schema
               return true;
             }
           }
@@ -572,11 +627,11 @@ class Typed {
     out = notnull ? std::move(v) : std::vector<uint32_t>();
   }
   void pod_spec(PodView& p) {
-    obj([&](std::string_view k) {
+    obj(sid("PodSpec"), [&](std::string_view k) {
       if (keq(k, "volumes")) volumes(p.vols);
-      else if (keq(k, "initcontainers")) containers(p.ctr[0]);
-      else if (keq(k, "containers")) containers(p.ctr[1]);
-      else if (keq(k, "ephemeralcontainers")) containers(p.ctr[2]);
+      else if (keq(k, "initcontainers")) containers(p.ctr[0], "Container");
+      else if (keq(k, "containers")) containers(p.ctr[1], "Container");
+      else if (keq(k, "ephemeralcontainers")) containers(p.ctr[2], "EphemeralContainer");
       else if (keq(k, "hostnetwork")) boolean(&p.hostnet);
       else if (keq(k, "hostpid")) boolean(&p.hostpid);
       else if (keq(k, "hostipc")) boolean(&p.hostipc);
@@ -587,7 +642,7 @@ class Typed {
           return true;
         }
         if (c_.peek() == JK::Obj) p.os = true;
-        obj([&](std::string_view k2) {
+        obj(sid("PodOS"), [&](std::string_view k2) {
           if (keq(k2, "name")) str(&p.os_name);
           else return false;
           return true;
@@ -608,7 +663,7 @@ class Typed {
     });
   }
   void label_selector() {
-    obj([&](std::string_view k) {
+    obj(sid("LabelSelector"), [&](std::string_view k) {
       if (keq(k, "matchlabels")) strmap(nullptr);
       else if (keq(k, "matchexpressions")) {
         arr([&]() {
@@ -616,7 +671,7 @@ class Typed {
             c_.null();
             return;
           }
-          obj([&](std::string_view k2) {
+          obj(sid("LabelSelectorRequirement"), [&](std::string_view k2) {
             if (keq(k2, "key") || keq(k2, "operator")) str(nullptr);
             else if (keq(k2, "values")) strlist(nullptr);
             else return false;
@@ -629,7 +684,7 @@ class Typed {
   }
   // PodTemplateSpec; `meta_ann` receives template annotations when non-null.
   void pod_template(PodView& p, bool take_meta) {
-    obj([&](std::string_view k) {
+    obj(sid("PodTemplateSpec"), [&](std::string_view k) {
       if (keq(k, "metadata")) object_meta(take_meta ? &p.ann : nullptr);
       else if (keq(k, "spec")) pod_spec(p);
       else return false;
@@ -756,6 +811,8 @@ class Flattener {
         meta(cur, t, k == "metadata", typed, cls == R_CLASS_POD);
       } else if (keq(k, "spec") && typed) {
         spec(t, cls);
+      } else if (typed) {  // status and the rest: type-checked against the decode target
+        t.member(cls == R_CLASS_POD ? sid("Pod") : cls == R_CLASS_CONTROLLER ? sid("Deployment") : sid("CronJob"), k);
       } else {
         cur.skip();
       }
@@ -860,7 +917,7 @@ class Flattener {
       else if (keq(k, "labels")) t.strmap(nullptr);
       else if (keq(k, "annotations")) t.strmap(pod_meta ? &pod.ann : nullptr);
       else if (keq(k, "finalizers")) t.strlist(nullptr);
-      else cur.skip();
+      else t.member(sid("ObjectMeta"), k);
     }
   }
   static void upsert(std::vector<std::pair<std::string, std::string>>& v, const std::string& k,
@@ -877,7 +934,7 @@ class Flattener {
     if (cls == R_CLASS_POD) {
       t.pod_spec(pod);
     } else if (cls == R_CLASS_CONTROLLER) {
-      t.obj([&](std::string_view k) {
+      t.obj(sid("DeploymentSpec"), [&](std::string_view k) {
         if (keq(k, "replicas") || keq(k, "revisionhistorylimit") || keq(k, "progressdeadlineseconds") ||
             keq(k, "minreadyseconds"))
           t.i32();
@@ -888,18 +945,18 @@ class Flattener {
         return true;
       });
     } else {  // CronJob
-      t.obj([&](std::string_view k) {
+      t.obj(sid("CronJobSpec"), [&](std::string_view k) {
         if (keq(k, "schedule") || keq(k, "concurrencypolicy")) t.str(nullptr);
         else if (keq(k, "timezone")) t.strp(nullptr, nullptr);
         else if (keq(k, "startingdeadlineseconds")) t.i64();
         else if (keq(k, "suspend")) t.tri(nullptr);
         else if (keq(k, "successfuljobshistorylimit") || keq(k, "failedjobshistorylimit")) t.i32();
         else if (keq(k, "jobtemplate")) {
-          t.obj([&](std::string_view k3) {
+          t.obj(sid("JobTemplateSpec"), [&](std::string_view k3) {
             // validate_pss.go:165-166: metadata from spec.jobTemplate.metadata
             if (keq(k3, "metadata")) t.object_meta(&pod.ann);
             else if (keq(k3, "spec")) {
-              t.obj([&](std::string_view k4) {
+              t.obj(sid("JobSpec"), [&](std::string_view k4) {
                 if (keq(k4, "parallelism") || keq(k4, "completions") || keq(k4, "backofflimit") ||
                     keq(k4, "ttlsecondsafterfinished"))
                   t.i32();

@@ -294,6 +294,17 @@ kpe_status kpe_corpus_flatten_ex(const char* ndjson, size_t len, const char* nsl
 }
 int64_t kpe_corpus_num_resources(const kpe_corpus* c) { return c ? c->c->n : 0; }
 int64_t kpe_corpus_bytes(const kpe_corpus* c) { return c ? c->c->bytes() : 0; }
+kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out) {
+  if (!c || !out) return fail(KPE_E_INVALID, "kpe_corpus_row_flags: null argument");
+  const kpe::Corpus& C = *c->c;
+  for (int64_t i = 0; i < C.n; ++i) {
+    const uint32_t f = C.r_flags[i];
+    out[i] = ((f & R_DECODE_ERR) ? KPE_ROW_DECODE_ERROR : 0u) | ((f & R_LIMIT) ? KPE_ROW_LIMIT : 0u) |
+             ((f & R_CLASS_MASK) == R_CLASS_OTHER ? KPE_ROW_NO_SPEC : 0u);
+  }
+  return KPE_OK;
+}
+
 uint64_t kpe_corpus_digest(const kpe_corpus* c) {
   if (!c) return 0;
   const kpe::Corpus& C = *c->c;

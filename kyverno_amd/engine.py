@@ -161,6 +161,13 @@ class Corpus:
         self.nbytes = int(L.kpe_corpus_bytes(h))
         self.device = None
 
+    def row_flags(self) -> np.ndarray:
+        """Per-row flatten status (kpe_corpus_row_flags): KPE_ROW_DECODE_ERROR = 1,
+        KPE_ROW_LIMIT = 2, KPE_ROW_NO_SPEC = 4."""
+        out = np.zeros(self.n, dtype=np.uint32)
+        check(load().kpe_corpus_row_flags(self.h, out.ctypes.data))
+        return out
+
     def digest(self) -> int:
         """64-bit digest of the columnar encoding (kpe_corpus_digest)."""
         return int(load().kpe_corpus_digest(self.h))

@@ -15,9 +15,9 @@
 //     integer literal in range. The resource went through unstructured
 //     (whole -> int64, else float64) and MarshalJSON first, so a float64 that is
 //     integral and < 1e21 in magnitude is re-encoded as an integer literal.
-// Typed-schema coverage (both this oracle and the product flattener check
-// exactly these fields; deeper unmodelled fields are not type-checked — see
-// DESIGN.md "typed-decode coverage").
+// Typed-schema coverage: every member of the decode target is type-checked against
+// k8s_schema.hpp (typecheck_struct, one pass over the whole document); the dec:: walkers
+// below extract (and re-check) the fields the PSS checks read. See DESIGN.md §10.
 #pragma once
 #include <algorithm>
 #include <cctype>
@@ -26,6 +26,8 @@
 #include <vector>
 
 #include "json_dom.hpp"
+#include "k8s_schema.hpp"
+#include "pattern.hpp"
 
 namespace oracle {
 
@@ -310,15 +312,6 @@ inline void seccomp(const JVal* v, std::optional<SeccompProfile>& o, const std::
   });
   o = s;
 }
-inline void apparmor(const JVal* v, const std::string& f) {
-  if (v->is_null()) return;
-  each_key(v, f, [&](const std::string& k, const JVal* x) {
-    std::string s;
-    std::optional<std::string> lp;
-    if (k == "type") str(x, s, f);
-    else if (k == "localhostprofile") strp(x, lp, f);
-  });
-}
 inline void winopts(const JVal* v, std::optional<WindowsOptions>& o, const std::string& f) {
   if (v->is_null()) return;
   WindowsOptions w = o ? *o : WindowsOptions{};
@@ -352,7 +345,6 @@ inline void security_context(const JVal* v, std::optional<SecurityContext>& o, c
     else if (k == "allowprivilegeescalation") boolp(x, s.allowPrivilegeEscalation, f);
     else if (k == "procmount") strp(x, s.procMount, f);
     else if (k == "seccompprofile") seccomp(x, s.seccompProfile, f);
-    else if (k == "apparmorprofile") apparmor(x, f);
   });
   o = s;
 }
@@ -369,7 +361,6 @@ inline void pod_security_context(const JVal* v, std::optional<PodSecurityContext
     else if (k == "supplementalgroups") i64list(x, f);
     else if (k == "fsgroupchangepolicy") strp(x, sp, f);
     else if (k == "seccompprofile") seccomp(x, s.seccompProfile, f);
-    else if (k == "apparmorprofile") apparmor(x, f);
     else if (k == "sysctls") {
       if (x->is_null()) {
         s.sysctls.clear();
@@ -537,6 +528,92 @@ inline void pod_template(const JVal* v, Pod& p, const std::string& f) {
 
 }  // namespace dec
 
+// ---------------------------------------------------------------------------
+// encoding/json.Unmarshal type checks over the Go struct table (k8s_schema.hpp).
+namespace tc {
+
+inline const GoStruct* find_struct(const std::string& n) {
+  static const auto idx = [] {
+    std::vector<std::pair<std::string, const GoStruct*>> v;
+    for (auto& s : go_structs()) v.emplace_back(s.name, &s);
+    return v;
+  }();
+  for (auto& e : idx)
+    if (e.first == n) return e.second;
+  return nullptr;
+}
+
+inline void value(const JVal* v, const std::string& ty, const std::string& f);
+
+// a struct: keys match members exactly, else case-insensitively (encoding/json field
+// matching); unknown members are ignored.
+inline void struct_value(const JVal* v, const GoStruct* s, const std::string& f) {
+  if (v->t != JT::Obj) dec::type_err(s->name, f);
+  for (auto& kv : v->o) {
+    const char* ty = nullptr;
+    for (auto& fd : s->fields)
+      if (kv.first == fd.first) {
+        ty = fd.second;
+        break;
+      }
+    if (!ty) {
+      const std::string k = dec::fold(kv.first);
+      for (auto& fd : s->fields)
+        if (k == dec::fold(fd.first)) {
+          ty = fd.second;
+          break;
+        }
+    }
+    if (ty) value(kv.second.get(), ty, f + "." + kv.first);
+  }
+}
+
+inline void value(const JVal* v, const std::string& ty, const std::string& f) {
+  if (v->is_null()) return;  // null leaves any Go value untouched
+  int64_t x;
+  if (ty == "string") {
+    if (v->t != JT::Str) dec::type_err("string", f);
+  } else if (ty == "bool") {
+    if (v->t != JT::Bool) dec::type_err("bool", f);
+  } else if (ty == "int32") {
+    if (!dec::integral_ok(v, INT32_MIN, INT32_MAX, &x)) dec::type_err("int32", f);
+  } else if (ty == "int64") {
+    if (!dec::integral_ok(v, INT64_MIN, INT64_MAX, &x)) dec::type_err("int64", f);
+  } else if (ty == "resource.Quantity") {
+    // Quantity.UnmarshalJSON: ParseQuantity(strings.TrimSpace(...)) of the string, or of the
+    // number's literal (any JSON number re-marshalled by Go parses as a quantity)
+    if (v->t == JT::Str) {
+      const std::string& s = v->s;
+      size_t a = s.find_first_not_of(" \t\n\r"), b = s.find_last_not_of(" \t\n\r");
+      pat::Qty q;
+      if (a == std::string::npos || !pat::go_parse_quantity(s.substr(a, b - a + 1), &q))
+        dec::type_err("Quantity", f);
+    } else if (v->t != JT::Int && v->t != JT::Float) {
+      dec::type_err("Quantity", f);
+    }
+  } else if (ty == "intstr.IntOrString") {  // a string, or an int32
+    if (v->t != JT::Str && !dec::integral_ok(v, INT32_MIN, INT32_MAX, &x)) dec::type_err("IntOrString", f);
+  } else if (ty == "metav1.Time") {
+    dec::timev(v, f);
+  } else if (ty == "metav1.FieldsV1") {
+    // any JSON
+  } else if (ty.rfind("[]", 0) == 0) {
+    if (v->t != JT::Arr) dec::type_err(ty.c_str(), f);
+    const std::string el = ty.substr(2);
+    for (auto& e : v->a) value(e.get(), el, f);
+  } else if (ty.rfind("map[string]", 0) == 0) {
+    if (v->t != JT::Obj) dec::type_err(ty.c_str(), f);
+    const std::string el = ty.substr(11);
+    for (auto& kv : v->o) value(kv.second.get(), el, f);
+  } else {
+    const GoStruct* s = find_struct(ty);
+    if (!s) throw std::logic_error("k8s_schema: unknown Go type " + ty);
+    struct_value(v, s, f);
+  }
+}
+
+}  // namespace tc
+
 enum class SpecKind { Pod, Controller, CronJob, Other };
 
 inline SpecKind spec_kind(const std::string& kind) {
@@ -554,6 +631,7 @@ inline Pod get_spec(const JVal& res, const std::string& kind) {
   using namespace dec;
   SpecKind sk = spec_kind(kind);
   if (sk == SpecKind::Other) throw DecodeError{"could not find correct resource type"};
+  tc::value(&res, sk == SpecKind::Pod ? "Pod" : sk == SpecKind::Controller ? "Deployment" : "CronJob", "");
   Pod out;
   ObjectMeta topmeta;
   each_key(&res, "", [&](const std::string& k, const JVal* x) {
