@@ -605,10 +605,9 @@ template <bool PSS, bool NARROW, bool PREP, bool LEAN = false>
 __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES)
     kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-  __shared__ __attribute__((aligned(16))) uint8_t s_capb[PSS ? KPE_MAX_CAPSETS : 4];
-
   if (KPE_DIAG & DIAG_EMPTY) return;
   CArgs& a0 = *launder(ap);
+  uint8_t* const s_capb = reinterpret_cast<uint8_t*>(dyn + a0.capb_lds);  // capability-set bits
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t ntiles = a0.ntiles;
   const uint32_t W = gridDim.x * (kBlock / 64u);
@@ -661,36 +660,13 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
   }
   {
     CArgs& a = a0;
-    // prepped: the prologue image, scattered to the bitsets / truth table / capability bits;
-    // fused dictionary pass: the fuse image, and the local bitsets cleared; otherwise the
-    // small-domain predicate bitsets (kpe_pred_kernel output)
-    if (prepped) {
-      const uint32_t* iw = reinterpret_cast<const uint32_t*>(&img0);
-#pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) {
-        const uint32_t i = t * 4 + k;
-        if (t < img_n4) {
-          if (i < a.blob_words) dyn[i] = iw[k];
-          else if (i >= a.pimg_tt && i < a.pimg_capb) dyn[a.tt_lds + i - a.pimg_tt] = iw[k];
-          else if (i >= a.pimg_kt && a.kt_lds != PRED_NONE) dyn[a.kt_lds + i - a.pimg_kt] = iw[k];
-          else if (i >= a.pimg_capb) reinterpret_cast<uint32_t*>(s_capb)[i - a.pimg_capb] = iw[k];
-        }
-      }
+    // prepped: the prologue image is a copy of LDS [0, pimg_words); fused dictionary pass: the
+    // fuse image, and the local bitsets cleared; otherwise the small-domain predicate bitsets
+    // (kpe_pred_kernel output)
+    uint4* d4 = reinterpret_cast<uint4*>(dyn + (fused ? a.fuse_lds : 0u));
+    if (t < img_n4) d4[t] = img0;
 #pragma unroll 1
-      for (uint32_t i = t * 4 + kBlock * 4; i < img_n4 * 4; ++i) {  // (images past 4 KiB: rare)
-        const uint32_t w = reinterpret_cast<const uint32_t*>(img)[i];
-        if (i < a.blob_words) dyn[i] = w;
-        else if (i >= a.pimg_tt && i < a.pimg_capb) dyn[a.tt_lds + i - a.pimg_tt] = w;
-        else if (i >= a.pimg_kt && a.kt_lds != PRED_NONE) dyn[a.kt_lds + i - a.pimg_kt] = w;
-        else if (i >= a.pimg_capb) reinterpret_cast<uint32_t*>(s_capb)[i - a.pimg_capb] = w;
-        if ((i & 3u) == 3u) i += (kBlock - 1) * 4;
-      }
-    } else {
-      uint4* d4 = reinterpret_cast<uint4*>(dyn + (fused ? a.fuse_lds : 0u));
-      if (t < img_n4) d4[t] = img0;
-#pragma unroll 1
-      for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
-    }
+    for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
     if (fused) {
 #pragma unroll 1
       for (uint32_t i = t; i < a.blob_words; i += kBlock) dyn[i] = 0;
@@ -765,28 +741,22 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     }
     __syncthreads();
   }
-  if constexpr (PREP) {  // store the prologue's products: bitsets, truth table, capability bits, kind table
+  if constexpr (PREP) {  // store the prologue's products: LDS [0, pimg_words) with the kind table filled in
     CArgs& a = a0;
     const Bits B{dyn, a.pbuf};
+    if (NARROW && a.kt_lds != PRED_NONE && a.tt_lds != PRED_NONE) {
+      // kt[k]: the truth table at kind k's term vector (kind-only terms; T_FALSE: never)
 #pragma unroll 1
-    for (uint32_t i = t; i < a.pimg_words; i += kBlock) {
-      uint32_t w = 0;
-      if (i < a.blob_words) {
-        w = dyn[i];
-      } else if (i >= a.pimg_tt && i < a.pimg_capb) {
-        w = a.tt_lds != PRED_NONE ? dyn[a.tt_lds + i - a.pimg_tt] : 0u;
-      } else if (i >= a.pimg_kt && a.kt_lds != PRED_NONE) {  // kt[k]: the truth table at kind k's term vector (kind-only terms)
-        const uint32_t k = i - a.pimg_kt;
+      for (uint32_t k = t; k < a.nkinds; k += kBlock) {
         uint32_t tv = 0;
-        if (NARROW && k < a.nkinds)
-          for (uint32_t ti = 0; ti < a.nterms; ++ti)  // T_KIND_PRED terms (T_FALSE: never)
-            tv |= hw(tm_type, ti) == T_KIND_PRED && B.bit(hw(tm_a, ti), k) ? (1u << ti) : 0u;
-        w = k < a.nkinds && a.tt_lds != PRED_NONE ? dyn[a.tt_lds + tv] : 0u;
-      } else if (i >= a.pimg_capb && (i - a.pimg_capb) * 4 < (PSS ? (uint32_t)KPE_MAX_CAPSETS : 4u)) {
-        w = reinterpret_cast<const uint32_t*>(s_capb)[i - a.pimg_capb];
+        for (uint32_t ti = 0; ti < a.nterms; ++ti)
+          tv |= hw(tm_type, ti) == T_KIND_PRED && B.bit(hw(tm_a, ti), k) ? (1u << ti) : 0u;
+        dyn[a.kt_lds + k] = dyn[a.tt_lds + tv];
       }
-      a.pimg[i] = w;
+      __syncthreads();
     }
+#pragma unroll 1
+    for (uint32_t i = t; i < a.pimg_words; i += kBlock) a.pimg[i] = dyn[i];
     return;
   }
   LeanPP lp{};

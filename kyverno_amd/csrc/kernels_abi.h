@@ -150,13 +150,14 @@ struct ScanArgs {
   uint32_t pp_apparmor_key, pp_apparmor_ok, pp_seccomp_pod_key, pp_seccomp_ann_ok;
   uint32_t pp_caps_ok, pp_cap_nbs, pp_cap_all, pp_sysctl0, pp_sysctl1, pp_sysctl2;
   uint32_t cv_union, need;
-  // Per-evaluation prologue image (kpe_scan_kernel<..., PREP = true>, one block, writes it):
-  // [0, blob_words) predicate bitsets, [pimg_tt, + 2^nterms) truth table, [pimg_capb, ...)
-  // capability-set bits (bytes). Null: every scan block computes its own prologue.
+  // Prologue image (kpe_scan_kernel<..., PREP = true>, one block per binding, writes it): a
+  // copy of the scan block's LDS words [0, pimg_words) = [predicate bitsets (blob_words)]
+  // [truth table at tt_lds][kind table at kt_lds][capability-set bits (bytes) at capb_lds].
+  // Every scan block copies it into LDS with straight 16-byte loads. Null: every scan block
+  // computes its own prologue (the fuse area then sits at fuse_lds, after the wave regions).
   uint32_t* pimg;
-  uint32_t pimg_tt, pimg_capb, pimg_words, pimg_kt;
-  // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask, computed by the
-  // prep kernel into the image at pimg_kt and copied to LDS at kt_lds (PRED_NONE: no table)
+  uint32_t pimg_words, capb_lds;
+  // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask (PRED_NONE: no table)
   uint32_t kt_lds, nkinds;
   // outputs
   uint8_t* verdicts;  // n x nrules

@@ -157,8 +157,13 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   bool pargs_valid = false;
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
-  DevBuf pimg;  // per-evaluation prologue image (kpe_launch_prep)
-  uint32_t pimg_tt = 0, pimg_capb = 0, pimg_words = 0, pimg_kt = 0;
+  DevBuf pimg;  // prologue image (kpe_launch_prep)
+  // The large-domain predicate bitsets (pbuf) and the prologue image depend only on the
+  // program and the corpus dictionaries: computed by the first evaluation of a binding and
+  // kept until the binding is rebuilt (KPE_NO_BIND_CACHE=1: recomputed every evaluation).
+  bool inv_ready = false;
+  uint32_t pimg_words = 0, capb_lds = 0;
+  size_t prep_dyn_bytes = 0;  // the prep kernel's LDS: the scan layout + the fuse area
   bool lean = false;  // LEAN scan instantiation (kind table; no check masks)
   uint32_t kt_lds = PRED_NONE, nkinds = 0;
   DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
@@ -596,7 +601,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   hipStream_t s = dev->stream;
   // Predicates over small dictionaries get LDS-resident bitsets ("local": every scan
   // block copies them from pbuf's blob), the rest are read from pbuf (HBM/L2). All are
-  // evaluated per evaluation by kpe_pred_kernel (grid x = strings / 256, y = predicate).
+  // evaluated once per binding by kpe_pred_kernel (grid x = strings / 256, y = predicate).
   // pbuf: [local bitsets (blob)][large-domain bitsets].
   // Dynamic LDS per scan block: [local bitsets][filters + filter terms][4 per-wave regions].
   const uint32_t npreds = (uint32_t)P.preds.size();
@@ -615,9 +620,10 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   for (const auto& tm : P.terms) lean = lean && (tm.type == T_KIND_PRED || tm.type == T_FALSE);
   lean = lean && !(need_flags(P) & (NEED_SANN | NEED_NAME | NEED_MNS));  // columns a LEAN tile never loads
   const uint32_t kt_words = lean ? (C.dict[D_KIND].size() + 3) & ~3u : 0u;
+  const uint32_t capb_words = P.any_pss ? ((uint32_t)C.capset_add.size() + 15) / 16 * 4 : 0u;  // 1 byte per set
   const int64_t budget =
       (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 -
-      (PD.tt ? (1 << KPE_TT_TERMS) : 0) - kt_words;
+      (PD.tt ? (1 << KPE_TT_TERMS) : 0) - kt_words - capb_words;
   if (budget < 0) return fail(KPE_E_LIMIT, "program does not fit the scan kernel's LDS budget");
   const uint32_t local_budget = (uint32_t)std::min<int64_t>(kMaxLocalWords, budget);
   std::vector<uint32_t> nwords(npreds);
@@ -654,6 +660,18 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const size_t fuse_est = 2 * fuse_pairs + 4 * PD.pats_h.size() + (PD.pat_bytes_h.size() + fuse_strings) / 4 + 16;
   const bool fused = fusable && fuse_pairs <= kMaxFusePairs && fuse_est <= kMaxFuseWords &&
                      budget - (int64_t)blob - (int64_t)fuse_est >= 0;
+  // LDS layout of a scan block (words): [bitsets][truth table][kind table][capability-set bits]
+  // = the prologue image [0, img_end), then [filters + filter terms][4 wave regions]; the fuse
+  // area (fused dictionary pass: the prep kernel, or scans without an image) comes last.
+  const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
+  const uint32_t tt_at = blob;
+  const uint32_t kt_at = tt_at + ((tt_words + 3) & ~3u);
+  const uint32_t capb_at = kt_at + kt_words;
+  const uint32_t img_end = capb_at + capb_words;
+  const uint32_t prog_at = img_end;
+  const uint32_t wave_at = (prog_at + (stage_prog ? prog_words : 0) + 1) & ~1u;
+  const uint32_t scan_end = wave_at + 4 * wave_words;
+  const uint32_t fuse_at = (scan_end + 3) & ~3u;
   std::vector<uint32_t> dir(npreds);
   std::vector<PredJob> jobs;
   std::vector<uint32_t> fimg;  // fuse image (words)
@@ -693,7 +711,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     if (n) {
       const uint32_t pend = p + 1 < PD.pat0.size() ? PD.pat0[p + 1] : (uint32_t)PD.pats_h.size();
       if (fused && local[p]) {
-        const uint32_t str0 = (blob + fstr_at) * 4 + (uint32_t)dom_byte[d];  // LDS byte address
+        const uint32_t str0 = (fuse_at + fstr_at) * 4 + (uint32_t)dom_byte[d];  // LDS byte address
         for (uint32_t i = 0; i < n; ++i)
           for (uint32_t k = PD.pat0[p]; k < pend; ++k) {
             const uint32_t w = at + (i >> 5);
@@ -820,35 +838,29 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   }
   if (fused) memcpy(fimg.data(), pairs.data(), pairs.size() * 4);
   const uint32_t fuse_words = fused ? (uint32_t)fimg.size() : 0u;
-  const uint32_t tt_words = PD.tt ? (1u << P.terms.size()) : 0u;
-  const uint32_t tt_at = blob + fuse_words;
-  const uint32_t kt_at = tt_at + ((tt_words + 3) & ~3u);
-  const uint32_t prog_at = kt_at + (lean ? kt_words : 0u);
   B.tt_lds = PD.tt ? tt_at : PRED_NONE;
   B.lean = lean;
   B.kt_lds = lean ? kt_at : PRED_NONE;
   B.nkinds = lean ? C.dict[D_KIND].size() : 0u;
-  B.fuse_lds = blob;
+  B.capb_lds = capb_at;
+  B.fuse_lds = fuse_at;
   B.fuse_words = fuse_words;
   B.npairs = fused ? (uint32_t)(pairs.size() / 2) : 0u;
-  B.fuse_pats = blob + fpats_at;
-  B.fuse_patb = blob + fpatb_at;
+  B.fuse_pats = fuse_at + fpats_at;
+  B.fuse_patb = fuse_at + fpatb_at;
   if (fused) HIPCHK(upload(B.fuse, fimg, s));
   B.filt_lds = stage_prog ? prog_at : PRED_NONE;
   B.fterm_lds = prog_at + 2 * (uint32_t)P.filters.size();
-  B.wave_lds = (prog_at + (stage_prog ? prog_words : 0) + 1) & ~1u;
-
+  B.wave_lds = wave_at;
   B.wave_words = wave_words;
-  B.dyn_bytes = (size_t)(B.wave_lds + 4 * wave_words) * 4;
-  if (!getenv("KPE_NO_PREP")) {  // prologue image: [bitsets][truth table][capability-set bits]
-    B.pimg_tt = blob;
-    B.pimg_capb = B.pimg_tt + tt_words;
-    const uint32_t kt0 = B.pimg_capb + (P.any_pss ? (uint32_t)(C.capset_add.size() + 3) / 4 : 0u);
-    B.pimg_words = (kt0 + (lean ? kt_words : 0u) + 3) & ~3u;
-    B.pimg_kt = lean ? kt0 : B.pimg_words;  // no kind table: an empty range
+  B.prep_dyn_bytes = (size_t)(fuse_at + fuse_words) * 4;
+  if (!getenv("KPE_NO_PREP")) {  // prologue image: LDS [0, img_end)
+    B.pimg_words = img_end;
     HIPCHK(B.pimg.ensure((size_t)B.pimg_words * 4 + 16));
+    B.dyn_bytes = (size_t)scan_end * 4;  // scans copy the image: no fuse area
   } else {
     B.pimg_words = 0;
+    B.dyn_bytes = B.prep_dyn_bytes;
   }
   HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
   HIPCHK(hipMemsetAsync(B.pbuf.p, 0, (size_t)go * 4 + 16, s));
@@ -875,6 +887,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   HIPCHK(hipStreamSynchronize(s));
   B.need = need_flags(P);
   B.args_valid = false;
+  B.inv_ready = false;
   B.prog = &P;
   B.cells = cells;
   return KPE_OK;
@@ -899,7 +912,9 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(hipEventRecord(ev.a, s));
   }
   const size_t R = P.rules.size();
-  if (B.nblocks) {  // dictionary pass for large-domain predicates
+  static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
+  const bool fresh = !B.inv_ready || no_cache;
+  if (B.nblocks && fresh) {  // dictionary pass for large-domain predicates
     PredArgs pa{};
     for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
       pa.dict_bytes[i] = D.dict_bytes[i].as<uint8_t>();
@@ -996,7 +1011,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.cv_union = P.cv_union;
   sa.need = B.need;
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
-  sa.pimg_tt = B.pimg_tt, sa.pimg_capb = B.pimg_capb, sa.pimg_words = B.pimg_words, sa.pimg_kt = B.pimg_kt;
+  sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
@@ -1007,13 +1022,15 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(hipStreamSynchronize(s));
     B.args_valid = true;
   }
-  if (sa.pimg) HIPCHK(kpe_launch_prep(B.dargs.as<ScanArgs>(), P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.dyn_bytes, s));
+  if (sa.pimg && fresh)
+    HIPCHK(kpe_launch_prep(B.dargs.as<ScanArgs>(), P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.prep_dyn_bytes, s));
+  B.inv_ready = true;
   if (sa.pimg && getenv("KPE_DEBUG_PIMG")) {
     std::vector<uint32_t> img(B.pimg_words);
     HIPCHK(hipMemcpyAsync(img.data(), B.pimg.p, img.size() * 4, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
-    fprintf(stderr, "pimg: words=%u blob=%u tt@%u capb@%u kt@%u kt_lds=%u tt_lds=%u nkinds=%u lean=%d nterms=%u\n",
-            B.pimg_words, B.blob_words, B.pimg_tt, B.pimg_capb, B.pimg_kt, B.kt_lds, B.tt_lds, B.nkinds, (int)B.lean,
+    fprintf(stderr, "pimg: words=%u blob=%u tt_lds=%u kt_lds=%u capb_lds=%u nkinds=%u lean=%d nterms=%u\n",
+            B.pimg_words, B.blob_words, B.tt_lds, B.kt_lds, B.capb_lds, B.nkinds, (int)B.lean,
             (unsigned)P.terms.size());
     for (uint32_t i = 0; i < B.pimg_words; ++i) fprintf(stderr, "%s%08x", i % 8 ? " " : "\n  ", img[i]);
     fprintf(stderr, "\n");
