@@ -178,6 +178,14 @@ kpe_status kpe_cli_summary(const kpe_program* prog, const kpe_counts* counts, in
  * buffer when it is >= cap), or a negative kpe_status. Host only; no device call. */
 long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row, char* buf,
                         size_t cap);
+/* kpe_report_results with the RuleResponse `message` of each result, rendered from the
+ * resource's JSON (the EngineResponse resource, resource_len bytes): podSecurity pass
+ * ("Validation rule '<rule>' passed.", validate_pss.go:85) and fail (validate_pss.go:108:
+ * FormatChecksPrint of the failing checks after convertChecks, rules without
+ * podSecurity.exclude) and validate.pattern pass ("validation rule '<rule>' passed.",
+ * validate_resource.go:339). Other results carry no message. Host only. */
+long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
+                            const char* resource_json, size_t resource_len, char* buf, size_t cap);
 
 /* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
 typedef struct kpe_kernel_stats {

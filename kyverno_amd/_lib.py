@@ -74,6 +74,8 @@ def load():
     L.kpe_pss_cv_check.argtypes = [i32]
     L.kpe_report_results.argtypes = [vp, vp, vp, ctypes.c_char_p, sz]
     L.kpe_report_results.restype = ctypes.c_long
+    L.kpe_report_results_msg.argtypes = [vp, vp, vp, ctypes.c_char_p, sz, ctypes.c_char_p, sz]
+    L.kpe_report_results_msg.restype = ctypes.c_long
     L.kpe_cli_summary.argtypes = [vp, ctypes.POINTER(Counts), i32, ctypes.POINTER(CliTotals)]
     L.kpe_device_set_timing.argtypes = [vp, i32]
     L.kpe_device_kernel_stats.argtypes = [vp, vp, vp, ctypes.POINTER(KernelStats), i32]

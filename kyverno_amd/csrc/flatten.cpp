@@ -25,6 +25,7 @@
 #include "goval.hpp"
 #include "jscan.hpp"
 #include "k8s_schema.hpp"
+#include "podview.hpp"
 
 namespace kpe {
 
@@ -54,53 +55,6 @@ uint32_t state_bitmap(uint32_t w) {
   if (w & C_SC_PRESENT) x |= CX_SC;
   return x;
 }
-
-struct CtrView {
-  std::string name, image;
-  bool sc = false;
-  uint32_t priv = TRI_UNSET, ape = TRI_UNSET, rnr = TRI_UNSET, rau = RAU_UNSET, whp = TRI_UNSET;
-  bool caps = false;
-  std::vector<std::string> add, drop;
-  bool sec = false;
-  std::string sec_type;
-  bool pm = false;
-  std::string pm_val;
-  bool sel = false;
-  std::string sel_type, sel_user, sel_role;
-  std::vector<int32_t> hostports;
-  void reset() { *this = CtrView(); }
-};
-
-struct PodView {
-  bool hostnet = false, hostpid = false, hostipc = false;
-  bool sc = false;
-  uint32_t rnr = TRI_UNSET, rau = RAU_UNSET, whp = TRI_UNSET;
-  bool sec = false;
-  std::string sec_type;
-  bool sel = false;
-  std::string sel_type, sel_user, sel_role;
-  bool os = false;
-  std::string os_name;
-  std::vector<std::string> sysctls;
-  std::vector<uint32_t> vols;
-  std::vector<CtrView> ctr[3];  // init, containers, ephemeral
-  std::vector<std::pair<std::string, std::string>> ann;  // typed metadata annotations (map: unique keys)
-  void reset() {
-    hostnet = hostpid = hostipc = sc = sec = sel = os = false;
-    rnr = TRI_UNSET;
-    rau = RAU_UNSET;
-    whp = TRI_UNSET;
-    sec_type.clear();
-    sel_type.clear();
-    sel_user.clear();
-    sel_role.clear();
-    os_name.clear();
-    sysctls.clear();
-    vols.clear();
-    for (auto& c : ctr) c.clear();
-    ann.clear();
-  }
-};
 
 struct UView {  // unstructured metadata view
   std::string kind, api_version, name, generate_name, ns;
@@ -776,6 +730,10 @@ struct NeedSequential {};  // a corpus-wide dictionary limit was crossed by the 
 class Flattener {
  public:
   explicit Flattener(Corpus& c) : C(c) {}
+  // typed_pod_view: walk one resource without emitting a row
+  bool no_emit = false, last_err = false;
+  uint32_t last_cls = R_CLASS_OTHER;
+  const PodView& view() const { return pod; }
 
   void add(const char* p, const char* e) {
     u.reset();
@@ -818,6 +776,11 @@ class Flattener {
       }
     }
     if (!cur.ok()) throw std::invalid_argument("malformed resource JSON");
+    if (no_emit) {
+      last_cls = cls;
+      last_err = typed && t.err;
+      return;
+    }
     emit(cls, typed && t.err);
   }
 
@@ -1400,6 +1363,21 @@ void load_ns_labels(Corpus& C, const char* js, size_t len) {
 }
 
 }  // namespace
+
+bool typed_pod_view(const char* json, size_t len, PodView* out, std::string* kind) {
+  Corpus scratch;
+  Flattener f(scratch);
+  f.no_emit = true;
+  if (kind) *kind = top_kind(json, json + len);
+  try {
+    f.add(json, json + len);
+  } catch (const std::exception&) {
+    return false;
+  }
+  if (f.last_cls == R_CLASS_OTHER || f.last_err) return false;
+  *out = f.view();
+  return true;
+}
 
 int64_t Corpus::bytes() const {
   int64_t b = 0;

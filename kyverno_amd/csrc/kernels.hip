@@ -20,6 +20,7 @@
 //  kpe_count_kernel  — per-rule status histogram of a verdict matrix (the CLI totals
 //                      of cmd/cli/kubectl-kyverno/processor/result.go:34-68); fetch time.
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <stdint.h>
 
 #include <algorithm>
@@ -1129,6 +1130,8 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
   int per_cu = 0;
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn(pss, narrow), kBlock, dyn_bytes) != hipSuccess)
     per_cu = 1;
+  static const int bpc_env = getenv("KPE_SCAN_BPC") ? atoi(getenv("KPE_SCAN_BPC")) : 0;  // experiments
+  if (bpc_env > 0 && bpc_env < per_cu) per_cu = bpc_env;
   const int64_t tiles = (n + kBlock - 1) / kBlock;
   const int64_t g = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
   return (uint32_t)(g < tiles ? g : tiles);

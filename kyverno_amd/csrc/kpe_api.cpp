@@ -20,6 +20,7 @@
 #include "kernels_abi.h"
 #include "patclass.hpp"
 #include "program.hpp"
+#include "pss_msg.hpp"
 
 namespace kpe {
 void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs);
@@ -1340,10 +1341,19 @@ kpe_status kpe_cli_summary(const kpe_program* prog, const kpe_counts* counts, in
 // over every policy of the program; toPolicyResult results.go:56-71.
 long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row, char* buf,
                         size_t cap) {
+  return kpe_report_results_msg(prog, verdict_row, cv_mask_row, nullptr, 0, buf, cap);
+}
+
+long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
+                            const char* resource_json, size_t resource_len, char* buf, size_t cap) {
   if (!prog || !verdict_row) {
     fail(KPE_E_INVALID, "null argument");
     return -KPE_E_INVALID;
   }
+  // the typed pod view for podSecurity fail messages, decoded on first use
+  int pod_state = 0;  // 0 not decoded, 1 ok, -1 getSpec fails
+  kpe::PodView pod;
+  std::string kind;
   static const char* const kResult[6] = {nullptr, "pass", "fail", "warn", "error", "skip"};
   const kpe::Program& P = *prog->p;
   std::string o = "[";
@@ -1358,6 +1368,21 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
     first = false;
     o += "\"source\":\"kyverno\",\"policy\":";
     json_str(o, rr.policy_key);
+    if (resource_json) {  // RuleResponse message (validate_pss.go:85,108; validate_resource.go:339)
+      std::string msg;
+      if (rr.pss && v == KPE_PASS) {
+        msg = kpe::pss_pass_message(rr.rule);
+      } else if (rr.pss && v == KPE_FAIL && !rr.pss_excl && cv_mask_row && cv_mask_row[r]) {
+        if (!pod_state) pod_state = kpe::typed_pod_view(resource_json, resource_len, &pod, &kind) ? 1 : -1;
+        if (pod_state > 0) msg = kpe::pss_fail_message(rr.rule, rr.pss_level, rr.pss_version, kind, pod, cv_mask_row[r]);
+      } else if (rr.msg_pattern && v == KPE_PASS) {
+        msg = "validation rule '" + rr.rule + "' passed.";
+      }
+      if (!msg.empty()) {
+        o += ",\"message\":";
+        json_str(o, msg);
+      }
+    }
     if (!rr.rule.empty()) {
       o += ",\"rule\":";
       json_str(o, rr.rule);

@@ -2042,6 +2042,7 @@ class Lowerer {
       }
     }
     KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0};
+    bool pss_excl = false, msg_pattern = false;
     if (!has_validate) {
       k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
       if (nonempty(r.get("verifyImages"))) throw CompileError("rule '" + rname + "': verifyImages is not supported");
@@ -2056,6 +2057,7 @@ class Lowerer {
       if (ok && ex && ex->t != JV::Null) {
         if (ex->t != JV::Arr) throw CompileError("rule '" + rname + "': podSecurity.exclude is not a list");
         if (!ex->a.empty()) {
+          pss_excl = true;
           if (apply_one)
             throw CompileError("rule '" + rname + "': applyRules=One with podSecurity.exclude is not supported");
           pss_exclusions(*ex, (uint32_t)P.rules.size(), k.cv_mask, rname);
@@ -2096,6 +2098,7 @@ class Lowerer {
         });
         KpePatRule pr{(uint32_t)P.rules.size(), 0, (uint32_t)(P.pat.roots.size() / 2), 0};
         if (present("pattern")) {
+          msg_pattern = true;
           const JV& pt = *v->get("pattern");
           if (pc::has_vars(pt)) throw CompileError("rule '" + rname + "': pattern variables are not supported yet");
           pcomp.root(pt);
@@ -2174,6 +2177,8 @@ class Lowerer {
       rr.pss_level = sv(ps->get("level"));
       rr.pss_version = sv(ps->get("version"));
     }
+    rr.pss_excl = pss_excl;
+    rr.msg_pattern = msg_pattern;
     P.reports.push_back(std::move(rr));
   }
 

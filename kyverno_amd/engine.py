@@ -296,18 +296,27 @@ class Engine:
         return self.validate_batch([policy_context.policy], [policy_context.resource], nsl)[0][0]
 
 
-def report_results(ps: PolicySet, verdict_row, cv_mask_row=None) -> List[dict]:
+def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None) -> List[dict]:
     """EngineResponseToReportResults (pkg/utils/report/results.go:89-156) for one resource row,
-    through kpe_report_results (message and timestamp are not produced)."""
+    through kpe_report_results, or kpe_report_results_msg when the resource (a dict or its JSON
+    bytes) is given: then results carry the RuleResponse message (podSecurity pass / fail,
+    validate.pattern pass; no timestamp)."""
     L = load()
     v = np.ascontiguousarray(verdict_row, dtype=np.uint8)
     m = None if cv_mask_row is None else np.ascontiguousarray(cv_mask_row, dtype=np.uint32)
     if v.size != ps.num_rules or (m is not None and m.size != ps.num_rules):
         raise ValueError("row length != number of rules")
+    raw = None
+    if resource is not None:
+        raw = resource if isinstance(resource, (bytes, bytearray)) else json.dumps(resource).encode()
     cap = 4096
     while True:
         buf = ctypes.create_string_buffer(cap)
-        n = L.kpe_report_results(ps.h, v.ctypes.data, None if m is None else m.ctypes.data, buf, cap)
+        mp = None if m is None else m.ctypes.data
+        if raw is None:
+            n = L.kpe_report_results(ps.h, v.ctypes.data, mp, buf, cap)
+        else:
+            n = L.kpe_report_results_msg(ps.h, v.ctypes.data, mp, raw, len(raw), buf, cap)
         if n < 0:
             check(-n)
         if n < cap:

@@ -96,6 +96,70 @@ int oracle_pss_failing_checks(const char* level, const char* version, const char
   }
 }
 
+// Failing versioned checks of one pod as a bit mask, bit = flat index of (check, version) in
+// default_checks() order (the kpe_fetch_cv_masks layout); evaluate.go:24-70 without exclusions.
+long long oracle_pss_failing_cv(const char* level, const char* version, const char* pod_json) {
+  try {
+    JPtr podj = parse_json(pod_json);
+    Pod pod = get_spec(*podj, "Pod");
+    Version v;
+    if (!parse_version(version, &v)) return -1;
+    std::string lvl = level;
+    const Level L = lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged);
+    long long m = 0;
+    int flat = 0;
+    for (auto& check : default_checks()) {
+      const int base = flat;
+      flat += (int)check.versions.size();
+      if (L == Level::Baseline && check.level != L) continue;
+      size_t latest = 0;
+      for (size_t i = 1; i < check.versions.size(); ++i)
+        if (!check.versions[i].min.older(check.versions[latest].min)) latest = i;
+      for (size_t i = 0; i < check.versions.size(); ++i) {
+        const bool run = v.latest ? i == latest : !v.older(check.versions[i].min);
+        if (run && !check.versions[i].fn(pod.meta, pod.spec).allowed) m |= 1ll << (base + (int)i);
+      }
+    }
+    return m;
+  } catch (...) {
+    return -1;
+  }
+}
+
+// RuleResponse message of a podSecurity rule without exclusions for one resource
+// (validate_pss.go:64-110): "Validation rule '<rule>' passed." or the FormatChecksPrint
+// failure text after convertChecks. Returns 1 pass, 0 fail, -1 getSpec / version error.
+int oracle_pss_message(const char* rule, const char* level, const char* version, const char* resource_json, char* buf,
+                       size_t cap) {
+  try {
+    JPtr res = parse_json(resource_json);
+    const std::string kind = jstr(res->get("kind"));
+    Pod pod = get_spec(*res, kind);
+    Version v;
+    if (!parse_version(version, &v)) return -1;
+    std::string lvl = level;
+    LevelVersion lv{lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged),
+                    v};
+    auto checks = evaluate_pss(lv, pod);
+    std::string msg;
+    if (checks.empty()) {
+      msg = std::string("Validation rule '") + rule + "' passed.";
+    } else {
+      convert_checks(checks, kind);
+      msg = std::string("Validation rule '") + rule + "' failed. It violates PodSecurity \"" + level + ":" + version +
+            "\": " + format_checks_print(checks);
+    }
+    snprintf(buf, cap, "%s", msg.c_str());
+    return checks.empty() ? 1 : 0;
+  } catch (const DecodeError& de) {
+    g_err = de.msg;
+    return -1;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 // Number of rules after autogen for a JSON array of policies; names written
 // newline-separated into buf as "<policy>/<rule>".
 int oracle_rule_names(const char* policies_json, char* buf, size_t cap) {

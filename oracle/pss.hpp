@@ -723,6 +723,64 @@ inline bool evaluate_pod(const LevelVersion& lv, const std::vector<PSSExclude>& 
   return res.empty() && !err;
 }
 
+// evaluate.go:331-362 FormatChecksPrint. A Forbidden error with a bad value (anything but the
+// empty string) prints "<field> is forbidden, don't set the BadValue: %+v"; every other error
+// prints field.Error.Error() = "<field>: <type>" (apimachinery v0.29.1 field/errors.go:
+// Required and Forbidden bodies are the type string alone).
+inline std::string format_checks_print(const std::vector<PSSCheckResult>& checks) {
+  std::string s;
+  for (auto& c : checks) {
+    s += "\n(Forbidden reason: " + c.result.reason + ", field error list: [";
+    for (size_t i = 0; i < c.result.errs.size(); ++i) {
+      const FieldError& e = c.result.errs[i];
+      const bool exist = !(e.bk == BVKind::Str && e.bs.empty());
+      if (e.type == "Forbidden" && exist) {
+        std::string v;  // %+v
+        switch (e.bk) {
+          case BVKind::Str: v = e.bs; break;
+          case BVKind::Bool: v = e.bb ? "true" : "false"; break;
+          case BVKind::Int:
+          case BVKind::Other: v = std::to_string(e.bi); break;
+          case BVKind::StrList:
+            v = "[";
+            for (size_t k = 0; k < e.bl.size(); ++k) v += (k ? " " : "") + e.bl[k];
+            v += "]";
+            break;
+          default: break;
+        }
+        s += e.field + " is forbidden, don't set the BadValue: " + v;
+      } else {
+        s += e.field + ": " + e.type;
+      }
+      if (i + 1 != c.result.errs.size()) s += ", ";
+    }
+    s += "])";
+  }
+  return s;
+}
+
+inline std::string go_replace_all(const std::string& s, const std::string& a, const std::string& b) {
+  std::string o;
+  size_t i = 0, j;
+  while ((j = s.find(a, i)) != std::string::npos) {
+    o += s.substr(i, j - i) + b;
+    i = j + a.size();
+  }
+  return o + s.substr(i);
+}
+// validate_pss.go:114-135 convertChecks: field paths of controllers / CronJobs, then every
+// "metadata" -> "spec.template.metadata" (for every kind, Pods included)
+inline void convert_checks(std::vector<PSSCheckResult>& checks, const std::string& kind) {
+  const bool ctl = kind == "DaemonSet" || kind == "Deployment" || kind == "Job" || kind == "StatefulSet" ||
+                   kind == "ReplicaSet" || kind == "ReplicationController";
+  for (auto& c : checks)
+    for (auto& e : c.result.errs) {
+      if (ctl) e.field = go_replace_all(e.field, "spec", "spec.template.spec");
+      else if (kind == "CronJob") e.field = go_replace_all(e.field, "spec", "spec.jobTemplate.spec.template.spec");
+      e.field = go_replace_all(e.field, "metadata", "spec.template.metadata");
+    }
+}
+
 // evaluate.go:221-239 + PSA api.ParseVersion (`latest` or `v1.<minor>`)
 inline bool parse_version(const std::string& v, Version* out) {
   if (v.empty() || v == "latest") {

@@ -13,7 +13,11 @@ Restated:
     only when at least one check failed (results.go:114-129); PodSecurityChecks.Level /
     Version are the rule's raw podSecurity strings (validate_pss.go:79-82)
   - JSON omitempty of PolicyReportResult (api/policyreport/v1alpha2/common.go:93-137)
-Not restated: message and timestamp (message text is SURVEY.md 8(f) rank 1), exception
+message (when a `pss_message` callable is given): podSecurity pass "Validation rule '<rule>'
+passed." (validate_pss.go:85), podSecurity fail without exclusions through the C++ oracle's
+FormatChecksPrint (validate_pss.go:108, oracle/pss.hpp format_checks_print), validate.pattern
+pass "validation rule '<rule>' passed." (validate_resource.go:339); other messages are not
+restated. Not restated: timestamp, exception
 and ValidatingAdmissionPolicy branches (out of the path's scope).
 Autogen rules are mapped back to their source rule by the "autogen-" / "autogen-cronjob-"
 prefix (pkg/autogen/autogen.go:213-222); names truncated to 63 characters are not mapped
@@ -52,7 +56,8 @@ def _source_rule(policy: dict, rule_name: str) -> dict:
 
 
 def report_results(policies: List[dict], rule_names: List[str], verdict_row, resource: dict,
-                   failing_checks: Callable[[str, str, dict], List[str]]) -> List[Dict]:
+                   failing_checks: Callable[[str, str, dict], List[str]],
+                   pss_message: Optional[Callable[[str, str, str, dict], Optional[str]]] = None) -> List[Dict]:
     """[]PolicyReportResult for one resource over all policies (rules in rule_names order)."""
     by_name = {p["metadata"]["name"]: p for p in policies}
     out = []
@@ -70,6 +75,18 @@ def report_results(policies: List[dict], rule_names: List[str], verdict_row, res
         if res == "fail" and not scored:
             res = "warn"
         item = {"source": "kyverno", "policy": f"{ns}/{pname}" if ns else pname}
+        val = _source_rule(pol, rname).get("validate") or {}
+        ps0 = val.get("podSecurity")
+        if pss_message is not None:
+            msg = None
+            if ps0 and cell == 1:
+                msg = f"Validation rule '{rname}' passed."
+            elif ps0 and cell == 2 and not ps0.get("exclude"):
+                msg = pss_message(rname, ps0.get("level", ""), ps0.get("version", ""), resource)
+            elif not ps0 and val.get("pattern") is not None and cell == 1:
+                msg = f"validation rule '{rname}' passed."
+            if msg:
+                item["message"] = msg
         if rname:
             item["rule"] = rname
         item["result"] = res

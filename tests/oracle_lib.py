@@ -21,6 +21,10 @@ class Oracle:
         L.oracle_pss_evaluate.argtypes = [ctypes.c_char_p, ctypes.c_char_p]
         L.oracle_pss_failing_checks.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                                 ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_pss_failing_cv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_pss_failing_cv.restype = ctypes.c_longlong
+        L.oracle_pss_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
+                                          ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_rule_names.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
@@ -47,6 +51,18 @@ class Oracle:
             return None
         s = buf.value.decode()
         return s.split(",") if s else []
+
+    def failing_cv(self, level, version, pod):
+        """Failing versioned checks (bit = CV index) of a pod, no exclusions; None on error."""
+        r = self.lib.oracle_pss_failing_cv(level.encode(), version.encode(), json.dumps(pod).encode())
+        return None if r < 0 else int(r)
+
+    def pss_message(self, rule, level, version, resource):
+        """RuleResponse message of a podSecurity rule without exclusions (None on error)."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        r = self.lib.oracle_pss_message(rule.encode(), level.encode(), version.encode(),
+                                        json.dumps(resource).encode(), buf, 1 << 16)
+        return None if r < 0 else buf.value.decode()
 
     def rule_names(self, policies):
         buf = ctypes.create_string_buffer(1 << 20)

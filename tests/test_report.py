@@ -42,12 +42,57 @@ def report_policy_set():
     return pols
 
 
+def _no_timestamp(results):
+    return [{k: v for k, v in r.items() if k != "timestamp"} for r in results]
+
+
 def test_oracle_pinned_by_background_report(oracle):
     bg = json.load(open(os.path.join(GOLD, "background_report.json")))
     names = oracle.rule_names([bg["policy"]])
     v = oracle.validate([bg["policy"]], json.dumps(bg["resource"]).encode())
     got = oracle_report.report_results([bg["policy"]], names, v[0], bg["resource"], oracle.failing_checks)
-    assert got == _no_message(bg["results"])  # report-assert.yaml, message aside
+    assert got == _no_message(bg["results"])
+    got = oracle_report.report_results([bg["policy"]], names, v[0], bg["resource"], oracle.failing_checks,
+                                       oracle.pss_message)
+    assert got == _no_timestamp(bg["results"])  # report-assert.yaml, message included
+
+
+def _oracle_cv_row(oracle, pols, names, row, doc):
+    """Versioned failing-check masks of one row from the oracle (the kpe_fetch_cv_masks layout:
+    bit v = versioned check v), for the fail cells of podSecurity rules."""
+    m = np.zeros(len(names), dtype=np.uint32)
+    for r, full in enumerate(names):
+        if int(row[r]) != 2:
+            continue
+        pname, rname = full.split("/", 1)
+        pol = next(p for p in pols if p["metadata"]["name"] == pname)
+        ps0 = (oracle_report._source_rule(pol, rname).get("validate") or {}).get("podSecurity")
+        if ps0:
+            m[r] = oracle.failing_cv(ps0.get("level", ""), ps0.get("version", ""), oracle_report.pod_of(doc)) or 0
+    return m
+
+
+def test_host_messages_match_oracle(oracle):
+    """kpe_report_results_msg renders podSecurity pass / fail and pattern pass messages from the
+    resource JSON and the failing versioned checks; with the oracle's verdicts and checks as
+    input it equals the oracle's report (oracle/pss.hpp FormatChecksPrint) on Pods and
+    controllers of two synthetic mixes."""
+    pols = [p for p in report_policy_set()
+            if not any(((r.get("validate") or {}).get("podSecurity") or {}).get("exclude")
+                       for r in p["spec"]["rules"])]
+    ps = K.PolicySet(pols)
+    names = oracle.rule_names(pols)
+    nmsg = 0
+    for mix, seed in ((0, 0xC2), (2, 31)):
+        nd = K.synth_resources(seed, 300, mix=mix)
+        docs = [json.loads(x) for x in nd.split(b"\n") if x.strip()]
+        v = oracle.validate(pols, nd, nthreads=4)
+        for i, doc in enumerate(docs):
+            want = oracle_report.report_results(pols, names, v[i], doc, oracle.failing_checks, oracle.pss_message)
+            got = K.report_results(ps, v[i], _oracle_cv_row(oracle, pols, names, v[i], doc), resource=doc)
+            assert got == want, (i, got, want)
+            nmsg += sum(1 for r in got if r.get("result") in ("fail", "warn") and "message" in r)
+    assert nmsg > 100
 
 
 def test_host_report_matches_oracle_without_controls(oracle):
@@ -102,6 +147,7 @@ def test_gpu_report_background_fixture():
     v, _, _ = eng.evaluate(ps, c, check_masks=True)
     m = eng.cv_masks(ps, c)
     assert K.report_results(ps, v[0], m[0]) == _no_message(bg["results"])
+    assert K.report_results(ps, v[0], m[0], resource=bg["resource"]) == _no_timestamp(bg["results"])
 
 
 @pytest.mark.gpu
@@ -128,6 +174,10 @@ def test_gpu_report_matches_oracle(oracle, mix, n, seed):
     for i in range(0, n, 3):
         want = oracle_report.report_results(pols, names, ref[i], docs[i], oracle.failing_checks)
         got = K.report_results(ps, v[i], cv[i])
+        assert got == want, (i, got, want)
+        # messages: rules with podSecurity.exclude render no fail message on either side
+        want = oracle_report.report_results(pols, names, ref[i], docs[i], oracle.failing_checks, oracle.pss_message)
+        got = K.report_results(ps, v[i], cv[i], resource=docs[i])
         assert got == want, (i, got, want)
         dup += sum(1 for r in got if "properties" in r and len(set(r["properties"]["controls"].split(","))) <
                    len(r["properties"]["controls"].split(",")))
