@@ -210,6 +210,16 @@ def main():
                      # shards overlap on two streams there) and the isolated single-stream step
                      "achieved_per_step": st.scan_bytes / (ms_per_step * 1e-3) / 1e9,
                      "single_stream_step_ms": single_stream_ms}
+        if pat_ms > scan_ms and st.pattern_bytes > 0:
+            # pattern-dominated configurations (C3, C5): the dominant kernel is the pattern VM;
+            # its algorithmic bytes are every resource's document tape once plus the verdicts
+            pat_achieved = st.pattern_bytes / (pat_ms * 1e-3) / 1e9
+            scan_roof = {"bound": "hbm", "achieved": pat_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": pat_achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "kpe_pattern_kernel",
+                         "kernel_ms": pat_ms, "alg_bytes_per_launch": st.pattern_bytes,
+                         "scan_kernel": {"kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes,
+                                         "frac": scan_achieved / HBM_PEAK_GBS},
+                         "single_stream_step_ms": single_stream_ms}
         e2e_s = t_flatten / replicas + t_upload / replicas + t_eval1
         line = {
             "metric": "resource-rule evals/sec, 1M Pods × PSS restricted, 1/8 GPU; % HBM BW",

@@ -193,7 +193,11 @@ typedef struct kpe_kernel_stats {
   double pss_kernel_ms;     /* summed duration of the resource-scan kernel      */
   double dict_kernel_ms;    /* summed duration of the dictionary predicate pass */
   double scan_bytes;        /* algorithmic bytes one scan-kernel launch reads+writes */
-  double pattern_kernel_ms; /* summed duration of the pattern-rule kernel (0 without pattern rules) */
+  double pattern_kernel_ms; /* summed duration of the kernels after the scan (condition, exclusion,
+                               pattern-rule kernels; 0 without such rules) */
+  double pattern_bytes;     /* algorithmic bytes of one pattern-kernel launch: every resource's
+                               document tape (8 B per entry) and root offset once, plus the verdict
+                               matrix read and written */
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);
 kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c,

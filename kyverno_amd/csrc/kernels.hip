@@ -142,6 +142,7 @@ constexpr uint32_t kBlock = 256;
 #define DIAG_NOLOOP 8u   // no tiles: launch + prologue only
 #define DIAG_EMPTY 16u   // return at entry: launch cost only
 #define DIAG_NOTT 32u    // no truth table in the prologue
+#define DIAG_NOSTORE 64u  // (LEAN kernel) no verdict row stores
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
@@ -1027,6 +1028,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
 }
 
 
+#include "lean.inl"
+
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers (called from kpe_api.cpp).
 // grid: x = blocks of the largest job, y = jobs
@@ -1045,9 +1048,13 @@ namespace {
 #include "patvm.inl"
 }  // namespace
 
+// grid: x = 256-row blocks; y = 1 (one lane per row, every rule) or the pattern rules (one rule
+// per wave, KPE_PAT_CELLS)
 __global__ void __launch_bounds__(256) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
   const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r < ap->n) pat_eval_row(*ap, r);
+  if (r >= ap->n) return;
+  if (gridDim.y == 1 && ap->npr > 1) pat_eval_row(*ap, r);
+  else pat_eval_cell(*ap, r, blockIdx.y);
 }
 
 // ===========================================================================
@@ -1092,9 +1099,13 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
   return hipGetLastError();
 }
 
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s) {
-  if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dargs);
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s) {
+  if (n <= 0 || npr == 0) return hipSuccess;
+  // one lane per row running every pattern rule; KPE_PAT_CELLS=1: a rows x rules grid (measured
+  // no faster on C5 and slower on C3's 600 rules: both are bound by the dependent tape loads of
+  // the longest walks, not by the rule loop)
+  static const bool rows = getenv("KPE_PAT_CELLS") == nullptr;
+  hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + 255) / 256), rows ? 1u : npr), dim3(256), 0, s, dargs);
   return hipGetLastError();
 }
 
@@ -1107,6 +1118,7 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipSt
 namespace {
 typedef void (*ScanFn)(const ScanArgs*);
 ScanFn scan_fn(int pss, int narrow) {
+  if (pss && narrow == 3) return nullptr;  // kpe_lean_kernel (by-value arguments): see scan_occupancy
   if (pss && narrow == 2) return kpe_scan_kernel<true, true, false, true>;
   if (pss) return narrow ? kpe_scan_kernel<true, true, false> : kpe_scan_kernel<true, false, false>;
   return narrow ? kpe_scan_kernel<false, true, false> : kpe_scan_kernel<false, false, false>;
@@ -1128,8 +1140,10 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
       cus = 256;
   }
   int per_cu = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn(pss, narrow), kBlock, dyn_bytes) != hipSuccess)
-    per_cu = 1;
+  const hipError_t oe = pss && narrow == 3
+                           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kpe_lean_kernel, kBlock, dyn_bytes)
+                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn(pss, narrow), kBlock, dyn_bytes);
+  if (oe != hipSuccess) per_cu = 1;
   static const int bpc_env = getenv("KPE_SCAN_BPC") ? atoi(getenv("KPE_SCAN_BPC")) : 0;  // experiments
   if (bpc_env > 0 && bpc_env < per_cu) per_cu = bpc_env;
   const int64_t tiles = (n + kBlock - 1) / kBlock;
@@ -1137,9 +1151,13 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
   return (uint32_t)(g < tiles ? g : tiles);
 }
 // `dargs` is the device copy of the arguments; `n` its row count.
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
-                                      size_t dyn_bytes, hipStream_t s) {
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* hargs, int64_t n, int pss, int narrow,
+                                      uint32_t grid, size_t dyn_bytes, hipStream_t s) {
   if (n == 0 || grid == 0) return hipSuccess;
+  if (pss && narrow == 3) {  // kpe_lean_kernel takes its arguments by value
+    hipLaunchKernelGGL(kpe_lean_kernel, dim3(grid), dim3(kBlock), dyn_bytes, s, *hargs);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
   return hipGetLastError();
 }

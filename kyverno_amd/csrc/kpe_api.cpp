@@ -28,13 +28,14 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s);
 extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
                                            uint8_t value, hipStream_t s);
 extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
 extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s);
-extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, int64_t n, int pss, int narrow, uint32_t grid,
+extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* hargs, int64_t n, int pss, int narrow,
+                                      uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
@@ -111,12 +112,12 @@ struct kpe_device {
   bool timing = false;
   struct EvPair {
     hipEvent_t a, b, c, d;
-    double bytes;
+    double bytes, pbytes;
   };
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
   uint64_t launches = 0;
-  double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0;
+  double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0, last_pbytes = 0;
   hipEvent_t get_ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -166,6 +167,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t pimg_words = 0, capb_lds = 0;
   size_t prep_dyn_bytes = 0;  // the prep kernel's LDS: the scan layout + the fuse area
   bool lean = false;  // LEAN scan instantiation (kind table; no check masks)
+  int lean_kind = 0;  // kpe_launch_scan narrow code of the LEAN scan: 3 kpe_lean_kernel, 2 the template
   uint32_t kt_lds = PRED_NONE, nkinds = 0;
   DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
   bool xargs_valid = false;
@@ -868,7 +870,15 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.blob_words = blob;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? 2 : narrow ? 1 : 0, B.dyn_bytes);
+  // LEAN scans run kpe_lean_kernel (buffer loads: every scanned column under 4 GiB, with a
+  // tile's slack) unless KPE_OLD_LEAN selects the template instantiation
+  const uint64_t lim = (1ull << 32) - (1ull << 20);
+  B.lean_kind = !lean ? 0 : (getenv("KPE_OLD_LEAN") || (uint64_t)C.n * 16 + 4096 > lim ||
+                             (uint64_t)C.c_sc.size() * 8 > lim || (uint64_t)C.vol_src.size() * 4 > lim ||
+                             (uint64_t)C.sys_id.size() * 4 > lim || (uint64_t)C.pann_kv.size() * 4 > lim)
+                                ? 2
+                                : 3;
+  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
   HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 8, 1) * 8));
@@ -1037,7 +1047,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     fprintf(stderr, "\n");
   }
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
-  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), C.n, P.any_pss ? 1 : 0, B.lean && !masks ? 2 : PD.narrow ? 1 : 0,
+  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, B.lean && !masks ? B.lean_kind : PD.narrow ? 1 : 0,
                          B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
@@ -1158,7 +1168,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       HIPCHK(hipStreamSynchronize(s));
       B.pargs_valid = true;
     }
-    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, s));
+    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;
       HIPCHK(hipMemcpyAsync(&e, B.perr.p, 4, hipMemcpyDeviceToHost, s));
@@ -1172,6 +1182,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.bytes = scan_bytes(P, C, B.need, masks);
+    ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     dev->pending.push_back(ev);
   }
   return KPE_OK;
@@ -1448,6 +1459,7 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
     dev->pss_ms += d2;
     dev->pat_ms += d3;
     dev->last_bytes = p.bytes;
+    dev->last_pbytes = p.pbytes;
     dev->launches++;
     dev->pool.push_back(p.a);
     dev->pool.push_back(p.b);
@@ -1460,6 +1472,7 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
   out->dict_kernel_ms = dev->dict_ms;
   out->scan_bytes = dev->last_bytes;
   out->pattern_kernel_ms = dev->pat_ms;
+  out->pattern_bytes = dev->last_pbytes;
   if (reset) {
     dev->launches = 0;
     dev->pss_ms = dev->dict_ms = dev->pat_ms = 0;

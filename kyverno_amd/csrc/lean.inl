@@ -1,0 +1,278 @@
+// LEAN scan (kpe_lean_kernel): the resource scan of a PSS program whose match terms are all
+// kind predicates, with the prologue image ready in HBM and no check masks (C2: restricted:latest
+// and its autogen columns). Same verdicts as kpe_scan_kernel<PSS, NARROW> (the reference path:
+// pkg/engine/engine.go:87-101 validate -> validatePssHandler.Process, validate_pss.go:64-110,
+// pkg/pss/evaluate.go:24-70), restructured for instruction count:
+//  * every column is read through a raw buffer descriptor: 32-bit byte offsets, and loads past
+//    a column's end return 0 (hardware range check) instead of being clamped per lane, so a
+//    tile's loads cost one address op each;
+//  * a pod ORs its first few staged list items with fixed clamped LDS reads (no loop); a loop
+//    runs only for the items past them, when some pod of the wave has more;
+//  * the matched-rule mask is one kind-table read, the fixed PSA predicates direct LDS reads.
+// Included by kernels.hip (uses its anonymous-namespace helpers).
+
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void* p, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint32_t bload1(Rsrc r, uint32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+__device__ __forceinline__ uint2 bload2(Rsrc r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
+  return make_uint2(v[0], v[1]);
+}
+__device__ __forceinline__ uint4 bload4(Rsrc r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+struct LeanCols {
+  Rsrc rec, hdr, crec, vol, sys, ann;
+};
+struct LeanTile {
+  uint32_t h;   // header words of the tile and the next (lane k < 8: word k)
+  uint32_t hn;  // header of the tile this buffer loads next (three steps later)
+  uint4 rec;
+  uint2 c0, c1, q0;
+  uint32_t v0, v1, s0;
+};
+__device__ __forceinline__ void pin_lean(LeanTile& d) {
+  pin(d.h), pin(d.rec), pin(d.c0), pin(d.c1), pin(d.q0), pin(d.v0), pin(d.v1), pin(d.s0);
+}
+// header words of tiles `tile` and `tile + 1` (lane k < 8: word k)
+__device__ __forceinline__ uint32_t lean_hdr(const LeanCols& L, uint32_t tile, uint32_t lane) {
+  return bload1(L.hdr, (tile * 4u + (lane & 7u)) * 4u);
+}
+// A tile's loads: pod records per lane, list items cooperatively (lane i: items base + i and
+// base + 64 + i). Items past the tile's range belong to the next tiles or read 0 past the
+// column's end; they are never used.
+__device__ __forceinline__ LeanTile lean_load(const LeanCols& L, uint32_t tile, uint32_t h, uint32_t lane) {
+  LeanTile d;
+  const uint32_t C0 = hw(h, 0), V0 = hw(h, 1), S0 = hw(h, 2), A0 = hw(h, 3);
+  d.h = h;
+  d.rec = bload4(L.rec, (tile * 64u + lane) * 16u);
+  d.c0 = bload2(L.crec, (C0 + lane) * 8u);
+  d.c1 = bload2(L.crec, (C0 + 64u + lane) * 8u);
+  d.v0 = bload1(L.vol, (V0 + lane) * 4u);
+  d.v1 = bload1(L.vol, (V0 + 64u + lane) * 4u);
+  d.s0 = bload1(L.sys, (S0 + lane) * 4u);
+  d.q0 = bload2(L.ann, (A0 + lane) * 8u);
+  return d;
+}
+
+#ifndef KPE_LEAN2_WAVES
+#define KPE_LEAN2_WAVES 6
+#endif
+// The arguments are passed by value (read from the kernarg segment: one hop less than a device
+// copy before the first header load); re-read through a laundered pointer per tile.
+__device__ __forceinline__ CArgs* kargs() {
+  uint64_t v = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(v));
+  return (CArgs*)v;
+}
+__global__ void __launch_bounds__(kBlock, KPE_LEAN2_WAVES) kpe_lean_kernel(ScanArgs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  if (KPE_DIAG & DIAG_EMPTY) return;
+  CArgs& a0 = *kargs();
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
+  const uint32_t W = gridDim.x * (kBlock / 64u);
+  uint32_t tile = blockIdx.x * (kBlock / 64u) + wv;
+  const uint32_t need = a0.need;
+  // columns a program does not read get zero-length descriptors: their loads return 0
+  LeanCols L;
+  L.rec = make_rsrc(a0.rec, n * 16u);
+  L.hdr = make_rsrc(a0.hdr, (ntiles + 1u) * 16u);
+  L.crec = make_rsrc(a0.crec, a0.nctr_total * 8u);
+  L.vol = make_rsrc(a0.vol_src, (need & NEED_VOL) ? a0.nvol_total * 4u : 0u);
+  L.sys = make_rsrc(a0.sys_id, (need & NEED_SYS) ? a0.nsys_total * 4u : 0u);
+  L.ann = make_rsrc(a0.pann_kv, (need & NEED_PANN) ? a0.npann_total * 8u : 0u);
+  const bool nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN;
+
+  // ---- Loads run two tiles ahead of the evaluation: step s evaluates tile s while the items
+  // of tiles s + 1 and s + 2 and the header of tile s + 3 are in flight. Issue order per step:
+  // header s + 3, then items s + 2 (which wait for header s + 2, issued one step earlier before
+  // items s + 1), so the only wait of a step leaves items s + 1, s + 2 and header s + 3 in flight.
+  // Prologue: headers 0, 1, 2; the image; items 0 and 1.
+  const uint32_t h0 = lean_hdr(L, tile, lane);
+  const uint32_t h1 = lean_hdr(L, tile + W, lane);
+  const uint32_t h2 = lean_hdr(L, tile + 2u * W, lane);
+  const uint32_t img_n4 = a0.pimg_words >> 2;
+  const uint4* img = reinterpret_cast<const uint4*>(a0.pimg);
+  const uint4 img0 = img[min(t, img_n4 - 1u)];
+  uint32_t cls_cv = 0, cls_rm = 0;  // (check set, rules failing on it) per PSS version class
+  if (lane < a0.ncls) {
+    const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
+    cls_cv = c.x, cls_rm = c.y;
+  }
+  LeanTile ta = lean_load(L, tile, h0, lane);
+  LeanTile tb = lean_load(L, tile + W, h1, lane);
+  LeanTile tc{};
+  tc.hn = h2;
+  {
+    uint4* d4 = reinterpret_cast<uint4*>(dyn);
+    if (t < img_n4) d4[t] = img0;
+#pragma unroll 1
+    for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
+  }
+  __syncthreads();
+  if (KPE_DIAG & DIAG_NOLOOP) {
+    if (tile < ntiles && lane == 0) a0.verdicts[tile] = (uint8_t)(dyn[0] + ta.rec.x + tb.rec.x);
+    return;
+  }
+  const uint8_t* s_capb = reinterpret_cast<const uint8_t*>(dyn + a0.capb_lds);
+  const LdsPtr lds = (LdsPtr)dyn;
+  const uint32_t p_sann = a0.pp_seccomp_ann_ok & ~PRED_LOCAL, p_aak = a0.pp_apparmor_key & ~PRED_LOCAL,
+                 p_aao = a0.pp_apparmor_ok & ~PRED_LOCAL, p_spk = a0.pp_seccomp_pod_key & ~PRED_LOCAL,
+                 p_s0 = a0.pp_sysctl0 & ~PRED_LOCAL, p_s1 = a0.pp_sysctl1 & ~PRED_LOCAL,
+                 p_s2 = a0.pp_sysctl2 & ~PRED_LOCAL;
+  auto pbit = [&](uint32_t loc, uint32_t id) -> uint32_t { return (lds[loc + (id >> 5)] >> (id & 31u)) & 1u; };
+  const uint32_t kt = a0.kt_lds;
+
+  // per-kernel constants (scalar registers)
+  const uint32_t R = a0.nrules, cv_union = a0.cv_union, pss_rules = a0.pss_rules, ncls = a0.ncls;
+  const uint32_t ep_rules = a0.err_rules | a0.pat_rules, pat_rules = a0.pat_rules;
+  uint8_t* const verdicts = a0.verdicts;
+  uint32_t* const stage = dyn + a0.wave_lds + wv * a0.wave_words;
+  const uint32_t cls_cv0 = hw(cls_cv, 0), cls_rm0 = hw(cls_rm, 0);
+  auto step = [&](LeanTile& cur, LeanTile& far) {
+    // header of tile s + 3 (into this buffer, which loads that tile two steps from now), then
+    // the items of tile s + 2 into the buffer tile s - 1 used (its header arrived a step ago);
+    // no register holding an in-flight load is ever copied
+    cur.hn = lean_hdr(L, tile + 3u * W, lane);
+    far = lean_load(L, tile + 2u * W, far.hn, lane);
+    pin_lean(cur);
+    const uint32_t C0 = hw(cur.h, 0), V0 = hw(cur.h, 1), S0 = hw(cur.h, 2), A0 = hw(cur.h, 3);
+    const uint32_t nct = hw(cur.h, 4) - C0, nvt = hw(cur.h, 5) - V0, nst = hw(cur.h, 6) - S0,
+                   nat = hw(cur.h, 7) - A0;
+    const uint32_t r = tile * 64u + lane;
+    const bool live = r < n;
+    if (KPE_DIAG & DIAG_NOPSS) {  // loads consumed, no PSS evaluation
+      if (live)
+        verdicts[(size_t)r * R] =
+            (uint8_t)(cur.rec.x ^ cur.rec.z ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.v1 ^ cur.s0 ^ cur.q0.x ^ nct);
+      return;
+    }
+    // ---- the pod's item offsets: exclusive wave scans of its packed counts ----
+    const uint32_t z = cur.rec.z;  // 0 for rows past n (range-checked load)
+    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+    const uint32_t c01 = nc | (nv << 16);
+    const uint32_t e01 = wave_incl_scan(c01) - c01;
+    uint32_t e23 = 0;
+    if (nst | nat) {
+      const uint32_t c23 = ns | (na << 16);
+      e23 = wave_incl_scan(c23) - c23;
+    }
+    const uint32_t oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
+    uint2* sc = reinterpret_cast<uint2*>(stage);
+    uint8_t* sbv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_CTR * 2);
+    uint8_t* sbs = sbv + KPE_STAGE_VOL;
+    uint8_t* sba = sbs + KPE_STAGE_SMALL;
+    auto ctr_code = [&](uint2 e) { return make_uint2(e.x, (uint32_t)s_capb[CY_CAPSET(e.y)]); };
+    auto vol_code = [&](uint32_t sv0) -> uint32_t { return ((sv0 >> VS_HOSTPATH) & 1u) | ((sv0 & kAllowedVolumes) ? 0u : 2u); };
+    auto sys_code = [&](uint32_t id) -> uint32_t {
+      return (pbit(p_s0, id) ^ 1u) | ((pbit(p_s1, id) ^ 1u) << 1) | ((pbit(p_s2, id) ^ 1u) << 2);
+    };
+    auto ann_code = [&](uint2 kv) -> uint32_t {
+      return (pbit(p_aak, kv.x) & (pbit(p_aao, kv.y) ^ 1u)) | ((pbit(p_spk, kv.x) & (pbit(p_sann, kv.y) ^ 1u)) << 1);
+    };
+    // ---- stage the tile's item codes, unconditionally: slots past the tile's items hold codes
+    // of the next tile's items (or of zeros past a column's end) that no pod reads ----
+    sc[lane] = ctr_code(cur.c0);
+    sc[lane + 64u] = ctr_code(cur.c1);
+    if (nvol) sbv[lane] = (uint8_t)vol_code(cur.v0), sbv[lane + 64u] = (uint8_t)vol_code(cur.v1);
+    if (nsys && nst) sbs[lane] = (uint8_t)sys_code(cur.s0);
+    if (npann && nat) sba[lane] = (uint8_t)ann_code(cur.q0);
+    __builtin_amdgcn_wave_barrier();
+    // ---- each pod ORs its first items with fixed clamped reads (a repeated item does not
+    // change an OR); pods without items of a list mask the read off ----
+    uint32_t xo, co, vcode = 0, scode = 0, acode = 0;
+    {
+      const uint32_t last = min(oc + (nc ? nc - 1u : 0u), KPE_STAGE_CTR - 1u);
+      const uint2 e0 = sc[min(oc, last)], e1 = sc[min(oc + 1u, last)], e2 = sc[min(oc + 2u, last)],
+                  e3 = sc[min(oc + 3u, last)];
+      const uint32_t m = nc ? ~0u : 0u;
+      xo = (e0.x | e1.x | e2.x | e3.x) & m;
+      co = (e0.y | e1.y | e2.y | e3.y) & m;
+    }
+    if (nvol) {
+      const uint32_t last = min(ov + (nv ? nv - 1u : 0u), KPE_STAGE_VOL - 1u);
+      const uint32_t x = (uint32_t)sbv[min(ov, last)] | sbv[min(ov + 1u, last)] | sbv[min(ov + 2u, last)] |
+                         sbv[min(ov + 3u, last)];
+      vcode = nv ? x : 0u;
+    }
+    if (nsys && nst) {
+      const uint32_t last = min(os + (ns ? ns - 1u : 0u), KPE_STAGE_SMALL - 1u);
+      const uint32_t x = (uint32_t)sbs[min(os, last)] | sbs[min(os + 1u, last)];
+      scode = ns ? x : 0u;
+    }
+    if (npann && nat) {
+      const uint32_t last = min(oa + (na ? na - 1u : 0u), KPE_STAGE_SMALL - 1u);
+      const uint32_t x = (uint32_t)sba[min(oa, last)] | sba[min(oa + 1u, last)];
+      acode = na ? x : 0u;
+    }
+    // ---- pods with more items than that, or a tile whose items overflow the staging area:
+    // recomputed over all their items (staged ones from LDS, the rest loaded) ----
+    const bool tile_over = nct > KPE_STAGE_CTR || (nvol && nvt > KPE_STAGE_VOL) || (nsys && nst > KPE_STAGE_SMALL) ||
+                           (npann && nat > KPE_STAGE_SMALL);
+    const bool more_c = nc > 4u, more_v = nvol && nv > 4u, more_s = nsys && ns > 2u, more_a = npann && na > 2u;
+    if (tile_over || __builtin_amdgcn_ballot_w64(more_c || more_v || more_s || more_a)) {
+      if (more_c || (tile_over && oc + nc > KPE_STAGE_CTR)) {
+        xo = co = 0;
+        for (uint32_t k = oc; k < oc + nc; ++k) {
+          const uint2 e = k < KPE_STAGE_CTR ? sc[k] : ctr_code(bload2(L.crec, (C0 + k) * 8u));
+          xo |= e.x, co |= e.y;
+        }
+      }
+      if (nvol && (more_v || (tile_over && ov + nv > KPE_STAGE_VOL))) {
+        vcode = 0;
+        for (uint32_t k = ov; k < ov + nv; ++k)
+          vcode |= k < KPE_STAGE_VOL ? (uint32_t)sbv[k] : vol_code(bload1(L.vol, (V0 + k) * 4u));
+      }
+      if (nsys && (more_s || (tile_over && os + ns > KPE_STAGE_SMALL))) {
+        scode = 0;
+        for (uint32_t k = os; k < os + ns; ++k)
+          scode |= k < KPE_STAGE_SMALL ? (uint32_t)sbs[k] : sys_code(bload1(L.sys, (S0 + k) * 4u));
+      }
+      if (npann && (more_a || (tile_over && oa + na > KPE_STAGE_SMALL))) {
+        acode = 0;
+        for (uint32_t k = oa; k < oa + na; ++k)
+          acode |= k < KPE_STAGE_SMALL ? (uint32_t)sba[k] : ann_code(bload2(L.ann, (A0 + k) * 8u));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    // ---- PSA checks, rule match (kind table), verdict bytes stored straight from the lane ----
+    const uint32_t pw = cur.rec.x;
+    const uint32_t fails = cv_fails(pw, xo, co & 7u, false, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & cv_union;
+    const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
+    const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
+    const uint32_t matched = dyn[kt + GVK_KIND(cur.rec.y)];
+    uint32_t failr;
+    if (ncls == 1u) {
+      failr = (fails & cls_cv0) ? cls_rm0 : 0u;
+    } else {
+      failr = 0;
+#pragma unroll 1
+      for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+    }
+    const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
+    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);  // F|E = PENDING
+    const uint32_t P = matched & pss_rules & ~failr & ~E;
+    if (live && !(KPE_DIAG & DIAG_NOSTORE)) {
+      uint8_t* row = verdicts + (size_t)r * R;
+#pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri)
+        row[ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  while (tile < ntiles) {  // three rotating buffers: (evaluate, load two ahead)
+    step(ta, tc);
+    tile += W;
+    if (tile >= ntiles) break;
+    step(tb, ta);
+    tile += W;
+    if (tile >= ntiles) break;
+    step(tc, tb);
+    tile += W;
+  }
+}
