@@ -15,7 +15,7 @@ tail -1 gpurun_out/bench_c2_old.log | cut -c 560-900
 [ -n "$SKIP_PAT" ] && exit 0
 for c in c5 c3; do
   timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/bench_$c.log 2>&1 || exit $?
-  echo "$c 2D: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/bench_$c.log | head -1)"
-  KPE_PAT_ROWS=1 timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/bench_${c}_rows.log 2>&1 || exit $?
-  echo "$c rows: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/bench_${c}_rows.log | head -1)"
+  echo "$c rows: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/bench_$c.log | head -1)"
+  KPE_PAT_CELLS=1 timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/bench_${c}_cells.log 2>&1 || exit $?
+  echo "$c cells: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/bench_${c}_cells.log | head -1)"
 done
