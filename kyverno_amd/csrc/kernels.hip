@@ -159,40 +159,45 @@ constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u
 __device__ __forceinline__ uint32_t cv_fails(uint32_t pw, uint32_t xo, uint32_t co, bool sec_ann_bad,
                                              bool vol_hostpath, bool vol_restricted, uint32_t sys_bad,
                                              bool apparmor_bad, bool sec_pod_ann_bad) {
+  // Branch-free: every condition is a 0/1 value combined with & and | (no short circuit), so the
+  // whole function is selects and shifts on the lane.
+  auto on = [](uint32_t c, uint32_t cv) -> uint32_t { return (c ? 1u : 0u) << cv; };
+  const uint32_t nwin = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS ? 0u : ~0u;
   uint32_t f = 0;
-  const bool win = FIELD(pw, P_OS_SH, 2) == OS_WINDOWS;
-  const uint32_t nwin = win ? 0u : ~0u;
   // allowPrivilegeEscalation: some container whose APE is unset (or SC nil) or true
-  if (xo & (CX_APE_T | CX_APE_U)) f |= (1u << CV_APE_1_8) | ((1u << CV_APE_1_25) & nwin);
-  if (apparmor_bad) f |= 1u << CV_APPARMOR_1_0;
-  if (co & CS_BASE) f |= 1u << CV_CAPS_BASELINE_1_0;
-  if (co & (CS_DROP | CS_ADD)) f |= (1u << CV_CAPS_RESTRICTED_1_22) | ((1u << CV_CAPS_RESTRICTED_1_25) & nwin);
-  if (pw & (P_HOSTNET | P_HOSTPID | P_HOSTIPC)) f |= 1u << CV_HOST_NS_1_0;
-  if (vol_hostpath) f |= 1u << CV_HOST_PATH_1_0;
-  if (xo & CX_HOSTPORT) f |= 1u << CV_HOST_PORTS_1_0;
-  if (xo & CX_PRIV_T) f |= 1u << CV_PRIVILEGED_1_0;
-  if (xo & CX_PM_OTHER) f |= 1u << CV_PROC_MOUNT_1_0;
-  if (vol_restricted) f |= 1u << CV_RESTRICTED_VOLUMES_1_0;
+  f |= (xo & (CX_APE_T | CX_APE_U)) ? (1u << CV_APE_1_8) | ((1u << CV_APE_1_25) & nwin) : 0u;
+  f |= on(apparmor_bad, CV_APPARMOR_1_0);
+  f |= on(co & CS_BASE, CV_CAPS_BASELINE_1_0);
+  f |= (co & (CS_DROP | CS_ADD)) ? (1u << CV_CAPS_RESTRICTED_1_22) | ((1u << CV_CAPS_RESTRICTED_1_25) & nwin) : 0u;
+  f |= on(pw & (P_HOSTNET | P_HOSTPID | P_HOSTIPC), CV_HOST_NS_1_0);
+  f |= on(vol_hostpath, CV_HOST_PATH_1_0);
+  f |= on(xo & CX_HOSTPORT, CV_HOST_PORTS_1_0);
+  f |= on(xo & CX_PRIV_T, CV_PRIVILEGED_1_0);
+  f |= on(xo & CX_PM_OTHER, CV_PROC_MOUNT_1_0);
+  f |= on(vol_restricted, CV_RESTRICTED_VOLUMES_1_0);
   const uint32_t prnr = FIELD(pw, P_RNR_SH, 2);
-  if (prnr == TRI_FALSE || (xo & CX_RNR_F) || (prnr != TRI_TRUE && (xo & CX_RNR_U)))
-    f |= 1u << CV_RUN_AS_NON_ROOT_1_0;
-  if (FIELD(pw, P_RAU_SH, 2) == RAU_ZERO || (xo & CX_RAU_Z)) f |= 1u << CV_RUN_AS_USER_1_23;
+  f |= on((uint32_t)(prnr == TRI_FALSE) | (uint32_t)((xo & CX_RNR_F) != 0u) |
+              ((uint32_t)(prnr != TRI_TRUE) & (uint32_t)((xo & CX_RNR_U) != 0u)),
+          CV_RUN_AS_NON_ROOT_1_0);
+  f |= on((uint32_t)(FIELD(pw, P_RAU_SH, 2) == RAU_ZERO) | (uint32_t)((xo & CX_RAU_Z) != 0u), CV_RUN_AS_USER_1_23);
   const uint32_t psel = FIELD(pw, P_SEL_SH, 3);
-  if ((psel != SEL_NONE && (psel == SEL_OTHER || (pw & (P_SEL_USER | P_SEL_ROLE)))) ||
-      (xo & (CX_SEL_OTHER | CX_SEL_USER | CX_SEL_ROLE)))
-    f |= 1u << CV_SELINUX_1_0;
-  if (sec_pod_ann_bad || sec_ann_bad) f |= 1u << CV_SECCOMP_BASELINE_1_0;
+  f |= on(((uint32_t)(psel != SEL_NONE) &
+           ((uint32_t)(psel == SEL_OTHER) | (uint32_t)((pw & (P_SEL_USER | P_SEL_ROLE)) != 0u))) |
+              (uint32_t)((xo & (CX_SEL_OTHER | CX_SEL_USER | CX_SEL_ROLE)) != 0u),
+          CV_SELINUX_1_0);
+  f |= on((uint32_t)sec_pod_ann_bad | (uint32_t)sec_ann_bad, CV_SECCOMP_BASELINE_1_0);
+  // pod seccomp type: valid = RuntimeDefault | Localhost, bad = set and not valid
   const uint32_t psec = FIELD(pw, P_SECCOMP_SH, 3);
-  const bool psec_valid = psec == SECCOMP_RUNTIMEDEFAULT || psec == SECCOMP_LOCALHOST;
-  const bool psec_bad = psec != SECCOMP_NONE && !psec_valid;
-  const bool csec_bad = xo & (CX_SEC_UNC | CX_SEC_OTHER);
-  if (psec_bad || csec_bad) f |= 1u << CV_SECCOMP_BASELINE_1_19;
-  if (psec_bad || csec_bad || (!psec_valid && (xo & CX_SEC_NONE)))
-    f |= (1u << CV_SECCOMP_RESTRICTED_1_19) | ((1u << CV_SECCOMP_RESTRICTED_1_25) & nwin);
-  if (sys_bad & 1u) f |= 1u << CV_SYSCTLS_1_0;
-  if (sys_bad & 2u) f |= 1u << CV_SYSCTLS_1_27;
-  if (sys_bad & 4u) f |= 1u << CV_SYSCTLS_1_29;
-  if (FIELD(pw, P_WHP_SH, 2) == TRI_TRUE || (xo & CX_WHP_T)) f |= 1u << CV_WIN_HOST_PROCESS_1_0;
+  constexpr uint32_t kSecValid = (1u << SECCOMP_RUNTIMEDEFAULT) | (1u << SECCOMP_LOCALHOST);
+  constexpr uint32_t kSecBad = 0xFFu & ~kSecValid & ~(1u << SECCOMP_NONE);
+  const uint32_t psec_valid = (kSecValid >> psec) & 1u, psec_bad = (kSecBad >> psec) & 1u;
+  const uint32_t sec_b = psec_bad | (uint32_t)((xo & (CX_SEC_UNC | CX_SEC_OTHER)) != 0u);
+  f |= on(sec_b, CV_SECCOMP_BASELINE_1_19);
+  f |= (sec_b | ((psec_valid ^ 1u) & (uint32_t)((xo & CX_SEC_NONE) != 0u)))
+           ? (1u << CV_SECCOMP_RESTRICTED_1_19) | ((1u << CV_SECCOMP_RESTRICTED_1_25) & nwin)
+           : 0u;
+  f |= on(sys_bad & 1u, CV_SYSCTLS_1_0) | on(sys_bad & 2u, CV_SYSCTLS_1_27) | on(sys_bad & 4u, CV_SYSCTLS_1_29);
+  f |= on((uint32_t)(FIELD(pw, P_WHP_SH, 2) == TRI_TRUE) | (uint32_t)((xo & CX_WHP_T) != 0u), CV_WIN_HOST_PROCESS_1_0);
   return f;
 }
 
@@ -1118,7 +1123,7 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipSt
 namespace {
 typedef void (*ScanFn)(const ScanArgs*);
 ScanFn scan_fn(int pss, int narrow) {
-  if (pss && narrow == 3) return nullptr;  // kpe_lean_kernel (by-value arguments): see scan_occupancy
+  if (pss && narrow >= 3) return nullptr;  // kpe_lean_kernel / kpe_lean3_kernel (by-value arguments)
   if (pss && narrow == 2) return kpe_scan_kernel<true, true, false, true>;
   if (pss) return narrow ? kpe_scan_kernel<true, true, false> : kpe_scan_kernel<true, false, false>;
   return narrow ? kpe_scan_kernel<false, true, false> : kpe_scan_kernel<false, false, false>;
@@ -1133,6 +1138,10 @@ ScanFn prep_fn(int pss, int narrow) {
 // capped by the number of 256-resource tiles.
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes) {
   if (n <= 0) return 0;
+  if (pss && narrow == 4) {  // kpe_lean3_kernel: KPE_LEAN_T tiles of 64 rows per wave, no persistent loop
+    const int64_t waves = ((n + 63) / 64 + KPE_LEAN_T - 1) / KPE_LEAN_T;
+    return (uint32_t)((waves + kBlock / 64 - 1) / (kBlock / 64));
+  }
   static thread_local int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1158,6 +1167,10 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
     hipLaunchKernelGGL(kpe_lean_kernel, dim3(grid), dim3(kBlock), dyn_bytes, s, *hargs);
     return hipGetLastError();
   }
+  if (pss && narrow == 4) {
+    hipLaunchKernelGGL(kpe_lean3_kernel, dim3(grid), dim3(kBlock), dyn_bytes, s, *hargs);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
   return hipGetLastError();
 }
@@ -1178,6 +1191,43 @@ extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const 
   if (cells == 0) return hipSuccess;
   hipLaunchKernelGGL(kpe_fill_rows_kernel, dim3((unsigned)((cells + 255) / 256)), dim3(256), 0, s, verdicts, R, rows,
                      nrows, value);
+  return hipGetLastError();
+}
+// applyRules: One (pkg/engine/validation.go:75-77: stop after the first rule whose response is
+// pass or fail, RulesAppliedCount) over the final verdicts: cells after an applied rule of the
+// policy give no response; after an undecided cell they are undecided (unless unmatched).
+__global__ void __launch_bounds__(256) kpe_apply_one_kernel(uint8_t* verdicts, uint32_t* masks, uint32_t n, uint32_t R,
+                                                            const uint2* segs, uint32_t nsegs) {
+  const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+  if (r >= n) return;
+  uint8_t* row = verdicts + (size_t)r * R;
+#pragma unroll 1
+  for (uint32_t s = 0; s < nsegs; ++s) {
+    const uint2 sg = segs[s];
+    uint32_t state = 0;  // 0 open, 1 applied, 2 an earlier cell undecided
+#pragma unroll 1
+    for (uint32_t i = sg.x; i < sg.y; ++i) {
+      const uint32_t v = row[i];
+      if (state == 1u) {
+        if (v != KPE_NA_) {
+          row[i] = KPE_NA_;
+          if (masks) masks[(size_t)r * R + i] = 0u;
+        }
+      } else if (state == 2u) {
+        if (v != KPE_NA_) row[i] = KPE_UNDECIDED_;
+      } else if (v == KPE_PASS_ || v == KPE_FAIL_) {
+        state = 1u;
+      } else if (v == KPE_UNDECIDED_) {
+        state = 2u;
+      }
+    }
+  }
+}
+extern "C" hipError_t kpe_launch_apply_one(uint8_t* verdicts, uint32_t* masks, int64_t n, uint32_t R, const uint32_t* segs,
+                                           uint32_t nsegs, hipStream_t s) {
+  if (n <= 0 || nsegs == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_apply_one_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, verdicts, masks,
+                     (uint32_t)n, R, reinterpret_cast<const uint2*>(segs), nsegs);
   return hipGetLastError();
 }
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,

@@ -34,6 +34,8 @@ extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const 
                                            uint8_t value, hipStream_t s);
 extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
 extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_apply_one(uint8_t* verdicts, uint32_t* masks, int64_t n, uint32_t R, const uint32_t* segs,
+                                           uint32_t nsegs, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* hargs, int64_t n, int pss, int narrow,
                                       uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
@@ -151,6 +153,8 @@ struct DeviceProgram {
 struct Binding {  // program x corpus (dictionary sizes decide predicate placement)
   const Program* prog = nullptr;
   DevBuf jobs, pbuf, verdicts, masks, counts_out;
+  DevBuf apply_segs;  // ApplyOne policies' rule ranges (uint2 r0, r1)
+  uint32_t napply_segs = 0;
   DevBuf dargs;        // device copy of the scan arguments (kernel reads them with scalar loads)
   DevBuf zero_page;    // 256 zero bytes (loads of columns a program does not read)
   DevBuf fuse;         // fused dictionary pass image (pairs, patterns, small dictionaries)
@@ -442,7 +446,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     uint32_t prev_policy = 0xFFFFFFFFu;
     for (auto& r : P.rules) {
       uint32_t x = r.handler | r.match_mode << 4 | r.excl_mode << 6;
-      if (r.apply_one) x |= NR_APPLY_ONE;
+      // ApplyOne runs after every evaluation kernel (kpe_apply_one_kernel), not in the scan
       if (r.policy != prev_policy) x |= NR_NEW_POLICY;
       prev_policy = r.policy;
       if (r.pol_term >= 0) x |= ((uint32_t)r.pol_term + 1u) << 16;
@@ -452,8 +456,8 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
       nrules.push_back(r.excl_f0 | r.excl_nf << 24);
     }
   }
-  // truth-table fast path: few terms, no ApplyOne; per PSS version set its rule mask
-  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_apply_one && !P.any_const;
+  // truth-table fast path: few terms; per PSS version set its rule mask
+  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_const;
   std::vector<uint32_t> cls;  // (cv_mask, rule mask) pairs
   uint32_t pss_rules = 0, err_rules = 0, pat_rules = 0;
   if (tt) {
@@ -877,9 +881,20 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
                              (uint64_t)C.c_sc.size() * 8 > lim || (uint64_t)C.vol_src.size() * 4 > lim ||
                              (uint64_t)C.sys_id.size() * 4 > lim || (uint64_t)C.pann_kv.size() * 4 > lim)
                                 ? 2
-                                : 3;
+                                : getenv("KPE_LEAN_PERSIST") ? 3 : 4;
   B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
+  {  // ApplyOne policies: contiguous rule ranges in ComputeRules order
+    std::vector<uint32_t> segs;
+    for (size_t r = 0; r < P.rules.size();) {
+      size_t e = r + 1;
+      while (e < P.rules.size() && P.rules[e].policy == P.rules[r].policy) ++e;
+      if (P.rules[r].apply_one && e - r > 1) segs.push_back((uint32_t)r), segs.push_back((uint32_t)e);
+      r = e;
+    }
+    B.napply_segs = (uint32_t)(segs.size() / 2);
+    if (!segs.empty()) HIPCHK(upload(B.apply_segs, segs, s));
+  }
   HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
   HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 8, 1) * 8));
   if (!B.zero_page.p) {
@@ -1001,7 +1016,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.cv_classes = B.cv_classes.as<uint32_t>();
   sa.nterms = (uint32_t)P.terms.size();
   sa.ncv = (uint32_t)P.cv_classes.size();
-  sa.any_apply_one = P.any_apply_one ? 1u : 0u;
+  sa.any_apply_one = 0u;  // ApplyOne: kpe_apply_one_kernel after every evaluation kernel
   sa.filt_lds = B.filt_lds;
   sa.fterm_lds = B.fterm_lds;
   sa.nfterms = (uint32_t)P.fterms.size();
@@ -1176,6 +1191,9 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       fprintf(stderr, "kpe patvm err=0x%x\n", e);
     }
   }
+  if (B.napply_segs)  // applyRules: One (validation.go:75-77) over the final verdicts of every kernel
+    HIPCHK(kpe_launch_apply_one(B.verdicts.as<uint8_t>(), masks ? B.masks.as<uint32_t>() : nullptr, C.n, (uint32_t)R,
+                                B.apply_segs.as<uint32_t>(), B.napply_segs, s));
   if (!C.limit_rows.empty())  // last: no later kernel may resolve these cells
     HIPCHK(kpe_launch_fill_rows(B.verdicts.as<uint8_t>(), (uint32_t)R, D.limit_rows.as<uint32_t>(),
                                 (uint32_t)C.limit_rows.size(), KPE_UNDECIDED_, s));

@@ -276,3 +276,208 @@ __global__ void __launch_bounds__(kBlock, KPE_LEAN2_WAVES) kpe_lean_kernel(ScanA
     tile += W;
   }
 }
+
+// ---- kpe_lean3_kernel: the same scan, non-persistent, every load of a wave issued up front ----
+// Each wave evaluates KPE_LEAN_T consecutive tiles. One load brings the header words of all of
+// them (lane k < 4T + 4: word k of tile t0 + k / 4), the pod records are issued before that
+// header arrives and the list items of all T tiles right after it, so a wave has one dependent
+// load step (header -> items) and then only evaluation; tile j waits for its own loads alone.
+// The grid covers the tiles (no persistent loop): the dispatcher starts a wave as soon as an
+// earlier one retires, which keeps every CU's memory pipeline full across waves.
+#ifndef KPE_LEAN_T
+#define KPE_LEAN_T 1
+#endif
+struct LeanItems {
+  uint4 rec;
+  uint2 c0, c1, q0;
+  uint32_t v0, v1, s0;
+};
+__global__ void __launch_bounds__(kBlock, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArgs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  if (KPE_DIAG & DIAG_EMPTY) return;
+  CArgs& a0 = *kargs();
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
+  const uint32_t t0 = (blockIdx.x * (kBlock / 64u) + wv) * KPE_LEAN_T;
+  const uint32_t need = a0.need;
+  LeanCols L;
+  L.rec = make_rsrc(a0.rec, n * 16u);
+  L.hdr = make_rsrc(a0.hdr, (ntiles + 1u) * 16u);
+  L.crec = make_rsrc(a0.crec, a0.nctr_total * 8u);
+  L.vol = make_rsrc(a0.vol_src, (need & NEED_VOL) ? a0.nvol_total * 4u : 0u);
+  L.sys = make_rsrc(a0.sys_id, (need & NEED_SYS) ? a0.nsys_total * 4u : 0u);
+  L.ann = make_rsrc(a0.pann_kv, (need & NEED_PANN) ? a0.npann_total * 8u : 0u);
+  const bool nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN;
+
+  // header words of tiles t0 .. t0 + T (past the last header: 0), image, pod records, items
+  const uint32_t hall = bload1(L.hdr, (t0 * 4u + min(lane, 4u * KPE_LEAN_T + 3u)) * 4u);
+  const uint32_t img_n4 = a0.pimg_words >> 2;
+  const uint4* img = reinterpret_cast<const uint4*>(a0.pimg);
+  const uint4 img0 = img[min(t, img_n4 - 1u)];
+  uint32_t cls_cv = 0, cls_rm = 0;
+  if (lane < a0.ncls) {
+    const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
+    cls_cv = c.x, cls_rm = c.y;
+  }
+  LeanItems it[KPE_LEAN_T];
+#pragma unroll
+  for (uint32_t j = 0; j < KPE_LEAN_T; ++j) it[j].rec = bload4(L.rec, ((t0 + j) * 64u + lane) * 16u);
+#pragma unroll
+  for (uint32_t j = 0; j < KPE_LEAN_T; ++j) {
+    const uint32_t C0 = hw(hall, 4u * j), V0 = hw(hall, 4u * j + 1u), S0 = hw(hall, 4u * j + 2u),
+                   A0 = hw(hall, 4u * j + 3u);
+    it[j].c0 = bload2(L.crec, (C0 + lane) * 8u);
+    it[j].c1 = bload2(L.crec, (C0 + 64u + lane) * 8u);
+    it[j].v0 = bload1(L.vol, (V0 + lane) * 4u);
+    it[j].v1 = bload1(L.vol, (V0 + 64u + lane) * 4u);
+    it[j].s0 = bload1(L.sys, (S0 + lane) * 4u);
+    it[j].q0 = bload2(L.ann, (A0 + lane) * 8u);
+  }
+  {
+    uint4* d4 = reinterpret_cast<uint4*>(dyn);
+    if (t < img_n4) d4[t] = img0;
+#pragma unroll 1
+    for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
+  }
+  __syncthreads();
+  if (KPE_DIAG & DIAG_NOLOOP) {
+    if (t0 < ntiles && lane == 0) a0.verdicts[t0] = (uint8_t)(dyn[0] + it[0].rec.x + it[0].c0.x);
+    return;
+  }
+  const uint8_t* s_capb = reinterpret_cast<const uint8_t*>(dyn + a0.capb_lds);
+  const LdsPtr lds = (LdsPtr)dyn;
+  const uint32_t p_sann = a0.pp_seccomp_ann_ok & ~PRED_LOCAL, p_aak = a0.pp_apparmor_key & ~PRED_LOCAL,
+                 p_aao = a0.pp_apparmor_ok & ~PRED_LOCAL, p_spk = a0.pp_seccomp_pod_key & ~PRED_LOCAL,
+                 p_s0 = a0.pp_sysctl0 & ~PRED_LOCAL, p_s1 = a0.pp_sysctl1 & ~PRED_LOCAL,
+                 p_s2 = a0.pp_sysctl2 & ~PRED_LOCAL;
+  auto pbit = [&](uint32_t loc, uint32_t id) -> uint32_t { return (lds[loc + (id >> 5)] >> (id & 31u)) & 1u; };
+  const uint32_t kt = a0.kt_lds;
+  const uint32_t R = a0.nrules, cv_union = a0.cv_union, pss_rules = a0.pss_rules, ncls = a0.ncls;
+  const uint32_t ep_rules = a0.err_rules | a0.pat_rules, pat_rules = a0.pat_rules;
+  uint8_t* const verdicts = a0.verdicts;
+  uint32_t* const stage = dyn + a0.wave_lds + wv * a0.wave_words;
+  const uint32_t cls_cv0 = hw(cls_cv, 0), cls_rm0 = hw(cls_rm, 0);
+#pragma unroll
+  for (uint32_t j = 0; j < KPE_LEAN_T; ++j) {
+    const uint32_t tile = t0 + j;
+    if (tile >= ntiles) break;
+    const LeanItems& cur = it[j];
+    const uint32_t C0 = hw(hall, 4u * j), V0 = hw(hall, 4u * j + 1u), S0 = hw(hall, 4u * j + 2u),
+                   A0 = hw(hall, 4u * j + 3u);
+    const uint32_t nct = hw(hall, 4u * j + 4u) - C0, nvt = hw(hall, 4u * j + 5u) - V0,
+                   nst = hw(hall, 4u * j + 6u) - S0, nat = hw(hall, 4u * j + 7u) - A0;
+    const uint32_t r = tile * 64u + lane;
+    const bool live = r < n;
+    if (KPE_DIAG & DIAG_NOPSS) {
+      if (live)
+        verdicts[(size_t)r * R] =
+            (uint8_t)(cur.rec.x ^ cur.rec.z ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.v1 ^ cur.s0 ^ cur.q0.x ^ nct);
+      continue;
+    }
+    const uint32_t z = cur.rec.z;
+    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+    uint32_t oc, ov, os, oa;
+    if ((nct | nvt | nst | nat) < 256u) {  // one scan of the four packed byte counts (no carries)
+      const uint32_t e = wave_incl_scan(z) - z;
+      oc = e & 0xFFu, ov = (e >> 8) & 0xFFu, os = (e >> 16) & 0xFFu, oa = e >> 24;
+    } else {
+      const uint32_t c01 = nc | (nv << 16), c23 = ns | (na << 16);
+      const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
+      oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
+    }
+    uint2* sc = reinterpret_cast<uint2*>(stage);
+    uint8_t* sbv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_CTR * 2);
+    uint8_t* sbs = sbv + KPE_STAGE_VOL;
+    uint8_t* sba = sbs + KPE_STAGE_SMALL;
+    auto ctr_code = [&](uint2 e) { return make_uint2(e.x, (uint32_t)s_capb[CY_CAPSET(e.y)]); };
+    auto vol_code = [&](uint32_t sv0) -> uint32_t { return ((sv0 >> VS_HOSTPATH) & 1u) | ((sv0 & kAllowedVolumes) ? 0u : 2u); };
+    auto sys_code = [&](uint32_t id) -> uint32_t {
+      return (pbit(p_s0, id) ^ 1u) | ((pbit(p_s1, id) ^ 1u) << 1) | ((pbit(p_s2, id) ^ 1u) << 2);
+    };
+    auto ann_code = [&](uint2 kv) -> uint32_t {
+      return (pbit(p_aak, kv.x) & (pbit(p_aao, kv.y) ^ 1u)) | ((pbit(p_spk, kv.x) & (pbit(p_sann, kv.y) ^ 1u)) << 1);
+    };
+    sc[lane] = ctr_code(cur.c0);
+    sc[lane + 64u] = ctr_code(cur.c1);
+    if (nvol) sbv[lane] = (uint8_t)vol_code(cur.v0), sbv[lane + 64u] = (uint8_t)vol_code(cur.v1);
+    if (nsys && nst) sbs[lane] = (uint8_t)sys_code(cur.s0);
+    if (npann && nat) sba[lane] = (uint8_t)ann_code(cur.q0);
+    __builtin_amdgcn_wave_barrier();
+    uint32_t xo, co, vcode = 0, scode = 0, acode = 0;
+    {
+      const uint32_t last = min(oc + (nc ? nc - 1u : 0u), KPE_STAGE_CTR - 1u);
+      const uint2 e0 = sc[min(oc, last)], e1 = sc[min(oc + 1u, last)], e2 = sc[min(oc + 2u, last)],
+                  e3 = sc[min(oc + 3u, last)];
+      const uint32_t m = nc ? ~0u : 0u;
+      xo = (e0.x | e1.x | e2.x | e3.x) & m;
+      co = (e0.y | e1.y | e2.y | e3.y) & m;
+    }
+    if (nvol) {
+      const uint32_t last = min(ov + (nv ? nv - 1u : 0u), KPE_STAGE_VOL - 1u);
+      const uint32_t x = (uint32_t)sbv[min(ov, last)] | sbv[min(ov + 1u, last)] | sbv[min(ov + 2u, last)] |
+                         sbv[min(ov + 3u, last)];
+      vcode = nv ? x : 0u;
+    }
+    if (nsys && nst) {
+      const uint32_t last = min(os + (ns ? ns - 1u : 0u), KPE_STAGE_SMALL - 1u);
+      const uint32_t x = (uint32_t)sbs[min(os, last)] | sbs[min(os + 1u, last)];
+      scode = ns ? x : 0u;
+    }
+    if (npann && nat) {
+      const uint32_t last = min(oa + (na ? na - 1u : 0u), KPE_STAGE_SMALL - 1u);
+      const uint32_t x = (uint32_t)sba[min(oa, last)] | sba[min(oa + 1u, last)];
+      acode = na ? x : 0u;
+    }
+    const bool tile_over = nct > KPE_STAGE_CTR || (nvol && nvt > KPE_STAGE_VOL) || (nsys && nst > KPE_STAGE_SMALL) ||
+                           (npann && nat > KPE_STAGE_SMALL);
+    const bool more_c = nc > 4u, more_v = nvol && nv > 4u, more_s = nsys && ns > 2u, more_a = npann && na > 2u;
+    if (tile_over || __builtin_amdgcn_ballot_w64(more_c || more_v || more_s || more_a)) {
+      if (more_c || (tile_over && oc + nc > KPE_STAGE_CTR)) {
+        xo = co = 0;
+        for (uint32_t k = oc; k < oc + nc; ++k) {
+          const uint2 e = k < KPE_STAGE_CTR ? sc[k] : ctr_code(bload2(L.crec, (C0 + k) * 8u));
+          xo |= e.x, co |= e.y;
+        }
+      }
+      if (nvol && (more_v || (tile_over && ov + nv > KPE_STAGE_VOL))) {
+        vcode = 0;
+        for (uint32_t k = ov; k < ov + nv; ++k)
+          vcode |= k < KPE_STAGE_VOL ? (uint32_t)sbv[k] : vol_code(bload1(L.vol, (V0 + k) * 4u));
+      }
+      if (nsys && (more_s || (tile_over && os + ns > KPE_STAGE_SMALL))) {
+        scode = 0;
+        for (uint32_t k = os; k < os + ns; ++k)
+          scode |= k < KPE_STAGE_SMALL ? (uint32_t)sbs[k] : sys_code(bload1(L.sys, (S0 + k) * 4u));
+      }
+      if (npann && (more_a || (tile_over && oa + na > KPE_STAGE_SMALL))) {
+        acode = 0;
+        for (uint32_t k = oa; k < oa + na; ++k)
+          acode |= k < KPE_STAGE_SMALL ? (uint32_t)sba[k] : ann_code(bload2(L.ann, (A0 + k) * 8u));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t pw = cur.rec.x;
+    const uint32_t fails = cv_fails(pw, xo, co & 7u, false, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & cv_union;
+    const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
+    const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
+    const uint32_t matched = dyn[kt + GVK_KIND(cur.rec.y)];
+    uint32_t failr;
+    if (ncls == 1u) {
+      failr = (fails & cls_cv0) ? cls_rm0 : 0u;
+    } else {
+      failr = 0;
+#pragma unroll 1
+      for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+    }
+    const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
+    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
+    const uint32_t P = matched & pss_rules & ~failr & ~E;
+    if (live && !(KPE_DIAG & DIAG_NOSTORE)) {
+      uint8_t* row = verdicts + (size_t)r * R;
+#pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri)
+        row[ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}

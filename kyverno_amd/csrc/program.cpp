@@ -2058,8 +2058,6 @@ class Lowerer {
         if (ex->t != JV::Arr) throw CompileError("rule '" + rname + "': podSecurity.exclude is not a list");
         if (!ex->a.empty()) {
           pss_excl = true;
-          if (apply_one)
-            throw CompileError("rule '" + rname + "': applyRules=One with podSecurity.exclude is not supported");
           pss_exclusions(*ex, (uint32_t)P.rules.size(), k.cv_mask, rname);
         }
       }
@@ -2090,7 +2088,6 @@ class Lowerer {
       } else if (pre == F_FALSE && (present("pattern") || present("anyPattern"))) {
         k.handler = H_CONST_SKIP;  // patterns are never evaluated
       } else if (present("pattern") || present("anyPattern")) {
-        if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with pattern rules is not supported");
         pc::PatCompiler pcomp(P.pat, [&](const std::string& g) {
           const int32_t id = pred(D_KEY, {g});
           P.preds[id].global_only = true;
@@ -2161,10 +2158,7 @@ class Lowerer {
       k.handler = H_COND;  // matched cells need the preconditions' skip / error
       crule.kind = CR_NONE;
     }
-    if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) {
-      if (apply_one) throw CompileError("rule '" + rname + "': applyRules=One with conditions is not supported");
-      P.any_const = true;
-    }
+    if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) P.any_const = true;
     if (pre_block != CE_NONE || k.handler == H_COND) P.cond.rules.push_back(crule);
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);

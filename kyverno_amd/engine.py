@@ -198,7 +198,8 @@ def synth_resources(seed: int, n: int, mix: int = 0, first_index: int = 0) -> by
     if L.kpe_synth_resources(seed, first_index, n, mix, ctypes.byref(p), ctypes.byref(ln)) != 0:
         raise KpeError(-1, "synth failed")
     try:
-        return ctypes.string_at(p, ln.value)
+        # string_at's size is a C int in Python 3.10: corpora past 2 GiB are copied by array
+        return bytes((ctypes.c_char * ln.value).from_address(p.value)) if ln.value else b""
     finally:
         L.kpe_synth_free(p)
 
@@ -211,7 +212,8 @@ def synth_ns_labels(seed: int, n_namespaces: int, mix: int = 0) -> bytes:
     if L.kpe_synth_ns_labels(seed, n_namespaces, mix, ctypes.byref(p), ctypes.byref(ln)) != 0:
         raise KpeError(-1, "synth failed")
     try:
-        return ctypes.string_at(p, ln.value)
+        # string_at's size is a C int in Python 3.10: corpora past 2 GiB are copied by array
+        return bytes((ctypes.c_char * ln.value).from_address(p.value)) if ln.value else b""
     finally:
         L.kpe_synth_free(p)
 

@@ -143,11 +143,58 @@ def test_unfoldable_compiled_per_resource(cond):
         K.PolicySet([pol])
 
 
-def test_apply_one_with_folded_refused():
-    pol = _policy("p", [_rule("a"), _rule("b")])
-    pol["spec"]["applyRules"] = "One"
-    with pytest.raises(K.KpeError):
-        K.PolicySet([pol])
+RES_COND = {"any": [{"key": "{{ request.object.spec.hostNetwork || `false` }}", "operator": "Equals",
+                     "value": True}]}
+
+
+def apply_one_policy_set():
+    """applyRules: One policies whose rules mix every handler the device has: constant (folded)
+    conditions, PSS with and without exclusions, patterns, resource-reading preconditions and
+    deny (validation.go:75-77 stops after the first pass / fail response)."""
+    one = []
+    one.append(_policy("one-folded", [_rule("a"), _rule("b", validate=PATTERN)]))
+    one.append(_policy("one-pattern-first", [
+        _rule("img", validate=PATTERN),
+        _rule("pss", validate={"podSecurity": {"level": "restricted", "version": "latest"}}),
+        _rule("deny", validate={"deny": {"conditions": RES_COND}})]))
+    one.append(_policy("one-cond-first", [
+        _rule("hostnet", pre=RES_COND, validate=PATTERN),
+        _rule("deny-hostnet", validate={"deny": {"conditions": RES_COND}}),
+        _rule("pss", validate={"podSecurity": {"level": "baseline", "version": "latest"}})]))
+    one.append(_policy("one-pssx", [
+        _rule("pss-excl", validate={"podSecurity": {"level": "baseline", "version": "latest", "exclude": [
+            {"controlName": "Host Namespaces"}, {"controlName": "Host Ports", "images": ["*nginx*"]}]}}),
+        _rule("img", validate=PATTERN),
+        _rule("pre-false", pre={"any": [{"key": OP, "operator": "Equals", "value": "DELETE"}]}, validate=PATTERN)]))
+    one.append(_policy("one-kinds", [
+        _rule("deploy-only", kinds=("Deployment",), validate=PATTERN),
+        _rule("pods", kinds=("Pod", "Deployment"), validate={"podSecurity": {"level": "restricted", "version": "v1.24"}}),
+        _rule("last", validate={"deny": {}})]))
+    for p in one:
+        p["spec"]["applyRules"] = "One"
+    return one
+
+
+def test_apply_one_compiles():
+    K.PolicySet(apply_one_policy_set())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mix,n,seed", [(0, 6000, 0xA1), (2, 6000, 0xA2)])
+def test_apply_one_bit_exact(oracle, mix, n, seed):
+    pols = apply_one_policy_set()
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(seed, n, mix=mix)
+    v, _, cnt = eng.evaluate(ps, K.Corpus(nd))
+    ref = oracle.validate(pols, nd, nthreads=8)
+    assert v.shape == ref.shape
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()} {v[tuple(bad[0])]} {ref[tuple(bad[0])]}"
+    # ApplyOne really cut rules: some row has a later rule without response after an applied one
+    assert ((v[:, 0] == 2) & (v[:, 1] == 0)).any() or ((v[:, 0] == 1) & (v[:, 1] == 0)).any()
+    for r in range(v.shape[1]):
+        assert cnt[r]["na"] == int((v[:, r] == 0).sum())
 
 
 @pytest.mark.gpu
