@@ -83,6 +83,19 @@ void kpe_device_close(kpe_device* dev);
  * applied (autogen.ComputeRules). Rules are laid out policy-major, in
  * ComputeRules order: column r of the verdict matrix is rule r. */
 kpe_status kpe_program_compile(const char* policies_json, size_t len, kpe_program** out);
+/* kpe_program_compile with PolicyExceptions (kyverno.io/v2beta1, api/kyverno/v2beta1/
+ * policy_exception_types.go; the exception lister of engine.NewEngine, pkg/engine/exceptions.go:12-35,
+ * consulted per rule at engine.go:286-293): exceptions_json is one PolicyException or a JSON array
+ * (NULL / 0: none). A matched cell of a rule an exception names (policyName = the policy key,
+ * ruleNames = go-wildcard globs) becomes KPE_SKIP when the exception's match block holds for the
+ * resource (pkg/engine/utils/exceptions.go:14-47, validate_resource.go:43-56, validate_pss.go:45-58).
+ * KPE_COMPILE_BACKGROUND drops exceptions with spec.background: false, as the background scanner's
+ * FetchPolicyExceptions does (pkg/controllers/report/utils/utils.go:113-124); kyverno apply uses
+ * every exception it is given. KPE_E_UNSUPPORTED: podSecurity exceptions, conditions that do not
+ * fold to true, rules whose preconditions read the resource. */
+#define KPE_COMPILE_BACKGROUND 1u
+kpe_status kpe_program_compile_ex(const char* policies_json, size_t len, const char* exceptions_json, size_t exc_len,
+                                  uint32_t flags, kpe_program** out);
 int kpe_program_num_rules(const kpe_program* prog);
 /* "<policy-name>/<rule-name>" of rule r (owned by prog). */
 const char* kpe_program_rule_name(const kpe_program* prog, int r);

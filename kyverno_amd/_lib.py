@@ -48,6 +48,7 @@ def load():
     L.kpe_device_open.argtypes = [i32, ctypes.POINTER(vp)]
     L.kpe_device_close.argtypes = [vp]
     L.kpe_program_compile.argtypes = [cp, sz, ctypes.POINTER(vp)]
+    L.kpe_program_compile_ex.argtypes = [cp, sz, cp, sz, ctypes.c_uint32, ctypes.POINTER(vp)]
     L.kpe_program_num_rules.argtypes = [vp]
     L.kpe_program_rule_name.argtypes = [vp, i32]
     L.kpe_program_rule_name.restype = cp

@@ -533,8 +533,8 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
       if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
       K = a.nsl_k, V = a.nsl_v;
       if (B.bit(S.p_kind_ns, kid)) {
-        ok = false, eval = false;
-      } else if (B.bit(S.p_kind_empty, kid) && !S.star_kind) {
+        ok = S.exc != 0u, eval = false;  // PolicyException blocks skip the check (match.go:184)
+      } else if (B.bit(S.p_kind_empty, kid) && (!S.star_kind || S.exc)) {
         ok = true, eval = false;
       } else if (S.invalid) {
         ok = false, eval = false;
@@ -889,7 +889,10 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         m = m && !block(NR_EXCL_MODE(x), RL_F0(nr.w), RL_NF(nr.w));
         const uint32_t hd = NR_HANDLER(x);
         uint32_t v = KPE_NA_;
-        if (m && hd == H_PSS) v = err ? KPE_ERROR_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
+        // PolicyExceptions of the rule: their match block holds => RuleSkip before any handler
+        const uint32_t xe = (m && a.rule_exc) ? sld(a.rule_exc, ri) : 0u;
+        if (xe && block((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe))) v = KPE_SKIP_;
+        else if (m && hd == H_PSS) v = err ? KPE_ERROR_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
         else if (m && hd == H_ERROR) v = KPE_ERROR_;
         else if (m && (hd == H_PATTERN || hd == H_COND)) v = KPE_PENDING_;
         else if (m && hd == H_CONST_SKIP) v = KPE_SKIP_;
@@ -967,6 +970,13 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
           fm = m;
         } else if (handler == H_CONST_PASS) {
           pm = m;
+        }
+        if (a.rule_exc && m) {  // PolicyExceptions: RuleSkip where their match block holds
+          const uint32_t xe = a.rule_exc[c0 + lane];
+          if (xe) {
+            const uint64_t xm = m & block_mask((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe));
+            pm |= xm, em |= xm, fm &= ~xm;
+          }
         }
         rmk[lane * 3 + 0] = pm;
         rmk[lane * 3 + 1] = fm;
@@ -1056,8 +1066,9 @@ namespace {
 // grid: x = 256-row blocks; y = 1 (one lane per row, every rule) or the pattern rules (one rule
 // per wave, KPE_PAT_CELLS)
 __global__ void __launch_bounds__(256) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
-  const int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (r >= ap->n) return;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= ap->n) return;
+  const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
   if (gridDim.y == 1 && ap->npr > 1) pat_eval_row(*ap, r);
   else pat_eval_cell(*ap, r, blockIdx.y);
 }
@@ -1074,8 +1085,8 @@ namespace {
 
 __global__ void __launch_bounds__(128) kpe_cond_kernel(const CondArgs* __restrict__ ap) {
   __shared__ char nb[128][2][16];
-  const int64_t r = (int64_t)blockIdx.x * 128 + threadIdx.x;
-  if (r < ap->n) cond_eval_row(*ap, r, nb[threadIdx.x]);
+  const int64_t i = (int64_t)blockIdx.x * 128 + threadIdx.x;
+  if (i < ap->n) cond_eval_row(*ap, ap->perm ? (int64_t)ap->perm[i] : i, nb[threadIdx.x]);
 }
 
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s) {

@@ -115,6 +115,7 @@ struct ScanArgs {
   const KpeRule* rules;
   const uint32_t* rule_lanes;  // packed rule lane records (RL_*)
   const uint32_t* narrow_rules;  // NARROW: 4 words per rule (NR_*)
+  const uint32_t* rule_exc;      // KpeRule::exc per rule (XE_*), or null: no PolicyExceptions
   const uint32_t* fmask;         // NARROW: term mask per filter
   uint32_t nfilters;
   // NARROW truth-table fast path (tt_lds != PRED_NONE: <= KPE_TT_TERMS terms, no ApplyOne):
@@ -170,6 +171,7 @@ struct PatArgs {
   uint32_t R, npr;                 // rules per row, pattern rules
   const uint32_t* doc;             // document tape (2 words per node)
   const uint64_t* doc_off;         // first node of each resource
+  const uint32_t* perm;            // lane -> row: rows by descending tape size (wave-uniform walk lengths)
   const KpeScalar* scal;
   const uint8_t* scal_text;
   const KpePNode* nodes;
@@ -195,6 +197,7 @@ struct CondArgs {
   uint32_t R, ncr;                 // rules per row, condition rules
   const uint32_t* doc;             // document tape (2 words per entry)
   const uint64_t* doc_off;         // root entry of each resource
+  const uint32_t* perm;            // lane -> row (PatArgs::perm)
   const KpeScalar* scal;
   const uint8_t* scal_text;
   const uint8_t* key_bytes;        // D_KEY dictionary (keys(@) results)

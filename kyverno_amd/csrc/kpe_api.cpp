@@ -135,6 +135,7 @@ struct kpe_device {
 namespace kpe {
 struct DeviceProgram {
   int ordinal = -1;
+  DevBuf rule_exc;  // KpeRule::exc per rule (PolicyExceptions)
   DevBuf rules, rule_lanes, narrow_rules, fmask, narrow_cls, filters, fterms, terms, kindsels, annpairs, selectors, selreqs,
       pat_bytes, pats;
   bool narrow = false;  // per-lane rule loop (kernels_abi.h NR_*)
@@ -198,6 +199,7 @@ struct DeviceCorpus {
   DevBuf lab_off, lab_k, lab_v, r_nsl, nsl_off, nsl_k, nsl_v;
   DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
   DevBuf doc, doc_off, scal, scal_text;  // document tape + scalar table (pattern rules)
+  DevBuf doc_perm;  // rows by descending tape size: the pattern / condition kernels' lane -> row map
   DevBuf limit_rows;                     // rows past a per-resource limit
   // cold pod columns, uploaded on the first binding of a program with podSecurity exclusions
   DevBuf ctr_off, vol_off, sys_off, pann_off, c_name, c_image, c_sann_key, c_sec_str, c_pm_str, c_selt_str, c_selu_str,
@@ -264,8 +266,12 @@ void kpe_device_close(kpe_device* d) {
 }
 
 kpe_status kpe_program_compile(const char* json, size_t len, kpe_program** out) {
+  return kpe_program_compile_ex(json, len, nullptr, 0, 0u, out);
+}
+kpe_status kpe_program_compile_ex(const char* json, size_t len, const char* exceptions, size_t exc_len, uint32_t flags,
+                                  kpe_program** out) {
   try {
-    auto p = kpe::compile_policies(json, len);
+    auto p = kpe::compile_policies(json, len, exceptions, exc_len, (flags & KPE_COMPILE_BACKGROUND) != 0u);
     *out = new kpe_program{std::move(p)};
     return KPE_OK;
   } catch (const kpe::CompileError& e) {
@@ -389,6 +395,21 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   if (C.has_docs) {
     HIPCHK(upload(D.doc, C.doc, s));
     HIPCHK(upload(D.doc_off, C.doc_off, s));
+    {  // A document walk's length follows its tape size (containers x pattern depth): lanes of a
+      // wave take rows of similar size, heaviest first, so a wave runs its mean walk, not its
+      // longest (1-64 containers per pod in C5). Counting sort, stable within a size.
+      constexpr uint64_t kMaxKey = 4095;
+      const uint64_t nd = C.doc.size() / 2;
+      std::vector<uint32_t> cnt(kMaxKey + 2, 0), perm(C.n);
+      auto key = [&](int64_t r) -> uint64_t {
+        const uint64_t b = C.doc_off[r], e = r + 1 < C.n ? C.doc_off[r + 1] : nd;
+        return kMaxKey - std::min<uint64_t>(e > b ? e - b : 0, kMaxKey);
+      };
+      for (int64_t r = 0; r < C.n; ++r) ++cnt[key(r) + 1];
+      for (uint64_t k = 1; k < cnt.size(); ++k) cnt[k] += cnt[k - 1];
+      for (int64_t r = 0; r < C.n; ++r) perm[cnt[key(r)]++] = (uint32_t)r;
+      HIPCHK(upload(D.doc_perm, perm, s));
+    }
     HIPCHK(upload(D.scal, C.scal, s));
     HIPCHK(upload(D.scal_text, C.scal_text, s));
   }
@@ -457,7 +478,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     }
   }
   // truth-table fast path: few terms; per PSS version set its rule mask
-  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_const;
+  const bool tt = narrow && P.terms.size() <= KPE_TT_TERMS && !P.any_const && !P.any_exc;
   std::vector<uint32_t> cls;  // (cv_mask, rule mask) pairs
   uint32_t pss_rules = 0, err_rules = 0, pat_rules = 0;
   if (tt) {
@@ -531,6 +552,11 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   }
   HIPCHK(upload(D.rules, P.rules, s));
   HIPCHK(upload(D.rule_lanes, lanes, s));
+  if (P.any_exc) {
+    std::vector<uint32_t> xe;
+    for (auto& r : P.rules) xe.push_back(r.exc);
+    HIPCHK(upload(D.rule_exc, xe, s));
+  }
   HIPCHK(upload(D.narrow_rules, nrules, s));
   HIPCHK(upload(D.fmask, fmask, s));
   HIPCHK(upload(D.narrow_cls, cls, s));
@@ -995,6 +1021,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.nsys_total = (uint32_t)C.sys_id.size();
   sa.npann_total = (uint32_t)(C.pann_kv.size() / 2);
   sa.rules = PD.rules.as<KpeRule>();
+  sa.rule_exc = P.any_exc ? PD.rule_exc.as<uint32_t>() : nullptr;
   sa.rule_lanes = PD.rule_lanes.as<uint32_t>();
   sa.narrow_rules = PD.narrow_rules.as<uint32_t>();
   sa.fmask = PD.fmask.as<uint32_t>();
@@ -1074,6 +1101,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.ncr = (uint32_t)P.cond.rules.size();
       ca.doc = D.doc.as<uint32_t>();
       ca.doc_off = D.doc_off.as<uint64_t>();
+      ca.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();
       ca.scal = D.scal.as<KpeScalar>();
       ca.scal_text = D.scal_text.as<uint8_t>();
       ca.key_bytes = D.dict_bytes[D_KEY].as<uint8_t>();
@@ -1157,6 +1185,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.npr = (uint32_t)P.pat.rules.size();
       pa.doc = D.doc.as<uint32_t>();
       pa.doc_off = D.doc_off.as<uint64_t>();
+      pa.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();
       pa.scal = D.scal.as<KpeScalar>();
       pa.scal_text = D.scal_text.as<uint8_t>();
       pa.nodes = PD.pnodes.as<KpePNode>();

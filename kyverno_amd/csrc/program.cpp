@@ -1748,7 +1748,9 @@ class Lowerer {
   }
 
   // one filter block -> terms; returns filter index
-  uint32_t filter(const JV* rd, bool has_userinfo, bool is_exclude) {
+  // exc: a PolicyException filter (pkg/utils/match/match.go:76-193 checkResourceFilter): no
+  // operations term, and userInfo is checked against the (empty) background admission info
+  uint32_t filter(const JV* rd, bool has_userinfo, bool is_exclude, bool exc = false) {
     KpeFilter f{(uint32_t)P.fterms.size(), 0};
     auto push = [&](KpeTerm t) {
       P.fterms.push_back(term(t));
@@ -1760,7 +1762,11 @@ class Lowerer {
       return x && x->t == JV::Obj;
     };
     bool rd_empty = !nonempty(rd) && !sel_obj("selector") && !sel_obj("namespaceSelector");
-    if (!is_exclude) {
+    if (exc) {
+      // "statement cannot be empty"; roles / clusterRoles / subjects never match the empty
+      // admission info of a background scan (checkUserInfo, match.go:105-126)
+      if (rd_empty || has_userinfo) push({T_FALSE, 0, 0, 0});
+    } else if (!is_exclude) {
       // userInfo is cleared for empty admission info (utils/match.go:263-265)
       if (rd_empty) push({T_FALSE, 0, 0, 0});  // "match cannot be empty"
     } else {
@@ -1769,7 +1775,7 @@ class Lowerer {
     }
     if (!rd_empty) {
       auto ops = svl(rd->get("operations"));
-      if (!ops.empty() && std::find(ops.begin(), ops.end(), "CREATE") == ops.end()) push({T_FALSE, 0, 0, 0});
+      if (!exc && !ops.empty() && std::find(ops.begin(), ops.end(), "CREATE") == ops.end()) push({T_FALSE, 0, 0, 0});
       auto kinds = svl(rd->get("kinds"));
       if (!kinds.empty()) {
         // CheckKind (pkg/utils/match/kind.go:14-26): OR over selectors of
@@ -1818,7 +1824,9 @@ class Lowerer {
       const JV* nsel = rd->get("namespaceSelector");
       if (nsel && nsel->t != JV::Null) {
         bool star = std::find(kinds.begin(), kinds.end(), "*") != kinds.end();
+        sel_exc_ = exc;
         selector(nsel, true, star, push);
+        sel_exc_ = false;
       }
     }
     P.filters.push_back(f);
@@ -1848,6 +1856,7 @@ class Lowerer {
       S.p_kind_ns = pred(D_KIND, {"Namespace"});
       S.p_kind_empty = pred(D_KIND, {""});
       S.star_kind = star_kind ? 1u : 0u;
+      S.exc = sel_exc_ ? 1u : 0u;
     }
     bool invalid = false;
     std::vector<KpeSelReq> reqs;
@@ -2159,6 +2168,7 @@ class Lowerer {
       crule.kind = CR_NONE;
     }
     if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) P.any_const = true;
+    rule_info_.push_back({pre_block != CE_NONE, has_validate, rname});
     if (pre_block != CE_NONE || k.handler == H_COND) P.cond.rules.push_back(crule);
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
@@ -2177,15 +2187,135 @@ class Lowerer {
   }
 
  private:
+  // PolicyExceptions (api/kyverno/v2beta1/policy_exception_types.go; engine.go:286-293,
+  // pkg/engine/utils/exceptions.go:14-47). An exception lists (policy key, rule-name globs)
+  // and a match block; a matched cell of such a rule whose preconditions held is RuleSkip when
+  // the block holds. The device evaluates the block like a rule's match (KpeRule::exc).
+  // Refused (KPE_E_UNSUPPORTED): podSecurity exceptions, conditions that do not fold to true
+  // (MatchesException stops at the first matching exception, so a false one changes which
+  // exception applies), rules whose preconditions read the resource (an erroring precondition
+  // wins over the exception), and several exceptions that are not all `any` blocks.
+ public:
+  void exceptions(const JV& root, bool background, const std::vector<std::string>& rule_pol_key) {
+    std::vector<const JV*> xs;
+    if (root.t == JV::Arr)
+      for (auto& e : root.a) xs.push_back(&e);
+    else if (root.t != JV::Null)
+      xs.push_back(&root);
+    struct X {
+      const JV* spec;
+      std::string key;
+    };
+    std::vector<X> keep;
+    for (const JV* e : xs) {
+      if (e->t != JV::Obj) throw std::invalid_argument("PolicyException is not an object");
+      const JV* spec = e->get("spec");
+      if (!spec || spec->t != JV::Obj) throw std::invalid_argument("PolicyException without spec");
+      const JV* meta = e->get("metadata");
+      const std::string name = meta ? sv(meta->get("name")) : "", ns = meta ? sv(meta->get("namespace")) : "";
+      const std::string key = ns.empty() ? name : ns + "/" + name;
+      // background scans only fetch exceptions with background processing enabled
+      // (pkg/controllers/report/utils/utils.go:113-124); kyverno apply uses every one given
+      const JV* bg = spec->get("background");
+      if (background && bg && bg->t == JV::Bool && !bg->b) continue;
+      if (nonempty(spec->get("podSecurity")))
+        throw CompileError("PolicyException " + key + ": podSecurity exceptions are not supported on the device");
+      // CheckAnyAllConditions (pkg/utils/conditions/condition.go:14-30): every `all` holds and
+      // some `any` holds, or `any` is empty
+      const JV* cond = spec->get("conditions");
+      if (cond && cond->t != JV::Null) {
+        bool ok = cond->t == JV::Obj;
+        const JV* all = ok ? cond->get("all") : nullptr;
+        const JV* any = ok ? cond->get("any") : nullptr;
+        if (all && all->t == JV::Arr)
+          for (auto& c : all->a) ok = ok && fold_condition(c) == F_TRUE;
+        else if (all && all->t != JV::Null)
+          ok = false;
+        if (any && any->t == JV::Arr && !any->a.empty()) {
+          bool hit = false;
+          for (auto& c : any->a) {
+            const Fold f = fold_condition(c);
+            if (f == F_NO) ok = false;
+            hit = hit || f == F_TRUE;
+          }
+          ok = ok && hit;
+        } else if (any && any->t != JV::Null && any->t != JV::Arr) {
+          ok = false;
+        }
+        if (!ok) throw CompileError("PolicyException " + key + ": conditions must fold to true at compile time");
+      }
+      keep.push_back({spec, key});
+    }
+    for (size_t r = 0; r < P.rules.size(); ++r) {
+      std::vector<const JV*> mine;  // match blocks of the exceptions that contain this rule
+      for (auto& x : keep) {
+        bool has = false;
+        const JV* ex = x.spec->get("exceptions");
+        if (ex && ex->t == JV::Arr)
+          for (auto& it : ex->a) {  // Exception.Contains: policy key, then rule-name globs
+            if (it.t != JV::Obj || sv(it.get("policyName")) != rule_pol_key[r]) continue;
+            for (auto& rn : svl(it.get("ruleNames")))
+              if (glob_host(rn, rule_info_[r].name)) has = true;
+          }
+        if (has) mine.push_back(x.spec->get("match"));
+      }
+      if (mine.empty()) continue;
+      const std::string rname = rule_names_at(r);
+      if (rule_info_[r].pre_dyn)
+        throw CompileError("rule '" + rname + "': PolicyExceptions on a rule whose preconditions read the resource");
+      if (P.rules[r].handler == H_NONE) {
+        if (rule_info_[r].has_validate)
+          throw CompileError("rule '" + rname + "': PolicyExceptions on a validate rule without a handler");
+        continue;  // no validate handler: the rule gives no response either way
+      }
+      auto blocks = [&](const JV* m, const char* k) -> const JV* {
+        const JV* b = m ? m->get(k) : nullptr;
+        return (b && b->t == JV::Arr && !b->a.empty()) ? b : nullptr;
+      };
+      bool always = false, any_only = true;
+      for (const JV* m : mine) {
+        if (!blocks(m, "any") && !blocks(m, "all")) always = true;  // CheckMatchesResources: no error
+        else if (!blocks(m, "any") && blocks(m, "all")->a.size() > 1) any_only = false;
+      }
+      uint32_t x = XE_PRESENT;
+      const uint32_t f0 = (uint32_t)P.filters.size();
+      if (always) {
+        x |= XE_ALL;  // no filters: holds
+      } else if (mine.size() == 1 && !blocks(mine[0], "any")) {
+        x |= XE_ALL;
+        for (auto& f : blocks(mine[0], "all")->a) filter(f.get("resources"), has_ui(&f), false, true);
+      } else {
+        if (!any_only) throw CompileError("rule '" + rname + "': several PolicyExceptions with `all` blocks");
+        for (const JV* m : mine) {
+          const JV* b = blocks(m, "any") ? blocks(m, "any") : blocks(m, "all");
+          for (auto& f : b->a) filter(f.get("resources"), has_ui(&f), false, true);
+        }
+      }
+      const uint32_t nf = (uint32_t)P.filters.size() - f0;
+      if (f0 > 0xFFFFFu || nf > 0x3FFu) throw CompileError("rule '" + rname + "': too many PolicyException filters");
+      P.rules[r].exc = x | f0 | nf << 20;
+      P.any_exc = true;
+    }
+  }
+  std::string rule_names_at(size_t r) const { return P.rule_names[r]; }
+ private:
+
   Program& P;
   cq::CondCompiler CC;
+  struct RuleInfo {
+    bool pre_dyn, has_validate;
+    std::string name;
+  };
+  std::vector<RuleInfo> rule_info_;
+  bool sel_exc_ = false;
 };
 
 }  // namespace
 
 Program::~Program() = default;
 
-std::unique_ptr<Program> compile_policies(const char* json, size_t len) {
+std::unique_ptr<Program> compile_policies(const char* json, size_t len, const char* exceptions, size_t exc_len,
+                                          bool background) {
   JV root = parse_all(json, len);
   std::vector<const JV*> pols;
   if (root.t == JV::Arr)
@@ -2224,6 +2354,11 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len) {
       rr.category = annv("policies.kyverno.io/category");
       rr.severity = sev;
     }
+  }
+  if (exceptions && exc_len) {
+    std::vector<std::string> keys;
+    for (auto& rr : prog->reports) keys.push_back(rr.policy_key);
+    L.exceptions(parse_all(exceptions, exc_len), background, keys);
   }
   return prog;
 }

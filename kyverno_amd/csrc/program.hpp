@@ -102,6 +102,7 @@ struct Program {
   uint32_t cv_union = 0;  // union of cv_mask over rules
   std::vector<uint32_t> cv_classes;  // distinct cv_masks of PSS rules
   bool any_apply_one = false;
+  bool any_exc = false;    // some rule has PolicyExceptions (KpeRule::exc)
   bool any_const = false;  // some rule has a constant handler (H_CONST_*)
   bool any_pss = false;
   PatProgram pat;  // pattern rules (H_PATTERN)
@@ -116,6 +117,7 @@ struct Program {
 struct CompileError : std::runtime_error {
   using std::runtime_error::runtime_error;
 };
-std::unique_ptr<Program> compile_policies(const char* json, size_t len);
+std::unique_ptr<Program> compile_policies(const char* json, size_t len, const char* exceptions = nullptr,
+                                          size_t exc_len = 0, bool background = false);
 
 }  // namespace kpe

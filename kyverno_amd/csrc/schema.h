@@ -328,7 +328,9 @@ typedef struct KpeSelector {
   int32_t p_kind_empty;  // namespaceSelector: D_KIND predicate "" (skipped unless kinds has "*")
   uint32_t star_kind;    // namespaceSelector: the block's kinds contain "*"
   uint32_t invalid;      // namespaceSelector that fails to build (false wherever it is evaluated)
-  uint32_t pad[2];
+  uint32_t exc;          // PolicyException block (pkg/utils/match/match.go:184-193): not checked
+                         // for kind Namespace or an empty kind
+  uint32_t pad;
 } KpeSelector;
 #define SR_EQ 0u        // matchLabels k: v (no wildcards): first label with key k has value v
 #define SR_WILD 1u      // matchLabels with wildcards: first label matching both globs, and that
@@ -363,8 +365,17 @@ typedef struct KpeRule {
   uint32_t apply_one;     // spec.applyRules == One
   uint32_t pss_excl0, pss_nexcl;  // PSS exclusions (reserved)
   uint32_t cv_class;      // PSS: index of cv_mask among the program's distinct cv_masks
-  uint32_t pad[2];        // 16 words
+  uint32_t exc;           // PolicyExceptions of the rule (XE_*): their match block; 0 = none
+  uint32_t pad;           // 16 words
 } KpeRule;
+// KpeRule::exc: a cell whose rule matched (and whose preconditions are constant) is
+// RuleSkip "rule skipped due to policy exception" when this block of filters holds
+// (pkg/engine/utils/exceptions.go:14-47 MatchesException, validate_resource.go:43-56,
+// validate_pss.go:45-58). Filters [f0, f0 + nf), any (OR) or all (AND; nf = 0: always).
+#define XE_PRESENT (1u << 31)
+#define XE_ALL (1u << 30)
+#define XE_F0(x) ((x) & 0xFFFFFu)
+#define XE_NF(x) (((x) >> 20) & 0x3FFu)
 
 // ---- podSecurity.exclude (pkg/pss/evaluate.go:72-317), evaluated by kpe_pssx_kernel ----------
 // A PSA field error is keyed by its field path with digit runs replaced by "*": a suffix

@@ -108,7 +108,9 @@ class Device:
 class PolicySet:
     """Compiled policies (autogen applied once, autogen.ComputeRules)."""
 
-    def __init__(self, policies):
+    def __init__(self, policies, exceptions=None, background=False):
+        """exceptions: PolicyException objects (kyverno.io/v2beta1) or their JSON; background:
+        drop exceptions with spec.background false, as the background scanner does."""
         L = load()
         if isinstance(policies, (bytes, str)):
             raw = policies if isinstance(policies, bytes) else policies.encode()
@@ -116,8 +118,15 @@ class PolicySet:
         else:
             self.policies = list(policies) if isinstance(policies, (list, tuple)) else [policies]
             raw = json.dumps(self.policies).encode()
+        if exceptions is None:
+            xraw = b""
+        elif isinstance(exceptions, (bytes, str)):
+            xraw = exceptions if isinstance(exceptions, bytes) else exceptions.encode()
+        else:
+            xraw = json.dumps(list(exceptions) if isinstance(exceptions, (list, tuple)) else [exceptions]).encode()
+        self.exceptions = exceptions
         h = ctypes.c_void_p()
-        check(L.kpe_program_compile(raw, len(raw), ctypes.byref(h)))
+        check(L.kpe_program_compile_ex(raw, len(raw), xraw or None, len(xraw), 1 if background else 0, ctypes.byref(h)))
         self.h = h
         n = L.kpe_program_num_rules(h)
         self.rule_names = [L.kpe_program_rule_name(h, i).decode() for i in range(n)]

@@ -184,10 +184,27 @@ int oracle_rule_names(const char* policies_json, char* buf, size_t cap) {
 //   ns_labels_json: {"<namespace>": {"k": "v"}, ...} or NULL.
 //   out: N x R bytes (row-major), values in oracle::Status.
 // Returns N (number of resources) or -1.
+long oracle_validate_ex(const char* policies_json, const char* exceptions_json, int background, const char* ndjson,
+                        size_t len, const char* ns_labels_json, uint8_t* out, size_t out_cap, int nthreads);
 long oracle_validate(const char* policies_json, const char* ndjson, size_t len, const char* ns_labels_json,
                      uint8_t* out, size_t out_cap, int nthreads) {
+  return oracle_validate_ex(policies_json, nullptr, 0, ndjson, len, ns_labels_json, out, out_cap, nthreads);
+}
+// oracle_validate with PolicyExceptions (a JSON array or object; background: drop those with
+// spec.background false, as FetchPolicyExceptions does).
+long oracle_validate_ex(const char* policies_json, const char* exceptions_json, int background, const char* ndjson,
+                        size_t len, const char* ns_labels_json, uint8_t* out, size_t out_cap, int nthreads) {
   try {
     auto ps = load_policies(policies_json);
+    std::vector<PolicyException> xs;
+    if (exceptions_json && *exceptions_json) {
+      JPtr x = parse_json(exceptions_json);
+      if (x->t == JT::Arr)
+        for (auto& e : x->a) xs.push_back(parse_exception(*e));
+      else
+        xs.push_back(parse_exception(*x));
+    }
+    for (auto& p : ps) attach_exceptions(p, xs, background != 0);
     size_t R = 0;
     for (auto& p : ps) R += p.rules.size();
     std::vector<std::pair<std::string, Labels>> nsl;

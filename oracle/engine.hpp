@@ -438,11 +438,34 @@ struct Rule {
   };
   std::vector<ForEach> foreach;
 };
+// PolicyException (api/kyverno/v2beta1/policy_exception_types.go): the exceptions that name
+// a (policy key, rule) pair, their match block and conditions.
+struct PolicyException {
+  std::string key;  // cache.MetaNamespaceKeyFunc
+  bool background = true;
+  std::vector<Filter> any, all;  // MatchResources (no legacy form)
+  bool has_conditions = false;
+  std::vector<cond::Condition> c_any, c_all;  // AnyAllConditions
+  bool has_pss = false;
+  bool unsupported = false;  // a condition this restatement does not cover
+  std::vector<std::pair<std::string, std::vector<std::string>>> refs;  // (policyName, ruleNames)
+  // Exception.Contains (policy_exception_types.go:136-145): policy key equal, a rule-name glob
+  bool contains(const std::string& policy, const std::string& rule) const {
+    for (auto& r : refs)
+      if (r.first == policy)
+        for (auto& g : r.second)
+          if (wildcard_match(g, rule)) return true;
+    return false;
+  }
+};
 struct Policy {
   std::string name, ns;
   bool namespaced = false;
   bool apply_one = false;
   std::vector<Rule> rules;  // after autogen
+  std::string key() const { return ns.empty() ? name : ns + "/" + name; }
+  // per rule: the exceptions that contain it (pkg/engine/exceptions.go:12-35), in list order
+  std::vector<std::vector<const PolicyException*>> exceptions;
 };
 
 inline ResourceDescription parse_rd(const JVal* v) {
@@ -1020,6 +1043,123 @@ inline Status pss_handler(const Rule& r, const JVal& res, const std::string& kin
   }
 }
 
+// ---- PolicyExceptions: pkg/utils/match/match.go:26-193 CheckMatchesResources ----------------
+inline int exc_filter_errors(const Filter& f, const MatchCtx& c) {
+  if (f.rd.empty && f.ui.empty) return 1;  // "statement cannot be empty"
+  const ResourceDescription& rd = f.rd;
+  int errs = 0;
+  if (!rd.kinds.empty() && !check_kind(rd.kinds, c.gvk, "")) ++errs;
+  std::string rname = c.res.name();
+  if (rname.empty()) rname = c.res.generate_name();
+  if (!rd.name.empty() && !wildcard_match(rd.name, rname)) ++errs;
+  if (!rd.names.empty()) {
+    bool any = false;
+    for (auto& n : rd.names) any = any || wildcard_match(n, rname);
+    if (!any) ++errs;
+  }
+  if (!rd.namespaces.empty()) {
+    std::string ns = c.res.kind() == "Namespace" ? c.res.name() : c.res.ns();
+    bool any = false;
+    for (auto& n : rd.namespaces) any = any || wildcard_match(n, ns);
+    if (!any) ++errs;
+  }
+  if (!rd.annotations.empty()) {  // CheckAnnotations: every pair matched by some annotation
+    auto actual = c.res.strmap("annotations");
+    for (auto& kv : rd.annotations) {
+      bool m = false;
+      for (auto& a : actual) m = m || (wildcard_match(kv.first, a.first) && wildcard_match(kv.second, a.second));
+      if (!m) {
+        ++errs;
+        break;
+      }
+    }
+  }
+  if (rd.selector.present && check_selector(rd.selector, c.res.strmap("labels")) != 1) ++errs;
+  if (rd.ns_selector.present && c.res.kind() != "Namespace" && !c.res.kind().empty() &&
+      check_selector(rd.ns_selector, c.ns_labels) != 1)
+    ++errs;
+  if (!f.ui.empty) ++errs;  // checkUserInfo against the empty admission info of a scan
+  return errs;
+}
+inline bool exc_matches(const PolicyException& e, const MatchCtx& c) {
+  if (!e.any.empty()) {
+    for (auto& f : e.any)
+      if (exc_filter_errors(f, c) == 0) return true;
+    return false;
+  }
+  for (auto& f : e.all)
+    if (exc_filter_errors(f, c) != 0) return false;
+  return true;  // no any / all: no error
+}
+// MatchesException (pkg/engine/utils/exceptions.go:14-47): the first exception whose match
+// block holds decides; its conditions (CheckAnyAllConditions, pkg/utils/conditions/condition.go:
+// 14-30) failing or erroring mean no exception. Returns the exception or null; throws
+// cond::Unsupported for conditions outside this restatement.
+inline const PolicyException* matches_exception(const std::vector<const PolicyException*>& xs, const MatchCtx& c,
+                                                const JVal& res, cond::Ctx& cx) {
+  for (const PolicyException* e : xs) {
+    if (!exc_matches(*e, c)) continue;
+    if (e->has_conditions) {
+      if (e->unsupported) throw cond::Unsupported("exception conditions");
+      if (!cx.root) cx.root = cond::request_context(res);
+      try {
+        for (auto& k : e->c_all)
+          if (!cond::eval_condition(k, cx)) return nullptr;
+        if (e->c_any.empty()) return e;
+        for (auto& k : e->c_any)
+          if (cond::eval_condition(k, cx)) return e;
+        return nullptr;
+      } catch (const cond::EvalError&) {
+        return nullptr;
+      }
+    }
+    return e;
+  }
+  return nullptr;
+}
+inline PolicyException parse_exception(const JVal& x) {
+  PolicyException e;
+  const JVal* meta = x.get("metadata");
+  const std::string name = meta ? jstr(meta->get("name")) : "", ns = meta ? jstr(meta->get("namespace")) : "";
+  e.key = ns.empty() ? name : ns + "/" + name;
+  const JVal* spec = x.get("spec");
+  if (!spec) return e;
+  const JVal* bg = spec->get("background");
+  e.background = !(bg && bg->t == JT::Bool && !bg->b);
+  MatchRes m = parse_match(spec->get("match"));
+  e.any = m.any, e.all = m.all;
+  e.has_pss = jnonempty(spec->get("podSecurity"));
+  const JVal* cnd = spec->get("conditions");
+  if (cnd && !cnd->is_null()) {
+    e.has_conditions = true;
+    try {
+      for (const char* k : {"any", "all"}) {
+        const JVal* l = cnd->get(k);
+        if (!l || l->t != JT::Arr) continue;
+        for (auto& c : l->a) {
+          cond::Condition cc = cond::parse_condition(*c);
+          cond::Conditions one;
+          one.present = true, one.old_list = true, one.list.push_back(cc);
+          cond::precompile(one);
+          (k[1] == 'n' ? e.c_any : e.c_all).push_back(cc);
+        }
+      }
+    } catch (const cond::Unsupported&) {
+      e.unsupported = true;
+    }
+  }
+  const JVal* ex = spec->get("exceptions");
+  if (ex && ex->t == JT::Arr)
+    for (auto& it : ex->a) e.refs.emplace_back(jstr(it->get("policyName")), jstrlist(it->get("ruleNames")));
+  return e;
+}
+inline void attach_exceptions(Policy& p, const std::vector<PolicyException>& xs, bool background) {
+  p.exceptions.assign(p.rules.size(), {});
+  for (size_t i = 0; i < p.rules.size(); ++i)
+    for (auto& e : xs)
+      if ((!background || e.background) && e.contains(p.key(), p.rules[i].name)) p.exceptions[i].push_back(&e);
+}
+
 // engine.go:87-101 + validation.go:16-80. out[i] = status of computed rule i.
 inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, std::vector<uint8_t>& out) {
   out.assign(p.rules.size(), NA);
@@ -1047,6 +1187,20 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
           if (!cond::eval_conditions(r.pre, cx)) s = SKIP, done = true;
         } catch (const cond::EvalError&) {
           s = ERROR, done = true;
+        } catch (const cond::Unsupported&) {
+          s = UNSUPPORTED, done = true;
+        }
+      }
+      // engine.go:286-293 + the handlers' first step: a matching PolicyException skips the
+      // rule (validate_resource.go:43-56 always; validate_pss.go:45-58 when it has no
+      // podSecurity controls: those are not restated here)
+      if (!done && i < p.exceptions.size() && !p.exceptions[i].empty()) {
+        try {
+          if (const PolicyException* e = matches_exception(p.exceptions[i], c, res, cx)) {
+            if (r.has_pss && e->has_pss) s = UNSUPPORTED;
+            else s = SKIP;
+            done = true;
+          }
         } catch (const cond::Unsupported&) {
           s = UNSUPPORTED, done = true;
         }

@@ -15,3 +15,10 @@ for i in 1 2; do
   done
 done
 cat gpurun_out/ab.jsonl
+[ -n "$PAT" ] || exit 0
+for c in c5 c3; do
+  timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/ab_$c.log 2>&1 || exit $?
+  echo "$c perm: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/ab_$c.log | head -1) step_ms $(grep -o '"ms_per_step": [0-9.]*' gpurun_out/ab_$c.log)"
+  KPE_NO_PERM=1 timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/ab_${c}_noperm.log 2>&1 || exit $?
+  echo "$c noperm: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/ab_${c}_noperm.log | head -1)"
+done

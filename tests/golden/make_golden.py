@@ -166,6 +166,36 @@ def chainsaw_psa():
     return out
 
 
+def chainsaw_exceptions():
+    """PolicyException scenarios: policy.yaml + exception.yaml + resources applied with an
+    expected admission error (Enforce policy: some rule failed) or not. Scenarios whose outcome
+    depends on the admission request itself (the requesting user, DELETE) are left out: a
+    background scan has neither."""
+    base = "test/conformance/chainsaw/exceptions"
+    admission_only = {"only-for-specific-user", "applies-to-delete", "events-creation", "background-mode"}
+    out = []
+    for d in sorted(os.listdir(os.path.join(REF, base))):
+        full = os.path.join(REF, base, d)
+        if d in admission_only or not os.path.exists(os.path.join(full, "exception.yaml")):
+            continue
+        test = _load_yaml_docs(os.path.join(full, "chainsaw-test.yaml"))[0]
+        policy = _load_yaml_docs(os.path.join(full, "policy.yaml"))[0]
+        exceptions = _load_yaml_docs(os.path.join(full, "exception.yaml"))
+        for step in test["spec"]["steps"]:
+            for op in step.get("try", []):
+                ap = op.get("apply")
+                if not ap or ap["file"].startswith(("policy", "exception", "ns")):
+                    continue
+                expect_err = any(c.get("check", {}).get("($error != null)") is True for c in ap.get("expect", []))
+                for doc in _load_yaml_docs(os.path.join(full, ap["file"])):
+                    if doc.get("kind") in ("Namespace", "PolicyException", "ClusterPolicy", "Policy"):
+                        continue
+                    out.append({"dir": d, "file": f"{base}/{d}/{ap['file']}", "policy": policy,
+                                "exceptions": exceptions, "resource": doc,
+                                "expect": "rejected" if expect_err else "allowed"})
+    return out
+
+
 def background_report():
     base = "test/conformance/chainsaw/reports/background/test-report-background-mode"
     policy = _load_yaml_docs(os.path.join(REF, base, "policy.yaml"))[0]
@@ -508,5 +538,6 @@ if __name__ == "__main__":
     _dump("wildcard_match.json", wildcard_cases())
     _dump("chainsaw_psa.json", chainsaw_psa())
     _dump("background_report.json", background_report())
+    _dump("chainsaw_exceptions.json", chainsaw_exceptions())
     _dump("check_selector.json", check_selector())
     _dump("match_rd_cases.json", match_rd_cases())

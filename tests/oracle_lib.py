@@ -29,6 +29,10 @@ class Oracle:
         L.oracle_validate.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                       ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.oracle_validate.restype = ctypes.c_long
+        L.oracle_validate_ex.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p,
+                                         ctypes.c_size_t, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_size_t,
+                                         ctypes.c_int]
+        L.oracle_validate_ex.restype = ctypes.c_long
         cp = ctypes.c_char_p
         L.oracle_pattern_validate.argtypes = [cp, cp]
         L.oracle_validate_string.argtypes = [cp, cp, cp]
@@ -71,8 +75,9 @@ class Oracle:
             raise RuntimeError(self.lib.oracle_last_error().decode())
         return buf.value.decode().splitlines()
 
-    def validate(self, policies, ndjson: bytes, ns_labels=None, nthreads=1):
-        """Verdict matrix (N x R uint8, oracle status codes) for NDJSON resources."""
+    def validate(self, policies, ndjson: bytes, ns_labels=None, nthreads=1, exceptions=None, background=False):
+        """Verdict matrix (N x R uint8, oracle status codes) for NDJSON resources, with
+        PolicyExceptions (kyverno.io/v2beta1 objects) when given."""
         R = len(self.rule_names(policies))
         N = ndjson.count(b"\n") + 1
         out = np.zeros(max(N * R, 1), dtype=np.uint8)
@@ -81,7 +86,9 @@ class Oracle:
             nl = bytes(ns_labels)
         else:
             nl = json.dumps(ns_labels).encode() if ns_labels else None
-        n = self.lib.oracle_validate(pj, ndjson, len(ndjson), nl, out.ctypes.data, out.size, nthreads)
+        xj = json.dumps(list(exceptions)).encode() if exceptions else None
+        n = self.lib.oracle_validate_ex(pj, xj, 1 if background else 0, ndjson, len(ndjson), nl, out.ctypes.data,
+                                        out.size, nthreads)
         if n < 0:
             raise RuntimeError(self.lib.oracle_last_error().decode())
         return out[: n * R].reshape(n, R)
