@@ -132,6 +132,16 @@ uint64_t kpe_corpus_digest(const kpe_corpus* c);
 #define KPE_ROW_LIMIT 2u
 #define KPE_ROW_NO_SPEC 4u
 kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out);
+/* Resource hash of incremental background scans: CalculateResourceHash
+ * (pkg/utils/report/metadata.go:137-155), md5 of json.Marshal([labels, annotations, the object
+ * without metadata / status / scale / spec.nodeName]) as 32 lower-case hex digits + NUL in out33.
+ * The background controller rescans a resource when it differs from the hash its report
+ * recorded (pkg/controllers/report/background/controller.go:247-297). Host only. */
+kpe_status kpe_resource_hash(const char* resource_json, size_t len, char* out33);
+/* The hash of every NDJSON row (the rows kpe_corpus_flatten makes), 32 hex digits per row into
+ * out (no NUL), on up to 16 threads. out == NULL: returns the row count. Returns the row count,
+ * or -kpe_status (a row that is not a JSON object: -KPE_E_INVALID). */
+int64_t kpe_resource_hashes(const char* ndjson, size_t len, char* out, int64_t cap_rows);
 /* Copy the columns to device memory (HBM). Evaluation requires this. */
 kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* c);
 void kpe_corpus_free(kpe_corpus* c);

@@ -27,8 +27,10 @@ from .engine import (  # noqa: F401
     synth_ns_labels,
     synth_resources,
 )
+from .scan import BackgroundScanner, resource_hash, resource_hashes  # noqa: F401
 
 __all__ = [
+    "BackgroundScanner",
     "Corpus",
     "Device",
     "Engine",
@@ -44,4 +46,6 @@ __all__ = [
     "synth_resources",
     "load",
     "lib_path",
+    "resource_hash",
+    "resource_hashes",
 ]

@@ -49,6 +49,9 @@ def load():
     L.kpe_device_close.argtypes = [vp]
     L.kpe_program_compile.argtypes = [cp, sz, ctypes.POINTER(vp)]
     L.kpe_program_compile_ex.argtypes = [cp, sz, cp, sz, ctypes.c_uint32, ctypes.POINTER(vp)]
+    L.kpe_resource_hash.argtypes = [cp, sz, ctypes.c_char_p]
+    L.kpe_resource_hashes.argtypes = [cp, sz, ctypes.c_char_p, i64]
+    L.kpe_resource_hashes.restype = i64
     L.kpe_program_num_rules.argtypes = [vp]
     L.kpe_program_rule_name.argtypes = [vp, i32]
     L.kpe_program_rule_name.restype = cp

@@ -1151,7 +1151,7 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
   if (n <= 0) return 0;
   if (pss && narrow == 4) {  // kpe_lean3_kernel: KPE_LEAN_T tiles of 64 rows per wave, no persistent loop
     const int64_t waves = ((n + 63) / 64 + KPE_LEAN_T - 1) / KPE_LEAN_T;
-    return (uint32_t)((waves + kBlock / 64 - 1) / (kBlock / 64));
+    return (uint32_t)((waves + kLB / 64 - 1) / (kLB / 64));
   }
   static thread_local int cus = 0;
   if (!cus) {
@@ -1179,7 +1179,7 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
     return hipGetLastError();
   }
   if (pss && narrow == 4) {
-    hipLaunchKernelGGL(kpe_lean3_kernel, dim3(grid), dim3(kBlock), dyn_bytes, s, *hargs);
+    hipLaunchKernelGGL(kpe_lean3_kernel, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);

@@ -292,13 +292,29 @@ struct LeanItems {
   uint2 c0, c1, q0;
   uint32_t v0, v1, s0;
 };
-__global__ void __launch_bounds__(kBlock, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArgs) {
+#ifndef KPE_LEAN3_BLOCK
+#define KPE_LEAN3_BLOCK 256
+#endif
+#ifndef KPE_LEAN3_XCD
+#define KPE_LEAN3_XCD 1
+#endif
+constexpr uint32_t kLB = KPE_LEAN3_BLOCK;
+// XCD-aware block order: the dispatcher deals workgroups round-robin to the 8 XCDs (block b on
+// XCD b % 8), so block b takes the (b / 8)-th block of XCD b % 8's contiguous share of the tiles.
+// A tile's list loads run past its end into the next tile's items, and the header of the next
+// tile is read too: with neighbouring tiles on one XCD those reads hit the L2 that loads them.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+  if (!KPE_LEAN3_XCD) return b;
+  const uint32_t q = nb >> 3, r = nb & 7u, x = b & 7u;
+  return x * q + min(x, r) + (b >> 3);
+}
+__global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArgs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   if (KPE_DIAG & DIAG_EMPTY) return;
   CArgs& a0 = *kargs();
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
-  const uint32_t t0 = (blockIdx.x * (kBlock / 64u) + wv) * KPE_LEAN_T;
+  const uint32_t t0 = (xcd_block(blockIdx.x, gridDim.x) * (kLB / 64u) + wv) * KPE_LEAN_T;
   const uint32_t need = a0.need;
   LeanCols L;
   L.rec = make_rsrc(a0.rec, n * 16u);
@@ -337,7 +353,7 @@ __global__ void __launch_bounds__(kBlock, KPE_LEAN2_WAVES) kpe_lean3_kernel(Scan
     uint4* d4 = reinterpret_cast<uint4*>(dyn);
     if (t < img_n4) d4[t] = img0;
 #pragma unroll 1
-    for (uint32_t i = t + kBlock; i < img_n4; i += kBlock) d4[i] = img[i];
+    for (uint32_t i = t + kLB; i < img_n4; i += kLB) d4[i] = img[i];
   }
   __syncthreads();
   if (KPE_DIAG & DIAG_NOLOOP) {

@@ -310,6 +310,12 @@ struct PatVM {
                   F.x = 1u, F.cur = doc[PVD(c)].y + 1u, F.c = c;
                   continue;  // search
                 }
+              } else if ((m.x & PMF_LEAF) && (c == kNoNode || DN_KIND(doc[PVD(c)].x) != DN_ARR)) {
+                // a scalar pattern against a scalar / absent value resolves in place: BEGIN's
+                // pattern.Validate and RET's anchor mapping without the two VM round trips
+                const uint32_t li = a.nodes[PV(m.z, a.nnodes, 1)].y;
+                const uint32_t v1 = pat_leaf(a, node_sid(a, doc, c), li) ? PE_OK : PE_OTHER;
+                e = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
               } else {
                 br = c, bpi = m.z, begin_child = true;
                 break;

@@ -864,6 +864,7 @@ class PatCompiler {
         }
       } else if (h != PM_NEG && !(flags & PMF_STAR)) {
         vn = node(val, depth + 1, repeated);
+        if (PP.nodes[vn].kind == PN_LEAF) flags |= PMF_LEAF;
       }
       uint32_t ki = 0;
       for (; ki < PP.keys.size() && PP.keys[ki] != name; ++ki) {

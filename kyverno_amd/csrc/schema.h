@@ -502,6 +502,7 @@ typedef struct KpePNode {
 #define PMF_STAR (1u << 3)   // default handler whose value is the string "*" (presence check)
 #define PMF_GLOB (1u << 4)   // ExpandInMetadata: first resource member matching the glob (string values)
 #define PMF_SLOT (1u << 5)   // condition / existence anchor tracked in the AnchorMap
+#define PMF_LEAF (1u << 6)   // the member's pattern value is a scalar leaf (PN_LEAF)
 #define PM_SLOT(x) (((x) >> 8) & 31u)
 // Leaf
 #define PL_BOOL 0u

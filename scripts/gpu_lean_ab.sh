@@ -10,7 +10,7 @@ rc=$?; [ "$TESTS" = none ] || { tail -3 gpurun_out/ab_tests.log; [ $rc -ne 0 ] &
 for i in 1 2; do
   timeout -k 10 120 python3 scripts/diag_time.py >> gpurun_out/ab.jsonl 2> gpurun_out/ab_err.log || exit $?
   KPE_LEAN_PERSIST=1 timeout -k 10 120 python3 scripts/diag_time.py | sed 's/"lib": "libkpe.so"/"lib": "persist"/' >> gpurun_out/ab.jsonl 2>> gpurun_out/ab_err.log || exit $?
-  for lib in kyverno_amd/build/diag/libkpe_*.so; do
+  for lib in kyverno_amd/build/diag/libkpe_*.so; do [ -e "$lib" ] || continue
     KPE_LIB=$PWD/$lib timeout -k 10 120 python3 scripts/diag_time.py >> gpurun_out/ab.jsonl 2>> gpurun_out/ab_err.log || exit $?
   done
 done
