@@ -82,10 +82,19 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # One rank per GPU over RCCL. KPE_DIST_BACKEND=gloo runs the collectives on host tensors: a
+    # functional check of the N-rank path with several ranks sharing one device (RCCL refuses two
+    # ranks on one GPU); ranks then take device LOCAL_RANK modulo the visible devices.
+    backend = os.environ.get("KPE_DIST_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
+    coll_dev = torch.device("cuda", local) if backend == "nccl" else torch.device("cpu")
 
     def barrier():
         if world > 1:
@@ -136,17 +145,17 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     barrier()
-    elapsed = max_over_ranks(elapsed, device="cuda")
+    elapsed = max_over_ranks(elapsed, device=coll_dev)
     # the exchanges, after the timed region: per-rule totals (R x 7 u64, one RCCL all-reduce over
     # xGMI) and the verdict rows of each rank's first shard gathered to rank 0 (grouped RCCL
     # point-to-point: one send per rank, all receives posted together on rank 0)
-    totals = allreduce_counts(totals, device="cuda")
+    totals = allreduce_counts(totals, device=coll_dev)
     v0, _, _ = eng.evaluate(ps, corpora[0])
     barrier()
     t1 = time.perf_counter()
-    full = gather_rows(v0, n * world, dst=0, device=torch.device("cuda", local))
+    full = gather_rows(v0, n * world, dst=0, device=coll_dev)
     torch.cuda.synchronize()
-    gather_s = max_over_ranks(time.perf_counter() - t1, device="cuda")
+    gather_s = max_over_ranks(time.perf_counter() - t1, device=coll_dev)
     gather = {"rows": n * world, "bytes": n * world * R, "seconds": gather_s,
               "rows_ok": bool(rank != 0 or (full is not None and full.shape == (n * world, R)))}
 
@@ -203,7 +212,8 @@ def main():
 
     if rank == 0:
         scan_roof = {"bound": "hbm", "achieved": scan_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": scan_achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "kpe_scan_kernel",
+                     "frac": scan_achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "kpe_lean3_kernel" if cfg == "c2" else "kpe_scan_kernel",
                      "kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes, "dict_kernel_ms": dict_ms,
                      "pattern_kernel_ms": pat_ms,
                      # the same bytes over the timed region's step time (launches of different

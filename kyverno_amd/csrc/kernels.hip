@@ -143,6 +143,8 @@ constexpr uint32_t kBlock = 256;
 #define DIAG_EMPTY 16u   // return at entry: launch cost only
 #define DIAG_NOTT 32u    // no truth table in the prologue
 #define DIAG_NOSTORE 64u  // (LEAN kernel) no verdict row stores
+#define DIAG_NOCV 128u    // (LEAN3) no PSA check logic: the OR-ed codes stand in for the failing checks
+#define DIAG_NOSTAGE 256u // (LEAN3) no list staging / per-pod OR: the lane's own first items stand in
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);

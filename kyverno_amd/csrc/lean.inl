@@ -298,6 +298,9 @@ struct LeanItems {
 #ifndef KPE_LEAN3_XCD
 #define KPE_LEAN3_XCD 1
 #endif
+#ifndef KPE_LEAN3_DIRECT
+#define KPE_LEAN3_DIRECT 1  // per-lane list loads (1) or cooperative loads staged through LDS (0)
+#endif
 constexpr uint32_t kLB = KPE_LEAN3_BLOCK;
 // XCD-aware block order: the dispatcher deals workgroups round-robin to the 8 XCDs (block b on
 // XCD b % 8), so block b takes the (b / 8)-th block of XCD b % 8's contiguous share of the tiles.
@@ -339,7 +342,7 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
 #pragma unroll
   for (uint32_t j = 0; j < KPE_LEAN_T; ++j) it[j].rec = bload4(L.rec, ((t0 + j) * 64u + lane) * 16u);
 #pragma unroll
-  for (uint32_t j = 0; j < KPE_LEAN_T; ++j) {
+  for (uint32_t j = 0; j < KPE_LEAN_T && !KPE_LEAN3_DIRECT; ++j) {
     const uint32_t C0 = hw(hall, 4u * j), V0 = hw(hall, 4u * j + 1u), S0 = hw(hall, 4u * j + 2u),
                    A0 = hw(hall, 4u * j + 3u);
     it[j].c0 = bload2(L.crec, (C0 + lane) * 8u);
@@ -401,6 +404,49 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
       const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
       oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
     }
+#if KPE_LEAN3_DIRECT
+    // Each lane reads its own pod's list items (its offsets from the scan): the first four
+    // containers, two volumes and (when the tile has any) two sysctls / annotations are issued
+    // together; an item past the pod's count reads past the column's end and returns 0. Pods
+    // with more items take a loop. No staging area, no wave barrier, no capacity limit.
+    (void)nvt;
+    constexpr uint32_t kOOB = 0xFFFFFFF0u;
+    const uint32_t cb = (C0 + oc) * 8u, vb = (V0 + ov) * 4u, sb = (S0 + os) * 4u, ab = (A0 + oa) * 8u;
+    const uint2 e0 = bload2(L.crec, nc > 0u ? cb : kOOB), e1 = bload2(L.crec, nc > 1u ? cb + 8u : kOOB),
+                e2 = bload2(L.crec, nc > 2u ? cb + 16u : kOOB), e3 = bload2(L.crec, nc > 3u ? cb + 24u : kOOB);
+    const uint32_t w0 = bload1(L.vol, nv > 0u ? vb : kOOB), w1 = bload1(L.vol, nv > 1u ? vb + 4u : kOOB);
+    uint32_t s0 = 0, s1 = 0;
+    uint2 q0 = make_uint2(0u, 0u), q1 = make_uint2(0u, 0u);
+    if (nsys && nst) s0 = bload1(L.sys, ns > 0u ? sb : kOOB), s1 = bload1(L.sys, ns > 1u ? sb + 4u : kOOB);
+    if (npann && nat) q0 = bload2(L.ann, na > 0u ? ab : kOOB), q1 = bload2(L.ann, na > 1u ? ab + 8u : kOOB);
+    auto vol_code = [&](uint32_t sv0) -> uint32_t { return ((sv0 >> VS_HOSTPATH) & 1u) | ((sv0 & kAllowedVolumes) ? 0u : 2u); };
+    auto sys_code = [&](uint32_t id) -> uint32_t {
+      return (pbit(p_s0, id) ^ 1u) | ((pbit(p_s1, id) ^ 1u) << 1) | ((pbit(p_s2, id) ^ 1u) << 2);
+    };
+    auto ann_code = [&](uint2 kv) -> uint32_t {
+      return (pbit(p_aak, kv.x) & (pbit(p_aao, kv.y) ^ 1u)) | ((pbit(p_spk, kv.x) & (pbit(p_sann, kv.y) ^ 1u)) << 1);
+    };
+    // a real container record always has state bits (every field state is one-hot)
+    auto cap = [&](uint2 e) -> uint32_t { return e.x ? (uint32_t)s_capb[CY_CAPSET(e.y)] : 0u; };
+    uint32_t xo = e0.x | e1.x | e2.x | e3.x;
+    uint32_t co = cap(e0) | cap(e1) | cap(e2) | cap(e3);
+    uint32_t vcode = 0, scode = 0, acode = 0;
+    if (nvol) vcode = (nv > 0u ? vol_code(w0) : 0u) | (nv > 1u ? vol_code(w1) : 0u);
+    if (nsys && nst) scode = (ns > 0u ? sys_code(s0) : 0u) | (ns > 1u ? sys_code(s1) : 0u);
+    if (npann && nat) acode = (na > 0u ? ann_code(q0) : 0u) | (na > 1u ? ann_code(q1) : 0u);
+    if (__builtin_amdgcn_ballot_w64(nc > 4u || (nvol && nv > 2u) || (nsys && ns > 2u) || (npann && na > 2u))) {
+      for (uint32_t k = 4; k < nc; ++k) {
+        const uint2 e = bload2(L.crec, cb + 8u * k);
+        xo |= e.x, co |= cap(e);
+      }
+      if (nvol)
+        for (uint32_t k = 2; k < nv; ++k) vcode |= vol_code(bload1(L.vol, vb + 4u * k));
+      if (nsys)
+        for (uint32_t k = 2; k < ns; ++k) scode |= sys_code(bload1(L.sys, sb + 4u * k));
+      if (npann)
+        for (uint32_t k = 2; k < na; ++k) acode |= ann_code(bload2(L.ann, ab + 8u * k));
+    }
+#else
     uint2* sc = reinterpret_cast<uint2*>(stage);
     uint8_t* sbv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_CTR * 2);
     uint8_t* sbs = sbv + KPE_STAGE_VOL;
@@ -413,6 +459,21 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
     auto ann_code = [&](uint2 kv) -> uint32_t {
       return (pbit(p_aak, kv.x) & (pbit(p_aao, kv.y) ^ 1u)) | ((pbit(p_spk, kv.x) & (pbit(p_sann, kv.y) ^ 1u)) << 1);
     };
+    if (KPE_DIAG & DIAG_NOSTAGE) {  // diagnostic: no staging, no per-pod OR
+      const uint32_t fails = (KPE_DIAG & DIAG_NOCV)
+                                 ? (cur.rec.x ^ cur.c0.x ^ cur.v0 ^ cur.s0 ^ cur.q0.x ^ oc)
+                                 : cv_fails(cur.rec.x, cur.c0.x | cur.c1.x, (cur.c0.y | cur.c1.y) & 7u, false, cur.v0 & 1u,
+                                            cur.v1 & 2u, cur.s0 & 7u, cur.q0.x & 1u, cur.q0.y & 2u) & cv_union;
+      const uint32_t matched = dyn[kt + GVK_KIND(cur.rec.y)];
+      const uint32_t failr = (fails & cls_cv0) ? cls_rm0 : 0u;
+      const uint32_t F = matched & failr, P = matched & ~failr;
+      if (live) {
+        uint8_t* row = verdicts + (size_t)r * R;
+#pragma unroll 1
+        for (uint32_t ri = 0; ri < R; ++ri) row[ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1));
+      }
+      continue;
+    }
     sc[lane] = ctr_code(cur.c0);
     sc[lane + 64u] = ctr_code(cur.c1);
     if (nvol) sbv[lane] = (uint8_t)vol_code(cur.v0), sbv[lane + 64u] = (uint8_t)vol_code(cur.v1);
@@ -472,8 +533,11 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
       }
     }
     __builtin_amdgcn_wave_barrier();
+#endif
     const uint32_t pw = cur.rec.x;
-    const uint32_t fails = cv_fails(pw, xo, co & 7u, false, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & cv_union;
+    const uint32_t fails = (KPE_DIAG & DIAG_NOCV)
+                               ? (pw ^ xo ^ co ^ vcode ^ scode ^ acode)
+                               : cv_fails(pw, xo, co & 7u, false, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & cv_union;
     const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
     const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
     const uint32_t matched = dyn[kt + GVK_KIND(cur.rec.y)];

@@ -160,8 +160,10 @@ def test_incremental_scan_matches_full(oracle):
         if i not in changed:
             rows[i]["status"] = {"phase": "Running"}
     nd2 = "\n".join(json.dumps(r) for r in rows).encode()
+    moved = sum(a != b for a, b in zip(K.resource_hashes(nd), K.resource_hashes(nd2)))
+    assert 0.9 * len(changed) <= moved <= len(changed)  # a spec that already had hostNetwork: true stays
     v1 = sc.scan(ps, nd2)
-    assert sc.last_stats["rescanned"] == len(changed) and not sc.last_stats["full"]
+    assert sc.last_stats["rescanned"] == moved and not sc.last_stats["full"]
     full, _, _ = eng.evaluate(ps, K.Corpus(nd2))
     assert (v1 == full).all()
     assert (v1 != v0).any()
