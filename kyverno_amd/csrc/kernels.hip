@@ -1065,14 +1065,15 @@ namespace {
 #include "patvm.inl"
 }  // namespace
 
-// grid: x = 256-row blocks; y = 1 (one lane per row, every rule) or the pattern rules (one rule
-// per wave, KPE_PAT_CELLS)
-__global__ void __launch_bounds__(256) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
+// grid: 256-row blocks, one lane per row running every pattern rule
+#ifndef KPE_PAT_WAVES
+#define KPE_PAT_WAVES 5  // 96 VGPRs: C5 29.0 -> 28.1 ms, C3 15.6 -> 14.4 ms (6: 80 VGPRs, C5 27.0, C3 15.5)
+#endif
+__global__ void __launch_bounds__(256, KPE_PAT_WAVES) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
   const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= ap->n) return;
   const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
-  if (gridDim.y == 1 && ap->npr > 1) pat_eval_row(*ap, r);
-  else pat_eval_cell(*ap, r, blockIdx.y);
+  pat_eval_row(*ap, r);
 }
 
 // ===========================================================================
@@ -1119,11 +1120,9 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
 
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s) {
   if (n <= 0 || npr == 0) return hipSuccess;
-  // one lane per row running every pattern rule; KPE_PAT_CELLS=1: a rows x rules grid (measured
-  // no faster on C5 and slower on C3's 600 rules: both are bound by the dependent tape loads of
-  // the longest walks, not by the rule loop)
-  static const bool rows = getenv("KPE_PAT_CELLS") == nullptr;
-  hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + 255) / 256), rows ? 1u : npr), dim3(256), 0, s, dargs);
+  // one lane per row running every pattern rule (a rows x rules grid measured no faster on C5 and
+  // slower on C3's 600 rules; it also doubled the VM code the kernel holds)
+  hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dargs);
   return hipGetLastError();
 }
 

@@ -388,56 +388,29 @@ __device__ __forceinline__ uint32_t pat_match_root(PatVM& vm, uint32_t root) {
 }
 
 // kpe_pattern_kernel's body for resource r: resolve the row's KPE_PENDING_ pattern cells
-// (validate_resource.go:316-398: one pattern, or anyPattern's first pass / skip / fail)
-// One (resource, pattern rule) cell: kpe_pattern_kernel runs a grid of rows x pattern rules, so
-// the lanes of a wave run one rule's program (cells of different rules are independent: applyRules
-// One with pattern rules is refused at compile time).
-__device__ __forceinline__ void pat_eval_cell(const PatArgs& a, int64_t r, uint32_t i) {
-  const KpePatRule pr = a.rules[i];
-  uint8_t* cell = a.verdicts + (size_t)r * a.R + pr.col;
-  if (*cell != KPE_PENDING_) return;
-  PatVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r]};
-  uint32_t v;
-  if (!(pr.flags & PR_ANY)) {
-    v = pat_match_root(vm, pr.r0);
-  } else if (pr.flags & PR_ANY_BAD) {
-    v = KPE_ERROR_;  // anyPattern is not a list
-  } else {
-    uint32_t fails = 0, skips = 0;
-    bool passed = false;
-    for (uint32_t k = 0; k < pr.nr && !passed; ++k) {
-      const uint32_t x = pat_match_root(vm, pr.r0 + k);
-      if (x == KPE_PASS_) passed = true;
-      else if (x == KPE_SKIP_) ++skips;
-      else ++fails;  // an empty-path error counts as a failure here
-    }
-    v = passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
-  }
-  *cell = (uint8_t)v;
-}
-
+// (validate_resource.go:316-398: one pattern, or anyPattern's first pass / skip / fail). The
+// pattern roots of every rule run through one VM call site (a plain pattern is one root), so
+// the kernel holds a single copy of the VM: its code stays within the instruction cache.
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
   PatVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r]};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   for (uint32_t i = 0; i < a.npr; ++i) {
     const KpePatRule pr = a.rules[i];
     if (row[pr.col] != KPE_PENDING_) continue;
-    uint32_t v;
-    if (!(pr.flags & PR_ANY)) {
-      v = pat_match_root(vm, pr.r0);
-    } else if (pr.flags & PR_ANY_BAD) {
-      v = KPE_ERROR_;  // anyPattern is not a list
-    } else {
-      uint32_t fails = 0, skips = 0;
-      bool passed = false;
-      for (uint32_t k = 0; k < pr.nr && !passed; ++k) {
-        const uint32_t x = pat_match_root(vm, pr.r0 + k);
-        if (x == KPE_PASS_) passed = true;
-        else if (x == KPE_SKIP_) ++skips;
-        else ++fails;  // an empty-path error counts as a failure here
-      }
-      v = passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
+    if (pr.flags & PR_ANY_BAD) {
+      row[pr.col] = (uint8_t)KPE_ERROR_;  // anyPattern is not a list
+      continue;
     }
+    const bool any = (pr.flags & PR_ANY) != 0u;
+    uint32_t fails = 0, skips = 0, last = KPE_PASS_;
+    bool passed = false;
+    for (uint32_t k = 0; k < pr.nr && !passed; ++k) {
+      last = pat_match_root(vm, pr.r0 + k);
+      if (last == KPE_PASS_) passed = true;
+      else if (last == KPE_SKIP_) ++skips;
+      else ++fails;  // anyPattern: an empty-path error counts as a failure
+    }
+    const uint32_t v = !any ? last : passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
     row[pr.col] = (uint8_t)v;
   }
 }
