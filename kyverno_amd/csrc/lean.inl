@@ -376,6 +376,43 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
   uint8_t* const verdicts = a0.verdicts;
   uint32_t* const stage = dyn + a0.wave_lds + wv * a0.wave_words;
   const uint32_t cls_cv0 = hw(cls_cv, 0), cls_rm0 = hw(cls_rm, 0);
+#if KPE_LEAN3_DIRECT
+  // Phase 1 for every tile of the wave: the scan of the pod records' packed counts, then every
+  // tile's list loads at once, so the wave has two dependent memory steps in all (records /
+  // headers, then items) whatever KPE_LEAN_T is; phase 2 (below) evaluates the tiles in turn.
+  struct DItems {
+    uint32_t oc, ov, os, oa;
+    uint2 e0, e1, e2, e3, q0, q1;
+    uint32_t w0, w1, s0, s1;
+  };
+  DItems di[KPE_LEAN_T];
+  constexpr uint32_t kOOB = 0xFFFFFFF0u;
+#pragma unroll
+  for (uint32_t j = 0; j < KPE_LEAN_T; ++j) {
+    DItems& d = di[j];
+    const uint32_t C0 = hw(hall, 4u * j), V0 = hw(hall, 4u * j + 1u), S0 = hw(hall, 4u * j + 2u),
+                   A0 = hw(hall, 4u * j + 3u);
+    const uint32_t nct = hw(hall, 4u * j + 4u) - C0, nvt = hw(hall, 4u * j + 5u) - V0,
+                   nst = hw(hall, 4u * j + 6u) - S0, nat = hw(hall, 4u * j + 7u) - A0;
+    const uint32_t z = it[j].rec.z;
+    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+    if ((nct | nvt | nst | nat) < 256u) {  // one scan of the four packed byte counts (no carries)
+      const uint32_t e = wave_incl_scan(z) - z;
+      d.oc = e & 0xFFu, d.ov = (e >> 8) & 0xFFu, d.os = (e >> 16) & 0xFFu, d.oa = e >> 24;
+    } else {
+      const uint32_t c01 = nc | (nv << 16), c23 = ns | (na << 16);
+      const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
+      d.oc = e01 & 0xFFFFu, d.ov = e01 >> 16, d.os = e23 & 0xFFFFu, d.oa = e23 >> 16;
+    }
+    const uint32_t cb = (C0 + d.oc) * 8u, vb = (V0 + d.ov) * 4u, sb = (S0 + d.os) * 4u, ab = (A0 + d.oa) * 8u;
+    d.e0 = bload2(L.crec, nc > 0u ? cb : kOOB), d.e1 = bload2(L.crec, nc > 1u ? cb + 8u : kOOB);
+    d.e2 = bload2(L.crec, nc > 2u ? cb + 16u : kOOB), d.e3 = bload2(L.crec, nc > 3u ? cb + 24u : kOOB);
+    d.w0 = nvol ? bload1(L.vol, nv > 0u ? vb : kOOB) : 0u, d.w1 = nvol ? bload1(L.vol, nv > 1u ? vb + 4u : kOOB) : 0u;
+    d.s0 = d.s1 = 0u, d.q0 = d.q1 = make_uint2(0u, 0u);
+    if (nsys && nst) d.s0 = bload1(L.sys, ns > 0u ? sb : kOOB), d.s1 = bload1(L.sys, ns > 1u ? sb + 4u : kOOB);
+    if (npann && nat) d.q0 = bload2(L.ann, na > 0u ? ab : kOOB), d.q1 = bload2(L.ann, na > 1u ? ab + 8u : kOOB);
+  }
+#endif
 #pragma unroll
   for (uint32_t j = 0; j < KPE_LEAN_T; ++j) {
     const uint32_t tile = t0 + j;
@@ -395,6 +432,9 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
     }
     const uint32_t z = cur.rec.z;
     const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+#if KPE_LEAN3_DIRECT
+    const uint32_t oc = di[j].oc, ov = di[j].ov, os = di[j].os, oa = di[j].oa;
+#else
     uint32_t oc, ov, os, oa;
     if ((nct | nvt | nst | nat) < 256u) {  // one scan of the four packed byte counts (no carries)
       const uint32_t e = wave_incl_scan(z) - z;
@@ -404,21 +444,16 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
       const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
       oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
     }
+#endif
 #if KPE_LEAN3_DIRECT
     // Each lane reads its own pod's list items (its offsets from the scan): the first four
     // containers, two volumes and (when the tile has any) two sysctls / annotations are issued
     // together; an item past the pod's count reads past the column's end and returns 0. Pods
     // with more items take a loop. No staging area, no wave barrier, no capacity limit.
     (void)nvt;
-    constexpr uint32_t kOOB = 0xFFFFFFF0u;
     const uint32_t cb = (C0 + oc) * 8u, vb = (V0 + ov) * 4u, sb = (S0 + os) * 4u, ab = (A0 + oa) * 8u;
-    const uint2 e0 = bload2(L.crec, nc > 0u ? cb : kOOB), e1 = bload2(L.crec, nc > 1u ? cb + 8u : kOOB),
-                e2 = bload2(L.crec, nc > 2u ? cb + 16u : kOOB), e3 = bload2(L.crec, nc > 3u ? cb + 24u : kOOB);
-    const uint32_t w0 = bload1(L.vol, nv > 0u ? vb : kOOB), w1 = bload1(L.vol, nv > 1u ? vb + 4u : kOOB);
-    uint32_t s0 = 0, s1 = 0;
-    uint2 q0 = make_uint2(0u, 0u), q1 = make_uint2(0u, 0u);
-    if (nsys && nst) s0 = bload1(L.sys, ns > 0u ? sb : kOOB), s1 = bload1(L.sys, ns > 1u ? sb + 4u : kOOB);
-    if (npann && nat) q0 = bload2(L.ann, na > 0u ? ab : kOOB), q1 = bload2(L.ann, na > 1u ? ab + 8u : kOOB);
+    const uint2 e0 = di[j].e0, e1 = di[j].e1, e2 = di[j].e2, e3 = di[j].e3, q0 = di[j].q0, q1 = di[j].q1;
+    const uint32_t w0 = di[j].w0, w1 = di[j].w1, s0 = di[j].s0, s1 = di[j].s1;
     auto vol_code = [&](uint32_t sv0) -> uint32_t { return ((sv0 >> VS_HOSTPATH) & 1u) | ((sv0 & kAllowedVolumes) ? 0u : 2u); };
     auto sys_code = [&](uint32_t id) -> uint32_t {
       return (pbit(p_s0, id) ^ 1u) | ((pbit(p_s1, id) ^ 1u) << 1) | ((pbit(p_s2, id) ^ 1u) << 2);
