@@ -183,6 +183,7 @@ struct PatArgs {
   const uint8_t* pat_bytes;
   const uint32_t* roots;           // (node, anchor slots) pairs
   const KpePatRule* rules;
+  const uint32_t* col2pr;          // verdict column -> pattern rule index + 1 (0: none), or null
   const uint32_t* pbuf;            // glob member-name bitsets (HBM)
   uint8_t* verdicts;
   // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)

@@ -143,6 +143,7 @@ struct DeviceProgram {
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
   DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
+  DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
   DevBuf cops, cexprs, ctmpls, cconds, cblocks, cfes, crules, cconsts, ctext, cclist;
   DevBuf xrules;  // podSecurity rules with exclusions (program.hpp PssxProgram)
@@ -531,6 +532,11 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.pbytes, pb, s0));
     HIPCHK(upload(D.proots, PP.roots, s0));
     HIPCHK(upload(D.prules, PP.rules, s0));
+    {
+      std::vector<uint32_t> c2p(P.rules.size() + 4, 0u);  // + slack: the kernel reads whole words
+      for (size_t i = 0; i < PP.rules.size(); ++i) c2p[PP.rules[i].col] = (uint32_t)i + 1u;
+      HIPCHK(upload(D.pcol2pr, c2p, s0));
+    }
     const auto& CP = P.cond;
     HIPCHK(upload(D.cops, CP.ops, s0));
     HIPCHK(upload(D.cexprs, CP.exprs, s0));
@@ -925,7 +931,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     B.napply_segs = (uint32_t)(segs.size() / 2);
     if (!segs.empty()) HIPCHK(upload(B.apply_segs, segs, s));
   }
-  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 4));
+  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 8));  // + slack: the pattern kernel reads two words past a row's cells
   HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 8, 1) * 8));
   if (!B.zero_page.p) {
     HIPCHK(B.zero_page.ensure(256));
@@ -1201,6 +1207,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.pat_bytes = PD.pbytes.as<uint8_t>();
       pa.roots = PD.proots.as<uint32_t>();
       pa.rules = PD.prules.as<KpePatRule>();
+      pa.col2pr = PD.pcol2pr.as<uint32_t>();
       pa.pbuf = B.pbuf.as<uint32_t>();
       pa.verdicts = B.verdicts.as<uint8_t>();
       pa.nnodes = (uint32_t)P.pat.nodes.size(), pa.nmembers = (uint32_t)(P.pat.members.size() / 4);

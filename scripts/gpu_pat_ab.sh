@@ -10,7 +10,5 @@ for c in c5 c3; do
     [ -e "$lib" ] || continue
     KPE_LIB=$PWD/$lib timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/pat_ab.log 2>&1 || { tail -3 gpurun_out/pat_ab.log; exit 1; }
     echo "$c $(basename $lib): $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/pat_ab.log | head -1)"
-    KPE_PERM=1 KPE_LIB=$PWD/$lib timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0 > gpurun_out/pat_ab.log 2>&1 || { tail -3 gpurun_out/pat_ab.log; exit 1; }
-    echo "$c $(basename $lib) KPE_PERM: $(grep -o '"kernel_ms": [0-9.]*' gpurun_out/pat_ab.log | head -1)"
   done
 done

@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
     mem[i] = m;
   }
   const uint32_t R = (uint32_t)P->rules.size();
-  std::vector<uint8_t> verdicts((size_t)C.n * R, 0);
+  std::vector<uint8_t> verdicts((size_t)C.n * R + 8, 0);  // + slack: the kernel reads whole words
   for (int64_t r = 0; r < C.n; ++r)
     for (auto& pr : PP.rules) verdicts[(size_t)r * R + pr.col] = KPE_PENDING_;
   std::vector<KpeScalar> scal(C.scal);
@@ -120,6 +120,9 @@ int main(int argc, char** argv) {
   a.nodes = PP.nodes.data(), a.members = mem.data(), a.lists = PP.lists.data(), a.leaves = PP.leaves.data();
   a.conds = PP.conds.data(), a.pats = pats.data(), a.pat_bytes = pb.data(), a.roots = PP.roots.data();
   a.rules = PP.rules.data(), a.pbuf = pbuf.data(), a.verdicts = verdicts.data();
+  std::vector<uint32_t> col2pr(R + 4, 0u);
+  for (size_t i = 0; i < PP.rules.size(); ++i) col2pr[PP.rules[i].col] = (uint32_t)i + 1u;
+  a.col2pr = col2pr.data();
   uint32_t err = 0;
   a.nnodes = (uint32_t)PP.nodes.size(), a.nmembers = (uint32_t)mem.size(), a.nlists = (uint32_t)PP.lists.size();
   a.nleaves = (uint32_t)PP.leaves.size(), a.nconds = (uint32_t)PP.conds.size(), a.npats = (uint32_t)pats.size();
@@ -127,7 +130,7 @@ int main(int argc, char** argv) {
   a.ndoc = C.doc.size() / 2, a.err = &err;
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r);  // kpe_pattern_kernel's lane body
   FILE* f = fopen(argv[3], "wb");
-  fwrite(verdicts.data(), 1, verdicts.size(), f);
+  fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
   printf("%lld %u err=0x%x\n", (long long)C.n, R, err);
   if (err) return 1;
