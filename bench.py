@@ -78,7 +78,9 @@ def main():
         workload = "C5: 1M Pods/Deployments with 1-64 containers x requests-limits/latest-tag/host-ports/anchor patterns"
     n = args.resources or n_def
     replicas = args.replicas or rep_def
-    traffic_json = args.traffic_json or os.path.join(ROOT, "profiles", f"pmc_traffic_{cfg}.json")
+    # HBM bytes per scan launch from the FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py);
+    # perf/ travels to the GPU box, profiles/ does not
+    traffic_json = args.traffic_json or os.path.join(ROOT, "perf", f"pmc_traffic_{cfg}.json")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

@@ -20,6 +20,9 @@ step() {  # step <name> <timeout> <cmd...>
 [ -n "$SKIP_TESTS" ] || step smoke 200 python -c "import __graft_entry__ as g; g.smoke()"
 step bench_c2 300 python bench.py
 step bench_ranks2 300 env KPE_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 50 --warmup 5 --cpu-sample 0
+for c in c3 c4 c5; do
+  step bench_$c 300 python bench.py --config $c --steps 10 --warmup 2
+done
 BENCH_ARGS="--steps 100 --warmup 10 --cpu-sample 0" bash scripts/profile.sh || exit $?
 for c in c3 c5; do
   step trace_$c 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace_$c -o $c --output-format csv -- python3 bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0

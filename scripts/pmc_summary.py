@@ -55,6 +55,6 @@ if fm is not None and wm is not None:
          "correction": "FETCH_SIZE x2 (gfx950 half-count of wide coalesced reads), KiB -> bytes",
          "source": f"profiles/{tag}/pmc_fetch_summary.csv, pmc_write_summary.csv"}
     cfg = os.environ.get("CFG", "c2")  # bench.py reads profiles/pmc_traffic_<config>.json
-    for out in (os.path.join(dst, "pmc_traffic.json"), os.path.join("profiles", f"pmc_traffic_{cfg}.json")):
+    for out in (os.path.join(dst, "pmc_traffic.json"), os.path.join("perf", f"pmc_traffic_{cfg}.json")):
         json.dump(t, open(out, "w"), indent=1)
     print("traffic", t["scan_bytes_per_launch"])
