@@ -490,10 +490,37 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
   return cv_fails(d.rec.x, xo, co & 7u, co & 8u, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & a.cv_union;
 }
 
+// The first kLabCache labels of the lane's resource (or of its namespace), loaded once per tile
+// with independent loads: selector terms then test them from registers (constant indices after
+// unrolling) instead of a dependent label load per requirement and term; longer label lists
+// continue from memory.
+constexpr uint32_t kLabCache = 8;
+struct LabCache {
+  uint32_t lo, hi;
+  uint32_t k[kLabCache], v[kLabCache];
+};
+__device__ __forceinline__ void lab_fill(LabCache& c, const uint32_t* K, const uint32_t* V, uint32_t lo, uint32_t hi) {
+  c.lo = lo, c.hi = hi;
+#pragma unroll
+  for (uint32_t j = 0; j < kLabCache; ++j) {
+    const bool in = lo + j < hi;
+    c.k[j] = in ? K[lo + j] : KPE_NO_STR;
+    c.v[j] = in ? V[lo + j] : KPE_NO_STR;
+  }
+}
+
+// the resource's label cache (label selectors; a namespace's labels are shared by its
+// resources and stay cache-resident, so namespaceSelector terms read them from memory)
+__device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC) {
+  uint32_t lo = 0, hi = 0;
+  if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = live ? a.lab_off[rc + 1] : lo;
+  lab_fill(LC, a.lab_k, a.lab_v, lo, hi);
+}
+
 // One match term for this lane's resource (utils/match.go:52-160 attributes).
 __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm& tm, uint32_t gvk,
                                           uint32_t nsa, uint32_t name_col, uint32_t mns_col, uint32_t rc,
-                                          bool live) {
+                                          bool live, const LabCache& LC) {
   bool ok = true;
   if (tm.type == T_KIND_PRED) {
     ok = B.bit(tm.a, GVK_KIND(gvk));
@@ -522,16 +549,15 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
     // CheckSelector (pkg/utils/match/labels.go:9-24) over the resource's labels or,
     // for namespaceSelector, its namespace's labels (utils/match.go:114-138)
     const KpeSelector S = sld(a.selectors, tm.a);
-    uint32_t lo = 0, hi = 0;
+    const bool nssel = tm.type == T_NSSELECTOR;
+    uint32_t lo = LC.lo, hi = LC.hi;
     const uint32_t *K = a.lab_k, *V = a.lab_v;
     bool eval = true;
-    if (tm.type == T_SELECTOR) {
-      lo = a.lab_off[rc];
-      hi = live ? a.lab_off[rc + 1] : lo;
-    } else {
+    if (nssel) {
       // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
       const uint32_t kid = GVK_KIND(gvk);
       const uint32_t row = a.r_nsl[rc];
+      lo = hi = 0;
       if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
       K = a.nsl_k, V = a.nsl_v;
       if (B.bit(S.p_kind_ns, kid)) {
@@ -547,12 +573,19 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
       for (uint32_t qi = 0; qi < S.nreq; ++qi) {
         const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
         const bool wild = q.op == SR_WILD;
-        uint32_t j = lo;
+        // first label with a matching key (and value, for wildcards): the cached ones, then memory
+        bool found = false;
+        uint32_t kid = KPE_NO_STR, vid = KPE_NO_STR;
+        if (!nssel) {
+#pragma unroll
+          for (uint32_t j = 0; j < kLabCache; ++j) {
+            const uint32_t kk = LC.k[j], vv = LC.v[j];
+            if (!found && lo + j < hi && B.bit(q.pk, kk) && (!wild || B.bit(q.pv, vv))) found = true, kid = kk, vid = vv;
+          }
+        }
 #pragma unroll 1
-        for (; j < hi; ++j)  // first label with a matching key (and value, for wildcards)
-          if (B.bit(q.pk, K[j]) && (!wild || B.bit(q.pv, V[j]))) break;
-        const bool found = j < hi;
-        const uint32_t kid = found ? K[j] : KPE_NO_STR, vid = found ? V[j] : KPE_NO_STR;
+        for (uint32_t j = nssel ? lo : lo + kLabCache; !found && j < hi; ++j)
+          if (B.bit(q.pk, K[j]) && (!wild || B.bit(q.pv, V[j]))) found = true, kid = K[j], vid = V[j];
         bool qok;
         switch (q.op) {
           case SR_EQ:
@@ -845,10 +878,12 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       // ---- terms -> bit vector ----
       uint32_t tb = 0;
       if constexpr (!LEAN) {
+        LabCache LC;
+        lab_cache(a, rc, live, LC);
 #pragma unroll 1
         for (uint32_t ti = 0; ti < a.nterms; ++ti) {
           const KpeTerm tm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u};
-          tb |= eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live) ? (1u << ti) : 0u;
+          tb |= eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live, LC) ? (1u << ti) : 0u;
         }
       }
       if (LEAN || (a.tt_lds != PRED_NONE && !a.masks)) {  // truth-table fast path (LEAN: the kind table)
@@ -915,9 +950,11 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     const KpeFilter* filt =
         a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
+    LabCache LC;
+    lab_cache(a, rc, live, LC);
 #pragma unroll 1
     for (uint32_t ti = 0; ti < a.nterms; ++ti) {
-      const uint64_t m = __ballot(eval_term(a, B, sld(a.terms, ti), gvk, nsa, name_col, mns_col, rc, live));
+      const uint64_t m = __ballot(eval_term(a, B, sld(a.terms, ti), gvk, nsa, name_col, mns_col, rc, live, LC));
       if (lane == 0) tmk[ti] = m;
     }
     // PSS version sets: resources failing some check of each distinct cv_mask
