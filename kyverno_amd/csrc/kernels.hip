@@ -496,7 +496,8 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
 // continue from memory.
 constexpr uint32_t kLabCache = 8;
 struct LabCache {
-  uint32_t lo, hi;
+  uint32_t lo, hi;    // the resource's labels
+  uint32_t nlo, nhi;  // its namespace's labels (namespaceSelector), read from memory
   uint32_t k[kLabCache], v[kLabCache];
 };
 __device__ __forceinline__ void lab_fill(LabCache& c, const uint32_t* K, const uint32_t* V, uint32_t lo, uint32_t hi) {
@@ -515,6 +516,11 @@ __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabC
   uint32_t lo = 0, hi = 0;
   if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = live ? a.lab_off[rc + 1] : lo;
   lab_fill(LC, a.lab_k, a.lab_v, lo, hi);
+  LC.nlo = LC.nhi = 0;
+  if (a.need & NEED_NSL) {  // the namespace row's bounds, once per resource instead of per term
+    const uint32_t row = a.r_nsl[rc];
+    if (live && row != KPE_NO_STR) LC.nlo = a.nsl_off[row], LC.nhi = a.nsl_off[row + 1];
+  }
 }
 
 // One match term for this lane's resource (utils/match.go:52-160 attributes).
@@ -556,9 +562,7 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
     if (nssel) {
       // never for kind Namespace; skipped for an empty kind unless kinds hold "*"
       const uint32_t kid = GVK_KIND(gvk);
-      const uint32_t row = a.r_nsl[rc];
-      lo = hi = 0;
-      if (live && row != KPE_NO_STR) lo = a.nsl_off[row], hi = a.nsl_off[row + 1];
+      lo = LC.nlo, hi = LC.nhi;
       K = a.nsl_k, V = a.nsl_v;
       if (B.bit(S.p_kind_ns, kid)) {
         ok = S.exc != 0u, eval = false;  // PolicyException blocks skip the check (match.go:184)
