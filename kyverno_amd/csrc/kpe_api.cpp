@@ -460,8 +460,9 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     lanes.push_back(r.pol_term < 0 ? PRED_NONE : (uint32_t)r.pol_term);
   }
   // NARROW programs: per-rule records + per-filter term masks (kernels_abi.h NR_*)
-  const bool narrow = !P.rules.empty() && P.rules.size() <= KPE_NARROW_R && P.terms.size() <= KPE_NARROW_TERMS &&
-                      P.filters.size() <= KPE_NARROW_FILTERS;
+  static const bool no_narrow = getenv("KPE_NO_NARROW") != nullptr;  // experiments: force the wide path
+  const bool narrow = !no_narrow && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
+                      P.terms.size() <= KPE_NARROW_TERMS && P.filters.size() <= KPE_NARROW_FILTERS;
   std::vector<uint32_t> nrules, fmask;
   if (narrow) {
     for (auto& f : P.filters) {
