@@ -1447,6 +1447,12 @@ long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row,
         if (pod_state > 0) msg = kpe::pss_fail_message(rr.rule, rr.pss_level, rr.pss_version, kind, pod, cv_mask_row[r]);
       } else if (rr.msg_pattern && v == KPE_PASS) {
         msg = "validation rule '" + rr.rule + "' passed.";
+      } else if (rr.msg_deny && v == KPE_PASS) {
+        msg = "validation rule '" + rr.rule + "' passed.";
+      } else if (rr.msg_deny && v == KPE_FAIL) {
+        msg = rr.deny_fail_msg;
+      } else if (rr.msg_deny && rr.msg_pre_skip && v == KPE_SKIP && P.rules[r].exc == 0u) {
+        msg = "preconditions not met";  // a PolicyException's skip has its own message
       }
       if (!msg.empty()) {
         o += ",\"message\":";

@@ -2184,6 +2184,28 @@ class Lowerer {
     }
     rr.pss_excl = pss_excl;
     rr.msg_pattern = msg_pattern;
+    if (has_validate && !(ps && ps->t == JV::Obj && nonempty(ps)) && v->get("deny") && v->get("deny")->t == JV::Obj) {
+      // a condition `message` would enter the rule's message: render only when there is none
+      std::function<bool(const JV*)> has_msg = [&](const JV* j) -> bool {
+        if (!j) return false;
+        if (j->t == JV::Arr) {
+          for (auto& e : j->a)
+            if (has_msg(&e)) return true;
+          return false;
+        }
+        if (j->t != JV::Obj) return false;
+        if (j->get("key") || j->get("operator")) return nonempty(j->get("message"));
+        return has_msg(j->get("any")) || has_msg(j->get("all"));
+      };
+      if (!has_msg(v->get("deny")->get("conditions")) && !has_msg(pre_raw)) {
+        rr.msg_deny = true;
+        rr.msg_pre_skip = pre_raw && pre_raw->t != JV::Null;
+        const JV* m = v->get("message");
+        const std::string mt = (m && m->t == JV::Str) ? m->s : std::string();
+        if (mt.empty()) rr.deny_fail_msg = "validation error: rule " + rname + " failed";
+        else if (mt.find("{{") == std::string::npos && mt.find("$(") == std::string::npos) rr.deny_fail_msg = mt;
+      }
+    }
     P.reports.push_back(std::move(rr));
   }
 

@@ -84,6 +84,13 @@ struct RuleReport {
   bool pss = false;
   bool pss_excl = false;      // podSecurity.exclude non-empty (fail messages not rendered)
   bool msg_pattern = false;   // validate.pattern rule: pass message "validation rule '<rule>' passed."
+  // validate.deny rule whose conditions (and preconditions) carry no `message`, so the reference's
+  // condition message is empty (variables/evaluate.go:14-28): pass "validation rule '<rule>'
+  // passed.", fail `deny_fail_msg` (getDenyMessage, validate_resource.go:279-300; empty when the
+  // rule message has variables), skip "preconditions not met" (engine.go:283) when it has
+  // preconditions
+  bool msg_deny = false, msg_pre_skip = false;
+  std::string deny_fail_msg;
 };
 
 struct Program {

@@ -16,8 +16,12 @@ Restated:
 message (when a `pss_message` callable is given): podSecurity pass "Validation rule '<rule>'
 passed." (validate_pss.go:85), podSecurity fail without exclusions through the C++ oracle's
 FormatChecksPrint (validate_pss.go:108, oracle/pss.hpp format_checks_print), validate.pattern
-pass "validation rule '<rule>' passed." (validate_resource.go:339); other messages are not
-restated. Not restated: timestamp, exception
+pass "validation rule '<rule>' passed." (validate_resource.go:339), validate.deny rules whose
+conditions and preconditions carry no `message` (so the condition message is empty,
+variables/evaluate.go:14-28): pass "validation rule '<rule>' passed." (validate_resource.go:275),
+fail getDenyMessage (validate_resource.go:279-300: the rule message, or "validation error: rule
+<rule> failed" when it is empty; not restated when it holds variables), preconditions skip
+"preconditions not met" (engine.go:283); other messages are not restated. Not restated: timestamp, exception
 and ValidatingAdmissionPolicy branches (out of the path's scope).
 Autogen rules are mapped back to their source rule by the "autogen-" / "autogen-cronjob-"
 prefix (pkg/autogen/autogen.go:213-222); names truncated to 63 characters are not mapped
@@ -55,6 +59,17 @@ def _source_rule(policy: dict, rule_name: str) -> dict:
     return {}
 
 
+def _cond_messages(block) -> bool:
+    """True when a condition in a conditions block (list, or any / all lists) has a message."""
+    if isinstance(block, list):
+        return any(_cond_messages(c) for c in block)
+    if not isinstance(block, dict):
+        return False
+    if "key" in block or "operator" in block:
+        return bool(block.get("message"))
+    return _cond_messages(block.get("any")) or _cond_messages(block.get("all"))
+
+
 def report_results(policies: List[dict], rule_names: List[str], verdict_row, resource: dict,
                    failing_checks: Callable[[str, str, dict], List[str]],
                    pss_message: Optional[Callable[[str, str, str, dict], Optional[str]]] = None) -> List[Dict]:
@@ -85,6 +100,17 @@ def report_results(policies: List[dict], rule_names: List[str], verdict_row, res
                 msg = pss_message(rname, ps0.get("level", ""), ps0.get("version", ""), resource)
             elif not ps0 and val.get("pattern") is not None and cell == 1:
                 msg = f"validation rule '{rname}' passed."
+            elif not ps0 and isinstance(val.get("deny"), dict) and not _cond_messages(val["deny"].get("conditions")) \
+                    and not _cond_messages(_source_rule(pol, rname).get("preconditions")):
+                m = val.get("message") if isinstance(val.get("message"), str) else ""
+                if cell == 1:
+                    msg = f"validation rule '{rname}' passed."
+                elif cell == 2 and not m:
+                    msg = f"validation error: rule {rname} failed"
+                elif cell == 2 and "{{" not in m and "$(" not in m:
+                    msg = m
+                elif cell == 5 and _source_rule(pol, rname).get("preconditions") is not None:
+                    msg = "preconditions not met"
             if msg:
                 item["message"] = msg
         if rname:

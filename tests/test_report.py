@@ -95,6 +95,58 @@ def test_host_messages_match_oracle(oracle):
     assert nmsg > 100
 
 
+def _deny_message_policies():
+    """cond_policy_set with the deny rule messages varied: kept, removed (default message),
+    with variables (not rendered), a condition message (not rendered) and preconditions."""
+    from tests.policies import cond_policy_set
+    pols = copy.deepcopy(cond_policy_set())
+    rules = pols[0]["spec"]["rules"]
+    for i, r in enumerate(rules):
+        val = r.get("validate") or {}
+        if "deny" not in val:
+            continue
+        if i % 4 == 1:
+            del val["message"]
+        elif i % 4 == 2:
+            val["message"] = "bad {{ request.object.metadata.name }}"
+        elif i % 4 == 3:
+            val["message"] = f"rule {i}: <no> & \"quotes\""
+    obj = "request.object"
+    rules.append({"name": "deny-pre", "match": {"any": [{"resources": {"kinds": ["Pod", "Deployment"]}}]},
+                  "preconditions": {"any": [{"key": "{{ " + obj + ".metadata.labels.tier || '' }}",
+                                             "operator": "Equals", "value": "frontend"}]},
+                  "validate": {"deny": {"conditions": {"all": [
+                      {"key": "{{ " + obj + ".metadata.labels.app || '' }}", "operator": "NotEquals",
+                       "value": "app-1*"}]}}}})
+    rules.append({"name": "deny-cond-msg", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+                  "validate": {"message": "m", "deny": {"conditions": {"any": [
+                      {"key": "{{ " + obj + ".metadata.labels.app || '' }}", "operator": "Equals",
+                       "value": "app-1*", "message": "app label"}]}}}})
+    return pols
+
+
+def test_host_deny_messages_match_oracle(oracle):
+    """kpe_report_results_msg renders deny pass / fail / preconditions-skip messages
+    (validate_resource.go:268-300, engine.go:283) like the oracle's report on the
+    condition-rule set, with the rule message kept, removed, templated or escaped."""
+    pols = _deny_message_policies()
+    ps = K.PolicySet(pols)
+    names = oracle.rule_names(pols)
+    seen = set()
+    for mix, seed in ((2, 0x3D), (4, 5)):
+        nd = K.synth_resources(seed, 300, mix=mix)
+        docs = [json.loads(x) for x in nd.split(b"\n") if x.strip()]
+        v = oracle.validate(pols, nd, nthreads=4)
+        for i, doc in enumerate(docs):
+            want = oracle_report.report_results(pols, names, v[i], doc, oracle.failing_checks, oracle.pss_message)
+            got = K.report_results(ps, v[i], _oracle_cv_row(oracle, pols, names, v[i], doc), resource=doc)
+            assert got == want, (i, got, want)
+            seen.update((r["result"], r.get("message", "")[:20]) for r in got)
+    msgs = {m for _, m in seen}
+    assert "validation error: ru" in msgs and "preconditions not me" in msgs and "m" in msgs
+    assert any(m.startswith("rule ") for m in msgs) and any(m.startswith("validation rule") for m in msgs)
+
+
 def test_host_report_matches_oracle_without_controls(oracle):
     pols = report_policy_set()
     ps = K.PolicySet(pols)
