@@ -206,7 +206,11 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
  * ("Validation rule '<rule>' passed.", validate_pss.go:85) and fail (validate_pss.go:108:
  * FormatChecksPrint of the failing checks after convertChecks, rules without
  * podSecurity.exclude) and validate.pattern pass ("validation rule '<rule>' passed.",
- * validate_resource.go:339). Other results carry no message. Host only. */
+ * validate_resource.go:339), and for validate.deny rules whose conditions carry no `message`:
+ * pass ("validation rule '<rule>' passed."), fail (getDenyMessage, validate_resource.go:279-300:
+ * the rule message, or "validation error: rule <rule> failed" when it is empty; none when it
+ * holds variables) and preconditions skip ("preconditions not met", engine.go:283). Other
+ * results carry no message. Host only. */
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
                             const char* resource_json, size_t resource_len, char* buf, size_t cap);
 
