@@ -461,7 +461,13 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   }
   // NARROW programs: per-rule records + per-filter term masks (kernels_abi.h NR_*)
   static const bool no_narrow = getenv("KPE_NO_NARROW") != nullptr;  // experiments: force the wide path
-  const bool narrow = !no_narrow && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
+  // Label selector terms stay on the wide path: per lane, the narrow loop walks every selector's
+  // requirement records with scalar loads and is issue-bound (C4: 0.22 ms narrow, 0.19 ms wide,
+  // profiles/r02_c4)
+  const bool sel_terms = std::any_of(P.terms.begin(), P.terms.end(), [](const KpeTerm& t) {
+    return t.type == T_SELECTOR || t.type == T_NSSELECTOR;
+  });
+  const bool narrow = !no_narrow && !sel_terms && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
                       P.terms.size() <= KPE_NARROW_TERMS && P.filters.size() <= KPE_NARROW_FILTERS;
   std::vector<uint32_t> nrules, fmask;
   if (narrow) {
