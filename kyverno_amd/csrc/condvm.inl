@@ -488,6 +488,20 @@ struct CondVM {
       *c0 = (uint32_t)s.ival, *cn = (uint32_t)((uint64_t)s.ival >> 32);
       return 1;
     }
+    if (v.k == VK_NODE) {  // the flattener's json.Valid (SC_JVALID / SC_JARR)
+      const uint8_t* t;
+      const KpeScalar* s = scalar(v, &t);
+      if (!(s->flags & SC_JVALID)) return 0;
+      if (s->flags & SC_JARR) return -1;  // a JSON array: its []string decode stays on the host
+      const SView x = str(v);
+      int i = 0;
+      while (i < x.n && (x.s[i] == ' ' || x.s[i] == '\t' || x.s[i] == '\n' || x.s[i] == '\r')) ++i;
+      if (i < x.n && x.s[i] == 'n') {  // null: a nil slice
+        *c0 = 0, *cn = 0;
+        return 1;
+      }
+      return 2;  // valid JSON that is not a list: the Unmarshal error (invalid type)
+    }
     const SView s = str(v);
     int i = 0;
     while (i < s.n && (s.s[i] == ' ' || s.s[i] == '\t' || s.s[i] == '\n' || s.s[i] == '\r')) ++i;
@@ -498,7 +512,7 @@ struct CondVM {
     return 0;
   }
   // anyin.go / allin.go / anynotin.go / allnotin.go
-  __device__ __forceinline__ int op_set(uint32_t op, CV k, CV v) {
+  __device__ __forceinline__ int op_set(uint32_t op, CV k, CV v, uint32_t rng) {
     const uint32_t kt = type(k), vt = type(v);
     if (kt == JT_NULL || kt == JT_OBJ) return 0;
     const bool notin = op == CO_ANYNOTIN || op == CO_ALLNOTIN;
@@ -517,6 +531,34 @@ struct CondVM {
         if (!sprint(aget(k, 0), 0, &x)) return -1;
         if (seq(x, vs)) return !notin;
       }
+      bool rt = false;  // a resource string in the InRange form
+      if (v.k == VK_NODE) {
+        const uint8_t* t;
+        const uint32_t f = scalar(v, &t)->flags;
+        if (f & SC_RANGEU) return -1;
+        rt = (f & SC_RANGE) != 0u;
+      }
+      if (rng || rt) {  // InRange value: handleRange per key (anyin.go:76-77,146-165; allin.go)
+        const uint32_t li = rng - 1u;
+        if (single) {
+          const int h = rt ? range_rt(k, v, false) : range_holds(k, li);
+          return h < 0 ? -1 : ((h == 1) != notin);
+        }
+        // AnyIn: some key in range; AnyNotIn: some key in the `!-` form; AllIn: every key;
+        // AllNotIn: no key
+        const uint32_t lj = op == CO_ANYNOTIN ? li + 1u : li;
+        int undec = 0, hits = 0;
+        for (uint32_t i = 0; i < nk; ++i) {
+          const int h = rt ? range_rt(aget(k, i), v, op == CO_ANYNOTIN) : range_holds(aget(k, i), lj);
+          if (h < 0) undec = 1;
+          else hits += h;
+        }
+        if (op == CO_ANYIN || op == CO_ANYNOTIN) return hits ? 1 : (undec ? -1 : 0);
+        if (op == CO_ALLIN) return (hits == (int)nk) ? 1 : (undec ? -1 : 0);
+        return hits ? 0 : (undec ? -1 : 1);  // CO_ALLNOTIN
+      }
+      // member names carry no attributes (json_list leaves digit / sign starts undecided)
+      if (v.k == VK_KEY && vs.n > 0 && (vs.s[0] == '+' || vs.s[0] == '|')) return -1;
       const int j = json_list(v, &vc0, &vcn);
       if (j < 0) return -1;
       if (j == 2) return 0;
@@ -641,6 +683,314 @@ struct CondVM {
     return notin ? any_missing : all;
   }
 
+  // ---- InRange values of the set operators -------------------------------------------------
+  // anyin.go:103-109 handleRange: pattern.Validate(key, value) with the key as its fmt.Sprint
+  // string: validateStringPatterns (pattern.go:152-215) of the compiled value leaf. 1 / 0, -1
+  // where the key's Sprint text has no parsed attributes on the device.
+  __device__ __forceinline__ bool rcond(const KpeScalar* v, uint32_t vf, SView vt, const KpeCond& cd) const {
+    const uint32_t cop = cd.op, op = PC_OP(cop);
+    if ((cop & PC_DUR) && (vf & SC_DUR)) return op_holds(op, v->dur < cd.dur ? -1 : (v->dur > cd.dur ? 1 : 0));
+    if ((cop & PC_QTY) && (vf & SC_QTY))
+      return op_holds(op, qcmp(vf & SC_QNEG, v->qexp, v->qlo, v->qhi, cop & PC_QNEG, cd.qexp, cd.qlo, cd.qhi));
+    if (op != PC_EQ && op != PC_NE) return false;
+    const bool m = pv_match(a.pats[cd.pat], a.pat_bytes, vt.s, vt.n);
+    return op == PC_NE ? !m : m;
+  }
+  // The key as the Go string handleRange receives (fmt.Sprint): its text, and the parsed
+  // duration / quantity attributes that stand for it (vf; *s holds the values). -1: undecided
+  // (a member name that may parse, a map / list, 0 against a duration operand, a number whose
+  // Sprint quantity is not its %f one).
+  __device__ __forceinline__ int key_text(CV k, bool dur_operand, const KpeScalar** sp, uint32_t* vfp, SView* tp) const {
+    const KpeScalar* s = nullptr;
+    uint32_t vf = SC_TEXT;
+    SView t;
+    switch (type(k)) {
+      case JT_NULL: t = SView{reinterpret_cast<const uint8_t*>("<nil>"), 5}; break;
+      case JT_BOOL:
+        t = btrue(k) ? SView{reinterpret_cast<const uint8_t*>("true"), 4}
+                     : SView{reinterpret_cast<const uint8_t*>("false"), 5};
+        break;
+      case JT_STR:
+        if (k.k == VK_KEY) {
+          if (numeric_looking(k, true)) return -1;
+          t = str(k);
+        } else {
+          const uint8_t* tb;
+          s = scalar(k, &tb);
+          vf = s->flags & (SC_DUR | SC_QTY | SC_QNEG | SC_TEXT);
+          t = SView{tb + s->text_off, (int)s->text_len};
+        }
+        break;
+      case JT_NUM: {
+        if (k.k == VK_NUM) return -1;
+        const uint8_t* tb;
+        s = scalar(k, &tb);
+        // the Sprint text (after the compareString text); its quantity equals the %f one
+        // (SC_SPQ); it is a duration only for 0 ("0")
+        if (!(s->flags & SC_SPQ) || (dur_operand && num(k) == 0.0)) return -1;
+        vf = (s->flags & (SC_QTY | SC_QNEG)) | SC_TEXT;
+        t = SView{tb + s->text_off + s->text_len, (int)s->sp_len};
+        break;
+      }
+      default: return -1;  // fmt.Sprint of a map / list
+    }
+    *sp = s, *vfp = vf, *tp = t;
+    return 0;
+  }
+  __device__ __forceinline__ int range_holds(CV k, uint32_t li) const {
+    const KpeLeaf L = a.leaves[li];
+    const KpeScalar* s = nullptr;
+    uint32_t vf;
+    SView t;
+    if (key_text(k, L.pad[0] != 0u, &s, &vf, &t) < 0) return -1;
+    if (pv_match(a.pats[L.exact], a.pat_bytes, t.s, t.n)) return 1;  // value == pattern
+    bool group = true;
+    const uint32_t c0 = L.c0, ce = c0 + L.nc;
+    for (uint32_t i = c0; i < ce; ++i) {
+      const KpeCond cd = a.pconds[i];
+      if ((cd.op & PC_NEWGROUP) && i != c0) {
+        if (group) return 1;
+        group = true;
+      }
+      bool r = group && rcond(s, vf, t, cd);
+      if (cd.op & PC_OR2) {
+        ++i;
+        r = group && (r || rcond(s, vf, t, a.pconds[i]));
+      }
+      group = group && r;
+    }
+    return group ? 1 : 0;
+  }
+
+  // A resource string value in the InRange form (SC_RANGE: endpoints interned by the flattener).
+  // notin: AnyNotIn's strings.Replace(value, "-", "!-", 1): `a!-b` (NotInRange), or for a value
+  // with a leading `-` the `!` (NotEqual) prefix before the whole value.
+  __device__ __forceinline__ bool bound(uint32_t op, const KpeScalar* ks, uint32_t vf, uint32_t id) const {
+    const KpeScalar e = a.scal[id];
+    if ((e.flags & SC_DUR) && (vf & SC_DUR)) return op_holds(op, ks->dur < e.dur ? -1 : (ks->dur > e.dur ? 1 : 0));
+    if ((e.flags & SC_QTY) && (vf & SC_QTY))
+      return op_holds(op, qcmp(vf & SC_QNEG, ks->qexp, ks->qlo, ks->qhi, e.flags & SC_QNEG, e.qexp, e.qlo, e.qhi));
+    return false;  // compareString: >=, <=, >, < never hold for strings
+  }
+  __device__ __forceinline__ int range_rt(CV k, CV v, bool notin) const {
+    const uint8_t* tb;
+    const KpeScalar* rs = scalar(v, &tb);
+    const SView r = str(v);
+    const uint32_t lo = (uint32_t)(uint64_t)rs->ival, hi = (uint32_t)((uint64_t)rs->ival >> 32);
+    const bool dur = ((a.scal[lo].flags | a.scal[hi].flags) & SC_DUR) != 0u;
+    const KpeScalar* s = nullptr;
+    uint32_t vf;
+    SView t;
+    if (key_text(k, dur, &s, &vf, &t) < 0) return -1;
+    if (!notin) {
+      if (seq(t, r)) return 1;  // value == pattern
+      return bound(PC_GE, s, vf, lo) && bound(PC_LE, s, vf, hi);
+    }
+    int d = 0;
+    while (d < r.n && r.s[d] != '-') ++d;
+    bool eqm = t.n == r.n + 1 && t.s[d] == '!';  // value == the replaced pattern
+    for (int i = 0; eqm && i < d; ++i) eqm = t.s[i] == r.s[i];
+    for (int i = d; eqm && i < r.n; ++i) eqm = t.s[i + 1] == r.s[i];
+    if (eqm) return 1;
+    if (d == 0) return !seq(t, r);  // `!-lo-hi`: NotEqual of `-lo-hi` (no glob characters)
+    return bound(PC_LT, s, vf, lo) || bound(PC_GT, s, vf, hi);
+  }
+
+  // ---- numeric.go / duration.go ---------------------------------------------------------------
+  __device__ __forceinline__ static int cmp_by(uint32_t nop, double x, double y) {  // compareByCondition
+    switch (nop) {
+      case CN_GE: return x >= y;
+      case CN_GT: return x > y;
+      case CN_LE: return x <= y;
+      case CN_LT: return x < y;
+      default: return 0;
+    }
+  }
+  // time.Duration(f) * time.Second: truncation, wrapping multiplication; false when out of range
+  __device__ __forceinline__ static bool f2dur(double f, int64_t* d) {
+    const double tr = trunc(f);
+    if (!(tr >= -9.2e18 && tr <= 9.2e18)) return false;
+    *d = (int64_t)((uint64_t)(int64_t)tr * 1000000000ull);
+    return true;
+  }
+  __device__ __forceinline__ static double dsecs(int64_t d) {
+    return (double)(d / 1000000000) + (double)(d % 1000000000) / 1e9;
+  }
+  // validateValueWithFloatPattern (numeric.go:102-128) of a float64 key
+  __device__ __forceinline__ int num_float(uint32_t nop, double kf, CV v) const {
+    const uint32_t vt = type(v);
+    if (vt == JT_NUM) return cmp_by(nop, kf, num(v));
+    if (vt != JT_STR) return 0;
+    if (v.k == VK_KEY) return numeric_looking(v, true) ? -1 : 0;
+    const uint8_t* t;
+    const KpeScalar* s = scalar(v, &t);
+    int64_t kd;
+    // parseDuration: the value a duration string other than "0", the key seconds
+    if ((s->flags & SC_DUR) && !(s->text_len == 1u && t[s->text_off] == '0') && f2dur(kf, &kd))
+      return cmp_by(nop, dsecs(kd), dsecs(s->dur));
+    if (s->flags & SC_PFLOAT) return cmp_by(nop, kf, s->fval);
+    return 0;
+  }
+  // blang/semver v4 Parse (oracle/conditions.hpp semver_parse): major, minor, patch and the
+  // prerelease text [*p0, *p1); false when not a version
+  __device__ __forceinline__ static bool sv_num(SView s, int b, int e, uint64_t* out) {
+    if (e <= b || (e - b > 1 && s.s[b] == '0')) return false;
+    uint64_t x = 0;
+    for (int i = b; i < e; ++i) {
+      const uint32_t c = s.s[i];
+      if (c < '0' || c > '9') return false;
+      const uint64_t d = c - '0';
+      if (x > (0xFFFFFFFFFFFFFFFFull - d) / 10u) return false;
+      x = x * 10u + d;
+    }
+    *out = x;
+    return true;
+  }
+  __device__ __forceinline__ static bool sv_ident_ok(SView s, int b, int e, bool pre) {
+    if (e <= b) return false;
+    bool digits = true;
+    for (int i = b; i < e; ++i) {
+      const uint32_t c = s.s[i];
+      const bool d = c >= '0' && c <= '9';
+      if (!(d || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '-')) return false;
+      digits = digits && d;
+    }
+    uint64_t x;
+    return !(pre && digits) || sv_num(s, b, e, &x);
+  }
+  __device__ __forceinline__ static bool semver(SView s, uint64_t* mmp, int* p0, int* p1) {
+    int d1 = -1, d2 = -1;
+    for (int i = 0; i < s.n && d2 < 0; ++i)
+      if (s.s[i] == '.') (d1 < 0 ? d1 : d2) = i;
+    if (d2 < 0) return false;
+    if (!sv_num(s, 0, d1, &mmp[0]) || !sv_num(s, d1 + 1, d2, &mmp[1])) return false;
+    int plus = s.n, minus = -1;
+    for (int i = d2 + 1; i < s.n; ++i)
+      if (s.s[i] == '+') {
+        plus = i;
+        break;
+      }
+    for (int i = d2 + 1; i < plus; ++i)
+      if (s.s[i] == '-') {
+        minus = i;
+        break;
+      }
+    if (!sv_num(s, d2 + 1, minus >= 0 ? minus : plus, &mmp[2])) return false;
+    *p0 = minus >= 0 ? minus + 1 : plus, *p1 = plus;
+    if (minus >= 0)  // prerelease identifiers
+      for (int b = minus + 1;;) {
+        int e = b;
+        while (e < plus && s.s[e] != '.') ++e;
+        if (!sv_ident_ok(s, b, e, true)) return false;
+        if (e >= plus) break;
+        b = e + 1;
+      }
+    if (plus < s.n)  // build identifiers
+      for (int b = plus + 1;;) {
+        int e = b;
+        while (e < s.n && s.s[e] != '.') ++e;
+        if (!sv_ident_ok(s, b, e, false)) return false;
+        if (e >= s.n) break;
+        b = e + 1;
+      }
+    return true;
+  }
+  __device__ __forceinline__ static int semver_cmp(SView x, SView y) {  // both valid
+    uint64_t a[3], b[3];
+    int xa, xb, ya, yb;
+    semver(x, a, &xa, &xb);
+    semver(y, b, &ya, &yb);
+    for (int i = 0; i < 3; ++i)
+      if (a[i] != b[i]) return a[i] > b[i] ? 1 : -1;
+    const bool xp = xa < xb, yp = ya < yb;
+    if (!xp && !yp) return 0;
+    if (!xp) return 1;
+    if (!yp) return -1;
+    int i = xa, j = ya;
+    for (;;) {  // identifiers in lockstep
+      int ie = i, je = j;
+      while (ie < xb && x.s[ie] != '.') ++ie;
+      while (je < yb && y.s[je] != '.') ++je;
+      bool xn = true, yn = true;
+      for (int k = i; k < ie; ++k) xn = xn && x.s[k] >= '0' && x.s[k] <= '9';
+      for (int k = j; k < je; ++k) yn = yn && y.s[k] >= '0' && y.s[k] <= '9';
+      int c = 0;
+      if (xn && !yn) c = -1;
+      else if (!xn && yn) c = 1;
+      else if (xn) {  // no leading zeros: longer is larger, else digit order
+        c = (ie - i) != (je - j) ? ((ie - i) > (je - j) ? 1 : -1) : 0;
+        for (int k = 0; c == 0 && k < ie - i; ++k)
+          if (x.s[i + k] != y.s[j + k]) c = x.s[i + k] > y.s[j + k] ? 1 : -1;
+      } else {  // byte order
+        const int n = (ie - i) < (je - j) ? (ie - i) : (je - j);
+        for (int k = 0; c == 0 && k < n; ++k)
+          if (x.s[i + k] != y.s[j + k]) c = x.s[i + k] > y.s[j + k] ? 1 : -1;
+        if (c == 0 && (ie - i) != (je - j)) c = (ie - i) > (je - j) ? 1 : -1;
+      }
+      if (c) return c;
+      const bool xend = ie >= xb, yend = je >= yb;
+      if (xend && yend) return 0;
+      if (xend) return -1;
+      if (yend) return 1;
+      i = ie + 1, j = je + 1;
+    }
+  }
+  // NumericOperatorHandler.Evaluate (numeric.go:62-77, 130-165)
+  __device__ __forceinline__ int op_num(uint32_t nop, CV k, CV v) {
+    const uint32_t kt = type(k);
+    if (kt == JT_NUM) return num_float(nop, num(k), v);
+    if (kt != JT_STR) return 0;
+    if (numeric_looking(k, true) || numeric_looking(v, true)) return -1;  // member names: no parsed attributes
+    double ks, vs;
+    if (duration2(k, v, &ks, &vs) > 0) return cmp_by(nop, ks, vs);
+    if (k.k != VK_KEY) {
+      const uint8_t* tk;
+      const KpeScalar* sk = scalar(k, &tk);
+      if ((sk->flags & SC_QTY) && type(v) == JT_STR && v.k != VK_KEY) {
+        const uint8_t* tv;
+        const KpeScalar* sv = scalar(v, &tv);
+        if (sv->flags & SC_QTY)
+          return cmp_by(nop, (double)qcmp(sk->flags & SC_QNEG, sk->qexp, sk->qlo, sk->qhi, sv->flags & SC_QNEG, sv->qexp,
+                                          sv->qlo, sv->qhi), 0.0);
+      }
+      if (sk->flags & SC_PFLOAT) return num_float(nop, sk->fval, v);
+    }
+    uint64_t m[3];
+    int p0, p1;
+    const SView ksv = str(k);
+    if (!semver(ksv, m, &p0, &p1)) return 0;
+    if (type(v) != JT_STR) return 0;
+    const SView vsv = str(v);
+    if (!semver(vsv, m, &p0, &p1)) return 0;
+    return cmp_by(nop, (double)semver_cmp(ksv, vsv), 0.0);
+  }
+  // DurationOperatorHandler.Evaluate (duration.go:42-120): int64 durations
+  __device__ __forceinline__ int dur_of(CV x, int64_t* d) const {  // 1 ok, 0 not a duration, -1 undecided
+    const uint32_t t = type(x);
+    if (t == JT_NUM) return f2dur(num(x), d) ? 1 : 0;
+    if (t != JT_STR) return 0;
+    if (x.k == VK_KEY) return numeric_looking(x, false) ? -1 : 0;
+    const uint8_t* tb;
+    const KpeScalar* s = scalar(x, &tb);
+    if (!(s->flags & SC_DUR)) return 0;
+    *d = s->dur;
+    return 1;
+  }
+  __device__ __forceinline__ int op_dur(uint32_t nop, CV k, CV v) {
+    int64_t kd = 0, vd = 0;
+    const int a1 = dur_of(k, &kd);
+    if (a1 <= 0) return a1;
+    const int a2 = dur_of(v, &vd);
+    if (a2 <= 0) return a2;
+    switch (nop) {
+      case CN_GE: return kd >= vd;
+      case CN_GT: return kd > vd;
+      case CN_LE: return kd <= vd;
+      case CN_LT: return kd < vd;
+      default: return 0;
+    }
+  }
+
   // ---- conditions ---------------------------------------------------------------------------
   __device__ __forceinline__ int condition(uint32_t ci, CV el, uint32_t eli) {
     const KpeCCond c = a.conds[ci];
@@ -654,8 +1004,11 @@ struct CondVM {
     const CV k = kv[0], v = kv[1];
     int r;
     if (c.op <= CO_NE) r = op_equals(k, v, c.op == CO_NE);
+    else if (c.op == CO_NUM) r = op_num(c.aux, k, v);
+    else if (c.op == CO_DUR) r = op_dur(c.aux, k, v);
+    else if (c.op == CO_BAD) r = -2;  // no operator handler: an error once key and value substituted
     else if (c.op >= CO_IN) r = op_in(k, v, c.op == CO_NOTIN);
-    else r = op_set(c.op, k, v);
+    else r = op_set(c.op, k, v, c.aux);
     if (r == -2) return CB_ERROR;
     if (r < 0) return CB_UNDEC;
     return r ? CB_TRUE : CB_FALSE;
@@ -694,6 +1047,10 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
     const KpeCRule cr = a.rules[i];
     const uint8_t cell = row[cr.col];
     if (cell == KPE_NA_) continue;  // the rule did not match
+    // a PolicyException already made the cell RuleSkip (validate_resource.go:44-56 returns before
+    // the deny / foreach is evaluated); exceptions compile only on rules without resource-reading
+    // preconditions, so every excepted cell is one with cr.pre == CE_NONE
+    if (cr.pre == CE_NONE && cell != KPE_PENDING_) continue;
     uint32_t v = cell;
     uint32_t ph = cr.pre != CE_NONE ? PH_PRE : PH_HANDLER;
     // foreach state (validateForEach / validateElements, validate_resource.go:186-254)

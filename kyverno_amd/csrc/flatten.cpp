@@ -1160,6 +1160,10 @@ void scalar_attrs(KpeScalar& e, std::string_view numstr) {
   }
 }
 
+void spq(KpeScalar& e, const std::string& sprint) {
+  if (goval::sprint_qty_same(sprint, e.flags & SC_QTY, e.flags & SC_QNEG, e.qexp, e.qlo, e.qhi)) e.flags |= SC_SPQ;
+}
+
 class DocBuilder {
  public:
   explicit DocBuilder(Corpus& c) : C(c) {
@@ -1217,6 +1221,7 @@ class DocBuilder {
     const std::string sp = goval::sprint_float((double)v);  // condition context numbers are float64
     text(sp), e.sp_len = (uint32_t)sp.size();
     scalar_attrs(e, t);
+    spq(e, sp);
     return C.scal_int[v] = push_scalar(e);
   }
   uint32_t float_id(double v) {
@@ -1232,6 +1237,7 @@ class DocBuilder {
     const std::string sp = goval::sprint_float(v);
     text(sp), e.sp_len = (uint32_t)sp.size();
     scalar_attrs(e, goval::fmt_f(v));
+    spq(e, sp);
     return C.scal_float[bits] = push_scalar(e);
   }
   uint32_t str_id(std::string_view v) {
@@ -1246,7 +1252,35 @@ class DocBuilder {
     if (goval::parse_int(v, &i)) e.flags |= SC_PINT, e.ival = i;
     if (goval::parse_float(v, &f)) e.flags |= SC_PFLOAT, e.fval = f;
     scalar_attrs(e, v);
+    json_attrs(e, v);
+    if (e.flags & SC_RANGE) {  // endpoints of the InRange form: their duration / quantity parses
+      size_t at = 0;
+      goval::range_split(v, "-", &at);
+      if (v.find('|') != std::string_view::npos) {
+        e.flags = (e.flags & ~SC_RANGE) | SC_RANGEU;  // validateStringPatterns splits on `|` first
+      } else {
+        const uint32_t lo = str_id(v.substr(0, at)), hi = str_id(v.substr(at + 1));
+        e.ival = (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
+      }
+    }
     return C.scal_str[k] = push_scalar(e);
+  }
+  // What the condition set operators read from a string value (anyin.go:73-93): json.Valid
+  // (and whether it is an array) and the InRange form
+  static void json_attrs(KpeScalar& e, std::string_view v) {
+    if (goval::in_range_form(v)) e.flags |= SC_RANGE;
+    size_t i = 0;
+    while (i < v.size() && (v[i] == ' ' || v[i] == '\t' || v[i] == '\n' || v[i] == '\r')) ++i;
+    if (i == v.size()) return;
+    const char c = v[i];
+    if (!(c == '[' || c == '{' || c == '"' || c == '-' || (c >= '0' && c <= '9') || c == 't' || c == 'f' || c == 'n'))
+      return;  // no JSON value starts here
+    JCur jc(v.data(), v.data() + v.size());
+    jc.ws();
+    if (!jc.skip()) return;
+    jc.ws();
+    if (!jc.ok() || jc.pos() != v.data() + v.size()) return;
+    e.flags |= SC_JVALID | (c == '[' ? SC_JARR : 0u);
   }
   static uint64_t entry(uint32_t kind, uint32_t key1, uint32_t y) {
     return (uint64_t)(kind | (key1 << 2)) | ((uint64_t)y << 32);
@@ -1458,6 +1492,10 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
         }
         if (*slot == 0xFFFFFFFFu) {
           KpeScalar g = e;
+          if ((g.flags & SC_RANGE) && SC_TYPE(g.flags) == SC_T_STR) {  // endpoint ids (lower indices: mapped)
+            const uint64_t x = (uint64_t)e.ival;
+            g.ival = (int64_t)((uint64_t)sm[(uint32_t)x] | ((uint64_t)sm[(uint32_t)(x >> 32)] << 32));
+          }
           const size_t nb = (size_t)e.text_len + e.sp_len;
           if (C.scal_text.size() + nb > 0xFFFFFFFFull) throw LimitError("scalar text pool exceeds 4 GiB");
           g.text_off = (uint32_t)C.scal_text.size();

@@ -417,5 +417,51 @@ inline std::string sprint_float(double v) {
   return sign + d.substr(0, dp) + "." + d.substr(dp);
 }
 
+// operator.GetOperatorFromStringPattern(s) == InRange (pkg/engine/operator/operator.go:36-61):
+// no >= <= > < ! prefix, not the NotInRange form, and
+// ^([-|+]?\d+(\.\d+)?[A-Za-z]*)-([-|+]?\d+(\.\d+)?[A-Za-z]*)$
+inline bool range_endpoint(std::string_view x) {
+  size_t i = 0;
+  auto dg = [&](size_t j) { return j < x.size() && x[j] >= '0' && x[j] <= '9'; };
+  if (i < x.size() && (x[i] == '-' || x[i] == '|' || x[i] == '+')) ++i;
+  if (!dg(i)) return false;
+  while (dg(i)) ++i;
+  if (i < x.size() && x[i] == '.') {
+    if (!dg(i + 1)) return false;
+    ++i;
+    while (dg(i)) ++i;
+  }
+  while (i < x.size() && ((x[i] >= 'a' && x[i] <= 'z') || (x[i] >= 'A' && x[i] <= 'Z'))) ++i;
+  return i == x.size();
+}
+inline bool range_split(std::string_view t, std::string_view sep, size_t* at = nullptr) {
+  for (size_t k = 1; k + sep.size() <= t.size(); ++k)
+    if (t.substr(k, sep.size()) == sep && range_endpoint(t.substr(0, k)) && range_endpoint(t.substr(k + sep.size()))) {
+      if (at) *at = k;
+      return true;
+    }
+  return false;
+}
+inline bool in_range_form(std::string_view s) {
+  if (s.size() < 2) return false;
+  if (s[0] == '>' || s[0] == '<' || s[0] == '!') return false;
+  if (range_split(s, "!-")) return false;
+  return range_split(s, "-");
+}
+
+// schema.h SC_SPQ: ParseQuantity of fmt.Sprint(v) (the text the condition set operators hand
+// to an InRange check) agrees with the quantity attributes computed from another text of v
+inline bool sprint_qty_same(const std::string& sp, bool has_qty, bool neg, int64_t qexp, uint64_t qlo, uint64_t qhi) {
+  Quantity q;
+  const bool ok = parse_quantity(sp, &q);
+  if (ok != has_qty) return false;
+  if (!ok) return true;
+  int64_t o;
+  uint64_t lo, hi;
+  qty_key(q, &o, &lo, &hi);
+  if ((lo | hi) == 0 && (qlo | qhi) == 0) return true;
+  return o == qexp && lo == qlo && hi == qhi && q.neg == neg;
+}
+
 }  // namespace goval
 }  // namespace kpe

@@ -88,6 +88,23 @@ class JCur {
       ++p_;
     }
     if (p_ == d0) return fail();
+    {  // encoding/json's number grammar: -?(0|[1-9][0-9]*)(\.[0-9]+)?([eE][+-]?[0-9]+)?
+      const char* q = d0;
+      auto digits = [&]() {
+        const char* k = q;
+        while (q < p_ && *q >= '0' && *q <= '9') ++q;
+        return (size_t)(q - k);
+      };
+      const size_t nd = digits();
+      bool ok = nd > 0 && !(nd > 1 && *d0 == '0');
+      if (ok && q < p_ && *q == '.') ++q, ok = digits() > 0;
+      if (ok && q < p_ && (*q == 'e' || *q == 'E')) {
+        ++q;
+        if (q < p_ && (*q == '+' || *q == '-')) ++q;
+        ok = digits() > 0;
+      }
+      if (!ok || q != p_) return fail();
+    }
     char buf[64];
     size_t len = (size_t)(p_ - s);
     if (len >= sizeof buf) {

@@ -214,6 +214,10 @@ struct CondArgs {
   const uint8_t* ctext;
   const uint32_t* clist;
   const uint32_t* fkeys;           // field index -> D_KEY id + 1 (0: absent from the corpus)
+  const KpeLeaf* leaves;           // InRange values of set operators (KpeCCond::aux): string-pattern
+  const KpeCond* pconds;           // leaves of the pattern program's tables
+  const KpePat* pats;
+  const uint8_t* pat_bytes;
   uint8_t* verdicts;
 };
 

@@ -1134,6 +1134,10 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.ctext = PD.ctext.as<uint8_t>();
       ca.clist = PD.cclist.as<uint32_t>();
       ca.fkeys = B.cfkeys.as<uint32_t>();
+      ca.leaves = PD.pleaves.as<KpeLeaf>();
+      ca.pconds = PD.pconds.as<KpeCond>();
+      ca.pats = PD.ppats.as<KpePat>();
+      ca.pat_bytes = PD.pbytes.as<uint8_t>();
       ca.verdicts = B.verdicts.as<uint8_t>();
       HIPCHK(B.cargs.ensure(sizeof(CondArgs)));
       HIPCHK(hipMemcpyAsync(B.cargs.p, &ca, sizeof(CondArgs), hipMemcpyHostToDevice, s));

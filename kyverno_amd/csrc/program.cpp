@@ -704,6 +704,9 @@ class PatCompiler {
     }
     PP.conds.push_back(c);
   }
+  // A scalar pattern leaf (pattern.Validate's pattern side). Also the InRange values of the
+  // condition set operators (anyin.go:103-109 handleRange: pattern.Validate(key, value)).
+ public:
   uint32_t leaf(const JV& v) {
     KpeLeaf l{};
     switch (v.t) {
@@ -756,6 +759,8 @@ class PatCompiler {
           }
         }
         l.nc = (uint32_t)PP.conds.size() - l.c0;
+        for (uint32_t i = l.c0; i < l.c0 + l.nc; ++i)
+          if (PP.conds[i].op & PC_DUR) l.pad[0] = 1u;  // some operand is a duration
         break;
       }
       default: l.type = PL_NEVER; break;
@@ -763,6 +768,7 @@ class PatCompiler {
     PP.leaves.push_back(l);
     return (uint32_t)PP.leaves.size() - 1;
   }
+ private:
 
   uint32_t node(const JV& v, int depth, bool repeated) {
     if (depth > kMaxDepth) throw CompileError("pattern nested deeper than 12 levels");
@@ -1152,6 +1158,8 @@ class Consts {
         const std::string sp = goval::sprint_float(f);
         CP.ctext.insert(CP.ctext.end(), sp.begin(), sp.end());
         e.sp_len = (uint32_t)sp.size();
+        attrs(e, goval::fmt_f(f));  // as the flattener's float scalars (convertNumberToString)
+        if (goval::sprint_qty_same(sp, e.flags & SC_QTY, e.flags & SC_QNEG, e.qexp, e.qlo, e.qhi)) e.flags |= SC_SPQ;
         break;
       }
       case JV::Str: {
@@ -1161,13 +1169,7 @@ class Consts {
         double f;
         if (goval::parse_int(v.s, &i)) e.flags |= SC_PINT, e.ival = i;
         if (goval::parse_float(v.s, &f)) e.flags |= SC_PFLOAT, e.fval = f;
-        int64_t d;
-        if (goval::parse_duration(v.s, &d)) e.flags |= SC_DUR, e.dur = d;
-        goval::Quantity q;
-        if (goval::parse_quantity(v.s, &q)) {
-          e.flags |= SC_QTY | (q.neg ? SC_QNEG : 0u);
-          goval::qty_key(q, &e.qexp, &e.qlo, &e.qhi);
-        }
+        attrs(e, v.s);
         json_list(e, v.s);
         break;
       }
@@ -1200,6 +1202,15 @@ class Consts {
 
  private:
   CondProgram& CP;
+  static void attrs(KpeScalar& e, const std::string& s) {  // ParseDuration / ParseQuantity of a text form
+    int64_t d;
+    if (goval::parse_duration(s, &d)) e.flags |= SC_DUR, e.dur = d;
+    goval::Quantity q;
+    if (goval::parse_quantity(s, &q)) {
+      e.flags |= SC_QTY | (q.neg ? SC_QNEG : 0u);
+      goval::qty_key(q, &e.qexp, &e.qlo, &e.qhi);
+    }
+  }
   void text(KpeScalar& e, const std::string& s) {
     e.text_off = (uint32_t)CP.ctext.size();
     e.text_len = (uint32_t)s.size();
@@ -1441,6 +1452,7 @@ bool next_var(const std::string& s, size_t from, size_t* st, size_t* en) {
 class CondCompiler {
  public:
   explicit CondCompiler(CondProgram& cp) : CP(cp), K(cp), Q(cp, K) {}
+  std::function<uint32_t(const std::string&)> range_leaf;  // string-pattern leaf of the pattern program
 
   // a condition key / value after substitution
   uint32_t tmpl(const JV& v, int depth = 0) {
@@ -1478,9 +1490,13 @@ class CondCompiler {
   }
   uint32_t condition(const JV& c) {
     if (c.t != JV::Obj) throw CompileError("condition is not an object");
+    // CreateOperatorHandler (operator.go:27-67) dispatches on the lower-cased name; the numeric
+    // and duration handlers then compare the name as written with the canonical spelling
+    // (numeric.go:32-45, duration.go:27-40), so another spelling always gives false
+    const std::string opw = sv(c.get("operator"));
     std::string op;
-    for (char ch : sv(c.get("operator"))) op += (char)tolower((unsigned char)ch);
-    uint32_t o;
+    for (char ch : opw) op += (char)tolower((unsigned char)ch);
+    uint32_t o = CO_BAD, aux = 0;
     if (op == "equal" || op == "equals") o = CO_EQ;
     else if (op == "notequal" || op == "notequals") o = CO_NE;
     else if (op == "anyin") o = CO_ANYIN;
@@ -1489,16 +1505,35 @@ class CondCompiler {
     else if (op == "allnotin") o = CO_ALLNOTIN;
     else if (op == "in") o = CO_IN;
     else if (op == "notin") o = CO_NOTIN;
-    else throw CompileError("condition operator '" + sv(c.get("operator")) + "' is not supported on the device");
+    static const char* const kNum[4] = {"GreaterThanOrEquals", "GreaterThan", "LessThanOrEquals", "LessThan"};
+    for (uint32_t d = 0; d < 2 && o == CO_BAD; ++d)
+      for (uint32_t i = 0; i < 4; ++i) {
+        const std::string canon = std::string(d ? "Duration" : "") + kNum[i];
+        std::string lc;
+        for (char ch : canon) lc += (char)tolower((unsigned char)ch);
+        if (op == lc) {
+          o = d ? CO_DUR : CO_NUM;
+          aux = opw == canon ? i : CN_NONE;
+          break;
+        }
+      }
     static const JV null_v;
     const JV* k = c.get("key");
     const JV* v = c.get("value");
     const JV& vv = v ? *v : null_v;
     if (vv.t == JV::Str && o >= CO_ANYIN && o <= CO_ALLNOTIN) {
       size_t st, en;
-      if (!next_var(vv.s, 0, &st, &en) && in_range(vv.s)) throw CompileError("InRange values of set operators");
+      if (!next_var(vv.s, 0, &st, &en) && in_range(vv.s)) {
+        // an InRange constant value (GetOperatorFromStringPattern): handleRange compares each key
+        // as pattern.Validate(key, value); AnyNotIn uses the value with its first `-` as `!-`
+        if (!range_leaf) throw CompileError("InRange values of set operators");
+        aux = 1u + range_leaf(vv.s);
+        std::string nr = vv.s;
+        nr.replace(nr.find('-'), 1, "!-");
+        range_leaf(nr);  // the next leaf
+      }
     }
-    KpeCCond cc{o, tmpl(k ? *k : null_v), tmpl(vv), 0};
+    KpeCCond cc{o, tmpl(k ? *k : null_v), tmpl(vv), aux};
     CP.conds.push_back(cc);
     return (uint32_t)CP.conds.size() - 1;
   }
@@ -1561,7 +1596,12 @@ class CondCompiler {
 
 class Lowerer {
  public:
-  explicit Lowerer(Program& p) : P(p), CC(p.cond) {}
+  explicit Lowerer(Program& p) : P(p), CC(p.cond) {
+    CC.range_leaf = [this](const std::string& text) {
+      pc::PatCompiler pcomp(P.pat, [](const std::string&) { return (int32_t)-1; });
+      return pcomp.leaf(JV::str(text));
+    };
+  }
 
   static void to_float(JV& v) {
     if (v.t == JV::Num && v.is_int) v.is_int = false, v.n = (double)v.i;

@@ -465,6 +465,13 @@ typedef struct KpeXRule {
 #define SC_JVALID (1u << 10)  // condition constant string: json.Valid
 #define SC_JLIST (1u << 11)   // ... and decodes as a []string (or null): elements = constant list
                               // [ival & 0xFFFFFFFF, + ival >> 32) of the constant-list table
+#define SC_JARR (1u << 13)     // corpus string: json.Valid and a JSON array (a []string decode the
+                              // device leaves undecided); SC_JVALID alone: valid JSON, not an array
+#define SC_RANGE (1u << 14)    // corpus string: GetOperatorFromStringPattern == InRange, its two
+                              // endpoints interned as scalars: ival = lo id | hi id << 32
+#define SC_RANGEU (1u << 15)   // corpus string: the InRange form with a `|` in it (undecided)
+#define SC_SPQ (1u << 12)     // number: the quantity of its fmt.Sprint text (%v) equals the quantity
+                              // of convertNumberToString (%f), so SC_QTY also stands for Sprint
 #define SC_T_ARR 5          // condition constants only: text_off = first element (constant list), text_len = count
 typedef struct KpeScalar {
   uint32_t flags, text_off, text_len;
@@ -586,8 +593,19 @@ typedef struct KpeVTmpl {
 #define CO_ALLNOTIN 5u
 #define CO_IN 6u
 #define CO_NOTIN 7u
+#define CO_NUM 8u   // numeric.go GreaterThan* / LessThan*: aux = CN_* (compareByCondition's operator)
+#define CO_DUR 9u   // duration.go Duration*: aux = CN_*
+#define CO_BAD 10u  // no operator handler: an evaluation error after the key / value substitution
+#define CN_GE 0u
+#define CN_GT 1u
+#define CN_LE 2u
+#define CN_LT 3u
+#define CN_NONE 4u  // a non-canonical spelling: compareByCondition's default (false)
 typedef struct KpeCCond {
-  uint32_t op, key, value, pad;  // key / value: template indices
+  uint32_t op, key, value;  // key / value: template indices
+  uint32_t aux;  // CO_NUM / CO_DUR: CN_*; set operators: 1 + leaf index of an InRange constant value
+                 // (validateStringPatterns of the value, pattern program leaf table; the NotInRange
+                 // form `a!-b` AnyNotIn uses is the next leaf), 0 = none
 } KpeCCond;
 // Condition block: AnyAllConditions (any = conds [c0, c0 + nany), all = the next nall), or the
 // deprecated list form (nany = 0, all = the list)

@@ -369,4 +369,26 @@ int oracle_match_pattern(const char* resource_json, const char* pattern_json, in
   }
 }
 
+// variables.Evaluate of one condition with constant key / value (JSON texts, decoded as the
+// context does: numbers float64) and the operator as written: 1 true, 0 false, -1 evaluation
+// error, -2 outside the restatement
+int oracle_condition(const char* key_json, const char* op, const char* value_json) {
+  try {
+    auto c = std::make_shared<JVal>();
+    c->t = JT::Obj;
+    c->o.push_back({"key", parse_json(key_json)});
+    c->o.push_back({"operator", cond::mk_str(op)});
+    c->o.push_back({"value", parse_json(value_json)});
+    cond::Condition cc = cond::parse_condition(*c);
+    cond::Ctx cx{cond::request_context(JVal())};
+    return cond::eval_condition(cc, cx) ? 1 : 0;
+  } catch (const cond::EvalError& e) {
+    g_err = e.msg;
+    return -1;
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -2;
+  }
+}
+
 }  // extern "C"

@@ -1026,8 +1026,16 @@ inline bool op_set(SetOp op, const JPtr& key, const JPtr& value) {
     for (auto& e : value->a) vals.push_back(go_sprint(e));
   } else if (value->t == JT::Str) {
     const std::string& vs = value->s;
+    // anyin.go:103-109 handleRange: pattern.Validate(key string, value) of an InRange value
+    auto in_range = [&](const std::string& k, const std::string& pat) {
+      JVal kv;
+      kv.t = JT::Str, kv.s = k;
+      return pat::validate_string_patterns(&kv, pat);
+    };
+    const bool range = pat::get_operator(vs) == pat::OP_IN_RANGE;
     if (single) {  // anyKeyExistsInArray / allKeyExistsInArray
       if (wmatch(vs, keys[0])) return !notin;
+      if (range) return in_range(keys[0], vs) != notin;
       std::vector<std::string> arr;
       bool invalid;
       if (!json_string_array(vs, &arr, &invalid)) arr = {vs};
@@ -1038,6 +1046,15 @@ inline bool op_set(SetOp op, const JPtr& key, const JPtr& value) {
       return ex != notin;
     }
     if (keys.size() == 1 && keys[0] == vs) return !notin;
+    if (range) {  // anySetExistsInArray / allSetExistsInArray (anyin.go:146-165, allin.go:133-155)
+      std::string nr = vs;
+      nr.replace(nr.find('-'), 1, "!-");  // strings.Replace(value, "-", "!-", 1) for AnyNotIn
+      int hits = 0;
+      for (auto& k : keys) hits += in_range(k, op == S_ANYNOTIN ? nr : vs) ? 1 : 0;
+      if (op == S_ANYIN || op == S_ANYNOTIN) return hits > 0;
+      if (op == S_ALLIN) return hits == (int)keys.size();
+      return hits == 0;
+    }
     bool invalid;
     if (!json_string_array(vs, &vals, &invalid)) vals = {vs};
     else if (invalid) return false;
@@ -1071,8 +1088,176 @@ inline bool op_set(SetOp op, const JPtr& key, const JPtr& value) {
   }
 }
 
-enum OpKind { O_EQ, O_NE, O_ANYIN, O_ALLIN, O_ANYNOTIN, O_ALLNOTIN, O_IN, O_NOTIN };
-inline OpKind parse_op(const std::string& o) {
+// ---- numeric.go / duration.go (the GreaterThan* / LessThan* / Duration* operators) -------
+// github.com/blang/semver/v4 v4.0.0 (go.mod; third-party, absent here) Parse and Compare, as
+// numeric.go:158-163 uses them for string keys that are neither durations, quantities nor
+// numbers. Restated from the published package: Major.Minor.Patch (decimal, no leading zero,
+// ParseUint range), `-` prerelease identifiers (numeric without leading zero, or [0-9A-Za-z-]),
+// `+` build identifiers (non-empty [0-9A-Za-z-]); build metadata never takes part in Compare.
+struct SemVer {
+  uint64_t mmp[3];
+  std::vector<std::pair<bool, std::string>> pre;  // (is numeric, text); numeric texts compare by value
+  std::vector<uint64_t> pre_num;
+};
+inline bool semver_uint(const std::string& s, uint64_t* out) {
+  if (s.empty()) return false;
+  for (char c : s)
+    if (c < '0' || c > '9') return false;
+  if (s.size() > 1 && s[0] == '0') return false;  // hasLeadingZeroes
+  uint64_t x = 0;
+  for (char c : s) {
+    const uint64_t d = (uint64_t)(c - '0');
+    if (x > (UINT64_MAX - d) / 10u) return false;  // strconv.ParseUint range error
+    x = x * 10u + d;
+  }
+  *out = x;
+  return true;
+}
+inline bool semver_alnum(const std::string& s) {
+  for (char c : s)
+    if (!((c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '-')) return false;
+  return true;
+}
+inline std::vector<std::string> split_all(const std::string& s, char sep) {
+  std::vector<std::string> out;
+  size_t a = 0;
+  for (;;) {
+    size_t b = s.find(sep, a);
+    out.push_back(s.substr(a, b == std::string::npos ? std::string::npos : b - a));
+    if (b == std::string::npos) return out;
+    a = b + 1;
+  }
+}
+inline bool semver_parse(const std::string& s, SemVer* v) {
+  if (s.empty()) return false;
+  const size_t d1 = s.find('.');
+  if (d1 == std::string::npos) return false;
+  const size_t d2 = s.find('.', d1 + 1);
+  if (d2 == std::string::npos) return false;  // SplitN(s, ".", 3) needs three parts
+  if (!semver_uint(s.substr(0, d1), &v->mmp[0]) || !semver_uint(s.substr(d1 + 1, d2 - d1 - 1), &v->mmp[1]))
+    return false;
+  std::string patch = s.substr(d2 + 1);
+  std::vector<std::string> build, pre;
+  const size_t bi = patch.find('+');
+  if (bi != std::string::npos) {
+    build = split_all(patch.substr(bi + 1), '.');
+    patch = patch.substr(0, bi);
+  }
+  const size_t pi = patch.find('-');
+  if (pi != std::string::npos) {
+    pre = split_all(patch.substr(pi + 1), '.');
+    patch = patch.substr(0, pi);
+  }
+  if (!semver_uint(patch, &v->mmp[2])) return false;
+  v->pre.clear(), v->pre_num.clear();
+  for (auto& p : pre) {  // NewPRVersion
+    if (p.empty()) return false;
+    bool digits = true;
+    for (char c : p) digits = digits && c >= '0' && c <= '9';
+    uint64_t n = 0;
+    if (digits) {
+      if (!semver_uint(p, &n)) return false;
+    } else if (!semver_alnum(p)) {
+      return false;
+    }
+    v->pre.push_back({digits, p});
+    v->pre_num.push_back(n);
+  }
+  for (auto& b : build)
+    if (b.empty() || !semver_alnum(b)) return false;
+  return true;
+}
+inline int semver_cmp(const SemVer& a, const SemVer& b) {
+  for (int i = 0; i < 3; ++i)
+    if (a.mmp[i] != b.mmp[i]) return a.mmp[i] > b.mmp[i] ? 1 : -1;
+  if (a.pre.empty() && b.pre.empty()) return 0;
+  if (a.pre.empty()) return 1;
+  if (b.pre.empty()) return -1;
+  size_t i = 0;
+  for (; i < a.pre.size() && i < b.pre.size(); ++i) {
+    const bool an = a.pre[i].first, bn = b.pre[i].first;
+    int c;
+    if (an && !bn) c = -1;
+    else if (!an && bn) c = 1;
+    else if (an) c = a.pre_num[i] == b.pre_num[i] ? 0 : (a.pre_num[i] > b.pre_num[i] ? 1 : -1);
+    else c = a.pre[i].second == b.pre[i].second ? 0 : (a.pre[i].second > b.pre[i].second ? 1 : -1);
+    if (c) return c;
+  }
+  if (i == a.pre.size() && i == b.pre.size()) return 0;
+  return i == a.pre.size() ? -1 : 1;
+}
+// compareByCondition (numeric.go:32-45) over a three-way result or two floats: `op` is the
+// operator as written; only the canonical spelling matches (a differently-cased one reaches the
+// handler through CreateOperatorHandler's lower-casing but falls to compareByCondition's default)
+enum NumOp { N_GE, N_GT, N_LE, N_LT, N_NONE };
+inline bool cmp_by(NumOp op, double k, double v) {
+  switch (op) {
+    case N_GE: return k >= v;
+    case N_GT: return k > v;
+    case N_LE: return k <= v;
+    case N_LT: return k < v;
+    default: return false;
+  }
+}
+inline bool op_numeric_float(NumOp op, double key, const JPtr& value) {  // validateValueWithFloatPattern
+  if (is_null(value)) return false;
+  if (value->t == JT::Float) return cmp_by(op, key, value->f);
+  if (value->t != JT::Str) return false;
+  double kd, vd;
+  if (parse_duration2(mk_num(key), value, &kd, &vd)) return cmp_by(op, kd, vd);
+  double f;
+  if (pat::go_parse_float(value->s, &f)) return cmp_by(op, key, f);
+  return false;  // strconv.ParseInt cannot succeed where ParseFloat failed
+}
+inline bool op_numeric(NumOp op, const JPtr& key, const JPtr& value) {  // NumericOperatorHandler.Evaluate
+  if (is_null(key)) return false;
+  if (key->t == JT::Float) return op_numeric_float(op, key->f, value);
+  if (key->t != JT::Str) return false;
+  double kd, vd;  // validateValueWithStringPattern: duration, quantity, float, int, semver
+  if (parse_duration2(key, value, &kd, &vd)) return cmp_by(op, kd, vd);
+  pat::Qty kq, vq;
+  if (pat::go_parse_quantity(key->s, &kq) && !is_null(value) && value->t == JT::Str &&
+      pat::go_parse_quantity(value->s, &vq))
+    return cmp_by(op, (double)pat::qty_cmp(kq, vq), 0.0);
+  double f;
+  if (pat::go_parse_float(key->s, &f)) return op_numeric_float(op, f, value);
+  SemVer ks, vs;
+  if (semver_parse(key->s, &ks)) {
+    if (is_null(value) || value->t != JT::Str || !semver_parse(value->s, &vs)) return false;
+    return cmp_by(op, (double)semver_cmp(ks, vs), 0.0);
+  }
+  return false;
+}
+// duration.go: time.Duration(number) * time.Second (float64 -> int64 truncation, wrapping
+// multiplication) or time.ParseDuration of a string; int64 compares
+inline bool dur_of(const JPtr& x, bool strings, int64_t* d) {
+  if (is_null(x)) return false;
+  if (x->t == JT::Float) {
+    const double t = std::trunc(x->f);
+    if (!(t >= -9.2e18 && t <= 9.2e18)) return false;  // Go conversion out of range: undefined
+    *d = (int64_t)((uint64_t)(int64_t)t * 1000000000ull);
+    return true;
+  }
+  return strings && x->t == JT::Str && pat::go_parse_duration(x->s, d);
+}
+inline bool op_duration(NumOp op, const JPtr& key, const JPtr& value) {  // DurationOperatorHandler
+  int64_t kd, vd;
+  if (is_null(key) || (key->t != JT::Float && key->t != JT::Str)) return false;
+  if (!dur_of(key, true, &kd)) return false;  // a string key that is no duration: false
+  if (!dur_of(value, true, &vd)) return false;
+  switch (op) {
+    case N_GE: return kd >= vd;
+    case N_GT: return kd > vd;
+    case N_LE: return kd <= vd;
+    case N_LT: return kd < vd;
+    default: return false;
+  }
+}
+
+enum OpKind { O_EQ, O_NE, O_ANYIN, O_ALLIN, O_ANYNOTIN, O_ALLNOTIN, O_IN, O_NOTIN, O_NUM, O_DUR, O_BAD };
+// CreateOperatorHandler (operator.go:27-67): dispatch on the lower-cased name; *num receives the
+// compareByCondition operator (N_NONE when the spelling is not the canonical one)
+inline OpKind parse_op(const std::string& o, NumOp* num = nullptr) {
   std::string l;
   for (char c : o) l += (char)tolower((unsigned char)c);
   if (l == "equal" || l == "equals") return O_EQ;
@@ -1083,7 +1268,18 @@ inline OpKind parse_op(const std::string& o) {
   if (l == "allnotin") return O_ALLNOTIN;
   if (l == "in") return O_IN;
   if (l == "notin") return O_NOTIN;
-  throw Unsupported("condition operator " + o);
+  static const char* const nums[4] = {"GreaterThanOrEquals", "GreaterThan", "LessThanOrEquals", "LessThan"};
+  for (int d = 0; d < 2; ++d)
+    for (int i = 0; i < 4; ++i) {
+      const std::string canon = std::string(d ? "Duration" : "") + nums[i];
+      std::string lc;
+      for (char c : canon) lc += (char)tolower((unsigned char)c);
+      if (l == lc) {
+        if (num) *num = o == canon ? (NumOp)i : N_NONE;
+        return d ? O_DUR : O_NUM;
+      }
+    }
+  return O_BAD;  // no handler: "failed to create handler for condition operator" (evaluate.go:23-25)
 }
 // in.go / notin.go (deprecated): key in value list / string
 inline bool op_in(const JPtr& key, const JPtr& value, bool notin) {
@@ -1157,8 +1353,11 @@ inline bool op_in(const JPtr& key, const JPtr& value, bool notin) {
     default: return false;
   }
 }
-inline bool apply_op(OpKind o, const JPtr& key, const JPtr& value) {
+inline bool apply_op(OpKind o, const JPtr& key, const JPtr& value, NumOp num = N_NONE) {
   switch (o) {
+    case O_NUM: return op_numeric(num, key, value);
+    case O_DUR: return op_duration(num, key, value);
+    case O_BAD: throw EvalError{"failed to create handler for condition operator"};
     case O_EQ: return op_equals(key, value, false);
     case O_NE: return op_equals(key, value, true);
     case O_ANYIN: return op_set(S_ANYIN, key, value);
@@ -1174,6 +1373,7 @@ inline bool apply_op(OpKind o, const JPtr& key, const JPtr& value) {
 struct Condition {
   JPtr key, value;
   OpKind op;
+  NumOp num = N_NONE;
 };
 struct AnyAll {
   bool has_any = false;
@@ -1192,16 +1392,12 @@ inline Condition parse_condition(const JVal& c) {
   o.key = k ? to_ctx(*k) : nullptr;
   o.value = v ? to_ctx(*v) : nullptr;
   const JVal* op = c.get("operator");
-  o.op = parse_op(op && op->t == JT::Str ? op->s : "");
+  o.op = parse_op(op && op->t == JT::Str ? op->s : "", &o.num);
   auto check = [](const JPtr& x) {
     if (x && x->t == JT::Str && x->s.find("$(") != std::string::npos) throw Unsupported("$(...) references");
   };
   check(o.key);
   check(o.value);
-  // a string value in InRange form ("a-b") switches the set operators to range compares
-  if (o.value && o.value->t == JT::Str && !has_vars(*o.value) && o.op >= O_ANYIN && o.op <= O_ALLNOTIN &&
-      pat::get_operator(o.value->s) == pat::OP_IN_RANGE)
-    throw Unsupported("InRange values of set operators");
   if (o.value && o.value->t == JT::Str && has_vars(*o.value) && o.op >= O_ANYIN && o.op <= O_ALLNOTIN) {
     // a value substituted into a string could take the InRange form at run time; only a
     // whole-string variable (typed result) is accepted
@@ -1242,7 +1438,7 @@ inline Conditions parse_conditions(const JVal* j) {
 inline bool eval_condition(const Condition& c, const Ctx& x) {
   JPtr k = substitute(c.key, x);
   JPtr v = substitute(c.value, x);
-  return apply_op(c.op, k, v);
+  return apply_op(c.op, k, v, c.num);
 }
 inline bool eval_conditions(const Conditions& c, const Ctx& x) {
   if (c.old_list) {

@@ -232,6 +232,24 @@ class JParser {
     }
     if (p_ == s) fail("unexpected character");
     std::string num(s, p_);
+    {  // RFC 8259 number grammar (encoding/json's scanner): -?(0|[1-9][0-9]*)(.[0-9]+)?([eE][+-]?[0-9]+)?
+      size_t i = num[0] == '-' ? 1 : 0;
+      auto digits = [&]() {
+        size_t k = i;
+        while (i < num.size() && num[i] >= '0' && num[i] <= '9') ++i;
+        return i - k;
+      };
+      const size_t lead = i;
+      const size_t nd = digits();
+      bool ok = nd > 0 && !(nd > 1 && num[lead] == '0');
+      if (ok && i < num.size() && num[i] == '.') ++i, ok = digits() > 0;
+      if (ok && i < num.size() && (num[i] == 'e' || num[i] == 'E')) {
+        ++i;
+        if (i < num.size() && (num[i] == '+' || num[i] == '-')) ++i;
+        ok = digits() > 0;
+      }
+      if (!ok || i != num.size()) fail("invalid number");
+    }
     if (isint) {
       errno = 0;
       char* end;

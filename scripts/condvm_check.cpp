@@ -30,6 +30,7 @@ using std::trunc;
 #include "../kyverno_amd/csrc/kernels_abi.h"
 #include "../kyverno_amd/csrc/program.hpp"
 #include "../kyverno_amd/csrc/schema.h"
+#include "../kyverno_amd/csrc/patclass.hpp"
 
 namespace kpe {
 void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, size_t nsl_len, bool docs);
@@ -79,6 +80,19 @@ int main(int argc, char** argv) {
   a.ops = ops.data(), a.exprs = CP.exprs.data(), a.tmpls = CP.tmpls.data(), a.conds = CP.conds.data();
   a.blocks = CP.blocks.data(), a.fes = CP.fes.data(), a.rules = CP.rules.data();
   a.ctab = CP.consts.data(), a.ctext = ctext.data(), a.clist = CP.clist.data(), a.fkeys = fk.data();
+  // pattern program operand records (InRange values of set operators), as kpe_api.cpp binds them
+  std::vector<uint8_t> pb;
+  std::vector<KpePat> pp;
+  for (size_t i = 0; i < P->pat.operands.size(); ++i) {
+    if (P->pat.operand_exact[i]) {
+      pp.push_back({PK_EXACT, (uint32_t)pb.size(), (uint32_t)P->pat.operands[i].size(), 0});
+      pb.insert(pb.end(), P->pat.operands[i].begin(), P->pat.operands[i].end());
+    } else {
+      pp.push_back(kpe::classify_pattern(P->pat.operands[i], pb));
+    }
+  }
+  pb.push_back(0);
+  a.leaves = P->pat.leaves.data(), a.pconds = P->pat.conds.data(), a.pats = pp.data(), a.pat_bytes = pb.data();
   a.verdicts = verdicts.data();
   char nb[2][16];
   for (int64_t r = 0; r < a.n; ++r) cond_eval_row(a, r, nb);  // kpe_cond_kernel's lane body

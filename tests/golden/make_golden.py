@@ -30,6 +30,8 @@ outputs) lifted from the reference's tests:
                               with the chart defaults (ClusterPolicy, Audit, background, every
                               `if`/`with` false except the file guard, `else` branches taken,
                               backtick-escaped JMESPath kept verbatim)
+  condition_cases.json     <- pkg/engine/variables/evaluate_test.go TestEvaluate (constant key,
+                              operator, value -> Evaluate result; ToJSON literals as JSON)
   match_rd_cases.json      <- pkg/engine/utils/utils_test.go:1828-2460, hand-transcribed below
                               (Go struct literals): MatchesResourceDescription on the nginx
                               Deployment with kinds/name/generateName/selector/exclude blocks
@@ -527,7 +529,67 @@ def best_practices():
     return out
 
 
+def _lit_json(v):
+    """golit value -> JSON text, with the typed slice / map literals ToJSON accepts."""
+    if v[0] == "other":
+        body = v[1]
+        if body is None:
+            return "null"
+        if isinstance(body, list):
+            return "[" + ",".join(_lit_json(x) for x in body) + "]"
+        return "{" + ",".join(json.dumps(k) + ":" + _lit_json(x) for k, x in body.items()) + "}"
+    if v[0] == "list":
+        return "[" + ",".join(_lit_json(x) for x in v[1]) + "]"
+    if v[0] == "map":
+        return "{" + ",".join(json.dumps(k) + ":" + _lit_json(x) for k, x in v[1].items()) + "}"
+    if v[0] == "struct":  # map[string]string{...} inside []interface{}{...}: an untyped brace body
+        return "{" + ",".join(json.dumps(k) + ":" + _lit_json(x) for k, x in v[1].items()) + "}"
+    return to_json(v)
+
+
+def condition_cases():
+    """pkg/engine/variables/evaluate_test.go TestEvaluate: one case per line,
+    {kyverno.Condition{RawKey: kyverno.ToJSON(K), Operator: kyverno.ConditionOperators["Op"],
+    RawValue: kyverno.ToJSON(V)}, result}. Key and value are JSON (ToJSON marshals them; the
+    engine decodes numbers as float64)."""
+    rel = "pkg/engine/variables/evaluate_test.go"
+    src = open(os.path.join(REF, rel)).read()
+    a = src.index("func TestEvaluate(")
+    b = src.index("\nfunc ", a + 10)
+    out, skipped = [], 0
+    for m in re.finditer(r"\{kyverno\.Condition\{RawKey: kyverno\.ToJSON\(", src[a:b]):
+        pos = a + m.end()
+        line = src.count("\n", 0, pos) + 1
+        try:
+            r = Reader(src, pos)
+            key = r.value()
+            r.eat(")")
+            r.eat(",")
+            r.eat("Operator:")
+            r.eat("kyverno.ConditionOperators[")
+            r.ws()
+            op = r.string()
+            r.eat("]")
+            r.eat(",")
+            r.eat("RawValue:")
+            r.eat("kyverno.ToJSON(")
+            val = r.value()
+            r.eat(")")
+            r.eat("}")
+            r.eat(",")
+            res = r.value()
+            if res[0] != "bool":
+                raise Unsupported("result")
+            out.append({"line": line, "key": json.loads(_lit_json(key)), "operator": op,
+                        "value": json.loads(_lit_json(val)), "result": res[1]})
+        except (Unsupported, ValueError, IndexError):
+            skipped += 1
+    print(f"condition_cases: {len(out)} cases, {skipped} skipped")
+    return out
+
+
 if __name__ == "__main__":
+    _dump("condition_cases.json", condition_cases())
     _dump("best_practices.json", best_practices())
     _dump("chart_policies.json", chart_policies())
     _dump("engine_validate_cases.json", engine_validate_cases())

@@ -41,6 +41,7 @@ class Oracle:
         L.oracle_number_to_string.argtypes = [cp, cp, ctypes.c_size_t]
         L.oracle_validate_element.argtypes = [cp, cp, ctypes.c_int, ctypes.c_int, cp, ctypes.c_size_t]
         L.oracle_match_pattern.argtypes = [cp, cp, ctypes.c_int, cp, ctypes.c_size_t]
+        L.oracle_condition.argtypes = [cp, cp, cp]
 
     def wildcard(self, pattern, text):
         return bool(self.lib.oracle_wildcard_match(pattern.encode(), text.encode()))
@@ -134,6 +135,12 @@ class Oracle:
         k = self._chk(self.lib.oracle_match_pattern(resource_json.encode(), pattern_json.encode(), int(all_float),
                                                     buf, 4096))
         return ["pass", "skip", "fail"][k], buf.value.decode()
+
+
+    def condition(self, key_json, op, value_json):
+        """variables.Evaluate of one constant condition: True / False, 'error' or 'unsupported'."""
+        r = self.lib.oracle_condition(key_json.encode(), op.encode(), value_json.encode())
+        return {1: True, 0: False, -1: "error"}.get(r, "unsupported")
 
 
 def build():

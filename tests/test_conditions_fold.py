@@ -119,7 +119,6 @@ def test_oracle_in_list_key_semantics(oracle):
 
 
 @pytest.mark.parametrize("cond", [
-    {"all": [{"key": OP, "operator": "GreaterThan", "value": "A"}]},          # operator outside the set
     {"all": [{"key": OP, "operator": "Equals", "value": "{{ request.operation }}-x"}]},  # partial variable
 ])
 def test_unfoldable_refused(cond):

@@ -96,6 +96,15 @@ def exception_set():
                                                         "value": "CREATE"}]},
                                validate={"message": "m", "deny": {}})]),
         _cpol("nsd", [_rule("ns-rule", kinds=("Pod",))], kind="Policy", ns=NS_POL),
+        # deny / foreach-deny rules whose conditions read the resource (kpe_cond_kernel): an
+        # exception's RuleSkip must survive the condition pass (validate_resource.go:44-56)
+        _cpol("dyn-deny", [
+            _rule("deny-name", kinds=("Pod", "ConfigMap"), validate={"message": "m", "deny": {"conditions": {"any": [
+                {"key": "{{ request.object.metadata.name }}", "operator": "Equals", "value": "res-*"}]}}}),
+            _rule("fe-deny", kinds=("Pod",), validate={"message": "m", "foreach": [{
+                "list": "request.object.spec.containers",
+                "deny": {"conditions": {"any": [{"key": "{{ element.name }}", "operator": "NotEquals",
+                                                 "value": "zz-*"}]}}}]})]),
     ]
     rname = restricted["spec"]["rules"][0]["name"]
     bname = baseline["spec"]["rules"][0]["name"]
@@ -118,6 +127,7 @@ def exception_set():
         _exc("no-bg", [(rpol, [rname])], _any({"kinds": ["Pod"], "names": ["res-3*"]}), background=False),
         _exc("folded-cond", [(bpol, ["autogen-" + bname])], _any({"names": ["res-4*"]}),
              conditions={"all": [{"key": "{{ request.operation }}", "operator": "Equals", "value": "CREATE"}]}),
+        _exc("dyn-deny-x", [("dyn-deny", ["deny-name", "fe-*"])], _any({"namespaces": ["ns-0*"]})),
     ]
     return pols, excs
 
