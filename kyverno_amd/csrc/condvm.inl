@@ -19,7 +19,8 @@
 #ifndef CV_LIST_CAP
 #define CV_LIST_CAP 32
 #endif
-constexpr int kCvBufs = 7;  // key: 0,1 (+2 list template); value: 3,4 (+5); foreach list: 6
+constexpr int kCvBufs = 6 + KPE_FE_DEPTH;  // key: 0,1 (+2 list template); value: 3,4 (+5); foreach
+                                           // lists: 6 + nesting level
 
 constexpr uint32_t VK_NULL = 0, VK_NODE = 1, VK_CONST = 2, VK_LIST = 3, VK_KEY = 4, VK_NUM = 5;
 constexpr uint32_t JT_NULL = 0, JT_BOOL = 1, JT_NUM = 2, JT_STR = 3, JT_ARR = 4, JT_OBJ = 5;
@@ -42,6 +43,9 @@ struct CondVM {
   uint32_t root;
   CV buf[kCvBufs][CV_LIST_CAP];
   uint32_t blen[kCvBufs];
+  int dep;                     // foreach nesting level of the current element (-1: none)
+  CV els[KPE_FE_DEPTH];        // element<n>
+  uint32_t elis[KPE_FE_DEPTH];  // elementIndex<n>
   char (*nb)[16];  // 2 x 16 bytes for fmt.Sprint of an elementIndex: LDS on the device, so that
                    // no generic pointer ever reaches the lane's private memory
 
@@ -219,7 +223,7 @@ struct CondVM {
   }
 
   // One expression (no `||`): the result may be a list in buffer b0 or b1.
-  __device__ __forceinline__ int run_ops(const KpeCExpr& e, CV el, uint32_t eli, uint32_t b0, uint32_t b1, CV* out) {
+  __device__ __forceinline__ int run_ops(const KpeCExpr& e, uint32_t b0, uint32_t b1, CV* out) {
     const bool strict = e.flags & CE_STRICT;
     uint32_t mode = 0;  // 0 single value, 1 projection over list `lb`, 2 dead projection (null)
     CV cur = cv(VK_NULL, 0);
@@ -242,8 +246,17 @@ struct CondVM {
       }
       switch (op) {
         case QO_OBJ: cur = node(root); break;
-        case QO_EL: cur = el; break;
-        case QO_IDX: cur = cv(VK_NUM, eli); break;
+        case QO_EL:
+        case QO_IDX: {  // element<n> / elementIndex<n> (n = innermost by default) of the foreach levels
+          const int lv = o.y == 0xFFFFFFFFu ? dep : (int)o.y;
+          if (lv < 0 || lv > dep) {  // not in the context: NotFoundError for a plain chain
+            if (strict) return CS_NOTFOUND;
+            cur = cv(VK_NULL, 0);
+          } else {
+            cur = op == QO_EL ? els[lv] : cv(VK_NUM, elis[lv]);
+          }
+          break;
+        }
         case QO_CONST: cur = SC_TYPE(a.ctab[o.y].flags) == SC_T_NULL ? cv(VK_NULL, 0) : cv(VK_CONST, o.y); break;
         case QO_FIELD:
         case QO_INDEX:
@@ -341,11 +354,11 @@ struct CondVM {
     return CS_OK;
   }
   // A query with its `||` operands: the first truthy one, else the last one's value.
-  __device__ __forceinline__ int query(uint32_t ei, CV el, uint32_t eli, uint32_t b0, uint32_t b1, CV* out) {
+  __device__ __forceinline__ int query(uint32_t ei, uint32_t b0, uint32_t b1, CV* out) {
     for (;;) {
       const KpeCExpr e = a.exprs[ei];
       CV r;
-      const int st = run_ops(e, el, eli, b0, b1, &r);
+      const int st = run_ops(e, b0, b1, &r);
       if (st == CS_NOTFOUND) return CS_ERROR;  // NotFoundError => "Unknown key" => RuleError
       if (st != CS_OK) return st;
       if (e.alt == CE_NONE || !is_false(r)) {
@@ -357,7 +370,7 @@ struct CondVM {
   }
   // A condition key / value after substitution (template `ti`); lists go to buffer bl. One
   // query() call site: a single query is a one-element template walk that returns its value.
-  __device__ __forceinline__ int value(uint32_t ti, CV el, uint32_t eli, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
+  __device__ __forceinline__ int value(uint32_t ti, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
     const KpeVTmpl t = a.tmpls[ti];
     const bool arr = t.kind == VT_ARRAY;
     const uint32_t n = arr ? t.b : 1u;
@@ -368,7 +381,7 @@ struct CondVM {
       if (te.kind == VT_CONST) {
         x = SC_TYPE(a.ctab[te.a].flags) == SC_T_NULL ? cv(VK_NULL, 0) : cv(VK_CONST, te.a);
       } else {
-        const int st = query(te.a, el, eli, b0, b1, &x);
+        const int st = query(te.a, b0, b1, &x);
         if (st != CS_OK) return st;
       }
       if (!arr) {
@@ -992,12 +1005,12 @@ struct CondVM {
   }
 
   // ---- conditions ---------------------------------------------------------------------------
-  __device__ __forceinline__ int condition(uint32_t ci, CV el, uint32_t eli) {
+  __device__ __forceinline__ int condition(uint32_t ci) {
     const KpeCCond c = a.conds[ci];
     CV kv[2];
     for (int side = 0; side < 2; ++side) {  // key (buffers 0, 1, 2), then value (3, 4, 5)
       const uint32_t b = side ? 3u : 0u;
-      const int st = value(side ? c.value : c.key, el, eli, b, b + 1u, b + 2u, &kv[side]);
+      const int st = value(side ? c.value : c.key, b, b + 1u, b + 2u, &kv[side]);
       if (st == CS_UNDEC) return CB_UNDEC;
       if (st != CS_OK) return CB_ERROR;
     }
@@ -1014,13 +1027,13 @@ struct CondVM {
     return r ? CB_TRUE : CB_FALSE;
   }
   // evaluateAnyAllConditions: any (when present) then all, each short-circuiting
-  __device__ __forceinline__ int block(uint32_t bi, CV el, uint32_t eli) {
+  __device__ __forceinline__ int block(uint32_t bi) {
     const KpeCBlock b = a.blocks[bi];
     const bool has_any = b.flags & CB_HAS_ANY;
     bool any_ok = !has_any;
     const uint32_t n = b.nany + b.nall;
     for (uint32_t i = has_any ? 0u : b.nany; i < n; ++i) {  // any (when present), then all
-      const int r = condition(b.c0 + i, el, eli);
+      const int r = condition(b.c0 + i);
       if (r >= CB_ERROR) return r;
       if (i < b.nany) {
         if (r == CB_TRUE) {  // the first true `any` condition ends the any loop
@@ -1036,13 +1049,63 @@ struct CondVM {
 };
 
 // kpe_cond_kernel's body for resource r: every condition rule whose cell the scan matched.
-// A small state machine so that block() (and the foreach list's value()) are each called
-// from one place: everything is inlined, and every extra call site would be another copy.
+// A state machine so that block() (conditions), value() (foreach lists and pattern variables)
+// and the pattern VM (foreach pattern entries) are each called from one place: everything is
+// inlined, and every extra call site would be another copy.
+//
+// Foreach (validateForEach / validateElements, validate_resource.go:186-254): a stack of
+// KPE_FE_DEPTH frames, one per nesting level; an element's verdict `ev` goes to the frame's
+// loop (FE_RES): nil / skip continue, an error counts only on the last element, a failure
+// ends the level, a pass counts; a level's result goes to its parent element (or the cell).
+// Pattern rules with {{ }} variables (substitutePatterns, :456-476): the rule's variables are
+// resolved after its preconditions into pvals (an error => RuleError, a value the pattern VM
+// cannot use => undecided) and the cell stays pending for kpe_pattern_kernel.
 constexpr uint32_t PH_PRE = 0, PH_HANDLER = 1, PH_DENY = 2, PH_FE_LIST = 3, PH_FE_EL = 4, PH_FE_PRE = 5,
-                   PH_FE_DENY = 6, PH_DONE = 7;
+                   PH_FE_DENY = 6, PH_DONE = 7, PH_PV = 8, PH_FE_BODY = 9, PH_FE_PAT = 10, PH_FE_RES = 11,
+                   PH_FE_POP = 12;
+struct FeFrame {
+  KpeCForeach fe;
+  uint32_t f, fend, idx, n, count, applied;
+  CV lst;
+  bool one;
+  uint32_t scoped;  // the innermost scoped element's tape entry (kNoNode: the resource)
+};
+// A resolved pattern variable (kpe_pattern_kernel reads it): 0 ok, else the cell's verdict
+__device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, uint2* dst) {
+  const CondArgs& a = vm.a;
+  const uint32_t t = vm.type(x);
+  if (t == JT_NULL) {
+    *dst = make_uint2(PVK_NULL, 0u);
+    return 0u;
+  }
+  if (t == JT_ARR || t == JT_OBJ || x.k == VK_KEY || x.k == VK_LIST) return KPE_UNDECIDED_;  // a subtree / key text
+  if (x.k == VK_NUM) {
+    *dst = make_uint2(PVK_NUM, x.p);
+    return 0u;
+  }
+  const uint8_t* tb;
+  const KpeScalar* sc = vm.scalar(x, &tb);
+  const uint32_t f = sc->flags;
+  if ((flags & PVF_WHOLE) && t == JT_STR && !(f & SC_PSIMPLE)) return KPE_UNDECIDED_;
+  if (flags & PVF_TEXT) {  // json.Marshal of a float64 equals its fmt.Sprint text only without exponent
+    if (t == JT_STR) {  // a substituted "{{" would be substituted again (vars.go nested loop)
+      for (uint32_t i = 0; i + 1u < sc->text_len; ++i)
+        if (tb[sc->text_off + i] == '{' && tb[sc->text_off + i + 1u] == '{') return KPE_UNDECIDED_;
+    }
+    if (SC_TYPE(f) == SC_T_INT && (sc->ival > (1ll << 53) || sc->ival < -(1ll << 53))) return KPE_UNDECIDED_;
+    if (SC_TYPE(f) == SC_T_FLOAT)
+      for (uint32_t i = 0; i < sc->sp_len; ++i)
+        if (tb[sc->text_off + sc->text_len + i] == 'e') return KPE_UNDECIDED_;
+  }
+  *dst = make_uint2(x.k == VK_NODE ? PVK_SCAL : PVK_CONST, x.k == VK_NODE ? vm.doc[x.p].y : x.p);
+  return 0u;
+}
+
+template <bool FEPAT>
 __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16]) {
-  CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], {}, {}, nb};
+  CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], {}, {}, -1, {}, {}, nb};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
+  uint2* pvrow = a.pvals ? a.pvals + (size_t)r * a.nvars : nullptr;
   for (uint32_t i = 0; i < a.ncr; ++i) {
     const KpeCRule cr = a.rules[i];
     const uint8_t cell = row[cr.col];
@@ -1053,75 +1116,196 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
     if (cr.pre == CE_NONE && cell != KPE_PENDING_) continue;
     uint32_t v = cell;
     uint32_t ph = cr.pre != CE_NONE ? PH_PRE : PH_HANDLER;
-    // foreach state (validateForEach / validateElements, validate_resource.go:186-254)
-    uint32_t f = 0, idx = 0, n = 0, count = 0, applied = 0;
-    KpeCForeach fe{};
-    CV lst = cv(VK_NULL, 0), el = cv(VK_NULL, 0);
-    bool one = false;
+    FeFrame fr[KPE_FE_DEPTH];
+    vm.dep = -1;
+    uint32_t ev = 0;            // the current element's verdict (PH_FE_RES) / a level's result (PH_FE_POP)
+    uint32_t pk = 0, pend = 0;  // pattern variable slots being resolved
     while (ph != PH_DONE) {
-      uint32_t bi = CE_NONE;
       if (ph == PH_HANDLER) {
         if (cr.kind == CR_DENY) {
           ph = PH_DENY;
         } else if (cr.kind == CR_FOREACH) {
+          vm.dep = 0;
+          fr[0].f = cr.fe0, fr[0].fend = cr.fe0 + cr.nfe, fr[0].applied = 0, fr[0].scoped = kNoNode;
           ph = PH_FE_LIST;
+        } else if (cr.npv) {
+          pk = cr.pv0, pend = cr.pv0 + cr.npv;
+          ph = PH_PV;
         } else {
           if (cr.kind == CR_NONE) v = KPE_NA_;  // no handler: no response
           ph = PH_DONE;
         }
         continue;
       }
-      if (ph == PH_FE_LIST) {  // next entry: EvaluateList (utils/foreach.go:12-24)
-        if (f >= cr.nfe) {
-          v = applied ? KPE_PASS_ : KPE_NA_;
+      if (ph == PH_FE_POP) {  // level vm.dep finished with ev
+        if (vm.dep == 0) {
+          v = ev;
           ph = PH_DONE;
-          continue;
+        } else {
+          --vm.dep;
+          ph = PH_FE_RES;
         }
-        fe = a.fes[cr.fe0 + f];
-        const int st = vm.value(fe.list, cv(VK_NULL, 0), 0, 0, 1, 2, &lst);
+        continue;
+      }
+      FeFrame& F = fr[vm.dep < 0 ? 0 : vm.dep];
+      if (ph == PH_FE_LIST && F.f >= F.fend) {  // every entry done: pass if any element applied
+        ev = F.applied ? KPE_PASS_ : KPE_NA_;
+        ph = PH_FE_POP;
+        continue;
+      }
+      if (ph == PH_FE_LIST || ph == PH_PV) {  // the one value() call site
+        uint32_t ti;
+        if (ph == PH_FE_LIST) {
+          F.fe = a.fes[F.f];
+          ti = F.fe.list;
+        } else {
+          if (pk >= pend) {  // every variable resolved
+            ph = vm.dep < 0 ? PH_DONE : PH_FE_PAT;
+            continue;
+          }
+          ti = a.pvars[pk].tmpl;
+        }
+        const uint32_t lb = 6u + (uint32_t)(vm.dep < 0 ? 0 : vm.dep);
+        const int saved = vm.dep;
+        if (ph == PH_FE_LIST) --vm.dep;  // a level's list is evaluated in its parent's context
+        CV res;
+        const int st = vm.value(ti, 0, 1, 2, &res);
+        vm.dep = saved;
         if (st == CS_UNDEC) {
           v = KPE_UNDECIDED_;
           ph = PH_DONE;
           continue;
         }
-        if (st != CS_OK) {  // "failed to evaluate list": the entry is skipped
-          ++f;
+        if (ph == PH_PV) {
+          uint32_t bad = st != CS_OK ? (uint32_t)KPE_ERROR_ : pv_store(vm, res, a.pvars[pk].flags, pvrow + pk);
+          ++pk;
+          if (bad == KPE_UNDECIDED_) {
+            v = KPE_UNDECIDED_;
+            ph = PH_DONE;
+          } else if (bad) {  // "variable substitution failed": RuleError
+            if (vm.dep < 0) {
+              v = KPE_ERROR_;
+              ph = PH_DONE;
+            } else {
+              ev = KPE_ERROR_;
+              ph = PH_FE_RES;
+            }
+          }
           continue;
         }
-        one = vm.type(lst) != JT_ARR;  // a non-list result is a one-element list
-        if (!one && lst.k == VK_LIST) {  // keep a computed list out of the key / value buffers
-          vm.blen[6] = vm.blen[lst.p];
-          for (uint32_t k = 0; k < vm.blen[6]; ++k) vm.buf[6][k] = vm.buf[lst.p][k];
-          lst = cv(VK_LIST, 6);
+        // EvaluateList (utils/foreach.go:12-24)
+        if (st != CS_OK) {  // "failed to evaluate list": the entry is skipped
+          ++F.f;
+          continue;
         }
-        n = one ? 1u : vm.alen(lst);
-        idx = 0, count = 0;
+        F.one = vm.type(res) != JT_ARR;  // a non-list result is a one-element list
+        if (!F.one && res.k == VK_LIST) {  // keep a computed list out of the key / value buffers
+          vm.blen[lb] = vm.blen[res.p];
+          for (uint32_t k = 0; k < vm.blen[lb]; ++k) vm.buf[lb][k] = vm.buf[res.p][k];
+          res = cv(VK_LIST, lb);
+        }
+        F.lst = res;
+        F.n = F.one ? 1u : vm.alen(res);
+        F.idx = 0, F.count = 0;
         ph = PH_FE_EL;
         continue;
       }
       if (ph == PH_FE_EL) {
-        if (idx >= n) {
-          applied += count;
-          ++f;
+        if (F.idx >= F.n) {
+          F.applied += F.count;
+          ++F.f;
           ph = PH_FE_LIST;
           continue;
         }
-        el = one ? lst : vm.aget(lst, idx);
+        const CV el = F.one ? F.lst : vm.aget(F.lst, F.idx);
         if (vm.type(el) == JT_NULL) {
-          ++idx;
+          ++F.idx;
           continue;
         }
-        if (fe.scope == 2u && vm.type(el) != JT_OBJ) {  // AddElementToContext: elementScope needs a map
-          v = KPE_ERROR_;
+        const bool is_map = vm.type(el) == JT_OBJ;
+        if (F.fe.scope == 2u && !is_map) {  // AddElementToContext: elementScope needs a map (RuleError)
+          ev = KPE_ERROR_;
+          ph = PH_FE_POP;
+          continue;
+        }
+        vm.els[vm.dep] = el, vm.elis[vm.dep] = F.idx;
+        const bool scoped = F.fe.scope == 0u ? is_map : F.fe.scope == 2u;
+        const uint32_t parent = vm.dep > 0 ? fr[vm.dep - 1].scoped : kNoNode;
+        // a scoped element is a map: a tape entry (VK_NODE) or a constant the pattern VM cannot walk
+        F.scoped = scoped ? (el.k == VK_NODE ? el.p : 0xFFFFFFFEu) : parent;
+        ph = F.fe.pre != CE_NONE ? PH_FE_PRE : PH_FE_BODY;
+        continue;
+      }
+      if (ph == PH_FE_BODY) {
+        if (F.fe.kind == FE_DENY) {
+          ph = PH_FE_DENY;
+        } else if (F.fe.kind == FE_PAT && FEPAT) {
+          pk = F.fe.c & 0xFFFFu, pend = pk + (F.fe.c >> 16);
+          ph = PH_PV;
+        } else if (F.fe.kind == FE_NEST && vm.dep + 1 < KPE_FE_DEPTH) {
+          FeFrame& G = fr[vm.dep + 1];
+          G.f = F.fe.a, G.fend = F.fe.a + F.fe.b, G.applied = 0, G.scoped = F.scoped;
+          ++vm.dep;
+          ph = PH_FE_LIST;
+        } else if (F.fe.kind == FE_NONE) {
+          ev = KPE_NA_;  // a nil response
+          ph = PH_FE_RES;
+        } else {
+          v = KPE_UNDECIDED_;  // not compiled into this kernel instance
           ph = PH_DONE;
-          continue;
         }
-        ph = fe.pre != CE_NONE ? PH_FE_PRE : PH_FE_DENY;
+        continue;
+      }
+      if (ph == PH_FE_PAT) {  // the entry's pattern / anyPattern (validatePatterns) on the element
+        if constexpr (FEPAT) {
+          if (F.scoped == 0xFFFFFFFEu) {
+            v = KPE_UNDECIDED_;
+            ph = PH_DONE;
+            continue;
+          }
+          const PatArgs& pa = *a.pat;
+          PatVM pvm{pa, vm.doc, F.scoped == kNoNode ? vm.root : F.scoped, pvrow, 0u};
+          const uint32_t nr = F.fe.b & 0xFFFFu, pf = F.fe.b >> 16;
+          uint32_t fails = 0, skips = 0, last = KPE_PASS_;
+          bool passed = false, undec = false;
+          if (pf & PR_ANY_BAD) last = KPE_ERROR_;
+          for (uint32_t k = 0; k < nr && !passed && !undec && !(pf & PR_ANY_BAD); ++k) {
+            last = pat_match_root(pvm, F.fe.a + k);
+            if (last == KPE_PASS_) passed = true;
+            else if (last == KPE_SKIP_) ++skips;
+            else if (last == KPE_UNDECIDED_) undec = true;
+            else ++fails;
+          }
+          if (undec) {
+            v = KPE_UNDECIDED_;
+            ph = PH_DONE;
+            continue;
+          }
+          ev = !(pf & PR_ANY) || (pf & PR_ANY_BAD) ? last
+                                                   : passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
+        }
+        ph = PH_FE_RES;
+        continue;
+      }
+      if (ph == PH_FE_RES) {  // the element's verdict ev
+        if (ev == KPE_UNDECIDED_) {
+          v = KPE_UNDECIDED_;
+          ph = PH_DONE;
+        } else if (ev == KPE_FAIL_ || (ev == KPE_ERROR_ && F.idx + 1u >= F.n)) {
+          ph = PH_FE_POP;  // the level ends with ev
+        } else {
+          if (ev == KPE_PASS_) ++F.count;
+          ++F.idx;
+          ph = PH_FE_EL;
+        }
         continue;
       }
       const bool elem = ph == PH_FE_PRE || ph == PH_FE_DENY;
-      bi = ph == PH_PRE ? cr.pre : ph == PH_DENY ? cr.deny : ph == PH_FE_PRE ? fe.pre : fe.deny;
-      const int res = vm.block(bi, elem ? el : cv(VK_NULL, 0), elem ? idx : 0u);  // the one call site
+      const uint32_t bi = ph == PH_PRE ? cr.pre : ph == PH_DENY ? cr.deny : ph == PH_FE_PRE ? F.fe.pre : F.fe.deny;
+      const int saved = vm.dep;
+      if (!elem) vm.dep = -1;  // rule-level conditions: no element in the context
+      const int res = vm.block(bi);  // the one call site
+      vm.dep = saved;
       if (res == CB_UNDEC) {
         v = KPE_UNDECIDED_;
         ph = PH_DONE;
@@ -1137,26 +1321,16 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
       } else if (ph == PH_DENY) {  // validateDeny (validate_resource.go:268-279)
         v = res == CB_TRUE ? KPE_FAIL_ : res == CB_FALSE ? KPE_PASS_ : KPE_ERROR_;
         ph = PH_DONE;
-      } else {  // an element's preconditions (false => skip) or deny (true => fail)
-        uint32_t ev;
-        if (res == CB_ERROR) ev = KPE_ERROR_;
-        else if (ph == PH_FE_PRE) ev = res == CB_FALSE ? KPE_SKIP_ : 0u;
-        else ev = res == CB_TRUE ? KPE_FAIL_ : KPE_PASS_;
-        if (ev == 0u) {  // preconditions hold: evaluate the deny conditions
-          ph = PH_FE_DENY;
-          continue;
+      } else if (ph == PH_FE_PRE) {  // an element's preconditions: false => skip, error => error
+        if (res == CB_TRUE) {
+          ph = PH_FE_BODY;
+        } else {
+          ev = res == CB_FALSE ? KPE_SKIP_ : KPE_ERROR_;
+          ph = PH_FE_RES;
         }
-        ph = PH_FE_EL;
-        ++idx;
-        if (ev == KPE_PASS_) {
-          ++count;
-        } else if (ev == KPE_FAIL_) {
-          v = KPE_FAIL_;
-          ph = PH_DONE;
-        } else if (ev == KPE_ERROR_ && idx >= n) {  // an error counts only on the last element
-          v = KPE_ERROR_;
-          ph = PH_DONE;
-        }
+      } else {  // an element's deny: true => fail
+        ev = res == CB_TRUE ? KPE_FAIL_ : res == CB_FALSE ? KPE_PASS_ : KPE_ERROR_;
+        ph = PH_FE_RES;
       }
     }
     row[cr.col] = (uint8_t)v;

@@ -1253,6 +1253,7 @@ class DocBuilder {
     if (goval::parse_float(v, &f)) e.flags |= SC_PFLOAT, e.fval = f;
     scalar_attrs(e, v);
     json_attrs(e, v);
+    if (goval::pattern_simple(v)) e.flags |= SC_PSIMPLE;
     if (e.flags & SC_RANGE) {  // endpoints of the InRange form: their duration / quantity parses
       size_t at = 0;
       goval::range_split(v, "-", &at);

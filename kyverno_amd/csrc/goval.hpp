@@ -449,6 +449,21 @@ inline bool in_range_form(std::string_view s) {
   return range_split(s, "-");
 }
 
+// schema.h SC_PSIMPLE: as a pattern string (pattern.go:152-215 validateStringPatterns) s is a
+// single condition equal to itself with the Equal operator: no `|` / `&` split, nothing trimmed
+// (strings.Trim " ", strings.TrimSpace; a non-ASCII boundary byte is taken as possible Unicode
+// space), no >= <= > < ! prefix, neither range form
+inline bool pattern_simple(std::string_view s) {
+  if (s.find('|') != std::string_view::npos || s.find('&') != std::string_view::npos) return false;
+  if (!s.empty()) {
+    auto edge = [](unsigned char c) { return c == ' ' || (c >= '\t' && c <= '\r') || c >= 0x80; };
+    if (edge((unsigned char)s.front()) || edge((unsigned char)s.back())) return false;
+  }
+  if (s.size() >= 2 && (s[0] == '>' || s[0] == '<' || s[0] == '!')) return false;
+  if (range_split(s, "!-") || range_split(s, "-")) return false;
+  return true;
+}
+
 // schema.h SC_SPQ: ParseQuantity of fmt.Sprint(v) (the text the condition set operators hand
 // to an InRange check) agrees with the quantity attributes computed from another text of v
 inline bool sprint_qty_same(const std::string& sp, bool has_qty, bool neg, int64_t qexp, uint64_t qlo, uint64_t qhi) {

@@ -1127,15 +1127,19 @@ namespace {
 #include "condvm.inl"
 }  // namespace
 
+// FEPAT: the instance that also holds the pattern VM, for programs with foreach pattern /
+// anyPattern entries (the VM's frame stack and code stay out of the plain instance)
+template <bool FEPAT>
 __global__ void __launch_bounds__(128) kpe_cond_kernel(const CondArgs* __restrict__ ap) {
   __shared__ char nb[128][2][16];
   const int64_t i = (int64_t)blockIdx.x * 128 + threadIdx.x;
-  if (i < ap->n) cond_eval_row(*ap, ap->perm ? (int64_t)ap->perm[i] : i, nb[threadIdx.x]);
+  if (i < ap->n) cond_eval_row<FEPAT>(*ap, ap->perm ? (int64_t)ap->perm[i] : i, nb[threadIdx.x]);
 }
 
-extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s) {
+extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(kpe_cond_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
+  if (fepat) hipLaunchKernelGGL(kpe_cond_kernel<true>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
+  else hipLaunchKernelGGL(kpe_cond_kernel<false>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
   return hipGetLastError();
 }
 

@@ -185,6 +185,14 @@ struct PatArgs {
   const KpePatRule* rules;
   const uint32_t* col2pr;          // verdict column -> pattern rule index + 1 (0: none), or null
   const uint32_t* pbuf;            // glob member-name bitsets (HBM)
+  // pattern variables: per-row values written by kpe_cond_kernel (pvals[row * nvars + slot]),
+  // template pieces / texts, and the condition-program constants a value may name
+  const uint2* pvals;
+  uint32_t nvars, pad_;
+  const uint2* ptmpl;
+  const uint8_t* ttext;
+  const KpeScalar* ctab;
+  const uint8_t* ctext;
   uint8_t* verdicts;
   // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)
   uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
@@ -218,6 +226,10 @@ struct CondArgs {
   const KpeCond* pconds;           // leaves of the pattern program's tables
   const KpePat* pats;
   const uint8_t* pat_bytes;
+  const PatArgs* pat;              // the pattern program (foreach pattern / anyPattern entries)
+  const KpePVar* pvars;            // pattern variable slots (query template, use flags)
+  uint2* pvals;                    // their per-row values (PatArgs::pvals), or null
+  uint32_t nvars, pad_;
   uint8_t* verdicts;
 };
 

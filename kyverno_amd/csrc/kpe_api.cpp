@@ -29,7 +29,7 @@ bool is_limit_error(const std::exception& e);
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
-extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s);
 extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
                                            uint8_t value, hipStream_t s);
 extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
@@ -54,6 +54,12 @@ kpe_status fail(kpe_status s, const std::string& m) {
   do {                                                                                             \
     hipError_t e_ = (x);                                                                           \
     if (e_ != hipSuccess) return fail(KPE_E_DEVICE, std::string(#x ": ") + hipGetErrorString(e_)); \
+  } while (0)
+
+#define PCHK(x)                     \
+  do {                              \
+    hipError_t e_ = (x);            \
+    if (e_ != hipSuccess) return e_; \
   } while (0)
 
 struct DevBuf {
@@ -143,6 +149,7 @@ struct DeviceProgram {
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
   DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
+  DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
   DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
   DevBuf cops, cexprs, ctmpls, cconds, cblocks, cfes, crules, cconsts, ctext, cclist;
@@ -163,6 +170,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t fuse_lds = 0, fuse_words = 0, npairs = 0, fuse_pats = 0, fuse_patb = 0;
   DevBuf pmembers, pargs, perr;  // pattern rules: resolved members, PatArgs copy, check flags
   bool pargs_valid = false;
+  DevBuf pvals;  // pattern variables: per-row values (kpe_cond_kernel -> kpe_pattern_kernel)
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
   DevBuf pimg;  // prologue image (kpe_launch_prep)
@@ -539,6 +547,9 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.pbytes, pb, s0));
     HIPCHK(upload(D.proots, PP.roots, s0));
     HIPCHK(upload(D.prules, PP.rules, s0));
+    HIPCHK(upload(D.pvars, PP.vars, s0));
+    HIPCHK(upload(D.ptmpl, PP.tpieces, s0));
+    HIPCHK(upload(D.ttext, PP.ttext, s0));
     {
       std::vector<uint32_t> c2p(P.rules.size() + 4, 0u);  // + slack: the kernel reads whole words
       for (size_t i = 0; i < PP.rules.size(); ++i) c2p[PP.rules[i].col] = (uint32_t)i + 1u;
@@ -803,7 +814,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
   for (int k : {0, 1, 2, 3, 7, 8, 9}) lean = lean && (B.pp[k] & PRED_LOCAL) && B.pp[k] != PRED_NONE;
   for (const auto& tm : terms) lean = lean && (tm.type != T_KIND_PRED || ((tm.a & PRED_LOCAL) && tm.a != PRED_NONE));
-  if (!P.pat.rules.empty()) {  // pattern members: names -> D_KEY ids + 1, glob names -> bitsets
+  if (!P.pat.rules.empty() || P.any_fe_pat) {  // pattern members: names -> D_KEY ids + 1, glob names -> bitsets
     if (!C.has_docs) return fail(KPE_E_STATE, "pattern rules need a corpus flattened with KPE_CORPUS_DOCS");
     const auto& PP = P.pat;
     std::vector<int64_t> kid(PP.keys.size());
@@ -825,6 +836,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     }
     HIPCHK(upload(B.cfkeys, fk, s));
     B.cargs_valid = false;
+    if (!P.pat.vars.empty()) HIPCHK(B.pvals.ensure((size_t)C.n * P.pat.vars.size() * 8 + 8));
   }
   if (!P.pssx.rules.empty()) {  // podSecurity exclusions: cold pod columns, key tables, resolved excludes
     auto& D = *cc->d;
@@ -1110,6 +1122,50 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
                          B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
+  auto ensure_pargs = [&]() -> hipError_t {  // the binding's PatArgs (pattern kernel, foreach patterns)
+    if (!B.pargs_valid) {
+      PatArgs pa{};
+      pa.n = C.n;
+      pa.R = (uint32_t)R;
+      pa.npr = (uint32_t)P.pat.rules.size();
+      pa.doc = D.doc.as<uint32_t>();
+      pa.doc_off = D.doc_off.as<uint64_t>();
+      pa.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();  // C3 14.0 -> 8.5 ms, C5 27.6 -> 19.4 ms
+      pa.scal = D.scal.as<KpeScalar>();
+      pa.scal_text = D.scal_text.as<uint8_t>();
+      pa.nodes = PD.pnodes.as<KpePNode>();
+      pa.members = B.pmembers.as<uint4>();
+      pa.lists = PD.plists.as<uint32_t>();
+      pa.leaves = PD.pleaves.as<KpeLeaf>();
+      pa.conds = PD.pconds.as<KpeCond>();
+      pa.pats = PD.ppats.as<KpePat>();
+      pa.pat_bytes = PD.pbytes.as<uint8_t>();
+      pa.roots = PD.proots.as<uint32_t>();
+      pa.rules = PD.prules.as<KpePatRule>();
+      pa.col2pr = PD.pcol2pr.as<uint32_t>();
+      pa.pbuf = B.pbuf.as<uint32_t>();
+      pa.pvals = P.pat.vars.empty() ? nullptr : B.pvals.as<uint2>();
+      pa.nvars = (uint32_t)P.pat.vars.size();
+      pa.ptmpl = PD.ptmpl.as<uint2>();
+      pa.ttext = PD.ttext.as<uint8_t>();
+      pa.ctab = PD.cconsts.as<KpeScalar>();
+      pa.ctext = PD.ctext.as<uint8_t>();
+      pa.verdicts = B.verdicts.as<uint8_t>();
+      pa.nnodes = (uint32_t)P.pat.nodes.size(), pa.nmembers = (uint32_t)(P.pat.members.size() / 4);
+      pa.nlists = (uint32_t)P.pat.lists.size(), pa.nleaves = (uint32_t)P.pat.leaves.size();
+      pa.nconds = (uint32_t)P.pat.conds.size(), pa.npats = (uint32_t)P.pat.operands.size();
+      pa.nroots = (uint32_t)P.pat.roots.size(), pa.npbuf = (uint32_t)(B.pbuf.bytes / 4);
+      pa.nscal = C.scal.size(), pa.ndoc = C.doc.size() / 2;
+      PCHK(B.perr.ensure(4));
+      PCHK(hipMemsetAsync(B.perr.p, 0, 4, s));
+      pa.err = B.perr.as<uint32_t>();
+      PCHK(B.pargs.ensure(sizeof(PatArgs)));
+      PCHK(hipMemcpyAsync(B.pargs.p, &pa, sizeof(PatArgs), hipMemcpyHostToDevice, s));
+      PCHK(hipStreamSynchronize(s));
+      B.pargs_valid = true;
+    }
+    return hipSuccess;
+  };
   if (!P.cond.rules.empty()) {
     if (!B.cargs_valid) {
       CondArgs ca{};
@@ -1138,13 +1194,20 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.pconds = PD.pconds.as<KpeCond>();
       ca.pats = PD.ppats.as<KpePat>();
       ca.pat_bytes = PD.pbytes.as<uint8_t>();
+      if (P.any_fe_pat) {
+        HIPCHK(ensure_pargs());
+        ca.pat = B.pargs.as<PatArgs>();
+      }
+      ca.pvars = PD.pvars.as<KpePVar>();
+      ca.pvals = P.pat.vars.empty() ? nullptr : B.pvals.as<uint2>();
+      ca.nvars = (uint32_t)P.pat.vars.size();
       ca.verdicts = B.verdicts.as<uint8_t>();
       HIPCHK(B.cargs.ensure(sizeof(CondArgs)));
       HIPCHK(hipMemcpyAsync(B.cargs.p, &ca, sizeof(CondArgs), hipMemcpyHostToDevice, s));
       HIPCHK(hipStreamSynchronize(s));
       B.cargs_valid = true;
     }
-    HIPCHK(kpe_launch_cond(B.cargs.as<CondArgs>(), C.n, s));
+    HIPCHK(kpe_launch_cond(B.cargs.as<CondArgs>(), C.n, P.any_fe_pat ? 1 : 0, s));
   }
   if (!P.pssx.rules.empty()) {
     if (!B.xargs_valid || (masks ? B.masks.p : nullptr) != B.xmasks) {
@@ -1199,41 +1262,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(kpe_launch_pssx(B.xargs.as<PssxArgs>(), C.n, s));
   }
   if (!P.pat.rules.empty()) {
-    if (!B.pargs_valid) {
-      PatArgs pa{};
-      pa.n = C.n;
-      pa.R = (uint32_t)R;
-      pa.npr = (uint32_t)P.pat.rules.size();
-      pa.doc = D.doc.as<uint32_t>();
-      pa.doc_off = D.doc_off.as<uint64_t>();
-      pa.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();  // C3 14.0 -> 8.5 ms, C5 27.6 -> 19.4 ms
-      pa.scal = D.scal.as<KpeScalar>();
-      pa.scal_text = D.scal_text.as<uint8_t>();
-      pa.nodes = PD.pnodes.as<KpePNode>();
-      pa.members = B.pmembers.as<uint4>();
-      pa.lists = PD.plists.as<uint32_t>();
-      pa.leaves = PD.pleaves.as<KpeLeaf>();
-      pa.conds = PD.pconds.as<KpeCond>();
-      pa.pats = PD.ppats.as<KpePat>();
-      pa.pat_bytes = PD.pbytes.as<uint8_t>();
-      pa.roots = PD.proots.as<uint32_t>();
-      pa.rules = PD.prules.as<KpePatRule>();
-      pa.col2pr = PD.pcol2pr.as<uint32_t>();
-      pa.pbuf = B.pbuf.as<uint32_t>();
-      pa.verdicts = B.verdicts.as<uint8_t>();
-      pa.nnodes = (uint32_t)P.pat.nodes.size(), pa.nmembers = (uint32_t)(P.pat.members.size() / 4);
-      pa.nlists = (uint32_t)P.pat.lists.size(), pa.nleaves = (uint32_t)P.pat.leaves.size();
-      pa.nconds = (uint32_t)P.pat.conds.size(), pa.npats = (uint32_t)P.pat.operands.size();
-      pa.nroots = (uint32_t)P.pat.roots.size(), pa.npbuf = (uint32_t)(B.pbuf.bytes / 4);
-      pa.nscal = C.scal.size(), pa.ndoc = C.doc.size() / 2;
-      HIPCHK(B.perr.ensure(4));
-      HIPCHK(hipMemsetAsync(B.perr.p, 0, 4, s));
-      pa.err = B.perr.as<uint32_t>();
-      HIPCHK(B.pargs.ensure(sizeof(PatArgs)));
-      HIPCHK(hipMemcpyAsync(B.pargs.p, &pa, sizeof(PatArgs), hipMemcpyHostToDevice, s));
-      HIPCHK(hipStreamSynchronize(s));
-      B.pargs_valid = true;
-    }
+    HIPCHK(ensure_pargs());
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;

@@ -117,12 +117,188 @@ __device__ __forceinline__ bool pat_cond(const PatArgs& a, const KpeScalar* v, u
 __device__ __forceinline__ int64_t go_f2i(double f) {
   return (f >= -9223372036854775808.0 && f < 9223372036854775808.0) ? (int64_t)f : INT64_MIN;
 }
-// pattern.Validate (pattern.go:26-50) of scalar `sid` (kNoNode: a map / list value)
-__device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li) {
+// ---- pattern variables (substitutePatterns, validate_resource.go:456-476) ----------------
+// A resolved variable of the row: its scalar record and text base (PVK_NUM: null record)
+__device__ __forceinline__ const KpeScalar* pv_scalar(const PatArgs& a, uint2 x, const uint8_t** tb) {
+  if (x.x == PVK_SCAL) {
+    *tb = a.scal_text;
+    return a.scal + PV(x.y, a.nscal, 7);
+  }
+  *tb = a.ctext;
+  return a.ctab + x.y;
+}
+struct TPiece {
+  const uint8_t* p;  // null: the decimal digits of `num` (an elementIndex)
+  int n;
+  uint32_t num;
+};
+constexpr int kTPieces = 8;  // program.cpp var_leaf bound
+// The template's pieces after substitution (substituteVarInPattern: a string as is, a number /
+// bool / null json.Marshal-ed; kpe_cond_kernel already made other values undecided). Returns
+// the total length.
+__device__ __forceinline__ int tmpl_pieces(const PatArgs& a, const KpeLeaf* L, const uint2* pv, TPiece* pc) {
+  int total = 0;
+  for (uint32_t k = 0; k < L->nc && k < (uint32_t)kTPieces; ++k) {
+    const uint2 t = a.ptmpl[L->c0 + k];
+    TPiece q;
+    if ((t.x & 1u) == PT_TEXT) {  // PT_TEXT | len << 1
+      q = TPiece{a.ttext + t.y, (int)(t.x >> 1), 0u};
+    } else {
+      const uint2 x = pv[t.y];
+      if (x.x == PVK_NULL) {
+        q = TPiece{reinterpret_cast<const uint8_t*>("null"), 4, 0u};
+      } else if (x.x == PVK_NUM) {  // json.Marshal of a float64 index: its decimal digits
+        int d = 1;
+        for (uint32_t y = x.y; y >= 10u; y /= 10u) ++d;
+        q = TPiece{nullptr, d, x.y};
+      } else {
+        const uint8_t* tb;
+        const KpeScalar* s = pv_scalar(a, x, &tb);
+        const uint32_t ty = SC_TYPE(s->flags);
+        // floats: the fmt.Sprint text after the compareString text (no exponent: checked)
+        q = ty == SC_T_FLOAT ? TPiece{tb + s->text_off + s->text_len, (int)s->sp_len, 0u}
+                             : TPiece{tb + s->text_off, (int)s->text_len, 0u};
+      }
+    }
+    pc[k] = q;
+    total += q.n;
+  }
+  return total;
+}
+__device__ __forceinline__ uint8_t tp_at(const TPiece* pc, int np, int i) {
+  for (int k = 0; k < np; ++k) {
+    if (i < pc[k].n) {
+      if (pc[k].p) return pc[k].p[i];
+      uint32_t x = pc[k].num;
+      for (int j = pc[k].n - 1; j > i; --j) x /= 10u;
+      return (uint8_t)('0' + x % 10u);
+    }
+    i -= pc[k].n;
+  }
+  return 0;
+}
+// go-wildcard glob of the template's bytes [pb, pe) against s (strmatch.inl glob)
+__device__ __forceinline__ bool tp_glob(const TPiece* pc, int np, int pb, int pe, const uint8_t* s, int sn) {
+  if (pe == pb) return sn == 0;
+  int pi = pb, si = 0, star = -1, mark = 0;
+  while (si < sn) {
+    const uint8_t c = pi < pe ? tp_at(pc, np, pi) : 0;
+    if (pi < pe && c == '?') {
+      ++pi;
+      si += rune_len(s, si, sn);
+    } else if (pi < pe && c == '*') {
+      star = pi++;
+      mark = si;
+    } else if (pi < pe && c == s[si]) {
+      ++pi;
+      ++si;
+    } else if (star >= 0) {
+      pi = star + 1;
+      mark += rune_len(s, mark, sn);
+      si = mark;
+    } else {
+      return false;
+    }
+  }
+  while (pi < pe && tp_at(pc, np, pi) == '*') ++pi;
+  return pi == pe;
+}
+// The resolved leaf equals the string "*" (the default handler's presence check)
+__device__ __forceinline__ bool pat_var_star(const PatArgs& a, uint32_t li, const uint2* pv) {
+  const KpeLeaf* L = a.leaves + PV(li, a.nleaves, 4);
+  if (L->type == PL_VAR) {
+    const uint2 x = pv[L->c0];
+    if (x.x != PVK_SCAL && x.x != PVK_CONST) return false;
+    const uint8_t* tb;
+    const KpeScalar* s = pv_scalar(a, x, &tb);
+    return SC_TYPE(s->flags) == SC_T_STR && s->text_len == 1u && tb[s->text_off] == '*';
+  }
+  if (L->type != PL_TMPL) return false;
+  TPiece pc[kTPieces];
+  const int np = (int)(L->nc < (uint32_t)kTPieces ? L->nc : (uint32_t)kTPieces);
+  return tmpl_pieces(a, L, pv, pc) == 1 && tp_at(pc, np, 0) == '*';
+}
+
+__device__ __forceinline__ bool leaf_float(const KpeScalar* v, uint32_t vf, double pf) {  // validateFloatPattern
+  const uint32_t t = SC_TYPE(vf);
+  if (t == SC_T_INT) return pf == trunc(pf) && go_f2i(pf) == v->ival;
+  if (t == SC_T_FLOAT) return v->fval == pf;
+  if (t == SC_T_STR) return (vf & SC_PFLOAT) && v->fval == pf;
+  return false;
+}
+__device__ __forceinline__ bool leaf_nil(const KpeScalar* v, uint32_t vf) {  // validateNilPattern
+  switch (SC_TYPE(vf)) {
+    case SC_T_NULL: return true;
+    case SC_T_BOOL: return !(vf & SC_BTRUE);
+    case SC_T_INT: return v->ival == 0;
+    case SC_T_FLOAT: return v->fval == 0.0;
+    default: return v->text_len == 0u;
+  }
+}
+
+// pattern.Validate (pattern.go:26-50) of scalar `sid` (kNoNode: a map / list value); pv: the
+// row's resolved pattern variables; *und set where the device leaves the cell undecided
+__device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li, const uint2* pv, uint32_t* und) {
   if (sid == kNoNode) return false;  // no scalar validator accepts a map / list
   const KpeLeaf* L = a.leaves + PV(li, a.nleaves, 4);
   const KpeScalar* v = a.scal + PV(sid, a.nscal, 7);
   const uint32_t vf = v->flags, t = SC_TYPE(vf);
+  if (L->type == PL_VAR) {  // the variable's typed value is the pattern (context numbers: float64)
+    const uint2 x = pv[L->c0];
+    if (x.x == PVK_NULL) return leaf_nil(v, vf);
+    if (x.x == PVK_NUM) return leaf_float(v, vf, (double)x.y);
+    const uint8_t* tb;
+    const KpeScalar* S = pv_scalar(a, x, &tb);
+    switch (SC_TYPE(S->flags)) {
+      case SC_T_NULL: return leaf_nil(v, vf);
+      case SC_T_BOOL: return t == SC_T_BOOL && ((vf & SC_BTRUE) != 0u) == ((S->flags & SC_BTRUE) != 0u);
+      case SC_T_INT: return leaf_float(v, vf, (double)S->ival);
+      case SC_T_FLOAT: return leaf_float(v, vf, S->fval);
+      default: {  // a plain string pattern (SC_PSIMPLE): value == pattern, then validateString Equal
+        const uint8_t* p = tb + S->text_off;
+        const int pn = (int)S->text_len;
+        if (t == SC_T_STR && (int)v->text_len == pn && bytes_eq(a.scal_text + v->text_off, p, pn)) return true;
+        if ((S->flags & SC_DUR) && (vf & SC_DUR)) return v->dur == S->dur;
+        if ((S->flags & SC_QTY) && (vf & SC_QTY))
+          return qcmp(vf & SC_QNEG, v->qexp, v->qlo, v->qhi, S->flags & SC_QNEG, S->qexp, S->qlo, S->qhi) == 0;
+        if (!(vf & SC_TEXT)) return false;
+        return glob(p, pn, a.scal_text + v->text_off, (int)v->text_len);
+      }
+    }
+  }
+  if (L->type == PL_TMPL) {  // a string with variables spliced in
+    TPiece pc[kTPieces];
+    const int np = (int)(L->nc < (uint32_t)kTPieces ? L->nc : (uint32_t)kTPieces);
+    const int n = tmpl_pieces(a, L, pv, pc);
+    if (t == SC_T_STR && (int)v->text_len == n) {  // value == pattern
+      const uint8_t* s = a.scal_text + v->text_off;
+      bool eq = true;
+      for (int i = 0; i < n && eq; ++i) eq = tp_at(pc, np, i) == s[i];
+      if (eq) return true;
+    }
+    for (int i = 0; i < n; ++i) {  // `|` / `&` splits: not restated on the device
+      const uint8_t c = tp_at(pc, np, i);
+      if (c == '|' || c == '&') {
+        *und = 1u;
+        return false;
+      }
+    }
+    int b = 0, e = n;  // strings.Trim(" ") and TrimSpace (ASCII; a non-ASCII edge: undecided)
+    auto ws = [](uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); };
+    while (b < e && ws(tp_at(pc, np, b))) ++b;
+    while (e > b && ws(tp_at(pc, np, e - 1))) --e;
+    if (b < e) {
+      const uint8_t c0 = tp_at(pc, np, b), c1 = tp_at(pc, np, e - 1);
+      // an operator prefix, a duration / quantity / range operand, or a non-ASCII edge
+      if (c0 >= 0x80 || c1 >= 0x80 || (e - b >= 2 && (c0 == '<' || c0 == '>' || c0 == '!')) || c0 == '+' ||
+          c0 == '-' || c0 == '.' || (c0 >= '0' && c0 <= '9')) {
+        *und = 1u;
+        return false;
+      }
+    }
+    if (!(vf & SC_TEXT)) return false;  // compareString of nil
+    return tp_glob(pc, np, b, e, a.scal_text + v->text_off, (int)v->text_len);
+  }
   switch (L->type) {
     case PL_BOOL: return t == SC_T_BOOL && ((vf & SC_BTRUE) != 0u) == (L->bval != 0u);
     case PL_INT:
@@ -195,7 +371,9 @@ constexpr uint32_t VM_BEGIN = 0, VM_STEP = 1, VM_RET = 2;
 struct PatVM {
   const PatArgs& a;
   const uint2* doc;   // the whole tape (absolute entry indices)
-  uint32_t root;      // this resource's root entry
+  uint32_t root;      // this resource's root entry (or a foreach element's entry)
+  const uint2* pv;    // the row's resolved pattern variables
+  uint32_t und;       // a leaf the device does not decide was reached
   uint32_t reg, val;  // AnchorMap: slots registered / present in the resource
   int sp;
   PFrame st[kPatStack];
@@ -211,7 +389,7 @@ struct PatVM {
         const uint32_t rk = br == kNoNode ? 0xFFu : DN_KIND(doc[PVD(br)].x);
         state = VM_RET;
         if (pn.kind == PN_LEAF && rk != DN_ARR) {
-          v = pat_leaf(a, node_sid(a, doc, br), pn.y) ? PE_OK : PE_OTHER;
+          v = pat_leaf(a, node_sid(a, doc, br), pn.y, pv, &und) ? PE_OK : PE_OTHER;
         } else if (pn.kind == PN_LEAF || pn.kind == PN_ARR_LEAF) {  // scalar pattern vs a list
           if (rk != DN_ARR) {
             v = PE_OTHER;
@@ -219,7 +397,7 @@ struct PatVM {
             PV_KIDS(br, c0, end);
             v = PE_OK;
             for (uint32_t c = c0; c < end && v == PE_OK; ++c)
-              if (!pat_leaf(a, node_sid(a, doc, c), pn.y)) v = PE_OTHER;
+              if (!pat_leaf(a, node_sid(a, doc, c), pn.y, pv, &und)) v = PE_OTHER;
           }
         } else if (pn.kind == PN_MAP) {
           if (rk != DN_MAP) {
@@ -301,7 +479,8 @@ struct PatVM {
                 e = c == kNoNode ? PE_OK : PE_NEG;
               } else if (c == kNoNode && h != PM_DEFAULT) {
                 e = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
-              } else if (m.x & PMF_STAR) {
+              } else if ((m.x & PMF_STAR) ||
+                         ((m.x & PMF_VSTAR) && pat_var_star(a, a.nodes[PV(m.z, a.nnodes, 1)].y, pv))) {
                 e = (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
               } else if (h == PM_EXIST) {
                 if (DN_KIND(doc[PVD(c)].x) != DN_ARR || a.nodes[PV(m.z, a.nnodes, 1)].kind != PN_EXLIST) {
@@ -314,7 +493,7 @@ struct PatVM {
                 // a scalar pattern against a scalar / absent value resolves in place: BEGIN's
                 // pattern.Validate and RET's anchor mapping without the two VM round trips
                 const uint32_t li = a.nodes[PV(m.z, a.nnodes, 1)].y;
-                const uint32_t v1 = pat_leaf(a, node_sid(a, doc, c), li) ? PE_OK : PE_OTHER;
+                const uint32_t v1 = pat_leaf(a, node_sid(a, doc, c), li, pv, &und) ? PE_OK : PE_OTHER;
                 e = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
               } else {
                 br = c, bpi = m.z, begin_child = true;
@@ -379,7 +558,9 @@ struct PatVM {
 // verdict of one pattern: pass / skip / fail, or error when the PatternError path is empty
 __device__ __forceinline__ uint32_t pat_match_root(PatVM& vm, uint32_t root) {
   const PatArgs& a = vm.a;
+  vm.und = 0u;
   const uint32_t e = vm.run(a.roots[PV(2 * root, a.nroots, 8)]);
+  if (vm.und) return KPE_UNDECIDED_;
   if (e == PE_OK) return KPE_PASS_;
   if (e == PE_SKIP) return KPE_SKIP_;
   if (e == PE_NEG) return KPE_FAIL_;
@@ -392,7 +573,7 @@ __device__ __forceinline__ uint32_t pat_match_root(PatVM& vm, uint32_t root) {
 // pattern roots of every rule run through one VM call site (a plain pattern is one root), so
 // the kernel holds a single copy of the VM: its code stays within the instruction cache.
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
-  PatVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r]};
+  PatVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], a.pvals + (size_t)r * a.nvars, 0u};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   // The row's cells are read four at a time (two aligned words funnel-shifted to the row's
   // byte offset), and the columns are visited in the same order by every lane, so the lanes of
@@ -424,14 +605,16 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
       }
       const bool any = (pr.flags & PR_ANY) != 0u;
       uint32_t fails = 0, skips = 0, last = KPE_PASS_;
-      bool passed = false;
-      for (uint32_t k = 0; k < pr.nr && !passed; ++k) {
+      bool passed = false, undec = false;
+      for (uint32_t k = 0; k < pr.nr && !passed && !undec; ++k) {
         last = pat_match_root(vm, pr.r0 + k);
         if (last == KPE_PASS_) passed = true;
         else if (last == KPE_SKIP_) ++skips;
+        else if (last == KPE_UNDECIDED_) undec = true;
         else ++fails;  // anyPattern: an empty-path error counts as a failure
       }
-      const uint32_t v = !any ? last : passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
+      const uint32_t v = undec ? KPE_UNDECIDED_ : !any ? last : passed ? KPE_PASS_
+                                                                 : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
       row[pr.col] = (uint8_t)v;
     }
   }

@@ -664,6 +664,9 @@ bool split_range(const std::string& t, const char* sep, std::string* l, std::str
 class PatCompiler {
  public:
   PatCompiler(PatProgram& pp, std::function<int32_t(const std::string&)> key_pred) : PP(pp), key_pred_(key_pred) {}
+  // Strings with {{ }} variables (substitutePatterns, validate_resource.go:456-476): fills a
+  // PL_VAR / PL_TMPL leaf and returns true; false for a plain string
+  std::function<bool(const std::string&, KpeLeaf&)> var_leaf;
 
   // one root (validate.MatchPattern call); returns the root table index
   uint32_t root(const JV& pattern) {
@@ -717,6 +720,7 @@ class PatCompiler {
         break;
       case JV::Null: l.type = PL_NIL; break;
       case JV::Str: {
+        if (var_leaf && var_leaf(v.s, l)) break;
         l.type = PL_STR;
         l.exact = operand(v.s, true);
         l.c0 = (uint32_t)PP.conds.size();
@@ -809,6 +813,8 @@ class PatCompiler {
     std::vector<std::string> first, front, back;
     for (auto& kv : v.o) {
       const Anc a = anchor_of(kv.first);
+      if (kv.first.find("{{") != std::string::npos || kv.first.find("$(") != std::string::npos)
+        throw CompileError("variables in pattern keys are not supported on the device");
       if (expanding && has_glob(kv.first)) {
         if (repeated) throw CompileError("wildcard metadata keys under an array pattern are not supported");
         if (a.k != AK_NONE && a.k != AK_EQ && a.k != AK_ADD)
@@ -870,7 +876,11 @@ class PatCompiler {
         }
       } else if (h != PM_NEG && !(flags & PMF_STAR)) {
         vn = node(val, depth + 1, repeated);
-        if (PP.nodes[vn].kind == PN_LEAF) flags |= PMF_LEAF;
+        if (PP.nodes[vn].kind == PN_LEAF) {
+          flags |= PMF_LEAF;
+          const uint32_t lt = PP.leaves[PP.nodes[vn].y].type;
+          if (h == PM_DEFAULT && (lt == PL_VAR || lt == PL_TMPL)) flags |= PMF_VSTAR;
+        }
       }
       uint32_t ki = 0;
       for (; ki < PP.keys.size() && PP.keys[ki] != name; ++ki) {
@@ -1170,6 +1180,7 @@ class Consts {
         if (goval::parse_int(v.s, &i)) e.flags |= SC_PINT, e.ival = i;
         if (goval::parse_float(v.s, &f)) e.flags |= SC_PFLOAT, e.fval = f;
         attrs(e, v.s);
+        if (goval::pattern_simple(v.s)) e.flags |= SC_PSIMPLE;
         json_list(e, v.s);
         break;
       }
@@ -1344,10 +1355,11 @@ class QueryParser {
       if (peek().s == "object") op(o, QO_OBJ);
       else op(o, QO_CONST, K.scalar(JV::str("CREATE")));  // background scans / CLI: CREATE
       i_ += 2;
-    } else if (r == "element" || r == "element0") {
-      op(o, QO_EL);
-    } else if (r == "elementIndex" || r == "elementIndex0") {
-      op(o, QO_IDX);
+    } else if (r == "element" || r == "elementIndex") {
+      op(o, r == "element" ? QO_EL : QO_IDX, 0xFFFFFFFFu);  // the innermost foreach element
+    } else if ((r.size() == 8 && !r.compare(0, 7, "element") && r[7] >= '0' && r[7] < '0' + KPE_FE_DEPTH) ||
+               (r.size() == 13 && !r.compare(0, 12, "elementIndex") && r[12] >= '0' && r[12] < '0' + KPE_FE_DEPTH)) {
+      op(o, r.size() == 8 ? QO_EL : QO_IDX, (uint32_t)(r.back() - '0'));  // element<n>: nesting level n
     } else {
       throw CompileError("context value " + r + " is not available to device conditions");
     }
@@ -1601,6 +1613,118 @@ class Lowerer {
       pc::PatCompiler pcomp(P.pat, [](const std::string&) { return (int32_t)-1; });
       return pcomp.leaf(JV::str(text));
     };
+    var_leaf_ = [this](const std::string& s, KpeLeaf& l) { return var_leaf(s, l); };
+  }
+  // validate.foreach entries of one level (newForEachValidator, validate_resource.go:76-119);
+  // nested levels are appended first, so each level's entries are contiguous. Returns the first.
+  uint32_t foreach_entries(const JV& arr, uint32_t depth) {
+    std::vector<KpeCForeach> fes;
+    for (auto& e : arr.a) {
+      if (e.t != JV::Obj) throw CompileError("foreach entry is not an object");
+      if (nonempty(e.get("context"))) throw CompileError("foreach context entries are not supported on the device");
+      KpeCForeach f{};
+      f.list = CC.list_query(sv(e.get("list")));
+      const JV* fp = e.get("preconditions");
+      f.pre = (fp && fp->t != JV::Null) ? CC.block(fp) : CE_NONE;
+      const JV* sc = e.get("elementScope");
+      f.scope = (sc && sc->t == JV::Bool) ? (sc->b ? 2u : 1u) : 0u;
+      auto present = [&](const char* key) { return e.get(key) && e.get(key)->t != JV::Null; };
+      if (present("deny")) {
+        const JV* dn = e.get("deny");
+        f.kind = FE_DENY;
+        f.deny = CC.block(dn->t == JV::Obj ? dn->get("conditions") : nullptr);
+      } else if (present("pattern") || present("anyPattern")) {
+        f.kind = FE_PAT;
+        fe_pat_ = true;
+        pc::PatCompiler pcomp(P.pat, [&](const std::string& g) {
+          const int32_t id = pred(D_KEY, {g});
+          P.preds[id].global_only = true;
+          return id;
+        });
+        pcomp.var_leaf = var_leaf_;
+        const uint32_t pv0 = (uint32_t)P.pat.vars.size();
+        f.a = (uint32_t)(P.pat.roots.size() / 2);
+        uint32_t nr = 0, flags = 0;
+        if (present("pattern")) {
+          pcomp.root(*e.get("pattern"));
+          nr = 1;
+        } else {
+          const JV& ap = *e.get("anyPattern");
+          flags = PR_ANY;
+          if (ap.t != JV::Arr) {
+            flags |= PR_ANY_BAD;
+          } else {
+            for (auto& x : ap.a) {
+              JV g = x;
+              to_float(g);  // deserializeAnyPattern's encoding/json round trip
+              pcomp.root(g);
+              ++nr;
+            }
+          }
+        }
+        const uint32_t npv = (uint32_t)P.pat.vars.size() - pv0;
+        if (nr > 0xFFFFu || pv0 > 0xFFFFu || npv > 0xFFFFu) throw CompileError("foreach pattern tables too large");
+        f.b = nr | flags << 16;
+        f.c = pv0 | npv << 16;
+      } else if (present("foreach")) {
+        const JV& nf = *e.get("foreach");
+        if (nf.t != JV::Arr) throw CompileError("nested foreach is not a list");
+        if (depth + 1 >= KPE_FE_DEPTH) throw CompileError("foreach nested deeper than the device evaluates");
+        f.kind = FE_NEST;
+        f.a = nf.a.empty() ? 0u : foreach_entries(nf, depth + 1);
+        f.b = (uint32_t)nf.a.size();
+      } else {
+        f.kind = FE_NONE;  // "invalid validation rule": a nil response
+      }
+      fes.push_back(f);
+    }
+    const uint32_t f0 = (uint32_t)P.cond.fes.size();
+    P.cond.fes.insert(P.cond.fes.end(), fes.begin(), fes.end());
+    return f0;
+  }
+  bool fe_pat_ = false;
+
+  // A pattern string with {{ }} variables (vars.go:311-389 substituteVariablesIfAny): a
+  // whole-string variable keeps the value's JSON type (PL_VAR); otherwise the variables'
+  // texts are spliced into the string (PL_TMPL: substituteVarInPattern). Each variable is a
+  // query of the condition program, resolved per row by kpe_cond_kernel.
+  bool var_leaf(const std::string& s, KpeLeaf& l) {
+    if (s.find("$(") != std::string::npos) throw CompileError("$(...) references in patterns are not supported");
+    size_t st, en;
+    if (!cq::next_var(s, 0, &st, &en)) return false;  // no complete {{ }}: a plain string
+    if (s.find("\\{{") != std::string::npos) throw CompileError("escaped variables in patterns are not supported");
+    auto slot = [&](const std::string& raw, uint32_t flags) {
+      const std::string q = cq::var_text(raw);
+      if (q == "@" || q.find("{{") != std::string::npos || q.find("}}") != std::string::npos)
+        throw CompileError("{{@}} / nested variables in patterns are not supported");
+      KpePVar pv{CC.list_query(q), flags};
+      P.pat.vars.push_back(pv);
+      return (uint32_t)P.pat.vars.size() - 1;
+    };
+    if (st == 0 && en == s.size()) {
+      l.type = PL_VAR;
+      l.c0 = slot(s, PVF_WHOLE);
+      return true;
+    }
+    l.type = PL_TMPL;
+    l.c0 = (uint32_t)P.pat.tpieces.size() / 2;
+    size_t pos = 0;
+    auto text = [&](size_t a, size_t b) {
+      if (b <= a) return;
+      P.pat.tpieces.push_back(PT_TEXT | (uint32_t)(b - a) << 1);
+      P.pat.tpieces.push_back((uint32_t)P.pat.ttext.size());
+      P.pat.ttext.insert(P.pat.ttext.end(), s.begin() + a, s.begin() + b);
+    };
+    while (cq::next_var(s, pos, &st, &en)) {
+      text(pos, st);
+      P.pat.tpieces.push_back(PT_VAR);
+      P.pat.tpieces.push_back(slot(s.substr(st, en - st), PVF_TEXT));
+      pos = en;
+    }
+    text(pos, s.size());
+    l.nc = (uint32_t)P.pat.tpieces.size() / 2 - l.c0;
+    if (l.nc > 8) throw CompileError("pattern string with more than 8 pieces around variables");
+    return true;
   }
 
   static void to_float(JV& v) {
@@ -2092,6 +2216,7 @@ class Lowerer {
       }
     }
     KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0};
+    crule.pv0 = (uint32_t)P.pat.vars.size();
     bool pss_excl = false, msg_pattern = false;
     if (!has_validate) {
       k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
@@ -2143,56 +2268,48 @@ class Lowerer {
           P.preds[id].global_only = true;
           return id;
         });
+        pcomp.var_leaf = var_leaf_;
+        crule.pv0 = (uint32_t)P.pat.vars.size();
         KpePatRule pr{(uint32_t)P.rules.size(), 0, (uint32_t)(P.pat.roots.size() / 2), 0};
-        if (present("pattern")) {
-          msg_pattern = true;
-          const JV& pt = *v->get("pattern");
-          if (pc::has_vars(pt)) throw CompileError("rule '" + rname + "': pattern variables are not supported yet");
-          pcomp.root(pt);
-          pr.nr = 1;
-        } else {
-          const JV& ap = *v->get("anyPattern");
-          pr.flags = PR_ANY;
-          if (ap.t != JV::Arr) {
-            pr.flags |= PR_ANY_BAD;  // deserializeAnyPattern fails: RuleStatusError
+        try {
+          if (present("pattern")) {
+            msg_pattern = true;
+            const JV& pt = *v->get("pattern");
+            msg_pattern = !pc::has_vars(pt);  // pass message of a substituted pattern: rendered alike
+            pcomp.root(pt);
+            pr.nr = 1;
           } else {
-            if (pc::has_vars(ap)) throw CompileError("rule '" + rname + "': pattern variables are not supported yet");
-            for (auto& e : ap.a) {
-              JV f = e;
-              to_float(f);  // encoding/json round trip (validate_resource.go:400-416)
-              pcomp.root(f);
-              ++pr.nr;
+            const JV& ap = *v->get("anyPattern");
+            pr.flags = PR_ANY;
+            if (ap.t != JV::Arr) {
+              pr.flags |= PR_ANY_BAD;  // deserializeAnyPattern fails: RuleStatusError
+            } else {
+              for (auto& e : ap.a) {
+                JV f = e;
+                to_float(f);  // encoding/json round trip (validate_resource.go:400-416)
+                pcomp.root(f);
+                ++pr.nr;
+              }
             }
           }
+        } catch (const CompileError& e) {
+          throw CompileError("rule '" + rname + "': " + e.what());
         }
+        crule.npv = (uint32_t)P.pat.vars.size() - crule.pv0;
         if (P.pat.rules.size() >= 65535) throw CompileError("more than 65535 pattern rules in one program");
         P.pat.rules.push_back(pr);
         k.handler = H_PATTERN;
       } else if (v->get("foreach") && v->get("foreach")->t == JV::Arr && !v->get("foreach")->a.empty()) {
-        // validateForEach (validate_resource.go:186-254): entries with a deny only
+        // validateForEach (validate_resource.go:186-254): deny, pattern / anyPattern and nested
+        // entries
         crule.kind = CR_FOREACH;
-        crule.fe0 = (uint32_t)P.cond.fes.size();
-        std::vector<KpeCForeach> fes;
         try {
-          for (auto& e : v->get("foreach")->a) {
-            if (e.t != JV::Obj || !e.get("deny") || nonempty(e.get("pattern")) || nonempty(e.get("anyPattern")) ||
-                nonempty(e.get("foreach")) || nonempty(e.get("context")))
-              throw CompileError("foreach entries other than deny are not supported on the device");
-            KpeCForeach f{};
-            f.list = CC.list_query(sv(e.get("list")));
-            const JV* fp = e.get("preconditions");
-            f.pre = (fp && fp->t != JV::Null) ? CC.block(fp) : CE_NONE;
-            const JV* dn = e.get("deny");
-            f.deny = CC.block(dn->t == JV::Obj ? dn->get("conditions") : nullptr);
-            const JV* sc = e.get("elementScope");
-            f.scope = (sc && sc->t == JV::Bool) ? (sc->b ? 2u : 1u) : 0u;
-            fes.push_back(f);
-          }
+          crule.fe0 = foreach_entries(*v->get("foreach"), 0);
         } catch (const CompileError& e) {
           throw CompileError("rule '" + rname + "': validate.foreach: " + e.what());
         }
-        P.cond.fes.insert(P.cond.fes.end(), fes.begin(), fes.end());
-        crule.nfe = (uint32_t)fes.size();
+        crule.nfe = (uint32_t)v->get("foreach")->a.size();
+        P.any_fe_pat = P.any_fe_pat || fe_pat_;
         k.handler = H_COND;
       } else if (nonempty(v->get("foreach")) || nonempty(v->get("cel"))) {
         throw CompileError("rule '" + rname + "': validate.foreach/cel are not supported on the device yet");
@@ -2210,7 +2327,7 @@ class Lowerer {
     }
     if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) P.any_const = true;
     rule_info_.push_back({pre_block != CE_NONE, has_validate, rname});
-    if (pre_block != CE_NONE || k.handler == H_COND) P.cond.rules.push_back(crule);
+    if (pre_block != CE_NONE || k.handler == H_COND || crule.npv) P.cond.rules.push_back(crule);
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
     P.rule_names.push_back(pol_name + "/" + rname);
@@ -2365,6 +2482,7 @@ class Lowerer {
 
   Program& P;
   cq::CondCompiler CC;
+  std::function<bool(const std::string&, KpeLeaf&)> var_leaf_;
   struct RuleInfo {
     bool pre_dyn, has_validate;
     std::string name;

@@ -31,6 +31,9 @@ struct PatProgram {
   std::vector<uint8_t> operand_exact;  // 1: compare verbatim (the `value == pattern` check)
   std::vector<uint32_t> roots;         // 2 words per root: node, anchor slots used
   std::vector<KpePatRule> rules;
+  std::vector<KpePVar> vars;           // pattern variable slots (PL_VAR / PT_VAR)
+  std::vector<uint32_t> tpieces;       // 2 words per template piece (PT_*)
+  std::vector<uint8_t> ttext;          // template texts
 };
 // Compiled preconditions / deny / foreach-deny programs (schema.h QO_* / KpeC*), evaluated per
 // resource by kpe_cond_kernel. Field names are kept as text: a binding resolves them to corpus
@@ -112,6 +115,7 @@ struct Program {
   bool any_exc = false;    // some rule has PolicyExceptions (KpeRule::exc)
   bool any_const = false;  // some rule has a constant handler (H_CONST_*)
   bool any_pss = false;
+  bool any_fe_pat = false;  // some foreach entry has a pattern / anyPattern (kpe_cond_kernel<true>)
   PatProgram pat;  // pattern rules (H_PATTERN)
   CondProgram cond;  // rules with preconditions / deny / foreach evaluated per resource
   PssxProgram pssx;  // podSecurity.exclude

@@ -470,6 +470,8 @@ typedef struct KpeXRule {
 #define SC_RANGE (1u << 14)    // corpus string: GetOperatorFromStringPattern == InRange, its two
                               // endpoints interned as scalars: ival = lo id | hi id << 32
 #define SC_RANGEU (1u << 15)   // corpus string: the InRange form with a `|` in it (undecided)
+#define SC_PSIMPLE (1u << 16)  // string: as a pattern, one plain condition equal to itself
+                              // (no `|` `&`, no operator prefix or range form, trim-invariant)
 #define SC_SPQ (1u << 12)     // number: the quantity of its fmt.Sprint text (%v) equals the quantity
                               // of convertNumberToString (%f), so SC_QTY also stands for Sprint
 #define SC_T_ARR 5          // condition constants only: text_off = first element (constant list), text_len = count
@@ -510,6 +512,8 @@ typedef struct KpePNode {
 #define PMF_GLOB (1u << 4)   // ExpandInMetadata: first resource member matching the glob (string values)
 #define PMF_SLOT (1u << 5)   // condition / existence anchor tracked in the AnchorMap
 #define PMF_LEAF (1u << 6)   // the member's pattern value is a scalar leaf (PN_LEAF)
+#define PMF_VSTAR (1u << 7)  // default-handler member whose leaf has variables: a value of "*"
+                             // is the presence check (anchor/handlers.go:130-133)
 #define PM_SLOT(x) (((x) >> 8) & 31u)
 // Leaf
 #define PL_BOOL 0u
@@ -518,6 +522,25 @@ typedef struct KpePNode {
 #define PL_NIL 3u
 #define PL_STR 4u
 #define PL_NEVER 5u  // array pattern in leaf position: always false
+#define PL_VAR 6u    // a whole-string {{ }} variable: the pattern is the variable's typed value;
+                     // c0 = variable slot (per-row value in PatArgs::pvals)
+#define PL_TMPL 7u   // a string with variables inside: pieces [c0, c0 + nc) of the template table
+// Template piece (uint2): x = PT_TEXT | len << 1 (y = offset in the template text) or PT_VAR
+// (y = variable slot; the value's text: a string as is, anything else json.Marshal-ed)
+#define PT_TEXT 0u
+#define PT_VAR 1u
+// Resolved pattern variable of a row (uint2 pvals[row * nvars + slot], written by
+// kpe_cond_kernel after the rule's preconditions): x = PVK_*, y = id
+#define PVK_NULL 0u
+#define PVK_SCAL 1u   // corpus scalar id
+#define PVK_CONST 2u  // condition-program constant id
+#define PVK_NUM 3u    // y = elementIndex (a float64)
+// Pattern variable slot: the query template (condition program) and how the pattern uses it
+#define PVF_WHOLE 1u  // a whole-string leaf: a string value must be SC_PSIMPLE
+#define PVF_TEXT 2u   // inside a template: numbers must print as json.Marshal does
+typedef struct KpePVar {
+  uint32_t tmpl, flags;
+} KpePVar;
 typedef struct KpeLeaf {
   uint32_t type, bval, c0, nc;  // PL_STR: conditions [c0, c0 + nc)
   int64_t ival;
@@ -556,8 +579,8 @@ typedef struct KpePatRule {
 // or `[*]` the following steps apply to every element of the projected list; the nulls they
 // produce are dropped when the projection ends (go-jmespath projection semantics).
 #define QO_OBJ 0u     // request.object: the resource's document root
-#define QO_EL 1u      // element / element0 (foreach)
-#define QO_IDX 2u     // elementIndex / elementIndex0 (a float64)
+#define QO_EL 1u      // element (y = 0xFFFFFFFF: the innermost) / element<y> (foreach nesting y)
+#define QO_IDX 2u     // elementIndex / elementIndex<y> (a float64)
 #define QO_CONST 3u   // y = constant (request.operation = "CREATE", raw-string / JSON literals)
 #define QO_FIELD 4u   // y = field-name index (a binding resolves it to D_KEY id + 1; 0 = absent)
 #define QO_INDEX 5u   // y = index (int32; negative counts from the end)
@@ -613,12 +636,21 @@ typedef struct KpeCCond {
 typedef struct KpeCBlock {
   uint32_t c0, nany, nall, flags;
 } KpeCBlock;
+// A validate.foreach entry (newForEachValidator, validate_resource.go:76-119): the list, its
+// preconditions, then one body: deny, pattern / anyPattern (against the innermost scoped element,
+// or the resource), or nested entries (nesting + 1)
+#define FE_NONE 0u  // no body: a nil response per element
+#define FE_DENY 1u  // deny = block
+#define FE_PAT 2u   // a = first pattern root, b = roots | PR_* << 16, c = pv0 | npv << 16
+#define FE_NEST 3u  // a = first nested entry, b = count
 typedef struct KpeCForeach {
-  uint32_t list;   // expression
+  uint32_t list;   // value template (a query)
   uint32_t pre;    // block or CE_NONE
-  uint32_t deny;   // block
+  uint32_t deny;   // block (FE_DENY)
   uint32_t scope;  // elementScope: 0 unset, 1 false, 2 true
+  uint32_t kind, a, b, c;
 } KpeCForeach;
+#define KPE_FE_DEPTH 3  // foreach nesting levels evaluated on the device
 #define CR_PRE_ONLY 0u  // only the rule's preconditions are evaluated here (other handler)
 #define CR_DENY 1u      // H_COND: validate.deny
 #define CR_FOREACH 2u   // H_COND: validate.foreach (deny entries)
@@ -626,5 +658,7 @@ typedef struct KpeCForeach {
                         // resource validator returns nil) behind per-resource preconditions
 typedef struct KpeCRule {
   uint32_t col, pre, kind, deny;  // pre / deny: block or CE_NONE
-  uint32_t fe0, nfe, pad0, pad1;
+  uint32_t fe0, nfe;
+  uint32_t pv0, npv;  // pattern rules with variables: slots [pv0, pv0 + npv) resolved after the
+                      // preconditions (validate_resource.go:456-476 substitutePatterns)
 } KpeCRule;

@@ -773,8 +773,9 @@ inline void check_roots(const Node& n) {
   std::vector<std::string> r;
   root_reads(n, r);
   for (auto& x : r)
-    if (x != "request.object" && x != "request.operation" && x != "element" && x != "element0" &&
-        x != "elementIndex" && x != "elementIndex0")
+    if (x != "request.object" && x != "request.operation" && x != "element" && x != "elementIndex" &&
+        !(x.size() == 8 && x.compare(0, 7, "element") == 0 && x[7] >= '0' && x[7] <= '3') &&
+        !(x.size() == 13 && x.compare(0, 12, "elementIndex") == 0 && x[12] >= '0' && x[12] <= '3'))
       throw Unsupported("context value " + x);
 }
 struct Query {
@@ -1507,13 +1508,23 @@ inline JPtr request_context(const JVal& res) {
   root->o.push_back({"request", req});
   return root;
 }
-// context.AddElement (nesting 0): element, element0, elementIndex, elementIndex0
-inline JPtr with_element(const JPtr& root, const JPtr& el, int64_t idx) {
+// context.AddElement (context.go:280-290): element, element<nesting>, elementIndex,
+// elementIndex<nesting> merged into the context (a nested element replaces `element`)
+inline JPtr with_element(const JPtr& root, const JPtr& el, int64_t idx, int nesting = 0) {
   auto o = std::make_shared<JVal>(*root);
-  o->o.push_back({"element", el});
-  o->o.push_back({"element0", el});
-  o->o.push_back({"elementIndex", mk_num((double)idx)});
-  o->o.push_back({"elementIndex0", mk_num((double)idx)});
+  auto put = [&](const std::string& k, const JPtr& v) {
+    for (auto& kv : o->o)
+      if (kv.first == k) {
+        kv.second = v;
+        return;
+      }
+    o->o.push_back({k, v});
+  };
+  const std::string n = std::to_string(nesting);
+  put("element", el);
+  put("element" + n, el);
+  put("elementIndex", mk_num((double)idx));
+  put("elementIndex" + n, mk_num((double)idx));
   return o;
 }
 

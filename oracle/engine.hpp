@@ -431,9 +431,14 @@ struct Rule {
   cond::Conditions pre;   // rule.preconditions (engine.go:278-286)
   cond::Conditions deny;  // validate.deny.conditions (validate_resource.go:268-279)
   bool has_deny = false;
-  struct ForEach {        // validate.foreach entry with a deny (validate_resource.go:186-254)
+  bool pattern_vars = false;  // {{ }} variables in pattern / anyPattern (substitutePatterns)
+  struct ForEach {        // validate.foreach entry (validate_resource.go:186-254, newForEachValidator)
     cond::Query list;
     cond::Conditions pre, deny;
+    bool has_deny = false;
+    JPtr pattern, any_pattern;  // the entry's pattern / anyPattern
+    bool pattern_vars = false;
+    std::vector<ForEach> nested;  // a nested foreach (nesting + 1)
     int scope = -1;       // elementScope: -1 unset, 0 false, 1 true
   };
   std::vector<ForEach> foreach;
@@ -746,6 +751,58 @@ inline std::vector<JPtr> compute_rules(const JVal& policy) {
   return out;
 }
 
+// Variables in a pattern (validate_resource.go:456-476 substitutePatterns, vars.go:311-389):
+// true when present; throws cond::Unsupported for what this restatement does not cover ($(...)
+// references, escaped or nested variables, {{@}}, queries outside the JMESPath restatement).
+inline bool pattern_vars_ok(const JVal& v) {
+  if (!pat::has_variables(v)) return false;
+  std::function<void(const JVal&)> walk = [&](const JVal& x) {
+    auto str = [](const std::string& t) {
+      if (t.find("$(") != std::string::npos) throw cond::Unsupported("$(...) references");
+      if (t.find("\\{{") != std::string::npos) throw cond::Unsupported("escaped variables");
+    };
+    if (x.t == JT::Str) str(x.s);
+    for (auto& e : x.a) walk(*e);
+    for (auto& kv : x.o) str(kv.first), walk(*kv.second);
+  };
+  walk(v);
+  cond::precompile_value(std::make_shared<JVal>(v));
+  return true;
+}
+// A validate.foreach entry (newForEachValidator): list, preconditions, then one of deny,
+// pattern / anyPattern, nested foreach. Context entries are not restated.
+inline Rule::ForEach parse_foreach(const JVal& e, int depth) {
+  if (e.t != JT::Obj || jnonempty(e.get("context"))) throw cond::Unsupported("foreach entry");
+  if (depth > 3) throw cond::Unsupported("foreach nested deeper than 4 levels");
+  Rule::ForEach f;
+  f.list = cond::compile_query(jstr(e.get("list")));
+  f.pre = cond::parse_conditions(e.get("preconditions"));
+  cond::precompile(f.pre);
+  const JVal* sc = e.get("elementScope");
+  if (sc && sc->t == JT::Bool) f.scope = sc->b ? 1 : 0;
+  const JVal* dn = e.get("deny");
+  const JVal* pt = e.get("pattern");
+  const JVal* ap = e.get("anyPattern");
+  const JVal* nf = e.get("foreach");
+  if (dn && !dn->is_null()) {
+    f.has_deny = true;
+    f.deny = cond::parse_conditions(dn->get("conditions"));
+    cond::precompile(f.deny);
+  } else if (pt && !pt->is_null()) {
+    f.pattern = deep_copy(*pt);
+    f.pattern_vars = pattern_vars_ok(*f.pattern);
+  } else if (ap && !ap->is_null()) {
+    f.any_pattern = deep_copy(*ap);
+    f.pattern_vars = pattern_vars_ok(*f.any_pattern);
+    if (!f.pattern_vars) pat::numbers_to_float(*f.any_pattern);
+  } else if (nf && !nf->is_null()) {
+    // api.DeserializeJSONArray[ForEachValidation]: a list of entries
+    if (nf->t != JT::Arr) throw cond::Unsupported("nested foreach is not a list");
+    for (auto& x : nf->a) f.nested.push_back(parse_foreach(*x, depth + 1));
+  }
+  return f;
+}
+
 inline Rule compile_rule(const JPtr& raw) {
   Rule r;
   r.raw = raw;
@@ -781,28 +838,24 @@ inline Rule compile_rule(const JPtr& raw) {
       }
     } else if (pt && !pt->is_null()) {
       r.pattern = deep_copy(*pt);
-      if (pat::has_variables(*r.pattern)) r.unsupported = true;
+      try {
+        r.pattern_vars = pattern_vars_ok(*r.pattern);
+      } catch (const cond::Unsupported&) {
+        r.unsupported = true;
+      }
     } else if (ap && !ap->is_null()) {
       r.any_pattern = deep_copy(*ap);
-      pat::numbers_to_float(*r.any_pattern);  // encoding/json round trip (validate_resource.go:400-416)
-      if (pat::has_variables(*r.any_pattern)) r.unsupported = true;
+      try {
+        r.pattern_vars = pattern_vars_ok(*r.any_pattern);
+      } catch (const cond::Unsupported&) {
+        r.unsupported = true;
+      }
+      // encoding/json round trip (validate_resource.go:400-416); with variables it follows the
+      // substitution
+      if (!r.pattern_vars) pat::numbers_to_float(*r.any_pattern);
     } else if (fe && fe->t == JT::Arr && !fe->a.empty()) {
       try {
-        for (auto& e : fe->a) {
-          // only deny foreach entries (no nested foreach, patterns or context) are restated
-          if (e->t != JT::Obj || !e->get("deny") || jnonempty(e->get("pattern")) || jnonempty(e->get("anyPattern")) ||
-              jnonempty(e->get("foreach")) || jnonempty(e->get("context")))
-            throw cond::Unsupported("foreach entry");
-          Rule::ForEach f;
-          f.list = cond::compile_query(jstr(e->get("list")));
-          f.pre = cond::parse_conditions(e->get("preconditions"));
-          f.deny = cond::parse_conditions(e->get("deny")->get("conditions"));
-          cond::precompile(f.pre);
-          cond::precompile(f.deny);
-          const JVal* sc = e->get("elementScope");
-          if (sc && sc->t == JT::Bool) f.scope = sc->b ? 1 : 0;
-          r.foreach.push_back(std::move(f));
-        }
+        for (auto& e : fe->a) r.foreach.push_back(parse_foreach(*e, 0));
       } catch (const cond::Unsupported&) {
         r.unsupported = true;
       } catch (const cond::EvalError&) {
@@ -947,17 +1000,33 @@ inline bool matches_resource_description(const Rule& r, const Policy& p, const M
   return fails == 0;
 }
 
-// validate_resource.go:316-398 validatePatterns (no exceptions, CREATE operation)
-inline Status pattern_handler(const Rule& r, const JVal& res) {
-  if (r.pattern) {
-    pat::MatchResult m = pat::match_pattern(res, *r.pattern);
+// validate_resource.go:316-398 validatePatterns (no exceptions, CREATE operation), after
+// substitutePatterns (:456-476: an error is RuleError "variable substitution failed")
+inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars, const JVal& res, const cond::Ctx* cx) {
+  JPtr pattern = pattern0, any = any0;
+  if (vars) {
+    try {
+      if (pattern) {
+        pattern = cond::substitute(pattern, *cx);
+      } else {
+        any = cond::substitute(any, *cx);
+        if (!cond::is_null(any)) any = deep_copy(*any), pat::numbers_to_float(*any);  // deserializeAnyPattern
+      }
+    } catch (const cond::EvalError&) {
+      return ERROR;
+    } catch (const cond::Unsupported&) {
+      return UNSUPPORTED;
+    }
+  }
+  if (pattern) {
+    pat::MatchResult m = pat::match_pattern(res, *pattern);
     if (m.k == pat::M_PASS) return PASS;
     if (m.k == pat::M_SKIP) return SKIP;
     return m.path.empty() ? ERROR : FAIL;
   }
-  if (r.any_pattern->t != JT::Arr) return ERROR;  // deserializeAnyPattern failure
+  if (cond::is_null(any) || any->t != JT::Arr) return ERROR;  // deserializeAnyPattern failure
   int fails = 0, skips = 0;
-  for (auto& p : r.any_pattern->a) {
+  for (auto& p : any->a) {
     pat::MatchResult m = pat::match_pattern(res, *p);
     if (m.k == pat::M_PASS) return PASS;
     if (m.k == pat::M_SKIP) ++skips;
@@ -978,49 +1047,70 @@ inline Status deny_handler(const Rule& r, const cond::Ctx& cx) {
     return UNSUPPORTED;
   }
 }
-// validate_resource.go:186-254 validateForEach / validateElements (deny entries), utils/foreach.go
-inline Status foreach_handler(const Rule& r, const cond::Ctx& cx) {
+// validate_resource.go:186-254 validateForEach / validateElements, utils/foreach.go: each entry's
+// list, then per non-null element (AddElementToContext at `nesting`) the entry's validator:
+// preconditions, then deny / pattern / anyPattern / nested foreach. `scoped` is the element the
+// patterns validate (policyContext.Element(): the innermost scoped element), or null for the
+// resource itself.
+inline Status foreach_entries(const std::vector<Rule::ForEach>& fes, const cond::Ctx& cx, const JPtr& scoped,
+                              const JVal& res, int nesting) {
   int apply_count = 0;
-  try {
-    for (auto& f : r.foreach) {
-      JPtr lst;
-      try {
-        lst = cond::run_query(f.list, cx.root);  // EvaluateList
-      } catch (const cond::NotFound&) {
-        continue;  // "failed to evaluate list": the entry is skipped
-      } catch (const cond::EvalError&) {
-        continue;
-      }
-      std::vector<JPtr> elems;
-      if (!cond::is_null(lst) && lst->t == JT::Arr) elems = lst->a;
-      else elems = {lst};
-      int count = 0;
-      for (size_t idx = 0; idx < elems.size(); ++idx) {
-        const JPtr& el = elems[idx];
-        if (cond::is_null(el)) continue;
-        if (f.scope == 1 && el->t != JT::Obj) return ERROR;  // AddElementToContext error
-        cond::Ctx ex{cond::with_element(cx.root, el, (int64_t)idx)};
-        Status st;
-        try {
-          if (f.pre.present && !cond::eval_conditions(f.pre, ex)) st = SKIP;
-          else st = cond::eval_conditions(f.deny, ex) ? FAIL : PASS;
-        } catch (const cond::EvalError&) {
-          st = f.pre.present ? ERROR : ERROR;
-        }
-        if (st == SKIP) continue;
-        if (st == ERROR) {
-          if (idx + 1 < elems.size()) continue;
-          return ERROR;
-        }
-        if (st == FAIL) return FAIL;
-        ++count;
-      }
-      apply_count += count;
+  for (auto& f : fes) {
+    JPtr lst;
+    try {
+      lst = cond::run_query(f.list, cx.root);  // EvaluateList
+    } catch (const cond::NotFound&) {
+      continue;  // "failed to evaluate list": the entry is skipped
+    } catch (const cond::EvalError&) {
+      continue;
     }
+    std::vector<JPtr> elems;
+    if (!cond::is_null(lst) && lst->t == JT::Arr) elems = lst->a;
+    else elems = {lst};
+    int count = 0;
+    for (size_t idx = 0; idx < elems.size(); ++idx) {
+      const JPtr& el = elems[idx];
+      if (cond::is_null(el)) continue;
+      const bool is_map = el->t == JT::Obj;
+      if (f.scope == 1 && !is_map) return ERROR;  // AddElementToContext error
+      const bool scope = f.scope == -1 ? is_map : f.scope == 1;
+      cond::Ctx ex{cond::with_element(cx.root, el, (int64_t)idx, nesting)};
+      const JPtr el_scoped = scope ? el : scoped;
+      Status st;
+      try {
+        if (f.pre.present && !cond::eval_conditions(f.pre, ex)) {
+          st = SKIP;
+        } else if (f.has_deny) {
+          st = cond::eval_conditions(f.deny, ex) ? FAIL : PASS;
+        } else if (f.pattern || f.any_pattern) {
+          st = pattern_handler(f.pattern, f.any_pattern, f.pattern_vars, el_scoped ? *el_scoped : res, &ex);
+        } else if (!f.nested.empty()) {
+          st = foreach_entries(f.nested, ex, el_scoped, res, nesting + 1);
+        } else {
+          st = NA;  // "invalid validation rule": nil response
+        }
+      } catch (const cond::EvalError&) {
+        st = ERROR;
+      }
+      if (st == UNSUPPORTED) return UNSUPPORTED;
+      if (st == NA || st == SKIP) continue;
+      if (st == ERROR) {
+        if (idx + 1 < elems.size()) continue;
+        return ERROR;
+      }
+      if (st == FAIL) return FAIL;
+      ++count;
+    }
+    apply_count += count;
+  }
+  return apply_count == 0 ? NA : PASS;
+}
+inline Status foreach_handler(const Rule& r, const cond::Ctx& cx, const JVal& res) {
+  try {
+    return foreach_entries(r.foreach, cx, nullptr, res, 0);
   } catch (const cond::Unsupported&) {
     return UNSUPPORTED;
   }
-  return apply_count == 0 ? NA : PASS;
 }
 
 // validate_pss.go:31-112 (no exceptions, CREATE operation)
@@ -1179,7 +1269,8 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
     if (r.unsupported) {
       s = UNSUPPORTED;
     } else {
-      if ((r.pre.present || r.has_deny || !r.foreach.empty()) && !cx.root) cx.root = cond::request_context(res);
+      if ((r.pre.present || r.has_deny || !r.foreach.empty() || r.pattern_vars) && !cx.root)
+        cx.root = cond::request_context(res);
       s = NA;
       bool done = false;
       if (r.pre.present) {  // engine.go:278-286: error => ERROR, false => SKIP
@@ -1208,8 +1299,8 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
       if (!done) {
         if (r.has_pss) s = pss_handler(r, res, u.kind());
         else if (r.has_deny) s = deny_handler(r, cx);
-        else if (r.pattern || r.any_pattern) s = pattern_handler(r, res);
-        else if (!r.foreach.empty()) s = foreach_handler(r, cx);
+        else if (r.pattern || r.any_pattern) s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx);
+        else if (!r.foreach.empty()) s = foreach_handler(r, cx, res);
       }
     }
     out[i] = s;

@@ -18,6 +18,7 @@
 
 #define __device__
 #define __forceinline__ inline
+#define KPE_PATVM_CHECK 1  // pattern VM table reads bounds-flagged (foreach pattern entries)
 struct uint2 {
   uint32_t x, y;
 };
@@ -25,6 +26,7 @@ struct uint4 {
   uint32_t x, y, z, w;
 };
 using std::trunc;
+inline uint2 make_uint2(uint32_t x, uint32_t y) { return uint2{x, y}; }
 
 #include "../kyverno_amd/csrc/corpus.hpp"
 #include "../kyverno_amd/csrc/kernels_abi.h"
@@ -63,6 +65,7 @@ int main(int argc, char** argv) {
   const uint32_t R = (uint32_t)P->rules.size();
   if (seed.size() != (size_t)C.n * R) return fprintf(stderr, "seed size %zu != %lld x %u\n", seed.size(), (long long)C.n, R), 1;
   std::vector<uint8_t> verdicts(seed.begin(), seed.end());
+  verdicts.resize(verdicts.size() + 8, 0);  // the pattern pass reads whole words
   std::vector<uint32_t> fk(CP.fields.size());
   for (size_t i = 0; i < fk.size(); ++i) {
     const int64_t id = C.dict[D_KEY].find(CP.fields[i]);
@@ -94,10 +97,60 @@ int main(int argc, char** argv) {
   pb.push_back(0);
   a.leaves = P->pat.leaves.data(), a.pconds = P->pat.conds.data(), a.pats = pp.data(), a.pat_bytes = pb.data();
   a.verdicts = verdicts.data();
+  // the pattern program as kpe_api.cpp binds it (members: names -> D_KEY ids, glob bitsets), for
+  // foreach pattern entries and the pattern pass after the condition pass
+  const auto& PP = P->pat;
+  std::vector<uint32_t> pbuf;
+  std::vector<uint4> mem(PP.members.size() / 4);
+  const auto& K = C.dict[D_KEY];
+  for (size_t i = 0; i < mem.size(); ++i) {
+    uint4 m{PP.members[4 * i], PP.members[4 * i + 1], PP.members[4 * i + 2], PP.members[4 * i + 3]};
+    const int64_t id = K.find(PP.keys[m.y]);
+    m.y = id < 0 ? 0u : (uint32_t)id + 1u;
+    if (m.x & PMF_GLOB) {
+      const auto& pr = P->preds[m.w];
+      m.w = (uint32_t)pbuf.size();
+      pbuf.resize(pbuf.size() + (K.size() + 31) / 32 + 1, 0u);
+      for (uint32_t s = 0; s < K.size(); ++s) {
+        const auto str = K.at(s);
+        bool hit = false;
+        for (auto& g : pr.globs)
+          hit = hit || glob(reinterpret_cast<const uint8_t*>(g.data()), (int)g.size(),
+                            reinterpret_cast<const uint8_t*>(str.data()), (int)str.size());
+        if (hit) pbuf[m.w + (s >> 5)] |= 1u << (s & 31u);
+      }
+    }
+    mem[i] = m;
+  }
+  pbuf.push_back(0);
+  std::vector<uint2> pvals((size_t)C.n * PP.vars.size() + 1);
+  std::vector<uint2> tp(PP.tpieces.size() / 2 + 1);
+  for (size_t i = 0; i + 1 < PP.tpieces.size(); i += 2) tp[i / 2] = uint2{PP.tpieces[i], PP.tpieces[i + 1]};
+  std::vector<uint8_t> tt(PP.ttext.begin(), PP.ttext.end());
+  tt.push_back(0);
+  std::vector<uint32_t> col2pr(R + 4, 0u);
+  for (size_t i = 0; i < PP.rules.size(); ++i) col2pr[PP.rules[i].col] = (uint32_t)i + 1u;
+  uint32_t perr = 0;
+  PatArgs pa{};
+  pa.n = C.n, pa.R = R, pa.npr = (uint32_t)PP.rules.size();
+  pa.doc = C.doc.data(), pa.doc_off = C.doc_off.data(), pa.scal = C.scal.data(), pa.scal_text = text.data();
+  pa.nodes = PP.nodes.data(), pa.members = mem.data(), pa.lists = PP.lists.data(), pa.leaves = PP.leaves.data();
+  pa.conds = PP.conds.data(), pa.pats = pp.data(), pa.pat_bytes = pb.data(), pa.roots = PP.roots.data();
+  pa.rules = PP.rules.data(), pa.col2pr = col2pr.data(), pa.pbuf = pbuf.data(), pa.verdicts = verdicts.data();
+  pa.pvals = pvals.data(), pa.nvars = (uint32_t)PP.vars.size(), pa.ptmpl = tp.data(), pa.ttext = tt.data();
+  pa.ctab = CP.consts.data(), pa.ctext = ctext.data();
+  pa.nnodes = (uint32_t)PP.nodes.size(), pa.nmembers = (uint32_t)mem.size(), pa.nlists = (uint32_t)PP.lists.size();
+  pa.nleaves = (uint32_t)PP.leaves.size(), pa.nconds = (uint32_t)PP.conds.size(), pa.npats = (uint32_t)pp.size();
+  pa.nroots = (uint32_t)PP.roots.size(), pa.npbuf = (uint32_t)pbuf.size(), pa.nscal = C.scal.size();
+  pa.ndoc = C.doc.size() / 2, pa.err = &perr;
+  a.pat = &pa, a.pvars = PP.vars.data(), a.pvals = pvals.data(), a.nvars = (uint32_t)PP.vars.size();
   char nb[2][16];
-  for (int64_t r = 0; r < a.n; ++r) cond_eval_row(a, r, nb);  // kpe_cond_kernel's lane body
+  for (int64_t r = 0; r < a.n; ++r) cond_eval_row<true>(a, r, nb);  // kpe_cond_kernel's lane body
+  if (!PP.rules.empty())
+    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(pa, r);  // then kpe_pattern_kernel's
+  if (perr) return fprintf(stderr, "pattern VM bounds flags 0x%x\n", perr), 1;
   FILE* f = fopen(argv[4], "wb");
-  fwrite(verdicts.data(), 1, verdicts.size(), f);
+  fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
   printf("%lld %u\n", (long long)C.n, R);
   return 0;

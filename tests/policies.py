@@ -316,3 +316,61 @@ def cond_policy_set():
     ]
     return [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "cond"},
              "spec": {"background": True, "validationFailureAction": "Audit", "rules": rules}}]
+
+
+def var_policy_set():
+    """Pattern rules with {{ }} variables (substitutePatterns, validate_resource.go:456-476) and
+    foreach entries with pattern / anyPattern / nested foreach bodies (validate_resource.go:
+    186-254), over the synth_resources mixes (kinds Pod, autogen controllers)."""
+    def rule(name, validate, pre=None):
+        r = {"name": name, "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
+             "validate": dict(validate, message="m")}
+        if pre is not None:
+            r["preconditions"] = pre
+        return r
+    ctr = "request.object.spec.containers"
+    rules = [
+        # whole-string variables keep the JSON type: strings, numbers, a missing key (error)
+        rule("v-same-tier", {"pattern": {"metadata": {"labels": {"tier": "{{request.object.metadata.labels.tier}}"}}}}),
+        rule("v-app-owner", {"pattern": {"metadata": {"labels": {"app": "{{request.object.metadata.annotations.owner}}"}}}}),
+        rule("v-default", {"pattern": {"metadata": {"labels": {"tier": "{{request.object.metadata.labels.zone || 'backend'}}"}}}}),
+        rule("v-star", {"pattern": {"spec": {"volumes": "{{request.object.metadata.labels.star || '*'}}"}}}),
+        rule("v-number", {"pattern": {"spec": {"containers": [{"name": "c-{{request.object.spec.containers[0].ports[0].containerPort || `0`}}*"}]}}}),
+        rule("v-idx", {"pattern": {"spec": {"containers": [{"image": "*{{request.object.metadata.labels.tier}}*"}]}}}),
+        rule("v-tmpl-name", {"pattern": {"metadata": {"name": "res-{{request.object.spec.containers[0].name}}"}}}),
+        rule("v-anchor", {"pattern": {"metadata": {"=(labels)": {"=(tier)": "{{request.object.metadata.labels.tier}}"},
+                                                   "name": "{{request.object.metadata.name}}"}}}),
+        rule("v-any", {"anyPattern": [{"metadata": {"labels": {"app": "{{request.object.metadata.labels.tier}}"}}},
+                                      {"metadata": {"namespace": "{{request.object.metadata.namespace}}"}}]}),
+        rule("v-pre", {"pattern": {"spec": {"containers": [{"name": "{{request.object.spec.containers[0].name}}"}]}}},
+             pre={"all": [{"key": "{{request.object.metadata.labels.tier}}", "operator": "Equals", "value": "backend"}]}),
+        rule("v-map", {"pattern": {"spec": {"securityContext": "{{request.object.spec.securityContext}}"}}}),
+        # foreach entries
+        rule("fe-pat", {"foreach": [{"list": ctr, "pattern": {"securityContext": {"=(privileged)": False}}}]}),
+        rule("fe-pat-var", {"foreach": [{"list": ctr, "pattern": {"name": "c-{{elementIndex}}"}}]}),
+        rule("fe-pat-el", {"foreach": [{"list": ctr, "pattern": {"image": "{{element.name}}*"}}]}),
+        rule("fe-any", {"foreach": [{"list": ctr, "anyPattern": [{"image": "*:latest"}, {"name": "init-*"}]}]}),
+        rule("fe-pre", {"foreach": [{"list": ctr, "preconditions": {"any": [{"key": "{{element.image}}", "operator": "Equals",
+                                                                             "value": "*:latest"}]},
+                                      "pattern": {"securityContext": {"runAsNonRoot": True}}}]}),
+        rule("fe-nested", {"foreach": [{"list": ctr, "foreach": [{"list": "element.ports",
+                                                                   "pattern": {"containerPort": "<9000"}}]}]}),
+        rule("fe-nested-el0", {"foreach": [{"list": ctr, "foreach": [{"list": "element.securityContext.capabilities.drop",
+                                                                       "deny": {"conditions": {"any": [
+                                                                           {"key": "{{element0.name}}", "operator": "Equals",
+                                                                            "value": "c-0"}]}}}]}]}),
+        rule("fe-unscoped", {"foreach": [{"list": "request.object.metadata.labels.tier", "elementScope": False,
+                                          "pattern": {"metadata": {"labels": {"tier": "{{element}}"}}}}]}),
+        rule("fe-scope-bad", {"foreach": [{"list": "request.object.metadata.labels.app", "elementScope": True,
+                                           "pattern": {"x": "y"}}]}),
+        rule("fe-two", {"foreach": [{"list": "request.object.spec.initContainers", "pattern": {"image": "*:1.*"}},
+                                    {"list": ctr, "pattern": {"image": "!*:latest"}}]}),
+        rule("fe-none", {"foreach": [{"list": ctr}]}),
+    ]
+    return [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "vars"},
+             "spec": {"validationFailureAction": "Audit", "background": True, "rules": rules}}]
+
+
+# rules of var_policy_set whose cells the device may leave KPE_UNDECIDED (a variable resolving
+# to a map is a pattern subtree; documented device limit)
+VAR_UNDECIDED_OK = {"v-map"}

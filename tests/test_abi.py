@@ -59,8 +59,8 @@ def test_compile_unsupported_is_loud():
     with pytest.raises(KpeError) as e:
         K.PolicySet([pol])
     assert e.value.status == 2  # KPE_E_UNSUPPORTED
-    # pattern variables need JMESPath substitution: refused too
-    pol["spec"]["rules"][0]["validate"] = {"pattern": {"metadata": {"name": "{{ request.object.kind }}"}}}
+    # pattern variables whose query is outside the subset: refused too
+    pol["spec"]["rules"][0]["validate"] = {"pattern": {"metadata": {"name": "{{ to_upper(request.object.kind) }}"}}}
     with pytest.raises(KpeError) as e:
         K.PolicySet([pol])
     assert e.value.status == 2

@@ -55,9 +55,10 @@ def test_outside_subset_refused(cond):
     assert e.value.status == 2
 
 
-def test_foreach_pattern_entries_refused():
+def test_foreach_context_entries_refused():
     r = {"name": "r", "match": {"any": [{"resources": {"kinds": ["Pod"]}}]},
-         "validate": {"foreach": [{"list": "request.object.spec.containers", "pattern": {"name": "*"}}]}}
+         "validate": {"foreach": [{"list": "request.object.spec.containers", "context": [{"name": "x", "variable": {
+             "value": 1}}], "pattern": {"name": "*"}}]}}
     with pytest.raises(K.KpeError):
         K.PolicySet([_pol(r)])
 
