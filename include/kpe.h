@@ -131,6 +131,10 @@ uint64_t kpe_corpus_digest(const kpe_corpus* c);
 #define KPE_ROW_DECODE_ERROR 1u
 #define KPE_ROW_LIMIT 2u
 #define KPE_ROW_NO_SPEC 4u
+/* KPE_ROW_CONTEXT_ERROR: NewPolicyContext fails for the resource (AddImageInfos: an invalid image
+ * reference or container entry, policycontext/policy_context.go:230), so the reference engine
+ * gives no response for any rule and the scanner records an error; every cell is KPE_UNDECIDED. */
+#define KPE_ROW_CONTEXT_ERROR 8u
 kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out);
 /* Resource hash of incremental background scans: CalculateResourceHash
  * (pkg/utils/report/metadata.go:137-155), md5 of json.Marshal([labels, annotations, the object

@@ -41,6 +41,7 @@ struct CondVM {
   const CondArgs& a;
   const uint2* doc;
   uint32_t root;
+  uint32_t img;  // the row's images map entry (kNoNode: no images in the context)
   CV buf[kCvBufs][CV_LIST_CAP];
   uint32_t blen[kCvBufs];
   int dep;                     // foreach nesting level of the current element (-1: none)
@@ -246,6 +247,14 @@ struct CondVM {
       }
       switch (op) {
         case QO_OBJ: cur = node(root); break;
+        case QO_IMG:
+          if (img == kNoNode) {  // no images: the context has no `images` key
+            if (strict) return CS_NOTFOUND;
+            cur = cv(VK_NULL, 0);
+          } else {
+            cur = node(img);
+          }
+          break;
         case QO_EL:
         case QO_IDX: {  // element<n> / elementIndex<n> (n = innermost by default) of the foreach levels
           const int lv = o.y == 0xFFFFFFFFu ? dep : (int)o.y;
@@ -278,6 +287,19 @@ struct CondVM {
             cur = cv(VK_LIST, fb);
           } else {
             keys_pending = true;  // fused with the `[]` that follows (compile-time check)
+          }
+          break;
+        case QO_VALS:  // (compile time: never inside a projection)
+          if (type(cur) != JT_OBJ) {
+            mode = 2;
+            break;
+          } else {
+            const uint32_t fb = free_buf();
+            blen[fb] = 0;
+            const uint32_t b = doc[cur.p].y, c0 = b + 1u, end = c0 + doc[b].x;
+            for (uint32_t c = c0; c < end; ++c)
+              if (push(fb, node(c))) return CS_UNDEC;
+            lb = fb, mode = 1;
           }
           break;
         case QO_FLAT:
@@ -1072,7 +1094,6 @@ struct FeFrame {
 };
 // A resolved pattern variable (kpe_pattern_kernel reads it): 0 ok, else the cell's verdict
 __device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, uint2* dst) {
-  const CondArgs& a = vm.a;
   const uint32_t t = vm.type(x);
   if (t == JT_NULL) {
     *dst = make_uint2(PVK_NULL, 0u);
@@ -1103,7 +1124,9 @@ __device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, u
 
 template <bool FEPAT>
 __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16]) {
-  CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], {}, {}, -1, {}, {}, nb};
+  const uint64_t im = a.img_off ? a.img_off[r] : ~0ull;
+  CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], im == ~0ull ? kNoNode : (uint32_t)im,
+            {}, {}, -1, {}, {}, nb};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   uint2* pvrow = a.pvals ? a.pvals + (size_t)r * a.nvars : nullptr;
   for (uint32_t i = 0; i < a.ncr; ++i) {

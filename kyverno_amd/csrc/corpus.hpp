@@ -10,6 +10,8 @@
 
 namespace kpe {
 
+constexpr uint64_t KPE_NO_IMAGES = ~0ull;
+
 struct Dict {
   std::unordered_map<std::string, uint32_t> map;
   std::vector<char> bytes;
@@ -71,6 +73,8 @@ struct Corpus {
   bool has_docs = false;
   std::vector<uint32_t> doc;          // 2 words per entry (schema.h DN_*)
   std::vector<uint64_t> doc_off;      // root entry (absolute tape index) of each resource
+  std::vector<uint64_t> img_off;      // root entry of each resource's `images` context map, or
+                                      // KPE_NO_IMAGES (no images: the context has no `images`)
   std::vector<KpeScalar> scal;        // scalar table (ids 0/1/2 = null/false/true)
   std::vector<char> scal_text;        // compareString texts
   std::unordered_map<std::string, uint32_t> scal_str;

@@ -23,6 +23,7 @@
 
 #include "corpus.hpp"
 #include "goval.hpp"
+#include "imageref.hpp"
 #include "jscan.hpp"
 #include "k8s_schema.hpp"
 #include "podview.hpp"
@@ -732,6 +733,21 @@ class Flattener {
   explicit Flattener(Corpus& c) : C(c) {}
   // typed_pod_view: walk one resource without emitting a row
   bool no_emit = false, last_err = false;
+  // without document tapes the images context is checked from the typed container images only
+  // (GetImageInfo validity per distinct image string); with tapes DocBuilder checks it exactly
+  bool check_images = false, bad_image = false;
+  std::vector<int8_t> img_ok_;  // per D_IMAGE id: -1 unknown, 0 invalid, 1 valid / blank
+  bool image_ok(uint32_t id) {
+    if (id >= img_ok_.size()) img_ok_.resize(id + 1, -1);
+    if (img_ok_[id] < 0) {
+      const std::string_view im = C.dict[D_IMAGE].at(id);
+      size_t a = 0;
+      while (a < im.size() && (im[a] == ' ' || (im[a] >= '\t' && im[a] <= '\r'))) ++a;
+      imageref::Info info;
+      img_ok_[id] = (a == im.size() || imageref::image_info(im, &info)) ? 1 : 0;
+    }
+    return img_ok_[id] == 1;
+  }
   uint32_t last_cls = R_CLASS_OTHER;
   const PodView& view() const { return pod; }
 
@@ -1118,6 +1134,7 @@ class Flattener {
         }
         C.c_name.push_back(C.dict[D_CNAME].intern(c.name));
         C.c_image.push_back(C.dict[D_IMAGE].intern(c.image));
+        if (check_images && !image_ok(C.c_image.back())) bad_image = true;
         uint32_t sann = KPE_NO_STR, sann_key = KPE_NO_STR;  // join: "container.seccomp...kubernetes.io/<name>"
         if (!pod.ann.empty()) {
           std::string key = seccomp_ctr_prefix + c.name;
@@ -1139,6 +1156,11 @@ class Flattener {
       }
     }
     C.ctr_off.push_back((uint32_t)C.c_sc.size());
+    if (bad_image && !limit) {  // NewPolicyContext's AddImageInfos fails: no response at all
+      C.r_flags.back() |= R_CTX_ERR;
+      C.limit_rows.push_back((uint32_t)C.n);
+    }
+    bad_image = false;
     C.rec.push_back(p | ((flags & R_CLASS_MASK) << PR_CLASS_SH) | (derr ? PR_DECODE_ERR : 0u));
     C.rec.push_back(C.r_gvk.back());
     C.rec.push_back((uint32_t)nctr | ((uint32_t)pod.vols.size() << 8) | ((uint32_t)pod.sysctls.size() << 16) |
@@ -1194,6 +1216,16 @@ class DocBuilder {
     }
     put(root);
     C.doc_off.push_back(C.doc.size() / 2 - 1);  // the resource's root entry
+    C.img_off.push_back(KPE_NO_IMAGES);
+    const uint32_t row = (uint32_t)(C.n - 1);
+    if (!(C.r_flags[row] & R_LIMIT) && DN_KIND((uint32_t)root) == DN_MAP) {
+      try {
+        images((uint32_t)(C.doc.size() / 2 - 1));
+      } catch (const ImageError&) {  // NewPolicyContext fails: no response for any rule
+        C.r_flags[row] |= R_CTX_ERR;
+        C.limit_rows.push_back(row);
+      }
+    }
   }
 
  private:
@@ -1282,6 +1314,127 @@ class DocBuilder {
     jc.ws();
     if (!jc.ok() || jc.pos() != v.data() + v.size()) return;
     e.flags |= SC_JVALID | (c == '[' ? SC_JARR : 0u);
+  }
+  // ---- the `images` context (context.go:306-348, pkg/utils/api/image.go:17-229) ----------
+  struct ImageError {};
+  uint32_t key1(const char* k) { return C.dict[D_KEY].intern(k) + 1u; }
+  uint64_t at(uint32_t e) const { return (uint64_t)C.doc[(size_t)e * 2] | ((uint64_t)C.doc[(size_t)e * 2 + 1] << 32); }
+  // member `k` of map entry e (the tape keeps the last of duplicate names), or ~0u
+  uint32_t member(uint32_t e, uint32_t k1) const {
+    const uint32_t b = C.doc[(size_t)e * 2 + 1], n = C.doc[(size_t)b * 2];
+    for (uint32_t i = 0; i < n; ++i)
+      if (DN_KEY(C.doc[(size_t)(b + 1 + i) * 2]) == k1) return b + 1 + i;
+    return ~0u;
+  }
+  bool is_null(uint32_t e) const {
+    const uint32_t x = C.doc[(size_t)e * 2];
+    return DN_KIND(x) == DN_SCALAR && C.doc[(size_t)e * 2 + 1] == SC_NULL_ID;
+  }
+  // a string scalar's text, or false
+  bool text(uint32_t e, std::string_view* out) const {
+    const uint32_t x = C.doc[(size_t)e * 2];
+    if (DN_KIND(x) != DN_SCALAR) return false;
+    const KpeScalar& sc = C.scal[C.doc[(size_t)e * 2 + 1]];
+    if (SC_TYPE(sc.flags) != SC_T_STR) return false;
+    *out = std::string_view(C.scal_text.data() + sc.text_off, sc.text_len);
+    return true;
+  }
+  void images(uint32_t root) {
+    // ExtractImagesFromResource: the standard extractors of the resource's kind
+    std::string_view kind;
+    const uint32_t ke = member(root, key1("kind"));
+    if (ke == ~0u || !text(ke, &kind)) return;
+    std::vector<const char*> prefix;
+    if (kind == "Pod") prefix = {"spec"};
+    else if (kind == "DaemonSet" || kind == "Deployment" || kind == "ReplicaSet" || kind == "ReplicationController" ||
+             kind == "StatefulSet" || kind == "Job")
+      prefix = {"spec", "template", "spec"};
+    else if (kind == "CronJob") prefix = {"spec", "jobTemplate", "spec", "template", "spec"};
+    else return;
+    uint32_t obj = root;
+    std::string path;
+    for (const char* f : prefix) {  // extract(): a nil value ends the walk, a non-map is an error
+      if (DN_KIND(C.doc[(size_t)obj * 2]) != DN_MAP) throw ImageError{};
+      const uint32_t c = member(obj, key1(f));
+      path += "/";
+      path += f;
+      if (c == ~0u || is_null(c)) return;
+      obj = c;
+    }
+    if (DN_KIND(C.doc[(size_t)obj * 2]) != DN_MAP) throw ImageError{};
+    struct One {
+      std::string name, pointer;
+      imageref::Info info;
+    };
+    std::vector<std::pair<std::string, std::vector<One>>> types;
+    for (const char* tag : {"containers", "ephemeralContainers", "initContainers"}) {  // JSON key order
+      const uint32_t lst = member(obj, key1(tag));
+      if (lst == ~0u || is_null(lst)) continue;
+      const uint32_t lx = C.doc[(size_t)lst * 2];
+      if (DN_KIND(lx) == DN_SCALAR) throw ImageError{};  // `*` over a scalar: "invalid type"
+      const uint32_t b = C.doc[(size_t)lst * 2 + 1], n = C.doc[(size_t)b * 2];
+      std::vector<One> got;
+      std::vector<std::pair<std::string, uint32_t>> elems;  // (path element, entry)
+      for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t e = b + 1 + i;
+        if (DN_KIND(lx) == DN_ARR) elems.push_back({std::to_string(i), e});
+        else elems.push_back({std::string(C.dict[D_KEY].at(DN_KEY(C.doc[(size_t)e * 2]) - 1)), e});
+      }
+      if (DN_KIND(lx) == DN_MAP) std::sort(elems.begin(), elems.end());  // Go map order: unpinned
+      for (auto& el : elems) {
+        const uint32_t e = el.second;
+        if (is_null(e)) continue;
+        if (DN_KIND(C.doc[(size_t)e * 2]) != DN_MAP) throw ImageError{};  // "invalid image config"
+        std::string_view nm, im;
+        const uint32_t ne = member(e, key1("name"));
+        if (ne == ~0u || !text(ne, &nm)) throw ImageError{};  // "invalid key"
+        const uint32_t ie = member(e, key1("image"));
+        if (ie == ~0u || !text(ie, &im)) continue;
+        size_t a = 0, z = im.size();
+        while (a < z && (im[a] == ' ' || (im[a] >= '\t' && im[a] <= '\r'))) ++a;
+        if (a == z) continue;  // strings.TrimSpace(value) == "": the image is not present
+        One o;
+        if (!imageref::image_info(im, &o.info)) throw ImageError{};  // "invalid image"
+        o.name.assign(nm);
+        o.pointer = path + "/" + tag + "/" + el.first + "/image";
+        got.push_back(std::move(o));
+      }
+      if (got.empty()) continue;
+      // a map keyed by container name (the last one wins), marshalled with sorted keys
+      std::stable_sort(got.begin(), got.end(), [](const One& x, const One& y) { return x.name < y.name; });
+      std::vector<One> uniq;
+      for (size_t q = 0; q < got.size(); ++q)
+        if (q + 1 == got.size() || got[q + 1].name != got[q].name) uniq.push_back(std::move(got[q]));
+      types.push_back({tag, std::move(uniq)});
+    }
+    if (types.empty()) return;
+    std::vector<uint64_t> tkids;
+    for (auto& t : types) {
+      std::vector<uint64_t> ckids;
+      for (auto& o : t.second) {
+        const imageref::Info& in = o.info;
+        const std::string base = (in.registry.empty() ? "" : in.registry + "/") + in.path;
+        const std::string reference = in.digest.empty() ? base + ":" + in.tag : base + "@" + in.digest;
+        const std::string rwt = base + ":" + in.tag;
+        std::vector<uint64_t> f;
+        auto put_str = [&](const char* k, const std::string& v, bool omitempty) {
+          if (omitempty && v.empty()) return;
+          f.push_back(entry(DN_SCALAR, key1(k), str_id(v)));
+        };
+        put_str("digest", in.digest, true);
+        put_str("jsonPointer", o.pointer, false);
+        put_str("name", in.name, false);
+        put_str("path", in.path, false);
+        put_str("reference", reference, true);
+        put_str("referenceWithTag", rwt, true);
+        put_str("registry", in.registry, true);
+        put_str("tag", in.tag, true);
+        ckids.push_back(entry(DN_MAP, C.dict[D_KEY].intern(o.name) + 1u, body(f)));
+      }
+      tkids.push_back(entry(DN_MAP, key1(t.first.c_str()), body(ckids)));
+    }
+    put(entry(DN_MAP, 0, body(tkids)));
+    C.img_off.back() = C.doc.size() / 2 - 1;
   }
   static uint64_t entry(uint32_t kind, uint32_t key1, uint32_t y) {
     return (uint64_t)(kind | (key1 << 2)) | ((uint64_t)y << 32);
@@ -1421,7 +1574,7 @@ int64_t Corpus::bytes() const {
   add(lab_off), add(lab_k), add(lab_v), add(ann_off), add(ann_k), add(ann_v);
   add(rec), add(hdr), add(crec), add(vol_src), add(sys_id), add(pann_kv), add(capset_add), add(capset_drop);
   add(c_sann);
-  add(doc), add(doc_off), add(scal), add(scal_text);
+  add(doc), add(doc_off), add(img_off), add(scal), add(scal_text);
   return b;
 }
 
@@ -1429,6 +1582,7 @@ namespace {
 
 void flatten_range(Corpus& C, const char* buf, size_t i, size_t len, bool docs) {
   Flattener fl(C);
+  fl.check_images = !docs;
   std::unique_ptr<DocBuilder> db;
   if (docs) db = std::make_unique<DocBuilder>(C), C.has_docs = true;
   while (i < len) {
@@ -1595,7 +1749,7 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
     v->resize(e.ctr);
   C.c_add.resize(e.ctr), C.c_drop.resize(e.ctr), C.crec.resize(e.ctr * 2), C.cport_off.resize(e.ctr + 1);
   C.cport_host.resize(e.port), C.cport_str.resize(e.port);
-  if (docs) C.doc.resize(e.doc * 2), C.doc_off.resize(e.n), C.has_docs = true;
+  if (docs) C.doc.resize(e.doc * 2), C.doc_off.resize(e.n), C.img_off.resize(e.n), C.has_docs = true;
   // ---- remap and place every part (parallel) ----
   auto place = [&](size_t t) {
     const Corpus& P = parts[t];
@@ -1652,10 +1806,12 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
       *oy = DN_KIND(x) == DN_SCALAR ? sm[y] : y + tb;
     };
     std::vector<uint32_t> stack;
-    for (size_t r = 0; r < (size_t)P.n; ++r) {  // walk every document from its root entry
+    for (size_t r = 0; r < (size_t)P.n; ++r) {  // walk every document (and images map) from its root entry
       const uint32_t root = (uint32_t)P.doc_off[r];
       C.doc_off[b.n + r] = tb + root;
       stack.assign(1, root);
+      C.img_off[b.n + r] = P.img_off[r] == KPE_NO_IMAGES ? KPE_NO_IMAGES : tb + P.img_off[r];
+      if (P.img_off[r] != KPE_NO_IMAGES) stack.push_back((uint32_t)P.img_off[r]);
       while (!stack.empty()) {
         const uint32_t en = stack.back();
         stack.pop_back();

@@ -206,6 +206,7 @@ struct CondArgs {
   uint32_t R, ncr;                 // rules per row, condition rules
   const uint32_t* doc;             // document tape (2 words per entry)
   const uint64_t* doc_off;         // root entry of each resource
+  const uint64_t* img_off;         // root entry of each resource's images map (KPE_NO_IMAGES: none)
   const uint32_t* perm;            // lane -> row (PatArgs::perm)
   const KpeScalar* scal;
   const uint8_t* scal_text;

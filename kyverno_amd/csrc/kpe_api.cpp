@@ -207,7 +207,7 @@ struct DeviceCorpus {
   DevBuf r_gvk, r_name, r_mns, r_nsa, ann_off, ann_k, ann_v;
   DevBuf lab_off, lab_k, lab_v, r_nsl, nsl_off, nsl_k, nsl_v;
   DevBuf rec, hdr, crec, vol_src, sys_id, pann_kv, c_sann, capsets;
-  DevBuf doc, doc_off, scal, scal_text;  // document tape + scalar table (pattern rules)
+  DevBuf doc, doc_off, img_off, scal, scal_text;  // document tape + scalar table (pattern rules)
   DevBuf doc_perm;  // rows by descending tape size: the pattern / condition kernels' lane -> row map
   DevBuf limit_rows;                     // rows past a per-resource limit
   // cold pod columns, uploaded on the first binding of a program with podSecurity exclusions
@@ -327,7 +327,8 @@ kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out) {
   for (int64_t i = 0; i < C.n; ++i) {
     const uint32_t f = C.r_flags[i];
     out[i] = ((f & R_DECODE_ERR) ? KPE_ROW_DECODE_ERROR : 0u) | ((f & R_LIMIT) ? KPE_ROW_LIMIT : 0u) |
-             ((f & R_CLASS_MASK) == R_CLASS_OTHER ? KPE_ROW_NO_SPEC : 0u);
+             ((f & R_CLASS_MASK) == R_CLASS_OTHER ? KPE_ROW_NO_SPEC : 0u) |
+             ((f & R_CTX_ERR) ? KPE_ROW_CONTEXT_ERROR : 0u);
   }
   return KPE_OK;
 }
@@ -404,6 +405,7 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   if (C.has_docs) {
     HIPCHK(upload(D.doc, C.doc, s));
     HIPCHK(upload(D.doc_off, C.doc_off, s));
+    HIPCHK(upload(D.img_off, C.img_off, s));
     {  // Lanes of a wave take rows of one kind (the rules a row matches, so the rule loop's VM runs
       // are shared by the whole wave, not by the lanes of one kind among mixed Pods and
       // Deployments) and, within a kind, of similar tape size, heaviest first (a document walk's
@@ -1174,6 +1176,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.ncr = (uint32_t)P.cond.rules.size();
       ca.doc = D.doc.as<uint32_t>();
       ca.doc_off = D.doc_off.as<uint64_t>();
+      ca.img_off = C.img_off.empty() ? nullptr : D.img_off.as<uint64_t>();
       ca.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();
       ca.scal = D.scal.as<KpeScalar>();
       ca.scal_text = D.scal_text.as<uint8_t>();

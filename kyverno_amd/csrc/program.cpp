@@ -1355,6 +1355,8 @@ class QueryParser {
       if (peek().s == "object") op(o, QO_OBJ);
       else op(o, QO_CONST, K.scalar(JV::str("CREATE")));  // background scans / CLI: CREATE
       i_ += 2;
+    } else if (r == "images") {
+      op(o, QO_IMG);  // AddImageInfos (context.go:306-348), built by the flattener
     } else if (r == "element" || r == "elementIndex") {
       op(o, r == "element" ? QO_EL : QO_IDX, 0xFFFFFFFFu);  // the innermost foreach element
     } else if ((r.size() == 8 && !r.compare(0, 7, "element") && r[7] >= '0' && r[7] < '0' + KPE_FE_DEPTH) ||
@@ -1388,6 +1390,14 @@ class QueryParser {
         *plain = false;
         proj = true, keys_open = false;
         ++i_;
+      } else if (t.t == T_DOT && peek().t == T_STAR) {
+        // `.*` value projection over an object (go-jmespath ASTValueProjection); nested in
+        // another projection it would produce lists per element: not on the device
+        if (proj) throw CompileError("`.*` inside a projection is not supported on the device");
+        op(o, QO_VALS);
+        *plain = false;
+        proj = true;
+        i_ += 2;
       } else if (t.t == T_LBRACK && peek().t == T_STAR && peek(2).t == T_RBRACK) {
         op(o, QO_STAR);
         *plain = false;

@@ -44,6 +44,8 @@ enum KpeDomain {
 #define R_ANNOT_NIL (1u << 5)
 #define R_LIMIT (1u << 6)       // a per-resource encoding limit (e.g. > 255 containers): every cell of
                                 // the row is KPE_UNDECIDED_ (Corpus::limit_rows)
+#define R_CTX_ERR (1u << 7)     // NewPolicyContext fails (AddImageInfos: an invalid image or container
+                                // entry): the reference gives no response; every cell KPE_UNDECIDED_
 
 // r_gvk = kind_id | version_id << 12 | group_id << 22
 #define GVK_KIND(x) ((x) & 0xFFFu)
@@ -591,6 +593,9 @@ typedef struct KpePatRule {
                       // QO_ITEM (QO_ARG = its op count) followed by a relative field / index chain
 #define QO_ITEM 10u
 #define QO_ERROR 11u  // the expression is empty: every evaluation is an error (RuleError)
+#define QO_VALS 13u   // `.*`: the member values of an object, then projected like `[*]`
+#define QO_IMG 12u    // images: the resource's images context map (context.go:306-348), absent
+                      // when the resource has no images
 #define QO_OP(x) ((x) & 0xFFu)
 #define QO_ARG(x) ((x) >> 8)
 typedef struct KpeCExpr {

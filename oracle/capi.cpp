@@ -391,4 +391,43 @@ int oracle_condition(const char* key_json, const char* op, const char* value_jso
   }
 }
 
+// GetImageInfo with the default configuration: 0 and the info as JSON in buf, 1 an error
+int oracle_image_info(const char* image, char* buf, size_t cap) {
+  try {
+    img::Info in = img::get_image_info(image);
+    JVal o;
+    o.t = JT::Obj;
+    for (auto& kv : {std::pair<const char*, std::string*>{"registry", &in.registry}, {"name", &in.name},
+                     {"path", &in.path}, {"tag", &in.tag}, {"digest", &in.digest}, {"reference", &in.reference},
+                     {"referenceWithTag", &in.reference_with_tag}})
+      o.o.push_back({kv.first, cond::mk_str(*kv.second)});
+    std::string out;
+    json_write(o, out);
+    snprintf(buf, cap, "%s", out.c_str());
+    return 0;
+  } catch (const img::ImageError& e) {
+    g_err = e.msg;
+    return 1;
+  }
+}
+// The `images` context of a resource as JSON ("null" when absent); 1 when extraction fails
+int oracle_images_context(const char* resource_json, char* buf, size_t cap) {
+  try {
+    JPtr r = parse_json(resource_json);
+    JPtr ctx = cond::request_context(*r);
+    img::extract_images(*r);  // throws on an extraction error
+    const JVal* im = ctx->get("images");
+    std::string out = "null";
+    if (im) out.clear(), json_write(*im, out);
+    snprintf(buf, cap, "%s", out.c_str());
+    return 0;
+  } catch (const img::ImageError& e) {
+    g_err = e.msg;
+    return 1;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
 }  // extern "C"

@@ -31,6 +31,7 @@
 #include <string>
 #include <vector>
 
+#include "image.hpp"
 #include "json_dom.hpp"
 #include "pattern.hpp"
 #include "wildcard.hpp"
@@ -773,7 +774,7 @@ inline void check_roots(const Node& n) {
   std::vector<std::string> r;
   root_reads(n, r);
   for (auto& x : r)
-    if (x != "request.object" && x != "request.operation" && x != "element" && x != "elementIndex" &&
+    if (x != "request.object" && x != "request.operation" && x != "element" && x != "elementIndex" && x != "images" &&
         !(x.size() == 8 && x.compare(0, 7, "element") == 0 && x[7] >= '0' && x[7] <= '3') &&
         !(x.size() == 13 && x.compare(0, 12, "elementIndex") == 0 && x[12] >= '0' && x[12] <= '3'))
       throw Unsupported("context value " + x);
@@ -1498,6 +1499,8 @@ inline void precompile(const Conditions& c) {
   }
 }
 // The background-scan / CLI JSON context: {"request": {"operation": "CREATE", "object": res}}
+// and, when the resource has images, "images" (context.go:306-348 AddImageInfos: per container
+// type, per container name, the ImageInfo fields with omitempty, and jsonPointer)
 inline JPtr request_context(const JVal& res) {
   auto req = std::make_shared<JVal>();
   req->t = JT::Obj;
@@ -1506,6 +1509,39 @@ inline JPtr request_context(const JVal& res) {
   auto root = std::make_shared<JVal>();
   root->t = JT::Obj;
   root->o.push_back({"request", req});
+  std::vector<img::Extracted> ims;
+  try {
+    ims = img::extract_images(res);
+  } catch (const img::ImageError&) {  // the caller treats the resource as not evaluable
+  }
+  if (!ims.empty()) {
+    auto all = std::make_shared<JVal>();
+    all->t = JT::Obj;
+    std::sort(ims.begin(), ims.end(), [](const img::Extracted& a, const img::Extracted& b) { return a.type < b.type; });
+    for (auto& ex : ims) {
+      auto per = std::make_shared<JVal>();
+      per->t = JT::Obj;
+      for (auto& kv : ex.infos) {
+        const img::Info& in = kv.second;
+        auto o = std::make_shared<JVal>();
+        o->t = JT::Obj;
+        auto put = [&](const char* k, const std::string& v, bool omitempty) {
+          if (!omitempty || !v.empty()) o->o.push_back({k, mk_str(v)});
+        };
+        put("digest", in.digest, true);
+        put("jsonPointer", in.pointer, false);
+        put("name", in.name, false);
+        put("path", in.path, false);
+        put("reference", in.reference, true);
+        put("referenceWithTag", in.reference_with_tag, true);
+        put("registry", in.registry, true);
+        put("tag", in.tag, true);
+        per->o.push_back({kv.first, o});
+      }
+      all->o.push_back({ex.type, per});
+    }
+    root->o.push_back({"images", all});
+  }
   return root;
 }
 // context.AddElement (context.go:280-290): element, element<nesting>, elementIndex,

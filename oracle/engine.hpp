@@ -1253,6 +1253,12 @@ inline void attach_exceptions(Policy& p, const std::vector<PolicyException>& xs,
 // engine.go:87-101 + validation.go:16-80. out[i] = status of computed rule i.
 inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, std::vector<uint8_t>& out) {
   out.assign(p.rules.size(), NA);
+  try {  // NewPolicyContext -> AddImageInfos (policy_context.go:230): an error means no response at all
+    img::extract_images(res);
+  } catch (const img::ImageError&) {
+    out.assign(p.rules.size(), UNSUPPORTED);
+    return;
+  }
   Unstructured u{&res};
   if (p.namespaced) {  // internal/match.go:54-67
     std::string rns = u.ns();

@@ -79,6 +79,7 @@ int main(int argc, char** argv) {
   CondArgs a{};
   a.n = C.n, a.R = R, a.ncr = (uint32_t)CP.rules.size();
   a.doc = C.doc.data(), a.doc_off = C.doc_off.data(), a.scal = C.scal.data(), a.scal_text = text.data();
+  a.img_off = C.img_off.empty() ? nullptr : C.img_off.data();
   a.key_bytes = kb.data(), a.key_off = C.dict[D_KEY].off.data();
   a.ops = ops.data(), a.exprs = CP.exprs.data(), a.tmpls = CP.tmpls.data(), a.conds = CP.conds.data();
   a.blocks = CP.blocks.data(), a.fes = CP.fes.data(), a.rules = CP.rules.data();

@@ -30,6 +30,10 @@ outputs) lifted from the reference's tests:
                               with the chart defaults (ClusterPolicy, Audit, background, every
                               `if`/`with` false except the file guard, `else` branches taken,
                               backtick-escaped JMESPath kept verbatim)
+  image_cases.json         <- pkg/utils/image/infos_test.go (GetImageInfo with the default
+                              configuration: docker.io, registry mutation on) and
+                              pkg/utils/api/image_test.go Test_extractImageInfo (resource ->
+                              images map) for the `images` context
   condition_cases.json     <- pkg/engine/variables/evaluate_test.go TestEvaluate (constant key,
                               operator, value -> Evaluate result; ToJSON literals as JSON)
   match_rd_cases.json      <- pkg/engine/utils/utils_test.go:1828-2460, hand-transcribed below
@@ -588,7 +592,54 @@ def condition_cases():
     return out
 
 
+def image_cases():
+    """GetImageInfo / ExtractImagesFromResource expectations (default config only)."""
+    src = open(os.path.join(REF, "pkg/utils/image/infos_test.go")).read()
+    infos = []
+    for m in re.finditer(r'validateImageInfo\(t,\s*"([^"]*)",\s*"([^"]*)",\s*"([^"]*)",\s*"([^"]*)",\s*"([^"]*)",'
+                         r'\s*"([^"]*)",\s*"([^"]*)",\s*"([^"]*)",\s*(true|false)\)', src):
+        raw, name, path, reg, tag, dig, string, defreg, mut = m.groups()
+        if defreg == "docker.io" and mut == "true":
+            infos.append({"image": raw, "name": name, "path": path, "registry": reg, "tag": tag, "digest": dig,
+                          "string": string})
+    refs = []
+    for m in re.finditer(r'input:\s*"([^"]*)",\s*expectedReference:\s*"([^"]*)",\s*expectedReferenceWithTag:\s*"([^"]*)"', src):
+        refs.append({"image": m.group(1), "reference": m.group(2), "referenceWithTag": m.group(3)})
+    errs = re.search(r"func Test_ParseError.*?testCases := \[\]string\{(.*?)\}", src, re.S).group(1)
+    errors = re.findall(r'"([^"]*)"', errs)
+    src2 = open(os.path.join(REF, "pkg/utils/api/image_test.go")).read()
+    body = src2[src2.index("func Test_extractImageInfo"):]
+    body = body[:body.index("\nfunc ")] if "\nfunc " in body else body
+    extract = []
+    parts = body.split("raw: []byte(`")[1:]
+    for part in parts:
+        raw = part[:part.index("`)")]
+        if "extractionConfig" in part[:part.index("`)")]:
+            continue
+        rest = part[part.index("`)"):]
+        # the case ends at the next raw (already split); skip cases with a custom extraction config
+        images = {}
+        for tm in re.finditer(r'"(initContainers|containers|ephemeralContainers|custom)":\s*\{', rest):
+            seg = rest[tm.end():]
+            for em in re.finditer(r'"([^"]+)":\s*\{\s*imageutils\.ImageInfo\{(.*?)\},\s*"([^"]*)",\s*\}', seg, re.S):
+                # stop at the next container-type section
+                nxt = re.search(r'"(initContainers|containers|ephemeralContainers|custom)":\s*\{', seg)
+                if nxt and nxt.start() < em.start():
+                    break
+                fields = dict(re.findall(r'(\w+):\s*"([^"]*)"', em.group(2)))
+                images.setdefault(tm.group(1), {})[em.group(1)] = {**fields, "Pointer": em.group(3)}
+        if not images or "custom" in images:
+            continue  # a case of a custom extraction config (kyvernov1.ImageExtractorConfigs)
+        try:
+            extract.append({"raw": json.loads(raw), "images": images})
+        except ValueError:
+            pass
+    print(f"image_cases: {len(infos)} infos, {len(refs)} references, {len(errors)} errors, {len(extract)} extractions")
+    return {"infos": infos, "references": refs, "errors": errors, "extract": extract}
+
+
 if __name__ == "__main__":
+    _dump("image_cases.json", image_cases())
     _dump("condition_cases.json", condition_cases())
     _dump("best_practices.json", best_practices())
     _dump("chart_policies.json", chart_policies())

@@ -42,6 +42,8 @@ class Oracle:
         L.oracle_validate_element.argtypes = [cp, cp, ctypes.c_int, ctypes.c_int, cp, ctypes.c_size_t]
         L.oracle_match_pattern.argtypes = [cp, cp, ctypes.c_int, cp, ctypes.c_size_t]
         L.oracle_condition.argtypes = [cp, cp, cp]
+        L.oracle_image_info.argtypes = [cp, cp, ctypes.c_size_t]
+        L.oracle_images_context.argtypes = [cp, cp, ctypes.c_size_t]
 
     def wildcard(self, pattern, text):
         return bool(self.lib.oracle_wildcard_match(pattern.encode(), text.encode()))
@@ -141,6 +143,22 @@ class Oracle:
         """variables.Evaluate of one constant condition: True / False, 'error' or 'unsupported'."""
         r = self.lib.oracle_condition(key_json.encode(), op.encode(), value_json.encode())
         return {1: True, 0: False, -1: "error"}.get(r, "unsupported")
+
+
+    def image_info(self, image):
+        """GetImageInfo (default configuration): a dict, or None on a parse error."""
+        buf = ctypes.create_string_buffer(8192)
+        r = self.lib.oracle_image_info(image.encode(), buf, 8192)
+        return json.loads(buf.value.decode()) if r == 0 else None
+
+    def images_context(self, resource):
+        """The `images` context map of a resource (None: absent); 'error' when extraction fails."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        r = self.lib.oracle_images_context(json.dumps(resource).encode(), buf, 1 << 16)
+        if r == 1:
+            return "error"
+        self._chk(r)
+        return json.loads(buf.value.decode())
 
 
 def build():

@@ -43,7 +43,8 @@ def test_condition_set_compiles(oracle):
 @pytest.mark.parametrize("cond", [
     {"key": "{{ request.object.metadata.name }}-x", "operator": "Equals", "value": "a"},       # partial variable
     {"key": "{{ request.object.metadata.labels | keys(@) }}", "operator": "Equals", "value": []},  # pipe
-    {"key": "{{ images.containers.*.registry }}", "operator": "AnyIn", "value": ["x"]},        # context value
+    {"key": "{{ request.userInfo.username }}", "operator": "AnyIn", "value": ["x"]},          # context value
+    {"key": "{{ request.object.spec.containers[*].* }}", "operator": "AnyIn", "value": ["x"]},  # nested `.*`
     {"key": "{{ request.object.spec.containers[?name == 'a'] }}", "operator": "Equals", "value": []},  # filter
     {"key": "{{ length(request.object.spec.containers) }}", "operator": "Equals", "value": 1},  # function
     {"key": "$(./name)", "operator": "Equals", "value": "a"},                                  # reference

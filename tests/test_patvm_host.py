@@ -58,6 +58,8 @@ def test_patvm_host_matches_oracle(harness, oracle, tmp_path, name, pols, nd):
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
     ref = oracle.validate(pols, nd)
     v = np.fromfile(vb, dtype=np.uint8).reshape(ref.shape)
-    applied = ref != 0  # the harness resolves every pattern cell as if its rule matched
+    # the harness resolves every pattern cell as if its rule matched; rows whose policy context
+    # fails (images, KPE_ROW_CONTEXT_ERROR: every oracle cell 7) are not the pattern VM's
+    applied = (ref != 0) & ~(ref == 7).all(axis=1, keepdims=True)
     bad = np.argwhere((v != ref) & applied)
     assert bad.size == 0, f"{len(bad)} cells differ, first {bad[:5].tolist()}"

@@ -219,6 +219,23 @@ def _expect():
     return rows, exp, nd
 
 
+def _context_error(r):
+    """NewPolicyContext fails before any rule runs (policy_context.go:230 AddImageInfos): the
+    standard image extractors (pkg/utils/api/image.go:54-180) need every non-null entry of
+    initContainers / containers / ephemeralContainers to be a map with a string `name`."""
+    spec = r
+    for k in _spec_root(r["kind"]).split("."):
+        spec = spec.get(k) if isinstance(spec, dict) else None
+    if not isinstance(spec, dict):
+        return False
+    for tag in ("initContainers", "containers", "ephemeralContainers"):
+        lst = spec.get(tag)
+        for c in (lst if isinstance(lst, list) else []):
+            if c is not None and (not isinstance(c, dict) or not isinstance(c.get("name"), str)):
+                return True
+    return False
+
+
 def test_injection_table_has_both_outcomes():
     _, exp, _ = _expect()
     assert 0.3 < exp.mean() < 0.8
@@ -234,10 +251,20 @@ def test_flattener_decode_flag_matches_go_types():
 
 def test_oracle_decode_error_matches_go_types(oracle):
     rows, exp, nd = _expect()
+    ctx = np.array([_context_error(r) for r in rows])
+    assert 0 < ctx.sum() < len(rows) // 4
     v = oracle.validate([restricted_latest()], nd, nthreads=4)
+    assert (v[ctx] == 7).all()  # no response at all
     got = (v == 4).any(axis=1)
-    bad = np.nonzero(got != exp)[0]
+    bad = np.nonzero(got != (exp & ~ctx))[0]
     assert bad.size == 0, [(int(i), json.dumps(rows[i])[:300], bool(exp[i])) for i in bad[:5]]
+
+
+def test_flattener_context_error_flag(oracle):
+    rows, exp, nd = _expect()
+    ctx = np.array([_context_error(r) for r in rows])
+    flags = K.Corpus(nd).row_flags()
+    assert np.array_equal((flags & 8).astype(bool), ctx)
 
 
 @pytest.mark.gpu
@@ -248,4 +275,6 @@ def test_gpu_typed_decode_parity(oracle):
     v, _, _ = eng.evaluate(K.PolicySet(pols), K.Corpus(nd))
     ref = oracle.validate(pols, nd, nthreads=8)
     assert np.array_equal(v, ref)
-    assert np.array_equal((v == 4).any(axis=1), exp)
+    ctx = np.array([_context_error(r) for r in rows])
+    assert (v[ctx] == 7).all()
+    assert np.array_equal((v == 4).any(axis=1), exp & ~ctx)
