@@ -209,7 +209,7 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
  * resource's JSON (the EngineResponse resource, resource_len bytes): podSecurity pass
  * ("Validation rule '<rule>' passed.", validate_pss.go:85) and fail (validate_pss.go:108:
  * FormatChecksPrint of the failing checks after convertChecks, rules without
- * podSecurity.exclude) and validate.pattern pass ("validation rule '<rule>' passed.",
+ * podSecurity.exclude or a podSecurity PolicyException) and validate.pattern pass ("validation rule '<rule>' passed.",
  * validate_resource.go:339), and for validate.deny rules whose conditions carry no `message`:
  * pass ("validation rule '<rule>' passed."), fail (getDenyMessage, validate_resource.go:279-300:
  * the rule message, or "validation error: rule <rule> failed" when it is empty; none when it

@@ -932,8 +932,10 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         uint32_t v = KPE_NA_;
         // PolicyExceptions of the rule: their match block holds => RuleSkip before any handler
         const uint32_t xe = (m && a.rule_exc) ? sld(a.rule_exc, ri) : 0u;
-        if (xe && block((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe))) v = KPE_SKIP_;
-        else if (m && hd == H_PSS) v = err ? KPE_ERROR_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
+        const bool xh = xe && block((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe));
+        if (xh && !(xe & XE_PSS)) v = KPE_SKIP_;
+        else if (m && hd == H_PSS)  // under a podSecurity exception kpe_pssx_kernel decides
+          v = err ? KPE_ERROR_ : xh ? KPE_XFAIL_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
         else if (m && hd == H_ERROR) v = KPE_ERROR_;
         else if (m && (hd == H_PATTERN || hd == H_COND)) v = KPE_PENDING_;
         else if (m && hd == H_CONST_SKIP) v = KPE_SKIP_;
@@ -1018,7 +1020,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
           const uint32_t xe = a.rule_exc[c0 + lane];
           if (xe) {
             const uint64_t xm = m & block_mask((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe));
-            pm |= xm, em |= xm, fm &= ~xm;
+            if (xe & XE_PSS) pm |= xm & ~em, fm |= xm & ~em;  // p and f: KPE_XFAIL_ (kpe_pssx_kernel decides)
+            else pm |= xm, em |= xm, fm &= ~xm;
           }
         }
         rmk[lane * 3 + 0] = pm;
@@ -1051,7 +1054,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         const uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
         const uint32_t f = (fm >> lane) & 1u, e = (em >> lane) & 1u;
         const uint32_t p = (pm >> lane) & 1u;
-        const uint32_t v = p ? (e ? KPE_SKIP_ : KPE_PASS_) : (f && e) ? KPE_PENDING_ : f ? KPE_FAIL_
+        const uint32_t v = p ? (e ? KPE_SKIP_ : f ? KPE_XFAIL_ : KPE_PASS_) : (f && e) ? KPE_PENDING_ : f ? KPE_FAIL_
                                                                    : e ? KPE_ERROR_ : KPE_NA_;
         sv[lane * nc + j] = (uint8_t)v;
       }

@@ -1833,6 +1833,38 @@ class Lowerer {
 
   // podSecurity.exclude (pkg/pss/evaluate.go:72-317; exclude.Validate, common_types.go:472-478)
   void pss_exclusions(const JV& ex, uint32_t col, uint32_t cvm, const std::string& rname) {
+    KpeXRule xr{};
+    xr.col = col, xr.cv_mask = cvm;
+    const int64_t last_invalid = excl_list(ex, "rule '" + rname + "'", &xr.excl0, &xr.nexcl, &xr.kx);
+    if (last_invalid >= 0)
+      xr.force = last_invalid == (int64_t)ex.a.size() - 1 ? XR_FORCE_FAIL : XR_FORCE_PASS;
+    pssx_fixed_preds();
+    P.pssx.rules.push_back(xr);
+  }
+  // A PolicyException's podSecurity controls on PSS rule col: the rule's KpeXRule (one with no
+  // excludes of its own when it has none) also holds the exception's excludes
+  void pss_exception(const JV& ex, uint32_t col, uint32_t cvm, const std::string& what) {
+    size_t i = 0;
+    while (i < P.pssx.rules.size() && P.pssx.rules[i].col != col) ++i;
+    if (i == P.pssx.rules.size()) {
+      KpeXRule xr{};
+      xr.col = col, xr.cv_mask = cvm, xr.excl0 = (uint32_t)P.pssx.excl.size();
+      pssx_fixed_preds();
+      P.pssx.rules.push_back(xr);
+    }
+    uint32_t x0, n, kx = 0;
+    const int64_t last_invalid = excl_list(ex, what, &x0, &n, &kx);
+    KpeXRule& xr = P.pssx.rules[i];
+    P.reports[col].pss_excl = true;  // fail messages are the checks after the exception's excludes
+    if (n > 0xFFFFFFu) throw CompileError(what + ": too many podSecurity controls");
+    xr.kx |= kx, xr.xexcl0 = x0;
+    xr.xn = n | (last_invalid < 0 ? XR_FORCE_NONE
+                 : last_invalid == (int64_t)ex.a.size() - 1 ? XR_FORCE_FAIL : XR_FORCE_PASS) << 24;
+  }
+  // The compiled KpeXExcl entries of one podSecurity exclude list (rule or PolicyException);
+  // returns the index of the last invalid entry (Validate: restrictedField and values go
+  // together), or -1
+  int64_t excl_list(const JV& ex, const std::string& who, uint32_t* x0, uint32_t* n, uint32_t* kx) {
     static const std::map<std::string, uint32_t> controls = {  // pkg/pss/utils/mapping.go:45-107
         {"Capabilities", (1u << CK_CAPS_BASELINE) | (1u << CK_CAPS_RESTRICTED)},
         {"Seccomp", (1u << CK_SECCOMP_BASELINE) | (1u << CK_SECCOMP_RESTRICTED)},
@@ -1853,24 +1885,23 @@ class Lowerer {
     auto strs = [&](const JV* j, const char* what) {
       std::vector<std::string> out;
       if (!j || j->t == JV::Null) return out;
-      if (j->t != JV::Arr) throw CompileError("rule '" + rname + "': podSecurity.exclude " + what + " is not a list");
+      if (j->t != JV::Arr) throw CompileError(who + ": podSecurity.exclude " + what + " is not a list");
       for (auto& e : j->a) {
-        if (e.t != JV::Str) throw CompileError("rule '" + rname + "': podSecurity.exclude " + what + " entry");
+        if (e.t != JV::Str) throw CompileError(who + ": podSecurity.exclude " + what + " entry");
         out.push_back(e.s);
       }
       return out;
     };
     auto str = [&](const JV* j, const char* what) {
       if (!j || j->t == JV::Null) return std::string();
-      if (j->t != JV::Str) throw CompileError("rule '" + rname + "': podSecurity.exclude " + what + " is not a string");
+      if (j->t != JV::Str) throw CompileError(who + ": podSecurity.exclude " + what + " is not a string");
       return j->s;
     };
-    KpeXRule xr{};
-    xr.col = col, xr.cv_mask = cvm, xr.excl0 = (uint32_t)P.pssx.excl.size(), xr.nexcl = (uint32_t)ex.a.size();
+    *x0 = (uint32_t)P.pssx.excl.size(), *n = (uint32_t)ex.a.size();
     int64_t last_invalid = -1;
     for (size_t i = 0; i < ex.a.size(); ++i) {
       const JV& e = ex.a[i];
-      if (e.t != JV::Obj) throw CompileError("rule '" + rname + "': podSecurity.exclude entry is not an object");
+      if (e.t != JV::Obj) throw CompileError(who + ": podSecurity.exclude entry is not an object");
       const std::string cn = str(e.get("controlName"), "controlName");
       const std::vector<std::string> images = strs(e.get("images"), "images");
       const std::string rf = str(e.get("restrictedField"), "restrictedField");
@@ -1895,11 +1926,12 @@ class Lowerer {
         x.pv_sys = gpred(D_SYSCTL, values);
         x.pv_cap = gpred(D_CAP, values);
       }
-      xr.kx |= x.checks;
+      *kx |= x.checks;
       P.pssx.excl.push_back(x);
     }
-    if (last_invalid >= 0)
-      xr.force = last_invalid == (int64_t)ex.a.size() - 1 ? XR_FORCE_FAIL : XR_FORCE_PASS;
+    return last_invalid;
+  }
+  void pssx_fixed_preds() {
     if (P.pssx.rules.empty()) {  // fixed PSA predicates, read from pbuf by kpe_pssx_kernel
       auto& g = P.pssx_preds;
       g[0] = gpred(D_ANNK, {"container.apparmor.security.beta.kubernetes.io/*"});
@@ -1910,7 +1942,6 @@ class Lowerer {
       g[5] = gpred(D_CAP, {"ALL"});
       for (int v = 0; v < 3; ++v) g[6 + v] = gpred(D_SYSCTL, P.preds[P.pss.sysctl[v]].globs);
     }
-    P.pssx.rules.push_back(xr);
   }
 
   uint32_t term(const KpeTerm& t) {  // distinct terms are evaluated once per resource
@@ -2395,6 +2426,7 @@ class Lowerer {
     struct X {
       const JV* spec;
       std::string key;
+      const JV* pss;  // spec.podSecurity when non-empty (HasPodSecurity)
     };
     std::vector<X> keep;
     for (const JV* e : xs) {
@@ -2408,8 +2440,10 @@ class Lowerer {
       // (pkg/controllers/report/utils/utils.go:113-124); kyverno apply uses every one given
       const JV* bg = spec->get("background");
       if (background && bg && bg->t == JV::Bool && !bg->b) continue;
-      if (nonempty(spec->get("podSecurity")))
-        throw CompileError("PolicyException " + key + ": podSecurity exceptions are not supported on the device");
+      const JV* pss = spec->get("podSecurity");
+      if (pss && pss->t != JV::Null && pss->t != JV::Arr)
+        throw CompileError("PolicyException " + key + ": podSecurity is not a list");
+      if (pss && (pss->t != JV::Arr || pss->a.empty())) pss = nullptr;
       // CheckAnyAllConditions (pkg/utils/conditions/condition.go:14-30): every `all` holds and
       // some `any` holds, or `any` is empty
       const JV* cond = spec->get("conditions");
@@ -2434,10 +2468,11 @@ class Lowerer {
         }
         if (!ok) throw CompileError("PolicyException " + key + ": conditions must fold to true at compile time");
       }
-      keep.push_back({spec, key});
+      keep.push_back({spec, key, pss});
     }
     for (size_t r = 0; r < P.rules.size(); ++r) {
       std::vector<const JV*> mine;  // match blocks of the exceptions that contain this rule
+      const X* with_pss = nullptr;
       for (auto& x : keep) {
         bool has = false;
         const JV* ex = x.spec->get("exceptions");
@@ -2448,9 +2483,16 @@ class Lowerer {
               if (glob_host(rn, rule_info_[r].name)) has = true;
           }
         if (has) mine.push_back(x.spec->get("match"));
+        if (has && x.pss) with_pss = &x;
       }
       if (mine.empty()) continue;
       const std::string rname = rule_names_at(r);
+      // validate_pss.go:45-58: on a podSecurity rule an exception with podSecurity controls does
+      // not skip; an unparsable level / version (H_ERROR) errors with or without it
+      if (with_pss && P.rules[r].handler == H_ERROR) continue;
+      const bool xpss = with_pss && P.rules[r].handler == H_PSS;
+      if (xpss && mine.size() > 1)  // MatchesException: the first matching one decides
+        throw CompileError("rule '" + rname + "': several PolicyExceptions, one with podSecurity controls");
       if (rule_info_[r].pre_dyn)
         throw CompileError("rule '" + rname + "': PolicyExceptions on a rule whose preconditions read the resource");
       if (P.rules[r].handler == H_NONE) {
@@ -2483,6 +2525,10 @@ class Lowerer {
       }
       const uint32_t nf = (uint32_t)P.filters.size() - f0;
       if (f0 > 0xFFFFFu || nf > 0x3FFu) throw CompileError("rule '" + rname + "': too many PolicyException filters");
+      if (xpss) {
+        x |= XE_PSS;
+        pss_exception(*with_pss->pss, (uint32_t)r, P.rules[r].cv_mask, "PolicyException " + with_pss->key);
+      }
       P.rules[r].exc = x | f0 | nf << 20;
       P.any_exc = true;
     }

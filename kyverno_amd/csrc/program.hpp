@@ -85,7 +85,7 @@ struct RuleReport {
   bool overrides = false;     // spec.validationFailureActionOverrides non-empty (per-namespace action)
   uint32_t name_mult = 1;     // validate rules of the policy with this name (result.go:44 name match)
   bool pss = false;
-  bool pss_excl = false;      // podSecurity.exclude non-empty (fail messages not rendered)
+  bool pss_excl = false;      // podSecurity.exclude or a podSecurity PolicyException (fail messages not rendered)
   bool msg_pattern = false;   // validate.pattern rule: pass message "validation rule '<rule>' passed."
   // validate.deny rule whose conditions (and preconditions) carry no `message`, so the reference's
   // condition message is empty (variables/evaluate.go:14-28): pass "validation rule '<rule>'

@@ -268,8 +268,9 @@ struct PssxVM {
       }
     }
   }
-  // exemptExclusions for one exclude over the errors E of its pod view
-  __device__ __forceinline__ void exempt(const KpeXExcl& e) {
+  // exemptExclusions for one exclude over the errors E of its pod view; conv: the defaults went
+  // through convertChecks (a PolicyException's excludes), so annotation fields never compare
+  __device__ __forceinline__ void exempt(const KpeXExcl& e, bool conv) {
     const bool by_image = e.img != -1;
     const uint32_t rf_ann = e.rf_kind == XRF_ANN ? a.rf_ann[e.rf_key] : KPE_NO_STR;
     const uint32_t n = ne < kXCap ? ne : kXCap;
@@ -277,6 +278,7 @@ struct PssxVM {
       const uint4 x = E[j];
       const uint32_t key = x.x & 0xFFFFu;
       if (e.rf_kind == XRF_NEVER) break;
+      if (conv && key == XKEY(XF_ANN, XT_POD)) continue;  // now spec.template.metadata.annotations[..]
       if (e.rf_kind == XRF_FIELD && key != e.rf_key) continue;
       if (e.rf_kind == XRF_ANN && (key != XKEY(XF_ANN, XT_POD) || x.y != rf_ann || rf_ann == KPE_NO_STR)) continue;
       if (!values_ok(e, x)) continue;
@@ -291,15 +293,18 @@ struct PssxVM {
   }
 };
 
-// kpe_pssx_kernel's body for pod r. The scan wrote each exclusion rule's plain PSS verdict;
-// a failing pod is re-evaluated with its exclusions (EvaluatePod). One gen() call site: the
-// loop walks (1) every versioned check on the pod, then per excluded failing check (2) its
-// default errors and (3) each naming exclude's errors of every version on that exclude's view.
+// kpe_pssx_kernel's body for pod r. The scan wrote each exclusion rule's plain PSS verdict
+// (KPE_XFAIL_ where a podSecurity PolicyException matched); a failing pod is re-evaluated with
+// its exclusions (EvaluatePod), then with the exception's (validate_pss.go:88-104). One gen()
+// call site: the loop walks (1) every versioned check on the pod, then per excluded failing
+// check (2) its default errors and (3) each naming exclude's errors of every version on that
+// exclude's view, the rule's excludes first.
 __device__ __forceinline__ void pssx_eval_row(const PssxArgs& a, int64_t r) {
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   PssxVM vm(a, r);
   const uint32_t* rec = a.rec + 4 * r;
   vm.pw = rec[0] & 0xFFFFFu;
+  const bool pod = ((rec[0] >> PR_CLASS_SH) & R_CLASS_MASK) == R_CLASS_POD;
   vm.c0 = a.ctr_off[r], vm.c1 = a.ctr_off[r + 1];
   vm.v0 = a.vol_off[r], vm.v1 = a.vol_off[r + 1];
   vm.s0 = a.sys_off[r], vm.s1 = a.sys_off[r + 1];
@@ -307,17 +312,23 @@ __device__ __forceinline__ void pssx_eval_row(const PssxArgs& a, int64_t r) {
   for (uint32_t ri = 0; ri < a.nxr; ++ri) {
     const KpeXRule xr = a.rules[ri];
     const uint8_t cell = row[xr.col];
-    if (cell != KPE_PASS_ && cell != KPE_FAIL_) continue;  // not evaluated (NA, error, skip, ...)
+    const bool xc = cell == KPE_XFAIL_;  // a podSecurity exception matched the pod
+    if (cell != KPE_PASS_ && cell != KPE_FAIL_ && !xc) continue;  // not evaluated (NA, error, skip, ...)
     uint32_t* mk = a.masks ? a.masks + (size_t)r * a.R + xr.col : nullptr;
+    const uint32_t xforce = XR_XFORCE(xr.xn);
     if (xr.force != XR_FORCE_NONE) {  // an invalid exclude: results nil (EvaluatePod)
-      row[xr.col] = xr.force == XR_FORCE_FAIL ? KPE_FAIL_ : KPE_PASS_;
+      // not allowed under the exception: ApplyPodSecurityExclusion over no checks
+      row[xr.col] = xr.force == XR_FORCE_PASS ? KPE_PASS_ : (!xc || xforce == XR_FORCE_FAIL) ? KPE_FAIL_ : KPE_SKIP_;
       if (mk) *mk = 0u;
       continue;
     }
-    if (cell == KPE_PASS_) continue;  // nothing to exempt
-    uint32_t ph = 0, rem_v = xr.cv_mask, fails = 0, rem_k = 0, k = 0, vk = 0, ei = 0, rem_x = 0, out = 0;
+    if (cell == KPE_PASS_ || (!xc && xr.nexcl == 0u)) continue;  // nothing to exempt
+    // the exception's excludes can remove errors only when they run (no invalid entry) on a Pod:
+    // convertChecks rewrites every field of a controller / CronJob
+    const uint32_t total = xr.nexcl + ((xc && xforce == XR_FORCE_NONE && pod) ? XR_XN(xr.xn) : 0u);
+    uint32_t ph = 0, rem_v = xr.cv_mask, fails = 0, rem_k = 0, k = 0, vk = 0, ei = 0, rem_x = 0, out = 0, out_rule = 0;
     KpeXExcl ex{};
-    bool undec = false;
+    bool undec = false, rdone = false, conv = false;
     for (;;) {
       uint32_t cv, view = VW_REAL, img = PRED_NONE;
       if (ph == 0u) {  // every versioned check on the pod (evaluatePSS)
@@ -327,6 +338,7 @@ __device__ __forceinline__ void pssx_eval_row(const PssxArgs& a, int64_t r) {
             if (fails & check_versions(c)) fk |= 1u << c;
           for (uint32_t m = fk & ~xr.kx; m; m &= m - 1u)  // failing checks no exclude names: kept
             out |= 1u << (31u - __builtin_clz(fails & check_versions(__builtin_ctz(m))));
+          out_rule = out;
           rem_k = fk & xr.kx;
           ph = 1u;
           continue;
@@ -338,16 +350,23 @@ __device__ __forceinline__ void pssx_eval_row(const PssxArgs& a, int64_t r) {
         k = __builtin_ctz(rem_k);
         rem_k &= rem_k - 1u;
         vk = 31u - __builtin_clz(fails & check_versions(k));
-        cv = vk, ei = 0, rem_x = 0;
+        cv = vk, ei = 0, rem_x = 0, rdone = false;
       } else {  // the next (exclude, version) of check k
         if (!rem_x) {
-          while (ei < xr.nexcl && !(a.excl[xr.excl0 + ei].checks & (1u << k))) ++ei;
-          if (ei >= xr.nexcl || vm.nd == 0u) {
+          while (ei < total && !(a.excl[ei < xr.nexcl ? xr.excl0 + ei : xr.xexcl0 + ei - xr.nexcl].checks & (1u << k)))
+            ++ei;
+          if (!rdone && (ei >= xr.nexcl || vm.nd == 0u)) {  // the rule's excludes are done
+            rdone = true;
+            if (vm.nd) out_rule |= 1u << vk;
+          }
+          if (ei >= total || vm.nd == 0u) {
             if (vm.nd) out |= 1u << vk;  // errors left: the check still fails
             ph = 1u;
             continue;
           }
-          ex = a.excl[xr.excl0 + ei++];
+          conv = ei >= xr.nexcl;
+          ex = a.excl[conv ? xr.xexcl0 + ei - xr.nexcl : xr.excl0 + ei];
+          ++ei;
           rem_x = xr.cv_mask & check_versions(k);
         }
         cv = __builtin_ctz(rem_x);
@@ -369,14 +388,19 @@ __device__ __forceinline__ void pssx_eval_row(const PssxArgs& a, int64_t r) {
         vm.nd = vm.ne;
         ph = 2u;
       } else {
-        vm.exempt(ex);
+        vm.exempt(ex, conv);
       }
     }
     if (undec) {
       row[xr.col] = KPE_UNDECIDED_;
       continue;
     }
-    row[xr.col] = out ? KPE_FAIL_ : KPE_PASS_;
-    if (mk) *mk = out;
+    // validate_pss.go:84-110: allowed => pass; else, under the exception, no checks left and no
+    // error => skip; the fail response carries the checks from before the exception
+    uint8_t v = KPE_PASS_;
+    if (out_rule)
+      v = (!xc || xforce == XR_FORCE_FAIL || (xforce == XR_FORCE_NONE && out)) ? KPE_FAIL_ : KPE_SKIP_;
+    row[xr.col] = v;
+    if (mk) *mk = v == KPE_FAIL_ ? out_rule : 0u;
   }
 }

@@ -284,6 +284,8 @@ enum KpeCheckVersion {
 #define KPE_PENDING_ 6  // device-internal: matched pattern / condition rule, resolved by a later kernel
 #define KPE_UNDECIDED_ 7  // the device cannot decide this cell (a documented device limit, e.g. a
                           // condition list longer than CV_LIST_CAP): the caller evaluates it
+#define KPE_XFAIL_ 8  // device-internal: a failing podSecurity cell whose PolicyException has
+                      // podSecurity controls (validate_pss.go:88-104), resolved by kpe_pssx_kernel
 
 // ---- policy program ------------------------------------------------------------------------------
 // Rule handlers
@@ -376,6 +378,8 @@ typedef struct KpeRule {
 // validate_pss.go:45-58). Filters [f0, f0 + nf), any (OR) or all (AND; nf = 0: always).
 #define XE_PRESENT (1u << 31)
 #define XE_ALL (1u << 30)
+#define XE_PSS (1u << 29)  // the rule's (single) exception has podSecurity controls: a failing PSS
+                           // cell becomes KPE_XFAIL_ instead of RuleSkip (ApplyPodSecurityExclusion)
 #define XE_F0(x) ((x) & 0xFFFFFu)
 #define XE_NF(x) (((x) >> 20) & 0x3FFu)
 
@@ -428,9 +432,15 @@ typedef struct KpeXExcl {
 #define XR_FORCE_FAIL 2u
 typedef struct KpeXRule {
   uint32_t col, cv_mask, excl0, nexcl;
-  uint32_t force, kx;  // kx: check ids some exclude names
-  uint32_t pad[2];
+  uint32_t force, kx;  // kx: check ids some exclude names (the rule's or its exception's)
+  // PolicyException podSecurity controls (KPE_XFAIL_ cells): excludes [xexcl0, + XR_XN(xn)),
+  // applied after the rule's to the converted checks (validate_pss.go:88-104, convertChecks
+  // :114-135: only a Pod's spec fields still compare), and the fold of invalid entries
+  uint32_t xexcl0, xn;
 } KpeXRule;
+#define XR_XN(x) ((x) & 0xFFFFFFu)
+#define XR_XFORCE(x) ((x) >> 24)  // XR_FORCE_NONE; XR_FORCE_PASS here means "every check cleared":
+                                  // SKIP; XR_FORCE_FAIL: the last exclude invalid, FAIL
 
 // ---- generic document tape (pattern rules) ---------------------------------------------
 // Every resource is also kept as its JSON document (the reference's unstructured map).

@@ -451,7 +451,8 @@ struct PolicyException {
   std::vector<Filter> any, all;  // MatchResources (no legacy form)
   bool has_conditions = false;
   std::vector<cond::Condition> c_any, c_all;  // AnyAllConditions
-  bool has_pss = false;
+  bool has_pss = false;                  // HasPodSecurity: spec.podSecurity non-empty
+  std::vector<PSSExclude> pss_excludes;  // spec.podSecurity
   bool unsupported = false;  // a condition this restatement does not cover
   std::vector<std::pair<std::string, std::vector<std::string>>> refs;  // (policyName, ruleNames)
   // Exception.Contains (policy_exception_types.go:136-145): policy key equal, a rule-name glob
@@ -803,6 +804,16 @@ inline Rule::ForEach parse_foreach(const JVal& e, int depth) {
   return f;
 }
 
+// kyvernov1.PodSecurityStandard entries (common_types.go:440-478)
+inline std::vector<PSSExclude> parse_pss_excludes(const JVal* ex) {
+  std::vector<PSSExclude> out;
+  if (ex && ex->t == JT::Arr)
+    for (auto& e : ex->a)
+      out.push_back({jstr(e->get("controlName")), jstrlist(e->get("images")), jstr(e->get("restrictedField")),
+                     jstrlist(e->get("values"))});
+  return out;
+}
+
 inline Rule compile_rule(const JPtr& raw) {
   Rule r;
   r.raw = raw;
@@ -817,11 +828,7 @@ inline Rule compile_rule(const JPtr& raw) {
     r.has_pss = true;
     r.pss_level = jstr(ps->get("level"));
     r.pss_version = jstr(ps->get("version"));
-    const JVal* ex = ps->get("exclude");
-    if (ex && ex->t == JT::Arr)
-      for (auto& e : ex->a)
-        r.pss_excludes.push_back({jstr(e->get("controlName")), jstrlist(e->get("images")),
-                                  jstr(e->get("restrictedField")), jstrlist(e->get("values"))});
+    r.pss_excludes = parse_pss_excludes(ps->get("exclude"));
   } else if (r.has_validate) {
     // validate_resource.go:121-170: deny, then pattern/anyPattern, then foreach
     const JVal* deny = v->get("deny");
@@ -1113,8 +1120,10 @@ inline Status foreach_handler(const Rule& r, const cond::Ctx& cx, const JVal& re
   }
 }
 
-// validate_pss.go:31-112 (no exceptions, CREATE operation)
-inline Status pss_handler(const Rule& r, const JVal& res, const std::string& kind) {
+// validate_pss.go:31-112 (CREATE operation). exc: the matching PolicyException when it has
+// podSecurity controls (:88-104): a pod they clear entirely (no error) is skipped
+inline Status pss_handler(const Rule& r, const JVal& res, const std::string& kind,
+                          const PolicyException* exc = nullptr) {
   Pod pod;
   try {
     pod = get_spec(res, kind);
@@ -1127,7 +1136,13 @@ inline Status pss_handler(const Rule& r, const JVal& res, const std::string& kin
                                             : (r.pss_level == "restricted" ? Level::Restricted : Level::Privileged),
                   v};
   try {
-    return evaluate_pod(lv, r.pss_excludes, pod) ? PASS : FAIL;
+    std::vector<PSSCheckResult> checks;
+    if (evaluate_pod(lv, r.pss_excludes, pod, &checks)) return PASS;
+    if (!exc) return FAIL;
+    convert_checks(checks, kind);
+    bool err = false;
+    checks = apply_exclusion(lv, exc->pss_excludes, checks, pod, &err);
+    return checks.empty() && !err ? SKIP : FAIL;
   } catch (const std::out_of_range&) {
     return ERROR;  // the Go reference would panic here
   }
@@ -1218,7 +1233,9 @@ inline PolicyException parse_exception(const JVal& x) {
   e.background = !(bg && bg->t == JT::Bool && !bg->b);
   MatchRes m = parse_match(spec->get("match"));
   e.any = m.any, e.all = m.all;
-  e.has_pss = jnonempty(spec->get("podSecurity"));
+  const JVal* ps = spec->get("podSecurity");
+  e.has_pss = ps && ps->t == JT::Arr && !ps->a.empty();
+  if (e.has_pss) e.pss_excludes = parse_pss_excludes(ps);
   const JVal* cnd = spec->get("conditions");
   if (cnd && !cnd->is_null()) {
     e.has_conditions = true;
@@ -1290,20 +1307,20 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
       }
       // engine.go:286-293 + the handlers' first step: a matching PolicyException skips the
       // rule (validate_resource.go:43-56 always; validate_pss.go:45-58 when it has no
-      // podSecurity controls: those are not restated here)
+      // podSecurity controls, else the PSS handler applies them to a failing pod)
+      const PolicyException* pss_exc = nullptr;
       if (!done && i < p.exceptions.size() && !p.exceptions[i].empty()) {
         try {
           if (const PolicyException* e = matches_exception(p.exceptions[i], c, res, cx)) {
-            if (r.has_pss && e->has_pss) s = UNSUPPORTED;
-            else s = SKIP;
-            done = true;
+            if (r.has_pss && e->has_pss) pss_exc = e;
+            else s = SKIP, done = true;
           }
         } catch (const cond::Unsupported&) {
           s = UNSUPPORTED, done = true;
         }
       }
       if (!done) {
-        if (r.has_pss) s = pss_handler(r, res, u.kind());
+        if (r.has_pss) s = pss_handler(r, res, u.kind(), pss_exc);
         else if (r.has_deny) s = deny_handler(r, cx);
         else if (r.pattern || r.any_pattern) s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx);
         else if (!r.foreach.empty()) s = foreach_handler(r, cx, res);

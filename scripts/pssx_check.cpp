@@ -1,11 +1,12 @@
 // Host build of the podSecurity exclusion pass (kyverno_amd/csrc/pssx.inl, the exact text
 // kpe_pssx_kernel runs) for sanitizer runs and parity checks without a GPU:
-//   scripts/build/pssx_check policies.json resources.ndjson seed.bin out.bin
+//   scripts/build/pssx_check policies.json resources.ndjson seed.bin out.bin [exceptions.json]
 // Flattens the resources, compiles the policies, evaluates the predicates the pass reads on
 // the host (go-wildcard globs over the corpus dictionaries, the pbuf layout of kpe_api.cpp)
 // and binds the exclusion tables the way kpe_api.cpp does, then runs pssx_eval_row over a
 // verdict matrix seeded from seed.bin (N x R bytes: the plain PSS verdicts the scan kernel
-// writes, i.e. the rules' verdicts without their exclusions). Writes N x R verdicts to out.bin.
+// writes, i.e. the rules' verdicts without their exclusions, KPE_XFAIL_ where a podSecurity
+// PolicyException matched). Writes N x R verdicts to out.bin.
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -77,9 +78,10 @@ int main(int argc, char** argv) {
     return 2;
   }
   const std::string pj = slurp(argv[1]), nd = slurp(argv[2]), seed = slurp(argv[3]);
+  const std::string xj = argc > 5 ? slurp(argv[5]) : std::string();
   kpe::Corpus C;
   kpe::flatten_ndjson(C, nd.data(), nd.size(), nullptr, 0, false);
-  auto P = kpe::compile_policies(pj.data(), pj.size());
+  auto P = kpe::compile_policies(pj.data(), pj.size(), xj.empty() ? nullptr : xj.data(), xj.size(), false);
   const uint32_t R = (uint32_t)P->rules.size();
   if (seed.size() != (size_t)C.n * R) return fprintf(stderr, "seed size %zu != %lld x %u\n", seed.size(), (long long)C.n, R), 1;
   std::vector<uint8_t> verdicts(seed.begin(), seed.end());

@@ -172,3 +172,67 @@ def strip_exclusions(pols):
         for r in p["spec"]["rules"]:
             r["validate"]["podSecurity"].pop("exclude", None)
     return out
+
+
+def _wrap(rng, pod):
+    """The pod itself, or as the template of a Deployment or a CronJob (whose converted check
+    fields no PolicyException podSecurity entry can match, validate_pss.go:114-135)."""
+    r = rng.random()
+    if r < 0.65:
+        return pod
+    meta = {"name": pod["metadata"]["name"], "namespace": "default"}
+    tmpl = {"metadata": {k: v for k, v in pod["metadata"].items() if k == "annotations"}, "spec": pod["spec"]}
+    if r < 0.85:
+        return {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": meta, "spec": {"template": tmpl}}
+    return {"apiVersion": "batch/v1", "kind": "CronJob", "metadata": meta,
+            "spec": {"schedule": "* * * * *", "jobTemplate": {"spec": {"template": tmpl}}}}
+
+
+def exception_case(seed, npods=600, nrules=16):
+    """(policies, exceptions, ndjson bytes): single-rule Pod policies (and their autogen rules),
+    some with their own exclusion lists, each with at most one PolicyException, most of them
+    with podSecurity controls (validate_pss.go:88-104), some plain (RuleSkip)."""
+    from tests.policies import pss_policy
+
+    rng = random.Random(seed)
+    pols, excs = [], []
+    for k in range(nrules):
+        level = rng.choice(["baseline", "restricted", "restricted"])
+        version = rng.choice(["latest", "latest", "v1.24", "v1.19", "v1.29"])
+        excl = random_exclusions(rng) if rng.random() < 0.35 else None
+        pols.append(pss_policy(f"e{k}", level, version, exclude=excl))
+        if rng.random() < 0.1:
+            continue
+        spec = {"exceptions": [{"policyName": f"pol-e{k}", "ruleNames": [f"e{k}", "autogen-*"]}],
+                "match": {"any": [{"resources": {"kinds": ["Pod", "Deployment", "CronJob"],
+                                                 "names": rng.sample(["p*", "p1*", "p?", "*3", "*7*"], 2)}}]}}
+        if rng.random() < 0.85:
+            x = random_exclusions(rng)
+            if rng.random() < 0.6:  # whole controls too, so that some failing pods clear entirely
+                x += [{"controlName": c} for c in rng.sample(CONTROLS[:-1], rng.randint(4, 12))]
+                rng.shuffle(x)
+            spec["podSecurity"] = x
+        excs.append({"apiVersion": "kyverno.io/v2beta1", "kind": "PolicyException",
+                     "metadata": {"name": f"x{k}", "namespace": "kyverno"}, "spec": spec})
+    docs = [_wrap(rng, random_pod(rng, i)) for i in range(npods)]
+    return pols, excs, "\n".join(json.dumps(d) for d in docs).encode()
+
+
+def xfail_seed(pols, excs, base, skipped):
+    """The scan kernel's verdicts for exception_case: `base` (no exclusions, no exceptions) with
+    the cells an exception matched (`skipped`: SKIP under the exceptions stripped of podSecurity)
+    set to RuleSkip, or to KPE_XFAIL_ (8) when that exception has podSecurity controls."""
+    seed = base.copy()
+    pss = {x["spec"]["exceptions"][0]["policyName"] for x in excs if x["spec"].get("podSecurity")}
+    col_pss = [pols[j // 3]["metadata"]["name"] in pss for j in range(base.shape[1])]
+    for j, p in enumerate(col_pss):
+        hit = (skipped[:, j] == 5) & ((base[:, j] == 1) | (base[:, j] == 2))
+        seed[hit, j] = 8 if p else 5
+    return seed
+
+
+def strip_pss(excs):
+    out = json.loads(json.dumps(excs))
+    for x in out:
+        x["spec"].pop("podSecurity", None)
+    return out

@@ -30,18 +30,19 @@ def _pss_exc(c):
 
 
 def test_oracle_chainsaw_exceptions(oracle):
-    """Admitted <=> no rule fails. podSecurity exceptions are outside the restatement
-    (ApplyPodSecurityExclusion after convertChecks): the oracle reports them unsupported."""
-    n = 0
+    """Admitted <=> no rule fails, podSecurity exceptions (ApplyPodSecurityExclusion after
+    convertChecks, validate_pss.go:88-104) included."""
+    n = npss = 0
     for c in _cases():
         v = oracle.validate([c["policy"]], json.dumps(c["resource"]).encode(), exceptions=c["exceptions"])[0]
-        if 7 in v.tolist():  # outside the restatement: podSecurity exceptions, length() / GreaterThan
-            assert _pss_exc(c) or c["dir"] == "conditions", c["file"]
+        if 7 in v.tolist():  # outside the restatement: conditions reading length() of a field
+            assert c["dir"] == "conditions", c["file"]
             continue
         rejected = FAIL in v.tolist()
         assert rejected == (c["expect"] == "rejected"), (c["file"], v.tolist())
         n += 1
-    assert n >= 6
+        npss += _pss_exc(c)
+    assert n >= 6 and npss >= 4
 
 
 NS_POL = "ns-0001"
@@ -136,11 +137,12 @@ def test_compile_accepts_and_refuses():
     pols, excs = exception_set()
     K.PolicySet(pols, excs)
     K.PolicySet(pols, excs, background=True)
-    pss = _exc("pss", [("baseline", ["*"])], _any({"kinds": ["Pod"]}),
+    pss = _exc("pss", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}),
                podSecurity=[{"controlName": "Host Ports"}])
-    with pytest.raises(K.KpeError):
-        K.PolicySet(pols, [pss])
-    cond = _exc("cond", [("baseline", ["*"])], _any({"kinds": ["Pod"]}), conditions={"any": [
+    K.PolicySet(pols, [pss])
+    with pytest.raises(K.KpeError):  # several exceptions on one PSS rule, one with podSecurity
+        K.PolicySet(pols, [pss, _exc("pss2", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}))])
+    cond = _exc("cond", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}), conditions={"any": [
         {"key": "{{ request.object.metadata.labels.color || '' }}", "operator": "Equals", "value": "blue"}]})
     with pytest.raises(K.KpeError):
         K.PolicySet(pols, [cond])
@@ -173,12 +175,12 @@ def test_gpu_chainsaw_exceptions(oracle):
         try:
             ps = K.PolicySet([c["policy"]], c["exceptions"])
         except K.KpeError:
-            assert _pss_exc(c) or c["dir"] == "conditions", c["file"]  # documented refusals
+            assert c["dir"] == "conditions", c["file"]  # documented refusals
             continue
         v, _, _ = eng.evaluate(ps, K.Corpus(json.dumps(c["resource"]).encode()))
         assert (FAIL in v[0].tolist()) == (c["expect"] == "rejected"), (c["file"], v[0].tolist())
         n += 1
-    assert n >= 4
+    assert n >= 8
 
 
 @pytest.mark.gpu

@@ -13,7 +13,7 @@ import pytest
 
 import kyverno_amd as K
 from tests.policies import pss_policy
-from tests.pss_fuzz import fuzz_case, strip_exclusions
+from tests.pss_fuzz import exception_case, fuzz_case, strip_exclusions, strip_pss, xfail_seed
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLD = os.path.join(ROOT, "tests", "golden")
@@ -45,12 +45,16 @@ def pssx_bin():
     return BIN
 
 
-def _host(pssx_bin, tmp_path, pols, nd, seed):
+def _host(pssx_bin, tmp_path, pols, nd, seed, excs=None):
     (tmp_path / "p.json").write_text(json.dumps(pols))
     (tmp_path / "r.ndjson").write_bytes(nd)
     (tmp_path / "seed.bin").write_bytes(np.ascontiguousarray(seed, dtype=np.uint8).tobytes())
+    extra = []
+    if excs is not None:
+        (tmp_path / "x.json").write_text(json.dumps(excs))
+        extra = [str(tmp_path / "x.json")]
     subprocess.check_call([pssx_bin, str(tmp_path / "p.json"), str(tmp_path / "r.ndjson"),
-                           str(tmp_path / "seed.bin"), str(tmp_path / "out.bin")], stdout=subprocess.DEVNULL)
+                           str(tmp_path / "seed.bin"), str(tmp_path / "out.bin")] + extra, stdout=subprocess.DEVNULL)
     return np.frombuffer((tmp_path / "out.bin").read_bytes(), dtype=np.uint8).reshape(seed.shape)
 
 
@@ -102,6 +106,43 @@ def test_fuzz_exclusions_host(pssx_bin, oracle, tmp_path, seed):
     assert ((base == 2) & (ref == 1)).sum() > 20
 
 
+def _exception_oracle(oracle, pols, excs, nd):
+    ref = oracle.validate(pols, nd, nthreads=8, exceptions=excs)
+    base = oracle.validate(strip_exclusions(pols), nd, nthreads=8)
+    skipped = oracle.validate(strip_exclusions(pols), nd, nthreads=8, exceptions=strip_pss(excs))
+    return ref, base, skipped
+
+
+@pytest.mark.parametrize("seed", [21, 22, 23, 24])
+def test_pss_exceptions_host(pssx_bin, oracle, tmp_path, seed):
+    """PolicyException podSecurity controls (validate_pss.go:45-110): the exclusion pass over the
+    cells the scan marks KPE_XFAIL_, after the rule's own exclusions, on Pods, Deployments and
+    CronJobs, with invalid entries in either list."""
+    pols, excs, nd = exception_case(seed)
+    ref, base, skipped = _exception_oracle(oracle, pols, excs, nd)
+    assert (ref == 7).sum() == 0
+    out = _host(pssx_bin, tmp_path, pols, nd, xfail_seed(pols, excs, base, skipped), excs)
+    bad = np.argwhere(out != ref)
+    assert bad.size == 0, [(int(i), int(j), int(out[i, j]), int(ref[i, j])) for i, j in bad[:8]]
+    # the exceptions both clear failing pods (skip) and leave others failing
+    xfail = xfail_seed(pols, excs, base, skipped) == 8
+    assert (xfail & (ref == 5)).sum() > 10 and (xfail & (ref == 2)).sum() > 10
+
+
+def test_pss_exception_compile():
+    pols, excs, _ = exception_case(21)
+    K.PolicySet(pols, excs)
+    first = next(x for x in excs if x["spec"].get("podSecurity"))
+    two = json.loads(json.dumps(first))
+    two["metadata"]["name"] = "second"
+    with pytest.raises(K.KpeError):  # the first matching exception decides: not restated
+        K.PolicySet(pols, excs + [two])
+    bad = json.loads(json.dumps(first))
+    bad["spec"]["podSecurity"] = {"controlName": "Capabilities"}
+    with pytest.raises(K.KpeError):
+        K.PolicySet(pols, [bad])
+
+
 # ---- GPU: the device path through the C-ABI ------------------------------------------------
 @pytest.mark.gpu
 def test_golden_evaluate_cases_gpu(oracle):
@@ -134,3 +175,16 @@ def test_fuzz_exclusions_gpu(oracle, seed):
     bad = np.argwhere(v != ref)
     assert bad.size == 0, [(int(i), int(j), int(v[i, j]), int(ref[i, j])) for i, j in bad[:8]]
     assert (masks[v != 2] == 0).all()  # masks: the checks still failing after the exclusions
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed,nrules", [(31, 24), (32, 8)])  # 72 rules: the WIDE scan; 24: NARROW
+def test_pss_exceptions_gpu(oracle, seed, nrules):
+    pols, excs, nd = exception_case(seed, npods=3000, nrules=nrules)
+    eng = K.Engine(ordinal=0)
+    v, masks, _ = eng.evaluate(K.PolicySet(pols, excs), K.Corpus(nd), check_masks=True)
+    ref = oracle.validate(pols, nd, nthreads=8, exceptions=excs)
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, [(int(i), int(j), int(v[i, j]), int(ref[i, j])) for i, j in bad[:8]]
+    assert (masks[v != 2] == 0).all()
+    assert (v == 5).any()
