@@ -165,6 +165,13 @@ kpe_status kpe_evaluate(kpe_device* dev, const kpe_program* prog, const kpe_corp
  * device stream; results stay in device buffers owned by the corpus. No host
  * synchronisation. Use kpe_device_sync() and kpe_fetch() afterwards. */
 kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c);
+/* kpe_evaluate_async with options: KPE_EVAL_MASKS also writes the check masks (device
+ * buffers read by kpe_fetch / kpe_fetch_cv_masks); KPE_EVAL_COLD re-runs the binding's
+ * per-corpus prologue (dictionary predicate pass, prologue image) as the first evaluation of a
+ * newly bound corpus does. */
+#define KPE_EVAL_MASKS 1u
+#define KPE_EVAL_COLD 2u
+kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, unsigned flags);
 kpe_status kpe_device_sync(kpe_device* dev);
 kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
                      uint32_t* check_masks, kpe_counts* counts);

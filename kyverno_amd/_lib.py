@@ -70,6 +70,7 @@ def load():
     L.kpe_corpus_free.argtypes = [vp]
     L.kpe_evaluate.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_evaluate_async.argtypes = [vp, vp, vp]
+    L.kpe_evaluate_async_ex.argtypes = [vp, vp, vp, ctypes.c_uint]
     L.kpe_device_sync.argtypes = [vp]
     L.kpe_fetch.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_pss_check_id.argtypes = [i32]

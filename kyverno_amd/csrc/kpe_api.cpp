@@ -121,6 +121,7 @@ struct kpe_device {
   struct EvPair {
     hipEvent_t a, b, c, d;
     double bytes, pbytes;
+    bool pre, post;  // a kernel ran between a and b (dictionary pass / prologue), c and d (later passes)
   };
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
@@ -976,7 +977,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   return KPE_OK;
 }
 
-kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool masks) {
+kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool masks, bool cold = false) {
   auto& P = *pp->p;
   auto& C = *cc->c;
   auto& D = *cc->d;
@@ -996,7 +997,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   const size_t R = P.rules.size();
   static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
-  const bool fresh = !B.inv_ready || no_cache;
+  const bool fresh = !B.inv_ready || no_cache || cold;
   if (B.nblocks && fresh) {  // dictionary pass for large-domain predicates
     PredArgs pa{};
     for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
@@ -1119,6 +1120,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     for (uint32_t i = 0; i < B.pimg_words; ++i) fprintf(stderr, "%s%08x", i % 8 ? " " : "\n  ", img[i]);
     fprintf(stderr, "\n");
   }
+  ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, B.lean && !masks ? B.lean_kind : PD.narrow ? 1 : 0,
                          B.scan_blocks,
@@ -1282,6 +1284,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
                                 (uint32_t)C.limit_rows.size(), KPE_UNDECIDED_, s));
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
+    ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
     ev.bytes = scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     dev->pending.push_back(ev);
@@ -1308,6 +1311,16 @@ kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kp
   kpe_status st = prepare(dev, prog, c, false);
   if (st) return st;
   return launch(dev, prog, const_cast<kpe_corpus*>(c), false);
+}
+
+kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, unsigned flags) {
+  if (!dev) return fail(KPE_E_INVALID, "null device");
+  if (flags & ~(unsigned)(KPE_EVAL_MASKS | KPE_EVAL_COLD)) return fail(KPE_E_INVALID, "unknown evaluation flags");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  const bool masks = (flags & KPE_EVAL_MASKS) != 0;
+  kpe_status st = prepare(dev, prog, c, masks);
+  if (st) return st;
+  return launch(dev, prog, const_cast<kpe_corpus*>(c), masks, (flags & KPE_EVAL_COLD) != 0);
 }
 
 kpe_status kpe_device_sync(kpe_device* dev) {
@@ -1562,9 +1575,9 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
     HIPCHK(hipEventElapsedTime(&d1, p.a, p.b));
     HIPCHK(hipEventElapsedTime(&d2, p.b, p.c));
     HIPCHK(hipEventElapsedTime(&d3, p.c, p.d));
-    dev->dict_ms += d1;
+    dev->dict_ms += p.pre ? d1 : 0.0f;  // an empty event interval is not a kernel (kpe.h)
     dev->pss_ms += d2;
-    dev->pat_ms += d3;
+    dev->pat_ms += p.post ? d3 : 0.0f;
     dev->last_bytes = p.bytes;
     dev->last_pbytes = p.pbytes;
     dev->launches++;

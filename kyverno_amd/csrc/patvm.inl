@@ -7,7 +7,7 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 #ifndef KPE_PAT_STACK
 #define KPE_PAT_STACK 14
 #endif
-constexpr int kPatStack = KPE_PAT_STACK;  // program.cpp kMaxDepth (12) + root + 1
+constexpr int kPatStack = KPE_PAT_STACK;  // frames of one lane; deeper walks give KPE_UNDECIDED
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
 
 // Bounds-checked table reads in KPE_PATVM_CHECK builds (scripts/patvm_check.cpp, the
@@ -406,10 +406,12 @@ struct PatVM {
             const uint32_t nmem = pn.z >> 16;
             for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
               const uint4 m = a.members[PV(pn.y + k, a.nmembers, 2)];
+              if (m.x & PMF_XSLOT) und = 1u;
               if (m.x & PMF_SLOT) {
                 const uint32_t bit = 1u << PM_SLOT(m.x);
-                reg |= bit;
-                if (pat_lookup(a, doc, br, m.y) != kNoNode) val |= bit;
+                reg |= bit;  // a glob key counts under its expansion (ExpandInMetadata ran first)
+                if (((m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, br, m.w) : pat_lookup(a, doc, br, m.y)) != kNoNode)
+                  val |= bit;
               }
             }
             v = push(PF_MAP, br, bpi, 0u);
@@ -548,7 +550,10 @@ struct PatVM {
   }
 
   __device__ __forceinline__ uint32_t push(uint32_t kind, uint32_t r, uint32_t pi, uint32_t cur) {
-    if (sp + 1 >= kPatStack) return PE_OTHER;  // unreachable: the compiler bounds pattern depth
+    if (sp + 1 >= kPatStack) {  // a resource as deep as a pattern nested past the lane's frame
+      und = 1u;                 // stack: the cell is KPE_UNDECIDED (the caller decides)
+      return PE_OTHER;
+    }
     ++sp;
     st[PV(sp, kPatStack, 11)] = PFrame{kind, r, pi, 0u, cur, 0u, 0u};
     return PE_PUSHED;

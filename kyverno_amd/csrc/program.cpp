@@ -679,7 +679,9 @@ class PatCompiler {
   }
 
  private:
-  static constexpr int kMaxDepth = 12;  // kernels.hip PatEval depth
+  // compile recursion bound only: walks deeper than the VM's frame stack (patvm.inl kPatStack)
+  // make their cells KPE_UNDECIDED at run time
+  static constexpr int kMaxDepth = 64;
   PatProgram& PP;
   std::function<int32_t(const std::string&)> key_pred_;
   std::map<std::string, uint32_t> slots_;  // AnchorMap key -> slot
@@ -775,7 +777,7 @@ class PatCompiler {
  private:
 
   uint32_t node(const JV& v, int depth, bool repeated) {
-    if (depth > kMaxDepth) throw CompileError("pattern nested deeper than 12 levels");
+    if (depth > kMaxDepth) throw CompileError("pattern nested deeper than 64 levels");
     if (v.t == JV::Obj) return map(v, depth, repeated);
     if (v.t == JV::Arr) {
       if (v.a.empty()) return push_node({PN_ARR_EMPTY, 0, 0, 0});
@@ -815,12 +817,26 @@ class PatCompiler {
       const Anc a = anchor_of(kv.first);
       if (kv.first.find("{{") != std::string::npos || kv.first.find("$(") != std::string::npos)
         throw CompileError("variables in pattern keys are not supported on the device");
-      if (expanding && has_glob(kv.first)) {
-        if (repeated) throw CompileError("wildcard metadata keys under an array pattern are not supported");
-        if (a.k != AK_NONE && a.k != AK_EQ && a.k != AK_ADD)
-          throw CompileError("wildcard condition/negation/existence/global anchors in metadata are not supported");
-      }
+      if (expanding && has_glob(kv.first) && repeated)  // the reference rewrites the shared pattern per element
+        throw CompileError("wildcard metadata keys under an array pattern are not supported");
       if (phase1(a.k)) first.push_back(kv.first);
+    }
+    if (expanding) {
+      // anchored glob keys are expanded per resource (wildcards.go:145-162) and the anchor phase
+      // / global members run in the sorted order of the expanded keys (validate.go:118-175): the
+      // order of the compile-time keys is the same unless another such member's key starts with
+      // the glob key's literal prefix
+      for (auto& kv : v.o) {
+        const AK ka = anchor_of(kv.first).k;
+        if (!has_glob(kv.first) || (!phase1(ka) && ka != AK_GLOBAL)) continue;
+        const std::string pre = kv.first.substr(0, kv.first.find_first_of("*?"));
+        for (auto& other : v.o) {
+          const AK ko = anchor_of(other.first).k;
+          if (&other == &kv || (phase1(ka) ? !phase1(ko) : ko != AK_GLOBAL)) continue;
+          if (other.first.compare(0, pre.size(), pre) == 0)
+            throw CompileError("anchored wildcard metadata keys whose expansion can reorder the anchors");
+        }
+      }
     }
     std::sort(first.begin(), first.end());
     std::vector<std::string> rest;
@@ -852,11 +868,9 @@ class PatCompiler {
       if (h != PM_DEFAULT) name = a.key;
       if (h == PM_COND || h == PM_EXIST) {
         auto it = slots_.find(k);
-        if (it == slots_.end()) {
-          if (slots_.size() >= 32) throw CompileError("more than 32 condition/existence anchors in one pattern");
-          it = slots_.emplace(k, (uint32_t)slots_.size()).first;
-        }
-        flags |= PMF_SLOT, slot = it->second;
+        if (it == slots_.end()) it = slots_.emplace(k, (uint32_t)slots_.size()).first;
+        if (it->second < 32) flags |= PMF_SLOT, slot = it->second;
+        else flags |= PMF_XSLOT;
       }
       if (h == PM_DEFAULT && val.t == JV::Str && val.s == "*") flags |= PMF_STAR;
       if (expanding && has_glob(k) && a.k != AK_ADD) {  // "+(...)" keys stay verbatim
@@ -2524,7 +2538,8 @@ class Lowerer {
         }
       }
       const uint32_t nf = (uint32_t)P.filters.size() - f0;
-      if (f0 > 0xFFFFFu || nf > 0x3FFu) throw CompileError("rule '" + rname + "': too many PolicyException filters");
+      static_assert(((XE_PRESENT | XE_ALL | XE_PSS) & (0x1FFu << 20 | 0xFFFFFu)) == 0, "KpeRule::exc fields overlap");
+      if (f0 > 0xFFFFFu || nf > 0x1FFu) throw CompileError("rule '" + rname + "': too many PolicyException filters");
       if (xpss) {
         x |= XE_PSS;
         pss_exception(*with_pss->pss, (uint32_t)r, P.rules[r].cv_mask, "PolicyException " + with_pss->key);

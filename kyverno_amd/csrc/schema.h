@@ -381,7 +381,7 @@ typedef struct KpeRule {
 #define XE_PSS (1u << 29)  // the rule's (single) exception has podSecurity controls: a failing PSS
                            // cell becomes KPE_XFAIL_ instead of RuleSkip (ApplyPodSecurityExclusion)
 #define XE_F0(x) ((x) & 0xFFFFFu)
-#define XE_NF(x) (((x) >> 20) & 0x3FFu)
+#define XE_NF(x) (((x) >> 20) & 0x1FFu)  // bits 20..28 (XE_PSS is bit 29)
 
 // ---- podSecurity.exclude (pkg/pss/evaluate.go:72-317), evaluated by kpe_pssx_kernel ----------
 // A PSA field error is keyed by its field path with digit runs replaced by "*": a suffix
@@ -527,6 +527,8 @@ typedef struct KpePNode {
 #define PMF_VSTAR (1u << 7)  // default-handler member whose leaf has variables: a value of "*"
                              // is the presence check (anchor/handlers.go:130-133)
 #define PM_SLOT(x) (((x) >> 8) & 31u)
+#define PMF_XSLOT (1u << 13)  // condition / existence anchor past the 32 AnchorMap slots: a map
+                              // holding it makes the cell KPE_UNDECIDED
 // Leaf
 #define PL_BOOL 0u
 #define PL_INT 1u

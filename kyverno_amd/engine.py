@@ -257,8 +257,13 @@ class Engine:
             check(load().kpe_fetch_cv_masks(self.device.h, ps.h, corpus.h, m.ctypes.data))
         return m
 
-    def evaluate_async(self, ps: PolicySet, corpus: Corpus):
-        check(load().kpe_evaluate_async(self.device.h, ps.h, corpus.h))
+    def evaluate_async(self, ps: PolicySet, corpus: Corpus, masks=False, cold=False):
+        """Enqueue one evaluation (results stay on the device). masks: also write the check masks;
+        cold: re-run the per-corpus prologue (dictionary pass, prologue image)."""
+        if not masks and not cold:
+            check(load().kpe_evaluate_async(self.device.h, ps.h, corpus.h))
+        else:
+            check(load().kpe_evaluate_async_ex(self.device.h, ps.h, corpus.h, (1 if masks else 0) | (2 if cold else 0)))
 
     # ---- reference-shaped API ----
     def validate_batch(self, policies: Sequence[dict], resources: Sequence[dict],

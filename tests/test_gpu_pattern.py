@@ -118,6 +118,10 @@ def edge_case_inputs(n=3000, seed=5):
         {"spec": {"^(containers)": [{"name": "sidecar-*"}], "X(hostNetwork)": "null"}},
         {"spec": {"<(priority)": 5, "containers": [{"(image)": "*:latest", "imagePullPolicy": "Always"}]}},
         {"metadata": {"labels": {"app*": "?*", "=(tier)": "front* | back*"}}},
+        # anchored glob keys, expanded per resource (wildcards.go:145-162)
+        {"metadata": {"labels": {"(app.kubernetes.io/*)": "web-* | 3", "tier": "?*"}}},
+        {"metadata": {"labels": {"X(team*)": "null", "=(ti?r)": "front* | 1*"}}},
+        {"metadata": {"annotations": {"<(owner*)": "team-*"}, "labels": {"=(app*)": "x | 2"}}},
         {"spec": {"values": [1.5], "flags": [True], "empty": [], "pos": [[1], [2]]}},
         {"spec": {"n": None, "z": 0, "s": "", "f": 0.0}},
     ]
@@ -142,9 +146,11 @@ def edge_case_inputs(n=3000, seed=5):
             ctrs.append(c)
         if rng.random() < 0.8:
             spec["containers"] = ctrs
-        labels = {k: str(pick()) for k in rng.choice(["app", "app.kubernetes.io/name", "tier", "x"], 2)}
-        docs.append({"apiVersion": "v1", "kind": "Thing", "metadata": {"name": f"d{i}", "labels": labels},
-                     "spec": spec})
+        labels = {k: str(pick()) for k in rng.choice(["app", "app.kubernetes.io/name", "tier", "x", "team-a"], 2)}
+        meta = {"name": f"d{i}", "labels": labels}
+        if rng.random() < 0.5:
+            meta["annotations"] = {rng.choice(["owner", "owner-b", "y"]): rng.choice(["team-a", "x", ""])}
+        docs.append({"apiVersion": "v1", "kind": "Thing", "metadata": meta, "spec": spec})
     return pols, "\n".join(json.dumps(d) for d in docs).encode()
 
 
@@ -157,3 +163,19 @@ def test_pattern_edge_documents(oracle):
     bad = np.argwhere(v != ref)
     assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()} " \
                           f"gpu={[int(v[i, j]) for i, j in bad[:5]]} ref={[int(ref[i, j]) for i, j in bad[:5]]}"
+
+
+def test_anchored_glob_metadata_keys_compile():
+    """Anchored glob keys in labels / annotations compile (ExpandInMetadata, wildcards.go:145-162)
+    unless another anchor-phase key starts with the glob's literal prefix: the anchors then run in
+    the sorted order of the per-resource expansions, which the compile-time order may not be."""
+    ok = [{"metadata": {"labels": {"(app.kubernetes.io/*)": "web-*", "tier": "?*"}}},
+          {"metadata": {"labels": {"X(team*)": "null", "=(tier)": "a"}}},
+          {"metadata": {"annotations": {"<(owner*)": "team-*"}}}]
+    for p in ok:
+        K.PolicySet([_policy_for("ok", p)])
+    bad = {"metadata": {"labels": {"(app*)": "x", "(app.kubernetes.io/name)": "y"}}}
+    with pytest.raises(K.KpeError):
+        K.PolicySet([_policy_for("bad", bad)])
+    with pytest.raises(K.KpeError):  # glob keys under an array pattern: the reference rewrites the shared pattern
+        K.PolicySet([_policy_for("arr", {"items": [{"metadata": {"labels": {"app*": "x"}}}]})])

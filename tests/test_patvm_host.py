@@ -63,3 +63,40 @@ def test_patvm_host_matches_oracle(harness, oracle, tmp_path, name, pols, nd):
     applied = (ref != 0) & ~(ref == 7).all(axis=1, keepdims=True)
     bad = np.argwhere((v != ref) & applied)
     assert bad.size == 0, f"{len(bad)} cells differ, first {bad[:5].tolist()}"
+
+
+def _nest(depth, leaf):
+    v = leaf
+    for _ in range(depth):
+        v = {"a": v}
+    return v
+
+
+def test_caps_are_undecided_cells(harness, oracle, tmp_path):
+    """Past the lane's frame stack (pattern and resource both nested deeper) or past the 32
+    AnchorMap slots, a cell is KPE_UNDECIDED (7) instead of the policy being refused; every
+    other cell stays bit-exact."""
+    deep = _policy_for("deep", {"spec": _nest(16, {"x": "1"})})
+    many = _policy_for("many", {"spec": {**{f"(k{i})": "v*" for i in range(34)}, "x": "?*"}})
+    docs = []
+    for i in range(40):
+        spec = _nest(16, {"x": str(i % 3)}) if i % 4 == 0 else ({"a": "flat"} if i % 4 == 1 else None)
+        d = {"apiVersion": "v1", "kind": "Thing", "metadata": {"name": f"d{i}"}}
+        if spec is not None:
+            d["spec"] = dict(spec, **({f"k{j}": "v1" for j in range(i % 5)} if i % 4 == 1 else {}))
+        docs.append(d)
+    nd = "\n".join(json.dumps(d) for d in docs).encode()
+    pols = [deep, many]
+    pj, rj, vb = tmp_path / "p.json", tmp_path / "r.ndjson", tmp_path / "v.bin"
+    pj.write_text(json.dumps(pols))
+    rj.write_bytes(nd)
+    r = subprocess.run([harness, str(pj), str(rj), str(vb)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+    ref = oracle.validate(pols, nd)
+    v = np.fromfile(vb, dtype=np.uint8).reshape(ref.shape)
+    und = v == 7
+    assert (v[~und] == ref[~und]).all()
+    deep_rows = np.array([i % 4 == 0 for i in range(len(docs))])
+    assert und[:, 0].tolist() == deep_rows.tolist()  # only resources as deep as the pattern
+    has_spec = np.array([d.get("spec") is not None for d in docs])
+    assert und[:, 1].tolist() == has_spec.tolist()  # any resource whose spec map is visited
