@@ -160,6 +160,9 @@ struct ScanArgs {
   uint32_t pimg_words, capb_lds;
   // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask (PRED_NONE: no table)
   uint32_t kt_lds, nkinds;
+  // LEAN4 tile slabs (DeviceCorpus::slab_*): tile t's first K items of a list at [t * K, t * K + K)
+  const uint32_t *slab_c, *slab_v, *slab_s, *slab_a;
+  uint32_t kc, kv, ks, ka;
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null

@@ -215,6 +215,10 @@ struct DeviceCorpus {
   DevBuf ctr_off, vol_off, sys_off, pann_off, c_name, c_image, c_sann_key, c_sec_str, c_pm_str, c_selt_str, c_selu_str,
       c_selr_str, cport_off, cport_str, pann_k, pann_v, p_cold;
   bool cold = false;
+  // LEAN4 tile slabs (kpe_lean4_kernel): tile t's first K items of each list at [t * K, t * K + K)
+  DevBuf slab_c, slab_v, slab_s, slab_a;
+  uint32_t kc = 0, kv = 0, ks = 0, ka = 0;
+  bool slabs = false;
   Binding bind;
   bool has_masks = false;
 };
@@ -629,6 +633,55 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   return need;
 }
+// kpe_lean4_kernel's tile slabs: per list, K = the 99.5th percentile of the per-tile item counts
+// (a multiple of 8, at least 8, at most the wave's staging capacity), and tile t's first
+// min(count, K) items copied to [t * K, ...), zero padded. Items past K stay in the CSR columns
+// (the kernel loads them at header offsets). Built once per corpus, on the host.
+kpe_status build_slabs(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
+  if (D.slabs) return KPE_OK;
+  const size_t nt = (size_t)((C.n + 63) / 64);
+  if (nt == 0) return KPE_OK;  // nothing is launched over an empty corpus
+  auto one = [&](int word, uint32_t cap, uint32_t width, const uint32_t* col, DevBuf& out, uint32_t* K) -> hipError_t {
+    std::vector<uint32_t> cnt(nt);
+    for (size_t t = 0; t < nt; ++t) cnt[t] = C.hdr[4 * (t + 1) + word] - C.hdr[4 * t + word];
+    std::vector<uint32_t> srt(cnt);
+    const size_t q = std::min(nt - 1, (size_t)((double)nt * 0.995));
+    std::nth_element(srt.begin(), srt.begin() + q, srt.end());
+    uint32_t k = nt ? (srt[q] + 7u) / 8u * 8u : 8u;
+    k = std::max(8u, std::min(cap, k));
+    *K = k;
+    std::vector<uint32_t> slab(nt * k * width + width, 0u);
+    for (size_t t = 0; t < nt; ++t) {
+      const uint32_t first = C.hdr[4 * t + word], m = std::min(cnt[t], k);
+      if (m) memcpy(&slab[t * k * width], col + (size_t)first * width, (size_t)m * width * 4);
+    }
+    return upload(out, slab, s);
+  };
+  HIPCHK(one(0, KPE_STAGE_CTR, 2, C.crec.data(), D.slab_c, &D.kc));
+  HIPCHK(one(1, KPE_STAGE_VOL, 1, C.vol_src.data(), D.slab_v, &D.kv));
+  HIPCHK(one(2, KPE_STAGE_SMALL, 1, C.sys_id.data(), D.slab_s, &D.ks));
+  HIPCHK(one(3, KPE_STAGE_SMALL, 2, C.pann_kv.data(), D.slab_a, &D.ka));
+  D.slabs = true;
+  return KPE_OK;
+}
+// bytes of one kpe_lean4_kernel launch: records, headers, every slab slot, the items past K
+double lean4_bytes(const kpe::Program& P, const kpe::Corpus& C, const kpe::DeviceCorpus& D, uint32_t need) {
+  const size_t nt = (size_t)((C.n + 63) / 64);
+  double b = 16.0 * (double)C.n + 16.0 * (double)nt + (double)C.n * (double)P.rules.size();
+  auto list = [&](int word, uint32_t k, double width) {
+    double over = 0;
+    for (size_t t = 0; t < nt; ++t) {
+      const uint32_t c = C.hdr[4 * (t + 1) + word] - C.hdr[4 * t + word];
+      if (c > k) over += c - k;
+    }
+    return width * ((double)nt * k + over);
+  };
+  b += list(0, D.kc, 8.0);
+  if (need & NEED_VOL) b += list(1, D.kv, 4.0);
+  if (need & NEED_SYS) b += list(2, D.ks, 4.0);
+  if (need & NEED_PANN) b += list(3, D.ka, 8.0);
+  return b;
+}
 double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
   double b = 0;
   const double n = (double)C.n;
@@ -939,7 +992,12 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
                              (uint64_t)C.c_sc.size() * 8 > lim || (uint64_t)C.vol_src.size() * 4 > lim ||
                              (uint64_t)C.sys_id.size() * 4 > lim || (uint64_t)C.pann_kv.size() * 4 > lim)
                                 ? 2
-                                : getenv("KPE_LEAN_PERSIST") ? 3 : 4;
+                                : getenv("KPE_LEAN_PERSIST") ? 3 : getenv("KPE_LEAN3") ? 4 : getenv("KPE_LEAN4_T2") ? 6 : 5;
+  if (B.lean_kind >= 5) {
+    const uint64_t slab_bytes = (uint64_t)((C.n + 63) / 64) * KPE_STAGE_CTR * 8;
+    if (slab_bytes > lim) B.lean_kind = 4;
+    else if (kpe_status st = build_slabs(C, *cc->d, s)) return st;
+  }
   B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   {  // ApplyOne policies: contiguous rule ranges in ComputeRules order
@@ -1098,6 +1156,11 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
   sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
+  if (D.slabs) {
+    sa.slab_c = D.slab_c.as<uint32_t>(), sa.slab_v = D.slab_v.as<uint32_t>();
+    sa.slab_s = D.slab_s.as<uint32_t>(), sa.slab_a = D.slab_a.as<uint32_t>();
+    sa.kc = D.kc, sa.kv = D.kv, sa.ks = D.ks, sa.ka = D.ka;
+  }
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   if (!B.args_valid || memcmp(&sa, &B.hargs, sizeof(ScanArgs)) != 0) {  // once per binding / masks mode
@@ -1285,7 +1348,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
-    ev.bytes = scan_bytes(P, C, B.need, masks);
+    ev.bytes = (B.lean && !masks && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) : scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     dev->pending.push_back(ev);
   }

@@ -596,3 +596,204 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean3_kernel(ScanArg
     __builtin_amdgcn_wave_barrier();
   }
 }
+
+// ---- kpe_lean4_kernel: one memory step per wave -------------------------------------------
+// kpe_lean3_kernel's waves wait on two dependent HBM round trips (pod records and tile header,
+// then the list items at header offsets), and 1M pods are ~2 generations of resident waves, so
+// the latency chain, not bandwidth, sets its time. Here every list is also laid out in tile
+// slabs (DeviceCorpus::slab_*: tile t's first K items at [t * K, (t + 1) * K), zero padded; K
+// per list from the corpus's per-tile counts), so the wave issues the pod records, the tile
+// header and its slab loads together: one round trip. The items are staged in LDS, a pod ORs its
+// range of slots, and only items past a tile's K (rare: K covers >= 99.5% of the tiles) are
+// loaded from the CSR columns at header offsets afterwards.
+struct Lean4Loads {
+  uint32_t hall;
+  uint4 rec;
+  uint2 c0, c1, q0;
+  uint32_t v0, v1, s0;
+};
+template <int T>
+__global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean4_kernel(ScanArgs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  if (KPE_DIAG & DIAG_EMPTY) return;
+  CArgs& a0 = *kargs();
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
+  const uint32_t tile0 = (xcd_block(blockIdx.x, gridDim.x) * (kLB / 64u) + wv) * (uint32_t)T;
+  const uint32_t need = a0.need;
+  const bool nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN;
+  const uint32_t kc = a0.kc, kv = nvol ? a0.kv : 0u, ks = nsys ? a0.ks : 0u, ka = npann ? a0.ka : 0u;
+  LeanCols L;
+  L.rec = make_rsrc(a0.rec, n * 16u);
+  L.hdr = make_rsrc(a0.hdr, (ntiles + 1u) * 16u);
+  L.crec = make_rsrc(a0.crec, a0.nctr_total * 8u);
+  L.vol = make_rsrc(a0.vol_src, nvol ? a0.nvol_total * 4u : 0u);
+  L.sys = make_rsrc(a0.sys_id, nsys ? a0.nsys_total * 4u : 0u);
+  L.ann = make_rsrc(a0.pann_kv, npann ? a0.npann_total * 8u : 0u);
+  const Rsrc SC = make_rsrc(a0.slab_c, ntiles * kc * 8u), SV = make_rsrc(a0.slab_v, ntiles * kv * 4u),
+             SS = make_rsrc(a0.slab_s, ntiles * ks * 4u), SA = make_rsrc(a0.slab_a, ntiles * ka * 8u);
+  constexpr uint32_t kOOB = 0xFFFFFFF0u;  // a range-checked load of 0
+
+  // ---- the one memory step: header words of this tile and the next, pod record, slab slots
+  // lane and lane + 64 of each list (slots past K read 0), the prologue image ----
+  Lean4Loads ld[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t tile = tile0 + (uint32_t)j;
+    Lean4Loads& d = ld[j];
+    d.hall = bload1(L.hdr, (tile * 4u + min(lane, 7u)) * 4u);
+    d.rec = bload4(L.rec, (tile * 64u + lane) * 16u);
+    d.c0 = bload2(SC, lane < kc ? (tile * kc + lane) * 8u : kOOB);
+    d.c1 = bload2(SC, lane + 64u < kc ? (tile * kc + 64u + lane) * 8u : kOOB);
+    d.v0 = bload1(SV, lane < kv ? (tile * kv + lane) * 4u : kOOB);
+    d.v1 = bload1(SV, lane + 64u < kv ? (tile * kv + 64u + lane) * 4u : kOOB);
+    d.s0 = bload1(SS, lane < ks ? (tile * ks + lane) * 4u : kOOB);
+    d.q0 = bload2(SA, lane < ka ? (tile * ka + lane) * 8u : kOOB);
+  }
+  const uint32_t img_n4 = a0.pimg_words >> 2;
+  const uint4* img = reinterpret_cast<const uint4*>(a0.pimg);
+  const uint4 img0 = img[min(t, img_n4 - 1u)];
+  uint32_t cls_cv = 0, cls_rm = 0;
+  if (lane < a0.ncls) {
+    const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
+    cls_cv = c.x, cls_rm = c.y;
+  }
+  {
+    uint4* d4 = reinterpret_cast<uint4*>(dyn);
+    if (t < img_n4) d4[t] = img0;
+#pragma unroll 1
+    for (uint32_t i = t + kLB; i < img_n4; i += kLB) d4[i] = img[i];
+  }
+  __syncthreads();
+  const uint8_t* s_capb = reinterpret_cast<const uint8_t*>(dyn + a0.capb_lds);
+  const LdsPtr lds = (LdsPtr)dyn;
+  const uint32_t p_sann = a0.pp_seccomp_ann_ok & ~PRED_LOCAL, p_aak = a0.pp_apparmor_key & ~PRED_LOCAL,
+                 p_aao = a0.pp_apparmor_ok & ~PRED_LOCAL, p_spk = a0.pp_seccomp_pod_key & ~PRED_LOCAL,
+                 p_s0 = a0.pp_sysctl0 & ~PRED_LOCAL, p_s1 = a0.pp_sysctl1 & ~PRED_LOCAL,
+                 p_s2 = a0.pp_sysctl2 & ~PRED_LOCAL;
+  auto pbit = [&](uint32_t loc, uint32_t id) -> uint32_t { return (lds[loc + (id >> 5)] >> (id & 31u)) & 1u; };
+  const uint32_t R = a0.nrules, cv_union = a0.cv_union, pss_rules = a0.pss_rules, ncls = a0.ncls;
+  const uint32_t ep_rules = a0.err_rules | a0.pat_rules, pat_rules = a0.pat_rules;
+  uint32_t* const stage = dyn + a0.wave_lds + wv * a0.wave_words;
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t tile = tile0 + (uint32_t)j;
+    if (tile >= ntiles) break;
+    const uint32_t hall = ld[j].hall;
+    const uint4 rec = ld[j].rec;
+    const uint2 c0 = ld[j].c0, c1 = ld[j].c1, q0 = ld[j].q0;
+    const uint32_t v0 = ld[j].v0, v1 = ld[j].v1, s0 = ld[j].s0;
+    const uint32_t C0 = hw(hall, 0), V0 = hw(hall, 1), S0 = hw(hall, 2), A0 = hw(hall, 3);
+    const uint32_t nct = hw(hall, 4) - C0, nvt = hw(hall, 5) - V0, nst = hw(hall, 6) - S0, nat = hw(hall, 7) - A0;
+    const uint32_t r = tile * 64u + lane;
+    const bool live = r < n;
+    // ---- the pod's slots: exclusive wave scans of its packed counts ----
+    const uint32_t z = rec.z;  // 0 for rows past n (range-checked load)
+    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+    uint32_t oc, ov, os, oa;
+    if ((nct | nvt | nst | nat) < 256u) {  // one scan of the four packed byte counts (no carries)
+      const uint32_t e = wave_incl_scan(z) - z;
+      oc = e & 0xFFu, ov = (e >> 8) & 0xFFu, os = (e >> 16) & 0xFFu, oa = e >> 24;
+    } else {
+      const uint32_t c01 = nc | (nv << 16), c23 = ns | (na << 16);
+      const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
+      oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
+    }
+    // ---- stage the slab slots' codes (slots past the tile's items hold padding no pod reads) ----
+    uint2* sc = reinterpret_cast<uint2*>(stage);
+    uint8_t* sbv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_CTR * 2);
+    uint8_t* sbs = sbv + KPE_STAGE_VOL;
+    uint8_t* sba = sbs + KPE_STAGE_SMALL;
+    auto ctr_code = [&](uint2 e) { return make_uint2(e.x, e.x ? (uint32_t)s_capb[CY_CAPSET(e.y)] : 0u); };
+    auto vol_code = [&](uint32_t sv0) -> uint32_t { return ((sv0 >> VS_HOSTPATH) & 1u) | ((sv0 & kAllowedVolumes) ? 0u : 2u); };
+    auto sys_code = [&](uint32_t id) -> uint32_t {
+      return (pbit(p_s0, id) ^ 1u) | ((pbit(p_s1, id) ^ 1u) << 1) | ((pbit(p_s2, id) ^ 1u) << 2);
+    };
+    auto ann_code = [&](uint2 kv2) -> uint32_t {
+      return (pbit(p_aak, kv2.x) & (pbit(p_aao, kv2.y) ^ 1u)) | ((pbit(p_spk, kv2.x) & (pbit(p_sann, kv2.y) ^ 1u)) << 1);
+    };
+    sc[lane] = ctr_code(c0);
+    sc[lane + 64u] = ctr_code(c1);
+    if (nvol) sbv[lane] = (uint8_t)vol_code(v0), sbv[lane + 64u] = (uint8_t)vol_code(v1);
+    if (nsys && nst) sbs[lane] = (uint8_t)sys_code(s0);
+    if (npann && nat) sba[lane] = (uint8_t)ann_code(q0);
+    __builtin_amdgcn_wave_barrier();
+    // ---- each pod ORs its first slots with fixed clamped reads (a repeated slot does not change
+    // an OR); pods without items of a list mask the read off ----
+    uint32_t xo, co, vcode = 0, scode = 0, acode = 0;
+    {
+      const uint32_t last = min(oc + (nc ? nc - 1u : 0u), kc - 1u);
+      const uint2 e0 = sc[min(oc, last)], e1 = sc[min(oc + 1u, last)], e2 = sc[min(oc + 2u, last)],
+                  e3 = sc[min(oc + 3u, last)];
+      const uint32_t m = (nc && oc < kc) ? ~0u : 0u;
+      xo = (e0.x | e1.x | e2.x | e3.x) & m;
+      co = (e0.y | e1.y | e2.y | e3.y) & m;
+    }
+    if (nvol) {
+      const uint32_t last = min(ov + (nv ? nv - 1u : 0u), kv - 1u);
+      const uint32_t x = (uint32_t)sbv[min(ov, last)] | sbv[min(ov + 1u, last)] | sbv[min(ov + 2u, last)] |
+                         sbv[min(ov + 3u, last)];
+      vcode = (nv && ov < kv) ? x : 0u;
+    }
+    if (nsys && nst) {
+      const uint32_t last = min(os + (ns ? ns - 1u : 0u), ks - 1u);
+      const uint32_t x = (uint32_t)sbs[min(os, last)] | sbs[min(os + 1u, last)];
+      scode = (ns && os < ks) ? x : 0u;
+    }
+    if (npann && nat) {
+      const uint32_t last = min(oa + (na ? na - 1u : 0u), ka - 1u);
+      const uint32_t x = (uint32_t)sba[min(oa, last)] | sba[min(oa + 1u, last)];
+      acode = (na && oa < ka) ? x : 0u;
+    }
+    // ---- pods with more items than the fixed reads cover, or whose items run past the tile's
+    // slab: recomputed over all their items (slab slots from LDS, the rest from the CSR columns) ----
+    const bool over = nct > kc || (nvol && nvt > kv) || (nsys && nst > ks) || (npann && nat > ka);
+    const bool more_c = nc > 4u, more_v = nvol && nv > 4u, more_s = nsys && ns > 2u, more_a = npann && na > 2u;
+    if (over || __builtin_amdgcn_ballot_w64(more_c || more_v || more_s || more_a)) {
+      if (more_c || oc + nc > kc) {
+        xo = co = 0;
+        for (uint32_t k = oc; k < oc + nc; ++k) {
+          const uint2 e = k < kc ? sc[k] : ctr_code(bload2(L.crec, (C0 + k) * 8u));
+          xo |= e.x, co |= e.y;
+        }
+      }
+      if (nvol && (more_v || ov + nv > kv)) {
+        vcode = 0;
+        for (uint32_t k = ov; k < ov + nv; ++k) vcode |= k < kv ? (uint32_t)sbv[k] : vol_code(bload1(L.vol, (V0 + k) * 4u));
+      }
+      if (nsys && (more_s || os + ns > ks)) {
+        scode = 0;
+        for (uint32_t k = os; k < os + ns; ++k) scode |= k < ks ? (uint32_t)sbs[k] : sys_code(bload1(L.sys, (S0 + k) * 4u));
+      }
+      if (npann && (more_a || oa + na > ka)) {
+        acode = 0;
+        for (uint32_t k = oa; k < oa + na; ++k)
+          acode |= k < ka ? (uint32_t)sba[k] : ann_code(bload2(L.ann, (A0 + k) * 8u));
+      }
+    }
+    // ---- PSA checks, rule match (kind table), verdict bytes stored straight from the lane ----
+    const uint32_t pw = rec.x;
+    const uint32_t fails = cv_fails(pw, xo, co & 7u, false, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & cv_union;
+    const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
+    const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
+    const uint32_t matched = dyn[a0.kt_lds + GVK_KIND(rec.y)];
+    uint32_t failr;
+    if (ncls == 1u) {
+      failr = (fails & hw(cls_cv, 0)) ? hw(cls_rm, 0) : 0u;
+    } else {
+      failr = 0;
+  #pragma unroll 1
+      for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+    }
+    const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
+    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
+    const uint32_t P = matched & pss_rules & ~failr & ~E;
+    if (live && !(KPE_DIAG & DIAG_NOSTORE)) {
+      uint8_t* row = a0.verdicts + (size_t)r * R;
+  #pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri)
+        row[ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    }
+    __builtin_amdgcn_wave_barrier();  // the next tile reuses the staging area
+  }
+}

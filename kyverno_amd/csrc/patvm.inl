@@ -241,6 +241,9 @@ __device__ __forceinline__ bool leaf_nil(const KpeScalar* v, uint32_t vf) {  // 
 __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li, const uint2* pv, uint32_t* und) {
   if (sid == kNoNode) return false;  // no scalar validator accepts a map / list
   const KpeLeaf* L = a.leaves + PV(li, a.nleaves, 4);
+#if defined(DIAG_PATLEAF) && (KPE_DIAG & DIAG_PATLEAF)
+  if (L->type != PL_VAR && L->type != PL_TMPL) return sid != 0xFFFFFFFEu;  // every leaf holds
+#endif
   const KpeScalar* v = a.scal + PV(sid, a.nscal, 7);
   const uint32_t vf = v->flags, t = SC_TYPE(vf);
   if (L->type == PL_VAR) {  // the variable's typed value is the pattern (context numbers: float64)

@@ -127,6 +127,21 @@ std::string selector_labels(Rng& r) {
 // C5: irregular fan-out pods for the require-pod-requests-limits /
 // disallow-latest-tag / disallow-host-ports pattern set. Container counts follow a geometric
 // law of mean ~6 truncated to [1, 64] (redrawn above 64).
+// 64 lowercase hex digits derived from x (splitmix64 rounds): a valid sha256 digest string
+// (go-digest), so the images context of the row builds (AddImageInfos, context.go:293-330)
+std::string hex_digest(uint64_t x) {
+  static const char* hx = "0123456789abcdef";
+  std::string d;
+  for (int k = 0; k < 4; ++k) {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    z ^= z >> 31;
+    for (int i = 0; i < 16; ++i) d += hx[(z >> (4 * i)) & 15u];
+  }
+  return d;
+}
+
 void gen_fanout(std::string& o, Rng& r, int64_t idx) {
   auto count = [&]() {
     for (;;) {
@@ -144,7 +159,7 @@ void gen_fanout(std::string& o, Rng& r, int64_t idx) {
     if (t < 0.45) s += img + ":1." + std::to_string(r.below(30)) + "." + std::to_string(r.below(10));
     else if (t < 0.65) s += img + ":latest";
     else if (t < 0.80) s += img;  // no tag
-    else if (t < 0.90) s += img + "@sha256:" + std::to_string(1000000 + r.below(1000000));
+    else if (t < 0.90) s += img + "@sha256:" + hex_digest(1000000 + r.below(1000000));  // a well-formed digest
     else s += "ghcr.io/org-" + std::to_string(r.below(9)) + "/" + img + (r.p(0.5) ? ":2.0" : ":latest");
     s += "\"";
     const double pp = r.u();

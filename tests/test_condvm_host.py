@@ -85,3 +85,40 @@ def test_condvm_host_chart(condvm_bin, oracle, tmp_path):
     bad = np.argwhere(out != ref)
     assert bad.size == 0, (bad[:5].tolist(), [int(out[i, j]) for i, j in bad[:5]], [int(ref[i, j]) for i, j in bad[:5]])
     assert {1, 2} <= set(np.unique(out).tolist())
+
+
+def test_condvm_host_chart_on_c5(condvm_bin, oracle, tmp_path):
+    """The chart's deny / foreach rules over the C5 fan-out corpus (Pods / Deployments with 1-64
+    containers): lists longer than the VM's CV_LIST_CAP give KPE_UNDECIDED cells, handed back to
+    the caller; every other cell is bit-exact. Prints the undecided fraction."""
+    chart = json.load(open(os.path.join(ROOT, "tests", "golden", "chart_policies.json")))
+    pols = [p for p in chart["baseline"] + chart["restricted"]
+            if any("deny" in r.get("validate", {}) or "foreach" in r.get("validate", {}) for r in p["spec"]["rules"])]
+    names = oracle.rule_names(pols)
+    nd = K.synth_resources(0xC5, 4000, mix=K.SYNTH_FANOUT)
+    lines = [l for l in nd.split(b"\n") if l]
+    kinds = [json.loads(l)["kind"] for l in lines]
+    ref = oracle.validate(pols, nd, nthreads=8)
+    N, R = ref.shape
+    ctrl = {"DaemonSet", "Deployment", "Job", "StatefulSet", "ReplicaSet", "ReplicationController"}
+    seedm = np.zeros((N, R), dtype=np.uint8)
+    for j, n in enumerate(names):
+        rule = n.split("/", 1)[1]
+        ks = {"CronJob"} if rule.startswith("autogen-cronjob-") else ctrl if rule.startswith("autogen-") else {"Pod"}
+        seedm[:, j] = [6 if k in ks else 0 for k in kinds]
+    (tmp_path / "p.json").write_text(json.dumps(pols))
+    (tmp_path / "r.ndjson").write_bytes(b"\n".join(lines))
+    (tmp_path / "seed.bin").write_bytes(seedm.tobytes())
+    subprocess.check_call([condvm_bin, str(tmp_path / "p.json"), str(tmp_path / "r.ndjson"),
+                           str(tmp_path / "seed.bin"), str(tmp_path / "out.bin")])
+    out = np.frombuffer((tmp_path / "out.bin").read_bytes(), dtype=np.uint8).reshape(N, R)
+    # rows whose policy context fails (an invalid image: every oracle cell 7, KPE_ROW_CONTEXT_ERROR
+    # on the device) are not the condition VM's
+    ctx = (ref == 7).all(axis=1, keepdims=True)
+    und = (out == 7) & ~ctx
+    applied = (ref != 0) & ~ctx
+    bad = np.argwhere((out != ref) & ~und & ~ctx)
+    assert bad.size == 0, (bad[:5].tolist(), [int(out[i, j]) for i, j in bad[:5]], [int(ref[i, j]) for i, j in bad[:5]])
+    frac = und.sum() / max(1, applied.sum())
+    print(f"C5 chart deny/foreach: {und.sum()} undecided of {applied.sum()} applicable cells ({frac:.4%})")
+    assert frac < 0.01
