@@ -59,7 +59,7 @@ def main():
     import torch.distributed as dist
 
     import kyverno_amd as K
-    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, gather_rows, max_over_ranks
+    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, gather_packed, max_over_ranks
     from tests.policies import c3_policy_set, c4_policy_set, c5_policy_set, restricted_latest
 
     cfg = args.config
@@ -149,16 +149,18 @@ def main():
     barrier()
     elapsed = max_over_ranks(elapsed, device=coll_dev)
     # the exchanges, after the timed region: per-rule totals (R x 7 u64, one RCCL all-reduce over
-    # xGMI) and the verdict rows of each rank's first shard gathered to rank 0 (grouped RCCL
-    # point-to-point: one send per rank, all receives posted together on rank 0)
+    # xGMI) and the verdict matrix of each rank's first shard, packed on its GPU to 3-bit cells
+    # and sent from HBM to rank 0 (grouped RCCL point-to-point: one send per rank, all receives
+    # posted together on rank 0, unpacked there)
     totals = allreduce_counts(totals, device=coll_dev)
-    v0, _, _ = eng.evaluate(ps, corpora[0])
+    eng.evaluate_async(ps, corpora[0])
+    eng.device.sync()
     barrier()
     t1 = time.perf_counter()
-    full = gather_rows(v0, n * world, dst=0, device=coll_dev)
+    full = gather_packed(eng, ps, corpora[0], n * world, dst=0, device=coll_dev)
     torch.cuda.synchronize()
     gather_s = max_over_ranks(time.perf_counter() - t1, device=coll_dev)
-    gather = {"rows": n * world, "bytes": n * world * R, "seconds": gather_s,
+    gather = {"rows": n * world, "bytes": 4 * K.packed_words(n * R) * world, "cell_bits": 3, "seconds": gather_s,
               "rows_ok": bool(rank != 0 or (full is not None and full.shape == (n * world, R)))}
 
     # ---- per-kernel timing pass: HIP events on the library's stream, launches serialised on

@@ -176,6 +176,27 @@ kpe_status kpe_device_sync(kpe_device* dev);
 kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
                      uint32_t* check_masks, kpe_counts* counts);
 
+/* ---- verdict exchange and several devices in one process ---------------- */
+/* Device address and size of the corpus's N x R verdict matrix after an evaluation of prog on
+ * dev (waits for it): valid until the next evaluation of the corpus. A collective can send it
+ * straight from HBM (RCCL over xGMI); SURVEY.md 8(e)'s verdict gather. */
+kpe_status kpe_device_verdicts(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, void** dptr,
+                               uint64_t* bytes);
+/* The verdict matrix packed on the device into 3-bit cells (the kpe_verdict alphabet fits),
+ * 10 per 32-bit word, row-major: cell i is bits 3*(i % 10) .. +2 of word i / 10. dst_dev is
+ * device memory of dev holding at least kpe_packed_words(N * R) words (e.g. a torch tensor
+ * that RCCL then sends); synchronous. kpe_unpack_verdicts expands it on the host. */
+uint64_t kpe_packed_words(uint64_t cells);
+kpe_status kpe_pack_verdicts(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint32_t* dst_dev,
+                             uint64_t words);
+kpe_status kpe_unpack_verdicts(const uint32_t* packed, uint64_t cells, uint8_t* out);
+/* One logical corpus sharded over several devices of this process: shards[i] uploaded to
+ * devs[i] (distinct devices), evaluated concurrently; verdicts = the shards' rows in order
+ * (sum of N_i x R bytes, may be NULL), counts = the per-rule sums (R entries, may be NULL). The
+ * Go host's single-process multi-GPU entry. */
+kpe_status kpe_evaluate_sharded(kpe_device* const* devs, kpe_corpus* const* shards, int nshards,
+                                const kpe_program* prog, uint8_t* verdicts, kpe_counts* counts);
+
 /* PSA check id k (bit k of a check mask), e.g. "capabilities_restricted". */
 const char* kpe_pss_check_id(int k);
 int kpe_pss_num_checks(void);

@@ -18,6 +18,9 @@ from .engine import (  # noqa: F401
     Device,
     Engine,
     EngineResponse,
+    evaluate_sharded,
+    packed_words,
+    unpack_verdicts,
     PolicyContext,
     PolicySet,
     RuleResponse,

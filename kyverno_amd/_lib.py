@@ -72,6 +72,12 @@ def load():
     L.kpe_evaluate_async.argtypes = [vp, vp, vp]
     L.kpe_evaluate_async_ex.argtypes = [vp, vp, vp, ctypes.c_uint]
     L.kpe_device_sync.argtypes = [vp]
+    L.kpe_device_verdicts.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
+    L.kpe_packed_words.argtypes = [ctypes.c_uint64]
+    L.kpe_packed_words.restype = ctypes.c_uint64
+    L.kpe_pack_verdicts.argtypes = [vp, vp, vp, vp, ctypes.c_uint64]
+    L.kpe_unpack_verdicts.argtypes = [vp, ctypes.c_uint64, vp]
+    L.kpe_evaluate_sharded.argtypes = [ctypes.POINTER(vp), ctypes.POINTER(vp), i32, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_fetch.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_pss_check_id.argtypes = [i32]
     L.kpe_pss_check_id.restype = cp

@@ -145,7 +145,8 @@ constexpr uint32_t kBlock = 256;
 #define DIAG_NOSTORE 64u  // (LEAN kernel) no verdict row stores
 #define DIAG_NOCV 128u    // (LEAN3) no PSA check logic: the OR-ed codes stand in for the failing checks
 #define DIAG_NOSTAGE 256u // (LEAN3) no list staging / per-pod OR: the lane's own first items stand in
-#define DIAG_PATLEAF 512u // (pattern VM) scalar leaves decided by a hash of (scalar, leaf): the walk alone
+#define DIAG_PATNOVM 512u // (pattern kernel) the rule loop without the VM: pending cells pass
+#define DIAG_PATLEAF 1024u // (pattern VM) every scalar leaf holds without evaluation: the walk alone
 constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
                                      (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
                                      (1u << VS_PROJECTED) | (1u << VS_SECRET);
@@ -1159,6 +1160,26 @@ namespace {
 __global__ void __launch_bounds__(128) kpe_pssx_kernel(const PssxArgs* __restrict__ ap) {
   const int64_t r = (int64_t)blockIdx.x * 128 + threadIdx.x;
   if (r < ap->n) pssx_eval_row(*ap, r);
+}
+
+// Verdict exchange (kpe_pack_verdicts): 3-bit cells, 10 per 32-bit word, row-major. One thread
+// per output word; neighbouring threads read neighbouring 10-byte runs (HBM-bound).
+__global__ void __launch_bounds__(256) kpe_pack3_kernel(const uint8_t* __restrict__ v, uint64_t cells,
+                                                        uint32_t* __restrict__ out, uint64_t words) {
+  const uint64_t w = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (w >= words) return;
+  const uint64_t c0 = w * 10u;
+  uint32_t x = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 10u; ++k)
+    if (c0 + k < cells) x |= (uint32_t)(v[c0 + k] & 7u) << (3u * k);
+  out[w] = x;
+}
+extern "C" hipError_t kpe_launch_pack3(const uint8_t* v, uint64_t cells, uint32_t* out, hipStream_t s) {
+  const uint64_t words = (cells + 9u) / 10u;
+  if (!words) return hipSuccess;
+  hipLaunchKernelGGL(kpe_pack3_kernel, dim3((unsigned)((words + 255u) / 256u)), dim3(256), 0, s, v, cells, out, words);
+  return hipGetLastError();
 }
 
 extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s) {

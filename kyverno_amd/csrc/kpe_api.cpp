@@ -34,6 +34,7 @@ extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const 
                                            uint8_t value, hipStream_t s);
 extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
 extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStream_t s);
+extern "C" hipError_t kpe_launch_pack3(const uint8_t* v, uint64_t cells, uint32_t* out, hipStream_t s);
 extern "C" hipError_t kpe_launch_apply_one(uint8_t* verdicts, uint32_t* masks, int64_t n, uint32_t R, const uint32_t* segs,
                                            uint32_t nsegs, hipStream_t s);
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* hargs, int64_t n, int pss, int narrow,
@@ -305,7 +306,7 @@ int kpe_program_rule_is_pss(const kpe_program* p, int r) {
 }
 void kpe_program_free(kpe_program* p) {
   if (p) {
-    delete p->p->dev;
+    for (auto* d : p->p->devs) delete d;
     delete p;
   }
 }
@@ -464,7 +465,8 @@ void append_words(std::vector<uint32_t>& img, const std::vector<T>& v, uint32_t*
 
 kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   auto& P = *pp->p;
-  if (P.dev && P.dev->ordinal == dev->ordinal) return KPE_OK;
+  if (dev->ordinal < 0 || dev->ordinal >= 16) return fail(KPE_E_DEVICE, "device ordinal past 15");
+  if (P.devs[dev->ordinal]) return KPE_OK;  // one copy per device: programs are shared across devices
   std::vector<uint32_t> lanes;  // rule lane records (kernels_abi.h RL_*)
   for (auto& r : P.rules) {
     if (r.match_nf > 255 || r.excl_nf > 255 || r.match_f0 > 0xFFFFFF || r.excl_f0 > 0xFFFFFF || r.cv_class > 0xFFF)
@@ -524,9 +526,8 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
       }
     }
   }
-  delete P.dev;
-  P.dev = new kpe::DeviceProgram();
-  auto& D = *P.dev;
+  P.devs[dev->ordinal] = new kpe::DeviceProgram();
+  auto& D = *P.devs[dev->ordinal];
   D.narrow = narrow;
   D.tt = tt;
   D.ncls = (uint32_t)cls.size() / 2;
@@ -710,7 +711,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   auto& P = *pp->p;
   auto& C = *cc->c;
   auto& B = cc->d->bind;
-  auto& PD = *P.dev;
+  auto& PD = *P.devs[dev->ordinal];
   size_t cells = (size_t)C.n * P.rules.size();
   if (B.prog == &P && B.cells == cells && (!want_masks || cc->d->has_masks)) return KPE_OK;
   if (B.last) HIPCHK(hipStreamSynchronize(B.last));  // no launch may still read what is rebuilt
@@ -1039,7 +1040,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   auto& P = *pp->p;
   auto& C = *cc->c;
   auto& D = *cc->d;
-  auto& PD = *P.dev;
+  auto& PD = *P.devs[dev->ordinal];
   auto& B = D.bind;
   // timed launches are serialised on stream 0 so each kernel's events measure it alone
   hipStream_t s = dev->timing || B.lane < 0 ? dev->stream : dev->lanes[B.lane];
@@ -1466,6 +1467,74 @@ kpe_status kpe_evaluate(kpe_device* dev, const kpe_program* prog, const kpe_corp
     if (st) return st;
   }
   return kpe_fetch(dev, prog, c, verdicts, masks, counts);
+}
+
+// ---- verdict exchange and multi-device evaluation --------------------------------------------
+kpe_status kpe_device_verdicts(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, void** dptr,
+                               uint64_t* bytes) {
+  if (!dev || !prog || !c || !c->d || !dptr) return fail(KPE_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& B = c->d->bind;
+  if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  if (B.last) HIPCHK(hipStreamSynchronize(B.last));
+  *dptr = B.verdicts.p;
+  if (bytes) *bytes = (uint64_t)c->c->n * prog->p->rules.size();
+  return KPE_OK;
+}
+
+uint64_t kpe_packed_words(uint64_t cells) { return (cells + 9u) / 10u; }
+
+kpe_status kpe_pack_verdicts(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint32_t* dst_dev,
+                             uint64_t words) {
+  if (!dev || !prog || !c || !c->d || !dst_dev) return fail(KPE_E_INVALID, "null argument");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& B = c->d->bind;
+  if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  const uint64_t cells = (uint64_t)c->c->n * prog->p->rules.size();
+  if (words < kpe_packed_words(cells)) return fail(KPE_E_INVALID, "packed buffer too small");
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, dst_dev) != hipSuccess || at.type != hipMemoryTypeDevice || at.device != dev->ordinal) {
+    (void)hipGetLastError();
+    return fail(KPE_E_INVALID, "dst_dev is not device memory of this device");
+  }
+  hipStream_t s = B.last ? B.last : dev->stream;
+  HIPCHK(kpe_launch_pack3(B.verdicts.as<uint8_t>(), cells, dst_dev, s));
+  HIPCHK(hipStreamSynchronize(s));
+  return KPE_OK;
+}
+
+kpe_status kpe_unpack_verdicts(const uint32_t* packed, uint64_t cells, uint8_t* out) {
+  if ((!packed || !out) && cells) return fail(KPE_E_INVALID, "null argument");
+  for (uint64_t i = 0; i < cells; ++i) out[i] = (uint8_t)((packed[i / 10u] >> (3u * (uint32_t)(i % 10u))) & 7u);
+  return KPE_OK;
+}
+
+kpe_status kpe_evaluate_sharded(kpe_device* const* devs, kpe_corpus* const* shards, int nshards,
+                                const kpe_program* prog, uint8_t* verdicts, kpe_counts* counts) {
+  if (!devs || !shards || !prog || nshards <= 0) return fail(KPE_E_INVALID, "null argument");
+  const size_t R = prog->p->rules.size();
+  for (int i = 0; i < nshards; ++i) {  // every launch first: the devices run together
+    if (!devs[i] || !shards[i]) return fail(KPE_E_INVALID, "null device or shard");
+    for (int j = 0; j < i; ++j)
+      if (devs[j] == devs[i]) return fail(KPE_E_INVALID, "one shard per device");
+    if (kpe_status st = kpe_evaluate_async(devs[i], prog, shards[i])) return st;
+  }
+  std::vector<kpe_counts> part(counts ? R : 0);
+  if (counts) memset(counts, 0, R * sizeof(kpe_counts));
+  uint64_t row = 0;
+  for (int i = 0; i < nshards; ++i) {
+    uint8_t* v = verdicts ? verdicts + row * R : nullptr;
+    if (kpe_status st = kpe_fetch(devs[i], prog, shards[i], v, nullptr, counts ? part.data() : nullptr)) return st;
+    for (size_t r = 0; counts && r < R; ++r) {
+      counts[r].na += part[r].na, counts[r].pass += part[r].pass, counts[r].fail += part[r].fail;
+      counts[r].warn += part[r].warn, counts[r].error += part[r].error, counts[r].skip += part[r].skip;
+      counts[r].undecided += part[r].undecided;
+    }
+    row += (uint64_t)shards[i]->c->n;
+  }
+  return KPE_OK;
 }
 
 static const char* const kCheckIds[KPE_NUM_CHECKS] = {

@@ -603,7 +603,7 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
       if (pi == 0u) continue;
       const uint32_t i = pi - 1u;
       const KpePatRule pr = a.rules[i];
-#if defined(KPE_DIAG) && (KPE_DIAG & 512)
+#if defined(DIAG_PATNOVM) && (KPE_DIAG & DIAG_PATNOVM)
       row[pr.col] = (uint8_t)KPE_PASS_;  // diagnostic: the rule loop without the VM
       continue;
 #endif

@@ -120,7 +120,7 @@ struct Program {
   CondProgram cond;  // rules with preconditions / deny / foreach evaluated per resource
   PssxProgram pssx;  // podSecurity.exclude
   int32_t pssx_preds[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // PSA predicates of kpe_pssx_kernel
-  DeviceProgram* dev = nullptr;
+  DeviceProgram* devs[16] = {};  // per device ordinal: the program's tables on that device (kpe_api.cpp)
   ~Program();
 };
 

@@ -199,6 +199,43 @@ class Corpus:
 SYNTH_PODS, SYNTH_MIXED, SYNTH_EDGE, SYNTH_SELECTORS, SYNTH_FANOUT, SYNTH_C3 = range(6)
 
 
+def packed_words(cells: int) -> int:
+    """32-bit words of a 3-bit packed verdict matrix of `cells` cells (10 cells per word)."""
+    return int(load().kpe_packed_words(cells))
+
+
+def unpack_verdicts(packed: np.ndarray, n: int, r: int) -> np.ndarray:
+    """Host expansion of kpe_pack_verdicts output into an n x r uint8 verdict matrix."""
+    packed = np.ascontiguousarray(packed, dtype=np.uint32)
+    if packed.size < packed_words(n * r):
+        raise ValueError("packed buffer too small")
+    out = np.empty((n, r), dtype=np.uint8)
+    check(load().kpe_unpack_verdicts(packed.ctypes.data, n * r, out.ctypes.data if n * r else None))
+    return out
+
+
+def evaluate_sharded(engines: Sequence["Engine"], ps: "PolicySet", shards: Sequence["Corpus"]):
+    """One logical corpus over several devices of this process (kpe_evaluate_sharded): the
+    shards' verdict rows in order and the summed per-rule counts."""
+    L = load()
+    k = len(shards)
+    if len(engines) != k or k == 0:
+        raise ValueError("one engine (device) per shard")
+    for e, c in zip(engines, shards):
+        if c.device is not e.device:
+            c.upload(e.device)
+    R = ps.num_rules
+    N = sum(c.n for c in shards)
+    v = np.zeros((N, R), dtype=np.uint8)
+    counts = (Counts * max(R, 1))()
+    devs = (ctypes.c_void_p * k)(*[e.device.h for e in engines])
+    cps = (ctypes.c_void_p * k)(*[c.h for c in shards])
+    check(L.kpe_evaluate_sharded(devs, cps, k, ps.h, v.ctypes.data if N * R else None, counts))
+    cnt = [{"na": c.na, "pass": c.pass_, "fail": c.fail, "warn": c.warn, "error": c.error, "skip": c.skip,
+            "undecided": c.undecided} for c in counts[:R]]
+    return v, cnt
+
+
 def synth_resources(seed: int, n: int, mix: int = 0, first_index: int = 0) -> bytes:
     """NDJSON from the synthetic generator (include/kpe_synth.h)."""
     L = load()
@@ -264,6 +301,17 @@ class Engine:
             check(load().kpe_evaluate_async(self.device.h, ps.h, corpus.h))
         else:
             check(load().kpe_evaluate_async_ex(self.device.h, ps.h, corpus.h, (1 if masks else 0) | (2 if cold else 0)))
+
+    # ---- verdict exchange (device-resident) ----
+    def device_verdicts(self, ps: PolicySet, corpus: Corpus):
+        """(device address, bytes) of the corpus's verdict matrix after an evaluation of ps."""
+        ptr, nb = ctypes.c_void_p(), ctypes.c_uint64()
+        check(load().kpe_device_verdicts(self.device.h, ps.h, corpus.h, ctypes.byref(ptr), ctypes.byref(nb)))
+        return ptr.value, nb.value
+
+    def pack_verdicts(self, ps: PolicySet, corpus: Corpus, dst_ptr: int, words: int):
+        """3-bit packing of the verdict matrix into device memory at dst_ptr (kpe_pack_verdicts)."""
+        check(load().kpe_pack_verdicts(self.device.h, ps.h, corpus.h, ctypes.c_void_p(dst_ptr), words))
 
     # ---- reference-shaped API ----
     def validate_batch(self, policies: Sequence[dict], resources: Sequence[dict],
