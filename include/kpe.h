@@ -144,7 +144,9 @@ kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out);
 kpe_status kpe_resource_hash(const char* resource_json, size_t len, char* out33);
 /* The hash of every NDJSON row (the rows kpe_corpus_flatten makes), 32 hex digits per row into
  * out (no NUL), on up to 16 threads. out == NULL: returns the row count. Returns the row count,
- * or -kpe_status (a row that is not a JSON object: -KPE_E_INVALID). */
+ * or -KPE_E_INVALID when cap_rows is too small. A row that is not a JSON object (which the
+ * flattener keeps with KPE_ROW_DECODE_ERROR) has no hash: its 32 bytes are '-' (never a hex
+ * digest), so an incremental scan always re-evaluates it. */
 int64_t kpe_resource_hashes(const char* ndjson, size_t len, char* out, int64_t cap_rows);
 /* Copy the columns to device memory (HBM). Evaluation requires this. */
 kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* c);

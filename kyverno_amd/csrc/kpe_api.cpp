@@ -634,8 +634,8 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   return need;
 }
-// kpe_lean4_kernel's tile slabs: per list, K = the 99.5th percentile of the per-tile item counts
-// (a multiple of 8, at least 8, at most the wave's staging capacity), and tile t's first
+// kpe_lean4_kernel's tile slabs: per list, K = the 99th percentile of the per-tile item counts
+// (a multiple of 4, at least 4, at most the wave's staging capacity), and tile t's first
 // min(count, K) items copied to [t * K, ...), zero padded. Items past K stay in the CSR columns
 // (the kernel loads them at header offsets). Built once per corpus, on the host.
 kpe_status build_slabs(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
@@ -646,10 +646,10 @@ kpe_status build_slabs(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s
     std::vector<uint32_t> cnt(nt);
     for (size_t t = 0; t < nt; ++t) cnt[t] = C.hdr[4 * (t + 1) + word] - C.hdr[4 * t + word];
     std::vector<uint32_t> srt(cnt);
-    const size_t q = std::min(nt - 1, (size_t)((double)nt * 0.995));
+    const size_t q = std::min(nt - 1, (size_t)((double)nt * 0.99));
     std::nth_element(srt.begin(), srt.begin() + q, srt.end());
-    uint32_t k = nt ? (srt[q] + 7u) / 8u * 8u : 8u;
-    k = std::max(8u, std::min(cap, k));
+    uint32_t k = (srt[q] + 3u) / 4u * 4u;
+    k = std::max(4u, std::min(cap, k));
     *K = k;
     std::vector<uint32_t> slab(nt * k * width + width, 0u);
     for (size_t t = 0; t < nt; ++t) {
@@ -1186,7 +1186,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
-  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, B.lean && !masks ? B.lean_kind : PD.narrow ? 1 : 0,
+  const bool lean_go = B.lean && (!masks || B.lean_kind >= 5);  // LEAN4 writes check masks too
+  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : PD.narrow ? 1 : 0,
                          B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
@@ -1349,7 +1350,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
-    ev.bytes = (B.lean && !masks && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) : scan_bytes(P, C, B.need, masks);
+    ev.bytes = (B.lean && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) + (masks ? 4.0 * (double)C.n * (double)R : 0.0)
+                                             : scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     dev->pending.push_back(ev);
   }

@@ -665,6 +665,14 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean4_kernel(ScanArg
     for (uint32_t i = t + kLB; i < img_n4; i += kLB) d4[i] = img[i];
   }
   __syncthreads();
+  if (KPE_DIAG & DIAG_NOLOOP) {  // loads and image only: every loaded value consumed
+    uint32_t x = dyn[0];
+#pragma unroll
+    for (int j = 0; j < T; ++j)
+      x += ld[j].hall + ld[j].rec.x + ld[j].rec.z + ld[j].c0.x + ld[j].c1.y + ld[j].v0 + ld[j].v1 + ld[j].s0 + ld[j].q0.x;
+    if (tile0 < ntiles) a0.verdicts[(size_t)tile0 * 64u + lane] = (uint8_t)x;
+    return;
+  }
   const uint8_t* s_capb = reinterpret_cast<const uint8_t*>(dyn + a0.capb_lds);
   const LdsPtr lds = (LdsPtr)dyn;
   const uint32_t p_sann = a0.pp_seccomp_ann_ok & ~PRED_LOCAL, p_aak = a0.pp_apparmor_key & ~PRED_LOCAL,
@@ -788,12 +796,24 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean4_kernel(ScanArg
     const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
     const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
     const uint32_t P = matched & pss_rules & ~failr & ~E;
-    if (live && !(KPE_DIAG & DIAG_NOSTORE)) {
-      uint8_t* row = a0.verdicts + (size_t)r * R;
-  #pragma unroll 1
-      for (uint32_t ri = 0; ri < R; ++ri)
-        row[ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    // verdict bytes: the wave's rows staged in LDS (row-major, R bytes per lane) and stored as
+    // dwords, 64 R contiguous bytes per tile; check masks (FAIL cells of PSS rules) per lane
+    uint8_t* sv = reinterpret_cast<uint8_t*>(stage + KPE_STAGE_WORDS);
+#pragma unroll 1
+    for (uint32_t ri = 0; ri < R; ++ri)
+      sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    if (a0.masks && live) {
+      uint32_t* mrow = a0.masks + (size_t)r * R;
+      const uint32_t fm = F & pss_rules;
+#pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri) {
+        uint32_t cv = 0;
+        for (uint32_t c = 0; c < ncls; ++c) cv = ((hw(cls_rm, c) >> ri) & 1u) ? hw(cls_cv, c) : cv;
+        mrow[ri] = ((fm >> ri) & 1u) ? (fails & cv) : 0u;
+      }
     }
+    __builtin_amdgcn_wave_barrier();
+    if (!(KPE_DIAG & DIAG_NOSTORE)) store_rows(a0.verdicts, sv, tile, R, 0, R, min(64u, n - tile * 64u), lane);
     __builtin_amdgcn_wave_barrier();  // the next tile reuses the staging area
   }
 }

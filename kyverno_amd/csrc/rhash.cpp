@@ -310,21 +310,14 @@ extern "C" int64_t kpe_resource_hashes(const char* ndjson, size_t len, char* out
   if (cap_rows < nl) return -KPE_E_INVALID;
   const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   std::vector<std::thread> th;
-  std::vector<int> bad(nt, 0);
   for (unsigned t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
       for (int64_t r = t; r < nl; r += nt) {
         char h[33];
-        if (!resource_hash(lines[r].first, lines[r].second, h)) {
-          bad[t] = 1;
-          memset(out + r * 32, '0', 32);
-        } else {
-          memcpy(out + r * 32, h, 32);
-        }
+        if (!resource_hash(lines[r].first, lines[r].second, h)) memset(out + r * 32, '-', 32);  // no hash
+        else memcpy(out + r * 32, h, 32);
       }
     });
   for (auto& x : th) x.join();
-  for (int b : bad)
-    if (b) return -KPE_E_INVALID;
   return nl;
 }

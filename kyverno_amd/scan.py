@@ -29,14 +29,18 @@ def resource_hash(resource) -> str:
     return out.value.decode()
 
 
+NO_HASH = "-" * 32  # kpe_resource_hashes' mark of a row that is not a JSON object
+
+
 def resource_hashes(ndjson: bytes):
-    """CalculateResourceHash of every NDJSON row (the rows kpe_corpus_flatten makes)."""
+    """CalculateResourceHash of every NDJSON row (the rows kpe_corpus_flatten makes); NO_HASH
+    for a row that is not a JSON object."""
     L = load()
     n = L.kpe_resource_hashes(ndjson, len(ndjson), None, 0)
     buf = ctypes.create_string_buffer(max(n, 1) * 32)
     m = L.kpe_resource_hashes(ndjson, len(ndjson), buf, n)
     if m < 0:
-        raise KpeError(-m, "a row is not a JSON object")
+        raise KpeError(-m, "resource hash buffer")
     raw = buf.raw
     return [raw[32 * i:32 * i + 32].decode() for i in range(m)]
 
@@ -51,9 +55,15 @@ def ndjson_rows(ndjson: bytes):
     return rows
 
 
-def _key(row: bytes):
-    """Report identity of a resource: its UID when set, else (apiVersion, kind, namespace, name)."""
-    d = json.loads(row)
+def _key(row: bytes, i: int):
+    """Report identity of a resource: its UID when set, else (apiVersion, kind, namespace, name);
+    a row that is not a JSON object is keyed by its position (it is re-evaluated every scan)."""
+    try:
+        d = json.loads(row)
+    except ValueError:
+        d = None
+    if not isinstance(d, dict):
+        return ("row", i)
     meta = d.get("metadata") if isinstance(d.get("metadata"), dict) else {}
     uid = meta.get("uid")
     if isinstance(uid, str) and uid:
@@ -68,6 +78,8 @@ class BackgroundScanner:
         self.engine = engine
         self._rows = {}  # key -> (hash, verdict row)
         self._policy_token = None
+        self._policies = None  # the PolicySet of the last scan (held: identity is the default token)
+        self._nrules = None
         self._ns_labels = None
         self.last_stats = {}
 
@@ -77,12 +89,15 @@ class BackgroundScanner:
         the PolicySet object itself."""
         rows = ndjson_rows(ndjson)
         hashes = resource_hashes(b"\n".join(rows))
-        keys = [_key(r) for r in rows]
-        token = policy_version if policy_version is not None else id(policies)
-        full = force or token != self._policy_token or ns_labels != self._ns_labels
-        dirty = [i for i, (k, h) in enumerate(zip(keys, hashes))
-                 if full or k not in self._rows or self._rows[k][0] != h]
+        keys = [_key(r, i) for i, r in enumerate(rows)]
         R = policies.num_rules
+        if policy_version is not None:
+            same_policies = policy_version == self._policy_token
+        else:  # the PolicySet itself: compared by identity while this scanner holds it
+            same_policies = self._policy_token is None and policies is self._policies
+        full = force or not same_policies or R != self._nrules or ns_labels != self._ns_labels
+        dirty = [i for i, (k, h) in enumerate(zip(keys, hashes))
+                 if full or h == NO_HASH or k not in self._rows or self._rows[k][0] != h]
         out = np.zeros((len(rows), R), dtype=np.uint8)
         if dirty:
             delta = b"\n".join(rows[i] for i in dirty)
@@ -96,6 +111,7 @@ class BackgroundScanner:
                 out[i] = self._rows[k][1]
             rows_next[k] = (h, out[i].copy())
         self._rows = rows_next  # resources absent from this scan are forgotten (deleted)
-        self._policy_token, self._ns_labels = token, ns_labels
+        self._policy_token, self._ns_labels = policy_version, ns_labels
+        self._policies, self._nrules = policies, R
         self.last_stats = {"rows": len(rows), "rescanned": len(dirty), "full": bool(full)}
         return out

@@ -79,24 +79,37 @@ def gather_rows(local, total: int, dst: int = 0, device=None):
     first, n = shard_range(total, rank, world)
     if local.shape[0] != n:
         raise ValueError(f"rank {rank} holds {local.shape[0]} rows, its shard has {n}")
-    ops = []
+    if R == 0:  # every rank knows R (the replicated program): nobody exchanges anything
+        return np.zeros((total, 0), dtype=np.uint8) if rank == dst else None
     out: Optional["torch.Tensor"] = None
     if rank == dst:
         out = torch.empty((total, R), dtype=torch.uint8, device=device)
         if n:
             out[first:first + n] = torch.from_numpy(local).to(device)
-        for r in range(world):
-            f, m = shard_range(total, r, world)
-            if r != dst and m and R:
-                ops.append(dist.P2POp(dist.irecv, out[f:f + m], r))
-    elif n and R:
-        ops.append(dist.P2POp(dist.isend, torch.from_numpy(local).to(device), dst))
+        recv = {r: out[f:f + m].view(-1) for r, (f, m) in ((r, shard_range(total, r, world)) for r in range(world))}
+        _p2p_to_root({r: v for r, v in recv.items() if r != dst}, None, dst, device)
+        return out.cpu().numpy()
+    _p2p_to_root(None, torch.from_numpy(local).to(device).view(-1), dst, device)
+    return None
+
+
+def _p2p_to_root(recv, send, dst, device):
+    """One batch_isend_irecv group joined by every rank: the root posts a receive per rank
+    (`recv`: rank -> flat tensor), each other rank one send. A rank with nothing to send (an
+    empty shard) sends a one-element placeholder, so no rank skips the group: RCCL requires
+    every rank of the group in the first point-to-point call."""
+    import torch
+    import torch.distributed as dist
+
+    ops = []
+    if recv is not None:
+        for r, t in recv.items():
+            ops.append(dist.P2POp(dist.irecv, t if t.numel() else torch.empty(1, dtype=t.dtype, device=t.device), r))
+    else:
+        ops.append(dist.P2POp(dist.isend, send if send.numel() else torch.zeros(1, dtype=send.dtype, device=send.device), dst))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
-    if rank != dst:
-        return None
-    return out.cpu().numpy()
 
 
 def gather_packed(engine, ps, corpus, total: int, dst: int = 0, device=None):
@@ -123,23 +136,16 @@ def gather_packed(engine, ps, corpus, total: int, dst: int = 0, device=None):
     first, m = shard_range(total, rank, world)
     if m != n:
         raise ValueError(f"rank {rank} holds {n} rows, its shard has {m}")
-    ops, parts = [], {}
-    if rank == dst:
-        for r in range(world):
-            f, mr = shard_range(total, r, world)
-            w = packed_words(mr * R)
-            if r == dst:
-                parts[r] = buf
-            elif w:
-                parts[r] = torch.empty(w, dtype=torch.int32, device=buf.device)
-                ops.append(dist.P2POp(dist.irecv, parts[r], r))
-    elif words:
-        ops.append(dist.P2POp(dist.isend, buf[:words], dst))
-    if ops:
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+    if R == 0:
+        return np.zeros((total, 0), dtype=np.uint8) if rank == dst else None
+    parts = {}
     if rank != dst:
+        _p2p_to_root(None, buf[:words], dst, device)
         return None
+    for r in range(world):
+        f, mr = shard_range(total, r, world)
+        parts[r] = buf if r == dst else torch.empty(packed_words(mr * R), dtype=torch.int32, device=buf.device)
+    _p2p_to_root({r: t for r, t in parts.items() if r != dst}, None, dst, device)
     out = np.empty((total, R), dtype=np.uint8)
     for r in range(world):
         f, mr = shard_range(total, r, world)

@@ -210,3 +210,39 @@ def test_gpu_sharded_single_process(oracle):
     assert np.array_equal(K.unpack_verdicts(buf.cpu().numpy().view(np.uint32), *v.shape), v)
     with pytest.raises(K.KpeError):  # one shard per device
         K.evaluate_sharded([eng, eng], ps, [c, K.Corpus(nd)])
+
+
+def _small_worker(rank, world, port, outdir, total):
+    """total < world: some ranks hold no rows and still join the gather group."""
+    import torch.distributed as dist
+
+    import kyverno_amd as K
+    from tests.oracle_lib import load as load_oracle
+    from tests.policies import parity_policy_set
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    first, n = shard.shard_range(total, rank, world)
+    pols = parity_policy_set()
+    R = K.PolicySet(pols).num_rules
+    v = load_oracle().validate(pols, K.synth_resources(0xC3, n, mix=2, first_index=first)) if n else \
+        np.zeros((0, R), dtype=np.uint8)
+    full = shard.gather_rows(v, total, dst=0)
+    if rank == 0:
+        np.save(os.path.join(outdir, "gathered.npy"), full)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_gather_with_empty_shards(tmp_path):
+    from tests.oracle_lib import load as load_oracle
+    from tests.policies import parity_policy_set
+
+    import kyverno_amd as K
+
+    total, world = 2, 3
+    mp.start_processes(_small_worker, args=(world, _free_port(), str(tmp_path), total), nprocs=world, join=True,
+                       start_method="spawn")
+    ref = load_oracle().validate(parity_policy_set(), K.synth_resources(0xC3, total, mix=2))
+    assert np.array_equal(np.load(tmp_path / "gathered.npy"), ref)

@@ -170,3 +170,15 @@ def test_incremental_scan_matches_full(oracle):
     assert (v1 == oracle.validate(pols, nd2, nthreads=8)).all()
     v2 = sc.scan(ps, nd2, force=True)
     assert sc.last_stats["full"] and (v2 == full).all()
+
+
+def test_batch_hash_rows_that_are_not_objects():
+    """kpe_resource_hashes keeps going past a row that is not a JSON object (the flattener keeps
+    such rows with KPE_ROW_DECODE_ERROR): that row has no hash and the others are unchanged."""
+    from kyverno_amd.scan import NO_HASH
+
+    good = K.synth_resources(7, 3, mix=0).decode().splitlines()
+    nd = "\n".join([good[0], "[1,2]", good[1], "7", good[2]]).encode()
+    hs = K.resource_hashes(nd)
+    assert hs[1] == NO_HASH and hs[3] == NO_HASH
+    assert [hs[0], hs[2], hs[4]] == K.resource_hashes("\n".join(good).encode())
