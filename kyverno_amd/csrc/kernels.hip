@@ -147,9 +147,7 @@ constexpr uint32_t kBlock = 256;
 #define DIAG_NOSTAGE 256u // (LEAN3) no list staging / per-pod OR: the lane's own first items stand in
 #define DIAG_PATNOVM 512u // (pattern kernel) the rule loop without the VM: pending cells pass
 #define DIAG_PATLEAF 1024u // (pattern VM) every scalar leaf holds without evaluation: the walk alone
-constexpr uint32_t kAllowedVolumes = (1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) |
-                                     (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | (1u << VS_PVC) |
-                                     (1u << VS_PROJECTED) | (1u << VS_SECRET);
+constexpr uint32_t kAllowedVolumes = PSS_ALLOWED_VOLUMES;
 
 
 // Capability-set violation bits (computed per block into LDS from the capset dictionary)
@@ -1220,8 +1218,9 @@ ScanFn prep_fn(int pss, int narrow) {
 // capped by the number of 256-resource tiles.
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes) {
   if (n <= 0) return 0;
-  if (pss && (narrow == 5 || narrow == 6)) {  // kpe_lean4_kernel<1> / <2>
-    const int64_t waves = ((n + 63) / 64 + (narrow - 4) - 1) / (narrow - 4);
+  if (pss && narrow >= 5 && narrow <= 8) {  // kpe_lean4_kernel<1> / <2>, kpe_lean5_kernel<1> / <2>
+    const int64_t tpw = (narrow == 6 || narrow == 8) ? 2 : 1;
+    const int64_t waves = ((n + 63) / 64 + tpw - 1) / tpw;
     return (uint32_t)((waves + kLB / 64 - 1) / (kLB / 64));
   }
   if (pss && narrow == 4) {  // kpe_lean3_kernel: KPE_LEAN_T tiles of 64 rows per wave, no persistent loop
@@ -1263,6 +1262,14 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
   }
   if (pss && narrow == 6) {
     hipLaunchKernelGGL(kpe_lean4_kernel<2>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
+    return hipGetLastError();
+  }
+  if (pss && narrow == 7) {
+    hipLaunchKernelGGL(kpe_lean5_kernel<1>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
+    return hipGetLastError();
+  }
+  if (pss && narrow == 8) {
+    hipLaunchKernelGGL(kpe_lean5_kernel<2>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);

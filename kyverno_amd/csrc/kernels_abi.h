@@ -163,6 +163,7 @@ struct ScanArgs {
   // LEAN4 tile slabs (DeviceCorpus::slab_*): tile t's first K items of a list at [t * K, t * K + K)
   const uint32_t *slab_c, *slab_v, *slab_s, *slab_a;
   uint32_t kc, kv, ks, ka;
+  const uint32_t* psum;  // LEAN5: per-pod PSA summary (2 words per pod, schema.h PS_*)
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null

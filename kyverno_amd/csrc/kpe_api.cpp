@@ -218,6 +218,7 @@ struct DeviceCorpus {
   bool cold = false;
   // LEAN4 tile slabs (kpe_lean4_kernel): tile t's first K items of each list at [t * K, t * K + K)
   DevBuf slab_c, slab_v, slab_s, slab_a;
+  DevBuf psum;  // LEAN5: per-pod PSA summaries (Corpus::psum)
   uint32_t kc = 0, kv = 0, ks = 0, ka = 0;
   bool slabs = false;
   Binding bind;
@@ -993,8 +994,11 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
                              (uint64_t)C.c_sc.size() * 8 > lim || (uint64_t)C.vol_src.size() * 4 > lim ||
                              (uint64_t)C.sys_id.size() * 4 > lim || (uint64_t)C.pann_kv.size() * 4 > lim)
                                 ? 2
-                                : getenv("KPE_LEAN_PERSIST") ? 3 : getenv("KPE_LEAN3") ? 4 : getenv("KPE_LEAN4_T2") ? 6 : 5;
-  if (B.lean_kind >= 5) {
+                                : getenv("KPE_LEAN_PERSIST") ? 3 : getenv("KPE_LEAN3") ? 4 : getenv("KPE_LEAN4_T2") ? 6
+                                  : getenv("KPE_LEAN4") ? 5 : getenv("KPE_LEAN5_T2") ? 8 : 7;
+  if (B.lean_kind >= 7 && (C.psum.size() != (size_t)C.n * 2 || (uint64_t)C.n * 16 > lim)) B.lean_kind = 5;
+  if (B.lean_kind >= 7 && !cc->d->psum.p) HIPCHK(upload(cc->d->psum, C.psum, s));
+  if (B.lean_kind == 5 || B.lean_kind == 6) {
     const uint64_t slab_bytes = (uint64_t)((C.n + 63) / 64) * KPE_STAGE_CTR * 8;
     if (slab_bytes > lim) B.lean_kind = 4;
     else if (kpe_status st = build_slabs(C, *cc->d, s)) return st;
@@ -1157,6 +1161,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
   sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
+  sa.psum = D.psum.p ? D.psum.as<uint32_t>() : nullptr;
   if (D.slabs) {
     sa.slab_c = D.slab_c.as<uint32_t>(), sa.slab_v = D.slab_v.as<uint32_t>();
     sa.slab_s = D.slab_s.as<uint32_t>(), sa.slab_a = D.slab_a.as<uint32_t>();
@@ -1350,8 +1355,10 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
-    ev.bytes = (B.lean && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) + (masks ? 4.0 * (double)C.n * (double)R : 0.0)
-                                             : scan_bytes(P, C, B.need, masks);
+    const double mb = masks ? 4.0 * (double)C.n * (double)R : 0.0;
+    ev.bytes = (B.lean && B.lean_kind >= 7)   ? 24.0 * (double)C.n + (double)C.n * (double)R + mb  // records, summaries, rows
+               : (B.lean && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) + mb
+                                              : scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     dev->pending.push_back(ev);
   }

@@ -817,3 +817,95 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean4_kernel(ScanArg
     __builtin_amdgcn_wave_barrier();  // the next tile reuses the staging area
   }
 }
+
+// ---- kpe_lean5_kernel: pod records and PSA summaries only --------------------------------
+// The corpus's per-pod PSA summary (Corpus::psum, schema.h PS_*: the OR of the container state
+// bitmaps and of the list items' codes under the PSA library's fixed sets, built once at
+// flatten) stands in for the container / volume / sysctl / annotation lists, so a wave loads
+// one 16-byte record and one 8-byte summary per pod in one memory step and evaluates with no
+// staging, scans or list loops: the versioned checks (cv_fails), the kind table, the rows
+// stored as dwords through LDS and, when asked, the check masks.
+template <int T>
+__global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArgs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  if (KPE_DIAG & DIAG_EMPTY) return;
+  CArgs& a0 = *kargs();
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
+  const uint32_t tile0 = (xcd_block(blockIdx.x, gridDim.x) * (kLB / 64u) + wv) * (uint32_t)T;
+  const Rsrc RC = make_rsrc(a0.rec, n * 16u), PS = make_rsrc(a0.psum, n * 8u);
+  uint4 rec[T];
+  uint2 sum[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t r = (tile0 + (uint32_t)j) * 64u + lane;
+    rec[j] = bload4(RC, r * 16u);
+    sum[j] = bload2(PS, r * 8u);
+  }
+  // the kind table and the class table of the prologue image (a few hundred words)
+  const uint32_t img_n4 = a0.pimg_words >> 2;
+  const uint4* img = reinterpret_cast<const uint4*>(a0.pimg);
+  const uint4 img0 = img[min(t, img_n4 - 1u)];
+  uint32_t cls_cv = 0, cls_rm = 0;
+  if (lane < a0.ncls) {
+    const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
+    cls_cv = c.x, cls_rm = c.y;
+  }
+  {
+    uint4* d4 = reinterpret_cast<uint4*>(dyn);
+    if (t < img_n4) d4[t] = img0;
+#pragma unroll 1
+    for (uint32_t i = t + kLB; i < img_n4; i += kLB) d4[i] = img[i];
+  }
+  __syncthreads();
+  if (KPE_DIAG & DIAG_NOLOOP) {
+    uint32_t x = dyn[0];
+#pragma unroll
+    for (int j = 0; j < T; ++j) x += rec[j].x + rec[j].y + sum[j].x + sum[j].y;
+    if (tile0 < ntiles) a0.verdicts[(size_t)tile0 * 64u + lane] = (uint8_t)x;
+    return;
+  }
+  const uint32_t R = a0.nrules, cv_union = a0.cv_union, pss_rules = a0.pss_rules, ncls = a0.ncls;
+  const uint32_t ep_rules = a0.err_rules | a0.pat_rules, pat_rules = a0.pat_rules;
+  uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a0.wave_lds + wv * a0.wave_words + KPE_STAGE_WORDS);
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    const uint32_t tile = tile0 + (uint32_t)j;
+    if (tile >= ntiles) break;
+    const uint32_t r = tile * 64u + lane;
+    const bool live = r < n;
+    const uint32_t pw = rec[j].x, y = sum[j].y;
+    const uint32_t fails = cv_fails(pw, sum[j].x, PS_CAPS(y), false, PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
+                                    PS_ANN(y) & 1u, PS_ANN(y) & 2u) & cv_union;
+    const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
+    const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
+    const uint32_t matched = dyn[a0.kt_lds + GVK_KIND(rec[j].y)];
+    uint32_t failr;
+    if (ncls == 1u) {
+      failr = (fails & hw(cls_cv, 0)) ? hw(cls_rm, 0) : 0u;
+    } else {
+      failr = 0;
+#pragma unroll 1
+      for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+    }
+    const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
+    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
+    const uint32_t P = matched & pss_rules & ~failr & ~E;
+#pragma unroll 1
+    for (uint32_t ri = 0; ri < R; ++ri)
+      sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    if (a0.masks && live) {
+      uint32_t* mrow = a0.masks + (size_t)r * R;
+      const uint32_t fm = F & pss_rules;
+#pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri) {
+        uint32_t cv = 0;
+        for (uint32_t c = 0; c < ncls; ++c) cv = ((hw(cls_rm, c) >> ri) & 1u) ? hw(cls_cv, c) : cv;
+        mrow[ri] = ((fm >> ri) & 1u) ? (fails & cv) : 0u;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (!(KPE_DIAG & DIAG_NOSTORE)) store_rows(a0.verdicts, sv, tile, R, 0, R, min(64u, n - tile * 64u), lane);
+    __builtin_amdgcn_wave_barrier();
+  }
+}

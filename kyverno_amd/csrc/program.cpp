@@ -20,6 +20,7 @@
 #include "goval.hpp"
 #include "jscan.hpp"
 #include "program.hpp"
+#include "pss_fixed.hpp"
 
 namespace kpe {
 
@@ -1768,29 +1769,17 @@ class Lowerer {
     return lit;
   }
 
-  void pss_preds() {
+  void pss_preds() {  // the PSA library's fixed sets (pss_fixed.hpp)
     auto& s = P.pss;
     if (s.apparmor_key >= 0) return;
-    s.apparmor_key = pred(D_ANNK, {"container.apparmor.security.beta.kubernetes.io/*"});
-    s.apparmor_val_ok = pred(D_ANNV, {"runtime/default", "localhost/*"});
-    s.seccomp_pod_key = pred(D_ANNK, {"seccomp.security.alpha.kubernetes.io/pod"});
-    s.seccomp_ann_ok = pred(D_ANNV, {"runtime/default", "docker/default", "localhost/*"});
-    s.caps_baseline_ok = pred(D_CAP, {"AUDIT_WRITE", "CHOWN", "DAC_OVERRIDE", "FOWNER", "FSETID", "KILL", "MKNOD",
-                                      "NET_BIND_SERVICE", "SETFCAP", "SETGID", "SETPCAP", "SETUID", "SYS_CHROOT"});
-    s.cap_nbs = pred(D_CAP, {"NET_BIND_SERVICE"});
-    s.cap_all = pred(D_CAP, {"ALL"});
-    std::vector<std::string> v10 = {"kernel.shm_rmid_forced", "net.ipv4.ip_local_port_range",
-                                    "net.ipv4.ip_unprivileged_port_start", "net.ipv4.tcp_syncookies",
-                                    "net.ipv4.ping_group_range"};
-    std::vector<std::string> v127 = v10;
-    v127.push_back("net.ipv4.ip_local_reserved_ports");
-    std::vector<std::string> v129 = v127;
-    for (auto n : {"net.ipv4.tcp_keepalive_time", "net.ipv4.tcp_fin_timeout", "net.ipv4.tcp_keepalive_intvl",
-                   "net.ipv4.tcp_keepalive_probes"})
-      v129.push_back(n);
-    s.sysctl[0] = pred(D_SYSCTL, v10);
-    s.sysctl[1] = pred(D_SYSCTL, v127);
-    s.sysctl[2] = pred(D_SYSCTL, v129);
+    s.apparmor_key = pred(D_ANNK, pssfix::kApparmorKey);
+    s.apparmor_val_ok = pred(D_ANNV, pssfix::kApparmorOk);
+    s.seccomp_pod_key = pred(D_ANNK, pssfix::kSeccompPodKey);
+    s.seccomp_ann_ok = pred(D_ANNV, pssfix::kSeccompAnnOk);
+    s.caps_baseline_ok = pred(D_CAP, pssfix::kCapsBaselineOk);
+    s.cap_nbs = pred(D_CAP, pssfix::kCapNbs);
+    s.cap_all = pred(D_CAP, pssfix::kCapAll);
+    for (int v = 0; v < 3; ++v) s.sysctl[v] = pred(D_SYSCTL, pssfix::sysctls(v));
   }
 
   // a predicate read only by a kernel after the scan: its bitset is always written to pbuf
@@ -1948,12 +1937,12 @@ class Lowerer {
   void pssx_fixed_preds() {
     if (P.pssx.rules.empty()) {  // fixed PSA predicates, read from pbuf by kpe_pssx_kernel
       auto& g = P.pssx_preds;
-      g[0] = gpred(D_ANNK, {"container.apparmor.security.beta.kubernetes.io/*"});
-      g[1] = gpred(D_ANNV, {"runtime/default", "localhost/*"});
-      g[2] = gpred(D_ANNV, {"runtime/default", "docker/default", "localhost/*"});
-      g[3] = gpred(D_CAP, P.preds[P.pss.caps_baseline_ok].globs);
-      g[4] = gpred(D_CAP, {"NET_BIND_SERVICE"});
-      g[5] = gpred(D_CAP, {"ALL"});
+      g[0] = gpred(D_ANNK, pssfix::kApparmorKey);
+      g[1] = gpred(D_ANNV, pssfix::kApparmorOk);
+      g[2] = gpred(D_ANNV, pssfix::kSeccompAnnOk);
+      g[3] = gpred(D_CAP, pssfix::kCapsBaselineOk);
+      g[4] = gpred(D_CAP, pssfix::kCapNbs);
+      g[5] = gpred(D_CAP, pssfix::kCapAll);
       for (int v = 0; v < 3; ++v) g[6 + v] = gpred(D_SYSCTL, P.preds[P.pss.sysctl[v]].globs);
     }
   }

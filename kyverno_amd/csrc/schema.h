@@ -197,6 +197,19 @@ enum KpeDomain {
 #define VS_STORAGEOS 26
 #define VS_CSI 27
 #define VS_EPHEMERAL 28
+// restrictedVolumes (check_restrictedVolumes.go): the volume sources a restricted pod may use
+#define PSS_ALLOWED_VOLUMES                                                                                     \
+  ((1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) | (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | \
+   (1u << VS_PVC) | (1u << VS_PROJECTED) | (1u << VS_SECRET))
+// Per-pod PSA summary (Corpus::psum, 2 words per row; flatten.cpp rebuild_summary): x = OR of
+// the container state bitmaps (CX_*), y = the OR-ed list codes under the PSA library's fixed
+// sets: capability-set bits (CS_* of kernels.hip) | volume codes << 3 (bit 0 hostPath, bit 1 a
+// source outside PSS_ALLOWED_VOLUMES) | sysctl codes << 5 (bit v: a sysctl outside version v's
+// set) | annotation codes << 8 (bit 0 AppArmor, bit 1 pod seccomp annotation not allowed)
+#define PS_CAPS(y) ((y) & 7u)
+#define PS_VOL(y) (((y) >> 3) & 3u)
+#define PS_SYS(y) (((y) >> 5) & 7u)
+#define PS_ANN(y) (((y) >> 8) & 3u)
 
 // ---- PSA checks (bit k of a check mask), policy.DefaultChecks() order ----------------------
 enum KpeCheck {

@@ -1,13 +1,14 @@
 #!/bin/bash
-# A/B of the C2 LEAN scan variants (kpe_lean3 / kpe_lean4<1> / kpe_lean4<2>) through bench.py;
+# A/B of the C2 LEAN scan variants (kpe_lean5<1> / <2>, kpe_lean4, kpe_lean3) through bench.py;
 # one JSON line per variant under gpurun_out/lean_ab/.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out/lean_ab
-for v in lean4 lean4_t2 lean3; do
+for v in lean5 lean5_t2 lean4 lean3; do
   case $v in
-    lean4) envs="" ;;
-    lean4_t2) envs="KPE_LEAN4_T2=1" ;;
+    lean5) envs="" ;;
+    lean5_t2) envs="KPE_LEAN5_T2=1" ;;
+    lean4) envs="KPE_LEAN4=1" ;;
     lean3) envs="KPE_LEAN3=1" ;;
   esac
   echo "== $v ($(date +%T))"
