@@ -248,6 +248,33 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
                             const char* resource_json, size_t resource_len, char* buf, size_t cap);
 
+/* Failing paths of pattern cells, for their report messages (validate_resource.go:316-454;
+ * validate.go MatchPattern PatternError.Path). After kpe_evaluate / kpe_evaluate_async of the
+ * same program and corpus, for each listed cell (row * R + column) the device re-walks every root
+ * of the cell's validate.pattern / anyPattern rule (at most KPE_TRACE_ROOTS) and records the
+ * path of the failure that decided it: out[i * KPE_TRACE_ROOTS * KPE_TRACE_WORDS + k *
+ * KPE_TRACE_WORDS + w], w = 0: component count (bits 0-7) | KPE_TR_TRUNC | the root's verdict
+ * << 16 | KPE_TR_VALID; w = 1..15: components (a pattern member, KPE_TC_KEY | key id, or
+ * KPE_TC_IDX | array index). A cell of a rule without patterns gives a zero record. */
+#define KPE_TRACE_WORDS 16u
+#define KPE_TRACE_ROOTS 4u
+#define KPE_TC_IDX 0x80000000u
+#define KPE_TC_KEY 0x40000000u
+#define KPE_TR_TRUNC 0x100u
+#define KPE_TR_VALID 0x1000000u
+kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, const uint64_t* cells,
+                              uint64_t ncells, uint32_t* out);
+/* kpe_report_results_msg plus the pattern messages: `traces` holds the row's R cells in
+ * kpe_pattern_traces layout (R * KPE_TRACE_ROOTS * KPE_TRACE_WORDS words; only pattern-rule
+ * cells are read). Adds: validate.pattern fail ("validation error: <message>. rule <rule> failed
+ * at path <path>", buildErrorMessage), anyPattern pass ("validation rule '<rule>' anyPattern[<i>]
+ * passed.") and fail (buildAnyPatternErrorMessage over "rule <rule>[<i>] failed at path <path>").
+ * Not rendered (no message): messages with variables, empty-path failures (their text is the Go
+ * error string), skips, anyPattern fails with more than KPE_TRACE_ROOTS patterns. */
+long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus, const uint8_t* verdict_row,
+                               const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
+                               size_t resource_len, char* buf, size_t cap);
+
 /* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
 typedef struct kpe_kernel_stats {
   uint64_t launches;        /* evaluations timed since the last reset           */

@@ -1287,7 +1287,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
             continue;
           }
           const PatArgs& pa = *a.pat;
-          PatVM pvm{pa, vm.doc, F.scoped == kNoNode ? vm.root : F.scoped, pvrow, 0u};
+          PatVM pvm{pa, PV_DOCVIEW(pa, vm.doc, 0u, pa.ndoc), F.scoped == kNoNode ? vm.root : F.scoped, pvrow, 0u};
           const uint32_t nr = F.fe.b & 0xFFFFu, pf = F.fe.b >> 16;
           uint32_t fails = 0, skips = 0, last = KPE_PASS_;
           bool passed = false, undec = false;

@@ -28,7 +28,9 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lds, hipStream_t s);
+extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
+                                               hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s);
 extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
                                            uint8_t value, hipStream_t s);
@@ -1204,7 +1206,13 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.npr = (uint32_t)P.pat.rules.size();
       pa.doc = D.doc.as<uint32_t>();
       pa.doc_off = D.doc_off.as<uint64_t>();
+      pa.img_off = D.img_off.as<uint64_t>();
       pa.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();  // C3 14.0 -> 8.5 ms, C5 27.6 -> 19.4 ms
+      {  // tape entries one batch of kpe_pattern_lds_kernel stages (KPE_PAT_STAGE: tests force the HBM walk)
+        const char* st = getenv("KPE_PAT_STAGE");
+        const long v = st ? atol(st) : (long)KPE_PAT_LDS_WORDS;
+        pa.stage_max = (uint32_t)std::min<long>(std::max<long>(v, 0L), (long)KPE_PAT_LDS_WORDS);
+      }
       pa.scal = D.scal.as<KpeScalar>();
       pa.scal_text = D.scal_text.as<uint8_t>();
       pa.nodes = PD.pnodes.as<KpePNode>();
@@ -1338,7 +1346,10 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
-    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
+    // kpe_pattern_kernel (lane per row); KPE_PAT_TAPE selects kpe_pattern_lds_kernel (rows' tapes
+    // staged in LDS, lane per cell: measured slower, C5 55 vs 19 ms, profiles/r03_b_ldstape)
+    const bool tape_kernel = getenv("KPE_PAT_TAPE") != nullptr;
+    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), tape_kernel ? 1 : 0, s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;
       HIPCHK(hipMemcpyAsync(&e, B.perr.p, 4, hipMemcpyDeviceToHost, s));
@@ -1520,6 +1531,38 @@ kpe_status kpe_unpack_verdicts(const uint32_t* packed, uint64_t cells, uint8_t* 
   return KPE_OK;
 }
 
+// ---- failing paths of pattern cells (report time) ---------------------------------------------
+kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, const uint64_t* cells,
+                              uint64_t ncells, uint32_t* out) {
+  if (!dev || !prog || !c || !c->d || (ncells && (!cells || !out))) return fail(KPE_E_INVALID, "null argument");
+  if (!ncells) return KPE_OK;
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& B = c->d->bind;
+  if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  const uint64_t total = (uint64_t)c->c->n * prog->p->rules.size();
+  for (uint64_t i = 0; i < ncells; ++i)
+    if (cells[i] >= total) return fail(KPE_E_INVALID, "cell index past the verdict matrix");
+  const size_t rec = (size_t)KPE_TRACE_ROOTS * KPE_TRACE_WORDS;
+  if (prog->p->pat.rules.empty() || !B.pargs_valid) {  // no pattern rule: every record is empty
+    memset(out, 0, ncells * rec * 4);
+    return KPE_OK;
+  }
+  hipStream_t s = B.last ? B.last : dev->stream;
+  void *dc = nullptr, *dout = nullptr;
+  hipError_t e = hipMalloc(&dc, ncells * 8);
+  if (e == hipSuccess) e = hipMalloc(&dout, ncells * rec * 4);
+  if (e == hipSuccess) e = hipMemcpyAsync(dc, cells, ncells * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess)
+    e = kpe_launch_pattern_trace(B.pargs.as<PatArgs>(), (const uint64_t*)dc, ncells, (uint32_t*)dout, s);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, dout, ncells * rec * 4, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (dc) (void)hipFree(dc);
+  if (dout) (void)hipFree(dout);
+  HIPCHK(e);
+  return KPE_OK;
+}
+
 kpe_status kpe_evaluate_sharded(kpe_device* const* devs, kpe_corpus* const* shards, int nshards,
                                 const kpe_program* prog, uint8_t* verdicts, kpe_counts* counts) {
   if (!devs || !shards || !prog || nshards <= 0) return fail(KPE_E_INVALID, "null argument");
@@ -1610,8 +1653,92 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
   return kpe_report_results_msg(prog, verdict_row, cv_mask_row, nullptr, 0, buf, cap);
 }
 
+// The PatternError.Path of a trace record (validate.go: "/" then each key or index followed by
+// "/"); false when the record is truncated
+static bool trace_path(const kpe::Program& P, const kpe::Corpus* C, const uint32_t* t, std::string* out) {
+  if (t[0] & KPE_TR_TRUNC) return false;
+  const uint32_t n = t[0] & 0xFFu;
+  std::string p = "/";
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t c = t[1 + i];
+    if (c & KPE_TC_IDX) {
+      p += std::to_string(c & ~KPE_TC_IDX);
+    } else if (c & KPE_TC_KEY) {
+      if (!C) return false;
+      const uint32_t id = c & ~KPE_TC_KEY;
+      if (id >= C->dict[D_KEY].size()) return false;
+      p += std::string(C->dict[D_KEY].at(id));
+    } else {
+      if ((size_t)c * 4 + 1 >= P.pat.members.size()) return false;
+      const uint32_t ki = P.pat.members[(size_t)c * 4 + 1];
+      if (ki >= P.pat.keys.size()) return false;
+      p += P.pat.keys[ki];
+    }
+    p += '/';
+  }
+  *out = std::move(p);
+  return true;
+}
+
+// validate_resource.go:316-454: pattern / anyPattern messages from the cell's trace (roots in
+// order); empty when the reference's text would need an error string the device does not keep
+// (an empty-path PatternError, a skip) or a substituted message
+static std::string pattern_message(const kpe::Program& P, const kpe::Corpus* C, const kpe::RuleReport& rr, uint8_t v,
+                                   const uint32_t* tr) {
+  auto root = [&](uint32_t k) { return tr + (size_t)k * KPE_TRACE_WORDS; };
+  auto rv = [&](uint32_t k) { return (root(k)[0] & KPE_TR_VALID) ? (root(k)[0] >> 16) & 0xFFu : 0xFFu; };
+  if (!rr.any_pattern) {
+    if (v != KPE_FAIL || rv(0) != KPE_FAIL) return "";
+    std::string path;
+    if (!trace_path(P, C, root(0), &path)) return "";
+    if (rr.vmsg.empty()) return "validation error: rule " + rr.rule + " failed at path " + path;  // buildErrorMessage
+    if (rr.vmsg_vars) return "";
+    std::string m = rr.vmsg;
+    if (m.empty() || m.back() != '.') m += '.';
+    return "validation error: " + m + " rule " + rr.rule + " failed at path " + path;
+  }
+  if (v == KPE_PASS) {
+    if (rr.pat_roots == 0) return rr.vmsg;  // no pattern at all: RulePass(rule.Validation.Message)
+    for (uint32_t k = 0; k < rr.pat_roots && k < KPE_TRACE_ROOTS; ++k) {
+      if (rv(k) == KPE_PASS) return "validation rule '" + rr.rule + "' anyPattern[" + std::to_string(k) + "] passed.";
+      if (rv(k) == 0xFFu || rv(k) == KPE_UNDECIDED) return "";
+    }
+    return "";
+  }
+  if (v != KPE_FAIL || rr.pat_roots > KPE_TRACE_ROOTS) return "";
+  std::string errs;
+  for (uint32_t k = 0; k < rr.pat_roots; ++k) {
+    const uint32_t x = rv(k);
+    if (x == KPE_SKIP) continue;  // skipped patterns are not listed once one failed
+    if (x != KPE_FAIL) return "";  // an empty-path failure's message is its error text
+    std::string path;
+    if (!trace_path(P, C, root(k), &path)) return "";
+    errs += (errs.empty() ? "" : " ") + ("rule " + rr.rule + "[" + std::to_string(k) + "] failed at path " + path);
+  }
+  if (errs.empty()) return "";
+  if (rr.vmsg.empty()) return "validation error: " + errs;  // buildAnyPatternErrorMessage
+  if (rr.vmsg.back() == '.') return "validation error: " + rr.vmsg + " " + errs;
+  return "validation error: " + rr.vmsg + ". " + errs;
+}
+
+static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const uint8_t* verdict_row,
+                        const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
+                        size_t resource_len, char* buf, size_t cap);
+
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
                             const char* resource_json, size_t resource_len, char* buf, size_t cap) {
+  return report_impl(prog, nullptr, verdict_row, cv_mask_row, nullptr, resource_json, resource_len, buf, cap);
+}
+
+long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus, const uint8_t* verdict_row,
+                               const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
+                               size_t resource_len, char* buf, size_t cap) {
+  return report_impl(prog, corpus, verdict_row, cv_mask_row, traces, resource_json, resource_len, buf, cap);
+}
+
+static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const uint8_t* verdict_row,
+                        const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
+                        size_t resource_len, char* buf, size_t cap) {
   if (!prog || !verdict_row) {
     fail(KPE_E_INVALID, "null argument");
     return -KPE_E_INVALID;
@@ -1641,6 +1768,9 @@ long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row,
       } else if (rr.pss && v == KPE_FAIL && !rr.pss_excl && cv_mask_row && cv_mask_row[r]) {
         if (!pod_state) pod_state = kpe::typed_pod_view(resource_json, resource_len, &pod, &kind) ? 1 : -1;
         if (pod_state > 0) msg = kpe::pss_fail_message(rr.rule, rr.pss_level, rr.pss_version, kind, pod, cv_mask_row[r]);
+      } else if (rr.pat_rule && traces && (v == KPE_FAIL || (v == KPE_PASS && rr.any_pattern))) {
+        msg = pattern_message(P, corp ? corp->c.get() : nullptr, rr, v,
+                              traces + r * (size_t)(KPE_TRACE_ROOTS * KPE_TRACE_WORDS));
       } else if (rr.msg_pattern && v == KPE_PASS) {
         msg = "validation rule '" + rr.rule + "' passed.";
       } else if (rr.msg_deny && v == KPE_PASS) {

@@ -10,6 +10,33 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 constexpr int kPatStack = KPE_PAT_STACK;  // frames of one lane; deeper walks give KPE_UNDECIDED
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
 
+// The tape as the VM reads it: entry i (an absolute tape index) is p[i - base]. The pattern
+// kernel stages a batch of rows' tape segments in LDS (p: the wave's LDS copy, base: the
+// batch's first entry); every other walk reads the tape itself (base 0). p is a generic
+// pointer, so the same VM code reads either.
+struct DocView {
+  const uint2* p;
+  uint32_t base;
+#if defined(KPE_PATVM_CHECK) && KPE_PATVM_CHECK
+  uint64_t lim;  // entries present at p (host check builds: an index outside flags bit 12)
+  uint32_t* err;
+  __device__ __forceinline__ uint2 operator[](uint64_t i) const {
+    if (i < base || i - base >= lim) {
+      *err |= 1u << 12;
+      return p[0];
+    }
+    return p[i - base];
+  }
+#else
+  __device__ __forceinline__ uint2 operator[](uint64_t i) const { return p[(uint32_t)i - base]; }
+#endif
+};
+#if defined(KPE_PATVM_CHECK) && KPE_PATVM_CHECK
+#define PV_DOCVIEW(a, ptr, b, n) DocView{(ptr), (b), (n), (a).err}
+#else
+#define PV_DOCVIEW(a, ptr, b, n) DocView{(ptr), (b)}
+#endif
+
 // Bounds-checked table reads in KPE_PATVM_CHECK builds (scripts/patvm_check.cpp, the
 // libkpe_pvchk.so diagnostic): an out-of-range index reads element 0 instead and sets
 // bit `code` of *a.err, so a bad index shows up as a flag, never as a fault.
@@ -37,7 +64,7 @@ __device__ __forceinline__ uint32_t pv_fail(const PatArgs& a, uint32_t code) {
 
 // member named key1 (the flattener keeps only the last of duplicate names, as a Go map
 // decode does); kNoNode if absent
-__device__ __forceinline__ uint32_t pat_lookup(const PatArgs& a, const uint2* doc, uint32_t m, uint32_t key1) {
+__device__ __forceinline__ uint32_t pat_lookup(const PatArgs& a, DocView doc, uint32_t m, uint32_t key1) {
   if (key1 == 0u) return kNoNode;
   PV_KIDS(m, c, end);
   uint32_t i = c;
@@ -53,7 +80,7 @@ __device__ __forceinline__ uint32_t pat_lookup(const PatArgs& a, const uint2* do
   return kNoNode;
 }
 // ExpandInMetadata: first string member whose name matches the glob (bitset over D_KEY)
-__device__ __forceinline__ uint32_t pat_lookup_glob(const PatArgs& a, const uint2* doc, uint32_t m, uint32_t loc) {
+__device__ __forceinline__ uint32_t pat_lookup_glob(const PatArgs& a, DocView doc, uint32_t m, uint32_t loc) {
   PV_KIDS(m, c0, end);
   for (uint32_t c = c0; c < end; ++c) {
     const uint2 n = doc[PVD(c)];
@@ -347,7 +374,7 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
   }
 }
 // scalar id of node c (kNoNode for maps / lists); an absent member is null
-__device__ __forceinline__ uint32_t node_sid(const PatArgs& a, const uint2* doc, uint32_t c) {
+__device__ __forceinline__ uint32_t node_sid(const PatArgs& a, DocView doc, uint32_t c) {
   if (c == kNoNode) return SC_NULL_ID;
   const uint2 n = doc[PVD(c)];
   return DN_KIND(n.x) == DN_SCALAR ? n.y : kNoNode;
@@ -371,17 +398,88 @@ struct PFrame {
 // stack through a generic pointer, and flat accesses into the private aperture fault.
 constexpr uint32_t VM_BEGIN = 0, VM_STEP = 1, VM_RET = 2;
 
-struct PatVM {
+// A lane's frame stack. FramesPriv: a lane-private array (scratch memory). FramesLds: LDS,
+// word-planar (word w of frame i of the lane at b[(w * kDepth + i) * 64], b already offset by
+// the lane's index in its wave), so 64 lanes at any mix of depths hit 64 distinct banks and a
+// frame access costs an LDS round trip instead of a scratch one (scratch spills of 20 waves per
+// CU do not fit the L1 / L2 and wait on the Infinity Cache).
+struct FramesPriv {
+  static constexpr int kDepth = kPatStack;
+  PFrame st[kPatStack];
+  __device__ __forceinline__ PFrame get(int i) const { return st[i]; }
+  __device__ __forceinline__ void put(int i, const PFrame& f) { st[i] = f; }
+};
+#ifndef KPE_PAT_LDS_STACK
+#define KPE_PAT_LDS_STACK 8
+#endif
+struct FramesLds {
+  static constexpr int kDepth = KPE_PAT_LDS_STACK;
+  static constexpr uint32_t kWords = 7u;  // PFrame
+  uint32_t* b;
+  __device__ __forceinline__ PFrame get(int i) const {
+    const uint32_t* q = b + (uint32_t)i * 64u;
+    constexpr uint32_t W = (uint32_t)kDepth * 64u;
+    return PFrame{q[0], q[W], q[2 * W], q[3 * W], q[4 * W], q[5 * W], q[6 * W]};
+  }
+  __device__ __forceinline__ void put(int i, const PFrame& f) {
+    uint32_t* q = b + (uint32_t)i * 64u;
+    constexpr uint32_t W = (uint32_t)kDepth * 64u;
+    q[0] = f.kind_k, q[W] = f.r, q[2 * W] = f.pi, q[3 * W] = f.cnt, q[4 * W] = f.cur, q[5 * W] = f.x, q[6 * W] = f.c;
+  }
+};
+
+template <class FS>
+struct PatVMT {
   const PatArgs& a;
-  const uint2* doc;   // the whole tape (absolute entry indices)
+  DocView doc;   // the whole tape (absolute entry indices)
   uint32_t root;      // this resource's root entry (or a foreach element's entry)
   const uint2* pv;    // the row's resolved pattern variables
   uint32_t und;       // a leaf the device does not decide was reached
   uint32_t reg, val;  // AnchorMap: slots registered / present in the resource
   int sp;
-  PFrame st[kPatStack];
+  FS fs;
+  uint32_t* tr;  // TRACE walks: the path record of the last failure (KPE_TRACE_WORDS words)
+
+  // ---- failing paths (TRACE walks only; kpe_pattern_trace_kernel) ----
+  // PatternError.Path (validate.go:31-56): the reference returns the path of the element where
+  // the failure was found; a failure a condition / global anchor or an existence search
+  // absorbs is followed by further walking, so the last failure recorded is the one that
+  // reaches the root. A component is a pattern member (the key the handler appends:
+  // anchor.Key() or the raw key), an ExpandInMetadata key (the matched resource member's
+  // name) or an array index.
+  __device__ __forceinline__ uint32_t mcomp(uint32_t r, uint32_t mi) {
+    const uint4 m = a.members[PV(mi, a.nmembers, 2)];
+    if (m.x & PMF_GLOB) {
+      const uint32_t c = pat_lookup_glob(a, doc, r, m.w);
+      if (c != kNoNode) return KPE_TC_KEY | (DN_KEY(doc[PVD(c)].x) - 1u);
+    }
+    return mi;
+  }
+  __device__ __forceinline__ void tput(uint32_t& n, uint32_t c) {
+    if (n < KPE_TRACE_WORDS - 1u) tr[1u + n] = c;
+    ++n;
+  }
+  // the path of frames [0, nf) (each frame's current child) followed by `extra` (~0u: none)
+  __device__ __forceinline__ void snap(int nf, uint32_t extra) {
+    uint32_t n = 0;
+    for (int i = 0; i < nf; ++i) {
+      const PFrame F = fs.get(PV(i, FS::kDepth, 11));
+      const uint32_t kind = F.kind_k & 3u;
+      if (kind == PF_MAP) {
+        tput(n, mcomp(F.r, a.nodes[PV(F.pi, a.nnodes, 1)].y + (F.kind_k >> 2)));
+        if (F.x) tput(n, KPE_TC_IDX | (F.cur - (doc[PVD(F.c)].y + 1u)));  // existence search element
+      } else if (kind == PF_AMAPS) {
+        tput(n, KPE_TC_IDX | (F.cur - (doc[PVD(F.r)].y + 1u)));
+      } else {
+        tput(n, KPE_TC_IDX | (F.kind_k >> 2));
+      }
+    }
+    if (extra != ~0u) tput(n, extra);
+    tr[0] = (tr[0] & 0xFFFF0000u) | (n < KPE_TRACE_WORDS ? n : (KPE_TRACE_WORDS - 1u) | KPE_TR_TRUNC);
+  }
 
   // validate.MatchPattern (validate.go:31-56) of pattern root node `root_pi`
+  template <bool TRACE>
   __device__ __forceinline__ uint32_t run(uint32_t root_pi) {
     sp = -1, reg = 0u, val = 0u;
     uint32_t state = VM_BEGIN, br = root, bpi = root_pi, v = PE_NONE;
@@ -426,6 +524,7 @@ struct PatVM {
           if (pn.kind == PN_ARR_POS && end - c0 < pn.z) v = PE_OTHER_NOPATH;  // length mismatch: no path
           else v = push(pn.kind == PN_ARR_POS ? PF_APOS : PF_AMAPS, br, bpi, c0);
         }
+        if (TRACE && v == PE_OTHER) snap(sp + 1, ~0u);  // validateResourceElement returns its path
         if (v == PE_PUSHED) state = VM_STEP, v = PE_NONE;
         continue;
       }
@@ -435,7 +534,7 @@ struct PatVM {
         continue;
       }
       // ---- VM_STEP: advance the top frame with child verdict v (PE_NONE: none pending) ----
-      PFrame& F = st[PV(sp, kPatStack, 11)];
+      PFrame F = fs.get(PV(sp, FS::kDepth, 11));
       const KpePNode pn = a.nodes[PV(F.pi, a.nnodes, 1)];
       if ((F.kind_k & 3u) == PF_MAP) {
         // validateMap (validate.go:118-175) + anchor/handlers.go
@@ -463,6 +562,7 @@ struct PatVM {
               const uint32_t pj = a.lists[PV(xl.y + F.x - 1u, a.nlists, 3)];
               if (a.nodes[PV(pj, a.nnodes, 1)].kind == PN_BAD || F.cur >= end) {
                 e = PE_OTHER, F.x = 0u;
+                if (TRACE) snap(sp, mcomp(F.r, m0 + k));  // existence: the anchor key's path
               } else {
                 br = F.cur, bpi = pj, begin_child = true;
                 break;
@@ -482,14 +582,17 @@ struct PatVM {
               const uint32_t c = (m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, F.r, m.w) : pat_lookup(a, doc, F.r, m.y);
               if (h == PM_NEG) {
                 e = c == kNoNode ? PE_OK : PE_NEG;
+                if (TRACE && e == PE_NEG) snap(sp, mcomp(F.r, m0 + k));
               } else if (c == kNoNode && h != PM_DEFAULT) {
                 e = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
               } else if ((m.x & PMF_STAR) ||
                          ((m.x & PMF_VSTAR) && pat_var_star(a, a.nodes[PV(m.z, a.nnodes, 1)].y, pv))) {
                 e = (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
+                if (TRACE && e == PE_OTHER) snap(sp, ~0u);  // "*": the map's own path (handlers.go:124-140)
               } else if (h == PM_EXIST) {
                 if (DN_KIND(doc[PVD(c)].x) != DN_ARR || a.nodes[PV(m.z, a.nnodes, 1)].kind != PN_EXLIST) {
-                  e = PE_OTHER;
+                  e = PE_OTHER;  // existence anchor on a non-list value / non-list pattern
+                  if (TRACE) snap(sp, mcomp(F.r, m0 + k));
                 } else {
                   F.x = 1u, F.cur = doc[PVD(c)].y + 1u, F.c = c;
                   continue;  // search
@@ -499,6 +602,7 @@ struct PatVM {
                 // pattern.Validate and RET's anchor mapping without the two VM round trips
                 const uint32_t li = a.nodes[PV(m.z, a.nnodes, 1)].y;
                 const uint32_t v1 = pat_leaf(a, node_sid(a, doc, c), li, pv, &und) ? PE_OK : PE_OTHER;
+                if (TRACE && v1 == PE_OTHER) snap(sp, mcomp(F.r, m0 + k));
                 e = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
               } else {
                 br = c, bpi = m.z, begin_child = true;
@@ -519,6 +623,7 @@ struct PatVM {
         }
         if (begin_child) {
           F.kind_k = PF_MAP | (k << 2), F.cnt = applied | (skips << 16);
+          fs.put(sp, F);
           state = VM_BEGIN, v = PE_NONE;
         } else {
           --sp;
@@ -545,6 +650,7 @@ struct PatVM {
           state = VM_RET, v = e;
         } else {
           F.kind_k = (F.kind_k & 3u) | (j << 2), F.cnt = applied, F.x = skips, F.cur = cur;
+          fs.put(sp, F);
           br = cur, bpi = pos ? a.lists[PV(pn.y + j, a.nlists, 3)] : pn.y;
           state = VM_BEGIN, v = PE_NONE;
         }
@@ -553,21 +659,24 @@ struct PatVM {
   }
 
   __device__ __forceinline__ uint32_t push(uint32_t kind, uint32_t r, uint32_t pi, uint32_t cur) {
-    if (sp + 1 >= kPatStack) {  // a resource as deep as a pattern nested past the lane's frame
+    if (sp + 1 >= FS::kDepth) {  // a resource as deep as a pattern nested past the lane's frame
       und = 1u;                 // stack: the cell is KPE_UNDECIDED (the caller decides)
       return PE_OTHER;
     }
     ++sp;
-    st[PV(sp, kPatStack, 11)] = PFrame{kind, r, pi, 0u, cur, 0u, 0u};
+    fs.put(PV(sp, FS::kDepth, 11), PFrame{kind, r, pi, 0u, cur, 0u, 0u});
     return PE_PUSHED;
   }
 };
 
 // verdict of one pattern: pass / skip / fail, or error when the PatternError path is empty
-__device__ __forceinline__ uint32_t pat_match_root(PatVM& vm, uint32_t root) {
+using PatVM = PatVMT<FramesPriv>;
+
+template <bool TRACE = false, class VM>
+__device__ __forceinline__ uint32_t pat_match_root(VM& vm, uint32_t root) {
   const PatArgs& a = vm.a;
   vm.und = 0u;
-  const uint32_t e = vm.run(a.roots[PV(2 * root, a.nroots, 8)]);
+  const uint32_t e = vm.template run<TRACE>(a.roots[PV(2 * root, a.nroots, 8)]);
   if (vm.und) return KPE_UNDECIDED_;
   if (e == PE_OK) return KPE_PASS_;
   if (e == PE_SKIP) return KPE_SKIP_;
@@ -576,12 +685,33 @@ __device__ __forceinline__ uint32_t pat_match_root(PatVM& vm, uint32_t root) {
   return KPE_FAIL_;
 }
 
-// kpe_pattern_kernel's body for resource r: resolve the row's KPE_PENDING_ pattern cells
-// (validate_resource.go:316-398: one pattern, or anyPattern's first pass / skip / fail). The
-// pattern roots of every rule run through one VM call site (a plain pattern is one root), so
-// the kernel holds a single copy of the VM: its code stays within the instruction cache.
-__device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
-  PatVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], a.pvals + (size_t)r * a.nvars, 0u};
+// One KPE_PENDING_ pattern cell (row r, column col) of pattern rule `pi` (col2pr - 1):
+// validate_resource.go:316-398: one pattern, or anyPattern's first pass / skip / fail
+template <class VM>
+__device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
+  const PatArgs& a = vm.a;
+  const KpePatRule pr = a.rules[pi];
+  if (pr.flags & PR_ANY_BAD) return KPE_ERROR_;  // anyPattern is not a list
+  const bool any = (pr.flags & PR_ANY) != 0u;
+  uint32_t fails = 0, skips = 0, last = KPE_PASS_;
+  bool passed = false, undec = false;
+  for (uint32_t k = 0; k < pr.nr && !passed && !undec; ++k) {
+    last = pat_match_root(vm, pr.r0 + k);
+    if (last == KPE_PASS_) passed = true;
+    else if (last == KPE_SKIP_) ++skips;
+    else if (last == KPE_UNDECIDED_) undec = true;
+    else ++fails;  // anyPattern: an empty-path error counts as a failure
+  }
+  return undec ? KPE_UNDECIDED_ : !any ? last : passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
+}
+
+// kpe_pattern_kernel's body for resource r: resolve the row's KPE_PENDING_ pattern cells.
+// The pattern roots of every rule run through one VM call site (a plain pattern is one root),
+// so the kernel holds a single copy of the VM: its code stays within the instruction cache.
+template <class FS>
+__device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs) {
+  PatVMT<FS> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
+                a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   // The row's cells are read four at a time (two aligned words funnel-shifted to the row's
   // byte offset), and the columns are visited in the same order by every lane, so the lanes of
@@ -601,29 +731,26 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r) {
       if (((x >> (8u * q)) & 0xFFu) != KPE_PENDING_) continue;
       const uint32_t pi = a.col2pr ? a.col2pr[c0 + q] : 0u;
       if (pi == 0u) continue;
-      const uint32_t i = pi - 1u;
-      const KpePatRule pr = a.rules[i];
 #if defined(DIAG_PATNOVM) && (KPE_DIAG & DIAG_PATNOVM)
-      row[pr.col] = (uint8_t)KPE_PASS_;  // diagnostic: the rule loop without the VM
+      row[c0 + q] = (uint8_t)KPE_PASS_;  // diagnostic: the rule loop without the VM
       continue;
 #endif
-      if (pr.flags & PR_ANY_BAD) {
-        row[pr.col] = (uint8_t)KPE_ERROR_;  // anyPattern is not a list
-        continue;
+      uint32_t v = pat_eval_cell(vm, pi - 1u);
+      if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
+        // a shallow (LDS) stack may have overflowed: the lane-private kPatStack-deep one decides
+        PatVMT<FramesPriv> deep{a, vm.doc, vm.root, vm.pv, 0u};
+        v = pat_eval_cell(deep, pi - 1u);
       }
-      const bool any = (pr.flags & PR_ANY) != 0u;
-      uint32_t fails = 0, skips = 0, last = KPE_PASS_;
-      bool passed = false, undec = false;
-      for (uint32_t k = 0; k < pr.nr && !passed && !undec; ++k) {
-        last = pat_match_root(vm, pr.r0 + k);
-        if (last == KPE_PASS_) passed = true;
-        else if (last == KPE_SKIP_) ++skips;
-        else if (last == KPE_UNDECIDED_) undec = true;
-        else ++fails;  // anyPattern: an empty-path error counts as a failure
-      }
-      const uint32_t v = undec ? KPE_UNDECIDED_ : !any ? last : passed ? KPE_PASS_
-                                                                 : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
-      row[pr.col] = (uint8_t)v;
+      row[c0 + q] = (uint8_t)v;
     }
   }
+}
+
+// First tape entry of row r's segment: the flattener appends a resource's bodies, then its
+// root entry (doc_off), then its images map (img_off), so row r starts right after row r - 1
+// (flatten.cpp DocBuilder::add). Every entry of row r's document lies in [beg, doc_off[r]].
+__device__ __forceinline__ uint64_t pat_row_beg(const PatArgs& a, int64_t r) {
+  if (r == 0) return 0;
+  const uint64_t im = a.img_off ? a.img_off[r - 1] : ~0ull;
+  return (im != ~0ull ? im : a.doc_off[r - 1]) + 1u;
 }

@@ -2262,6 +2262,7 @@ class Lowerer {
     KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0};
     crule.pv0 = (uint32_t)P.pat.vars.size();
     bool pss_excl = false, msg_pattern = false;
+    struct { bool on, any; uint32_t roots; } pat_report{false, false, 0u};
     if (!has_validate) {
       k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
       if (nonempty(r.get("verifyImages"))) throw CompileError("rule '" + rname + "': verifyImages is not supported");
@@ -2343,6 +2344,7 @@ class Lowerer {
         if (P.pat.rules.size() >= 65535) throw CompileError("more than 65535 pattern rules in one program");
         P.pat.rules.push_back(pr);
         k.handler = H_PATTERN;
+        if (!(pr.flags & PR_ANY_BAD)) pat_report = {true, (pr.flags & PR_ANY) != 0u, pr.nr};
       } else if (v->get("foreach") && v->get("foreach")->t == JV::Arr && !v->get("foreach")->a.empty()) {
         // validateForEach (validate_resource.go:186-254): deny, pattern / anyPattern and nested
         // entries
@@ -2385,6 +2387,12 @@ class Lowerer {
     }
     rr.pss_excl = pss_excl;
     rr.msg_pattern = msg_pattern;
+    if (pat_report.on) {
+      rr.pat_rule = true, rr.any_pattern = pat_report.any, rr.pat_roots = pat_report.roots;
+      const JV* m = v ? v->get("message") : nullptr;
+      rr.vmsg = (m && m->t == JV::Str) ? m->s : std::string();
+      rr.vmsg_vars = rr.vmsg.find("{{") != std::string::npos || rr.vmsg.find("$(") != std::string::npos;
+    }
     if (has_validate && !(ps && ps->t == JV::Obj && nonempty(ps)) && v->get("deny") && v->get("deny")->t == JV::Obj) {
       // a condition `message` would enter the rule's message: render only when there is none
       std::function<bool(const JV*)> has_msg = [&](const JV* j) -> bool {

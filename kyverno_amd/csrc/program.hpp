@@ -94,6 +94,12 @@ struct RuleReport {
   // preconditions
   bool msg_deny = false, msg_pre_skip = false;
   std::string deny_fail_msg;
+  // validate.pattern / anyPattern rule (kpe_pattern_traces paths): failure messages are
+  // buildErrorMessage / buildAnyPatternErrorMessage (validate_resource.go:418-454) of the rule's
+  // validate.message; `vmsg_vars`: it holds variables (the substituted text is not rendered)
+  bool pat_rule = false, any_pattern = false, vmsg_vars = false;
+  uint32_t pat_roots = 0;
+  std::string vmsg;
 };
 
 struct Program {

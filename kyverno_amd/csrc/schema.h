@@ -599,6 +599,16 @@ typedef struct KpeCond {
 typedef struct KpePatRule {
   uint32_t col, flags, r0, nr;
 } KpePatRule;
+// Failing-path record of one pattern root (kpe_pattern_traces, include/kpe.h): word 0 =
+// component count | KPE_TR_TRUNC | verdict << 16 | KPE_TR_VALID; words 1..15 = components from
+// the root: a pattern member index (the key its handler appends to the path), KPE_TC_KEY | D_KEY
+// id (an ExpandInMetadata key: the matched resource member's name) or KPE_TC_IDX | array index
+#define KPE_TRACE_WORDS 16u
+#define KPE_TRACE_ROOTS 4u
+#define KPE_TC_IDX 0x80000000u
+#define KPE_TC_KEY 0x40000000u
+#define KPE_TR_TRUNC 0x100u
+#define KPE_TR_VALID 0x1000000u
 
 // ---- condition programs (preconditions / deny / foreach-deny; kpe_cond_kernel) -------------
 // A query is the JMESPath expression of a whole-string {{ }} variable (or a foreach `list`),

@@ -313,6 +313,21 @@ class Engine:
         """3-bit packing of the verdict matrix into device memory at dst_ptr (kpe_pack_verdicts)."""
         check(load().kpe_pack_verdicts(self.device.h, ps.h, corpus.h, ctypes.c_void_p(dst_ptr), words))
 
+    def pattern_traces(self, ps: PolicySet, corpus: Corpus, cells) -> np.ndarray:
+        """Failing-path records of pattern cells (kpe_pattern_traces) after an evaluation of ps on
+        corpus: cells = flat indices row * R + column; returns (len(cells), KPE_TRACE_ROOTS,
+        KPE_TRACE_WORDS) uint32."""
+        c = np.ascontiguousarray(cells, dtype=np.uint64)
+        out = np.zeros((c.size, TRACE_ROOTS, TRACE_WORDS), dtype=np.uint32)
+        if c.size:
+            check(load().kpe_pattern_traces(self.device.h, ps.h, corpus.h, c.ctypes.data, c.size, out.ctypes.data))
+        return out
+
+    def row_traces(self, ps: PolicySet, corpus: Corpus, row: int) -> np.ndarray:
+        """Trace records of every cell of one row (the layout report_results(traces=) takes)."""
+        R = ps.num_rules
+        return self.pattern_traces(ps, corpus, np.arange(row * R, row * R + R, dtype=np.uint64))
+
     # ---- reference-shaped API ----
     def validate_batch(self, policies: Sequence[dict], resources: Sequence[dict],
                        namespace_labels: Optional[Dict[str, Dict[str, str]]] = None) -> List[List[EngineResponse]]:
@@ -360,11 +375,17 @@ class Engine:
         return self.validate_batch([policy_context.policy], [policy_context.resource], nsl)[0][0]
 
 
-def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None) -> List[dict]:
+TRACE_WORDS, TRACE_ROOTS = 16, 4  # include/kpe.h KPE_TRACE_WORDS / KPE_TRACE_ROOTS
+
+
+def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None, traces=None,
+                   corpus: Optional[Corpus] = None) -> List[dict]:
     """EngineResponseToReportResults (pkg/utils/report/results.go:89-156) for one resource row,
     through kpe_report_results, or kpe_report_results_msg when the resource (a dict or its JSON
     bytes) is given: then results carry the RuleResponse message (podSecurity pass / fail,
-    validate.pattern pass; no timestamp)."""
+    validate.pattern pass; no timestamp). With traces (Engine.row_traces of the row) and the
+    corpus, kpe_report_results_msg_tr adds the pattern / anyPattern failure and anyPattern pass
+    messages."""
     L = load()
     v = np.ascontiguousarray(verdict_row, dtype=np.uint8)
     m = None if cv_mask_row is None else np.ascontiguousarray(cv_mask_row, dtype=np.uint32)
@@ -379,6 +400,12 @@ def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None) 
         mp = None if m is None else m.ctypes.data
         if raw is None:
             n = L.kpe_report_results(ps.h, v.ctypes.data, mp, buf, cap)
+        elif traces is not None:
+            t = np.ascontiguousarray(traces, dtype=np.uint32)
+            if t.size != ps.num_rules * TRACE_ROOTS * TRACE_WORDS:
+                raise ValueError("traces: one record per rule of the row")
+            n = L.kpe_report_results_msg_tr(ps.h, corpus.h if corpus is not None else None, v.ctypes.data, mp,
+                                            t.ctypes.data, raw, len(raw), buf, cap)
         else:
             n = L.kpe_report_results_msg(ps.h, v.ctypes.data, mp, raw, len(raw), buf, cap)
         if n < 0:

@@ -270,6 +270,48 @@ long oracle_validate_ex(const char* policies_json, const char* exceptions_json, 
   }
 }
 
+// Per row, per rule: the RuleResponse message of pattern / anyPattern rules (validate_resource.go
+// :316-454; "" for other rules or no response, "\u0001" where the reference's text embeds a Go
+// error string). JSON array of rows. Single-threaded; test sizes only.
+long oracle_pattern_messages(const char* policies_json, const char* ndjson, size_t len, char* buf, size_t cap) {
+  try {
+    auto ps = load_policies(policies_json);
+    auto lines = split_lines(ndjson, len);
+    static const Labels empty;
+    std::string o = "[";
+    std::vector<uint8_t> row;
+    std::vector<std::string> msgs;
+    for (size_t i = 0; i < lines.size(); ++i) {
+      JPtr res = parse_json(std::string(lines[i].first, lines[i].second));
+      o += i ? ",[" : "[";
+      bool first = true;
+      for (auto& p : ps) {
+        validate(p, *res, empty, row, &msgs);
+        for (auto& m : msgs) {
+          o += first ? "\"" : ",\"";
+          first = false;
+          for (unsigned char ch : m) {
+            if (ch == '"' || ch == '\\') o += '\\', o += (char)ch;
+            else if (ch < 0x20) {
+              char t[8];
+              snprintf(t, sizeof t, "\\u%04x", ch);
+              o += t;
+            } else o += (char)ch;
+          }
+          o += '"';
+        }
+      }
+      o += ']';
+    }
+    o += ']';
+    if (o.size() + 1 <= cap) memcpy(buf, o.c_str(), o.size() + 1);
+    return (long)o.size();
+  } catch (const std::exception& ex) {
+    g_err = ex.what();
+    return -1;
+  }
+}
+
 // ---- pattern path (pkg/engine/{pattern,validate}) ----------------------------------
 // Values are JSON texts; numbers keep their literal type (integer literal -> int, else
 // float), so Go literals such as `7`, `7.0`, `nil`, `"x"` map 1:1. all_float=1 decodes

@@ -432,6 +432,7 @@ struct Rule {
   cond::Conditions deny;  // validate.deny.conditions (validate_resource.go:268-279)
   bool has_deny = false;
   bool pattern_vars = false;  // {{ }} variables in pattern / anyPattern (substitutePatterns)
+  std::string vmsg;           // validate.message (Validation.Message)
   struct ForEach {        // validate.foreach entry (validate_resource.go:186-254, newForEachValidator)
     cond::Query list;
     cond::Conditions pre, deny;
@@ -830,6 +831,7 @@ inline Rule compile_rule(const JPtr& raw) {
     r.pss_version = jstr(ps->get("version"));
     r.pss_excludes = parse_pss_excludes(ps->get("exclude"));
   } else if (r.has_validate) {
+    if (const JVal* m = v->get("message"); m && m->t == JT::Str) r.vmsg = m->s;
     // validate_resource.go:121-170: deny, then pattern/anyPattern, then foreach
     const JVal* deny = v->get("deny");
     const JVal* pt = v->get("pattern");
@@ -1007,9 +1009,33 @@ inline bool matches_resource_description(const Rule& r, const Policy& p, const M
   return fails == 0;
 }
 
+// RuleResponse messages of validatePatterns (validate_resource.go:316-454): *msg gets the text, or
+// kNeedsErrText when the reference's text embeds a Go error string (skips, empty-path
+// failures: PatternError.Error()) or a substituted message, which this restatement does not
+// produce
+constexpr const char* kNeedsErrText = "\x01";
+struct PatMsg {
+  const std::string* rule;
+  const std::string* vmsg;
+  std::string* out;
+};
+inline const std::string* pm_rule(const PatMsg* pm) {
+  static const std::string none;
+  return pm ? pm->rule : &none;
+}
+inline std::string build_error_message(const PatMsg& pm, const std::string& path) {  // :418-441
+  if (path.empty()) return kNeedsErrText;  // "... execution error: <err>"
+  if (pm.vmsg->empty()) return "validation error: rule " + *pm.rule + " failed at path " + path;
+  if (pm.vmsg->find("{{") != std::string::npos || pm.vmsg->find("$(") != std::string::npos) return kNeedsErrText;
+  std::string m = *pm.vmsg;
+  if (m.back() != '.') m += '.';
+  return "validation error: " + m + " rule " + *pm.rule + " failed at path " + path;
+}
+
 // validate_resource.go:316-398 validatePatterns (no exceptions, CREATE operation), after
 // substitutePatterns (:456-476: an error is RuleError "variable substitution failed")
-inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars, const JVal& res, const cond::Ctx* cx) {
+inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars, const JVal& res, const cond::Ctx* cx,
+                              const PatMsg* pm = nullptr) {
   JPtr pattern = pattern0, any = any0;
   if (vars) {
     try {
@@ -1025,23 +1051,45 @@ inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars,
       return UNSUPPORTED;
     }
   }
+  auto say = [&](const std::string& m) {
+    if (pm) *pm->out = m;
+  };
   if (pattern) {
     pat::MatchResult m = pat::match_pattern(res, *pattern);
-    if (m.k == pat::M_PASS) return PASS;
-    if (m.k == pat::M_SKIP) return SKIP;
+    if (m.k == pat::M_PASS) return say("validation rule '" + *pm_rule(pm) + "' passed."), PASS;
+    if (m.k == pat::M_SKIP) return say(kNeedsErrText), SKIP;  // pe.Error()
+    if (pm) say(build_error_message(*pm, m.path));
     return m.path.empty() ? ERROR : FAIL;
   }
-  if (cond::is_null(any) || any->t != JT::Arr) return ERROR;  // deserializeAnyPattern failure
-  int fails = 0, skips = 0;
+  if (cond::is_null(any) || any->t != JT::Arr) return say(kNeedsErrText), ERROR;  // deserializeAnyPattern failure
+  int fails = 0, skips = 0, idx = 0;
+  std::string errs;
+  bool err_text = false;
   for (auto& p : any->a) {
     pat::MatchResult m = pat::match_pattern(res, *p);
-    if (m.k == pat::M_PASS) return PASS;
-    if (m.k == pat::M_SKIP) ++skips;
-    else ++fails;  // an empty-path PatternError counts as a failure here
+    if (m.k == pat::M_PASS)
+      return say("validation rule '" + *pm_rule(pm) + "' anyPattern[" + std::to_string(idx) + "] passed."), PASS;
+    if (m.k == pat::M_SKIP) {
+      ++skips;
+    } else {
+      ++fails;  // an empty-path PatternError counts as a failure here
+      if (m.path.empty()) err_text = true;  // "rule %s[%d] failed: <err>"
+      errs += (errs.empty() ? "" : " ") + ("rule " + *pm_rule(pm) + "[" + std::to_string(idx) + "] failed at path " + m.path);
+    }
+    ++idx;
   }
-  if (skips > 0 && fails == 0) return SKIP;
-  if (fails > 0) return FAIL;
-  return PASS;
+  if (skips > 0 && fails == 0) return say(kNeedsErrText), SKIP;
+  if (fails > 0) {
+    if (pm) {  // buildAnyPatternErrorMessage (:443-454)
+      const std::string& vm = *pm->vmsg;
+      say(err_text ? std::string(kNeedsErrText)
+                   : vm.empty() ? "validation error: " + errs
+                                : vm.back() == '.' ? "validation error: " + vm + " " + errs
+                                                   : "validation error: " + vm + ". " + errs);
+    }
+    return FAIL;
+  }
+  return say(pm ? *pm->vmsg : std::string()), PASS;  // RulePass(rule.Validation.Message)
 }
 
 // validate_resource.go:268-279 validateDeny: conditions true => FAIL, false => PASS, error => ERROR
@@ -1268,8 +1316,10 @@ inline void attach_exceptions(Policy& p, const std::vector<PolicyException>& xs,
 }
 
 // engine.go:87-101 + validation.go:16-80. out[i] = status of computed rule i.
-inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, std::vector<uint8_t>& out) {
+inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, std::vector<uint8_t>& out,
+                     std::vector<std::string>* msgs = nullptr) {
   out.assign(p.rules.size(), NA);
+  if (msgs) msgs->assign(p.rules.size(), std::string());
   try {  // NewPolicyContext -> AddImageInfos (policy_context.go:230): an error means no response at all
     img::extract_images(res);
   } catch (const img::ImageError&) {
@@ -1322,7 +1372,10 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
       if (!done) {
         if (r.has_pss) s = pss_handler(r, res, u.kind(), pss_exc);
         else if (r.has_deny) s = deny_handler(r, cx);
-        else if (r.pattern || r.any_pattern) s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx);
+        else if (r.pattern || r.any_pattern) {
+          PatMsg pm{&r.name, &r.vmsg, msgs ? &(*msgs)[i] : nullptr};
+          s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx, msgs ? &pm : nullptr);
+        }
         else if (!r.foreach.empty()) s = foreach_handler(r, cx, res);
       }
     }

@@ -148,7 +148,7 @@ int main(int argc, char** argv) {
   char nb[2][16];
   for (int64_t r = 0; r < a.n; ++r) cond_eval_row<true>(a, r, nb);  // kpe_cond_kernel's lane body
   if (!PP.rules.empty())
-    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(pa, r);  // then kpe_pattern_kernel's
+    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(pa, r, FramesPriv{});  // then kpe_pattern_kernel's
   if (perr) return fprintf(stderr, "pattern VM bounds flags 0x%x\n", perr), 1;
   FILE* f = fopen(argv[4], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);

@@ -484,6 +484,42 @@ def engine_validate_cases():
     return out
 
 
+def engine_message_cases():
+    """pkg/engine/validation_test.go: tests whose policy / resource are raw JSON literals and
+    that assert RuleResponse messages, either a `msgs := []string{...}` list checked against
+    er.PolicyResponse.Rules in order or `er.PolicyResponse.Rules[i].Message()` equalities."""
+    path = os.path.join(REF, "pkg/engine/validation_test.go")
+    src = open(path).read()
+    out = []
+    funcs = [(m.start(), m.group(1)) for m in re.finditer(r"^func (Test\w+)\(t \*testing\.T\)", src, re.M)]
+    funcs.append((len(src), None))
+    gostr = r'"((?:[^"\\]|\\.)*)"'
+    for (a, name), (b, _) in zip(funcs, funcs[1:]):
+        body = src[a:b]
+        if "Message()" not in body:
+            continue
+        raws = {}
+        for m in re.finditer(r"(\w+)\s*:?=\s*\[\]byte\(`(.*?)`\)", body, re.S):
+            raws[m.group(1).lower()] = m.group(2)
+        try:
+            pol = json.loads(raws.get("rawpolicy") or raws.get("policyraw") or "")
+            res = json.loads(raws.get("rawresource") or raws.get("resourceraw") or "")
+        except ValueError:
+            continue
+        msgs = {}
+        m = re.search(r"msgs\s*:=\s*\[\]string\{(.*?)\n\s*\}", body, re.S)
+        if m:
+            for i, x in enumerate(re.finditer(gostr, m.group(1))):
+                msgs[i] = json.loads('"' + x.group(1) + '"')
+        for x in re.finditer(r"Rules\[(\d+)\]\.Message\(\),\s*" + gostr, body):
+            msgs[int(x.group(1))] = json.loads('"' + x.group(2) + '"')
+        if msgs:
+            out.append({"name": name, "line": src.count("\n", 0, a) + 1, "policy": pol, "resource": res,
+                        "messages": {str(k): v for k, v in sorted(msgs.items())}})
+    print(f"engine_message_cases: {len(out)} tests")
+    return out
+
+
 def _render_chart_template(text):
     name = re.search(r'\$name := "([^"]+)"', text).group(1)
     out, stack = [], []  # stack of "branch active" flags
@@ -639,6 +675,7 @@ def image_cases():
 
 
 if __name__ == "__main__":
+    _dump("engine_message_cases.json", engine_message_cases())
     _dump("image_cases.json", image_cases())
     _dump("condition_cases.json", condition_cases())
     _dump("best_practices.json", best_practices())

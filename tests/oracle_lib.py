@@ -44,6 +44,8 @@ class Oracle:
         L.oracle_condition.argtypes = [cp, cp, cp]
         L.oracle_image_info.argtypes = [cp, cp, ctypes.c_size_t]
         L.oracle_images_context.argtypes = [cp, cp, ctypes.c_size_t]
+        L.oracle_pattern_messages.argtypes = [cp, cp, ctypes.c_size_t, cp, ctypes.c_size_t]
+        L.oracle_pattern_messages.restype = ctypes.c_long
 
     def wildcard(self, pattern, text):
         return bool(self.lib.oracle_wildcard_match(pattern.encode(), text.encode()))
@@ -77,6 +79,22 @@ class Oracle:
         if n < 0:
             raise RuntimeError(self.lib.oracle_last_error().decode())
         return buf.value.decode().splitlines()
+
+    NEEDS_ERR_TEXT = "\x01"  # the reference's message embeds a Go error string (not restated)
+
+    def pattern_messages(self, policies, ndjson: bytes):
+        """Per row, per rule: the pattern / anyPattern RuleResponse message (validate_resource.go
+        :316-454), "" for other rules / no response, NEEDS_ERR_TEXT where it embeds an error."""
+        pj = json.dumps(policies).encode()
+        cap = 1 << 20
+        while True:
+            buf = ctypes.create_string_buffer(cap)
+            n = self.lib.oracle_pattern_messages(pj, ndjson, len(ndjson), buf, cap)
+            if n < 0:
+                raise RuntimeError(self.lib.oracle_last_error().decode())
+            if n < cap:
+                return json.loads(buf.value.decode())
+            cap = n + 1
 
     def validate(self, policies, ndjson: bytes, ns_labels=None, nthreads=1, exceptions=None, background=False):
         """Verdict matrix (N x R uint8, oracle status codes) for NDJSON resources, with
