@@ -7,9 +7,8 @@ are all-reduced once over RCCL after the timed region).
     x the PSS restricted:latest policy (R = 3 rules after autogen) per GPU.
 --config c3: a 1/8 shard (1.25M rows) of 10M mixed resources x 200 wildcard ClusterPolicies
     per GPU (configs[2]; the full 10M is the 8-GPU job).
---config c4: a 1/8 shard (625k rows) of 5M Deployments + Services x the selector policy set
-    (matchLabels with wildcards, matchExpressions, namespaceSelector over a 10k-namespace
-    label table) per GPU (configs[3]).
+--config c4: 5M Deployments + Services x the selector policy set (matchLabels with wildcards,
+    matchExpressions, namespaceSelector over a 10k-namespace label table) per GPU (configs[3]).
 --config c5: 1M Pods / Deployments with 1-64 containers x the require-requests-limits /
     disallow-latest-tag / host-ports / anchor pattern set per GPU (configs[4]).
 
@@ -29,6 +28,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# kpe_kernel_stats.scan_kernel -> kernel name (as rocprofv3 lists it)
+SCAN_KERNELS = {1: "kpe_scan_kernel", 3: "kpe_lean_kernel", 4: "kpe_lean3_kernel", 5: "kpe_lean4_kernel<1>",
+                6: "kpe_lean4_kernel<2>", 7: "kpe_lean5_kernel<1>", 8: "kpe_lean5_kernel<2>"}
 
 
 def cpu_model():
@@ -70,9 +72,9 @@ def main():
         policies, mix, seed, n_def, rep_def, docs = c3_policy_set(), K.SYNTH_C3, 0xC3, 1_250_000, 1, True
         workload = ("C3: 1/8 shard (1.25M rows) of 10M mixed resources x 200 wildcard ClusterPolicies per GPU")
     elif cfg == "c4":
-        policies, mix, seed, n_def, rep_def, docs = c4_policy_set(), K.SYNTH_SELECTORS, 0xC4, 625_000, 1, False
-        workload = ("C4: 1/8 shard (625k rows) of 5M Deployments + Services x selector policies "
-                    "(namespaceSelector over 10k namespaces) per GPU")
+        policies, mix, seed, n_def, rep_def, docs = c4_policy_set(), K.SYNTH_SELECTORS, 0xC4, 5_000_000, 1, False
+        workload = ("C4: 5M Deployments + Services x selector policies (namespaceSelector over 10k namespaces) "
+                    "per GPU")
     else:
         policies, mix, seed, n_def, rep_def, docs = c5_policy_set(), K.SYNTH_FANOUT, 0xC5, 1_000_000, 1, True
         workload = "C5: 1M Pods/Deployments with 1-64 containers x requests-limits/latest-tag/host-ports/anchor patterns"
@@ -210,9 +212,13 @@ def main():
     value = evals / elapsed
 
     traffic = None
+    scan_kernel = SCAN_KERNELS.get(st.scan_kernel, "kpe_scan_kernel")
     if os.path.exists(traffic_json):
         try:
-            traffic = json.load(open(traffic_json)).get("scan_bytes_per_launch")
+            tj = json.load(open(traffic_json))
+            # only counters taken on the kernel this run launched (a stale file is not this kernel's)
+            if tj.get("kernel", "").split("(")[0].replace(" ", "") == scan_kernel.replace(" ", ""):
+                traffic = tj.get("scan_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -243,7 +249,7 @@ def main():
     if rank == 0:
         scan_roof = {"bound": "hbm", "achieved": scan_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": scan_achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "kpe_lean3_kernel" if cfg == "c2" else "kpe_scan_kernel",
+                     "kernel": scan_kernel,
                      "kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes, "dict_kernel_ms": dict_ms,
                      "pattern_kernel_ms": pat_ms,
                      # the same bytes over the timed region's step time (launches of different

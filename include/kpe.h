@@ -286,6 +286,10 @@ typedef struct kpe_kernel_stats {
   double pattern_bytes;     /* algorithmic bytes of one pattern-kernel launch: every resource's
                                document tape (8 B per entry) and root offset once, plus the verdict
                                matrix read and written */
+  int32_t scan_kernel;      /* the scan instantiation of the last timed launch: 1 kpe_scan_kernel
+                               (general), 4 kpe_lean3_kernel, 5/6 kpe_lean4_kernel<1/2>, 7/8
+                               kpe_lean5_kernel<1/2> (KPE_SCAN_* codes) */
+  int32_t pad_;
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);
 kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c,

@@ -26,7 +26,8 @@ class Counts(ctypes.Structure):
 class KernelStats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("pss_kernel_ms", ctypes.c_double),
                 ("dict_kernel_ms", ctypes.c_double), ("scan_bytes", ctypes.c_double),
-                ("pattern_kernel_ms", ctypes.c_double), ("pattern_bytes", ctypes.c_double)]
+                ("pattern_kernel_ms", ctypes.c_double), ("pattern_bytes", ctypes.c_double),
+                ("scan_kernel", ctypes.c_int32), ("pad_", ctypes.c_int32)]
 
 
 def lib_path():

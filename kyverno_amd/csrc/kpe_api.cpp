@@ -124,12 +124,14 @@ struct kpe_device {
   struct EvPair {
     hipEvent_t a, b, c, d;
     double bytes, pbytes;
+    int kind;        // scan instantiation (kpe_kernel_stats::scan_kernel)
     bool pre, post;  // a kernel ran between a and b (dictionary pass / prologue), c and d (later passes)
   };
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
   uint64_t launches = 0;
   double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0, last_pbytes = 0;
+  int last_kind = 0;
   hipEvent_t get_ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -1371,6 +1373,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
                : (B.lean && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) + mb
                                               : scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
+    ev.kind = lean_go ? B.lean_kind : 1;
     dev->pending.push_back(ev);
   }
   return KPE_OK;
@@ -1851,6 +1854,7 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
     dev->pat_ms += p.post ? d3 : 0.0f;
     dev->last_bytes = p.bytes;
     dev->last_pbytes = p.pbytes;
+    dev->last_kind = p.kind;
     dev->launches++;
     dev->pool.push_back(p.a);
     dev->pool.push_back(p.b);
@@ -1864,6 +1868,8 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
   out->scan_bytes = dev->last_bytes;
   out->pattern_kernel_ms = dev->pat_ms;
   out->pattern_bytes = dev->last_pbytes;
+  out->scan_kernel = dev->last_kind;
+  out->pad_ = 0;
   if (reset) {
     dev->launches = 0;
     dev->pss_ms = dev->dict_ms = dev->pat_ms = 0;

@@ -410,7 +410,7 @@ struct FramesPriv {
   __device__ __forceinline__ void put(int i, const PFrame& f) { st[i] = f; }
 };
 #ifndef KPE_PAT_LDS_STACK
-#define KPE_PAT_LDS_STACK 8
+#define KPE_PAT_LDS_STACK 6  // deeper walks re-run on the private stack (FramesPriv)
 #endif
 struct FramesLds {
   static constexpr int kDepth = KPE_PAT_LDS_STACK;

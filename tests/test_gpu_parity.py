@@ -126,7 +126,7 @@ def test_selector_golden(engine):
         assert (v[0, 0] != 0) == case["matched"], case["name"]
 
 
-@pytest.mark.parametrize("n,seed", [(20000, 0xC4), (50000, 41), (625_000, 0xC4)])  # 625k: the C4 1/8 shard
+@pytest.mark.parametrize("n,seed", [(20000, 0xC4), (50000, 41), (625_000, 0xC4), (5_000_000, 0xC4)])  # 5M: C4 on one GPU
 def test_c4_selectors_bit_exact(engine, oracle, n, seed):
     from tests.policies import c4_policy_set
 

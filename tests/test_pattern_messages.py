@@ -86,10 +86,24 @@ def test_device_messages_match_reference(case):
     eng = K.Engine(ordinal=0)
     ps, corpus = K.PolicySet(pols), K.Corpus(nd)
     v, _, _ = eng.evaluate(ps, corpus)
+    if (v == 7).any():  # a `!` / `|` formed by a substituted variable: undecided on the device
+        pytest.skip("cell beyond the device's documented limits (KPE_UNDECIDED)")
     dm = _device_messages(eng, ps, corpus, v, [nd])
     resp = _responses(v[0])
     for i, want in case["messages"].items():
         assert dm[(0, resp[int(i)])] == want, (case["name"], i)
+
+
+def pattern_rule_names(pols):
+    """'<policy>/<rule>' of the validate.pattern / anyPattern rules, with their autogen forms."""
+    out = set()
+    for p in pols:
+        for r in p["spec"]["rules"]:
+            v = r.get("validate") or {}
+            if v.get("pattern") is not None or v.get("anyPattern") is not None:
+                for pre in ("", "autogen-", "autogen-cronjob-"):
+                    out.add(p["metadata"]["name"] + "/" + (pre + r["name"])[:63])
+    return out
 
 
 def _compare_with_oracle(oracle, pols, nd, max_rows=None):
@@ -100,9 +114,12 @@ def _compare_with_oracle(oracle, pols, nd, max_rows=None):
     rows = range(v.shape[0]) if max_rows is None else range(min(max_rows, v.shape[0]))
     om = oracle.pattern_messages(pols, b"\n".join(lines[: rows.stop]))
     dm = _device_messages(eng, ps, corpus, v, lines, rows)
-    pat_cols = {r for r in range(ps.num_rules)}
+    names = pattern_rule_names(pols)
+    pat_cols = {r for r in range(ps.num_rules) if ps.rule_names[r] in names}
     checked = rendered = 0
     for (i, r), got in dm.items():
+        if r not in pat_cols:
+            continue
         want = om[i][r]
         if want == "" and got == "":
             continue
