@@ -217,7 +217,8 @@ def main():
         try:
             tj = json.load(open(traffic_json))
             # only counters taken on the kernel this run launched (a stale file is not this kernel's)
-            if tj.get("kernel", "").split("(")[0].replace(" ", "") == scan_kernel.replace(" ", ""):
+            norm = lambda k: k.split("(")[0].replace("void ", "").replace(" ", "")  # noqa: E731
+            if norm(tj.get("kernel", "")) == norm(scan_kernel):
                 traffic = tj.get("scan_bytes_per_launch")
         except Exception:
             traffic = None
