@@ -1126,102 +1126,6 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
   pat_eval_row(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]});
 }
 
-// LDS-staged pattern evaluation. Each wave owns a contiguous range of rows and walks it in
-// batches: the longest run of consecutive rows whose tape segments fit the wave's LDS slot
-// is copied there with coalesced loads (a row's segment is contiguous and consecutive rows'
-// segments are adjacent, so a batch is one contiguous tape range), then the batch's
-// KPE_PENDING_ pattern cells, found by a coalesced read of its verdict block (rows are
-// contiguous there too), are queued in LDS and evaluated one cell per lane. The VM's
-// document reads, the dependent chain of every walk, then hit LDS instead of L2 / HBM,
-// and a wave's lanes carry cells of a few rows, so a long document occupies many lanes
-// instead of stretching one lane's walk. A row whose segment alone exceeds the slot is a
-// batch of its own that walks the tape in HBM.
-#ifndef KPE_PAT_LDS_BLOCKS
-#define KPE_PAT_LDS_BLOCKS 3  // 256-thread blocks per CU (LDS: 4 x (8 KiB + 2 KiB) each)
-#endif
-constexpr uint32_t kPatTape = KPE_PAT_LDS_WORDS;
-constexpr uint32_t kPatRing = 512;  // queued cells per wave (byte offsets into the batch's verdict block)
-
-__global__ void __launch_bounds__(256, KPE_PAT_LDS_BLOCKS)
-    kpe_pattern_lds_kernel(const PatArgs* __restrict__ ap, int64_t rows_per_wave) {
-  __shared__ uint2 s_tape[4][kPatTape];
-  __shared__ uint32_t s_ring[4][kPatRing];
-  const PatArgs& a = *ap;
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  uint2* tape = s_tape[wv];
-  uint32_t* ring = s_ring[wv];
-  const uint2* gdoc = reinterpret_cast<const uint2*>(a.doc);
-  const uint32_t R = a.R;
-  const uint64_t lt = lane ? (~0ull >> (64u - lane)) : 0ull;  // lanes below this one
-  int64_t r0 = ((int64_t)blockIdx.x * 4 + wv) * rows_per_wave;
-  const int64_t rend = r0 + rows_per_wave < a.n ? r0 + rows_per_wave : a.n;
-  while (r0 < rend) {
-    // ---- the batch: rows [r0, r0 + nb) (wave-uniform values from ballots / readlanes)
-    const uint64_t beg = pat_row_beg(a, r0);
-    const int64_t rr = r0 + lane;
-    const uint64_t e = rr < rend ? a.doc_off[rr] + 1u : ~0ull;  // segment ends grow with the row
-    const uint64_t fit = __ballot(e - beg <= (uint64_t)a.stage_max);
-    uint32_t nb = fit == ~0ull ? 64u : (uint32_t)__builtin_ctzll(~fit);
-    const bool staged = nb > 0u;
-    if (!staged) nb = 1u;
-    DocView doc = PV_DOCVIEW(a, gdoc, 0u, a.ndoc);
-    if (staged) {
-      const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)e, nb - 1u);
-      const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(e >> 32), nb - 1u);
-      const uint32_t cnt = (uint32_t)((((uint64_t)hi << 32) | lo) - beg);
-      for (uint32_t i = lane; i < cnt; i += 64u) tape[i] = gdoc[beg + i];
-      __builtin_amdgcn_wave_barrier();
-      doc = PV_DOCVIEW(a, tape, (uint32_t)beg, cnt);
-    }
-    // ---- the batch's pending cells: its verdict block [r0 R, (r0 + nb) R) read a word per lane
-    const uint64_t vb = (uint64_t)r0 * R, ve = vb + (uint64_t)nb * R;
-    const uint32_t* vw = reinterpret_cast<const uint32_t*>(a.verdicts);
-    uint32_t head = 0u, tail = 0u;  // ring [head, tail), wave-uniform
-    for (uint64_t w0 = vb & ~3ull;; w0 += 256u) {
-      const bool more = w0 < ve;
-      if (more) {
-        const uint64_t p = w0 + 4u * lane;
-        const uint32_t x = p < ve ? vw[p >> 2] : 0u;
-        uint32_t cnt = 0u;
-        uint64_t m[4];
-#pragma unroll
-        for (uint32_t q = 0; q < 4u; ++q) {
-          const uint64_t c = p + q;
-          const bool pend = c >= vb && c < ve && ((x >> (8u * q)) & 0xFFu) == KPE_PENDING_ &&
-                            a.col2pr[(uint32_t)(c - vb) % R] != 0u;
-          m[q] = __ballot(pend);
-          if (pend) {
-            const uint32_t slot = tail + cnt + (uint32_t)__builtin_popcountll(m[q] & lt);
-            ring[slot & (kPatRing - 1u)] = (uint32_t)(c - vb);
-          }
-          cnt += (uint32_t)__builtin_popcountll(m[q]);
-        }
-        tail += cnt;
-        __builtin_amdgcn_wave_barrier();
-      }
-      // evaluate full rounds; at the end of the block, the rest
-      while (tail - head >= 64u || (!more && tail != head)) {
-        const uint32_t k = head + lane;
-        if (k < tail) {
-          const uint32_t off = ring[k & (kPatRing - 1u)];
-          const uint32_t rl = off / R, col = off - rl * R;
-          const int64_t row = r0 + rl;
-#if defined(DIAG_PATNOVM) && (KPE_DIAG & DIAG_PATNOVM)
-          a.verdicts[vb + off] = (uint8_t)KPE_PASS_;
-#else
-          PatVM vm{a, doc, (uint32_t)a.doc_off[row], a.pvals + (size_t)row * a.nvars, 0u};
-          a.verdicts[vb + off] = (uint8_t)pat_eval_cell(vm, a.col2pr[col] - 1u);
-#endif
-        }
-        head += tail - head < 64u ? tail - head : 64u;
-      }
-      if (!more) break;
-    }
-    __builtin_amdgcn_wave_barrier();  // the next batch overwrites the tape slot
-    r0 += nb;
-  }
-}
-
 // ===========================================================================
 // Preconditions / deny / foreach-deny conditions (condvm.inl): one lane per resource resolves
 // the cells of the rules whose conditions read the resource. Runs after the scan kernel (which
@@ -1325,24 +1229,8 @@ extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint6
   return hipGetLastError();
 }
 
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lds, hipStream_t s) {
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s) {
   if (n <= 0 || npr == 0) return hipSuccess;
-  if (lds) {
-    // about two waves per resident wave slot, each a contiguous run of rows
-    static thread_local int cus = 0;
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    }
-    const int64_t slots = (int64_t)cus * KPE_PAT_LDS_BLOCKS * 4 * 2;
-    int64_t waves = (n + 31) / 32;
-    if (waves > slots) waves = slots;
-    const int64_t rpw = (n + waves - 1) / waves;
-    const int64_t blocks = ((n + rpw - 1) / rpw + 3) / 4;
-    hipLaunchKernelGGL(kpe_pattern_lds_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dargs, rpw);
-    return hipGetLastError();
-  }
   // one lane per row running every pattern rule (a rows x rules grid measured no faster on C5 and
   // slower on C3's 600 rules; it also doubled the VM code the kernel holds)
   hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK)), dim3(KPE_PAT_BLOCK), 0,

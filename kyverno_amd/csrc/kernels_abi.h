@@ -29,6 +29,7 @@
 #define PK_GLOB 5u      // general: full pattern text
 #define PK_QNAME 6u     // validation.IsQualifiedName (apimachinery v0.29.1, label keys)
 #define PK_LABVAL 7u    // validation.IsValidLabelValue
+#define PK_NONEMPTY 8u  // '*'s around one '?' ("?*", "*?", "*?*"): one rune or more, i.e. non-empty
 struct KpePat {
   uint32_t kind, off, len, pad;  // literal (or full pattern for PK_GLOB) = pat_bytes[off, off+len)
 };
@@ -169,20 +170,13 @@ struct ScanArgs {
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null
 };
 
-#ifndef KPE_PAT_LDS_WORDS
-#define KPE_PAT_LDS_WORDS 1024  // kpe_pattern_lds_kernel: tape entries (8 B) staged per wave, 8 KiB
-#endif
 // kpe_pattern_kernel arguments (device-resident, one copy per binding)
 struct PatArgs {
   int64_t n;
   uint32_t R, npr;                 // rules per row, pattern rules
   const uint32_t* doc;             // document tape (2 words per node)
   const uint64_t* doc_off;         // first node of each resource
-  const uint64_t* img_off;         // root entry of each resource's images map (~0: none); with
-                                   // doc_off it bounds each row's tape segment (patvm.inl pat_row_beg)
   const uint32_t* perm;            // lane -> row: rows by descending tape size (wave-uniform walk lengths)
-  uint32_t stage_max;              // kpe_pattern_lds_kernel: tape entries a batch may stage in LDS
-  uint32_t pad2_;
   const KpeScalar* scal;
   const uint8_t* scal_text;
   const KpePNode* nodes;

@@ -28,7 +28,7 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lds, hipStream_t s);
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
                                                hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s);
@@ -91,7 +91,7 @@ struct DevBuf {
 
 template <class T>
 hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
-  hipError_t e = b.ensure(v.size() * sizeof(T));
+  hipError_t e = b.ensure(v.size() * sizeof(T) + 16);  // + slack: word-wide text compares read past a string
   if (e != hipSuccess) return e;
   if (!v.empty()) return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
   return hipSuccess;
@@ -1208,13 +1208,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.npr = (uint32_t)P.pat.rules.size();
       pa.doc = D.doc.as<uint32_t>();
       pa.doc_off = D.doc_off.as<uint64_t>();
-      pa.img_off = D.img_off.as<uint64_t>();
       pa.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();  // C3 14.0 -> 8.5 ms, C5 27.6 -> 19.4 ms
-      {  // tape entries one batch of kpe_pattern_lds_kernel stages (KPE_PAT_STAGE: tests force the HBM walk)
-        const char* st = getenv("KPE_PAT_STAGE");
-        const long v = st ? atol(st) : (long)KPE_PAT_LDS_WORDS;
-        pa.stage_max = (uint32_t)std::min<long>(std::max<long>(v, 0L), (long)KPE_PAT_LDS_WORDS);
-      }
       pa.scal = D.scal.as<KpeScalar>();
       pa.scal_text = D.scal_text.as<uint8_t>();
       pa.nodes = PD.pnodes.as<KpePNode>();
@@ -1348,10 +1342,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
-    // kpe_pattern_kernel (lane per row); KPE_PAT_TAPE selects kpe_pattern_lds_kernel (rows' tapes
-    // staged in LDS, lane per cell: measured slower, C5 55 vs 19 ms, profiles/r03_b_ldstape)
-    const bool tape_kernel = getenv("KPE_PAT_TAPE") != nullptr;
-    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), tape_kernel ? 1 : 0, s));
+    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;
       HIPCHK(hipMemcpyAsync(&e, B.perr.p, 4, hipMemcpyDeviceToHost, s));

@@ -23,6 +23,7 @@ inline KpePat classify_pattern(const std::string& g, std::vector<uint8_t>& bytes
   else if (!q && stars == 1 && g.back() == '*') p.kind = PK_PREFIX;
   else if (!q && stars == 1 && g.front() == '*') p.kind = PK_SUFFIX;
   else if (!q && stars == 2 && g.size() >= 2 && g.front() == '*' && g.back() == '*') p.kind = PK_CONTAINS;
+  else if (stars >= 1 && std::count(g.begin(), g.end(), '?') == 1 && stars + 1 == g.size()) p.kind = PK_NONEMPTY;
   switch (p.kind) {
     case PK_ANY: put(""); break;
     case PK_EXACT: put(g); break;

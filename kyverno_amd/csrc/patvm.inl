@@ -10,10 +10,11 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 constexpr int kPatStack = KPE_PAT_STACK;  // frames of one lane; deeper walks give KPE_UNDECIDED
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
 
-// The tape as the VM reads it: entry i (an absolute tape index) is p[i - base]. The pattern
-// kernel stages a batch of rows' tape segments in LDS (p: the wave's LDS copy, base: the
-// batch's first entry); every other walk reads the tape itself (base 0). p is a generic
-// pointer, so the same VM code reads either.
+// The tape as the VM reads it: entry i (an absolute tape index) is p[i - base] (a staged copy of a
+// tape range, or the tape itself with base 0). Round 3 measured a kernel that staged batches of
+// rows' tape segments in LDS and ran one lane per cell: C5 55-120 ms against the lane-per-row
+// kernel's 15.6 (profiles/r03_b_ldstape, r03_d_tapeframes), so every walk now reads the tape in
+// HBM; the view stays for the host check builds' bounded copies.
 struct DocView {
   const uint2* p;
   uint32_t base;
@@ -56,6 +57,24 @@ __device__ __forceinline__ uint32_t pv_fail(const PatArgs& a, uint32_t code) {
 #define PVD(i) (i)
 #endif
 
+// Program tables (nodes, members, lists, leaves, string conditions, operand records): the lanes
+// of a wave walk the same rule's pattern in step, so an index is usually the same in every active
+// lane; then the record is read with a scalar load through the constant cache instead of a vector
+// load through L1 / L2 (the tables are read-only while the kernel runs).
+template <class T>
+__device__ __forceinline__ T pu_load(const T* p, uint32_t i) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const uint32_t u = __builtin_amdgcn_readfirstlane(i);
+  if (__ballot(i != u) == 0ull) return sld(p, u);
+#endif
+  return p[i];
+}
+#if defined(KPE_PATVM_CHECK) && KPE_PATVM_CHECK
+#define PU(tbl, i, n, code) ((tbl)[PV(i, n, code)])
+#else
+#define PU(tbl, i, n, code) pu_load((tbl), (uint32_t)(i))
+#endif
+
 // children of container entry e: entries [first, end) of its body
 #define PV_KIDS(e, first, end)                   \
   const uint32_t first##_b = doc[PVD(e)].y;      \
@@ -92,15 +111,34 @@ __device__ __forceinline__ uint32_t pat_lookup_glob(const PatArgs& a, DocView do
   return kNoNode;
 }
 
+// Eight bytes at any address of a device text buffer (pattern bytes, scalar texts): two aligned
+// 8-byte loads and a funnel shift instead of eight byte loads (buffers carry 16 bytes of slack,
+// kpe_api.cpp upload; the bytes past a string are masked off by the caller)
+__device__ __forceinline__ uint64_t ld8u(const uint8_t* p) {
+  const uintptr_t x = reinterpret_cast<uintptr_t>(p);
+  const uint64_t* w = reinterpret_cast<const uint64_t*>(x & ~(uintptr_t)7);
+  const uint32_t sh = (uint32_t)(x & 7u) * 8u;
+  const uint64_t lo = w[0];
+  return sh ? (lo >> sh) | (w[1] << (64u - sh)) : lo;
+}
+__device__ __forceinline__ bool bytes_eq_w(const uint8_t* a, const uint8_t* b, int n) {
+  for (int i = 0; i < n; i += 8) {
+    uint64_t d = ld8u(a + i) ^ ld8u(b + i);
+    if (n - i < 8) d &= (1ull << (8u * (uint32_t)(n - i))) - 1ull;
+    if (d) return false;
+  }
+  return true;
+}
 // compareString / exact-equality match: literal classes inline, contains / glob out of line
 __device__ __forceinline__ bool pv_match(const KpePat pt, const uint8_t* pb, const uint8_t* s, int sn) {
   const uint8_t* lit = pb + pt.off;
   const int ln = (int)pt.len;
   switch (pt.kind) {
     case PK_ANY: return true;
-    case PK_EXACT: return sn == ln && bytes_eq(lit, s, ln);
-    case PK_PREFIX: return sn >= ln && bytes_eq(lit, s, ln);
-    case PK_SUFFIX: return sn >= ln && bytes_eq(lit, s + sn - ln, ln);
+    case PK_NONEMPTY: return sn > 0;
+    case PK_EXACT: return sn == ln && bytes_eq_w(lit, s, ln);
+    case PK_PREFIX: return sn >= ln && bytes_eq_w(lit, s, ln);
+    case PK_SUFFIX: return sn >= ln && bytes_eq_w(lit, s + sn - ln, ln);
     default: return pat_match(pt, pb, s, sn);
   }
 }
@@ -138,7 +176,7 @@ __device__ __forceinline__ bool pat_cond(const PatArgs& a, const KpeScalar* v, u
     return op_holds(op, qcmp(vf & SC_QNEG, v->qexp, v->qlo, v->qhi, cop & PC_QNEG, cd->qexp, cd->qlo, cd->qhi));
   if (op != PC_EQ && op != PC_NE) return false;
   if (!(vf & SC_TEXT)) return false;
-  const bool m = pv_match(a.pats[PV(cd->pat, a.npats, 6)], a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len);
+  const bool m = pv_match(PU(a.pats, cd->pat, a.npats, 6), a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len);
   return op == PC_NE ? !m : m;
 }
 __device__ __forceinline__ int64_t go_f2i(double f) {
@@ -232,7 +270,8 @@ __device__ __forceinline__ bool tp_glob(const TPiece* pc, int np, int pb, int pe
 }
 // The resolved leaf equals the string "*" (the default handler's presence check)
 __device__ __forceinline__ bool pat_var_star(const PatArgs& a, uint32_t li, const uint2* pv) {
-  const KpeLeaf* L = a.leaves + PV(li, a.nleaves, 4);
+  const KpeLeaf Lv = PU(a.leaves, li, a.nleaves, 4);
+  const KpeLeaf* L = &Lv;
   if (L->type == PL_VAR) {
     const uint2 x = pv[L->c0];
     if (x.x != PVK_SCAL && x.x != PVK_CONST) return false;
@@ -267,7 +306,8 @@ __device__ __forceinline__ bool leaf_nil(const KpeScalar* v, uint32_t vf) {  // 
 // row's resolved pattern variables; *und set where the device leaves the cell undecided
 __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li, const uint2* pv, uint32_t* und) {
   if (sid == kNoNode) return false;  // no scalar validator accepts a map / list
-  const KpeLeaf* L = a.leaves + PV(li, a.nleaves, 4);
+  const KpeLeaf Lv = PU(a.leaves, li, a.nleaves, 4);
+  const KpeLeaf* L = &Lv;
 #if defined(DIAG_PATLEAF) && (KPE_DIAG & DIAG_PATLEAF)
   if (L->type != PL_VAR && L->type != PL_TMPL) return sid != 0xFFFFFFFEu;  // every leaf holds
 #endif
@@ -287,7 +327,7 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
       default: {  // a plain string pattern (SC_PSIMPLE): value == pattern, then validateString Equal
         const uint8_t* p = tb + S->text_off;
         const int pn = (int)S->text_len;
-        if (t == SC_T_STR && (int)v->text_len == pn && bytes_eq(a.scal_text + v->text_off, p, pn)) return true;
+        if (t == SC_T_STR && (int)v->text_len == pn && bytes_eq_w(a.scal_text + v->text_off, p, pn)) return true;
         if ((S->flags & SC_DUR) && (vf & SC_DUR)) return v->dur == S->dur;
         if ((S->flags & SC_QTY) && (vf & SC_QTY))
           return qcmp(vf & SC_QNEG, v->qexp, v->qlo, v->qhi, S->flags & SC_QNEG, S->qexp, S->qlo, S->qhi) == 0;
@@ -350,12 +390,13 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
         default: return v->text_len == 0u;
       }
     case PL_STR: {
-      if (t == SC_T_STR && pv_match(a.pats[PV(L->exact, a.npats, 6)], a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len))
+      if (t == SC_T_STR && pv_match(PU(a.pats, L->exact, a.npats, 6), a.pat_bytes, a.scal_text + v->text_off, (int)v->text_len))
         return true;  // value == pattern
       bool group = true;  // OR over `|` alternatives of an AND over their `&` terms
       const uint32_t c0 = L->c0, ce = c0 + L->nc;
       for (uint32_t i = c0; i < ce; ++i) {
-        const KpeCond* cd = a.conds + PV(i, a.nconds, 5);
+        const KpeCond cdv = PU(a.conds, i, a.nconds, 5);
+        const KpeCond* cd = &cdv;
         const uint32_t cop = cd->op;
         if ((cop & PC_NEWGROUP) && i != c0) {
           if (group) return true;
@@ -364,7 +405,8 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
         bool r = group && pat_cond(a, v, vf, cd);
         if (cop & PC_OR2) {  // NotInRange: `< lo` OR `> hi`
           ++i;
-          r = group && (r || pat_cond(a, v, vf, a.conds + PV(i, a.nconds, 5)));
+          const KpeCond cd2 = PU(a.conds, i, a.nconds, 5);
+          r = group && (r || pat_cond(a, v, vf, &cd2));
         }
         group = group && r;
       }
@@ -448,7 +490,7 @@ struct PatVMT {
   // anchor.Key() or the raw key), an ExpandInMetadata key (the matched resource member's
   // name) or an array index.
   __device__ __forceinline__ uint32_t mcomp(uint32_t r, uint32_t mi) {
-    const uint4 m = a.members[PV(mi, a.nmembers, 2)];
+    const uint4 m = PU(a.members, mi, a.nmembers, 2);
     if (m.x & PMF_GLOB) {
       const uint32_t c = pat_lookup_glob(a, doc, r, m.w);
       if (c != kNoNode) return KPE_TC_KEY | (DN_KEY(doc[PVD(c)].x) - 1u);
@@ -466,7 +508,7 @@ struct PatVMT {
       const PFrame F = fs.get(PV(i, FS::kDepth, 11));
       const uint32_t kind = F.kind_k & 3u;
       if (kind == PF_MAP) {
-        tput(n, mcomp(F.r, a.nodes[PV(F.pi, a.nnodes, 1)].y + (F.kind_k >> 2)));
+        tput(n, mcomp(F.r, PU(a.nodes, F.pi, a.nnodes, 1).y + (F.kind_k >> 2)));
         if (F.x) tput(n, KPE_TC_IDX | (F.cur - (doc[PVD(F.c)].y + 1u)));  // existence search element
       } else if (kind == PF_AMAPS) {
         tput(n, KPE_TC_IDX | (F.cur - (doc[PVD(F.r)].y + 1u)));
@@ -486,7 +528,7 @@ struct PatVMT {
     for (;;) {
       if (state == VM_BEGIN) {
         // ---- validateResourceElement (validate.go:71-114) ----
-        const KpePNode pn = a.nodes[PV(bpi, a.nnodes, 1)];
+        const KpePNode pn = PU(a.nodes, bpi, a.nnodes, 1);
         const uint32_t rk = br == kNoNode ? 0xFFu : DN_KIND(doc[PVD(br)].x);
         state = VM_RET;
         if (pn.kind == PN_LEAF && rk != DN_ARR) {
@@ -506,7 +548,7 @@ struct PatVMT {
           } else {
             const uint32_t nmem = pn.z >> 16;
             for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
-              const uint4 m = a.members[PV(pn.y + k, a.nmembers, 2)];
+              const uint4 m = PU(a.members, pn.y + k, a.nmembers, 2);
               if (m.x & PMF_XSLOT) und = 1u;
               if (m.x & PMF_SLOT) {
                 const uint32_t bit = 1u << PM_SLOT(m.x);
@@ -535,7 +577,7 @@ struct PatVMT {
       }
       // ---- VM_STEP: advance the top frame with child verdict v (PE_NONE: none pending) ----
       PFrame F = fs.get(PV(sp, FS::kDepth, 11));
-      const KpePNode pn = a.nodes[PV(F.pi, a.nnodes, 1)];
+      const KpePNode pn = PU(a.nodes, F.pi, a.nnodes, 1);
       if ((F.kind_k & 3u) == PF_MAP) {
         // validateMap (validate.go:118-175) + anchor/handlers.go
         const uint32_t m0 = pn.y, nanch = pn.z & 0xFFFFu, nmem = pn.z >> 16;
@@ -543,7 +585,7 @@ struct PatVMT {
         uint32_t e = PE_NONE;
         bool begin_child = false;
         if (v != PE_NONE) {  // the child BEGIN of member k finished with v
-          const uint32_t h = PM_HANDLER(a.members[PV(m0 + k, a.nmembers, 2)].x);
+          const uint32_t h = PM_HANDLER(PU(a.members, m0 + k, a.nmembers, 2).x);
           if (F.x) {  // existence search: element F.cur against pattern element F.x - 1
             if (v == PE_OK) F.x += 1u, F.cur = doc[PVD(F.c)].y + 1u;
             else F.cur += 1u;
@@ -553,14 +595,14 @@ struct PatVMT {
         }
         for (;;) {
           if (e == PE_NONE && F.x) {  // existence anchor: each pattern map needs one matching element
-            const KpePNode xl = a.nodes[PV(a.members[PV(m0 + k, a.nmembers, 2)].z, a.nnodes, 1)];
+            const KpePNode xl = PU(a.nodes, PU(a.members, m0 + k, a.nmembers, 2).z, a.nnodes, 1);
             PV_KIDS(F.c, c0, end);
             (void)c0;
             if (F.x - 1u >= xl.z) {
               e = PE_OK, F.x = 0u;
             } else {
-              const uint32_t pj = a.lists[PV(xl.y + F.x - 1u, a.nlists, 3)];
-              if (a.nodes[PV(pj, a.nnodes, 1)].kind == PN_BAD || F.cur >= end) {
+              const uint32_t pj = PU(a.lists, xl.y + F.x - 1u, a.nlists, 3);
+              if (PU(a.nodes, pj, a.nnodes, 1).kind == PN_BAD || F.cur >= end) {
                 e = PE_OTHER, F.x = 0u;
                 if (TRACE) snap(sp, mcomp(F.r, m0 + k));  // existence: the anchor key's path
               } else {
@@ -577,7 +619,7 @@ struct PatVMT {
               e = PE_OK;
               k = nmem + 1u;
             } else {
-              const uint4 m = a.members[PV(m0 + k, a.nmembers, 2)];
+              const uint4 m = PU(a.members, m0 + k, a.nmembers, 2);
               const uint32_t h = PM_HANDLER(m.x);
               const uint32_t c = (m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, F.r, m.w) : pat_lookup(a, doc, F.r, m.y);
               if (h == PM_NEG) {
@@ -586,11 +628,11 @@ struct PatVMT {
               } else if (c == kNoNode && h != PM_DEFAULT) {
                 e = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
               } else if ((m.x & PMF_STAR) ||
-                         ((m.x & PMF_VSTAR) && pat_var_star(a, a.nodes[PV(m.z, a.nnodes, 1)].y, pv))) {
+                         ((m.x & PMF_VSTAR) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv))) {
                 e = (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
                 if (TRACE && e == PE_OTHER) snap(sp, ~0u);  // "*": the map's own path (handlers.go:124-140)
               } else if (h == PM_EXIST) {
-                if (DN_KIND(doc[PVD(c)].x) != DN_ARR || a.nodes[PV(m.z, a.nnodes, 1)].kind != PN_EXLIST) {
+                if (DN_KIND(doc[PVD(c)].x) != DN_ARR || PU(a.nodes, m.z, a.nnodes, 1).kind != PN_EXLIST) {
                   e = PE_OTHER;  // existence anchor on a non-list value / non-list pattern
                   if (TRACE) snap(sp, mcomp(F.r, m0 + k));
                 } else {
@@ -600,7 +642,7 @@ struct PatVMT {
               } else if ((m.x & PMF_LEAF) && (c == kNoNode || DN_KIND(doc[PVD(c)].x) != DN_ARR)) {
                 // a scalar pattern against a scalar / absent value resolves in place: BEGIN's
                 // pattern.Validate and RET's anchor mapping without the two VM round trips
-                const uint32_t li = a.nodes[PV(m.z, a.nnodes, 1)].y;
+                const uint32_t li = PU(a.nodes, m.z, a.nnodes, 1).y;
                 const uint32_t v1 = pat_leaf(a, node_sid(a, doc, c), li, pv, &und) ? PE_OK : PE_OTHER;
                 if (TRACE && v1 == PE_OTHER) snap(sp, mcomp(F.r, m0 + k));
                 e = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
@@ -651,7 +693,7 @@ struct PatVMT {
         } else {
           F.kind_k = (F.kind_k & 3u) | (j << 2), F.cnt = applied, F.x = skips, F.cur = cur;
           fs.put(sp, F);
-          br = cur, bpi = pos ? a.lists[PV(pn.y + j, a.nlists, 3)] : pn.y;
+          br = cur, bpi = pos ? PU(a.lists, pn.y + j, a.nlists, 3) : pn.y;
           state = VM_BEGIN, v = PE_NONE;
         }
       }
@@ -744,13 +786,4 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs)
       row[c0 + q] = (uint8_t)v;
     }
   }
-}
-
-// First tape entry of row r's segment: the flattener appends a resource's bodies, then its
-// root entry (doc_off), then its images map (img_off), so row r starts right after row r - 1
-// (flatten.cpp DocBuilder::add). Every entry of row r's document lies in [beg, doc_off[r]].
-__device__ __forceinline__ uint64_t pat_row_beg(const PatArgs& a, int64_t r) {
-  if (r == 0) return 0;
-  const uint64_t im = a.img_off ? a.img_off[r - 1] : ~0ull;
-  return (im != ~0ull ? im : a.doc_off[r - 1]) + 1u;
 }

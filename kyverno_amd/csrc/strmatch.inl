@@ -101,6 +101,7 @@ __device__ bool pat_match(const KpePat& pt, const uint8_t* pb, const uint8_t* s,
       return false;
     case PK_QNAME: return qualified_name_ok(s, sn);
     case PK_LABVAL: return sn == 0 || name_part_ok(s, sn);
+    case PK_NONEMPTY: return sn > 0;
     default: return glob(lit, ln, s, sn);
   }
 }

@@ -73,7 +73,7 @@ int main(int argc, char** argv) {
   }
   std::vector<uint8_t> text(C.scal_text.begin(), C.scal_text.end()), ctext(CP.ctext.begin(), CP.ctext.end()),
       kb(C.dict[D_KEY].bytes.begin(), C.dict[D_KEY].bytes.end());
-  text.push_back(0), ctext.push_back(0), kb.push_back(0);
+  text.resize(text.size() + 17, 0), ctext.resize(ctext.size() + 17, 0), kb.push_back(0);
   std::vector<uint2> ops(CP.ops.size() / 2);
   for (size_t i = 0; i < ops.size(); ++i) ops[i] = uint2{CP.ops[2 * i], CP.ops[2 * i + 1]};
   CondArgs a{};
@@ -95,7 +95,7 @@ int main(int argc, char** argv) {
       pp.push_back(kpe::classify_pattern(P->pat.operands[i], pb));
     }
   }
-  pb.push_back(0);
+  pb.resize(pb.size() + 17, 0);
   a.leaves = P->pat.leaves.data(), a.pconds = P->pat.conds.data(), a.pats = pp.data(), a.pat_bytes = pb.data();
   a.verdicts = verdicts.data();
   // the pattern program as kpe_api.cpp binds it (members: names -> D_KEY ids, glob bitsets), for
@@ -128,7 +128,7 @@ int main(int argc, char** argv) {
   std::vector<uint2> tp(PP.tpieces.size() / 2 + 1);
   for (size_t i = 0; i + 1 < PP.tpieces.size(); i += 2) tp[i / 2] = uint2{PP.tpieces[i], PP.tpieces[i + 1]};
   std::vector<uint8_t> tt(PP.ttext.begin(), PP.ttext.end());
-  tt.push_back(0);
+  tt.resize(tt.size() + 17, 0);
   std::vector<uint32_t> col2pr(R + 4, 0u);
   for (size_t i = 0; i < PP.rules.size(); ++i) col2pr[PP.rules[i].col] = (uint32_t)i + 1u;
   uint32_t perr = 0;

