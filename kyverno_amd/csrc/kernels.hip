@@ -1115,7 +1115,7 @@ namespace {
 #endif                     // 128 x 8 18.1 / 7.8, 256 x 6 17.2 / 7.0, 128 x 6 16.8 / 6.9, + 4 waves/SIMD 15.6 / 7.0
 // the lane's frame stack lives in LDS (FramesLds, word-planar: conflict-free at any mix of depths)
 #ifndef KPE_PAT_MINW
-#define KPE_PAT_MINW 4  // 128 VGPRs
+#define KPE_PAT_MINW 3  // 168 VGPRs: the inline map path spills at 128 (profiles/r03_e_inline)
 #endif
 __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
   constexpr uint32_t kWaveWords = FramesLds::kWords * FramesLds::kDepth * 64u;

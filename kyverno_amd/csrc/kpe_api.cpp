@@ -91,7 +91,8 @@ struct DevBuf {
 
 template <class T>
 hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
-  hipError_t e = b.ensure(v.size() * sizeof(T) + 16);  // + slack: word-wide text compares read past a string
+  hipError_t e = b.ensure(v.size() * sizeof(T) + 128);  // + slack: word-wide text compares and the pattern
+                                                        // VM's 8-slot body loads read past the end
   if (e != hipSuccess) return e;
   if (!v.empty()) return hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
   return hipSuccess;

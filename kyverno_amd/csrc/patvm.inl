@@ -9,6 +9,11 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 #endif
 constexpr int kPatStack = KPE_PAT_STACK;  // frames of one lane; deeper walks give KPE_UNDECIDED
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
+#ifndef KPE_PAT_FLAT
+#define KPE_PAT_FLAT 2  // maps of inline depth <= this resolve in their BEGIN step (0: all through frames;
+                        // C5 / C3 ms, profiles/r03_e_inline: 0 14.2 / 5.3, 1 12.9 / 5.6, 2 at 4 waves 15.1 / 7.1
+                        // (spills), 2 at 3 waves 13.0 / 5.2, 3 15.3 / 8.0)
+#endif
 
 // The tape as the VM reads it: entry i (an absolute tape index) is p[i - base] (a staged copy of a
 // tape range, or the tape itself with base 0). Round 3 measured a kernel that staged batches of
@@ -520,6 +525,98 @@ struct PatVMT {
     tr[0] = (tr[0] & 0xFFFF0000u) | (n < KPE_TRACE_WORDS ? n : (KPE_TRACE_WORDS - 1u) | KPE_TR_TRUNC);
   }
 
+  // validateMap (validate.go:118-175) of a map of inline depth <= D (schema.h PNF_FLAT) against the
+  // resource map whose body is at tape index b: the body (at most 8 entries) is read once into
+  // registers, every member's handler (anchor/handlers.go) resolves against it in the member order
+  // the STEP state uses, and a map-valued member recurses. PE_NONE: some body on the way holds
+  // more than 8 entries, and the frame path validates the whole map (what the attempt set in the
+  // AnchorMap and `und` the frame walk sets again: it visits the same maps and leaves first).
+  template <int D>
+  __device__ __forceinline__ uint32_t flat_map(uint32_t b, const KpePNode pn) {
+    // the body header and its first 8 entry slots in one round of independent loads (the tape
+    // carries slack past its last body, kpe_api.cpp upload), then the slots past the count cleared
+    uint2 e[8];
+#if defined(KPE_PATVM_CHECK) && KPE_PATVM_CHECK
+    const uint32_t cnt = doc[PVD(b)].x;
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) e[j] = j < cnt ? doc[PVD(b + 1u + j)] : uint2{0u, 0u};
+#else
+    const uint32_t cnt = doc[b].x;
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) e[j] = doc[b + 1u + j];
+#pragma unroll
+    for (uint32_t j = 0; j < 8u; ++j) e[j] = j < cnt ? e[j] : uint2{0u, 0u};
+#endif
+    if (cnt > 8u) return PE_NONE;
+    // the entry named key1 (key ids are >= 1; padding entries carry key 0): index j, or 8
+    auto find = [&](uint32_t key1) -> uint32_t {
+      uint32_t f = 8u;
+#pragma unroll
+      for (uint32_t j = 0; j < 8u; ++j) f = (key1 != 0u && DN_KEY(e[j].x) == key1) ? j : f;
+      return f;
+    };
+    auto entry = [&](uint32_t j) -> uint2 {
+      uint2 x{0u, 0u};
+#pragma unroll
+      for (uint32_t q = 0; q < 8u; ++q) x = q == j ? e[q] : x;
+      return x;
+    };
+    const uint32_t m0 = pn.y, nanch = pn.z & 0xFFFFu, nmem = pn.z >> 16;
+    for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
+      const uint4 m = PU(a.members, m0 + k, a.nmembers, 2);
+      if (m.x & PMF_SLOT) {
+        const uint32_t bit = 1u << PM_SLOT(m.x);
+        reg |= bit;
+        if (find(m.y) < 8u) val |= bit;
+      }
+    }
+    uint32_t applied = 0, skips = 0;
+    for (uint32_t k = 0;; ++k) {
+      if (k == nanch && applied == 0u && skips > 0u) return PE_SKIP;  // every anchor skipped
+      if (k == nmem) return PE_OK;
+      const uint4 m = PU(a.members, m0 + k, a.nmembers, 2);
+      const uint32_t h = PM_HANDLER(m.x), j = find(m.y);
+      const uint2 x = entry(j);
+      uint32_t ek;
+      if (h == PM_NEG) {
+        ek = j < 8u ? PE_NEG : PE_OK;
+      } else if (j == 8u && h != PM_DEFAULT) {
+        ek = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
+      } else if ((m.x & PMF_STAR) ||
+                 ((m.x & PMF_VSTAR) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv))) {
+        ek = (j < 8u && (DN_KIND(x.x) != DN_SCALAR || x.y != SC_NULL_ID)) ? PE_OK : PE_OTHER;
+      } else {
+        const KpePNode vn = PU(a.nodes, m.z, a.nnodes, 1);
+        uint32_t v1;
+        if (!(m.x & PMF_LEAF)) {  // a map value: validateResourceElement needs a map
+          if (D <= 1) return PE_NONE;  // not reached: the compiler bounds the depth
+          if (j == 8u || DN_KIND(x.x) != DN_MAP) {
+            v1 = PE_OTHER;
+          } else {
+            v1 = flat_map<(D > 1 ? D - 1 : 1)>(x.y, vn);
+            if (v1 == PE_NONE) return PE_NONE;
+          }
+        } else if (j < 8u && DN_KIND(x.x) == DN_ARR) {  // a scalar leaf against a list: every element
+          const uint32_t l0 = x.y + 1u, le = l0 + doc[PVD(x.y)].x;
+          v1 = PE_OK;
+          for (uint32_t c = l0; c < le && v1 == PE_OK; ++c)
+            if (!pat_leaf(a, node_sid(a, doc, c), vn.y, pv, &und)) v1 = PE_OTHER;
+        } else {
+          const uint32_t sid = j == 8u ? SC_NULL_ID : (DN_KIND(x.x) == DN_SCALAR ? x.y : kNoNode);
+          v1 = pat_leaf(a, sid, vn.y, pv, &und) ? PE_OK : PE_OTHER;
+        }
+        ek = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
+      }
+      if (k < nanch) {
+        if (ek == PE_SKIP) ++skips;
+        else if (ek != PE_OK) return ek;
+        else ++applied;
+      } else if (ek != PE_OK) {
+        return ek;
+      }
+    }
+  }
+
   // validate.MatchPattern (validate.go:31-56) of pattern root node `root_pi`
   template <bool TRACE>
   __device__ __forceinline__ uint32_t run(uint32_t root_pi) {
@@ -545,6 +642,9 @@ struct PatVMT {
         } else if (pn.kind == PN_MAP) {
           if (rk != DN_MAP) {
             v = PE_OTHER;
+          } else if (KPE_PAT_FLAT && !TRACE && pn.w && pn.w <= (uint32_t)KPE_PAT_FLAT &&
+                     (v = flat_map<KPE_PAT_FLAT>(doc[PVD(br)].y, pn)) != PE_NONE) {
+            // resolved from the body in registers
           } else {
             const uint32_t nmem = pn.z >> 16;
             for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)

@@ -905,7 +905,17 @@ class PatCompiler {
     }
     const uint32_t m0 = (uint32_t)(PP.members.size() / 4);
     PP.members.insert(PP.members.end(), mem.begin(), mem.end());
-    return push_node({PN_MAP, m0, (uint32_t)first.size() | ((uint32_t)order.size() << 16), 0});
+    uint32_t depth_in = order.size() <= 8 ? 1u : 0u;  // inline depth (schema.h PNF_FLAT)
+    for (size_t i = 0; i < mem.size() && depth_in; i += 4) {
+      const uint32_t x = mem[i], h = PM_HANDLER(x);
+      if (h == PM_EXIST || (x & (PMF_GLOB | PMF_XSLOT))) {
+        depth_in = 0;
+      } else if (h != PM_NEG && !(x & (PMF_STAR | PMF_LEAF))) {  // a map (or list) value
+        const KpePNode& c = PP.nodes[mem[i + 2]];
+        depth_in = (c.kind == PN_MAP && c.w && c.w < PNF_MAXDEPTH) ? std::max(depth_in, c.w + 1u) : 0u;
+      }
+    }
+    return push_node({PN_MAP, m0, (uint32_t)first.size() | ((uint32_t)order.size() << 16), depth_in});
   }
 };
 

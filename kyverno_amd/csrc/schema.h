@@ -513,7 +513,8 @@ typedef struct KpeScalar {
 // ---- compiled patterns -------------------------------------------------------------------
 // Pattern node
 #define PN_LEAF 0u       // y = leaf index
-#define PN_MAP 1u        // y = first member, z = number of anchor-phase members | total << 16
+#define PN_MAP 1u        // y = first member, z = number of anchor-phase members | total << 16,
+                         // w = inline depth (see PNF_FLAT)
 #define PN_ARR_EMPTY 2u  // []: "pattern Array empty"
 #define PN_ARR_MAPS 3u   // [map, ...]: y = node of element 0 (validateArrayOfMaps)
 #define PN_ARR_LEAF 4u   // [scalar, ...]: y = leaf of element 0 (every element must match)
@@ -523,6 +524,14 @@ typedef struct KpeScalar {
 typedef struct KpePNode {
   uint32_t kind, y, z, w;
 } KpePNode;
+// Inline depth of a map node (KpePNode::w, 0 = none): a map of at most 8 members each of which is a
+// scalar leaf, a negation anchor, a "*" presence check or a map of inline depth d - 1 (so depth 1
+// holds leaves only), with no existence anchor, ExpandInMetadata key or AnchorMap slot past the
+// 32 tracked, and d <= PNF_MAXDEPTH. The VM validates such a map in its BEGIN step, each level
+// from one load of the resource map's body (patvm.inl flat_map), instead of a frame and a step
+// per member.
+#define PNF_FLAT 1u
+#define PNF_MAXDEPTH 3u
 // Pattern member (uint4): x = handler | PMF_* | slot << 8, y = member-name id + 1 (per
 // binding; 0 = name absent from the corpus), z = value node, w = glob-key predicate
 // location (PMF_GLOB) or PRED_NONE
