@@ -29,6 +29,7 @@ bool is_limit_error(const std::exception& e);
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
+extern "C" hipError_t kpe_launch_sites(const PatArgs* dargs, int64_t n, uint32_t nsites, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
                                                hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s);
@@ -155,7 +156,7 @@ struct DeviceProgram {
   bool tt = false;      // + truth-table fast path
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
-  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
+  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules, psites, pschain;
   DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
   DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
@@ -178,6 +179,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf pmembers, pargs, perr;  // pattern rules: resolved members, PatArgs copy, check flags
   bool pargs_valid = false;
   DevBuf pvals;  // pattern variables: per-row values (kpe_cond_kernel -> kpe_pattern_kernel)
+  DevBuf site_res;  // array-site results (kpe_site_kernel -> kpe_pattern_kernel), nsites x n uint4
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
   DevBuf pimg;  // prologue image (kpe_launch_prep)
@@ -561,6 +563,8 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.pbytes, pb, s0));
     HIPCHK(upload(D.proots, PP.roots, s0));
     HIPCHK(upload(D.prules, PP.rules, s0));
+    HIPCHK(upload(D.psites, PP.sites, s0));
+    HIPCHK(upload(D.pschain, PP.site_chain, s0));
     HIPCHK(upload(D.pvars, PP.vars, s0));
     HIPCHK(upload(D.ptmpl, PP.tpieces, s0));
     HIPCHK(upload(D.ttext, PP.ttext, s0));
@@ -1221,6 +1225,13 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.pat_bytes = PD.pbytes.as<uint8_t>();
       pa.roots = PD.proots.as<uint32_t>();
       pa.rules = PD.prules.as<KpePatRule>();
+      pa.nsites = getenv("KPE_NO_SITES") ? 0u : (uint32_t)P.pat.sites.size();
+      if (pa.nsites) {
+        PCHK(B.site_res.ensure((size_t)pa.nsites * (size_t)C.n * 16));
+        pa.sites = PD.psites.as<KpeSite>();
+        pa.site_chain = PD.pschain.as<uint32_t>();
+        pa.site_res = B.site_res.as<uint4>();
+      }
       pa.col2pr = PD.pcol2pr.as<uint32_t>();
       pa.pbuf = B.pbuf.as<uint32_t>();
       pa.pvals = P.pat.vars.empty() ? nullptr : B.pvals.as<uint2>();
@@ -1343,6 +1354,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
+    if (!P.pat.sites.empty() && !getenv("KPE_NO_SITES"))  // array elements one lane each, before the walks
+      HIPCHK(kpe_launch_sites(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.sites.size(), s));
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;

@@ -450,6 +450,11 @@ constexpr uint32_t VM_BEGIN = 0, VM_STEP = 1, VM_RET = 2;
 // the lane's index in its wave), so 64 lanes at any mix of depths hit 64 distinct banks and a
 // frame access costs an LDS round trip instead of a scratch one (scratch spills of 20 waves per
 // CU do not fit the L1 / L2 and wait on the Infinity Cache).
+struct FramesNone {  // walks that never push a frame (kpe_site_kernel's inline element maps)
+  static constexpr int kDepth = 1;
+  __device__ __forceinline__ PFrame get(int) const { return PFrame{0u, 0u, 0u, 0u, 0u, 0u, 0u}; }
+  __device__ __forceinline__ void put(int, const PFrame&) {}
+};
 struct FramesPriv {
   static constexpr int kDepth = kPatStack;
   PFrame st[kPatStack];
@@ -486,6 +491,7 @@ struct PatVMT {
   int sp;
   FS fs;
   uint32_t* tr;  // TRACE walks: the path record of the last failure (KPE_TRACE_WORDS words)
+  int64_t row = -1;  // the row whose document root the walk starts from (array-site results)
 
   // ---- failing paths (TRACE walks only; kpe_pattern_trace_kernel) ----
   // PatternError.Path (validate.go:31-56): the reference returns the path of the element where
@@ -662,9 +668,18 @@ struct PatVMT {
         } else if (rk != DN_ARR || pn.kind == PN_ARR_EMPTY) {
           v = PE_OTHER;  // a list pattern needs a list; [] is "pattern Array empty"
         } else {
-          PV_KIDS(br, c0, end);
-          if (pn.kind == PN_ARR_POS && end - c0 < pn.z) v = PE_OTHER_NOPATH;  // length mismatch: no path
-          else v = push(pn.kind == PN_ARR_POS ? PF_APOS : PF_AMAPS, br, bpi, c0);
+          uint4 sr{0u, 0u, 0u, 0u};
+          if (!TRACE && pn.kind == PN_ARR_MAPS && pn.w && a.site_res && row >= 0)  // an array site
+            sr = a.site_res[(size_t)(pn.w - 1u) * (size_t)a.n + (size_t)row];
+          if ((sr.x & KPE_SR_VALID) && sr.w == br) {  // kpe_site_kernel validated its elements
+            v = sr.x & 0xFFu;
+            und |= (sr.x >> 8) & 1u;
+            reg |= sr.y, val |= sr.z;
+          } else {
+            PV_KIDS(br, c0, end);
+            if (pn.kind == PN_ARR_POS && end - c0 < pn.z) v = PE_OTHER_NOPATH;  // length mismatch: no path
+            else v = push(pn.kind == PN_ARR_POS ? PF_APOS : PF_AMAPS, br, bpi, c0);
+          }
         }
         if (TRACE && v == PE_OTHER) snap(sp + 1, ~0u);  // validateResourceElement returns its path
         if (v == PE_PUSHED) state = VM_STEP, v = PE_NONE;
@@ -853,7 +868,7 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 template <class FS>
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs) {
   PatVMT<FS> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
-                a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr};
+                a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr, r};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   // The row's cells are read four at a time (two aligned words funnel-shifted to the row's
   // byte offset), and the columns are visited in the same order by every lane, so the lanes of
@@ -881,9 +896,57 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs)
       if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
         // a shallow (LDS) stack may have overflowed: the lane-private kPatStack-deep one decides
         PatVMT<FramesPriv> deep{a, vm.doc, vm.root, vm.pv, 0u};
+        deep.row = r;
         v = pat_eval_cell(deep, pi - 1u);
       }
       row[c0 + q] = (uint8_t)v;
     }
   }
 }
+
+// ---- array sites (schema.h KpeSite) ------------------------------------------------------
+// The site's array entry of row r: the member chain looked up from the document root (every
+// link a map holding the key), or kNoNode when the row does not reach a list there (the VM then
+// walks whatever it finds itself)
+__device__ __forceinline__ uint32_t site_array(const PatArgs& a, DocView doc, const KpeSite& S, int64_t r) {
+  uint32_t cur = (uint32_t)a.doc_off[r];
+  for (uint32_t i = 0; i < S.nchain; ++i) {
+    if (DN_KIND(doc[PVD(cur)].x) != DN_MAP) return kNoNode;
+    const uint4 m = PU(a.members, a.site_chain[S.chain0 + i], a.nmembers, 2);
+    cur = pat_lookup(a, doc, cur, m.y);
+    if (cur == kNoNode) return kNoNode;
+  }
+  return DN_KIND(doc[PVD(cur)].x) == DN_ARR ? cur : kNoNode;
+}
+// One element of a site's array against its element map (validateResourceElement): x = verdict |
+// und << 8, y / z = AnchorMap slots registered / present; PE_NONE: a body past the inline limit
+__device__ __forceinline__ uint4 site_elem(const PatArgs& a, DocView doc, const KpeSite& S, int64_t r, uint32_t e) {
+  PatVMT<FramesNone> vm{a, doc, 0u, a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, FramesNone{}, nullptr, r};
+  const uint2 x = doc[PVD(e)];
+  const uint32_t v = DN_KIND(x.x) != DN_MAP ? PE_OTHER : vm.template flat_map<PNF_MAXDEPTH>(x.y, PU(a.nodes, S.elem, a.nnodes, 1));
+  return uint4{v | (vm.und << 8), vm.reg, vm.val, 0u};
+}
+// validateArrayOfMaps' fold (validate.go:224-261) over element results in order: skips counted,
+// the first other error ends it; AnchorMap slots and `und` of the elements visited
+struct SiteFold {
+  uint32_t applied = 0, skips = 0, verdict = PE_NONE, und = 0, reg = 0, val = 0;
+  bool none = false;
+  __device__ __forceinline__ bool done() const { return none || verdict != PE_NONE; }
+  __device__ __forceinline__ void add(const uint4 x) {
+    const uint32_t c = x.x & 0xFFu;
+    if (c == PE_NONE) {
+      none = true;
+      return;
+    }
+    und |= (x.x >> 8) & 1u, reg |= x.y, val |= x.z;
+    if (c == PE_SKIP) ++skips;
+    else if (c != PE_OK) verdict = c;
+    else ++applied;
+  }
+  __device__ __forceinline__ uint4 result(uint32_t arr) const {
+    if (none) return uint4{0u, 0u, 0u, 0u};
+    const uint32_t v = verdict != PE_NONE ? verdict : (applied == 0u && skips > 0u ? PE_SKIP : PE_OK);
+    return uint4{v | (und << 8) | KPE_SR_VALID, reg, val, arr};
+  }
+};
+

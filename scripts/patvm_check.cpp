@@ -141,6 +141,39 @@ int main(int argc, char** argv) {
   // ... and the lane-private stack
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
   if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk differs from the private-stack walk\n"), 1;
+  // array sites (kpe_site_kernel's results, folded element by element here) must not change a cell
+  if (!PP.sites.empty()) {
+    std::vector<uint4> sres(PP.sites.size() * (size_t)C.n, uint4{0u, 0u, 0u, 0u});
+    a.sites = PP.sites.data(), a.site_chain = PP.site_chain.data(), a.nsites = (uint32_t)PP.sites.size();
+    const DocView doc{reinterpret_cast<const uint2*>(C.doc.data()), 0u, a.ndoc, &err};
+    uint64_t valid = 0;
+    for (size_t si = 0; si < PP.sites.size(); ++si)
+      for (int64_t r = 0; r < a.n; ++r) {
+        const KpeSite& S = PP.sites[si];
+        const uint32_t arr = site_array(a, doc, S, r);
+        if (arr == kNoNode) continue;
+        SiteFold fold;
+        const uint32_t b = doc[arr].y;
+        for (uint32_t q = 0; q < doc[b].x && !fold.done(); ++q) fold.add(site_elem(a, doc, S, r, b + 1u + q));
+        sres[si * (size_t)C.n + (size_t)r] = fold.result(arr);
+        valid += (fold.result(arr).x & KPE_SR_VALID) ? 1 : 0;
+      }
+    a.site_res = sres.data();
+    std::vector<uint8_t> site_v(lds_v);
+    for (int64_t r = 0; r < a.n; ++r)
+      for (uint32_t c = 0; c < R; ++c) site_v[(size_t)r * R + c] = col2pr[c] ? KPE_PENDING_ : site_v[(size_t)r * R + c];
+    uint8_t* keep = a.verdicts;
+    a.verdicts = site_v.data();
+    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
+    a.verdicts = keep;
+    a.site_res = nullptr;
+    if (site_v != verdicts) {
+      size_t bad = 0;
+      for (size_t i = 0; i < site_v.size(); ++i) bad += site_v[i] != verdicts[i];
+      return fprintf(stderr, "array-site walk differs from the element-by-element walk in %zu cells\n", bad), 1;
+    }
+    printf("sites %zu valid results %llu\n", PP.sites.size(), (unsigned long long)valid);
+  }
   FILE* f = fopen(argv[3], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
