@@ -1192,7 +1192,7 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
   return hipGetLastError();
 }
 
-// Array sites (schema.h KpeSite): grid (64-row tiles per wave, sites). A wave resolves the site's
+// Array sites (schema.h KpeSite): 64-row tiles per wave, every site in turn. A wave resolves a site's
 // member chain for its 64 rows (rows whose cell of the site's rule is still pending), takes a
 // wave prefix sum of their arrays' element counts and then validates the elements of all 64 rows
 // one lane per element, 64 at a time (the element map inline, patvm.inl flat_map); each chunk's
@@ -1200,56 +1200,65 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
 // (validateArrayOfMaps). A row's array of n elements thus costs ~n/64 of a wave's element pass
 // instead of n sequential walks of one lane, and the pattern kernel then takes the row's result
 // at the array node instead of walking the elements.
-__global__ void __launch_bounds__(256) kpe_site_kernel(const PatArgs* __restrict__ ap) {
+#ifndef KPE_SITE_MINW
+#define KPE_SITE_MINW 2
+#endif
+__global__ void __launch_bounds__(256, KPE_SITE_MINW) kpe_site_kernel(const PatArgs* __restrict__ ap) {
   __shared__ uint32_t s_off[4][65];
   __shared__ uint32_t s_arr[4][64];
   __shared__ uint4 s_res[4][64];
   const PatArgs& a = *ap;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const KpeSite S = sld(a.sites, blockIdx.y);
   const int64_t row = ((int64_t)blockIdx.x * 4 + wv) * 64 + lane;
   const bool live = row < a.n;
   const DocView doc = PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc);
-  uint32_t arr = kNoNode, cnt = 0;
-  // only rows whose cell is pending get a result: the pattern kernel reads a site's result only
-  // while walking that cell's rule, so every result it reads was written by this launch
-  const bool pend = live && a.verdicts[(size_t)row * a.R + S.col] == KPE_PENDING_;
-  if (pend) {
-    arr = site_array(a, doc, S, row);
-    if (arr != kNoNode) cnt = doc[doc[arr].y].x;
-  }
-  const uint32_t incl = wave_incl_scan(cnt), excl = incl - cnt;
-  const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-  s_off[wv][lane] = excl;
-  s_arr[wv][lane] = arr;
-  if (lane == 63u) s_off[wv][64] = total;
-  __builtin_amdgcn_wave_barrier();
-  SiteFold fold;
-  for (uint32_t g0 = 0; g0 < total; g0 += 64u) {
-    const uint32_t g = g0 + lane;
-    uint4 r{0u, 0u, 0u, 0u};
-    if (g < total) {
-      uint32_t o = 0;  // the row lane whose [offset, offset + count) holds element g
+  // every site for this wave's 64 rows in turn: a row's document (root and list bodies) stays in
+  // L1 / L2 from one site to the next
+  for (uint32_t site = 0; site < a.nsites; ++site) {
+    const KpeSite S = sld(a.sites, site);
+    uint32_t arr = kNoNode, cnt = 0;
+    // only rows whose cell is pending get a result: the pattern kernel reads a site's result only
+    // while walking that cell's rule, so every result it reads was written by this launch
+    const bool pend = live && a.verdicts[(size_t)row * a.R + S.col] == KPE_PENDING_;
+    if (__ballot(pend) == 0ull) continue;
+    if (pend) {
+      arr = site_array(a, doc, S, row);
+      if (arr != kNoNode) cnt = doc[doc[arr].y].x;
+    }
+    const uint32_t incl = wave_incl_scan(cnt), excl = incl - cnt;
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    __builtin_amdgcn_wave_barrier();  // the previous site's readers of s_off / s_arr are done
+    s_off[wv][lane] = excl;
+    s_arr[wv][lane] = arr;
+    if (lane == 63u) s_off[wv][64] = total;
+    __builtin_amdgcn_wave_barrier();
+    SiteFold fold;
+    for (uint32_t g0 = 0; g0 < total; g0 += 64u) {
+      const uint32_t g = g0 + lane;
+      uint4 r{0u, 0u, 0u, 0u};
+      if (g < total) {
+        uint32_t o = 0;  // the row lane whose [offset, offset + count) holds element g
 #pragma unroll
-      for (uint32_t step = 32u; step; step >>= 1)
-        if (s_off[wv][o + step] <= g) o += step;
-      const uint32_t e = doc[s_arr[wv][o]].y + 1u + (g - s_off[wv][o]);
-      r = site_elem(a, doc, S, row - lane + o, e);
+        for (uint32_t step = 32u; step; step >>= 1)
+          if (s_off[wv][o + step] <= g) o += step;
+        const uint32_t e = doc[s_arr[wv][o]].y + 1u + (g - s_off[wv][o]);
+        r = site_elem(a, doc, S, row - lane + o, e);
+      }
+      s_res[wv][lane] = r;
+      __builtin_amdgcn_wave_barrier();
+      if (cnt) {  // this row's elements within the chunk, in order
+        const uint32_t lo = excl > g0 ? excl : g0, hi = incl < g0 + 64u ? incl : g0 + 64u;
+        for (uint32_t q = lo; q < hi && !fold.done(); ++q) fold.add(s_res[wv][q - g0]);
+      }
+      __builtin_amdgcn_wave_barrier();
     }
-    s_res[wv][lane] = r;
-    __builtin_amdgcn_wave_barrier();
-    if (cnt) {  // this row's elements within the chunk, in order
-      const uint32_t lo = excl > g0 ? excl : g0, hi = incl < g0 + 64u ? incl : g0 + 64u;
-      for (uint32_t q = lo; q < hi && !fold.done(); ++q) fold.add(s_res[wv][q - g0]);
-    }
-    __builtin_amdgcn_wave_barrier();
+    if (pend) a.site_res[(size_t)site * (size_t)a.n + (size_t)row] = arr != kNoNode ? fold.result(arr) : uint4{0u, 0u, 0u, 0u};
   }
-  if (pend) a.site_res[(size_t)blockIdx.y * (size_t)a.n + (size_t)row] = arr != kNoNode ? fold.result(arr) : uint4{0u, 0u, 0u, 0u};
 }
 
 extern "C" hipError_t kpe_launch_sites(const PatArgs* dargs, int64_t n, uint32_t nsites, hipStream_t s) {
   if (n <= 0 || !nsites) return hipSuccess;
-  hipLaunchKernelGGL(kpe_site_kernel, dim3((unsigned)((n + 255) / 256), nsites), dim3(256), 0, s, dargs);
+  hipLaunchKernelGGL(kpe_site_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dargs);
   return hipGetLastError();
 }
 

@@ -115,6 +115,14 @@ constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated 
 // launch's prologue overlaps another's tail. Setup (uploads, binds) and timed launches
 // use stream 0.
 constexpr int kMaxLanes = 4;
+// Array sites (kpe_site_kernel) are opt-in (KPE_SITES=1): they shorten the pattern walks (C5 13.0
+// -> 5.5 ms) but the per-site element pass measured slower than what it saves (C5 11.3 ms, C3
+// 2.3 ms against 4.8 ms of walking saved; profiles/r03_f_sites)
+static bool sites_on() {
+  const char* e = getenv("KPE_SITES");
+  return e && *e == '1';
+}
+
 struct kpe_device {
   int ordinal = 0;
   hipStream_t stream = nullptr;  // == lanes[0]
@@ -1225,7 +1233,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.pat_bytes = PD.pbytes.as<uint8_t>();
       pa.roots = PD.proots.as<uint32_t>();
       pa.rules = PD.prules.as<KpePatRule>();
-      pa.nsites = getenv("KPE_NO_SITES") ? 0u : (uint32_t)P.pat.sites.size();
+      pa.nsites = sites_on() ? (uint32_t)P.pat.sites.size() : 0u;
       if (pa.nsites) {
         PCHK(B.site_res.ensure((size_t)pa.nsites * (size_t)C.n * 16));
         pa.sites = PD.psites.as<KpeSite>();
@@ -1354,7 +1362,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
-    if (!P.pat.sites.empty() && !getenv("KPE_NO_SITES"))  // array elements one lane each, before the walks
+    if (!P.pat.sites.empty() && sites_on())  // array elements one lane each, before the walks
       HIPCHK(kpe_launch_sites(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.sites.size(), s));
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
