@@ -1201,7 +1201,7 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
 // instead of n sequential walks of one lane, and the pattern kernel then takes the row's result
 // at the array node instead of walking the elements.
 #ifndef KPE_SITE_MINW
-#define KPE_SITE_MINW 2
+#define KPE_SITE_MINW 4  // C5 site pass 10.8 -> 8.9 ms at 4 waves/SIMD (profiles/r03_f_sites)
 #endif
 __global__ void __launch_bounds__(256, KPE_SITE_MINW) kpe_site_kernel(const PatArgs* __restrict__ ap) {
   __shared__ uint32_t s_off[4][65];
