@@ -1203,56 +1203,97 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
 #ifndef KPE_SITE_MINW
 #define KPE_SITE_MINW 4  // C5 site pass 10.8 -> 8.9 ms at 4 waves/SIMD (profiles/r03_f_sites)
 #endif
+// packed SiteFold of one (site, row): applied | skips << 8 | verdict << 16 (PE_NONE: open) |
+// und << 20 | none << 21, plus the AnchorMap words
+__device__ __forceinline__ void sfold_add(uint32_t& st, uint32_t& rg, uint32_t& vl, const uint4 x) {
+  if (((st >> 16) & 0xFu) != PE_NONE || (st >> 21) & 1u) return;  // decided
+  const uint32_t c = x.x & 0xFFu;
+  if (c == PE_NONE) {
+    st |= 1u << 21;
+    return;
+  }
+  st |= (x.x & 0x100u) << 12, rg |= x.y, vl |= x.z;
+  if (c == PE_SKIP) st += 1u << 8;
+  else if (c != PE_OK) st = (st & ~(0xFu << 16)) | (c << 16);
+  else st += 1u;
+}
+__device__ __forceinline__ uint4 sfold_result(uint32_t st, uint32_t rg, uint32_t vl, uint32_t arr) {
+  if ((st >> 21) & 1u) return uint4{0u, 0u, 0u, 0u};
+  uint32_t v = (st >> 16) & 0xFu;
+  if (v == PE_NONE) v = ((st & 0xFFu) == 0u && ((st >> 8) & 0xFFu) > 0u) ? PE_SKIP : PE_OK;
+  return uint4{v | (((st >> 20) & 1u) << 8) | KPE_SR_VALID, rg, vl, arr};
+}
+
 __global__ void __launch_bounds__(256, KPE_SITE_MINW) kpe_site_kernel(const PatArgs* __restrict__ ap) {
   __shared__ uint32_t s_off[4][65];
   __shared__ uint32_t s_arr[4][64];
-  __shared__ uint4 s_res[4][64];
+  __shared__ uint32_t s_pm[4][64];
+  __shared__ uint4 s_res[4][8][64];
   const PatArgs& a = *ap;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const int64_t row = ((int64_t)blockIdx.x * 4 + wv) * 64 + lane;
   const bool live = row < a.n;
   const DocView doc = PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc);
-  // every site for this wave's 64 rows in turn: a row's document (root and list bodies) stays in
-  // L1 / L2 from one site to the next
-  for (uint32_t site = 0; site < a.nsites; ++site) {
-    const KpeSite S = sld(a.sites, site);
+  // site groups in turn (sites whose chains name the same keys): the chain is resolved once and
+  // an element is validated for every pending site of the group back to back, so all but the
+  // first read its body from L1; a row's lists stay in L1 / L2 from one group to the next
+  for (uint32_t grp = 0; grp < a.ngroups; ++grp) {
+    const uint2 G = sld(a.site_groups, grp);
+    uint32_t pm = 0;  // sites of the group whose cell of this row is pending
+    for (uint32_t i = 0; i < G.y; ++i) {
+      const KpeSite S = sld(a.sites, sld(a.group_sites, G.x + i));
+      if (live && a.verdicts[(size_t)row * a.R + S.col] == KPE_PENDING_) pm |= 1u << i;
+    }
+    if (__ballot(pm != 0u) == 0ull) continue;
+    const KpeSite S0 = sld(a.sites, sld(a.group_sites, G.x));
     uint32_t arr = kNoNode, cnt = 0;
-    // only rows whose cell is pending get a result: the pattern kernel reads a site's result only
-    // while walking that cell's rule, so every result it reads was written by this launch
-    const bool pend = live && a.verdicts[(size_t)row * a.R + S.col] == KPE_PENDING_;
-    if (__ballot(pend) == 0ull) continue;
-    if (pend) {
-      arr = site_array(a, doc, S, row);
+    if (pm) {
+      arr = site_array(a, doc, S0, row);
       if (arr != kNoNode) cnt = doc[doc[arr].y].x;
     }
     const uint32_t incl = wave_incl_scan(cnt), excl = incl - cnt;
     const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    __builtin_amdgcn_wave_barrier();  // the previous site's readers of s_off / s_arr are done
+    __builtin_amdgcn_wave_barrier();  // the previous group's readers of the LDS rows are done
     s_off[wv][lane] = excl;
     s_arr[wv][lane] = arr;
+    s_pm[wv][lane] = pm;
     if (lane == 63u) s_off[wv][64] = total;
     __builtin_amdgcn_wave_barrier();
-    SiteFold fold;
+    uint32_t st[8], rg[8], vl[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i) st[i] = PE_NONE << 16, rg[i] = 0u, vl[i] = 0u;
     for (uint32_t g0 = 0; g0 < total; g0 += 64u) {
       const uint32_t g = g0 + lane;
-      uint4 r{0u, 0u, 0u, 0u};
+      uint32_t o = 0, e = 0, opm = 0;
       if (g < total) {
-        uint32_t o = 0;  // the row lane whose [offset, offset + count) holds element g
 #pragma unroll
-        for (uint32_t step = 32u; step; step >>= 1)
+        for (uint32_t step = 32u; step; step >>= 1)  // the row lane whose [offset, offset + count) holds g
           if (s_off[wv][o + step] <= g) o += step;
-        const uint32_t e = doc[s_arr[wv][o]].y + 1u + (g - s_off[wv][o]);
-        r = site_elem(a, doc, S, row - lane + o, e);
+        e = doc[s_arr[wv][o]].y + 1u + (g - s_off[wv][o]);
+        opm = s_pm[wv][o];
       }
-      s_res[wv][lane] = r;
+      for (uint32_t i = 0; i < G.y; ++i) {
+        uint4 r{0u, 0u, 0u, 0u};
+        if ((opm >> i) & 1u) r = site_elem(a, doc, sld(a.sites, sld(a.group_sites, G.x + i)), row - lane + o, e);
+        s_res[wv][i][lane] = r;
+      }
       __builtin_amdgcn_wave_barrier();
-      if (cnt) {  // this row's elements within the chunk, in order
+      if (cnt) {  // this row's elements within the chunk, in order, for each of its pending sites
         const uint32_t lo = excl > g0 ? excl : g0, hi = incl < g0 + 64u ? incl : g0 + 64u;
-        for (uint32_t q = lo; q < hi && !fold.done(); ++q) fold.add(s_res[wv][q - g0]);
+#pragma unroll
+        for (uint32_t i = 0; i < 8u; ++i)
+          if ((pm >> i) & 1u)
+            for (uint32_t q = lo; q < hi; ++q) sfold_add(st[i], rg[i], vl[i], s_res[wv][i][q - g0]);
       }
       __builtin_amdgcn_wave_barrier();
     }
-    if (pend) a.site_res[(size_t)site * (size_t)a.n + (size_t)row] = arr != kNoNode ? fold.result(arr) : uint4{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i)
+      if ((pm >> i) & 1u) {
+        const uint32_t site = sld(a.group_sites, G.x + i);
+        a.site_res[(size_t)site * (size_t)a.n + (size_t)row] =
+            arr != kNoNode ? sfold_result(st[i], rg[i], vl[i], arr) : uint4{0u, 0u, 0u, 0u};
+      }
   }
 }
 

@@ -204,7 +204,9 @@ struct PatArgs {
   const KpeSite* sites;
   const uint32_t* site_chain;
   uint4* site_res;
-  uint32_t nsites, pad3_;
+  uint32_t nsites, ngroups;
+  const uint2* site_groups;        // (first, count) into group_sites: sites sharing one chain (<= 8)
+  const uint32_t* group_sites;
   // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)
   uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
   uint64_t nscal, ndoc;

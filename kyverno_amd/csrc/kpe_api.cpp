@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <new>
@@ -164,7 +165,8 @@ struct DeviceProgram {
   bool tt = false;      // + truth-table fast path
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
-  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules, psites, pschain;
+  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules, psites, pschain, psgroups, psorder;
+  uint32_t nsite_groups = 0;
   DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
   DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
@@ -573,6 +575,27 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.prules, PP.rules, s0));
     HIPCHK(upload(D.psites, PP.sites, s0));
     HIPCHK(upload(D.pschain, PP.site_chain, s0));
+    {  // site groups: sites whose chains name the same keys reach the same list of a row, so
+       // kpe_site_kernel resolves it once and evaluates an element for every site of the group
+       // while its body is in L1 (at most 8 sites per group)
+      std::map<std::vector<std::string>, std::vector<uint32_t>> by_chain;
+      for (uint32_t i = 0; i < PP.sites.size(); ++i) {
+        std::vector<std::string> keys;
+        const KpeSite& st = PP.sites[i];
+        for (uint32_t k = 0; k < st.nchain; ++k) keys.push_back(PP.keys[PP.members[4 * (size_t)PP.site_chain[st.chain0 + k] + 1]]);
+        by_chain[keys].push_back(i);
+      }
+      std::vector<uint32_t> order, groups;
+      for (auto& kv : by_chain)
+        for (size_t j = 0; j < kv.second.size(); j += 8) {
+          groups.push_back((uint32_t)order.size());
+          groups.push_back((uint32_t)std::min<size_t>(8, kv.second.size() - j));
+          order.insert(order.end(), kv.second.begin() + j, kv.second.begin() + std::min(kv.second.size(), j + 8));
+        }
+      D.nsite_groups = (uint32_t)(groups.size() / 2);
+      HIPCHK(upload(D.psgroups, groups, s0));
+      HIPCHK(upload(D.psorder, order, s0));
+    }
     HIPCHK(upload(D.pvars, PP.vars, s0));
     HIPCHK(upload(D.ptmpl, PP.tpieces, s0));
     HIPCHK(upload(D.ttext, PP.ttext, s0));
@@ -1239,6 +1262,9 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
         pa.sites = PD.psites.as<KpeSite>();
         pa.site_chain = PD.pschain.as<uint32_t>();
         pa.site_res = B.site_res.as<uint4>();
+        pa.site_groups = PD.psgroups.as<uint2>();
+        pa.group_sites = PD.psorder.as<uint32_t>();
+        pa.ngroups = PD.nsite_groups;
       }
       pa.col2pr = PD.pcol2pr.as<uint32_t>();
       pa.pbuf = B.pbuf.as<uint32_t>();

@@ -182,14 +182,20 @@ def test_anchored_glob_metadata_keys_compile():
 
 
 @pytest.mark.gpu
-def test_pattern_kernel_c5_fanout_bit_exact(oracle):
+@pytest.mark.parametrize("cfg,sites", [("c5", False), ("c5", True), ("c3", True)])
+def test_pattern_kernel_fanout_bit_exact(oracle, monkeypatch, cfg, sites):
     """The lane-per-row kernel (LDS frame stacks, deep walks retried on the private stack) gives
     the oracle's matrix on the C5 fan-out corpus (1-64 containers, Pods and Deployments: the
-    Deployments' walks are deeper than the LDS stack) with the C5 pattern set."""
-    from tests.policies import c5_policy_set
+    Deployments' walks are deeper than the LDS stack) with the C5 pattern set, and with the
+    array sites on (KPE_SITES=1: kpe_site_kernel validates the elements of arrays of maps one lane
+    per element and the walk takes the row's result) on C5 and C3."""
+    from tests.policies import c3_policy_set, c5_policy_set
 
-    pols = c5_policy_set()
-    nd = K.synth_resources(0xC5, 6000, mix=K.SYNTH_FANOUT)
+    if sites:
+        monkeypatch.setenv("KPE_SITES", "1")
+    pols = c5_policy_set() if cfg == "c5" else c3_policy_set()
+    nd = (K.synth_resources(0xC5, 6000, mix=K.SYNTH_FANOUT) if cfg == "c5"
+          else K.synth_resources(0xC3 + 5, 20000, mix=K.SYNTH_C3))
     eng = K.Engine(ordinal=0)
     v, _, _ = eng.evaluate(K.PolicySet(pols), K.Corpus(nd))
     ref = oracle.validate(pols, nd, nthreads=8)
