@@ -1201,7 +1201,7 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
 // instead of n sequential walks of one lane, and the pattern kernel then takes the row's result
 // at the array node instead of walking the elements.
 #ifndef KPE_SITE_MINW
-#define KPE_SITE_MINW 4  // C5 site pass 10.8 -> 8.9 ms at 4 waves/SIMD (profiles/r03_f_sites)
+#define KPE_SITE_MINW 3  // grouped pass, C5 / C3: 2 waves/SIMD 9.6 / 1.43 ms, 3 8.1 / 1.28, 4 8.9 / 1.28 (r03_g_sitegroups)
 #endif
 // packed SiteFold of one (site, row): applied | skips << 8 | verdict << 16 (PE_NONE: open) |
 // und << 20 | none << 21, plus the AnchorMap words
