@@ -265,8 +265,15 @@ def main():
             # pattern-dominated configurations (C3, C5): the dominant kernel is the pattern VM;
             # its algorithmic bytes are every resource's document tape once plus the verdicts
             pat_achieved = st.pattern_bytes / (pat_ms * 1e-3) / 1e9
+            pat_traffic = None
+            try:  # FETCH_SIZE / WRITE_SIZE of the pattern kernel (scripts/gpu_pat_pmc.sh)
+                tj = json.load(open(traffic_json))
+                if tj.get("kernel") == "kpe_pattern_kernel":
+                    pat_traffic = tj.get("scan_bytes_per_launch")
+            except Exception:
+                pat_traffic = None
             scan_roof = {"bound": "hbm", "achieved": pat_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": pat_achieved / HBM_PEAK_GBS, "traffic": None, "kernel": "kpe_pattern_kernel",
+                         "frac": pat_achieved / HBM_PEAK_GBS, "traffic": pat_traffic, "kernel": "kpe_pattern_kernel",
                          "kernel_ms": pat_ms, "alg_bytes_per_launch": st.pattern_bytes,
                          "scan_kernel": {"kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes,
                                          "frac": scan_achieved / HBM_PEAK_GBS},
