@@ -218,7 +218,8 @@ def main():
             tj = json.load(open(traffic_json))
             # only counters taken on the kernel this run launched (a stale file is not this kernel's)
             norm = lambda k: k.split("(")[0].replace("void ", "").replace(" ", "")  # noqa: E731
-            if norm(tj.get("kernel", "")) == norm(scan_kernel):
+            if norm(tj.get("kernel", "")) == norm(scan_kernel) or (
+                    scan_kernel == "kpe_scan_kernel" and norm(tj.get("kernel", "")).startswith("kpe_scan_kernel")):
                 traffic = tj.get("scan_bytes_per_launch")
         except Exception:
             traffic = None

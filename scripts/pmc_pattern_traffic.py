@@ -9,14 +9,16 @@ import os
 import sys
 
 cfg = sys.argv[1]
-KERNEL = "kpe_pattern_kernel"
+KERNEL = sys.argv[2] if len(sys.argv) > 2 else "kpe_pattern_kernel"  # a kernel-name prefix
 
 
 def mean(counter, tag):
     vals = []
     for f in glob.glob(f"gpurun_out/pt_{cfg}_{tag}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            if r["Kernel_Name"].startswith(KERNEL) and r["Counter_Name"] == counter:
+            name = r["Kernel_Name"].replace("void ", "")
+            # the evaluation launches (the per-binding prologue instance, <..., true, ...>, is not one)
+            if name.startswith(KERNEL) and ", true, false>" not in name.split("(")[0][-14:] and r["Counter_Name"] == counter:
                 vals.append(float(r["Counter_Value"]))
     return sum(vals) / len(vals) if vals else None
 
