@@ -13,11 +13,16 @@ are all-reduced once over RCCL after the timed region).
     disallow-latest-tag / host-ports / anchor pattern set per GPU (configs[4]).
 
 One step = one evaluation pass of the compiled program over one resident shard
-(kpe_evaluate_async: dictionary predicate pass, resource-scan kernel, pattern kernel when the
-program has pattern rules). `--replicas` distinct shards are rotated so consecutive C2 steps do
-not re-read a corpus out of the 256 MiB Infinity Cache. Per-rule counters are built once, after
-the timed region (kpe_fetch), not per step.
+(kpe_evaluate_async: resource-scan kernel, then the condition / exclusion / pattern kernels when
+the program has such rules). Distinct shards are rotated so that the bytes a step's scan reads
+were last touched more than twice the 256 MiB Infinity Cache ago: C2 reads 24 B per pod (record
++ PSA summary) and writes R B, 27 MB per 1M-pod shard, so it rotates 24 shards (648 MB; the
+count is derived from the scan's algorithmic bytes, `--replicas` overrides). The per-pod PSA
+summaries are built on the device when a shard is first bound (policy-independent, like the
+records); the cold leg re-runs them with the rest of the per-corpus prologue. Per-rule counters
+are built once, after the timed region (kpe_fetch), not per step.
 """
+import math
 import argparse
 import json
 import os
@@ -28,9 +33,33 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+IC_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
 # kpe_kernel_stats.scan_kernel -> kernel name (as rocprofv3 lists it)
-SCAN_KERNELS = {1: "kpe_scan_kernel", 3: "kpe_lean_kernel", 4: "kpe_lean3_kernel", 5: "kpe_lean4_kernel<1>",
-                6: "kpe_lean4_kernel<2>", 7: "kpe_lean5_kernel<1>", 8: "kpe_lean5_kernel<2>"}
+SCAN_KERNELS = {1: "kpe_scan_kernel", 2: "kpe_scan_kernel", 7: "kpe_lean5_kernel"}
+
+
+def cpu_budget():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup v2 / v1 CPU quota
+    (a GPU box grants each job a share of a larger machine: os.cpu_count() is the machine)."""
+    machine = os.cpu_count() or 1
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = machine
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            quota = None
+    usable = max(1, min(aff, math.floor(quota) if quota else aff))
+    return {"machine": machine, "affinity": aff, "cgroup_quota": quota, "usable": usable}
 
 
 def cpu_model():
@@ -52,7 +81,7 @@ def main():
     ap.add_argument("--resources", type=int, default=0, help="rows per GPU (0 = the config's size)")
     ap.add_argument("--replicas", type=int, default=0, help="distinct shards rotated (0 = the config's default)")
     ap.add_argument("--cpu-sample", type=int, default=-1, help="rows in the CPU-baseline sample (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use (cpu_budget)")
     ap.add_argument("--traffic-json", default="")
     args = ap.parse_args()
 
@@ -66,7 +95,7 @@ def main():
 
     cfg = args.config
     if cfg == "c2":
-        policies, mix, seed, n_def, rep_def, docs = [restricted_latest()], K.SYNTH_PODS, 0xC2, 1_000_000, 8, False
+        policies, mix, seed, n_def, rep_def, docs = [restricted_latest()], K.SYNTH_PODS, 0xC2, 1_000_000, 0, False
         workload = "C2: 1M synthetic Pods x PSS restricted:latest per GPU (R=3 rules after autogen)"
     elif cfg == "c3":
         policies, mix, seed, n_def, rep_def, docs = c3_policy_set(), K.SYNTH_C3, 0xC3, 1_250_000, 1, True
@@ -79,7 +108,13 @@ def main():
         policies, mix, seed, n_def, rep_def, docs = c5_policy_set(), K.SYNTH_FANOUT, 0xC5, 1_000_000, 1, True
         workload = "C5: 1M Pods/Deployments with 1-64 containers x requests-limits/latest-tag/host-ports/anchor patterns"
     n = args.resources or n_def
-    replicas = args.replicas or rep_def
+    if args.replicas:
+        replicas = args.replicas
+    elif rep_def:
+        replicas = rep_def
+    else:  # C2: enough shards that a shard's scan bytes leave the Infinity Cache before its next use
+        alg = (24.0 + 3.0) * n  # LEAN5: record + PSA summary read, R = 3 verdict bytes written per pod
+        replicas = max(2, math.ceil(2.25 * IC_BYTES / alg))
     # HBM bytes per scan launch from the FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py);
     # perf/ travels to the GPU box, profiles/ does not
     traffic_json = args.traffic_json or os.path.join(ROOT, "perf", f"pmc_traffic_{cfg}.json")
@@ -109,19 +144,26 @@ def main():
     R = ps.num_rules
     corpora = []
     t_flatten = t_upload = 0.0
-    for k in range(replicas):
-        # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus
-        first = (rank * replicas + k) * n
-        nd = K.synth_resources(seed, n, mix=mix, first_index=first)
-        nsl = K.synth_ns_labels(seed, 10000, mix=mix) if cfg == "c4" else None
-        t0 = time.perf_counter()
-        c = K.Corpus(nd, namespace_labels=nsl, docs=docs)
-        t1 = time.perf_counter()
-        del nd
-        c.upload(eng.device)
-        t_flatten += t1 - t0
-        t_upload += time.perf_counter() - t1
-        corpora.append(c)
+    nsl = K.synth_ns_labels(seed, 10000, mix=mix) if cfg == "c4" else None
+    from concurrent.futures import ThreadPoolExecutor
+
+    # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus; the synthetic NDJSON
+    # of the next shards is generated on two threads while this one is flattened and uploaded
+    with ThreadPoolExecutor(max_workers=2) as pool:
+        futs = [pool.submit(K.synth_resources, seed, n, mix, (rank * replicas + k) * n) for k in range(replicas)]
+        for k in range(replicas):
+            nd = futs[k].result()
+            futs[k] = None
+            t0 = time.perf_counter()
+            c = K.Corpus(nd, namespace_labels=nsl, docs=docs)
+            t1 = time.perf_counter()
+            del nd
+            c.upload(eng.device)
+            t_flatten += t1 - t0
+            t_upload += time.perf_counter() - t1
+            corpora.append(c)
+            if rank == 0 and (k % 4 == 3 or k == replicas - 1):
+                print(f"[bench] {k + 1}/{replicas} shards of {n} rows flattened and uploaded", file=sys.stderr, flush=True)
     # end-to-end leg for one shard: flatten + H2D (measured above) + one synchronous evaluation
     t0 = time.perf_counter()
     eng.evaluate_async(ps, corpora[0])
@@ -135,7 +177,9 @@ def main():
             for f in COUNT_FIELDS:
                 totals[r][f] += cnt[r][f]
 
-    for i in range(args.warmup):
+    # warm-up: every shard at least once (first binding: program upload, prologue image, PSA
+    # summaries), then W more steps
+    for i in range(len(corpora) + args.warmup):
         eng.evaluate_async(ps, corpora[i % len(corpora)])
     eng.device.sync()
 
@@ -184,7 +228,8 @@ def main():
     # checks) and a cold step (per-corpus prologue re-run: dictionary predicate pass + prologue
     # image, as the first evaluation of a newly bound corpus), wall-clock and per kernel ----
     def leg(**kw):
-        eng.evaluate_async(ps, corpora[0], **kw)  # mode switch (argument block upload) untimed
+        for c in corpora:  # mode switch (argument block upload, masks buffer allocation) untimed
+            eng.evaluate_async(ps, c, **kw)
         eng.device.sync()
         eng.device.set_timing(False)
         ks = max(1, args.steps // 4)
@@ -233,7 +278,8 @@ def main():
         orc = load_oracle()
         nd = K.synth_resources(seed, sample, mix=mix)
         nsl_s = K.synth_ns_labels(seed, 10000, mix=mix) if cfg == "c4" else None
-        thr = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+        budget = cpu_budget()
+        thr = args.cpu_threads or budget["usable"]
         t1 = time.perf_counter()
         ref = orc.validate(policies, nd, ns_labels=nsl_s, nthreads=thr)
         dt = time.perf_counter() - t1
@@ -243,7 +289,7 @@ def main():
         ref1 = orc.validate(policies, sub, ns_labels=nsl_s, nthreads=1)
         dt1 = time.perf_counter() - t1
         cpu = {"value": ref.size / dt, "unit": "resource-rule evals/s", "cores": thr, "kind": "port",
-               "single_thread_value": ref1.size / dt1, "cpu_model": cpu_model(),
+               "single_thread_value": ref1.size / dt1, "cpu_model": cpu_model(), "cpu_budget": budget,
                "sample": f"{sample} {cfg.upper()} rows x {R} rules (NDJSON parse + typed decode + evaluate), "
                          f"oracle/ CPU restatement, {thr} threads {dt:.2f}s; single-thread leg "
                          f"{max(1, sample // 8)} rows {dt1:.2f}s"}
@@ -295,6 +341,8 @@ def main():
             "data": f"synthetic (kpe_synth {cfg.upper()} generator, seed {seed:#x})",
             "config": {"workload": workload, "resources_per_gpu": n, "rules": R, "global_resources": n * world,
                        "replicas_rotated": replicas, "parallelism": f"resource-sharded x{world}",
+                       # scan bytes touched between two uses of one shard vs the Infinity Cache
+                       "rotated_scan_bytes": st.scan_bytes * replicas, "infinity_cache_bytes": IC_BYTES,
                        # cells where the rule matched the resource (a RuleResponse exists), per s
                        "matched_cell_evals_per_s": value * sum(n * replicas * world - totals[r]["na"]
                                                                for r in range(R)) / float(n * replicas * world * R),

@@ -150,6 +150,11 @@ kpe_status kpe_resource_hash(const char* resource_json, size_t len, char* out33)
 int64_t kpe_resource_hashes(const char* ndjson, size_t len, char* out, int64_t cap_rows);
 /* Copy the columns to device memory (HBM). Evaluation requires this. */
 kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* c);
+/* The corpus's per-pod PSA summary, built on dev (waits for it; builds it first when no LEAN
+ * evaluation has yet): 2 words per row (include-free layout of kyverno_amd/csrc/schema.h PS_*:
+ * x = OR of the pod's container state bitmaps, y = the list codes under the PSA library's fixed
+ * sets). Diagnostics and the summary's digest test; evaluation never needs it on the host. */
+kpe_status kpe_corpus_psa_summary(kpe_device* dev, kpe_corpus* c, uint32_t* out);
 void kpe_corpus_free(kpe_corpus* c);
 
 /* ---- evaluation -------------------------------------------------------- */
@@ -169,8 +174,8 @@ kpe_status kpe_evaluate(kpe_device* dev, const kpe_program* prog, const kpe_corp
 kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c);
 /* kpe_evaluate_async with options: KPE_EVAL_MASKS also writes the check masks (device
  * buffers read by kpe_fetch / kpe_fetch_cv_masks); KPE_EVAL_COLD re-runs the binding's
- * per-corpus prologue (dictionary predicate pass, prologue image) as the first evaluation of a
- * newly bound corpus does. */
+ * per-corpus prologue (dictionary predicate pass, prologue image and, for a LEAN program, the
+ * per-pod PSA summaries) as the first evaluation of a newly bound corpus does. */
 #define KPE_EVAL_MASKS 1u
 #define KPE_EVAL_COLD 2u
 kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, unsigned flags);
@@ -287,8 +292,8 @@ typedef struct kpe_kernel_stats {
                                document tape (8 B per entry) and root offset once, plus the verdict
                                matrix read and written */
   int32_t scan_kernel;      /* the scan instantiation of the last timed launch: 1 kpe_scan_kernel
-                               (general), 4 kpe_lean3_kernel, 5/6 kpe_lean4_kernel<1/2>, 7/8
-                               kpe_lean5_kernel<1/2> (KPE_SCAN_* codes) */
+                               (general), 2 its LEAN instantiation (corpora past 4 GiB of pod
+                               records), 7 kpe_lean5_kernel */
   int32_t pad_;
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);

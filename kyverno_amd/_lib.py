@@ -68,6 +68,7 @@ def load():
     L.kpe_corpus_digest.restype = ctypes.c_uint64
     L.kpe_corpus_row_flags.argtypes = [vp, vp]
     L.kpe_corpus_upload.argtypes = [vp, vp]
+    L.kpe_corpus_psa_summary.argtypes = [vp, vp, vp]
     L.kpe_corpus_free.argtypes = [vp]
     L.kpe_evaluate.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_evaluate_async.argtypes = [vp, vp, vp]

@@ -240,6 +240,7 @@ struct CondVM {
       const uint2 o = a.ops[i++];
       const uint32_t op = QO_OP(o.x);
       if (mode == 2) {  // a projection over a non-list: the rest of the expression is null
+        if (op == QO_LEN) return CS_ERROR;  // length(null): invalid type
         if (op == QO_MSL) {
           for (uint32_t k = 0; k < QO_ARG(o.x); ++k) i += 1u + QO_ARG(a.ops[i].x);
         }
@@ -360,6 +361,28 @@ struct CondVM {
             if (push(fb, x)) return CS_UNDEC;
           }
           cur = cv(VK_LIST, fb);
+          break;
+        }
+        case QO_LEN: {  // jpfLength (go-jmespath functions.go): runes / items / members
+          uint32_t len = 0;
+          if (mode == 1) {
+            drop_nulls(lb);
+            len = blen[lb];
+            mode = 0;
+          } else {
+            const uint32_t t = type(cur);
+            if (t == JT_ARR) {
+              len = alen(cur);
+            } else if (t == JT_OBJ) {
+              len = doc[doc[cur.p].y].x;
+            } else if (t == JT_STR) {
+              const SView sv = str(cur);
+              for (int k = 0; k < sv.n; ++k) len += (sv.s[k] & 0xC0u) != 0x80u;
+            } else {
+              return CS_ERROR;
+            }
+          }
+          cur = cv(VK_NUM, len);
           break;
         }
         default: return CS_ERROR;  // QO_ERROR: an empty expression
@@ -1084,7 +1107,7 @@ struct CondVM {
 // cannot use => undecided) and the cell stays pending for kpe_pattern_kernel.
 constexpr uint32_t PH_PRE = 0, PH_HANDLER = 1, PH_DENY = 2, PH_FE_LIST = 3, PH_FE_EL = 4, PH_FE_PRE = 5,
                    PH_FE_DENY = 6, PH_DONE = 7, PH_PV = 8, PH_FE_BODY = 9, PH_FE_PAT = 10, PH_FE_RES = 11,
-                   PH_FE_POP = 12;
+                   PH_FE_POP = 12, PH_EXC = 13;
 struct FeFrame {
   KpeCForeach fe;
   uint32_t f, fend, idx, n, count, applied;
@@ -1133,12 +1156,13 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
     const KpeCRule cr = a.rules[i];
     const uint8_t cell = row[cr.col];
     if (cell == KPE_NA_) continue;  // the rule did not match
-    // a PolicyException already made the cell RuleSkip (validate_resource.go:44-56 returns before
-    // the deny / foreach is evaluated); exceptions compile only on rules without resource-reading
-    // preconditions, so every excepted cell is one with cr.pre == CE_NONE
-    if (cr.pre == CE_NONE && cell != KPE_PENDING_) continue;
-    uint32_t v = cell;
-    uint32_t ph = cr.pre != CE_NONE ? PH_PRE : PH_HANDLER;
+    // A PolicyException the scan decided already made the cell RuleSkip (validate_resource.go:
+    // 44-56 returns before the deny / foreach is evaluated). A deferred one (XC_DEFER) is applied
+    // here after the preconditions, in the cells whose exception match held (KPE_XDEFER_).
+    const bool xd = (cr.xflags & XC_DEFER) && (cell & KPE_XDEFER_);
+    uint32_t v = xd ? cell & ~(uint32_t)KPE_XDEFER_ : cell;
+    if (cr.pre == CE_NONE && !xd && cell != KPE_PENDING_) continue;
+    uint32_t ph = cr.pre != CE_NONE ? PH_PRE : xd ? PH_EXC : PH_HANDLER;
     FeFrame fr[KPE_FE_DEPTH];
     vm.dep = -1;
     uint32_t ev = 0;            // the current element's verdict (PH_FE_RES) / a level's result (PH_FE_POP)
@@ -1324,10 +1348,15 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         continue;
       }
       const bool elem = ph == PH_FE_PRE || ph == PH_FE_DENY;
-      const uint32_t bi = ph == PH_PRE ? cr.pre : ph == PH_DENY ? cr.deny : ph == PH_FE_PRE ? F.fe.pre : F.fe.deny;
+      const uint32_t bi = ph == PH_PRE   ? cr.pre
+                          : ph == PH_EXC ? cr.exc
+                          : ph == PH_DENY ? cr.deny
+                          : ph == PH_FE_PRE ? F.fe.pre
+                                            : F.fe.deny;
       const int saved = vm.dep;
       if (!elem) vm.dep = -1;  // rule-level conditions: no element in the context
-      const int res = vm.block(bi);  // the one call site
+      const int res = bi == CE_NONE ? CB_TRUE : vm.block(bi);  // the one call site (an exception
+                                                               // without conditions holds)
       vm.dep = saved;
       if (res == CB_UNDEC) {
         v = KPE_UNDECIDED_;
@@ -1336,10 +1365,20 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
       }
       if (ph == PH_PRE) {  // engine.go:278-285: false => skip, error => error
         if (res == CB_TRUE) {
-          ph = PH_HANDLER;
+          ph = xd ? PH_EXC : PH_HANDLER;
         } else {
           v = res == CB_FALSE ? KPE_SKIP_ : KPE_ERROR_;
           ph = PH_DONE;
+        }
+      } else if (ph == PH_EXC) {  // MatchesException (exceptions.go:33-41): only true applies it
+        if (res == CB_TRUE) {
+          // validate_resource.go:43-56 skips; validate_pss.go:45-104 with podSecurity controls
+          // evaluates the pod under the exception's exclusions (kpe_pssx_kernel, KPE_XFAIL_)
+          if (cr.xflags & XC_PSS) v = v == KPE_FAIL_ ? KPE_XFAIL_ : v;
+          else v = KPE_SKIP_;
+          ph = PH_DONE;
+        } else {
+          ph = PH_HANDLER;
         }
       } else if (ph == PH_DENY) {  // validateDeny (validate_resource.go:268-279)
         v = res == CB_TRUE ? KPE_FAIL_ : res == CB_FALSE ? KPE_PASS_ : KPE_ERROR_;

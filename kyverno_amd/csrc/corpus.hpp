@@ -62,7 +62,6 @@ struct Corpus {
   std::vector<uint32_t> rec;   // 4 words per pod
   std::vector<uint32_t> hdr;   // 4 words per 64 pods
   std::vector<uint32_t> crec;  // 2 words per container
-  std::vector<uint32_t> psum;  // 2 words per pod: the PSA summary (schema.h PS_*, flatten.cpp rebuild_summary)
   std::vector<uint32_t> pann_kv;  // (key, value) pairs of pod-template annotations
   std::vector<uint64_t> capset_add, capset_drop;
   std::unordered_map<std::string, uint32_t> capset_index;

@@ -27,7 +27,6 @@
 #include "jscan.hpp"
 #include "k8s_schema.hpp"
 #include "podview.hpp"
-#include "pss_fixed.hpp"
 
 namespace kpe {
 
@@ -1223,8 +1222,10 @@ class DocBuilder {
       try {
         images((uint32_t)(C.doc.size() / 2 - 1));
       } catch (const ImageError&) {  // NewPolicyContext fails: no response for any rule
-        C.r_flags[row] |= R_CTX_ERR;
-        C.limit_rows.push_back(row);
+        if (!(C.r_flags[row] & R_CTX_ERR)) {  // the pod-column pass may have flagged the row already
+          C.r_flags[row] |= R_CTX_ERR;
+          if (C.limit_rows.empty() || C.limit_rows.back() != row) C.limit_rows.push_back(row);
+        }
       }
     }
   }
@@ -1615,77 +1616,6 @@ void rebuild_headers(Corpus& C) {
 
 unsigned flatten_threads();
 
-// Per-pod PSA summary (Corpus::psum, read by kpe_lean5_kernel): the OR of each pod's container
-// state bitmaps and of its list items' codes under the PSA library's fixed sets (pss_fixed.hpp),
-// the same codes the scan kernels compute per item from the fixed predicates (kernels.hip
-// CS_* capability-set bits, lean.inl vol_code / sys_code / ann_code). Policy-independent; a
-// LEAN scan then reads one record pair per pod instead of its lists.
-void rebuild_summary(Corpus& C) {
-  const int64_t n = C.n;
-  C.psum.assign((size_t)n * 2, 0u);
-  if (n == 0) return;
-  const Dict& capd = C.dict[D_CAP];
-  uint64_t ok = 0, nbs = 0, all = 0;
-  for (uint32_t i = 0; i < capd.size() && i < 64; ++i) {
-    const std::string c(capd.at(i));
-    if (pssfix::fixed_match(pssfix::kCapsBaselineOk, c)) ok |= 1ull << i;
-    if (pssfix::fixed_match(pssfix::kCapNbs, c)) nbs |= 1ull << i;
-    if (pssfix::fixed_match(pssfix::kCapAll, c)) all |= 1ull << i;
-  }
-  std::vector<uint8_t> csb(C.capset_add.size());
-  for (size_t j = 0; j < csb.size(); ++j) {
-    const uint64_t ad = C.capset_add[j], dr = C.capset_drop[j];
-    csb[j] = (uint8_t)(((ad & ~ok) ? 1u : 0u) | ((dr & all) ? 0u : 2u) | ((ad & ~nbs) ? 4u : 0u));
-  }
-  const Dict& sysd = C.dict[D_SYSCTL];
-  std::vector<uint8_t> sysb(sysd.size());
-  const std::vector<std::string> sv[3] = {pssfix::sysctls(0), pssfix::sysctls(1), pssfix::sysctls(2)};
-  for (uint32_t i = 0; i < sysd.size(); ++i) {
-    const std::string x(sysd.at(i));
-    for (int v = 0; v < 3; ++v) sysb[i] |= pssfix::fixed_match(sv[v], x) ? 0u : (uint8_t)(1u << v);
-  }
-  const Dict &akd = C.dict[D_ANNK], &avd = C.dict[D_ANNV];
-  std::vector<uint8_t> ak(akd.size()), av(avd.size());
-  for (uint32_t i = 0; i < akd.size(); ++i) {
-    const std::string x(akd.at(i));
-    ak[i] = (pssfix::fixed_match(pssfix::kApparmorKey, x) ? 1u : 0u) | (pssfix::fixed_match(pssfix::kSeccompPodKey, x) ? 2u : 0u);
-  }
-  for (uint32_t i = 0; i < avd.size(); ++i) {
-    const std::string x(avd.at(i));
-    av[i] = (pssfix::fixed_match(pssfix::kApparmorOk, x) ? 1u : 0u) | (pssfix::fixed_match(pssfix::kSeccompAnnOk, x) ? 2u : 0u);
-  }
-  auto range = [&](int64_t r0, int64_t r1) {
-    for (int64_t r = r0; r < r1; ++r) {
-      uint32_t xo = 0, co = 0, vc = 0, sc = 0, ac = 0;
-      for (uint32_t k = C.ctr_off[r]; k < C.ctr_off[r + 1]; ++k) {
-        const uint32_t x = C.crec[2 * k];
-        xo |= x;
-        if (x) co |= csb[CY_CAPSET(C.crec[2 * k + 1])];
-      }
-      for (uint32_t k = C.vol_off[r]; k < C.vol_off[r + 1]; ++k) {
-        const uint32_t v = C.vol_src[k];
-        vc |= ((v >> VS_HOSTPATH) & 1u) | ((v & PSS_ALLOWED_VOLUMES) ? 0u : 2u);
-      }
-      for (uint32_t k = C.sys_off[r]; k < C.sys_off[r + 1]; ++k) sc |= C.sys_id[k] < sysb.size() ? sysb[C.sys_id[k]] : 7u;
-      for (uint32_t k = C.pann_off[r]; k < C.pann_off[r + 1]; ++k) {
-        const uint32_t kk = C.pann_k[k], vv = C.pann_v[k];
-        const uint32_t a = kk < ak.size() ? ak[kk] : 0u, b = vv < av.size() ? av[vv] : 0u;
-        ac |= ((a & 1u) && !(b & 1u) ? 1u : 0u) | ((a & 2u) && !(b & 2u) ? 2u : 0u);
-      }
-      C.psum[2 * r] = xo;
-      C.psum[2 * r + 1] = co | (vc << 3) | (sc << 5) | (ac << 8);
-    }
-  };
-  const unsigned T = std::max(1u, std::min<unsigned>(flatten_threads(), (unsigned)(n / 65536)));
-  if (T <= 1) {
-    range(0, n);
-    return;
-  }
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < T; ++t) th.emplace_back(range, n * t / T, n * (t + 1) / T);
-  for (auto& x : th) x.join();
-}
-
 template <class T>
 void grow(std::vector<T>& v, size_t n) {
   v.resize(v.size() + n);
@@ -1938,7 +1868,6 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
   if (T <= 1 || C.n != 0) {
     flatten_range(C, buf, 0, len, docs);
     rebuild_headers(C);
-    rebuild_summary(C);
     return;
   }
   std::vector<size_t> cut(T + 1, len);
@@ -1976,7 +1905,6 @@ void flatten_ndjson(Corpus& C, const char* buf, size_t len, const char* nsl, siz
     flatten_range(C, buf, 0, len, docs);
   }
   rebuild_headers(C);
-  rebuild_summary(C);
   if (getenv("KPE_DEBUG")) {
     const auto t2 = std::chrono::steady_clock::now();
     fprintf(stderr, "kpe flatten: %u threads, chunks %.3f s, merge %.3f s\n", T,

@@ -835,9 +835,9 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     uint32_t* wrest = wbase + (PSS ? KPE_STAGE_WORDS : 0u);
     uint64_t* tmk = reinterpret_cast<uint64_t*>(wrest);
     uint64_t* cvm = tmk + a.nterms;
-    uint64_t* rmk = cvm + a.ncv;  // kRC x (P, F, E)
+    uint64_t* rmk = cvm + a.ncv;  // kRC x (P, F, E, D): D = KPE_XDEFER_ cells
     uint8_t* sv = NARROW ? reinterpret_cast<uint8_t*>(wrest) + buf * 64 * R
-                         : reinterpret_cast<uint8_t*>(rmk + 3 * KPE_RULE_CHUNK);
+                         : reinterpret_cast<uint8_t*>(rmk + 4 * KPE_RULE_CHUNK);
     // ---- prefetch the next tile into the other buffer, then evaluate `cur` ----
     // (unconditional, clamped: past the end it re-reads the last tile, never used)
     nxt = load_tile<PSS, LEAN>(a, min(tile + W, ntiles - 1), h, lane);
@@ -931,8 +931,10 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         const uint32_t hd = NR_HANDLER(x);
         uint32_t v = KPE_NA_;
         // PolicyExceptions of the rule: their match block holds => RuleSkip before any handler
+        // (XE_DEFER: the cell's verdict without the exception, flagged for kpe_cond_kernel)
         const uint32_t xe = (m && a.rule_exc) ? sld(a.rule_exc, ri) : 0u;
-        const bool xh = xe && block((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe));
+        const bool xm = xe && block((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe));
+        const bool xh = xm && !(xe & XE_DEFER);
         if (xh && !(xe & XE_PSS)) v = KPE_SKIP_;
         else if (m && hd == H_PSS)  // under a podSecurity exception kpe_pssx_kernel decides
           v = err ? KPE_ERROR_ : xh ? KPE_XFAIL_ : ((fails & nr.y) ? KPE_FAIL_ : KPE_PASS_);
@@ -944,7 +946,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         if (x & NR_NEW_POLICY) applied = false;
         if ((x & NR_APPLY_ONE) && applied) v = KPE_NA_;
         applied |= v == KPE_PASS_ || v == KPE_FAIL_;
-        sv[lane * R + ri] = (uint8_t)v;
+        sv[lane * R + ri] = (uint8_t)(v | (xm && !xh && v != KPE_NA_ ? (uint32_t)KPE_XDEFER_ : 0u));
         if (a.masks && live) a.masks[(size_t)r * R + ri] = v == KPE_FAIL_ ? (fails & nr.y) : 0u;
       }
       __builtin_amdgcn_wave_barrier();
@@ -1016,17 +1018,20 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         } else if (handler == H_CONST_PASS) {
           pm = m;
         }
+        uint64_t dm = 0;
         if (a.rule_exc && m) {  // PolicyExceptions: RuleSkip where their match block holds
           const uint32_t xe = a.rule_exc[c0 + lane];
           if (xe) {
             const uint64_t xm = m & block_mask((xe & XE_ALL) ? MODE_ALL : MODE_ANY, XE_F0(xe), XE_NF(xe));
-            if (xe & XE_PSS) pm |= xm & ~em, fm |= xm & ~em;  // p and f: KPE_XFAIL_ (kpe_pssx_kernel decides)
+            if (xe & XE_DEFER) dm = xm;  // kpe_cond_kernel applies it after the preconditions
+            else if (xe & XE_PSS) pm |= xm & ~em, fm |= xm & ~em;  // p and f: KPE_XFAIL_ (kpe_pssx_kernel decides)
             else pm |= xm, em |= xm, fm &= ~xm;
           }
         }
-        rmk[lane * 3 + 0] = pm;
-        rmk[lane * 3 + 1] = fm;
-        rmk[lane * 3 + 2] = em;
+        rmk[lane * 4 + 0] = pm;
+        rmk[lane * 4 + 1] = fm;
+        rmk[lane * 4 + 2] = em;
+        rmk[lane * 4 + 3] = dm;
       }
       __builtin_amdgcn_wave_barrier();
       if (a.any_apply_one) {  // ApplyOne: later rules of a policy skip resources already applied
@@ -1038,10 +1043,10 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
               cur_policy = rule.policy;
               applied = 0;
             }
-            uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
+            uint64_t pm = rmk[j * 4], fm = rmk[j * 4 + 1], em = rmk[j * 4 + 2];
             if (rule.apply_one) {
               pm &= ~applied, fm &= ~applied, em &= ~applied;
-              rmk[j * 3] = pm, rmk[j * 3 + 1] = fm, rmk[j * 3 + 2] = em;
+              rmk[j * 4] = pm, rmk[j * 4 + 1] = fm, rmk[j * 4 + 2] = em;
             }
             applied |= pm | fm;
           }
@@ -1051,17 +1056,17 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       // (b) verdict bytes (resource lanes)
 #pragma unroll 4
       for (uint32_t j = 0; j < nc; ++j) {
-        const uint64_t pm = rmk[j * 3], fm = rmk[j * 3 + 1], em = rmk[j * 3 + 2];
+        const uint64_t pm = rmk[j * 4], fm = rmk[j * 4 + 1], em = rmk[j * 4 + 2], dm = rmk[j * 4 + 3];
         const uint32_t f = (fm >> lane) & 1u, e = (em >> lane) & 1u;
         const uint32_t p = (pm >> lane) & 1u;
         const uint32_t v = p ? (e ? KPE_SKIP_ : f ? KPE_XFAIL_ : KPE_PASS_) : (f && e) ? KPE_PENDING_ : f ? KPE_FAIL_
                                                                    : e ? KPE_ERROR_ : KPE_NA_;
-        sv[lane * nc + j] = (uint8_t)v;
+        sv[lane * nc + j] = (uint8_t)(v | (((dm >> lane) & 1u) && v != KPE_NA_ ? (uint32_t)KPE_XDEFER_ : 0u));
       }
       if (a.masks && live) {
 #pragma unroll 1
         for (uint32_t j = 0; j < nc; ++j) {
-          const uint32_t cm = ((rmk[j * 3 + 1] >> lane) & 1u) ? (fails & sld(a.rules, c0 + j).cv_mask) : 0u;
+          const uint32_t cm = ((rmk[j * 4 + 1] >> lane) & 1u) ? (fails & sld(a.rules, c0 + j).cv_mask) : 0u;
           a.masks[(size_t)r * R + c0 + j] = cm;
         }
       }
@@ -1358,7 +1363,6 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipSt
 namespace {
 typedef void (*ScanFn)(const ScanArgs*);
 ScanFn scan_fn(int pss, int narrow) {
-  if (pss && narrow >= 3) return nullptr;  // kpe_lean_kernel / kpe_lean3_kernel (by-value arguments)
   if (pss && narrow == 2) return kpe_scan_kernel<true, true, false, true>;
   if (pss) return narrow ? kpe_scan_kernel<true, true, false> : kpe_scan_kernel<true, false, false>;
   return narrow ? kpe_scan_kernel<false, true, false> : kpe_scan_kernel<false, false, false>;
@@ -1369,17 +1373,13 @@ ScanFn prep_fn(int pss, int narrow) {
 }
 }  // namespace
 
-// Persistent grid: as many blocks as can be resident at once (occupancy x CUs),
-// capped by the number of 256-resource tiles.
+// Scan grid. kpe_lean5_kernel (narrow code 7): one 64-pod tile per wave, no persistent loop.
+// The others: persistent, as many blocks as can be resident at once (occupancy x CUs), capped
+// by the number of 256-resource tiles.
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes) {
   if (n <= 0) return 0;
-  if (pss && narrow >= 5 && narrow <= 8) {  // kpe_lean4_kernel<1> / <2>, kpe_lean5_kernel<1> / <2>
-    const int64_t tpw = (narrow == 6 || narrow == 8) ? 2 : 1;
-    const int64_t waves = ((n + 63) / 64 + tpw - 1) / tpw;
-    return (uint32_t)((waves + kLB / 64 - 1) / (kLB / 64));
-  }
-  if (pss && narrow == 4) {  // kpe_lean3_kernel: KPE_LEAN_T tiles of 64 rows per wave, no persistent loop
-    const int64_t waves = ((n + 63) / 64 + KPE_LEAN_T - 1) / KPE_LEAN_T;
+  if (pss && narrow == 7) {
+    const int64_t waves = (n + 63) / 64;
     return (uint32_t)((waves + kLB / 64 - 1) / (kLB / 64));
   }
   static thread_local int cus = 0;
@@ -1389,12 +1389,8 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
       cus = 256;
   }
   int per_cu = 0;
-  const hipError_t oe = pss && narrow == 3
-                           ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kpe_lean_kernel, kBlock, dyn_bytes)
-                           : hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn(pss, narrow), kBlock, dyn_bytes);
-  if (oe != hipSuccess) per_cu = 1;
-  static const int bpc_env = getenv("KPE_SCAN_BPC") ? atoi(getenv("KPE_SCAN_BPC")) : 0;  // experiments
-  if (bpc_env > 0 && bpc_env < per_cu) per_cu = bpc_env;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, scan_fn(pss, narrow), kBlock, dyn_bytes) != hipSuccess)
+    per_cu = 1;
   const int64_t tiles = (n + kBlock - 1) / kBlock;
   const int64_t g = (int64_t)cus * (per_cu > 0 ? per_cu : 1);
   return (uint32_t)(g < tiles ? g : tiles);
@@ -1403,31 +1399,30 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* hargs, int64_t n, int pss, int narrow,
                                       uint32_t grid, size_t dyn_bytes, hipStream_t s) {
   if (n == 0 || grid == 0) return hipSuccess;
-  if (pss && narrow == 3) {  // kpe_lean_kernel takes its arguments by value
-    hipLaunchKernelGGL(kpe_lean_kernel, dim3(grid), dim3(kBlock), dyn_bytes, s, *hargs);
-    return hipGetLastError();
-  }
-  if (pss && narrow == 4) {
-    hipLaunchKernelGGL(kpe_lean3_kernel, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
-    return hipGetLastError();
-  }
-  if (pss && narrow == 5) {
-    hipLaunchKernelGGL(kpe_lean4_kernel<1>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
-    return hipGetLastError();
-  }
-  if (pss && narrow == 6) {
-    hipLaunchKernelGGL(kpe_lean4_kernel<2>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
-    return hipGetLastError();
-  }
-  if (pss && narrow == 7) {
-    hipLaunchKernelGGL(kpe_lean5_kernel<1>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
-    return hipGetLastError();
-  }
-  if (pss && narrow == 8) {
-    hipLaunchKernelGGL(kpe_lean5_kernel<2>, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
+  if (pss && narrow == 7) {  // kpe_lean5_kernel takes its arguments by value
+    hipLaunchKernelGGL(kpe_lean5_kernel, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
+  return hipGetLastError();
+}
+// The per-pod PSA summary of a corpus (lean.inl): dictionary codes, capability-set codes, then
+// one wave per 64-pod tile.
+extern "C" hipError_t kpe_launch_psum(const PsumArgs* a, hipStream_t s) {
+  if (a->n <= 0) return hipSuccess;
+  uint32_t dmax = 0;
+  for (int d = 0; d < 4; ++d) dmax = std::max(dmax, a->dict_n[d]);
+  if (dmax) {
+    hipLaunchKernelGGL(kpe_psa_dict_kernel, dim3((dmax + 255u) / 256u, 4), dim3(256), 0, s, *a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  if (a->ncapsets) {
+    hipLaunchKernelGGL(kpe_psa_capset_kernel, dim3((a->ncapsets + 255u) / 256u), dim3(256), 0, s, *a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(kpe_psum_kernel, dim3((a->ntiles + 3u) / 4u), dim3(256), 0, s, *a);
   return hipGetLastError();
 }
 // One block: the evaluation's prologue image (ScanArgs::pimg).

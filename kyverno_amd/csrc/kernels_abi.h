@@ -161,13 +161,41 @@ struct ScanArgs {
   uint32_t pimg_words, capb_lds;
   // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask (PRED_NONE: no table)
   uint32_t kt_lds, nkinds;
-  // LEAN4 tile slabs (DeviceCorpus::slab_*): tile t's first K items of a list at [t * K, t * K + K)
-  const uint32_t *slab_c, *slab_v, *slab_s, *slab_a;
-  uint32_t kc, kv, ks, ka;
-  const uint32_t* psum;  // LEAN5: per-pod PSA summary (2 words per pod, schema.h PS_*)
+  const uint32_t* psum;  // LEAN5: per-pod PSA summary (2 words per pod, schema.h PS_*; kpe_psum_kernel)
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null
+};
+
+// The per-pod PSA summary (lean.inl kpe_psa_dict_kernel / kpe_psa_capset_kernel / kpe_psum_kernel):
+// the four dictionaries it codes (PsumArgs::dict_*[PSD_*]) and the fixed sets of the PSA library
+// (pss_fixed.hpp) as bits of a string's set-hit word (PsumArgs::fixed entries' set numbers).
+#define PSD_CAP 0
+#define PSD_SYSCTL 1
+#define PSD_ANNK 2
+#define PSD_ANNV 3
+#define PSF_CAPS_OK 0
+#define PSF_CAP_NBS 1
+#define PSF_CAP_ALL 2
+#define PSF_SYSCTL0 3
+#define PSF_SYSCTL1 4
+#define PSF_SYSCTL2 5
+#define PSF_APPARMOR_KEY 6
+#define PSF_SECCOMP_POD_KEY 7
+#define PSF_APPARMOR_OK 8
+#define PSF_SECCOMP_ANN_OK 9
+struct PsumArgs {
+  int64_t n;
+  uint32_t ntiles, ncapsets;
+  const uint32_t *rec, *hdr, *crec, *vol_src, *sys_id, *pann_kv, *capsets;
+  const uint8_t* dict_bytes[4];
+  const uint32_t* dict_off[4];
+  uint32_t dict_n[4];
+  const uint8_t* fixed;  // fixed-set table: [set | prefix << 7 | len << 8] + literal, 4-byte padded
+  uint32_t fixed_len, pad_;
+  uint8_t* codes[4];     // code byte per dictionary string (scratch)
+  uint8_t* csb;          // code byte per capability set (scratch)
+  uint32_t* psum;        // out: 2 words per pod
 };
 
 // kpe_pattern_kernel arguments (device-resident, one copy per binding)

@@ -21,6 +21,7 @@
 #include "kernels_abi.h"
 #include "patclass.hpp"
 #include "program.hpp"
+#include "pss_fixed.hpp"
 #include "pss_msg.hpp"
 
 namespace kpe {
@@ -45,6 +46,7 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
                                       uint32_t grid,
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
+extern "C" hipError_t kpe_launch_psum(const PsumArgs* a, hipStream_t s);
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
                                        hipStream_t s);
 
@@ -233,11 +235,10 @@ struct DeviceCorpus {
   DevBuf ctr_off, vol_off, sys_off, pann_off, c_name, c_image, c_sann_key, c_sec_str, c_pm_str, c_selt_str, c_selu_str,
       c_selr_str, cport_off, cport_str, pann_k, pann_v, p_cold;
   bool cold = false;
-  // LEAN4 tile slabs (kpe_lean4_kernel): tile t's first K items of each list at [t * K, t * K + K)
-  DevBuf slab_c, slab_v, slab_s, slab_a;
-  DevBuf psum;  // LEAN5: per-pod PSA summaries (Corpus::psum)
-  uint32_t kc = 0, kv = 0, ks = 0, ka = 0;
-  bool slabs = false;
+  // per-pod PSA summaries (kpe_psum_kernel; read by kpe_lean5_kernel), built on the device at the
+  // first binding of a LEAN program; the dictionary / capability-set codes are its scratch
+  DevBuf psum, psa_codes, psa_csb, psa_fixed;
+  bool psum_ready = false;
   Binding bind;
   bool has_masks = false;
 };
@@ -484,6 +485,7 @@ void append_words(std::vector<uint32_t>& img, const std::vector<T>& v, uint32_t*
 kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   auto& P = *pp->p;
   if (dev->ordinal < 0 || dev->ordinal >= 16) return fail(KPE_E_DEVICE, "device ordinal past 15");
+  std::lock_guard<std::mutex> plk(P.dev_mu);
   if (P.devs[dev->ordinal]) return KPE_OK;  // one copy per device: programs are shared across devices
   std::vector<uint32_t> lanes;  // rule lane records (kernels_abi.h RL_*)
   for (auto& r : P.rules) {
@@ -675,54 +677,64 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   return need;
 }
-// kpe_lean4_kernel's tile slabs: per list, K = the 99th percentile of the per-tile item counts
-// (a multiple of 4, at least 4, at most the wave's staging capacity), and tile t's first
-// min(count, K) items copied to [t * K, ...), zero padded. Items past K stay in the CSR columns
-// (the kernel loads them at header offsets). Built once per corpus, on the host.
-kpe_status build_slabs(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
-  if (D.slabs) return KPE_OK;
-  const size_t nt = (size_t)((C.n + 63) / 64);
-  if (nt == 0) return KPE_OK;  // nothing is launched over an empty corpus
-  auto one = [&](int word, uint32_t cap, uint32_t width, const uint32_t* col, DevBuf& out, uint32_t* K) -> hipError_t {
-    std::vector<uint32_t> cnt(nt);
-    for (size_t t = 0; t < nt; ++t) cnt[t] = C.hdr[4 * (t + 1) + word] - C.hdr[4 * t + word];
-    std::vector<uint32_t> srt(cnt);
-    const size_t q = std::min(nt - 1, (size_t)((double)nt * 0.99));
-    std::nth_element(srt.begin(), srt.begin() + q, srt.end());
-    uint32_t k = (srt[q] + 3u) / 4u * 4u;
-    k = std::max(4u, std::min(cap, k));
-    *K = k;
-    std::vector<uint32_t> slab(nt * k * width + width, 0u);
-    for (size_t t = 0; t < nt; ++t) {
-      const uint32_t first = C.hdr[4 * t + word], m = std::min(cnt[t], k);
-      if (m) memcpy(&slab[t * k * width], col + (size_t)first * width, (size_t)m * width * 4);
-    }
-    return upload(out, slab, s);
-  };
-  HIPCHK(one(0, KPE_STAGE_CTR, 2, C.crec.data(), D.slab_c, &D.kc));
-  HIPCHK(one(1, KPE_STAGE_VOL, 1, C.vol_src.data(), D.slab_v, &D.kv));
-  HIPCHK(one(2, KPE_STAGE_SMALL, 1, C.sys_id.data(), D.slab_s, &D.ks));
-  HIPCHK(one(3, KPE_STAGE_SMALL, 2, C.pann_kv.data(), D.slab_a, &D.ka));
-  D.slabs = true;
-  return KPE_OK;
+// The fixed-set table of kpe_psa_dict_kernel (kernels_abi.h PsumArgs::fixed) from the PSA
+// library's sets (pss_fixed.hpp): [set | prefix << 7 | len << 8] + literal, 4-byte padded.
+const std::vector<uint8_t>& psa_fixed_table() {
+  static const std::vector<uint8_t> tab = [] {
+    std::vector<uint8_t> t;
+    auto add = [&](uint32_t set, const std::vector<std::string>& globs) {
+      for (const auto& g : globs) {
+        const bool prefix = !g.empty() && g.back() == '*';
+        const std::string lit = prefix ? g.substr(0, g.size() - 1) : g;
+        const uint32_t h = set | (prefix ? 1u << 7 : 0u) | (uint32_t)lit.size() << 8;
+        for (int k = 0; k < 4; ++k) t.push_back((uint8_t)(h >> (8 * k)));
+        t.insert(t.end(), lit.begin(), lit.end());
+        while (t.size() % 4) t.push_back(0);
+      }
+    };
+    namespace F = kpe::pssfix;
+    add(PSF_CAPS_OK, F::kCapsBaselineOk), add(PSF_CAP_NBS, F::kCapNbs), add(PSF_CAP_ALL, F::kCapAll);
+    add(PSF_SYSCTL0, F::sysctls(0)), add(PSF_SYSCTL1, F::sysctls(1)), add(PSF_SYSCTL2, F::sysctls(2));
+    add(PSF_APPARMOR_KEY, F::kApparmorKey), add(PSF_SECCOMP_POD_KEY, F::kSeccompPodKey);
+    add(PSF_APPARMOR_OK, F::kApparmorOk), add(PSF_SECCOMP_ANN_OK, F::kSeccompAnnOk);
+    return t;
+  }();
+  return tab;
 }
-// bytes of one kpe_lean4_kernel launch: records, headers, every slab slot, the items past K
-double lean4_bytes(const kpe::Program& P, const kpe::Corpus& C, const kpe::DeviceCorpus& D, uint32_t need) {
-  const size_t nt = (size_t)((C.n + 63) / 64);
-  double b = 16.0 * (double)C.n + 16.0 * (double)nt + (double)C.n * (double)P.rules.size();
-  auto list = [&](int word, uint32_t k, double width) {
-    double over = 0;
-    for (size_t t = 0; t < nt; ++t) {
-      const uint32_t c = C.hdr[4 * (t + 1) + word] - C.hdr[4 * t + word];
-      if (c > k) over += c - k;
-    }
-    return width * ((double)nt * k + over);
-  };
-  b += list(0, D.kc, 8.0);
-  if (need & NEED_VOL) b += list(1, D.kv, 4.0);
-  if (need & NEED_SYS) b += list(2, D.ks, 4.0);
-  if (need & NEED_PANN) b += list(3, D.ka, 8.0);
-  return b;
+// Launch the per-pod PSA summary of an uploaded corpus on stream s (kpe_launch_psum).
+kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
+  const int dom[4] = {D_CAP, D_SYSCTL, D_ANNK, D_ANNV};
+  PsumArgs a{};
+  a.n = C.n;
+  a.ntiles = (uint32_t)((C.n + 63) / 64);
+  a.ncapsets = (uint32_t)C.capset_add.size();
+  a.rec = D.rec.as<uint32_t>(), a.hdr = D.hdr.as<uint32_t>(), a.crec = D.crec.as<uint32_t>();
+  a.vol_src = D.vol_src.as<uint32_t>(), a.sys_id = D.sys_id.as<uint32_t>(), a.pann_kv = D.pann_kv.as<uint32_t>();
+  a.capsets = D.capsets.as<uint32_t>();
+  size_t code_bytes = 0;
+  for (int d = 0; d < 4; ++d) code_bytes += (C.dict[dom[d]].size() + 15) & ~(size_t)15;
+  if (!D.psum_ready) {
+    const auto& tab = psa_fixed_table();
+    HIPCHK(upload(D.psa_fixed, tab, s));
+    HIPCHK(D.psa_codes.ensure(code_bytes + 16));
+    HIPCHK(D.psa_csb.ensure(C.capset_add.size() + 16));
+    HIPCHK(D.psum.ensure((size_t)C.n * 8 + 16));
+  }
+  a.fixed = D.psa_fixed.as<uint8_t>();
+  a.fixed_len = (uint32_t)psa_fixed_table().size();
+  size_t at = 0;
+  for (int d = 0; d < 4; ++d) {
+    a.dict_bytes[d] = D.dict_bytes[dom[d]].as<uint8_t>();
+    a.dict_off[d] = D.dict_off[dom[d]].as<uint32_t>();
+    a.dict_n[d] = C.dict[dom[d]].size();
+    a.codes[d] = D.psa_codes.as<uint8_t>() + at;
+    at += (C.dict[dom[d]].size() + 15) & ~(size_t)15;
+  }
+  a.csb = D.psa_csb.as<uint8_t>();
+  a.psum = D.psum.as<uint32_t>();
+  HIPCHK(kpe_launch_psum(&a, s));
+  D.psum_ready = true;
+  return KPE_OK;
 }
 double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
   double b = 0;
@@ -769,7 +781,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const bool narrow = PD.narrow;
   const uint32_t wave_words = (P.any_pss ? KPE_STAGE_WORDS : 0u) +
                               (narrow ? 2 * 64 * (uint32_t)P.rules.size() / 4  // double-buffered rows
-                                      : 2 * nterms + 2 * ncv + 2 * 3 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4);
+                                      : 2 * nterms + 2 * ncv + 2 * 4 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4);
   const uint32_t prog_words = 2 * (uint32_t)P.filters.size() + (uint32_t)P.fterms.size();
   const bool stage_prog = !narrow && prog_words <= kMaxProgLds;
   // LEAN scan candidate: prepped, NARROW truth-table program of kind-only terms (a kind table
@@ -1027,22 +1039,12 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.blob_words = blob;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  // LEAN scans run kpe_lean_kernel (buffer loads: every scanned column under 4 GiB, with a
-  // tile's slack) unless KPE_OLD_LEAN selects the template instantiation
+  // LEAN scans run kpe_lean5_kernel over the per-pod PSA summaries (buffer loads with 32-bit
+  // offsets: the pod records under 4 GiB), else the template instantiation
   const uint64_t lim = (1ull << 32) - (1ull << 20);
-  B.lean_kind = !lean ? 0 : (getenv("KPE_OLD_LEAN") || (uint64_t)C.n * 16 + 4096 > lim ||
-                             (uint64_t)C.c_sc.size() * 8 > lim || (uint64_t)C.vol_src.size() * 4 > lim ||
-                             (uint64_t)C.sys_id.size() * 4 > lim || (uint64_t)C.pann_kv.size() * 4 > lim)
-                                ? 2
-                                : getenv("KPE_LEAN_PERSIST") ? 3 : getenv("KPE_LEAN3") ? 4 : getenv("KPE_LEAN4_T2") ? 6
-                                  : getenv("KPE_LEAN4") ? 5 : getenv("KPE_LEAN5_T2") ? 8 : 7;
-  if (B.lean_kind >= 7 && (C.psum.size() != (size_t)C.n * 2 || (uint64_t)C.n * 16 > lim)) B.lean_kind = 5;
-  if (B.lean_kind >= 7 && !cc->d->psum.p) HIPCHK(upload(cc->d->psum, C.psum, s));
-  if (B.lean_kind == 5 || B.lean_kind == 6) {
-    const uint64_t slab_bytes = (uint64_t)((C.n + 63) / 64) * KPE_STAGE_CTR * 8;
-    if (slab_bytes > lim) B.lean_kind = 4;
-    else if (kpe_status st = build_slabs(C, *cc->d, s)) return st;
-  }
+  B.lean_kind = !lean ? 0 : (uint64_t)C.n * 16 + 4096 > lim ? 2 : 7;
+  if (B.lean_kind == 7 && !cc->d->psum_ready)
+    if (kpe_status st = run_psum(C, *cc->d, s)) return st;
   B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : narrow ? 1 : 0, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   {  // ApplyOne policies: contiguous rule ranges in ComputeRules order
@@ -1101,6 +1103,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   const size_t R = P.rules.size();
   static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
   const bool fresh = !B.inv_ready || no_cache || cold;
+  if (cold && B.lean && B.lean_kind == 7)  // a cold evaluation rebuilds the corpus's PSA summaries too
+    if (kpe_status st = run_psum(C, D, s)) return st;
   if (B.nblocks && fresh) {  // dictionary pass for large-domain predicates
     PredArgs pa{};
     for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
@@ -1201,12 +1205,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
   sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
-  sa.psum = D.psum.p ? D.psum.as<uint32_t>() : nullptr;
-  if (D.slabs) {
-    sa.slab_c = D.slab_c.as<uint32_t>(), sa.slab_v = D.slab_v.as<uint32_t>();
-    sa.slab_s = D.slab_s.as<uint32_t>(), sa.slab_a = D.slab_a.as<uint32_t>();
-    sa.kc = D.kc, sa.kv = D.kv, sa.ks = D.ks, sa.ka = D.ka;
-  }
+  sa.psum = D.psum_ready ? D.psum.as<uint32_t>() : nullptr;
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   if (!B.args_valid || memcmp(&sa, &B.hargs, sizeof(ScanArgs)) != 0) {  // once per binding / masks mode
@@ -1231,7 +1230,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
-  const bool lean_go = B.lean && (!masks || B.lean_kind >= 5);  // LEAN4 writes check masks too
+  const bool lean_go = B.lean && (!masks || B.lean_kind == 7);  // LEAN5 writes check masks too
   HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : PD.narrow ? 1 : 0,
                          B.scan_blocks,
                          B.dyn_bytes, s));
@@ -1408,9 +1407,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
     const double mb = masks ? 4.0 * (double)C.n * (double)R : 0.0;
-    ev.bytes = (B.lean && B.lean_kind >= 7)   ? 24.0 * (double)C.n + (double)C.n * (double)R + mb  // records, summaries, rows
-               : (B.lean && B.lean_kind >= 5) ? lean4_bytes(P, C, D, B.need) + mb
-                                              : scan_bytes(P, C, B.need, masks);
+    ev.bytes = lean_go && B.lean_kind == 7 ? 24.0 * (double)C.n + (double)C.n * (double)R + mb  // records, summaries, rows
+                                           : scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     ev.kind = lean_go ? B.lean_kind : 1;
     dev->pending.push_back(ev);
@@ -1453,6 +1451,20 @@ kpe_status kpe_device_sync(kpe_device* dev) {
   if (!dev) return fail(KPE_E_INVALID, "null device");
   HIPCHK(hipSetDevice(dev->ordinal));
   for (int k = 0; k < dev->nlanes; ++k) HIPCHK(hipStreamSynchronize(dev->lanes[k]));
+  return KPE_OK;
+}
+
+kpe_status kpe_corpus_psa_summary(kpe_device* dev, kpe_corpus* c, uint32_t* out) {
+  if (!dev || !c || !out) return fail(KPE_E_INVALID, "null argument");
+  if (!c->d || c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& D = *c->d;
+  if (D.bind.last) HIPCHK(hipStreamSynchronize(D.bind.last));
+  if (!D.psum_ready)
+    if (kpe_status st = run_psum(*c->c, D, dev->stream)) return st;
+  if (c->c->n) HIPCHK(hipMemcpyAsync(out, D.psum.p, (size_t)c->c->n * 8, hipMemcpyDeviceToHost, dev->stream));
+  HIPCHK(hipStreamSynchronize(dev->stream));
   return KPE_OK;
 }
 
@@ -1539,6 +1551,7 @@ kpe_status kpe_device_verdicts(kpe_device* dev, const kpe_program* prog, const k
   HIPCHK(hipSetDevice(dev->ordinal));
   auto& B = c->d->bind;
   if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  if (c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
   if (B.last) HIPCHK(hipStreamSynchronize(B.last));
   *dptr = B.verdicts.p;
   if (bytes) *bytes = (uint64_t)c->c->n * prog->p->rules.size();
@@ -1554,6 +1567,7 @@ kpe_status kpe_pack_verdicts(kpe_device* dev, const kpe_program* prog, const kpe
   HIPCHK(hipSetDevice(dev->ordinal));
   auto& B = c->d->bind;
   if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  if (c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
   const uint64_t cells = (uint64_t)c->c->n * prog->p->rules.size();
   if (words < kpe_packed_words(cells)) return fail(KPE_E_INVALID, "packed buffer too small");
   hipPointerAttribute_t at{};
@@ -1582,11 +1596,14 @@ kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kp
   HIPCHK(hipSetDevice(dev->ordinal));
   auto& B = c->d->bind;
   if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  if (c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
   const uint64_t total = (uint64_t)c->c->n * prog->p->rules.size();
   for (uint64_t i = 0; i < ncells; ++i)
     if (cells[i] >= total) return fail(KPE_E_INVALID, "cell index past the verdict matrix");
   const size_t rec = (size_t)KPE_TRACE_ROOTS * KPE_TRACE_WORDS;
-  if (prog->p->pat.rules.empty() || !B.pargs_valid) {  // no pattern rule: every record is empty
+  if (!prog->p->pat.rules.empty() && !B.pargs_valid)
+    return fail(KPE_E_STATE, "the binding has no completed evaluation of its pattern rules");
+  if (prog->p->pat.rules.empty()) {  // no pattern rule: every record is empty
     memset(out, 0, ncells * rec * 4);
     return KPE_OK;
   }
@@ -1612,7 +1629,7 @@ kpe_status kpe_evaluate_sharded(kpe_device* const* devs, kpe_corpus* const* shar
   for (int i = 0; i < nshards; ++i) {  // every launch first: the devices run together
     if (!devs[i] || !shards[i]) return fail(KPE_E_INVALID, "null device or shard");
     for (int j = 0; j < i; ++j)
-      if (devs[j] == devs[i]) return fail(KPE_E_INVALID, "one shard per device");
+      if (devs[j]->ordinal == devs[i]->ordinal) return fail(KPE_E_INVALID, "one shard per device");
     if (kpe_status st = kpe_evaluate_async(devs[i], prog, shards[i])) return st;
   }
   std::vector<kpe_counts> part(counts ? R : 0);

@@ -1082,14 +1082,16 @@ Fold fold_conditions(const JV* j) {
 //   * JMESPath (github.com/kyverno/go-jmespath, go.mod:33) over request.object,
 //     request.operation ("CREATE"), element / elementIndex: fields, quoted fields, [n], `[]`,
 //     `[*]`, `.[a, b]` multi-select of relative field chains, keys(@), `||` with a literal or
-//     another chain, raw-string and JSON literals. Parse errors of an empty expression are
-//     run-time errors; anything outside the subset is refused;
+//     another chain, raw-string and JSON literals, length(<chain>) and `<chain> | length(@)`
+//     (functions.go jpfLength: runes of a string, items of an array, members of an object, else
+//     an invalid-type error). Parse errors of an empty expression are run-time errors; anything
+//     outside the subset is refused;
 //   * operators Equals / NotEquals / AnyIn / AllIn / AnyNotIn / AllNotIn / In / NotIn
 //     (variables/operator/*.go); InRange values of set operators are refused (as the oracle).
 namespace cq {
 
 enum Tok { T_EOF, T_ID, T_QID, T_NUM, T_DOT, T_STAR, T_FLAT, T_LBRACK, T_RBRACK, T_COMMA, T_LPAREN, T_RPAREN,
-           T_CUR, T_OR, T_LIT, T_RAW, T_OTHER };
+           T_CUR, T_OR, T_LIT, T_RAW, T_PIPE, T_OTHER };
 struct Token {
   Tok t;
   std::string s;
@@ -1195,6 +1197,7 @@ std::vector<Token> lex(const std::string& q) {
       case '(': t = T_LPAREN; break;
       case ')': t = T_RPAREN; break;
       case '@': t = T_CUR; break;
+      case '|': t = T_PIPE; break;
       default: break;
     }
     if (t == T_OTHER) throw CompileError(std::string("JMESPath construct '") + c + "' is not supported on the device");
@@ -1333,6 +1336,22 @@ class QueryParser {
     }
     t_ = lex(q);
     i_ = 0;
+    if (std::any_of(t_.begin(), t_.end(), [](const Token& t) { return t.t == T_PIPE; })) {
+      // `<chain> | length(@)`, the one pipe on the device: the pipe binds loosest (a `||` would
+      // sit inside one of its sides), so no `||` is accepted with it
+      if (std::any_of(t_.begin(), t_.end(), [](const Token& t) { return t.t == T_OR; }))
+        throw CompileError("JMESPath pipe with `||` is not supported on the device: " + q);
+      bool pl = true;
+      std::vector<uint32_t> c = chain(&pl);
+      if (!(cur().t == T_PIPE && peek().t == T_ID && peek().s == "length" && peek(2).t == T_LPAREN &&
+            peek(3).t == T_CUR && peek(4).t == T_RPAREN && peek(5).t == T_EOF))
+        throw CompileError("JMESPath pipe other than `| length(@)` is not supported on the device: " + q);
+      op(c, QO_LEN);
+      KpeCExpr e{(uint32_t)CP.ops.size() / 2, (uint32_t)c.size() / 2, 0, CE_NONE};  // a pipe: not strict
+      CP.ops.insert(CP.ops.end(), c.begin(), c.end());
+      CP.exprs.push_back(e);
+      return (uint32_t)CP.exprs.size() - 1;
+    }
     std::vector<std::vector<uint32_t>> chains;
     std::vector<bool> plain;
     for (;;) {
@@ -1405,6 +1424,16 @@ class QueryParser {
     if (cur().t != T_ID) throw CompileError("JMESPath root outside the device subset");
     const std::string r = cur().s;
     ++i_;
+    if (r == "length" && cur().t == T_LPAREN) {  // length(<chain>): a number, no further steps
+      ++i_;
+      bool pl = true;
+      o = chain(&pl);
+      if (cur().t != T_RPAREN) throw CompileError("length() argument outside the device subset");
+      ++i_;
+      op(o, QO_LEN);
+      *plain = false;
+      return o;
+    }
     if (r == "request") {
       if (cur().t != T_DOT || peek().t != T_ID || (peek().s != "object" && peek().s != "operation"))
         throw CompileError("context value request." + (peek().t == T_ID ? peek().s : std::string("?")) +
@@ -2301,7 +2330,7 @@ class Lowerer {
         }
       }
     }
-    KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0};
+    KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0, CE_NONE, 0};
     crule.pv0 = (uint32_t)P.pat.vars.size();
     bool pss_excl = false, msg_pattern = false;
     struct { bool on, any; uint32_t roots; } pat_report{false, false, 0u};
@@ -2466,10 +2495,15 @@ class Lowerer {
   // pkg/engine/utils/exceptions.go:14-47). An exception lists (policy key, rule-name globs)
   // and a match block; a matched cell of such a rule whose preconditions held is RuleSkip when
   // the block holds. The device evaluates the block like a rule's match (KpeRule::exc).
-  // Refused (KPE_E_UNSUPPORTED): podSecurity exceptions, conditions that do not fold to true
-  // (MatchesException stops at the first matching exception, so a false one changes which
-  // exception applies), rules whose preconditions read the resource (an erroring precondition
-  // wins over the exception), and several exceptions that are not all `any` blocks.
+  // An exception's conditions (CheckAnyAllConditions, pkg/utils/conditions/condition.go:14-30)
+  // that fold at compile time keep the decision in the scan; conditions that read the resource,
+  // and rules whose preconditions read it (preconditions run first, engine.go:278-293), defer it
+  // (XE_DEFER): the scan marks a cell whose exception match holds (KPE_XDEFER_ | its verdict
+  // without the exception) and kpe_cond_kernel evaluates preconditions, then the exception's
+  // conditions (error or false: no exception), then the handler. Refused (KPE_E_UNSUPPORTED):
+  // several exceptions on a rule when one has conditions that do not fold to true or podSecurity
+  // controls (MatchesException stops at the first matching one, so it decides which applies),
+  // and several exceptions that are not all `any` blocks.
  public:
   void exceptions(const JV& root, bool background, const std::vector<std::string>& rule_pol_key) {
     std::vector<const JV*> xs;
@@ -2481,6 +2515,8 @@ class Lowerer {
       const JV* spec;
       std::string key;
       const JV* pss;  // spec.podSecurity when non-empty (HasPodSecurity)
+      JV cond;        // spec.conditions, an empty `any` dropped (CheckAnyAllConditions: it holds)
+      Fold fold;      // F_TRUE: no conditions, or conditions true for every resource
     };
     std::vector<X> keep;
     for (const JV* e : xs) {
@@ -2499,33 +2535,23 @@ class Lowerer {
         throw CompileError("PolicyException " + key + ": podSecurity is not a list");
       if (pss && (pss->t != JV::Arr || pss->a.empty())) pss = nullptr;
       // CheckAnyAllConditions (pkg/utils/conditions/condition.go:14-30): every `all` holds and
-      // some `any` holds, or `any` is empty
+      // some `any` holds, or `any` is empty. Only true matters (an error or false both mean no
+      // exception, exceptions.go:33-41), and on that the preconditions' evaluation order agrees
+      // (variables/evaluate.go:57-100) once an empty `any` list is dropped.
+      X x{spec, key, pss, JV(), F_TRUE};
       const JV* cond = spec->get("conditions");
       if (cond && cond->t != JV::Null) {
-        bool ok = cond->t == JV::Obj;
-        const JV* all = ok ? cond->get("all") : nullptr;
-        const JV* any = ok ? cond->get("any") : nullptr;
-        if (all && all->t == JV::Arr)
-          for (auto& c : all->a) ok = ok && fold_condition(c) == F_TRUE;
-        else if (all && all->t != JV::Null)
-          ok = false;
-        if (any && any->t == JV::Arr && !any->a.empty()) {
-          bool hit = false;
-          for (auto& c : any->a) {
-            const Fold f = fold_condition(c);
-            if (f == F_NO) ok = false;
-            hit = hit || f == F_TRUE;
-          }
-          ok = ok && hit;
-        } else if (any && any->t != JV::Null && any->t != JV::Arr) {
-          ok = false;
-        }
-        if (!ok) throw CompileError("PolicyException " + key + ": conditions must fold to true at compile time");
+        if (cond->t != JV::Obj) throw CompileError("PolicyException " + key + ": conditions is not an object");
+        x.cond = *cond;
+        JV* any = x.cond.getm("any");
+        if (any && any->t == JV::Arr && any->a.empty()) *any = JV();
+        x.fold = fold_conditions(&x.cond);
       }
-      keep.push_back({spec, key, pss});
+      keep.push_back(std::move(x));
     }
     for (size_t r = 0; r < P.rules.size(); ++r) {
       std::vector<const JV*> mine;  // match blocks of the exceptions that contain this rule
+      std::vector<const X*> mine_x;
       const X* with_pss = nullptr;
       for (auto& x : keep) {
         bool has = false;
@@ -2536,19 +2562,25 @@ class Lowerer {
             for (auto& rn : svl(it.get("ruleNames")))
               if (glob_host(rn, rule_info_[r].name)) has = true;
           }
-        if (has) mine.push_back(x.spec->get("match"));
+        if (has) mine.push_back(x.spec->get("match")), mine_x.push_back(&x);
         if (has && x.pss) with_pss = &x;
       }
       if (mine.empty()) continue;
       const std::string rname = rule_names_at(r);
+      bool dyn_cond = false;
+      for (const X* x : mine_x) dyn_cond = dyn_cond || x->fold == F_NO;
+      if (mine.size() > 1)
+        for (const X* x : mine_x)
+          if (x->fold != F_TRUE)
+            throw CompileError("rule '" + rname + "': several PolicyExceptions, one with conditions (" + x->key + ")");
+      if (mine_x[0]->fold == F_FALSE) continue;  // its conditions never hold: the exception never applies
       // validate_pss.go:45-58: on a podSecurity rule an exception with podSecurity controls does
       // not skip; an unparsable level / version (H_ERROR) errors with or without it
       if (with_pss && P.rules[r].handler == H_ERROR) continue;
       const bool xpss = with_pss && P.rules[r].handler == H_PSS;
       if (xpss && mine.size() > 1)  // MatchesException: the first matching one decides
         throw CompileError("rule '" + rname + "': several PolicyExceptions, one with podSecurity controls");
-      if (rule_info_[r].pre_dyn)
-        throw CompileError("rule '" + rname + "': PolicyExceptions on a rule whose preconditions read the resource");
+      const bool defer = rule_info_[r].pre_dyn || dyn_cond;
       if (P.rules[r].handler == H_NONE) {
         if (rule_info_[r].has_validate)
           throw CompileError("rule '" + rname + "': PolicyExceptions on a validate rule without a handler");
@@ -2578,11 +2610,33 @@ class Lowerer {
         }
       }
       const uint32_t nf = (uint32_t)P.filters.size() - f0;
-      static_assert(((XE_PRESENT | XE_ALL | XE_PSS) & (0x1FFu << 20 | 0xFFFFFu)) == 0, "KpeRule::exc fields overlap");
-      if (f0 > 0xFFFFFu || nf > 0x1FFu) throw CompileError("rule '" + rname + "': too many PolicyException filters");
+      static_assert(((XE_PRESENT | XE_ALL | XE_PSS | XE_DEFER) & (0xFFu << 20 | 0xFFFFFu)) == 0,
+                    "KpeRule::exc fields overlap");
+      if (f0 > 0xFFFFFu || nf > 0xFFu) throw CompileError("rule '" + rname + "': too many PolicyException filters");
       if (xpss) {
         x |= XE_PSS;
         pss_exception(*with_pss->pss, (uint32_t)r, P.rules[r].cv_mask, "PolicyException " + with_pss->key);
+      }
+      if (defer) {  // kpe_cond_kernel decides: the rule's condition record carries the exception
+        x |= XE_DEFER;
+        uint32_t xb = CE_NONE;
+        if (dyn_cond) {
+          try {
+            xb = CC.block(&mine_x[0]->cond);
+          } catch (const CompileError& e) {
+            throw CompileError("PolicyException " + mine_x[0]->key + ": conditions: " + e.what());
+          }
+        }
+        KpeCRule* cr = nullptr;
+        for (auto& c : P.cond.rules)
+          if (c.col == (uint32_t)r) cr = &c;
+        if (!cr) {
+          P.cond.rules.push_back(KpeCRule{(uint32_t)r, CE_NONE, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0, CE_NONE, 0});
+          cr = &P.cond.rules.back();
+        }
+        cr->exc = xb;
+        cr->xflags = XC_DEFER | (xpss ? XC_PSS : 0u);
+        P.any_const = true;
       }
       P.rules[r].exc = x | f0 | nf << 20;
       P.any_exc = true;

@@ -3,6 +3,7 @@
 // device evaluates over the corpus dictionaries.
 #pragma once
 #include <memory>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -129,6 +130,7 @@ struct Program {
   PssxProgram pssx;  // podSecurity.exclude
   int32_t pssx_preds[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // PSA predicates of kpe_pssx_kernel
   DeviceProgram* devs[16] = {};  // per device ordinal: the program's tables on that device (kpe_api.cpp)
+  std::mutex dev_mu;  // first-time creation of a devs[] slot (two device handles may share an ordinal)
   ~Program();
 };
 

@@ -1,8 +1,8 @@
 // The PSA library's fixed value sets (pod-security-admission v0.29 policy/check_*.go, restated in
 // oracle/pss.hpp): shared by the compiler (program.cpp pss_preds: dictionary predicates the scan
-// kernels read) and the flattener's per-pod summary column (flatten.cpp build_pod_summary). None
-// of them depends on a policy: a podSecurity rule only picks the level / version (which checks
-// run) and its exclusions.
+// kernels read) and the device's per-pod summary (kpe_api.cpp psa_fixed_table -> lean.inl
+// kpe_psa_dict_kernel). None of them depends on a policy: a podSecurity rule only picks the
+// level / version (which checks run) and its exclusions.
 #pragma once
 #include <string>
 #include <vector>

@@ -201,7 +201,7 @@ enum KpeDomain {
 #define PSS_ALLOWED_VOLUMES                                                                                     \
   ((1u << VS_CONFIGMAP) | (1u << VS_CSI) | (1u << VS_DOWNWARDAPI) | (1u << VS_EMPTYDIR) | (1u << VS_EPHEMERAL) | \
    (1u << VS_PVC) | (1u << VS_PROJECTED) | (1u << VS_SECRET))
-// Per-pod PSA summary (Corpus::psum, 2 words per row; flatten.cpp rebuild_summary): x = OR of
+// Per-pod PSA summary (2 words per row, built on the device: lean.inl kpe_psum_kernel): x = OR of
 // the container state bitmaps (CX_*), y = the OR-ed list codes under the PSA library's fixed
 // sets: capability-set bits (CS_* of kernels.hip) | volume codes << 3 (bit 0 hostPath, bit 1 a
 // source outside PSS_ALLOWED_VOLUMES) | sysctl codes << 5 (bit v: a sysctl outside version v's
@@ -299,6 +299,8 @@ enum KpeCheckVersion {
                           // condition list longer than CV_LIST_CAP): the caller evaluates it
 #define KPE_XFAIL_ 8  // device-internal: a failing podSecurity cell whose PolicyException has
                       // podSecurity controls (validate_pss.go:88-104), resolved by kpe_pssx_kernel
+#define KPE_XDEFER_ 0x10  // device-internal flag (XE_DEFER rules): the exception's match block
+                          // held; kpe_cond_kernel applies the exception after the preconditions
 
 // ---- policy program ------------------------------------------------------------------------------
 // Rule handlers
@@ -393,8 +395,11 @@ typedef struct KpeRule {
 #define XE_ALL (1u << 30)
 #define XE_PSS (1u << 29)  // the rule's (single) exception has podSecurity controls: a failing PSS
                            // cell becomes KPE_XFAIL_ instead of RuleSkip (ApplyPodSecurityExclusion)
+#define XE_DEFER (1u << 28)  // kpe_cond_kernel decides (the exception's conditions or the rule's
+                             // preconditions read the resource): a cell whose block holds is
+                             // written as KPE_XDEFER_ | its verdict without the exception
 #define XE_F0(x) ((x) & 0xFFFFFu)
-#define XE_NF(x) (((x) >> 20) & 0x1FFu)  // bits 20..28 (XE_PSS is bit 29)
+#define XE_NF(x) (((x) >> 20) & 0xFFu)  // bits 20..27
 
 // ---- podSecurity.exclude (pkg/pss/evaluate.go:72-317), evaluated by kpe_pssx_kernel ----------
 // A PSA field error is keyed by its field path with digit runs replaced by "*": a suffix
@@ -651,6 +656,9 @@ typedef struct KpeSite {
 #define QO_ITEM 10u
 #define QO_ERROR 11u  // the expression is empty: every evaluation is an error (RuleError)
 #define QO_VALS 13u   // `.*`: the member values of an object, then projected like `[*]`
+#define QO_LEN 14u    // length() of the current value (functions.go jpfLength): a projection's
+                      // items, a string's runes, an array's items, an object's members; other
+                      // types an invalid-type error
 #define QO_IMG 12u    // images: the resource's images context map (context.go:306-348), absent
                       // when the resource has no images
 #define QO_OP(x) ((x) & 0xFFu)
@@ -723,4 +731,12 @@ typedef struct KpeCRule {
   uint32_t fe0, nfe;
   uint32_t pv0, npv;  // pattern rules with variables: slots [pv0, pv0 + npv) resolved after the
                       // preconditions (validate_resource.go:456-476 substitutePatterns)
+  uint32_t exc;       // XC_DEFER: the exception's conditions (block; CE_NONE: none, it holds)
+  uint32_t xflags;    // XC_*
 } KpeCRule;
+// KpeCRule::xflags: the rule's PolicyException is applied here (XE_DEFER), after the
+// preconditions: in a cell flagged KPE_XDEFER_ its conditions holding make the cell RuleSkip
+// (validate_resource.go:43-56) or, with podSecurity controls (XC_PSS), a failing cell KPE_XFAIL_
+// (validate_pss.go:45-104); false or an error: no exception (exceptions.go:33-41)
+#define XC_DEFER 1u
+#define XC_PSS 2u

@@ -186,6 +186,15 @@ class Corpus:
         self.device = dev
         return self
 
+    def psa_summary(self) -> np.ndarray:
+        """The per-pod PSA summary built on the corpus's device (kpe_corpus_psa_summary):
+        n x 2 uint32 (schema.h PS_*)."""
+        if self.device is None:
+            raise KpeError(5, "corpus not uploaded")  # KPE_E_STATE
+        out = np.zeros((self.n, 2), dtype=np.uint32)
+        check(load().kpe_corpus_psa_summary(self.device.h, self.h, out.ctypes.data))
+        return out
+
     def __del__(self):
         try:
             if self.h:

@@ -98,32 +98,63 @@ int oracle_pss_failing_checks(const char* level, const char* version, const char
 
 // Failing versioned checks of one pod as a bit mask, bit = flat index of (check, version) in
 // default_checks() order (the kpe_fetch_cv_masks layout); evaluate.go:24-70 without exclusions.
+static long long failing_cv_mask(const Pod& pod, const std::string& lvl, const Version& v) {
+  const Level L = lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged);
+  long long m = 0;
+  int flat = 0;
+  for (auto& check : default_checks()) {
+    const int base = flat;
+    flat += (int)check.versions.size();
+    if (L == Level::Baseline && check.level != L) continue;
+    size_t latest = 0;
+    for (size_t i = 1; i < check.versions.size(); ++i)
+      if (!check.versions[i].min.older(check.versions[latest].min)) latest = i;
+    for (size_t i = 0; i < check.versions.size(); ++i) {
+      const bool run = v.latest ? i == latest : !v.older(check.versions[i].min);
+      if (run && !check.versions[i].fn(pod.meta, pod.spec).allowed) m |= 1ll << (base + (int)i);
+    }
+  }
+  return m;
+}
 long long oracle_pss_failing_cv(const char* level, const char* version, const char* pod_json) {
   try {
     JPtr podj = parse_json(pod_json);
     Pod pod = get_spec(*podj, "Pod");
     Version v;
     if (!parse_version(version, &v)) return -1;
-    std::string lvl = level;
-    const Level L = lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged);
-    long long m = 0;
-    int flat = 0;
-    for (auto& check : default_checks()) {
-      const int base = flat;
-      flat += (int)check.versions.size();
-      if (L == Level::Baseline && check.level != L) continue;
-      size_t latest = 0;
-      for (size_t i = 1; i < check.versions.size(); ++i)
-        if (!check.versions[i].min.older(check.versions[latest].min)) latest = i;
-      for (size_t i = 0; i < check.versions.size(); ++i) {
-        const bool run = v.latest ? i == latest : !v.older(check.versions[i].min);
-        if (run && !check.versions[i].fn(pod.meta, pod.spec).allowed) m |= 1ll << (base + (int)i);
-      }
-    }
-    return m;
+    return failing_cv_mask(pod, level, v);
   } catch (...) {
     return -1;
   }
+}
+// The same for every row of an NDJSON batch, each decoded by its own kind (getSpec,
+// validate_pss.go:137-188: a controller's pod template, a CronJob's job template); -1 for a row
+// getSpec rejects. out: N entries. Returns N or -1.
+long oracle_pss_failing_cv_batch(const char* level, const char* version, const char* ndjson, size_t len, long long* out,
+                                 size_t out_cap, int nthreads) {
+  Version v;
+  if (!parse_version(version, &v)) return -1;
+  auto lines = split_lines(ndjson, len);
+  const size_t N = lines.size();
+  if (N > out_cap) return -1;
+  const std::string lvl = level;
+  std::atomic<size_t> next{0};
+  auto work = [&]() {
+    for (size_t i; (i = next.fetch_add(1)) < N;) {
+      try {
+        JPtr res = parse_json(std::string(lines[i].first, lines[i].second));
+        Unstructured u{res.get()};
+        out[i] = failing_cv_mask(get_spec(*res, u.kind()), lvl, v);
+      } catch (...) {
+        out[i] = -1;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < nthreads; ++t) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+  return (long)N;
 }
 
 // RuleResponse message of a podSecurity rule without exclusions for one resource

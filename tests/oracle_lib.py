@@ -22,6 +22,9 @@ class Oracle:
         L.oracle_pss_failing_checks.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                                 ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_pss_failing_cv.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p]
+        L.oracle_pss_failing_cv_batch.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t,
+                                                  ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        L.oracle_pss_failing_cv_batch.restype = ctypes.c_long
         L.oracle_pss_failing_cv.restype = ctypes.c_longlong
         L.oracle_pss_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                           ctypes.c_char_p, ctypes.c_size_t]
@@ -65,6 +68,17 @@ class Oracle:
         """Failing versioned checks (bit = CV index) of a pod, no exclusions; None on error."""
         r = self.lib.oracle_pss_failing_cv(level.encode(), version.encode(), json.dumps(pod).encode())
         return None if r < 0 else int(r)
+
+    def failing_cv_batch(self, level, version, ndjson: bytes, nthreads=8):
+        """failing_cv for every NDJSON row, each decoded by its own kind (getSpec); -1 where
+        getSpec rejects the row. int64 array of N."""
+        n = ndjson.count(b"\n") + 2
+        out = np.zeros(n, dtype=np.int64)
+        r = self.lib.oracle_pss_failing_cv_batch(level.encode(), version.encode(), ndjson, len(ndjson),
+                                                 out.ctypes.data, n, nthreads)
+        if r < 0:
+            raise RuntimeError("oracle_pss_failing_cv_batch failed")
+        return out[:r]
 
     def pss_message(self, rule, level, version, resource):
         """RuleResponse message of a podSecurity rule without exclusions (None on error)."""

@@ -313,6 +313,14 @@ def cond_policy_set():
             "list": obj + ".spec.missing[]",
             "deny": {"conditions": {"all": [c("{{ element }}", "Equals", "x")]}}}]}),
         rule("spec-ctrs-count", deny(c(spec_ctrs, "Equals", []))),
+        # length() (go-jmespath functions.go jpfLength) as a function and after a pipe
+        rule("len-pipe", deny(c("{{ " + obj + ".spec.containers[] | length(@) }}", "GreaterThan", "2"))),
+        rule("len-name", deny(c("{{ length(" + obj + ".metadata.name) }}", "LessThanOrEquals", 5))),
+        rule("len-labels", deny(c("{{ length(" + obj + ".metadata.labels) }}", "Equals", 2))),
+        rule("len-missing", deny(c("{{ length(" + obj + ".spec.nothing) }}", "Equals", 0))),  # null => error
+        rule("len-vols", deny(c("{{ length(" + obj + ".spec.volumes[]) }}", "AnyIn", ["1", "3"]))),
+        rule("len-proj", deny(c("{{ " + obj + ".spec.containers[*].ports[] | length(@) }}", "GreaterThanOrEquals",
+                                1))),
     ]
     return [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "cond"},
              "spec": {"background": True, "validationFailureAction": "Audit", "rules": rules}}]
@@ -345,6 +353,8 @@ def var_policy_set():
         rule("v-pre", {"pattern": {"spec": {"containers": [{"name": "{{request.object.spec.containers[0].name}}"}]}}},
              pre={"all": [{"key": "{{request.object.metadata.labels.tier}}", "operator": "Equals", "value": "backend"}]}),
         rule("v-map", {"pattern": {"spec": {"securityContext": "{{request.object.spec.securityContext}}"}}}),
+        rule("v-len", {"pattern": {"spec": {"containers": [{"ports": [{"containerPort": "{{ length(request.object.spec.containers) }}"}]}]}}}),
+        rule("v-len-pipe", {"pattern": {"metadata": {"labels": "{{ request.object.metadata.labels | length(@) }}"}}}),
         # foreach entries
         rule("fe-pat", {"foreach": [{"list": ctr, "pattern": {"securityContext": {"=(privileged)": False}}}]}),
         rule("fe-pat-var", {"foreach": [{"list": ctr, "pattern": {"name": "c-{{elementIndex}}"}}]}),

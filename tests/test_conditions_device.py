@@ -46,7 +46,9 @@ def test_condition_set_compiles(oracle):
     {"key": "{{ request.userInfo.username }}", "operator": "AnyIn", "value": ["x"]},          # context value
     {"key": "{{ request.object.spec.containers[*].* }}", "operator": "AnyIn", "value": ["x"]},  # nested `.*`
     {"key": "{{ request.object.spec.containers[?name == 'a'] }}", "operator": "Equals", "value": []},  # filter
-    {"key": "{{ length(request.object.spec.containers) }}", "operator": "Equals", "value": 1},  # function
+    {"key": "{{ to_upper(request.object.metadata.name) }}", "operator": "Equals", "value": "A"},  # function
+    {"key": "{{ request.object.spec.containers | [0] }}", "operator": "Equals", "value": "a"},  # pipe
+    {"key": "{{ request.object.spec.containers | length(@) || `0` }}", "operator": "Equals", "value": 1},
     {"key": "$(./name)", "operator": "Equals", "value": "a"},                                  # reference
     {"key": "{{ request.object.metadata }}", "operator": "Equals", "value": {"a": 1}},        # object value
 ])

@@ -35,14 +35,12 @@ def test_oracle_chainsaw_exceptions(oracle):
     n = npss = 0
     for c in _cases():
         v = oracle.validate([c["policy"]], json.dumps(c["resource"]).encode(), exceptions=c["exceptions"])[0]
-        if 7 in v.tolist():  # outside the restatement: conditions reading length() of a field
-            assert c["dir"] == "conditions", c["file"]
-            continue
+        assert 7 not in v.tolist(), c["file"]
         rejected = FAIL in v.tolist()
         assert rejected == (c["expect"] == "rejected"), (c["file"], v.tolist())
         n += 1
         npss += _pss_exc(c)
-    assert n >= 6 and npss >= 4
+    assert n >= 8 and npss >= 4
 
 
 NS_POL = "ns-0001"
@@ -130,6 +128,36 @@ def exception_set():
              conditions={"all": [{"key": "{{ request.operation }}", "operator": "Equals", "value": "CREATE"}]}),
         _exc("dyn-deny-x", [("dyn-deny", ["deny-name", "fe-*"])], _any({"namespaces": ["ns-0*"]})),
     ]
+    # exceptions whose conditions read the resource (CheckAnyAllConditions after the match,
+    # exceptions.go:33-41: error or false => no exception) and rules whose preconditions read it
+    # (preconditions first, engine.go:278-293): kpe_cond_kernel applies them (XE_DEFER)
+    pols += [
+        pss_policy("cond-pss", "baseline", "latest", kinds=("Pod", "Deployment")),
+        _cpol("cond-rules", [
+            _rule("team-label", kinds=("Pod", "ConfigMap", "Deployment")),
+            _rule("deny-many", kinds=("Pod",), validate={"message": "m", "deny": {"conditions": {"any": [
+                {"key": "{{ request.object.spec.containers[] | length(@) }}", "operator": "GreaterThan",
+                 "value": "1"}]}}}),
+            _rule("pre-dyn", kinds=("Pod", "ConfigMap"), pre={"any": [
+                {"key": "{{ request.object.metadata.labels.tier || '' }}", "operator": "NotEquals", "value": ""}]},
+                validate={"message": "m", "pattern": {"metadata": {"labels": {"app": "?*"}}}}),
+            _rule("pre-dyn-deny", kinds=("Pod",), pre={"all": [
+                {"key": "{{ length(request.object.metadata.name) }}", "operator": "GreaterThan", "value": 5}]},
+                validate={"message": "m", "deny": {"conditions": {"any": [
+                    {"key": "{{ request.object.metadata.namespace }}", "operator": "Equals", "value": "ns-00*"}]}}}),
+        ]),
+    ]
+    excs += [
+        _exc("cond-pss-x", [("pol-cond-pss", ["*"])], _any({"kinds": ["Pod", "Deployment"]}), conditions={"any": [
+            {"key": "{{ request.object.metadata.labels.tier || '' }}", "operator": "Equals", "value": "front*"}]}),
+        _exc("cond-team", [("cond-rules", ["team-label", "autogen-team-label"])], _any({"kinds": ["*"]}),
+             conditions={"all": [{"key": "{{ request.object.metadata.name }}", "operator": "Equals", "value": "res-*1"}],
+                         "any": []}),
+        _exc("cond-many", [("cond-rules", ["deny-many"])], None, conditions={"any": [
+            {"key": "{{ request.object.spec.containers[0].image }}", "operator": "Equals", "value": "*:latest"},
+            {"key": "{{ request.object.spec.nope.deeper }}", "operator": "Equals", "value": "x"}]}),
+        _exc("pre-dyn-x", [("cond-rules", ["pre-dyn", "pre-dyn-deny"])], _any({"namespaces": ["ns-0*"]})),
+    ]
     return pols, excs
 
 
@@ -144,12 +172,15 @@ def test_compile_accepts_and_refuses():
         K.PolicySet(pols, [pss, _exc("pss2", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}))])
     cond = _exc("cond", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}), conditions={"any": [
         {"key": "{{ request.object.metadata.labels.color || '' }}", "operator": "Equals", "value": "blue"}]})
-    with pytest.raises(K.KpeError):
-        K.PolicySet(pols, [cond])
+    K.PolicySet(pols, [cond])  # resource-reading conditions: deferred to kpe_cond_kernel
+    with pytest.raises(K.KpeError):  # several exceptions on a rule, one with conditions: the first decides
+        K.PolicySet(pols, [cond, _exc("plain", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}))])
     dyn = _cpol("dyn", [_rule("r", pre={"all": [{"key": "{{ request.object.metadata.name }}", "operator": "Equals",
                                                  "value": "x"}]})])
-    with pytest.raises(K.KpeError):
-        K.PolicySet(pols + [dyn], [_exc("d", [("dyn", ["r"])], _any({"kinds": ["Pod"]}))])
+    K.PolicySet(pols + [dyn], [_exc("d", [("dyn", ["r"])], _any({"kinds": ["Pod"]}))])
+    with pytest.raises(K.KpeError):  # a pipe other than `| length(@)`
+        K.PolicySet(pols, [_exc("p", [("pol-baseline", ["*"])], _any({"kinds": ["Pod"]}), conditions={"any": [
+            {"key": "{{ request.object.spec.containers | [0] }}", "operator": "Equals", "value": "x"}]})])
     # an exception that names no compiled rule changes nothing and compiles
     K.PolicySet(pols, [_exc("none", [("missing", ["*"])], _any({"kinds": ["Pod"]}))])
 
@@ -171,16 +202,12 @@ def test_oracle_exception_set_has_skips(oracle):
 def test_gpu_chainsaw_exceptions(oracle):
     eng = K.Engine(ordinal=0)
     n = 0
-    for c in _cases():
-        try:
-            ps = K.PolicySet([c["policy"]], c["exceptions"])
-        except K.KpeError:
-            assert c["dir"] == "conditions", c["file"]  # documented refusals
-            continue
+    for c in _cases():  # every scenario compiles, conditions included
+        ps = K.PolicySet([c["policy"]], c["exceptions"])
         v, _, _ = eng.evaluate(ps, K.Corpus(json.dumps(c["resource"]).encode()))
         assert (FAIL in v[0].tolist()) == (c["expect"] == "rejected"), (c["file"], v[0].tolist())
         n += 1
-    assert n >= 8
+    assert n == len(_cases()) and n >= 10
 
 
 @pytest.mark.gpu

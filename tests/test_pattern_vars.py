@@ -54,7 +54,7 @@ def test_var_policy_set_compiles(oracle):
     {"metadata": {"labels": {"{{request.object.metadata.name}}": "x"}}},  # a variable in a key
     {"metadata": {"name": "$(./namespace)"}},                              # a reference
     {"metadata": {"name": "{{ @ }}"}},                                     # {{@}}
-    {"metadata": {"name": "{{ length(request.object.metadata.name) }}"}},  # a function
+    {"metadata": {"name": "{{ to_upper(request.object.metadata.name) }}"}},  # a function
 ])
 def test_refused(pattern):
     pol = var_policy_set()[0]
