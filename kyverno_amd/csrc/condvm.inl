@@ -22,7 +22,11 @@
 constexpr int kCvBufs = 6 + KPE_FE_DEPTH;  // key: 0,1 (+2 list template); value: 3,4 (+5); foreach
                                            // lists: 6 + nesting level
 
-constexpr uint32_t VK_NULL = 0, VK_NODE = 1, VK_CONST = 2, VK_LIST = 3, VK_KEY = 4, VK_NUM = 5;
+constexpr uint32_t VK_NULL = 0, VK_NODE = 1, VK_CONST = 2, VK_LIST = 3, VK_KEY = 4, VK_NUM = 5,
+                   VK_TXT = 6;  // a string built by substitution (VT_TMPL) in the lane's LDS text slot p
+#ifndef KPE_TXT_CAP
+#define KPE_TXT_CAP 120  // bytes of one substituted string (key / value slot); longer: undecided
+#endif
 constexpr uint32_t JT_NULL = 0, JT_BOOL = 1, JT_NUM = 2, JT_STR = 3, JT_ARR = 4, JT_OBJ = 5;
 constexpr int CS_OK = 0, CS_NOTFOUND = 1, CS_ERROR = 2, CS_UNDEC = 3;
 constexpr int CB_FALSE = 0, CB_TRUE = 1, CB_ERROR = 2, CB_UNDEC = 3;
@@ -49,6 +53,9 @@ struct CondVM {
   uint32_t elis[KPE_FE_DEPTH];  // elementIndex<n>
   char (*nb)[16];  // 2 x 16 bytes for fmt.Sprint of an elementIndex: LDS on the device, so that
                    // no generic pointer ever reaches the lane's private memory
+  uint8_t* tx;       // 2 x KPE_TXT_CAP bytes of LDS: substituted key / value strings (VK_TXT), or
+                     // null when the program has no partial-string variables
+  uint32_t tlen[2];
 
   // ---- value access ----------------------------------------------------------------------
   __device__ __forceinline__ CV node(uint32_t e) const {  // a tape entry; a null scalar is the null value
@@ -79,7 +86,8 @@ struct CondVM {
                                                                                                             : JT_NUM;
       }
       case VK_LIST: return JT_ARR;
-      case VK_KEY: return JT_STR;
+      case VK_KEY:
+      case VK_TXT: return JT_STR;
       case VK_NUM: return JT_NUM;
       default: return JT_NULL;
     }
@@ -99,6 +107,7 @@ struct CondVM {
   }
   __device__ __forceinline__ SView str(CV v) const {  // a JT_STR value's text
     if (v.k == VK_KEY) return SView{a.key_bytes + a.key_off[v.p], (int)(a.key_off[v.p + 1] - a.key_off[v.p])};
+    if (v.k == VK_TXT) return SView{tx + v.p * KPE_TXT_CAP, (int)tlen[v.p]};
     const uint8_t* t;
     const KpeScalar* s = scalar(v, &t);
     return SView{t + s->text_off, (int)s->text_len};
@@ -153,6 +162,8 @@ struct CondVM {
     }
   }
   __device__ __forceinline__ static bool seq(SView x, SView y) { return x.n == y.n && bytes_eq(x.s, y.s, x.n); }
+  // a string with no scalar record (a member name, a substituted string): no parsed attributes
+  __device__ __forceinline__ static bool raw(CV x) { return x.k == VK_KEY || x.k == VK_TXT; }
   __device__ __forceinline__ static bool wm(SView pat, SView s) { return glob(pat.s, pat.n, s.s, s.n); }
 
   // ---- JMESPath subset ------------------------------------------------------------------
@@ -413,10 +424,79 @@ struct CondVM {
       ei = e.alt;
     }
   }
+  // substituteVariablesIfAny (variables/vars.go:311-389) of a string with variables inside it:
+  // every {{ }} replaced by its value (substituteVarInPattern :403-420: a string as is, anything
+  // else json.Marshal-ed), into the lane's LDS text slot `slot`. Undecided: a substituted text
+  // holding "{{" (vars.go substitutes again), a map / list value, a number whose json.Marshal text
+  // the device does not hold (an exponent, an integer past 2^53), a result past KPE_TXT_CAP.
+  __device__ __forceinline__ int substitute(const KpeVTmpl& t, uint32_t b0, uint32_t b1, uint32_t slot, CV* out) {
+    uint8_t* d = tx + slot * KPE_TXT_CAP;
+    uint32_t len = 0;
+    auto put = [&](const uint8_t* p, uint32_t n) -> bool {
+      if (len + n > (uint32_t)KPE_TXT_CAP) return false;
+      for (uint32_t i = 0; i < n; ++i) d[len + i] = p[i];
+      len += n;
+      return true;
+    };
+    for (uint32_t k = 0; k < t.b; ++k) {
+      const uint2 pc = a.tpieces[t.a + k];
+      if ((pc.x & 1u) == PT_TEXT) {
+        if (!put(a.ctext + pc.y, pc.x >> 1)) return CS_UNDEC;
+        continue;
+      }
+      CV x;
+      const int st = query(pc.y, b0, b1, &x);
+      if (st != CS_OK) return st;
+      switch (type(x)) {
+        case JT_NULL:
+          if (!put(reinterpret_cast<const uint8_t*>("null"), 4u)) return CS_UNDEC;
+          break;
+        case JT_BOOL:
+          if (btrue(x) ? !put(reinterpret_cast<const uint8_t*>("true"), 4u)
+                       : !put(reinterpret_cast<const uint8_t*>("false"), 5u))
+            return CS_UNDEC;
+          break;
+        case JT_STR: {
+          const SView sv = str(x);
+          for (int i = 0; i + 1 < sv.n; ++i)
+            if (sv.s[i] == '{' && sv.s[i + 1] == '{') return CS_UNDEC;
+          if (!put(sv.s, (uint32_t)sv.n)) return CS_UNDEC;
+          break;
+        }
+        case JT_NUM: {
+          if (x.k == VK_NUM) {  // a count / index: its decimal digits
+            uint8_t dg[10];
+            uint32_t n = 0, y = x.p;
+            do dg[9 - n++] = (uint8_t)('0' + y % 10u), y /= 10u;
+            while (y);
+            if (!put(dg + 10 - n, n)) return CS_UNDEC;
+            break;
+          }
+          const uint8_t* tb;
+          const KpeScalar* s = scalar(x, &tb);
+          if (SC_TYPE(s->flags) == SC_T_INT) {  // a float64 in the JSON context: exact below 2^53
+            if (s->ival > (1ll << 53) || s->ival < -(1ll << 53)) return CS_UNDEC;
+            if (!put(tb + s->text_off, s->text_len)) return CS_UNDEC;
+          } else {  // json.Marshal equals the fmt.Sprint text when that has no exponent
+            const uint8_t* sp = tb + s->text_off + s->text_len;
+            for (uint32_t i = 0; i < s->sp_len; ++i)
+              if (sp[i] == 'e') return CS_UNDEC;
+            if (!put(sp, s->sp_len)) return CS_UNDEC;
+          }
+          break;
+        }
+        default: return CS_UNDEC;  // json.Marshal of a map / list
+      }
+    }
+    tlen[slot] = len;
+    *out = cv(VK_TXT, slot);
+    return CS_OK;
+  }
   // A condition key / value after substitution (template `ti`); lists go to buffer bl. One
   // query() call site: a single query is a one-element template walk that returns its value.
   __device__ __forceinline__ int value(uint32_t ti, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
     const KpeVTmpl t = a.tmpls[ti];
+    if (t.kind == VT_TMPL) return substitute(t, b0, b1, b0 == 3u ? 1u : 0u, out);
     const bool arr = t.kind == VT_ARRAY;
     const uint32_t n = arr ? t.b : 1u;
     blen[bl] = 0;
@@ -445,7 +525,7 @@ struct CondVM {
   // number of seconds beside one; -1 when neither side is a duration string
   __device__ __forceinline__ int duration2(CV k, CV v, double* ks, double* vs) const {
     auto dstr = [&](CV x, int64_t* d) -> bool {
-      if (type(x) != JT_STR || x.k == VK_KEY) return false;
+      if (type(x) != JT_STR || raw(x)) return false;
       const uint8_t* t;
       const KpeScalar* s = scalar(x, &t);
       if (!(s->flags & SC_DUR)) return false;
@@ -473,12 +553,22 @@ struct CondVM {
   // number, duration or quantity.
   // (durations and quantities start with [-+.0-9]; strconv.ParseFloat also takes inf / nan)
   __device__ __forceinline__ bool numeric_looking(CV x, bool floats) const {
-    if (x.k != VK_KEY) return false;
+    if (!raw(x)) return false;
     const SView s = str(x);
     if (s.n == 0) return false;
     const uint8_t c = s.s[0];
-    if ((c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.') return true;
-    return floats && (c == 'I' || c == 'i' || c == 'N' || c == 'n');
+    if (!((c >= '0' && c <= '9') || c == '+' || c == '-' || c == '.') &&
+        !(floats && (c == 'I' || c == 'i' || c == 'N' || c == 'n')))
+      return false;
+    // numbers (hex floats, Inf / NaN included), durations (µs) and quantities hold only ASCII
+    // letters and digits, '+', '-', '.', '_' and the bytes of U+00B5: any other byte rules them out
+    for (int i = 1; i < s.n; ++i) {
+      const uint8_t b = s.s[i];
+      if (!((b >= '0' && b <= '9') || (b >= 'a' && b <= 'z') || (b >= 'A' && b <= 'Z') || b == '+' || b == '-' ||
+            b == '.' || b == '_' || b == 0xC2u || b == 0xB5u))
+        return false;
+    }
+    return true;
   }
   // equal.go / notequal.go
   __device__ __forceinline__ int op_equals(CV k, CV v, bool neg) {
@@ -489,7 +579,7 @@ struct CondVM {
       case JT_NUM:
         if (vt == JT_NUM) return (num(v) == num(k)) != neg;
         if (vt == JT_STR) {
-          if (v.k == VK_KEY) return numeric_looking(v, true) ? -1 : neg;
+          if (raw(v)) return numeric_looking(v, true) ? -1 : neg;
           const uint8_t* t;
           const KpeScalar* s = scalar(v, &t);
           if (!(s->flags & SC_PFLOAT)) return neg;
@@ -501,10 +591,10 @@ struct CondVM {
         double ks, vs;
         if (duration2(k, v, &ks, &vs) > 0) return (ks == vs) != neg;
         const uint8_t *tk, *tv;
-        const KpeScalar* sk = k.k == VK_KEY ? nullptr : scalar(k, &tk);
+        const KpeScalar* sk = raw(k) ? nullptr : scalar(k, &tk);
         if (sk && (sk->flags & SC_QTY) && vt == JT_STR) {
           if (neg && str(v).n == 0) return !wm(str(v), str(k));
-          const KpeScalar* sv = v.k == VK_KEY ? nullptr : scalar(v, &tv);
+          const KpeScalar* sv = raw(v) ? nullptr : scalar(v, &tv);
           if (!sv || !(sv->flags & SC_QTY)) return 0;
           const int c = qcmp(sk->flags & SC_QNEG, sk->qexp, sk->qlo, sk->qhi, sv->flags & SC_QNEG, sv->qexp, sv->qlo,
                              sv->qhi);
@@ -616,7 +706,7 @@ struct CondVM {
         return hits ? 0 : (undec ? -1 : 1);  // CO_ALLNOTIN
       }
       // member names carry no attributes (json_list leaves digit / sign starts undecided)
-      if (v.k == VK_KEY && vs.n > 0 && (vs.s[0] == '+' || vs.s[0] == '|')) return -1;
+      if (raw(v) && vs.n > 0 && (vs.s[0] == '+' || vs.s[0] == '|')) return -1;
       const int j = json_list(v, &vc0, &vcn);
       if (j < 0) return -1;
       if (j == 2) return 0;
@@ -769,7 +859,7 @@ struct CondVM {
                      : SView{reinterpret_cast<const uint8_t*>("false"), 5};
         break;
       case JT_STR:
-        if (k.k == VK_KEY) {
+        if (raw(k)) {
           if (numeric_looking(k, true)) return -1;
           t = str(k);
         } else {
@@ -879,7 +969,7 @@ struct CondVM {
     const uint32_t vt = type(v);
     if (vt == JT_NUM) return cmp_by(nop, kf, num(v));
     if (vt != JT_STR) return 0;
-    if (v.k == VK_KEY) return numeric_looking(v, true) ? -1 : 0;
+    if (raw(v)) return numeric_looking(v, true) ? -1 : 0;
     const uint8_t* t;
     const KpeScalar* s = scalar(v, &t);
     int64_t kd;
@@ -1001,10 +1091,10 @@ struct CondVM {
     if (numeric_looking(k, true) || numeric_looking(v, true)) return -1;  // member names: no parsed attributes
     double ks, vs;
     if (duration2(k, v, &ks, &vs) > 0) return cmp_by(nop, ks, vs);
-    if (k.k != VK_KEY) {
+    if (!raw(k)) {
       const uint8_t* tk;
       const KpeScalar* sk = scalar(k, &tk);
-      if ((sk->flags & SC_QTY) && type(v) == JT_STR && v.k != VK_KEY) {
+      if ((sk->flags & SC_QTY) && type(v) == JT_STR && !raw(v)) {
         const uint8_t* tv;
         const KpeScalar* sv = scalar(v, &tv);
         if (sv->flags & SC_QTY)
@@ -1027,7 +1117,7 @@ struct CondVM {
     const uint32_t t = type(x);
     if (t == JT_NUM) return f2dur(num(x), d) ? 1 : 0;
     if (t != JT_STR) return 0;
-    if (x.k == VK_KEY) return numeric_looking(x, false) ? -1 : 0;
+    if (raw(x)) return numeric_looking(x, false) ? -1 : 0;
     const uint8_t* tb;
     const KpeScalar* s = scalar(x, &tb);
     if (!(s->flags & SC_DUR)) return 0;
@@ -1122,7 +1212,7 @@ __device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, u
     *dst = make_uint2(PVK_NULL, 0u);
     return 0u;
   }
-  if (t == JT_ARR || t == JT_OBJ || x.k == VK_KEY || x.k == VK_LIST) return KPE_UNDECIDED_;  // a subtree / key text
+  if (t == JT_ARR || t == JT_OBJ || CondVM::raw(x) || x.k == VK_LIST) return KPE_UNDECIDED_;  // a subtree / key text
   if (x.k == VK_NUM) {
     *dst = make_uint2(PVK_NUM, x.p);
     return 0u;
@@ -1146,10 +1236,10 @@ __device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, u
 }
 
 template <bool FEPAT>
-__device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16]) {
+__device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16], uint8_t* tx) {
   const uint64_t im = a.img_off ? a.img_off[r] : ~0ull;
   CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], im == ~0ull ? kNoNode : (uint32_t)im,
-            {}, {}, -1, {}, {}, nb};
+            {}, {}, -1, {}, {}, nb, tx, {}};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   uint2* pvrow = a.pvals ? a.pvals + (size_t)r * a.nvars : nullptr;
   for (uint32_t i = 0; i < a.ncr; ++i) {

@@ -1143,17 +1143,22 @@ namespace {
 
 // FEPAT: the instance that also holds the pattern VM, for programs with foreach pattern /
 // anyPattern entries (the VM's frame stack and code stay out of the plain instance)
+// Programs with partial-string variables (VT_TMPL) get 2 x KPE_TXT_CAP bytes of dynamic LDS per
+// lane for the substituted key / value strings; the others launch without it.
 template <bool FEPAT>
 __global__ void __launch_bounds__(128) kpe_cond_kernel(const CondArgs* __restrict__ ap) {
   __shared__ char nb[128][2][16];
+  extern __shared__ __attribute__((aligned(16))) uint8_t ctx[];
   const int64_t i = (int64_t)blockIdx.x * 128 + threadIdx.x;
-  if (i < ap->n) cond_eval_row<FEPAT>(*ap, ap->perm ? (int64_t)ap->perm[i] : i, nb[threadIdx.x]);
+  uint8_t* tx = ap->txt ? ctx + threadIdx.x * (2u * KPE_TXT_CAP) : nullptr;
+  if (i < ap->n) cond_eval_row<FEPAT>(*ap, ap->perm ? (int64_t)ap->perm[i] : i, nb[threadIdx.x], tx);
 }
 
-extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s) {
+extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, int txt, hipStream_t s) {
   if (n <= 0) return hipSuccess;
-  if (fepat) hipLaunchKernelGGL(kpe_cond_kernel<true>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
-  else hipLaunchKernelGGL(kpe_cond_kernel<false>, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs);
+  const size_t lds = txt ? 128u * 2u * KPE_TXT_CAP : 0u;
+  if (fepat) hipLaunchKernelGGL(kpe_cond_kernel<true>, dim3((unsigned)((n + 127) / 128)), dim3(128), lds, s, dargs);
+  else hipLaunchKernelGGL(kpe_cond_kernel<false>, dim3((unsigned)((n + 127) / 128)), dim3(128), lds, s, dargs);
   return hipGetLastError();
 }
 

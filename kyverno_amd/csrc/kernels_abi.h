@@ -269,6 +269,8 @@ struct CondArgs {
   const KpePat* pats;
   const uint8_t* pat_bytes;
   const PatArgs* pat;              // the pattern program (foreach pattern / anyPattern entries)
+  const uint2* tpieces;            // VT_TMPL pieces (CondProgram::tpieces)
+  uint32_t txt, pad2_;             // 1: VT_TMPL templates exist (the kernel's LDS text slots)
   const KpePVar* pvars;            // pattern variable slots (query template, use flags)
   uint2* pvals;                    // their per-row values (PatArgs::pvals), or null
   uint32_t nvars, pad_;

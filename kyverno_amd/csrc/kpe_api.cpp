@@ -34,7 +34,7 @@ extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32
 extern "C" hipError_t kpe_launch_sites(const PatArgs* dargs, int64_t n, uint32_t nsites, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
                                                hipStream_t s);
-extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, hipStream_t s);
+extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, int txt, hipStream_t s);
 extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
                                            uint8_t value, hipStream_t s);
 extern "C" hipError_t kpe_launch_prep(const ScanArgs* dargs, int pss, int narrow, size_t dyn_bytes, hipStream_t s);
@@ -172,7 +172,7 @@ struct DeviceProgram {
   DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
   DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
-  DevBuf cops, cexprs, ctmpls, cconds, cblocks, cfes, crules, cconsts, ctext, cclist;
+  DevBuf cops, cexprs, ctmpls, cconds, cblocks, cfes, crules, cconsts, ctext, cclist, ctpieces;
   DevBuf xrules;  // podSecurity rules with exclusions (program.hpp PssxProgram)
   std::vector<uint8_t> pat_bytes_h;
   std::vector<KpePat> pats_h;  // pattern k of predicate p: pats_h[pat0[p] + k]
@@ -617,6 +617,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.cconsts, CP.consts, s0));
     HIPCHK(upload(D.ctext, CP.ctext, s0));
     HIPCHK(upload(D.cclist, CP.clist, s0));
+    HIPCHK(upload(D.ctpieces, CP.tpieces, s0));
     HIPCHK(upload(D.xrules, P.pssx.rules, s0));
   }
   D.ordinal = dev->ordinal;
@@ -1313,6 +1314,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.ctab = PD.cconsts.as<KpeScalar>();
       ca.ctext = PD.ctext.as<uint8_t>();
       ca.clist = PD.cclist.as<uint32_t>();
+      ca.tpieces = PD.ctpieces.as<uint2>();
+      ca.txt = P.cond.tpieces.empty() ? 0u : 1u;
       ca.fkeys = B.cfkeys.as<uint32_t>();
       ca.leaves = PD.pleaves.as<KpeLeaf>();
       ca.pconds = PD.pconds.as<KpeCond>();
@@ -1331,7 +1334,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       HIPCHK(hipStreamSynchronize(s));
       B.cargs_valid = true;
     }
-    HIPCHK(kpe_launch_cond(B.cargs.as<CondArgs>(), C.n, P.any_fe_pat ? 1 : 0, s));
+    HIPCHK(kpe_launch_cond(B.cargs.as<CondArgs>(), C.n, P.any_fe_pat ? 1 : 0, P.cond.tpieces.empty() ? 0 : 1, s));
   }
   if (!P.pssx.rules.empty()) {
     if (!B.xargs_valid || (masks ? B.masks.p : nullptr) != B.xmasks) {

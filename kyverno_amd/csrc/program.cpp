@@ -1571,11 +1571,31 @@ class CondCompiler {
       if (!next_var(v.s, 0, &st, &en)) {
         if (v.s.find("\\{{") != std::string::npos) throw CompileError("escaped variables in conditions");
         t.kind = VT_CONST, t.a = K.scalar(v);
-      } else {
-        if (st != 0 || en != v.s.size()) throw CompileError("partial-string variables in conditions are not supported");
+      } else if (st == 0 && en == v.s.size()) {  // the whole string: the value keeps its JSON type
         const std::string q = var_text(v.s);
         if (q == "@" || q.find("{{") != std::string::npos) throw CompileError("{{@}} / nested variables");
         t.kind = VT_QUERY, t.a = Q.compile(q);
+      } else {  // variables inside a string (vars.go:311-389): text and variable pieces
+        if (depth > 0) throw CompileError("partial-string variables inside a condition list");
+        if (v.s.find("\\{{") != std::string::npos) throw CompileError("escaped variables in conditions");
+        t.kind = VT_TMPL, t.a = (uint32_t)CP.tpieces.size() / 2;
+        auto text = [&](size_t b, size_t e) {
+          if (e <= b) return;
+          CP.tpieces.push_back(PT_TEXT | (uint32_t)(e - b) << 1);
+          CP.tpieces.push_back((uint32_t)CP.ctext.size());
+          CP.ctext.insert(CP.ctext.end(), v.s.begin() + b, v.s.begin() + e);
+        };
+        size_t pos = 0;
+        while (next_var(v.s, pos, &st, &en)) {
+          text(pos, st);
+          const std::string q = var_text(v.s.substr(st, en - st));
+          if (q == "@" || q.find("{{") != std::string::npos) throw CompileError("{{@}} / nested variables");
+          CP.tpieces.push_back(PT_VAR);
+          CP.tpieces.push_back(Q.compile(q));
+          pos = en;
+        }
+        text(pos, v.s.size());
+        t.b = (uint32_t)CP.tpieces.size() / 2 - t.a;
       }
     } else if (v.t == JV::Arr && depth == 0 && has_var(v)) {
       std::vector<uint32_t> el;

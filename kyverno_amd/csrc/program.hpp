@@ -52,6 +52,8 @@ struct CondProgram {
   std::vector<KpeScalar> consts;  // constant table (SC_T_* types, SC_T_ARR lists in clist)
   std::vector<char> ctext;        // constant texts
   std::vector<uint32_t> clist;    // elements of constant lists
+  std::vector<uint32_t> tpieces;  // VT_TMPL pieces, 2 words each: PT_TEXT | len << 1, ctext offset /
+                                  // PT_VAR, expression
   std::vector<std::string> fields;
 };
 // podSecurity rules with exclusions (schema.h KpeXRule / KpeXExcl), evaluated per pod by

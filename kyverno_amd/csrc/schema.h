@@ -674,6 +674,7 @@ typedef struct KpeCExpr {
 #define VT_CONST 0u  // a = constant
 #define VT_QUERY 1u  // a = expression
 #define VT_ARRAY 2u  // a = first element template, b = count (a list with variables inside)
+#define VT_TMPL 3u   // a string with variables inside it: pieces [a, a + b) of CondArgs::tpieces
 typedef struct KpeVTmpl {
   uint32_t kind, a, b, pad;
 } KpeVTmpl;

@@ -84,6 +84,9 @@ int main(int argc, char** argv) {
   a.ops = ops.data(), a.exprs = CP.exprs.data(), a.tmpls = CP.tmpls.data(), a.conds = CP.conds.data();
   a.blocks = CP.blocks.data(), a.fes = CP.fes.data(), a.rules = CP.rules.data();
   a.ctab = CP.consts.data(), a.ctext = ctext.data(), a.clist = CP.clist.data(), a.fkeys = fk.data();
+  std::vector<uint2> ctp(CP.tpieces.size() / 2 + 1);
+  for (size_t i = 0; i + 1 < CP.tpieces.size(); i += 2) ctp[i / 2] = uint2{CP.tpieces[i], CP.tpieces[i + 1]};
+  a.tpieces = ctp.data(), a.txt = CP.tpieces.empty() ? 0u : 1u;
   // pattern program operand records (InRange values of set operators), as kpe_api.cpp binds them
   std::vector<uint8_t> pb;
   std::vector<KpePat> pp;
@@ -146,7 +149,8 @@ int main(int argc, char** argv) {
   pa.ndoc = C.doc.size() / 2, pa.err = &perr;
   a.pat = &pa, a.pvars = PP.vars.data(), a.pvals = pvals.data(), a.nvars = (uint32_t)PP.vars.size();
   char nb[2][16];
-  for (int64_t r = 0; r < a.n; ++r) cond_eval_row<true>(a, r, nb);  // kpe_cond_kernel's lane body
+  std::vector<uint8_t> txt(2 * KPE_TXT_CAP);
+  for (int64_t r = 0; r < a.n; ++r) cond_eval_row<true>(a, r, nb, txt.data());  // kpe_cond_kernel's lane body
   if (!PP.rules.empty())
     for (int64_t r = 0; r < a.n; ++r) pat_eval_row(pa, r, FramesPriv{});  // then kpe_pattern_kernel's
   if (perr) return fprintf(stderr, "pattern VM bounds flags 0x%x\n", perr), 1;

@@ -16,7 +16,7 @@ step() {  # step <name> <timeout> <cmd...>
   return 0
 }
 python3 -c "import bench, json; print(json.dumps(bench.cpu_budget()))" > $O/cpu_budget.json 2>&1
-TAILN=12 step pytest_new 600 python -u -m pytest tests/test_psum.py tests/test_gpu_lean.py tests/test_exceptions.py tests/test_conditions_device.py -m gpu -x -v --timeout 300 --timeout-method thread
+TAILN=12 step pytest_new 600 python -u -m pytest tests/test_psum.py tests/test_gpu_lean.py tests/test_exceptions.py tests/test_conditions_device.py tests/test_pattern_vars.py -m gpu -x -v --timeout 300 --timeout-method thread
 step bench_c2 300 python bench.py --steps 200 --warmup 20
 step bench_c2_k20 300 python bench.py --steps 20 --warmup 5 --cpu-sample 0
 step trace_c2 300 rocprofv3 --kernel-trace --stats -d $O/prof_c2 -o c2 --output-format csv -- python3 bench.py --steps 200 --warmup 20 --cpu-sample 0

@@ -321,6 +321,22 @@ def cond_policy_set():
         rule("len-vols", deny(c("{{ length(" + obj + ".spec.volumes[]) }}", "AnyIn", ["1", "3"]))),
         rule("len-proj", deny(c("{{ " + obj + ".spec.containers[*].ports[] | length(@) }}", "GreaterThanOrEquals",
                                 1))),
+        # variables inside strings (substituteVariablesIfAny, vars.go:311-389): strings as is, other
+        # values json.Marshal-ed
+        rule("tmpl-ns-name", deny(c("{{ " + obj + ".metadata.namespace }}/{{ " + obj + ".metadata.name }}",
+                                    "Equals", "ns-000*/res-1*"))),
+        rule("tmpl-value", deny(c("{{ " + obj + ".metadata.name }}", "NotEquals",
+                                  "res-{{ " + obj + ".metadata.labels.tier || 'x' }}*"))),
+        rule("tmpl-number", deny(c("n={{ " + obj + ".spec.replicas || `1` }}", "AnyIn", ["n=3", "n=1"]))),
+        rule("tmpl-bool-null", deny(c("{{ " + obj + ".spec.hostNetwork || `false` }}:{{ " + obj +
+                                      ".spec.nothing || `null` }}", "Equals", "false:null"))),
+        rule("tmpl-len", deny(c("{{ length(" + obj + ".metadata.name) }}-{{ " + obj + ".kind }}", "In",
+                                ["5-Pod", "6-Pod", "7-Service"]))),
+        rule("tmpl-missing", deny(c("x-{{ " + obj + ".metadata.labels.team }}", "Equals", "x-team-1"))),  # error
+        rule("foreach-tmpl", {"message": "m", "foreach": [{
+            "list": obj + ".spec.containers",
+            "deny": {"conditions": {"any": [c("{{ element.name }}@{{ element.image }}", "Equals", "c-0@*:latest"),
+                                            c("{{ elementIndex }}:{{ element.name }}", "Equals", "1:c-?")]}}}]}),
     ]
     return [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "cond"},
              "spec": {"background": True, "validationFailureAction": "Audit", "rules": rules}}]
