@@ -119,7 +119,7 @@ def test_oracle_in_list_key_semantics(oracle):
 
 
 @pytest.mark.parametrize("cond", [
-    {"all": [{"key": OP, "operator": "Equals", "value": "{{ request.operation }}-x"}]},  # partial variable
+    {"all": [{"key": OP, "operator": "Equals", "value": "$(./x)"}]},  # a $(...) reference
 ])
 def test_unfoldable_refused(cond):
     for pol in (_policy("p", [_rule("r", pre=cond, validate=PATTERN)]),
