@@ -1125,10 +1125,11 @@ namespace {
 __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
   constexpr uint32_t kWaveWords = FramesLds::kWords * FramesLds::kDepth * 64u;
   __shared__ uint32_t s_fs[KPE_PAT_BLOCK / 64][kWaveWords];
+  __shared__ uint8_t s_memo[KPE_PAT_MEMO][KPE_PAT_BLOCK];  // byte-planar: a lane's slot s at [s][lane]
   const int64_t i = (int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x;
   if (i >= ap->n) return;
   const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
-  pat_eval_row(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]});
+  pat_eval_row(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]}, &s_memo[0][threadIdx.x], KPE_PAT_BLOCK);
 }
 
 // ===========================================================================

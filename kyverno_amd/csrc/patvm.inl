@@ -909,8 +909,13 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 // kpe_pattern_kernel's body for resource r: resolve the row's KPE_PENDING_ pattern cells.
 // The pattern roots of every rule run through one VM call site (a plain pattern is one root),
 // so the kernel holds a single copy of the VM: its code stays within the instruction cache.
+// Rules that carry the same pattern share a memo slot (PR_MEMO_SH): the row's first pending cell
+// of the slot is evaluated and the others take its verdict from `memo` (LDS bytes, slot s at
+// memo[s * memo_stride]; null: no memo).
 template <class FS>
-__device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs) {
+__device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs, uint8_t* memo = nullptr,
+                                             uint32_t memo_stride = 0) {
+  uint32_t memo_ok = 0;  // slots holding this row's verdict
   PatVMT<FS> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
                 a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr, r};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
@@ -936,6 +941,11 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs)
       row[c0 + q] = (uint8_t)KPE_PASS_;  // diagnostic: the rule loop without the VM
       continue;
 #endif
+      const uint32_t slot = memo ? a.rules[pi - 1u].flags >> PR_MEMO_SH : PR_NO_MEMO;
+      if (slot < KPE_PAT_MEMO && ((memo_ok >> slot) & 1u)) {
+        row[c0 + q] = memo[slot * memo_stride];
+        continue;
+      }
       uint32_t v = pat_eval_cell(vm, pi - 1u);
       if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
         // a shallow (LDS) stack may have overflowed: the lane-private kPatStack-deep one decides
@@ -944,6 +954,7 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs)
         v = pat_eval_cell(deep, pi - 1u);
       }
       row[c0 + q] = (uint8_t)v;
+      if (slot < KPE_PAT_MEMO) memo[slot * memo_stride] = (uint8_t)v, memo_ok |= 1u << slot;
     }
   }
 }

@@ -2432,6 +2432,13 @@ class Lowerer {
           throw CompileError("rule '" + rname + "': " + e.what());
         }
         crule.npv = (uint32_t)P.pat.vars.size() - crule.pv0;
+        pr.flags |= PR_NO_MEMO << PR_MEMO_SH;
+        if (!crule.npv) {  // equal patterns give equal verdicts on a row: memo candidates
+          std::string sig = std::to_string(pr.flags & 0xFFFFu) + "|";
+          if (present("pattern")) jv_sig(*v->get("pattern"), sig);
+          else jv_sig(*v->get("anyPattern"), sig);
+          pat_sigs_.emplace_back((uint32_t)P.pat.rules.size(), std::move(sig));
+        }
         for (uint32_t k = 0; k < pr.nr; ++k) pc::find_sites(P.pat, P.pat.roots[2 * (pr.r0 + k)], pr.col);
         if (P.pat.rules.size() >= 65535) throw CompileError("more than 65535 pattern rules in one program");
         P.pat.rules.push_back(pr);
@@ -2663,7 +2670,49 @@ class Lowerer {
     }
   }
   std::string rule_names_at(size_t r) const { return P.rule_names[r]; }
+  // memo slots of the pattern rules (KpePatRule::flags >> PR_MEMO_SH): patterns shared by several
+  // rules, the most shared first, KPE_PAT_MEMO of them
+  void assign_pattern_memo() {
+    std::map<std::string, std::vector<uint32_t>> by;
+    for (auto& x : pat_sigs_) by[x.second].push_back(x.first);
+    std::vector<const std::vector<uint32_t>*> groups;
+    for (auto& kv : by)
+      if (kv.second.size() > 1) groups.push_back(&kv.second);
+    std::stable_sort(groups.begin(), groups.end(), [](auto* x, auto* y) { return x->size() > y->size(); });
+    for (size_t g = 0; g < groups.size() && g < KPE_PAT_MEMO; ++g)
+      for (uint32_t pi : *groups[g])
+        P.pat.rules[pi].flags = (P.pat.rules[pi].flags & 0xFFFFu) | ((uint32_t)g << PR_MEMO_SH);
+  }
  private:
+  // type-tagged canonical text of a pattern value (members in document order, as compiled)
+  static void jv_sig(const JV& v, std::string& o) {
+    switch (v.t) {
+      case JV::Null: o += 'n'; break;
+      case JV::Bool: o += v.b ? 't' : 'f'; break;
+      case JV::Num:
+        o += v.is_int ? 'i' : 'd';
+        o += v.is_int ? std::to_string(v.i) : goval::fmt_E(v.n);
+        o += ';';
+        break;
+      case JV::Str:
+        o += 's' + std::to_string(v.s.size()) + ':' + v.s;
+        break;
+      case JV::Arr:
+        o += '[';
+        for (auto& x : v.a) jv_sig(x, o);
+        o += ']';
+        break;
+      case JV::Obj:
+        o += '{';
+        for (auto& kv : v.o) {
+          o += std::to_string(kv.first.size()) + ':' + kv.first;
+          jv_sig(kv.second, o);
+        }
+        o += '}';
+        break;
+    }
+  }
+  std::vector<std::pair<uint32_t, std::string>> pat_sigs_;
 
   Program& P;
   cq::CondCompiler CC;
@@ -2726,6 +2775,7 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len, const ch
     for (auto& rr : prog->reports) keys.push_back(rr.policy_key);
     L.exceptions(parse_all(exceptions, exc_len), background, keys);
   }
+  L.assign_pattern_memo();
   return prog;
 }
 

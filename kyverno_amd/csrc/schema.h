@@ -610,6 +610,13 @@ typedef struct KpeCond {
 // Pattern rule: roots [r0, r0 + nr) of the root table (uint2: node, anchor slots)
 #define PR_ANY 1u        // anyPattern
 #define PR_ANY_BAD 2u    // anyPattern that is not a list: RuleStatusError
+// KpePatRule::flags >> PR_MEMO_SH: the rule's memo slot (< KPE_PAT_MEMO) when other pattern rules of
+// the program carry the same pattern (equal JSON, no variables): a row evaluates it once and
+// every rule of the slot takes that verdict (the pattern verdict depends on the row alone);
+// PR_NO_MEMO: none
+#define PR_MEMO_SH 16
+#define PR_NO_MEMO 0xFFFFu
+#define KPE_PAT_MEMO 32
 typedef struct KpePatRule {
   uint32_t col, flags, r0, nr;
 } KpePatRule;

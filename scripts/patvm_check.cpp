@@ -135,12 +135,13 @@ int main(int argc, char** argv) {
     std::vector<uint32_t> plane(FramesLds::kWords * FramesLds::kDepth * 64u, 0xDEADBEEFu);
     uint8_t* keep = a.verdicts;
     a.verdicts = lds_v.data();
-    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesLds{plane.data()});
+    std::vector<uint8_t> memo(KPE_PAT_MEMO, 0xEE);  // with the shared-pattern memo (the private walk below has none)
+    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesLds{plane.data()}, memo.data(), 1u);
     a.verdicts = keep;
   }
   // ... and the lane-private stack
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
-  if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk differs from the private-stack walk\n"), 1;
+  if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk (with memo) differs from the private-stack walk\n"), 1;
   // array sites (kpe_site_kernel's results, folded element by element here) must not change a cell
   if (!PP.sites.empty()) {
     std::vector<uint4> sres(PP.sites.size() * (size_t)C.n, uint4{0u, 0u, 0u, 0u});

@@ -35,6 +35,10 @@ def _sets():
            ("chart-mix2", pattern_only(chart_pattern_policies()), K.synth_resources(22, 1500, mix=2))]
     pols, nd = edge_case_inputs(1500)
     out.append(("edge", pols, nd))
+    # C3's 200 policies share a handful of patterns: the memo slots (PR_MEMO_SH) carry verdicts
+    from tests.policies import c3_policy_set
+    c3p = [q for q in c3_policy_set(60) if "pattern" in q["spec"]["rules"][0]["validate"]]
+    out.append(("c3-memo", c3p, K.synth_resources(0xC3, 1500, mix=5)))
     cases = [c for c in PTREE if isinstance(json.loads(c["resource"]), dict)]
     pols = pattern_only(device_policies([_policy_for(f"t{i}", json.loads(c["pattern"])) for i, c in enumerate(cases)]))
     out.append(("validate_test.go", pols, "\n".join(json.dumps(json.loads(c["resource"])) for c in cases).encode()))
