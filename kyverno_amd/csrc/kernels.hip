@@ -1203,117 +1203,6 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
   return hipGetLastError();
 }
 
-// Array sites (schema.h KpeSite): 64-row tiles per wave, every site in turn. A wave resolves a site's
-// member chain for its 64 rows (rows whose cell of the site's rule is still pending), takes a
-// wave prefix sum of their arrays' element counts and then validates the elements of all 64 rows
-// one lane per element, 64 at a time (the element map inline, patvm.inl flat_map); each chunk's
-// results go through LDS to the lanes of their rows, which fold them in order
-// (validateArrayOfMaps). A row's array of n elements thus costs ~n/64 of a wave's element pass
-// instead of n sequential walks of one lane, and the pattern kernel then takes the row's result
-// at the array node instead of walking the elements.
-#ifndef KPE_SITE_MINW
-#define KPE_SITE_MINW 3  // grouped pass, C5 / C3: 2 waves/SIMD 9.6 / 1.43 ms, 3 8.1 / 1.28, 4 8.9 / 1.28 (r03_g_sitegroups)
-#endif
-// packed SiteFold of one (site, row): applied | skips << 8 | verdict << 16 (PE_NONE: open) |
-// und << 20 | none << 21, plus the AnchorMap words
-__device__ __forceinline__ void sfold_add(uint32_t& st, uint32_t& rg, uint32_t& vl, const uint4 x) {
-  if (((st >> 16) & 0xFu) != PE_NONE || (st >> 21) & 1u) return;  // decided
-  const uint32_t c = x.x & 0xFFu;
-  if (c == PE_NONE) {
-    st |= 1u << 21;
-    return;
-  }
-  st |= (x.x & 0x100u) << 12, rg |= x.y, vl |= x.z;
-  if (c == PE_SKIP) st += 1u << 8;
-  else if (c != PE_OK) st = (st & ~(0xFu << 16)) | (c << 16);
-  else st += 1u;
-}
-__device__ __forceinline__ uint4 sfold_result(uint32_t st, uint32_t rg, uint32_t vl, uint32_t arr) {
-  if ((st >> 21) & 1u) return uint4{0u, 0u, 0u, 0u};
-  uint32_t v = (st >> 16) & 0xFu;
-  if (v == PE_NONE) v = ((st & 0xFFu) == 0u && ((st >> 8) & 0xFFu) > 0u) ? PE_SKIP : PE_OK;
-  return uint4{v | (((st >> 20) & 1u) << 8) | KPE_SR_VALID, rg, vl, arr};
-}
-
-__global__ void __launch_bounds__(256, KPE_SITE_MINW) kpe_site_kernel(const PatArgs* __restrict__ ap) {
-  __shared__ uint32_t s_off[4][65];
-  __shared__ uint32_t s_arr[4][64];
-  __shared__ uint32_t s_pm[4][64];
-  __shared__ uint4 s_res[4][8][64];
-  const PatArgs& a = *ap;
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const int64_t row = ((int64_t)blockIdx.x * 4 + wv) * 64 + lane;
-  const bool live = row < a.n;
-  const DocView doc = PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc);
-  // site groups in turn (sites whose chains name the same keys): the chain is resolved once and
-  // an element is validated for every pending site of the group back to back, so all but the
-  // first read its body from L1; a row's lists stay in L1 / L2 from one group to the next
-  for (uint32_t grp = 0; grp < a.ngroups; ++grp) {
-    const uint2 G = sld(a.site_groups, grp);
-    uint32_t pm = 0;  // sites of the group whose cell of this row is pending
-    for (uint32_t i = 0; i < G.y; ++i) {
-      const KpeSite S = sld(a.sites, sld(a.group_sites, G.x + i));
-      if (live && a.verdicts[(size_t)row * a.R + S.col] == KPE_PENDING_) pm |= 1u << i;
-    }
-    if (__ballot(pm != 0u) == 0ull) continue;
-    const KpeSite S0 = sld(a.sites, sld(a.group_sites, G.x));
-    uint32_t arr = kNoNode, cnt = 0;
-    if (pm) {
-      arr = site_array(a, doc, S0, row);
-      if (arr != kNoNode) cnt = doc[doc[arr].y].x;
-    }
-    const uint32_t incl = wave_incl_scan(cnt), excl = incl - cnt;
-    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
-    __builtin_amdgcn_wave_barrier();  // the previous group's readers of the LDS rows are done
-    s_off[wv][lane] = excl;
-    s_arr[wv][lane] = arr;
-    s_pm[wv][lane] = pm;
-    if (lane == 63u) s_off[wv][64] = total;
-    __builtin_amdgcn_wave_barrier();
-    uint32_t st[8], rg[8], vl[8];
-#pragma unroll
-    for (uint32_t i = 0; i < 8u; ++i) st[i] = PE_NONE << 16, rg[i] = 0u, vl[i] = 0u;
-    for (uint32_t g0 = 0; g0 < total; g0 += 64u) {
-      const uint32_t g = g0 + lane;
-      uint32_t o = 0, e = 0, opm = 0;
-      if (g < total) {
-#pragma unroll
-        for (uint32_t step = 32u; step; step >>= 1)  // the row lane whose [offset, offset + count) holds g
-          if (s_off[wv][o + step] <= g) o += step;
-        e = doc[s_arr[wv][o]].y + 1u + (g - s_off[wv][o]);
-        opm = s_pm[wv][o];
-      }
-      for (uint32_t i = 0; i < G.y; ++i) {
-        uint4 r{0u, 0u, 0u, 0u};
-        if ((opm >> i) & 1u) r = site_elem(a, doc, sld(a.sites, sld(a.group_sites, G.x + i)), row - lane + o, e);
-        s_res[wv][i][lane] = r;
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (cnt) {  // this row's elements within the chunk, in order, for each of its pending sites
-        const uint32_t lo = excl > g0 ? excl : g0, hi = incl < g0 + 64u ? incl : g0 + 64u;
-#pragma unroll
-        for (uint32_t i = 0; i < 8u; ++i)
-          if ((pm >> i) & 1u)
-            for (uint32_t q = lo; q < hi; ++q) sfold_add(st[i], rg[i], vl[i], s_res[wv][i][q - g0]);
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < 8u; ++i)
-      if ((pm >> i) & 1u) {
-        const uint32_t site = sld(a.group_sites, G.x + i);
-        a.site_res[(size_t)site * (size_t)a.n + (size_t)row] =
-            arr != kNoNode ? sfold_result(st[i], rg[i], vl[i], arr) : uint4{0u, 0u, 0u, 0u};
-      }
-  }
-}
-
-extern "C" hipError_t kpe_launch_sites(const PatArgs* dargs, int64_t n, uint32_t nsites, hipStream_t s) {
-  if (n <= 0 || !nsites) return hipSuccess;
-  hipLaunchKernelGGL(kpe_site_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dargs);
-  return hipGetLastError();
-}
-
 // Failing paths of listed pattern cells (kpe_pattern_traces): one lane per cell (row * R + col)
 // walks each root of the cell's rule (at most KPE_TRACE_ROOTS) from the tape in HBM with the
 // VM's TRACE instance, which records the path of the last failure (PatternError.Path). Report

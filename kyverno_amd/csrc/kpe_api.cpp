@@ -31,7 +31,6 @@ bool is_limit_error(const std::exception& e);
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
-extern "C" hipError_t kpe_launch_sites(const PatArgs* dargs, int64_t n, uint32_t nsites, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
                                                hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, int txt, hipStream_t s);
@@ -118,12 +117,12 @@ constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated 
 // launch's prologue overlaps another's tail. Setup (uploads, binds) and timed launches
 // use stream 0.
 constexpr int kMaxLanes = 4;
-// Array sites (kpe_site_kernel) are opt-in (KPE_SITES=1): they shorten the pattern walks (C5 13.0
-// -> 5.5 ms) but the per-site element pass measured slower than what it saves (C5 11.3 ms, C3
-// 2.3 ms against 4.8 ms of walking saved; profiles/r03_f_sites)
+// Array sites (schema.h KpeSite): validated in the pattern kernel's per-row site pass
+// (patvm.inl pat_sites_row) before the rule walks; KPE_NO_SITES=1 walks every array per rule
+// (A/B measurement)
 static bool sites_on() {
-  const char* e = getenv("KPE_SITES");
-  return e && *e == '1';
+  static const bool off = getenv("KPE_NO_SITES") != nullptr;
+  return !off;
 }
 
 struct kpe_device {
@@ -1390,8 +1389,6 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
-    if (!P.pat.sites.empty() && sites_on())  // array elements one lane each, before the walks
-      HIPCHK(kpe_launch_sites(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.sites.size(), s));
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
     if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;

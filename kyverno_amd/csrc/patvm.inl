@@ -912,10 +912,13 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 // Rules that carry the same pattern share a memo slot (PR_MEMO_SH): the row's first pending cell
 // of the slot is evaluated and the others take its verdict from `memo` (LDS bytes, slot s at
 // memo[s * memo_stride]; null: no memo).
+__device__ __forceinline__ void pat_sites_row(const PatArgs& a, DocView doc, int64_t r, const uint8_t* row);
 template <class FS>
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs, uint8_t* memo = nullptr,
                                              uint32_t memo_stride = 0) {
   uint32_t memo_ok = 0;  // slots holding this row's verdict
+  if (a.ngroups) pat_sites_row(a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), r,
+                               a.verdicts + (size_t)r * a.R);
   PatVMT<FS> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
                 a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr, r};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
@@ -980,6 +983,71 @@ __device__ __forceinline__ uint4 site_elem(const PatArgs& a, DocView doc, const 
   const uint2 x = doc[PVD(e)];
   const uint32_t v = DN_KIND(x.x) != DN_MAP ? PE_OTHER : vm.template flat_map<PNF_MAXDEPTH>(x.y, PU(a.nodes, S.elem, a.nnodes, 1));
   return uint4{v | (vm.und << 8), vm.reg, vm.val, 0u};
+}
+// validateArrayOfMaps' fold (validate.go:224-261), packed in one word per site: applied | skips << 8
+// | verdict << 16 (PE_NONE: open) | und << 20 | none << 21 (a body past the inline limit: the VM
+// walks the array itself), plus the AnchorMap words
+__device__ __forceinline__ void sfold_add(uint32_t& st, uint32_t& rg, uint32_t& vl, const uint4 x) {
+  if (((st >> 16) & 0xFu) != PE_NONE || (st >> 21) & 1u) return;  // decided
+  const uint32_t c = x.x & 0xFFu;
+  if (c == PE_NONE) {
+    st |= 1u << 21;
+    return;
+  }
+  st |= (x.x & 0x100u) << 12, rg |= x.y, vl |= x.z;
+  if (c == PE_SKIP) st += 1u << 8;
+  else if (c != PE_OK) st = (st & ~(0xFu << 16)) | (c << 16);
+  else st += 1u;
+}
+__device__ __forceinline__ bool sfold_done(uint32_t st) { return ((st >> 16) & 0xFu) != PE_NONE || ((st >> 21) & 1u); }
+__device__ __forceinline__ uint4 sfold_result(uint32_t st, uint32_t rg, uint32_t vl, uint32_t arr) {
+  if ((st >> 21) & 1u) return uint4{0u, 0u, 0u, 0u};
+  uint32_t v = (st >> 16) & 0xFu;
+  if (v == PE_NONE) v = ((st & 0xFFu) == 0u && ((st >> 8) & 0xFFu) > 0u) ? PE_SKIP : PE_OK;
+  return uint4{v | (((st >> 20) & 1u) << 8) | KPE_SR_VALID, rg, vl, arr};
+}
+// The row's array sites before its rule loop (validateArrayOfMaps of each site's elements): the
+// sites of a group share their member chain (same keys), so it is resolved once and every element
+// is validated for every pending site of the group back to back, while its body and scalars are
+// in the L1; the results go to site_res, where the rules' walks take them at the array node. A
+// row's elements are thus read once for all the rules that iterate them instead of once per rule.
+__device__ __forceinline__ void pat_sites_row(const PatArgs& a, DocView doc, int64_t r, const uint8_t* row) {
+  for (uint32_t grp = 0; grp < a.ngroups; ++grp) {
+    const uint2 G = a.site_groups[grp];
+    uint32_t pm = 0;  // sites of the group whose cell of this row is pending
+    for (uint32_t i = 0; i < G.y; ++i) {
+      const KpeSite S = a.sites[a.group_sites[G.x + i]];
+      if (row[S.col] == KPE_PENDING_) pm |= 1u << i;
+    }
+    if (!pm) continue;
+    const KpeSite S0 = a.sites[a.group_sites[G.x]];
+    const uint32_t arr = site_array(a, doc, S0, r);
+    uint32_t st[8], rg[8], vl[8];
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i) st[i] = ((pm >> i) & 1u) ? PE_NONE << 16 : 1u << 21, rg[i] = 0u, vl[i] = 0u;
+    if (arr != kNoNode) {
+      const uint32_t b = doc[PVD(arr)].y, cnt = doc[PVD(b)].x;
+      for (uint32_t q = 0; q < cnt; ++q) {
+        bool open = false;
+        for (uint32_t i = 0; i < G.y; ++i) {  // one site_elem call site: the fold state is selected
+          uint32_t s = 0, g = 0, l = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < 8u; ++k) s = k == i ? st[k] : s, g = k == i ? rg[k] : g, l = k == i ? vl[k] : l;
+          if (sfold_done(s)) continue;
+          sfold_add(s, g, l, site_elem(a, doc, a.sites[a.group_sites[G.x + i]], r, b + 1u + q));
+#pragma unroll
+          for (uint32_t k = 0; k < 8u; ++k) st[k] = k == i ? s : st[k], rg[k] = k == i ? g : rg[k], vl[k] = k == i ? l : vl[k];
+          open = open || !sfold_done(s);
+        }
+        if (!open) break;
+      }
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < 8u; ++i)
+      if ((pm >> i) & 1u)
+        a.site_res[(size_t)a.group_sites[G.x + i] * (size_t)a.n + (size_t)r] =
+            arr != kNoNode ? sfold_result(st[i], rg[i], vl[i], arr) : uint4{0u, 0u, 0u, 0u};
+  }
 }
 // validateArrayOfMaps' fold (validate.go:224-261) over element results in order: skips counted,
 // the first other error ends it; AnchorMap slots and `und` of the elements visited

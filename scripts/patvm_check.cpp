@@ -7,6 +7,7 @@
 // N x R verdict bytes (non-pattern columns 0) to out.bin.
 #include <cmath>
 #include <cstdint>
+#include <map>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -147,18 +148,23 @@ int main(int argc, char** argv) {
     std::vector<uint4> sres(PP.sites.size() * (size_t)C.n, uint4{0u, 0u, 0u, 0u});
     a.sites = PP.sites.data(), a.site_chain = PP.site_chain.data(), a.nsites = (uint32_t)PP.sites.size();
     const DocView doc{reinterpret_cast<const uint2*>(C.doc.data()), 0u, a.ndoc, &err};
-    uint64_t valid = 0;
-    for (size_t si = 0; si < PP.sites.size(); ++si)
-      for (int64_t r = 0; r < a.n; ++r) {
-        const KpeSite& S = PP.sites[si];
-        const uint32_t arr = site_array(a, doc, S, r);
-        if (arr == kNoNode) continue;
-        SiteFold fold;
-        const uint32_t b = doc[arr].y;
-        for (uint32_t q = 0; q < doc[b].x && !fold.done(); ++q) fold.add(site_elem(a, doc, S, r, b + 1u + q));
-        sres[si * (size_t)C.n + (size_t)r] = fold.result(arr);
-        valid += (fold.result(arr).x & KPE_SR_VALID) ? 1 : 0;
+    // site groups as kpe_api.cpp builds them: sites whose chains name the same keys, <= 8 each;
+    // pat_eval_row's site pass (pat_sites_row) then fills site_res before the walks
+    std::map<std::vector<std::string>, std::vector<uint32_t>> by_chain;
+    for (uint32_t i = 0; i < PP.sites.size(); ++i) {
+      std::vector<std::string> keys;
+      for (uint32_t k = 0; k < PP.sites[i].nchain; ++k)
+        keys.push_back(PP.keys[PP.members[4 * (size_t)PP.site_chain[PP.sites[i].chain0 + k] + 1]]);
+      by_chain[keys].push_back(i);
+    }
+    std::vector<uint2> groups;
+    std::vector<uint32_t> order;
+    for (auto& kv : by_chain)
+      for (size_t j = 0; j < kv.second.size(); j += 8) {
+        groups.push_back(uint2{(uint32_t)order.size(), (uint32_t)std::min<size_t>(8, kv.second.size() - j)});
+        order.insert(order.end(), kv.second.begin() + j, kv.second.begin() + std::min(kv.second.size(), j + 8));
       }
+    a.site_groups = groups.data(), a.group_sites = order.data(), a.ngroups = (uint32_t)groups.size();
     a.site_res = sres.data();
     std::vector<uint8_t> site_v(lds_v);
     for (int64_t r = 0; r < a.n; ++r)
@@ -167,7 +173,9 @@ int main(int argc, char** argv) {
     a.verdicts = site_v.data();
     for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
     a.verdicts = keep;
-    a.site_res = nullptr;
+    a.site_res = nullptr, a.ngroups = 0;
+    uint64_t valid = 0;
+    for (auto& x : sres) valid += (x.x & KPE_SR_VALID) ? 1 : 0;
     if (site_v != verdicts) {
       size_t bad = 0;
       for (size_t i = 0; i < site_v.size(); ++i) bad += site_v[i] != verdicts[i];
