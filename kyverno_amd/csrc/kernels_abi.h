@@ -187,7 +187,7 @@ struct ScanArgs {
 struct PsumArgs {
   int64_t n;
   uint32_t ntiles, ncapsets;
-  const uint32_t *rec, *hdr, *crec, *vol_src, *sys_id, *pann_kv, *capsets;
+  const uint32_t *rec, *hdr, *crec, *vol_src, *sys_id, *pann_kv, *capsets, *c_sann;
   const uint8_t* dict_bytes[4];
   const uint32_t* dict_off[4];
   uint32_t dict_n[4];

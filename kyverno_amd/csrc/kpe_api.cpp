@@ -710,7 +710,7 @@ kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
   a.ncapsets = (uint32_t)C.capset_add.size();
   a.rec = D.rec.as<uint32_t>(), a.hdr = D.hdr.as<uint32_t>(), a.crec = D.crec.as<uint32_t>();
   a.vol_src = D.vol_src.as<uint32_t>(), a.sys_id = D.sys_id.as<uint32_t>(), a.pann_kv = D.pann_kv.as<uint32_t>();
-  a.capsets = D.capsets.as<uint32_t>();
+  a.capsets = D.capsets.as<uint32_t>(), a.c_sann = D.c_sann.as<uint32_t>();
   size_t code_bytes = 0;
   for (int d = 0; d < 4; ++d) code_bytes += (C.dict[dom[d]].size() + 15) & ~(size_t)15;
   if (!D.psum_ready) {
@@ -789,7 +789,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   bool lean = !getenv("KPE_NO_PREP") && !getenv("KPE_NO_LEAN") && narrow && PD.tt && P.any_pss &&
               C.dict[D_KIND].size() <= 4096;
   for (const auto& tm : P.terms) lean = lean && (tm.type == T_KIND_PRED || tm.type == T_FALSE);
-  lean = lean && !(need_flags(P) & (NEED_SANN | NEED_NAME | NEED_MNS));  // columns a LEAN tile never loads
+  lean = lean && !(need_flags(P) & (NEED_NAME | NEED_MNS));  // columns a LEAN scan never loads
   const uint32_t kt_words = lean ? (C.dict[D_KIND].size() + 3) & ~3u : 0u;
   const uint32_t capb_words = P.any_pss ? ((uint32_t)C.capset_add.size() + 15) / 16 * 4 : 0u;  // 1 byte per set
   const int64_t budget =
@@ -922,7 +922,6 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const int32_t fixed[10] = {ps.apparmor_key, ps.apparmor_val_ok, ps.seccomp_pod_key, ps.seccomp_ann_ok,
                              ps.caps_baseline_ok, ps.cap_nbs, ps.cap_all, ps.sysctl[0], ps.sysctl[1], ps.sysctl[2]};
   for (int k = 0; k < 10; ++k) B.pp[k] = loc(fixed[k]);
-  for (int k : {0, 1, 2, 3, 7, 8, 9}) lean = lean && (B.pp[k] & PRED_LOCAL) && B.pp[k] != PRED_NONE;
   for (const auto& tm : terms) lean = lean && (tm.type != T_KIND_PRED || ((tm.a & PRED_LOCAL) && tm.a != PRED_NONE));
   if (!P.pat.rules.empty() || P.any_fe_pat) {  // pattern members: names -> D_KEY ids + 1, glob names -> bitsets
     if (!C.has_docs) return fail(KPE_E_STATE, "pattern rules need a corpus flattened with KPE_CORPUS_DOCS");

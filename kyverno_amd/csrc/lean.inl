@@ -130,12 +130,15 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   const uint32_t oc = hw(h, 0) + (e01 & 0xFFFFu), ov = hw(h, 1) + (e01 >> 16), os = hw(h, 2) + (e23 & 0xFFFFu),
                  oa = hw(h, 3) + (e23 >> 16);
   if (!live) return;
-  uint32_t xo = 0, co = 0, vc = 0, sc = 0, ac = 0;
+  uint32_t xo = 0, co = 0, vc = 0, sc = 0, ac = 0, sa = 0;
   const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
+  const uint32_t nsv = a.dict_n[PSD_ANNV];
   for (uint32_t k = 0; k < nc; ++k) {
     const uint2 e = crec[oc + k];
     xo |= e.x;
     if (e.x) co |= a.csb[CY_CAPSET(e.y)];  // a real container record always has state bits
+    const uint32_t cs = a.c_sann[oc + k];  // the container's seccomp annotation value (v1.0 check)
+    if (cs != KPE_NO_STR) sa |= (cs < nsv ? ((uint32_t)a.codes[PSD_ANNV][cs] >> 1) & 1u : 0u) ^ 1u;
   }
   for (uint32_t k = 0; k < nv; ++k) {
     const uint32_t v = a.vol_src[ov + k];
@@ -153,7 +156,7 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
     const uint32_t va = q.y < nav ? (uint32_t)a.codes[PSD_ANNV][q.y] : 0u;
     ac |= ((ka & 1u) && !(va & 1u) ? 1u : 0u) | ((ka & 2u) && !(va & 2u) ? 2u : 0u);
   }
-  reinterpret_cast<uint2*>(a.psum)[r] = make_uint2(xo, co | (vc << 3) | (sc << 5) | (ac << 8));
+  reinterpret_cast<uint2*>(a.psum)[r] = make_uint2(xo, co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10));
 }
 
 // ---- kpe_lean5_kernel: pod records and PSA summaries only --------------------------------
@@ -192,7 +195,7 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArg
   uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a0.wave_lds + wv * a0.wave_words + KPE_STAGE_WORDS);
   const bool live = r < n;
   const uint32_t pw = rec.x, y = sum.y;
-  const uint32_t fails = cv_fails(pw, sum.x, PS_CAPS(y), false, PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
+  const uint32_t fails = cv_fails(pw, sum.x, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
                                   PS_ANN(y) & 1u, PS_ANN(y) & 2u) & cv_union;
   const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
   const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);

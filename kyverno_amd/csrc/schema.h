@@ -205,8 +205,11 @@ enum KpeDomain {
 // the container state bitmaps (CX_*), y = the OR-ed list codes under the PSA library's fixed
 // sets: capability-set bits (CS_* of kernels.hip) | volume codes << 3 (bit 0 hostPath, bit 1 a
 // source outside PSS_ALLOWED_VOLUMES) | sysctl codes << 5 (bit v: a sysctl outside version v's
-// set) | annotation codes << 8 (bit 0 AppArmor, bit 1 pod seccomp annotation not allowed)
+// set) | annotation codes << 8 (bit 0 AppArmor, bit 1 pod seccomp annotation not allowed) | bit
+// 10: a container's seccomp annotation (c_sann) outside the allowed profiles (check_seccompProfile
+// v1.0)
 #define PS_CAPS(y) ((y) & 7u)
+#define PS_SECANN(y) (((y) >> 10) & 1u)
 #define PS_VOL(y) (((y) >> 3) & 3u)
 #define PS_SYS(y) (((y) >> 5) & 7u)
 #define PS_ANN(y) (((y) >> 8) & 3u)

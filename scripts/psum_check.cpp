@@ -4,8 +4,9 @@
 //   scripts/build/psum_check resources.ndjson out.bin
 // Flattens the resources with the product flattener and writes 2 words per row (schema.h PS_*):
 // x = OR of the pod's container state bitmaps, y = capability-set bits | volume codes << 3 |
-// sysctl codes << 5 | annotation codes << 8, each code taken under the PSA library's fixed sets
-// (pss_fixed.hpp) from the list items in the corpus's CSR columns.
+// sysctl codes << 5 | annotation codes << 8 | a container seccomp annotation not allowed << 10,
+// each code taken under the PSA library's fixed sets (pss_fixed.hpp) from the list items in the
+// corpus's CSR columns.
 #include <cstdint>
 #include <cstdio>
 #include <fstream>
@@ -60,11 +61,13 @@ static std::vector<uint32_t> summary(const Corpus& C) {
             (pssfix::fixed_match(pssfix::kSeccompAnnOk, x) ? 2u : 0u);
   }
   for (int64_t r = 0; r < n; ++r) {
-    uint32_t xo = 0, co = 0, vc = 0, sc = 0, ac = 0;
+    uint32_t xo = 0, co = 0, vc = 0, sc = 0, ac = 0, sa = 0;
     for (uint32_t k = C.ctr_off[r]; k < C.ctr_off[r + 1]; ++k) {
       const uint32_t x = C.crec[2 * k];
       xo |= x;
       if (x) co |= csb[CY_CAPSET(C.crec[2 * k + 1])];
+      const uint32_t cs = C.c_sann[k];  // container seccomp annotation: bad unless an allowed profile
+      if (cs != KPE_NO_STR && !(cs < av.size() && (av[cs] & 2u))) sa = 1u;
     }
     for (uint32_t k = C.vol_off[r]; k < C.vol_off[r + 1]; ++k) {
       const uint32_t v = C.vol_src[k];
@@ -77,7 +80,7 @@ static std::vector<uint32_t> summary(const Corpus& C) {
       ac |= ((a & 1u) && !(b & 1u) ? 1u : 0u) | ((a & 2u) && !(b & 2u) ? 2u : 0u);
     }
     ps[2 * r] = xo;
-    ps[2 * r + 1] = co | (vc << 3) | (sc << 5) | (ac << 8);
+    ps[2 * r + 1] = co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10);
   }
   return ps;
 }

@@ -25,10 +25,14 @@ def engine():
     return K.Engine(ordinal=0)
 
 
-@pytest.fixture(scope="module", params=[(1, 20000, 0x51), (2, 20000, 0x52)], ids=["mixed", "edge"])
+@pytest.fixture(scope="module", params=[(1, 20000, 0x51), (2, 20000, 0x52), (-1, 400, 0)], ids=["mixed", "edge", "seccomp"])
 def corpus(request, engine):
     mix, n, seed = request.param
-    nd = K.synth_resources(seed, n, mix=mix)
+    if mix < 0:  # container / pod seccomp and AppArmor annotations (the v1.0 checks)
+        from tests.golden.make_psum_digests import seccomp_ndjson
+        nd = seccomp_ndjson(n)
+    else:
+        nd = K.synth_resources(seed, n, mix=mix)
     return nd, K.Corpus(nd, docs=False).upload(engine.device)
 
 
