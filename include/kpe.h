@@ -91,8 +91,11 @@ kpe_status kpe_program_compile(const char* policies_json, size_t len, kpe_progra
  * resource (pkg/engine/utils/exceptions.go:14-47, validate_resource.go:43-56, validate_pss.go:45-58).
  * KPE_COMPILE_BACKGROUND drops exceptions with spec.background: false, as the background scanner's
  * FetchPolicyExceptions does (pkg/controllers/report/utils/utils.go:113-124); kyverno apply uses
- * every exception it is given. KPE_E_UNSUPPORTED: podSecurity exceptions, conditions that do not
- * fold to true, rules whose preconditions read the resource. */
+ * every exception it is given. An exception with podSecurity controls re-evaluates a failing pod
+ * under them (validate_pss.go:88-104); `conditions` that read the resource, and exceptions on rules
+ * whose preconditions read it, are applied after the preconditions (exceptions.go:33-41).
+ * KPE_E_UNSUPPORTED: several exceptions on one rule when one has podSecurity controls or
+ * conditions that do not fold to true (the first matching one decides). */
 #define KPE_COMPILE_BACKGROUND 1u
 kpe_status kpe_program_compile_ex(const char* policies_json, size_t len, const char* exceptions_json, size_t exc_len,
                                   uint32_t flags, kpe_program** out);

@@ -128,25 +128,10 @@ __global__ void __launch_bounds__(256) kpe_count_kernel(const uint8_t* v, int64_
 namespace {
 
 constexpr uint32_t kBlock = 256;
-// Diagnostic builds only (scripts/diag_variants.sh): phases skipped to time the others.
-#ifndef KPE_DIAG
-#define KPE_DIAG 0
-#endif
 // Minimum waves per SIMD the scan kernel is compiled for (register budget).
 #ifndef KPE_SCAN_WAVES
 #define KPE_SCAN_WAVES 7  // C4 wide scan: 6 -> 0.191 ms, 7 -> 0.182 ms, 8 (spills) -> 0.208 ms
 #endif
-#define DIAG_NOPRO 1u    // no fused dictionary pass / capability bits in the prologue
-#define DIAG_NOPSS 2u    // PSS lists loaded but not evaluated
-#define DIAG_NORULES 4u  // no terms / rules: a verdict derived from the PSS bits
-#define DIAG_NOLOOP 8u   // no tiles: launch + prologue only
-#define DIAG_EMPTY 16u   // return at entry: launch cost only
-#define DIAG_NOTT 32u    // no truth table in the prologue
-#define DIAG_NOSTORE 64u  // (LEAN kernel) no verdict row stores
-#define DIAG_NOCV 128u    // (LEAN3) no PSA check logic: the OR-ed codes stand in for the failing checks
-#define DIAG_NOSTAGE 256u // (LEAN3) no list staging / per-pod OR: the lane's own first items stand in
-#define DIAG_PATNOVM 512u // (pattern kernel) the rule loop without the VM: pending cells pass
-#define DIAG_PATLEAF 1024u // (pattern VM) every scalar leaf holds without evaluation: the walk alone
 constexpr uint32_t kAllowedVolumes = PSS_ALLOWED_VOLUMES;
 
 
@@ -651,7 +636,6 @@ template <bool PSS, bool NARROW, bool PREP, bool LEAN = false>
 __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES)
     kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-  if (KPE_DIAG & DIAG_EMPTY) return;
   CArgs& a0 = *launder(ap);
   uint8_t* const s_capb = reinterpret_cast<uint8_t*>(dyn + a0.capb_lds);  // capability-set bits
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -726,7 +710,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     }
   }
   __syncthreads();
-  if (fused && !(KPE_DIAG & DIAG_NOPRO)) {  // one short LDS compare per (string, pattern)
+  if (fused) {  // one short LDS compare per (string, pattern)
     CArgs& a = a0;
     const uint2* pairs = reinterpret_cast<const uint2*>(dyn + a.fuse_lds);
     const KpePat* pats = reinterpret_cast<const KpePat*>(dyn + a.fuse_pats);
@@ -740,7 +724,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     }
     __syncthreads();
   }
-  if (PSS && !prepped && !(KPE_DIAG & DIAG_NOPRO)) {
+  if (PSS && !prepped) {
     CArgs& a = a0;
     const Bits B{dyn, a.pbuf};
     if (a.need & NEED_CAPS) {  // capability-set violation bits (add/drop masks vs the fixed allow-lists)
@@ -761,7 +745,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
 
   // NARROW truth table: tt[v] = rules whose match / exclude / namespaced-policy term
   // conditions hold for term vector v (pkg/engine/utils/match.go:168-300 over filters)
-  if (NARROW && !prepped && a0.tt_lds != PRED_NONE && !(KPE_DIAG & DIAG_NOTT)) {
+  if (NARROW && !prepped && a0.tt_lds != PRED_NONE) {
     const uint32_t R = a0.nrules, nv = 1u << a0.nterms;
     for (uint32_t tb = t; tb < nv; tb += kBlock) {
       uint32_t mm = 0;
@@ -816,10 +800,6 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
   // next tile's loads are issued, so no wait for those loads ever covers a store.
   uint32_t prev_tile = 0xFFFFFFFFu, prev_rows = 0, buf = 0;
 
-  if (KPE_DIAG & DIAG_NOLOOP) {
-    if (tile < ntiles && lane == 0) a0.verdicts[tile] = (uint8_t)(dyn[0] + s_capb[0]);
-    return;
-  }
   // Ping-pong tile buffers: the tile evaluated in one step was loaded into its own
   // registers during the previous step, and the next tile is loaded into the other
   // buffer, so no register holding an in-flight load is ever copied (a loop-carried
@@ -850,10 +830,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     bool err = false;
     const uint32_t need = a.need;
     if constexpr (PSS) {
-      if (KPE_DIAG & DIAG_NOPSS)
-        fails = cur.rec.x ^ cur.c0.x ^ cur.c1.y ^ cur.v0 ^ cur.v1 ^ cur.s0 ^ cur.q0.x ^ cur.q0.y ^ cur.C0;
-      else
-        fails = pss_tile<LEAN>(a, B, s_capb, cur, live, stage, lane, lp);
+      fails = pss_tile<LEAN>(a, B, s_capb, cur, live, stage, lane, lp);
       const uint32_t cls = (cur.rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
       err = live && (cls == R_CLASS_OTHER || (cur.rec.x & PR_DECODE_ERR));
       gvk = live ? cur.rec.y : 0u;
@@ -871,13 +848,6 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       prev_tile = 0xFFFFFFFFu;
     }
 
-    if (KPE_DIAG & DIAG_NORULES) {
-      sv[lane * R] = (uint8_t)(fails ^ (err ? 1u : 0u) ^ gvk);
-      __builtin_amdgcn_wave_barrier();
-      store_rows(a.verdicts, sv, tile, R, 0, R, nrows, lane);
-      __builtin_amdgcn_wave_barrier();
-      return;
-    }
     if (NARROW) {
       // ---- terms -> bit vector ----
       uint32_t tb = 0;

@@ -496,14 +496,13 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     lanes.push_back(r.pol_term < 0 ? PRED_NONE : (uint32_t)r.pol_term);
   }
   // NARROW programs: per-rule records + per-filter term masks (kernels_abi.h NR_*)
-  static const bool no_narrow = getenv("KPE_NO_NARROW") != nullptr;  // experiments: force the wide path
   // Label selector terms stay on the wide path: per lane, the narrow loop walks every selector's
   // requirement records with scalar loads and is issue-bound (C4: 0.22 ms narrow, 0.19 ms wide,
   // profiles/r02_c4)
   const bool sel_terms = std::any_of(P.terms.begin(), P.terms.end(), [](const KpeTerm& t) {
     return t.type == T_SELECTOR || t.type == T_NSSELECTOR;
   });
-  const bool narrow = !no_narrow && !sel_terms && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
+  const bool narrow = !sel_terms && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
                       P.terms.size() <= KPE_NARROW_TERMS && P.filters.size() <= KPE_NARROW_FILTERS;
   std::vector<uint32_t> nrules, fmask;
   if (narrow) {
@@ -786,7 +785,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const bool stage_prog = !narrow && prog_words <= kMaxProgLds;
   // LEAN scan candidate: prepped, NARROW truth-table program of kind-only terms (a kind table
   // replaces the per-resource term loop); confirmed below once predicate placement is known
-  bool lean = !getenv("KPE_NO_PREP") && !getenv("KPE_NO_LEAN") && narrow && PD.tt && P.any_pss &&
+  bool lean = narrow && PD.tt && P.any_pss &&
               C.dict[D_KIND].size() <= 4096;
   for (const auto& tm : P.terms) lean = lean && (tm.type == T_KIND_PRED || tm.type == T_FALSE);
   lean = lean && !(need_flags(P) & (NEED_NAME | NEED_MNS));  // columns a LEAN scan never loads
@@ -1025,14 +1024,9 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.wave_lds = wave_at;
   B.wave_words = wave_words;
   B.prep_dyn_bytes = (size_t)(fuse_at + fuse_words) * 4;
-  if (!getenv("KPE_NO_PREP")) {  // prologue image: LDS [0, img_end)
-    B.pimg_words = img_end;
-    HIPCHK(B.pimg.ensure((size_t)B.pimg_words * 4 + 16));
-    B.dyn_bytes = (size_t)scan_end * 4;  // scans copy the image: no fuse area
-  } else {
-    B.pimg_words = 0;
-    B.dyn_bytes = B.prep_dyn_bytes;
-  }
+  B.pimg_words = img_end;  // prologue image: LDS [0, img_end)
+  HIPCHK(B.pimg.ensure((size_t)B.pimg_words * 4 + 16));
+  B.dyn_bytes = (size_t)scan_end * 4;  // scans copy the image: no fuse area
   HIPCHK(B.pbuf.ensure((size_t)go * 4 + 16));
   HIPCHK(hipMemsetAsync(B.pbuf.p, 0, (size_t)go * 4 + 16, s));
   B.blob_words = blob;
@@ -1217,16 +1211,6 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (sa.pimg && fresh)
     HIPCHK(kpe_launch_prep(B.dargs.as<ScanArgs>(), P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.prep_dyn_bytes, s));
   B.inv_ready = true;
-  if (sa.pimg && getenv("KPE_DEBUG_PIMG")) {
-    std::vector<uint32_t> img(B.pimg_words);
-    HIPCHK(hipMemcpyAsync(img.data(), B.pimg.p, img.size() * 4, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
-    fprintf(stderr, "pimg: words=%u blob=%u tt_lds=%u kt_lds=%u capb_lds=%u nkinds=%u lean=%d nterms=%u\n",
-            B.pimg_words, B.blob_words, B.tt_lds, B.kt_lds, B.capb_lds, B.nkinds, (int)B.lean,
-            (unsigned)P.terms.size());
-    for (uint32_t i = 0; i < B.pimg_words; ++i) fprintf(stderr, "%s%08x", i % 8 ? " " : "\n  ", img[i]);
-    fprintf(stderr, "\n");
-  }
   ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   const bool lean_go = B.lean && (!masks || B.lean_kind == 7);  // LEAN5 writes check masks too
@@ -1242,7 +1226,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.npr = (uint32_t)P.pat.rules.size();
       pa.doc = D.doc.as<uint32_t>();
       pa.doc_off = D.doc_off.as<uint64_t>();
-      pa.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();  // C3 14.0 -> 8.5 ms, C5 27.6 -> 19.4 ms
+      pa.perm = D.doc_perm.as<uint32_t>();  // rows by kind and tape size: C3 14.0 -> 8.5 ms, C5 27.6 -> 19.4 ms
       pa.scal = D.scal.as<KpeScalar>();
       pa.scal_text = D.scal_text.as<uint8_t>();
       pa.nodes = PD.pnodes.as<KpePNode>();
@@ -1297,7 +1281,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.doc = D.doc.as<uint32_t>();
       ca.doc_off = D.doc_off.as<uint64_t>();
       ca.img_off = C.img_off.empty() ? nullptr : D.img_off.as<uint64_t>();
-      ca.perm = getenv("KPE_NO_PERM") ? nullptr : D.doc_perm.as<uint32_t>();
+      ca.perm = D.doc_perm.as<uint32_t>();
       ca.scal = D.scal.as<KpeScalar>();
       ca.scal_text = D.scal_text.as<uint8_t>();
       ca.key_bytes = D.dict_bytes[D_KEY].as<uint8_t>();
@@ -1389,7 +1373,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
-    if (getenv("KPE_PATVM_ERR")) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
+    static const bool patvm_err = getenv("KPE_PATVM_ERR") != nullptr;
+    if (patvm_err) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;
       HIPCHK(hipMemcpyAsync(&e, B.perr.p, 4, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));

@@ -9,9 +9,6 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 #endif
 constexpr int kPatStack = KPE_PAT_STACK;  // frames of one lane; deeper walks give KPE_UNDECIDED
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
-#ifndef KPE_PAT_SINGLE
-#define KPE_PAT_SINGLE 0  // one-member maps over an inline map resolve without a frame (single_map)
-#endif
 #ifndef KPE_PAT_FLAT
 #define KPE_PAT_FLAT 2  // maps of inline depth <= this resolve in their BEGIN step (0: all through frames;
                         // C5 / C3 ms, profiles/r03_e_inline: 0 14.2 / 5.3, 1 12.9 / 5.6, 2 at 4 waves 15.1 / 7.1
@@ -316,9 +313,6 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
   if (sid == kNoNode) return false;  // no scalar validator accepts a map / list
   const KpeLeaf Lv = PU(a.leaves, li, a.nleaves, 4);
   const KpeLeaf* L = &Lv;
-#if defined(DIAG_PATLEAF) && (KPE_DIAG & DIAG_PATLEAF)
-  if (L->type != PL_VAR && L->type != PL_TMPL) return sid != 0xFFFFFFFEu;  // every leaf holds
-#endif
   const KpeScalar* v = a.scal + PV(sid, a.nscal, 7);
   const uint32_t vf = v->flags, t = SC_TYPE(vf);
   if (L->type == PL_VAR) {  // the variable's typed value is the pattern (context numbers: float64)
@@ -626,44 +620,6 @@ struct PatVMT {
     }
   }
 
-  // validateMap of a map whose only member's value is a map of inline depth KPE_PAT_FLAT (e.g.
-  // {metadata: {labels: {...}}}): the member is looked up in the body (no registers held across
-  // the child), the child map resolves inline, and a one-member map's verdict is its member's
-  // (validate.go:118-175: an anchor member that skips makes every anchor skipped). PE_NONE: the
-  // child's body is past the inline limit (the frame path redoes the map).
-  __device__ __forceinline__ uint32_t single_map(uint32_t br, const KpePNode pn) {
-    const uint4 m = PU(a.members, pn.y, a.nmembers, 2);
-    const uint32_t h = PM_HANDLER(m.x);
-    const uint32_t c = pat_lookup(a, doc, br, m.y);
-    if (m.x & PMF_SLOT) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
-      const uint32_t bit = 1u << PM_SLOT(m.x);
-      reg |= bit;
-      if (c != kNoNode) val |= bit;
-    }
-    if (h == PM_NEG) return c != kNoNode ? PE_NEG : PE_OK;
-    if (c == kNoNode && h != PM_DEFAULT) return h == PM_COND ? PE_SKIP : PE_OK;
-    if ((m.x & PMF_STAR) || ((m.x & PMF_VSTAR) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv)))
-      return (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
-    const KpePNode vn = PU(a.nodes, m.z, a.nnodes, 1);
-    uint32_t v1;
-    if (!(m.x & PMF_LEAF)) {
-      if (c == kNoNode || DN_KIND(doc[PVD(c)].x) != DN_MAP) {
-        v1 = PE_OTHER;
-      } else {
-        v1 = flat_map<(KPE_PAT_FLAT >= 1 ? KPE_PAT_FLAT : 1)>(doc[PVD(c)].y, vn);
-        if (v1 == PE_NONE) return PE_NONE;
-      }
-    } else if (c != kNoNode && DN_KIND(doc[PVD(c)].x) == DN_ARR) {
-      PV_KIDS(c, l0, le);
-      v1 = PE_OK;
-      for (uint32_t q = l0; q < le && v1 == PE_OK; ++q)
-        if (!pat_leaf(a, node_sid(a, doc, q), vn.y, pv, &und)) v1 = PE_OTHER;
-    } else {
-      v1 = pat_leaf(a, node_sid(a, doc, c), vn.y, pv, &und) ? PE_OK : PE_OTHER;
-    }
-    return (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
-  }
-
   // validate.MatchPattern (validate.go:31-56) of pattern root node `root_pi`
   template <bool TRACE>
   __device__ __forceinline__ uint32_t run(uint32_t root_pi) {
@@ -692,9 +648,6 @@ struct PatVMT {
           } else if (KPE_PAT_FLAT && !TRACE && pn.w && pn.w <= (uint32_t)KPE_PAT_FLAT &&
                      (v = flat_map<KPE_PAT_FLAT>(doc[PVD(br)].y, pn)) != PE_NONE) {
             // resolved from the body in registers
-          } else if (KPE_PAT_SINGLE && KPE_PAT_FLAT >= 2 && !TRACE && pn.w == KPE_PAT_FLAT + 1u && (pn.z >> 16) == 1u &&
-                     (v = single_map(br, pn)) != PE_NONE) {
-            // one member over an inline map: resolved without a frame
           } else {
             const uint32_t nmem = pn.z >> 16;
             for (uint32_t k = 0; k < nmem; ++k) {  // AnchorMap.CheckAnchorInResource (anchormap.go:33-48)
@@ -940,10 +893,6 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       if (((x >> (8u * q)) & 0xFFu) != KPE_PENDING_) continue;
       const uint32_t pi = a.col2pr ? a.col2pr[c0 + q] : 0u;
       if (pi == 0u) continue;
-#if defined(DIAG_PATNOVM) && (KPE_DIAG & DIAG_PATNOVM)
-      row[c0 + q] = (uint8_t)KPE_PASS_;  // diagnostic: the rule loop without the VM
-      continue;
-#endif
       const uint32_t slot = memo ? a.rules[pi - 1u].flags >> PR_MEMO_SH : PR_NO_MEMO;
       if (slot < KPE_PAT_MEMO && ((memo_ok >> slot) & 1u)) {
         row[c0 + q] = memo[slot * memo_stride];
