@@ -182,6 +182,11 @@ kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kp
 #define KPE_EVAL_MASKS 1u
 #define KPE_EVAL_COLD 2u
 kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, unsigned flags);
+/* n evaluations enqueued by one call, corpora cs[0 .. n-1] in order (a corpus may repeat), each
+ * as kpe_evaluate_async_ex(dev, prog, cs[i], flags) would enqueue it: the batch form a scanner
+ * driving many resident shards (or a benchmark) uses instead of n foreign-function calls. */
+kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* const* cs, int n,
+                                    unsigned flags);
 kpe_status kpe_device_sync(kpe_device* dev);
 kpe_status kpe_fetch(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint8_t* verdicts,
                      uint32_t* check_masks, kpe_counts* counts);

@@ -73,6 +73,7 @@ def load():
     L.kpe_evaluate.argtypes = [vp, vp, vp, vp, vp, ctypes.POINTER(Counts)]
     L.kpe_evaluate_async.argtypes = [vp, vp, vp]
     L.kpe_evaluate_async_ex.argtypes = [vp, vp, vp, ctypes.c_uint]
+    L.kpe_evaluate_batch_async.argtypes = [vp, vp, vp, ctypes.c_int, ctypes.c_uint]
     L.kpe_device_sync.argtypes = [vp]
     L.kpe_device_verdicts.argtypes = [vp, vp, vp, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_uint64)]
     L.kpe_packed_words.argtypes = [ctypes.c_uint64]

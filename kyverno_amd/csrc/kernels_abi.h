@@ -161,7 +161,7 @@ struct ScanArgs {
   uint32_t pimg_words, capb_lds;
   // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask (PRED_NONE: no table)
   uint32_t kt_lds, nkinds;
-  const uint32_t* psum;  // LEAN5: per-pod PSA summary (2 words per pod, schema.h PS_*; kpe_psum_kernel)
+  const uint32_t* psum;  // LEAN5: per-pod scan records (3 words per pod: pod word, schema.h PS_* summary | kind << 16)
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null
@@ -195,7 +195,7 @@ struct PsumArgs {
   uint32_t fixed_len, pad_;
   uint8_t* codes[4];     // code byte per dictionary string (scratch)
   uint8_t* csb;          // code byte per capability set (scratch)
-  uint32_t* psum;        // out: 2 words per pod
+  uint32_t* psum;        // out: 3 words per pod (pod word, OR of container states, codes | kind << 16)
 };
 
 // kpe_pattern_kernel arguments (device-resident, one copy per binding)

@@ -717,7 +717,7 @@ kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
     HIPCHK(upload(D.psa_fixed, tab, s));
     HIPCHK(D.psa_codes.ensure(code_bytes + 16));
     HIPCHK(D.psa_csb.ensure(C.capset_add.size() + 16));
-    HIPCHK(D.psum.ensure((size_t)C.n * 8 + 16));
+    HIPCHK(D.psum.ensure((size_t)C.n * 12 + 16));
   }
   a.fixed = D.psa_fixed.as<uint8_t>();
   a.fixed_len = (uint32_t)psa_fixed_table().size();
@@ -1391,7 +1391,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
     const double mb = masks ? 4.0 * (double)C.n * (double)R : 0.0;
-    ev.bytes = lean_go && B.lean_kind == 7 ? 24.0 * (double)C.n + (double)C.n * (double)R + mb  // records, summaries, rows
+    ev.bytes = lean_go && B.lean_kind == 7 ? 12.0 * (double)C.n + (double)C.n * (double)R + mb  // scan records, rows
                                            : scan_bytes(P, C, B.need, masks);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     ev.kind = lean_go ? B.lean_kind : 1;
@@ -1431,6 +1431,20 @@ kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const
   return launch(dev, prog, const_cast<kpe_corpus*>(c), masks, (flags & KPE_EVAL_COLD) != 0);
 }
 
+kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* const* cs, int n,
+                                    unsigned flags) {
+  if (!dev || (n > 0 && !cs)) return fail(KPE_E_INVALID, "null argument");
+  if (flags & ~(unsigned)(KPE_EVAL_MASKS | KPE_EVAL_COLD)) return fail(KPE_E_INVALID, "unknown evaluation flags");
+  std::lock_guard<std::mutex> lk(dev->mu);
+  const bool masks = (flags & KPE_EVAL_MASKS) != 0;
+  for (int i = 0; i < n; ++i) {
+    if (kpe_status st = prepare(dev, prog, cs[i], masks)) return st;
+    if (kpe_status st = launch(dev, prog, const_cast<kpe_corpus*>(cs[i]), masks, (flags & KPE_EVAL_COLD) != 0))
+      return st;
+  }
+  return KPE_OK;
+}
+
 kpe_status kpe_device_sync(kpe_device* dev) {
   if (!dev) return fail(KPE_E_INVALID, "null device");
   HIPCHK(hipSetDevice(dev->ordinal));
@@ -1447,8 +1461,10 @@ kpe_status kpe_corpus_psa_summary(kpe_device* dev, kpe_corpus* c, uint32_t* out)
   if (D.bind.last) HIPCHK(hipStreamSynchronize(D.bind.last));
   if (!D.psum_ready)
     if (kpe_status st = run_psum(*c->c, D, dev->stream)) return st;
-  if (c->c->n) HIPCHK(hipMemcpyAsync(out, D.psum.p, (size_t)c->c->n * 8, hipMemcpyDeviceToHost, dev->stream));
+  std::vector<uint32_t> rec((size_t)c->c->n * 3);
+  if (c->c->n) HIPCHK(hipMemcpyAsync(rec.data(), D.psum.p, rec.size() * 4, hipMemcpyDeviceToHost, dev->stream));
   HIPCHK(hipStreamSynchronize(dev->stream));
+  for (int64_t i = 0; i < c->c->n; ++i) out[2 * i] = rec[3 * i + 1], out[2 * i + 1] = rec[3 * i + 2] & 0xFFFFu;
   return KPE_OK;
 }
 

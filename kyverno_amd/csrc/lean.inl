@@ -7,8 +7,9 @@
 // for fixed, policy-independent sets s (pss_fixed.hpp), so a pod reduces to one summary: the OR
 // of its container state bitmaps and of its list items' codes under those sets. The summary is
 // built on the device once per corpus (kpe_psa_dict_kernel -> kpe_psa_capset_kernel ->
-// kpe_psum_kernel, at the first binding of a LEAN program and again on a cold evaluation); an
-// evaluation then reads 16 + 8 bytes per pod and decides its versioned checks branch-free.
+// kpe_psum_kernel, at the first binding of a LEAN program and again on a cold evaluation), as a
+// 12-byte scan record per pod: the pod word and kind id of the pod record beside the summary. An
+// evaluation then reads 12 bytes per pod and decides its versioned checks branch-free.
 // Included by kernels.hip (uses its anonymous-namespace helpers).
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -19,6 +20,10 @@ __device__ __forceinline__ uint32_t bload1(Rsrc r, uint32_t off) { return __buil
 __device__ __forceinline__ uint2 bload2(Rsrc r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
   return make_uint2(v[0], v[1]);
+}
+__device__ __forceinline__ uint3 bload3(Rsrc r, uint32_t off) {
+  auto v = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0);
+  return make_uint3(v[0], v[1], v[2]);
 }
 __device__ __forceinline__ uint4 bload4(Rsrc r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
@@ -115,7 +120,8 @@ __global__ void __launch_bounds__(256) kpe_psa_capset_kernel(PsumArgs a) {
 }
 
 // One wave per 64-pod tile: list offsets from the tile header plus a wave scan of the pod
-// records' packed counts, then each lane ORs its own pod's items (schema.h PS_* layout).
+// records' packed counts, then each lane ORs its own pod's items (schema.h PS_* layout). Out: the
+// pod's LEAN scan record {pod word, OR of container states, list codes | kind id << 16}.
 __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -123,7 +129,8 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   const uint32_t r = tile * 64u + lane;
   const bool live = r < (uint32_t)a.n;
   const uint32_t h = a.hdr[tile * 4u + (lane & 3u)];
-  const uint32_t z = live ? reinterpret_cast<const uint4*>(a.rec)[r].z : 0u;
+  const uint4 rc = live ? reinterpret_cast<const uint4*>(a.rec)[r] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t z = rc.z;
   const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
   const uint32_t c01 = nc | (nv << 16), c23 = ns | (na << 16);
   const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
@@ -156,11 +163,12 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
     const uint32_t va = q.y < nav ? (uint32_t)a.codes[PSD_ANNV][q.y] : 0u;
     ac |= ((ka & 1u) && !(va & 1u) ? 1u : 0u) | ((ka & 2u) && !(va & 2u) ? 2u : 0u);
   }
-  reinterpret_cast<uint2*>(a.psum)[r] = make_uint2(xo, co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10));
+  uint32_t* o = a.psum + 3u * r;
+  o[0] = rc.x, o[1] = xo, o[2] = co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10) | (GVK_KIND(rc.y) << 16);
 }
 
-// ---- kpe_lean5_kernel: pod records and PSA summaries only --------------------------------
-// A wave loads one 16-byte record and one 8-byte summary per pod in one memory step and
+// ---- kpe_lean5_kernel: the 12-byte scan records only ------------------------------------
+// A wave loads one 12-byte record per pod (768 contiguous bytes) in one memory step and
 // evaluates with no staging, scans or list loops: the versioned checks (cv_fails), the kind
 // table, the rows stored as dwords through LDS and, when asked, the check masks.
 __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArgs) {
@@ -169,10 +177,9 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArg
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
   const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
   const uint32_t tile = xcd_block(blockIdx.x, gridDim.x) * (kLB / 64u) + wv;
-  const Rsrc RC = make_rsrc(a0.rec, n * 16u), PS = make_rsrc(a0.psum, n * 8u);
+  const Rsrc PS = make_rsrc(a0.psum, n * 12u);
   const uint32_t r = tile * 64u + lane;
-  const uint4 rec = bload4(RC, r * 16u);
-  const uint2 sum = bload2(PS, r * 8u);
+  const uint3 sr = bload3(PS, r * 12u);
   // the kind table and the class table of the prologue image (a few hundred words)
   const uint32_t img_n4 = a0.pimg_words >> 2;
   const uint4* img = reinterpret_cast<const uint4*>(a0.pimg);
@@ -194,12 +201,12 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArg
   const uint32_t ep_rules = a0.err_rules | a0.pat_rules, pat_rules = a0.pat_rules;
   uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a0.wave_lds + wv * a0.wave_words + KPE_STAGE_WORDS);
   const bool live = r < n;
-  const uint32_t pw = rec.x, y = sum.y;
-  const uint32_t fails = cv_fails(pw, sum.x, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
+  const uint32_t pw = sr.x, y = sr.z;
+  const uint32_t fails = cv_fails(pw, sr.y, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
                                   PS_ANN(y) & 1u, PS_ANN(y) & 2u) & cv_union;
   const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
   const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
-  const uint32_t matched = dyn[a0.kt_lds + GVK_KIND(rec.y)];
+  const uint32_t matched = dyn[a0.kt_lds + (y >> 16)];
   uint32_t failr;
   if (ncls == 1u) {
     failr = (fails & hw(cls_cv, 0)) ? hw(cls_rm, 0) : 0u;

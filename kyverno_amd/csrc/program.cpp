@@ -1581,6 +1581,9 @@ class CondCompiler {
         t.kind = VT_TMPL, t.a = (uint32_t)CP.tpieces.size() / 2;
         auto text = [&](size_t b, size_t e) {
           if (e <= b) return;
+          const std::string piece = v.s.substr(b, e - b);
+          if (piece.find("{{") != std::string::npos || piece.find("}}") != std::string::npos)
+            throw CompileError("nested variables in conditions");  // vars.go substitutes the result again
           CP.tpieces.push_back(PT_TEXT | (uint32_t)(e - b) << 1);
           CP.tpieces.push_back((uint32_t)CP.ctext.size());
           CP.ctext.insert(CP.ctext.end(), v.s.begin() + b, v.s.begin() + e);

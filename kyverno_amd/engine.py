@@ -273,6 +273,15 @@ def synth_ns_labels(seed: int, n_namespaces: int, mix: int = 0) -> bytes:
         L.kpe_synth_free(p)
 
 
+class CorpusBatch:
+    """Corpus handles packed once for kpe_evaluate_batch_async (keeps the corpora alive)."""
+
+    def __init__(self, corpora: Sequence[Corpus]):
+        self.corpora = list(corpora)
+        self.n = len(self.corpora)
+        self.arr = (ctypes.c_void_p * max(self.n, 1))(*[c.h for c in self.corpora])
+
+
 class Engine:
     """engineapi.Engine (validate path) on one MI355X."""
 
@@ -310,6 +319,19 @@ class Engine:
             check(load().kpe_evaluate_async(self.device.h, ps.h, corpus.h))
         else:
             check(load().kpe_evaluate_async_ex(self.device.h, ps.h, corpus.h, (1 if masks else 0) | (2 if cold else 0)))
+
+    def batch(self, corpora: Sequence[Corpus]) -> "CorpusBatch":
+        """A reusable list of corpora on this engine's device for evaluate_batch_async."""
+        for c in corpora:
+            if c.device is not self.device:
+                raise KpeError(5, "corpus not uploaded to this engine's device")  # KPE_E_STATE
+        return CorpusBatch(corpora)
+
+    def evaluate_batch_async(self, ps: PolicySet, batch, masks=False, cold=False):
+        """Enqueue one evaluation per corpus of `batch` (a CorpusBatch or a list), in order, with
+        one call (kpe_evaluate_batch_async)."""
+        b = batch if isinstance(batch, CorpusBatch) else self.batch(batch)
+        check(load().kpe_evaluate_batch_async(self.device.h, ps.h, b.arr, b.n, (1 if masks else 0) | (2 if cold else 0)))
 
     # ---- verdict exchange (device-resident) ----
     def device_verdicts(self, ps: PolicySet, corpus: Corpus):

@@ -50,6 +50,7 @@ def test_condition_set_compiles(oracle):
     {"key": "{{ request.object.spec.containers | [0] }}", "operator": "Equals", "value": "a"},  # pipe
     {"key": "{{ request.object.spec.containers | length(@) || `0` }}", "operator": "Equals", "value": 1},
     {"key": "$(./name)", "operator": "Equals", "value": "a"},                                  # reference
+    {"key": "{{ divide('{{ request.object.spec.replicas }}', '2') }}", "operator": "Equals", "value": 1},  # nested
     {"key": "{{ request.object.metadata }}", "operator": "Equals", "value": {"a": 1}},        # object value
 ])
 def test_outside_subset_refused(cond):
