@@ -1,5 +1,6 @@
 // Host-side columnar corpus: string dictionaries + SoA columns (see schema.h).
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <string>
 #include <string_view>
@@ -12,24 +13,72 @@ namespace kpe {
 
 constexpr uint64_t KPE_NO_IMAGES = ~0ull;
 
+// String dictionary: ids in first-intern order over one byte pool; the index is an
+// open-addressing table of (hash, id + 1) slots keyed by the pool bytes (no per-string
+// allocation, no std::string built for a lookup).
 struct Dict {
-  std::unordered_map<std::string, uint32_t> map;
   std::vector<char> bytes;
   std::vector<uint32_t> off{0};
   uint32_t intern(std::string_view s) {
-    const uint32_t id = (uint32_t)(off.size() - 1);
-    auto r = map.try_emplace(std::string(s), id);
-    if (!r.second) return r.first->second;
+    const uint64_t h = hash(s);
+    if ((size() + 1) * 2 > slots.size()) grow(std::max<size_t>(64, slots.size() * 2));
+    const size_t mask = slots.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot& e = slots[i];
+      if (e.id1 == 0) break;
+      if (e.h == (uint32_t)(h >> 32) && at(e.id1 - 1) == s) return e.id1 - 1;
+    }
+    const uint32_t id = size();
     bytes.insert(bytes.end(), s.begin(), s.end());
     off.push_back((uint32_t)bytes.size());
+    put(h, id);
     return id;
   }
   int64_t find(std::string_view s) const {
-    auto it = map.find(std::string(s));
-    return it == map.end() ? -1 : (int64_t)it->second;
+    if (slots.empty()) return -1;
+    const uint64_t h = hash(s);
+    const size_t mask = slots.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot& e = slots[i];
+      if (e.id1 == 0) return -1;
+      if (e.h == (uint32_t)(h >> 32) && at(e.id1 - 1) == s) return (int64_t)(e.id1 - 1);
+    }
+  }
+  void reserve(size_t n) {
+    size_t cap = 64;
+    while (cap < n * 2) cap *= 2;
+    if (cap > slots.size()) grow(cap);
   }
   uint32_t size() const { return (uint32_t)(off.size() - 1); }
   std::string_view at(uint32_t i) const { return std::string_view(bytes.data() + off[i], off[i + 1] - off[i]); }
+
+ private:
+  struct Slot {
+    uint32_t h, id1;  // high hash bits, id + 1 (0: empty)
+  };
+  std::vector<Slot> slots;
+  static uint64_t hash(std::string_view s) {  // 64-bit FNV-1a over 8-byte words, then a finalizer
+    uint64_t h = 0xcbf29ce484222325ull ^ s.size();
+    size_t i = 0;
+    for (; i + 8 <= s.size(); i += 8) {
+      uint64_t w;
+      __builtin_memcpy(&w, s.data() + i, 8);
+      h = (h ^ w) * 0x100000001b3ull;
+    }
+    for (; i < s.size(); ++i) h = (h ^ (unsigned char)s[i]) * 0x100000001b3ull;
+    h ^= h >> 33, h *= 0xff51afd7ed558ccdull, h ^= h >> 33, h *= 0xc4ceb9fe1a85ec53ull, h ^= h >> 33;
+    return h;
+  }
+  void put(uint64_t h, uint32_t id) {
+    const size_t mask = slots.size() - 1;
+    size_t i = h & mask;
+    while (slots[i].id1) i = (i + 1) & mask;
+    slots[i] = Slot{(uint32_t)(h >> 32), id + 1};
+  }
+  void grow(size_t cap) {
+    slots.assign(cap, Slot{0u, 0u});
+    for (uint32_t id = 0; id < size(); ++id) put(hash(at(id)), id);
+  }
 };
 
 struct DeviceCorpus;  // defined in kpe_api.cpp

@@ -1682,7 +1682,7 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
       th.emplace_back([&, d] {
         size_t tot = C.dict[d].size();
         for (size_t t = 0; t < T; ++t) tot += parts[t].dict[d].size();
-        C.dict[d].map.reserve(tot);
+        C.dict[d].reserve(tot);
         for (size_t t = 0; t < T; ++t) {
           const Dict& D = parts[t].dict[d];
           auto& m = dmap[t][d];
