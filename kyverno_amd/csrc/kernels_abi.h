@@ -227,14 +227,6 @@ struct PatArgs {
   const KpeScalar* ctab;
   const uint8_t* ctext;
   uint8_t* verdicts;
-  // array sites (schema.h KpeSite): kpe_site_kernel writes one result per (site, row) before the
-  // pattern kernel reads them (site_res[site * n + row]); null: no sites
-  const KpeSite* sites;
-  const uint32_t* site_chain;
-  uint4* site_res;
-  uint32_t nsites, ngroups;
-  const uint2* site_groups;        // (first, count) into group_sites: sites sharing one chain (<= 8)
-  const uint32_t* group_sites;
   // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)
   uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
   uint64_t nscal, ndoc;

@@ -117,14 +117,6 @@ constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated 
 // launch's prologue overlaps another's tail. Setup (uploads, binds) and timed launches
 // use stream 0.
 constexpr int kMaxLanes = 4;
-// Array sites (schema.h KpeSite): validated in the pattern kernel's per-row site pass
-// (patvm.inl pat_sites_row) before the rule walks; KPE_NO_SITES=1 walks every array per rule
-// (A/B measurement)
-static bool sites_on() {
-  static const bool off = getenv("KPE_NO_SITES") != nullptr;
-  return !off;
-}
-
 struct kpe_device {
   int ordinal = 0;
   hipStream_t stream = nullptr;  // == lanes[0]
@@ -166,8 +158,7 @@ struct DeviceProgram {
   bool tt = false;      // + truth-table fast path
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
-  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules, psites, pschain, psgroups, psorder;
-  uint32_t nsite_groups = 0;
+  DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
   DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
   DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
@@ -190,7 +181,6 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf pmembers, pargs, perr;  // pattern rules: resolved members, PatArgs copy, check flags
   bool pargs_valid = false;
   DevBuf pvals;  // pattern variables: per-row values (kpe_cond_kernel -> kpe_pattern_kernel)
-  DevBuf site_res;  // array-site results (kpe_site_kernel -> kpe_pattern_kernel), nsites x n uint4
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
   bool cargs_valid = false;
   DevBuf pimg;  // prologue image (kpe_launch_prep)
@@ -573,29 +563,6 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.pbytes, pb, s0));
     HIPCHK(upload(D.proots, PP.roots, s0));
     HIPCHK(upload(D.prules, PP.rules, s0));
-    HIPCHK(upload(D.psites, PP.sites, s0));
-    HIPCHK(upload(D.pschain, PP.site_chain, s0));
-    {  // site groups: sites whose chains name the same keys reach the same list of a row, so
-       // kpe_site_kernel resolves it once and evaluates an element for every site of the group
-       // while its body is in L1 (at most 8 sites per group)
-      std::map<std::vector<std::string>, std::vector<uint32_t>> by_chain;
-      for (uint32_t i = 0; i < PP.sites.size(); ++i) {
-        std::vector<std::string> keys;
-        const KpeSite& st = PP.sites[i];
-        for (uint32_t k = 0; k < st.nchain; ++k) keys.push_back(PP.keys[PP.members[4 * (size_t)PP.site_chain[st.chain0 + k] + 1]]);
-        by_chain[keys].push_back(i);
-      }
-      std::vector<uint32_t> order, groups;
-      for (auto& kv : by_chain)
-        for (size_t j = 0; j < kv.second.size(); j += 8) {
-          groups.push_back((uint32_t)order.size());
-          groups.push_back((uint32_t)std::min<size_t>(8, kv.second.size() - j));
-          order.insert(order.end(), kv.second.begin() + j, kv.second.begin() + std::min(kv.second.size(), j + 8));
-        }
-      D.nsite_groups = (uint32_t)(groups.size() / 2);
-      HIPCHK(upload(D.psgroups, groups, s0));
-      HIPCHK(upload(D.psorder, order, s0));
-    }
     HIPCHK(upload(D.pvars, PP.vars, s0));
     HIPCHK(upload(D.ptmpl, PP.tpieces, s0));
     HIPCHK(upload(D.ttext, PP.ttext, s0));
@@ -1051,7 +1018,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     B.napply_segs = (uint32_t)(segs.size() / 2);
     if (!segs.empty()) HIPCHK(upload(B.apply_segs, segs, s));
   }
-  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + 8));  // + slack: the pattern kernel reads two words past a row's cells
+  HIPCHK(B.verdicts.ensure(std::max<size_t>(cells, 4) + KPE_VERDICT_SLACK));  // the pattern kernel's row scan
   HIPCHK(B.counts_out.ensure(std::max<size_t>(P.rules.size() * 8, 1) * 8));
   if (!B.zero_page.p) {
     HIPCHK(B.zero_page.ensure(256));
@@ -1238,16 +1205,6 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.pat_bytes = PD.pbytes.as<uint8_t>();
       pa.roots = PD.proots.as<uint32_t>();
       pa.rules = PD.prules.as<KpePatRule>();
-      pa.nsites = sites_on() ? (uint32_t)P.pat.sites.size() : 0u;
-      if (pa.nsites) {
-        PCHK(B.site_res.ensure((size_t)pa.nsites * (size_t)C.n * 16));
-        pa.sites = PD.psites.as<KpeSite>();
-        pa.site_chain = PD.pschain.as<uint32_t>();
-        pa.site_res = B.site_res.as<uint4>();
-        pa.site_groups = PD.psgroups.as<uint2>();
-        pa.group_sites = PD.psorder.as<uint32_t>();
-        pa.ngroups = PD.nsite_groups;
-      }
       pa.col2pr = PD.pcol2pr.as<uint32_t>();
       pa.pbuf = B.pbuf.as<uint32_t>();
       pa.pvals = P.pat.vars.empty() ? nullptr : B.pvals.as<uint2>();

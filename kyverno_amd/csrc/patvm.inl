@@ -447,11 +447,6 @@ constexpr uint32_t VM_BEGIN = 0, VM_STEP = 1, VM_RET = 2;
 // the lane's index in its wave), so 64 lanes at any mix of depths hit 64 distinct banks and a
 // frame access costs an LDS round trip instead of a scratch one (scratch spills of 20 waves per
 // CU do not fit the L1 / L2 and wait on the Infinity Cache).
-struct FramesNone {  // walks that never push a frame (kpe_site_kernel's inline element maps)
-  static constexpr int kDepth = 1;
-  __device__ __forceinline__ PFrame get(int) const { return PFrame{0u, 0u, 0u, 0u, 0u, 0u, 0u}; }
-  __device__ __forceinline__ void put(int, const PFrame&) {}
-};
 struct FramesPriv {
   static constexpr int kDepth = kPatStack;
   PFrame st[kPatStack];
@@ -488,7 +483,6 @@ struct PatVMT {
   int sp;
   FS fs;
   uint32_t* tr;  // TRACE walks: the path record of the last failure (KPE_TRACE_WORDS words)
-  int64_t row = -1;  // the row whose document root the walk starts from (array-site results)
 
   // ---- failing paths (TRACE walks only; kpe_pattern_trace_kernel) ----
   // PatternError.Path (validate.go:31-56): the reference returns the path of the element where
@@ -665,18 +659,9 @@ struct PatVMT {
         } else if (rk != DN_ARR || pn.kind == PN_ARR_EMPTY) {
           v = PE_OTHER;  // a list pattern needs a list; [] is "pattern Array empty"
         } else {
-          uint4 sr{0u, 0u, 0u, 0u};
-          if (!TRACE && pn.kind == PN_ARR_MAPS && pn.w && a.site_res && row >= 0)  // an array site
-            sr = a.site_res[(size_t)(pn.w - 1u) * (size_t)a.n + (size_t)row];
-          if ((sr.x & KPE_SR_VALID) && sr.w == br) {  // kpe_site_kernel validated its elements
-            v = sr.x & 0xFFu;
-            und |= (sr.x >> 8) & 1u;
-            reg |= sr.y, val |= sr.z;
-          } else {
-            PV_KIDS(br, c0, end);
-            if (pn.kind == PN_ARR_POS && end - c0 < pn.z) v = PE_OTHER_NOPATH;  // length mismatch: no path
-            else v = push(pn.kind == PN_ARR_POS ? PF_APOS : PF_AMAPS, br, bpi, c0);
-          }
+          PV_KIDS(br, c0, end);
+          if (pn.kind == PN_ARR_POS && end - c0 < pn.z) v = PE_OTHER_NOPATH;  // length mismatch: no path
+          else v = push(pn.kind == PN_ARR_POS ? PF_APOS : PF_AMAPS, br, bpi, c0);
         }
         if (TRACE && v == PE_OTHER) snap(sp + 1, ~0u);  // validateResourceElement returns its path
         if (v == PE_PUSHED) state = VM_STEP, v = PE_NONE;
@@ -865,160 +850,54 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 // Rules that carry the same pattern share a memo slot (PR_MEMO_SH): the row's first pending cell
 // of the slot is evaluated and the others take its verdict from `memo` (LDS bytes, slot s at
 // memo[s * memo_stride]; null: no memo).
-__device__ __forceinline__ void pat_sites_row(const PatArgs& a, DocView doc, int64_t r, const uint8_t* row);
 template <class FS>
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs, uint8_t* memo = nullptr,
                                              uint32_t memo_stride = 0) {
   uint32_t memo_ok = 0;  // slots holding this row's verdict
-  if (a.ngroups) pat_sites_row(a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), r,
-                               a.verdicts + (size_t)r * a.R);
   PatVMT<FS> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
-                a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr, r};
+                a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
-  // The row's cells are read four at a time (two aligned words funnel-shifted to the row's
-  // byte offset), and the columns are visited in the same order by every lane, so the lanes of
-  // a wave run the VM for the same pattern rule together; a group of four cells without a
-  // KPE_PENDING_ byte costs two loads and a few ALU operations (C3: 600 pattern columns).
+  // The row's cells are scanned 64 columns at a time: the 17 aligned words that cover them are
+  // loaded together (one memory round trip per 64 columns instead of one per 4) and reduced to a
+  // mask of the KPE_PENDING_ cells, whose rules then run in column order, so the lanes of a wave
+  // run the VM for the same pattern rule together.
   const uint64_t start = (uint64_t)r * a.R;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(a.verdicts);
-  for (uint32_t c0 = 0; c0 < a.R; c0 += 4u) {
-    const uint64_t p = start + c0;
-    const uint32_t sh = (uint32_t)(p & 3u);
-    const uint32_t lo = words[p >> 2], hi = words[(p >> 2) + 1u];
-    uint32_t x = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh)) : lo;  // cells c0 .. c0 + 3
-    if (c0 + 4u > a.R) x |= ~0u << (8u * (a.R - c0));  // past the row: 0xFF, never pending
-    const uint32_t t = x ^ 0x06060606u;                 // KPE_PENDING_ cells -> 0
-    if (!((t - 0x01010101u) & ~t & 0x80808080u)) continue;
-    for (uint32_t q = 0; q < 4u; ++q) {
-      if (((x >> (8u * q)) & 0xFFu) != KPE_PENDING_) continue;
-      const uint32_t pi = a.col2pr ? a.col2pr[c0 + q] : 0u;
+  for (uint32_t c00 = 0; c00 < a.R; c00 += 64u) {
+    const uint64_t p0 = start + c00;
+    const uint32_t sh = (uint32_t)(p0 & 3u);
+    uint32_t w[17];
+#pragma unroll
+    for (uint32_t j = 0; j < 17u; ++j) w[j] = words[(p0 >> 2) + j];  // the buffer carries slack past the matrix
+    uint64_t pend = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16u; ++j) {
+      uint32_t x = sh ? (uint32_t)((((uint64_t)w[j + 1u] << 32) | w[j]) >> (8u * sh)) : w[j];  // cells 4j .. 4j + 3
+      const uint32_t t = x ^ 0x06060606u;  // KPE_PENDING_ cells -> 0
+      // exact zero-byte test (no borrow between bytes): bit 8q + 7 set iff byte q was pending
+      const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+      pend |= (uint64_t)(((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4u * j);
+    }
+    if (a.R - c00 < 64u) pend &= (1ull << (a.R - c00)) - 1ull;  // past the row
+    while (pend) {
+      const uint32_t q = (uint32_t)__builtin_ctzll(pend);
+      pend &= pend - 1ull;
+      const uint32_t cq = c00 + q;
+      const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
       if (pi == 0u) continue;
       const uint32_t slot = memo ? a.rules[pi - 1u].flags >> PR_MEMO_SH : PR_NO_MEMO;
       if (slot < KPE_PAT_MEMO && ((memo_ok >> slot) & 1u)) {
-        row[c0 + q] = memo[slot * memo_stride];
+        row[cq] = memo[slot * memo_stride];
         continue;
       }
       uint32_t v = pat_eval_cell(vm, pi - 1u);
       if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
         // a shallow (LDS) stack may have overflowed: the lane-private kPatStack-deep one decides
         PatVMT<FramesPriv> deep{a, vm.doc, vm.root, vm.pv, 0u};
-        deep.row = r;
         v = pat_eval_cell(deep, pi - 1u);
       }
-      row[c0 + q] = (uint8_t)v;
+      row[cq] = (uint8_t)v;
       if (slot < KPE_PAT_MEMO) memo[slot * memo_stride] = (uint8_t)v, memo_ok |= 1u << slot;
     }
   }
 }
-
-// ---- array sites (schema.h KpeSite) ------------------------------------------------------
-// The site's array entry of row r: the member chain looked up from the document root (every
-// link a map holding the key), or kNoNode when the row does not reach a list there (the VM then
-// walks whatever it finds itself)
-__device__ __forceinline__ uint32_t site_array(const PatArgs& a, DocView doc, const KpeSite& S, int64_t r) {
-  uint32_t cur = (uint32_t)a.doc_off[r];
-  for (uint32_t i = 0; i < S.nchain; ++i) {
-    if (DN_KIND(doc[PVD(cur)].x) != DN_MAP) return kNoNode;
-    const uint4 m = PU(a.members, a.site_chain[S.chain0 + i], a.nmembers, 2);
-    cur = pat_lookup(a, doc, cur, m.y);
-    if (cur == kNoNode) return kNoNode;
-  }
-  return DN_KIND(doc[PVD(cur)].x) == DN_ARR ? cur : kNoNode;
-}
-// One element of a site's array against its element map (validateResourceElement): x = verdict |
-// und << 8, y / z = AnchorMap slots registered / present; PE_NONE: a body past the inline limit
-__device__ __forceinline__ uint4 site_elem(const PatArgs& a, DocView doc, const KpeSite& S, int64_t r, uint32_t e) {
-  PatVMT<FramesNone> vm{a, doc, 0u, a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, FramesNone{}, nullptr, r};
-  const uint2 x = doc[PVD(e)];
-  const uint32_t v = DN_KIND(x.x) != DN_MAP ? PE_OTHER : vm.template flat_map<PNF_MAXDEPTH>(x.y, PU(a.nodes, S.elem, a.nnodes, 1));
-  return uint4{v | (vm.und << 8), vm.reg, vm.val, 0u};
-}
-// validateArrayOfMaps' fold (validate.go:224-261), packed in one word per site: applied | skips << 8
-// | verdict << 16 (PE_NONE: open) | und << 20 | none << 21 (a body past the inline limit: the VM
-// walks the array itself), plus the AnchorMap words
-__device__ __forceinline__ void sfold_add(uint32_t& st, uint32_t& rg, uint32_t& vl, const uint4 x) {
-  if (((st >> 16) & 0xFu) != PE_NONE || (st >> 21) & 1u) return;  // decided
-  const uint32_t c = x.x & 0xFFu;
-  if (c == PE_NONE) {
-    st |= 1u << 21;
-    return;
-  }
-  st |= (x.x & 0x100u) << 12, rg |= x.y, vl |= x.z;
-  if (c == PE_SKIP) st += 1u << 8;
-  else if (c != PE_OK) st = (st & ~(0xFu << 16)) | (c << 16);
-  else st += 1u;
-}
-__device__ __forceinline__ bool sfold_done(uint32_t st) { return ((st >> 16) & 0xFu) != PE_NONE || ((st >> 21) & 1u); }
-__device__ __forceinline__ uint4 sfold_result(uint32_t st, uint32_t rg, uint32_t vl, uint32_t arr) {
-  if ((st >> 21) & 1u) return uint4{0u, 0u, 0u, 0u};
-  uint32_t v = (st >> 16) & 0xFu;
-  if (v == PE_NONE) v = ((st & 0xFFu) == 0u && ((st >> 8) & 0xFFu) > 0u) ? PE_SKIP : PE_OK;
-  return uint4{v | (((st >> 20) & 1u) << 8) | KPE_SR_VALID, rg, vl, arr};
-}
-// The row's array sites before its rule loop (validateArrayOfMaps of each site's elements): the
-// sites of a group share their member chain (same keys), so it is resolved once and every element
-// is validated for every pending site of the group back to back, while its body and scalars are
-// in the L1; the results go to site_res, where the rules' walks take them at the array node. A
-// row's elements are thus read once for all the rules that iterate them instead of once per rule.
-__device__ __forceinline__ void pat_sites_row(const PatArgs& a, DocView doc, int64_t r, const uint8_t* row) {
-  for (uint32_t grp = 0; grp < a.ngroups; ++grp) {
-    const uint2 G = a.site_groups[grp];
-    uint32_t pm = 0;  // sites of the group whose cell of this row is pending
-    for (uint32_t i = 0; i < G.y; ++i) {
-      const KpeSite S = a.sites[a.group_sites[G.x + i]];
-      if (row[S.col] == KPE_PENDING_) pm |= 1u << i;
-    }
-    if (!pm) continue;
-    const KpeSite S0 = a.sites[a.group_sites[G.x]];
-    const uint32_t arr = site_array(a, doc, S0, r);
-    uint32_t st[8], rg[8], vl[8];
-#pragma unroll
-    for (uint32_t i = 0; i < 8u; ++i) st[i] = ((pm >> i) & 1u) ? PE_NONE << 16 : 1u << 21, rg[i] = 0u, vl[i] = 0u;
-    if (arr != kNoNode) {
-      const uint32_t b = doc[PVD(arr)].y, cnt = doc[PVD(b)].x;
-      for (uint32_t q = 0; q < cnt; ++q) {
-        bool open = false;
-        for (uint32_t i = 0; i < G.y; ++i) {  // one site_elem call site: the fold state is selected
-          uint32_t s = 0, g = 0, l = 0;
-#pragma unroll
-          for (uint32_t k = 0; k < 8u; ++k) s = k == i ? st[k] : s, g = k == i ? rg[k] : g, l = k == i ? vl[k] : l;
-          if (sfold_done(s)) continue;
-          sfold_add(s, g, l, site_elem(a, doc, a.sites[a.group_sites[G.x + i]], r, b + 1u + q));
-#pragma unroll
-          for (uint32_t k = 0; k < 8u; ++k) st[k] = k == i ? s : st[k], rg[k] = k == i ? g : rg[k], vl[k] = k == i ? l : vl[k];
-          open = open || !sfold_done(s);
-        }
-        if (!open) break;
-      }
-    }
-#pragma unroll
-    for (uint32_t i = 0; i < 8u; ++i)
-      if ((pm >> i) & 1u)
-        a.site_res[(size_t)a.group_sites[G.x + i] * (size_t)a.n + (size_t)r] =
-            arr != kNoNode ? sfold_result(st[i], rg[i], vl[i], arr) : uint4{0u, 0u, 0u, 0u};
-  }
-}
-// validateArrayOfMaps' fold (validate.go:224-261) over element results in order: skips counted,
-// the first other error ends it; AnchorMap slots and `und` of the elements visited
-struct SiteFold {
-  uint32_t applied = 0, skips = 0, verdict = PE_NONE, und = 0, reg = 0, val = 0;
-  bool none = false;
-  __device__ __forceinline__ bool done() const { return none || verdict != PE_NONE; }
-  __device__ __forceinline__ void add(const uint4 x) {
-    const uint32_t c = x.x & 0xFFu;
-    if (c == PE_NONE) {
-      none = true;
-      return;
-    }
-    und |= (x.x >> 8) & 1u, reg |= x.y, val |= x.z;
-    if (c == PE_SKIP) ++skips;
-    else if (c != PE_OK) verdict = c;
-    else ++applied;
-  }
-  __device__ __forceinline__ uint4 result(uint32_t arr) const {
-    if (none) return uint4{0u, 0u, 0u, 0u};
-    const uint32_t v = verdict != PE_NONE ? verdict : (applied == 0u && skips > 0u ? PE_SKIP : PE_OK);
-    return uint4{v | (und << 8) | KPE_SR_VALID, reg, val, arr};
-  }
-};
-

@@ -919,38 +919,6 @@ class PatCompiler {
   }
 };
 
-// Array sites (schema.h KpeSite) below pattern node n: walk map members with a plain key and the
-// default / equality / condition / global handler (the VM then reaches a member's value node only
-// with the entry a lookup of that key returns, so a site's resource node is a function of the row)
-void find_sites(PatProgram& PP, uint32_t n, uint32_t col, std::vector<uint32_t>& chain) {
-  const KpePNode nd = PP.nodes[n];
-  if (nd.kind == PN_ARR_MAPS) {
-    const KpePNode el = PP.nodes[nd.y];
-    if (el.kind == PN_MAP && el.w != 0 && !chain.empty() && chain.size() <= KPE_SITE_MAXCHAIN &&
-        PP.sites.size() < 0xFFFFu) {
-      KpeSite s{};
-      s.col = col, s.arr = n, s.elem = nd.y, s.chain0 = (uint32_t)PP.site_chain.size(), s.nchain = (uint32_t)chain.size();
-      PP.site_chain.insert(PP.site_chain.end(), chain.begin(), chain.end());
-      PP.sites.push_back(s);
-      PP.nodes[n].w = (uint32_t)PP.sites.size();  // site + 1
-    }
-    return;
-  }
-  if (nd.kind != PN_MAP) return;
-  const uint32_t nmem = nd.z >> 16;
-  for (uint32_t k = 0; k < nmem; ++k) {
-    const uint32_t mi = nd.y + k, x = PP.members[4 * mi], h = PM_HANDLER(x), vn = PP.members[4 * mi + 2];
-    if (h == PM_NEG || h == PM_EXIST || (x & (PMF_GLOB | PMF_STAR | PMF_LEAF)) || vn >= PP.nodes.size()) continue;
-    chain.push_back(mi);
-    find_sites(PP, vn, col, chain);
-    chain.pop_back();
-  }
-}
-void find_sites(PatProgram& PP, uint32_t root_node, uint32_t col) {
-  std::vector<uint32_t> chain;
-  find_sites(PP, root_node, col, chain);
-}
-
 }  // namespace pc
 
 // ---- lowering ----
@@ -2442,7 +2410,6 @@ class Lowerer {
           else jv_sig(*v->get("anyPattern"), sig);
           pat_sigs_.emplace_back((uint32_t)P.pat.rules.size(), std::move(sig));
         }
-        for (uint32_t k = 0; k < pr.nr; ++k) pc::find_sites(P.pat, P.pat.roots[2 * (pr.r0 + k)], pr.col);
         if (P.pat.rules.size() >= 65535) throw CompileError("more than 65535 pattern rules in one program");
         P.pat.rules.push_back(pr);
         k.handler = H_PATTERN;

@@ -35,8 +35,6 @@ struct PatProgram {
   std::vector<KpePVar> vars;           // pattern variable slots (PL_VAR / PT_VAR)
   std::vector<uint32_t> tpieces;       // 2 words per template piece (PT_*)
   std::vector<uint8_t> ttext;          // template texts
-  std::vector<KpeSite> sites;          // array sites of the rules' roots (schema.h KpeSite)
-  std::vector<uint32_t> site_chain;    // member indices of the sites' chains
 };
 // Compiled preconditions / deny / foreach-deny programs (schema.h QO_* / KpeC*), evaluated per
 // resource by kpe_cond_kernel. Field names are kept as text: a binding resolves them to corpus

@@ -302,6 +302,8 @@ enum KpeCheckVersion {
                           // condition list longer than CV_LIST_CAP): the caller evaluates it
 #define KPE_XFAIL_ 8  // device-internal: a failing podSecurity cell whose PolicyException has
                       // podSecurity controls (validate_pss.go:88-104), resolved by kpe_pssx_kernel
+#define KPE_VERDICT_SLACK 72u  // bytes past the N x R matrix: the pattern kernel's 64-column row
+                               // scan reads 17 whole words from a row's start
 #define KPE_XDEFER_ 0x10  // device-internal flag (XE_DEFER rules): the exception's match block
                           // held; kpe_cond_kernel applies the exception after the preconditions
 
@@ -524,7 +526,7 @@ typedef struct KpeScalar {
 #define PN_MAP 1u        // y = first member, z = number of anchor-phase members | total << 16,
                          // w = inline depth (see PNF_FLAT)
 #define PN_ARR_EMPTY 2u  // []: "pattern Array empty"
-#define PN_ARR_MAPS 3u   // [map, ...]: y = node of element 0 (validateArrayOfMaps), w = site + 1 (KpeSite) or 0
+#define PN_ARR_MAPS 3u   // [map, ...]: y = node of element 0 (validateArrayOfMaps)
 #define PN_ARR_LEAF 4u   // [scalar, ...]: y = leaf of element 0 (every element must match)
 #define PN_ARR_POS 5u    // [[...], ...]: y = first entry of the node list, z = count (positional)
 #define PN_EXLIST 6u     // existence-anchor value: y = node list entry, z = count (PN_BAD entries allowed)
@@ -623,19 +625,6 @@ typedef struct KpeCond {
 typedef struct KpePatRule {
   uint32_t col, flags, r0, nr;
 } KpePatRule;
-// Array site: a PN_ARR_MAPS node of a rule's pattern reached from its root through map members
-// only (plain keys with the default, equality, condition or global handler), whose element map
-// has an inline depth (PNF_FLAT). kpe_site_kernel resolves the member chain per row (chain0:
-// members [chain0, chain0 + nchain) of the site_chain table, member indices) and validates the
-// array's elements one lane per element (validateArrayOfMaps, validate.go:224-261); the pattern
-// VM takes the row's result when it reaches the node (patvm.inl).
-typedef struct KpeSite {
-  uint32_t col, arr, elem, chain0, nchain, pad[3];
-} KpeSite;
-// Site result of a row (uint4): x = verdict (PE_*) | und << 8 | KPE_SR_VALID, y / z = AnchorMap
-// slots registered / present in the array's subtree, w = the array's tape entry
-#define KPE_SR_VALID 0x80000000u
-#define KPE_SITE_MAXCHAIN 8u
 // Failing-path record of one pattern root (kpe_pattern_traces, include/kpe.h): word 0 =
 // component count | KPE_TR_TRUNC | verdict << 16 | KPE_TR_VALID; words 1..15 = components from
 // the root: a pattern member index (the key its handler appends to the path), KPE_TC_KEY | D_KEY

@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
   const uint32_t R = (uint32_t)P->rules.size();
   if (seed.size() != (size_t)C.n * R) return fprintf(stderr, "seed size %zu != %lld x %u\n", seed.size(), (long long)C.n, R), 1;
   std::vector<uint8_t> verdicts(seed.begin(), seed.end());
-  verdicts.resize(verdicts.size() + 8, 0);  // the pattern pass reads whole words
+  verdicts.resize(verdicts.size() + KPE_VERDICT_SLACK, 0);  // the pattern pass reads whole words
   std::vector<uint32_t> fk(CP.fields.size());
   for (size_t i = 0; i < fk.size(); ++i) {
     const int64_t id = C.dict[D_KEY].find(CP.fields[i]);

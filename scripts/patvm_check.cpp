@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
     mem[i] = m;
   }
   const uint32_t R = (uint32_t)P->rules.size();
-  std::vector<uint8_t> verdicts((size_t)C.n * R + 8, 0);  // + slack: the kernel reads whole words
+  std::vector<uint8_t> verdicts((size_t)C.n * R + KPE_VERDICT_SLACK, 0);  // + slack: the kernel reads whole words
   for (int64_t r = 0; r < C.n; ++r)
     for (auto& pr : PP.rules) verdicts[(size_t)r * R + pr.col] = KPE_PENDING_;
   std::vector<KpeScalar> scal(C.scal);
@@ -143,46 +143,6 @@ int main(int argc, char** argv) {
   // ... and the lane-private stack
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
   if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk (with memo) differs from the private-stack walk\n"), 1;
-  // array sites (kpe_site_kernel's results, folded element by element here) must not change a cell
-  if (!PP.sites.empty()) {
-    std::vector<uint4> sres(PP.sites.size() * (size_t)C.n, uint4{0u, 0u, 0u, 0u});
-    a.sites = PP.sites.data(), a.site_chain = PP.site_chain.data(), a.nsites = (uint32_t)PP.sites.size();
-    const DocView doc{reinterpret_cast<const uint2*>(C.doc.data()), 0u, a.ndoc, &err};
-    // site groups as kpe_api.cpp builds them: sites whose chains name the same keys, <= 8 each;
-    // pat_eval_row's site pass (pat_sites_row) then fills site_res before the walks
-    std::map<std::vector<std::string>, std::vector<uint32_t>> by_chain;
-    for (uint32_t i = 0; i < PP.sites.size(); ++i) {
-      std::vector<std::string> keys;
-      for (uint32_t k = 0; k < PP.sites[i].nchain; ++k)
-        keys.push_back(PP.keys[PP.members[4 * (size_t)PP.site_chain[PP.sites[i].chain0 + k] + 1]]);
-      by_chain[keys].push_back(i);
-    }
-    std::vector<uint2> groups;
-    std::vector<uint32_t> order;
-    for (auto& kv : by_chain)
-      for (size_t j = 0; j < kv.second.size(); j += 8) {
-        groups.push_back(uint2{(uint32_t)order.size(), (uint32_t)std::min<size_t>(8, kv.second.size() - j)});
-        order.insert(order.end(), kv.second.begin() + j, kv.second.begin() + std::min(kv.second.size(), j + 8));
-      }
-    a.site_groups = groups.data(), a.group_sites = order.data(), a.ngroups = (uint32_t)groups.size();
-    a.site_res = sres.data();
-    std::vector<uint8_t> site_v(lds_v);
-    for (int64_t r = 0; r < a.n; ++r)
-      for (uint32_t c = 0; c < R; ++c) site_v[(size_t)r * R + c] = col2pr[c] ? KPE_PENDING_ : site_v[(size_t)r * R + c];
-    uint8_t* keep = a.verdicts;
-    a.verdicts = site_v.data();
-    for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
-    a.verdicts = keep;
-    a.site_res = nullptr, a.ngroups = 0;
-    uint64_t valid = 0;
-    for (auto& x : sres) valid += (x.x & KPE_SR_VALID) ? 1 : 0;
-    if (site_v != verdicts) {
-      size_t bad = 0;
-      for (size_t i = 0; i < site_v.size(); ++i) bad += site_v[i] != verdicts[i];
-      return fprintf(stderr, "array-site walk differs from the element-by-element walk in %zu cells\n", bad), 1;
-    }
-    printf("sites %zu valid results %llu\n", PP.sites.size(), (unsigned long long)valid);
-  }
   FILE* f = fopen(argv[3], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
