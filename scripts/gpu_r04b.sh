@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 4 pattern-kernel pass: C3 / C5 benches with the in-row array-site pass (default) and
-# without it (KPE_NO_SITES=1), the pattern parity tests, and rocprofv3 kernel traces.
+# Round 4 pattern-kernel pass: the pattern parity tests, C3 / C5 benches and rocprofv3 kernel
+# traces of both.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 TAG=${TAG:-r04_b}
@@ -18,7 +18,6 @@ step() {  # step <name> <timeout> <cmd...>
 TAILN=8 step pytest_pat 600 python -u -m pytest tests/test_gpu_pattern.py tests/test_gpu_configs.py -m gpu -x -q --timeout 300 --timeout-method thread
 for c in c5 c3; do
   step bench_$c 400 python bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0
-  step bench_${c}_nosites 400 env KPE_NO_SITES=1 python bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0
 done
 for c in c5 c3; do
   step trace_$c 300 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o $c --output-format csv -- python3 bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0
