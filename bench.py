@@ -14,7 +14,9 @@ are all-reduced once over RCCL after the timed region).
 
 One step = one evaluation pass of the compiled program over one resident shard
 (kpe_evaluate_async: resource-scan kernel, then the condition / exclusion / pattern kernels when
-the program has such rules); the K timed steps are enqueued by one kpe_evaluate_batch_async call.
+the program has such rules); the K timed steps are enqueued by one kpe_evaluate_batch_async call,
+which sends a run of LEAN5 steps (C2) as ceil(K / 64) multi-shard launches of
+kpe_lean5_batch_kernel (one grid over the steps' shards) and every other step as its own launch.
 Distinct shards are rotated so that the bytes a step's scan reads were last touched more than
 twice the 256 MiB Infinity Cache ago: C2 reads a 12-byte scan record per pod and writes R bytes,
 15 MB per 1M-pod shard, so it rotates 41 shards (615 MB; the count is derived from the scan's
@@ -36,7 +38,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 IC_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
 # kpe_kernel_stats.scan_kernel -> kernel name (as rocprofv3 lists it)
-SCAN_KERNELS = {1: "kpe_scan_kernel", 2: "kpe_scan_kernel", 7: "kpe_lean5_kernel"}
+SCAN_KERNELS = {1: "kpe_scan_kernel", 2: "kpe_scan_kernel", 7: "kpe_lean5_kernel", 9: "kpe_lean5_batch_kernel"}
 
 
 def cpu_budget():
@@ -186,7 +188,10 @@ def main():
 
     # ---- timed region: exactly K steps, enqueued by one call (kpe_evaluate_batch_async) ----
     steps_batch = eng.batch([corpora[i % len(corpora)] for i in range(args.steps)])
-    eng.evaluate_batch_async(ps, steps_batch)  # the same K-step batch once, untimed
+    # untimed: one rotation over every shard, in the timed region's order, so that each timed
+    # step's shard was last read a whole rotation earlier (see the module docstring)
+    rotation = eng.batch(corpora)
+    eng.evaluate_batch_async(ps, rotation)
     eng.device.sync()
     barrier()
     torch.cuda.synchronize()
@@ -212,16 +217,19 @@ def main():
     gather = {"rows": n * world, "bytes": 4 * K.packed_words(n * R) * world, "cell_bits": 3, "seconds": gather_s,
               "rows_ok": bool(rank != 0 or (full is not None and full.shape == (n * world, R)))}
 
-    # ---- per-kernel timing pass: HIP events on the library's stream, launches serialised on
-    # one stream so each kernel's duration is its own (isolated, single-stream figure) ----
+    # ---- per-kernel timing pass: the timed region's K steps again, with HIP events around every
+    # launch on the library's stream (launches serialised there, so each duration is its own; a
+    # multi-shard LEAN5 launch covers several steps) ----
+    eng.evaluate_batch_async(ps, rotation)
+    eng.device.sync()
     eng.device.set_timing(True)
     eng.device.kernel_stats(reset=True)
     t1 = time.perf_counter()
-    for i in range(args.steps):
-        eng.evaluate_async(ps, corpora[i % len(corpora)])
+    eng.evaluate_batch_async(ps, steps_batch)
     st = eng.device.kernel_stats(reset=True)
     single_stream_ms = (time.perf_counter() - t1) / args.steps * 1e3
     L = max(st.launches, 1)
+    step_bytes = st.scan_bytes * L / args.steps  # launches carry near-equal shares of the K steps
     scan_ms = st.pss_kernel_ms / L
     dict_ms = st.dict_kernel_ms / L
     pat_ms = st.pattern_kernel_ms / L
@@ -265,7 +273,7 @@ def main():
         try:
             tj = json.load(open(traffic_json))
             # only counters taken on the kernel this run launched (a stale file is not this kernel's)
-            norm = lambda k: k.split("(")[0].replace("void ", "").replace(" ", "")  # noqa: E731
+            norm = lambda k: k.split("(")[0].replace("void ", "").replace(" ", "").split("<")[0]  # noqa: E731
             if norm(tj.get("kernel", "")) == norm(scan_kernel) or (
                     scan_kernel == "kpe_scan_kernel" and norm(tj.get("kernel", "")).startswith("kpe_scan_kernel")):
                 traffic = tj.get("scan_bytes_per_launch")
@@ -305,12 +313,14 @@ def main():
                      "pattern_kernel_ms": pat_ms,
                      # the same bytes over the timed region's step time (launches of different
                      # shards overlap on two streams there) and the isolated single-stream step
-                     "achieved_per_step": st.scan_bytes / (ms_per_step * 1e-3) / 1e9,
+                     "launches": st.launches, "alg_bytes_per_step": step_bytes,
+                     "achieved_per_step": step_bytes / (ms_per_step * 1e-3) / 1e9,
                      "single_stream_step_ms": single_stream_ms,
-                     "note": ("kernel_ms: HIP events, launches serialised on one stream; ms_per_step: "
-                              "wall clock with consecutive shards' launches overlapping on two streams, "
-                              "so ms_per_step can be below kernel_ms; dict / pattern kernel ms are 0 "
-                              "when no such kernel ran")}
+                     "note": ("kernel_ms: HIP events per launch, launches serialised on one stream "
+                              "(kpe_lean5_batch_kernel: one launch over up to 64 shards, i.e. several "
+                              "steps, alg_bytes_per_launch its shards' bytes); other kernels: one launch "
+                              "per step, and consecutive shards' launches overlap on two streams in the "
+                              "timed region; dict / pattern kernel ms are 0 when no such kernel ran")}
         if pat_ms > scan_ms and st.pattern_bytes > 0:
             # pattern-dominated configurations (C3, C5): the dominant kernel is the pattern VM;
             # its algorithmic bytes are every resource's document tape once plus the verdicts

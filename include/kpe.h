@@ -183,8 +183,11 @@ kpe_status kpe_evaluate_async(kpe_device* dev, const kpe_program* prog, const kp
 #define KPE_EVAL_COLD 2u
 kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, unsigned flags);
 /* n evaluations enqueued by one call, corpora cs[0 .. n-1] in order (a corpus may repeat), each
- * as kpe_evaluate_async_ex(dev, prog, cs[i], flags) would enqueue it: the batch form a scanner
- * driving many resident shards (or a benchmark) uses instead of n foreign-function calls. */
+ * with the results kpe_evaluate_async_ex(dev, prog, cs[i], flags) gives: the batch form a scanner
+ * driving many resident shards (or a benchmark) uses instead of n foreign-function calls. A run of
+ * consecutive warm shards whose evaluation is the LEAN5 scan alone (a bound kind-only podSecurity
+ * program, no later kernels) goes out as ceil(m / 64) multi-shard launches of
+ * kpe_lean5_batch_kernel: one grid over the shards' tiles instead of one launch per shard. */
 kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* const* cs, int n,
                                     unsigned flags);
 kpe_status kpe_device_sync(kpe_device* dev);
@@ -290,7 +293,8 @@ long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus
 
 /* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
 typedef struct kpe_kernel_stats {
-  uint64_t launches;        /* evaluations timed since the last reset           */
+  uint64_t launches;        /* timed launches since the last reset: one per evaluation, one per
+                               multi-shard LEAN5 launch of kpe_evaluate_batch_async */
   double pss_kernel_ms;     /* summed duration of the resource-scan kernel      */
   double dict_kernel_ms;    /* summed duration of the dictionary predicate pass */
   double scan_bytes;        /* algorithmic bytes one scan-kernel launch reads+writes */
@@ -301,7 +305,7 @@ typedef struct kpe_kernel_stats {
                                matrix read and written */
   int32_t scan_kernel;      /* the scan instantiation of the last timed launch: 1 kpe_scan_kernel
                                (general), 2 its LEAN instantiation (corpora past 4 GiB of pod
-                               records), 7 kpe_lean5_kernel */
+                               records), 7 kpe_lean5_kernel, 9 kpe_lean5_batch_kernel */
   int32_t pad_;
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);

@@ -475,37 +475,63 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
   return cv_fails(d.rec.x, xo, co & 7u, co & 8u, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & a.cv_union;
 }
 
-// The first kLabCache labels of the lane's resource (or of its namespace), loaded once per tile
-// with independent loads: selector terms then test them from registers (constant indices after
-// unrolling) instead of a dependent label load per requirement and term; longer label lists
-// continue from memory.
+// Label bounds of the lane's resource and of its namespace row, and the selector requirement
+// masks (ScanArgs::selm) once per tile: every selector term is then one mask test. Without masks
+// (more than 64 requirements in a space) a term walks the labels per requirement.
 constexpr uint32_t kLabCache = 8;
 struct LabCache {
   uint32_t lo, hi;    // the resource's labels
   uint32_t nlo, nhi;  // its namespace's labels (namespaceSelector), read from memory
-  uint32_t k[kLabCache], v[kLabCache];
+  uint64_t selq, nsq;  // ScanArgs::selm: requirements that hold on its labels / its namespace's
 };
-__device__ __forceinline__ void lab_fill(LabCache& c, const uint32_t* K, const uint32_t* V, uint32_t lo, uint32_t hi) {
-  c.lo = lo, c.hi = hi;
-#pragma unroll
-  for (uint32_t j = 0; j < kLabCache; ++j) {
-    const bool in = lo + j < hi;
-    c.k[j] = in ? K[lo + j] : KPE_NO_STR;
-    c.v[j] = in ? V[lo + j] : KPE_NO_STR;
-  }
-}
 
 // the resource's label cache (label selectors; a namespace's labels are shared by its
 // resources and stay cache-resident, so namespaceSelector terms read them from memory)
+// Label-selector requirement mask of one resource (ScanArgs::selm bit 0): its labels folded in
+// order. Requirement q is decided by the first label whose key matches it (and whose value
+// matches too, for a wildcard matchLabels entry), as the per-requirement loop of eval_term.
+__device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC) {
+  uint64_t notyet = ~0ull, okacc = 0;
+  const uint64_t nwild = ~a.sm_wild;
+  auto fold = [&](uint32_t k, uint32_t v) {
+    const uint4 kq = k < a.nlabk ? a.sel_km[k] : make_uint4(0u, 0u, 0u, 0u);
+    const uint4 vq = v < a.nlabv ? a.sel_vm[v] : make_uint4(0u, 0u, 0u, 0u);
+    const uint64_t km = kq.x | (uint64_t)kq.y << 32, kok = kq.z | (uint64_t)kq.w << 32;
+    const uint64_t vm = vq.x | (uint64_t)vq.y << 32, vok = vq.z | (uint64_t)vq.w << 32;
+    const uint64_t f = km & (nwild | vm);  // this label is the requirement's first match
+    const uint64_t val = (vm & a.sm_pos) | (kok & vok & a.sm_wild) | (~vm & a.sm_notin);
+    okacc |= f & notyet & val;
+    notyet &= ~f;
+  };
+  uint32_t k[kLabCache], v[kLabCache];  // the first labels with independent loads
+#pragma unroll
+  for (uint32_t j = 0; j < kLabCache; ++j) {
+    const bool in = LC.lo + j < LC.hi;
+    k[j] = in ? a.lab_k[LC.lo + j] : KPE_NO_STR;
+    v[j] = in ? a.lab_v[LC.lo + j] : KPE_NO_STR;
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kLabCache; ++j)
+    if (LC.lo + j < LC.hi) fold(k[j], v[j]);
+#pragma unroll 1
+  for (uint32_t j = LC.lo + kLabCache; j < LC.hi; ++j) fold(a.lab_k[j], a.lab_v[j]);
+  const uint64_t found = ~notyet;
+  return (found & okacc & (a.sm_pos | a.sm_wild)) | ((notyet | okacc) & a.sm_notin) | (found & a.sm_exists) |
+         (notyet & a.sm_dne);
+}
+
 __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC) {
   uint32_t lo = 0, hi = 0;
   if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = live ? a.lab_off[rc + 1] : lo;
-  lab_fill(LC, a.lab_k, a.lab_v, lo, hi);
+  LC.lo = lo, LC.hi = hi;
   LC.nlo = LC.nhi = 0;
+  LC.selq = LC.nsq = 0;
   if (a.need & NEED_NSL) {  // the namespace row's bounds, once per resource instead of per term
     const uint32_t row = a.r_nsl[rc];
     if (live && row != KPE_NO_STR) LC.nlo = a.nsl_off[row], LC.nhi = a.nsl_off[row + 1];
+    if (a.selm & 2u) LC.nsq = a.ns_q[live && row != KPE_NO_STR ? row : a.ns_none];
   }
+  if (a.selm & 1u) LC.selq = sel_fold(a, LC);
 }
 
 // One match term for this lane's resource (utils/match.go:52-160 attributes).
@@ -557,7 +583,10 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
         ok = false, eval = false;
       }
     }
-    if (eval) {
+    if (eval && S.qbit != KPE_NO_QBIT) {  // requirement masks (ScanArgs::selm)
+      const uint64_t need = (S.nreq >= 64u ? ~0ull : ((1ull << S.nreq) - 1ull)) << S.qbit;
+      ok = ((nssel ? LC.nsq : LC.selq) & need) == need;
+    } else if (eval) {
 #pragma unroll 1
       for (uint32_t qi = 0; qi < S.nreq; ++qi) {
         const KpeSelReq q = sld(a.selreqs, S.req0 + qi);
@@ -565,15 +594,8 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
         // first label with a matching key (and value, for wildcards): the cached ones, then memory
         bool found = false;
         uint32_t kid = KPE_NO_STR, vid = KPE_NO_STR;
-        if (!nssel) {
-#pragma unroll
-          for (uint32_t j = 0; j < kLabCache; ++j) {
-            const uint32_t kk = LC.k[j], vv = LC.v[j];
-            if (!found && lo + j < hi && B.bit(q.pk, kk) && (!wild || B.bit(q.pv, vv))) found = true, kid = kk, vid = vv;
-          }
-        }
 #pragma unroll 1
-        for (uint32_t j = nssel ? lo : lo + kLabCache; !found && j < hi; ++j)
+        for (uint32_t j = lo; !found && j < hi; ++j)
           if (B.bit(q.pk, K[j]) && (!wild || B.bit(q.pv, V[j]))) found = true, kid = K[j], vid = V[j];
         bool qok;
         switch (q.op) {
@@ -1269,6 +1291,79 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
     return hipGetLastError();
   }
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
+  return hipGetLastError();
+}
+// ---- selector requirement masks (ScanArgs::selm), once per binding ----------------------------
+__device__ __forceinline__ bool sm_bit(const SelMaskArgs& a, uint32_t loc, uint32_t id) {
+  if (loc == PRED_NONE || id == KPE_NO_STR) return false;
+  const uint32_t w = (loc & PRED_LOCAL) ? a.pimg[(loc & ~PRED_LOCAL) + (id >> 5)] : a.pbuf[loc + (id >> 5)];
+  return (w >> (id & 31u)) & 1u;
+}
+// grid y = 0: label keys (sel_km), 1: label values (sel_vm), 2: namespace rows (ns_q; row nrows:
+// no namespace row, i.e. no labels). The namespace rows run eval_term's requirement loop.
+__global__ void __launch_bounds__(256) kpe_selmask_kernel(SelMaskArgs a) {
+  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+  if (blockIdx.y == 0) {
+    if (i >= a.nlabk) return;
+    uint64_t km = 0, kok = 0;
+    for (uint32_t b = 0; b < a.nrq; ++b) {
+      const KpeSelReq q = a.reqs[a.rq[b]];
+      km |= sm_bit(a, (uint32_t)q.pk, i) ? 1ull << b : 0ull;
+      kok |= q.op == SR_WILD && sm_bit(a, (uint32_t)q.pk_ok, i) ? 1ull << b : 0ull;
+    }
+    a.km[i] = make_uint4((uint32_t)km, (uint32_t)(km >> 32), (uint32_t)kok, (uint32_t)(kok >> 32));
+  } else if (blockIdx.y == 1) {
+    if (i >= a.nlabv) return;
+    uint64_t vm = 0, vok = 0;
+    for (uint32_t b = 0; b < a.nrq; ++b) {
+      const KpeSelReq q = a.reqs[a.rq[b]];
+      const bool has_pv = q.op == SR_EQ || q.op == SR_IN || q.op == SR_NOTIN || q.op == SR_WILD;
+      vm |= has_pv && sm_bit(a, (uint32_t)q.pv, i) ? 1ull << b : 0ull;
+      vok |= q.op == SR_WILD && sm_bit(a, (uint32_t)q.pv_ok, i) ? 1ull << b : 0ull;
+    }
+    a.vm[i] = make_uint4((uint32_t)vm, (uint32_t)(vm >> 32), (uint32_t)vok, (uint32_t)(vok >> 32));
+  } else {
+    if (i > a.nrows) return;
+    const uint32_t lo = i < a.nrows ? a.nsl_off[i] : 0u, hi = i < a.nrows ? a.nsl_off[i + 1] : 0u;
+    uint64_t okm = 0;
+    for (uint32_t b = 0; b < a.nnq; ++b) {
+      const KpeSelReq q = a.reqs[a.nq[b]];
+      const bool wild = q.op == SR_WILD;
+      bool found = false;
+      uint32_t kid = KPE_NO_STR, vid = KPE_NO_STR;
+      for (uint32_t j = lo; !found && j < hi; ++j)
+        if (sm_bit(a, (uint32_t)q.pk, a.nsl_k[j]) && (!wild || sm_bit(a, (uint32_t)q.pv, a.nsl_v[j])))
+          found = true, kid = a.nsl_k[j], vid = a.nsl_v[j];
+      bool qok;
+      switch (q.op) {
+        case SR_EQ:
+        case SR_IN: qok = found && sm_bit(a, (uint32_t)q.pv, vid); break;
+        case SR_WILD: qok = found && sm_bit(a, (uint32_t)q.pk_ok, kid) && sm_bit(a, (uint32_t)q.pv_ok, vid); break;
+        case SR_NOTIN: qok = !found || !sm_bit(a, (uint32_t)q.pv, vid); break;
+        case SR_EXISTS: qok = found; break;
+        default: qok = !found; break;
+      }
+      okm |= qok ? 1ull << b : 0ull;
+    }
+    a.nsq[i] = okm;
+  }
+}
+extern "C" hipError_t kpe_launch_selmask(const SelMaskArgs* a, hipStream_t s) {
+  const uint32_t m = std::max(std::max(a->nlabk, a->nlabv), a->nrows + 1);
+  hipLaunchKernelGGL(kpe_selmask_kernel, dim3((m + 255u) / 256u, 3), dim3(256), 0, s, *a);
+  return hipGetLastError();
+}
+// Several bound shards of one LEAN5 program in one grid (kpe_evaluate_batch_async).
+extern "C" hipError_t kpe_launch_lean_batch(const LeanBatchArgs* a, size_t dyn_bytes, hipStream_t s) {
+  const uint32_t grid = a->blk0[a->nshards];
+  if (a->nshards == 0 || grid == 0) return hipSuccess;
+  switch (a->tpw) {
+    case 8: hipLaunchKernelGGL(kpe_lean5_batch_kernel<8>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
+    case 4: hipLaunchKernelGGL(kpe_lean5_batch_kernel<4>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
+    case 2: hipLaunchKernelGGL(kpe_lean5_batch_kernel<2>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
+    case 1: hipLaunchKernelGGL(kpe_lean5_batch_kernel<1>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 // The per-pod PSA summary of a corpus (lean.inl): dictionary codes, capability-set codes, then

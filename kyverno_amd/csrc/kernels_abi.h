@@ -162,6 +162,19 @@ struct ScanArgs {
   // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask (PRED_NONE: no table)
   uint32_t kt_lds, nkinds;
   const uint32_t* psum;  // LEAN5: per-pod scan records (3 words per pod: pod word, schema.h PS_* summary | kind << 16)
+  // Selector requirement masks (selm bit 0: label selectors, bit 1: namespaceSelectors; built
+  // per binding by kpe_selmask_kernel). Requirement q of a selector is bit qbit + q. Label
+  // selectors: sel_km[key id] = {requirements whose key glob holds, wildcard requirements whose
+  // key is a valid qualified name} and sel_vm[value id] = {requirements whose value set holds,
+  // wildcard requirements whose value is a valid label value}, 64-bit each, folded per row over
+  // its labels in order; sm_* = the requirements of each operator class. namespaceSelectors:
+  // ns_q[namespace row] = the requirements that hold on that namespace's labels (row ns_none:
+  // a resource without a namespace row).
+  const uint4* sel_km;
+  const uint4* sel_vm;
+  const uint64_t* ns_q;
+  uint32_t selm, ns_none, nlabk, nlabv;
+  uint64_t sm_pos, sm_wild, sm_notin, sm_exists, sm_dne;
   // outputs
   uint8_t* verdicts;  // n x nrules
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null
@@ -196,6 +209,41 @@ struct PsumArgs {
   uint8_t* codes[4];     // code byte per dictionary string (scratch)
   uint8_t* csb;          // code byte per capability set (scratch)
   uint32_t* psum;        // out: 3 words per pod (pod word, OR of container states, codes | kind << 16)
+};
+
+// kpe_selmask_kernel: the selector requirement masks of a binding (ScanArgs::sel_km / sel_vm /
+// ns_q) from the predicate bitsets (prologue image for local ones, pbuf for the rest).
+struct SelMaskArgs {
+  const uint32_t* pimg;      // prologue image: local bitsets at their LDS word index
+  const uint32_t* pbuf;      // global bitsets
+  const KpeSelReq* reqs;     // resolved requirement records (binding copy)
+  const uint32_t* rq;        // label-selector requirement of bit b (selreqs index), nrq entries
+  const uint32_t* nq;        // namespaceSelector requirement of bit b, nnq entries
+  uint32_t nrq, nnq, nlabk, nlabv, nrows;  // nrows: namespace label table rows (ns_q has nrows + 1)
+  uint32_t pad_;
+  const uint32_t *nsl_off, *nsl_k, *nsl_v;
+  uint4* km;                 // out: nlabk entries
+  uint4* vm;                 // out: nlabv entries
+  uint64_t* nsq;             // out: nrows + 1 entries
+};
+
+// kpe_lean5_batch_kernel: one launch over up to KPE_LEAN_BATCH bound shards of one LEAN5 program
+// (kpe_evaluate_batch_async). Passed by value (< 4 KiB of kernel arguments): block b of the grid
+// belongs to the shard s with blk0[s] <= b < blk0[s + 1].
+#define KPE_LEAN_BATCH 64
+struct LeanShard {
+  const uint32_t* psum;   // 3 words per pod (PsumArgs::psum)
+  const uint32_t* kt;     // the binding's kind table: matched-rule mask per kind id (prologue image)
+  uint8_t* verdicts;      // n x R
+  uint32_t* masks;        // n x R failing versioned checks, or null
+  uint32_t n, nkinds;
+};
+struct LeanBatchArgs {
+  uint32_t nshards, nrules, ncls, cv_union, pss_rules, err_rules, pat_rules, kt_words;  // kt_words: max nkinds
+  const uint32_t* narrow_cls;  // (cv classes, rule mask) pairs of the program
+  uint32_t blk0[KPE_LEAN_BATCH + 1];  // a block covers 4 * tpw tiles of 64 pods
+  uint32_t tpw;                       // tiles per wave: 1, 2, 4 or 8
+  LeanShard sh[KPE_LEAN_BATCH];
 };
 
 // kpe_pattern_kernel arguments (device-resident, one copy per binding)

@@ -46,6 +46,8 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
 extern "C" hipError_t kpe_launch_psum(const PsumArgs* a, hipStream_t s);
+extern "C" hipError_t kpe_launch_lean_batch(const LeanBatchArgs* a, size_t dyn_bytes, hipStream_t s);
+extern "C" hipError_t kpe_launch_selmask(const SelMaskArgs* a, hipStream_t s);
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
                                        hipStream_t s);
 
@@ -108,6 +110,8 @@ constexpr uint32_t kMaxTerms = 1024;       // distinct match terms (term masks: 
 constexpr uint32_t kMaxProgLds = 4096;     // filters + filter terms staged in LDS
 constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
 constexpr uint32_t kMaxFuseWords = 4096;   // fuse image <= 16 KiB of LDS
+constexpr uint32_t kLeanBatchKinds = 8192; // kind table words a multi-shard LEAN5 block stages
+constexpr uint64_t kLeanBatchMinWaves = 16384;  // 256 CUs x 4 SIMDs x 16 waves
 constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated per block
 
 }  // namespace
@@ -200,6 +204,10 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   ScanArgs hargs{};    // what dargs holds
   bool args_valid = false;
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
+  // selector requirement masks (ScanArgs::selm): requirement lists per space, the tables
+  DevBuf sel_rq, sel_nq, sel_km, sel_vm, sel_nsq;
+  uint32_t selm = 0, sel_nrq = 0, sel_nnq = 0;
+  uint64_t sm[5] = {};  // pos (EQ / In), wild, NotIn, Exists, DoesNotExist
   uint32_t pp[10] = {};  // fixed PSS predicate locations
   uint32_t wave_lds = 0, wave_words = 0, filt_lds = PRED_NONE, fterm_lds = 0, tt_lds = PRED_NONE;
   size_t dyn_bytes = 0;
@@ -878,6 +886,38 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   std::vector<KpeSelReq> selreqs = P.selreqs;
   for (auto& x : selreqs)
     x.pk = (int32_t)loc(x.pk), x.pv = (int32_t)loc(x.pv), x.pk_ok = (int32_t)loc(x.pk_ok), x.pv_ok = (int32_t)loc(x.pv_ok);
+  {  // selector requirement masks: one bit per requirement of each space, when it fits 64
+    std::vector<uint32_t> rsel, nsel, rq, nq;
+    for (const auto& t : P.terms)
+      if (t.type == T_SELECTOR) rsel.push_back(t.a);
+      else if (t.type == T_NSSELECTOR) nsel.push_back(t.a);
+    for (auto& x : selectors) x.qbit = KPE_NO_QBIT;
+    auto assign = [&](const std::vector<uint32_t>& sels, std::vector<uint32_t>& bits) -> bool {
+      size_t tot = 0;
+      for (uint32_t si : sels) tot += selectors[si].nreq;
+      if (sels.empty() || tot > 64) return false;
+      for (uint32_t si : sels) {
+        selectors[si].qbit = (uint32_t)bits.size();
+        for (uint32_t q = 0; q < selectors[si].nreq; ++q) bits.push_back(selectors[si].req0 + q);
+      }
+      return true;
+    };
+    B.selm = (assign(rsel, rq) ? 1u : 0u) | (assign(nsel, nq) ? 2u : 0u);
+    for (auto& m : B.sm) m = 0;
+    for (size_t b = 0; b < rq.size(); ++b) {
+      const uint32_t op = selreqs[rq[b]].op;
+      const int k = op == SR_EQ || op == SR_IN ? 0 : op == SR_WILD ? 1 : op == SR_NOTIN ? 2 : op == SR_EXISTS ? 3 : 4;
+      B.sm[k] |= 1ull << b;
+    }
+    B.sel_nrq = (uint32_t)rq.size(), B.sel_nnq = (uint32_t)nq.size();
+    if (B.selm) {
+      HIPCHK(upload(B.sel_rq, rq.empty() ? std::vector<uint32_t>{0} : rq, s));
+      HIPCHK(upload(B.sel_nq, nq.empty() ? std::vector<uint32_t>{0} : nq, s));
+      HIPCHK(B.sel_km.ensure((size_t)std::max<uint32_t>(C.dict[D_LABK].size(), 1) * 16));
+      HIPCHK(B.sel_vm.ensure((size_t)std::max<uint32_t>(C.dict[D_LABV].size(), 1) * 16));
+      HIPCHK(B.sel_nsq.ensure(C.nsl_off.size() * 8));
+    }
+  }
   HIPCHK(upload(B.terms_r, terms, s));
   HIPCHK(upload(B.kindsels_r, kindsels, s));
   HIPCHK(upload(B.annpairs_r, annpairs, s));
@@ -1030,8 +1070,9 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   }
   if (getenv("KPE_DEBUG")) {
     fprintf(stderr, "kpe bind: n=%lld R=%zu narrow=%d blob=%u pred_jobs=%u pred_xblocks=%u scan_blocks=%u dyn=%zu "
-            "wave_words=%u npairs=%u fuse_words=%u ncapsets=%zu\n", (long long)C.n, P.rules.size(), (int)narrow, blob,
-            (unsigned)jobs.size(), blk, B.scan_blocks, B.dyn_bytes, wave_words, B.npairs, fuse_words, C.capset_add.size());
+            "wave_words=%u npairs=%u fuse_words=%u ncapsets=%zu selm=%u (%u, %u requirement bits)\n", (long long)C.n,
+            P.rules.size(), (int)narrow, blob, (unsigned)jobs.size(), blk, B.scan_blocks, B.dyn_bytes, wave_words, B.npairs,
+            fuse_words, C.capset_add.size(), B.selm, B.sel_nrq, B.sel_nnq);
   }
   HIPCHK(hipStreamSynchronize(s));
   B.need = need_flags(P);
@@ -1166,6 +1207,13 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
   sa.psum = D.psum_ready ? D.psum.as<uint32_t>() : nullptr;
+  sa.selm = B.selm;
+  if (B.selm) {
+    sa.sel_km = B.sel_km.as<uint4>(), sa.sel_vm = B.sel_vm.as<uint4>(), sa.ns_q = B.sel_nsq.as<uint64_t>();
+    sa.ns_none = (uint32_t)C.nsl_off.size() - 1;
+    sa.nlabk = C.dict[D_LABK].size(), sa.nlabv = C.dict[D_LABV].size();
+    sa.sm_pos = B.sm[0], sa.sm_wild = B.sm[1], sa.sm_notin = B.sm[2], sa.sm_exists = B.sm[3], sa.sm_dne = B.sm[4];
+  }
   sa.verdicts = B.verdicts.as<uint8_t>();
   sa.masks = masks ? B.masks.as<uint32_t>() : nullptr;
   if (!B.args_valid || memcmp(&sa, &B.hargs, sizeof(ScanArgs)) != 0) {  // once per binding / masks mode
@@ -1177,6 +1225,19 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (sa.pimg && fresh)
     HIPCHK(kpe_launch_prep(B.dargs.as<ScanArgs>(), P.any_pss ? 1 : 0, PD.narrow ? 1 : 0, B.prep_dyn_bytes, s));
+  if (B.selm && fresh) {  // selector requirement masks, from the image's and pbuf's bitsets
+    SelMaskArgs ma{};
+    ma.pimg = B.pimg.as<uint32_t>();
+    ma.pbuf = B.pbuf.as<uint32_t>();
+    ma.reqs = B.selreqs_r.as<KpeSelReq>();
+    ma.rq = B.sel_rq.as<uint32_t>(), ma.nq = B.sel_nq.as<uint32_t>();
+    ma.nrq = B.sel_nrq, ma.nnq = B.sel_nnq;
+    ma.nlabk = C.dict[D_LABK].size(), ma.nlabv = C.dict[D_LABV].size();
+    ma.nrows = (uint32_t)C.nsl_off.size() - 1;
+    ma.nsl_off = D.nsl_off.as<uint32_t>(), ma.nsl_k = D.nsl_k.as<uint32_t>(), ma.nsl_v = D.nsl_v.as<uint32_t>();
+    ma.km = B.sel_km.as<uint4>(), ma.vm = B.sel_vm.as<uint4>(), ma.nsq = B.sel_nsq.as<uint64_t>();
+    HIPCHK(kpe_launch_selmask(&ma, s));
+  }
   B.inv_ready = true;
   ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
@@ -1357,6 +1418,87 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   return KPE_OK;
 }
 
+// A shard can ride in a multi-shard LEAN5 launch when its evaluation is that one kernel: a bound
+// LEAN5 binding (prologue image and PSA summary built) of a program with no later kernels, and
+// no rows past an encoding limit.
+bool lean_batchable(const kpe_program* pp, const kpe_corpus* cc) {
+  static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
+  const auto& P = *pp->p;
+  const auto& C = *cc->c;
+  const auto& D = *cc->d;
+  const auto& B = D.bind;
+  return !no_cache && B.prog == &P && B.inv_ready && B.lean && B.lean_kind == 7 && D.psum_ready && C.n > 0 &&
+         B.nkinds <= kLeanBatchKinds && P.cond.rules.empty() && P.pssx.rules.empty() && P.pat.rules.empty() &&
+         !B.napply_segs && C.limit_rows.empty();
+}
+
+// The shards of `run` in ceil(m / KPE_LEAN_BATCH) launches of near-equal size on the device
+// stream (equal per-launch bytes, so a launch's events time the same work); clears `run`.
+kpe_status launch_lean_run(kpe_device* dev, const kpe_program* pp, std::vector<kpe_corpus*>& run, bool masks) {
+  if (run.empty()) return KPE_OK;
+  if (run.size() == 1) {
+    kpe_corpus* c = run[0];
+    run.clear();
+    return launch(dev, pp, c, masks);
+  }
+  auto& P = *pp->p;
+  auto& PD = *P.devs[dev->ordinal];
+  const uint32_t R = (uint32_t)P.rules.size();
+  hipStream_t s = dev->stream;
+  const size_t m = run.size(), nl = (m + KPE_LEAN_BATCH - 1) / KPE_LEAN_BATCH;
+  for (size_t l = 0, i = 0; l < nl; ++l) {
+    const size_t cnt = (m - i) / (nl - l);
+    LeanBatchArgs a;
+    memset(&a, 0, sizeof(a));
+    a.nshards = (uint32_t)cnt, a.nrules = R, a.ncls = PD.ncls, a.cv_union = P.cv_union;
+    a.pss_rules = PD.pss_rules, a.err_rules = PD.err_rules, a.pat_rules = PD.pat_rules;
+    a.narrow_cls = PD.narrow_cls.as<uint32_t>();
+    // tiles per wave: the most (up to 8) that still leaves >= 16 waves per SIMD of the chip
+    uint64_t tiles = 0;
+    for (size_t k = 0; k < cnt; ++k) tiles += (uint64_t)(run[i + k]->c->n + 63) / 64;
+    uint32_t tpw = 8;
+    while (tpw > 1 && tiles / tpw < kLeanBatchMinWaves) tpw >>= 1;
+    a.tpw = tpw;
+    uint32_t acc = 0, ktw = 0;
+    double bytes = 0;
+    for (size_t k = 0; k < cnt; ++k, ++i) {
+      auto& C = *run[i]->c;
+      auto& D = *run[i]->d;
+      auto& B = D.bind;
+      if (B.last && B.last != s) HIPCHK(hipStreamSynchronize(B.last));  // keep this corpus's launches ordered
+      B.last = s;
+      LeanShard& sh = a.sh[k];
+      sh.psum = D.psum.as<uint32_t>();
+      sh.kt = B.pimg.as<uint32_t>() + B.kt_lds;
+      sh.verdicts = B.verdicts.as<uint8_t>();
+      sh.masks = masks ? B.masks.as<uint32_t>() : nullptr;
+      sh.n = (uint32_t)C.n, sh.nkinds = B.nkinds;
+      a.blk0[k] = acc;
+      acc += (uint32_t)((C.n + 256 * tpw - 1) / (256 * tpw));  // 4 waves x tpw tiles of 64 pods per block
+      ktw = std::max(ktw, B.nkinds);
+      bytes += (12.0 + R) * (double)C.n + (masks ? 4.0 * R * (double)C.n : 0.0);
+    }
+    a.blk0[cnt] = acc;
+    a.kt_words = (ktw + 3u) & ~3u;
+    const size_t dyn = (size_t)a.kt_words * 4 + 4 * 64 * (size_t)R;
+    kpe_device::EvPair ev{};
+    if (dev->timing) {
+      ev.a = dev->get_ev(), ev.b = dev->get_ev(), ev.c = dev->get_ev(), ev.d = dev->get_ev();
+      HIPCHK(hipEventRecord(ev.a, s));
+      HIPCHK(hipEventRecord(ev.b, s));
+    }
+    HIPCHK(kpe_launch_lean_batch(&a, dyn, s));
+    if (dev->timing) {
+      HIPCHK(hipEventRecord(ev.c, s));
+      HIPCHK(hipEventRecord(ev.d, s));
+      ev.bytes = bytes, ev.pbytes = 0, ev.kind = 9, ev.pre = ev.post = false;
+      dev->pending.push_back(ev);
+    }
+  }
+  run.clear();
+  return KPE_OK;
+}
+
 kpe_status prepare(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, bool masks) {
   if (!dev || !prog || !c) return fail(KPE_E_INVALID, "null argument");
   if (!c->d || c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
@@ -1393,13 +1535,21 @@ kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, co
   if (!dev || (n > 0 && !cs)) return fail(KPE_E_INVALID, "null argument");
   if (flags & ~(unsigned)(KPE_EVAL_MASKS | KPE_EVAL_COLD)) return fail(KPE_E_INVALID, "unknown evaluation flags");
   std::lock_guard<std::mutex> lk(dev->mu);
-  const bool masks = (flags & KPE_EVAL_MASKS) != 0;
+  const bool masks = (flags & KPE_EVAL_MASKS) != 0, cold = (flags & KPE_EVAL_COLD) != 0;
+  // Consecutive shards whose evaluation is the LEAN5 scan alone go out as multi-shard launches
+  // (kpe_lean5_batch_kernel); any other shard is launched on its own, in order.
+  std::vector<kpe_corpus*> run;
   for (int i = 0; i < n; ++i) {
     if (kpe_status st = prepare(dev, prog, cs[i], masks)) return st;
-    if (kpe_status st = launch(dev, prog, const_cast<kpe_corpus*>(cs[i]), masks, (flags & KPE_EVAL_COLD) != 0))
-      return st;
+    kpe_corpus* c = const_cast<kpe_corpus*>(cs[i]);
+    if (!cold && lean_batchable(prog, c)) {
+      run.push_back(c);
+      continue;
+    }
+    if (kpe_status st = launch_lean_run(dev, prog, run, masks)) return st;
+    if (kpe_status st = launch(dev, prog, c, masks, cold)) return st;
   }
-  return KPE_OK;
+  return launch_lean_run(dev, prog, run, masks);
 }
 
 kpe_status kpe_device_sync(kpe_device* dev) {

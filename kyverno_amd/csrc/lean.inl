@@ -234,3 +234,84 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArg
   __builtin_amdgcn_wave_barrier();
   store_rows(a0.verdicts, sv, tile, R, 0, R, min(64u, n - tile * 64u), lane);
 }
+
+typedef const __attribute__((address_space(4))) LeanBatchArgs CBArgs;
+// ---- kpe_lean5_batch_kernel: many shards in one launch ---------------------------------------
+// The same per-pod evaluation as kpe_lean5_kernel over up to KPE_LEAN_BATCH bound shards of one
+// program (each with its own corpus dictionaries, hence its own kind table): the shards' blocks
+// are one grid, so a batch of K steps costs one launch and one ramp instead of K. Every block
+// finds its shard by a scalar binary search over LeanBatchArgs::blk0 (kernel arguments) and
+// stages only that shard's kind table in LDS. A wave takes T tiles of its block's 4T (tiles
+// b*4T + 4i + wave): the T record loads are issued together, then the tiles are evaluated and
+// stored one by one. One tile per wave leaves a streaming launch bound by the wave launch rate
+// (20 shards, 312k waves: 2.9 TB/s).
+template <int T>
+__global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_batch_kernel(LeanBatchArgs) {
+  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+  CBArgs& a = *(CBArgs*)kargs();
+  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
+  const uint32_t gb = xcd_block(blockIdx.x, gridDim.x);
+  uint32_t lo = 0, hi = a.nshards;  // blk0[lo] <= gb < blk0[hi]
+  while (hi - lo > 1u) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.blk0[mid] <= gb) lo = mid;
+    else hi = mid;
+  }
+  const __attribute__((address_space(4))) LeanShard& S = a.sh[lo];
+  const uint32_t n = S.n, tile0 = (gb - a.blk0[lo]) * (4u * T) + wv;
+  const Rsrc PS = make_rsrc(S.psum, n * 12u);
+  uint3 sr[T];
+#pragma unroll
+  for (int i = 0; i < T; ++i) sr[i] = bload3(PS, ((tile0 + 4u * i) * 64u + lane) * 12u);  // past n: zeros
+  const uint32_t nk = S.nkinds;
+  const uint32_t k0 = t < nk ? S.kt[t] : 0u;
+  uint32_t cls_cv = 0, cls_rm = 0;
+  const uint32_t ncls = a.ncls;
+  if (lane < ncls) {
+    const uint2 c = reinterpret_cast<const uint2*>(a.narrow_cls)[lane];
+    cls_cv = c.x, cls_rm = c.y;
+  }
+  if (t < nk) dyn[t] = k0;
+#pragma unroll 1
+  for (uint32_t i = t + kLB; i < nk; i += kLB) dyn[i] = S.kt[i];
+  __syncthreads();
+  const uint32_t R = a.nrules, cv_union = a.cv_union, pss_rules = a.pss_rules;
+  const uint32_t ep_rules = a.err_rules | a.pat_rules, pat_rules = a.pat_rules;
+  uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a.kt_words) + wv * 64u * R;
+#pragma unroll
+  for (int i = 0; i < T; ++i) {
+    const uint32_t tile = tile0 + 4u * i;
+    if (tile * 64u >= n) break;
+    const uint32_t r = tile * 64u + lane;
+    const bool live = r < n;
+    const uint32_t pw = sr[i].x, y = sr[i].z;
+    const uint32_t fails = cv_fails(pw, sr[i].y, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
+                                    PS_ANN(y) & 1u, PS_ANN(y) & 2u) & cv_union;
+    const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
+    const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
+    const uint32_t kind = y >> 16;
+    const uint32_t matched = live && kind < nk ? dyn[kind] : 0u;
+    uint32_t failr = 0;
+#pragma unroll 1
+    for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+    const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
+    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
+    const uint32_t P = matched & pss_rules & ~failr & ~E;
+    __builtin_amdgcn_wave_barrier();  // the previous tile's rows are out of the staging area
+#pragma unroll 1
+    for (uint32_t ri = 0; ri < R; ++ri)
+      sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    if (S.masks && live) {
+      uint32_t* mrow = S.masks + (size_t)r * R;
+      const uint32_t fm = F & pss_rules;
+#pragma unroll 1
+      for (uint32_t ri = 0; ri < R; ++ri) {
+        uint32_t cv = 0;
+        for (uint32_t c = 0; c < ncls; ++c) cv = ((hw(cls_rm, c) >> ri) & 1u) ? hw(cls_cv, c) : cv;
+        mrow[ri] = ((fm >> ri) & 1u) ? (fails & cv) : 0u;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    store_rows(S.verdicts, sv, tile, R, 0, R, min(64u, n - tile * 64u), lane);
+  }
+}

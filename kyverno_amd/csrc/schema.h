@@ -354,8 +354,10 @@ typedef struct KpeSelector {
   uint32_t invalid;      // namespaceSelector that fails to build (false wherever it is evaluated)
   uint32_t exc;          // PolicyException block (pkg/utils/match/match.go:184-193): not checked
                          // for kind Namespace or an empty kind
-  uint32_t pad;
+  uint32_t qbit;         // binding: first bit of the selector's requirements in the per-row
+                         // requirement mask (ScanArgs::selm), KPE_NO_QBIT: evaluated per requirement
 } KpeSelector;
+#define KPE_NO_QBIT 0xFFFFFFFFu
 #define SR_EQ 0u        // matchLabels k: v (no wildcards): first label with key k has value v
 #define SR_WILD 1u      // matchLabels with wildcards: first label matching both globs, and that
                         // label is a valid key/value (else LabelSelectorAsSelector fails)

@@ -304,6 +304,19 @@ class Engine:
                 "undecided": c.undecided} for c in counts[:R]]
         return v, m, cnt
 
+    def fetch(self, ps: PolicySet, corpus: Corpus, check_masks=False):
+        """(verdicts, masks or None, counts) of the last enqueued evaluation of ps on corpus
+        (kpe_fetch): the read-back half of evaluate_async / evaluate_batch_async."""
+        N, R = corpus.n, ps.num_rules
+        v = np.zeros((N, R), dtype=np.uint8)
+        m = np.zeros((N, R), dtype=np.uint32) if check_masks else None
+        counts = (Counts * max(R, 1))()
+        check(load().kpe_fetch(self.device.h, ps.h, corpus.h, v.ctypes.data if N * R else None,
+                               m.ctypes.data if (m is not None and N * R) else None, counts))
+        cnt = [{"na": c.na, "pass": c.pass_, "fail": c.fail, "warn": c.warn, "error": c.error, "skip": c.skip,
+                "undecided": c.undecided} for c in counts[:R]]
+        return v, m, cnt
+
     def cv_masks(self, ps: PolicySet, corpus: Corpus):
         """Failing versioned PSS checks (N x R uint32, bit v = kpe_pss_cv_check(v)) of the last
         evaluation with check_masks=True (kpe_fetch_cv_masks)."""

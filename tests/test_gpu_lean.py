@@ -68,3 +68,88 @@ def test_lean5_full_matrix_every_version(engine, oracle, corpus, level):
         assert bad.size == 0, (level, ver, len(bad), bad[:5].tolist())
         if level != "privileged":
             assert fail.sum() > 0 and (got[fail] != 0).all()
+
+
+def test_lean5_batch_launch(engine, oracle):
+    """kpe_evaluate_batch_async over warm LEAN5 shards of different sizes (one pod, a partial
+    tile, repeats in one launch): one kpe_lean5_batch_kernel launch, and every shard's verdict
+    matrix (poisoned on the device beforehand) and check masks equal the oracle's."""
+    import ctypes
+    from tests.golden.make_psum_digests import seccomp_ndjson
+    pols = [pss_policy("restricted-latest", "restricted", "latest")]
+    ps = K.PolicySet(pols)
+    nds = [K.synth_resources(0x61, 5000, mix=1), K.synth_resources(0x62, 1, mix=1),
+           K.synth_resources(0x63, 64, mix=2), K.synth_resources(0x64, 20000, mix=2), seccomp_ndjson(777)]
+    cs = [K.Corpus(nd, docs=False).upload(engine.device) for nd in nds]
+    refs = [oracle.validate(pols, nd, nthreads=8) for nd in nds]
+    hip = ctypes.CDLL("libamdhip64.so")
+    for masks in (False, True):
+        for c in cs:  # bind (prologue image, PSA summary), then poison the verdicts
+            engine.evaluate(ps, c, check_masks=masks)
+            ptr, nb = engine.device_verdicts(ps, c)
+            assert hip.hipMemset(ctypes.c_void_p(ptr), 0xFF, ctypes.c_size_t(nb)) == 0
+        assert hip.hipDeviceSynchronize() == 0
+        order = [0, 1, 2, 3, 4, 3, 0]
+        engine.device.set_timing(True)
+        engine.device.kernel_stats(reset=True)
+        engine.evaluate_batch_async(ps, [cs[i] for i in order], masks=masks)
+        st = engine.device.kernel_stats(reset=True)
+        engine.device.set_timing(False)
+        assert st.launches == 1 and st.scan_kernel == 9, (st.launches, st.scan_kernel)
+        engine.device.sync()
+        for i, (c, ref) in enumerate(zip(cs, refs)):
+            v, m, _ = engine.fetch(ps, c, check_masks=masks)
+            bad = np.argwhere(v != ref)
+            assert bad.size == 0, (masks, i, len(bad), bad[:5].tolist())
+            if masks:
+                want_row = oracle.failing_cv_batch("restricted", "latest", nds[i])
+                fail = v == 2
+                want = np.where(fail, np.maximum(want_row, 0)[:, None], 0).astype(np.int64)
+                got = engine.cv_masks(ps, c).astype(np.int64)
+                assert np.array_equal(got, want), (i, int((got != want).sum()))
+
+
+def test_lean5_batch_many_shards(engine, oracle):
+    """More than 64 shards in one call: near-equal multi-shard launches, verdicts unchanged."""
+    pols = [pss_policy("baseline-latest", "baseline", "latest")]
+    ps = K.PolicySet(pols)
+    nd = K.synth_resources(0x65, 3000, mix=1)
+    cs = [K.Corpus(nd, docs=False).upload(engine.device) for _ in range(3)]
+    ref = oracle.validate(pols, nd, nthreads=8)
+    for c in cs:
+        engine.evaluate(ps, c)
+    engine.device.set_timing(True)
+    engine.device.kernel_stats(reset=True)
+    engine.evaluate_batch_async(ps, [cs[i % 3] for i in range(130)])
+    st = engine.device.kernel_stats(reset=True)
+    engine.device.set_timing(False)
+    assert st.launches == 3 and st.scan_kernel == 9
+    assert abs(st.scan_bytes - 44 * 3000 * (12 + 3)) < 1  # 130 -> 43 + 43 + 44 shards
+    engine.device.sync()
+    for c in cs:
+        v, _, _ = engine.fetch(ps, c)
+        assert np.array_equal(v, ref)
+
+
+def test_lean5_batch_tiles_per_wave(engine):
+    """A batch large enough for 8 tiles per wave (one 1M + 37-pod shard nine times: 140k tiles;
+    the last block of every shard partial): the same verdicts as the single-shard kernel, whose
+    parity with the oracle the tests above pin."""
+    import ctypes
+    pols = [pss_policy("restricted-latest", "restricted", "latest")]
+    ps = K.PolicySet(pols)
+    c = K.Corpus(K.synth_resources(0x66, 1_000_037, mix=1), docs=False).upload(engine.device)
+    want, _, _ = engine.evaluate(ps, c)
+    ptr, nb = engine.device_verdicts(ps, c)
+    hip = ctypes.CDLL("libamdhip64.so")
+    assert hip.hipMemset(ctypes.c_void_p(ptr), 0xFF, ctypes.c_size_t(nb)) == 0
+    assert hip.hipDeviceSynchronize() == 0
+    engine.device.set_timing(True)
+    engine.device.kernel_stats(reset=True)
+    engine.evaluate_batch_async(ps, [c] * 9)
+    st = engine.device.kernel_stats(reset=True)
+    engine.device.set_timing(False)
+    assert st.launches == 1 and st.scan_kernel == 9
+    engine.device.sync()
+    got, _, _ = engine.fetch(ps, c)
+    assert np.array_equal(got, want)

@@ -139,3 +139,27 @@ def test_c4_selectors_bit_exact(engine, oracle, n, seed):
     assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()}"
     for r in range(v.shape[1]):
         assert cnt[r]["pass"] == int((v[:, r] == 1).sum()) and cnt[r]["na"] == int((v[:, r] == 0).sum())
+
+
+@pytest.mark.parametrize("copies", [1, 4, 8, 9])
+def test_selector_requirement_masks_and_fallback(engine, oracle, copies):
+    """Selector terms decided from the per-binding requirement masks (<= 64 requirements per
+    space: label selectors, namespaceSelectors) and, past 64, by the per-requirement label walk:
+    C4's policy set (19 label-selector and 8 namespaceSelector requirements that build) repeated
+    `copies` times: 1 both spaces masked; 4 label selectors past 64; 8 namespaceSelectors at
+    exactly 64 bits; 9 both past 64. Bit-exact against the oracle."""
+    import copy as _copy
+    from tests.policies import c4_policy_set
+
+    pols = []
+    for k in range(copies):
+        for p in c4_policy_set():
+            q = _copy.deepcopy(p)
+            q["metadata"]["name"] += f"-{k}"
+            pols.append(q)
+    nd = K.synth_resources(0x5E1 + copies, 30000, mix=3)
+    nsl = K.synth_ns_labels(0x5E1, 10000, mix=3)
+    v, _, _ = _gpu(engine, pols, nd, nsl)
+    ref = oracle.validate(pols, nd, ns_labels=nsl, nthreads=16)
+    bad = np.argwhere(v != ref)
+    assert bad.size == 0, f"{len(bad)} mismatching cells, first {bad[:5].tolist()}"
