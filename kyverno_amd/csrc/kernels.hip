@@ -1114,6 +1114,8 @@ namespace {
 #ifndef KPE_PAT_MINW
 #define KPE_PAT_MINW 3  // 168 VGPRs: the inline map path spills at 128 (profiles/r03_e_inline)
 #endif
+// LT: the leaf-table instance (PatVMT LT), for programs whose leaves all have table slots.
+template <bool LT>
 __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
   constexpr uint32_t kWaveWords = FramesLds::kWords * FramesLds::kDepth * 64u;
   __shared__ uint32_t s_fs[KPE_PAT_BLOCK / 64][kWaveWords];
@@ -1121,7 +1123,31 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
   const int64_t i = (int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x;
   if (i >= ap->n) return;
   const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
-  pat_eval_row(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]}, &s_memo[0][threadIdx.x], KPE_PAT_BLOCK);
+  pat_eval_row<FramesLds, LT>(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]}, &s_memo[0][threadIdx.x],
+                              KPE_PAT_BLOCK);
+}
+
+// Leaf table of a binding (PatArgs::ltab): grid y = slot, one thread per scalar of the corpus;
+// a wave's 64 results are one ballot, stored as two words (ltab_words covers whole waves).
+__global__ void __launch_bounds__(256) kpe_leaf_table_kernel(const PatArgs* __restrict__ ap,
+                                                             const uint32_t* __restrict__ slot_leaf) {
+  const PatArgs& a = *ap;
+  const uint32_t sid = blockIdx.x * 256u + threadIdx.x, slot = blockIdx.y;
+  uint32_t und = 0;
+  const bool r = sid < a.nscal && pat_leaf_eval(a, sid, slot_leaf[slot], nullptr, &und);
+  const uint64_t m = __ballot(r);
+  if ((threadIdx.x & 63u) == 0u && sid < a.nscal) {
+    uint32_t* w = a.ltab + (size_t)slot * a.ltab_words + (sid >> 5);
+    w[0] = (uint32_t)m;
+    w[1] = (uint32_t)(m >> 32);
+  }
+}
+extern "C" hipError_t kpe_launch_leaf_table(const PatArgs* dargs, const uint32_t* slot_leaf, uint32_t nslots,
+                                            uint64_t nscal, hipStream_t s) {
+  if (nslots == 0 || nscal == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_leaf_table_kernel, dim3((unsigned)((nscal + 255) / 256), nslots), dim3(256), 0, s, dargs,
+                     slot_leaf);
+  return hipGetLastError();
 }
 
 // ===========================================================================
@@ -1232,12 +1258,13 @@ extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint6
   return hipGetLastError();
 }
 
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s) {
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lt, hipStream_t s) {
   if (n <= 0 || npr == 0) return hipSuccess;
   // one lane per row running every pattern rule (a rows x rules grid measured no faster on C5 and
   // slower on C3's 600 rules; it also doubled the VM code the kernel holds)
-  hipLaunchKernelGGL(kpe_pattern_kernel, dim3((unsigned)((n + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK)), dim3(KPE_PAT_BLOCK), 0,
-                     s, dargs);
+  const dim3 grid((unsigned)((n + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK));
+  if (lt) hipLaunchKernelGGL(kpe_pattern_kernel<true>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
+  else hipLaunchKernelGGL(kpe_pattern_kernel<false>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
   return hipGetLastError();
 }
 

@@ -275,6 +275,12 @@ struct PatArgs {
   const KpeScalar* ctab;
   const uint8_t* ctext;
   uint8_t* verdicts;
+  // Leaf table (kpe_leaf_table_kernel, once per binding): a leaf whose result depends only on
+  // the scalar (no variables) has a slot, lslot[leaf] (KPE_NO_LSLOT: none), and bit sid of
+  // ltab[slot * ltab_words ...] is pattern.Validate of scalar sid against it. Null: no table.
+  const uint32_t* lslot;
+  uint32_t* ltab;
+  uint32_t ltab_words, pad3_;
   // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)
   uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
   uint64_t nscal, ndoc;

@@ -30,7 +30,7 @@ bool is_limit_error(const std::exception& e);
 }  // namespace kpe
 
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
-extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, hipStream_t s);
+extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lt, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
                                                hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, int txt, hipStream_t s);
@@ -48,6 +48,8 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
 extern "C" hipError_t kpe_launch_psum(const PsumArgs* a, hipStream_t s);
 extern "C" hipError_t kpe_launch_lean_batch(const LeanBatchArgs* a, size_t dyn_bytes, hipStream_t s);
 extern "C" hipError_t kpe_launch_selmask(const SelMaskArgs* a, hipStream_t s);
+extern "C" hipError_t kpe_launch_leaf_table(const PatArgs* dargs, const uint32_t* slot_leaf, uint32_t nslots,
+                                            uint64_t nscal, hipStream_t s);
 extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint32_t R, unsigned long long* out,
                                        hipStream_t s);
 
@@ -163,6 +165,9 @@ struct DeviceProgram {
   uint32_t ncls = 0, pss_rules = 0, err_rules = 0, pat_rules = 0;
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
   DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
+  DevBuf plslot, pslot_leaf;  // leaf-table slot per leaf, leaf per slot (PatArgs::lslot)
+  uint32_t nlslots = 0;
+  bool ltab_all = false;  // every leaf has a slot or is PL_NEVER: the pattern kernel's LT instance
   DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
   DevBuf pcol2pr;  // verdict column -> pattern rule index + 1 (0: not a pattern rule)
   // condition rules: compiled programs (program.hpp CondProgram)
@@ -206,6 +211,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf terms_r, kindsels_r, annpairs_r, selectors_r, selreqs_r, cv_classes;  // resolved tables
   // selector requirement masks (ScanArgs::selm): requirement lists per space, the tables
   DevBuf sel_rq, sel_nq, sel_km, sel_vm, sel_nsq;
+  DevBuf ltab;  // leaf table (PatArgs::ltab)
+  uint32_t ltab_words = 0;
   uint32_t selm = 0, sel_nrq = 0, sel_nnq = 0;
   uint64_t sm[5] = {};  // pos (EQ / In), wild, NotIn, Exists, DoesNotExist
   uint32_t pp[10] = {};  // fixed PSS predicate locations
@@ -566,6 +573,38 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.pnodes, PP.nodes, s0));
     HIPCHK(upload(D.plists, PP.lists, s0));
     HIPCHK(upload(D.pleaves, PP.leaves, s0));
+    {  // leaf-table slots: leaves decided by the scalar alone (no variables), up to KPE_LTAB_SLOTS;
+       // leaves with the same content (type, value, pattern text) share a slot
+      std::vector<uint32_t> lslot(std::max<size_t>(PP.leaves.size(), 1), KPE_NO_LSLOT), slot_leaf;
+      std::map<std::string, uint32_t> seen;
+      bool all = true;
+      for (size_t i = 0; i < PP.leaves.size(); ++i) {
+        const KpeLeaf& L = PP.leaves[i];
+        if (L.type == PL_NEVER) continue;
+        if (L.type > PL_STR) {
+          all = false;
+          continue;
+        }
+        std::string key((const char*)&L.type, 4);
+        key.append((const char*)&L.bval, 4).append((const char*)&L.ival, 8).append((const char*)&L.fval, 8);
+        if (L.type == PL_STR) key += PP.operands[L.exact];
+        auto it = seen.find(key);
+        if (it != seen.end()) {
+          lslot[i] = it->second;
+        } else if (slot_leaf.size() < KPE_LTAB_SLOTS) {
+          lslot[i] = (uint32_t)slot_leaf.size();
+          seen.emplace(key, lslot[i]);
+          slot_leaf.push_back((uint32_t)i);
+        } else {
+          all = false;
+        }
+      }
+      D.nlslots = (uint32_t)slot_leaf.size();
+      D.ltab_all = all && D.nlslots > 0;
+      if (slot_leaf.empty()) slot_leaf.push_back(0);
+      HIPCHK(upload(D.plslot, lslot, s0));
+      HIPCHK(upload(D.pslot_leaf, slot_leaf, s0));
+    }
     HIPCHK(upload(D.pconds, PP.conds, s0));
     HIPCHK(upload(D.ppats, pp, s0));
     HIPCHK(upload(D.pbytes, pb, s0));
@@ -941,6 +980,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     }
     HIPCHK(upload(B.pmembers, mem, s));
     B.pargs_valid = false;
+    B.ltab_words = (uint32_t)(((uint64_t)C.scal.size() + 63) / 64 * 2);
+    if (PD.nlslots) HIPCHK(B.ltab.ensure((size_t)PD.nlslots * B.ltab_words * 4 + 16));
   }
   if (!P.cond.rules.empty()) {  // condition field names -> D_KEY ids + 1
     if (!C.has_docs) return fail(KPE_E_STATE, "condition rules need a corpus flattened with KPE_CORPUS_DOCS");
@@ -1275,6 +1316,9 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.ctab = PD.cconsts.as<KpeScalar>();
       pa.ctext = PD.ctext.as<uint8_t>();
       pa.verdicts = B.verdicts.as<uint8_t>();
+      pa.lslot = PD.plslot.as<uint32_t>();
+      pa.ltab = PD.nlslots ? B.ltab.as<uint32_t>() : nullptr;
+      pa.ltab_words = B.ltab_words;
       pa.nnodes = (uint32_t)P.pat.nodes.size(), pa.nmembers = (uint32_t)(P.pat.members.size() / 4);
       pa.nlists = (uint32_t)P.pat.lists.size(), pa.nleaves = (uint32_t)P.pat.leaves.size();
       pa.nconds = (uint32_t)P.pat.conds.size(), pa.npats = (uint32_t)P.pat.operands.size();
@@ -1290,6 +1334,10 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     }
     return hipSuccess;
   };
+  if (fresh && PD.nlslots && (!P.pat.rules.empty() || P.any_fe_pat)) {  // the binding's leaf table
+    HIPCHK(ensure_pargs());
+    HIPCHK(kpe_launch_leaf_table(B.pargs.as<PatArgs>(), PD.pslot_leaf.as<uint32_t>(), PD.nlslots, C.scal.size(), s));
+  }
   if (!P.cond.rules.empty()) {
     if (!B.cargs_valid) {
       CondArgs ca{};
@@ -1390,7 +1438,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
-    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), s));
+    HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), PD.ltab_all ? 1 : 0, s));
     static const bool patvm_err = getenv("KPE_PATVM_ERR") != nullptr;
     if (patvm_err) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;

@@ -309,7 +309,8 @@ __device__ __forceinline__ bool leaf_nil(const KpeScalar* v, uint32_t vf) {  // 
 
 // pattern.Validate (pattern.go:26-50) of scalar `sid` (kNoNode: a map / list value); pv: the
 // row's resolved pattern variables; *und set where the device leaves the cell undecided
-__device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li, const uint2* pv, uint32_t* und) {
+__device__ __forceinline__ bool pat_leaf_eval(const PatArgs& a, uint32_t sid, uint32_t li, const uint2* pv,
+                                              uint32_t* und) {
   if (sid == kNoNode) return false;  // no scalar validator accepts a map / list
   const KpeLeaf Lv = PU(a.leaves, li, a.nleaves, 4);
   const KpeLeaf* L = &Lv;
@@ -417,6 +418,23 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
     default: return false;
   }
 }
+// pat_leaf_eval through the binding's leaf table where the leaf has a slot: one bit load
+// instead of the scalar record, its text and the comparison. LT: the program's every leaf has a
+// slot or is PL_NEVER (no variables), so the instance holds no comparison code at all.
+template <bool LT = false>
+__device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_t li, const uint2* pv, uint32_t* und) {
+  if (sid == kNoNode) return false;
+  if (LT) {
+    const uint32_t slot = PU(a.lslot, li, a.nleaves, 4);
+    return slot != KPE_NO_LSLOT && ((a.ltab[(size_t)slot * a.ltab_words + (sid >> 5)] >> (sid & 31u)) & 1u);
+  }
+  if (a.ltab) {
+    const uint32_t slot = PU(a.lslot, li, a.nleaves, 4);
+    if (slot != KPE_NO_LSLOT) return (a.ltab[(size_t)slot * a.ltab_words + (sid >> 5)] >> (sid & 31u)) & 1u;
+  }
+  return pat_leaf_eval(a, sid, li, pv, und);
+}
+
 // scalar id of node c (kNoNode for maps / lists); an absent member is null
 __device__ __forceinline__ uint32_t node_sid(const PatArgs& a, DocView doc, uint32_t c) {
   if (c == kNoNode) return SC_NULL_ID;
@@ -472,7 +490,7 @@ struct FramesLds {
   }
 };
 
-template <class FS>
+template <class FS, bool LT = false>
 struct PatVMT {
   const PatArgs& a;
   DocView doc;   // the whole tape (absolute entry indices)
@@ -580,7 +598,7 @@ struct PatVMT {
       } else if (j == 8u && h != PM_DEFAULT) {
         ek = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
       } else if ((m.x & PMF_STAR) ||
-                 ((m.x & PMF_VSTAR) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv))) {
+                 ((!LT && (m.x & PMF_VSTAR)) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv))) {
         ek = (j < 8u && (DN_KIND(x.x) != DN_SCALAR || x.y != SC_NULL_ID)) ? PE_OK : PE_OTHER;
       } else {
         const KpePNode vn = PU(a.nodes, m.z, a.nnodes, 1);
@@ -597,10 +615,10 @@ struct PatVMT {
           const uint32_t l0 = x.y + 1u, le = l0 + doc[PVD(x.y)].x;
           v1 = PE_OK;
           for (uint32_t c = l0; c < le && v1 == PE_OK; ++c)
-            if (!pat_leaf(a, node_sid(a, doc, c), vn.y, pv, &und)) v1 = PE_OTHER;
+            if (!pat_leaf<LT>(a, node_sid(a, doc, c), vn.y, pv, &und)) v1 = PE_OTHER;
         } else {
           const uint32_t sid = j == 8u ? SC_NULL_ID : (DN_KIND(x.x) == DN_SCALAR ? x.y : kNoNode);
-          v1 = pat_leaf(a, sid, vn.y, pv, &und) ? PE_OK : PE_OTHER;
+          v1 = pat_leaf<LT>(a, sid, vn.y, pv, &und) ? PE_OK : PE_OTHER;
         }
         ek = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
       }
@@ -626,7 +644,7 @@ struct PatVMT {
         const uint32_t rk = br == kNoNode ? 0xFFu : DN_KIND(doc[PVD(br)].x);
         state = VM_RET;
         if (pn.kind == PN_LEAF && rk != DN_ARR) {
-          v = pat_leaf(a, node_sid(a, doc, br), pn.y, pv, &und) ? PE_OK : PE_OTHER;
+          v = pat_leaf<LT>(a, node_sid(a, doc, br), pn.y, pv, &und) ? PE_OK : PE_OTHER;
         } else if (pn.kind == PN_LEAF || pn.kind == PN_ARR_LEAF) {  // scalar pattern vs a list
           if (rk != DN_ARR) {
             v = PE_OTHER;
@@ -634,7 +652,7 @@ struct PatVMT {
             PV_KIDS(br, c0, end);
             v = PE_OK;
             for (uint32_t c = c0; c < end && v == PE_OK; ++c)
-              if (!pat_leaf(a, node_sid(a, doc, c), pn.y, pv, &und)) v = PE_OTHER;
+              if (!pat_leaf<LT>(a, node_sid(a, doc, c), pn.y, pv, &und)) v = PE_OTHER;
           }
         } else if (pn.kind == PN_MAP) {
           if (rk != DN_MAP) {
@@ -725,7 +743,7 @@ struct PatVMT {
               } else if (c == kNoNode && h != PM_DEFAULT) {
                 e = h == PM_COND ? PE_SKIP : PE_OK;  // absent: condition skips, =() <() ^() hold
               } else if ((m.x & PMF_STAR) ||
-                         ((m.x & PMF_VSTAR) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv))) {
+                         ((!LT && (m.x & PMF_VSTAR)) && pat_var_star(a, PU(a.nodes, m.z, a.nnodes, 1).y, pv))) {
                 e = (c != kNoNode && node_sid(a, doc, c) != SC_NULL_ID) ? PE_OK : PE_OTHER;
                 if (TRACE && e == PE_OTHER) snap(sp, ~0u);  // "*": the map's own path (handlers.go:124-140)
               } else if (h == PM_EXIST) {
@@ -740,7 +758,7 @@ struct PatVMT {
                 // a scalar pattern against a scalar / absent value resolves in place: BEGIN's
                 // pattern.Validate and RET's anchor mapping without the two VM round trips
                 const uint32_t li = PU(a.nodes, m.z, a.nnodes, 1).y;
-                const uint32_t v1 = pat_leaf(a, node_sid(a, doc, c), li, pv, &und) ? PE_OK : PE_OTHER;
+                const uint32_t v1 = pat_leaf<LT>(a, node_sid(a, doc, c), li, pv, &und) ? PE_OK : PE_OTHER;
                 if (TRACE && v1 == PE_OTHER) snap(sp, mcomp(F.r, m0 + k));
                 e = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
               } else {
@@ -850,11 +868,11 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 // Rules that carry the same pattern share a memo slot (PR_MEMO_SH): the row's first pending cell
 // of the slot is evaluated and the others take its verdict from `memo` (LDS bytes, slot s at
 // memo[s * memo_stride]; null: no memo).
-template <class FS>
+template <class FS, bool LT = false>
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs, uint8_t* memo = nullptr,
                                              uint32_t memo_stride = 0) {
   uint32_t memo_ok = 0;  // slots holding this row's verdict
-  PatVMT<FS> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
+  PatVMT<FS, LT> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
                 a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   // The row's cells are scanned 64 columns at a time: the 17 aligned words that cover them are

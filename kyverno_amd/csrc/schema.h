@@ -596,6 +596,8 @@ typedef struct KpeLeaf {
   uint32_t exact;               // PL_STR: pattern-operand record of the whole pattern (value == pattern)
   uint32_t pad[3];
 } KpeLeaf;  // 40 -> 48 bytes
+#define KPE_NO_LSLOT 0xFFFFFFFFu
+#define KPE_LTAB_SLOTS 256u  // distinct leaves with a leaf-table slot per program
 // String-pattern condition (one `&`-term of one `|`-alternative)
 #define PC_OP(x) ((x) & 7u)
 #define PC_EQ 0u

@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 4: multi-shard LEAN5 with tiles per wave, selector requirement masks (C4). Parity tests,
-# C2 / C4 benches, rocprofv3 traces, FETCH_SIZE / WRITE_SIZE passes of both dominant kernels.
+# Round 4: multi-shard LEAN5 with tiles per wave, selector requirement masks (C4), the pattern
+# kernel's leaf table (C3 / C5). Parity tests, C2 / C4 / C5 / C3 benches, rocprofv3 traces, FETCH_SIZE / WRITE_SIZE passes of both dominant kernels.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 TAG=${TAG:-r04_d}
@@ -15,7 +15,10 @@ step() {  # step <name> <timeout> <cmd...>
   [ $rc -ne 0 ] && exit $rc
   return 0
 }
-TAILN=6 step pytest_sel 900 python -u -m pytest tests/test_gpu_lean.py tests/test_gpu_parity.py -m gpu -x -q --timeout 600 --timeout-method thread
+TAILN=6 step pytest_sel 600 python -u -m pytest tests/test_gpu_lean.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread
+TAILN=6 step pytest_pat 400 python -u -m pytest tests/test_gpu_pattern.py tests/test_gpu_configs.py tests/test_pattern_vars.py -m gpu -x -q --timeout 300 --timeout-method thread
+step bench_c5 200 python bench.py --config c5 --steps 20 --warmup 3 --cpu-sample 0
+step bench_c3 200 python bench.py --config c3 --steps 20 --warmup 3 --cpu-sample 0
 step bench_c2_k20 300 python bench.py --steps 20 --warmup 5
 step bench_c2_k200 300 python bench.py --steps 200 --warmup 20 --cpu-sample 0
 step bench_c4 300 python bench.py --config c4 --steps 20 --warmup 3 --cpu-sample 0

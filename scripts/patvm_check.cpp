@@ -140,9 +140,38 @@ int main(int argc, char** argv) {
     for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesLds{plane.data()}, memo.data(), 1u);
     a.verdicts = keep;
   }
+  // ... through the leaf table (kpe_leaf_table_kernel restated: one slot per leaf without
+  // variables; the LT instance when every leaf has one) ...
+  std::vector<uint8_t> lt_v(verdicts);
+  {
+    std::vector<uint32_t> lslot(std::max<size_t>(PP.leaves.size(), 1), KPE_NO_LSLOT), slot_leaf;
+    bool all = true;
+    for (size_t i = 0; i < PP.leaves.size(); ++i) {
+      if (PP.leaves[i].type <= PL_STR) lslot[i] = (uint32_t)slot_leaf.size(), slot_leaf.push_back((uint32_t)i);
+      else if (PP.leaves[i].type != PL_NEVER) all = false;
+    }
+    const uint32_t words = (uint32_t)((scal.size() + 63) / 64 * 2);
+    std::vector<uint32_t> ltab((size_t)std::max<size_t>(slot_leaf.size(), 1) * words + 2, 0u);
+    for (size_t k = 0; k < slot_leaf.size(); ++k)
+      for (uint32_t sid = 0; sid < scal.size(); ++sid) {
+        uint32_t und = 0;
+        if (pat_leaf_eval(a, sid, slot_leaf[k], nullptr, &und)) ltab[k * words + (sid >> 5)] |= 1u << (sid & 31u);
+      }
+    uint8_t* keep = a.verdicts;
+    a.verdicts = lt_v.data();
+    a.lslot = lslot.data(), a.ltab = ltab.data(), a.ltab_words = words;
+    std::vector<uint32_t> plane(FramesLds::kWords * FramesLds::kDepth * 64u, 0xDEADBEEFu);
+    for (int64_t r = 0; r < a.n; ++r) {
+      if (all && !slot_leaf.empty()) pat_eval_row<FramesLds, true>(a, r, FramesLds{plane.data()});
+      else pat_eval_row(a, r, FramesLds{plane.data()});
+    }
+    a.lslot = nullptr, a.ltab = nullptr, a.ltab_words = 0;
+    a.verdicts = keep;
+  }
   // ... and the lane-private stack
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
   if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk (with memo) differs from the private-stack walk\n"), 1;
+  if (lt_v != verdicts) return fprintf(stderr, "leaf-table walk differs from the private-stack walk\n"), 1;
   FILE* f = fopen(argv[3], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
