@@ -714,8 +714,9 @@ const std::vector<uint8_t>& psa_fixed_table() {
   }();
   return tab;
 }
-// Launch the per-pod PSA summary of an uploaded corpus on stream s (kpe_launch_psum).
-kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
+// Launch the per-pod PSA summary of an uploaded corpus on stream s (kpe_launch_psum); summ:
+// also the 2-word summaries (kpe_corpus_psa_summary), or null.
+kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s, uint32_t* summ = nullptr) {
   const int dom[4] = {D_CAP, D_SYSCTL, D_ANNK, D_ANNV};
   PsumArgs a{};
   a.n = C.n;
@@ -745,6 +746,7 @@ kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
   }
   a.csb = D.psa_csb.as<uint8_t>();
   a.psum = D.psum.as<uint32_t>();
+  a.summ = summ;
   HIPCHK(kpe_launch_psum(&a, s));
   D.psum_ready = true;
   return KPE_OK;
@@ -1614,12 +1616,13 @@ kpe_status kpe_corpus_psa_summary(kpe_device* dev, kpe_corpus* c, uint32_t* out)
   HIPCHK(hipSetDevice(dev->ordinal));
   auto& D = *c->d;
   if (D.bind.last) HIPCHK(hipStreamSynchronize(D.bind.last));
-  if (!D.psum_ready)
-    if (kpe_status st = run_psum(*c->c, D, dev->stream)) return st;
-  std::vector<uint32_t> rec((size_t)c->c->n * 3);
-  if (c->c->n) HIPCHK(hipMemcpyAsync(rec.data(), D.psum.p, rec.size() * 4, hipMemcpyDeviceToHost, dev->stream));
+  // the summary pass again, with its 2-word summaries written out (the scan records it rewrites
+  // are the same)
+  DevBuf summ;
+  HIPCHK(summ.ensure((size_t)c->c->n * 8 + 16));
+  if (kpe_status st = run_psum(*c->c, D, dev->stream, summ.as<uint32_t>())) return st;
+  if (c->c->n) HIPCHK(hipMemcpyAsync(out, summ.p, (size_t)c->c->n * 8, hipMemcpyDeviceToHost, dev->stream));
   HIPCHK(hipStreamSynchronize(dev->stream));
-  for (int64_t i = 0; i < c->c->n; ++i) out[2 * i] = rec[3 * i + 1], out[2 * i + 1] = rec[3 * i + 2] & 0xFFFFu;
   return KPE_OK;
 }
 
@@ -1898,7 +1901,7 @@ static bool trace_path(const kpe::Program& P, const kpe::Corpus* C, const uint32
 // order); empty when the reference's text would need an error string the device does not keep
 // (an empty-path PatternError, a skip) or a substituted message
 static std::string pattern_message(const kpe::Program& P, const kpe::Corpus* C, const kpe::RuleReport& rr, uint8_t v,
-                                   const uint32_t* tr) {
+                                   const uint32_t* tr, const char* json, size_t json_len) {
   auto root = [&](uint32_t k) { return tr + (size_t)k * KPE_TRACE_WORDS; };
   auto rv = [&](uint32_t k) { return (root(k)[0] & KPE_TR_VALID) ? (root(k)[0] >> 16) & 0xFFu : 0xFFu; };
   if (!rr.any_pattern) {
@@ -1906,8 +1909,11 @@ static std::string pattern_message(const kpe::Program& P, const kpe::Corpus* C, 
     std::string path;
     if (!trace_path(P, C, root(0), &path)) return "";
     if (rr.vmsg.empty()) return "validation error: rule " + rr.rule + " failed at path " + path;  // buildErrorMessage
-    if (rr.vmsg_vars) return "";
     std::string m = rr.vmsg;
+    if (rr.vmsg_vars) {  // buildErrorMessage: SubstituteAll of the message (a non-string value: no text)
+      bool nonstring = false;
+      if (!kpe::substitute_message(rr.vmsg, json, json_len, &m, &nonstring) || nonstring) return "";
+    }
     if (m.empty() || m.back() != '.') m += '.';
     return "validation error: " + m + " rule " + rr.rule + " failed at path " + path;
   }
@@ -1984,13 +1990,18 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
         if (pod_state > 0) msg = kpe::pss_fail_message(rr.rule, rr.pss_level, rr.pss_version, kind, pod, cv_mask_row[r]);
       } else if (rr.pat_rule && traces && (v == KPE_FAIL || (v == KPE_PASS && rr.any_pattern))) {
         msg = pattern_message(P, corp ? corp->c.get() : nullptr, rr, v,
-                              traces + r * (size_t)(KPE_TRACE_ROOTS * KPE_TRACE_WORDS));
+                              traces + r * (size_t)(KPE_TRACE_ROOTS * KPE_TRACE_WORDS), resource_json, resource_len);
       } else if (rr.msg_pattern && v == KPE_PASS) {
         msg = "validation rule '" + rr.rule + "' passed.";
       } else if (rr.msg_deny && v == KPE_PASS) {
         msg = "validation rule '" + rr.rule + "' passed.";
       } else if (rr.msg_deny && v == KPE_FAIL) {
         msg = rr.deny_fail_msg;
+        if (msg.empty() && !rr.deny_tmpl.empty()) {  // getDenyMessage: SubstituteAll of the message
+          bool nonstring = false;
+          if (!kpe::substitute_message(rr.deny_tmpl, resource_json, resource_len, &msg, &nonstring)) msg.clear();
+          else if (nonstring) msg = "the produced message didn't resolve to a string, check your policy definition.";
+        }
       } else if (rr.msg_deny && rr.msg_pre_skip && v == KPE_SKIP && P.rules[r].exc == 0u) {
         msg = "preconditions not met";  // a PolicyException's skip has its own message
       }

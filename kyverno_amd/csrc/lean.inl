@@ -8,8 +8,9 @@
 // of its container state bitmaps and of its list items' codes under those sets. The summary is
 // built on the device once per corpus (kpe_psa_dict_kernel -> kpe_psa_capset_kernel ->
 // kpe_psum_kernel, at the first binding of a LEAN program and again on a cold evaluation), as a
-// 12-byte scan record per pod: the pod word and kind id of the pod record beside the summary. An
-// evaluation then reads 12 bytes per pod and decides its versioned checks branch-free.
+// 12-byte scan record per pod: the pod word and kind id of the pod record beside the pod's
+// failing versioned checks (cv_fails of the summary: also policy-independent). An evaluation then
+// reads 12 bytes per pod and masks the checks with the program's version classes.
 // Included by kernels.hip (uses its anonymous-namespace helpers).
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -121,7 +122,8 @@ __global__ void __launch_bounds__(256) kpe_psa_capset_kernel(PsumArgs a) {
 
 // One wave per 64-pod tile: list offsets from the tile header plus a wave scan of the pod
 // records' packed counts, then each lane ORs its own pod's items (schema.h PS_* layout). Out: the
-// pod's LEAN scan record {pod word, OR of container states, list codes | kind id << 16}.
+// pod's LEAN scan record {pod word, failing versioned checks, kind id << 16} and, when asked
+// (PsumArgs::summ), the summary itself {OR of container states, list codes} (schema.h PS_*).
 __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -163,13 +165,18 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
     const uint32_t va = q.y < nav ? (uint32_t)a.codes[PSD_ANNV][q.y] : 0u;
     ac |= ((ka & 1u) && !(va & 1u) ? 1u : 0u) | ((ka & 2u) && !(va & 2u) ? 2u : 0u);
   }
+  const uint32_t y = co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10);
   uint32_t* o = a.psum + 3u * r;
-  o[0] = rc.x, o[1] = xo, o[2] = co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10) | (GVK_KIND(rc.y) << 16);
+  o[0] = rc.x;
+  o[1] = cv_fails(rc.x, xo, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y), PS_ANN(y) & 1u,
+                  PS_ANN(y) & 2u);
+  o[2] = GVK_KIND(rc.y) << 16;
+  if (a.summ) a.summ[2u * r] = xo, a.summ[2u * r + 1u] = y;
 }
 
 // ---- kpe_lean5_kernel: the 12-byte scan records only ------------------------------------
 // A wave loads one 12-byte record per pod (768 contiguous bytes) in one memory step and
-// evaluates with no staging, scans or list loops: the versioned checks (cv_fails), the kind
+// evaluates with no staging, scans or list loops: the failing checks of the program's classes, the kind
 // table, the rows stored as dwords through LDS and, when asked, the check masks.
 __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArgs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
@@ -202,8 +209,7 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArg
   uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a0.wave_lds + wv * a0.wave_words + KPE_STAGE_WORDS);
   const bool live = r < n;
   const uint32_t pw = sr.x, y = sr.z;
-  const uint32_t fails = cv_fails(pw, sr.y, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
-                                  PS_ANN(y) & 1u, PS_ANN(y) & 2u) & cv_union;
+  const uint32_t fails = sr.y & cv_union;
   const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
   const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
   const uint32_t matched = dyn[a0.kt_lds + (y >> 16)];
@@ -285,8 +291,7 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_batch_kernel(L
     const uint32_t r = tile * 64u + lane;
     const bool live = r < n;
     const uint32_t pw = sr[i].x, y = sr[i].z;
-    const uint32_t fails = cv_fails(pw, sr[i].y, PS_CAPS(y), PS_SECANN(y), PS_VOL(y) & 1u, PS_VOL(y) & 2u, PS_SYS(y),
-                                    PS_ANN(y) & 1u, PS_ANN(y) & 2u) & cv_union;
+    const uint32_t fails = sr[i].y & cv_union;
     const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
     const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
     const uint32_t kind = y >> 16;

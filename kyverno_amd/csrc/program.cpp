@@ -8,6 +8,7 @@
 //   kind selectors           pkg/utils/kube/kind.go:11-46
 //   PSS version selection    pkg/pss/evaluate.go:24-70 + ParseVersion :221-239 (folded into cv_mask)
 #include <algorithm>
+#include <charconv>
 #include <cmath>
 #include <cstring>
 #include <functional>
@@ -2482,6 +2483,7 @@ class Lowerer {
         const std::string mt = (m && m->t == JV::Str) ? m->s : std::string();
         if (mt.empty()) rr.deny_fail_msg = "validation error: rule " + rname + " failed";
         else if (mt.find("{{") == std::string::npos && mt.find("$(") == std::string::npos) rr.deny_fail_msg = mt;
+        else rr.deny_tmpl = mt;  // SubstituteAll per resource (substitute_message)
       }
     }
     P.reports.push_back(std::move(rr));
@@ -2747,6 +2749,232 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len, const ch
   }
   L.assign_pattern_memo();
   return prog;
+}
+
+// ---------------------------------------------------------------------------
+// variables.SubstituteAll of a rule message (pkg/engine/variables/vars.go:161-167,311-389) on a
+// background scan's context, where `request.object` is the resource decoded as
+// map[string]interface{} (numbers float64). Restated for `request.object` paths of identifiers,
+// quoted identifiers and [N] indexes; anything else (other roots, functions, `@`, `$(...)`
+// references, a variable inside a substituted value) returns false and the message is left to the
+// Go engine.
+namespace {
+
+// encoding/json float64 (encode.go floatEncoder): 'f' with the shortest round-trip digits, 'e'
+// below 1e-6 or from 1e21, exponent without leading zeros
+void go_json_float(std::string& o, double f) {
+  char buf[64];
+  const double a = std::fabs(f);
+  if (a != 0 && (a < 1e-6 || a >= 1e21)) {
+    auto r = std::to_chars(buf, buf + sizeof buf, f, std::chars_format::scientific);
+    std::string t(buf, r.ptr);
+    const size_t e = t.find('e');
+    if (e != std::string::npos && e + 3 < t.size() && t[e + 2] == '0') t.erase(e + 2, 1);  // e-07 -> e-7
+    o += t;
+    return;
+  }
+  auto r = std::to_chars(buf, buf + sizeof buf, f, std::chars_format::fixed);
+  o.append(buf, r.ptr);
+}
+
+// encoding/json string with HTML escaping (encode.go appendString, escapeHTML)
+void go_json_str(std::string& o, const std::string& s) {
+  static const char* hex = "0123456789abcdef";
+  o += '"';
+  for (size_t i = 0; i < s.size(); ++i) {
+    const unsigned char c = (unsigned char)s[i];
+    if (c == '"' || c == '\\') {
+      o += '\\';
+      o += (char)c;
+    } else if (c == '\n') {
+      o += "\\n";
+    } else if (c == '\r') {
+      o += "\\r";
+    } else if (c == '\t') {
+      o += "\\t";
+    } else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
+      o += "\\u00";
+      o += hex[c >> 4];
+      o += hex[c & 15];
+    } else if (c == 0xE2 && i + 2 < s.size() && (unsigned char)s[i + 1] == 0x80 &&
+               ((unsigned char)s[i + 2] == 0xA8 || (unsigned char)s[i + 2] == 0xA9)) {
+      o += (unsigned char)s[i + 2] == 0xA8 ? "\\u2028" : "\\u2029";
+      i += 2;
+    } else {
+      o += (char)c;
+    }
+  }
+  o += '"';
+}
+
+// json.Marshal of a decoded value (maps: sorted keys, the last of duplicate keys)
+void go_json(std::string& o, const JV& v) {
+  switch (v.t) {
+    case JV::Null: o += "null"; break;
+    case JV::Bool: o += v.b ? "true" : "false"; break;
+    case JV::Num: go_json_float(o, v.is_int ? (double)v.i : v.n); break;
+    case JV::Str: go_json_str(o, v.s); break;
+    case JV::Arr:
+      o += '[';
+      for (size_t k = 0; k < v.a.size(); ++k) {
+        if (k) o += ',';
+        go_json(o, v.a[k]);
+      }
+      o += ']';
+      break;
+    case JV::Obj: {
+      std::map<std::string, const JV*> m;
+      for (auto& kv : v.o) m[kv.first] = &kv.second;
+      o += '{';
+      bool first = true;
+      for (auto& kv : m) {
+        if (!first) o += ',';
+        first = false;
+        go_json_str(o, kv.first);
+        o += ':';
+        go_json(o, *kv.second);
+      }
+      o += '}';
+      break;
+    }
+  }
+}
+
+// A `request.object...` JMESPath over the resource: identifiers, "quoted" identifiers and [N]
+// (negative from the end); a missing member or a mismatched type gives null. false: not this
+// grammar.
+bool object_path(const std::string& q, const JV& res, const JV** out) {
+  static const JV kNull;
+  const std::string root = "request.object";
+  if (q.compare(0, root.size(), root) != 0) return false;
+  const JV* cur = &res;
+  size_t i = root.size();
+  auto ident0 = [](char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_'; };
+  auto ident1 = [&](char c) { return ident0(c) || (c >= '0' && c <= '9'); };
+  while (i < q.size()) {
+    if (q[i] == '.') {
+      ++i;
+      std::string key;
+      if (i < q.size() && q[i] == '"') {
+        const size_t e = q.find('"', i + 1);
+        if (e == std::string::npos) return false;
+        key = q.substr(i + 1, e - i - 1);
+        if (key.find('\\') != std::string::npos) return false;
+        i = e + 1;
+      } else {
+        if (i >= q.size() || !ident0(q[i])) return false;
+        const size_t b = i;
+        while (i < q.size() && ident1(q[i])) ++i;
+        key = q.substr(b, i - b);
+      }
+      const JV* nx = cur && cur->t == JV::Obj ? cur->get(key.c_str()) : nullptr;
+      cur = nx;
+    } else if (q[i] == '[') {
+      size_t e = q.find(']', i);
+      if (e == std::string::npos) return false;
+      const std::string num = q.substr(i + 1, e - i - 1);
+      if (num.empty() || num.size() > 9) return false;
+      size_t d = num[0] == '-' ? 1 : 0;
+      if (d == num.size()) return false;
+      for (size_t k = d; k < num.size(); ++k)
+        if (num[k] < '0' || num[k] > '9') return false;
+      long idx = std::stol(num);
+      if (cur && cur->t == JV::Arr) {
+        if (idx < 0) idx += (long)cur->a.size();
+        cur = idx >= 0 && idx < (long)cur->a.size() ? &cur->a[(size_t)idx] : nullptr;
+      } else {
+        cur = nullptr;
+      }
+      i = e + 1;
+    } else {
+      return false;
+    }
+    if (!cur) cur = nullptr;
+  }
+  *out = cur ? cur : &kNull;
+  return true;
+}
+
+// the end of the variable starting at s[i] == '{' s[i+1] == '{' (RegexVariables: `{...}` groups
+// or non-brace bytes, then "}}"); npos: none
+size_t var_end(const std::string& s, size_t i) {
+  size_t j = i + 2;
+  while (j < s.size()) {
+    if (s[j] == '}') return j + 1 < s.size() && s[j + 1] == '}' ? j + 2 : std::string::npos;
+    if (s[j] == '{') {
+      const size_t e = s.find_first_of("{}", j + 1);
+      if (e == std::string::npos || s[e] != '}') return std::string::npos;
+      j = e + 1;
+      continue;
+    }
+    ++j;
+  }
+  return std::string::npos;
+}
+
+}  // namespace
+
+bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring) {
+  *nonstring = false;
+  if (msg.find("$(") != std::string::npos) return false;  // substituteReferences: not restated
+  if (msg.find("{{") == std::string::npos) {
+    *out = msg;
+    return true;
+  }
+  JV res;
+  try {
+    res = parse_all(json, n);
+  } catch (...) {
+    return false;
+  }
+  std::string o;
+  size_t i = 0;
+  bool any = false;
+  while (i < msg.size()) {
+    if (msg[i] == '{' && i + 1 < msg.size() && msg[i + 1] == '{') {
+      const size_t e = var_end(msg, i);
+      if (e == std::string::npos) {
+        o += msg[i++];
+        continue;
+      }
+      if (i > 0 && msg[i - 1] == '\\') {  // escaped: RegexEscpVariables drops the backslash
+        o.pop_back();
+        o.append(msg, i, e - i);
+        i = e;
+        continue;
+      }
+      std::string q = msg.substr(i, e - i);  // replaceBracesAndTrimSpaces
+      for (size_t p; (p = q.find("{{")) != std::string::npos;) q.erase(p, 2);
+      for (size_t p; (p = q.find("}}")) != std::string::npos;) q.erase(p, 2);
+      const size_t b = q.find_first_not_of(" \t\n\r\f\v"), z = q.find_last_not_of(" \t\n\r\f\v");
+      q = b == std::string::npos ? std::string() : q.substr(b, z - b + 1);
+      const JV* v = nullptr;
+      if (!object_path(q, res, &v)) return false;
+      if (i == 0 && e == msg.size()) {  // the whole message is the variable: its value as is
+        if (v->t == JV::Str) {
+          if (v->s.find("{{") != std::string::npos) return false;
+          *out = v->s;
+          return true;
+        }
+        *nonstring = true;
+        out->clear();
+        go_json(*out, *v);
+        return true;
+      }
+      std::string val;
+      if (v->t == JV::Str) val = v->s;
+      else go_json(val, *v);
+      if (val.find("{{") != std::string::npos) return false;  // a second round would substitute it
+      o += val;
+      any = true;
+      i = e;
+      continue;
+    }
+    o += msg[i++];
+  }
+  (void)any;
+  *out = std::move(o);
+  return true;
 }
 
 }  // namespace kpe

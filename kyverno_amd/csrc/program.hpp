@@ -97,9 +97,10 @@ struct RuleReport {
   // preconditions
   bool msg_deny = false, msg_pre_skip = false;
   std::string deny_fail_msg;
+  std::string deny_tmpl;  // the rule message when it holds variables (substituted per resource)
   // validate.pattern / anyPattern rule (kpe_pattern_traces paths): failure messages are
   // buildErrorMessage / buildAnyPatternErrorMessage (validate_resource.go:418-454) of the rule's
-  // validate.message; `vmsg_vars`: it holds variables (the substituted text is not rendered)
+  // validate.message; `vmsg_vars`: it holds variables (substituted per resource, substitute_message)
   bool pat_rule = false, any_pattern = false, vmsg_vars = false;
   uint32_t pat_roots = 0;
   std::string vmsg;
@@ -140,5 +141,10 @@ struct CompileError : std::runtime_error {
 };
 std::unique_ptr<Program> compile_policies(const char* json, size_t len, const char* exceptions = nullptr,
                                           size_t exc_len = 0, bool background = false);
+
+// variables.SubstituteAll of a rule message over one resource (program.cpp): false when the
+// message holds variables outside the restated `request.object` path grammar; *nonstring: the
+// message is one variable whose value is not a string (*out is its JSON).
+bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring);
 
 }  // namespace kpe

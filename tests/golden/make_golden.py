@@ -14,6 +14,9 @@ outputs) lifted from the reference's tests:
                               `($error != null): true` => fail, otherwise pass)
   background_report.json   <- test/conformance/chainsaw/reports/background/test-report-background-mode
                               (restricted:latest policy, badpod01, expected report result)
+  report_message_cases.json <- test/conformance/chainsaw/reports/admission/update (disallow-latest-tag
+                              on a Deployment: autogen pattern fail / pass messages) and
+                              .../test-report-admission-mode (require-owner pass message)
   check_selector.json      <- pkg/utils/match/labels_test.go (TestCheckSelector table:
                               expected LabelSelector.MatchLabels, actual labels, want, wantErr)
   pattern_leaf_cases.json  <- pkg/engine/pattern/pattern_test.go (Validate / validateNilPattern /
@@ -208,6 +211,26 @@ def background_report():
     pod = _load_yaml_docs(os.path.join(REF, base, "pod.yaml"))[0]
     rep = _load_yaml_docs(os.path.join(REF, base, "report-assert.yaml"))[0]
     return {"src": base, "policy": policy, "resource": pod, "results": rep["results"], "summary": rep["summary"]}
+
+
+def report_message_cases():
+    """Admission-report fixtures whose results carry messages: policy, resource, expected results
+    (the message of a pattern rule's fail on an autogen rule, and a pass message)."""
+    out = []
+    base = "test/conformance/chainsaw/reports/admission/update"
+    policy = _load_yaml_docs(os.path.join(REF, base, "policy.yaml"))[0]
+    for res, rep in (("deployment-fail.yaml", "report-fail-assert.yaml"), ("deployment-pass.yaml", "report-pass-assert.yaml")):
+        doc = _load_yaml_docs(os.path.join(REF, base, res))[0]
+        r = _load_yaml_docs(os.path.join(REF, base, rep))[0]
+        out.append({"src": f"{base}/{rep}", "policy": policy, "resource": doc, "results": r["results"],
+                    "summary": r.get("summary")})
+    base = "test/conformance/chainsaw/reports/admission/test-report-admission-mode"
+    policy = _load_yaml_docs(os.path.join(REF, base, "chainsaw-step-01-apply-1.yaml"))[0]
+    doc = _load_yaml_docs(os.path.join(REF, base, "chainsaw-step-02-apply-1.yaml"))[0]
+    r = _load_yaml_docs(os.path.join(REF, base, "chainsaw-step-03-assert-1.yaml"))[0]
+    out.append({"src": f"{base}/chainsaw-step-03-assert-1.yaml", "policy": policy, "resource": doc,
+                "results": r["results"], "summary": r.get("summary")})
+    return out
 
 
 def _go_string_map(body):
@@ -688,6 +711,7 @@ if __name__ == "__main__":
     _dump("wildcard_match.json", wildcard_cases())
     _dump("chainsaw_psa.json", chainsaw_psa())
     _dump("background_report.json", background_report())
+    _dump("report_message_cases.json", report_message_cases())
     _dump("chainsaw_exceptions.json", chainsaw_exceptions())
     _dump("check_selector.json", check_selector())
     _dump("match_rd_cases.json", match_rd_cases())

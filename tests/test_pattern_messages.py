@@ -156,3 +156,46 @@ def test_tree_pattern_messages_equal_oracle(oracle):
     nd = "\n".join(json.dumps(json.loads(c["resource"])) for c in cases).encode()
     checked, rendered = _compare_with_oracle(oracle, pols, nd)
     assert rendered > 0
+
+
+REPORTS = json.load(open(os.path.join(GOLD, "report_message_cases.json")))
+
+
+def _expected(case, names):
+    """{rule column: message} of the report case's results (rule names as the program lists them)."""
+    out = {}
+    for res in case["results"]:
+        cols = [r for r, n in enumerate(names) if n.split("/", 1)[1] == res["rule"]]
+        assert len(cols) == 1, res["rule"]
+        out[cols[0]] = (res["result"], res["message"])
+    return out
+
+
+@pytest.mark.parametrize("case", REPORTS, ids=lambda c: c["src"].split("/")[-2] + "/" + c["src"].split("/")[-1])
+def test_report_fixture_messages_oracle(oracle, case):
+    """Admission-report fixtures (reports/admission/update/report-*-assert.yaml: an autogen rule's
+    failure path with its trailing '/'; test-report-admission-mode: a pass message): the oracle's
+    RuleResponse messages equal the report's."""
+    pols = [case["policy"]]
+    nd = json.dumps(case["resource"]).encode()
+    names = K.PolicySet(pols).rule_names
+    st = oracle.validate(pols, nd)[0]
+    msgs = oracle.pattern_messages(pols, nd)[0]
+    for col, (result, msg) in _expected(case, names).items():
+        assert {1: "pass", 2: "fail"}.get(int(st[col])) == result, (case["src"], col)
+        assert msgs[col] == msg, (case["src"], msgs[col], msg)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", REPORTS, ids=lambda c: c["src"].split("/")[-2] + "/" + c["src"].split("/")[-1])
+def test_report_fixture_messages_device(case):
+    """The same report fixtures through the device: verdicts, traces and kpe_report_results_msg_tr."""
+    pols = [case["policy"]]
+    nd = json.dumps(case["resource"]).encode()
+    eng = K.Engine(ordinal=0)
+    ps, corpus = K.PolicySet(pols), K.Corpus(nd)
+    v, _, _ = eng.evaluate(ps, corpus)
+    dm = _device_messages(eng, ps, corpus, v, [nd])
+    for col, (result, msg) in _expected(case, ps.rule_names).items():
+        assert {1: "pass", 2: "fail"}.get(int(v[0, col])) == result, (case["src"], col)
+        assert dm[(0, col)] == msg, (case["src"], dm[(0, col)], msg)
