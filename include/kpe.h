@@ -258,9 +258,12 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
  * podSecurity.exclude or a podSecurity PolicyException) and validate.pattern pass ("validation rule '<rule>' passed.",
  * validate_resource.go:339), and for validate.deny rules whose conditions carry no `message`:
  * pass ("validation rule '<rule>' passed."), fail (getDenyMessage, validate_resource.go:279-300:
- * the rule message, or "validation error: rule <rule> failed" when it is empty; none when it
- * holds variables) and preconditions skip ("preconditions not met", engine.go:283). Other
- * results carry no message. Host only. */
+ * the rule message, or "validation error: rule <rule> failed" when it is empty) and
+ * preconditions skip ("preconditions not met", engine.go:283). A rule message with variables is
+ * substituted over the resource (variables.SubstituteAll, vars.go:311-389) when every variable is
+ * a `request.object` path of members and [N] indexes; a substitution error (a member missing
+ * from an object) leaves no message, as in the reference, and other variables are not rendered.
+ * Other results carry no message. Host only. */
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
                             const char* resource_json, size_t resource_len, char* buf, size_t cap);
 
@@ -285,8 +288,9 @@ kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kp
  * cells are read). Adds: validate.pattern fail ("validation error: <message>. rule <rule> failed
  * at path <path>", buildErrorMessage), anyPattern pass ("validation rule '<rule>' anyPattern[<i>]
  * passed.") and fail (buildAnyPatternErrorMessage over "rule <rule>[<i>] failed at path <path>").
- * Not rendered (no message): messages with variables, empty-path failures (their text is the Go
- * error string), skips, anyPattern fails with more than KPE_TRACE_ROOTS patterns. */
+ * The rule message is substituted as in kpe_report_results_msg. Not rendered (no message):
+ * messages with other variables or a failed substitution, empty-path failures (their text is the
+ * Go error string), skips, anyPattern fails with more than KPE_TRACE_ROOTS patterns. */
 long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus, const uint8_t* verdict_row,
                                const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
                                size_t resource_len, char* buf, size_t cap);

@@ -2757,7 +2757,8 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len, const ch
 // map[string]interface{} (numbers float64). Restated for `request.object` paths of identifiers,
 // quoted identifiers and [N] indexes; anything else (other roots, functions, `@`, `$(...)`
 // references, a variable inside a substituted value) returns false and the message is left to the
-// Go engine.
+// Go engine, as does a substitution error (a member missing from an object: the message is then
+// empty in the reference too).
 namespace {
 
 // encoding/json float64 (encode.go floatEncoder): 'f' with the shortest round-trip digits, 'e'
@@ -2841,14 +2842,17 @@ void go_json(std::string& o, const JV& v) {
 }
 
 // A `request.object...` JMESPath over the resource: identifiers, "quoted" identifiers and [N]
-// (negative from the end); a missing member or a mismatched type gives null. false: not this
-// grammar.
-bool object_path(const std::string& q, const JV& res, const JV** out) {
+// (negative from the end). In a chain of members only, a member missing from an object is the
+// kyverno go-jmespath fork's NotFoundError (*missing: SubstituteAll fails); otherwise, and for a
+// member of a non-object or an index past a list, the value is null. false: not this grammar.
+bool object_path(const std::string& q, const JV& res, const JV** out, bool* missing) {
+  *missing = false;
   static const JV kNull;
   const std::string root = "request.object";
   if (q.compare(0, root.size(), root) != 0) return false;
   const JV* cur = &res;
   size_t i = root.size();
+  bool indexed = false;
   auto ident0 = [](char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_'; };
   auto ident1 = [&](char c) { return ident0(c) || (c >= '0' && c <= '9'); };
   while (i < q.size()) {
@@ -2868,6 +2872,7 @@ bool object_path(const std::string& q, const JV& res, const JV** out) {
         key = q.substr(b, i - b);
       }
       const JV* nx = cur && cur->t == JV::Obj ? cur->get(key.c_str()) : nullptr;
+      if (cur && cur->t == JV::Obj && !nx) *missing = true;
       cur = nx;
     } else if (q[i] == '[') {
       size_t e = q.find(']', i);
@@ -2879,6 +2884,7 @@ bool object_path(const std::string& q, const JV& res, const JV** out) {
       for (size_t k = d; k < num.size(); ++k)
         if (num[k] < '0' || num[k] > '9') return false;
       long idx = std::stol(num);
+      indexed = true;
       if (cur && cur->t == JV::Arr) {
         if (idx < 0) idx += (long)cur->a.size();
         cur = idx >= 0 && idx < (long)cur->a.size() ? &cur->a[(size_t)idx] : nullptr;
@@ -2891,6 +2897,7 @@ bool object_path(const std::string& q, const JV& res, const JV** out) {
     }
     if (!cur) cur = nullptr;
   }
+  if (indexed) *missing = false;  // not a plain member chain
   *out = cur ? cur : &kNull;
   return true;
 }
@@ -2949,7 +2956,8 @@ bool substitute_message(const std::string& msg, const char* json, size_t n, std:
       const size_t b = q.find_first_not_of(" \t\n\r\f\v"), z = q.find_last_not_of(" \t\n\r\f\v");
       q = b == std::string::npos ? std::string() : q.substr(b, z - b + 1);
       const JV* v = nullptr;
-      if (!object_path(q, res, &v)) return false;
+      bool missing = false;
+      if (!object_path(q, res, &v, &missing) || missing) return false;
       if (i == 0 && e == msg.size()) {  // the whole message is the variable: its value as is
         if (v->t == JV::Str) {
           if (v->s.find("{{") != std::string::npos) return false;

@@ -160,6 +160,29 @@ long oracle_pss_failing_cv_batch(const char* level, const char* version, const c
 // RuleResponse message of a podSecurity rule without exclusions for one resource
 // (validate_pss.go:64-110): "Validation rule '<rule>' passed." or the FormatChecksPrint
 // failure text after convertChecks. Returns 1 pass, 0 fail, -1 getSpec / version error.
+// variables.SubstituteAll of a rule message (vars.go:311-389) over the background-scan context of
+// one resource ({"request": {"operation", "object"}}): 0 a string (in buf), 1 a non-string value
+// (its JSON in buf), -1 a substitution error, -2 outside the restated JMESPath subset.
+int oracle_substitute(const char* resource_json, const char* msg, char* buf, size_t cap) {
+  try {
+    JPtr res = parse_json(resource_json);
+    cond::Ctx cx{cond::request_context(*res)};
+    const JPtr r = cond::substitute_string(msg, cx);
+    if (!cond::is_null(r) && r->t == JT::Str) {
+      snprintf(buf, cap, "%s", r->s.c_str());
+      return 0;
+    }
+    snprintf(buf, cap, "%s", cond::json_marshal(r).c_str());
+    return 1;
+  } catch (const cond::EvalError&) {
+    return -1;
+  } catch (const cond::Unsupported&) {
+    return -2;
+  } catch (...) {
+    return -1;
+  }
+}
+
 int oracle_pss_message(const char* rule, const char* level, const char* version, const char* resource_json, char* buf,
                        size_t cap) {
   try {

@@ -1011,13 +1011,14 @@ inline bool matches_resource_description(const Rule& r, const Policy& p, const M
 
 // RuleResponse messages of validatePatterns (validate_resource.go:316-454): *msg gets the text, or
 // kNeedsErrText when the reference's text embeds a Go error string (skips, empty-path
-// failures: PatternError.Error()) or a substituted message, which this restatement does not
-// produce
+// failures: PatternError.Error(), a failed message substitution) or the message resolves to a
+// non-string (a Go type-assertion panic)
 constexpr const char* kNeedsErrText = "\x01";
 struct PatMsg {
   const std::string* rule;
   const std::string* vmsg;
   std::string* out;
+  const cond::Ctx* cx = nullptr;  // the JSON context (request.object) for SubstituteAll of vmsg
 };
 inline const std::string* pm_rule(const PatMsg* pm) {
   static const std::string none;
@@ -1026,9 +1027,21 @@ inline const std::string* pm_rule(const PatMsg* pm) {
 inline std::string build_error_message(const PatMsg& pm, const std::string& path) {  // :418-441
   if (path.empty()) return kNeedsErrText;  // "... execution error: <err>"
   if (pm.vmsg->empty()) return "validation error: rule " + *pm.rule + " failed at path " + path;
-  if (pm.vmsg->find("{{") != std::string::npos || pm.vmsg->find("$(") != std::string::npos) return kNeedsErrText;
   std::string m = *pm.vmsg;
-  if (m.back() != '.') m += '.';
+  if (pm.vmsg->find("$(") != std::string::npos) return kNeedsErrText;  // substituteReferences: not restated
+  if (pm.vmsg->find("{{") != std::string::npos) {  // variables.SubstituteAll (:428-433)
+    if (!pm.cx || !pm.cx->root) return kNeedsErrText;
+    try {
+      const JPtr r = cond::substitute_string(*pm.vmsg, *pm.cx);
+      if (cond::is_null(r) || r->t != JT::Str) return kNeedsErrText;  // msgRaw.(string) panics
+      m = r->s;
+    } catch (const cond::EvalError&) {
+      return kNeedsErrText;  // "variables substitution error in rule ... execution error: <err>"
+    } catch (const cond::Unsupported&) {
+      return kNeedsErrText;
+    }
+  }
+  if (m.empty() || m.back() != '.') m += '.';
   return "validation error: " + m + " rule " + *pm.rule + " failed at path " + path;
 }
 
@@ -1342,7 +1355,8 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
     if (r.unsupported) {
       s = UNSUPPORTED;
     } else {
-      if ((r.pre.present || r.has_deny || !r.foreach.empty() || r.pattern_vars) && !cx.root)
+      if ((r.pre.present || r.has_deny || !r.foreach.empty() || r.pattern_vars ||
+           (msgs && r.vmsg.find("{{") != std::string::npos)) && !cx.root)
         cx.root = cond::request_context(res);
       s = NA;
       bool done = false;
@@ -1373,7 +1387,7 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
         if (r.has_pss) s = pss_handler(r, res, u.kind(), pss_exc);
         else if (r.has_deny) s = deny_handler(r, cx);
         else if (r.pattern || r.any_pattern) {
-          PatMsg pm{&r.name, &r.vmsg, msgs ? &(*msgs)[i] : nullptr};
+          PatMsg pm{&r.name, &r.vmsg, msgs ? &(*msgs)[i] : nullptr, &cx};
           s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx, msgs ? &pm : nullptr);
         }
         else if (!r.foreach.empty()) s = foreach_handler(r, cx, res);

@@ -20,7 +20,8 @@ pass "validation rule '<rule>' passed." (validate_resource.go:339), validate.den
 conditions and preconditions carry no `message` (so the condition message is empty,
 variables/evaluate.go:14-28): pass "validation rule '<rule>' passed." (validate_resource.go:275),
 fail getDenyMessage (validate_resource.go:279-300: the rule message, or "validation error: rule
-<rule> failed" when it is empty; not restated when it holds variables), preconditions skip
+<rule> failed" when it is empty; with variables, SubstituteAll through the oracle's JMESPath when a
+`substitute` callable is given), preconditions skip
 "preconditions not met" (engine.go:283); other messages are not restated. Not restated: timestamp, exception
 and ValidatingAdmissionPolicy branches (out of the path's scope).
 Autogen rules are mapped back to their source rule by the "autogen-" / "autogen-cronjob-"
@@ -72,8 +73,11 @@ def _cond_messages(block) -> bool:
 
 def report_results(policies: List[dict], rule_names: List[str], verdict_row, resource: dict,
                    failing_checks: Callable[[str, str, dict], List[str]],
-                   pss_message: Optional[Callable[[str, str, str, dict], Optional[str]]] = None) -> List[Dict]:
-    """[]PolicyReportResult for one resource over all policies (rules in rule_names order)."""
+                   pss_message: Optional[Callable[[str, str, str, dict], Optional[str]]] = None,
+                   substitute: Optional[Callable[[str, dict], tuple]] = None) -> List[Dict]:
+    """[]PolicyReportResult for one resource over all policies (rules in rule_names order).
+    substitute: variables.SubstituteAll of a message over the resource (the oracle's), for deny
+    rule messages with variables; without it such messages are not restated."""
     by_name = {p["metadata"]["name"]: p for p in policies}
     out = []
     for r, full in enumerate(rule_names):
@@ -109,6 +113,14 @@ def report_results(policies: List[dict], rule_names: List[str], verdict_row, res
                     msg = f"validation error: rule {rname} failed"
                 elif cell == 2 and "{{" not in m and "$(" not in m:
                     msg = m
+                elif cell == 2 and substitute is not None and "$(" not in m:
+                    # getDenyMessage (validate_resource.go:288-299): SubstituteAll; an error gives the
+                    # (empty) condition message, a non-string value a fixed text
+                    k, text = substitute(m, resource)
+                    if k == 0:
+                        msg = text
+                    elif k == 1:
+                        msg = "the produced message didn't resolve to a string, check your policy definition."
                 elif cell == 5 and _source_rule(pol, rname).get("preconditions") is not None:
                     msg = "preconditions not met"
             if msg:

@@ -26,6 +26,8 @@ class Oracle:
                                                   ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         L.oracle_pss_failing_cv_batch.restype = ctypes.c_long
         L.oracle_pss_failing_cv.restype = ctypes.c_longlong
+        L.oracle_substitute.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_substitute.restype = ctypes.c_int
         L.oracle_pss_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                           ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_rule_names.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
@@ -86,6 +88,13 @@ class Oracle:
         r = self.lib.oracle_pss_message(rule.encode(), level.encode(), version.encode(),
                                         json.dumps(resource).encode(), buf, 1 << 16)
         return None if r < 0 else buf.value.decode()
+
+    def substitute(self, msg, resource):
+        """variables.SubstituteAll of a message over the resource's context: (0, text) a string,
+        (1, json) another value, (-1, None) an error, (-2, None) outside the restated subset."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        r = self.lib.oracle_substitute(json.dumps(resource).encode(), msg.encode(), buf, 1 << 16)
+        return (r, buf.value.decode() if r >= 0 else None)
 
     def rule_names(self, policies):
         buf = ctypes.create_string_buffer(1 << 20)

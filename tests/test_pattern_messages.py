@@ -199,3 +199,25 @@ def test_report_fixture_messages_device(case):
     for col, (result, msg) in _expected(case, ps.rule_names).items():
         assert {1: "pass", 2: "fail"}.get(int(v[0, col])) == result, (case["src"], col)
         assert dm[(0, col)] == msg, (case["src"], dm[(0, col)], msg)
+
+
+@pytest.mark.gpu
+def test_substituted_pattern_messages_equal_oracle(oracle):
+    """buildErrorMessage's SubstituteAll of the rule message (validate_resource.go:428-433): the C5
+    pattern policies with their messages templated on the resource (names, labels as JSON, a
+    missing member: a substitution error, so no message), device against the oracle."""
+    import copy as _copy
+
+    pols = _copy.deepcopy(c5_policy_set())
+    tmpl = ["{{ request.object.metadata.name }} breaks it", "labels {{ request.object.metadata.labels }}",
+            "kind {{request.object.kind}}", "missing {{ request.object.metadata.nope }}"]
+    k = 0
+    for p in pols:
+        for r in p["spec"]["rules"]:
+            v = r.get("validate") or {}
+            if v.get("pattern") is not None:
+                v["message"] = tmpl[k % len(tmpl)]
+                k += 1
+    nd = K.synth_resources(0xC5 + 1, 300, mix=K.SYNTH_FANOUT)
+    checked, rendered = _compare_with_oracle(oracle, pols, nd)
+    assert rendered > 50

@@ -97,7 +97,7 @@ def test_host_messages_match_oracle(oracle):
 
 def _deny_message_policies():
     """cond_policy_set with the deny rule messages varied: kept, removed (default message),
-    with variables (not rendered), a condition message (not rendered) and preconditions."""
+    with variables (substituted), a condition message (not rendered) and preconditions."""
     from tests.policies import cond_policy_set
     pols = copy.deepcopy(cond_policy_set())
     rules = pols[0]["spec"]["rules"]
@@ -122,6 +122,21 @@ def _deny_message_policies():
                   "validate": {"message": "m", "deny": {"conditions": {"any": [
                       {"key": "{{ " + obj + ".metadata.labels.app || '' }}", "operator": "Equals",
                        "value": "app-1*", "message": "app label"}]}}}})
+    # SubstituteAll of the rule message (validate_resource.go:288-299) on rules that always deny:
+    # strings, maps (json.Marshal: sorted keys, HTML escapes), numbers, missing members (null),
+    # indexes, quoted identifiers, a whole-message non-string, an escaped variable, two variables
+    always = {"conditions": {"all": [{"key": "x", "operator": "Equals", "value": "x"}]}}
+    for k, m in enumerate([
+            "pod {{ request.object.metadata.name }} in {{request.object.metadata.namespace}}",
+            "labels={{ request.object.metadata.labels }}",
+            "replicas {{ request.object.spec.replicas }}, missing {{ request.object.spec.nope }}",
+            "first {{ request.object.spec.containers[0].image }} last {{ request.object.spec.containers[-1].name }}",
+            'ann {{ request.object.metadata."annotations" }}',
+            "{{ request.object.metadata.labels }}",
+            "{{ request.object.metadata.name }}",
+            "literal \\{{ request.object.metadata.name }} and {{ request.object.kind }}"]):
+        rules.append({"name": f"deny-subst-{k}", "match": {"any": [{"resources": {"kinds": ["Pod", "Deployment"]}}]},
+                      "validate": {"message": m, "deny": copy.deepcopy(always)}})
     return pols
 
 
@@ -138,12 +153,15 @@ def test_host_deny_messages_match_oracle(oracle):
         docs = [json.loads(x) for x in nd.split(b"\n") if x.strip()]
         v = oracle.validate(pols, nd, nthreads=4)
         for i, doc in enumerate(docs):
-            want = oracle_report.report_results(pols, names, v[i], doc, oracle.failing_checks, oracle.pss_message)
+            want = oracle_report.report_results(pols, names, v[i], doc, oracle.failing_checks, oracle.pss_message,
+                                                oracle.substitute)
             got = K.report_results(ps, v[i], _oracle_cv_row(oracle, pols, names, v[i], doc), resource=doc)
             assert got == want, (i, got, want)
             seen.update((r["result"], r.get("message", "")[:20]) for r in got)
     msgs = {m for _, m in seen}
     assert "validation error: ru" in msgs and "preconditions not me" in msgs and "m" in msgs
+    assert any(m.startswith("pod ") for m in msgs) and any(m.startswith("labels={") for m in msgs)
+    assert any(m.startswith("the produced messag") for m in msgs) and any(m.startswith("literal {{") for m in msgs)
     assert any(m.startswith("rule ") for m in msgs) and any(m.startswith("validation rule") for m in msgs)
 
 
@@ -315,3 +333,20 @@ def test_gpu_report_chart_policies(oracle):
         seen.update((r["result"], "category" in r) for r in got)
     assert ("fail", True) in seen and ("pass", True) in seen
     assert K.cli_summary(ps, cnt) == oracle_report.cli_summary(pols, names, ref)
+
+
+def test_deny_message_substitution_pinned(oracle):
+    """getDenyMessage's SubstituteAll (validate_resource.go:288-299) pinned by
+    pkg/engine/validation_test.go Test_VariableSubstitutionValidate_VariablesInMessageAreResolved:
+    the host report and the oracle's both render "The animal cow is not in the allowed list of
+    animals." from the resource."""
+    cases = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "engine_message_cases.json")))
+    case = next(c for c in cases if c["name"] == "Test_VariableSubstitutionValidate_VariablesInMessageAreResolved")
+    pols, doc = [case["policy"]], case["resource"]
+    v = oracle.validate(pols, json.dumps(doc).encode())
+    assert int(v[0][0]) == 2
+    names = oracle.rule_names(pols)
+    got = K.report_results(K.PolicySet(pols), v[0], None, resource=doc)
+    want = oracle_report.report_results(pols, names, v[0], doc, oracle.failing_checks, oracle.pss_message,
+                                        oracle.substitute)
+    assert got[0]["message"] == case["messages"]["0"] == want[0]["message"]
