@@ -130,7 +130,7 @@ namespace {
 constexpr uint32_t kBlock = 256;
 // Minimum waves per SIMD the scan kernel is compiled for (register budget).
 #ifndef KPE_SCAN_WAVES
-#define KPE_SCAN_WAVES 7  // C4 wide scan: 6 -> 0.191 ms, 7 -> 0.182 ms, 8 (spills) -> 0.208 ms
+#define KPE_SCAN_WAVES 6  // C4 wide scan, round 4 (profiles/r04_f): 5 / 6 / 7 waves per SIMD 0.567 / 0.553 / 0.643 ms (7: 65 VGPRs spilled)
 #endif
 constexpr uint32_t kAllowedVolumes = PSS_ALLOWED_VOLUMES;
 

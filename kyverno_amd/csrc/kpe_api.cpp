@@ -2005,6 +2005,7 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
       } else if (rr.msg_deny && rr.msg_pre_skip && v == KPE_SKIP && P.rules[r].exc == 0u) {
         msg = "preconditions not met";  // a PolicyException's skip has its own message
       }
+      if (v == KPE_SKIP && !rr.exc_key.empty()) msg = "rule skipped due to policy exception " + rr.exc_key;
       if (!msg.empty()) {
         o += ",\"message\":";
         json_str(o, msg);
@@ -2032,6 +2033,11 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
       json_str(o, rr.pss_level);
       o += ",\"version\":";
       json_str(o, rr.pss_version);
+      o += '}';
+    }
+    if (v == KPE_SKIP && !rr.exc_name.empty()) {  // results.go:107-111: the exception's name
+      o += ",\"properties\":{\"exception\":";
+      json_str(o, rr.exc_name);
       o += '}';
     }
     if (!rr.category.empty()) {

@@ -2324,7 +2324,7 @@ class Lowerer {
     }
     KpeCRule crule{(uint32_t)P.rules.size(), pre_block, CR_PRE_ONLY, CE_NONE, 0, 0, 0, 0, CE_NONE, 0};
     crule.pv0 = (uint32_t)P.pat.vars.size();
-    bool pss_excl = false, msg_pattern = false;
+    bool pss_excl = false, msg_pattern = false, pat_may_skip = true;
     struct { bool on, any; uint32_t roots; } pat_report{false, false, 0u};
     if (!has_validate) {
       k.handler = H_NONE;  // mutate/generate/verifyImages-only rules give no validate response
@@ -2414,6 +2414,8 @@ class Lowerer {
         if (P.pat.rules.size() >= 65535) throw CompileError("more than 65535 pattern rules in one program");
         P.pat.rules.push_back(pr);
         k.handler = H_PATTERN;
+        // a pattern skips only through conditional / global anchors (validate.go: pe.Skip)
+        pat_may_skip = present("pattern") ? anchor_skips(*v->get("pattern")) : anchor_skips(*v->get("anyPattern"));
         if (!(pr.flags & PR_ANY_BAD)) pat_report = {true, (pr.flags & PR_ANY) != 0u, pr.nr};
       } else if (v->get("foreach") && v->get("foreach")->t == JV::Arr && !v->get("foreach")->a.empty()) {
         // validateForEach (validate_resource.go:186-254): deny, pattern / anyPattern and nested
@@ -2442,7 +2444,7 @@ class Lowerer {
       crule.kind = CR_NONE;
     }
     if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) P.any_const = true;
-    rule_info_.push_back({pre_block != CE_NONE, has_validate, rname});
+    rule_info_.push_back({pre_block != CE_NONE, has_validate, rname, k.handler == H_PATTERN && !pat_may_skip});
     if (pre_block != CE_NONE || k.handler == H_COND || crule.npv) P.cond.rules.push_back(crule);
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
@@ -2516,6 +2518,7 @@ class Lowerer {
       const JV* pss;  // spec.podSecurity when non-empty (HasPodSecurity)
       JV cond;        // spec.conditions, an empty `any` dropped (CheckAnyAllConditions: it holds)
       Fold fold;      // F_TRUE: no conditions, or conditions true for every resource
+      std::string name;
     };
     std::vector<X> keep;
     for (const JV* e : xs) {
@@ -2537,7 +2540,7 @@ class Lowerer {
       // some `any` holds, or `any` is empty. Only true matters (an error or false both mean no
       // exception, exceptions.go:33-41), and on that the preconditions' evaluation order agrees
       // (variables/evaluate.go:57-100) once an empty `any` list is dropped.
-      X x{spec, key, pss, JV(), F_TRUE};
+      X x{spec, key, pss, JV(), F_TRUE, name};
       const JV* cond = spec->get("conditions");
       if (cond && cond->t != JV::Null) {
         if (cond->t != JV::Obj) throw CompileError("PolicyException " + key + ": conditions is not an object");
@@ -2639,6 +2642,17 @@ class Lowerer {
       }
       P.rules[r].exc = x | f0 | nf << 20;
       P.any_exc = true;
+      // the report of a skip this exception caused (validate_resource.go:43-55): unambiguous when
+      // it is the rule's only exception and no other skip is possible (no resource-reading
+      // preconditions; a podSecurity, deny or constant handler, or a pattern without conditional /
+      // global anchors: no anchor or foreach skip)
+      const uint32_t hd = P.rules[r].handler;
+      if (mine.size() == 1 && !xpss && !rule_info_[r].pre_dyn &&
+          (hd == H_PSS || hd == H_CONST_PASS || hd == H_CONST_FAIL || P.reports[r].msg_deny ||
+           rule_info_[r].pat_noskip)) {
+        P.reports[r].exc_key = mine_x[0]->key;
+        P.reports[r].exc_name = mine_x[0]->name;
+      }
     }
   }
   std::string rule_names_at(size_t r) const { return P.rule_names[r]; }
@@ -2692,7 +2706,19 @@ class Lowerer {
   struct RuleInfo {
     bool pre_dyn, has_validate;
     std::string name;
+    bool pat_noskip;  // a pattern rule without conditional / global anchors: it never skips
   };
+  // a key with a conditional "(k)" or global "<(k)" anchor anywhere in the pattern
+  static bool anchor_skips(const JV& v) {
+    if (v.t == JV::Arr) {
+      for (auto& e : v.a)
+        if (anchor_skips(e)) return true;
+    } else if (v.t == JV::Obj) {
+      for (auto& kv : v.o)
+        if (kv.first.rfind("(", 0) == 0 || kv.first.rfind("<(", 0) == 0 || anchor_skips(kv.second)) return true;
+    }
+    return false;
+  }
   std::vector<RuleInfo> rule_info_;
   bool sel_exc_ = false;
 };

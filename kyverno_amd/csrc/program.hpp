@@ -101,6 +101,9 @@ struct RuleReport {
   // validate.pattern / anyPattern rule (kpe_pattern_traces paths): failure messages are
   // buildErrorMessage / buildAnyPatternErrorMessage (validate_resource.go:418-454) of the rule's
   // validate.message; `vmsg_vars`: it holds variables (substituted per resource, substitute_message)
+  // the rule's only PolicyException when its skips can only come from it: RuleSkip message
+  // "rule skipped due to policy exception <key>" and report property exception: <name>
+  std::string exc_key, exc_name;
   bool pat_rule = false, any_pattern = false, vmsg_vars = false;
   uint32_t pat_roots = 0;
   std::string vmsg;

@@ -17,6 +17,8 @@ outputs) lifted from the reference's tests:
   report_message_cases.json <- test/conformance/chainsaw/reports/admission/update (disallow-latest-tag
                               on a Deployment: autogen pattern fail / pass messages) and
                               .../test-report-admission-mode (require-owner pass message)
+  report_exception_cases.json <- test/conformance/chainsaw/reports/{background,admission}/exception
+                              (pattern rule, PolicyException, ConfigMap, skip result + property)
   check_selector.json      <- pkg/utils/match/labels_test.go (TestCheckSelector table:
                               expected LabelSelector.MatchLabels, actual labels, want, wantErr)
   pattern_leaf_cases.json  <- pkg/engine/pattern/pattern_test.go (Validate / validateNilPattern /
@@ -230,6 +232,21 @@ def report_message_cases():
     r = _load_yaml_docs(os.path.join(REF, base, "chainsaw-step-03-assert-1.yaml"))[0]
     out.append({"src": f"{base}/chainsaw-step-03-assert-1.yaml", "policy": policy, "resource": doc,
                 "results": r["results"], "summary": r.get("summary")})
+    return out
+
+
+def report_exception_cases():
+    """reports/{background,admission}/exception: a pattern rule, a PolicyException naming it, the
+    excepted ConfigMap and the report's skip result with its `exception` property."""
+    out = []
+    for mode in ("background", "admission"):
+        base = f"test/conformance/chainsaw/reports/{mode}/exception"
+        rep = _load_yaml_docs(os.path.join(REF, base, "report-assert.yaml"))[0]
+        out.append({"src": f"{base}/report-assert.yaml",
+                    "policy": _load_yaml_docs(os.path.join(REF, base, "policy.yaml"))[0],
+                    "exception": _load_yaml_docs(os.path.join(REF, base, "exception.yaml"))[0],
+                    "resource": _load_yaml_docs(os.path.join(REF, base, "configmap.yaml"))[0],
+                    "results": rep["results"], "summary": rep.get("summary")})
     return out
 
 
@@ -712,6 +729,7 @@ if __name__ == "__main__":
     _dump("chainsaw_psa.json", chainsaw_psa())
     _dump("background_report.json", background_report())
     _dump("report_message_cases.json", report_message_cases())
+    _dump("report_exception_cases.json", report_exception_cases())
     _dump("chainsaw_exceptions.json", chainsaw_exceptions())
     _dump("check_selector.json", check_selector())
     _dump("match_rd_cases.json", match_rd_cases())

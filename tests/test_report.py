@@ -350,3 +350,42 @@ def test_deny_message_substitution_pinned(oracle):
     want = oracle_report.report_results(pols, names, v[0], doc, oracle.failing_checks, oracle.pss_message,
                                         oracle.substitute)
     assert got[0]["message"] == case["messages"]["0"] == want[0]["message"]
+
+
+EXC_REPORTS = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "report_exception_cases.json")))
+
+
+def _exc_case_report(case, verdicts):
+    pols = [case["policy"]]
+    ps = K.PolicySet(pols, exceptions=[case["exception"]], background="background" in case["src"])
+    return K.report_results(ps, verdicts, None, resource=case["resource"])
+
+
+def _check_exc_report(case, got):
+    meta = case["exception"]["metadata"]
+    key = f"{meta['namespace']}/{meta['name']}" if meta.get("namespace") else meta["name"]
+    assert len(got) == len(case["results"]) == 1
+    want = dict(case["results"][0])
+    assert {k: got[0].get(k) for k in want} == want, (got, want)
+    # the RuleSkip message (validate_resource.go:43-55): the chainsaw assert leaves it out
+    assert got[0]["message"] == "rule skipped due to policy exception " + key
+
+
+@pytest.mark.parametrize("case", EXC_REPORTS, ids=lambda c: c["src"].split("/")[-3])
+def test_exception_skip_report_fixture(oracle, case):
+    """reports/{background,admission}/exception: the excepted ConfigMap's skip result carries the
+    exception's name as a property and the RuleSkip message (oracle verdicts, host report)."""
+    nd = json.dumps(case["resource"]).encode()
+    v = oracle.validate([case["policy"]], nd, exceptions=[case["exception"]])
+    assert int(v[0][0]) == 5
+    _check_exc_report(case, _exc_case_report(case, v[0]))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", EXC_REPORTS, ids=lambda c: c["src"].split("/")[-3])
+def test_exception_skip_report_fixture_device(case):
+    eng = K.Engine(ordinal=0)
+    ps = K.PolicySet([case["policy"]], exceptions=[case["exception"]], background="background" in case["src"])
+    v, _, _ = eng.evaluate(ps, K.Corpus(json.dumps(case["resource"]).encode()))
+    assert int(v[0, 0]) == 5
+    _check_exc_report(case, _exc_case_report(case, v[0]))
