@@ -269,7 +269,7 @@ __device__ __forceinline__ uint32_t load_hdr(CArgs& a, uint32_t tile, uint32_t l
 }
 __device__ __forceinline__ uint32_t hw(uint32_t h, uint32_t k) { return __builtin_amdgcn_readlane(h, k); }
 
-template <bool PSS, bool LEAN = false>
+template <bool PSS, bool LEAN = false, bool PSUM = false>
 __device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane);
 
 // Pin a tile's registers here: code that uses them cannot be hoisted above this point
@@ -294,7 +294,7 @@ __device__ __forceinline__ const T* col(bool on, const void* p, const uint32_t* 
 }
 // PSS tile. LEAN (no container seccomp annotations, names or match namespaces read): only
 // the pod records and the list slots are loaded.
-template <bool LEAN>
+template <bool LEAN, bool PSUM>
 __device__ __forceinline__ Tile<true> load_pss_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane) {
   Tile<true> d;
   const uint32_t n = (uint32_t)a.n, need = a.need;
@@ -309,6 +309,18 @@ __device__ __forceinline__ Tile<true> load_pss_tile(CArgs& a, uint32_t tile, uin
     const uint32_t i = b0 + min(k, cnt ? cnt - 1 : 0u);
     return total ? min(i, total - 1) : 0u;
   };
+  // PSUM: the corpus's scan records (ScanArgs::psum: each pod's failing versioned checks, built by
+  // the summary pass) replace the lists: sa0 carries the pod's checks, nothing else is loaded
+  if constexpr (PSUM) {
+    d.C0 = d.V0 = d.S0 = d.A0 = d.nct = d.nvt = d.nst = d.nat = 0;
+    d.rec = reinterpret_cast<const uint4*>(a.rec)[rc];
+    d.sa0 = a.psum[3u * rc + 1u];
+    d.c0 = d.c1 = make_uint2(0u, 0u), d.v0 = d.v1 = d.s0 = d.sa1 = 0u, d.q0 = make_uint2(0u, 0u);
+    const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
+    d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
+    d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+    return d;
+  }
   const bool on_c = a.nctr_total, on_sa = on_c && (need & NEED_SANN);
   const bool on_v = (need & NEED_VOL) && a.nvol_total, on_s = (need & NEED_SYS) && a.nsys_total;
   const bool on_q = (need & NEED_PANN) && a.npann_total;
@@ -353,9 +365,9 @@ __device__ __forceinline__ Tile<false> load_match_tile(CArgs& a, uint32_t tile, 
   return d;
 }
 
-template <bool PSS, bool LEAN>
+template <bool PSS, bool LEAN, bool PSUM>
 __device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t h, uint32_t lane) {
-  if constexpr (PSS) return load_pss_tile<LEAN>(a, tile, h, lane);
+  if constexpr (PSS) return load_pss_tile<LEAN, PSUM>(a, tile, h, lane);
   else return load_match_tile(a, tile, lane);
 }
 
@@ -370,9 +382,10 @@ __device__ __forceinline__ Tile<PSS> load_tile(CArgs& a, uint32_t tile, uint32_t
 struct LeanPP {
   uint32_t sann_ok, aa_key, aa_ok, sp_key, sys0, sys1, sys2;
 };
-template <bool LEAN>
+template <bool LEAN, bool PSUM>
 __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint8_t* s_capb, const Tile<true>& d,
                                              bool live, uint32_t* stage, uint32_t lane, const LeanPP& lp) {
+  if constexpr (PSUM) return live ? d.sa0 & a.cv_union : 0u;  // the scan record's checks (load_pss_tile)
   const uint32_t need = a.need;
   // LEAN: every predicate here is LDS-resident (checked by the host) and every id a real
   // dictionary id (sysctl names, annotation keys / values): a branch-free bit read
@@ -654,7 +667,7 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
 #ifndef KPE_LEAN_WAVES
 #define KPE_LEAN_WAVES 5
 #endif
-template <bool PSS, bool NARROW, bool PREP, bool LEAN = false>
+template <bool PSS, bool NARROW, bool PREP, bool LEAN = false, bool PSUM = false>
 __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES)
     kpe_scan_kernel(const ScanArgs* __restrict__ ap) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
@@ -672,7 +685,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
   // unconditional, clamped (a wave without a tile re-reads the last one and never uses
   // it): the number of loads in flight is the same on every path, so waits are counted
   const uint32_t tile0 = min(tile, ntiles - 1u);
-  if (PSS && !PREP) h = load_hdr(a0, tile0, lane);
+  if (PSS && !PREP && !PSUM) h = load_hdr(a0, tile0, lane);
   // capability sets (tiny dictionary) and the first slice of the LDS image, clamped and
   // unconditional (a zero page stands in for an absent table)
   const bool prepped = LEAN || (!PREP && a0.pimg != nullptr);  // the prologue image is ready in HBM
@@ -707,7 +720,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
   }
   Tile<PSS> ta{};
   if constexpr (!PREP) {
-    ta = load_tile<PSS, LEAN>(a0, tile0, h, lane);
+    ta = load_tile<PSS, LEAN, PSUM>(a0, tile0, h, lane);
     if (PSS) h = load_hdr(a0, min(tile + W, ntiles - 1u), lane);
   }
   {
@@ -842,8 +855,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
                          : reinterpret_cast<uint8_t*>(rmk + 4 * KPE_RULE_CHUNK);
     // ---- prefetch the next tile into the other buffer, then evaluate `cur` ----
     // (unconditional, clamped: past the end it re-reads the last tile, never used)
-    nxt = load_tile<PSS, LEAN>(a, min(tile + W, ntiles - 1), h, lane);
-    if (PSS) h = load_hdr(a, min(tile + 2 * W, ntiles - 1), lane);
+    nxt = load_tile<PSS, LEAN, PSUM>(a, min(tile + W, ntiles - 1), h, lane);
+    if (PSS && !PSUM) h = load_hdr(a, min(tile + 2 * W, ntiles - 1), lane);
     pin_tile(cur);
     const uint32_t r = tile * 64 + lane;
     const bool live = r < n;
@@ -852,7 +865,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     bool err = false;
     const uint32_t need = a.need;
     if constexpr (PSS) {
-      fails = pss_tile<LEAN>(a, B, s_capb, cur, live, stage, lane, lp);
+      fails = pss_tile<LEAN, PSUM>(a, B, s_capb, cur, live, stage, lane, lp);
       const uint32_t cls = (cur.rec.x >> PR_CLASS_SH) & R_CLASS_MASK;
       err = live && (cls == R_CLASS_OTHER || (cur.rec.x & PR_DECODE_ERR));
       gvk = live ? cur.rec.y : 0u;
@@ -1111,6 +1124,9 @@ namespace {
 #define KPE_PAT_BLOCK 128  // C5 / C3 pattern kernel (events, profiles/r03_c_ldsframes): 256 x 8 frames 20.7 / 9.2 ms,
 #endif                     // 128 x 8 18.1 / 7.8, 256 x 6 17.2 / 7.0, 128 x 6 16.8 / 6.9, + 4 waves/SIMD 15.6 / 7.0
 // the lane's frame stack lives in LDS (FramesLds, word-planar: conflict-free at any mix of depths)
+#ifndef KPE_PAT_SPLIT
+#define KPE_PAT_SPLIT 1  // lanes per row (each takes every KPE_PAT_SPLIT-th pattern cell)
+#endif
 #ifndef KPE_PAT_MINW
 #define KPE_PAT_MINW 3  // 168 VGPRs: the inline map path spills at 128 (profiles/r03_e_inline)
 #endif
@@ -1120,11 +1136,12 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
   constexpr uint32_t kWaveWords = FramesLds::kWords * FramesLds::kDepth * 64u;
   __shared__ uint32_t s_fs[KPE_PAT_BLOCK / 64][kWaveWords];
   __shared__ uint8_t s_memo[KPE_PAT_MEMO][KPE_PAT_BLOCK];  // byte-planar: a lane's slot s at [s][lane]
-  const int64_t i = (int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x;
+  const int64_t i = ((int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x) / KPE_PAT_SPLIT;
+  const uint32_t part = threadIdx.x % KPE_PAT_SPLIT;
   if (i >= ap->n) return;
   const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
   pat_eval_row<FramesLds, LT>(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]}, &s_memo[0][threadIdx.x],
-                              KPE_PAT_BLOCK);
+                              KPE_PAT_BLOCK, part, KPE_PAT_SPLIT);
 }
 
 // Leaf table of a binding (PatArgs::ltab): grid y = slot, one thread per scalar of the corpus;
@@ -1262,7 +1279,7 @@ extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32
   if (n <= 0 || npr == 0) return hipSuccess;
   // one lane per row running every pattern rule (a rows x rules grid measured no faster on C5 and
   // slower on C3's 600 rules; it also doubled the VM code the kernel holds)
-  const dim3 grid((unsigned)((n + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK));
+  const dim3 grid((unsigned)((n * KPE_PAT_SPLIT + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK));
   if (lt) hipLaunchKernelGGL(kpe_pattern_kernel<true>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
   else hipLaunchKernelGGL(kpe_pattern_kernel<false>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
   return hipGetLastError();
@@ -1276,8 +1293,11 @@ extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipSt
 
 namespace {
 typedef void (*ScanFn)(const ScanArgs*);
+// narrow codes: 0 wide, 1 narrow, 2 the LEAN instantiation, | 4: PSUM (scan records, no lists)
 ScanFn scan_fn(int pss, int narrow) {
   if (pss && narrow == 2) return kpe_scan_kernel<true, true, false, true>;
+  if (pss && (narrow & 4))
+    return (narrow & 1) ? kpe_scan_kernel<true, true, false, false, true> : kpe_scan_kernel<true, false, false, false, true>;
   if (pss) return narrow ? kpe_scan_kernel<true, true, false> : kpe_scan_kernel<true, false, false>;
   return narrow ? kpe_scan_kernel<false, true, false> : kpe_scan_kernel<false, false, false>;
 }

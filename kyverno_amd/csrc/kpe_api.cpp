@@ -200,7 +200,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t pimg_words = 0, capb_lds = 0;
   size_t prep_dyn_bytes = 0;  // the prep kernel's LDS: the scan layout + the fuse area
   bool lean = false;  // LEAN scan instantiation (kind table; no check masks)
-  int lean_kind = 0;  // kpe_launch_scan narrow code of the LEAN scan: 3 kpe_lean_kernel, 2 the template
+  int lean_kind = 0;  // kpe_launch_scan narrow code of the LEAN scan: 7 kpe_lean5_kernel, 2 the template
+  int gen_code = 0;   // narrow code of the general scan: narrow | 4 with scan records (PSUM)
   uint32_t kt_lds = PRED_NONE, nkinds = 0;
   DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
   bool xargs_valid = false;
@@ -751,10 +752,12 @@ kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s, u
   D.psum_ready = true;
   return KPE_OK;
 }
-double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks) {
+double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks, bool psum) {
   double b = 0;
   const double n = (double)C.n;
-  if (P.any_pss) {
+  if (P.any_pss && psum) {
+    b += 16 * n + 12 * n;  // pod records + the scan records (each pod's failing versioned checks)
+  } else if (P.any_pss) {
     b += 16 * n + 16.0 * ((C.n + 63) / 64);  // pod records + wave headers
     b += 8.0 * C.c_sc.size();               // container records
     if (need & NEED_CAPS) b += 16.0 * C.capset_add.size();
@@ -1086,9 +1089,13 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   // offsets: the pod records under 4 GiB), else the template instantiation
   const uint64_t lim = (1ull << 32) - (1ull << 20);
   B.lean_kind = !lean ? 0 : (uint64_t)C.n * 16 + 4096 > lim ? 2 : 7;
-  if (B.lean_kind == 7 && !cc->d->psum_ready)
+  // every podSecurity program reads the corpus's scan records (LEAN5 alone, the general scan for
+  // each pod's failing versioned checks instead of its lists)
+  if (P.any_pss && !cc->d->psum_ready)
     if (kpe_status st = run_psum(C, *cc->d, s)) return st;
-  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : narrow ? 1 : 0, B.dyn_bytes);
+  // the general scan of a podSecurity program reads the scan records (PSUM instantiation, code | 4)
+  B.gen_code = (narrow ? 1 : 0) | (P.any_pss && cc->d->psum_ready ? 4 : 0);
+  B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : B.gen_code, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   {  // ApplyOne policies: contiguous rule ranges in ComputeRules order
     std::vector<uint32_t> segs;
@@ -1147,7 +1154,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   const size_t R = P.rules.size();
   static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
   const bool fresh = !B.inv_ready || no_cache || cold;
-  if (cold && B.lean && B.lean_kind == 7)  // a cold evaluation rebuilds the corpus's PSA summaries too
+  if (cold && P.any_pss)  // a cold evaluation rebuilds the corpus's PSA summaries too
     if (kpe_status st = run_psum(C, D, s)) return st;
   if (B.nblocks && fresh) {  // dictionary pass for large-domain predicates
     PredArgs pa{};
@@ -1285,7 +1292,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
   const bool lean_go = B.lean && (!masks || B.lean_kind == 7);  // LEAN5 writes check masks too
-  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : PD.narrow ? 1 : 0,
+  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : B.gen_code,
                          B.scan_blocks,
                          B.dyn_bytes, s));
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
@@ -1460,7 +1467,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
     const double mb = masks ? 4.0 * (double)C.n * (double)R : 0.0;
     ev.bytes = lean_go && B.lean_kind == 7 ? 12.0 * (double)C.n + (double)C.n * (double)R + mb  // scan records, rows
-                                           : scan_bytes(P, C, B.need, masks);
+                                           : scan_bytes(P, C, B.need, masks, D.psum_ready);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     ev.kind = lean_go ? B.lean_kind : 1;
     dev->pending.push_back(ev);
