@@ -197,8 +197,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     eng.evaluate_batch_async(ps, steps_batch)
-    eng.device.sync()
-    torch.cuda.synchronize()
+    torch.cuda.synchronize()  # hipDeviceSynchronize: every stream of the device, the library's included
     elapsed = time.perf_counter() - t0
     barrier()
     elapsed = max_over_ranks(elapsed, device=coll_dev)
