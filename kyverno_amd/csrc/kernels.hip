@@ -1124,9 +1124,6 @@ namespace {
 #define KPE_PAT_BLOCK 128  // C5 / C3 pattern kernel (events, profiles/r03_c_ldsframes): 256 x 8 frames 20.7 / 9.2 ms,
 #endif                     // 128 x 8 18.1 / 7.8, 256 x 6 17.2 / 7.0, 128 x 6 16.8 / 6.9, + 4 waves/SIMD 15.6 / 7.0
 // the lane's frame stack lives in LDS (FramesLds, word-planar: conflict-free at any mix of depths)
-#ifndef KPE_PAT_SPLIT
-#define KPE_PAT_SPLIT 1  // lanes per row (each takes every KPE_PAT_SPLIT-th pattern cell)
-#endif
 #ifndef KPE_PAT_MINW
 #define KPE_PAT_MINW 3  // 168 VGPRs: the inline map path spills at 128 (profiles/r03_e_inline)
 #endif
@@ -1136,12 +1133,11 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
   constexpr uint32_t kWaveWords = FramesLds::kWords * FramesLds::kDepth * 64u;
   __shared__ uint32_t s_fs[KPE_PAT_BLOCK / 64][kWaveWords];
   __shared__ uint8_t s_memo[KPE_PAT_MEMO][KPE_PAT_BLOCK];  // byte-planar: a lane's slot s at [s][lane]
-  const int64_t i = ((int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x) / KPE_PAT_SPLIT;
-  const uint32_t part = threadIdx.x % KPE_PAT_SPLIT;
+  const int64_t i = (int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x;
   if (i >= ap->n) return;
   const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
   pat_eval_row<FramesLds, LT>(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]}, &s_memo[0][threadIdx.x],
-                              KPE_PAT_BLOCK, part, KPE_PAT_SPLIT);
+                              KPE_PAT_BLOCK);
 }
 
 // Leaf table of a binding (PatArgs::ltab): grid y = slot, one thread per scalar of the corpus;
@@ -1279,7 +1275,11 @@ extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32
   if (n <= 0 || npr == 0) return hipSuccess;
   // one lane per row running every pattern rule (a rows x rules grid measured no faster on C5 and
   // slower on C3's 600 rules; it also doubled the VM code the kernel holds)
-  const dim3 grid((unsigned)((n * KPE_PAT_SPLIT + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK));
+  // (two or four lanes per row, each taking every 2nd / 4th pattern cell: C5 12.3 / 19.3 ms against
+  // 8.5, profiles/r04_i: the lanes of a wave then walk different rules; verdicts of a 64-column
+  // chunk written back once as whole words: C5 8.6 / C3 3.66 ms against 8.5 / 3.34, more spills,
+  // profiles/r04_j)
+  const dim3 grid((unsigned)((n + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK));
   if (lt) hipLaunchKernelGGL(kpe_pattern_kernel<true>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
   else hipLaunchKernelGGL(kpe_pattern_kernel<false>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
   return hipGetLastError();

@@ -868,13 +868,10 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 // Rules that carry the same pattern share a memo slot (PR_MEMO_SH): the row's first pending cell
 // of the slot is evaluated and the others take its verdict from `memo` (LDS bytes, slot s at
 // memo[s * memo_stride]; null: no memo).
-// part / nparts: this lane resolves every nparts-th pattern cell of the row from the part-th
-// (several lanes per row: more independent walks in flight per SIMD)
 template <class FS, bool LT = false>
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs, uint8_t* memo = nullptr,
-                                             uint32_t memo_stride = 0, uint32_t part = 0, uint32_t nparts = 1) {
+                                             uint32_t memo_stride = 0) {
   uint32_t memo_ok = 0;  // slots holding this row's verdict
-  uint32_t kc = 0;       // pattern cells of the row seen so far
   PatVMT<FS, LT> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
                 a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
@@ -906,7 +903,6 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       const uint32_t cq = c00 + q;
       const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
       if (pi == 0u) continue;
-      if (nparts > 1u && (kc++ % nparts) != part) continue;
       const uint32_t slot = memo ? a.rules[pi - 1u].flags >> PR_MEMO_SH : PR_NO_MEMO;
       if (slot < KPE_PAT_MEMO && ((memo_ok >> slot) & 1u)) {
         row[cq] = memo[slot * memo_stride];
