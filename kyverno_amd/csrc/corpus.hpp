@@ -81,6 +81,57 @@ struct Dict {
   }
 };
 
+// String -> id index whose strings live elsewhere (the caller's text pool): open addressing over
+// (hash, id + 1) slots like Dict, lookups by string_view with no allocation.
+struct StrIndex {
+  template <class Get>  // Get(id) -> std::string_view of that id's string
+  int64_t find(std::string_view s, uint64_t h, Get get) const {
+    if (slots.empty()) return -1;
+    const size_t mask = slots.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot& e = slots[i];
+      if (e.id1 == 0) return -1;
+      if (e.h == (uint32_t)(h >> 32) && get(e.id1 - 1) == s) return (int64_t)(e.id1 - 1);
+    }
+  }
+  void insert(uint64_t h, uint32_t id) {
+    if ((n + 1) * 2 > slots.size()) {  // grow: re-place every slot by its kept hash bits
+      std::vector<Slot> old;
+      old.swap(slots);
+      slots.assign(std::max<size_t>(64, old.size() * 2), Slot{0u, 0u, 0u});
+      for (const Slot& e : old)
+        if (e.id1) place(e);
+    }
+    place(Slot{(uint32_t)(h >> 32), id + 1, (uint32_t)h});
+    ++n;
+  }
+  static uint64_t hash(std::string_view s) {  // Dict's hash
+    uint64_t h = 0xcbf29ce484222325ull ^ s.size();
+    size_t i = 0;
+    for (; i + 8 <= s.size(); i += 8) {
+      uint64_t w;
+      __builtin_memcpy(&w, s.data() + i, 8);
+      h = (h ^ w) * 0x100000001b3ull;
+    }
+    for (; i < s.size(); ++i) h = (h ^ (unsigned char)s[i]) * 0x100000001b3ull;
+    h ^= h >> 33, h *= 0xff51afd7ed558ccdull, h ^= h >> 33, h *= 0xc4ceb9fe1a85ec53ull, h ^= h >> 33;
+    return h;
+  }
+
+ private:
+  struct Slot {
+    uint32_t h, id1, lo;  // high hash bits, id + 1 (0: empty), low hash bits (the slot index)
+  };
+  void place(const Slot& e) {
+    const size_t mask = slots.size() - 1;
+    size_t i = e.lo & mask;
+    while (slots[i].id1) i = (i + 1) & mask;
+    slots[i] = e;
+  }
+  std::vector<Slot> slots;
+  size_t n = 0;
+};
+
 struct DeviceCorpus;  // defined in kpe_api.cpp
 
 struct Corpus {
@@ -126,7 +177,10 @@ struct Corpus {
                                       // KPE_NO_IMAGES (no images: the context has no `images`)
   std::vector<KpeScalar> scal;        // scalar table (ids 0/1/2 = null/false/true)
   std::vector<char> scal_text;        // compareString texts
-  std::unordered_map<std::string, uint32_t> scal_str;
+  StrIndex scal_str;                  // string scalars by their text (scal_text)
+  std::string_view scal_text_of(uint32_t id) const {
+    return std::string_view(scal_text.data() + scal[id].text_off, scal[id].text_len);
+  }
   std::unordered_map<int64_t, uint32_t> scal_int;
   std::unordered_map<uint64_t, uint32_t> scal_float;
 

@@ -1275,9 +1275,9 @@ class DocBuilder {
     return C.scal_float[bits] = push_scalar(e);
   }
   uint32_t str_id(std::string_view v) {
-    std::string k(v);
-    auto it = C.scal_str.find(k);
-    if (it != C.scal_str.end()) return it->second;
+    const uint64_t h = StrIndex::hash(v);
+    const int64_t found = C.scal_str.find(v, h, [&](uint32_t id) { return C.scal_text_of(id); });
+    if (found >= 0) return (uint32_t)found;
     KpeScalar e{};
     e.flags = SC_T_STR | SC_TEXT;
     e.text_off = text(v), e.text_len = (uint32_t)v.size();
@@ -1298,7 +1298,9 @@ class DocBuilder {
         e.ival = (int64_t)((uint64_t)lo | ((uint64_t)hi << 32));
       }
     }
-    return C.scal_str[k] = push_scalar(e);
+    const uint32_t id = push_scalar(e);
+    C.scal_str.insert(h, id);
+    return id;
   }
   // What the condition set operators read from a string value (anyin.go:73-93): json.Valid
   // (and whether it is an array) and the InRange form
@@ -1640,6 +1642,8 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
         const KpeScalar& e = P.scal[k];
         const uint32_t ty = SC_TYPE(e.flags);
         uint32_t* slot = nullptr;
+        uint32_t str_slot = 0xFFFFFFFFu;  // string scalars: the index lookup's result
+        uint64_t str_h = 0;
         if (ty == SC_T_INT) {
           slot = &C.scal_int.emplace(e.ival, 0xFFFFFFFFu).first->second;
         } else if (ty == SC_T_FLOAT) {
@@ -1647,7 +1651,12 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
           memcpy(&bits, &e.fval, 8);
           slot = &C.scal_float.emplace(bits, 0xFFFFFFFFu).first->second;
         } else {
-          slot = &C.scal_str.emplace(std::string(P.scal_text.data() + e.text_off, e.text_len), 0xFFFFFFFFu).first->second;
+          const std::string_view sv(P.scal_text.data() + e.text_off, e.text_len);
+          const uint64_t h = StrIndex::hash(sv);
+          const int64_t found = C.scal_str.find(sv, h, [&](uint32_t id) { return C.scal_text_of(id); });
+          str_slot = found >= 0 ? (uint32_t)found : 0xFFFFFFFFu;
+          slot = &str_slot;
+          str_h = h;
         }
         if (*slot == 0xFFFFFFFFu) {
           KpeScalar g = e;
@@ -1661,6 +1670,7 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
           C.scal_text.insert(C.scal_text.end(), P.scal_text.begin() + e.text_off, P.scal_text.begin() + e.text_off + nb);
           *slot = (uint32_t)C.scal.size();
           C.scal.push_back(g);
+          if (slot == &str_slot) C.scal_str.insert(str_h, *slot);
         }
         sm[k] = *slot;
       }
