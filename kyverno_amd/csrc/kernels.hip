@@ -1136,8 +1136,16 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
   const int64_t i = (int64_t)blockIdx.x * KPE_PAT_BLOCK + threadIdx.x;
   if (i >= ap->n) return;
   const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
-  pat_eval_row<FramesLds, LT>(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]}, &s_memo[0][threadIdx.x],
-                              KPE_PAT_BLOCK);
+  pat_eval_row<FramesLds, LT, true>(*ap, r, FramesLds{&s_fs[threadIdx.x >> 6][threadIdx.x & 63u]},
+                                    &s_memo[0][threadIdx.x], KPE_PAT_BLOCK);
+}
+// The cells kpe_pattern_kernel marked KPE_DEEP_ (one lane per row; rows without marks only scan),
+// on a kPatStack-deep LDS frame stack (one-wave blocks: 25 KiB of LDS each).
+template <bool LT>
+__global__ void __launch_bounds__(64) kpe_pattern_deep_kernel(const PatArgs* __restrict__ ap) {
+  __shared__ uint32_t s_fs[FramesLdsDeep::kWords * FramesLdsDeep::kDepth * 64u];
+  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (r < ap->n) pat_deep_row<LT>(*ap, r, FramesLdsDeep{&s_fs[threadIdx.x]});
 }
 
 // Leaf table of a binding (PatArgs::ltab): grid y = slot, one thread per scalar of the corpus;
@@ -1280,8 +1288,14 @@ extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32
   // chunk written back once as whole words: C5 8.6 / C3 3.66 ms against 8.5 / 3.34, more spills,
   // profiles/r04_j)
   const dim3 grid((unsigned)((n + KPE_PAT_BLOCK - 1) / KPE_PAT_BLOCK));
-  if (lt) hipLaunchKernelGGL(kpe_pattern_kernel<true>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
-  else hipLaunchKernelGGL(kpe_pattern_kernel<false>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
+  const dim3 rows((unsigned)((n + 63) / 64));
+  if (lt) {
+    hipLaunchKernelGGL(kpe_pattern_kernel<true>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
+    hipLaunchKernelGGL(kpe_pattern_deep_kernel<true>, rows, dim3(64), 0, s, dargs);
+  } else {
+    hipLaunchKernelGGL(kpe_pattern_kernel<false>, grid, dim3(KPE_PAT_BLOCK), 0, s, dargs);
+    hipLaunchKernelGGL(kpe_pattern_deep_kernel<false>, rows, dim3(64), 0, s, dargs);
+  }
   return hipGetLastError();
 }
 

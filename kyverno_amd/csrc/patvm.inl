@@ -474,8 +474,9 @@ struct FramesPriv {
 #ifndef KPE_PAT_LDS_STACK
 #define KPE_PAT_LDS_STACK 6  // deeper walks re-run on the private stack (FramesPriv)
 #endif
-struct FramesLds {
-  static constexpr int kDepth = KPE_PAT_LDS_STACK;
+template <int D>
+struct FramesLdsD {
+  static constexpr int kDepth = D;
   static constexpr uint32_t kWords = 7u;  // PFrame
   uint32_t* b;
   __device__ __forceinline__ PFrame get(int i) const {
@@ -489,6 +490,8 @@ struct FramesLds {
     q[0] = f.kind_k, q[W] = f.r, q[2 * W] = f.pi, q[3 * W] = f.cnt, q[4 * W] = f.cur, q[5 * W] = f.x, q[6 * W] = f.c;
   }
 };
+using FramesLds = FramesLdsD<KPE_PAT_LDS_STACK>;   // kpe_pattern_kernel
+using FramesLdsDeep = FramesLdsD<kPatStack>;       // kpe_pattern_deep_kernel
 
 template <class FS, bool LT = false>
 struct PatVMT {
@@ -868,7 +871,10 @@ __device__ __forceinline__ uint32_t pat_eval_cell(VM& vm, uint32_t pi) {
 // Rules that carry the same pattern share a memo slot (PR_MEMO_SH): the row's first pending cell
 // of the slot is evaluated and the others take its verdict from `memo` (LDS bytes, slot s at
 // memo[s * memo_stride]; null: no memo).
-template <class FS, bool LT = false>
+// DEFER: a cell that comes back undecided from a shallow (LDS) stack is marked KPE_DEEP_ for
+// kpe_pattern_deep_kernel instead of being re-walked here (the kernel then holds one copy of the
+// VM, not two).
+template <class FS, bool LT = false, bool DEFER = false>
 __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs, uint8_t* memo = nullptr,
                                              uint32_t memo_stride = 0) {
   uint32_t memo_ok = 0;  // slots holding this row's verdict
@@ -911,11 +917,52 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       uint32_t v = pat_eval_cell(vm, pi - 1u);
       if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
         // a shallow (LDS) stack may have overflowed: the lane-private kPatStack-deep one decides
-        PatVMT<FramesPriv> deep{a, vm.doc, vm.root, vm.pv, 0u};
-        v = pat_eval_cell(deep, pi - 1u);
+        if constexpr (DEFER) {
+          row[cq] = (uint8_t)KPE_DEEP_;
+          continue;
+        } else {
+          PatVMT<FramesPriv, LT> deep{a, vm.doc, vm.root, vm.pv, 0u};
+          v = pat_eval_cell(deep, pi - 1u);
+        }
       }
       row[cq] = (uint8_t)v;
       if (slot < KPE_PAT_MEMO) memo[slot * memo_stride] = (uint8_t)v, memo_ok |= 1u << slot;
+    }
+  }
+}
+
+// kpe_pattern_deep_kernel's body for row r: its KPE_DEEP_ cells walked again on a kPatStack-deep
+// frame stack (the kernel's LDS one; the host check's private one): walks deeper than the main
+// kernel's LDS stack, and cells undecided for other reasons, which come back undecided again.
+template <bool LT = false, class FS = FramesPriv>
+__device__ __forceinline__ void pat_deep_row(const PatArgs& a, int64_t r, FS fs = FS{}) {
+  uint8_t* row = a.verdicts + (size_t)r * a.R;
+  const uint64_t start = (uint64_t)r * a.R;
+  const uint32_t* words = reinterpret_cast<const uint32_t*>(a.verdicts);
+  for (uint32_t c00 = 0; c00 < a.R; c00 += 64u) {
+    const uint64_t p0 = start + c00;
+    const uint32_t sh = (uint32_t)(p0 & 3u);
+    uint32_t w[17];
+#pragma unroll
+    for (uint32_t j = 0; j < 17u; ++j) w[j] = words[(p0 >> 2) + j];
+    uint64_t mark = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 16u; ++j) {
+      const uint32_t x = sh ? (uint32_t)((((uint64_t)w[j + 1u] << 32) | w[j]) >> (8u * sh)) : w[j];
+      const uint32_t t = x ^ 0x26262626u;  // KPE_DEEP_ cells -> 0
+      const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
+      mark |= (uint64_t)(((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4u * j);
+    }
+    if (a.R - c00 < 64u) mark &= (1ull << (a.R - c00)) - 1ull;
+    if (!mark) continue;
+    PatVMT<FS, LT> vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[r],
+                      a.pvals + (size_t)r * a.nvars, 0u, 0u, 0u, -1, fs, nullptr};
+    while (mark) {
+      const uint32_t q = (uint32_t)__builtin_ctzll(mark);
+      mark &= mark - 1ull;
+      const uint32_t cq = c00 + q;
+      const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
+      row[cq] = (uint8_t)(pi ? pat_eval_cell(vm, pi - 1u) : KPE_UNDECIDED_);
     }
   }
 }

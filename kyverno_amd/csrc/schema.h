@@ -304,6 +304,8 @@ enum KpeCheckVersion {
                       // podSecurity controls (validate_pss.go:88-104), resolved by kpe_pssx_kernel
 #define KPE_VERDICT_SLACK 72u  // bytes past the N x R matrix: the pattern kernel's 64-column row
                                // scan reads 17 whole words from a row's start
+#define KPE_DEEP_ 0x26  // device-internal: a pattern cell whose walk overflowed the LDS frame stack,
+                       // re-walked by kpe_pattern_deep_kernel on the lane-private stack
 #define KPE_XDEFER_ 0x10  // device-internal flag (XE_DEFER rules): the exception's match block
                           // held; kpe_cond_kernel applies the exception after the preconditions
 

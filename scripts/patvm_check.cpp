@@ -140,6 +140,18 @@ int main(int argc, char** argv) {
     for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesLds{plane.data()}, memo.data(), 1u);
     a.verdicts = keep;
   }
+  // ... with undecided cells of the LDS stack deferred to the deep pass (kpe_pattern_kernel +
+  // kpe_pattern_deep_kernel) ...
+  std::vector<uint8_t> defer_v(verdicts);
+  {
+    std::vector<uint32_t> plane(FramesLds::kWords * FramesLds::kDepth * 64u, 0xDEADBEEFu);
+    uint8_t* keep = a.verdicts;
+    a.verdicts = defer_v.data();
+    std::vector<uint8_t> memo(KPE_PAT_MEMO, 0xEE);
+    for (int64_t r = 0; r < a.n; ++r) pat_eval_row<FramesLds, false, true>(a, r, FramesLds{plane.data()}, memo.data(), 1u);
+    for (int64_t r = 0; r < a.n; ++r) pat_deep_row(a, r);
+    a.verdicts = keep;
+  }
   // ... through the leaf table (kpe_leaf_table_kernel restated: one slot per leaf without
   // variables; the LT instance when every leaf has one) ...
   std::vector<uint8_t> lt_v(verdicts);
@@ -172,6 +184,7 @@ int main(int argc, char** argv) {
   for (int64_t r = 0; r < a.n; ++r) pat_eval_row(a, r, FramesPriv{});
   if (lds_v != verdicts) return fprintf(stderr, "LDS frame-stack walk (with memo) differs from the private-stack walk\n"), 1;
   if (lt_v != verdicts) return fprintf(stderr, "leaf-table walk differs from the private-stack walk\n"), 1;
+  if (defer_v != verdicts) return fprintf(stderr, "deferred deep walk differs from the private-stack walk\n"), 1;
   FILE* f = fopen(argv[3], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
