@@ -1144,8 +1144,12 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
 template <bool LT>
 __global__ void __launch_bounds__(64) kpe_pattern_deep_kernel(const PatArgs* __restrict__ ap) {
   __shared__ uint32_t s_fs[FramesLdsDeep::kWords * FramesLdsDeep::kDepth * 64u];
-  const int64_t r = (int64_t)blockIdx.x * 64 + threadIdx.x;
-  if (r < ap->n) pat_deep_row<LT>(*ap, r, FramesLdsDeep{&s_fs[threadIdx.x]});
+  const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i >= ap->n) return;
+  // rows through doc_perm (grouped by kind, then tape size) like the main kernel: the rows with deep
+  // cells (one kind's deeper autogen patterns) fill whole waves instead of a few lanes of each
+  const int64_t r = ap->perm ? (int64_t)ap->perm[i] : i;
+  pat_deep_row<LT>(*ap, r, FramesLdsDeep{&s_fs[threadIdx.x]});
 }
 
 // Leaf table of a binding (PatArgs::ltab): grid y = slot, one thread per scalar of the corpus;

@@ -4,7 +4,7 @@
 # (LDS stack depth 6 default, 4 / 5 via KPE_LIB variant builds), traces and traffic passes.
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
-TAG=${TAG:-r04_l}
+TAG=${TAG:-r04_m}
 O=gpurun_out/$TAG
 mkdir -p $O
 step() {  # step <name> <timeout> <cmd...>
@@ -19,7 +19,7 @@ step() {  # step <name> <timeout> <cmd...>
 TAILN=4 step pytest_pat 500 python -u -m pytest tests/test_gpu_pattern.py tests/test_gpu_configs.py tests/test_pattern_vars.py tests/test_pattern_messages.py tests/test_conditions_device.py -m gpu -x -q --timeout 300 --timeout-method thread
 for c in c5 c3; do
   step bench_$c 200 python bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0
-  for v in d4 d5; do
+  for v in ; do
     step ${c}_$v 200 env KPE_LIB=kyverno_amd/build/diag/libkpe_$v.so python bench.py --config $c --steps 20 --warmup 3 --cpu-sample 0
   done
   step trace_$c 200 rocprofv3 --kernel-trace --stats -d $O/prof_$c -o $c --output-format csv -- python3 bench.py --config $c --steps 10 --warmup 2 --cpu-sample 0
