@@ -472,7 +472,7 @@ struct FramesPriv {
   __device__ __forceinline__ void put(int i, const PFrame& f) { st[i] = f; }
 };
 #ifndef KPE_PAT_LDS_STACK
-#define KPE_PAT_LDS_STACK 6  // deeper walks re-run on the private stack (FramesPriv)
+#define KPE_PAT_LDS_STACK 5  // deeper walks: kpe_pattern_deep_kernel. 4 / 5 / 6 frames, C5 9.0 / 7.0 / 7.6 ms, C3 3.1 / 3.2 / 3.5 ms (profiles/r04_n)
 #endif
 template <int D>
 struct FramesLdsD {
