@@ -627,7 +627,9 @@ typedef struct KpeCond {
 // PR_NO_MEMO: none
 #define PR_MEMO_SH 16
 #define PR_NO_MEMO 0xFFFFu
+#ifndef KPE_PAT_MEMO
 #define KPE_PAT_MEMO 32
+#endif
 typedef struct KpePatRule {
   uint32_t col, flags, r0, nr;
 } KpePatRule;
