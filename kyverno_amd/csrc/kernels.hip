@@ -1125,7 +1125,8 @@ namespace {
 #endif                     // 128 x 8 18.1 / 7.8, 256 x 6 17.2 / 7.0, 128 x 6 16.8 / 6.9, + 4 waves/SIMD 15.6 / 7.0
 // the lane's frame stack lives in LDS (FramesLds, word-planar: conflict-free at any mix of depths)
 #ifndef KPE_PAT_MINW
-#define KPE_PAT_MINW 3  // 168 VGPRs: the inline map path spills at 128 (profiles/r03_e_inline)
+#define KPE_PAT_MINW 3  // the leaf-table instance takes 111 VGPRs (4 waves/SIMD, as many as the 8 LDS-bound
+                        // blocks per CU hold), the one without 166; the inline map path spills at 128 (r03_e_inline)
 #endif
 // LT: the leaf-table instance (PatVMT LT), for programs whose leaves all have table slots.
 template <bool LT>
