@@ -15,15 +15,16 @@ are all-reduced once over RCCL after the timed region).
 One step = one evaluation pass of the compiled program over one resident shard
 (kpe_evaluate_async: resource-scan kernel, then the condition / exclusion / pattern kernels when
 the program has such rules); the K timed steps are enqueued by one kpe_evaluate_batch_async call,
-which sends a run of LEAN5 steps (C2) as ceil(K / 64) multi-shard launches of
-kpe_lean5_batch_kernel (one grid over the steps' shards) and every other step as its own launch.
-Distinct shards are rotated so that the bytes a step's scan reads were last touched more than
-twice the 256 MiB Infinity Cache ago: C2 reads a 12-byte scan record per pod and writes R bytes,
-15 MB per 1M-pod shard, so it rotates 41 shards (615 MB; the count is derived from the scan's
-algorithmic bytes, `--replicas` overrides). The per-pod scan records (pod word, kind and PSA
-summary) are built on the device when a shard is first bound (policy-independent, like the pod
-records); the cold leg re-runs them with the rest of the per-corpus prologue. Per-rule counters
-are built once, after the timed region (kpe_fetch), not per step.
+which sends a run of LEAN steps (C2) as ceil(K / 24) multi-shard launches of kpe_lean6_kernel (one
+grid over the steps' shards) and every other step as its own launch. Every C2 step reads each
+pod's 16-byte record, its tile header and its container / volume / sysctl / annotation list items
+and decides the 17 PSA checks from them: nothing per pod is carried from one step to the next.
+What a step does not rebuild is per corpus DICTIONARY: one code byte per distinct capability set,
+sysctl name and annotation key / value (kpe_psa_codes_kernel), like the interned ids themselves,
+and the binding's kind table; the cold leg rebuilds those too. Distinct shards are rotated so that
+the bytes a step reads were last touched more than twice the 256 MiB Infinity Cache ago (the count
+is derived from the algorithmic bytes of one step, `--replicas` overrides). Per-rule counters are
+built once, after the timed region (kpe_fetch), not per step.
 """
 import math
 import argparse
@@ -38,7 +39,7 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 IC_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
 # kpe_kernel_stats.scan_kernel -> kernel name (as rocprofv3 lists it)
-SCAN_KERNELS = {1: "kpe_scan_kernel", 2: "kpe_scan_kernel", 7: "kpe_lean5_kernel", 9: "kpe_lean5_batch_kernel"}
+SCAN_KERNELS = {1: "kpe_scan_kernel", 2: "kpe_scan_kernel", 7: "kpe_lean6_kernel", 9: "kpe_lean6_kernel"}
 
 
 def cpu_budget():
@@ -116,7 +117,7 @@ def main():
     elif rep_def:
         replicas = rep_def
     else:  # C2: enough shards that a shard's scan bytes leave the Infinity Cache before its next use
-        alg = (12.0 + 3.0) * n  # LEAN5: 12-byte scan record read, R = 3 verdict bytes written per pod
+        alg = 43.0 * n  # LEAN6 on the C2 mix: ~40 B of pod record, header and list items read, R = 3 written
         replicas = max(2, math.ceil(2.25 * IC_BYTES / alg))
     # HBM bytes per scan launch from the FETCH_SIZE / WRITE_SIZE passes (scripts/pmc_summary.py);
     # perf/ travels to the GPU box, profiles/ does not
@@ -316,9 +317,10 @@ def main():
                      "achieved_per_step": step_bytes / (ms_per_step * 1e-3) / 1e9,
                      "single_stream_step_ms": single_stream_ms,
                      "note": ("kernel_ms: HIP events per launch, launches serialised on one stream "
-                              "(kpe_lean5_batch_kernel: one launch over up to 64 shards, i.e. several "
-                              "steps, alg_bytes_per_launch its shards' bytes); other kernels: one launch "
-                              "per step, and consecutive shards' launches overlap on two streams in the "
+                              "(kpe_lean6_kernel over several shards: one launch over up to 24 shards, i.e. "
+                              "several steps, alg_bytes_per_launch its shards' bytes: pod records, tile headers, "
+                              "container / volume / sysctl / annotation items, code bytes, verdicts); other kernels: "
+                              "one launch per step, and consecutive shards' launches overlap on two streams in the "
                               "timed region; dict / pattern kernel ms are 0 when no such kernel ran")}
         if pat_ms > scan_ms and st.pattern_bytes > 0:
             # pattern-dominated configurations (C3, C5): the dominant kernel is the pattern VM;

@@ -1326,15 +1326,10 @@ ScanFn prep_fn(int pss, int narrow) {
 }
 }  // namespace
 
-// Scan grid. kpe_lean5_kernel (narrow code 7): one 64-pod tile per wave, no persistent loop.
-// The others: persistent, as many blocks as can be resident at once (occupancy x CUs), capped
-// by the number of 256-resource tiles.
+// Scan grid: persistent, as many blocks as can be resident at once (occupancy x CUs), capped by
+// the number of 256-resource tiles. (The LEAN evaluation, kpe_lean6_kernel, sizes its own grid.)
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes) {
-  if (n <= 0) return 0;
-  if (pss && narrow == 7) {
-    const int64_t waves = (n + 63) / 64;
-    return (uint32_t)((waves + kLB / 64 - 1) / (kLB / 64));
-  }
+  if (n <= 0 || (pss && narrow == 7)) return 0;
   static thread_local int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -1352,10 +1347,7 @@ extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_byt
 extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* hargs, int64_t n, int pss, int narrow,
                                       uint32_t grid, size_t dyn_bytes, hipStream_t s) {
   if (n == 0 || grid == 0) return hipSuccess;
-  if (pss && narrow == 7) {  // kpe_lean5_kernel takes its arguments by value
-    hipLaunchKernelGGL(kpe_lean5_kernel, dim3(grid), dim3(kLB), dyn_bytes, s, *hargs);
-    return hipGetLastError();
-  }
+  (void)hargs;
   hipLaunchKernelGGL(scan_fn(pss, narrow), dim3(grid), dim3(kBlock), dyn_bytes, s, dargs);
   return hipGetLastError();
 }
@@ -1419,35 +1411,34 @@ extern "C" hipError_t kpe_launch_selmask(const SelMaskArgs* a, hipStream_t s) {
   hipLaunchKernelGGL(kpe_selmask_kernel, dim3((m + 255u) / 256u, 3), dim3(256), 0, s, *a);
   return hipGetLastError();
 }
-// Several bound shards of one LEAN5 program in one grid (kpe_evaluate_batch_async).
-extern "C" hipError_t kpe_launch_lean_batch(const LeanBatchArgs* a, size_t dyn_bytes, hipStream_t s) {
+// The LEAN evaluation of one or more bound shards of one program in one grid (lean.inl).
+template <int T>
+static hipError_t lean6_go(const LeanBatchArgs* a, uint32_t grid, size_t dyn_bytes, int lc, hipStream_t s) {
+  if (lc) hipLaunchKernelGGL((kpe_lean6_kernel<T, true>), dim3(grid), dim3(kLB), dyn_bytes, s, *a);
+  else hipLaunchKernelGGL((kpe_lean6_kernel<T, false>), dim3(grid), dim3(kLB), dyn_bytes, s, *a);
+  return hipGetLastError();
+}
+extern "C" hipError_t kpe_launch_lean6(const LeanBatchArgs* a, size_t dyn_bytes, int lc, hipStream_t s) {
   const uint32_t grid = a->blk0[a->nshards];
   if (a->nshards == 0 || grid == 0) return hipSuccess;
   switch (a->tpw) {
-    case 8: hipLaunchKernelGGL(kpe_lean5_batch_kernel<8>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
-    case 4: hipLaunchKernelGGL(kpe_lean5_batch_kernel<4>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
-    case 2: hipLaunchKernelGGL(kpe_lean5_batch_kernel<2>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
-    case 1: hipLaunchKernelGGL(kpe_lean5_batch_kernel<1>, dim3(grid), dim3(kLB), dyn_bytes, s, *a); break;
+    case 4: return lean6_go<4>(a, grid, dyn_bytes, lc, s);
+    case 2: return lean6_go<2>(a, grid, dyn_bytes, lc, s);
+    case 1: return lean6_go<1>(a, grid, dyn_bytes, lc, s);
     default: return hipErrorInvalidValue;
   }
+}
+// The PSA dictionary codes of a corpus (lean.inl), one launch.
+extern "C" hipError_t kpe_launch_psa_codes(const PsaCodeArgs* a, hipStream_t s) {
+  uint32_t m = a->L.ncapsets;
+  for (int d = 1; d < 4; ++d) m = std::max(m, a->dict_n[d]);
+  if (m == 0) return hipSuccess;
+  hipLaunchKernelGGL(kpe_psa_codes_kernel, dim3((m + 255u) / 256u, 4), dim3(256), 0, s, *a);
   return hipGetLastError();
 }
-// The per-pod PSA summary of a corpus (lean.inl): dictionary codes, capability-set codes, then
-// one wave per 64-pod tile.
+// The general scan's per-pod PSA records (lean.inl), one wave per 64-pod tile.
 extern "C" hipError_t kpe_launch_psum(const PsumArgs* a, hipStream_t s) {
   if (a->n <= 0) return hipSuccess;
-  uint32_t dmax = 0;
-  for (int d = 0; d < 4; ++d) dmax = std::max(dmax, a->dict_n[d]);
-  if (dmax) {
-    hipLaunchKernelGGL(kpe_psa_dict_kernel, dim3((dmax + 255u) / 256u, 4), dim3(256), 0, s, *a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
-  if (a->ncapsets) {
-    hipLaunchKernelGGL(kpe_psa_capset_kernel, dim3((a->ncapsets + 255u) / 256u), dim3(256), 0, s, *a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-  }
   hipLaunchKernelGGL(kpe_psum_kernel, dim3((a->ntiles + 3u) / 4u), dim3(256), 0, s, *a);
   return hipGetLastError();
 }

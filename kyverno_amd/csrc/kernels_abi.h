@@ -180,9 +180,9 @@ struct ScanArgs {
   uint32_t* masks;    // n x nrules failing versioned checks (bit v = KpeCheckVersion v) or null
 };
 
-// The per-pod PSA summary (lean.inl kpe_psa_dict_kernel / kpe_psa_capset_kernel / kpe_psum_kernel):
-// the four dictionaries it codes (PsumArgs::dict_*[PSD_*]) and the fixed sets of the PSA library
-// (pss_fixed.hpp) as bits of a string's set-hit word (PsumArgs::fixed entries' set numbers).
+// The PSA dictionary codes of a corpus (lean.inl kpe_psa_codes_kernel): the four dictionaries it
+// codes (PsaCodeArgs::dict_*[PSD_*]) and the fixed sets of the PSA library (pss_fixed.hpp) as bits
+// of a string's set-hit word (the fixed table's set numbers).
 #define PSD_CAP 0
 #define PSD_SYSCTL 1
 #define PSD_ANNK 2
@@ -197,17 +197,40 @@ struct ScanArgs {
 #define PSF_SECCOMP_POD_KEY 7
 #define PSF_APPARMOR_OK 8
 #define PSF_SECCOMP_ANN_OK 9
-struct PsumArgs {
-  int64_t n;
-  uint32_t ntiles, ncapsets;
-  const uint32_t *rec, *hdr, *crec, *vol_src, *sys_id, *pann_kv, *capsets, *c_sann;
+// Fixed-set table (psa_fixed_table in kpe_api.cpp), 32-bit words:
+//   [0] exact entries E, [1] prefix entries X, [2 + len] (first | end << 16) of the exact entries
+//   of byte length len < KPE_PSF_MAXLEN (sorted by length), then E + X entries of 2 words
+//   {set | prefix << 7 | len << 8, word index of the literal}, then the literals (4-byte padded).
+// A prefix entry is a literal followed by one trailing '*' (go-wildcard: a byte-prefix match).
+#define KPE_PSF_MAXLEN 64u
+#define KPE_PSF_ENT0 (2u + KPE_PSF_MAXLEN)
+// Code bytes of a corpus: [capability sets | sysctls | annotation keys | annotation values], each
+// part 4-byte aligned (PsaCodes offsets). Capability set: CS_* bits (kernels.hip) | 8: the set
+// holds a capability id >= 64 (never read: such a resource is a per-resource limit row); sysctl:
+// bit v = outside version v's allowed set; annotation key: bit 0 AppArmor container key, bit 1
+// pod seccomp key; annotation value: bit 0 allowed AppArmor profile, bit 1 allowed seccomp profile.
+struct PsaCodes {
+  uint32_t ncapsets, nsysd, nannk, nannv;  // entries of each part
+  uint32_t o_sys, o_annk, o_annv, bytes;   // byte offsets of the parts, total bytes
+};
+struct PsaCodeArgs {
   const uint8_t* dict_bytes[4];
   const uint32_t* dict_off[4];
   uint32_t dict_n[4];
-  const uint8_t* fixed;  // fixed-set table: [set | prefix << 7 | len << 8] + literal, 4-byte padded
-  uint32_t fixed_len, pad_;
-  uint8_t* codes[4];     // code byte per dictionary string (scratch)
-  uint8_t* csb;          // code byte per capability set (scratch)
+  const uint32_t* capsets;  // (add lo, add hi, drop lo, drop hi) capability-id masks per set
+  const uint32_t* fixed;    // fixed-set table (above)
+  uint32_t fixed_words, pad_;
+  PsaCodes L;
+  uint8_t* codes;           // out
+};
+// kpe_psum_kernel (the general scan's per-pod PSA records, rebuilt by every evaluation of a
+// podSecurity program that is not LEAN, and kpe_corpus_psa_summary)
+struct PsumArgs {
+  int64_t n;
+  uint32_t ntiles, pad_;
+  const uint32_t *rec, *hdr, *crec, *vol_src, *sys_id, *pann_kv, *c_sann;
+  const uint8_t* codes;  // PsaCodeArgs::codes
+  PsaCodes L;
   uint32_t* psum;        // out: 3 words per pod (pod word, failing versioned checks, kind << 16)
   uint32_t* summ;        // out (or null): 2 words per pod (OR of container states, codes; schema.h PS_*)
 };
@@ -228,24 +251,34 @@ struct SelMaskArgs {
   uint64_t* nsq;             // out: nrows + 1 entries
 };
 
-// kpe_lean5_batch_kernel: one launch over up to KPE_LEAN_BATCH bound shards of one LEAN5 program
-// (kpe_evaluate_batch_async). Passed by value (< 4 KiB of kernel arguments): block b of the grid
-// belongs to the shard s with blk0[s] <= b < blk0[s + 1].
-#define KPE_LEAN_BATCH 64
+// kpe_lean6_kernel: the LEAN evaluation of one or more bound shards of one program in one launch
+// (kpe_evaluate_async: one shard; kpe_evaluate_batch_async: up to KPE_LEAN_BATCH). Passed by
+// value (< 4 KiB of kernel arguments): block b of the grid belongs to the shard s with
+// blk0[s] <= b < blk0[s + 1]. Every launch reads each pod's record and its container, volume,
+// sysctl and annotation lists: nothing per pod is carried over from an earlier evaluation.
+#define KPE_LEAN_BATCH 24
 struct LeanShard {
-  const uint32_t* psum;   // 3 words per pod (PsumArgs::psum)
+  const uint32_t *rec, *hdr, *crec, *vol, *sys, *pann, *sann;  // the corpus's PSS columns
+  const uint8_t* codes;   // the corpus's PSA dictionary codes (PsaCodeArgs::codes)
   const uint32_t* kt;     // the binding's kind table: matched-rule mask per kind id (prologue image)
   uint8_t* verdicts;      // n x R
   uint32_t* masks;        // n x R failing versioned checks, or null
-  uint32_t n, nkinds;
+  uint32_t n, nkinds, nctr, nvol, nsys, npann;
+  PsaCodes L;
 };
 struct LeanBatchArgs {
-  uint32_t nshards, nrules, ncls, cv_union, pss_rules, err_rules, pat_rules, kt_words;  // kt_words: max nkinds
+  uint32_t nshards, nrules, ncls, cv_union, pss_rules, err_rules, pat_rules, need;
+  uint32_t kt_words, code_words, wave_words, tpw;  // LDS: kind table, codes (LC), per-wave stage
   const uint32_t* narrow_cls;  // (cv classes, rule mask) pairs of the program
   uint32_t blk0[KPE_LEAN_BATCH + 1];  // a block covers 4 * tpw tiles of 64 pods
-  uint32_t tpw;                       // tiles per wave: 1, 2, 4 or 8
   LeanShard sh[KPE_LEAN_BATCH];
 };
+// Per-wave LDS stage of kpe_lean6_kernel: a tile's staged list items (container codes as uint2,
+// volume / sysctl / annotation codes as bytes); items past these counts are loaded again.
+#define KPE_L6_CTR 128u
+#define KPE_L6_VOL 128u
+#define KPE_L6_SMALL 64u
+#define KPE_L6_STAGE_BYTES (KPE_L6_CTR * 8u + KPE_L6_VOL + 2u * KPE_L6_SMALL)
 
 // kpe_pattern_kernel arguments (device-resident, one copy per binding)
 struct PatArgs {

@@ -46,7 +46,8 @@ extern "C" hipError_t kpe_launch_scan(const ScanArgs* dargs, const ScanArgs* har
                                       size_t dyn_bytes, hipStream_t s);
 extern "C" uint32_t kpe_scan_grid(int64_t n, int pss, int narrow, size_t dyn_bytes);
 extern "C" hipError_t kpe_launch_psum(const PsumArgs* a, hipStream_t s);
-extern "C" hipError_t kpe_launch_lean_batch(const LeanBatchArgs* a, size_t dyn_bytes, hipStream_t s);
+extern "C" hipError_t kpe_launch_psa_codes(const PsaCodeArgs* a, hipStream_t s);
+extern "C" hipError_t kpe_launch_lean6(const LeanBatchArgs* a, size_t dyn_bytes, int lc, hipStream_t s);
 extern "C" hipError_t kpe_launch_selmask(const SelMaskArgs* a, hipStream_t s);
 extern "C" hipError_t kpe_launch_leaf_table(const PatArgs* dargs, const uint32_t* slot_leaf, uint32_t nslots,
                                             uint64_t nscal, hipStream_t s);
@@ -112,8 +113,8 @@ constexpr uint32_t kMaxTerms = 1024;       // distinct match terms (term masks: 
 constexpr uint32_t kMaxProgLds = 4096;     // filters + filter terms staged in LDS
 constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
 constexpr uint32_t kMaxFuseWords = 4096;   // fuse image <= 16 KiB of LDS
-constexpr uint32_t kLeanBatchKinds = 8192; // kind table words a multi-shard LEAN5 block stages
-constexpr uint64_t kLeanBatchMinWaves = 16384;  // 256 CUs x 4 SIMDs x 16 waves
+constexpr uint32_t kLeanBatchKinds = 4096; // kind table words a LEAN6 block stages
+constexpr uint32_t kLeanCodeLds = 8192;    // code bytes a LEAN6 block stages in LDS (else read from L2)
 constexpr size_t kMaxFusePairs = 1024;     // (string, pattern) pairs evaluated per block
 
 }  // namespace
@@ -142,6 +143,12 @@ struct kpe_device {
   uint64_t launches = 0;
   double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0, last_pbytes = 0;
   int last_kind = 0;
+  // knobs, read once at kpe_device_open: KPE_NO_BIND_CACHE (recompute per-binding products every
+  // evaluation), KPE_PATVM_ERR (report a KPE_PATVM_CHECK build's bounds flags), KPE_LEAN6_MINW /
+  // KPE_LEAN6_TPW (waves a LEAN6 launch keeps / tiles per wave, for A/B runs)
+  bool no_cache = false, patvm_err = false;
+  uint64_t lean_min_waves = 16384;  // 256 CUs x 4 SIMDs x 16 waves
+  uint32_t lean_tpw = 0;
   hipEvent_t get_ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -240,10 +247,12 @@ struct DeviceCorpus {
   DevBuf ctr_off, vol_off, sys_off, pann_off, c_name, c_image, c_sann_key, c_sec_str, c_pm_str, c_selt_str, c_selu_str,
       c_selr_str, cport_off, cport_str, pann_k, pann_v, p_cold;
   bool cold = false;
-  // per-pod PSA summaries (kpe_psum_kernel; read by kpe_lean5_kernel), built on the device at the
-  // first binding of a LEAN program; the dictionary / capability-set codes are its scratch
-  DevBuf psum, psa_codes, psa_csb, psa_fixed;
-  bool psum_ready = false;
+  // PSA dictionary codes (kpe_psa_codes_kernel; policy-independent, per distinct string), built at
+  // the first binding of a podSecurity program; psum: the general scan's per-pod records, scratch
+  // rebuilt by every evaluation that reads them (kpe_psum_kernel)
+  DevBuf psum, psa_codes, psa_fixed;
+  PsaCodes psa_L{};
+  bool codes_ready = false;
   Binding bind;
   bool has_masks = false;
 };
@@ -276,6 +285,13 @@ kpe_status kpe_device_open(int ordinal, kpe_device** out) {
   if (!d) return fail(KPE_E_DEVICE, "oom");
   d->ordinal = ordinal;
   if (const char* ev = getenv("KPE_LANES")) d->nlanes = std::max(1, std::min(kMaxLanes, atoi(ev)));
+  d->no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
+  d->patvm_err = getenv("KPE_PATVM_ERR") != nullptr;
+  if (const char* ev = getenv("KPE_LEAN6_MINW")) d->lean_min_waves = std::max(1, atoi(ev));
+  if (const char* ev = getenv("KPE_LEAN6_TPW")) {
+    const int t = atoi(ev);
+    d->lean_tpw = t == 1 || t == 2 || t == 4 ? (uint32_t)t : 0u;
+  }
   for (int k = 0; k < d->nlanes; ++k) {
     e = hipStreamCreateWithFlags(&d->lanes[k], hipStreamNonBlocking);
     if (e != hipSuccess) {
@@ -691,19 +707,20 @@ uint32_t need_flags(const kpe::Program& P) {
   }
   return need;
 }
-// The fixed-set table of kpe_psa_dict_kernel (kernels_abi.h PsumArgs::fixed) from the PSA
-// library's sets (pss_fixed.hpp): [set | prefix << 7 | len << 8] + literal, 4-byte padded.
-const std::vector<uint8_t>& psa_fixed_table() {
-  static const std::vector<uint8_t> tab = [] {
-    std::vector<uint8_t> t;
+// The fixed-set table of kpe_psa_codes_kernel (layout: kernels_abi.h KPE_PSF_*) from the PSA
+// library's sets (pss_fixed.hpp): exact literals bucketed by byte length, then the prefix globs.
+const std::vector<uint32_t>& psa_fixed_table() {
+  static const std::vector<uint32_t> tab = [] {
+    struct Ent {
+      uint32_t set;
+      bool prefix;
+      std::string lit;
+    };
+    std::vector<Ent> ex, px;
     auto add = [&](uint32_t set, const std::vector<std::string>& globs) {
       for (const auto& g : globs) {
         const bool prefix = !g.empty() && g.back() == '*';
-        const std::string lit = prefix ? g.substr(0, g.size() - 1) : g;
-        const uint32_t h = set | (prefix ? 1u << 7 : 0u) | (uint32_t)lit.size() << 8;
-        for (int k = 0; k < 4; ++k) t.push_back((uint8_t)(h >> (8 * k)));
-        t.insert(t.end(), lit.begin(), lit.end());
-        while (t.size() % 4) t.push_back(0);
+        (prefix ? px : ex).push_back({set, prefix, prefix ? g.substr(0, g.size() - 1) : g});
       }
     };
     namespace F = kpe::pssfix;
@@ -711,46 +728,98 @@ const std::vector<uint8_t>& psa_fixed_table() {
     add(PSF_SYSCTL0, F::sysctls(0)), add(PSF_SYSCTL1, F::sysctls(1)), add(PSF_SYSCTL2, F::sysctls(2));
     add(PSF_APPARMOR_KEY, F::kApparmorKey), add(PSF_SECCOMP_POD_KEY, F::kSeccompPodKey);
     add(PSF_APPARMOR_OK, F::kApparmorOk), add(PSF_SECCOMP_ANN_OK, F::kSeccompAnnOk);
+    std::stable_sort(ex.begin(), ex.end(), [](const Ent& a, const Ent& b) { return a.lit.size() < b.lit.size(); });
+    std::vector<uint32_t> t(KPE_PSF_ENT0, 0u);
+    t[0] = (uint32_t)ex.size(), t[1] = (uint32_t)px.size();
+    for (size_t e = 0; e < ex.size(); ++e) {
+      const size_t len = ex[e].lit.size();
+      if (len >= KPE_PSF_MAXLEN) throw std::logic_error("PSA fixed literal too long");
+      uint32_t& rg = t[2 + len];
+      if ((rg >> 16) == 0) rg = (uint32_t)e;  // first entry of this length
+      rg = (rg & 0xFFFFu) | (uint32_t)(e + 1) << 16;
+    }
+    std::vector<Ent> all = ex;
+    all.insert(all.end(), px.begin(), px.end());
+    size_t lit = KPE_PSF_ENT0 + 2 * all.size();
+    t.resize(lit, 0u);
+    for (size_t e = 0; e < all.size(); ++e) {
+      const std::string& L = all[e].lit;
+      t[KPE_PSF_ENT0 + 2 * e] = all[e].set | (all[e].prefix ? 1u << 7 : 0u) | (uint32_t)L.size() << 8;
+      t[KPE_PSF_ENT0 + 2 * e + 1] = (uint32_t)t.size();
+      for (size_t k = 0; k < L.size(); k += 4) {
+        uint32_t w = 0;
+        for (size_t b = 0; b < 4 && k + b < L.size(); ++b) w |= (uint32_t)(uint8_t)L[k + b] << (8 * b);
+        t.push_back(w);
+      }
+    }
+    if (t.size() > 1024) throw std::logic_error("PSA fixed table past its LDS area");
     return t;
   }();
   return tab;
 }
-// Launch the per-pod PSA summary of an uploaded corpus on stream s (kpe_launch_psum); summ:
-// also the 2-word summaries (kpe_corpus_psa_summary), or null.
-kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s, uint32_t* summ = nullptr) {
+// The corpus's PSA dictionary codes (kpe_psa_codes_kernel, one launch): built on the first binding
+// of a podSecurity program and again by a cold evaluation. Policy-independent, per distinct string.
+kpe_status run_codes(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s) {
   const int dom[4] = {D_CAP, D_SYSCTL, D_ANNK, D_ANNV};
-  PsumArgs a{};
-  a.n = C.n;
-  a.ntiles = (uint32_t)((C.n + 63) / 64);
-  a.ncapsets = (uint32_t)C.capset_add.size();
-  a.rec = D.rec.as<uint32_t>(), a.hdr = D.hdr.as<uint32_t>(), a.crec = D.crec.as<uint32_t>();
-  a.vol_src = D.vol_src.as<uint32_t>(), a.sys_id = D.sys_id.as<uint32_t>(), a.pann_kv = D.pann_kv.as<uint32_t>();
-  a.capsets = D.capsets.as<uint32_t>(), a.c_sann = D.c_sann.as<uint32_t>();
-  size_t code_bytes = 0;
-  for (int d = 0; d < 4; ++d) code_bytes += (C.dict[dom[d]].size() + 15) & ~(size_t)15;
-  if (!D.psum_ready) {
-    const auto& tab = psa_fixed_table();
-    HIPCHK(upload(D.psa_fixed, tab, s));
-    HIPCHK(D.psa_codes.ensure(code_bytes + 16));
-    HIPCHK(D.psa_csb.ensure(C.capset_add.size() + 16));
-    HIPCHK(D.psum.ensure((size_t)C.n * 12 + 16));
+  PsaCodeArgs a{};
+  PsaCodes& L = a.L;
+  auto al = [](size_t x) { return (uint32_t)((x + 3) & ~(size_t)3); };
+  L.ncapsets = (uint32_t)C.capset_add.size();
+  L.nsysd = (uint32_t)C.dict[D_SYSCTL].size(), L.nannk = (uint32_t)C.dict[D_ANNK].size();
+  L.nannv = (uint32_t)C.dict[D_ANNV].size();
+  L.o_sys = al(L.ncapsets), L.o_annk = L.o_sys + al(L.nsysd), L.o_annv = L.o_annk + al(L.nannk);
+  L.bytes = L.o_annv + al(L.nannv);
+  if (!D.codes_ready) {
+    HIPCHK(upload(D.psa_fixed, psa_fixed_table(), s));
+    HIPCHK(D.psa_codes.ensure((size_t)L.bytes + 16));
   }
-  a.fixed = D.psa_fixed.as<uint8_t>();
-  a.fixed_len = (uint32_t)psa_fixed_table().size();
-  size_t at = 0;
   for (int d = 0; d < 4; ++d) {
     a.dict_bytes[d] = D.dict_bytes[dom[d]].as<uint8_t>();
     a.dict_off[d] = D.dict_off[dom[d]].as<uint32_t>();
     a.dict_n[d] = C.dict[dom[d]].size();
-    a.codes[d] = D.psa_codes.as<uint8_t>() + at;
-    at += (C.dict[dom[d]].size() + 15) & ~(size_t)15;
   }
-  a.csb = D.psa_csb.as<uint8_t>();
+  a.capsets = D.capsets.as<uint32_t>();
+  a.fixed = D.psa_fixed.as<uint32_t>();
+  a.fixed_words = (uint32_t)psa_fixed_table().size();
+  a.codes = D.psa_codes.as<uint8_t>();
+  HIPCHK(kpe_launch_psa_codes(&a, s));
+  D.psa_L = L;
+  D.codes_ready = true;
+  return KPE_OK;
+}
+// The general scan's per-pod PSA records of an uploaded corpus on stream s (kpe_launch_psum), run
+// by every evaluation that reads them; summ: also the 2-word summaries (kpe_corpus_psa_summary),
+// or null.
+kpe_status run_psum(const kpe::Corpus& C, kpe::DeviceCorpus& D, hipStream_t s, uint32_t* summ = nullptr) {
+  if (!D.codes_ready)
+    if (kpe_status st = run_codes(C, D, s)) return st;
+  PsumArgs a{};
+  a.n = C.n;
+  a.ntiles = (uint32_t)((C.n + 63) / 64);
+  a.rec = D.rec.as<uint32_t>(), a.hdr = D.hdr.as<uint32_t>(), a.crec = D.crec.as<uint32_t>();
+  a.vol_src = D.vol_src.as<uint32_t>(), a.sys_id = D.sys_id.as<uint32_t>(), a.pann_kv = D.pann_kv.as<uint32_t>();
+  a.c_sann = D.c_sann.as<uint32_t>();
+  a.codes = D.psa_codes.as<uint8_t>();
+  a.L = D.psa_L;
+  HIPCHK(D.psum.ensure((size_t)C.n * 12 + 16));
   a.psum = D.psum.as<uint32_t>();
   a.summ = summ;
   HIPCHK(kpe_launch_psum(&a, s));
-  D.psum_ready = true;
   return KPE_OK;
+}
+// Algorithmic bytes of one LEAN evaluation of a shard (kpe_lean6_kernel): the pod records, the tile
+// headers, the list columns the program reads, the code bytes and kind table its blocks stage
+// (counted once), the verdict cells and, in the masks mode, the check masks.
+double lean_bytes(const kpe::Corpus& C, const kpe::DeviceCorpus& D, uint32_t need, uint32_t R, bool masks) {
+  const double n = (double)C.n;
+  double b = 16.0 * n + 16.0 * (double)((C.n + 63) / 64 + 1) + 8.0 * (double)C.c_sc.size();
+  if (need & NEED_SANN) b += 4.0 * (double)C.c_sc.size();
+  if (need & NEED_VOL) b += 4.0 * (double)C.vol_src.size();
+  if (need & NEED_SYS) b += 4.0 * (double)C.sys_id.size();
+  if (need & NEED_PANN) b += 8.0 * (double)(C.pann_kv.size() / 2);
+  b += (double)D.psa_L.bytes + 4.0 * (double)D.bind.nkinds;
+  b += n * R * (masks ? 5.0 : 1.0);
+  return b;
 }
 double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bool masks, bool psum) {
   double b = 0;
@@ -776,6 +845,12 @@ double scan_bytes(const kpe::Program& P, const kpe::Corpus& C, uint32_t need, bo
   if (need & NEED_NSL) b += 4.0 * n;  // r_nsl; the namespace table itself is cache-resident
   b += n * P.rules.size() * (masks ? 5.0 : 1.0);  // verdict cells (+ check masks)
   return b;
+}
+
+// Algorithmic bytes of kpe_psum_kernel: the pod records, tile headers and the list columns the
+// program reads, the code bytes, and the 12-byte records written.
+double psum_bytes(const kpe::Corpus& C, const kpe::DeviceCorpus& D, uint32_t need) {
+  return lean_bytes(C, D, need, 0, false) - 4.0 * (double)D.bind.nkinds + 12.0 * (double)C.n;
 }
 
 kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool want_masks) {
@@ -1085,16 +1160,17 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.blob_words = blob;
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
-  // LEAN scans run kpe_lean5_kernel over the per-pod PSA summaries (buffer loads with 32-bit
-  // offsets: the pod records under 4 GiB), else the template instantiation
+  // LEAN evaluations run kpe_lean6_kernel (buffer loads with 32-bit byte offsets: every column it
+  // reads under 4 GiB), else the template instantiation
   const uint64_t lim = (1ull << 32) - (1ull << 20);
-  B.lean_kind = !lean ? 0 : (uint64_t)C.n * 16 + 4096 > lim ? 2 : 7;
-  // every podSecurity program reads the corpus's scan records (LEAN5 alone, the general scan for
-  // each pod's failing versioned checks instead of its lists)
-  if (P.any_pss && !cc->d->psum_ready)
-    if (kpe_status st = run_psum(C, *cc->d, s)) return st;
-  // the general scan of a podSecurity program reads the scan records (PSUM instantiation, code | 4)
-  B.gen_code = (narrow ? 1 : 0) | (P.any_pss && cc->d->psum_ready ? 4 : 0);
+  const uint64_t col_max = std::max<uint64_t>((uint64_t)C.n * 16, (uint64_t)C.c_sc.size() * 8);
+  B.lean_kind = !lean ? 0 : col_max + 4096 > lim ? 2 : 7;
+  // the PSA dictionary codes of the corpus (policy-independent; per distinct string)
+  if (P.any_pss && !cc->d->codes_ready)
+    if (kpe_status st = run_codes(C, *cc->d, s)) return st;
+  // the general scan of a podSecurity program reads per-pod PSA records (PSUM instantiation, code
+  // | 4), which kpe_psum_kernel rebuilds right before it in every evaluation
+  B.gen_code = (narrow ? 1 : 0) | (P.any_pss ? 4 : 0);
   B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : B.gen_code, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   {  // ApplyOne policies: contiguous rule ranges in ComputeRules order
@@ -1133,6 +1209,9 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   return KPE_OK;
 }
 
+kpe_status lean6_launch(kpe_device* dev, const kpe::Program& P, const kpe::DeviceProgram& PD, kpe_corpus* const* cs,
+                        size_t m, bool masks, hipStream_t s, double* bytes);
+
 kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool masks, bool cold = false) {
   auto& P = *pp->p;
   auto& C = *cc->c;
@@ -1152,10 +1231,12 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     HIPCHK(hipEventRecord(ev.a, s));
   }
   const size_t R = P.rules.size();
-  static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
-  const bool fresh = !B.inv_ready || no_cache || cold;
-  if (cold && P.any_pss)  // a cold evaluation rebuilds the corpus's PSA summaries too
-    if (kpe_status st = run_psum(C, D, s)) return st;
+  const bool fresh = !B.inv_ready || dev->no_cache || cold;
+  if (cold && P.any_pss)  // a cold evaluation rebuilds the corpus's PSA dictionary codes too
+    if (kpe_status st = run_codes(C, D, s)) return st;
+  const bool lean_go = B.lean && (!masks || B.lean_kind == 7);  // LEAN6 writes check masks too
+  const bool six = lean_go && B.lean_kind == 7;
+  if (P.any_pss && !lean_go) HIPCHK(D.psum.ensure((size_t)C.n * 12 + 16));  // the PSUM scan's records
   if (B.nblocks && fresh) {  // dictionary pass for large-domain predicates
     PredArgs pa{};
     for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
@@ -1256,7 +1337,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
   sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
-  sa.psum = D.psum_ready ? D.psum.as<uint32_t>() : nullptr;
+  sa.psum = P.any_pss && !lean_go ? D.psum.as<uint32_t>() : nullptr;
   sa.selm = B.selm;
   if (B.selm) {
     sa.sel_km = B.sel_km.as<uint4>(), sa.sel_vm = B.sel_vm.as<uint4>(), sa.ns_q = B.sel_nsq.as<uint64_t>();
@@ -1291,10 +1372,17 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   B.inv_ready = true;
   ev.pre = fresh;
   if (dev->timing) HIPCHK(hipEventRecord(ev.b, s));
-  const bool lean_go = B.lean && (!masks || B.lean_kind == 7);  // LEAN5 writes check masks too
-  HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : B.gen_code,
-                         B.scan_blocks,
-                         B.dyn_bytes, s));
+  double lbytes = 0;
+  if (six) {  // the LEAN evaluation: every pod's record and lists, one kpe_lean6_kernel launch
+    kpe_corpus* one = cc;
+    if (kpe_status st = lean6_launch(dev, P, PD, &one, 1, masks, s, &lbytes)) return st;
+  } else {
+    // the general scan of a podSecurity program reads per-pod PSA records built right here
+    if (P.any_pss && !lean_go)
+      if (kpe_status st = run_psum(C, D, s)) return st;
+    HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : B.gen_code,
+                           B.scan_blocks, B.dyn_bytes, s));
+  }
   if (dev->timing) HIPCHK(hipEventRecord(ev.c, s));
   auto ensure_pargs = [&]() -> hipError_t {  // the binding's PatArgs (pattern kernel, foreach patterns)
     if (!B.pargs_valid) {
@@ -1448,8 +1536,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), PD.ltab_all ? 1 : 0, s));
-    static const bool patvm_err = getenv("KPE_PATVM_ERR") != nullptr;
-    if (patvm_err) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
+    if (dev->patvm_err) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;
       HIPCHK(hipMemcpyAsync(&e, B.perr.p, 4, hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
@@ -1465,9 +1552,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
-    const double mb = masks ? 4.0 * (double)C.n * (double)R : 0.0;
-    ev.bytes = lean_go && B.lean_kind == 7 ? 12.0 * (double)C.n + (double)C.n * (double)R + mb  // scan records, rows
-                                           : scan_bytes(P, C, B.need, masks, D.psum_ready);
+    const bool ps = P.any_pss && !lean_go;  // the PSUM scan and its per-pod records
+    ev.bytes = six ? lbytes : scan_bytes(P, C, B.need, masks, ps) + (ps ? psum_bytes(C, D, B.need) : 0.0);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     ev.kind = lean_go ? B.lean_kind : 1;
     dev->pending.push_back(ev);
@@ -1475,16 +1561,67 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   return KPE_OK;
 }
 
-// A shard can ride in a multi-shard LEAN5 launch when its evaluation is that one kernel: a bound
-// LEAN5 binding (prologue image and PSA summary built) of a program with no later kernels, and
-// no rows past an encoding limit.
-bool lean_batchable(const kpe_program* pp, const kpe_corpus* cc) {
-  static const bool no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
+// One kpe_lean6_kernel launch over the m bound shards cs of program P on stream s (bytes: their
+// algorithmic bytes). Tiles per wave: the most (up to 4) that still leaves dev->lean_min_waves
+// waves; the corpora's code bytes are staged in LDS per block when they fit (LC).
+kpe_status lean6_launch(kpe_device* dev, const kpe::Program& P, const kpe::DeviceProgram& PD, kpe_corpus* const* cs,
+                        size_t m, bool masks, hipStream_t s, double* bytes) {
+  const uint32_t R = (uint32_t)P.rules.size();
+  LeanBatchArgs a;
+  memset(&a, 0, sizeof(a));
+  a.nshards = (uint32_t)m, a.nrules = R, a.ncls = PD.ncls, a.cv_union = P.cv_union;
+  a.pss_rules = PD.pss_rules, a.err_rules = PD.err_rules, a.pat_rules = PD.pat_rules;
+  a.narrow_cls = PD.narrow_cls.as<uint32_t>();
+  uint64_t tiles = 0;
+  for (size_t k = 0; k < m; ++k) tiles += (uint64_t)(cs[k]->c->n + 63) / 64;
+  uint32_t tpw = 4;
+  while (tpw > 1 && tiles / tpw < dev->lean_min_waves) tpw >>= 1;
+  if (dev->lean_tpw) tpw = dev->lean_tpw;
+  a.tpw = tpw;
+  uint32_t acc = 0, kt_max = 0, code_max = 0;
+  *bytes = 0;
+  for (size_t k = 0; k < m; ++k) {
+    auto& C = *cs[k]->c;
+    auto& D = *cs[k]->d;
+    auto& B = D.bind;
+    LeanShard& sh = a.sh[k];
+    sh.rec = D.rec.as<uint32_t>(), sh.hdr = D.hdr.as<uint32_t>(), sh.crec = D.crec.as<uint32_t>();
+    sh.vol = D.vol_src.as<uint32_t>(), sh.sys = D.sys_id.as<uint32_t>(), sh.pann = D.pann_kv.as<uint32_t>();
+    sh.sann = D.c_sann.as<uint32_t>();
+    sh.codes = D.psa_codes.as<uint8_t>();
+    sh.kt = B.pimg.as<uint32_t>() + B.kt_lds;
+    sh.verdicts = B.verdicts.as<uint8_t>();
+    sh.masks = masks ? B.masks.as<uint32_t>() : nullptr;
+    sh.n = (uint32_t)C.n, sh.nkinds = B.nkinds;
+    sh.nctr = (uint32_t)C.c_sc.size(), sh.nvol = (uint32_t)C.vol_src.size(), sh.nsys = (uint32_t)C.sys_id.size();
+    sh.npann = (uint32_t)(C.pann_kv.size() / 2);
+    sh.L = D.psa_L;
+    a.blk0[k] = acc;
+    acc += (uint32_t)((C.n + 256 * tpw - 1) / (256 * tpw));  // 4 waves x tpw tiles of 64 pods per block
+    kt_max = std::max(kt_max, B.nkinds);
+    code_max = std::max(code_max, D.psa_L.bytes);
+    a.need |= B.need;
+    *bytes += lean_bytes(C, D, B.need, R, masks);
+  }
+  a.blk0[m] = acc;
+  const bool lc = code_max <= kLeanCodeLds;
+  a.kt_words = (kt_max + 3u) & ~3u;
+  a.code_words = lc ? ((code_max + 15u) / 16u) * 4u : 0u;
+  a.wave_words = ((KPE_L6_STAGE_BYTES + 64u * R + 15u) / 16u) * 4u;
+  const size_t dyn = 4 * ((size_t)a.kt_words + a.code_words + 4 * (size_t)a.wave_words);
+  HIPCHK(kpe_launch_lean6(&a, dyn, lc ? 1 : 0, s));
+  return KPE_OK;
+}
+
+// A shard can ride in a multi-shard LEAN launch when its evaluation is that one kernel: a bound
+// LEAN binding (prologue image and PSA dictionary codes built) of a program with no later
+// kernels, and no rows past an encoding limit.
+bool lean_batchable(const kpe_device* dev, const kpe_program* pp, const kpe_corpus* cc) {
   const auto& P = *pp->p;
   const auto& C = *cc->c;
   const auto& D = *cc->d;
   const auto& B = D.bind;
-  return !no_cache && B.prog == &P && B.inv_ready && B.lean && B.lean_kind == 7 && D.psum_ready && C.n > 0 &&
+  return !dev->no_cache && B.prog == &P && B.inv_ready && B.lean && B.lean_kind == 7 && D.codes_ready && C.n > 0 &&
          B.nkinds <= kLeanBatchKinds && P.cond.rules.empty() && P.pssx.rules.empty() && P.pat.rules.empty() &&
          !B.napply_segs && C.limit_rows.empty();
 }
@@ -1500,51 +1637,24 @@ kpe_status launch_lean_run(kpe_device* dev, const kpe_program* pp, std::vector<k
   }
   auto& P = *pp->p;
   auto& PD = *P.devs[dev->ordinal];
-  const uint32_t R = (uint32_t)P.rules.size();
   hipStream_t s = dev->stream;
   const size_t m = run.size(), nl = (m + KPE_LEAN_BATCH - 1) / KPE_LEAN_BATCH;
   for (size_t l = 0, i = 0; l < nl; ++l) {
     const size_t cnt = (m - i) / (nl - l);
-    LeanBatchArgs a;
-    memset(&a, 0, sizeof(a));
-    a.nshards = (uint32_t)cnt, a.nrules = R, a.ncls = PD.ncls, a.cv_union = P.cv_union;
-    a.pss_rules = PD.pss_rules, a.err_rules = PD.err_rules, a.pat_rules = PD.pat_rules;
-    a.narrow_cls = PD.narrow_cls.as<uint32_t>();
-    // tiles per wave: the most (up to 8) that still leaves >= 16 waves per SIMD of the chip
-    uint64_t tiles = 0;
-    for (size_t k = 0; k < cnt; ++k) tiles += (uint64_t)(run[i + k]->c->n + 63) / 64;
-    uint32_t tpw = 8;
-    while (tpw > 1 && tiles / tpw < kLeanBatchMinWaves) tpw >>= 1;
-    a.tpw = tpw;
-    uint32_t acc = 0, ktw = 0;
-    double bytes = 0;
-    for (size_t k = 0; k < cnt; ++k, ++i) {
-      auto& C = *run[i]->c;
-      auto& D = *run[i]->d;
-      auto& B = D.bind;
+    for (size_t k = 0; k < cnt; ++k) {
+      auto& B = run[i + k]->d->bind;
       if (B.last && B.last != s) HIPCHK(hipStreamSynchronize(B.last));  // keep this corpus's launches ordered
       B.last = s;
-      LeanShard& sh = a.sh[k];
-      sh.psum = D.psum.as<uint32_t>();
-      sh.kt = B.pimg.as<uint32_t>() + B.kt_lds;
-      sh.verdicts = B.verdicts.as<uint8_t>();
-      sh.masks = masks ? B.masks.as<uint32_t>() : nullptr;
-      sh.n = (uint32_t)C.n, sh.nkinds = B.nkinds;
-      a.blk0[k] = acc;
-      acc += (uint32_t)((C.n + 256 * tpw - 1) / (256 * tpw));  // 4 waves x tpw tiles of 64 pods per block
-      ktw = std::max(ktw, B.nkinds);
-      bytes += (12.0 + R) * (double)C.n + (masks ? 4.0 * R * (double)C.n : 0.0);
     }
-    a.blk0[cnt] = acc;
-    a.kt_words = (ktw + 3u) & ~3u;
-    const size_t dyn = (size_t)a.kt_words * 4 + 4 * 64 * (size_t)R;
     kpe_device::EvPair ev{};
     if (dev->timing) {
       ev.a = dev->get_ev(), ev.b = dev->get_ev(), ev.c = dev->get_ev(), ev.d = dev->get_ev();
       HIPCHK(hipEventRecord(ev.a, s));
       HIPCHK(hipEventRecord(ev.b, s));
     }
-    HIPCHK(kpe_launch_lean_batch(&a, dyn, s));
+    double bytes = 0;
+    if (kpe_status st = lean6_launch(dev, P, PD, run.data() + i, cnt, masks, s, &bytes)) return st;
+    i += cnt;
     if (dev->timing) {
       HIPCHK(hipEventRecord(ev.c, s));
       HIPCHK(hipEventRecord(ev.d, s));
@@ -1599,7 +1709,7 @@ kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, co
   for (int i = 0; i < n; ++i) {
     if (kpe_status st = prepare(dev, prog, cs[i], masks)) return st;
     kpe_corpus* c = const_cast<kpe_corpus*>(cs[i]);
-    if (!cold && lean_batchable(prog, c)) {
+    if (!cold && lean_batchable(dev, prog, c)) {
       run.push_back(c);
       continue;
     }

@@ -1,16 +1,14 @@
-// LEAN scan of kind-matched PSS programs (C2: restricted:latest and its autogen columns), and the
-// per-pod PSA summary it reads. Same verdicts as kpe_scan_kernel<PSS, NARROW> (the reference path:
-// pkg/engine/engine.go:87-101 validate -> validatePssHandler.Process, validate_pss.go:64-110,
-// pkg/pss/evaluate.go:24-70).
+// LEAN evaluation of kind-matched PSS programs (C2: restricted:latest and its autogen columns), the
+// PSA dictionary codes it reads, and the general scan's per-pod PSA records. Same verdicts as
+// kpe_scan_kernel<PSS, NARROW> (the reference path: pkg/engine/engine.go:87-101 validate ->
+// validatePssHandler.Process, validate_pss.go:64-110, pkg/pss/evaluate.go:24-70).
 //
 // Every PSA check of the v0.29 library is "some container / list item of the pod is in state s"
-// for fixed, policy-independent sets s (pss_fixed.hpp), so a pod reduces to one summary: the OR
-// of its container state bitmaps and of its list items' codes under those sets. The summary is
-// built on the device once per corpus (kpe_psa_dict_kernel -> kpe_psa_capset_kernel ->
-// kpe_psum_kernel, at the first binding of a LEAN program and again on a cold evaluation), as a
-// 12-byte scan record per pod: the pod word and kind id of the pod record beside the pod's
-// failing versioned checks (cv_fails of the summary: also policy-independent). An evaluation then
-// reads 12 bytes per pod and masks the checks with the program's version classes.
+// for fixed, policy-independent sets s (pss_fixed.hpp). A pod's checks are therefore decided from
+// the OR of its containers' state bitmaps and of its list items' codes under those sets. The codes
+// belong to the corpus's dictionaries (one byte per distinct capability set, sysctl name and
+// annotation key / value: kpe_psa_codes_kernel, once per corpus, like the interned ids
+// themselves); everything per pod is read and decided by every evaluation (kpe_lean6_kernel).
 // Included by kernels.hip (uses its anonymous-namespace helpers).
 
 typedef __amdgpu_buffer_rsrc_t Rsrc;
@@ -22,108 +20,145 @@ __device__ __forceinline__ uint2 bload2(Rsrc r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
   return make_uint2(v[0], v[1]);
 }
-__device__ __forceinline__ uint3 bload3(Rsrc r, uint32_t off) {
-  auto v = __builtin_amdgcn_raw_buffer_load_b96(r, off, 0, 0);
-  return make_uint3(v[0], v[1], v[2]);
-}
 __device__ __forceinline__ uint4 bload4(Rsrc r, uint32_t off) {
   auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-// The arguments are passed by value (read from the kernarg segment: one hop less than a device
-// copy before the first load).
-__device__ __forceinline__ CArgs* kargs() {
+// The kernel arguments, read from the kernarg segment through a laundered pointer (one hop less
+// than a device copy before the first load).
+__device__ __forceinline__ const __attribute__((address_space(4))) void* kargs() {
   uint64_t v = (uint64_t)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(v));
-  return (CArgs*)v;
+  return (const __attribute__((address_space(4))) void*)v;
 }
 
-#ifndef KPE_LEAN2_WAVES
-#define KPE_LEAN2_WAVES 6
+#ifndef KPE_LEAN6_WAVES
+#define KPE_LEAN6_WAVES 6
 #endif
 constexpr uint32_t kLB = 256;
 // XCD-aware block order: the dispatcher deals workgroups round-robin to the 8 XCDs (block b on
 // XCD b % 8), so block b takes the (b / 8)-th block of XCD b % 8's contiguous share of the tiles:
-// neighbouring tiles (whose record lines share L2 sectors) stay on one XCD's L2.
+// neighbouring tiles (whose list items share cache lines) stay on one XCD's L2.
 __device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
   const uint32_t q = nb >> 3, r = nb & 7u, x = b & 7u;
   return x * q + min(x, r) + (b >> 3);
 }
 
-// ---- the per-pod PSA summary ---------------------------------------------------------------
-// Fixed-set table (PsumArgs::fixed, built on the host from pss_fixed.hpp): entries of
-// [set | prefix << 7 | len << 8] then the literal, padded to 4 bytes. A prefix entry is a literal
-// followed by one trailing '*' (go-wildcard: a byte-prefix match, pss_fixed.hpp fixed_match).
-__device__ __forceinline__ uint32_t psa_sets(const uint8_t* tab, uint32_t tab_len, const uint8_t* s, uint32_t n) {
-  uint32_t hit = 0;
-  for (uint32_t o = 0; o + 4u <= tab_len;) {
-    const uint32_t h = *reinterpret_cast<const uint32_t*>(tab + o);
-    const uint32_t set = h & 0x7Fu, prefix = (h >> 7) & 1u, len = h >> 8;
-    const uint8_t* lit = tab + o + 4u;
-    if (prefix ? n >= len : n == len) {
-      bool eq = true;
-      for (uint32_t i = 0; i < len && eq; ++i) eq = s[i] == lit[i];
-      if (eq) hit |= 1u << set;
+// ---- PSA dictionary codes (once per corpus) -----------------------------------------------------
+// Four bytes of s from p on (any alignment): two aligned dword loads and a shift. Dictionary
+// buffers carry 128 bytes of slack past their end (kpe_api.cpp upload).
+__device__ __forceinline__ uint32_t ld4u(const uint8_t* p) {
+  const uintptr_t a = (uintptr_t)p;
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(a & ~(uintptr_t)3);
+  const uint64_t v = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+  return (uint32_t)(v >> ((a & 3u) * 8u));
+}
+// Set-hit word of string s (n bytes): bit k = s matches a glob of fixed set k. Exact entries are
+// bucketed by length, so a string is compared only with the literals of its own length, then with
+// the few prefix entries; literals are compared four bytes per step from the LDS-staged table
+// (layout in kernels_abi.h).
+__device__ __forceinline__ uint32_t psa_sets(const uint32_t* fx, const uint8_t* s, uint32_t n) {
+  auto eq = [&](uint32_t e, uint32_t len) -> bool {
+    const uint32_t lit = fx[KPE_PSF_ENT0 + 2u * e + 1u];
+    for (uint32_t i = 0; i < len; i += 4u) {
+      const uint32_t m = len - i >= 4u ? ~0u : (1u << (8u * (len - i))) - 1u;
+      if ((ld4u(s + i) ^ fx[lit + (i >> 2)]) & m) return false;
     }
-    o += 4u + ((len + 3u) & ~3u);
+    return true;
+  };
+  uint32_t hit = 0;
+  if (n < KPE_PSF_MAXLEN) {
+    const uint32_t rg = fx[2u + n];
+    for (uint32_t e = rg & 0xFFFFu; e < (rg >> 16); ++e)
+      if (eq(e, n)) hit |= 1u << (fx[KPE_PSF_ENT0 + 2u * e] & 0x7Fu);
+  }
+  const uint32_t E = fx[0], X = fx[1];
+  for (uint32_t e = E; e < E + X; ++e) {
+    const uint32_t h = fx[KPE_PSF_ENT0 + 2u * e], len = h >> 8;
+    if (n >= len && eq(e, len)) hit |= 1u << (h & 0x7Fu);
   }
   return hit;
 }
-
-// Code byte of every string of the four dictionaries the summary reads (grid y = PSD_*):
-//   capabilities: bit 0 baseline-allowed, bit 1 NET_BIND_SERVICE, bit 2 "ALL";
-//   sysctls: bit v = outside version v's allowed set (check_sysctls.go v1.0 / v1.27 / v1.29);
-//   annotation keys: bit 0 AppArmor container key, bit 1 pod seccomp key;
-//   annotation values: bit 0 allowed AppArmor profile, bit 1 allowed seccomp profile.
-__global__ void __launch_bounds__(256) kpe_psa_dict_kernel(PsumArgs a) {
-  const uint32_t d = blockIdx.y;
-  const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-  if (i >= a.dict_n[d]) return;
-  const uint32_t* off = a.dict_off[d];
-  const uint32_t o0 = off[i], o1 = off[i + 1];
-  const uint32_t h = psa_sets(a.fixed, a.fixed_len, a.dict_bytes[d] + o0, o1 - o0);
-  uint32_t c = 0;
-  if (d == PSD_CAP) {
-    c = ((h >> PSF_CAPS_OK) & 1u) | (((h >> PSF_CAP_NBS) & 1u) << 1) | (((h >> PSF_CAP_ALL) & 1u) << 2);
-  } else if (d == PSD_SYSCTL) {
-    c = (((h >> PSF_SYSCTL0) & 1u) ^ 1u) | ((((h >> PSF_SYSCTL1) & 1u) ^ 1u) << 1) | ((((h >> PSF_SYSCTL2) & 1u) ^ 1u) << 2);
-  } else if (d == PSD_ANNK) {
-    c = ((h >> PSF_APPARMOR_KEY) & 1u) | (((h >> PSF_SECCOMP_POD_KEY) & 1u) << 1);
-  } else {
-    c = ((h >> PSF_APPARMOR_OK) & 1u) | (((h >> PSF_SECCOMP_ANN_OK) & 1u) << 1);
-  }
-  a.codes[d][i] = (uint8_t)c;
-}
-
-// Capability-set code byte (CS_* of kernels.hip) of every (add, drop) pair of the corpus's
-// capability-set dictionary, from the capability codes (capability ids < 64: a 65th name is a
-// per-resource limit).
-__global__ void __launch_bounds__(256) kpe_psa_capset_kernel(PsumArgs a) {
+#define KPE_PSF_LDS_WORDS 1024u
+// One launch: grid y = 0 capability sets (each block first codes the capability names, ids < 64),
+// 1 sysctls, 2 annotation keys, 3 annotation values (PSD_*); one thread per entry.
+__global__ void __launch_bounds__(256) kpe_psa_codes_kernel(PsaCodeArgs a) {
+  __shared__ uint32_t fx[KPE_PSF_LDS_WORDS];
   __shared__ uint32_t s_m[6];
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, y = blockIdx.y;
+  for (uint32_t i = t; i < a.fixed_words; i += 256u) fx[i] = a.fixed[i];
   if (t < 6) s_m[t] = 0;
   __syncthreads();
-  const uint32_t ncap = min(a.dict_n[PSD_CAP], 64u);
-  if (t < ncap) {
-    const uint32_t c = a.codes[PSD_CAP][t];
-    for (uint32_t k = 0; k < 3; ++k)
-      if ((c >> k) & 1u) atomicOr(&s_m[2 * k + (t >> 5)], 1u << (t & 31u));
+  const uint32_t i = blockIdx.x * 256u + t;
+  if (y == 0) {
+    const uint32_t ncap = min(a.dict_n[PSD_CAP], 64u);
+    if (t < ncap) {
+      const uint32_t o0 = a.dict_off[PSD_CAP][t], o1 = a.dict_off[PSD_CAP][t + 1];
+      const uint32_t h = psa_sets(fx, a.dict_bytes[PSD_CAP] + o0, o1 - o0);
+      const uint32_t c = ((h >> PSF_CAPS_OK) & 1u) | (((h >> PSF_CAP_NBS) & 1u) << 1) | (((h >> PSF_CAP_ALL) & 1u) << 2);
+      for (uint32_t k = 0; k < 3; ++k)
+        if ((c >> k) & 1u) atomicOr(&s_m[2 * k + (t >> 5)], 1u << (t & 31u));
+    }
+    __syncthreads();
+    if (i >= a.L.ncapsets) return;
+    const uint64_t ok = s_m[0] | (uint64_t)s_m[1] << 32, nbs = s_m[2] | (uint64_t)s_m[3] << 32,
+                   all = s_m[4] | (uint64_t)s_m[5] << 32;
+    const uint4 cs = reinterpret_cast<const uint4*>(a.capsets)[i];
+    const uint64_t ad = cs.x | (uint64_t)cs.y << 32, dr = cs.z | (uint64_t)cs.w << 32;
+    a.codes[i] = (uint8_t)(((ad & ~ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+    return;
   }
-  __syncthreads();
-  const uint64_t ok = s_m[0] | (uint64_t)s_m[1] << 32, nbs = s_m[2] | (uint64_t)s_m[3] << 32,
-                 all = s_m[4] | (uint64_t)s_m[5] << 32;
-  const uint32_t j = blockIdx.x * 256u + t;
-  if (j >= a.ncapsets) return;
-  const uint4 cs = reinterpret_cast<const uint4*>(a.capsets)[j];
-  const uint64_t ad = cs.x | (uint64_t)cs.y << 32, dr = cs.z | (uint64_t)cs.w << 32;
-  a.csb[j] = (uint8_t)(((ad & ~ok) ? CS_BASE : 0u) | ((dr & all) ? 0u : CS_DROP) | ((ad & ~nbs) ? CS_ADD : 0u));
+  if (i >= a.dict_n[y]) return;
+  const uint32_t o0 = a.dict_off[y][i], o1 = a.dict_off[y][i + 1];
+  const uint32_t h = psa_sets(fx, a.dict_bytes[y] + o0, o1 - o0);
+  uint32_t c, at;
+  if (y == PSD_SYSCTL) {
+    c = (((h >> PSF_SYSCTL0) & 1u) ^ 1u) | ((((h >> PSF_SYSCTL1) & 1u) ^ 1u) << 1) | ((((h >> PSF_SYSCTL2) & 1u) ^ 1u) << 2);
+    at = a.L.o_sys;
+  } else if (y == PSD_ANNK) {
+    c = ((h >> PSF_APPARMOR_KEY) & 1u) | (((h >> PSF_SECCOMP_POD_KEY) & 1u) << 1);
+    at = a.L.o_annk;
+  } else {
+    c = ((h >> PSF_APPARMOR_OK) & 1u) | (((h >> PSF_SECCOMP_ANN_OK) & 1u) << 1);
+    at = a.L.o_annv;
+  }
+  a.codes[at + i] = (uint8_t)c;
 }
 
+// Code of one list item from the corpus's code bytes (`cb`: LDS or global), shared by the LEAN
+// evaluation and the general scan's per-pod records.
+struct PsaCoder {
+  const PsaCodes& L;
+  template <class CB>
+  __device__ __forceinline__ uint32_t cap(const CB& cb, uint32_t capset) const { return cb(capset) & 7u; }
+  // a container's seccomp annotation value (check_seccompProfile v1.0): 1 when set and not allowed
+  template <class CB>
+  __device__ __forceinline__ uint32_t sann(const CB& cb, uint32_t cs) const {
+    if (cs == KPE_NO_STR) return 0u;
+    return (cs < L.nannv ? (cb(L.o_annv + cs) >> 1) & 1u : 0u) ^ 1u;
+  }
+  template <class CB>
+  __device__ __forceinline__ uint32_t sys(const CB& cb, uint32_t id) const {
+    return id < L.nsysd ? cb(L.o_sys + id) : 7u;
+  }
+  template <class CB>
+  __device__ __forceinline__ uint32_t ann(const CB& cb, uint2 q) const {
+    const uint32_t ka = q.x < L.nannk ? cb(L.o_annk + q.x) : 0u;
+    const uint32_t va = q.y < L.nannv ? cb(L.o_annv + q.y) : 0u;
+    return ((ka & 1u) && !(va & 1u) ? 1u : 0u) | ((ka & 2u) && !(va & 2u) ? 2u : 0u);
+  }
+};
+__device__ __forceinline__ uint32_t vol_code(uint32_t v) {
+  return ((v >> VS_HOSTPATH) & 1u) | ((v & kAllowedVolumes) ? 0u : 2u);
+}
+
+// ---- kpe_psum_kernel: the general scan's per-pod PSA records ----------------------------------
 // One wave per 64-pod tile: list offsets from the tile header plus a wave scan of the pod
-// records' packed counts, then each lane ORs its own pod's items (schema.h PS_* layout). Out: the
-// pod's LEAN scan record {pod word, failing versioned checks, kind id << 16} and, when asked
-// (PsumArgs::summ), the summary itself {OR of container states, list codes} (schema.h PS_*).
+// records' packed counts, then each lane ORs its own pod's items. Out: {pod word, failing
+// versioned checks, kind id << 16} per pod and, when asked (PsumArgs::summ), the summary {OR of
+// container states, list codes} (schema.h PS_*). Launched by every evaluation of a podSecurity
+// program that takes the general scan, right before it.
 __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t tile = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -139,32 +174,21 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   const uint32_t oc = hw(h, 0) + (e01 & 0xFFFFu), ov = hw(h, 1) + (e01 >> 16), os = hw(h, 2) + (e23 & 0xFFFFu),
                  oa = hw(h, 3) + (e23 >> 16);
   if (!live) return;
+  const PsaCoder K{a.L};
+  const uint8_t* codes = a.codes;
+  auto cb = [&](uint32_t i) -> uint32_t { return codes[i]; };
   uint32_t xo = 0, co = 0, vc = 0, sc = 0, ac = 0, sa = 0;
   const uint2* crec = reinterpret_cast<const uint2*>(a.crec);
-  const uint32_t nsv = a.dict_n[PSD_ANNV];
   for (uint32_t k = 0; k < nc; ++k) {
     const uint2 e = crec[oc + k];
     xo |= e.x;
-    if (e.x) co |= a.csb[CY_CAPSET(e.y)];  // a real container record always has state bits
-    const uint32_t cs = a.c_sann[oc + k];  // the container's seccomp annotation value (v1.0 check)
-    if (cs != KPE_NO_STR) sa |= (cs < nsv ? ((uint32_t)a.codes[PSD_ANNV][cs] >> 1) & 1u : 0u) ^ 1u;
+    if (e.x) co |= K.cap(cb, CY_CAPSET(e.y));  // a real container record always has state bits
+    sa |= K.sann(cb, a.c_sann[oc + k]);
   }
-  for (uint32_t k = 0; k < nv; ++k) {
-    const uint32_t v = a.vol_src[ov + k];
-    vc |= ((v >> VS_HOSTPATH) & 1u) | ((v & kAllowedVolumes) ? 0u : 2u);
-  }
-  const uint32_t nsys = a.dict_n[PSD_SYSCTL], nak = a.dict_n[PSD_ANNK], nav = a.dict_n[PSD_ANNV];
-  for (uint32_t k = 0; k < ns; ++k) {
-    const uint32_t id = a.sys_id[os + k];
-    sc |= id < nsys ? (uint32_t)a.codes[PSD_SYSCTL][id] : 7u;
-  }
+  for (uint32_t k = 0; k < nv; ++k) vc |= vol_code(a.vol_src[ov + k]);
+  for (uint32_t k = 0; k < ns; ++k) sc |= K.sys(cb, a.sys_id[os + k]);
   const uint2* kv = reinterpret_cast<const uint2*>(a.pann_kv);
-  for (uint32_t k = 0; k < na; ++k) {
-    const uint2 q = kv[oa + k];
-    const uint32_t ka = q.x < nak ? (uint32_t)a.codes[PSD_ANNK][q.x] : 0u;
-    const uint32_t va = q.y < nav ? (uint32_t)a.codes[PSD_ANNV][q.y] : 0u;
-    ac |= ((ka & 1u) && !(va & 1u) ? 1u : 0u) | ((ka & 2u) && !(va & 2u) ? 2u : 0u);
-  }
+  for (uint32_t k = 0; k < na; ++k) ac |= K.ann(cb, kv[oa + k]);
   const uint32_t y = co | (vc << 3) | (sc << 5) | (ac << 8) | (sa << 10);
   uint32_t* o = a.psum + 3u * r;
   o[0] = rc.x;
@@ -174,85 +198,28 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   if (a.summ) a.summ[2u * r] = xo, a.summ[2u * r + 1u] = y;
 }
 
-// ---- kpe_lean5_kernel: the 12-byte scan records only ------------------------------------
-// A wave loads one 12-byte record per pod (768 contiguous bytes) in one memory step and
-// evaluates with no staging, scans or list loops: the failing checks of the program's classes, the kind
-// table, the rows stored as dwords through LDS and, when asked, the check masks.
-__global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_kernel(ScanArgs) {
-  extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-  CArgs& a0 = *kargs();
-  const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
-  const uint32_t ntiles = a0.ntiles, n = (uint32_t)a0.n;
-  const uint32_t tile = xcd_block(blockIdx.x, gridDim.x) * (kLB / 64u) + wv;
-  const Rsrc PS = make_rsrc(a0.psum, n * 12u);
-  const uint32_t r = tile * 64u + lane;
-  const uint3 sr = bload3(PS, r * 12u);
-  // the kind table and the class table of the prologue image (a few hundred words)
-  const uint32_t img_n4 = a0.pimg_words >> 2;
-  const uint4* img = reinterpret_cast<const uint4*>(a0.pimg);
-  const uint4 img0 = img[min(t, img_n4 - 1u)];
-  uint32_t cls_cv = 0, cls_rm = 0;
-  if (lane < a0.ncls) {
-    const uint2 c = reinterpret_cast<const uint2*>(a0.narrow_cls)[lane];
-    cls_cv = c.x, cls_rm = c.y;
-  }
-  {
-    uint4* d4 = reinterpret_cast<uint4*>(dyn);
-    if (t < img_n4) d4[t] = img0;
-#pragma unroll 1
-    for (uint32_t i = t + kLB; i < img_n4; i += kLB) d4[i] = img[i];
-  }
-  __syncthreads();
-  if (tile >= ntiles) return;
-  const uint32_t R = a0.nrules, cv_union = a0.cv_union, pss_rules = a0.pss_rules, ncls = a0.ncls;
-  const uint32_t ep_rules = a0.err_rules | a0.pat_rules, pat_rules = a0.pat_rules;
-  uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a0.wave_lds + wv * a0.wave_words + KPE_STAGE_WORDS);
-  const bool live = r < n;
-  const uint32_t pw = sr.x, y = sr.z;
-  const uint32_t fails = sr.y & cv_union;
-  const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
-  const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
-  const uint32_t matched = dyn[a0.kt_lds + (y >> 16)];
-  uint32_t failr;
-  if (ncls == 1u) {
-    failr = (fails & hw(cls_cv, 0)) ? hw(cls_rm, 0) : 0u;
-  } else {
-    failr = 0;
-#pragma unroll 1
-    for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
-  }
-  const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
-  const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
-  const uint32_t P = matched & pss_rules & ~failr & ~E;
-#pragma unroll 1
-  for (uint32_t ri = 0; ri < R; ++ri)
-    sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
-  if (a0.masks && live) {
-    uint32_t* mrow = a0.masks + (size_t)r * R;
-    const uint32_t fm = F & pss_rules;
-#pragma unroll 1
-    for (uint32_t ri = 0; ri < R; ++ri) {
-      uint32_t cv = 0;
-      for (uint32_t c = 0; c < ncls; ++c) cv = ((hw(cls_rm, c) >> ri) & 1u) ? hw(cls_cv, c) : cv;
-      mrow[ri] = ((fm >> ri) & 1u) ? (fails & cv) : 0u;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  store_rows(a0.verdicts, sv, tile, R, 0, R, min(64u, n - tile * 64u), lane);
-}
-
+// ---- kpe_lean6_kernel: the LEAN evaluation, one or many shards per launch ----------------------
+// A wave evaluates T consecutive 64-pod tiles of its block's shard (blocks find their shard by a
+// scalar binary search over LeanBatchArgs::blk0). Two dependent memory steps per wave:
+//   1. the T + 1 tile headers (one dword per lane) and the T tiles' pod records (16 B per lane);
+//   2. every tile's list items, cooperatively and coalesced: lane i loads container i and 64 + i
+//      of the tile (crec, and c_sann when a v1.0 seccomp check runs), volumes i and 64 + i,
+//      sysctl i and annotation i, from the tile's first item (header) on.
+// Then per tile: lane i codes its staged items (capability-set / sysctl / annotation codes from
+// the corpus's code bytes, LDS-staged per block when they fit: LC) into the wave's LDS stage, each
+// pod ORs its own items from there (its offsets: one wave scan of the packed list counts), pods
+// with more items than the clamped reads cover (or items past the stage) loop over the rest, the
+// PSA checks are decided (cv_fails), masked by the program's version classes and the kind table,
+// and the tile's rows are stored as dwords through LDS (with the failing versioned checks per
+// cell in the masks mode).
 typedef const __attribute__((address_space(4))) LeanBatchArgs CBArgs;
-// ---- kpe_lean5_batch_kernel: many shards in one launch ---------------------------------------
-// The same per-pod evaluation as kpe_lean5_kernel over up to KPE_LEAN_BATCH bound shards of one
-// program (each with its own corpus dictionaries, hence its own kind table): the shards' blocks
-// are one grid, so a batch of K steps costs one launch and one ramp instead of K. Every block
-// finds its shard by a scalar binary search over LeanBatchArgs::blk0 (kernel arguments) and
-// stages only that shard's kind table in LDS. A wave takes T tiles of its block's 4T (tiles
-// b*4T + 4i + wave): the T record loads are issued together, then the tiles are evaluated and
-// stored one by one. One tile per wave leaves a streaming launch bound by the wave launch rate
-// (20 shards, 312k waves: 2.9 TB/s).
-template <int T>
-__global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_batch_kernel(LeanBatchArgs) {
+typedef const __attribute__((address_space(4))) LeanShard CShard;
+struct L6Items {
+  uint2 c0, c1, q0;
+  uint32_t v0, v1, s0, a0, a1;
+};
+template <int T, bool LC>
+__global__ void __launch_bounds__(kLB, KPE_LEAN6_WAVES) kpe_lean6_kernel(LeanBatchArgs) {
   extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
   CBArgs& a = *(CBArgs*)kargs();
   const uint32_t t = threadIdx.x, lane = t & 63u, wv = t >> 6;
@@ -263,46 +230,182 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN2_WAVES) kpe_lean5_batch_kernel(L
     if (a.blk0[mid] <= gb) lo = mid;
     else hi = mid;
   }
-  const __attribute__((address_space(4))) LeanShard& S = a.sh[lo];
-  const uint32_t n = S.n, tile0 = (gb - a.blk0[lo]) * (4u * T) + wv;
-  const Rsrc PS = make_rsrc(S.psum, n * 12u);
-  uint3 sr[T];
+  CShard& S = a.sh[lo];
+  const uint32_t n = S.n, ntiles = (n + 63u) >> 6;
+  const uint32_t tile0 = ((gb - a.blk0[lo]) * 4u + wv) * (uint32_t)T;
+  const uint32_t need = a.need;
+  // columns a program does not read get zero-length descriptors: their loads return 0 and move
+  // no data (so do loads past a column's end)
+  const Rsrc REC = make_rsrc(S.rec, n * 16u), HDR = make_rsrc(S.hdr, (ntiles + 1u) * 16u);
+  const Rsrc CREC = make_rsrc(S.crec, S.nctr * 8u);
+  const Rsrc SAN = make_rsrc(S.sann, (need & NEED_SANN) ? S.nctr * 4u : 0u);
+  const Rsrc VOL = make_rsrc(S.vol, (need & NEED_VOL) ? S.nvol * 4u : 0u);
+  const Rsrc SYS = make_rsrc(S.sys, (need & NEED_SYS) ? S.nsys * 4u : 0u);
+  const Rsrc ANN = make_rsrc(S.pann, (need & NEED_PANN) ? S.npann * 8u : 0u);
+  // ---- step 1: headers (lane k: word k of hdr[tile0 + k / 4]; past the sentinel: 0), records
+  const uint32_t hall = bload1(HDR, (tile0 * 4u + min(lane, 4u * T + 3u)) * 4u);
+  uint4 rec[T];
 #pragma unroll
-  for (int i = 0; i < T; ++i) sr[i] = bload3(PS, ((tile0 + 4u * i) * 64u + lane) * 12u);  // past n: zeros
+  for (int j = 0; j < T; ++j) rec[j] = bload4(REC, ((tile0 + j) * 64u + lane) * 16u);  // past n: zeros
+  // the block's kind table and (LC) code bytes, for the LDS below
   const uint32_t nk = S.nkinds;
   const uint32_t k0 = t < nk ? S.kt[t] : 0u;
+  const uint32_t ncw = LC ? (S.L.bytes + 3u) >> 2 : 0u;
+  const uint32_t* gcw = reinterpret_cast<const uint32_t*>(S.codes);
+  const uint32_t cw0 = LC && t < ncw ? gcw[t] : 0u;
+  // ---- step 2: the list items of every tile
+  L6Items it[T];
+#pragma unroll
+  for (int j = 0; j < T; ++j) {
+    if (tile0 + j >= ntiles) break;
+    const uint32_t C0 = hw(hall, 4u * j), V0 = hw(hall, 4u * j + 1u), S0 = hw(hall, 4u * j + 2u),
+                   A0 = hw(hall, 4u * j + 3u);
+    it[j].c0 = bload2(CREC, (C0 + lane) * 8u);
+    it[j].c1 = bload2(CREC, (C0 + 64u + lane) * 8u);
+    it[j].a0 = bload1(SAN, (C0 + lane) * 4u);
+    it[j].a1 = bload1(SAN, (C0 + 64u + lane) * 4u);
+    it[j].v0 = bload1(VOL, (V0 + lane) * 4u);
+    it[j].v1 = bload1(VOL, (V0 + 64u + lane) * 4u);
+    it[j].s0 = bload1(SYS, (S0 + lane) * 4u);
+    it[j].q0 = bload2(ANN, (A0 + lane) * 8u);
+  }
+  if (t < nk) dyn[t] = k0;
+#pragma unroll 1
+  for (uint32_t i = t + kLB; i < nk; i += kLB) dyn[i] = S.kt[i];
+  uint32_t* const cl = dyn + a.kt_words;
+  if (LC) {
+    if (t < ncw) cl[t] = cw0;
+#pragma unroll 1
+    for (uint32_t i = t + kLB; i < ncw; i += kLB) cl[i] = gcw[i];
+  }
   uint32_t cls_cv = 0, cls_rm = 0;
   const uint32_t ncls = a.ncls;
   if (lane < ncls) {
     const uint2 c = reinterpret_cast<const uint2*>(a.narrow_cls)[lane];
     cls_cv = c.x, cls_rm = c.y;
   }
-  if (t < nk) dyn[t] = k0;
-#pragma unroll 1
-  for (uint32_t i = t + kLB; i < nk; i += kLB) dyn[i] = S.kt[i];
   __syncthreads();
+  const uint8_t* const lcodes = reinterpret_cast<const uint8_t*>(cl);
+  const uint8_t* const gcodes = S.codes;
+  auto cb = [&](uint32_t i) -> uint32_t { return LC ? (uint32_t)lcodes[i] : (uint32_t)gcodes[i]; };
+  PsaCodes L;
+  L.ncapsets = S.L.ncapsets, L.nsysd = S.L.nsysd, L.nannk = S.L.nannk, L.nannv = S.L.nannv;
+  L.o_sys = S.L.o_sys, L.o_annk = S.L.o_annk, L.o_annv = S.L.o_annv, L.bytes = S.L.bytes;
+  const PsaCoder K{L};
+  const bool nsann = need & NEED_SANN, nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN;
+  auto ctr_code = [&](uint2 e, uint32_t cs) -> uint2 {  // a real container record always has state bits
+    return make_uint2(e.x, e.x ? K.cap(cb, CY_CAPSET(e.y)) | (nsann ? K.sann(cb, cs) << 3 : 0u) : 0u);
+  };
   const uint32_t R = a.nrules, cv_union = a.cv_union, pss_rules = a.pss_rules;
   const uint32_t ep_rules = a.err_rules | a.pat_rules, pat_rules = a.pat_rules;
-  uint8_t* sv = reinterpret_cast<uint8_t*>(dyn + a.kt_words) + wv * 64u * R;
+  uint8_t* const stg = reinterpret_cast<uint8_t*>(cl + a.code_words + wv * a.wave_words);
+  uint2* const sc = reinterpret_cast<uint2*>(stg);
+  uint8_t* const sbv = stg + 8u * KPE_L6_CTR;
+  uint8_t* const sbs = sbv + KPE_L6_VOL;
+  uint8_t* const sba = sbs + KPE_L6_SMALL;
+  uint8_t* const sv = sba + KPE_L6_SMALL;  // the tile's verdict rows (64 x R bytes)
 #pragma unroll
-  for (int i = 0; i < T; ++i) {
-    const uint32_t tile = tile0 + 4u * i;
-    if (tile * 64u >= n) break;
+  for (int j = 0; j < T; ++j) {
+    const uint32_t tile = tile0 + j;
+    if (tile >= ntiles) break;
+    const L6Items& d = it[j];
+    const uint32_t C0 = hw(hall, 4u * j), V0 = hw(hall, 4u * j + 1u), S0 = hw(hall, 4u * j + 2u),
+                   A0 = hw(hall, 4u * j + 3u);
+    const uint32_t nct = hw(hall, 4u * j + 4u) - C0, nvt = hw(hall, 4u * j + 5u) - V0,
+                   nst = hw(hall, 4u * j + 6u) - S0, nat = hw(hall, 4u * j + 7u) - A0;
     const uint32_t r = tile * 64u + lane;
     const bool live = r < n;
-    const uint32_t pw = sr[i].x, y = sr[i].z;
-    const uint32_t fails = sr[i].y & cv_union;
+    // the pod's item offsets: exclusive wave scans of its packed counts
+    const uint32_t z = rec[j].z;  // 0 for rows past n
+    const uint32_t nc = PRC_CTR(z), nv = PRC_VOL(z), ns = PRC_SYS(z), na = PRC_PANN(z);
+    uint32_t oc, ov, os, oa;
+    if ((nct | nvt | nst | nat) < 256u) {  // one scan of the four packed byte counts (no carries)
+      const uint32_t e = wave_incl_scan(z) - z;
+      oc = e & 0xFFu, ov = (e >> 8) & 0xFFu, os = (e >> 16) & 0xFFu, oa = e >> 24;
+    } else {
+      const uint32_t c01 = nc | (nv << 16), c23 = ns | (na << 16);
+      const uint32_t e01 = wave_incl_scan(c01) - c01, e23 = wave_incl_scan(c23) - c23;
+      oc = e01 & 0xFFFFu, ov = e01 >> 16, os = e23 & 0xFFFFu, oa = e23 >> 16;
+    }
+    // stage the codes of the loaded slots (slots past the tile's items hold codes of the next
+    // tile's items, or of zeros past a column's end, that no pod reads)
+    __builtin_amdgcn_wave_barrier();  // the previous tile's stage reads are done
+    sc[lane] = ctr_code(d.c0, d.a0);
+    sc[lane + 64u] = ctr_code(d.c1, d.a1);
+    if (nvol) sbv[lane] = (uint8_t)vol_code(d.v0), sbv[lane + 64u] = (uint8_t)vol_code(d.v1);
+    if (nsys && nst) sbs[lane] = (uint8_t)K.sys(cb, d.s0);
+    if (npann && nat) sba[lane] = (uint8_t)K.ann(cb, d.q0);
+    __builtin_amdgcn_wave_barrier();
+    // each pod ORs its first items with clamped reads (a repeated item does not change an OR)
+    uint32_t xo, co, vcode = 0, scode = 0, acode = 0;
+    {
+      const uint32_t last = min(oc + (nc ? nc - 1u : 0u), KPE_L6_CTR - 1u);
+      const uint2 e0 = sc[min(oc, last)], e1 = sc[min(oc + 1u, last)], e2 = sc[min(oc + 2u, last)],
+                  e3 = sc[min(oc + 3u, last)];
+      const uint32_t m = nc ? ~0u : 0u;
+      xo = (e0.x | e1.x | e2.x | e3.x) & m;
+      co = (e0.y | e1.y | e2.y | e3.y) & m;
+    }
+    if (nvol) {
+      const uint32_t last = min(ov + (nv ? nv - 1u : 0u), KPE_L6_VOL - 1u);
+      const uint32_t x = (uint32_t)sbv[min(ov, last)] | sbv[min(ov + 1u, last)] | sbv[min(ov + 2u, last)] |
+                         sbv[min(ov + 3u, last)];
+      vcode = nv ? x : 0u;
+    }
+    if (nsys && nst) {
+      const uint32_t last = min(os + (ns ? ns - 1u : 0u), KPE_L6_SMALL - 1u);
+      const uint32_t x = (uint32_t)sbs[min(os, last)] | sbs[min(os + 1u, last)];
+      scode = ns ? x : 0u;
+    }
+    if (npann && nat) {
+      const uint32_t last = min(oa + (na ? na - 1u : 0u), KPE_L6_SMALL - 1u);
+      const uint32_t x = (uint32_t)sba[min(oa, last)] | sba[min(oa + 1u, last)];
+      acode = na ? x : 0u;
+    }
+    // pods with more items than that, or items past the stage: recomputed over all their items
+    // (staged ones from LDS, the rest loaded)
+    const bool tile_over = nct > KPE_L6_CTR || (nvol && nvt > KPE_L6_VOL) || (nsys && nst > KPE_L6_SMALL) ||
+                           (npann && nat > KPE_L6_SMALL);
+    const bool more_c = nc > 4u, more_v = nvol && nv > 4u, more_s = nsys && ns > 2u, more_a = npann && na > 2u;
+    if (tile_over || __builtin_amdgcn_ballot_w64(more_c || more_v || more_s || more_a)) {
+      if (more_c || oc + nc > KPE_L6_CTR) {
+        xo = co = 0;
+        for (uint32_t k = oc; k < oc + nc; ++k) {
+          const uint2 e = k < KPE_L6_CTR ? sc[k]
+                                         : ctr_code(bload2(CREC, (C0 + k) * 8u), nsann ? bload1(SAN, (C0 + k) * 4u) : 0u);
+          xo |= e.x, co |= e.y;
+        }
+      }
+      if (nvol && (more_v || ov + nv > KPE_L6_VOL)) {
+        vcode = 0;
+        for (uint32_t k = ov; k < ov + nv; ++k)
+          vcode |= k < KPE_L6_VOL ? (uint32_t)sbv[k] : vol_code(bload1(VOL, (V0 + k) * 4u));
+      }
+      if (nsys && (more_s || os + ns > KPE_L6_SMALL)) {
+        scode = 0;
+        for (uint32_t k = os; k < os + ns; ++k)
+          scode |= k < KPE_L6_SMALL ? (uint32_t)sbs[k] : K.sys(cb, bload1(SYS, (S0 + k) * 4u));
+      }
+      if (npann && (more_a || oa + na > KPE_L6_SMALL)) {
+        acode = 0;
+        for (uint32_t k = oa; k < oa + na; ++k)
+          acode |= k < KPE_L6_SMALL ? (uint32_t)sba[k] : K.ann(cb, bload2(ANN, (A0 + k) * 8u));
+      }
+    }
+    // ---- the PSA checks, the rule match (kind table) and the verdict bytes ----
+    const uint32_t pw = rec[j].x;
+    const uint32_t fails =
+        cv_fails(pw, xo, co & 7u, (co >> 3) & 1u, vcode & 1u, vcode & 2u, scode, acode & 1u, acode & 2u) & cv_union;
     const uint32_t cls = (pw >> PR_CLASS_SH) & R_CLASS_MASK;
     const bool err = cls == R_CLASS_OTHER || (pw & PR_DECODE_ERR);
-    const uint32_t kind = y >> 16;
+    const uint32_t kind = GVK_KIND(rec[j].y);
     const uint32_t matched = live && kind < nk ? dyn[kind] : 0u;
     uint32_t failr = 0;
 #pragma unroll 1
     for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
     const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
-    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);
+    const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);  // F|E = PENDING
     const uint32_t P = matched & pss_rules & ~failr & ~E;
-    __builtin_amdgcn_wave_barrier();  // the previous tile's rows are out of the staging area
 #pragma unroll 1
     for (uint32_t ri = 0; ri < R; ++ri)
       sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));

@@ -1,12 +1,13 @@
-"""kpe_lean5_kernel (the headline C2 scan) over full matrices at every PSS level and version.
+"""kpe_lean6_kernel (the headline C2 evaluation) over full matrices at every PSS level and version.
 
 Every kind-only podSecurity policy (baseline / restricted / privileged x latest and each version
-a PSA check changes at) is forced through the LEAN5 instantiation, asserted by the kernel stats,
+a PSA check changes at) is forced through the LEAN6 evaluation, asserted by the kernel stats,
 over 20k-row synthetic mixes with Deployments, CronJobs, nulls, type errors and windows pods.
 Compared with the oracle: the whole verdict matrix, and with masks the whole versioned-check
 matrix (kpe_fetch_cv_masks: a FAIL cell holds the failing versioned checks of its level /
-version, evaluate.go:24-70; every other cell 0). That pins the per-pod PSA summary
-(tests/test_psum.py) semantically: each versioned check's failure reaches the masks."""
+version, evaluate.go:24-70; every other cell 0). Every evaluation reads each pod's record and its
+container / volume / sysctl / annotation lists; only the PSA dictionary codes (per distinct
+string, tests/test_psum.py) are kept per corpus."""
 import numpy as np
 import pytest
 
@@ -17,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 LEVELS = ("baseline", "restricted", "privileged")
 VERSIONS = ("latest", "v1.0", "v1.8", "v1.19", "v1.22", "v1.23", "v1.24", "v1.25", "v1.27", "v1.29")
-LEAN5 = 7  # kpe_kernel_stats.scan_kernel of kpe_lean5_kernel
+LEAN6 = 7  # kpe_kernel_stats.scan_kernel of a one-shard kpe_lean6_kernel launch
 
 
 @pytest.fixture(scope="module")
@@ -37,20 +38,20 @@ def corpus(request, engine):
 
 
 @pytest.mark.parametrize("level", LEVELS)
-def test_lean5_full_matrix_every_version(engine, oracle, corpus, level):
+def test_lean6_full_matrix_every_version(engine, oracle, corpus, level):
     nd, c = corpus
     for ver in VERSIONS:
         pol = pss_policy(f"{level}-{ver.replace('.', '-')}", level, ver)
         ps = K.PolicySet([pol])
         assert ps.num_rules == 3  # Pod + the autogen controller and CronJob rules
         ref = oracle.validate([pol], nd, nthreads=8)
-        # verdicts, no masks: the LEAN5 instantiation must be the one that ran
+        # verdicts, no masks: the LEAN6 evaluation must be the one that ran
         engine.device.set_timing(True)
         engine.device.kernel_stats(reset=True)
         engine.evaluate_async(ps, c)
         st = engine.device.kernel_stats(reset=True)
         engine.device.set_timing(False)
-        assert st.launches == 1 and st.scan_kernel == LEAN5, (level, ver, st.scan_kernel)
+        assert st.launches == 1 and st.scan_kernel == LEAN6, (level, ver, st.scan_kernel)
         v, _, _ = engine.evaluate(ps, c)
         bad = np.argwhere(v != ref)
         assert bad.size == 0, (level, ver, len(bad), bad[:5].tolist())
@@ -70,9 +71,9 @@ def test_lean5_full_matrix_every_version(engine, oracle, corpus, level):
             assert fail.sum() > 0 and (got[fail] != 0).all()
 
 
-def test_lean5_batch_launch(engine, oracle):
-    """kpe_evaluate_batch_async over warm LEAN5 shards of different sizes (one pod, a partial
-    tile, repeats in one launch): one kpe_lean5_batch_kernel launch, and every shard's verdict
+def test_lean6_batch_launch(engine, oracle):
+    """kpe_evaluate_batch_async over warm LEAN shards of different sizes (one pod, a partial
+    tile, repeats in one launch): one multi-shard kpe_lean6_kernel launch, and every shard's verdict
     matrix (poisoned on the device beforehand) and check masks equal the oracle's."""
     import ctypes
     from tests.golden.make_psum_digests import seccomp_ndjson
@@ -84,7 +85,7 @@ def test_lean5_batch_launch(engine, oracle):
     refs = [oracle.validate(pols, nd, nthreads=8) for nd in nds]
     hip = ctypes.CDLL("libamdhip64.so")
     for masks in (False, True):
-        for c in cs:  # bind (prologue image, PSA summary), then poison the verdicts
+        for c in cs:  # bind (prologue image, PSA dictionary codes), then poison the verdicts
             engine.evaluate(ps, c, check_masks=masks)
             ptr, nb = engine.device_verdicts(ps, c)
             assert hip.hipMemset(ctypes.c_void_p(ptr), 0xFF, ctypes.c_size_t(nb)) == 0
@@ -109,8 +110,9 @@ def test_lean5_batch_launch(engine, oracle):
                 assert np.array_equal(got, want), (i, int((got != want).sum()))
 
 
-def test_lean5_batch_many_shards(engine, oracle):
-    """More than 64 shards in one call: near-equal multi-shard launches, verdicts unchanged."""
+def test_lean6_batch_many_shards(engine, oracle):
+    """More than KPE_LEAN_BATCH (24) shards in one call: near-equal multi-shard launches, verdicts
+    unchanged, and each launch's algorithmic bytes the sum of its shards' one-shard bytes."""
     pols = [pss_policy("baseline-latest", "baseline", "latest")]
     ps = K.PolicySet(pols)
     nd = K.synth_resources(0x65, 3000, mix=1)
@@ -120,19 +122,22 @@ def test_lean5_batch_many_shards(engine, oracle):
         engine.evaluate(ps, c)
     engine.device.set_timing(True)
     engine.device.kernel_stats(reset=True)
+    engine.evaluate_async(ps, cs[0])
+    one = engine.device.kernel_stats(reset=True)
+    assert one.launches == 1 and one.scan_kernel == LEAN6
     engine.evaluate_batch_async(ps, [cs[i % 3] for i in range(130)])
     st = engine.device.kernel_stats(reset=True)
     engine.device.set_timing(False)
-    assert st.launches == 3 and st.scan_kernel == 9
-    assert abs(st.scan_bytes - 44 * 3000 * (12 + 3)) < 1  # 130 -> 43 + 43 + 44 shards
+    assert st.launches == 6 and st.scan_kernel == 9
+    assert abs(st.scan_bytes - 22 * one.scan_bytes) < 1  # 130 -> 21 + 21 + 22 + 22 + 22 + 22 shards (the last)
     engine.device.sync()
     for c in cs:
         v, _, _ = engine.fetch(ps, c)
         assert np.array_equal(v, ref)
 
 
-def test_lean5_batch_tiles_per_wave(engine):
-    """A batch large enough for 8 tiles per wave (one 1M + 37-pod shard nine times: 140k tiles;
+def test_lean6_batch_tiles_per_wave(engine):
+    """A batch large enough for 4 tiles per wave (one 1M + 37-pod shard nine times: 140k tiles;
     the last block of every shard partial): the same verdicts as the single-shard kernel, whose
     parity with the oracle the tests above pin."""
     import ctypes
