@@ -76,9 +76,53 @@ def cpu_model():
     return "unknown"
 
 
-def main():
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _rank_main(rank, world, argv):
+    """A rank started by launch_ranks: the torchrun environment, then the bench."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                      GROUP_RANK="0")
+    main(argv)
+
+
+def spawn_check():
+    """Each rank joins the process group and all-reduces its rank; rank 0 prints the result."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group(os.environ.get("KPE_DIST_BACKEND", "gloo"))
+    t = torch.tensor([rank], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"spawn_check": True, "n_gpus": world, "rank_sum": int(t.item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def launch_ranks(world, argv):
+    """`--gpus N` without an external launcher: N rank processes on this node, one per GPU, started
+    with the spawn method before this process makes any GPU call (a child process each, never an
+    exec of this one); rendezvous over 127.0.0.1. A failing rank fails the run."""
+    import torch.multiprocessing as mp
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", str(_free_port()))
+    mp.start_processes(_rank_main, args=(world, argv), nprocs=world, start_method="spawn", join=True)
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1, help="ranks (one per GPU); without an external launcher "
+                                                        "(WORLD_SIZE unset) bench.py starts them itself")
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", choices=("c2", "c3", "c4", "c5"), default="c2")
@@ -87,14 +131,27 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=-1, help="rows in the CPU-baseline sample (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use (cpu_budget)")
     ap.add_argument("--traffic-json", default="")
-    args = ap.parse_args()
+    ap.add_argument("--total-resources", type=int, default=0,
+                    help="strong scaling: this many rows in all, split over the ranks (C3 10M over 8 GPUs)")
+    ap.add_argument("--spawn-check", action="store_true",
+                    help="start the ranks, all-reduce their ids over the process group and exit (CPU check)")
+    args = ap.parse_args(argv)
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:  # no external launcher: start the ranks here
+        return launch_ranks(args.gpus, sys.argv[1:] if argv is None else argv)
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks")
+    if args.spawn_check:
+        return spawn_check()
 
     import numpy as np  # noqa: F401
     import torch
     import torch.distributed as dist
 
     import kyverno_amd as K
-    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, gather_packed, max_over_ranks
+    from kyverno_amd.shard import COUNT_FIELDS, allreduce_counts, gather_packed, max_over_ranks, shard_range
     from tests.policies import c3_policy_set, c4_policy_set, c5_policy_set, restricted_latest
 
     cfg = args.config
@@ -111,7 +168,16 @@ def main():
     else:
         policies, mix, seed, n_def, rep_def, docs = c5_policy_set(), K.SYNTH_FANOUT, 0xC5, 1_000_000, 1, True
         workload = "C5: 1M Pods/Deployments with 1-64 containers x requests-limits/latest-tag/host-ports/anchor patterns"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
     n = args.resources or n_def
+    first = None  # strong scaling: this rank's first row of the --total-resources corpus
+    if args.total_resources:
+        first, n = shard_range(args.total_resources, rank, world)
+        rep_def = 1
+        workload = (f"{cfg.upper()}: {args.total_resources} rows in all, split over {world} GPU(s) "
+                    f"(contiguous row ranges); " + workload.split(": ", 1)[1].split(" per GPU")[0])
+    n_all = args.total_resources or n * world
     if args.replicas:
         replicas = args.replicas
     elif rep_def:
@@ -123,8 +189,6 @@ def main():
     # perf/ travels to the GPU box, profiles/ does not
     traffic_json = args.traffic_json or os.path.join(ROOT, "perf", f"pmc_traffic_{cfg}.json")
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
     # One rank per GPU over RCCL. KPE_DIST_BACKEND=gloo runs the collectives on host tensors: a
     # functional check of the N-rank path with several ranks sharing one device (RCCL refuses two
     # ranks on one GPU); ranks then take device LOCAL_RANK modulo the visible devices.
@@ -154,7 +218,8 @@ def main():
     # shard k of rank r: rows [(r*replicas + k)*n, ...) of one logical corpus; the synthetic NDJSON
     # of the next shards is generated on two threads while this one is flattened and uploaded
     with ThreadPoolExecutor(max_workers=2) as pool:
-        futs = [pool.submit(K.synth_resources, seed, n, mix, (rank * replicas + k) * n) for k in range(replicas)]
+        futs = [pool.submit(K.synth_resources, seed, n, mix, first if first is not None else (rank * replicas + k) * n)
+                for k in range(replicas)]
         for k in range(replicas):
             nd = futs[k].result()
             futs[k] = None
@@ -211,11 +276,12 @@ def main():
     eng.device.sync()
     barrier()
     t1 = time.perf_counter()
-    full = gather_packed(eng, ps, corpora[0], n * world, dst=0, device=coll_dev)
+    full = gather_packed(eng, ps, corpora[0], n_all, dst=0, device=coll_dev)
     torch.cuda.synchronize()
     gather_s = max_over_ranks(time.perf_counter() - t1, device=coll_dev)
-    gather = {"rows": n * world, "bytes": 4 * K.packed_words(n * R) * world, "cell_bits": 3, "seconds": gather_s,
-              "rows_ok": bool(rank != 0 or (full is not None and full.shape == (n * world, R)))}
+    gather = {"rows": n_all, "bytes": sum(4 * K.packed_words(shard_range(n_all, r, world)[1] * R) for r in range(world)),
+              "cell_bits": 3, "seconds": gather_s, "backend": backend if world > 1 else None,
+              "rows_ok": bool(rank != 0 or (full is not None and full.shape == (n_all, R)))}
 
     # ---- per-kernel timing pass: the timed region's K steps again, with HIP events around every
     # launch on the library's stream (launches serialised there, so each duration is its own; a
@@ -264,7 +330,7 @@ def main():
     eng.device.set_timing(False)
 
     ms_per_step = elapsed / args.steps * 1e3
-    evals = float(n) * R * world * args.steps
+    evals = float(n_all) * R * args.steps
     value = evals / elapsed
 
     traffic = None
@@ -327,7 +393,7 @@ def main():
             # its algorithmic bytes are every resource's document tape once plus the verdicts
             pat_achieved = st.pattern_bytes / (pat_ms * 1e-3) / 1e9
             pat_traffic = None
-            try:  # FETCH_SIZE / WRITE_SIZE of the pattern kernel (scripts/gpu_pat_pmc.sh)
+            try:  # FETCH_SIZE / WRITE_SIZE of the pattern kernel (scripts/gpu_pass.sh traffic:<cfg>:kpe_pattern_kernel)
                 tj = json.load(open(traffic_json))
                 if tj.get("kernel") == "kpe_pattern_kernel":
                     pat_traffic = tj.get("scan_bytes_per_launch")
@@ -349,17 +415,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total_resources else "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": f"synthetic (kpe_synth {cfg.upper()} generator, seed {seed:#x})",
-            "config": {"workload": workload, "resources_per_gpu": n, "rules": R, "global_resources": n * world,
+            "config": {"workload": workload, "resources_per_gpu": n, "rules": R, "global_resources": n_all,
                        "replicas_rotated": replicas, "parallelism": f"resource-sharded x{world}",
                        # scan bytes touched between two uses of one shard vs the Infinity Cache
                        "rotated_scan_bytes": st.scan_bytes * replicas, "infinity_cache_bytes": IC_BYTES,
                        # cells where the rule matched the resource (a RuleResponse exists), per s
-                       "matched_cell_evals_per_s": value * sum(n * replicas * world - totals[r]["na"]
-                                                               for r in range(R)) / float(n * replicas * world * R),
+                       "matched_cell_evals_per_s": value * sum(n_all * replicas - totals[r]["na"]
+                                                               for r in range(R)) / float(n_all * replicas * R),
                        "counts_rule0": totals[0]},
             "roofline": scan_roof,
             "cpu_baseline": cpu,
