@@ -1412,21 +1412,18 @@ extern "C" hipError_t kpe_launch_selmask(const SelMaskArgs* a, hipStream_t s) {
   return hipGetLastError();
 }
 // The LEAN evaluation of one or more bound shards of one program in one grid (lean.inl).
-template <int T>
-static hipError_t lean6_go(const LeanBatchArgs* a, uint32_t grid, size_t dyn_bytes, int lc, hipStream_t s) {
-  if (lc) hipLaunchKernelGGL((kpe_lean6_kernel<T, true>), dim3(grid), dim3(kLB), dyn_bytes, s, *a);
-  else hipLaunchKernelGGL((kpe_lean6_kernel<T, false>), dim3(grid), dim3(kLB), dyn_bytes, s, *a);
-  return hipGetLastError();
-}
+// tpw: tiles per wave (1, 2 or 4; 4 only with the code bytes in LDS, lc).
 extern "C" hipError_t kpe_launch_lean6(const LeanBatchArgs* a, size_t dyn_bytes, int lc, hipStream_t s) {
   const uint32_t grid = a->blk0[a->nshards];
   if (a->nshards == 0 || grid == 0) return hipSuccess;
-  switch (a->tpw) {
-    case 4: return lean6_go<4>(a, grid, dyn_bytes, lc, s);
-    case 2: return lean6_go<2>(a, grid, dyn_bytes, lc, s);
-    case 1: return lean6_go<1>(a, grid, dyn_bytes, lc, s);
-    default: return hipErrorInvalidValue;
-  }
+  const dim3 g(grid), b(kLB);
+  if (a->tpw == 4 && lc) hipLaunchKernelGGL((kpe_lean6_kernel<4, true>), g, b, dyn_bytes, s, *a);
+  else if (a->tpw == 2 && lc) hipLaunchKernelGGL((kpe_lean6_kernel<2, true>), g, b, dyn_bytes, s, *a);
+  else if (a->tpw == 1 && lc) hipLaunchKernelGGL((kpe_lean6_kernel<1, true>), g, b, dyn_bytes, s, *a);
+  else if (a->tpw == 2) hipLaunchKernelGGL((kpe_lean6_kernel<2, false>), g, b, dyn_bytes, s, *a);
+  else if (a->tpw == 1) hipLaunchKernelGGL((kpe_lean6_kernel<1, false>), g, b, dyn_bytes, s, *a);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
 }
 // The PSA dictionary codes of a corpus (lean.inl), one launch.
 extern "C" hipError_t kpe_launch_psa_codes(const PsaCodeArgs* a, hipStream_t s) {

@@ -1573,12 +1573,17 @@ kpe_status lean6_launch(kpe_device* dev, const kpe::Program& P, const kpe::Devic
   a.pss_rules = PD.pss_rules, a.err_rules = PD.err_rules, a.pat_rules = PD.pat_rules;
   a.narrow_cls = PD.narrow_cls.as<uint32_t>();
   uint64_t tiles = 0;
-  for (size_t k = 0; k < m; ++k) tiles += (uint64_t)(cs[k]->c->n + 63) / 64;
-  uint32_t tpw = 4;
+  uint32_t code_max = 0;
+  for (size_t k = 0; k < m; ++k) {
+    tiles += (uint64_t)(cs[k]->c->n + 63) / 64;
+    code_max = std::max(code_max, cs[k]->d->psa_L.bytes);
+  }
+  const bool lc = code_max <= kLeanCodeLds;
+  uint32_t tpw = lc ? 4 : 2;  // 4 tiles with global code reads would spill
   while (tpw > 1 && tiles / tpw < dev->lean_min_waves) tpw >>= 1;
-  if (dev->lean_tpw) tpw = dev->lean_tpw;
+  if (dev->lean_tpw) tpw = std::min(dev->lean_tpw, lc ? 4u : 2u);
   a.tpw = tpw;
-  uint32_t acc = 0, kt_max = 0, code_max = 0;
+  uint32_t acc = 0, kt_max = 0;
   *bytes = 0;
   for (size_t k = 0; k < m; ++k) {
     auto& C = *cs[k]->c;
@@ -1599,12 +1604,10 @@ kpe_status lean6_launch(kpe_device* dev, const kpe::Program& P, const kpe::Devic
     a.blk0[k] = acc;
     acc += (uint32_t)((C.n + 256 * tpw - 1) / (256 * tpw));  // 4 waves x tpw tiles of 64 pods per block
     kt_max = std::max(kt_max, B.nkinds);
-    code_max = std::max(code_max, D.psa_L.bytes);
     a.need |= B.need;
     *bytes += lean_bytes(C, D, B.need, R, masks);
   }
   a.blk0[m] = acc;
-  const bool lc = code_max <= kLeanCodeLds;
   a.kt_words = (kt_max + 3u) & ~3u;
   a.code_words = lc ? ((code_max + 15u) / 16u) * 4u : 0u;
   a.wave_words = ((KPE_L6_STAGE_BYTES + 64u * R + 15u) / 16u) * 4u;

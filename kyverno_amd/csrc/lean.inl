@@ -127,26 +127,34 @@ __global__ void __launch_bounds__(256) kpe_psa_codes_kernel(PsaCodeArgs a) {
 }
 
 // Code of one list item from the corpus's code bytes (`cb`: LDS or global), shared by the LEAN
-// evaluation and the general scan's per-pod records.
+// evaluation and the general scan's per-pod records. Branch-free: every code byte is read at an
+// index clamped into the code table (the part's pad byte stands in for an id past the part) and
+// the result selected afterwards, so no lane waits on a divergent load.
 struct PsaCoder {
   const PsaCodes& L;
+  // capability-set code of a container record (0 for an empty slot: no state bits)
   template <class CB>
-  __device__ __forceinline__ uint32_t cap(const CB& cb, uint32_t capset) const { return cb(capset) & 7u; }
+  __device__ __forceinline__ uint32_t cap(const CB& cb, uint2 e) const {
+    const uint32_t c = cb(CY_CAPSET(e.y)) & 7u;  // a real record's set id is < ncapsets; a zero slot reads set 0
+    return e.x ? c : 0u;
+  }
   // a container's seccomp annotation value (check_seccompProfile v1.0): 1 when set and not allowed
   template <class CB>
   __device__ __forceinline__ uint32_t sann(const CB& cb, uint32_t cs) const {
-    if (cs == KPE_NO_STR) return 0u;
-    return (cs < L.nannv ? (cb(L.o_annv + cs) >> 1) & 1u : 0u) ^ 1u;
+    const uint32_t v = cb(L.o_annv + min(cs, L.nannv));
+    const uint32_t ok = cs < L.nannv ? (v >> 1) & 1u : 0u;
+    return cs == KPE_NO_STR ? 0u : ok ^ 1u;
   }
   template <class CB>
   __device__ __forceinline__ uint32_t sys(const CB& cb, uint32_t id) const {
-    return id < L.nsysd ? cb(L.o_sys + id) : 7u;
+    const uint32_t v = cb(L.o_sys + min(id, L.nsysd));
+    return id < L.nsysd ? v : 7u;
   }
   template <class CB>
   __device__ __forceinline__ uint32_t ann(const CB& cb, uint2 q) const {
-    const uint32_t ka = q.x < L.nannk ? cb(L.o_annk + q.x) : 0u;
-    const uint32_t va = q.y < L.nannv ? cb(L.o_annv + q.y) : 0u;
-    return ((ka & 1u) && !(va & 1u) ? 1u : 0u) | ((ka & 2u) && !(va & 2u) ? 2u : 0u);
+    const uint32_t k = cb(L.o_annk + min(q.x, L.nannk)), v = cb(L.o_annv + min(q.y, L.nannv));
+    const uint32_t ka = q.x < L.nannk ? k : 0u, va = q.y < L.nannv ? v : 0u;
+    return ka & ~va & 3u;  // bit 0 AppArmor key with a disallowed profile, bit 1 pod seccomp key likewise
   }
 };
 __device__ __forceinline__ uint32_t vol_code(uint32_t v) {
@@ -182,7 +190,7 @@ __global__ void __launch_bounds__(256) kpe_psum_kernel(PsumArgs a) {
   for (uint32_t k = 0; k < nc; ++k) {
     const uint2 e = crec[oc + k];
     xo |= e.x;
-    if (e.x) co |= K.cap(cb, CY_CAPSET(e.y));  // a real container record always has state bits
+    co |= K.cap(cb, e);
     sa |= K.sann(cb, a.c_sann[oc + k]);
   }
   for (uint32_t k = 0; k < nv; ++k) vc |= vol_code(a.vol_src[ov + k]);
@@ -294,7 +302,8 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN6_WAVES) kpe_lean6_kernel(LeanBat
   const PsaCoder K{L};
   const bool nsann = need & NEED_SANN, nvol = need & NEED_VOL, nsys = need & NEED_SYS, npann = need & NEED_PANN;
   auto ctr_code = [&](uint2 e, uint32_t cs) -> uint2 {  // a real container record always has state bits
-    return make_uint2(e.x, e.x ? K.cap(cb, CY_CAPSET(e.y)) | (nsann ? K.sann(cb, cs) << 3 : 0u) : 0u);
+    const uint32_t sa = nsann ? K.sann(cb, cs) << 3 : 0u;
+    return make_uint2(e.x, K.cap(cb, e) | (e.x ? sa : 0u));
   };
   const uint32_t R = a.nrules, cv_union = a.cv_union, pss_rules = a.pss_rules;
   const uint32_t ep_rules = a.err_rules | a.pat_rules, pat_rules = a.pat_rules;

@@ -9,7 +9,7 @@
 #   pmc:<cfg>:<counters>[:<args>]  one rocprofv3 --pmc pass (counters comma-separated; one block's
 #                         limits per pass, MI355X_MICROARCH.md)
 #   traffic:<cfg>:<kernel prefix>[:<args>]  FETCH_SIZE and WRITE_SIZE passes summarised into
-#                         perf/pmc_traffic_<cfg>.json (scripts/pmc_summary.py)
+#                         gpurun_out/<tag>/pmc_traffic_<cfg>.json (scripts/pmc_summary.py; copy it to perf/)
 #   ranks:<n>[:<args>]    bench.py --gpus <n> with gloo collectives (several ranks on one device)
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
@@ -41,19 +41,22 @@ for st in "$@"; do
       run "bench_$a1" 400 python bench.py --config "$a1" ${a2//,/ }
       grep '^{' "$O/bench_$a1.log" > "$O/bench_$a1.json" ;;
     trace)
+      x=${a2:---steps,20,--warmup,3,--cpu-sample,0}
       run "trace_$a1" 400 rocprofv3 --kernel-trace --stats -d "$O/prof_$a1" -o "$a1" --output-format csv -- \
-        python3 bench.py --config "$a1" ${a2:---steps,20,--warmup,3,--cpu-sample,0} ;;
+        python3 bench.py --config "$a1" ${x//,/ } ;;
     pmc)
-      run "pmc_${a1}_$(echo "$a2" | tr ',' '_' | cut -c1-40)" 120 rocprofv3 --pmc ${a2//,/ } -d "$O/pmc_$a1" \
-        -o "pmc_$(echo "$a2" | tr ',' '_' | cut -c1-40)" --output-format csv -- \
-        python3 bench.py --config "$a1" ${a3:---steps,5,--warmup,1,--cpu-sample,0} ;;
+      x=${a3:---steps,5,--warmup,1,--cpu-sample,0}
+      nm=$(echo "$a2" | tr ',' '_' | cut -c1-40)
+      run "pmc_${a1}_$nm" 120 rocprofv3 --pmc ${a2//,/ } -d "$O/pmc_$a1" -o "pmc_$nm" --output-format csv -- \
+        python3 bench.py --config "$a1" ${x//,/ } ;;
     traffic)
+      x=${a3:---steps,20,--warmup,3,--cpu-sample,0,--replicas,20}
       for k in FETCH_SIZE WRITE_SIZE; do
         run "traffic_${a1}_$k" 120 rocprofv3 --pmc $k -d "$O/traffic_$a1" -o "$k" --output-format csv -- \
-          python3 bench.py --config "$a1" ${a3:---steps,20,--warmup,3,--cpu-sample,0,--replicas,20}
+          python3 bench.py --config "$a1" ${x//,/ }
       done
       run "traffic_${a1}_summary" 60 python3 scripts/pmc_summary.py --dir "$O/traffic_$a1" --kernel "$a2" \
-        --out "perf/pmc_traffic_$a1.json" ;;
+        --out "$O/pmc_traffic_$a1.json" ;;  # copy into perf/ (bench.py reads it there) after the call
     ranks)
       KPE_DIST_BACKEND=gloo run "ranks_$a1" 400 python bench.py --gpus "$a1" ${a2//,/ }
       grep '^{' "$O/ranks_$a1.log" > "$O/ranks_$a1.json" ;;

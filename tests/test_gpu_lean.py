@@ -158,3 +158,106 @@ def test_lean6_batch_tiles_per_wave(engine):
     engine.device.sync()
     got, _, _ = engine.fetch(ps, c)
     assert np.array_equal(got, want)
+
+
+def lean_stress_ndjson(n, seed, unique_strings=True):
+    """Pods that take every slow path of kpe_lean6_kernel: 1-12 containers (tiles past the 128
+    staged containers, pods past the 4 clamped reads), 0-9 volumes, 0-4 sysctls and 1-7
+    annotations per pod (past the 2 clamped reads and the 64 staged items), and, with
+    unique_strings, a distinct annotation key / value and sysctl name per pod (code tables too large
+    for the LDS: the global-code instantiation)."""
+    import json
+    import random
+
+    rnd = random.Random(seed)
+    caps = ["NET_BIND_SERVICE", "CHOWN", "SYS_ADMIN", "ALL", "NET_RAW", "KILL"]
+    sec = [None, "RuntimeDefault", "Localhost", "Unconfined", "Bogus"]
+    srcs = [("configMap", {"name": "c"}), ("emptyDir", {}), ("hostPath", {"path": "/x"}), ("nfs", {"server": "s", "path": "/"}),
+            ("secret", {"secretName": "s"}), ("csi", {"driver": "d"}), ("gitRepo", {"repository": "r"}), ("projected", {"sources": []})]
+    sysctls = ["kernel.shm_rmid_forced", "net.ipv4.ip_local_port_range", "kernel.msgmax", "net.ipv4.tcp_keepalive_time",
+               "net.ipv4.ip_local_reserved_ports", "vm.swappiness"]
+    aa = ["runtime/default", "localhost/p", "unconfined"]
+    sva = ["runtime/default", "docker/default", "localhost/p", "unconfined"]
+    out = []
+    for i in range(n):
+        ctrs = []
+        for k in range(1 + rnd.randrange(12)):
+            sc = {}
+            if rnd.random() < 0.8:
+                if rnd.random() < 0.5:
+                    sc["allowPrivilegeEscalation"] = rnd.random() < 0.2
+                if rnd.random() < 0.1:
+                    sc["privileged"] = True
+                if rnd.random() < 0.6:
+                    sc["capabilities"] = {"drop": rnd.sample(caps, rnd.randrange(3)), "add": rnd.sample(caps, rnd.randrange(2))}
+                if rnd.random() < 0.5:
+                    sc["runAsNonRoot"] = rnd.random() < 0.8
+                s = rnd.choice(sec)
+                if s:
+                    sc["seccompProfile"] = {"type": s}
+                if rnd.random() < 0.05:
+                    sc["procMount"] = "Unmasked"
+            c = {"name": f"c{k}", "image": "nginx:1.0", "securityContext": sc}
+            if rnd.random() < 0.05:
+                c["ports"] = [{"containerPort": 80, "hostPort": 8080}]
+            ctrs.append(c)
+        vols = [{"name": f"v{k}", src: dict(body)} for k, (src, body) in
+                enumerate(rnd.choice(srcs) for _ in range(rnd.randrange(10)))]
+        ann = {f"note-{i}" if unique_strings else "note": f"v-{i}" if unique_strings else "v"}
+        for k in range(rnd.randrange(7)):
+            r = rnd.random()
+            if r < 0.3:
+                ann[f"container.apparmor.security.beta.kubernetes.io/c{k}"] = rnd.choice(aa)
+            elif r < 0.6:
+                ann[f"container.seccomp.security.alpha.kubernetes.io/c{k}"] = rnd.choice(sva)
+            elif r < 0.7:
+                ann["seccomp.security.alpha.kubernetes.io/pod"] = rnd.choice(sva)
+            else:
+                ann[f"extra-{k}"] = f"x{rnd.randrange(5)}"
+        spec = {"containers": ctrs, "volumes": vols}
+        psc = {}
+        if rnd.random() < 0.4:
+            names = rnd.sample(sysctls, rnd.randrange(5))
+            if unique_strings and rnd.random() < 0.5:
+                names.append(f"net.custom.knob{i}")
+            psc["sysctls"] = [{"name": nm, "value": "1"} for nm in names]
+        if rnd.random() < 0.3:
+            psc["runAsNonRoot"] = True
+        if rnd.random() < 0.3:
+            psc["seccompProfile"] = {"type": "RuntimeDefault"}
+        if psc:
+            spec["securityContext"] = psc
+        out.append({"apiVersion": "v1", "kind": "Pod",
+                    "metadata": {"name": f"st-{i}", "namespace": "default", "annotations": ann}, "spec": spec})
+    return "\n".join(json.dumps(o, separators=(",", ":")) for o in out).encode()
+
+
+@pytest.mark.parametrize("unique", [False, True], ids=["lds-codes", "global-codes"])
+def test_lean6_slow_paths(engine, oracle, unique):
+    """Long lists and large dictionaries: every overflow path of kpe_lean6_kernel, and the
+    instantiation that reads the code bytes from global memory, bit-exact with the oracle (verdicts
+    and check masks) at three level / version pairs, single-shard and multi-shard launches."""
+    nd = lean_stress_ndjson(12000, 0x5E + unique, unique_strings=unique)
+    c = K.Corpus(nd, docs=False).upload(engine.device)
+    c2 = K.Corpus(nd, docs=False).upload(engine.device)
+    for level, ver in (("restricted", "latest"), ("baseline", "v1.0"), ("restricted", "v1.25")):
+        pol = pss_policy(f"{level}-{ver.replace('.', '-')}", level, ver)
+        ps = K.PolicySet([pol])
+        ref = oracle.validate([pol], nd, nthreads=8)
+        engine.device.set_timing(True)
+        engine.device.kernel_stats(reset=True)
+        v, _, _ = engine.evaluate(ps, c, check_masks=True)
+        st = engine.device.kernel_stats(reset=True)
+        engine.device.set_timing(False)
+        assert st.scan_kernel == LEAN6, st.scan_kernel
+        bad = np.argwhere(v != ref)
+        assert bad.size == 0, (level, ver, len(bad), bad[:5].tolist())
+        want_row = oracle.failing_cv_batch(level, ver, nd)
+        want = np.where(v == 2, np.maximum(want_row, 0)[:, None], 0).astype(np.int64)
+        assert np.array_equal(engine.cv_masks(ps, c).astype(np.int64), want), (level, ver)
+        engine.evaluate(ps, c2)
+        engine.evaluate_batch_async(ps, [c, c2, c])
+        engine.device.sync()
+        for cc in (c, c2):
+            vb, _, _ = engine.fetch(ps, cc)
+            assert np.array_equal(vb, ref), (level, ver)
