@@ -493,18 +493,24 @@ struct CondVM {
     return CS_OK;
   }
   // A condition key / value after substitution (template `ti`); lists go to buffer bl. One
-  // query() call site: a single query is a one-element template walk that returns its value.
+  // query() call site: a single query is a one-element template walk that returns its value. A
+  // string with variables inside it (alone, or the one such element of a list: program.cpp
+  // CondCompiler::tmpl) is built in the side's lane text slot (key 0, value 1).
   __device__ __forceinline__ int value(uint32_t ti, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
     const KpeVTmpl t = a.tmpls[ti];
-    if (t.kind == VT_TMPL) return substitute(t, b0, b1, b0 == 3u ? 1u : 0u, out);
+    const uint32_t slot = b0 == 3u ? 1u : 0u;
+    if (t.kind == VT_TMPL) return substitute(t, b0, b1, slot, out);
     const bool arr = t.kind == VT_ARRAY;
     const uint32_t n = arr ? t.b : 1u;
     blen[bl] = 0;
-    for (uint32_t k = 0; k < n; ++k) {  // list elements: constants or queries (no nested lists)
+    for (uint32_t k = 0; k < n; ++k) {  // list elements: constants, queries or one template
       const KpeVTmpl te = arr ? a.tmpls[t.a + k] : t;
       CV x;
       if (te.kind == VT_CONST) {
         x = SC_TYPE(a.ctab[te.a].flags) == SC_T_NULL ? cv(VK_NULL, 0) : cv(VK_CONST, te.a);
+      } else if (te.kind == VT_TMPL) {
+        const int st = substitute(te, b0, b1, slot, &x);
+        if (st != CS_OK) return st;
       } else {
         const int st = query(te.a, b0, b1, &x);
         if (st != CS_OK) return st;

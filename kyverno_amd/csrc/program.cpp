@@ -1545,7 +1545,9 @@ class CondCompiler {
         if (q == "@" || q.find("{{") != std::string::npos) throw CompileError("{{@}} / nested variables");
         t.kind = VT_QUERY, t.a = Q.compile(q);
       } else {  // variables inside a string (vars.go:311-389): text and variable pieces
-        if (depth > 0) throw CompileError("partial-string variables inside a condition list");
+        // a list element is substituted into the side's one lane text slot (condvm.inl value())
+        if (depth > 0 && ++list_tmpls_ > 1)
+          throw CompileError("more than one partial-string variable element in a condition list");
         if (v.s.find("\\{{") != std::string::npos) throw CompileError("escaped variables in conditions");
         t.kind = VT_TMPL, t.a = (uint32_t)CP.tpieces.size() / 2;
         auto text = [&](size_t b, size_t e) {
@@ -1571,6 +1573,7 @@ class CondCompiler {
       }
     } else if (v.t == JV::Arr && depth == 0 && has_var(v)) {
       std::vector<uint32_t> el;
+      list_tmpls_ = 0;
       for (auto& x : v.a) {
         if (x.t == JV::Arr || x.t == JV::Obj) throw CompileError("nested lists with variables");
         el.push_back(tmpl(x, 1));
@@ -1675,6 +1678,7 @@ class CondCompiler {
   CondProgram& CP;
   Consts K;
   QueryParser Q;
+  uint32_t list_tmpls_ = 0;  // partial-string elements of the list being compiled
   static bool has_var(const JV& v) {
     size_t a, b;
     if (v.t == JV::Str) return next_var(v.s, 0, &a, &b);

@@ -632,6 +632,10 @@ typedef struct KpeCond {
 #ifndef KPE_PAT_MEMO
 #define KPE_PAT_MEMO 16
 #endif
+// the pattern kernel keeps the memo slots' valid bits in one 32-bit word (patvm.inl memo_ok)
+#if KPE_PAT_MEMO > 32
+#error "KPE_PAT_MEMO must be <= 32"
+#endif
 typedef struct KpePatRule {
   uint32_t col, flags, r0, nr;
 } KpePatRule;

@@ -279,6 +279,11 @@ def cond_policy_set():
         rule("ports-first", deny(c("{{ " + obj + ".spec.containers[0].ports[0].containerPort || `0` }}", "Equals",
                                    "8080"))),
         rule("ns-list-key", deny(c(["{{ " + obj + ".metadata.namespace }}"], "NotIn", ["ns-0001", "ns-0002"]))),
+        # a string with a variable inside it as one element of a list (value side, then key side)
+        rule("list-tmpl-value", deny(c("{{ " + obj + ".metadata.name }}", "AnyIn",
+                                       ["{{ " + obj + ".metadata.namespace }}-x", "res-1*", "web"]))),
+        rule("list-tmpl-key", deny(c(["{{ " + obj + ".metadata.namespace }}/{{ " + obj + ".metadata.name }}",
+                                      "{{ " + obj + ".kind }}"], "AnyIn", ["ns-000?/res-2*", "Service"]))),
         rule("vol-keys", deny(c("{{ " + obj + ".spec.volumes[].keys(@)[] || '' }}", "AnyNotIn",
                                 ["name", "configMap", "emptyDir", ""]))),
         rule("caps-add", deny(c("{{ " + obj + ".spec.[ephemeralContainers, initContainers, containers][]."
