@@ -1214,6 +1214,10 @@ struct FeFrame {
 // A resolved pattern variable (kpe_pattern_kernel reads it): 0 ok, else the cell's verdict
 __device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, uint2* dst) {
   const uint32_t t = vm.type(x);
+  if (flags & PVF_KEY) {  // a whole-string variable naming a map key (traverse.go:90-117)
+    if (t == JT_NULL) return KPE_UNDECIDED_;  // the key stays as written
+    if (t != JT_STR) return KPE_ERROR_;       // "expected string after substituting variables in key"
+  }
   if (t == JT_NULL) {
     *dst = make_uint2(PVK_NULL, 0u);
     return 0u;

@@ -314,7 +314,11 @@ struct PatArgs {
   // ltab[slot * ltab_words ...] is pattern.Validate of scalar sid against it. Null: no table.
   const uint32_t* lslot;
   uint32_t* ltab;
-  uint32_t ltab_words, pad3_;
+  uint32_t ltab_words, nkeyd;  // nkeyd: strings of the member-name dictionary (D_KEY)
+  // the member-name dictionary (D_KEY): keys named by substituted key templates (PMF_VKEY) are
+  // looked up by text
+  const uint8_t* key_bytes;
+  const uint32_t* key_off;
   // table sizes and an error word: read only by KPE_PATVM_CHECK builds (bounds flags)
   uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
   uint64_t nscal, ndoc;

@@ -1055,7 +1055,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     for (size_t i = 0; i < PP.keys.size(); ++i) kid[i] = C.dict[D_KEY].find(PP.keys[i]);
     std::vector<uint32_t> mem(PP.members);
     for (size_t i = 0; i < mem.size(); i += 4) {
-      mem[i + 1] = kid[mem[i + 1]] < 0 ? 0u : (uint32_t)kid[mem[i + 1]] + 1u;
+      mem[i + 1] = kid[mem[i + 1]] < 0 || (mem[i] & PMF_VKEY) ? 0u : (uint32_t)kid[mem[i + 1]] + 1u;
       if (mem[i] & PMF_GLOB) mem[i + 3] = loc((int32_t)mem[i + 3]);
     }
     HIPCHK(upload(B.pmembers, mem, s));
@@ -1416,6 +1416,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.lslot = PD.plslot.as<uint32_t>();
       pa.ltab = PD.nlslots ? B.ltab.as<uint32_t>() : nullptr;
       pa.ltab_words = B.ltab_words;
+      pa.key_bytes = D.dict_bytes[D_KEY].as<uint8_t>(), pa.key_off = D.dict_off[D_KEY].as<uint32_t>();
+      pa.nkeyd = C.dict[D_KEY].size();
       pa.nnodes = (uint32_t)P.pat.nodes.size(), pa.nmembers = (uint32_t)(P.pat.members.size() / 4);
       pa.nlists = (uint32_t)P.pat.lists.size(), pa.nleaves = (uint32_t)P.pat.leaves.size();
       pa.nconds = (uint32_t)P.pat.conds.size(), pa.npats = (uint32_t)P.pat.operands.size();
@@ -2007,6 +2009,7 @@ static bool trace_path(const kpe::Program& P, const kpe::Corpus* C, const uint32
       p += std::string(C->dict[D_KEY].at(id));
     } else {
       if ((size_t)c * 4 + 1 >= P.pat.members.size()) return false;
+      if (P.pat.members[(size_t)c * 4] & PMF_VKEY) return false;  // an absent substituted key: no text kept
       const uint32_t ki = P.pat.members[(size_t)c * 4 + 1];
       if (ki >= P.pat.keys.size()) return false;
       p += P.pat.keys[ki];

@@ -290,6 +290,78 @@ __device__ __forceinline__ bool pat_var_star(const PatArgs& a, uint32_t li, cons
   return tmpl_pieces(a, L, pv, pc) == 1 && tp_at(pc, np, 0) == '*';
 }
 
+// PMF_VKEY: the member of resource map m named by the row's substituted key template (leaf li),
+// kNoNode if absent. *und is set where the device does not follow the reference: a substituted
+// key that parses as an anchor (anchor.Parse: TrimSpace, then `^([+<=X^])?\((.+)\)$`), that
+// equals another key of the map (a rename onto it, traverse.go:108-114, depends on Go's map
+// order), that holds a glob under ExpandInMetadata, or (ORDER: the failure-path walk) that sorts
+// to another place among the map's plain keys than the compiled walk order gives it.
+template <bool ORDER>
+__device__ __forceinline__ uint32_t pat_lookup_vkey(const PatArgs& a, DocView doc, uint32_t m, uint32_t li,
+                                                    const uint2* pv, uint32_t* und) {
+  const KpeLeaf L = PU(a.leaves, li, a.nleaves, 4);
+  TPiece pc[kTPieces];
+  int np = 1, n;
+  if (L.type == PL_VAR) {  // a string (kpe_cond_kernel: PVF_KEY)
+    const uint8_t* tb;
+    const KpeScalar* s = pv_scalar(a, pv[L.c0], &tb);
+    pc[0] = TPiece{tb + s->text_off, (int)s->text_len, 0u};
+    n = (int)s->text_len;
+  } else {
+    np = (int)(L.nc < (uint32_t)kTPieces ? L.nc : (uint32_t)kTPieces);
+    n = tmpl_pieces(a, &L, pv, pc);
+  }
+  // anchor.Parse of the substituted key
+  int b = 0, e = n;
+  auto ws = [](uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); };
+  while (b < e && ws(tp_at(pc, np, b))) ++b;
+  while (e > b && ws(tp_at(pc, np, e - 1))) --e;
+  if (e - b >= 3 && tp_at(pc, np, e - 1) == ')') {
+    const uint8_t c0 = tp_at(pc, np, b);
+    const bool mod = c0 == '+' || c0 == '<' || c0 == '=' || c0 == 'X' || c0 == '^';
+    if (c0 == '(' || (mod && e - b >= 4 && tp_at(pc, np, b + 1) == '(')) {
+      *und = 1u;
+      return kNoNode;
+    }
+  }
+  if (L.bval) {  // ExpandInMetadata target: a substituted glob would be expanded
+    for (int i = 0; i < n; ++i) {
+      const uint8_t c = tp_at(pc, np, i);
+      if (c == '*' || c == '?') {
+        *und = 1u;
+        return kNoNode;
+      }
+    }
+  }
+  // Go string order against the neighbours: -1 / 0 / 1
+  auto cmp = [&](const uint8_t* t, int tn) -> int {
+    for (int i = 0; i < n && i < tn; ++i) {
+      const uint8_t x = tp_at(pc, np, i);
+      if (x != t[i]) return x < t[i] ? -1 : 1;
+    }
+    return n == tn ? 0 : (n < tn ? -1 : 1);
+  };
+  const uint8_t* sib = a.ttext + L.pad[0];
+  const uint32_t nsib = L.pad[1] & 0xFFFFu, at = L.pad[1] >> 16;
+  for (uint32_t k = 0; k < nsib; ++k) {
+    const int tn = (int)sib[0] | (int)sib[1] << 8;
+    const int c = cmp(sib + 2, tn);
+    if (c == 0 || (ORDER && (k < at ? c < 0 : c > 0))) {
+      *und = 1u;
+      return kNoNode;
+    }
+    sib += 2 + tn;
+  }
+  PV_KIDS(m, c0, end);
+  for (uint32_t c = c0; c < end; ++c) {
+    const uint32_t k1 = DN_KEY(doc[PVD(c)].x);
+    if (!k1 || k1 > a.nkeyd) continue;
+    const uint32_t o0 = a.key_off[k1 - 1u], o1 = a.key_off[k1];
+    if ((int)(o1 - o0) == n && cmp(a.key_bytes + o0, n) == 0) return c;
+  }
+  return kNoNode;
+}
+
 __device__ __forceinline__ bool leaf_float(const KpeScalar* v, uint32_t vf, double pf) {  // validateFloatPattern
   const uint32_t t = SC_TYPE(vf);
   if (t == SC_T_INT) return pf == trunc(pf) && go_f2i(pf) == v->ival;
@@ -514,11 +586,18 @@ struct PatVMT {
   // name) or an array index.
   __device__ __forceinline__ uint32_t mcomp(uint32_t r, uint32_t mi) {
     const uint4 m = PU(a.members, mi, a.nmembers, 2);
-    if (m.x & PMF_GLOB) {
-      const uint32_t c = pat_lookup_glob(a, doc, r, m.w);
+    if (m.x & (PMF_GLOB | PMF_VKEY)) {  // the resource member's name (a VKEY member found by it)
+      const uint32_t c = lookup<true>(m, r);
       if (c != kNoNode) return KPE_TC_KEY | (DN_KEY(doc[PVD(c)].x) - 1u);
     }
-    return mi;
+    return mi;  // an absent VKEY member: the host renders no path for it
+  }
+  // the resource member a pattern member names (kNoNode: absent); TRACE: failure-path walks
+  template <bool TRACE>
+  __device__ __forceinline__ uint32_t lookup(const uint4& m, uint32_t r) {
+    if (m.x & PMF_GLOB) return pat_lookup_glob(a, doc, r, m.w);
+    if (m.x & PMF_VKEY) return pat_lookup_vkey<TRACE>(a, doc, r, m.w, pv, &und);
+    return pat_lookup(a, doc, r, m.y);
   }
   __device__ __forceinline__ void tput(uint32_t& n, uint32_t c) {
     if (n < KPE_TRACE_WORDS - 1u) tr[1u + n] = c;
@@ -671,8 +750,7 @@ struct PatVMT {
               if (m.x & PMF_SLOT) {
                 const uint32_t bit = 1u << PM_SLOT(m.x);
                 reg |= bit;  // a glob key counts under its expansion (ExpandInMetadata ran first)
-                if (((m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, br, m.w) : pat_lookup(a, doc, br, m.y)) != kNoNode)
-                  val |= bit;
+                if (lookup<TRACE>(m, br) != kNoNode) val |= bit;
               }
             }
             v = push(PF_MAP, br, bpi, 0u);
@@ -739,7 +817,7 @@ struct PatVMT {
             } else {
               const uint4 m = PU(a.members, m0 + k, a.nmembers, 2);
               const uint32_t h = PM_HANDLER(m.x);
-              const uint32_t c = (m.x & PMF_GLOB) ? pat_lookup_glob(a, doc, F.r, m.w) : pat_lookup(a, doc, F.r, m.y);
+              const uint32_t c = lookup<TRACE>(m, F.r);
               if (h == PM_NEG) {
                 e = c == kNoNode ? PE_OK : PE_NEG;
                 if (TRACE && e == PE_NEG) snap(sp, mcomp(F.r, m0 + k));

@@ -669,6 +669,8 @@ class PatCompiler {
   // Strings with {{ }} variables (substitutePatterns, validate_resource.go:456-476): fills a
   // PL_VAR / PL_TMPL leaf and returns true; false for a plain string
   std::function<bool(const std::string&, KpeLeaf&)> var_leaf;
+  // A map key with {{ }} variables (jsonutils/traverse.go:90-117): its template leaf (PMF_VKEY)
+  std::function<bool(const std::string&, KpeLeaf&)> key_leaf;
 
   // one root (validate.MatchPattern call); returns the root table index
   uint32_t root(const JV& pattern) {
@@ -815,10 +817,19 @@ class PatCompiler {
           }
     const bool expanding = expand_.count(&v) > 0;
     std::vector<std::string> first, front, back;
+    std::string vkey;  // the map's one key with variables, if any
     for (auto& kv : v.o) {
       const Anc a = anchor_of(kv.first);
-      if (kv.first.find("{{") != std::string::npos || kv.first.find("$(") != std::string::npos)
-        throw CompileError("variables in pattern keys are not supported on the device");
+      if (kv.first.find("$(") != std::string::npos)
+        throw CompileError("$(...) references in pattern keys are not supported on the device");
+      if (kv.first.find("{{") != std::string::npos) {
+        if (!key_leaf) throw CompileError("variables in pattern keys are not supported here");
+        if (a.k != AK_NONE) throw CompileError("anchored pattern keys with variables are not supported");
+        if (!vkey.empty()) throw CompileError("more than one pattern key with variables in one map");
+        if (expanding && has_glob(kv.first)) throw CompileError("wildcard metadata keys with variables");
+        if (expanding && repeated) throw CompileError("metadata keys with variables under an array pattern");
+        vkey = kv.first;
+      }
       if (expanding && has_glob(kv.first) && repeated)  // the reference rewrites the shared pattern per element
         throw CompileError("wildcard metadata keys under an array pattern are not supported");
       if (phase1(a.k)) first.push_back(kv.first);
@@ -844,7 +855,12 @@ class PatCompiler {
     std::vector<std::string> rest;
     for (auto& kv : v.o)
       if (!phase1(anchor_of(kv.first).k)) rest.push_back(kv.first);
-    std::sort(rest.begin(), rest.end());
+    // a key with variables takes the place of its text before the first variable (any place is
+    // correct: the device checks per row that the substituted key sorts between the same
+    // neighbours, else the cell is undecided)
+    auto sort_text = [&](const std::string& k) { return k == vkey ? k.substr(0, k.find("{{")) : k; };
+    std::sort(rest.begin(), rest.end(),
+              [&](const std::string& x, const std::string& y) { return sort_text(x) < sort_text(y); });
     for (auto& k : rest) {
       if (anchor_of(k).k == AK_GLOBAL || nested_anchor(*v.get(k.c_str()))) front.insert(front.begin(), k);
       else back.push_back(k);
@@ -875,6 +891,34 @@ class PatCompiler {
         else flags |= PMF_XSLOT;
       }
       if (h == PM_DEFAULT && val.t == JV::Str && val.s == "*") flags |= PMF_STAR;
+      if (k == vkey) {
+        // validateMap walks the plain keys without nested anchors in sorted order and returns the
+        // first error; such members can only fail plainly, so the verdict does not depend on where
+        // the substituted key sorts (only the failure path of a message does: checked per row by
+        // the trace walk). A key whose value holds anchors would move among members that skip.
+        if (nested_anchor(val)) throw CompileError("a pattern key with variables whose value holds anchors");
+        KpeLeaf kl{};
+        if (!key_leaf(k, kl)) throw CompileError("pattern key template");
+        kl.bval = expanding ? 1u : 0u;
+        // the map's other plain keys in walk order, [u16 length][bytes] each, and this key's place
+        kl.pad[0] = (uint32_t)PP.ttext.size();
+        uint32_t nsib = 0, at = 0;
+        for (auto& t : rest) {
+          if (t == k) {
+            at = nsib;
+            continue;
+          }
+          if (t.size() >= 0xFFFFu) throw CompileError("pattern key longer than 64 KiB");
+          PP.ttext.push_back((uint8_t)(t.size() & 0xFF)), PP.ttext.push_back((uint8_t)(t.size() >> 8));
+          PP.ttext.insert(PP.ttext.end(), t.begin(), t.end());
+          ++nsib;
+        }
+        if (nsib > 0xFFFFu) throw CompileError("pattern map with too many keys");
+        kl.pad[1] = nsib | at << 16;
+        PP.leaves.push_back(kl);
+        flags |= PMF_VKEY;
+        w = (uint32_t)PP.leaves.size() - 1;
+      }
       if (expanding && has_glob(k) && a.k != AK_ADD) {  // "+(...)" keys stay verbatim
         flags |= PMF_GLOB;
         w = (uint32_t)key_pred_(name);
@@ -909,7 +953,7 @@ class PatCompiler {
     uint32_t depth_in = order.size() <= 8 ? 1u : 0u;  // inline depth (schema.h PNF_FLAT)
     for (size_t i = 0; i < mem.size() && depth_in; i += 4) {
       const uint32_t x = mem[i], h = PM_HANDLER(x);
-      if (h == PM_EXIST || (x & (PMF_GLOB | PMF_XSLOT))) {
+      if (h == PM_EXIST || (x & (PMF_GLOB | PMF_XSLOT | PMF_VKEY))) {
         depth_in = 0;
       } else if (h != PM_NEG && !(x & (PMF_STAR | PMF_LEAF))) {  // a map (or list) value
         const KpePNode& c = PP.nodes[mem[i + 2]];
@@ -1706,6 +1750,7 @@ class Lowerer {
       return pcomp.leaf(JV::str(text));
     };
     var_leaf_ = [this](const std::string& s, KpeLeaf& l) { return var_leaf(s, l); };
+    key_leaf_ = [this](const std::string& s, KpeLeaf& l) { return var_leaf(s, l, PVF_KEY); };
   }
   // validate.foreach entries of one level (newForEachValidator, validate_resource.go:76-119);
   // nested levels are appended first, so each level's entries are contiguous. Returns the first.
@@ -1734,6 +1779,7 @@ class Lowerer {
           return id;
         });
         pcomp.var_leaf = var_leaf_;
+        pcomp.key_leaf = key_leaf_;
         const uint32_t pv0 = (uint32_t)P.pat.vars.size();
         f.a = (uint32_t)(P.pat.roots.size() / 2);
         uint32_t nr = 0, flags = 0;
@@ -1780,7 +1826,7 @@ class Lowerer {
   // whole-string variable keeps the value's JSON type (PL_VAR); otherwise the variables'
   // texts are spliced into the string (PL_TMPL: substituteVarInPattern). Each variable is a
   // query of the condition program, resolved per row by kpe_cond_kernel.
-  bool var_leaf(const std::string& s, KpeLeaf& l) {
+  bool var_leaf(const std::string& s, KpeLeaf& l, uint32_t key_flags = 0) {
     if (s.find("$(") != std::string::npos) throw CompileError("$(...) references in patterns are not supported");
     size_t st, en;
     if (!cq::next_var(s, 0, &st, &en)) return false;  // no complete {{ }}: a plain string
@@ -1795,7 +1841,7 @@ class Lowerer {
     };
     if (st == 0 && en == s.size()) {
       l.type = PL_VAR;
-      l.c0 = slot(s, PVF_WHOLE);
+      l.c0 = slot(s, key_flags ? key_flags : PVF_WHOLE);
       return true;
     }
     l.type = PL_TMPL;
@@ -2381,6 +2427,7 @@ class Lowerer {
           return id;
         });
         pcomp.var_leaf = var_leaf_;
+        pcomp.key_leaf = key_leaf_;
         crule.pv0 = (uint32_t)P.pat.vars.size();
         KpePatRule pr{(uint32_t)P.rules.size(), 0, (uint32_t)(P.pat.roots.size() / 2), 0};
         try {
@@ -2706,7 +2753,7 @@ class Lowerer {
 
   Program& P;
   cq::CondCompiler CC;
-  std::function<bool(const std::string&, KpeLeaf&)> var_leaf_;
+  std::function<bool(const std::string&, KpeLeaf&)> var_leaf_, key_leaf_;
   struct RuleInfo {
     bool pre_dyn, has_validate;
     std::string name;
@@ -2872,9 +2919,10 @@ void go_json(std::string& o, const JV& v) {
 }
 
 // A `request.object...` JMESPath over the resource: identifiers, "quoted" identifiers and [N]
-// (negative from the end). In a chain of members only, a member missing from an object is the
-// kyverno go-jmespath fork's NotFoundError (*missing: SubstituteAll fails); otherwise, and for a
-// member of a non-object or an index past a list, the value is null. false: not this grammar.
+// (negative from the end). A member missing from an object is the kyverno go-jmespath fork's
+// NotFoundError (*missing: SubstituteAll fails) in this chain of member / index accesses, as in
+// kpe_cond_kernel's queries and the oracle's plain chains; a member of a non-object or an index
+// past a list is null. false: not this grammar.
 bool object_path(const std::string& q, const JV& res, const JV** out, bool* missing) {
   *missing = false;
   static const JV kNull;
@@ -2927,7 +2975,7 @@ bool object_path(const std::string& q, const JV& res, const JV** out, bool* miss
     }
     if (!cur) cur = nullptr;
   }
-  if (indexed) *missing = false;  // not a plain member chain
+  (void)indexed;
   *out = cur ? cur : &kNull;
   return true;
 }

@@ -565,6 +565,11 @@ typedef struct KpePNode {
 #define PM_SLOT(x) (((x) >> 8) & 31u)
 #define PMF_XSLOT (1u << 13)  // condition / existence anchor past the 32 AnchorMap slots: a map
                               // holding it makes the cell KPE_UNDECIDED
+#define PMF_VKEY (1u << 14)   // a plain key with {{ }} variables (substitutePatterns renames it per
+                              // row, jsonutils/traverse.go:90-117): w = the key's template leaf
+                              // (PL_VAR / PL_TMPL; bval 1: under ExpandInMetadata; pad[0] = template-
+                              // text offset of the map's other plain keys in walk order, [u16 length]
+                              // [bytes] each; pad[1] = their count | this key's place << 16)
 // Leaf
 #define PL_BOOL 0u
 #define PL_INT 1u
@@ -588,6 +593,8 @@ typedef struct KpePNode {
 // Pattern variable slot: the query template (condition program) and how the pattern uses it
 #define PVF_WHOLE 1u  // a whole-string leaf: a string value must be SC_PSIMPLE
 #define PVF_TEXT 2u   // inside a template: numbers must print as json.Marshal does
+#define PVF_KEY 4u    // a whole-string variable naming a map key: a string (traverse.go:101-103:
+                      // another type is an error; null keeps the key as written: undecided)
 typedef struct KpePVar {
   uint32_t tmpl, flags;
 } KpePVar;

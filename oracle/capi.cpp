@@ -183,6 +183,25 @@ int oracle_substitute(const char* resource_json, const char* msg, char* buf, siz
   }
 }
 
+// variables.SubstituteAll of a JSON document (vars.go:311-313 OnlyForLeafsAndKeys: every leaf
+// and every map key, jsonutils/traverse.go:64-130) over one resource's background-scan context:
+// 0 the substituted document's JSON in buf, -1 a substitution error, -2 outside the restatement.
+int oracle_substitute_doc(const char* resource_json, const char* doc_json, char* buf, size_t cap) {
+  try {
+    JPtr res = parse_json(resource_json);
+    cond::Ctx cx{cond::request_context(*res)};
+    const JPtr r = cond::substitute(parse_json(doc_json), cx);
+    snprintf(buf, cap, "%s", cond::json_marshal(r).c_str());
+    return 0;
+  } catch (const cond::EvalError&) {
+    return -1;
+  } catch (const cond::Unsupported&) {
+    return -2;
+  } catch (...) {
+    return -1;
+  }
+}
+
 int oracle_pss_message(const char* rule, const char* level, const char* version, const char* resource_json, char* buf,
                        size_t cap) {
   try {

@@ -578,10 +578,12 @@ class Parser {
   }
 };
 
-// A plain chain of field / index accesses from the root (where NotFoundError is raised).
+// A plain chain of field / index accesses from the root (where NotFoundError is raised). The
+// parser binds an index to the field before it (`a.b[0].c` = SUB(SUB(a, INDEX(b, 0)), c)), so
+// the right side of a SUB is a field or an indexed field.
 inline bool plain_chain(const Node& n) {
   if (n.t == N_FIELD) return true;
-  if (n.t == N_SUB) return plain_chain(*n.k[0]) && (n.k[1]->t == N_FIELD);
+  if (n.t == N_SUB) return plain_chain(*n.k[0]) && plain_chain(*n.k[1]);
   if (n.t == N_INDEX) return plain_chain(*n.k[0]);
   return false;
 }
@@ -892,19 +894,38 @@ inline JPtr substitute_string(const std::string& in, const Ctx& c) {
 }
 inline JPtr substitute(const JPtr& v, const Ctx& c) {
   if (is_null(v)) return v;
-  if (v->t == JT::Str) return substitute_string(v->s, c);
+  if (v->t == JT::Str) {  // a JSON null result as a node (substituted trees are walked as documents)
+    JPtr r = substitute_string(v->s, c);
+    if (!r) {
+      r = std::make_shared<JVal>();
+      r->t = JT::Null;
+    }
+    return r;
+  }
   if (v->t == JT::Arr) {
     std::vector<JPtr> o;
     for (auto& e : v->a) o.push_back(substitute(e, c));
     return mk_arr(o);
   }
   if (v->t == JT::Obj) {
+    // jsonutils/traverse.go:90-117 traverseObject: every key goes through the action too
+    // (OnlyForLeafsAndKeys, vars.go:311-313); a nil result keeps the key, another non-string
+    // result is an error ("expected string after substituting variables in key"), a key that
+    // changed is renamed (a rename onto another key of the map depends on Go's map order: not
+    // restated)
     auto o = std::make_shared<JVal>();
     o->t = JT::Obj;
+    std::set<std::string> seen;
+    for (auto& kv : v->o) seen.insert(kv.first);
     for (auto& kv : v->o) {
       JPtr k = substitute_string(kv.first, c);
-      if (is_null(k) || k->t != JT::Str) throw Unsupported("non-string variable in a map key");
-      o->o.push_back({k->s, substitute(kv.second, c)});
+      std::string nk;
+      if (is_null(k)) nk = kv.first;
+      else if (k->t != JT::Str) throw EvalError{"expected string after substituting variables in key \"" + kv.first + "\""};
+      else nk = k->s;
+      if (nk != kv.first && seen.count(nk)) throw Unsupported("a substituted map key equal to another key of the map");
+      seen.insert(nk);
+      o->o.push_back({nk, substitute(kv.second, c)});
     }
     return o;
   }

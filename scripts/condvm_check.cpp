@@ -110,7 +110,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < mem.size(); ++i) {
     uint4 m{PP.members[4 * i], PP.members[4 * i + 1], PP.members[4 * i + 2], PP.members[4 * i + 3]};
     const int64_t id = K.find(PP.keys[m.y]);
-    m.y = id < 0 ? 0u : (uint32_t)id + 1u;
+    m.y = id < 0 || (m.x & PMF_VKEY) ? 0u : (uint32_t)id + 1u;
     if (m.x & PMF_GLOB) {
       const auto& pr = P->preds[m.w];
       m.w = (uint32_t)pbuf.size();
@@ -147,6 +147,7 @@ int main(int argc, char** argv) {
   pa.nleaves = (uint32_t)PP.leaves.size(), pa.nconds = (uint32_t)PP.conds.size(), pa.npats = (uint32_t)pp.size();
   pa.nroots = (uint32_t)PP.roots.size(), pa.npbuf = (uint32_t)pbuf.size(), pa.nscal = C.scal.size();
   pa.ndoc = C.doc.size() / 2, pa.err = &perr;
+  pa.key_bytes = kb.data(), pa.key_off = K.off.data(), pa.nkeyd = (uint32_t)K.size();
   a.pat = &pa, a.pvars = PP.vars.data(), a.pvals = pvals.data(), a.nvars = (uint32_t)PP.vars.size();
   char nb[2][16];
   std::vector<uint8_t> txt(2 * KPE_TXT_CAP);

@@ -92,7 +92,7 @@ int main(int argc, char** argv) {
   for (size_t i = 0; i < mem.size(); ++i) {
     uint4 m{PP.members[4 * i], PP.members[4 * i + 1], PP.members[4 * i + 2], PP.members[4 * i + 3]};
     const int64_t id = K.find(PP.keys[m.y]);
-    m.y = id < 0 ? 0u : (uint32_t)id + 1u;
+    m.y = id < 0 || (m.x & PMF_VKEY) ? 0u : (uint32_t)id + 1u;
     if (m.x & PMF_GLOB) {
       const auto& pr = P->preds[m.w];
       m.w = (uint32_t)pbuf.size();
@@ -129,6 +129,9 @@ int main(int argc, char** argv) {
   a.nleaves = (uint32_t)PP.leaves.size(), a.nconds = (uint32_t)PP.conds.size(), a.npats = (uint32_t)pats.size();
   a.nroots = (uint32_t)PP.roots.size(), a.npbuf = (uint32_t)pbuf.size(), a.nscal = scal.size();
   a.ndoc = C.doc.size() / 2, a.err = &err;
+  std::vector<uint8_t> kb(K.bytes.begin(), K.bytes.end());
+  kb.resize(kb.size() + 17, 0);
+  a.key_bytes = kb.data(), a.key_off = K.off.data(), a.nkeyd = (uint32_t)K.size();
   // kpe_pattern_kernel's lane body: the LDS frame stack (word-planar, lane 0 of a 64-lane plane;
   // an overflow of its KPE_PAT_LDS_STACK frames re-walks on the private stack) ...
   std::vector<uint8_t> lds_v(verdicts);

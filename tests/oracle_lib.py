@@ -28,6 +28,8 @@ class Oracle:
         L.oracle_pss_failing_cv.restype = ctypes.c_longlong
         L.oracle_substitute.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_substitute.restype = ctypes.c_int
+        L.oracle_substitute_doc.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_substitute_doc.restype = ctypes.c_int
         L.oracle_pss_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                           ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_rule_names.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
@@ -95,6 +97,13 @@ class Oracle:
         buf = ctypes.create_string_buffer(1 << 16)
         r = self.lib.oracle_substitute(json.dumps(resource).encode(), msg.encode(), buf, 1 << 16)
         return (r, buf.value.decode() if r >= 0 else None)
+
+    def substitute_doc(self, doc, resource):
+        """variables.SubstituteAll of a JSON document (leaves and map keys) over the resource's
+        context: (0, document) or (-1, None) an error, (-2, None) outside the restatement."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        r = self.lib.oracle_substitute_doc(json.dumps(resource).encode(), json.dumps(doc).encode(), buf, 1 << 16)
+        return (r, json.loads(buf.value.decode()) if r == 0 else None)
 
     def rule_names(self, policies):
         buf = ctypes.create_string_buffer(1 << 20)

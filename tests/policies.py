@@ -376,6 +376,15 @@ def var_policy_set():
         rule("v-map", {"pattern": {"spec": {"securityContext": "{{request.object.spec.securityContext}}"}}}),
         rule("v-len", {"pattern": {"spec": {"containers": [{"ports": [{"containerPort": "{{ length(request.object.spec.containers) }}"}]}]}}}),
         rule("v-len-pipe", {"pattern": {"metadata": {"labels": "{{ request.object.metadata.labels | length(@) }}"}}}),
+        # variables in map keys (jsonutils/traverse.go:90-117: keys are substituted and renamed)
+        rule("vk-default", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.kind || 'team'}}": "team-?"}}}}),
+        rule("vk-tmpl", {"pattern": {"metadata": {"labels": {"ti{{request.object.metadata.labels.zone || 'er'}}": "back*"}}}}),
+        rule("vk-own", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.tier}}": "*"}}}}),
+        rule("vk-order", {"pattern": {"metadata": {"labels": {"app": "?*", "{{request.object.metadata.labels.tier}}": "*",
+                                                              "zzz": "!x"}}}}),
+        rule("vk-collide", {"pattern": {"metadata": {"labels": {"app": "?*", "{{request.object.metadata.labels.kind || 'app'}}": "x"}}}}),
+        rule("vk-number", {"pattern": {"spec": {"{{request.object.spec.containers[0].ports[0].containerPort}}": "x"}}}),
+        rule("vk-spec", {"pattern": {"spec": {"{{request.object.metadata.labels.field || 'containers'}}": [{"name": "c-*"}]}}}),
         # foreach entries
         rule("fe-pat", {"foreach": [{"list": ctr, "pattern": {"securityContext": {"=(privileged)": False}}}]}),
         rule("fe-pat-var", {"foreach": [{"list": ctr, "pattern": {"name": "c-{{elementIndex}}"}}]}),
@@ -404,4 +413,4 @@ def var_policy_set():
 
 # rules of var_policy_set whose cells the device may leave KPE_UNDECIDED (a variable resolving
 # to a map is a pattern subtree; documented device limit)
-VAR_UNDECIDED_OK = {"v-map"}
+VAR_UNDECIDED_OK = {"v-map", "vk-collide"}  # vk-collide: a key renamed onto another key of the map

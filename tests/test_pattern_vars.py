@@ -51,7 +51,8 @@ def test_var_policy_set_compiles(oracle):
 
 
 @pytest.mark.parametrize("pattern", [
-    {"metadata": {"labels": {"{{request.object.metadata.name}}": "x"}}},  # a variable in a key
+    {"metadata": {"labels": {"=({{request.object.metadata.name}})": "x"}}},  # a variable in an anchored key
+    {"metadata": {"labels": {"{{request.object.metadata.name}}": "x", "{{request.object.kind}}": "y"}}},  # two
     {"metadata": {"name": "$(./namespace)"}},                              # a reference
     {"metadata": {"name": "{{ @ }}"}},                                     # {{@}}
     {"metadata": {"name": "{{ to_upper(request.object.metadata.name) }}"}},  # a function
@@ -104,3 +105,30 @@ def test_gpu_pattern_vars_bit_exact(oracle, mix, n, seed):
     bad = _check(v, ref, oracle.rule_names(pols))
     assert not bad, bad[:12]
     assert {1, 2, 4} <= set(np.unique(v).tolist())
+
+
+# pkg/engine/jsonutils/traverse_test.go's document (Test_TraverseLeafsCheckIfTheyHit: every leaf
+# and every key is visited once), with the variables moved into keys as well
+TRAVERSE_DOC = {
+    "kind": "{{request.object.metadata.name1}}",
+    "name": "ns-owner-{{request.object.metadata.name}}",
+    "data": {"rules": [{"apiGroups": ["{{request.object.metadata.name}}"], "resources": ["namespaces"], "verbs": ["*"]}]},
+    "{{request.object.metadata.name}}": {"ns-owner-{{request.object.metadata.name}}": "{{request.object.metadata.name}}"},
+}
+
+
+def test_oracle_substitutes_keys_and_leaves(oracle):
+    """SubstituteAll (vars.go:311-313: OnlyForLeafsAndKeys) renames map keys with variables
+    (traverse.go:90-117) and substitutes every leaf, nested ones included; a key variable that is
+    not a string is an error; a missing member is the fork's NotFoundError."""
+    res = {"apiVersion": "v1", "kind": "Pod", "metadata": {"name": "web", "name1": "Kind1"}}
+    st, doc = oracle.substitute_doc(TRAVERSE_DOC, res)
+    assert st == 0
+    assert doc == {"kind": "Kind1", "name": "ns-owner-web",
+                   "data": {"rules": [{"apiGroups": ["web"], "resources": ["namespaces"], "verbs": ["*"]}]},
+                   "web": {"ns-owner-web": "web"}}
+    st, _ = oracle.substitute_doc({"{{request.object.metadata.labels.n}}": "x"},
+                                  dict(res, metadata={"name": "a", "labels": {"n": 3}}))
+    assert st == -1  # "expected string after substituting variables in key"
+    st, _ = oracle.substitute_doc({"{{request.object.metadata.labels.n}}": "x"}, res)
+    assert st == -1  # Unknown key "labels"
