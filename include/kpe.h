@@ -223,7 +223,10 @@ int kpe_pss_num_checks(void);
  * masks): N x R uint32, bit v = PSA versioned check v failed (0 unless the cell is FAIL).
  * A rule pinned to a version runs every version of a check up to it
  * (pkg/pss/evaluate.go:51-66, evaluatePSS), so one check id can fail more than once;
- * kpe_pss_cv_check(v) is the check id index of versioned check v. */
+ * kpe_pss_cv_check(v) is the check id index of versioned check v. Bit 31 (KPE_CVM_XMATCH)
+ * of a FAIL cell of a rule with a podSecurity PolicyException: the exception matched the
+ * resource, so its exclusions shape the cell's fail message (kpe_report_results_msg). */
+#define KPE_CVM_XMATCH (1u << 31)
 kpe_status kpe_fetch_cv_masks(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint32_t* cv_masks);
 int kpe_pss_num_cv(void);
 int kpe_pss_cv_check(int v);

@@ -1753,7 +1753,7 @@ static const uint8_t kCvCheck[KPE_NUM_CV] = KPE_CV_CHECK_TABLE;
 // The scan kernel stores failing versioned checks; the public masks are per PSA check id.
 static void cv_to_check_masks(uint32_t* m, size_t cells) {
   for (size_t i = 0; i < cells; ++i) {
-    uint32_t f = m[i], c = 0;
+    uint32_t f = m[i] & KPE_CVM_CHECKS, c = 0;
     while (f) {
       c |= 1u << kCvCheck[__builtin_ctz(f)];
       f &= f - 1;
@@ -2108,9 +2108,18 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
       std::string msg;
       if (rr.pss && v == KPE_PASS) {
         msg = kpe::pss_pass_message(rr.rule);
-      } else if (rr.pss && v == KPE_FAIL && !rr.pss_excl && cv_mask_row && cv_mask_row[r]) {
+      } else if (rr.pss && v == KPE_FAIL && !rr.pss_excl && cv_mask_row && (cv_mask_row[r] & KPE_CVM_CHECKS)) {
         if (!pod_state) pod_state = kpe::typed_pod_view(resource_json, resource_len, &pod, &kind) ? 1 : -1;
-        if (pod_state > 0) msg = kpe::pss_fail_message(rr.rule, rr.pss_level, rr.pss_version, kind, pod, cv_mask_row[r]);
+        if (pod_state > 0)
+          msg = kpe::pss_fail_message(rr.rule, rr.pss_level, rr.pss_version, kind, pod, cv_mask_row[r] & KPE_CVM_CHECKS);
+      } else if (rr.pss && v == KPE_FAIL && rr.pss_excl && cv_mask_row) {
+        // the checks EvaluatePod's exclusions and, when it matched (KPE_CVM_XMATCH), the podSecurity
+        // PolicyException's leave (validate_pss.go:76-110)
+        if (!pod_state) pod_state = kpe::typed_pod_view(resource_json, resource_len, &pod, &kind) ? 1 : -1;
+        const bool xm = rr.pss_has_xexcl && (cv_mask_row[r] & KPE_CVM_XMATCH);
+        if (pod_state > 0)
+          msg = kpe::pss_fail_message_ex(rr.rule, rr.pss_level, rr.pss_version, kind, pod, rr.pss_cv, &rr.pss_excludes,
+                                         xm ? &rr.pss_xexcludes : nullptr);
       } else if (rr.pat_rule && traces && (v == KPE_FAIL || (v == KPE_PASS && rr.any_pattern))) {
         msg = pattern_message(P, corp ? corp->c.get() : nullptr, rr, v,
                               traces + r * (size_t)(KPE_TRACE_ROOTS * KPE_TRACE_WORDS), resource_json, resource_len);
@@ -2143,7 +2152,7 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
     o += '"';
     if (rr.scored) o += ",\"scored\":true";
     // results.go:114-129: failing check ids (one per failing versioned check), sorted
-    const uint32_t f = (rr.pss && v == KPE_FAIL && cv_mask_row) ? cv_mask_row[r] : 0u;
+    const uint32_t f = (rr.pss && v == KPE_FAIL && cv_mask_row) ? cv_mask_row[r] & KPE_CVM_CHECKS : 0u;
     if (f) {
       std::vector<std::string> ids;
       for (uint32_t b = f; b; b &= b - 1) ids.push_back(kCheckIds[kCvCheck[__builtin_ctz(b)]]);

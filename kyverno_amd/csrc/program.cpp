@@ -21,6 +21,7 @@
 #include "goval.hpp"
 #include "jscan.hpp"
 #include "program.hpp"
+#include "pss_msg.hpp"
 #include "pss_fixed.hpp"
 
 namespace kpe {
@@ -1951,7 +1952,8 @@ class Lowerer {
   void pss_exclusions(const JV& ex, uint32_t col, uint32_t cvm, const std::string& rname) {
     KpeXRule xr{};
     xr.col = col, xr.cv_mask = cvm;
-    const int64_t last_invalid = excl_list(ex, "rule '" + rname + "'", &xr.excl0, &xr.nexcl, &xr.kx);
+    pending_excl_.clear();
+    const int64_t last_invalid = excl_list(ex, "rule '" + rname + "'", &xr.excl0, &xr.nexcl, &xr.kx, &pending_excl_);
     if (last_invalid >= 0)
       xr.force = last_invalid == (int64_t)ex.a.size() - 1 ? XR_FORCE_FAIL : XR_FORCE_PASS;
     pssx_fixed_preds();
@@ -1969,9 +1971,12 @@ class Lowerer {
       P.pssx.rules.push_back(xr);
     }
     uint32_t x0, n, kx = 0;
-    const int64_t last_invalid = excl_list(ex, what, &x0, &n, &kx);
+    std::vector<PssExcl> specs;
+    const int64_t last_invalid = excl_list(ex, what, &x0, &n, &kx, &specs);
     KpeXRule& xr = P.pssx.rules[i];
     P.reports[col].pss_excl = true;  // fail messages are the checks after the exception's excludes
+    P.reports[col].pss_xexcludes = std::move(specs);
+    P.reports[col].pss_has_xexcl = true;
     if (n > 0xFFFFFFu) throw CompileError(what + ": too many podSecurity controls");
     xr.kx |= kx, xr.xexcl0 = x0;
     xr.xn = n | (last_invalid < 0 ? XR_FORCE_NONE
@@ -1980,7 +1985,8 @@ class Lowerer {
   // The compiled KpeXExcl entries of one podSecurity exclude list (rule or PolicyException);
   // returns the index of the last invalid entry (Validate: restrictedField and values go
   // together), or -1
-  int64_t excl_list(const JV& ex, const std::string& who, uint32_t* x0, uint32_t* n, uint32_t* kx) {
+  int64_t excl_list(const JV& ex, const std::string& who, uint32_t* x0, uint32_t* n, uint32_t* kx,
+                    std::vector<PssExcl>* specs) {
     static const std::map<std::string, uint32_t> controls = {  // pkg/pss/utils/mapping.go:45-107
         {"Capabilities", (1u << CK_CAPS_BASELINE) | (1u << CK_CAPS_RESTRICTED)},
         {"Seccomp", (1u << CK_SECCOMP_BASELINE) | (1u << CK_SECCOMP_RESTRICTED)},
@@ -2022,6 +2028,7 @@ class Lowerer {
       const std::vector<std::string> images = strs(e.get("images"), "images");
       const std::string rf = str(e.get("restrictedField"), "restrictedField");
       const std::vector<std::string> values = strs(e.get("values"), "values");
+      specs->push_back(PssExcl{cn, images, rf, values});
       if ((!rf.empty() && values.empty()) || (rf.empty() && !values.empty())) last_invalid = (int64_t)i;
       KpeXExcl x{};
       auto it = controls.find(cn);
@@ -2509,6 +2516,8 @@ class Lowerer {
       rr.pss_version = sv(ps->get("version"));
     }
     rr.pss_excl = pss_excl;
+    rr.pss_cv = k.cv_mask;
+    if (pss_excl) rr.pss_excludes = std::move(pending_excl_);
     rr.msg_pattern = msg_pattern;
     if (pat_report.on) {
       rr.pat_rule = true, rr.any_pattern = pat_report.any, rr.pat_roots = pat_report.roots;
@@ -2754,6 +2763,7 @@ class Lowerer {
   Program& P;
   cq::CondCompiler CC;
   std::function<bool(const std::string&, KpeLeaf&)> var_leaf_, key_leaf_;
+  std::vector<PssExcl> pending_excl_;  // the podSecurity.exclude entries of the rule being lowered
   struct RuleInfo {
     bool pre_dyn, has_validate;
     std::string name;
@@ -2998,6 +3008,8 @@ size_t var_end(const std::string& s, size_t i) {
 }
 
 }  // namespace
+
+bool go_wildcard(const std::string& pattern, const std::string& s) { return glob_host(pattern, s); }
 
 bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring) {
   *nonstring = false;

@@ -7,6 +7,7 @@
 #include <string>
 #include <vector>
 
+#include "pss_msg.hpp"
 #include "schema.h"
 
 namespace kpe {
@@ -104,6 +105,11 @@ struct RuleReport {
   // the rule's only PolicyException when its skips can only come from it: RuleSkip message
   // "rule skipped due to policy exception <key>" and report property exception: <name>
   std::string exc_key, exc_name;
+  // podSecurity rules with exclusions: the rule's versioned checks and exclude entries, and a
+  // podSecurity PolicyException's (fail messages after ApplyPodSecurityExclusion, pss_msg.cpp)
+  uint32_t pss_cv = 0;
+  std::vector<PssExcl> pss_excludes, pss_xexcludes;
+  bool pss_has_xexcl = false;
   bool pat_rule = false, any_pattern = false, vmsg_vars = false;
   uint32_t pat_roots = 0;
   std::string vmsg;

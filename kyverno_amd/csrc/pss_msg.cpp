@@ -13,6 +13,7 @@
 // strings.ReplaceAll field rewrites (validate_pss.go:114-135) and field.Error.Error()
 // (apimachinery v0.29.1 field/errors.go: "<field>: <type>" for Required / Forbidden).
 #include <cstdint>
+#include <cstdlib>
 #include <set>
 #include <string>
 #include <vector>
@@ -30,6 +31,7 @@ struct FieldErr {
   std::string field;
   BV kind = BV_NONE;  // field.Required / field.Forbidden default BadValue is ""
   std::string val;    // %+v of the bad value
+  std::vector<std::string> list;  // BV_LIST: the values
 };
 struct Failed {
   const char* reason;
@@ -46,7 +48,7 @@ FieldErr forbidden_int(std::string f, long long v) { return FieldErr{true, std::
 FieldErr forbidden_list(std::string f, const std::vector<std::string>& v) {
   std::string s = "[";  // %+v of a []string
   for (size_t i = 0; i < v.size(); ++i) s += (i ? " " : "") + v[i];
-  return FieldErr{true, std::move(f), BV_LIST, s + "]"};
+  return FieldErr{true, std::move(f), BV_LIST, s + "]", v};
 }
 
 template <class F>
@@ -283,7 +285,254 @@ void replace_all(std::string& s, const std::string& from, const std::string& to)
   s = o + s.substr(i);
 }
 
+// ---- exclusions (pkg/pss/evaluate.go:72-317) ---------------------------------------------
+static const uint8_t kCvCheckM[KPE_NUM_CV] = KPE_CV_CHECK_TABLE;
+// one failing versioned check of evaluatePSS: its check id (CK_*) and field errors
+struct PCheck {
+  uint32_t ck;
+  const char* reason;
+  std::vector<FieldErr> errs;
+};
+// evaluatePSS (evaluate.go:24-70) of the rule's versioned checks over a pod view
+std::vector<PCheck> evaluate_view(const PodView& p, uint32_t cv_mask) {
+  std::vector<PCheck> out;
+  for (uint32_t cv = 0; cv < KPE_NUM_CV; ++cv) {
+    if (!((cv_mask >> cv) & 1u)) continue;
+    // the 1.25 versions of these checks allow a pod whose spec.os.name is windows
+    if ((cv == CV_APE_1_25 || cv == CV_CAPS_RESTRICTED_1_25 || cv == CV_SECCOMP_RESTRICTED_1_25) && windows(p)) continue;
+    Failed f = check_errors(cv, p);
+    if (!f.errs.empty()) out.push_back({kCvCheckM[cv], f.reason, std::move(f.errs)});
+  }
+  return out;
+}
+// PSS_controls_to_check_id (pkg/pss/utils/mapping.go:45-107): the check ids of a control, in order
+const std::vector<uint32_t>& control_checks(const std::string& control) {
+  static const std::vector<std::pair<std::string, std::vector<uint32_t>>> m = {
+      {"Capabilities", {CK_CAPS_BASELINE, CK_CAPS_RESTRICTED}},
+      {"Seccomp", {CK_SECCOMP_BASELINE, CK_SECCOMP_RESTRICTED}},
+      {"Privileged Containers", {CK_PRIVILEGED}},
+      {"Host Ports", {CK_HOST_PORTS}},
+      {"/proc Mount Type", {CK_PROC_MOUNT}},
+      {"HostProcess", {CK_WIN_HOST_PROCESS}},
+      {"SELinux", {CK_SELINUX}},
+      {"Host Namespaces", {CK_HOST_NS}},
+      {"HostPath Volumes", {CK_HOST_PATH}},
+      {"Sysctls", {CK_SYSCTLS}},
+      {"AppArmor", {CK_APPARMOR}},
+      {"Privilege Escalation", {CK_APE}},
+      {"Running as Non-root", {CK_RUN_AS_NON_ROOT}},
+      {"Running as Non-root user", {CK_RUN_AS_USER}},
+      {"Volume Types", {CK_RESTRICTED_VOLUMES}},
+  };
+  static const std::vector<uint32_t> none;
+  for (auto& kv : m)
+    if (kv.first == control) return kv.second;
+  return none;
+}
+// regexIndex `\d+` -> "*"
+std::string star_digits(const std::string& f) {
+  std::string o;
+  for (size_t i = 0; i < f.size();) {
+    if (f[i] >= '0' && f[i] <= '9') {
+      while (i < f.size() && f[i] >= '0' && f[i] <= '9') ++i;
+      o += '*';
+    } else {
+      o += f[i++];
+    }
+  }
+  return o;
+}
+// parseField (evaluate.go:193-204): the starred field, the first index, the container list word
+struct PField {
+  std::string field, ctype;
+  long idx = -1;
+  bool ctr = false;
+};
+PField parse_field(const std::string& f) {
+  PField p;
+  p.field = star_digits(f);
+  std::vector<std::string> words;
+  for (size_t i = 0; i < f.size();) {
+    const char c = f[i];
+    if (c >= '0' && c <= '9') {
+      const size_t b = i;
+      while (i < f.size() && f[i] >= '0' && f[i] <= '9') ++i;
+      if (p.idx < 0) p.idx = std::atol(f.substr(b, i - b).c_str());
+    } else if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) {
+      const size_t b = i;
+      while (i < f.size() && ((f[i] >= 'a' && f[i] <= 'z') || (f[i] >= 'A' && f[i] <= 'Z'))) ++i;
+      words.push_back(f.substr(b, i - b));
+    } else {
+      ++i;
+    }
+  }
+  p.ctype = words.size() > 1 ? words[1] : "";
+  p.ctr = p.ctype == "containers" || p.ctype == "initContainers" || p.ctype == "ephemeralContainers";
+  return p;
+}
+// getContainerInfo (evaluate.go:206-219); null past the list (the reference would panic)
+const CtrView* container_info(const PodView& p, long idx, const std::string& ctype) {
+  const int l = ctype == "initContainers" ? 0 : ctype == "containers" ? 1 : ctype == "ephemeralContainers" ? 2 : -1;
+  if (l < 0 || idx < 0 || (size_t)idx >= p.ctr[l].size()) return nullptr;
+  return &p.ctr[l][(size_t)idx];
+}
+// extractBadValues (evaluate.go:163-182): a string (non-empty), bool, Go int or []string
+std::vector<std::string> bad_values(const FieldErr& e) {
+  switch (e.kind) {
+    case BV_STR: return {e.val};
+    case BV_BOOL:
+    case BV_INT: return {e.val};
+    case BV_LIST: return e.list;
+    default: return {};
+  }
+}
+bool check_patterns(const std::vector<std::string>& pats, const std::string& s) {  // wildcard.CheckPatterns
+  for (auto& p : pats)
+    if (go_wildcard(p, s)) return true;
+  return false;
+}
+// exemptExclusions (evaluate.go:72-161): defaults keyed by check id (the last result of an id
+// wins, as in the Go map), each exclude field error removing the first matching default error
+// (remove: swap with the last); *err: an invalid exclude (Validate: restrictedField and values
+// go together)
+std::vector<PCheck> exempt(const std::vector<PCheck>& defaults, const std::vector<PCheck>& xres, const PssExcl& ex,
+                           const PodView& pod, const PodView* matching, bool ctr_level, bool* err) {
+  *err = false;
+  if (ex.field.empty() != ex.values.empty()) {
+    *err = true;
+    return {};
+  }
+  std::vector<uint32_t> order;
+  std::vector<PCheck> m(KPE_NUM_CHECKS);
+  std::vector<bool> has(KPE_NUM_CHECKS, false);
+  for (auto& r : defaults) {
+    if (!has[r.ck]) order.push_back(r.ck);
+    m[r.ck] = r, has[r.ck] = true;
+  }
+  const std::vector<uint32_t>& ids = control_checks(ex.control);
+  for (auto& xr : xres)
+    for (uint32_t id : ids) {
+      if (xr.ck != id) continue;
+      for (auto& xe : xr.errs) {
+        std::string xfield;
+        const CtrView* xc = nullptr;
+        bool xcl = false;
+        if (ctr_level) {
+          const PField pf = parse_field(xe.field);
+          xfield = pf.field, xcl = pf.ctr;
+          if (xcl) xc = container_info(*matching, pf.idx, pf.ctype);
+        } else {
+          xfield = star_digits(xe.field);
+        }
+        if (!(xfield == ex.field || ex.field.empty())) continue;
+        bool flag = true;
+        if (!ex.values.empty())
+          for (auto& b : bad_values(xe))
+            if (!check_patterns(ex.values, b)) {
+              flag = false;
+              break;
+            }
+        if (!flag || !has[id]) continue;  // a missing id: the zero result, a nil ErrList
+        auto& errs = m[id].errs;
+        for (size_t i = 0; i < errs.size(); ++i) {
+          std::string dfield;
+          const CtrView* dc = nullptr;
+          bool dcl = false;
+          if (ctr_level) {
+            const PField pf = parse_field(errs[i].field);
+            dfield = pf.field, dcl = pf.ctr;
+            if (dcl) dc = container_info(pod, pf.idx, pf.ctype);
+          } else {
+            dfield = star_digits(errs[i].field);
+          }
+          const bool hit = dcl ? (xfield == dfield && xc && dc && xc->name == dc->name) : xfield == dfield;
+          if (hit) {
+            errs[i] = errs.back();
+            errs.pop_back();
+            break;
+          }
+        }
+        if (errs.empty()) has[id] = false;
+      }
+    }
+  std::vector<PCheck> out;
+  for (uint32_t id : order)
+    if (has[id]) out.push_back(m[id]);
+  return out;
+}
+// ApplyPodSecurityExclusion (evaluate.go:255-279) with GetPodWithMatchingContainers (:283-317):
+// a pod-level exclude evaluates the pod with one empty "fake" container, an image exclude a pod of
+// the matching containers only (name / namespace metadata, no other spec field); *err: the last
+// exclude's error
+std::vector<PCheck> apply_exclusion(const std::vector<PCheck>& defaults0, const std::vector<PssExcl>& excl,
+                                    const PodView& pod, uint32_t cv_mask, bool* err) {
+  std::vector<PCheck> defaults = defaults0;
+  *err = false;
+  for (auto& ex : excl) {
+    bool e = false;
+    if (ex.images.empty()) {
+      PodView spec = pod;
+      CtrView fake;
+      fake.name = "fake";
+      spec.ctr[0].clear(), spec.ctr[1].assign(1, fake), spec.ctr[2].clear();
+      defaults = exempt(defaults, evaluate_view(spec, cv_mask), ex, pod, nullptr, false, &e);
+    } else {
+      PodView match;
+      for (int l = 0; l < 3; ++l)
+        for (auto& c : pod.ctr[l])
+          if (check_patterns(ex.images, c.image)) match.ctr[l].push_back(c);
+      defaults = exempt(defaults, evaluate_view(match, cv_mask), ex, pod, &match, true, &e);
+    }
+    *err = e;
+  }
+  return defaults;
+}
+// convertChecks (validate_pss.go:114-135) then FormatChecksPrint (evaluate.go:331-362)
+std::string format_checks(std::vector<PCheck>& checks, const std::string& kind, bool convert) {
+  const bool tmpl = kind == "DaemonSet" || kind == "Deployment" || kind == "Job" || kind == "StatefulSet" ||
+                    kind == "ReplicaSet" || kind == "ReplicationController";
+  std::string out;
+  for (auto& c : checks) {
+    out += "\n(Forbidden reason: ";
+    out += c.reason;
+    out += ", field error list: [";
+    for (size_t i = 0; i < c.errs.size(); ++i) {
+      FieldErr& x = c.errs[i];
+      if (convert) {
+        if (tmpl) replace_all(x.field, "spec", "spec.template.spec");
+        else if (kind == "CronJob") replace_all(x.field, "spec", "spec.jobTemplate.spec.template.spec");
+        replace_all(x.field, "metadata", "spec.template.metadata");
+      }
+      if (x.forbidden && x.kind != BV_NONE) out += x.field + " is forbidden, don't set the BadValue: " + x.val;
+      else out += x.field + (x.forbidden ? ": Forbidden" : ": Required value");
+      if (i + 1 != c.errs.size()) out += ", ";
+    }
+    out += "])";
+  }
+  return out;
+}
+
 }  // namespace
+
+std::string pss_fail_message_ex(const std::string& rule, const std::string& level, const std::string& version,
+                                const std::string& kind, const PodView& pod, uint32_t cv_mask,
+                                const std::vector<PssExcl>* rule_ex, const std::vector<PssExcl>* exc) {
+  std::vector<PCheck> checks = evaluate_view(pod, cv_mask);  // EvaluatePod
+  bool err = false;
+  if (rule_ex && !rule_ex->empty()) checks = apply_exclusion(checks, *rule_ex, pod, cv_mask, &err);
+  // convertChecks rewrites the fields in place; the exception's exclusions compare against them
+  const bool tmpl = kind == "DaemonSet" || kind == "Deployment" || kind == "Job" || kind == "StatefulSet" ||
+                    kind == "ReplicaSet" || kind == "ReplicationController";
+  for (auto& c : checks)
+    for (auto& x : c.errs) {
+      if (tmpl) replace_all(x.field, "spec", "spec.template.spec");
+      else if (kind == "CronJob") replace_all(x.field, "spec", "spec.jobTemplate.spec.template.spec");
+      replace_all(x.field, "metadata", "spec.template.metadata");
+    }
+  if (exc) checks = apply_exclusion(checks, *exc, pod, cv_mask, &err);
+  return "Validation rule '" + rule + "' failed. It violates PodSecurity \"" + level + ":" + version + "\": " +
+         format_checks(checks, kind, false);
+}
 
 std::string pss_pass_message(const std::string& rule) { return "Validation rule '" + rule + "' passed."; }
 

@@ -401,6 +401,6 @@ __device__ __forceinline__ void pssx_eval_row(const PssxArgs& a, int64_t r) {
     if (out_rule)
       v = (!xc || xforce == XR_FORCE_FAIL || (xforce == XR_FORCE_NONE && out)) ? KPE_FAIL_ : KPE_SKIP_;
     row[xr.col] = v;
-    if (mk) *mk = v == KPE_FAIL_ ? out_rule : 0u;
+    if (mk) *mk = v == KPE_FAIL_ ? out_rule | (xc ? KPE_CVM_XMATCH : 0u) : 0u;
   }
 }

@@ -264,6 +264,11 @@ enum KpeCheckVersion {
   KPE_NUM_CV
 };
 
+// A check-mask word (kpe_fetch_cv_masks) of a podSecurity cell with a PolicyException's
+// podSecurity controls: bit 31 set when the exception matched the resource (its exclusions then
+// shaped the fail message, validate_pss.go:88-110); the checks are bits [0, KPE_NUM_CV)
+#define KPE_CVM_XMATCH (1u << 31)
+#define KPE_CVM_CHECKS ((1u << KPE_NUM_CV) - 1u)
 // PSA check of each versioned check (KpeCheckVersion -> KpeCheck); shared by the device
 // (per-ID check masks) and the host (report `controls`, one entry per failing versioned check).
 #define KPE_CV_CHECK_TABLE                                                                              \

@@ -233,6 +233,53 @@ int oracle_pss_message(const char* rule, const char* level, const char* version,
   }
 }
 
+// The fail / pass message of a podSecurity rule with podSecurity.exclude entries (`excludes`, a
+// JSON array or null) and, when a podSecurity PolicyException matched the resource, its entries
+// (`xexcludes`, or null): validate_pss.go:76-110 (EvaluatePod with the rule's exclusions,
+// convertChecks, ApplyPodSecurityExclusion of the exception's). After an exclusion pass the
+// reference's check order is Go map order: here, evaluation order (exempt_exclusions). Returns 1
+// pass, 0 fail, 2 skip (the exception left no check), -1 an error.
+int oracle_pss_message_ex(const char* rule, const char* level, const char* version, const char* resource_json,
+                          const char* excludes_json, const char* xexcludes_json, char* buf, size_t cap) {
+  try {
+    JPtr res = parse_json(resource_json);
+    const std::string kind = jstr(res->get("kind"));
+    Pod pod = get_spec(*res, kind);
+    Version v;
+    if (!parse_version(version, &v)) return -1;
+    std::string lvl = level;
+    LevelVersion lv{lvl == "baseline" ? Level::Baseline : (lvl == "restricted" ? Level::Restricted : Level::Privileged),
+                    v};
+    JPtr ej = parse_json(excludes_json), xj = parse_json(xexcludes_json);
+    const auto ex = parse_pss_excludes(ej.get());
+    std::vector<PSSCheckResult> checks;
+    const bool allowed = evaluate_pod(lv, ex, pod, &checks);
+    if (allowed) {
+      snprintf(buf, cap, "Validation rule '%s' passed.", rule);
+      return 1;
+    }
+    convert_checks(checks, kind);
+    if (xj && xj->t == JT::Arr) {
+      bool err = false;
+      checks = apply_exclusion(lv, parse_pss_excludes(xj.get()), checks, pod, &err);
+      if (checks.empty() && !err) {
+        snprintf(buf, cap, "%s", "");
+        return 2;
+      }
+    }
+    const std::string msg = std::string("Validation rule '") + rule + "' failed. It violates PodSecurity \"" + level + ":" +
+                            version + "\": " + format_checks_print(checks);
+    snprintf(buf, cap, "%s", msg.c_str());
+    return 0;
+  } catch (const DecodeError& de) {
+    g_err = de.msg;
+    return -1;
+  } catch (const std::exception& e) {
+    g_err = e.what();
+    return -1;
+  }
+}
+
 // Number of rules after autogen for a JSON array of policies; names written
 // newline-separated into buf as "<policy>/<rule>".
 int oracle_rule_names(const char* policies_json, char* buf, size_t cap) {

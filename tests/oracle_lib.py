@@ -30,6 +30,8 @@ class Oracle:
         L.oracle_substitute.restype = ctypes.c_int
         L.oracle_substitute_doc.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_substitute_doc.restype = ctypes.c_int
+        L.oracle_pss_message_ex.argtypes = [ctypes.c_char_p] * 6 + [ctypes.c_char_p, ctypes.c_size_t]
+        L.oracle_pss_message_ex.restype = ctypes.c_int
         L.oracle_pss_message.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p,
                                           ctypes.c_char_p, ctypes.c_size_t]
         L.oracle_rule_names.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
@@ -90,6 +92,15 @@ class Oracle:
         r = self.lib.oracle_pss_message(rule.encode(), level.encode(), version.encode(),
                                         json.dumps(resource).encode(), buf, 1 << 16)
         return None if r < 0 else buf.value.decode()
+
+    def pss_message_ex(self, rule, level, version, resource, excludes, xexcludes=None):
+        """(status, message) of a podSecurity rule with exclusions and, when a podSecurity
+        PolicyException matched, its exclusions: 1 pass, 0 fail, 2 skip, -1 error."""
+        buf = ctypes.create_string_buffer(1 << 16)
+        r = self.lib.oracle_pss_message_ex(rule.encode(), level.encode(), version.encode(),
+                                           json.dumps(resource).encode(), json.dumps(excludes).encode(),
+                                           json.dumps(xexcludes).encode(), buf, 1 << 16)
+        return r, (buf.value.decode() if r >= 0 else None)
 
     def substitute(self, msg, resource):
         """variables.SubstituteAll of a message over the resource's context: (0, text) a string,

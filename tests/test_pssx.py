@@ -12,6 +12,7 @@ import numpy as np
 import pytest
 
 import kyverno_amd as K
+from oracle.report import pod_of
 from tests.policies import pss_policy
 from tests.pss_fuzz import exception_case, fuzz_case, strip_exclusions, strip_pss, xfail_seed
 
@@ -188,3 +189,127 @@ def test_pss_exceptions_gpu(oracle, seed, nrules):
     assert bad.size == 0, [(int(i), int(j), int(v[i, j]), int(ref[i, j])) for i, j in bad[:8]]
     assert (masks[v != 2] == 0).all()
     assert (v == 5).any()
+
+
+# ---- messages: FormatChecksPrint after the exclusions (validate_pss.go:76-110) -----------------
+def _excl_messages(oracle, pols, nd, excs=None, xmatch=None):
+    """(device-side message, oracle message) of every FAIL cell of the podSecurity rules: the host
+    report (kpe_report_results_msg) given the oracle's verdict row and, for PolicyException rules,
+    whether the exception matched (KPE_CVM_XMATCH); the oracle's EvaluatePod / convertChecks /
+    ApplyPodSecurityExclusion restatement."""
+    ps = K.PolicySet(pols, excs) if excs else K.PolicySet(pols)
+    names = ps.rule_names
+    ref = oracle.validate(pols, nd, nthreads=8, exceptions=excs) if excs else oracle.validate(pols, nd, nthreads=8)
+    by_name = {p["metadata"]["name"]: p for p in pols}
+    xby = {x["spec"]["exceptions"][0]["policyName"]: x["spec"].get("podSecurity") for x in (excs or [])}
+    docs = [json.loads(l) for l in nd.split(b"\n") if l.strip()]
+    pairs = []
+    for i, doc in enumerate(docs):
+        row = ref[i]
+        cv = np.zeros(len(names), dtype=np.uint32)
+        for j, full in enumerate(names):
+            if row[j] == 2:  # the failing versioned checks (they render the rules without exclusions)
+                ps0 = by_name[full.split("/", 1)[0]]["spec"]["rules"][0]["validate"]["podSecurity"]
+                f = max(oracle.failing_cv(ps0["level"], ps0.get("version", "latest"), pod_of(doc)), 0)
+                cv[j] = (f or 1) | ((1 << 31) if xmatch is not None and xmatch[i, j] else 0)
+        got = {r["rule"]: r.get("message") for r in K.report_results(ps, row, cv, resource=doc)}
+        for j, full in enumerate(names):
+            if row[j] != 2:
+                continue
+            pname, rname = full.split("/", 1)
+            ps0 = by_name[pname]["spec"]["rules"][0]["validate"]["podSecurity"]
+            if not ps0.get("exclude") and not xby.get(pname):
+                continue  # no exclusions: the plain message (tests/test_report.py)
+            xex = xby.get(pname) if xmatch is not None and xmatch[i, j] else None
+            st, want = oracle.pss_message_ex(rname, ps0["level"], ps0.get("version", "latest"), doc,
+                                             ps0.get("exclude"), xex)
+            assert st == 0, (full, st)
+            pairs.append((full, i, got.get(rname), want))
+    return pairs
+
+
+def test_exclusion_messages_golden_host(oracle):
+    """The 222 evaluate_test.go exclusion cases: every FAIL cell's message."""
+    cases, pols = golden_cases()
+    nd = "\n".join(json.dumps(c["pod"]) for c in cases).encode()
+    pairs = _excl_messages(oracle, pols, nd)
+    bad = [p for p in pairs if p[2] != p[3]]
+    assert pairs and not bad, bad[:3]
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_exclusion_messages_fuzz_host(oracle, seed):
+    """Random pods x random exclusion lists (pod-level and image entries on one control, values):
+    where at most one check id survives the exclusions the reference's order is fixed and the
+    message must match exactly; with several, the reference lists them in Go map order, so only
+    the set of per-check texts is compared."""
+    pols, nd = fuzz_case(seed, npods=300, nrules=16)
+    pairs = _excl_messages(oracle, pols, nd)
+    assert len(pairs) > 100
+    for full, i, got, want in pairs:
+        assert got is not None, (full, i)
+        head, sep, rest = want.partition('": ')
+        ghead, gsep, grest = got.partition('": ')
+        assert ghead == head
+        if rest.count("\n(Forbidden reason") <= 1:
+            assert got == want, (full, i)
+        else:
+            assert sorted(grest.split("\n")) == sorted(rest.split("\n")), (full, i)
+
+
+@pytest.mark.parametrize("seed", [21, 22])
+def test_exception_messages_host(oracle, seed):
+    """PolicyException podSecurity controls: the fail message after the exception's exclusions
+    when it matched (KPE_CVM_XMATCH; the scan's KPE_XFAIL_ cells), after the rule's own otherwise."""
+    pols, excs, nd = exception_case(seed, npods=300)
+    base = oracle.validate(strip_exclusions(pols), nd, nthreads=8)
+    skipped = oracle.validate(strip_exclusions(pols), nd, nthreads=8, exceptions=strip_pss(excs))
+    xmatch = xfail_seed(pols, excs, base, skipped) == 8
+    pairs = _excl_messages(oracle, pols, nd, excs, xmatch)
+    assert len(pairs) > 50
+    for full, i, got, want in pairs:
+        assert got is not None, (full, i)
+        rest, grest = want.partition('": ')[2], got.partition('": ')[2]
+        if rest.count("\n(Forbidden reason") <= 1:
+            assert got == want, (full, i)
+        else:
+            assert sorted(grest.split("\n")) == sorted(rest.split("\n")), (full, i)
+
+
+@pytest.mark.gpu
+def test_exception_messages_gpu(oracle):
+    """End to end: the device's check masks carry KPE_CVM_XMATCH exactly on the FAIL cells whose
+    podSecurity PolicyException matched, and the messages rendered from them equal the oracle's."""
+    pols, excs, nd = exception_case(41, npods=400)
+    eng = K.Engine(ordinal=0)
+    ps, c = K.PolicySet(pols, excs), K.Corpus(nd)
+    v, _, _ = eng.evaluate(ps, c, check_masks=True)
+    ref = oracle.validate(pols, nd, nthreads=8, exceptions=excs)
+    assert np.array_equal(v, ref)
+    cvm = eng.cv_masks(ps, c)
+    base = oracle.validate(strip_exclusions(pols), nd, nthreads=8)
+    skipped = oracle.validate(strip_exclusions(pols), nd, nthreads=8, exceptions=strip_pss(excs))
+    xm = xfail_seed(pols, excs, base, skipped) == 8
+    fail = v == 2
+    assert np.array_equal(((cvm >> 31) & 1).astype(bool) & fail, xm & fail)
+    assert (xm & fail).sum() > 10
+    by_name = {p["metadata"]["name"]: p for p in pols}
+    xby = {x["spec"]["exceptions"][0]["policyName"]: x["spec"].get("podSecurity") for x in excs}
+    docs = [json.loads(l) for l in nd.split(b"\n") if l.strip()]
+    n = 0
+    for i, doc in enumerate(docs):
+        got = {r["rule"]: r.get("message") for r in K.report_results(ps, v[i], cvm[i], resource=doc)}
+        for j, full in enumerate(ps.rule_names):
+            pname, rname = full.split("/", 1)
+            ps0 = by_name[pname]["spec"]["rules"][0]["validate"]["podSecurity"]
+            if v[i, j] != 2 or not (ps0.get("exclude") or xby.get(pname)):
+                continue
+            st, want = oracle.pss_message_ex(rname, ps0["level"], ps0.get("version", "latest"), doc,
+                                             ps0.get("exclude"), xby.get(pname) if xm[i, j] else None)
+            rest, grest = want.partition('": ')[2], got[rname].partition('": ')[2]
+            if rest.count("\n(Forbidden reason") <= 1:
+                assert got[rname] == want, (full, i)
+            else:
+                assert sorted(grest.split("\n")) == sorted(rest.split("\n")), (full, i)
+            n += 1
+    assert n > 50
