@@ -247,7 +247,7 @@ kpe_status kpe_cli_summary(const kpe_program* prog, const kpe_counts* counts, in
  * []PolicyReportResult: one object per rule with a response, in rule order, with
  * source, policy (cache.MetaNamespaceKeyFunc key), rule, result (unscored fail => warn),
  * scored, properties {controls, standard, version} for failing podSecurity rules,
- * category and severity. message and timestamp are not produced.
+ * category and severity. No message (kpe_report_results_msg / _ex) and no timestamp.
  *   verdict_row : R verdict cells of the resource (kpe_evaluate row)
  *   cv_mask_row : R cells of kpe_fetch_cv_masks, or NULL (then no controls)
  * Writes at most cap-1 bytes plus NUL; returns the full length (call again with a larger
@@ -257,16 +257,22 @@ long kpe_report_results(const kpe_program* prog, const uint8_t* verdict_row, con
 /* kpe_report_results with the RuleResponse `message` of each result, rendered from the
  * resource's JSON (the EngineResponse resource, resource_len bytes): podSecurity pass
  * ("Validation rule '<rule>' passed.", validate_pss.go:85) and fail (validate_pss.go:108:
- * FormatChecksPrint of the failing checks after convertChecks, rules without
- * podSecurity.exclude or a podSecurity PolicyException) and validate.pattern pass ("validation rule '<rule>' passed.",
- * validate_resource.go:339), and for validate.deny rules whose conditions carry no `message`:
- * pass ("validation rule '<rule>' passed."), fail (getDenyMessage, validate_resource.go:279-300:
- * the rule message, or "validation error: rule <rule> failed" when it is empty) and
- * preconditions skip ("preconditions not met", engine.go:283). A rule message with variables is
- * substituted over the resource (variables.SubstituteAll, vars.go:311-389) when every variable is
- * a `request.object` path of members and [N] indexes; a substitution error (a member missing
- * from an object) leaves no message, as in the reference, and other variables are not rendered.
- * Other results carry no message. Host only. */
+ * FormatChecksPrint of the failing checks after convertChecks; with podSecurity.exclude or a
+ * podSecurity PolicyException, over the checks their exclusions leave), validate.pattern pass
+ * ("validation rule '<rule>' passed.", validate_resource.go:339), validate.deny pass
+ * ("validation rule '<rule>' passed.") and, when the deny block's condition message is known
+ * without the resource (no condition `message`, or conditions folded at compile time), fail
+ * (getDenyMessage, validate_resource.go:279-300: the rule message joined with the condition
+ * message, or "validation error: rule <rule> failed" when both are empty); preconditions skips
+ * of deny rules whose preconditions carry no `message` ("preconditions not met", engine.go:283)
+ * and of preconditions folded at compile time; a PolicyException skip ("rule skipped due to
+ * policy exception <key>") when it is the skip's only cause. A message with variables is
+ * substituted over the resource (variables.SubstituteAll, vars.go:311-389) when every variable
+ * is a `request.object` path of members and [N] indexes. A substitution error (a member missing
+ * from an object) fails SubstituteAll: the pattern message is then not rendered (its reference
+ * text embeds the Go error string), and getDenyMessage returns the condition message as is.
+ * Messages with other variables are not rendered. Condition messages that depend on where a
+ * block stopped need the condition traces (kpe_report_results_ex). Host only. */
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
                             const char* resource_json, size_t resource_len, char* buf, size_t cap);
 
@@ -297,6 +303,40 @@ kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kp
 long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus, const uint8_t* verdict_row,
                                const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
                                size_t resource_len, char* buf, size_t cap);
+
+/* Condition traces, for the condition messages of validate rules (variables/evaluate.go:31-125):
+ * after kpe_evaluate / kpe_evaluate_async of the same program and corpus, rows [row0, row0 +
+ * nrows) into out (nrows x R words, row-major). A rule whose preconditions are evaluated per
+ * resource, or whose validate.deny conditions carry a `message`, records where each block
+ * stopped: the preconditions in bits 0-15, the deny block in bits 16-31, each as the index of
+ * the first true `any` condition (bits 0-6), of the first false `all` condition (bits 7-13),
+ * 0x4000 evaluated without an error, 0x8000 it held. Other cells (and blocks of more than 127
+ * conditions) are 0. */
+kpe_status kpe_fetch_cond_traces(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint64_t row0,
+                                 uint64_t nrows, uint32_t* out);
+/* kpe_report_results_msg_tr plus the condition messages of kpe_fetch_cond_traces (cond_traces:
+ * the row's R words, or NULL):
+ *   - a preconditions skip (engine.go:282-284): "preconditions not met; <condition message>" of
+ *     any validate rule, for preconditions evaluated per resource or folded at compile time;
+ *   - validate.deny fail: getDenyMessage (validate_resource.go:279-300), the rule message joined
+ *     with the deny block's condition message by "; " and substituted over the resource (on a
+ *     substitution error the condition message as is);
+ *   - a PolicyException skip of a rule whose preconditions read the resource, once the trace
+ *     shows they held ("rule skipped due to policy exception <key>").
+ * Preconditions and deny conditions are not substituted into condition messages before they join
+ * (the reference substitutes only getDenyMessage's joined text). Not rendered: messages of
+ * validate.foreach rules and their elements, and RuleError texts (the Go error strings). */
+typedef struct kpe_report_args {
+  const kpe_program* prog;
+  const kpe_corpus* corpus;        /* pattern traces' key names; may be NULL without pattern traces */
+  const uint8_t* verdict_row;      /* R verdict cells */
+  const uint32_t* cv_mask_row;     /* R cells of kpe_fetch_cv_masks, or NULL */
+  const uint32_t* pattern_traces;  /* kpe_pattern_traces layout for the row, or NULL */
+  const uint32_t* cond_traces;     /* R words of kpe_fetch_cond_traces, or NULL */
+  const char* resource_json;       /* the resource (NULL: no messages) */
+  size_t resource_len;
+} kpe_report_args;
+long kpe_report_results_ex(const kpe_report_args* args, char* buf, size_t cap);
 
 /* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
 typedef struct kpe_kernel_stats {

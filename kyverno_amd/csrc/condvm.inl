@@ -56,6 +56,7 @@ struct CondVM {
   uint8_t* tx;       // 2 x KPE_TXT_CAP bytes of LDS: substituted key / value strings (VK_TXT), or
                      // null when the program has no partial-string variables
   uint32_t tlen[2];
+  uint32_t bt;  // where the last block() stopped: first true `any` | first false `all` << 7
 
   // ---- value access ----------------------------------------------------------------------
   __device__ __forceinline__ CV node(uint32_t e) const {  // a tape entry; a null scalar is the null value
@@ -1172,6 +1173,7 @@ struct CondVM {
     const KpeCBlock b = a.blocks[bi];
     const bool has_any = b.flags & CB_HAS_ANY;
     bool any_ok = !has_any;
+    uint32_t as = b.nany;
     const uint32_t n = b.nany + b.nall;
     for (uint32_t i = has_any ? 0u : b.nany; i < n; ++i) {  // any (when present), then all
       const int r = condition(b.c0 + i);
@@ -1179,12 +1181,15 @@ struct CondVM {
       if (i < b.nany) {
         if (r == CB_TRUE) {  // the first true `any` condition ends the any loop
           any_ok = true;
+          as = i;
           i = b.nany - 1u;
         }
       } else if (r == CB_FALSE) {
+        bt = as | (i - b.nany) << 7;
         return CB_FALSE;
       }
     }
+    bt = as | b.nall << 7;
     return any_ok ? CB_TRUE : CB_FALSE;
   }
 };
@@ -1249,12 +1254,15 @@ template <bool FEPAT>
 __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16], uint8_t* tx) {
   const uint64_t im = a.img_off ? a.img_off[r] : ~0ull;
   CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], im == ~0ull ? kNoNode : (uint32_t)im,
-            {}, {}, -1, {}, {}, nb, tx, {}};
+            {}, {}, -1, {}, {}, nb, tx, {}, 0u};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   uint2* pvrow = a.pvals ? a.pvals + (size_t)r * a.nvars : nullptr;
   for (uint32_t i = 0; i < a.ncr; ++i) {
     const KpeCRule cr = a.rules[i];
     const uint8_t cell = row[cr.col];
+    uint32_t* mt = cr.mslot && a.mtrace ? a.mtrace + (size_t)r * a.nmsg + (cr.mslot - 1u) : nullptr;
+    uint32_t mtv = 0;
+    if (mt) *mt = 0u;
     if (cell == KPE_NA_) continue;  // the rule did not match
     // A PolicyException the scan decided already made the cell RuleSkip (validate_resource.go:
     // 44-56 returns before the deny / foreach is evaluated). A deferred one (XC_DEFER) is applied
@@ -1463,6 +1471,8 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         ph = PH_DONE;
         continue;
       }
+      if (mt && (ph == PH_PRE || ph == PH_DENY) && res <= CB_TRUE)  // the block's messages (CT_*)
+        mtv |= ((vm.bt & 0x3FFFu) | CT_EVAL | (res == CB_TRUE ? CT_TRUE : 0u)) << (ph == PH_DENY ? 16u : 0u);
       if (ph == PH_PRE) {  // engine.go:278-285: false => skip, error => error
         if (res == CB_TRUE) {
           ph = xd ? PH_EXC : PH_HANDLER;
@@ -1496,5 +1506,6 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
       }
     }
     row[cr.col] = (uint8_t)v;
+    if (mtv) *mt = mtv;
   }
 }

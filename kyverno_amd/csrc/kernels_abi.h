@@ -357,8 +357,9 @@ struct CondArgs {
   uint32_t txt, pad2_;             // 1: VT_TMPL templates exist (the kernel's LDS text slots)
   const KpePVar* pvars;            // pattern variable slots (query template, use flags)
   uint2* pvals;                    // their per-row values (PatArgs::pvals), or null
-  uint32_t nvars, pad_;
+  uint32_t nvars, nmsg;             // pattern variable slots; condition trace slots per row
   uint8_t* verdicts;
+  uint32_t* mtrace;                // N x nmsg condition traces (schema.h CT_*), or null
 };
 
 // kpe_pssx_kernel arguments (device-resident, one copy per binding): podSecurity rules with

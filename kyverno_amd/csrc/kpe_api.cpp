@@ -198,6 +198,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   bool pargs_valid = false;
   DevBuf pvals;  // pattern variables: per-row values (kpe_cond_kernel -> kpe_pattern_kernel)
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
+  DevBuf mtrace;         // condition traces: N x CondProgram::nmsg words (schema.h CT_*)
   bool cargs_valid = false;
   DevBuf pimg;  // prologue image (kpe_launch_prep)
   // The large-domain predicate bitsets (pbuf) and the prologue image depend only on the
@@ -1073,6 +1074,11 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     HIPCHK(upload(B.cfkeys, fk, s));
     B.cargs_valid = false;
     if (!P.pat.vars.empty()) HIPCHK(B.pvals.ensure((size_t)C.n * P.pat.vars.size() * 8 + 8));
+    if (P.cond.nmsg) {
+      const size_t bytes = (size_t)C.n * P.cond.nmsg * 4;
+      HIPCHK(B.mtrace.ensure(bytes + 4));
+      HIPCHK(hipMemsetAsync(B.mtrace.p, 0, bytes + 4, s));
+    }
   }
   if (!P.pssx.rules.empty()) {  // podSecurity exclusions: cold pod columns, key tables, resolved excludes
     auto& D = *cc->d;
@@ -1476,6 +1482,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       ca.pvals = P.pat.vars.empty() ? nullptr : B.pvals.as<uint2>();
       ca.nvars = (uint32_t)P.pat.vars.size();
       ca.verdicts = B.verdicts.as<uint8_t>();
+      ca.nmsg = P.cond.nmsg;
+      ca.mtrace = P.cond.nmsg ? B.mtrace.as<uint32_t>() : nullptr;
       HIPCHK(B.cargs.ensure(sizeof(CondArgs)));
       HIPCHK(hipMemcpyAsync(B.cargs.p, &ca, sizeof(CondArgs), hipMemcpyHostToDevice, s));
       HIPCHK(hipStreamSynchronize(s));
@@ -1902,6 +1910,33 @@ kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kp
   return KPE_OK;
 }
 
+// ---- condition traces (report time) -----------------------------------------------------------
+kpe_status kpe_fetch_cond_traces(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint64_t row0,
+                                 uint64_t nrows, uint32_t* out) {
+  if (!dev || !prog || !c || !c->d || (nrows && !out)) return fail(KPE_E_INVALID, "null argument");
+  if (row0 > (uint64_t)c->c->n || nrows > (uint64_t)c->c->n - row0) return fail(KPE_E_INVALID, "rows past the corpus");
+  if (!nrows) return KPE_OK;
+  const kpe::Program& P = *prog->p;
+  const size_t R = P.rules.size();
+  memset(out, 0, nrows * R * 4);
+  if (!P.cond.nmsg) return KPE_OK;
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& B = c->d->bind;
+  if (B.prog != prog->p.get() || !B.cargs_valid)
+    return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  if (c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
+  const size_t m = P.cond.nmsg;
+  std::vector<uint32_t> h(nrows * m);
+  hipStream_t s = B.last ? B.last : dev->stream;
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(h.data(), B.mtrace.as<uint32_t>() + row0 * m, h.size() * 4, hipMemcpyDeviceToHost));
+  for (const KpeCRule& cr : P.cond.rules)
+    if (cr.mslot)
+      for (uint64_t i = 0; i < nrows; ++i) out[i * R + cr.col] = h[i * m + cr.mslot - 1u];
+  return KPE_OK;
+}
+
 kpe_status kpe_evaluate_sharded(kpe_device* const* devs, kpe_corpus* const* shards, int nshards,
                                 const kpe_program* prog, uint8_t* verdicts, kpe_counts* counts) {
   if (!devs || !shards || !prog || nshards <= 0) return fail(KPE_E_INVALID, "null argument");
@@ -2065,23 +2100,44 @@ static std::string pattern_message(const kpe::Program& P, const kpe::Corpus* C, 
 }
 
 static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const uint8_t* verdict_row,
-                        const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
-                        size_t resource_len, char* buf, size_t cap);
+                        const uint32_t* cv_mask_row, const uint32_t* traces, const uint32_t* cond_traces,
+                        const char* resource_json, size_t resource_len, char* buf, size_t cap);
+
+// getDenyMessage (validate_resource.go:279-300) of a failing deny rule whose deny block's
+// condition message is `cm`: SubstituteAll of JoinNonEmpty(rule message, cm); on a substitution
+// error the condition message as is; a message outside the restated variables: none
+static std::string deny_message(const kpe::RuleReport& rr, const std::string& cm, const char* json, size_t n) {
+  if (rr.deny_vmsg.empty() && cm.empty()) return "validation error: rule " + rr.rule + " failed";
+  const std::string j = kpe::join_non_empty({rr.deny_vmsg, cm}, "; ");
+  std::string out;
+  bool nonstring = false, serr = false;
+  if (!kpe::substitute_message(j, json, n, &out, &nonstring, &serr)) return serr ? cm : std::string();
+  return nonstring ? "the produced message didn't resolve to a string, check your policy definition." : out;
+}
+
+long kpe_report_results_ex(const kpe_report_args* a, char* buf, size_t cap) {
+  if (!a) {
+    fail(KPE_E_INVALID, "null argument");
+    return -KPE_E_INVALID;
+  }
+  return report_impl(a->prog, a->corpus, a->verdict_row, a->cv_mask_row, a->pattern_traces, a->cond_traces,
+                     a->resource_json, a->resource_len, buf, cap);
+}
 
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
                             const char* resource_json, size_t resource_len, char* buf, size_t cap) {
-  return report_impl(prog, nullptr, verdict_row, cv_mask_row, nullptr, resource_json, resource_len, buf, cap);
+  return report_impl(prog, nullptr, verdict_row, cv_mask_row, nullptr, nullptr, resource_json, resource_len, buf, cap);
 }
 
 long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus, const uint8_t* verdict_row,
                                const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
                                size_t resource_len, char* buf, size_t cap) {
-  return report_impl(prog, corpus, verdict_row, cv_mask_row, traces, resource_json, resource_len, buf, cap);
+  return report_impl(prog, corpus, verdict_row, cv_mask_row, traces, nullptr, resource_json, resource_len, buf, cap);
 }
 
 static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const uint8_t* verdict_row,
-                        const uint32_t* cv_mask_row, const uint32_t* traces, const char* resource_json,
-                        size_t resource_len, char* buf, size_t cap) {
+                        const uint32_t* cv_mask_row, const uint32_t* traces, const uint32_t* cond_traces,
+                        const char* resource_json, size_t resource_len, char* buf, size_t cap) {
   if (!prog || !verdict_row) {
     fail(KPE_E_INVALID, "null argument");
     return -KPE_E_INVALID;
@@ -2104,6 +2160,13 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
     first = false;
     o += "\"source\":\"kyverno\",\"policy\":";
     json_str(o, rr.policy_key);
+    // the skip's cause: preconditions false (folded at compile time, or the condition trace's
+    // preconditions half) or the rule's PolicyException (after preconditions that held)
+    const uint32_t ct = (cond_traces && rr.cond_slot) ? cond_traces[r] : 0u;
+    const uint32_t held = CT_EVAL | CT_TRUE;
+    const bool pre_skip = v == KPE_SKIP && (rr.pre_const_skip || (ct & held) == CT_EVAL);
+    const bool exc_skip = v == KPE_SKIP && !rr.exc_key.empty() && !pre_skip &&
+                          (!rr.exc_after_pre || (ct & held) == held);
     if (resource_json) {  // RuleResponse message (validate_pss.go:85,108; validate_resource.go:339)
       std::string msg;
       if (rr.pss && v == KPE_PASS) {
@@ -2125,19 +2188,21 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
                               traces + r * (size_t)(KPE_TRACE_ROOTS * KPE_TRACE_WORDS), resource_json, resource_len);
       } else if (rr.msg_pattern && v == KPE_PASS) {
         msg = "validation rule '" + rr.rule + "' passed.";
+      } else if (pre_skip) {  // engine.go:282-284
+        msg = rr.pre_const_skip
+                  ? rr.pre_skip_msg
+                  : kpe::join_non_empty({"preconditions not met", rr.pre_msgs.render(CT_ANY(ct), CT_ALL(ct), false)}, "; ");
       } else if (rr.msg_deny && v == KPE_PASS) {
         msg = "validation rule '" + rr.rule + "' passed.";
       } else if (rr.msg_deny && v == KPE_FAIL) {
-        msg = rr.deny_fail_msg;
-        if (msg.empty() && !rr.deny_tmpl.empty()) {  // getDenyMessage: SubstituteAll of the message
-          bool nonstring = false;
-          if (!kpe::substitute_message(rr.deny_tmpl, resource_json, resource_len, &msg, &nonstring)) msg.clear();
-          else if (nonstring) msg = "the produced message didn't resolve to a string, check your policy definition.";
-        }
+        const uint32_t dt = ct >> 16;
+        if (!rr.cond_deny) msg = deny_message(rr, rr.deny_cm, resource_json, resource_len);
+        else if ((dt & held) == held)
+          msg = deny_message(rr, rr.deny_msgs.render(CT_ANY(dt), CT_ALL(dt), true), resource_json, resource_len);
       } else if (rr.msg_deny && rr.msg_pre_skip && v == KPE_SKIP && P.rules[r].exc == 0u) {
-        msg = "preconditions not met";  // a PolicyException's skip has its own message
+        msg = "preconditions not met";  // no exception: the skip is the preconditions'
       }
-      if (v == KPE_SKIP && !rr.exc_key.empty()) msg = "rule skipped due to policy exception " + rr.exc_key;
+      if (exc_skip) msg = "rule skipped due to policy exception " + rr.exc_key;
       if (!msg.empty()) {
         o += ",\"message\":";
         json_str(o, msg);
@@ -2167,7 +2232,7 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
       json_str(o, rr.pss_version);
       o += '}';
     }
-    if (v == KPE_SKIP && !rr.exc_name.empty()) {  // results.go:107-111: the exception's name
+    if (exc_skip && !rr.exc_name.empty()) {  // results.go:107-111: the exception's name
       o += ",\"properties\":{\"exception\":";
       json_str(o, rr.exc_name);
       o += '}';

@@ -1087,6 +1087,56 @@ Fold fold_conditions(const JV* j) {
   return (any_ok == F_TRUE && all_ok == F_TRUE) ? F_TRUE : F_FALSE;
 }
 
+// where a block that folds (fold_conditions != F_NO) stops: its first true `any` condition and
+// first false `all` condition (schema.h CT_ANY / CT_ALL)
+void fold_stops(const JV* j, uint32_t* as, uint32_t* ls) {
+  *as = *ls = 0;
+  if (!j || j->t == JV::Null) return;
+  auto first = [](const JV& arr, Fold want) {
+    uint32_t i = 0;
+    for (auto& e : arr.a) {
+      if (fold_condition(e) == want) break;
+      ++i;
+    }
+    return i;
+  };
+  if (j->t == JV::Arr) {
+    *ls = first(*j, F_FALSE);
+    return;
+  }
+  const JV* any = j->get("any");
+  const JV* all = j->get("all");
+  if (any && any->t == JV::Arr) *as = first(*any, F_TRUE);
+  if (all && all->t == JV::Arr) *ls = first(*all, F_FALSE);
+}
+
+// The `message` of every condition of a block (utils.TransformConditions: a list is the
+// deprecated form, an object holds `any` / `all`), in the order CondCompiler::block lays them out
+CondMsgs cond_msgs(const JV* j) {
+  CondMsgs m;
+  if (!j || j->t == JV::Null) return m;
+  m.present = true;
+  auto text = [](const JV& c) {
+    const JV* x = c.t == JV::Obj ? c.get("message") : nullptr;
+    return x && x->t == JV::Str ? x->s : std::string();
+  };
+  if (j->t == JV::Arr) {
+    m.old = true;
+    for (auto& e : j->a) m.all.push_back(text(e));
+    return m;
+  }
+  if (j->t != JV::Obj) return m;
+  const JV* any = j->get("any");
+  const JV* all = j->get("all");
+  if (any && any->t == JV::Arr) {
+    m.has_any = true;
+    for (auto& e : any->a) m.any.push_back(text(e));
+  }
+  if (all && all->t == JV::Arr)
+    for (auto& e : all->a) m.all.push_back(text(e));
+  return m;
+}
+
 // ---- condition programs evaluated per resource (kpe_cond_kernel) -------------------------
 // Conditions that read the resource (or a foreach element) are compiled to the device program
 // of schema.h QO_* / KpeC*. The restated subset, with everything else refused (CompileError):
@@ -2502,12 +2552,45 @@ class Lowerer {
       crule.kind = CR_NONE;
     }
     if (k.handler >= H_CONST_SKIP || pre_block != CE_NONE) P.any_const = true;
+    RuleReport rr;
+    // condition messages (variables/evaluate.go:31-125): the preconditions skip (engine.go:282-284)
+    // and getDenyMessage (validate_resource.go:279-300). A block evaluated per resource whose
+    // message depends on where it stopped gets a condition trace slot (KpeCRule::mslot).
+    const bool is_pss = ps && ps->t == JV::Obj && nonempty(ps);
+    if (has_validate && pre_raw && pre_raw->t != JV::Null) {
+      rr.pre_msgs = cond_msgs(pre_raw);
+      if (pre == F_FALSE) {
+        uint32_t as, ls;
+        fold_stops(pre_raw, &as, &ls);
+        rr.pre_const_skip = true;
+        rr.pre_skip_msg = join_non_empty({"preconditions not met", rr.pre_msgs.render(as, ls, false)}, "; ");
+      }
+      rr.msg_pre_skip = !rr.pre_msgs.has_text();
+    }
+    if (has_validate && !is_pss && v->get("deny") && v->get("deny")->t == JV::Obj) {
+      const JV* m = v->get("message");
+      const JV* dc = v->get("deny")->get("conditions");
+      rr.msg_deny = true;
+      rr.deny_vmsg = (m && m->t == JV::Str) ? m->s : std::string();
+      rr.deny_msgs = cond_msgs(dc);
+      if (crule.kind != CR_DENY) {  // folded: the message the block gives when it holds
+        uint32_t as, ls;
+        fold_stops(dc, &as, &ls);
+        rr.deny_cm = rr.deny_msgs.render(as, ls, true);
+      } else {
+        rr.cond_deny = rr.deny_msgs.has_text();
+      }
+    }
+    auto fits = [](const CondMsgs& m) { return m.any.size() <= CT_MAXC && m.all.size() <= CT_MAXC; };
+    if ((pre_block != CE_NONE || rr.cond_deny) && fits(rr.pre_msgs) && fits(rr.deny_msgs)) {
+      crule.mslot = ++P.cond.nmsg;
+      rr.cond_slot = true;
+    }
     rule_info_.push_back({pre_block != CE_NONE, has_validate, rname, k.handler == H_PATTERN && !pat_may_skip});
     if (pre_block != CE_NONE || k.handler == H_COND || crule.npv) P.cond.rules.push_back(crule);
     if (k.apply_one) P.any_apply_one = true;
     P.rules.push_back(k);
     P.rule_names.push_back(pol_name + "/" + rname);
-    RuleReport rr;
     rr.rule = rname;
     rr.has_validate = has_validate;
     if (ps && ps->t == JV::Obj && nonempty(ps)) {
@@ -2524,29 +2607,6 @@ class Lowerer {
       const JV* m = v ? v->get("message") : nullptr;
       rr.vmsg = (m && m->t == JV::Str) ? m->s : std::string();
       rr.vmsg_vars = rr.vmsg.find("{{") != std::string::npos || rr.vmsg.find("$(") != std::string::npos;
-    }
-    if (has_validate && !(ps && ps->t == JV::Obj && nonempty(ps)) && v->get("deny") && v->get("deny")->t == JV::Obj) {
-      // a condition `message` would enter the rule's message: render only when there is none
-      std::function<bool(const JV*)> has_msg = [&](const JV* j) -> bool {
-        if (!j) return false;
-        if (j->t == JV::Arr) {
-          for (auto& e : j->a)
-            if (has_msg(&e)) return true;
-          return false;
-        }
-        if (j->t != JV::Obj) return false;
-        if (j->get("key") || j->get("operator")) return nonempty(j->get("message"));
-        return has_msg(j->get("any")) || has_msg(j->get("all"));
-      };
-      if (!has_msg(v->get("deny")->get("conditions")) && !has_msg(pre_raw)) {
-        rr.msg_deny = true;
-        rr.msg_pre_skip = pre_raw && pre_raw->t != JV::Null;
-        const JV* m = v->get("message");
-        const std::string mt = (m && m->t == JV::Str) ? m->s : std::string();
-        if (mt.empty()) rr.deny_fail_msg = "validation error: rule " + rname + " failed";
-        else if (mt.find("{{") == std::string::npos && mt.find("$(") == std::string::npos) rr.deny_fail_msg = mt;
-        else rr.deny_tmpl = mt;  // SubstituteAll per resource (substitute_message)
-      }
     }
     P.reports.push_back(std::move(rr));
   }
@@ -2707,11 +2767,13 @@ class Lowerer {
       // preconditions; a podSecurity, deny or constant handler, or a pattern without conditional /
       // global anchors: no anchor or foreach skip)
       const uint32_t hd = P.rules[r].handler;
-      if (mine.size() == 1 && !xpss && !rule_info_[r].pre_dyn &&
+      // (resource-reading preconditions: a skip after they held, which the condition trace shows)
+      if (mine.size() == 1 && !xpss && (!rule_info_[r].pre_dyn || P.reports[r].cond_slot) &&
           (hd == H_PSS || hd == H_CONST_PASS || hd == H_CONST_FAIL || P.reports[r].msg_deny ||
            rule_info_[r].pat_noskip)) {
         P.reports[r].exc_key = mine_x[0]->key;
         P.reports[r].exc_name = mine_x[0]->name;
+        P.reports[r].exc_after_pre = rule_info_[r].pre_dyn;
       }
     }
   }
@@ -3011,8 +3073,42 @@ size_t var_end(const std::string& s, size_t i) {
 
 bool go_wildcard(const std::string& pattern, const std::string& s) { return glob_host(pattern, s); }
 
-bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring) {
+std::string join_non_empty(const std::vector<std::string>& v, const std::string& sep) {
+  std::string o;
+  for (auto& x : v)
+    if (!x.empty()) o += (o.empty() ? "" : sep) + x;
+  return o;
+}
+
+bool CondMsgs::has_text() const {
+  for (auto& x : any)
+    if (!x.empty()) return true;
+  for (auto& x : all)
+    if (!x.empty()) return true;
+  return false;
+}
+
+// evaluateOldConditions: the first false condition's message, else the true ones joined by ";";
+// evaluateAnyAllConditions: the true ones (the first true `any`, every `all`) joined by "; "
+// when the block held, else the false ones (the `any` conditions before the first true one,
+// the first false `all`)
+std::string CondMsgs::render(uint32_t as, uint32_t ls, bool held) const {
+  if (old) return held ? join_non_empty(all, ";") : (ls < all.size() ? all[ls] : std::string());
+  std::vector<std::string> v;
+  if (held) {
+    if (has_any && as < any.size()) v.push_back(any[as]);
+    v.insert(v.end(), all.begin(), all.end());
+  } else {
+    for (size_t i = 0; i < std::min<size_t>(as, any.size()); ++i) v.push_back(any[i]);
+    if (ls < all.size()) v.push_back(all[ls]);
+  }
+  return join_non_empty(v, "; ");
+}
+
+bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring,
+                        bool* subst_err) {
   *nonstring = false;
+  if (subst_err) *subst_err = false;
   if (msg.find("$(") != std::string::npos) return false;  // substituteReferences: not restated
   if (msg.find("{{") == std::string::npos) {
     *out = msg;
@@ -3047,7 +3143,11 @@ bool substitute_message(const std::string& msg, const char* json, size_t n, std:
       q = b == std::string::npos ? std::string() : q.substr(b, z - b + 1);
       const JV* v = nullptr;
       bool missing = false;
-      if (!object_path(q, res, &v, &missing) || missing) return false;
+      if (!object_path(q, res, &v, &missing)) return false;
+      if (missing) {
+        if (subst_err) *subst_err = true;
+        return false;
+      }
       if (i == 0 && e == msg.size()) {  // the whole message is the variable: its value as is
         if (v->t == JV::Str) {
           if (v->s.find("{{") != std::string::npos) return false;

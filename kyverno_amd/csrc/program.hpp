@@ -54,6 +54,7 @@ struct CondProgram {
   std::vector<uint32_t> tpieces;  // VT_TMPL pieces, 2 words each: PT_TEXT | len << 1, ctext offset /
                                   // PT_VAR, expression
   std::vector<std::string> fields;
+  uint32_t nmsg = 0;  // condition trace slots (KpeCRule::mslot)
 };
 // podSecurity rules with exclusions (schema.h KpeXRule / KpeXExcl), evaluated per pod by
 // kpe_pssx_kernel after the scan. Predicate fields hold predicate ids (resolved per binding).
@@ -77,6 +78,20 @@ struct DeviceProgram;  // kpe_api.cpp
 
 // What a PolicyReportResult carries for rule r besides its verdict
 // (pkg/utils/report/results.go:89-156, EngineResponseToReportResults).
+// The `message`s of one condition block (kyvernov1.Condition.Message) in evaluation order, and
+// EvaluateConditions' message (variables/evaluate.go:31-125) from where the block stopped.
+struct CondMsgs {
+  bool present = false;  // a non-null block
+  bool old = false;      // the deprecated list form (evaluateOldConditions)
+  bool has_any = false;  // an `any` list (even empty: it then never holds)
+  std::vector<std::string> any, all;  // the old form's list is `all`
+  bool has_text() const;
+  // as / ls: the first true `any` / first false `all` condition (schema.h CT_ANY / CT_ALL)
+  std::string render(uint32_t as, uint32_t ls, bool held) const;
+};
+// stringutils.JoinNonEmpty
+std::string join_non_empty(const std::vector<std::string>& v, const std::string& sep);
+
 struct RuleReport {
   std::string policy_key;  // cache.MetaNamespaceKeyFunc: "<ns>/<name>" or "<name>"
   std::string rule;        // rule name after autogen
@@ -91,20 +106,28 @@ struct RuleReport {
   bool pss = false;
   bool pss_excl = false;      // podSecurity.exclude or a podSecurity PolicyException (fail messages not rendered)
   bool msg_pattern = false;   // validate.pattern rule: pass message "validation rule '<rule>' passed."
-  // validate.deny rule whose conditions (and preconditions) carry no `message`, so the reference's
-  // condition message is empty (variables/evaluate.go:14-28): pass "validation rule '<rule>'
-  // passed.", fail `deny_fail_msg` (getDenyMessage, validate_resource.go:279-300; empty when the
-  // rule message has variables), skip "preconditions not met" (engine.go:283) when it has
-  // preconditions
-  bool msg_deny = false, msg_pre_skip = false;
-  std::string deny_fail_msg;
-  std::string deny_tmpl;  // the rule message when it holds variables (substituted per resource)
+  // validate.deny rule (`msg_deny`): pass "validation rule '<rule>' passed.", fail getDenyMessage
+  // (validate_resource.go:279-300) of the rule message `deny_vmsg` and the deny block's condition
+  // message: `deny_cm` when it is known at compile time (no condition `message`, or a block that
+  // folds), else (`cond_deny`) rendered from the cell's condition trace. `msg_pre_skip`: its
+  // preconditions carry no `message`, so a skip without a PolicyException is "preconditions not
+  // met" (engine.go:283) even without condition traces.
+  bool msg_deny = false, msg_pre_skip = false, cond_deny = false;
+  std::string deny_vmsg, deny_cm;
+  // Condition messages (variables/evaluate.go:31-125) of the preconditions and the deny block;
+  // `cond_slot`: the rule has a condition trace slot (KpeCRule::mslot)
+  CondMsgs pre_msgs, deny_msgs;
+  bool cond_slot = false;
+  // preconditions that fold to false at compile time: the skip message (engine.go:282-284)
+  bool pre_const_skip = false;
+  std::string pre_skip_msg;
   // validate.pattern / anyPattern rule (kpe_pattern_traces paths): failure messages are
   // buildErrorMessage / buildAnyPatternErrorMessage (validate_resource.go:418-454) of the rule's
   // validate.message; `vmsg_vars`: it holds variables (substituted per resource, substitute_message)
   // the rule's only PolicyException when its skips can only come from it: RuleSkip message
   // "rule skipped due to policy exception <key>" and report property exception: <name>
   std::string exc_key, exc_name;
+  bool exc_after_pre = false;  // preconditions read the resource: only a skip after they held (trace)
   // podSecurity rules with exclusions: the rule's versioned checks and exclude entries, and a
   // podSecurity PolicyException's (fail messages after ApplyPodSecurityExclusion, pss_msg.cpp)
   uint32_t pss_cv = 0;
@@ -154,6 +177,9 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len, const ch
 // variables.SubstituteAll of a rule message over one resource (program.cpp): false when the
 // message holds variables outside the restated `request.object` path grammar; *nonstring: the
 // message is one variable whose value is not a string (*out is its JSON).
-bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring);
+// *subst_err (when given): false was returned for a substitution error (a member missing from
+// an object, go-jmespath NotFound), not for an unrestated variable.
+bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring,
+                        bool* subst_err = nullptr);
 
 }  // namespace kpe

@@ -759,7 +759,19 @@ typedef struct KpeCRule {
                       // preconditions (validate_resource.go:456-476 substitutePatterns)
   uint32_t exc;       // XC_DEFER: the exception's conditions (block; CE_NONE: none, it holds)
   uint32_t xflags;    // XC_*
+  uint32_t mslot;     // condition trace slot + 1 (CondArgs::mtrace; 0: none)
 } KpeCRule;
+// A condition trace word (CondArgs::mtrace, one per row and rule with a slot): where the rule's
+// preconditions block (low half) and deny block (high half << 16) stopped, for the messages of
+// variables/evaluate.go:31-125 (program.hpp CondMsgs): the index of the first true `any`
+// condition (nany: none) and of the first false `all` condition (nall: none), CT_EVAL when the
+// block was evaluated without an error and CT_TRUE when it held. Blocks of more than CT_MAXC
+// conditions get no slot.
+#define CT_ANY(t) ((t) & 0x7Fu)
+#define CT_ALL(t) (((t) >> 7) & 0x7Fu)
+#define CT_EVAL 0x4000u
+#define CT_TRUE 0x8000u
+#define CT_MAXC 127u
 // KpeCRule::xflags: the rule's PolicyException is applied here (XE_DEFER), after the
 // preconditions: in a cell flagged KPE_XDEFER_ its conditions holding make the cell RuleSkip
 // (validate_resource.go:43-56) or, with podSecurity controls (XC_PSS), a failing cell KPE_XFAIL_

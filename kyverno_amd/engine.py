@@ -372,6 +372,15 @@ class Engine:
         R = ps.num_rules
         return self.pattern_traces(ps, corpus, np.arange(row * R, row * R + R, dtype=np.uint64))
 
+    def cond_traces(self, ps: PolicySet, corpus: Corpus, row0: int = 0, nrows: Optional[int] = None) -> np.ndarray:
+        """Condition traces (kpe_fetch_cond_traces) of rows [row0, row0 + nrows) after an evaluation
+        of ps on corpus: (nrows, R) uint32, the layout report_results(cond_traces=) takes per row."""
+        n = corpus.n - row0 if nrows is None else nrows
+        out = np.zeros((n, ps.num_rules), dtype=np.uint32)
+        if n:
+            check(load().kpe_fetch_cond_traces(self.device.h, ps.h, corpus.h, row0, n, out.ctypes.data))
+        return out
+
     # ---- reference-shaped API ----
     def validate_batch(self, policies: Sequence[dict], resources: Sequence[dict],
                        namespace_labels: Optional[Dict[str, Dict[str, str]]] = None) -> List[List[EngineResponse]]:
@@ -422,14 +431,23 @@ class Engine:
 TRACE_WORDS, TRACE_ROOTS = 16, 4  # include/kpe.h KPE_TRACE_WORDS / KPE_TRACE_ROOTS
 
 
+class ReportArgs(ctypes.Structure):
+    """include/kpe.h kpe_report_args"""
+    _fields_ = [("prog", ctypes.c_void_p), ("corpus", ctypes.c_void_p), ("verdict_row", ctypes.c_void_p),
+                ("cv_mask_row", ctypes.c_void_p), ("pattern_traces", ctypes.c_void_p),
+                ("cond_traces", ctypes.c_void_p), ("resource_json", ctypes.c_char_p),
+                ("resource_len", ctypes.c_size_t)]
+
+
 def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None, traces=None,
-                   corpus: Optional[Corpus] = None) -> List[dict]:
+                   corpus: Optional[Corpus] = None, cond_traces=None) -> List[dict]:
     """EngineResponseToReportResults (pkg/utils/report/results.go:89-156) for one resource row,
     through kpe_report_results, or kpe_report_results_msg when the resource (a dict or its JSON
     bytes) is given: then results carry the RuleResponse message (podSecurity pass / fail,
     validate.pattern pass; no timestamp). With traces (Engine.row_traces of the row) and the
     corpus, kpe_report_results_msg_tr adds the pattern / anyPattern failure and anyPattern pass
-    messages."""
+    messages; with cond_traces (a row of Engine.cond_traces), kpe_report_results_ex adds the
+    condition messages (preconditions skips, deny fails with condition messages)."""
     L = load()
     v = np.ascontiguousarray(verdict_row, dtype=np.uint8)
     m = None if cv_mask_row is None else np.ascontiguousarray(cv_mask_row, dtype=np.uint32)
@@ -444,6 +462,18 @@ def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None, 
         mp = None if m is None else m.ctypes.data
         if raw is None:
             n = L.kpe_report_results(ps.h, v.ctypes.data, mp, buf, cap)
+        elif cond_traces is not None:
+            ct = np.ascontiguousarray(cond_traces, dtype=np.uint32)
+            if ct.size != ps.num_rules:
+                raise ValueError("cond_traces: one word per rule of the row")
+            t = None
+            if traces is not None:
+                t = np.ascontiguousarray(traces, dtype=np.uint32)
+                if t.size != ps.num_rules * TRACE_ROOTS * TRACE_WORDS:
+                    raise ValueError("traces: one record per rule of the row")
+            a = ReportArgs(ps.h, corpus.h if corpus is not None else None, v.ctypes.data, mp,
+                           None if t is None else t.ctypes.data, ct.ctypes.data, raw, len(raw))
+            n = L.kpe_report_results_ex(ctypes.byref(a), buf, cap)
         elif traces is not None:
             t = np.ascontiguousarray(traces, dtype=np.uint32)
             if t.size != ps.num_rules * TRACE_ROOTS * TRACE_WORDS:

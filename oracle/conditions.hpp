@@ -1397,6 +1397,7 @@ struct Condition {
   JPtr key, value;
   OpKind op;
   NumOp num = N_NONE;
+  std::string message;  // kyvernov1.Condition.Message
 };
 struct AnyAll {
   bool has_any = false;
@@ -1416,6 +1417,8 @@ inline Condition parse_condition(const JVal& c) {
   o.value = v ? to_ctx(*v) : nullptr;
   const JVal* op = c.get("operator");
   o.op = parse_op(op && op->t == JT::Str ? op->s : "", &o.num);
+  const JVal* m = c.get("message");
+  if (m && m->t == JT::Str) o.message = m->s;
   auto check = [](const JPtr& x) {
     if (x && x->t == JT::Str && x->s.find("$(") != std::string::npos) throw Unsupported("$(...) references");
   };
@@ -1484,6 +1487,59 @@ inline bool eval_conditions(const Conditions& c, const Ctx& x) {
         all_ok = false;
         break;
       }
+    if (!(any_ok && all_ok)) return false;
+  }
+  return true;
+}
+
+// stringutils.JoinNonEmpty (pkg/utils/strings)
+inline std::string join_non_empty(const std::vector<std::string>& v, const std::string& sep) {
+  std::string o;
+  for (auto& x : v)
+    if (!x.empty()) o += (o.empty() ? "" : sep) + x;
+  return o;
+}
+// variables/evaluate.go:31-125 EvaluateConditions with its message: evaluateAnyAllConditions
+// (the `any` block's messages up to its first true condition, the `all` block's up to its first
+// false one; the true ones joined by "; " when both hold, else the false ones) or
+// evaluateOldConditions (the first false condition's message, else the true ones joined by ";")
+inline bool eval_conditions_msg(const Conditions& c, const Ctx& x, std::string* msg) {
+  msg->clear();
+  if (c.old_list) {
+    std::vector<std::string> t;
+    for (auto& e : c.list) {
+      if (!eval_condition(e, x)) {
+        *msg = e.message;
+        return false;
+      }
+      t.push_back(e.message);
+    }
+    *msg = join_non_empty(t, ";");
+    return true;
+  }
+  for (auto& b : c.blocks) {  // one block (utils.TransformConditions)
+    bool any_ok = true, all_ok = true;
+    std::vector<std::string> t, f;
+    if (b.has_any) {
+      any_ok = false;
+      for (auto& e : b.any) {
+        if (eval_condition(e, x)) {
+          any_ok = true;
+          t.push_back(e.message);
+          break;
+        }
+        f.push_back(e.message);
+      }
+    }
+    for (auto& e : b.all) {
+      if (!eval_condition(e, x)) {
+        all_ok = false;
+        f.push_back(e.message);
+        break;
+      }
+      t.push_back(e.message);
+    }
+    *msg = join_non_empty(any_ok && all_ok ? t : f, "; ");
     if (!(any_ok && all_ok)) return false;
   }
   return true;

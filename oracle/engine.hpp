@@ -1106,9 +1106,36 @@ inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars,
 }
 
 // validate_resource.go:268-279 validateDeny: conditions true => FAIL, false => PASS, error => ERROR
-inline Status deny_handler(const Rule& r, const cond::Ctx& cx) {
+// validate_resource.go:268-300 validateDeny + getDenyMessage (*msg: the RuleResponse message; a
+// `$(...)` reference in the rule message is not restated: no message)
+inline Status deny_handler(const Rule& r, const cond::Ctx& cx, std::string* msg = nullptr) {
   try {
-    return cond::eval_conditions(r.deny, cx) ? FAIL : PASS;
+    std::string cm;
+    const bool deny = cond::eval_conditions_msg(r.deny, cx, &cm);
+    if (msg) {
+      if (!deny) {
+        *msg = "validation rule '" + r.name + "' passed.";
+      } else if (r.vmsg.empty() && cm.empty()) {
+        *msg = "validation error: rule " + r.name + " failed";
+      } else {
+        const std::string j = cond::join_non_empty({r.vmsg, cm}, "; ");
+        if (j.find("$(") != std::string::npos) {
+          msg->clear();
+        } else {
+          try {
+            const JPtr v = cond::substitute_string(j, cx);
+            *msg = (!cond::is_null(v) && v->t == JT::Str)
+                       ? v->s
+                       : "the produced message didn't resolve to a string, check your policy definition.";
+          } catch (const cond::EvalError&) {
+            *msg = cm;  // SubstituteAll failed: the condition message as is
+          } catch (const cond::Unsupported&) {
+            msg->clear();
+          }
+        }
+      }
+    }
+    return deny ? FAIL : PASS;
   } catch (const cond::EvalError&) {
     return ERROR;
   } catch (const cond::Unsupported&) {
@@ -1362,7 +1389,11 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
       bool done = false;
       if (r.pre.present) {  // engine.go:278-286: error => ERROR, false => SKIP
         try {
-          if (!cond::eval_conditions(r.pre, cx)) s = SKIP, done = true;
+          std::string pm;
+          if (!cond::eval_conditions_msg(r.pre, cx, &pm)) {
+            s = SKIP, done = true;
+            if (msgs) (*msgs)[i] = cond::join_non_empty({"preconditions not met", pm}, "; ");
+          }
         } catch (const cond::EvalError&) {
           s = ERROR, done = true;
         } catch (const cond::Unsupported&) {
@@ -1385,7 +1416,7 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
       }
       if (!done) {
         if (r.has_pss) s = pss_handler(r, res, u.kind(), pss_exc);
-        else if (r.has_deny) s = deny_handler(r, cx);
+        else if (r.has_deny) s = deny_handler(r, cx, msgs ? &(*msgs)[i] : nullptr);
         else if (r.pattern || r.any_pattern) {
           PatMsg pm{&r.name, &r.vmsg, msgs ? &(*msgs)[i] : nullptr, &cx};
           s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx, msgs ? &pm : nullptr);

@@ -16,13 +16,14 @@ Restated:
 message (when a `pss_message` callable is given): podSecurity pass "Validation rule '<rule>'
 passed." (validate_pss.go:85), podSecurity fail without exclusions through the C++ oracle's
 FormatChecksPrint (validate_pss.go:108, oracle/pss.hpp format_checks_print), validate.pattern
-pass "validation rule '<rule>' passed." (validate_resource.go:339), validate.deny rules whose
-conditions and preconditions carry no `message` (so the condition message is empty,
-variables/evaluate.go:14-28): pass "validation rule '<rule>' passed." (validate_resource.go:275),
-fail getDenyMessage (validate_resource.go:279-300: the rule message, or "validation error: rule
-<rule> failed" when it is empty; with variables, SubstituteAll through the oracle's JMESPath when a
-`substitute` callable is given), preconditions skip
-"preconditions not met" (engine.go:283); other messages are not restated. Not restated: timestamp, exception
+pass "validation rule '<rule>' passed." (validate_resource.go:339), validate.deny rules: pass
+"validation rule '<rule>' passed." (validate_resource.go:275) and, when their conditions (fail) or
+preconditions (skip) carry no `message` (so the condition message is empty,
+variables/evaluate.go:14-28), fail getDenyMessage (validate_resource.go:279-300: the rule message,
+or "validation error: rule <rule> failed" when it is empty; with variables, SubstituteAll through
+the oracle's JMESPath when a `substitute` callable is given), preconditions skip "preconditions
+not met" (engine.go:283); other messages are not restated (condition messages need the device's
+condition traces: tests/test_cond_messages.py checks them against the C++ oracle). Not restated: timestamp, exception
 and ValidatingAdmissionPolicy branches (out of the path's scope).
 Autogen rules are mapped back to their source rule by the "autogen-" / "autogen-cronjob-"
 prefix (pkg/autogen/autogen.go:213-222); names truncated to 63 characters are not mapped
@@ -104,11 +105,14 @@ def report_results(policies: List[dict], rule_names: List[str], verdict_row, res
                 msg = pss_message(rname, ps0.get("level", ""), ps0.get("version", ""), resource)
             elif not ps0 and val.get("pattern") is not None and cell == 1:
                 msg = f"validation rule '{rname}' passed."
-            elif not ps0 and isinstance(val.get("deny"), dict) and not _cond_messages(val["deny"].get("conditions")) \
-                    and not _cond_messages(_source_rule(pol, rname).get("preconditions")):
+            elif not ps0 and isinstance(val.get("deny"), dict):
                 m = val.get("message") if isinstance(val.get("message"), str) else ""
+                cond_msgs = _cond_messages(val["deny"].get("conditions"))
+                pre_msgs = _cond_messages(_source_rule(pol, rname).get("preconditions"))
                 if cell == 1:
                     msg = f"validation rule '{rname}' passed."
+                elif (cell == 2 and cond_msgs) or (cell == 5 and pre_msgs):
+                    msg = None  # the condition message depends on where the block stopped (traces)
                 elif cell == 2 and not m:
                     msg = f"validation error: rule {rname} failed"
                 elif cell == 2 and "{{" not in m and "$(" not in m:

@@ -149,6 +149,8 @@ int main(int argc, char** argv) {
   pa.ndoc = C.doc.size() / 2, pa.err = &perr;
   pa.key_bytes = kb.data(), pa.key_off = K.off.data(), pa.nkeyd = (uint32_t)K.size();
   a.pat = &pa, a.pvars = PP.vars.data(), a.pvals = pvals.data(), a.nvars = (uint32_t)PP.vars.size();
+  std::vector<uint32_t> mtrace((size_t)C.n * CP.nmsg + 1, 0u);
+  a.nmsg = CP.nmsg, a.mtrace = CP.nmsg ? mtrace.data() : nullptr;
   char nb[2][16];
   std::vector<uint8_t> txt(2 * KPE_TXT_CAP);
   for (int64_t r = 0; r < a.n; ++r) cond_eval_row<true>(a, r, nb, txt.data());  // kpe_cond_kernel's lane body
@@ -158,6 +160,15 @@ int main(int argc, char** argv) {
   FILE* f = fopen(argv[4], "wb");
   fwrite(verdicts.data(), 1, (size_t)C.n * R, f);
   fclose(f);
+  if (argc > 5) {  // condition traces, N x R words (kpe_fetch_cond_traces layout)
+    std::vector<uint32_t> ct((size_t)C.n * R, 0u);
+    for (const KpeCRule& cr : CP.rules)
+      if (cr.mslot)
+        for (int64_t r = 0; r < C.n; ++r) ct[(size_t)r * R + cr.col] = mtrace[(size_t)r * CP.nmsg + cr.mslot - 1u];
+    FILE* g = fopen(argv[5], "wb");
+    fwrite(ct.data(), 4, ct.size(), g);
+    fclose(g);
+  }
   printf("%lld %u\n", (long long)C.n, R);
   return 0;
 }

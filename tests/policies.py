@@ -347,6 +347,79 @@ def cond_policy_set():
              "spec": {"background": True, "validationFailureAction": "Audit", "rules": rules}}]
 
 
+def cond_message_policy_set():
+    """cond_policy_set with a `message` on every condition of its preconditions and deny blocks
+    (kyvernov1.Condition.Message) and rule messages that vary: none, plain text, a substituted
+    resource field, a non-string value and a missing member (getDenyMessage,
+    validate_resource.go:279-300), plus old-style and any + all blocks with messages, some empty,
+    some with variables (substituted only after the join). EvaluateConditions' message
+    (variables/evaluate.go:31-125) depends on where each block stopped."""
+    import copy
+
+    pols = copy.deepcopy(cond_policy_set())
+    obj = "request.object"
+    rmsgs = ["", "m", "{{ " + obj + ".metadata.name }} is denied", "{{ " + obj + ".metadata.labels }}",
+             "x {{ " + obj + ".metadata.nope }}", "kind {{ " + obj + ".kind }}."]
+
+    def tag(block, prefix):
+        if isinstance(block, list):
+            for k, cnd in enumerate(block):
+                cnd["message"] = f"{prefix}{k}" if k % 3 != 2 else ""
+            return
+        for part in ("any", "all"):
+            for k, cnd in enumerate(block.get(part) or []):
+                cnd["message"] = f"{prefix}{part}{k}" + (" {{ " + obj + ".kind }}" if k == 1 else "")
+
+    rules = pols[0]["spec"]["rules"]
+    for i, r in enumerate(rules):
+        v = r["validate"]
+        if "preconditions" in r:
+            tag(r["preconditions"], f"p{i}.")
+        if "deny" in v:
+            tag(v["deny"]["conditions"], f"d{i}.")
+            m = rmsgs[i % len(rmsgs)]
+            if m:
+                v["message"] = m
+            else:
+                v.pop("message", None)
+
+    def c(key, op, value, msg):
+        return {"key": key, "operator": op, "value": value, "message": msg}
+
+    name = "{{ " + obj + ".metadata.name }}"
+    ns = "{{ " + obj + ".metadata.namespace }}"
+    k_ = ("Pod", "Deployment", "Service", "ConfigMap")
+
+    def rule(rn, validate, pre=None):
+        r = {"name": rn, "match": {"any": [{"resources": {"kinds": list(k_)}}]}, "validate": validate}
+        if pre is not None:
+            r["preconditions"] = pre
+        return r
+
+    rules += [
+        # any + all: the true `any` message and every `all` message, or the false ones
+        rule("msg-any-all", {"message": "deny {{ " + obj + ".kind }}", "deny": {"conditions": {
+            "any": [c(name, "Equals", "res-1*", "name-1"), c(ns, "Equals", "ns-0001", "ns-1")],
+            "all": [c("{{ " + obj + ".kind }}", "NotEquals", "Service", "not-svc"),
+                    c(name, "NotEquals", "res-19*", "")]}}}),
+        # old-style deny list: the first false message, else the true ones joined by ";"
+        rule("msg-old-deny", {"deny": {"conditions": [c(name, "Equals", "res-*", "a"), c(ns, "NotEquals", "ns-0003", "b"),
+                                                      c(name, "Equals", "res-2*", "")]}}),
+        # preconditions with messages on a pattern rule (its skip) and an old-style list
+        rule("msg-pre-pattern", {"message": "m", "pattern": {"metadata": {"name": "res-*"}}},
+             pre={"any": [c(ns, "Equals", "ns-0001", "in ns-1"), c(name, "Equals", "res-3*", "name res-3")],
+                  "all": [c("{{ " + obj + ".kind }}", "Equals", "Pod", "a pod")]}),
+        rule("msg-pre-old", {"message": "m", "deny": {"conditions": {"all": [c(name, "Equals", "res-1*", "res-1 {{ " + obj + ".kind }}")]}}},
+             pre=[c("{{ " + obj + ".kind }}", "NotEquals", "ConfigMap", "not a cm"), c(ns, "NotEquals", "ns-0002", "")]),
+        # a deny block whose messages are all empty, and one holding only a variable message
+        rule("msg-empty", {"deny": {"conditions": {"any": [c(name, "Equals", "res-1*", ""), c(ns, "Equals", "ns-0002", "")]}}}),
+        rule("msg-var-only", {"deny": {"conditions": {"all": [c(ns, "Equals", "ns-000*", "{{ " + obj + ".metadata.namespace }}")]}}}),
+        rule("msg-var-missing", {"message": "r", "deny": {"conditions": {"all": [c(ns, "Equals", "ns-000*",
+                                                                                   "{{ " + obj + ".metadata.zzz }}")]}}}),
+    ]
+    return pols
+
+
 def var_policy_set():
     """Pattern rules with {{ }} variables (substitutePatterns, validate_resource.go:456-476) and
     foreach entries with pattern / anyPattern / nested foreach bodies (validate_resource.go:
