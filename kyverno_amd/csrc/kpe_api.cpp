@@ -173,6 +173,7 @@ struct DeviceProgram {
   // pattern rules: compiled trees + operand records (program.hpp PatProgram)
   DevBuf pnodes, plists, pleaves, pconds, ppats, pbytes, proots, prules;
   DevBuf plslot, pslot_leaf;  // leaf-table slot per leaf, leaf per slot (PatArgs::lslot)
+  std::vector<uint32_t> lslot_h;  // host copy of plslot (bound into the scalar-leaf members' w)
   uint32_t nlslots = 0;
   bool ltab_all = false;  // every leaf has a slot or is PL_NEVER: the pattern kernel's LT instance
   DevBuf pvars, ptmpl, ttext;  // pattern variables: slots, template pieces, template texts
@@ -621,6 +622,7 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
       D.ltab_all = all && D.nlslots > 0;
       if (slot_leaf.empty()) slot_leaf.push_back(0);
       HIPCHK(upload(D.plslot, lslot, s0));
+      D.lslot_h = lslot;
       HIPCHK(upload(D.pslot_leaf, slot_leaf, s0));
     }
     HIPCHK(upload(D.pconds, PP.conds, s0));
@@ -1058,6 +1060,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     for (size_t i = 0; i < mem.size(); i += 4) {
       mem[i + 1] = kid[mem[i + 1]] < 0 || (mem[i] & PMF_VKEY) ? 0u : (uint32_t)kid[mem[i + 1]] + 1u;
       if (mem[i] & PMF_GLOB) mem[i + 3] = loc((int32_t)mem[i + 3]);
+      else if ((mem[i] & PMF_LEAF) && !(mem[i] & PMF_VKEY))  // the leaf's table slot (schema.h PMF_LEAF)
+        mem[i + 3] = PD.lslot_h.empty() ? KPE_NO_LSLOT : PD.lslot_h[PP.nodes[mem[i + 2]].y];
     }
     HIPCHK(upload(B.pmembers, mem, s));
     B.pargs_valid = false;

@@ -507,6 +507,17 @@ __device__ __forceinline__ bool pat_leaf(const PatArgs& a, uint32_t sid, uint32_
   return pat_leaf_eval(a, sid, li, pv, und);
 }
 
+// pat_leaf of a scalar-leaf member m (leaf li): its bound table slot (m.w) instead of lslot[li]
+template <bool LT = false>
+__device__ __forceinline__ bool pat_leaf_mem(const PatArgs& a, uint32_t sid, const uint4& m, uint32_t li,
+                                             const uint2* pv, uint32_t* und) {
+  if (m.x & (PMF_GLOB | PMF_VKEY)) return pat_leaf<LT>(a, sid, li, pv, und);
+  if (sid == kNoNode) return false;
+  if (LT) return m.w != KPE_NO_LSLOT && ((a.ltab[(size_t)m.w * a.ltab_words + (sid >> 5)] >> (sid & 31u)) & 1u);
+  if (a.ltab && m.w != KPE_NO_LSLOT) return (a.ltab[(size_t)m.w * a.ltab_words + (sid >> 5)] >> (sid & 31u)) & 1u;
+  return pat_leaf_eval(a, sid, li, pv, und);
+}
+
 // scalar id of node c (kNoNode for maps / lists); an absent member is null
 __device__ __forceinline__ uint32_t node_sid(const PatArgs& a, DocView doc, uint32_t c) {
   if (c == kNoNode) return SC_NULL_ID;
@@ -700,7 +711,7 @@ struct PatVMT {
             if (!pat_leaf<LT>(a, node_sid(a, doc, c), vn.y, pv, &und)) v1 = PE_OTHER;
         } else {
           const uint32_t sid = j == 8u ? SC_NULL_ID : (DN_KIND(x.x) == DN_SCALAR ? x.y : kNoNode);
-          v1 = pat_leaf<LT>(a, sid, vn.y, pv, &und) ? PE_OK : PE_OTHER;
+          v1 = pat_leaf_mem<LT>(a, sid, m, vn.y, pv, &und) ? PE_OK : PE_OTHER;
         }
         ek = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
       }
@@ -737,9 +748,16 @@ struct PatVMT {
               if (!pat_leaf<LT>(a, node_sid(a, doc, c), pn.y, pv, &und)) v = PE_OTHER;
           }
         } else if (pn.kind == PN_MAP) {
+          const uint32_t pw = pn.w & PNW_DEPTH;
           if (rk != DN_MAP) {
             v = PE_OTHER;
-          } else if (KPE_PAT_FLAT && !TRACE && pn.w && pn.w <= (uint32_t)KPE_PAT_FLAT &&
+          } else if (!TRACE && (pn.w & PNW_CHAIN) && !(pw && pw <= (uint32_t)KPE_PAT_FLAT)) {
+            // one plain member: its value's verdict is the map's (no frame; TRACE walks keep the
+            // frame for the member's path component)
+            const uint4 m = PU(a.members, pn.y, a.nmembers, 2);
+            br = pat_lookup(a, doc, br, m.y), bpi = m.z, state = VM_BEGIN;
+            continue;
+          } else if (KPE_PAT_FLAT && !TRACE && pw && pw <= (uint32_t)KPE_PAT_FLAT &&
                      (v = flat_map<KPE_PAT_FLAT>(doc[PVD(br)].y, pn)) != PE_NONE) {
             // resolved from the body in registers
           } else {
@@ -839,7 +857,7 @@ struct PatVMT {
                 // a scalar pattern against a scalar / absent value resolves in place: BEGIN's
                 // pattern.Validate and RET's anchor mapping without the two VM round trips
                 const uint32_t li = PU(a.nodes, m.z, a.nnodes, 1).y;
-                const uint32_t v1 = pat_leaf<LT>(a, node_sid(a, doc, c), li, pv, &und) ? PE_OK : PE_OTHER;
+                const uint32_t v1 = pat_leaf_mem<LT>(a, node_sid(a, doc, c), m, li, pv, &und) ? PE_OK : PE_OTHER;
                 if (TRACE && v1 == PE_OTHER) snap(sp, mcomp(F.r, m0 + k));
                 e = (h == PM_COND || h == PM_GLOBAL) ? (v1 == PE_OK ? PE_OK : PE_SKIP) : v1;
               } else {

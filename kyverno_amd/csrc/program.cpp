@@ -958,10 +958,13 @@ class PatCompiler {
         depth_in = 0;
       } else if (h != PM_NEG && !(x & (PMF_STAR | PMF_LEAF))) {  // a map (or list) value
         const KpePNode& c = PP.nodes[mem[i + 2]];
-        depth_in = (c.kind == PN_MAP && c.w && c.w < PNF_MAXDEPTH) ? std::max(depth_in, c.w + 1u) : 0u;
+        const uint32_t cw = c.w & PNW_DEPTH;
+        depth_in = (c.kind == PN_MAP && cw && cw < PNF_MAXDEPTH) ? std::max(depth_in, cw + 1u) : 0u;
       }
     }
-    return push_node({PN_MAP, m0, (uint32_t)first.size() | ((uint32_t)order.size() << 16), depth_in});
+    const bool chain = mem.size() == 4 && first.empty() && mem[0] == PM_DEFAULT && PP.nodes[mem[2]].kind != PN_LEAF;
+    return push_node({PN_MAP, m0, (uint32_t)first.size() | ((uint32_t)order.size() << 16),
+                      depth_in | (chain ? PNW_CHAIN : 0u)});
   }
 };
 

@@ -551,6 +551,11 @@ typedef struct KpePNode {
 // per member.
 #define PNF_FLAT 1u
 #define PNF_MAXDEPTH 3u
+#define PNW_DEPTH 0xFFu       // KpePNode::w of a map: the inline depth bits
+#define PNW_CHAIN (1u << 8)   // a map whose only member is a plain key (default handler, no flags)
+                              // with a map / list value: validateMap's verdict is that value's
+                              // (validate.go:118-175 with one member, anchor/handlers.go:23-41), so
+                              // the walk descends to it without a frame
 // Pattern member (uint4): x = handler | PMF_* | slot << 8, y = member-name id + 1 (per
 // binding; 0 = name absent from the corpus), z = value node, w = glob-key predicate
 // location (PMF_GLOB) or PRED_NONE
@@ -564,7 +569,8 @@ typedef struct KpePNode {
 #define PMF_STAR (1u << 3)   // default handler whose value is the string "*" (presence check)
 #define PMF_GLOB (1u << 4)   // ExpandInMetadata: first resource member matching the glob (string values)
 #define PMF_SLOT (1u << 5)   // condition / existence anchor tracked in the AnchorMap
-#define PMF_LEAF (1u << 6)   // the member's pattern value is a scalar leaf (PN_LEAF)
+#define PMF_LEAF (1u << 6)   // the member's pattern value is a scalar leaf (PN_LEAF); bound: w = its
+                             // leaf-table slot (PatArgs::lslot of the leaf) unless PMF_GLOB / PMF_VKEY
 #define PMF_VSTAR (1u << 7)  // default-handler member whose leaf has variables: a value of "*"
                              // is the presence check (anchor/handlers.go:130-133)
 #define PM_SLOT(x) (((x) >> 8) & 31u)

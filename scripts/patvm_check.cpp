@@ -175,6 +175,8 @@ int main(int argc, char** argv) {
     uint8_t* keep = a.verdicts;
     a.verdicts = lt_v.data();
     a.lslot = lslot.data(), a.ltab = ltab.data(), a.ltab_words = words;
+    for (auto& m : mem)  // scalar-leaf members carry their slot, as kpe_api.cpp binds them
+      if ((m.x & PMF_LEAF) && !(m.x & (PMF_GLOB | PMF_VKEY))) m.w = lslot[PP.nodes[m.z].y];
     std::vector<uint32_t> plane(FramesLds::kWords * FramesLds::kDepth * 64u, 0xDEADBEEFu);
     for (int64_t r = 0; r < a.n; ++r) {
       if (all && !slot_leaf.empty()) pat_eval_row<FramesLds, true>(a, r, FramesLds{plane.data()});

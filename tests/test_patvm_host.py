@@ -69,28 +69,30 @@ def test_patvm_host_matches_oracle(harness, oracle, tmp_path, name, pols, nd):
     assert bad.size == 0, f"{len(bad)} cells differ, first {bad[:5].tolist()}"
 
 
-def _nest(depth, leaf):
+def _nest(depth, leaf, side=None):
     v = leaf
     for _ in range(depth):
-        v = {"a": v}
+        v = {"a": v} if side is None else {"a": v, "b": side}
     return v
 
 
 def test_caps_are_undecided_cells(harness, oracle, tmp_path):
     """Past the lane's frame stack (pattern and resource both nested deeper) or past the 32
     AnchorMap slots, a cell is KPE_UNDECIDED (7) instead of the policy being refused; every
-    other cell stays bit-exact."""
-    deep = _policy_for("deep", {"spec": _nest(16, {"x": "1"})})
+    other cell stays bit-exact. A chain of one-member maps needs no frames (schema.h PNW_CHAIN):
+    as deep, it is decided."""
+    deep = _policy_for("deep", {"spec": _nest(16, {"x": "1"}, side="*")})
     many = _policy_for("many", {"spec": {**{f"(k{i})": "v*" for i in range(34)}, "x": "?*"}})
+    chain = _policy_for("chain", {"spec": _nest(16, {"x": "1"})})
     docs = []
     for i in range(40):
-        spec = _nest(16, {"x": str(i % 3)}) if i % 4 == 0 else ({"a": "flat"} if i % 4 == 1 else None)
+        spec = _nest(16, {"x": str(i % 3)}, side="s") if i % 4 == 0 else ({"a": "flat"} if i % 4 == 1 else None)
         d = {"apiVersion": "v1", "kind": "Thing", "metadata": {"name": f"d{i}"}}
         if spec is not None:
             d["spec"] = dict(spec, **({f"k{j}": "v1" for j in range(i % 5)} if i % 4 == 1 else {}))
         docs.append(d)
     nd = "\n".join(json.dumps(d) for d in docs).encode()
-    pols = [deep, many]
+    pols = [deep, many, chain]
     pj, rj, vb = tmp_path / "p.json", tmp_path / "r.ndjson", tmp_path / "v.bin"
     pj.write_text(json.dumps(pols))
     rj.write_bytes(nd)
@@ -104,3 +106,4 @@ def test_caps_are_undecided_cells(harness, oracle, tmp_path):
     assert und[:, 0].tolist() == deep_rows.tolist()  # only resources as deep as the pattern
     has_spec = np.array([d.get("spec") is not None for d in docs])
     assert und[:, 1].tolist() == has_spec.tolist()  # any resource whose spec map is visited
+    assert not und[:, 2].any() and (ref[:, 2] == 2).sum() >= 10  # the chain walk: every cell decided
