@@ -285,7 +285,7 @@ def main(argv=None):
 
     # ---- per-kernel timing pass: the timed region's K steps again, with HIP events around every
     # launch on the library's stream (launches serialised there, so each duration is its own; a
-    # multi-shard LEAN5 launch covers several steps) ----
+    # multi-shard LEAN launch covers several steps) ----
     eng.evaluate_batch_async(ps, rotation)
     eng.device.sync()
     eng.device.set_timing(True)

@@ -185,9 +185,10 @@ kpe_status kpe_evaluate_async_ex(kpe_device* dev, const kpe_program* prog, const
 /* n evaluations enqueued by one call, corpora cs[0 .. n-1] in order (a corpus may repeat), each
  * with the results kpe_evaluate_async_ex(dev, prog, cs[i], flags) gives: the batch form a scanner
  * driving many resident shards (or a benchmark) uses instead of n foreign-function calls. A run of
- * consecutive warm shards whose evaluation is the LEAN5 scan alone (a bound kind-only podSecurity
- * program, no later kernels) goes out as ceil(m / 64) multi-shard launches of
- * kpe_lean5_batch_kernel: one grid over the shards' tiles instead of one launch per shard. */
+ * consecutive warm shards whose evaluation is the LEAN evaluation alone (a bound kind-only
+ * podSecurity program, no later kernels) goes out as ceil(m / 24) multi-shard launches of
+ * kpe_lean6_kernel: one grid over the shards' tiles instead of one launch per shard. Every launch
+ * evaluates each pod's PSA checks from its pod, container, volume, sysctl and annotation columns. */
 kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, const kpe_corpus* const* cs, int n,
                                     unsigned flags);
 kpe_status kpe_device_sync(kpe_device* dev);
@@ -341,7 +342,7 @@ long kpe_report_results_ex(const kpe_report_args* args, char* buf, size_t cap);
 /* ---- instrumentation (HIP events on the evaluation stream) ---------------- */
 typedef struct kpe_kernel_stats {
   uint64_t launches;        /* timed launches since the last reset: one per evaluation, one per
-                               multi-shard LEAN5 launch of kpe_evaluate_batch_async */
+                               multi-shard LEAN launch of kpe_evaluate_batch_async */
   double pss_kernel_ms;     /* summed duration of the resource-scan kernel      */
   double dict_kernel_ms;    /* summed duration of the dictionary predicate pass */
   double scan_bytes;        /* algorithmic bytes one scan-kernel launch reads+writes */
@@ -352,7 +353,7 @@ typedef struct kpe_kernel_stats {
                                matrix read and written */
   int32_t scan_kernel;      /* the scan instantiation of the last timed launch: 1 kpe_scan_kernel
                                (general), 2 its LEAN instantiation (corpora past 4 GiB of pod
-                               records), 7 kpe_lean5_kernel, 9 kpe_lean5_batch_kernel */
+                               records), 7 kpe_lean6_kernel (one shard), 9 kpe_lean6_kernel (a multi-shard launch) */
   int32_t pad_;
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);

@@ -161,7 +161,7 @@ struct ScanArgs {
   uint32_t pimg_words, capb_lds;
   // LEAN scans (kind-only match terms): kt[kind id] = matched-rule mask (PRED_NONE: no table)
   uint32_t kt_lds, nkinds;
-  const uint32_t* psum;  // LEAN5: per-pod scan records (3 words per pod: pod word, failing versioned checks, kind << 16)
+  const uint32_t* psum;  // PSUM general scan: per-pod scan records (3 words per pod: pod word, failing versioned checks, kind << 16)
   // Selector requirement masks (selm bit 0: label selectors, bit 1: namespaceSelectors; built
   // per binding by kpe_selmask_kernel). Requirement q of a selector is bit qbit + q. Label
   // selectors: sel_km[key id] = {requirements whose key glob holds, wildcard requirements whose

@@ -209,7 +209,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t pimg_words = 0, capb_lds = 0;
   size_t prep_dyn_bytes = 0;  // the prep kernel's LDS: the scan layout + the fuse area
   bool lean = false;  // LEAN scan instantiation (kind table; no check masks)
-  int lean_kind = 0;  // kpe_launch_scan narrow code of the LEAN scan: 7 kpe_lean5_kernel, 2 the template
+  int lean_kind = 0;  // kpe_launch_scan narrow code of the LEAN scan: 7 kpe_lean6_kernel, 2 the template
   int gen_code = 0;   // narrow code of the general scan: narrow | 4 with scan records (PSUM)
   uint32_t kt_lds = PRED_NONE, nkinds = 0;
   DevBuf xexcl, ann_norm, rf_ann, xargs;  // podSecurity exclusions: resolved excludes, key tables, PssxArgs
@@ -1720,8 +1720,8 @@ kpe_status kpe_evaluate_batch_async(kpe_device* dev, const kpe_program* prog, co
   if (flags & ~(unsigned)(KPE_EVAL_MASKS | KPE_EVAL_COLD)) return fail(KPE_E_INVALID, "unknown evaluation flags");
   std::lock_guard<std::mutex> lk(dev->mu);
   const bool masks = (flags & KPE_EVAL_MASKS) != 0, cold = (flags & KPE_EVAL_COLD) != 0;
-  // Consecutive shards whose evaluation is the LEAN5 scan alone go out as multi-shard launches
-  // (kpe_lean5_batch_kernel); any other shard is launched on its own, in order.
+  // Consecutive shards whose evaluation is the LEAN evaluation alone go out as multi-shard launches
+  // (kpe_lean6_kernel); any other shard is launched on its own, in order.
   std::vector<kpe_corpus*> run;
   for (int i = 0; i < n; ++i) {
     if (kpe_status st = prepare(dev, prog, cs[i], masks)) return st;

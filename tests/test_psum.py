@@ -1,11 +1,11 @@
-"""The per-pod PSA summary (kyverno_amd/csrc/lean.inl kpe_psa_dict_kernel -> kpe_psa_capset_kernel
--> kpe_psum_kernel), which kpe_lean5_kernel reads in place of each pod's container / volume /
-sysctl / annotation lists. Every PSA v0.29 check is "some item of the pod is in state s" for
+"""The per-pod PSA summary (kyverno_amd/csrc/lean.inl: kpe_psa_codes_kernel's dictionary codes, then
+kpe_psum_kernel's per-pod pass, the same OR-reduction kpe_lean6_kernel runs inside every LEAN
+evaluation) over each pod's container / volume / sysctl / annotation lists. Every PSA v0.29 check is "some item of the pod is in state s" for
 fixed sets s (pss_fixed.hpp), so the summary is the OR of the items' codes.
 
 Pinned two ways: digests of the summary over seeded corpora and the reference's PSS fixtures
 (tests/golden/psum_digests.json, from the host restatement scripts/psum_check.cpp, which is the
-flattener's round-3 summary moved verbatim), and, semantically, by the LEAN5 full-matrix tests in
+flattener's round-3 summary moved verbatim), and, semantically, by the LEAN full-matrix tests in
 tests/test_gpu_parity.py (every versioned check's failure reaches the check masks)."""
 import hashlib
 import json
