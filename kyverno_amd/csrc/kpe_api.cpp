@@ -149,6 +149,13 @@ struct kpe_device {
   bool no_cache = false, patvm_err = false;
   uint64_t lean_min_waves = 16384;  // 256 CUs x 4 SIMDs x 16 waves
   uint32_t lean_tpw = 0;
+  // pinned staging for corpus uploads (two halves, double-buffered; allocated on first use): a
+  // pageable hipMemcpyAsync is staged by the runtime chunk by chunk, a pinned one is one DMA
+  static constexpr size_t kStageHalf = 16u << 20;
+  char* stage = nullptr;
+  hipEvent_t stage_ev[2] = {};
+  bool stage_busy[2] = {};
+  int stage_cur = 0;
   hipEvent_t get_ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -318,6 +325,10 @@ void kpe_device_close(kpe_device* d) {
     (void)hipEventDestroy(p.d);
   }
   for (auto e : d->pool) (void)hipEventDestroy(e);
+  if (d->stage) {
+    (void)hipHostFree(d->stage);
+    for (auto e : d->stage_ev) (void)hipEventDestroy(e);
+  }
   for (int k = 0; k < d->nlanes; ++k) (void)hipStreamDestroy(d->lanes[k]);
   delete d;
 }
@@ -415,6 +426,41 @@ void kpe_corpus_free(kpe_corpus* c) {
   delete c;
 }
 
+}  // extern "C"
+
+// Copy v into b (allocated with the upload() slack) through the device's pinned staging halves:
+// the CPU fills one half while the DMA drains the other. The caller synchronises the stream.
+template <class T>
+hipError_t upload_staged(kpe_device* dev, DevBuf& b, const std::vector<T>& v, hipStream_t s) {
+  const size_t n = v.size() * sizeof(T);
+  hipError_t e = b.ensure(n + 128);
+  if (e != hipSuccess || n == 0) return e;
+  if (!dev->stage) {
+    e = hipHostMalloc(reinterpret_cast<void**>(&dev->stage), 2 * kpe_device::kStageHalf, hipHostMallocDefault);
+    if (e != hipSuccess) {
+      dev->stage = nullptr;
+      return hipMemcpyAsync(b.p, v.data(), n, hipMemcpyHostToDevice, s);  // pageable copy
+    }
+    for (auto& ev : dev->stage_ev) (void)hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+  }
+  const char* src = reinterpret_cast<const char*>(v.data());
+  for (size_t off = 0; off < n;) {
+    const size_t k = std::min(kpe_device::kStageHalf, n - off);
+    const int h = dev->stage_cur;
+    if (dev->stage_busy[h] && (e = hipEventSynchronize(dev->stage_ev[h])) != hipSuccess) return e;
+    char* dst = dev->stage + (size_t)h * kpe_device::kStageHalf;
+    memcpy(dst, src + off, k);
+    if ((e = hipMemcpyAsync(static_cast<char*>(b.p) + off, dst, k, hipMemcpyHostToDevice, s)) != hipSuccess) return e;
+    if ((e = hipEventRecord(dev->stage_ev[h], s)) != hipSuccess) return e;
+    dev->stage_busy[h] = true;
+    dev->stage_cur ^= 1;
+    off += k;
+  }
+  return hipSuccess;
+}
+
+extern "C" {
+
 kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   if (!dev || !cc) return fail(KPE_E_INVALID, "null argument");
   std::lock_guard<std::mutex> lk(dev->mu);
@@ -424,6 +470,7 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   auto& D = *cc->d;
   D.ordinal = dev->ordinal;
   hipStream_t s = dev->stream;
+  const auto upload = [dev](DevBuf& b, const auto& v, hipStream_t st) { return upload_staged(dev, b, v, st); };
   for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
     HIPCHK(upload(D.dict_bytes[i], C.dict[i].bytes, s));
     HIPCHK(upload(D.dict_off[i], C.dict[i].off, s));

@@ -56,7 +56,7 @@ for st in "$@"; do
           python3 bench.py --config "$a1" ${x//,/ }
       done
       run "traffic_${a1}_summary" 60 python3 scripts/pmc_summary.py --dir "$O/traffic_$a1" --kernel "$a2" \
-        --out "$O/pmc_traffic_$a1.json" ;;  # copy into perf/ (bench.py reads it there) after the call
+        --out "$O/pmc_traffic_$a1.json" --bench-log "$O/traffic_${a1}_WRITE_SIZE.log" ;;  # copy into perf/ (bench.py reads it there) after the call
     ranks)
       KPE_DIST_BACKEND=gloo run "ranks_$a1" 400 python bench.py --gpus "$a1" ${a2//,/ }
       grep '^{' "$O/ranks_$a1.log" > "$O/ranks_$a1.json" ;;

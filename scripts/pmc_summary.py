@@ -4,8 +4,9 @@
     pmc_summary.py --dir <rocprofv3 -d dir> --kernel <name prefix> --out <json>
 
 Reads every *counter_collection.csv under --dir (one pass per counter: a TCC block cannot hold both,
-MI355X_MICROARCH.md), averages each counter over the dispatches of the kernels whose name starts
-with --kernel, and writes {fetch, write, bytes per launch}. Units: FETCH_SIZE / WRITE_SIZE are KiB;
+MI355X_MICROARCH.md), takes each counter's median over the dispatches of the kernels whose name
+starts with --kernel (a pass's bench run also launches other legs of the same kernel, e.g. the
+masks mode), and writes {fetch, write, bytes per launch}. Units: FETCH_SIZE / WRITE_SIZE are KiB;
 gfx950 correction (MI355X_MICROARCH.md § HBM): FETCH_SIZE reports half the bytes of a wide
 coalesced streaming read, so it is doubled; WRITE_SIZE is taken as is. bench.py reports the result
 as roofline.traffic when its kernel is the one measured (perf/pmc_traffic_<config>.json).
@@ -27,6 +28,8 @@ def main():
     ap.add_argument("--dir", required=True)
     ap.add_argument("--kernel", required=True)
     ap.add_argument("--out", required=True)
+    ap.add_argument("--bench-log", default="", help="the pass's bench.py output: its roofline.alg_bytes_per_launch "
+                                                     "(the same launches) gives traffic / algorithmic bytes")
     a = ap.parse_args()
     agg = collections.defaultdict(list)
     for f in glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True):
@@ -37,13 +40,13 @@ def main():
         for (k, c), v in sorted(agg.items()):
             o.write(f'"{k}",{c},{sum(v) / len(v):.1f},{len(v)}\n')
 
-    def mean(counter):
+    def mean(counter):  # the median dispatch: a pass mixes leg kinds (e.g. masks-mode launches)
         vals, names = [], set()
         for (k, c), v in agg.items():
             if c == counter and k.startswith(a.kernel):
                 vals += v
                 names.add(k)
-        return (sum(vals) / len(vals), len(vals), sorted(names)) if vals else None
+        return (sorted(vals)[len(vals) // 2], len(vals), sorted(names)) if vals else None
 
     fm, wm = mean("FETCH_SIZE"), mean("WRITE_SIZE")
     if fm is None or wm is None:
@@ -53,6 +56,13 @@ def main():
          "scan_bytes_per_launch": fm[0] * 1024 * 2 + wm[0] * 1024,
          "correction": "FETCH_SIZE x2 (gfx950 half-count of wide coalesced reads), KiB -> bytes",
          "source": a.dir}
+    if a.bench_log and os.path.exists(a.bench_log):
+        for line in open(a.bench_log):
+            if line.startswith("{"):
+                alg = (json.loads(line).get("roofline") or {}).get("alg_bytes_per_launch")
+                if alg:  # bench.py scales this ratio to its own launches' algorithmic bytes
+                    t["alg_bytes_per_launch"] = alg
+                    t["traffic_ratio"] = t["scan_bytes_per_launch"] / alg
     json.dump(t, open(a.out, "w"), indent=1)
     print("traffic", t["kernel"], t["scan_bytes_per_launch"])
 
