@@ -51,12 +51,22 @@ struct Dict {
   }
   uint32_t size() const { return (uint32_t)(off.size() - 1); }
   std::string_view at(uint32_t i) const { return std::string_view(bytes.data() + off[i], off[i + 1] - off[i]); }
-
- private:
-  struct Slot {
-    uint32_t h, id1;  // high hash bits, id + 1 (0: empty)
-  };
-  std::vector<Slot> slots;
+  // lookup with the string's hash already known (read-only: safe from several threads)
+  int64_t find_h(std::string_view s, uint64_t h) const {
+    if (slots.empty()) return -1;
+    const size_t mask = slots.size() - 1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const Slot& e = slots[i];
+      if (e.id1 == 0) return -1;
+      if (e.h == (uint32_t)(h >> 32) && at(e.id1 - 1) == s) return (int64_t)(e.id1 - 1);
+    }
+  }
+  // Rebuild the index over every id from their hashes (hs[id]) on up to nth threads: the slot
+  // table is cut into nth contiguous ranges, each thread places the ids whose home slot is in its
+  // range and defers those whose probe would leave it; the deferred ones are placed afterwards.
+  // The result is a valid linear-probing table (every id at or after its home slot, no empty slot
+  // between), like inserting them one by one.
+  void reindex(const std::vector<uint64_t>& hs, unsigned nth);  // flatten.cpp
   static uint64_t hash(std::string_view s) {  // 64-bit FNV-1a over 8-byte words, then a finalizer
     uint64_t h = 0xcbf29ce484222325ull ^ s.size();
     size_t i = 0;
@@ -69,6 +79,12 @@ struct Dict {
     h ^= h >> 33, h *= 0xff51afd7ed558ccdull, h ^= h >> 33, h *= 0xc4ceb9fe1a85ec53ull, h ^= h >> 33;
     return h;
   }
+
+ private:
+  struct Slot {
+    uint32_t h, id1;  // high hash bits, id + 1 (0: empty)
+  };
+  std::vector<Slot> slots;
   void put(uint64_t h, uint32_t id) {
     const size_t mask = slots.size() - 1;
     size_t i = h & mask;

@@ -18,6 +18,8 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <atomic>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -1623,11 +1625,183 @@ void grow(std::vector<T>& v, size_t n) {
   v.resize(v.size() + n);
 }
 
+// f(i) for i in [0, n) on up to nth threads (dynamic assignment)
+template <class F>
+void parallel_for(size_t n, unsigned nth, F f) {
+  const unsigned T = (unsigned)std::min<size_t>(n, std::max(1u, nth));
+  if (T <= 1) {
+    for (size_t i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::vector<std::exception_ptr> err(T);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t)
+    th.emplace_back([&, t] {
+      try {
+        for (size_t i; (i = next.fetch_add(1)) < n;) f(i);
+      } catch (...) {
+        err[t] = std::current_exception();
+        next = n;  // the others stop at their next item
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+}
+
+// Dictionary domain d of every part merged into G in document order on up to nth threads, with
+// the ids a sequential merge (G.intern of each part's strings in order) gives: a string's id is
+// its first occurrence's rank. Strings are hash-partitioned into buckets, each bucket's thread
+// finds every string's first occurrence (or its id in G) walking the parts in order; the parts
+// then number their first occurrences in local order after G's size plus the earlier parts'
+// counts, references take their first occurrence's id, the bytes are appended per part, and the
+// index is rebuilt in parallel (Dict::reindex). dmap[t][d][i]: G id of part t's string i.
+void merge_dict_parallel(Dict& G, std::vector<Corpus>& parts, int d,
+                         std::vector<std::vector<std::vector<uint32_t>>>& dmap, unsigned nth) {
+  const size_t T = parts.size();
+  constexpr uint32_t kB = 64, kFirst = 0xFFFFFFFEu, kRef = 0xFFFFFFFDu;
+  std::vector<std::vector<uint64_t>> hs(T), ref(T);
+  std::vector<std::vector<std::vector<uint32_t>>> lists(T, std::vector<std::vector<uint32_t>>(kB));
+  parallel_for(T, nth, [&](size_t t) {
+    const Dict& D = parts[t].dict[d];
+    hs[t].resize(D.size());
+    ref[t].assign(D.size(), ~0ull);
+    dmap[t][d].assign(D.size(), kFirst);
+    for (uint32_t i = 0; i < D.size(); ++i) {
+      const uint64_t h = Dict::hash(D.at(i));
+      hs[t][i] = h;
+      lists[t][h >> 58].push_back(i);
+    }
+  });
+  const bool gempty = G.size() == 0;
+  parallel_for(kB, nth, [&](size_t b) {
+    size_t n = 0;
+    for (size_t t = 0; t < T; ++t) n += lists[t][b].size();
+    size_t cap = 16;
+    while (cap < n * 2) cap *= 2;
+    std::vector<uint64_t> tab(cap, ~0ull);  // first occurrences: t << 32 | i
+    const size_t mask = cap - 1;
+    for (size_t t = 0; t < T; ++t) {
+      const Dict& D = parts[t].dict[d];
+      for (uint32_t i : lists[t][b]) {
+        const std::string_view sv = D.at(i);
+        const uint64_t h = hs[t][i];
+        if (!gempty) {
+          const int64_t g = G.find_h(sv, h);
+          if (g >= 0) {
+            dmap[t][d][i] = (uint32_t)g;
+            continue;
+          }
+        }
+        for (size_t k = h & mask;; k = (k + 1) & mask) {
+          const uint64_t e = tab[k];
+          if (e == ~0ull) {
+            tab[k] = (uint64_t)t << 32 | i;  // dmap stays kFirst
+            break;
+          }
+          const size_t t0 = (size_t)(e >> 32);
+          const uint32_t i0 = (uint32_t)e;
+          if (hs[t0][i0] == h && parts[t0].dict[d].at(i0) == sv) {
+            ref[t][i] = e;
+            dmap[t][d][i] = kRef;
+            break;
+          }
+        }
+      }
+    }
+  });
+  // first occurrences per part -> ids; their bytes
+  std::vector<size_t> nf(T, 0), nb(T, 0);
+  std::vector<std::vector<uint8_t>> first(T);
+  parallel_for(T, nth, [&](size_t t) {
+    const Dict& D = parts[t].dict[d];
+    first[t].assign(D.size(), 0);
+    for (uint32_t i = 0; i < D.size(); ++i)
+      if (dmap[t][d][i] == kFirst) first[t][i] = 1, ++nf[t], nb[t] += D.at(i).size();
+  });
+  const uint32_t g0 = G.size();
+  std::vector<size_t> idb(T + 1, g0), byb(T + 1, G.bytes.size());
+  for (size_t t = 0; t < T; ++t) idb[t + 1] = idb[t] + nf[t], byb[t + 1] = byb[t] + nb[t];
+  if (byb[T] > 0xFFFFFFFFull) throw LimitError("a dictionary's text exceeds 4 GiB");
+  G.bytes.resize(byb[T]);
+  G.off.resize(idb[T] + 1);
+  parallel_for(T, nth, [&](size_t t) {
+    const Dict& D = parts[t].dict[d];
+    uint32_t id = (uint32_t)idb[t];
+    size_t pos = byb[t];
+    for (uint32_t i = 0; i < D.size(); ++i) {
+      if (!first[t][i]) continue;
+      const std::string_view sv = D.at(i);
+      memcpy(G.bytes.data() + pos, sv.data(), sv.size());
+      pos += sv.size();
+      G.off[id + 1] = (uint32_t)pos;
+      dmap[t][d][i] = id++;
+    }
+  });
+  parallel_for(T, nth, [&](size_t t) {  // references: their first occurrence's id (an earlier part or index)
+    for (uint32_t i = 0; i < dmap[t][d].size(); ++i)
+      if (dmap[t][d][i] == kRef) {
+        const uint64_t e = ref[t][i];
+        dmap[t][d][i] = dmap[(size_t)(e >> 32)][d][(uint32_t)e];
+      }
+  });
+  std::vector<uint64_t> gh(G.size());
+  parallel_for((g0 + 4095) / 4096, nth, [&](size_t c) {
+    for (uint32_t id = (uint32_t)(c * 4096); id < g0 && id < (c + 1) * 4096; ++id) gh[id] = Dict::hash(G.at(id));
+  });
+  parallel_for(T, nth, [&](size_t t) {
+    for (uint32_t i = 0; i < first[t].size(); ++i)
+      if (first[t][i]) gh[dmap[t][d][i]] = hs[t][i];
+  });
+  G.reindex(gh, nth);
+}
+
+}  // namespace
+
+void Dict::reindex(const std::vector<uint64_t>& hs, unsigned nth) {
+  const size_t n = size();
+  size_t cap = 64;
+  while (cap < (n + 1) * 2) cap *= 2;
+  slots.assign(cap, Slot{0u, 0u});
+  const size_t mask = cap - 1;
+  unsigned P = 1;
+  while (P * 2 <= std::max(1u, nth) && cap / (P * 2) >= 4096) P *= 2;
+  const size_t span = cap / P;
+  std::vector<size_t> cnt(P + 1, 0);
+  for (size_t id = 0; id < n; ++id) ++cnt[(hs[id] & mask) / span + 1];
+  for (unsigned p = 0; p < P; ++p) cnt[p + 1] += cnt[p];
+  std::vector<uint32_t> order(n);
+  {
+    std::vector<size_t> at(cnt.begin(), cnt.end() - 1);
+    for (size_t id = 0; id < n; ++id) order[at[(hs[id] & mask) / span]++] = (uint32_t)id;
+  }
+  std::vector<std::vector<uint32_t>> deferred(P);
+  parallel_for(P, P, [&](size_t p) {
+    const size_t end = (p + 1) * span;
+    for (size_t q = cnt[p]; q < cnt[p + 1]; ++q) {
+      const uint32_t id = order[q];
+      size_t i = hs[id] & mask;
+      while (i < end && slots[i].id1) ++i;
+      if (i == end) {  // the probe leaves the range: placed after every range is done
+        deferred[p].push_back(id);
+        continue;
+      }
+      slots[i] = Slot{(uint32_t)(hs[id] >> 32), id + 1};
+    }
+  });
+  for (auto& v : deferred)
+    for (uint32_t id : v) put(hs[id], id);
+}
+
+namespace {
+
 // Concatenate per-chunk corpora (flattened in parallel, each with its own dictionaries) into
 // C. Parts are merged in document order, so every dictionary, scalar and capability-set id
 // is the one a sequential flatten assigns (first occurrence order).
 void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthreads) {
   const size_t T = parts.size();
+  const auto tm0 = std::chrono::steady_clock::now();
   // ---- id maps (sequential, document order) ----
   std::vector<std::vector<std::vector<uint32_t>>> dmap(T, std::vector<std::vector<uint32_t>>(KPE_NUM_DOMAINS));
   std::vector<std::vector<uint32_t>> capmap(T), scmap(T);
@@ -1688,10 +1862,19 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
           serr = std::current_exception();
         }
       });
+    std::vector<std::exception_ptr> derr(KPE_NUM_DOMAINS);
     for (int d = 0; d < KPE_NUM_DOMAINS; ++d)
       th.emplace_back([&, d] {
         size_t tot = C.dict[d].size();
         for (size_t t = 0; t < T; ++t) tot += parts[t].dict[d].size();
+        if (tot >= (1u << 16) && nthreads > 1) {  // e.g. resource names (one per resource)
+          try {
+            merge_dict_parallel(C.dict[d], parts, d, dmap, nthreads);
+          } catch (...) {
+            derr[d] = std::current_exception();
+          }
+          return;
+        }
         C.dict[d].reserve(tot);
         for (size_t t = 0; t < T; ++t) {
           const Dict& D = parts[t].dict[d];
@@ -1702,7 +1885,10 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
       });
     for (auto& x : th) x.join();
     if (serr) std::rethrow_exception(serr);
+    for (auto& e : derr)
+      if (e) std::rethrow_exception(e);
   }
+  const auto tm1 = std::chrono::steady_clock::now();
   // per-resource limits decided against one part's dictionaries may differ from the merged
   // ones: such a corpus is flattened again on one thread
   if (C.dict[D_CAP].size() > 64 || C.dict[D_KIND].size() > 4096 || C.dict[D_VERSION].size() > 1024 ||
@@ -1752,18 +1938,37 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
   if (e.n >= 0x7FFFFFC0ull) throw LimitError("more than 2^31 - 64 resources in one corpus (32-bit row ids)");
   if (e.doc > 0xFFFFFFFFull) throw LimitError("document tape exceeds 2^32 entries");
   const size_t n0 = C.n;
-  for (auto* v : {&C.r_flags, &C.r_gvk, &C.r_name, &C.r_mns, &C.r_nsa, &C.r_nsl, &C.p_sc}) v->resize(e.n);
-  C.p_cold.resize(e.n * 4), C.rec.resize(e.n * 4);
-  for (auto* v : {&C.lab_off, &C.ann_off, &C.ctr_off, &C.vol_off, &C.sys_off, &C.pann_off}) v->resize(e.n + 1);
-  C.lab_k.resize(e.lab), C.lab_v.resize(e.lab), C.ann_k.resize(e.ann), C.ann_v.resize(e.ann);
-  C.vol_src.resize(e.vol), C.sys_id.resize(e.sys), C.pann_k.resize(e.pann), C.pann_v.resize(e.pann);
-  C.pann_kv.resize(e.pann * 2);
+  // the merged columns, sized on several threads (their zero fill is the first touch of fresh
+  // pages, which costs more than the placement itself)
+  std::vector<std::function<void()>> sz;
+  for (auto* v : {&C.r_flags, &C.r_gvk, &C.r_name, &C.r_mns, &C.r_nsa, &C.r_nsl, &C.p_sc})
+    sz.push_back([v, &e] { v->resize(e.n); });
+  sz.push_back([&] { C.p_cold.resize(e.n * 4); });
+  sz.push_back([&] { C.rec.resize(e.n * 4); });
+  for (auto* v : {&C.lab_off, &C.ann_off, &C.ctr_off, &C.vol_off, &C.sys_off, &C.pann_off})
+    sz.push_back([v, &e] { v->resize(e.n + 1); });
+  for (auto* v : {&C.lab_k, &C.lab_v}) sz.push_back([v, &e] { v->resize(e.lab); });
+  for (auto* v : {&C.ann_k, &C.ann_v}) sz.push_back([v, &e] { v->resize(e.ann); });
+  sz.push_back([&] { C.vol_src.resize(e.vol); });
+  sz.push_back([&] { C.sys_id.resize(e.sys); });
+  for (auto* v : {&C.pann_k, &C.pann_v}) sz.push_back([v, &e] { v->resize(e.pann); });
+  sz.push_back([&] { C.pann_kv.resize(e.pann * 2); });
   for (auto* v : {&C.c_sc, &C.c_name, &C.c_image, &C.c_sann, &C.c_sann_key, &C.c_sec_str, &C.c_pm_str, &C.c_selt_str,
                   &C.c_selu_str, &C.c_selr_str})
-    v->resize(e.ctr);
-  C.c_add.resize(e.ctr), C.c_drop.resize(e.ctr), C.crec.resize(e.ctr * 2), C.cport_off.resize(e.ctr + 1);
-  C.cport_host.resize(e.port), C.cport_str.resize(e.port);
-  if (docs) C.doc.resize(e.doc * 2), C.doc_off.resize(e.n), C.img_off.resize(e.n), C.has_docs = true;
+    sz.push_back([v, &e] { v->resize(e.ctr); });
+  sz.push_back([&] { C.c_add.resize(e.ctr); });
+  sz.push_back([&] { C.c_drop.resize(e.ctr); });
+  sz.push_back([&] { C.crec.resize(e.ctr * 2); });
+  sz.push_back([&] { C.cport_off.resize(e.ctr + 1); });
+  sz.push_back([&] { C.cport_host.resize(e.port); });
+  sz.push_back([&] { C.cport_str.resize(e.port); });
+  if (docs) {
+    sz.push_back([&] { C.doc.resize(e.doc * 2); });
+    sz.push_back([&] { C.doc_off.resize(e.n); });
+    sz.push_back([&] { C.img_off.resize(e.n); });
+    C.has_docs = true;
+  }
+  parallel_for(sz.size(), nthreads, [&](size_t i) { sz[i](); });
   // ---- remap and place every part (parallel) ----
   auto place = [&](size_t t) {
     const Corpus& P = parts[t];
@@ -1851,6 +2056,7 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
   if (base[0].ctr < C.cport_off.size()) C.cport_off[base[0].ctr] = (uint32_t)base[0].port;
   for (size_t t = 0; t < T; ++t)
     for (uint32_t row : parts[t].limit_rows) C.limit_rows.push_back((uint32_t)(base[t].n + row));
+  const auto tm2 = std::chrono::steady_clock::now();
   std::vector<std::thread> th;
   for (size_t t = 0; t < T; ++t) {
     if (th.size() >= nthreads) th.front().join(), th.erase(th.begin());
@@ -1858,6 +2064,12 @@ void merge_parts(Corpus& C, std::vector<Corpus>& parts, bool docs, unsigned nthr
   }
   for (auto& x : th) x.join();
   C.n = (int64_t)e.n;
+  if (getenv("KPE_DEBUG")) {
+    const auto tm3 = std::chrono::steady_clock::now();
+    fprintf(stderr, "kpe merge: dictionaries %.3f s, capability sets + sizing %.3f s, placement %.3f s\n",
+            std::chrono::duration<double>(tm1 - tm0).count(), std::chrono::duration<double>(tm2 - tm1).count(),
+            std::chrono::duration<double>(tm3 - tm2).count());
+  }
 }
 
 unsigned flatten_threads() {

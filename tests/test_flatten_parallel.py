@@ -44,3 +44,21 @@ def test_parallel_flatten_errors_in_document_order():
             assert e.value.status == 1
         finally:
             os.environ.pop("KPE_FLATTEN_THREADS")
+
+
+@pytest.mark.parametrize("threads", [2, 5, 8])
+def test_parallel_dictionary_merge_is_sequential(threads):
+    """Dictionaries past 65536 strings are merged by hash buckets on several threads
+    (flatten.cpp merge_dict_parallel) with the ids of a sequential merge: resource names repeating
+    across chunks (first occurrence in an earlier chunk, or later in the same one), and strings
+    that only some chunks hold."""
+    import json
+
+    rows = []
+    for i in range(90000):
+        name = f"res-{(i * 7919) % 70000}"
+        rows.append(json.dumps({"apiVersion": "v1", "kind": "ConfigMap",
+                                "metadata": {"name": name, "namespace": f"ns-{i % 13}",
+                                             "labels": {"app": f"a-{i % 70001}"}}}))
+    nd = "\n".join(rows).encode()
+    assert _digest(nd, threads, False) == _digest(nd, 1, False)
