@@ -410,14 +410,27 @@ __global__ void __launch_bounds__(kLB, KPE_LEAN6_WAVES) kpe_lean6_kernel(LeanBat
     const uint32_t kind = GVK_KIND(rec[j].y);
     const uint32_t matched = live && kind < nk ? dyn[kind] : 0u;
     uint32_t failr = 0;
+    if (ncls <= 4u) {  // the usual few version classes: no loop
+#pragma unroll
+      for (uint32_t c = 0; c < 4u; ++c)
+        failr |= (c < ncls && (fails & hw(cls_cv, c))) ? hw(cls_rm, c) : 0u;
+    } else {
 #pragma unroll 1
-    for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+      for (uint32_t c = 0; c < ncls; ++c) failr |= (fails & hw(cls_cv, c)) ? hw(cls_rm, c) : 0u;
+    }
     const uint32_t E = matched & ((err ? pss_rules : 0u) | ep_rules);
     const uint32_t F = (matched & pss_rules & failr & ~E) | (matched & pat_rules);  // F|E = PENDING
     const uint32_t P = matched & pss_rules & ~failr & ~E;
+    if (R <= 4u) {  // (C2: R = 3) the row's bytes without a loop
+#pragma unroll
+      for (uint32_t ri = 0; ri < 4u; ++ri)
+        if (ri < R)
+          sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    } else {
 #pragma unroll 1
-    for (uint32_t ri = 0; ri < R; ++ri)
-      sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+      for (uint32_t ri = 0; ri < R; ++ri)
+        sv[lane * R + ri] = (uint8_t)(((P >> ri) & 1u) | (((F >> ri) & 1u) << 1) | (((E >> ri) & 1u) << 2));
+    }
     if (S.masks && live) {
       uint32_t* mrow = S.masks + (size_t)r * R;
       const uint32_t fm = F & pss_rules;
