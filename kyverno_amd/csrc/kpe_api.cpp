@@ -148,6 +148,10 @@ struct kpe_device {
   // evaluation), KPE_PATVM_ERR (report a KPE_PATVM_CHECK build's bounds flags), KPE_LEAN6_MINW /
   // KPE_LEAN6_TPW (waves a LEAN6 launch keeps / tiles per wave, for A/B runs)
   bool no_cache = false, patvm_err = false;
+  // the general scan of a podSecurity program reads per-pod records kpe_psum_kernel builds right
+  // before it; KPE_PSUM=0: it walks each pod's lists itself (C4 0.546 vs 0.566 ms per step, but 1.98x
+  // its algorithmic bytes against 0.92x; C3 2.66 vs 2.64 ms: profiles/r05_psA, r05_psB, r05_final5)
+  bool no_psum = false;
   uint64_t lean_min_waves = 16384;  // 256 CUs x 4 SIMDs x 16 waves
   uint32_t lean_tpw = 0;
   // pinned staging for corpus uploads (two halves, double-buffered; allocated on first use): a
@@ -297,6 +301,7 @@ kpe_status kpe_device_open(int ordinal, kpe_device** out) {
   if (const char* ev = getenv("KPE_LANES")) d->nlanes = std::max(1, std::min(kMaxLanes, atoi(ev)));
   d->no_cache = getenv("KPE_NO_BIND_CACHE") != nullptr;
   d->patvm_err = getenv("KPE_PATVM_ERR") != nullptr;
+  if (const char* ev = getenv("KPE_PSUM")) d->no_psum = atoi(ev) == 0;
   if (const char* ev = getenv("KPE_LEAN6_MINW")) d->lean_min_waves = std::max(1, atoi(ev));
   if (const char* ev = getenv("KPE_LEAN6_TPW")) {
     const int t = atoi(ev);
@@ -1241,8 +1246,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   if (P.any_pss && !cc->d->codes_ready)
     if (kpe_status st = run_codes(C, *cc->d, s)) return st;
   // the general scan of a podSecurity program reads per-pod PSA records (PSUM instantiation, code
-  // | 4), which kpe_psum_kernel rebuilds right before it in every evaluation
-  B.gen_code = (narrow ? 1 : 0) | (P.any_pss ? 4 : 0);
+  // | 4) that kpe_psum_kernel rebuilds before it every time, or (KPE_PSUM=0) walks the pods' lists
+  B.gen_code = (narrow ? 1 : 0) | (P.any_pss && !dev->no_psum ? 4 : 0);
   B.scan_blocks = kpe_scan_grid(C.n, P.any_pss ? 1 : 0, lean ? B.lean_kind : B.gen_code, B.dyn_bytes);
   HIPCHK(upload(B.jobs, jobs, s));
   {  // ApplyOne policies: contiguous rule ranges in ComputeRules order
@@ -1308,7 +1313,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     if (kpe_status st = run_codes(C, D, s)) return st;
   const bool lean_go = B.lean && (!masks || B.lean_kind == 7);  // LEAN6 writes check masks too
   const bool six = lean_go && B.lean_kind == 7;
-  if (P.any_pss && !lean_go) HIPCHK(D.psum.ensure((size_t)C.n * 12 + 16));  // the PSUM scan's records
+  const bool psum_go = P.any_pss && !lean_go && !dev->no_psum;  // the PSUM scan and its per-pod records
+  if (psum_go) HIPCHK(D.psum.ensure((size_t)C.n * 12 + 16));
   if (B.nblocks && fresh) {  // dictionary pass for large-domain predicates
     PredArgs pa{};
     for (int i = 0; i < KPE_NUM_DOMAINS; ++i) {
@@ -1409,7 +1415,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.pimg = B.pimg_words ? B.pimg.as<uint32_t>() : nullptr;
   sa.pimg_words = B.pimg_words, sa.capb_lds = B.capb_lds;
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
-  sa.psum = P.any_pss && !lean_go ? D.psum.as<uint32_t>() : nullptr;
+  sa.psum = psum_go ? D.psum.as<uint32_t>() : nullptr;
   sa.selm = B.selm;
   if (B.selm) {
     sa.sel_km = B.sel_km.as<uint4>(), sa.sel_vm = B.sel_vm.as<uint4>(), sa.ns_q = B.sel_nsq.as<uint64_t>();
@@ -1450,7 +1456,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
     if (kpe_status st = lean6_launch(dev, P, PD, &one, 1, masks, s, &lbytes)) return st;
   } else {
     // the general scan of a podSecurity program reads per-pod PSA records built right here
-    if (P.any_pss && !lean_go)
+    if (psum_go)
       if (kpe_status st = run_psum(C, D, s)) return st;
     HIPCHK(kpe_launch_scan(B.dargs.as<ScanArgs>(), &B.hargs, C.n, P.any_pss ? 1 : 0, lean_go ? B.lean_kind : B.gen_code,
                            B.scan_blocks, B.dyn_bytes, s));
@@ -1628,7 +1634,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   if (dev->timing) {
     HIPCHK(hipEventRecord(ev.d, s));
     ev.post = !P.cond.rules.empty() || !P.pssx.rules.empty() || !P.pat.rules.empty() || B.napply_segs || !C.limit_rows.empty();
-    const bool ps = P.any_pss && !lean_go;  // the PSUM scan and its per-pod records
+    const bool ps = psum_go;
     ev.bytes = six ? lbytes : scan_bytes(P, C, B.need, masks, ps) + (ps ? psum_bytes(C, D, B.need) : 0.0);
     ev.pbytes = P.pat.rules.empty() ? 0.0 : (double)C.doc.size() * 4.0 + (double)C.n * (8.0 + 2.0 * (double)R);
     ev.kind = lean_go ? B.lean_kind : 1;
