@@ -161,6 +161,7 @@ struct kpe_device {
   hipEvent_t stage_ev[2] = {};
   bool stage_busy[2] = {};
   int stage_cur = 0;
+  double up_alloc_s = 0, up_copy_s = 0;  // KPE_DEBUG upload breakdown (under mu)
   hipEvent_t get_ev() {
     if (!pool.empty()) {
       hipEvent_t e = pool.back();
@@ -436,18 +437,18 @@ void kpe_corpus_free(kpe_corpus* c) {
 
 // Copy v into b (allocated with the upload() slack) through the device's pinned staging halves:
 // the CPU fills one half while the DMA drains the other. The caller synchronises the stream.
-static double g_up_alloc_s = 0, g_up_copy_s = 0;  // KPE_DEBUG upload breakdown
 template <class T>
 hipError_t upload_staged(kpe_device* dev, DevBuf& b, const std::vector<T>& v, hipStream_t s) {
   const size_t n = v.size() * sizeof(T);
   const auto t0 = std::chrono::steady_clock::now();
   hipError_t e = b.ensure(n + 128);
   const auto t1 = std::chrono::steady_clock::now();
-  g_up_alloc_s += std::chrono::duration<double>(t1 - t0).count();
+  dev->up_alloc_s += std::chrono::duration<double>(t1 - t0).count();
   struct CopyTimer {
+    double* acc;
     std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
-    ~CopyTimer() { g_up_copy_s += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count(); }
-  } ct;
+    ~CopyTimer() { *acc += std::chrono::duration<double>(std::chrono::steady_clock::now() - t).count(); }
+  } ct{&dev->up_copy_s};
   if (e != hipSuccess || n == 0) return e;
   if (!dev->stage) {
     e = hipHostMalloc(reinterpret_cast<void**>(&dev->stage), 2 * kpe_device::kStageHalf, hipHostMallocDefault);
@@ -551,9 +552,9 @@ kpe_status kpe_corpus_upload(kpe_device* dev, kpe_corpus* cc) {
   HIPCHK(hipStreamSynchronize(s));
   static const bool dbg = getenv("KPE_DEBUG") != nullptr;
   if (dbg)
-    fprintf(stderr, "kpe upload: alloc %.4f s, stage + enqueue %.4f s, final sync %.4f s\n", g_up_alloc_s, g_up_copy_s,
+    fprintf(stderr, "kpe upload: alloc %.4f s, stage + enqueue %.4f s, final sync %.4f s\n", dev->up_alloc_s, dev->up_copy_s,
             std::chrono::duration<double>(std::chrono::steady_clock::now() - ts).count());
-  g_up_alloc_s = g_up_copy_s = 0;
+  dev->up_alloc_s = dev->up_copy_s = 0;
   return KPE_OK;
 }
 
