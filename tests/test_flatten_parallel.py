@@ -46,8 +46,9 @@ def test_parallel_flatten_errors_in_document_order():
             os.environ.pop("KPE_FLATTEN_THREADS")
 
 
-@pytest.mark.parametrize("threads", [2, 5, 8])
-def test_parallel_dictionary_merge_is_sequential(threads):
+@pytest.mark.parametrize("threads", [2, 5, 8, 16])
+@pytest.mark.parametrize("docs", [False, True])
+def test_parallel_dictionary_merge_is_sequential(threads, docs):
     """Dictionaries past 65536 strings are merged by hash buckets on several threads
     (flatten.cpp merge_dict_parallel) with the ids of a sequential merge: resource names repeating
     across chunks (first occurrence in an earlier chunk, or later in the same one), and strings
@@ -61,4 +62,4 @@ def test_parallel_dictionary_merge_is_sequential(threads):
                                 "metadata": {"name": name, "namespace": f"ns-{i % 13}",
                                              "labels": {"app": f"a-{i % 70001}"}}}))
     nd = "\n".join(rows).encode()
-    assert _digest(nd, threads, False) == _digest(nd, 1, False)
+    assert _digest(nd, threads, docs) == _digest(nd, 1, docs)
