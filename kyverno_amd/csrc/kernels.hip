@@ -47,6 +47,7 @@ __device__ __forceinline__ T sld(const T* p, uint32_t i) {
 
 }  // namespace
 
+#ifndef KPE_VM_ONLY
 // ---------------------------------------------------------------------------
 constexpr uint32_t kPredStrLds = 16384;  // staged dictionary bytes per block
 constexpr uint32_t kPredPatLds = 4096;   // staged pattern bytes
@@ -123,6 +124,8 @@ __global__ void __launch_bounds__(256) kpe_count_kernel(const uint8_t* v, int64_
   for (uint32_t i = t; i < rn * 8; i += 256)
     if (hist[i]) atomicAdd(&out[(size_t)r0 * 8 + i], (unsigned long long)hist[i]);
 }
+
+#endif  // !KPE_VM_ONLY
 
 // ---------------------------------------------------------------------------
 namespace {
@@ -710,8 +713,13 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       const KpeTerm tm = a0.terms[lane];
       tm_type = tm.type, tm_a = tm.a, tm_b = tm.b;
     }
-  } else if (a0.nrules <= KPE_RULE_CHUNK && lane < a0.nrules) {
-    myrule = reinterpret_cast<const uint4*>(a0.rule_lanes)[lane];
+  } else {
+    if (a0.nrules <= KPE_RULE_CHUNK && lane < a0.nrules) myrule = reinterpret_cast<const uint4*>(a0.rule_lanes)[lane];
+    // WIDE: term t's record in lane t as well (<= 64 terms): no scalar load per term and tile
+    if (a0.nterms <= 64u && lane < a0.nterms) {
+      const KpeTerm tm = a0.terms[lane];
+      tm_type = tm.type, tm_a = tm.a, tm_b = tm.b;
+    }
   }
   uint32_t cls_cv = 0, cls_rm = 0;  // NARROW PSS classes: (check set, rules failing on it)
   if (NARROW && a0.tt_lds != PRED_NONE && lane < a0.ncls) {
@@ -967,7 +975,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     lab_cache(a, rc, live, LC);
 #pragma unroll 1
     for (uint32_t ti = 0; ti < a.nterms; ++ti) {
-      const uint64_t m = __ballot(eval_term(a, B, sld(a.terms, ti), gvk, nsa, name_col, mns_col, rc, live, LC));
+      const KpeTerm tm = a.nterms <= 64u ? KpeTerm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u} : sld(a.terms, ti);
+      const uint64_t m = __ballot(eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live, LC));
       if (lane == 0) tmk[ti] = m;
     }
     // PSS version sets: resources failing some check of each distinct cv_mask
@@ -1099,7 +1108,9 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
 }
 
 
+#ifndef KPE_VM_ONLY
 #include "lean.inl"
+#endif
 
 // ---------------------------------------------------------------------------
 // Host-side launch wrappers (called from kpe_api.cpp).
@@ -1119,6 +1130,7 @@ namespace {
 #include "patvm.inl"
 }  // namespace
 
+#ifndef KPE_SCAN_ONLY
 // grid: 256-row blocks, one lane per row running every pattern rule
 #ifndef KPE_PAT_BLOCK
 #define KPE_PAT_BLOCK 128  // C5 / C3 pattern kernel (events, profiles/r03_c_ldsframes): 256 x 8 frames 20.7 / 9.2 ms,
@@ -1304,6 +1316,9 @@ extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32
   return hipGetLastError();
 }
 
+#endif  // !KPE_SCAN_ONLY
+
+#ifndef KPE_VM_ONLY
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t xblocks, hipStream_t s) {
   if (xblocks == 0 || a->njobs == 0) return hipSuccess;
   hipLaunchKernelGGL(kpe_pred_kernel, dim3(xblocks, a->njobs), dim3(256), 0, s, *a);
@@ -1510,3 +1525,4 @@ extern "C" hipError_t kpe_launch_count(const uint8_t* verdicts, int64_t n, uint3
   }
   return hipSuccess;
 }
+#endif  // !KPE_VM_ONLY
