@@ -42,6 +42,25 @@ IC_BYTES = 256 << 20  # MI355X Infinity Cache (MALL)
 SCAN_KERNELS = {1: "kpe_scan_kernel", 2: "kpe_scan_kernel", 7: "kpe_lean6_kernel", 9: "kpe_lean6_kernel"}
 
 
+def scan_accounting(launches, kernel_ms_sum, bytes_sum, steps, ms_per_step, replicas):
+    """Algorithmic-byte accounting of the timed steps' scan launches (pure arithmetic, tested on
+    CPU in tests/test_bench_accounting.py). A multi-shard kpe_lean6_kernel launch carries a
+    different number of steps than its neighbours (ceil(K / 24) launches over K steps), so the
+    bytes are SUMMED over the launches and the time too: achieved = sum of bytes / sum of kernel
+    time, the mean launch = sum / launches, and one step (one shard) = sum / K at any K."""
+    L = max(int(launches), 1)
+    per_step = bytes_sum / steps if steps else 0.0
+    kernel_ms = kernel_ms_sum / L
+    return {"launches": int(launches),
+            "alg_bytes_per_launch": bytes_sum / L,  # the mean launch
+            "alg_bytes_per_step": per_step,         # one shard's evaluation
+            "kernel_ms": kernel_ms,
+            "achieved_gbs": bytes_sum / (kernel_ms_sum * 1e-3) / 1e9 if kernel_ms_sum > 0 else 0.0,
+            "achieved_per_step_gbs": per_step / (ms_per_step * 1e-3) / 1e9 if ms_per_step > 0 else 0.0,
+            # the bytes read between two uses of one shard (each step evaluates one shard)
+            "rotated_scan_bytes": per_step * replicas}
+
+
 def cpu_budget():
     """CPUs this process may run on: the affinity mask, capped by a cgroup v2 / v1 CPU quota
     (a GPU box grants each job a share of a larger machine: os.cpu_count() is the machine)."""
@@ -205,8 +224,9 @@ def main(argv=None):
     n = args.resources or n_def
     first = None  # strong scaling: this rank's first row of the --total-resources corpus
     if args.total_resources:
+        # (C2 keeps its derived replica count: copies of the rank's row range are rotated so the
+        # steps stay HBM-bound; the others rotate one shard)
         first, n = shard_range(args.total_resources, rank, world)
-        rep_def = 1
         workload = (f"{cfg.upper()}: {args.total_resources} rows in all, split over {world} GPU(s) "
                     f"(contiguous row ranges); " + workload.split(": ", 1)[1].split(" per GPU")[0])
     n_all = args.total_resources or n * world
@@ -326,41 +346,61 @@ def main(argv=None):
     st = eng.device.kernel_stats(reset=True)
     single_stream_ms = (time.perf_counter() - t1) / args.steps * 1e3
     L = max(st.launches, 1)
-    step_bytes = st.scan_bytes * L / args.steps  # launches carry near-equal shares of the K steps
-    scan_ms = st.pss_kernel_ms / L
+    ms_per_step = elapsed / args.steps * 1e3
+    acct = scan_accounting(st.launches, st.pss_kernel_ms, st.scan_bytes_sum, args.steps, ms_per_step, replicas)
+    step_bytes = acct["alg_bytes_per_step"]
+    scan_ms = acct["kernel_ms"]
     dict_ms = st.dict_kernel_ms / L
     pat_ms = st.pattern_kernel_ms / L
-    scan_achieved = st.scan_bytes / (scan_ms * 1e-3) / 1e9 if scan_ms > 0 else 0.0
+    scan_achieved = acct["achieved_gbs"]
 
     # ---- the masks-producing instantiation (what a report needs for each FAIL cell's PSS
     # checks) and a cold step (per-corpus prologue re-run: dictionary predicate pass + prologue
     # image, as the first evaluation of a newly bound corpus), wall-clock and per kernel ----
-    def leg(**kw):
+    def leg(serial=False, batch=False, **kw):
+        """serial: one evaluation at a time (enqueue, wait), i.e. one 1M-row shard's latency;
+        batch: the K / 4 steps through kpe_evaluate_batch_async (multi-shard launches);
+        otherwise per-evaluation launches enqueued back to back (two streams)."""
         for c in corpora:  # mode switch (argument block upload, masks buffer allocation) untimed
             eng.evaluate_async(ps, c, **kw)
         eng.device.sync()
         eng.device.set_timing(False)
         ks = max(1, args.steps // 4)
+        sub = eng.batch([corpora[i % len(corpora)] for i in range(ks)]) if batch else None
+
+        def run():
+            if batch:
+                eng.evaluate_batch_async(ps, sub, **kw)
+                return
+            for i in range(ks):
+                eng.evaluate_async(ps, corpora[i % len(corpora)], **kw)
+                if serial:
+                    eng.device.sync()
+
+        if batch:  # rotation first, as the timed region does
+            eng.evaluate_batch_async(ps, rotation, **kw)
+            eng.device.sync()
         t1 = time.perf_counter()
-        for i in range(ks):
-            eng.evaluate_async(ps, corpora[i % len(corpora)], **kw)
+        run()
         eng.device.sync()
         wall = (time.perf_counter() - t1) / ks * 1e3
         eng.device.set_timing(True)
         eng.device.kernel_stats(reset=True)
-        for i in range(ks):
-            eng.evaluate_async(ps, corpora[i % len(corpora)], **kw)
+        run()
         k = eng.device.kernel_stats(reset=True)
+        a = scan_accounting(k.launches, k.pss_kernel_ms, k.scan_bytes_sum, ks, wall, replicas)
         kl = max(k.launches, 1)
         return {"ms_per_step": wall, "evals_per_s": float(n) * R / (wall * 1e-3), "steps": ks,
-                "scan_kernel_ms": k.pss_kernel_ms / kl, "prologue_ms": k.dict_kernel_ms / kl,
-                "later_kernels_ms": k.pattern_kernel_ms / kl, "scan_bytes_per_launch": k.scan_bytes}
+                "launches": k.launches, "scan_kernel_ms": a["kernel_ms"], "prologue_ms": k.dict_kernel_ms / kl,
+                "later_kernels_ms": k.pattern_kernel_ms / kl, "scan_bytes_per_launch": a["alg_bytes_per_launch"],
+                "scan_bytes_per_step": a["alg_bytes_per_step"], "scan_frac": a["achieved_gbs"] / HBM_PEAK_GBS}
 
-    masks_leg = leg(masks=True)
+    single_leg = leg(serial=True)               # one shard, no masks: the single-corpus latency
+    masks_leg = leg(masks=True)                 # per-evaluation launches with check masks
+    masks_batch_leg = leg(masks=True, batch=True)  # the same through the multi-shard launches
     cold_leg = leg(masks=True, cold=True)
     eng.device.set_timing(False)
 
-    ms_per_step = elapsed / args.steps * 1e3
     evals = float(n_all) * R * args.steps
     value = evals / elapsed
 
@@ -376,7 +416,7 @@ def main(argv=None):
                 # counter bytes over the algorithmic bytes of the same launches, applied to this run's
                 # launches (a multi-shard launch's size follows K); else the pass's bytes as they are
                 ratio = tj.get("traffic_ratio")
-                traffic = ratio * st.scan_bytes if ratio else tj.get("scan_bytes_per_launch")
+                traffic = ratio * acct["alg_bytes_per_launch"] if ratio else tj.get("scan_bytes_per_launch")
         except Exception:
             traffic = None
 
@@ -409,23 +449,26 @@ def main(argv=None):
         scan_roof = {"bound": "hbm", "achieved": scan_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": scan_achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": scan_kernel,
-                     "kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes, "dict_kernel_ms": dict_ms,
+                     "kernel_ms": scan_ms, "alg_bytes_per_launch": acct["alg_bytes_per_launch"],
+                     "dict_kernel_ms": dict_ms,
                      "pattern_kernel_ms": pat_ms,
                      # the same bytes over the timed region's step time (launches of different
                      # shards overlap on two streams there) and the isolated single-stream step
                      "launches": st.launches, "alg_bytes_per_step": step_bytes,
-                     "achieved_per_step": step_bytes / (ms_per_step * 1e-3) / 1e9,
+                     "achieved_per_step": acct["achieved_per_step_gbs"],
                      "single_stream_step_ms": single_stream_ms,
                      "note": ("kernel_ms: HIP events per launch, launches serialised on one stream "
                               "(kpe_lean6_kernel over several shards: one launch over up to 24 shards, i.e. "
-                              "several steps, alg_bytes_per_launch its shards' bytes: pod records, tile headers, "
+                              "several steps, alg_bytes_per_launch the mean launch's shards' bytes (summed over "
+                              "the launches / launches): pod records, tile headers, "
                               "container / volume / sysctl / annotation items, code bytes, verdicts); other kernels: "
                               "one launch per step, and consecutive shards' launches overlap on two streams in the "
                               "timed region; dict / pattern kernel ms are 0 when no such kernel ran")}
         if pat_ms > scan_ms and st.pattern_bytes > 0:
             # pattern-dominated configurations (C3, C5): the dominant kernel is the pattern VM;
             # its algorithmic bytes are every resource's document tape once plus the verdicts
-            pat_achieved = st.pattern_bytes / (pat_ms * 1e-3) / 1e9
+            pat_sum = st.pattern_bytes_sum or st.pattern_bytes * L
+            pat_achieved = pat_sum / (st.pattern_kernel_ms * 1e-3) / 1e9
             pat_traffic = None
             try:  # FETCH_SIZE / WRITE_SIZE of the pattern kernel (scripts/gpu_pass.sh traffic:<cfg>:kpe_pattern_kernel)
                 tj = json.load(open(traffic_json))
@@ -435,8 +478,8 @@ def main(argv=None):
                 pat_traffic = None
             scan_roof = {"bound": "hbm", "achieved": pat_achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": pat_achieved / HBM_PEAK_GBS, "traffic": pat_traffic, "kernel": "kpe_pattern_kernel",
-                         "kernel_ms": pat_ms, "alg_bytes_per_launch": st.pattern_bytes,
-                         "scan_kernel": {"kernel_ms": scan_ms, "alg_bytes_per_launch": st.scan_bytes,
+                         "kernel_ms": pat_ms, "alg_bytes_per_launch": pat_sum / L,
+                         "scan_kernel": {"kernel_ms": scan_ms, "alg_bytes_per_launch": acct["alg_bytes_per_launch"],
                                          "frac": scan_achieved / HBM_PEAK_GBS},
                          "single_stream_step_ms": single_stream_ms}
         # end-to-end ingestion of shard 0's NDJSON again (generated untimed, nothing else running):
@@ -476,7 +519,8 @@ def main(argv=None):
             "config": {"workload": workload, "resources_per_gpu": n, "rules": R, "global_resources": n_all,
                        "replicas_rotated": replicas, "parallelism": f"resource-sharded x{world}",
                        # scan bytes touched between two uses of one shard vs the Infinity Cache
-                       "rotated_scan_bytes": st.scan_bytes * replicas, "infinity_cache_bytes": IC_BYTES,
+                       "rotated_scan_bytes": acct["rotated_scan_bytes"], "infinity_cache_bytes": IC_BYTES,
+                       "rotation_exceeds_infinity_cache": acct["rotated_scan_bytes"] >= 2 * IC_BYTES,
                        # cells where the rule matched the resource (a RuleResponse exists), per s
                        "matched_cell_evals_per_s": value * sum(n_all * replicas - totals[r]["na"]
                                                                for r in range(R)) / float(n_all * replicas * R),
@@ -484,7 +528,9 @@ def main(argv=None):
             "roofline": scan_roof,
             "cpu_baseline": cpu,
             "gather": gather,
+            "single_shard_step": single_leg,
             "masks_step": masks_leg,
+            "masks_batch_step": masks_batch_leg,
             "cold_masks_step": cold_leg,
             "e2e": {"e2e_evals_per_s": float(n) * R / e2e_s, "flatten_s": e2e_flat,
                     "upload_s": e2e_up, "first_eval_s": t_eval1,

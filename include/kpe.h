@@ -228,6 +228,9 @@ int kpe_pss_num_checks(void);
  * of a FAIL cell of a rule with a podSecurity PolicyException: the exception matched the
  * resource, so its exclusions shape the cell's fail message (kpe_report_results_msg). */
 #define KPE_CVM_XMATCH (1u << 31)
+/* The versioned-check bits of a cv mask word (bits 0 .. kpe_pss_num_cv() - 1): mask with it
+ * before walking set bits as versioned checks (bit 31 is a flag, not a check). */
+#define KPE_CVM_CHECKS_ALL 0x7FFFFFFFu
 kpe_status kpe_fetch_cv_masks(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint32_t* cv_masks);
 int kpe_pss_num_cv(void);
 int kpe_pss_cv_check(int v);
@@ -355,6 +358,10 @@ typedef struct kpe_kernel_stats {
                                (general), 2 its LEAN instantiation (corpora past 4 GiB of pod
                                records), 7 kpe_lean6_kernel (one shard), 9 kpe_lean6_kernel (a multi-shard launch) */
   int32_t pad_;
+  double scan_bytes_sum;    /* algorithmic bytes of every timed scan-kernel launch since the last reset,
+                               summed (multi-shard launches differ in size: the mean launch carries
+                               scan_bytes_sum / launches, not the last launch's scan_bytes) */
+  double pattern_bytes_sum; /* the same for the pattern kernel's algorithmic bytes */
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);
 kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c,

@@ -27,7 +27,8 @@ class KernelStats(ctypes.Structure):
     _fields_ = [("launches", ctypes.c_uint64), ("pss_kernel_ms", ctypes.c_double),
                 ("dict_kernel_ms", ctypes.c_double), ("scan_bytes", ctypes.c_double),
                 ("pattern_kernel_ms", ctypes.c_double), ("pattern_bytes", ctypes.c_double),
-                ("scan_kernel", ctypes.c_int32), ("pad_", ctypes.c_int32)]
+                ("scan_kernel", ctypes.c_int32), ("pad_", ctypes.c_int32),
+                ("scan_bytes_sum", ctypes.c_double), ("pattern_bytes_sum", ctypes.c_double)]
 
 
 def lib_path():
@@ -104,6 +105,7 @@ def load():
     L.kpe_synth_resources.argtypes = [ctypes.c_uint64, i64, i64, i32, ctypes.POINTER(ctypes.c_void_p),
                                       ctypes.POINTER(sz)]
     L.kpe_synth_free.argtypes = [vp]
+    L.kpe_debug_lean_kind.argtypes = [vp, ctypes.c_uint64]
     L.kpe_synth_ns_labels.argtypes = [ctypes.c_uint64, i64, i32, ctypes.POINTER(ctypes.c_void_p),
                                       ctypes.POINTER(ctypes.c_size_t)]
     _LIB = L

@@ -142,7 +142,7 @@ struct kpe_device {
   std::vector<EvPair> pending;
   std::vector<hipEvent_t> pool;
   uint64_t launches = 0;
-  double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0, last_pbytes = 0;
+  double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0, last_pbytes = 0, sum_bytes = 0, sum_pbytes = 0;
   int last_kind = 0;
   // knobs, read once at kpe_device_open: KPE_NO_BIND_CACHE (recompute per-binding products every
   // evaluation), KPE_PATVM_ERR (report a KPE_PATVM_CHECK build's bounds flags), KPE_LEAN6_MINW /
@@ -387,6 +387,34 @@ kpe_status kpe_corpus_flatten_ex(const char* ndjson, size_t len, const char* nsl
 }
 int64_t kpe_corpus_num_resources(const kpe_corpus* c) { return c ? c->c->n : 0; }
 int64_t kpe_corpus_bytes(const kpe_corpus* c) { return c ? c->c->bytes() : 0; }
+
+// kpe_lean6_kernel reads every column through buffer descriptors with 32-bit byte offsets
+// (lean.inl: pod records, tile headers, container records and seccomp annotations, volume /
+// sysctl items and the pod annotation pairs); a corpus with any of them past `lim` bytes takes the
+// LEAN template instantiation, which indexes with 64-bit pointers. Offsets past a descriptor would
+// read 0, i.e. silently pass an AppArmor / seccomp / sysctl check.
+static constexpr uint64_t kLean6Limit = (1ull << 32) - (1ull << 20);
+static bool lean6_fits(const kpe::Corpus& C, uint64_t lim) {
+  const uint64_t cols[] = {
+      (uint64_t)C.n * 16,                 // pod records
+      ((uint64_t)C.n / 64 + 2) * 16,      // tile headers
+      (uint64_t)C.c_sc.size() * 8,        // container records
+      (uint64_t)C.c_sann.size() * 4,      // container seccomp annotations
+      (uint64_t)C.vol_src.size() * 4,     // volume items
+      (uint64_t)C.sys_id.size() * 4,      // sysctl items
+      (uint64_t)C.pann_kv.size() * 4,     // pod annotation (key, value) pairs, 8 bytes each
+  };
+  for (uint64_t b : cols)
+    if (b + 4096 > lim) return false;
+  return true;
+}
+// Diagnostic (not in kpe.h): the LEAN instantiation a binding of c would pick under a column
+// limit of `lim` bytes (0: the real limit): 7 kpe_lean6_kernel, 2 the template scan.
+int kpe_debug_lean_kind(const kpe_corpus* c, uint64_t lim) {
+  if (!c) return -KPE_E_INVALID;
+  return lean6_fits(*c->c, lim ? lim : kLean6Limit) ? 7 : 2;
+}
+
 kpe_status kpe_corpus_row_flags(const kpe_corpus* c, uint32_t* out) {
   if (!c || !out) return fail(KPE_E_INVALID, "kpe_corpus_row_flags: null argument");
   const kpe::Corpus& C = *c->c;
@@ -1239,10 +1267,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.njobs = (uint32_t)jobs.size();
   B.nblocks = blk;
   // LEAN evaluations run kpe_lean6_kernel (buffer loads with 32-bit byte offsets: every column it
-  // reads under 4 GiB), else the template instantiation
-  const uint64_t lim = (1ull << 32) - (1ull << 20);
-  const uint64_t col_max = std::max<uint64_t>((uint64_t)C.n * 16, (uint64_t)C.c_sc.size() * 8);
-  B.lean_kind = !lean ? 0 : col_max + 4096 > lim ? 2 : 7;
+  // reads under 4 GiB), else the template instantiation (64-bit pointers)
+  B.lean_kind = !lean ? 0 : lean6_fits(C, kLean6Limit) ? 7 : 2;
   // the PSA dictionary codes of the corpus (policy-independent; per distinct string)
   if (P.any_pss && !cc->d->codes_ready)
     if (kpe_status st = run_codes(C, *cc->d, s)) return st;
@@ -2352,6 +2378,8 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
     dev->pat_ms += p.post ? d3 : 0.0f;
     dev->last_bytes = p.bytes;
     dev->last_pbytes = p.pbytes;
+    dev->sum_bytes += p.bytes;
+    dev->sum_pbytes += p.post ? p.pbytes : 0.0;
     dev->last_kind = p.kind;
     dev->launches++;
     dev->pool.push_back(p.a);
@@ -2368,9 +2396,11 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
   out->pattern_bytes = dev->last_pbytes;
   out->scan_kernel = dev->last_kind;
   out->pad_ = 0;
+  out->scan_bytes_sum = dev->sum_bytes;
+  out->pattern_bytes_sum = dev->sum_pbytes;
   if (reset) {
     dev->launches = 0;
-    dev->pss_ms = dev->dict_ms = dev->pat_ms = 0;
+    dev->pss_ms = dev->dict_ms = dev->pat_ms = dev->sum_bytes = dev->sum_pbytes = 0;
   }
   return KPE_OK;
 }

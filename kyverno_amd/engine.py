@@ -317,13 +317,17 @@ class Engine:
                 "undecided": c.undecided} for c in counts[:R]]
         return v, m, cnt
 
-    def cv_masks(self, ps: PolicySet, corpus: Corpus):
+    CVM_XMATCH = 1 << 31  # KPE_CVM_XMATCH: a flag of FAIL cells, not a versioned check
+
+    def cv_masks(self, ps: PolicySet, corpus: Corpus, raw=False):
         """Failing versioned PSS checks (N x R uint32, bit v = kpe_pss_cv_check(v)) of the last
-        evaluation with check_masks=True (kpe_fetch_cv_masks)."""
+        evaluation with check_masks=True (kpe_fetch_cv_masks). Bit 31 (KPE_CVM_XMATCH: the
+        cell's podSecurity PolicyException matched) is cleared unless raw=True; the report
+        functions take the raw words."""
         m = np.zeros((corpus.n, ps.num_rules), dtype=np.uint32)
         if m.size:
             check(load().kpe_fetch_cv_masks(self.device.h, ps.h, corpus.h, m.ctypes.data))
-        return m
+        return m if raw else m & np.uint32(0x7FFFFFFF)
 
     def evaluate_async(self, ps: PolicySet, corpus: Corpus, masks=False, cold=False):
         """Enqueue one evaluation (results stay on the device). masks: also write the check masks;

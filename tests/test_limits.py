@@ -77,3 +77,25 @@ def test_limited_rows_undecided(oracle):
     ref = oracle.validate(pols, nd, nthreads=8)
     assert (v[keep] == ref[keep]).all()
     assert sum(c["undecided"] for c in cnt) == len(limited) * v.shape[1]
+
+
+def test_lean6_column_guard():
+    """kpe_lean6_kernel addresses every column it reads with 32-bit byte offsets: a corpus whose
+    pod annotation pairs (or volume / sysctl / container annotation items) pass the limit must take
+    the 64-bit template scan, not only one whose pod or container records do."""
+    L = K._lib.load()
+    many_ann = [{"apiVersion": "v1", "kind": "Pod",
+                 "metadata": {"name": f"p{i}", "namespace": "default",
+                              "annotations": {f"a{j}": "v" for j in range(20)}},
+                 "spec": {"containers": [{"name": "c", "image": "nginx"}]}} for i in range(64)]
+    c = K.Corpus(many_ann, docs=False)
+    assert L.kpe_debug_lean_kind(c.h, 0) == 7  # far below 4 GiB
+    # pods: 64 x 16 B; containers 64 x 8 B; annotation pairs 64 x 20 x 8 B = 10240 B
+    assert L.kpe_debug_lean_kind(c.h, 4096 + 64 * 20 * 8 - 1) == 2
+    assert L.kpe_debug_lean_kind(c.h, 4096 + 64 * 20 * 8 + 1) == 7
+    vols = [{"apiVersion": "v1", "kind": "Pod", "metadata": {"name": f"v{i}", "namespace": "default"},
+             "spec": {"containers": [{"name": "c", "image": "nginx"}],
+                      "volumes": [{"name": f"x{j}", "emptyDir": {}} for j in range(100)]}} for i in range(8)]
+    c2 = K.Corpus(vols, docs=False)
+    assert L.kpe_debug_lean_kind(c2.h, 4096 + 8 * 100 * 4 - 1) == 2
+    assert L.kpe_debug_lean_kind(c2.h, 4096 + 8 * 100 * 4 + 1) == 7

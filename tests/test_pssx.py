@@ -286,7 +286,7 @@ def test_exception_messages_gpu(oracle):
     v, _, _ = eng.evaluate(ps, c, check_masks=True)
     ref = oracle.validate(pols, nd, nthreads=8, exceptions=excs)
     assert np.array_equal(v, ref)
-    cvm = eng.cv_masks(ps, c)
+    cvm = eng.cv_masks(ps, c, raw=True)
     base = oracle.validate(strip_exclusions(pols), nd, nthreads=8)
     skipped = oracle.validate(strip_exclusions(pols), nd, nthreads=8, exceptions=strip_pss(excs))
     xm = xfail_seed(pols, excs, base, skipped) == 8
