@@ -283,7 +283,9 @@ long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row,
 /* Failing paths of pattern cells, for their report messages (validate_resource.go:316-454;
  * validate.go MatchPattern PatternError.Path). After kpe_evaluate / kpe_evaluate_async of the
  * same program and corpus, for each listed cell (row * R + column) the device re-walks every root
- * of the cell's validate.pattern / anyPattern rule (at most KPE_TRACE_ROOTS) and records the
+ * of the cell's validate.pattern / anyPattern rule (at most KPE_TRACE_ROOTS; for a FAIL / ERROR
+ * cell of a validate.foreach rule that a pattern entry decided, that entry's roots on the
+ * element it validated, kpe_fetch_cond_traces_ex) and records the
  * path of the failure that decided it: out[i * KPE_TRACE_ROOTS * KPE_TRACE_WORDS + k *
  * KPE_TRACE_WORDS + w], w = 0: component count (bits 0-7) | KPE_TR_TRUNC | the root's verdict
  * << 16 | KPE_TR_VALID; w = 1..15: components (a pattern member, KPE_TC_KEY | key id, or
@@ -318,8 +320,23 @@ long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus
  * conditions) are 0. */
 kpe_status kpe_fetch_cond_traces(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint64_t row0,
                                  uint64_t nrows, uint32_t* out);
+/* Condition traces with the foreach and error records (report time): rows [row0, row0 + nrows)
+ * into out, nrows x R x KPE_CTRACE_WORDS words. Word 0 of a cell is kpe_fetch_cond_traces' word,
+ * where a block that raised an error records which condition raised it and on which side
+ * (KPE_CT_ERR without the evaluated bit 0x4000: bits 0-6 the condition, any conditions first,
+ * then all; bits 7-8 0 the key's substitution, 1 the value's, 2 the operator). For validate.foreach
+ * rules (validateElements, validate_resource.go:206-254) the words describe the element that
+ * decided a FAIL / ERROR cell: word 0 bits 16-31 its deny block (or its preconditions' error),
+ * word 1 its path (nesting depth, what decided it, per level the entry and the element index),
+ * words 2 and 3 the element's and the validated element's document nodes. The words of other cells
+ * and of foreach cells that are not FAIL / ERROR are unspecified. */
+#define KPE_CTRACE_WORDS 4u
+#define KPE_CT_ERR 0x8000u
+kpe_status kpe_fetch_cond_traces_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint64_t row0,
+                                    uint64_t nrows, uint32_t* out);
 /* kpe_report_results_msg_tr plus the condition messages of kpe_fetch_cond_traces (cond_traces:
- * the row's R words, or NULL):
+ * the row's R words, or NULL) or kpe_fetch_cond_traces_ex (cond_traces_ex, the row's R x
+ * KPE_CTRACE_WORDS words; it takes precedence):
  *   - a preconditions skip (engine.go:282-284): "preconditions not met; <condition message>" of
  *     any validate rule, for preconditions evaluated per resource or folded at compile time;
  *   - validate.deny fail: getDenyMessage (validate_resource.go:279-300), the rule message joined
@@ -328,8 +345,26 @@ kpe_status kpe_fetch_cond_traces(kpe_device* dev, const kpe_program* prog, const
  *   - a PolicyException skip of a rule whose preconditions read the resource, once the trace
  *     shows they held ("rule skipped due to policy exception <key>").
  * Preconditions and deny conditions are not substituted into condition messages before they join
- * (the reference substitutes only getDenyMessage's joined text). Not rendered: messages of
- * validate.foreach rules and their elements, and RuleError texts (the Go error strings). */
+ * (the reference substitutes only getDenyMessage's joined text).
+ * With cond_traces_ex (and the corpus, for the element's document):
+ *   - validate.foreach pass: "rule passed" (validate_resource.go:203); fail / error: the deciding
+ *     element's response wrapped once per nesting level, "validation failure: <message>"
+ *     (:239-247), where <message> is getDenyMessage over the element's context, the pattern /
+ *     anyPattern message of the entry's walk on the element (kpe_pattern_traces records the
+ *     foreach cell's element walk), or a RuleError text below; AddElementToContext's
+ *     "failed to process foreach: cannot use elementScope=true ..." (:218-221);
+ *   - RuleError texts: "failed to evaluate preconditions: <err>" (engine.go:279-281,
+ *     validate_resource.go:125-128), "failed to check deny conditions: <err>" (:269-271),
+ *     "variable substitution failed: <err>" (:139-141), "failed to deserialize anyPattern, expected
+ *     type array: <err>" (:347-350), with <err> the substitution error the reference words itself:
+ *     "failed to substitute variables in condition key|value: failed to resolve <var> at path <path>:
+ *     JMESPath query failed: Unknown key \"<k>\" in path" (variables/evaluate.go:14-27, vars.go:
+ *     311-389, context/evaluate.go:27-31), "invalid query (nil)", "expected string after
+ *     substituting variables in key ...", "failed to create handler for condition operator".
+ * Not rendered: pattern skips and empty-path pattern errors (their text is validate.go's chain of
+ * anchor errors with Go %v renderings of resource and pattern values), errors whose text
+ * go-jmespath words itself (a function's argument error), messages with variables outside the
+ * restated paths, element<n> variables of an outer foreach level, and the RuleResponse timestamp. */
 typedef struct kpe_report_args {
   const kpe_program* prog;
   const kpe_corpus* corpus;        /* pattern traces' key names; may be NULL without pattern traces */
@@ -339,6 +374,7 @@ typedef struct kpe_report_args {
   const uint32_t* cond_traces;     /* R words of kpe_fetch_cond_traces, or NULL */
   const char* resource_json;       /* the resource (NULL: no messages) */
   size_t resource_len;
+  const uint32_t* cond_traces_ex;  /* R x KPE_CTRACE_WORDS words of kpe_fetch_cond_traces_ex, or NULL */
 } kpe_report_args;
 long kpe_report_results_ex(const kpe_report_args* args, char* buf, size_t cap);
 

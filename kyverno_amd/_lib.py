@@ -98,6 +98,7 @@ def load():
     L.kpe_fetch_cond_traces.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp]
     L.kpe_fetch_cond_traces.restype = ctypes.c_int
     L.kpe_report_results_ex.argtypes = [vp, ctypes.c_char_p, sz]
+    L.kpe_fetch_cond_traces_ex.argtypes = [vp, vp, vp, ctypes.c_uint64, ctypes.c_uint64, vp]
     L.kpe_report_results_ex.restype = ctypes.c_long
     L.kpe_cli_summary.argtypes = [vp, ctypes.POINTER(Counts), i32, ctypes.POINTER(CliTotals)]
     L.kpe_device_set_timing.argtypes = [vp, i32]

@@ -1154,8 +1154,12 @@ struct CondVM {
       const uint32_t b = side ? 3u : 0u;
       const int st = value(side ? c.value : c.key, b, b + 1u, b + 2u, &kv[side]);
       if (st == CS_UNDEC) return CB_UNDEC;
-      if (st != CS_OK) return CB_ERROR;
+      if (st != CS_OK) {
+        bt = (uint32_t)side << 7;  // the substitution error's side (CT_ERR_SIDE)
+        return CB_ERROR;
+      }
     }
+    bt = 2u << 7;  // an operator error
     const CV k = kv[0], v = kv[1];
     int r;
     if (c.op <= CO_NE) r = op_equals(k, v, c.op == CO_NE);
@@ -1177,7 +1181,10 @@ struct CondVM {
     const uint32_t n = b.nany + b.nall;
     for (uint32_t i = has_any ? 0u : b.nany; i < n; ++i) {  // any (when present), then all
       const int r = condition(b.c0 + i);
-      if (r >= CB_ERROR) return r;
+      if (r >= CB_ERROR) {
+        bt |= i;  // CT_ERR_COND: the condition that raised it
+        return r;
+      }
       if (i < b.nany) {
         if (r == CB_TRUE) {  // the first true `any` condition ends the any loop
           any_ok = true;
@@ -1264,6 +1271,8 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
     uint32_t mtv = 0;
     if (mt) *mt = 0u;
     if (cell == KPE_NA_) continue;  // the rule did not match
+    const bool fe_tr = mt && cr.kind == CR_FOREACH;  // four trace words (KPE_FE_TRACE_WORDS)
+    if (fe_tr) mt[1] = 0u;
     // A PolicyException the scan decided already made the cell RuleSkip (validate_resource.go:
     // 44-56 returns before the deny / foreach is evaluated). A deferred one (XC_DEFER) is applied
     // here after the preconditions, in the cells whose exception match held (KPE_XDEFER_).
@@ -1275,6 +1284,22 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
     vm.dep = -1;
     uint32_t ev = 0;            // the current element's verdict (PH_FE_RES) / a level's result (PH_FE_POP)
     uint32_t pk = 0, pend = 0;  // pattern variable slots being resolved
+    // a foreach element whose verdict may decide the cell (FAIL / ERROR): its path, what decided
+    // it and its tape entries (schema.h FT_*); a later candidate replaces it, and the one that
+    // propagates to the cell is always the last
+    auto cand = [&](uint32_t kind, uint32_t ct, CV el, uint32_t scoped) {
+      if (!fe_tr) return;
+      uint32_t b = (uint32_t)vm.dep | kind << 2 | FT_VALID;
+      for (int l = 0; l <= vm.dep; ++l) {
+        const uint32_t left = fr[l].fend - fr[l].f, idx = fr[l].idx;
+        if (left > 7u || idx > 31u) b |= FT_OVERFLOW;
+        b |= ((left & 7u) | (idx & 31u) << 3) << (8u + 8u * (uint32_t)l);
+      }
+      mt[1] = b;
+      mt[2] = el.k == VK_NODE ? el.p : 0xFFFFFFFFu;
+      mt[3] = scoped;
+      mtv = (mtv & 0xFFFFu) | ct << 16;
+    };
     while (ph != PH_DONE) {
       if (ph == PH_HANDLER) {
         if (cr.kind == CR_DENY) {
@@ -1342,6 +1367,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
               v = KPE_ERROR_;
               ph = PH_DONE;
             } else {
+              cand(FT_PVAR_ERR, 0u, vm.els[vm.dep], F.scoped);
               ev = KPE_ERROR_;
               ph = PH_FE_RES;
             }
@@ -1379,6 +1405,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         }
         const bool is_map = vm.type(el) == JT_OBJ;
         if (F.fe.scope == 2u && !is_map) {  // AddElementToContext: elementScope needs a map (RuleError)
+          cand(FT_SCOPE_ERR, 0u, el, kNoNode);
           ev = KPE_ERROR_;
           ph = PH_FE_POP;
           continue;
@@ -1438,6 +1465,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
           }
           ev = !(pf & PR_ANY) || (pf & PR_ANY_BAD) ? last
                                                    : passed ? KPE_PASS_ : (fails ? KPE_FAIL_ : (skips ? KPE_SKIP_ : KPE_PASS_));
+          if (ev == KPE_FAIL_ || ev == KPE_ERROR_) cand(FT_PAT, 0u, vm.els[vm.dep], F.scoped);
         }
         ph = PH_FE_RES;
         continue;
@@ -1471,8 +1499,11 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         ph = PH_DONE;
         continue;
       }
-      if (mt && (ph == PH_PRE || ph == PH_DENY) && res <= CB_TRUE)  // the block's messages (CT_*)
-        mtv |= ((vm.bt & 0x3FFFu) | CT_EVAL | (res == CB_TRUE ? CT_TRUE : 0u)) << (ph == PH_DENY ? 16u : 0u);
+      if (mt && (ph == PH_PRE || ph == PH_DENY)) {  // the block's messages (CT_*) or its error
+        const uint32_t t = res == CB_ERROR ? (vm.bt & 0x1FFu) | CT_ERR
+                                           : (vm.bt & 0x3FFFu) | CT_EVAL | (res == CB_TRUE ? CT_TRUE : 0u);
+        mtv |= t << (ph == PH_DENY ? 16u : 0u);
+      }
       if (ph == PH_PRE) {  // engine.go:278-285: false => skip, error => error
         if (res == CB_TRUE) {
           ph = xd ? PH_EXC : PH_HANDLER;
@@ -1497,10 +1528,13 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         if (res == CB_TRUE) {
           ph = PH_FE_BODY;
         } else {
+          if (res == CB_ERROR) cand(FT_PRE_ERR, (vm.bt & 0x1FFu) | CT_ERR, vm.els[vm.dep], F.scoped);
           ev = res == CB_FALSE ? KPE_SKIP_ : KPE_ERROR_;
           ph = PH_FE_RES;
         }
       } else {  // an element's deny: true => fail
+        if (res == CB_TRUE) cand(FT_DENY, (vm.bt & 0x3FFFu) | CT_EVAL | CT_TRUE, vm.els[vm.dep], F.scoped);
+        else if (res == CB_ERROR) cand(FT_DENY, (vm.bt & 0x1FFu) | CT_ERR, vm.els[vm.dep], F.scoped);
         ev = res == CB_TRUE ? KPE_FAIL_ : res == CB_FALSE ? KPE_PASS_ : KPE_ERROR_;
         ph = PH_FE_RES;
       }

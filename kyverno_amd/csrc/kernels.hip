@@ -1261,11 +1261,14 @@ extern "C" hipError_t kpe_launch_pssx(const PssxArgs* dargs, int64_t n, hipStrea
 
 // Failing paths of listed pattern cells (kpe_pattern_traces): one lane per cell (row * R + col)
 // walks each root of the cell's rule (at most KPE_TRACE_ROOTS) from the tape in HBM with the
-// VM's TRACE instance, which records the path of the last failure (PatternError.Path). Report
-// time only; the evaluation kernels never carry the tracing code.
+// VM's TRACE instance, which records the path of the last failure (PatternError.Path). A cell
+// with a job (jobs[i].w != 0: a validate.foreach cell that a pattern entry decided) walks the
+// entry's roots [x, x + y & 0xFFFF) (PR_* flags in y >> 16) from the element node z (kNoNode: the
+// resource root) instead. Report time only; the evaluation kernels never carry the tracing code.
 __global__ void __launch_bounds__(128) kpe_pattern_trace_kernel(const PatArgs* __restrict__ ap,
                                                                  const uint64_t* __restrict__ cells, uint64_t n,
-                                                                 uint32_t* __restrict__ out) {
+                                                                 uint32_t* __restrict__ out,
+                                                                 const uint4* __restrict__ jobs) {
   const uint64_t i = (uint64_t)blockIdx.x * 128u + threadIdx.x;
   if (i >= n) return;
   const PatArgs& a = *ap;
@@ -1274,9 +1277,18 @@ __global__ void __launch_bounds__(128) kpe_pattern_trace_kernel(const PatArgs* _
   const uint64_t cell = cells[i];
   const uint64_t row = cell / a.R;
   const uint32_t col = (uint32_t)(cell - row * a.R);
-  if (row >= (uint64_t)a.n || !a.col2pr || a.col2pr[col] == 0u) return;
-  const KpePatRule pr = a.rules[a.col2pr[col] - 1u];
-  PatVM vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), (uint32_t)a.doc_off[row],
+  if (row >= (uint64_t)a.n) return;
+  const uint4 job = jobs ? jobs[i] : make_uint4(0u, 0u, 0u, 0u);
+  KpePatRule pr;
+  uint32_t start = (uint32_t)a.doc_off[row];
+  if (job.w) {
+    pr.r0 = job.x, pr.nr = job.y & 0xFFFFu, pr.flags = job.y >> 16;
+    if (job.z != kNoNode) start = job.z;
+  } else {
+    if (!a.col2pr || a.col2pr[col] == 0u) return;
+    pr = a.rules[a.col2pr[col] - 1u];
+  }
+  PatVM vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), start,
            a.pvals + (size_t)row * a.nvars, 0u};
   if (pr.flags & PR_ANY_BAD) {
     rec[0] = KPE_TR_VALID | ((uint32_t)KPE_ERROR_ << 16);
@@ -1290,9 +1302,10 @@ __global__ void __launch_bounds__(128) kpe_pattern_trace_kernel(const PatArgs* _
 }
 
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
-                                               hipStream_t s) {
+                                               const uint4* jobs, hipStream_t s) {
   if (!n) return hipSuccess;
-  hipLaunchKernelGGL(kpe_pattern_trace_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs, cells, n, out);
+  hipLaunchKernelGGL(kpe_pattern_trace_kernel, dim3((unsigned)((n + 127) / 128)), dim3(128), 0, s, dargs, cells, n, out,
+                     jobs);
   return hipGetLastError();
 }
 

@@ -33,7 +33,7 @@ bool is_limit_error(const std::exception& e);
 extern "C" hipError_t kpe_launch_pred(const PredArgs* a, uint32_t nblocks, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lt, hipStream_t s);
 extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint64_t* cells, uint64_t n, uint32_t* out,
-                                               hipStream_t s);
+                                               const uint4* jobs, hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, int txt, hipStream_t s);
 extern "C" hipError_t kpe_launch_fill_rows(uint8_t* verdicts, uint32_t R, const uint32_t* rows, uint32_t nrows,
                                            uint8_t value, hipStream_t s);
@@ -1975,6 +1975,26 @@ kpe_status kpe_unpack_verdicts(const uint32_t* packed, uint64_t cells, uint8_t* 
 }
 
 // ---- failing paths of pattern cells (report time) ---------------------------------------------
+// The foreach entry that decided a FAIL / ERROR cell from its trace words (schema.h FT_*): the
+// entry index in Program::fe_reports, or -1 (no valid path)
+static int64_t fe_decider(const kpe::Program& P, const kpe::RuleReport& rr, uint32_t b) {
+  if (!rr.foreach || !(b & FT_VALID) || (b & FT_OVERFLOW)) return -1;
+  uint32_t first = rr.fe0, count = rr.nfe;
+  int64_t e = -1;
+  for (uint32_t l = 0; l <= FT_DEPTH(b); ++l) {
+    const uint32_t left = FT_LEFT(b, l);
+    if (left == 0 || left > count) return -1;
+    e = (int64_t)first + (count - left);
+    if ((size_t)e >= P.fe_reports.size()) return -1;
+    if (l < FT_DEPTH(b)) {
+      const kpe::FeReport& f = P.fe_reports[(size_t)e];
+      if (f.kind != FE_NEST) return -1;
+      first = f.nested0, count = f.nnested;
+    }
+  }
+  return e;
+}
+
 kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, const uint64_t* cells,
                               uint64_t ncells, uint32_t* out) {
   if (!dev || !prog || !c || !c->d || (ncells && (!cells || !out))) return fail(KPE_E_INVALID, "null argument");
@@ -1982,29 +2002,58 @@ kpe_status kpe_pattern_traces(kpe_device* dev, const kpe_program* prog, const kp
   std::lock_guard<std::mutex> lk(dev->mu);
   HIPCHK(hipSetDevice(dev->ordinal));
   auto& B = c->d->bind;
+  const kpe::Program& P = *prog->p;
   if (B.prog != prog->p.get()) return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
   if (c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
-  const uint64_t total = (uint64_t)c->c->n * prog->p->rules.size();
+  const size_t R = P.rules.size();
+  const uint64_t total = (uint64_t)c->c->n * R;
   for (uint64_t i = 0; i < ncells; ++i)
     if (cells[i] >= total) return fail(KPE_E_INVALID, "cell index past the verdict matrix");
   const size_t rec = (size_t)KPE_TRACE_ROOTS * KPE_TRACE_WORDS;
-  if (!prog->p->pat.rules.empty() && !B.pargs_valid)
-    return fail(KPE_E_STATE, "the binding has no completed evaluation of its pattern rules");
-  if (prog->p->pat.rules.empty()) {  // no pattern rule: every record is empty
+  hipStream_t s = B.last ? B.last : dev->stream;
+  // foreach cells decided by a pattern entry: the entry's roots on the element (the condition
+  // kernel's trace words of the cell)
+  std::vector<uint4> jobs;
+  if (P.any_fe_pat && B.cargs_valid && P.cond.nmsg) {
+    std::vector<int32_t> slot(R, -1);
+    for (const KpeCRule& cr : P.cond.rules)
+      if (cr.mslot && cr.kind == CR_FOREACH) slot[cr.col] = (int32_t)cr.mslot - 1;
+    HIPCHK(hipStreamSynchronize(s));
+    for (uint64_t i = 0; i < ncells; ++i) {
+      const uint64_t row = cells[i] / R;
+      const uint32_t col = (uint32_t)(cells[i] % R);
+      if (slot[col] < 0) continue;
+      if (jobs.empty()) jobs.assign(ncells, make_uint4(0u, 0u, 0u, 0u));
+      uint32_t w[KPE_FE_TRACE_WORDS];
+      HIPCHK(hipMemcpy(w, B.mtrace.as<uint32_t>() + row * P.cond.nmsg + (size_t)slot[col], sizeof w,
+                       hipMemcpyDeviceToHost));
+      if (FT_KIND(w[1]) != FT_PAT || w[3] == 0xFFFFFFFEu) continue;
+      const int64_t e = fe_decider(P, P.reports[col], w[1]);
+      if (e < 0) continue;
+      const KpeCForeach& fe = P.cond.fes[(size_t)e];
+      if (fe.kind != FE_PAT) continue;
+      jobs[i] = make_uint4(fe.a, fe.b, w[3], 1u);
+    }
+  }
+  if (P.pat.rules.empty() && jobs.empty()) {  // no pattern walk: every record is empty
     memset(out, 0, ncells * rec * 4);
     return KPE_OK;
   }
-  hipStream_t s = B.last ? B.last : dev->stream;
-  void *dc = nullptr, *dout = nullptr;
+  if (!B.pargs_valid) return fail(KPE_E_STATE, "the binding has no completed evaluation of its pattern rules");
+  void *dc = nullptr, *dout = nullptr, *dj = nullptr;
   hipError_t e = hipMalloc(&dc, ncells * 8);
   if (e == hipSuccess) e = hipMalloc(&dout, ncells * rec * 4);
+  if (e == hipSuccess && !jobs.empty()) e = hipMalloc(&dj, ncells * sizeof(uint4));
   if (e == hipSuccess) e = hipMemcpyAsync(dc, cells, ncells * 8, hipMemcpyHostToDevice, s);
+  if (e == hipSuccess && dj) e = hipMemcpyAsync(dj, jobs.data(), ncells * sizeof(uint4), hipMemcpyHostToDevice, s);
   if (e == hipSuccess)
-    e = kpe_launch_pattern_trace(B.pargs.as<PatArgs>(), (const uint64_t*)dc, ncells, (uint32_t*)dout, s);
+    e = kpe_launch_pattern_trace(B.pargs.as<PatArgs>(), (const uint64_t*)dc, ncells, (uint32_t*)dout,
+                                 (const uint4*)dj, s);
   if (e == hipSuccess) e = hipMemcpyAsync(out, dout, ncells * rec * 4, hipMemcpyDeviceToHost, s);
   if (e == hipSuccess) e = hipStreamSynchronize(s);
   if (dc) (void)hipFree(dc);
   if (dout) (void)hipFree(dout);
+  if (dj) (void)hipFree(dj);
   HIPCHK(e);
   return KPE_OK;
 }
@@ -2033,6 +2082,35 @@ kpe_status kpe_fetch_cond_traces(kpe_device* dev, const kpe_program* prog, const
   for (const KpeCRule& cr : P.cond.rules)
     if (cr.mslot)
       for (uint64_t i = 0; i < nrows; ++i) out[i * R + cr.col] = h[i * m + cr.mslot - 1u];
+  return KPE_OK;
+}
+
+kpe_status kpe_fetch_cond_traces_ex(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c, uint64_t row0,
+                                    uint64_t nrows, uint32_t* out) {
+  if (!dev || !prog || !c || !c->d || (nrows && !out)) return fail(KPE_E_INVALID, "null argument");
+  if (row0 > (uint64_t)c->c->n || nrows > (uint64_t)c->c->n - row0) return fail(KPE_E_INVALID, "rows past the corpus");
+  if (!nrows) return KPE_OK;
+  const kpe::Program& P = *prog->p;
+  const size_t R = P.rules.size(), W = KPE_CTRACE_WORDS;
+  memset(out, 0, nrows * R * W * 4);
+  if (!P.cond.nmsg) return KPE_OK;
+  std::lock_guard<std::mutex> lk(dev->mu);
+  HIPCHK(hipSetDevice(dev->ordinal));
+  auto& B = c->d->bind;
+  if (B.prog != prog->p.get() || !B.cargs_valid)
+    return fail(KPE_E_STATE, "no evaluation of this program on this corpus");
+  if (c->d->ordinal != dev->ordinal) return fail(KPE_E_STATE, "corpus not uploaded to this device");
+  const size_t m = P.cond.nmsg;
+  std::vector<uint32_t> h(nrows * m);
+  hipStream_t s = B.last ? B.last : dev->stream;
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipMemcpy(h.data(), B.mtrace.as<uint32_t>() + row0 * m, h.size() * 4, hipMemcpyDeviceToHost));
+  for (const KpeCRule& cr : P.cond.rules) {
+    if (!cr.mslot) continue;
+    const size_t nw = cr.kind == CR_FOREACH ? KPE_FE_TRACE_WORDS : 1u;
+    for (uint64_t i = 0; i < nrows; ++i)
+      for (size_t w = 0; w < nw; ++w) out[(i * R + cr.col) * W + w] = h[i * m + cr.mslot - 1u + w];
+  }
   return KPE_OK;
 }
 
@@ -2155,63 +2233,205 @@ static bool trace_path(const kpe::Program& P, const kpe::Corpus* C, const uint32
 }
 
 // validate_resource.go:316-454: pattern / anyPattern messages from the cell's trace (roots in
-// order); empty when the reference's text would need an error string the device does not keep
-// (an empty-path PatternError, a skip) or a substituted message
-static std::string pattern_message(const kpe::Program& P, const kpe::Corpus* C, const kpe::RuleReport& rr, uint8_t v,
-                                   const uint32_t* tr, const char* json, size_t json_len) {
+// order) of rule `rule` with validate.message `vmsg` (substituted over the resource and, in a
+// foreach, the element `el`); empty when the reference's text would need an error string the
+// device does not keep (an empty-path PatternError, a skip) or a substituted message
+static std::string pattern_msg(const kpe::Program& P, const kpe::Corpus* C, const std::string& rule,
+                               const std::string& vmsg, bool any, uint32_t roots, uint8_t v, const uint32_t* tr,
+                               const char* json, size_t json_len, const kpe::MsgElem* el) {
   auto root = [&](uint32_t k) { return tr + (size_t)k * KPE_TRACE_WORDS; };
   auto rv = [&](uint32_t k) { return (root(k)[0] & KPE_TR_VALID) ? (root(k)[0] >> 16) & 0xFFu : 0xFFu; };
-  if (!rr.any_pattern) {
+  if (!any) {
     if (v != KPE_FAIL || rv(0) != KPE_FAIL) return "";
     std::string path;
     if (!trace_path(P, C, root(0), &path)) return "";
-    if (rr.vmsg.empty()) return "validation error: rule " + rr.rule + " failed at path " + path;  // buildErrorMessage
-    std::string m = rr.vmsg;
-    if (rr.vmsg_vars) {  // buildErrorMessage: SubstituteAll of the message (a non-string value: no text)
+    if (vmsg.empty()) return "validation error: rule " + rule + " failed at path " + path;  // buildErrorMessage
+    std::string m = vmsg;
+    if (vmsg.find("{{") != std::string::npos || vmsg.find("$(") != std::string::npos) {
+      // buildErrorMessage: SubstituteAll of the message (a non-string value: no text)
       bool nonstring = false;
-      if (!kpe::substitute_message(rr.vmsg, json, json_len, &m, &nonstring) || nonstring) return "";
+      if (!kpe::substitute_message(vmsg, json, json_len, &m, &nonstring, nullptr, el) || nonstring) return "";
     }
     if (m.empty() || m.back() != '.') m += '.';
-    return "validation error: " + m + " rule " + rr.rule + " failed at path " + path;
+    return "validation error: " + m + " rule " + rule + " failed at path " + path;
   }
   if (v == KPE_PASS) {
-    if (rr.pat_roots == 0) return rr.vmsg;  // no pattern at all: RulePass(rule.Validation.Message)
-    for (uint32_t k = 0; k < rr.pat_roots && k < KPE_TRACE_ROOTS; ++k) {
-      if (rv(k) == KPE_PASS) return "validation rule '" + rr.rule + "' anyPattern[" + std::to_string(k) + "] passed.";
+    if (roots == 0) return vmsg;  // no pattern at all: RulePass(rule.Validation.Message)
+    for (uint32_t k = 0; k < roots && k < KPE_TRACE_ROOTS; ++k) {
+      if (rv(k) == KPE_PASS) return "validation rule '" + rule + "' anyPattern[" + std::to_string(k) + "] passed.";
       if (rv(k) == 0xFFu || rv(k) == KPE_UNDECIDED) return "";
     }
     return "";
   }
-  if (v != KPE_FAIL || rr.pat_roots > KPE_TRACE_ROOTS) return "";
+  if (v != KPE_FAIL || roots > KPE_TRACE_ROOTS) return "";
   std::string errs;
-  for (uint32_t k = 0; k < rr.pat_roots; ++k) {
+  for (uint32_t k = 0; k < roots; ++k) {
     const uint32_t x = rv(k);
     if (x == KPE_SKIP) continue;  // skipped patterns are not listed once one failed
     if (x != KPE_FAIL) return "";  // an empty-path failure's message is its error text
     std::string path;
     if (!trace_path(P, C, root(k), &path)) return "";
-    errs += (errs.empty() ? "" : " ") + ("rule " + rr.rule + "[" + std::to_string(k) + "] failed at path " + path);
+    errs += (errs.empty() ? "" : " ") + ("rule " + rule + "[" + std::to_string(k) + "] failed at path " + path);
   }
   if (errs.empty()) return "";
-  if (rr.vmsg.empty()) return "validation error: " + errs;  // buildAnyPatternErrorMessage
-  if (rr.vmsg.back() == '.') return "validation error: " + rr.vmsg + " " + errs;
-  return "validation error: " + rr.vmsg + ". " + errs;
+  if (vmsg.empty()) return "validation error: " + errs;  // buildAnyPatternErrorMessage
+  if (vmsg.back() == '.') return "validation error: " + vmsg + " " + errs;
+  return "validation error: " + vmsg + ". " + errs;
+}
+static std::string pattern_message(const kpe::Program& P, const kpe::Corpus* C, const kpe::RuleReport& rr, uint8_t v,
+                                   const uint32_t* tr, const char* json, size_t json_len) {
+  return pattern_msg(P, C, rr.rule, rr.vmsg, rr.any_pattern, rr.pat_roots, v, tr, json, json_len, nullptr);
+}
+
+// getDenyMessage (validate_resource.go:279-300) of a failing deny block whose condition message is
+// `cm`: SubstituteAll of JoinNonEmpty(rule message, cm) over the context (the resource, and the
+// foreach element `el`); on a substitution error the condition message as is; a message outside
+// the restated variables: none
+static std::string deny_msg(const std::string& rule, const std::string& vmsg, const std::string& cm, const char* json,
+                            size_t n, const kpe::MsgElem* el) {
+  if (vmsg.empty() && cm.empty()) return "validation error: rule " + rule + " failed";
+  const std::string j = kpe::join_non_empty({vmsg, cm}, "; ");
+  std::string out;
+  bool nonstring = false, serr = false;
+  if (!kpe::substitute_message(j, json, n, &out, &nonstring, &serr, el)) return serr ? cm : std::string();
+  return nonstring ? "the produced message didn't resolve to a string, check your policy definition." : out;
+}
+
+// The document of tape entry e as JSON text (the foreach element: a node of the resource's
+// document; Go's JSON context holds it with float64 numbers, which the renderers print alike)
+static bool tape_json(const kpe::Corpus& C, uint32_t e, std::string& o, int depth = 0) {
+  if ((size_t)e * 2 + 1 >= C.doc.size() || depth > 300) return false;
+  const uint32_t x = C.doc[(size_t)e * 2], y = C.doc[(size_t)e * 2 + 1];
+  auto str = [&](std::string_view t) {
+    o += '"';
+    for (unsigned char ch : t) {
+      if (ch == '"' || ch == '\\') o += '\\', o += (char)ch;
+      else if (ch < 0x20) {
+        char b[8];
+        snprintf(b, sizeof b, "\\u%04x", ch);
+        o += b;
+      } else o += (char)ch;
+    }
+    o += '"';
+  };
+  if (DN_KIND(x) == DN_SCALAR) {
+    if (y >= C.scal.size()) return false;
+    const KpeScalar& sc = C.scal[y];
+    char b[40];
+    switch (SC_TYPE(sc.flags)) {
+      case SC_T_NULL: o += "null"; break;
+      case SC_T_BOOL: o += (y == SC_TRUE_ID || (sc.flags & SC_BTRUE)) ? "true" : "false"; break;
+      case SC_T_INT: o += std::to_string(sc.ival); break;
+      case SC_T_FLOAT:
+        snprintf(b, sizeof b, "%.17g", sc.fval);
+        o += b;
+        break;
+      default: str(C.scal_text_of(y));
+    }
+    return true;
+  }
+  if ((size_t)y * 2 + 1 >= C.doc.size()) return false;
+  const uint32_t cnt = C.doc[(size_t)y * 2];
+  const bool map = DN_KIND(x) == DN_MAP;
+  o += map ? '{' : '[';
+  for (uint32_t k = 0; k < cnt; ++k) {
+    const uint32_t m = y + 1 + k;
+    if ((size_t)m * 2 >= C.doc.size()) return false;
+    if (k) o += ',';
+    if (map) {
+      const uint32_t key = DN_KEY(C.doc[(size_t)m * 2]);
+      if (key == 0 || key - 1 >= C.dict[D_KEY].size()) return false;
+      str(C.dict[D_KEY].at(key - 1));
+      o += ':';
+    }
+    if (!tape_json(C, m, o, depth + 1)) return false;
+  }
+  o += map ? '}' : ']';
+  return true;
+}
+// %T of a tape entry as the JSON context holds it
+static const char* tape_go_type(const kpe::Corpus& C, uint32_t e) {
+  if ((size_t)e * 2 + 1 >= C.doc.size()) return nullptr;
+  const uint32_t x = C.doc[(size_t)e * 2], y = C.doc[(size_t)e * 2 + 1];
+  if (DN_KIND(x) == DN_MAP) return "map[string]interface {}";
+  if (DN_KIND(x) == DN_ARR) return "[]interface {}";
+  if (y >= C.scal.size()) return nullptr;
+  switch (SC_TYPE(C.scal[y].flags)) {
+    case SC_T_BOOL: return "bool";
+    case SC_T_INT:
+    case SC_T_FLOAT: return "float64";
+    case SC_T_STR: return "string";
+    default: return nullptr;
+  }
+}
+
+// The message of a validate.foreach cell (validateForEach / validateElements,
+// validate_resource.go:186-254) from its condition trace words `w` (schema.h FT_*) and, for an
+// entry's pattern, the cell's pattern trace `ptr`
+static std::string foreach_message(const kpe::Program& P, const kpe::Corpus* C, const kpe::RuleReport& rr, uint8_t v,
+                                   const uint32_t* w, const uint32_t* ptr, const char* json, size_t n) {
+  if (v == KPE_PASS) return "rule passed";  // :203
+  if ((v != KPE_FAIL && v != KPE_ERROR) || !w) return "";
+  const uint32_t b = w[1];
+  const int64_t ei = fe_decider(P, rr, b);
+  if (ei < 0) return "";
+  const kpe::FeReport& f = P.fe_reports[(size_t)ei];
+  const uint32_t depth = FT_DEPTH(b), ct = w[0] >> 16;
+  kpe::MsgElem me;
+  const kpe::MsgElem* el = nullptr;
+  if (C && w[2] != 0xFFFFFFFFu && tape_json(*C, w[2], me.json)) {
+    me.depth = (int)depth, me.index = FT_IDX(b, depth);
+    el = &me;
+  }
+  std::string leaf, e;
+  uint32_t wraps = depth + 1;  // validateElements wraps the response once per level
+  switch (FT_KIND(b)) {
+    case FT_SCOPE_ERR: {  // AddElementToContext (:218-221, utils/foreach.go:51-54): not wrapped at its level
+      const char* t = C && w[2] != 0xFFFFFFFFu ? tape_go_type(*C, w[2]) : nullptr;
+      if (!t) return "";
+      leaf = std::string("failed to process foreach: cannot use elementScope=true foreach rules for elements that "
+                         "are not maps, expected type=map got type=") + t;
+      wraps = depth;
+      break;
+    }
+    case FT_PRE_ERR:  // the element's preconditions (:125-128)
+      if ((e = kpe::block_error_text(f.pre_json, ct, json, n, el)).empty()) return "";
+      leaf = "failed to evaluate preconditions: " + e;
+      break;
+    case FT_DENY:
+      if (CT_IS_ERR(ct)) {  // :269-271
+        if ((e = kpe::block_error_text(f.deny_json, ct, json, n, el)).empty()) return "";
+        leaf = "failed to check deny conditions: " + e;
+      } else if ((ct & (CT_EVAL | CT_TRUE)) == (CT_EVAL | CT_TRUE)) {  // getDenyMessage over the element
+        leaf = deny_msg(rr.rule, rr.vmsg, f.deny_msgs.render(CT_ANY(ct), CT_ALL(ct), true), json, n, el);
+      }
+      break;
+    case FT_PVAR_ERR:  // substitutePatterns (:139-141)
+      if ((e = kpe::doc_subst_error(f.pattern_json, json, n, el)).empty()) return "";
+      leaf = "variable substitution failed: " + e;
+      break;
+    case FT_PAT:
+      if (!f.any_bad_type.empty()) {  // deserializeAnyPattern (:347-350)
+        leaf = "failed to deserialize anyPattern, expected type array: json: cannot unmarshal " + f.any_bad_type +
+               " into Go value of type []interface {}";
+      } else if (ptr) {
+        leaf = pattern_msg(P, C, rr.rule, rr.vmsg, f.any, f.nroots, v, ptr, json, n, el);
+      }
+      break;
+    default: break;
+  }
+  if (leaf.empty()) return "";
+  for (uint32_t k = 0; k < wraps; ++k) leaf = "validation failure: " + leaf;
+  return leaf;
 }
 
 static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const uint8_t* verdict_row,
                         const uint32_t* cv_mask_row, const uint32_t* traces, const uint32_t* cond_traces,
-                        const char* resource_json, size_t resource_len, char* buf, size_t cap);
+                        const char* resource_json, size_t resource_len, char* buf, size_t cap,
+                        const uint32_t* cond_traces_ex = nullptr);
 
-// getDenyMessage (validate_resource.go:279-300) of a failing deny rule whose deny block's
-// condition message is `cm`: SubstituteAll of JoinNonEmpty(rule message, cm); on a substitution
-// error the condition message as is; a message outside the restated variables: none
 static std::string deny_message(const kpe::RuleReport& rr, const std::string& cm, const char* json, size_t n) {
-  if (rr.deny_vmsg.empty() && cm.empty()) return "validation error: rule " + rr.rule + " failed";
-  const std::string j = kpe::join_non_empty({rr.deny_vmsg, cm}, "; ");
-  std::string out;
-  bool nonstring = false, serr = false;
-  if (!kpe::substitute_message(j, json, n, &out, &nonstring, &serr)) return serr ? cm : std::string();
-  return nonstring ? "the produced message didn't resolve to a string, check your policy definition." : out;
+  return deny_msg(rr.rule, rr.deny_vmsg, cm, json, n, nullptr);
 }
 
 long kpe_report_results_ex(const kpe_report_args* a, char* buf, size_t cap) {
@@ -2220,7 +2440,7 @@ long kpe_report_results_ex(const kpe_report_args* a, char* buf, size_t cap) {
     return -KPE_E_INVALID;
   }
   return report_impl(a->prog, a->corpus, a->verdict_row, a->cv_mask_row, a->pattern_traces, a->cond_traces,
-                     a->resource_json, a->resource_len, buf, cap);
+                     a->resource_json, a->resource_len, buf, cap, a->cond_traces_ex);
 }
 
 long kpe_report_results_msg(const kpe_program* prog, const uint8_t* verdict_row, const uint32_t* cv_mask_row,
@@ -2236,7 +2456,8 @@ long kpe_report_results_msg_tr(const kpe_program* prog, const kpe_corpus* corpus
 
 static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const uint8_t* verdict_row,
                         const uint32_t* cv_mask_row, const uint32_t* traces, const uint32_t* cond_traces,
-                        const char* resource_json, size_t resource_len, char* buf, size_t cap) {
+                        const char* resource_json, size_t resource_len, char* buf, size_t cap,
+                        const uint32_t* cond_traces_ex) {
   if (!prog || !verdict_row) {
     fail(KPE_E_INVALID, "null argument");
     return -KPE_E_INVALID;
@@ -2261,14 +2482,32 @@ static long report_impl(const kpe_program* prog, const kpe_corpus* corp, const u
     json_str(o, rr.policy_key);
     // the skip's cause: preconditions false (folded at compile time, or the condition trace's
     // preconditions half) or the rule's PolicyException (after preconditions that held)
-    const uint32_t ct = (cond_traces && rr.cond_slot) ? cond_traces[r] : 0u;
+    const uint32_t* cx = (cond_traces_ex && rr.cond_slot) ? cond_traces_ex + r * (size_t)KPE_CTRACE_WORDS : nullptr;
+    const uint32_t ct = cx ? cx[0] : (cond_traces && rr.cond_slot) ? cond_traces[r] : 0u;
     const uint32_t held = CT_EVAL | CT_TRUE;
     const bool pre_skip = v == KPE_SKIP && (rr.pre_const_skip || (ct & held) == CT_EVAL);
     const bool exc_skip = v == KPE_SKIP && !rr.exc_key.empty() && !pre_skip &&
                           (!rr.exc_after_pre || (ct & held) == held);
     if (resource_json) {  // RuleResponse message (validate_pss.go:85,108; validate_resource.go:339)
       std::string msg;
-      if (rr.pss && v == KPE_PASS) {
+      const kpe::Corpus* C = corp ? corp->c.get() : nullptr;
+      const uint32_t* ptr = traces ? traces + r * (size_t)(KPE_TRACE_ROOTS * KPE_TRACE_WORDS) : nullptr;
+      std::string e;
+      if (v == KPE_ERROR && rr.cond_slot && CT_IS_ERR(ct & 0xFFFFu)) {  // engine.go:279-281
+        if (!(e = kpe::block_error_text(rr.pre_json, ct & 0xFFFFu, resource_json, resource_len, nullptr)).empty())
+          msg = "failed to evaluate preconditions: " + e;
+      } else if (rr.foreach) {
+        msg = foreach_message(P, C, rr, v, cx, ptr, resource_json, resource_len);
+      } else if (v == KPE_ERROR && rr.msg_deny && rr.cond_slot && CT_IS_ERR(ct >> 16)) {  // :269-271
+        if (!(e = kpe::block_error_text(rr.deny_json, ct >> 16, resource_json, resource_len, nullptr)).empty())
+          msg = "failed to check deny conditions: " + e;
+      } else if (v == KPE_ERROR && !rr.any_bad_type.empty()) {  // :347-350
+        msg = "failed to deserialize anyPattern, expected type array: json: cannot unmarshal " + rr.any_bad_type +
+              " into Go value of type []interface {}";
+      } else if (v == KPE_ERROR && rr.pat_vars &&
+                 !(e = kpe::doc_subst_error(rr.pattern_json, resource_json, resource_len, nullptr)).empty()) {
+        msg = "variable substitution failed: " + e;  // :139-141
+      } else if (rr.pss && v == KPE_PASS) {
         msg = kpe::pss_pass_message(rr.rule);
       } else if (rr.pss && v == KPE_FAIL && !rr.pss_excl && cv_mask_row && (cv_mask_row[r] & KPE_CVM_CHECKS)) {
         if (!pod_state) pod_state = kpe::typed_pod_view(resource_json, resource_len, &pod, &kind) ? 1 : -1;

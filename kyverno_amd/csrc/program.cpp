@@ -189,6 +189,23 @@ JV parse_all(const char* p, size_t n) {
   if (!c.ok() || c.pos() != p + n) throw std::invalid_argument("malformed policy JSON");
   return v;
 }
+// document-order JSON of a policy fragment (reparsed by the message renderers)
+std::string doc_text(const JV& v) {
+  std::string o;
+  write(v, o);
+  return o;
+}
+// the JSON type encoding/json's UnmarshalTypeError names (decode.go: "object", "string", ...)
+const char* json_type_name(const JV& v) {
+  switch (v.t) {
+    case JV::Obj: return "object";
+    case JV::Str: return "string";
+    case JV::Bool: return "bool";
+    case JV::Num: return "number";
+    case JV::Arr: return "array";
+    default: return "null";
+  }
+}
 
 std::string sv(const JV* v) { return (v && v->t == JV::Str) ? v->s : std::string(); }
 std::vector<std::string> svl(const JV* v) {
@@ -1810,13 +1827,16 @@ class Lowerer {
   // nested levels are appended first, so each level's entries are contiguous. Returns the first.
   uint32_t foreach_entries(const JV& arr, uint32_t depth) {
     std::vector<KpeCForeach> fes;
+    std::vector<FeReport> reps;
     for (auto& e : arr.a) {
       if (e.t != JV::Obj) throw CompileError("foreach entry is not an object");
       if (nonempty(e.get("context"))) throw CompileError("foreach context entries are not supported on the device");
       KpeCForeach f{};
+      FeReport fr;
       f.list = CC.list_query(sv(e.get("list")));
       const JV* fp = e.get("preconditions");
       f.pre = (fp && fp->t != JV::Null) ? CC.block(fp) : CE_NONE;
+      if (f.pre != CE_NONE) fr.pre_json = doc_text(*fp);
       const JV* sc = e.get("elementScope");
       f.scope = (sc && sc->t == JV::Bool) ? (sc->b ? 2u : 1u) : 0u;
       auto present = [&](const char* key) { return e.get(key) && e.get(key)->t != JV::Null; };
@@ -1824,6 +1844,10 @@ class Lowerer {
         const JV* dn = e.get("deny");
         f.kind = FE_DENY;
         f.deny = CC.block(dn->t == JV::Obj ? dn->get("conditions") : nullptr);
+        if (dn->t == JV::Obj && dn->get("conditions")) {
+          fr.deny_json = doc_text(*dn->get("conditions"));
+          fr.deny_msgs = cond_msgs(dn->get("conditions"));
+        }
       } else if (present("pattern") || present("anyPattern")) {
         f.kind = FE_PAT;
         fe_pat_ = true;
@@ -1840,11 +1864,15 @@ class Lowerer {
         if (present("pattern")) {
           pcomp.root(*e.get("pattern"));
           nr = 1;
+          fr.pattern_json = doc_text(*e.get("pattern"));
         } else {
           const JV& ap = *e.get("anyPattern");
           flags = PR_ANY;
+          fr.any = true;
+          fr.pattern_json = doc_text(ap);
           if (ap.t != JV::Arr) {
             flags |= PR_ANY_BAD;
+            fr.any_bad_type = json_type_name(ap);
           } else {
             for (auto& x : ap.a) {
               JV g = x;
@@ -1858,6 +1886,7 @@ class Lowerer {
         if (nr > 0xFFFFu || pv0 > 0xFFFFu || npv > 0xFFFFu) throw CompileError("foreach pattern tables too large");
         f.b = nr | flags << 16;
         f.c = pv0 | npv << 16;
+        fr.root0 = f.a, fr.nroots = nr;
       } else if (present("foreach")) {
         const JV& nf = *e.get("foreach");
         if (nf.t != JV::Arr) throw CompileError("nested foreach is not a list");
@@ -1865,13 +1894,17 @@ class Lowerer {
         f.kind = FE_NEST;
         f.a = nf.a.empty() ? 0u : foreach_entries(nf, depth + 1);
         f.b = (uint32_t)nf.a.size();
+        fr.nested0 = f.a, fr.nnested = f.b;
       } else {
         f.kind = FE_NONE;  // "invalid validation rule": a nil response
       }
+      fr.kind = f.kind;
       fes.push_back(f);
+      reps.push_back(std::move(fr));
     }
     const uint32_t f0 = (uint32_t)P.cond.fes.size();
     P.cond.fes.insert(P.cond.fes.end(), fes.begin(), fes.end());
+    P.fe_reports.insert(P.fe_reports.end(), std::make_move_iterator(reps.begin()), std::make_move_iterator(reps.end()));
     return f0;
   }
   bool fe_pat_ = false;
@@ -2584,10 +2617,22 @@ class Lowerer {
         rr.cond_deny = rr.deny_msgs.has_text();
       }
     }
+    // a trace slot for every rule whose conditions are evaluated per resource (their messages and
+    // RuleError texts depend on where a block stopped or which condition raised the error), four
+    // words for foreach rules (schema.h FT_*)
     auto fits = [](const CondMsgs& m) { return m.any.size() <= CT_MAXC && m.all.size() <= CT_MAXC; };
-    if ((pre_block != CE_NONE || rr.cond_deny) && fits(rr.pre_msgs) && fits(rr.deny_msgs)) {
-      crule.mslot = ++P.cond.nmsg;
+    if ((pre_block != CE_NONE || crule.kind == CR_DENY || crule.kind == CR_FOREACH) && fits(rr.pre_msgs) &&
+        fits(rr.deny_msgs)) {
+      crule.mslot = P.cond.nmsg + 1u;
+      P.cond.nmsg += crule.kind == CR_FOREACH ? KPE_FE_TRACE_WORDS : 1u;
       rr.cond_slot = true;
+    }
+    if (pre_block != CE_NONE) rr.pre_json = doc_text(*pre_raw);
+    if (crule.kind == CR_DENY && v->get("deny")->get("conditions")) rr.deny_json = doc_text(*v->get("deny")->get("conditions"));
+    if (crule.kind == CR_FOREACH) {
+      rr.foreach = true, rr.fe0 = crule.fe0, rr.nfe = crule.nfe;
+      const JV* m = v->get("message");
+      rr.vmsg = (m && m->t == JV::Str) ? m->s : std::string();
     }
     rule_info_.push_back({pre_block != CE_NONE, has_validate, rname, k.handler == H_PATTERN && !pat_may_skip});
     if (pre_block != CE_NONE || k.handler == H_COND || crule.npv) P.cond.rules.push_back(crule);
@@ -2605,6 +2650,14 @@ class Lowerer {
     rr.pss_cv = k.cv_mask;
     if (pss_excl) rr.pss_excludes = std::move(pending_excl_);
     rr.msg_pattern = msg_pattern;
+    if (k.handler == H_PATTERN) {  // RuleError texts of substitutePatterns / deserializeAnyPattern
+      const JV* pt = v->get("pattern") && v->get("pattern")->t != JV::Null ? v->get("pattern") : v->get("anyPattern");
+      rr.pattern_json = doc_text(*pt);
+      rr.pat_vars = crule.npv != 0;
+      if (pt == v->get("anyPattern") && pt->t != JV::Arr) rr.any_bad_type = json_type_name(*pt);
+      const JV* m = v->get("message");
+      rr.vmsg = (m && m->t == JV::Str) ? m->s : std::string();
+    }
     if (pat_report.on) {
       rr.pat_rule = true, rr.any_pattern = pat_report.any, rr.pat_roots = pat_report.roots;
       const JV* m = v ? v->get("message") : nullptr;
@@ -2993,21 +3046,51 @@ void go_json(std::string& o, const JV& v) {
   }
 }
 
-// A `request.object...` JMESPath over the resource: identifiers, "quoted" identifiers and [N]
-// (negative from the end). A member missing from an object is the kyverno go-jmespath fork's
-// NotFoundError (*missing: SubstituteAll fails) in this chain of member / index accesses, as in
-// kpe_cond_kernel's queries and the oracle's plain chains; a member of a non-object or an index
-// past a list is null. false: not this grammar.
-bool object_path(const std::string& q, const JV& res, const JV** out, bool* missing) {
-  *missing = false;
+// A plain chain of the message context (the queries kpe_cond_kernel marks CE_STRICT): the roots
+// request.object (the resource), request.operation ("CREATE", background scans and the CLI),
+// element / element<depth> and elementIndex / elementIndex<depth> (the foreach element, when
+// given), then identifiers, "quoted" identifiers and [N] (negative from the end). A member
+// missing from an object is the kyverno go-jmespath fork's NotFoundError (*missing_key: the
+// member; SubstituteAll fails); a member of a non-object or an index past a list is null.
+// false: not this grammar (another root, a projection, a function).
+bool ctx_path(const std::string& q, const JV& res, const JV* el, const MsgElem* me, JV* scratch, const JV** out,
+              std::string* missing_key) {
+  missing_key->clear();
   static const JV kNull;
-  const std::string root = "request.object";
-  if (q.compare(0, root.size(), root) != 0) return false;
-  const JV* cur = &res;
-  size_t i = root.size();
-  bool indexed = false;
   auto ident0 = [](char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || c == '_'; };
   auto ident1 = [&](char c) { return ident0(c) || (c >= '0' && c <= '9'); };
+  auto root_is = [&](const std::string& r) {
+    return q.compare(0, r.size(), r) == 0 && (q.size() == r.size() || q[r.size()] == '.' || q[r.size()] == '[');
+  };
+  const JV* cur = nullptr;
+  size_t i = 0;
+  if (root_is("request.object")) {
+    cur = &res, i = 14;
+  } else if (root_is("request.operation")) {
+    *scratch = JV::str("CREATE");
+    cur = scratch, i = 17;
+  } else if (me && el && q.compare(0, 7, "element") == 0) {
+    size_t j = 7;
+    const bool index = q.compare(0, 12, "elementIndex") == 0;
+    if (index) j = 12;
+    if (j < q.size() && q[j] >= '0' && q[j] <= '9') {  // element<n>: only the innermost level is kept
+      if (q[j] - '0' != me->depth) return false;
+      ++j;
+    }
+    if (j < q.size() && q[j] != '.' && q[j] != '[') return false;
+    if (index) {
+      JV x;
+      x.t = JV::Num, x.is_int = true, x.i = me->index, x.n = (double)me->index;
+      *scratch = x;
+      cur = scratch;
+    } else {
+      cur = el;
+    }
+    i = j;
+  } else {
+    return false;
+  }
+  bool missing = false;
   while (i < q.size()) {
     if (q[i] == '.') {
       ++i;
@@ -3025,7 +3108,7 @@ bool object_path(const std::string& q, const JV& res, const JV** out, bool* miss
         key = q.substr(b, i - b);
       }
       const JV* nx = cur && cur->t == JV::Obj ? cur->get(key.c_str()) : nullptr;
-      if (cur && cur->t == JV::Obj && !nx) *missing = true;
+      if (cur && cur->t == JV::Obj && !nx && !missing) missing = true, *missing_key = key;
       cur = nx;
     } else if (q[i] == '[') {
       size_t e = q.find(']', i);
@@ -3037,7 +3120,6 @@ bool object_path(const std::string& q, const JV& res, const JV** out, bool* miss
       for (size_t k = d; k < num.size(); ++k)
         if (num[k] < '0' || num[k] > '9') return false;
       long idx = std::stol(num);
-      indexed = true;
       if (cur && cur->t == JV::Arr) {
         if (idx < 0) idx += (long)cur->a.size();
         cur = idx >= 0 && idx < (long)cur->a.size() ? &cur->a[(size_t)idx] : nullptr;
@@ -3048,11 +3130,17 @@ bool object_path(const std::string& q, const JV& res, const JV** out, bool* miss
     } else {
       return false;
     }
-    if (!cur) cur = nullptr;
   }
-  (void)indexed;
   *out = cur ? cur : &kNull;
   return true;
+}
+bool object_path(const std::string& q, const JV& res, const JV** out, bool* missing) {
+  JV scratch;
+  std::string mk;
+  if (q.compare(0, 14, "request.object") != 0) return false;
+  const bool ok = ctx_path(q, res, nullptr, nullptr, &scratch, out, &mk);
+  *missing = !mk.empty();
+  return ok;
 }
 
 // the end of the variable starting at s[i] == '{' s[i+1] == '{' (RegexVariables: `{...}` groups
@@ -3108,8 +3196,107 @@ std::string CondMsgs::render(uint32_t as, uint32_t ls, bool held) const {
   return join_non_empty(v, "; ");
 }
 
+namespace {
+// The message context: the resource and, in a foreach, the element's document
+struct MsgCtx {
+  JV res;
+  JV el;
+  const MsgElem* me = nullptr;
+  bool ok = false;
+  MsgCtx(const char* json, size_t n, const MsgElem* e) : me(e) {
+    try {
+      res = parse_all(json, n);
+      if (e) el = parse_all(e->json.data(), e->json.size());
+      ok = true;
+    } catch (...) {
+      ok = false;
+    }
+  }
+  bool path(const std::string& q, JV* scratch, const JV** out, std::string* missing) const {
+    return ctx_path(q, res, me ? &el : nullptr, me, scratch, out, missing);
+  }
+};
+std::string trim_var(const std::string& v) {  // replaceBracesAndTrimSpaces (vars.go:422-427)
+  std::string q = v;
+  for (size_t p; (p = q.find("{{")) != std::string::npos;) q.erase(p, 2);
+  for (size_t p; (p = q.find("}}")) != std::string::npos;) q.erase(p, 2);
+  const size_t b = q.find_first_not_of(" \t\n\r\f\v"), z = q.find_last_not_of(" \t\n\r\f\v");
+  return b == std::string::npos ? std::string() : q.substr(b, z - b + 1);
+}
+// substituteVariablesIfAny (vars.go:311-389) over one string leaf at `path`, checking for the
+// resolver errors only: 0 no error (*whole: the leaf is one variable, its value), 1 an error
+// (*err: the reference's text), 2 a variable whose error the host cannot tell (a construct
+// outside the plain chains that may raise one).
+int leaf_error(const std::string& s, const MsgCtx& cx, const std::string& path, std::string* err, const JV** whole,
+               JV* scratch) {
+  *whole = nullptr;
+  for (size_t i = 0; i + 1 < s.size();) {
+    if (!(s[i] == '{' && s[i + 1] == '{') || (i > 0 && s[i - 1] == '\\')) {
+      ++i;
+      continue;
+    }
+    const size_t e = var_end(s, i);
+    if (e == std::string::npos) {
+      ++i;
+      continue;
+    }
+    const std::string q = trim_var(s.substr(i, e - i));
+    const std::string pre = "failed to resolve " + q + " at path " + path + ": ";
+    if (q.empty()) {  // context/evaluate.go:16-19
+      *err = pre + "invalid query (nil)";
+      return 1;
+    }
+    const JV* v = nullptr;
+    std::string missing;
+    if (!cx.path(q, scratch, &v, &missing)) {
+      // not a plain chain of the context: a projection, `||` or a literal raises no NotFoundError
+      // (the device's CE_STRICT queries); a function (length) or a plain chain over a root the
+      // host does not hold (images, an outer foreach element) may raise one
+      const bool projects = q.find("||") != std::string::npos || q.find("[]") != std::string::npos ||
+                            q.find("[*]") != std::string::npos || q.find(".*") != std::string::npos ||
+                            q.find(".[") != std::string::npos || q.find('|') != std::string::npos ||
+                            q.find('`') != std::string::npos || q.find('\'') != std::string::npos;
+      if (!projects || q.find('(') != std::string::npos || q.find("{{") != std::string::npos) return 2;
+    } else if (!missing.empty()) {
+      *err = pre + "JMESPath query failed: Unknown key \"" + missing + "\" in path";
+      return 1;
+    } else if (i == 0 && e == s.size()) {
+      *whole = v;
+    }
+    i = e;
+  }
+  return 0;
+}
+// jsonutils traverse.go:64-130 with OnlyForLeafsAndKeys: keys (at their map's path) and leaves;
+// the first error in traversal order (document order for maps)
+int doc_error(const JV& d, const MsgCtx& cx, const std::string& path, std::string* err) {
+  JV scratch;
+  const JV* whole = nullptr;
+  switch (d.t) {
+    case JV::Str: return leaf_error(d.s, cx, path, err, &whole, &scratch);
+    case JV::Arr:
+      for (size_t k = 0; k < d.a.size(); ++k)
+        if (int r = doc_error(d.a[k], cx, path + "/" + std::to_string(k), err)) return r;
+      return 0;
+    case JV::Obj:
+      for (auto& kv : d.o) {
+        if (int r = leaf_error(kv.first, cx, path, err, &whole, &scratch)) return r;
+        if (whole && whole->t != JV::Null && whole->t != JV::Str) {  // traverse.go:97-104
+          *err = "expected string after substituting variables in key \"" + kv.first + "\"";
+          return 1;
+        }
+        std::string kp;
+        for (char ch : kv.first) kp += ch == '/' ? std::string("\\/") : std::string(1, ch);
+        if (int r = doc_error(kv.second, cx, path + "/" + kp, err)) return r;
+      }
+      return 0;
+    default: return 0;
+  }
+}
+}  // namespace
+
 bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring,
-                        bool* subst_err) {
+                        bool* subst_err, const MsgElem* elem) {
   *nonstring = false;
   if (subst_err) *subst_err = false;
   if (msg.find("$(") != std::string::npos) return false;  // substituteReferences: not restated
@@ -3117,15 +3304,11 @@ bool substitute_message(const std::string& msg, const char* json, size_t n, std:
     *out = msg;
     return true;
   }
-  JV res;
-  try {
-    res = parse_all(json, n);
-  } catch (...) {
-    return false;
-  }
+  MsgCtx cx(json, n, elem);
+  if (!cx.ok) return false;
   std::string o;
   size_t i = 0;
-  bool any = false;
+  JV scratch;
   while (i < msg.size()) {
     if (msg[i] == '{' && i + 1 < msg.size() && msg[i + 1] == '{') {
       const size_t e = var_end(msg, i);
@@ -3139,15 +3322,11 @@ bool substitute_message(const std::string& msg, const char* json, size_t n, std:
         i = e;
         continue;
       }
-      std::string q = msg.substr(i, e - i);  // replaceBracesAndTrimSpaces
-      for (size_t p; (p = q.find("{{")) != std::string::npos;) q.erase(p, 2);
-      for (size_t p; (p = q.find("}}")) != std::string::npos;) q.erase(p, 2);
-      const size_t b = q.find_first_not_of(" \t\n\r\f\v"), z = q.find_last_not_of(" \t\n\r\f\v");
-      q = b == std::string::npos ? std::string() : q.substr(b, z - b + 1);
+      const std::string q = trim_var(msg.substr(i, e - i));
       const JV* v = nullptr;
-      bool missing = false;
-      if (!object_path(q, res, &v, &missing)) return false;
-      if (missing) {
+      std::string missing;
+      if (!cx.path(q, &scratch, &v, &missing)) return false;
+      if (!missing.empty()) {
         if (subst_err) *subst_err = true;
         return false;
       }
@@ -3167,15 +3346,69 @@ bool substitute_message(const std::string& msg, const char* json, size_t n, std:
       else go_json(val, *v);
       if (val.find("{{") != std::string::npos) return false;  // a second round would substitute it
       o += val;
-      any = true;
       i = e;
       continue;
     }
     o += msg[i++];
   }
-  (void)any;
   *out = std::move(o);
   return true;
+}
+
+std::string doc_subst_error(const std::string& doc_json, const char* json, size_t n, const MsgElem* el) {
+  MsgCtx cx(json, n, el);
+  if (!cx.ok) return "";
+  JV d;
+  try {
+    d = parse_all(doc_json.data(), doc_json.size());
+  } catch (...) {
+    return "";
+  }
+  std::string err;
+  return doc_error(d, cx, "", &err) == 1 ? err : std::string();
+}
+
+std::string block_error_text(const std::string& block_json, uint32_t t, const char* json, size_t n,
+                             const MsgElem* el) {
+  if (!CT_IS_ERR(t) || block_json.empty()) return "";
+  JV b;
+  try {
+    b = parse_all(block_json.data(), block_json.size());
+  } catch (...) {
+    return "";
+  }
+  // the conditions in the device's order: `any` then `all`, or the deprecated list
+  std::vector<const JV*> cs;
+  if (b.t == JV::Arr) {
+    for (auto& c : b.a) cs.push_back(&c);
+  } else if (b.t == JV::Obj) {
+    for (const char* k : {"any", "all"})
+      if (const JV* l = b.get(k))
+        if (l->t == JV::Arr)
+          for (auto& c : l->a) cs.push_back(&c);
+  }
+  const uint32_t ci = CT_ERR_COND(t), side = CT_ERR_SIDE(t);
+  if (ci >= cs.size() || cs[ci]->t != JV::Obj) return "";
+  const JV& c = *cs[ci];
+  if (side == 2) {  // CreateOperatorHandler found no handler (evaluate.go:22-25; the value's err is nil)
+    std::string op;
+    for (char ch : sv(c.get("operator"))) op += (char)tolower((unsigned char)ch);
+    static const char* const kOps[] = {"equal", "equals", "notequal", "notequals", "anyin", "allin", "anynotin",
+                                       "allnotin", "in", "notin", "greaterthanorequals", "greaterthan",
+                                       "lessthanorequals", "lessthan", "durationgreaterthanorequals",
+                                       "durationgreaterthan", "durationlessthanorequals", "durationlessthan"};
+    for (const char* k : kOps)
+      if (op == k) return "";  // an operator's own error (In / NotIn over a non-string list): not restated
+    return "failed to create handler for condition operator: %!w(<nil>)";
+  }
+  MsgCtx cx(json, n, el);
+  if (!cx.ok) return "";
+  static const JV kNull;
+  const JV* d = c.get(side ? "value" : "key");
+  std::string err;
+  if (doc_error(d ? *d : kNull, cx, "", &err) != 1) return "";
+  return std::string(side ? "failed to substitute variables in condition value: "
+                          : "failed to substitute variables in condition key: ") + err;
 }
 
 }  // namespace kpe

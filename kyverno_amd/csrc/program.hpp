@@ -92,6 +92,18 @@ struct CondMsgs {
 // stringutils.JoinNonEmpty
 std::string join_non_empty(const std::vector<std::string>& v, const std::string& sep);
 
+// A validate.foreach entry as the messages need it (parallel to CondProgram::fes): the raw blocks
+// and pattern (document-order JSON, reparsed for a failing cell) and the deny block's messages
+struct FeReport {
+  uint32_t kind = FE_NONE;  // FE_*
+  std::string pre_json, deny_json, pattern_json;
+  CondMsgs deny_msgs;
+  bool any = false;          // anyPattern
+  std::string any_bad_type;  // an anyPattern that is not a list: its JSON type name
+  uint32_t nested0 = 0, nnested = 0;  // FE_NEST: entries [nested0, + nnested)
+  uint32_t root0 = 0, nroots = 0;     // FE_PAT: pattern roots
+};
+
 struct RuleReport {
   std::string policy_key;  // cache.MetaNamespaceKeyFunc: "<ns>/<name>" or "<name>"
   std::string rule;        // rule name after autogen
@@ -136,6 +148,15 @@ struct RuleReport {
   bool pat_rule = false, any_pattern = false, vmsg_vars = false;
   uint32_t pat_roots = 0;
   std::string vmsg;
+  // RuleError texts (validate_resource.go:127,140,270,349; engine.go:279-281): the rule's raw
+  // preconditions, deny conditions and pattern / anyPattern (document-order JSON), reparsed for an
+  // erroring cell; `pat_vars`: the pattern has {{ }} variables (a substitution error is possible)
+  std::string pre_json, deny_json, pattern_json, any_bad_type;
+  bool pat_vars = false;
+  // validate.foreach rules: the entries [fe0, fe0 + nfe) of Program::fe_reports and the four-word
+  // condition trace slot (schema.h FT_*); the entries' messages use `vmsg` (the rule's message)
+  bool foreach = false;
+  uint32_t fe0 = 0, nfe = 0;
 };
 
 struct Program {
@@ -160,6 +181,7 @@ struct Program {
   bool any_fe_pat = false;  // some foreach entry has a pattern / anyPattern (kpe_cond_kernel<true>)
   PatProgram pat;  // pattern rules (H_PATTERN)
   CondProgram cond;  // rules with preconditions / deny / foreach evaluated per resource
+  std::vector<FeReport> fe_reports;  // per CondProgram::fes entry
   PssxProgram pssx;  // podSecurity.exclude
   int32_t pssx_preds[9] = {-1, -1, -1, -1, -1, -1, -1, -1, -1};  // PSA predicates of kpe_pssx_kernel
   DeviceProgram* devs[16] = {};  // per device ordinal: the program's tables on that device (kpe_api.cpp)
@@ -179,7 +201,24 @@ std::unique_ptr<Program> compile_policies(const char* json, size_t len, const ch
 // message is one variable whose value is not a string (*out is its JSON).
 // *subst_err (when given): false was returned for a substitution error (a member missing from
 // an object, go-jmespath NotFound), not for an unrestated variable.
+// MsgElem: the foreach element of the context (AddElement, context.go: element, element<depth>,
+// elementIndex, elementIndex<depth>), as the JSON of its document node.
+struct MsgElem {
+  std::string json;
+  int depth = 0;
+  int64_t index = 0;
+};
 bool substitute_message(const std::string& msg, const char* json, size_t n, std::string* out, bool* nonstring,
-                        bool* subst_err = nullptr);
+                        bool* subst_err = nullptr, const MsgElem* el = nullptr);
+// The error text of a condition block that raised one (`t`: its schema.h CT_ERR trace half), as
+// variables/evaluate.go:14-27 and vars.go:311-389 word it: "failed to substitute variables in
+// condition key: failed to resolve <var> at path <path>: JMESPath query failed: Unknown key \"<k>\"
+// in path", the value's likewise, or the operator's. "" when the error is not one the host
+// restates (an error go-jmespath words itself).
+std::string block_error_text(const std::string& block_json, uint32_t t, const char* json, size_t n,
+                             const MsgElem* el);
+// SubstituteAll's error over a document (substitutePatterns, validate_resource.go:456-476): the
+// first failing variable in traversal order (document order for maps, Go's is random), or "".
+std::string doc_subst_error(const std::string& doc_json, const char* json, size_t n, const MsgElem* el);
 
 }  // namespace kpe

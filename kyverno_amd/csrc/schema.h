@@ -778,6 +778,36 @@ typedef struct KpeCRule {
 #define CT_EVAL 0x4000u
 #define CT_TRUE 0x8000u
 #define CT_MAXC 127u
+// A block that raised an error (RuleError texts, validate_resource.go:127,270 and engine.go:279-281):
+// CT_ERR without CT_EVAL, the index of the condition that raised it (any conditions first, then
+// all; the old list form: its index) and the side: 0 the key's substitution, 1 the value's, 2 the
+// operator (variables/evaluate.go:14-27)
+#define CT_ERR 0x8000u
+#define CT_IS_ERR(t) (((t) & (CT_ERR | CT_EVAL)) == CT_ERR)
+#define CT_ERR_COND(t) ((t) & 0x7Fu)
+#define CT_ERR_SIDE(t) (((t) >> 7) & 3u)
+// validate.foreach rules have four trace words (KpeCRule::mslot .. + 3), written for the element
+// that decided a FAIL / ERROR cell (validateElements, validate_resource.go:206-254):
+//   word 0: the rule's preconditions (low half, as above) | the deciding element's block << 16
+//           (its deny block, or its preconditions for FT_PRE_ERR; CT_* / CT_ERR form)
+//   word 1: FT_* path: nesting depth of the element (0 .. KPE_FE_DEPTH - 1), what decided it, and
+//           per level l <= depth the foreach entries left in that level's list when it ran (the
+//           entry is count - left) and the element index
+//   word 2: the element's tape entry (a document node), or 0xFFFFFFFF (a constant element)
+//   word 3: the tape entry its patterns validate (the innermost scoped element; 0xFFFFFFFF: the
+//           resource root, 0xFFFFFFFE: a constant)
+#define KPE_FE_TRACE_WORDS 4u
+#define FT_DEPTH(b) ((b) & 3u)
+#define FT_KIND(b) (((b) >> 2) & 7u)
+#define FT_DENY 1u      // the element's deny block held (FAIL) or raised an error
+#define FT_PRE_ERR 2u   // the element's preconditions raised an error
+#define FT_PAT 3u       // the entry's pattern / anyPattern on the element failed or errored
+#define FT_PVAR_ERR 4u  // the entry's pattern variables failed to substitute
+#define FT_SCOPE_ERR 5u // elementScope: true on an element that is not a map (AddElementToContext)
+#define FT_VALID 0x20u
+#define FT_OVERFLOW 0x40u  // an element index > 31 or more than 7 entries left: no path
+#define FT_LEFT(b, l) (((b) >> (8u + 8u * (l))) & 7u)
+#define FT_IDX(b, l) (((b) >> (11u + 8u * (l))) & 31u)
 // KpeCRule::xflags: the rule's PolicyException is applied here (XE_DEFER), after the
 // preconditions: in a cell flagged KPE_XDEFER_ its conditions holding make the cell RuleSkip
 // (validate_resource.go:43-56) or, with podSecurity controls (XC_PSS), a failing cell KPE_XFAIL_

@@ -376,13 +376,17 @@ class Engine:
         R = ps.num_rules
         return self.pattern_traces(ps, corpus, np.arange(row * R, row * R + R, dtype=np.uint64))
 
-    def cond_traces(self, ps: PolicySet, corpus: Corpus, row0: int = 0, nrows: Optional[int] = None) -> np.ndarray:
+    def cond_traces(self, ps: PolicySet, corpus: Corpus, row0: int = 0, nrows: Optional[int] = None,
+                    ex: bool = False) -> np.ndarray:
         """Condition traces (kpe_fetch_cond_traces) of rows [row0, row0 + nrows) after an evaluation
-        of ps on corpus: (nrows, R) uint32, the layout report_results(cond_traces=) takes per row."""
+        of ps on corpus: (nrows, R) uint32, the layout report_results(cond_traces=) takes per row.
+        ex: kpe_fetch_cond_traces_ex, (nrows, R, KPE_CTRACE_WORDS) with the foreach and error
+        records (foreach messages, RuleError texts)."""
         n = corpus.n - row0 if nrows is None else nrows
-        out = np.zeros((n, ps.num_rules), dtype=np.uint32)
+        out = np.zeros((n, ps.num_rules, CTRACE_WORDS) if ex else (n, ps.num_rules), dtype=np.uint32)
         if n:
-            check(load().kpe_fetch_cond_traces(self.device.h, ps.h, corpus.h, row0, n, out.ctypes.data))
+            f = load().kpe_fetch_cond_traces_ex if ex else load().kpe_fetch_cond_traces
+            check(f(self.device.h, ps.h, corpus.h, row0, n, out.ctypes.data))
         return out
 
     # ---- reference-shaped API ----
@@ -433,6 +437,7 @@ class Engine:
 
 
 TRACE_WORDS, TRACE_ROOTS = 16, 4  # include/kpe.h KPE_TRACE_WORDS / KPE_TRACE_ROOTS
+CTRACE_WORDS = 4  # include/kpe.h KPE_CTRACE_WORDS (kpe_fetch_cond_traces_ex)
 
 
 class ReportArgs(ctypes.Structure):
@@ -440,7 +445,7 @@ class ReportArgs(ctypes.Structure):
     _fields_ = [("prog", ctypes.c_void_p), ("corpus", ctypes.c_void_p), ("verdict_row", ctypes.c_void_p),
                 ("cv_mask_row", ctypes.c_void_p), ("pattern_traces", ctypes.c_void_p),
                 ("cond_traces", ctypes.c_void_p), ("resource_json", ctypes.c_char_p),
-                ("resource_len", ctypes.c_size_t)]
+                ("resource_len", ctypes.c_size_t), ("cond_traces_ex", ctypes.c_void_p)]
 
 
 def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None, traces=None,
@@ -468,15 +473,17 @@ def report_results(ps: PolicySet, verdict_row, cv_mask_row=None, resource=None, 
             n = L.kpe_report_results(ps.h, v.ctypes.data, mp, buf, cap)
         elif cond_traces is not None:
             ct = np.ascontiguousarray(cond_traces, dtype=np.uint32)
-            if ct.size != ps.num_rules:
-                raise ValueError("cond_traces: one word per rule of the row")
+            ex = ct.ndim == 2  # a row of Engine.cond_traces(ex=True): KPE_CTRACE_WORDS per rule
+            if ct.size != ps.num_rules * (CTRACE_WORDS if ex else 1):
+                raise ValueError("cond_traces: one word (or KPE_CTRACE_WORDS words) per rule of the row")
             t = None
             if traces is not None:
                 t = np.ascontiguousarray(traces, dtype=np.uint32)
                 if t.size != ps.num_rules * TRACE_ROOTS * TRACE_WORDS:
                     raise ValueError("traces: one record per rule of the row")
             a = ReportArgs(ps.h, corpus.h if corpus is not None else None, v.ctypes.data, mp,
-                           None if t is None else t.ctypes.data, ct.ctypes.data, raw, len(raw))
+                           None if t is None else t.ctypes.data, None if ex else ct.ctypes.data, raw, len(raw),
+                           ct.ctypes.data if ex else None)
             n = L.kpe_report_results_ex(ctypes.byref(a), buf, cap)
         elif traces is not None:
             t = np.ascontiguousarray(traces, dtype=np.uint32)

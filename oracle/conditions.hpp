@@ -47,6 +47,7 @@ struct NotFound {  // go-jmespath fork NotFoundError
 };
 struct EvalError {  // any other evaluation / substitution error => rule ERROR
   std::string msg;
+  bool restated = false;  // msg is the reference's error text (else a description only)
 };
 
 // ---- values -------------------------------------------------------------------------
@@ -865,7 +866,12 @@ inline std::string var_text(const std::string& v) {  // replaceBracesAndTrimSpac
   }
   return pat::trim_space(s);
 }
-inline JPtr substitute_string(const std::string& in, const Ctx& c) {
+// vars.go:311-389 substituteVariablesIfAny over one string leaf at `path` (the JSON-pointer-like
+// path jsonutils.traverse.go builds: "" at the root, "/<key>" / "/<index>" below). An error is
+// the reference's text: ctx.Query wraps a search error as "JMESPath query failed: %w"
+// (context/evaluate.go:27-31), which the type switch of :349-355 does not unwrap, so every
+// resolver error is "failed to resolve <variable> at path <path>: <err>".
+inline JPtr substitute_string(const std::string& in, const Ctx& c, const std::string& path = "") {
   std::string value = in;
   size_t st, en;
   for (int guard = 0; next_var(value, 0, &st, &en); ++guard) {
@@ -875,10 +881,15 @@ inline JPtr substitute_string(const std::string& in, const Ctx& c) {
     if (var == "@") throw Unsupported("{{@}} variables");
     if (var.find("{{") != std::string::npos) throw Unsupported("nested variables");
     JPtr r;
+    const std::string pre = "failed to resolve " + var + " at path " + path + ": ";
     try {
       r = run_query(compile_query(var), c.root);
     } catch (const NotFound& nf) {
-      throw EvalError{"Unknown key \"" + nf.key + "\" in path"};
+      throw EvalError{pre + "JMESPath query failed: Unknown key \"" + nf.key + "\" in path", true};
+    } catch (const EvalError& e) {
+      // "invalid query (nil)" (evaluate.go:17-19) is the reference's text; a parse or function
+      // error would embed go-jmespath's own text, which is not restated
+      throw EvalError{pre + e.msg, e.msg == "invalid query (nil)"};
     }
     if (value == v) return r;  // a whole-string variable keeps its JSON type
     const std::string sub = (!is_null(r) && r->t == JT::Str) ? r->s : json_marshal(r);
@@ -892,10 +903,10 @@ inline JPtr substitute_string(const std::string& in, const Ctx& c) {
   }
   return mk_str(o);
 }
-inline JPtr substitute(const JPtr& v, const Ctx& c) {
+inline JPtr substitute(const JPtr& v, const Ctx& c, const std::string& path = "") {
   if (is_null(v)) return v;
   if (v->t == JT::Str) {  // a JSON null result as a node (substituted trees are walked as documents)
-    JPtr r = substitute_string(v->s, c);
+    JPtr r = substitute_string(v->s, c, path);
     if (!r) {
       r = std::make_shared<JVal>();
       r->t = JT::Null;
@@ -904,7 +915,7 @@ inline JPtr substitute(const JPtr& v, const Ctx& c) {
   }
   if (v->t == JT::Arr) {
     std::vector<JPtr> o;
-    for (auto& e : v->a) o.push_back(substitute(e, c));
+    for (size_t i = 0; i < v->a.size(); ++i) o.push_back(substitute(v->a[i], c, path + "/" + std::to_string(i)));
     return mk_arr(o);
   }
   if (v->t == JT::Obj) {
@@ -918,14 +929,17 @@ inline JPtr substitute(const JPtr& v, const Ctx& c) {
     std::set<std::string> seen;
     for (auto& kv : v->o) seen.insert(kv.first);
     for (auto& kv : v->o) {
-      JPtr k = substitute_string(kv.first, c);
+      JPtr k = substitute_string(kv.first, c, path);  // a key's action sees its map's path
       std::string nk;
       if (is_null(k)) nk = kv.first;
-      else if (k->t != JT::Str) throw EvalError{"expected string after substituting variables in key \"" + kv.first + "\""};
+      else if (k->t != JT::Str)
+        throw EvalError{"expected string after substituting variables in key \"" + kv.first + "\"", true};
       else nk = k->s;
       if (nk != kv.first && seen.count(nk)) throw Unsupported("a substituted map key equal to another key of the map");
       seen.insert(nk);
-      o->o.push_back({nk, substitute(kv.second, c)});
+      std::string kp;  // traverse.go:107: path + "/" + key with "/" escaped as "\/"
+      for (char ch : kv.first) kp += ch == '/' ? std::string("\\/") : std::string(1, ch);
+      o->o.push_back({nk, substitute(kv.second, c, path + "/" + kp)});
     }
     return o;
   }
@@ -1380,7 +1394,8 @@ inline bool apply_op(OpKind o, const JPtr& key, const JPtr& value, NumOp num = N
   switch (o) {
     case O_NUM: return op_numeric(num, key, value);
     case O_DUR: return op_duration(num, key, value);
-    case O_BAD: throw EvalError{"failed to create handler for condition operator"};
+    // evaluate.go:23-25: fmt.Errorf("...: %w", err) with the nil err of the value substitution
+    case O_BAD: throw EvalError{"failed to create handler for condition operator: %!w(<nil>)", true};
     case O_EQ: return op_equals(key, value, false);
     case O_NE: return op_equals(key, value, true);
     case O_ANYIN: return op_set(S_ANYIN, key, value);
@@ -1462,8 +1477,17 @@ inline Conditions parse_conditions(const JVal* j) {
 }
 // evaluate.go:14-27: substitute key and value, then the operator; throws EvalError
 inline bool eval_condition(const Condition& c, const Ctx& x) {
-  JPtr k = substitute(c.key, x);
-  JPtr v = substitute(c.value, x);
+  JPtr k, v;
+  try {
+    k = substitute(c.key, x);
+  } catch (const EvalError& e) {
+    throw EvalError{"failed to substitute variables in condition key: " + e.msg, e.restated};
+  }
+  try {
+    v = substitute(c.value, x);
+  } catch (const EvalError& e) {
+    throw EvalError{"failed to substitute variables in condition value: " + e.msg, e.restated};
+  }
   return apply_op(c.op, k, v, c.num);
 }
 inline bool eval_conditions(const Conditions& c, const Ctx& x) {

@@ -1050,6 +1050,9 @@ inline std::string build_error_message(const PatMsg& pm, const std::string& path
 inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars, const JVal& res, const cond::Ctx* cx,
                               const PatMsg* pm = nullptr) {
   JPtr pattern = pattern0, any = any0;
+  auto say = [&](const std::string& m) {
+    if (pm) *pm->out = m;
+  };
   if (vars) {
     try {
       if (pattern) {
@@ -1058,15 +1061,13 @@ inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars,
         any = cond::substitute(any, *cx);
         if (!cond::is_null(any)) any = deep_copy(*any), pat::numbers_to_float(*any);  // deserializeAnyPattern
       }
-    } catch (const cond::EvalError&) {
+    } catch (const cond::EvalError& e) {  // RuleError "variable substitution failed" (:139-141)
+      say(e.restated ? "variable substitution failed: " + e.msg : std::string(kNeedsErrText));
       return ERROR;
     } catch (const cond::Unsupported&) {
       return UNSUPPORTED;
     }
   }
-  auto say = [&](const std::string& m) {
-    if (pm) *pm->out = m;
-  };
   if (pattern) {
     pat::MatchResult m = pat::match_pattern(res, *pattern);
     if (m.k == pat::M_PASS) return say("validation rule '" + *pm_rule(pm) + "' passed."), PASS;
@@ -1074,7 +1075,17 @@ inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars,
     if (pm) say(build_error_message(*pm, m.path));
     return m.path.empty() ? ERROR : FAIL;
   }
-  if (cond::is_null(any) || any->t != JT::Arr) return say(kNeedsErrText), ERROR;  // deserializeAnyPattern failure
+  if (cond::is_null(any) || any->t != JT::Arr) {  // deserializeAnyPattern: json.Unmarshal into []interface{}
+    const char* t = cond::is_null(any) ? nullptr
+                    : any->t == JT::Obj ? "object"
+                    : any->t == JT::Str ? "string"
+                    : any->t == JT::Bool ? "bool"
+                                         : "number";
+    say(t ? std::string("failed to deserialize anyPattern, expected type array: json: cannot unmarshal ") + t +
+                " into Go value of type []interface {}"
+          : std::string(kNeedsErrText));
+    return ERROR;
+  }
   int fails = 0, skips = 0, idx = 0;
   std::string errs;
   bool err_text = false;
@@ -1105,20 +1116,23 @@ inline Status pattern_handler(const JPtr& pattern0, const JPtr& any0, bool vars,
   return say(pm ? *pm->vmsg : std::string()), PASS;  // RulePass(rule.Validation.Message)
 }
 
-// validate_resource.go:268-279 validateDeny: conditions true => FAIL, false => PASS, error => ERROR
-// validate_resource.go:268-300 validateDeny + getDenyMessage (*msg: the RuleResponse message; a
-// `$(...)` reference in the rule message is not restated: no message)
-inline Status deny_handler(const Rule& r, const cond::Ctx& cx, std::string* msg = nullptr) {
+// validate_resource.go:268-300 validateDeny + getDenyMessage over a deny block `d` in context cx
+// (the rule's deny, or a foreach entry's with the element in cx): conditions true => FAIL, false
+// => PASS, error => ERROR ("failed to check deny conditions: <err>", :269-271). *msg: the
+// RuleResponse message (a `$(...)` reference in the rule message is not restated: no message;
+// kNeedsErrText: an error text the restatement does not hold)
+inline Status deny_eval(const std::string& name, const std::string& vmsg, const cond::Conditions& d,
+                        const cond::Ctx& cx, std::string* msg) {
   try {
     std::string cm;
-    const bool deny = cond::eval_conditions_msg(r.deny, cx, &cm);
+    const bool deny = cond::eval_conditions_msg(d, cx, &cm);
     if (msg) {
       if (!deny) {
-        *msg = "validation rule '" + r.name + "' passed.";
-      } else if (r.vmsg.empty() && cm.empty()) {
-        *msg = "validation error: rule " + r.name + " failed";
+        *msg = "validation rule '" + name + "' passed.";
+      } else if (vmsg.empty() && cm.empty()) {
+        *msg = "validation error: rule " + name + " failed";
       } else {
-        const std::string j = cond::join_non_empty({r.vmsg, cm}, "; ");
+        const std::string j = cond::join_non_empty({vmsg, cm}, "; ");
         if (j.find("$(") != std::string::npos) {
           msg->clear();
         } else {
@@ -1136,19 +1150,40 @@ inline Status deny_handler(const Rule& r, const cond::Ctx& cx, std::string* msg 
       }
     }
     return deny ? FAIL : PASS;
-  } catch (const cond::EvalError&) {
+  } catch (const cond::EvalError& e) {
+    if (msg) *msg = e.restated ? "failed to check deny conditions: " + e.msg : std::string(kNeedsErrText);
     return ERROR;
   } catch (const cond::Unsupported&) {
     return UNSUPPORTED;
   }
 }
+inline Status deny_handler(const Rule& r, const cond::Ctx& cx, std::string* msg = nullptr) {
+  return deny_eval(r.name, r.vmsg, r.deny, cx, msg);
+}
+
+// %T of a JSON-context value (encoding/json into interface{}), for AddElementToContext's error
+inline const char* go_type_name(const JPtr& v) {
+  if (cond::is_null(v)) return "<nil>";
+  switch (v->t) {
+    case JT::Str: return "string";
+    case JT::Bool: return "bool";
+    case JT::Arr: return "[]interface {}";
+    case JT::Obj: return "map[string]interface {}";
+    default: return "float64";
+  }
+}
+// validateElements wraps an element's failing (or last erroring) response: "validation failure:
+// <message>" (validate_resource.go:239-247)
+inline std::string fe_wrap(const std::string& m) { return m == kNeedsErrText ? m : "validation failure: " + m; }
+
 // validate_resource.go:186-254 validateForEach / validateElements, utils/foreach.go: each entry's
-// list, then per non-null element (AddElementToContext at `nesting`) the entry's validator:
-// preconditions, then deny / pattern / anyPattern / nested foreach. `scoped` is the element the
-// patterns validate (policyContext.Element(): the innermost scoped element), or null for the
-// resource itself.
-inline Status foreach_entries(const std::vector<Rule::ForEach>& fes, const cond::Ctx& cx, const JPtr& scoped,
-                              const JVal& res, int nesting) {
+// list, then per non-null element (AddElementToContext at `nesting`) the entry's validator
+// (newForEachValidator: the rule's name and validate.message, the entry's body): preconditions,
+// then deny / pattern / anyPattern / nested foreach. `scoped` is the element the patterns validate
+// (policyContext.Element(): the innermost scoped element), or null for the resource itself.
+// *msg: the level's response message (the deciding element's, wrapped), when it is FAIL / ERROR.
+inline Status foreach_entries(const Rule& r, const std::vector<Rule::ForEach>& fes, const cond::Ctx& cx,
+                              const JPtr& scoped, const JVal& res, int nesting, std::string* msg) {
   int apply_count = 0;
   for (auto& f : fes) {
     JPtr lst;
@@ -1167,42 +1202,66 @@ inline Status foreach_entries(const std::vector<Rule::ForEach>& fes, const cond:
       const JPtr& el = elems[idx];
       if (cond::is_null(el)) continue;
       const bool is_map = el->t == JT::Obj;
-      if (f.scope == 1 && !is_map) return ERROR;  // AddElementToContext error
+      if (f.scope == 1 && !is_map) {  // AddElementToContext: RuleError "failed to process foreach" (:218-221)
+        if (msg)
+          *msg = std::string("failed to process foreach: cannot use elementScope=true foreach rules for elements "
+                             "that are not maps, expected type=map got type=") + go_type_name(el);
+        return ERROR;
+      }
       const bool scope = f.scope == -1 ? is_map : f.scope == 1;
       cond::Ctx ex{cond::with_element(cx.root, el, (int64_t)idx, nesting)};
       const JPtr el_scoped = scope ? el : scoped;
-      Status st;
+      Status st = NA;
+      std::string em;  // the element validator's response message
+      bool done = false;
       try {
-        if (f.pre.present && !cond::eval_conditions(f.pre, ex)) {
-          st = SKIP;
+        if (f.pre.present) {
+          try {
+            if (!cond::eval_conditions(f.pre, ex)) st = SKIP, done = true;
+          } catch (const cond::EvalError& e) {  // validate_resource.go:125-128
+            st = ERROR, done = true;
+            em = e.restated ? "failed to evaluate preconditions: " + e.msg : std::string(kNeedsErrText);
+          }
+        }
+        if (done) {
         } else if (f.has_deny) {
-          st = cond::eval_conditions(f.deny, ex) ? FAIL : PASS;
+          st = deny_eval(r.name, r.vmsg, f.deny, ex, msg ? &em : nullptr);
         } else if (f.pattern || f.any_pattern) {
-          st = pattern_handler(f.pattern, f.any_pattern, f.pattern_vars, el_scoped ? *el_scoped : res, &ex);
+          PatMsg pm{&r.name, &r.vmsg, &em, &ex};
+          st = pattern_handler(f.pattern, f.any_pattern, f.pattern_vars, el_scoped ? *el_scoped : res, &ex,
+                               msg ? &pm : nullptr);
         } else if (!f.nested.empty()) {
-          st = foreach_entries(f.nested, ex, el_scoped, res, nesting + 1);
+          st = foreach_entries(r, f.nested, ex, el_scoped, res, nesting + 1, msg ? &em : nullptr);
         } else {
           st = NA;  // "invalid validation rule": nil response
         }
       } catch (const cond::EvalError&) {
         st = ERROR;
+        em = kNeedsErrText;
       }
       if (st == UNSUPPORTED) return UNSUPPORTED;
       if (st == NA || st == SKIP) continue;
       if (st == ERROR) {
         if (idx + 1 < elems.size()) continue;
+        if (msg) *msg = fe_wrap(em);
         return ERROR;
       }
-      if (st == FAIL) return FAIL;
+      if (st == FAIL) {
+        if (msg) *msg = fe_wrap(em);
+        return FAIL;
+      }
       ++count;
     }
     apply_count += count;
   }
   return apply_count == 0 ? NA : PASS;
 }
-inline Status foreach_handler(const Rule& r, const cond::Ctx& cx, const JVal& res) {
+inline Status foreach_handler(const Rule& r, const cond::Ctx& cx, const JVal& res, std::string* msg = nullptr) {
   try {
-    return foreach_entries(r.foreach, cx, nullptr, res, 0);
+    const Status s = foreach_entries(r, r.foreach, cx, nullptr, res, 0, msg);
+    if (msg && s == PASS) *msg = "rule passed";  // validate_resource.go:203
+    if (msg && s == NA) msg->clear();
+    return s;
   } catch (const cond::Unsupported&) {
     return UNSUPPORTED;
   }
@@ -1394,8 +1453,9 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
             s = SKIP, done = true;
             if (msgs) (*msgs)[i] = cond::join_non_empty({"preconditions not met", pm}, "; ");
           }
-        } catch (const cond::EvalError&) {
+        } catch (const cond::EvalError& e) {  // engine.go:279-281: RuleError "failed to evaluate preconditions"
           s = ERROR, done = true;
+          if (msgs) (*msgs)[i] = e.restated ? "failed to evaluate preconditions: " + e.msg : std::string(kNeedsErrText);
         } catch (const cond::Unsupported&) {
           s = UNSUPPORTED, done = true;
         }
@@ -1421,7 +1481,7 @@ inline void validate(const Policy& p, const JVal& res, const Labels& ns_labels, 
           PatMsg pm{&r.name, &r.vmsg, msgs ? &(*msgs)[i] : nullptr, &cx};
           s = pattern_handler(r.pattern, r.any_pattern, r.pattern_vars, res, &cx, msgs ? &pm : nullptr);
         }
-        else if (!r.foreach.empty()) s = foreach_handler(r, cx, res);
+        else if (!r.foreach.empty()) s = foreach_handler(r, cx, res, msgs ? &(*msgs)[i] : nullptr);
       }
     }
     out[i] = s;

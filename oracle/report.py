@@ -127,6 +127,9 @@ def report_results(policies: List[dict], rule_names: List[str], verdict_row, res
                         msg = "the produced message didn't resolve to a string, check your policy definition."
                 elif cell == 5 and _source_rule(pol, rname).get("preconditions") is not None:
                     msg = "preconditions not met"
+            elif (not ps0 and val.get("pattern") is None and val.get("anyPattern") is None
+                  and isinstance(val.get("foreach"), list) and val["foreach"] and cell == 1):
+                msg = "rule passed"  # validateForEach (validate_resource.go:203)
             if msg:
                 item["message"] = msg
         if rname:

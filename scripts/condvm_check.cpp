@@ -169,6 +169,19 @@ int main(int argc, char** argv) {
     fwrite(ct.data(), 4, ct.size(), g);
     fclose(g);
   }
+  if (argc > 6) {  // N x R x KPE_CTRACE_WORDS (kpe_fetch_cond_traces_ex layout)
+    std::vector<uint32_t> cx((size_t)C.n * R * 4u, 0u);  // KPE_CTRACE_WORDS (include/kpe.h)
+    for (const KpeCRule& cr : CP.rules) {
+      if (!cr.mslot) continue;
+      const uint32_t nw = cr.kind == CR_FOREACH ? KPE_FE_TRACE_WORDS : 1u;
+      for (int64_t r = 0; r < C.n; ++r)
+        for (uint32_t w = 0; w < nw; ++w)
+          cx[((size_t)r * R + cr.col) * 4u + w] = mtrace[(size_t)r * CP.nmsg + cr.mslot - 1u + w];
+    }
+    FILE* g = fopen(argv[6], "wb");
+    fwrite(cx.data(), 4, cx.size(), g);
+    fclose(g);
+  }
   printf("%lld %u\n", (long long)C.n, R);
   return 0;
 }

@@ -560,6 +560,42 @@ def engine_message_cases():
     return out
 
 
+def engine_table_message_cases():
+    """pkg/engine/validation_test.go table-driven tests with `policyRaw: []byte(...)`,
+    `resourceRaw: []byte(...)`, `expectedResults` and `expectedMessages` fields (one entry per
+    table row; e.g. Test_Flux_Kustomization_PathNotPresent, whose first row pins a RuleError
+    text: "failed to check deny conditions: failed to substitute variables in condition key: ...")."""
+    path = os.path.join(REF, "pkg/engine/validation_test.go")
+    src = open(path).read()
+    out = []
+    funcs = [(m.start(), m.group(1)) for m in re.finditer(r"^func (Test\w+)\(t \*testing\.T\)", src, re.M)]
+    funcs.append((len(src), None))
+    gostr = r'"((?:[^"\\]|\\.)*)"'
+    status = {"RuleStatusPass": "pass", "RuleStatusFail": "fail", "RuleStatusError": "error",
+              "RuleStatusSkip": "skip", "RuleStatusWarn": "warn"}
+    for (a, name), (b, _) in zip(funcs, funcs[1:]):
+        body = src[a:b]
+        if "expectedMessages:" not in body:
+            continue
+        for row in re.finditer(r"\{\s*name:\s*" + gostr + r"(.*?)expectedMessages:\s*\[\]string\{(.*?)\},\s*\n\s*\}",
+                               body, re.S):
+            fields = row.group(2)
+            raws = {m.group(1).lower(): m.group(2) for m in re.finditer(r"(\w+):\s*\[\]byte\(`(.*?)`\)", fields, re.S)}
+            try:
+                pol = json.loads(raws["policyraw"])
+                res = json.loads(raws["resourceraw"])
+            except (KeyError, ValueError):
+                continue
+            rs = re.search(r"expectedResults:\s*\[\]engineapi\.RuleStatus\{(.*?)\}", fields, re.S)
+            results = [status[x] for x in re.findall(r"engineapi\.(RuleStatus\w+)", rs.group(1))] if rs else []
+            msgs = [json.loads('"' + x.group(1) + '"') for x in re.finditer(gostr, row.group(3))]
+            out.append({"name": name, "row": json.loads('"' + row.group(1) + '"'),
+                        "line": src.count("\n", 0, a + row.start()) + 1, "policy": pol, "resource": res,
+                        "results": results, "messages": msgs})
+    print(f"engine_table_message_cases: {len(out)} rows")
+    return out
+
+
 def _render_chart_template(text):
     name = re.search(r'\$name := "([^"]+)"', text).group(1)
     out, stack = [], []  # stack of "branch active" flags
@@ -716,6 +752,7 @@ def image_cases():
 
 if __name__ == "__main__":
     _dump("engine_message_cases.json", engine_message_cases())
+    _dump("engine_table_message_cases.json", engine_table_message_cases())
     _dump("image_cases.json", image_cases())
     _dump("condition_cases.json", condition_cases())
     _dump("best_practices.json", best_practices())

@@ -487,3 +487,83 @@ def var_policy_set():
 # rules of var_policy_set whose cells the device may leave KPE_UNDECIDED (a variable resolving
 # to a map is a pattern subtree; documented device limit)
 VAR_UNDECIDED_OK = {"v-map", "vk-collide"}  # vk-collide: a key renamed onto another key of the map
+
+
+def foreach_message_policy_set():
+    """validate.foreach rules and RuleError texts for the message renderers (validate_resource.go:
+    121-254: foreach pass "rule passed", "validation failure: <element message>" once per nesting
+    level, and the RuleError texts of preconditions / deny / pattern substitution errors, engine.go
+    :279-281). The chart's restricted disallow-capabilities-strict rules first (charts/kyverno-
+    policies/templates/restricted/disallow-capabilities-strict.yaml, rendered with the default
+    values)."""
+    obj = "request.object"
+    ctrs = obj + ".spec.[ephemeralContainers, initContainers, containers][]"
+    not_delete = {"all": [{"key": "{{ request.operation || 'BACKGROUND' }}", "operator": "NotEquals", "value": "DELETE"}]}
+
+    def rule(name, validate, pre=None, kinds=("Pod",)):
+        r = {"name": name, "match": {"any": [{"resources": {"kinds": list(kinds)}}]}, "validate": validate}
+        if pre is not None:
+            r["preconditions"] = pre
+        return r
+
+    def c(key, op, value, message=None):
+        x = {"key": key, "operator": op, "value": value}
+        if message is not None:
+            x["message"] = message
+        return x
+
+    rules = [
+        rule("require-drop-all", {"message": "Containers must drop `ALL` capabilities.", "foreach": [
+            {"list": ctrs, "deny": {"conditions": {"all": [
+                c("ALL", "AnyNotIn", "{{ element.securityContext.capabilities.drop[] || `[]` }}")]}}}]}, pre=not_delete),
+        rule("adding-capabilities-strict", {
+            "message": "Any capabilities added other than NET_BIND_SERVICE are disallowed.", "foreach": [
+                {"list": ctrs, "deny": {"conditions": {"all": [
+                    c("{{ element.securityContext.capabilities.add[] || `[]` }}", "AnyNotIn",
+                      ["NET_BIND_SERVICE", ""])]}}}]}, pre=not_delete),
+        # condition messages, element variables in the rule message
+        rule("fe-cond-msg", {"message": "container {{ element.name }} ({{ elementIndex }}) of {{ request.object.metadata.name }}",
+                             "foreach": [{"list": obj + ".spec.containers", "deny": {"conditions": {"any": [
+                                 c("{{ element.image }}", "Equals", "*:latest", "latest tag"),
+                                 c("{{ element.securityContext.privileged || `false` }}", "Equals", True, "privileged")]}}}]}),
+        rule("fe-no-msg", {"foreach": [{"list": obj + ".spec.containers[].image", "deny": {"conditions": {"all": [
+            c("{{ element }}", "NotEquals", "nginx*")]}}}]}),
+        rule("fe-all-msgs", {"message": "m.", "foreach": [{"list": obj + ".spec.containers", "deny": {"conditions": {"all": [
+            c("{{ element.name }}", "Equals", "c-*", "named c-"),
+            c("{{ element.image }}", "NotEquals", "redis:*", "not redis")]}}}]}),
+        # nested foreach: wrapped twice
+        rule("fe-nested-deny", {"message": "port {{ element.containerPort }} at {{ elementIndex1 }}", "foreach": [
+            {"list": obj + ".spec.containers", "foreach": [{"list": "element.ports", "deny": {"conditions": {"all": [
+                c("{{ element.containerPort }}", "GreaterThan", 8000)]}}}]}]}),
+        # errors raised by an element: preconditions / deny substitutions (NotFound), elementScope
+        rule("fe-pre-err", {"message": "m", "foreach": [{"list": obj + ".spec.containers", "preconditions": {"all": [
+            c("{{ element.securityContext.runAsUser }}", "Equals", 0)]},
+            "deny": {"conditions": {"all": [c("a", "Equals", "a")]}}}]}),
+        rule("fe-deny-err", {"message": "m", "foreach": [{"list": obj + ".spec.containers", "deny": {"conditions": {"any": [
+            c("x", "Equals", ["{{ element.name }}", "{{ element.resources.limits.memory }}"])]}}}]}),
+        rule("fe-scope-err", {"message": "m", "foreach": [{"list": obj + ".spec.containers[].name", "elementScope": True,
+                                                          "deny": {"conditions": {"all": [c("a", "Equals", "a")]}}}]}),
+        # pattern entries on the element
+        rule("fe-pattern", {"message": "image of {{ element.name }} must be pinned",
+                            "foreach": [{"list": obj + ".spec.containers", "pattern": {"image": "!*:latest"}}]}),
+        rule("fe-pattern-nomsg", {"foreach": [{"list": ctrs, "pattern": {"securityContext": {"runAsNonRoot": True}}}]}),
+        rule("fe-any", {"message": "pinned or init", "foreach": [{"list": obj + ".spec.containers", "anyPattern": [
+            {"image": "*:1.*"}, {"name": "init-*"}]}]}),
+        rule("fe-pvar-err", {"foreach": [{"list": obj + ".spec.containers", "pattern": {
+            "image": "{{ element.imagePullPolicy }}*"}}]}),
+        rule("fe-any-bad", {"foreach": [{"list": obj + ".spec.containers", "anyPattern": {"image": "x"}}]}),
+        rule("fe-nested-pat", {"foreach": [{"list": obj + ".spec.containers", "foreach": [
+            {"list": "element.ports", "pattern": {"containerPort": "<8000"}}]}]}),
+        # rule-level RuleErrors
+        rule("pre-err", {"message": "m", "pattern": {"metadata": {"name": "?*"}}},
+             pre={"all": [c("{{ " + obj + ".metadata.labels.team }}", "Equals", "x")]}),
+        rule("pre-nil-query", {"message": "m", "deny": {"conditions": {"all": [c("{{ " + obj + ".kind }}", "Equals", "Pod")]}}},
+             pre={"any": [c("{{ }}", "Equals", "x")]}),
+        rule("deny-err-value", {"message": "m", "deny": {"conditions": [
+            c("{{ " + obj + ".kind }}", "In", ["Pod", "{{ " + obj + ".metadata.labels.team }}"])]}}),
+        rule("deny-bad-op", {"message": "m", "deny": {"conditions": {"all": [c("{{ " + obj + ".kind }}", "Bogus", "Pod")]}}}),
+        rule("pat-var-err", {"message": "m", "pattern": {"metadata": {"labels": {"app": "{{ " + obj + ".metadata.labels.team }}"}}}}),
+        rule("any-bad", {"message": "m", "anyPattern": {"metadata": {"name": "x"}}}),
+    ]
+    return [{"apiVersion": "kyverno.io/v1", "kind": "ClusterPolicy", "metadata": {"name": "femsg"},
+             "spec": {"validationFailureAction": "Audit", "background": True, "rules": rules}}]
