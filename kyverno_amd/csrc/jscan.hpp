@@ -8,10 +8,40 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <emmintrin.h>  // SSE2 (x86-64 baseline): 16-byte scans of strings and skipped values
+
 #include <string>
 #include <string_view>
 
 namespace kpe {
+
+// The first byte of [p, e) that is `"` or a backslash (16 bytes per step)
+inline const char* jscan_quote(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), b = _mm_set1_epi8('\\');
+  while (e - p >= 16) {
+    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+    const int m = _mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_cmpeq_epi8(x, b)));
+    if (m) return p + __builtin_ctz((unsigned)m);
+    p += 16;
+  }
+  while (p < e && *p != '"' && *p != '\\') ++p;
+  return p;
+}
+// The first structural byte of [p, e) for skipping a container: `"` `{` `}` `[` `]`
+// ('[' | 0x20 == '{' and ']' | 0x20 == '}': two compares after an OR cover the brackets)
+inline const char* jscan_struct(const char* p, const char* e) {
+  const __m128i q = _mm_set1_epi8('"'), lo = _mm_set1_epi8('{'), hi = _mm_set1_epi8('}'), bit = _mm_set1_epi8(0x20);
+  while (e - p >= 16) {
+    const __m128i x = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+    const __m128i y = _mm_or_si128(x, bit);
+    const int m = _mm_movemask_epi8(
+        _mm_or_si128(_mm_cmpeq_epi8(x, q), _mm_or_si128(_mm_cmpeq_epi8(y, lo), _mm_cmpeq_epi8(y, hi))));
+    if (m) return p + __builtin_ctz((unsigned)m);
+    p += 16;
+  }
+  while (p < e && *p != '"' && *p != '{' && *p != '}' && *p != '[' && *p != ']') ++p;
+  return p;
+}
 
 enum class JK : uint8_t { End, Null, Bool, Num, Str, Arr, Obj, Bad };
 
@@ -135,7 +165,7 @@ class JCur {
     if (p_ >= e_ || *p_ != '"') return fail();
     ++p_;
     const char* s = p_;
-    while (p_ < e_ && *p_ != '"' && *p_ != '\\') ++p_;
+    p_ = jscan_quote(p_, e_);
     if (p_ < e_ && *p_ == '"') {
       *out = std::string_view(s, (size_t)(p_ - s));
       ++p_;
@@ -244,19 +274,18 @@ class JCur {
       case JK::Str: return skip_str();
       case JK::Arr:
       case JK::Obj: {
-        // bracket matching with string awareness
+        // bracket matching with string awareness ('[' / ']' are '{' / '}' without bit 5, and
+        // only structural bytes are visited)
         int depth = 0;
-        while (p_ < e_) {
-          char c = *p_;
+        while ((p_ = jscan_struct(p_, e_)) < e_) {
+          const char c = *p_;
           if (c == '"') {
             if (!skip_str()) return false;
             continue;
           }
           ++p_;
-          if (c == '{' || c == '[') ++depth;
-          else if (c == '}' || c == ']') {
-            if (--depth == 0) return true;
-          }
+          if ((c | 0x20) == '{') ++depth;
+          else if (--depth == 0) return true;
         }
         return fail();
       }
@@ -281,13 +310,10 @@ class JCur {
     ws();
     if (p_ >= e_ || *p_ != '"') return fail();
     ++p_;
-    while (p_ < e_) {
-      char c = *p_++;
-      if (c == '"') return true;
-      if (c == '\\') {
-        if (p_ >= e_) return fail();
-        ++p_;
-      }
+    while ((p_ = jscan_quote(p_, e_)) < e_) {
+      if (*p_++ == '"') return true;
+      if (p_ >= e_) return fail();  // a backslash: skip the escaped byte
+      ++p_;
     }
     return fail();
   }

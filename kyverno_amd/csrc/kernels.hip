@@ -33,6 +33,9 @@ namespace {
 
 // Wave-uniform table read: the address is uniform, so this is a scalar (SMEM) load
 // through the constant cache — no LDS round trip and no readfirstlane to branch on it.
+#ifndef KPE_DIAG
+#define KPE_DIAG 0  // diagnostic builds only (scripts/diag_scan.sh): sections of the WIDE scan left out
+#endif
 template <class T>
 __device__ __forceinline__ T sld(const T* p, uint32_t i) {
   static_assert(sizeof(T) % 4 == 0, "word-sized tables");
@@ -547,7 +550,11 @@ __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabC
     if (live && row != KPE_NO_STR) LC.nlo = a.nsl_off[row], LC.nhi = a.nsl_off[row + 1];
     if (a.selm & 2u) LC.nsq = a.ns_q[live && row != KPE_NO_STR ? row : a.ns_none];
   }
+#if KPE_DIAG & 4  // diagnostic build: no label fold
+  LC.selq = LC.lo ^ LC.hi;
+#else
   if (a.selm & 1u) LC.selq = sel_fold(a, LC);
+#endif
 }
 
 // One match term for this lane's resource (utils/match.go:52-160 attributes).
@@ -973,12 +980,16 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
     LabCache LC;
     lab_cache(a, rc, live, LC);
+#if KPE_DIAG & 2  // diagnostic build: no term evaluation
+    if (lane < a.nterms) tmk[lane] = LC.selq ^ gvk ^ nsa;
+#else
 #pragma unroll 1
     for (uint32_t ti = 0; ti < a.nterms; ++ti) {
       const KpeTerm tm = a.nterms <= 64u ? KpeTerm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u} : sld(a.terms, ti);
       const uint64_t m = __ballot(eval_term(a, B, tm, gvk, nsa, name_col, mns_col, rc, live, LC));
       if (lane == 0) tmk[ti] = m;
     }
+#endif
     // PSS version sets: resources failing some check of each distinct cv_mask
 #pragma unroll 1
     for (uint32_t c = 0; c < a.ncv; ++c) {
@@ -989,6 +1000,16 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     const uint64_t err_m = __ballot(err);
     __builtin_amdgcn_wave_barrier();
 
+#if KPE_DIAG & 1  // diagnostic build: no rule evaluation, the term masks' low bytes as verdicts
+    {
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t i = lane; i < nrows * R; i += 64) sv[i] = (uint8_t)(tmk[i % a.nterms] >> (i & 7u)) & 7u;
+      __builtin_amdgcn_wave_barrier();
+      store_rows(a.verdicts, sv, tile, R, 0, R, nrows, lane);
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
+#endif
     // ---- rules, KPE_RULE_CHUNK at a time ----
     uint64_t applied = 0;  // ApplyOne state (lane 0, rule order)
     uint32_t cur_policy = 0xFFFFFFFFu;

@@ -622,7 +622,13 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
   const bool sel_terms = std::any_of(P.terms.begin(), P.terms.end(), [](const KpeTerm& t) {
     return t.type == T_SELECTOR || t.type == T_NSSELECTOR;
   });
-  const bool narrow = !sel_terms && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
+  // (KPE_SEL_NARROW=1: selector programs on the narrow path too, for A/B runs: since the
+  // requirement masks, a selector term is one mask compare per lane on either path)
+  static const bool sel_narrow = [] {
+    const char* e = getenv("KPE_SEL_NARROW");
+    return e && atoi(e) != 0;
+  }();
+  const bool narrow = (!sel_terms || sel_narrow) && !P.rules.empty() && P.rules.size() <= KPE_NARROW_R &&
                       P.terms.size() <= KPE_NARROW_TERMS && P.filters.size() <= KPE_NARROW_FILTERS;
   std::vector<uint32_t> nrules, fmask;
   if (narrow) {
