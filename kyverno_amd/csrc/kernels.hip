@@ -562,7 +562,18 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
                                           uint32_t nsa, uint32_t name_col, uint32_t mns_col, uint32_t rc,
                                           bool live, const LabCache& LC) {
   bool ok = true;
-  if (tm.type == T_KIND_PRED) {
+  if (tm.type == T_SELQ || tm.type == T_NSSELQ) {  // requirement-mask selectors (binding form)
+    const uint32_t q = tm.a & 0xFFu, nq = (tm.a >> 8) & 0xFFu, f = tm.a >> 16;
+    const uint64_t need = (nq >= 64u ? ~0ull : ((1ull << nq) - 1ull)) << q;
+    if (tm.type == T_SELQ) {
+      ok = (LC.selq & need) == need;
+    } else {  // namespaceSelector: never for kind Namespace; skipped for an empty kind unless kinds hold "*"
+      const uint32_t kid = GVK_KIND(gvk);
+      if (kid == (tm.b & 0xFFFFu)) ok = (f & TSQ_EXC) != 0u;
+      else if (kid == (tm.b >> 16) && (!(f & TSQ_STAR) || (f & TSQ_EXC))) ok = true;
+      else ok = !(f & TSQ_INVALID) && (LC.nsq & need) == need;
+    }
+  } else if (tm.type == T_KIND_PRED) {
     ok = B.bit(tm.a, GVK_KIND(gvk));
   } else if (tm.type == T_KINDS) {  // CheckKind: OR over kind selectors
     ok = false;

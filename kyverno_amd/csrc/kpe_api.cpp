@@ -1142,6 +1142,33 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
       HIPCHK(B.sel_nsq.ensure(C.nsl_off.size() * 8));
     }
   }
+  // selector terms with requirement-mask bits: the binding form (T_SELQ / T_NSSELQ) the scan
+  // evaluates with one mask compare (KPE_SELQ=0 keeps the selector-record form, for A/B runs)
+  static const bool selq_off = [] {
+    const char* e = getenv("KPE_SELQ");
+    return e && atoi(e) == 0;
+  }();
+  if (!selq_off) {
+    auto kind_id = [&](const char* k) -> uint32_t {
+      const int64_t id = C.dict[D_KIND].find(k);
+      return id < 0 || id >= 0xFFFF ? 0xFFFFu : (uint32_t)id;
+    };
+    const uint32_t ns_kid = kind_id("Namespace"), empty_kid = kind_id("");
+    for (auto& t : terms) {
+      if ((t.type != T_SELECTOR || !(B.selm & 1u)) && (t.type != T_NSSELECTOR || !(B.selm & 2u))) continue;
+      const KpeSelector& S = selectors[t.a];
+      if (S.qbit == KPE_NO_QBIT || S.qbit > 63 || S.nreq > 64) continue;
+      const bool ns = t.type == T_NSSELECTOR;
+      // the kind predicates of a namespaceSelector are exactly "Namespace" and "" (program.cpp)
+      if (ns && (P.preds[P.selectors[t.a].p_kind_ns].globs != std::vector<std::string>{"Namespace"} ||
+                 P.preds[P.selectors[t.a].p_kind_empty].globs != std::vector<std::string>{""}))
+        continue;
+      const uint32_t f = (S.exc ? TSQ_EXC : 0u) | (S.star_kind ? TSQ_STAR : 0u) | (S.invalid ? TSQ_INVALID : 0u);
+      t.a = S.qbit | S.nreq << 8 | f << 16;
+      t.b = ns ? (ns_kid | empty_kid << 16) : 0u;
+      t.type = ns ? T_NSSELQ : T_SELQ;
+    }
+  }
   HIPCHK(upload(B.terms_r, terms, s));
   HIPCHK(upload(B.kindsels_r, kindsels, s));
   HIPCHK(upload(B.annpairs_r, annpairs, s));

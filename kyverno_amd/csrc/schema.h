@@ -335,8 +335,17 @@ enum KpeTermType {
   T_ANNOTATIONS = 3,  // every pair [a, a+b) of the annotation-pair table must be matched by some annotation
   T_SELECTOR = 4,     // label selector a (selector table) over resource labels
   T_NSSELECTOR = 5,   // label selector a over the namespace's labels (not for kind Namespace)
-  T_KIND_PRED = 6     // kind-only selectors folded into one predicate a over D_KIND
+  T_KIND_PRED = 6,    // kind-only selectors folded into one predicate a over D_KIND
+  // binding-time forms of T_SELECTOR / T_NSSELECTOR whose requirements have bits in the
+  // requirement masks (ScanArgs::selm): a = qbit | nreq << 8 | TSQ_* << 16, b (T_NSSELQ) = the
+  // D_KIND ids of "Namespace" | "" << 16 (0xFFFF: not in the corpus). One mask compare per lane,
+  // no selector record load in the tile loop.
+  T_SELQ = 7,
+  T_NSSELQ = 8
 };
+#define TSQ_EXC 1u      // KpeSelector::exc
+#define TSQ_STAR 2u     // KpeSelector::star_kind
+#define TSQ_INVALID 4u  // KpeSelector::invalid
 enum KpeCol { COL_NAME = 0, COL_MNS = 1, COL_NSA = 2 };
 
 typedef struct KpeTerm {
