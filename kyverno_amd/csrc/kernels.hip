@@ -509,12 +509,24 @@ struct LabCache {
 // Label-selector requirement mask of one resource (ScanArgs::selm bit 0): its labels folded in
 // order. Requirement q is decided by the first label whose key matches it (and whose value
 // matches too, for a wildcard matchLabels entry), as the per-requirement loop of eval_term.
-__device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC) {
+__device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC, const uint32_t* dyn) {
   uint64_t notyet = ~0ull, okacc = 0;
   const uint64_t nwild = ~a.sm_wild;
+  // the requirement tables from LDS when the block staged them (ScanArgs::selt_lds), else L2;
+  // the branch is uniform and each side's loads are typed, so no flat load's wait covers the
+  // prefetch of the next tile
+  const bool in_lds = a.selt_lds != PRED_NONE;
+  const LdsPtr lt = (LdsPtr)(dyn + (in_lds ? a.selt_lds : 0u));
   auto fold = [&](uint32_t k, uint32_t v) {
-    const uint4 kq = k < a.nlabk ? a.sel_km[k] : make_uint4(0u, 0u, 0u, 0u);
-    const uint4 vq = v < a.nlabv ? a.sel_vm[v] : make_uint4(0u, 0u, 0u, 0u);
+    uint4 kq = make_uint4(0u, 0u, 0u, 0u), vq = make_uint4(0u, 0u, 0u, 0u);
+    if (in_lds) {
+      const uint32_t vi = 4u * (a.nlabk + v);
+      if (k < a.nlabk) kq = make_uint4(lt[4u * k], lt[4u * k + 1u], lt[4u * k + 2u], lt[4u * k + 3u]);
+      if (v < a.nlabv) vq = make_uint4(lt[vi], lt[vi + 1u], lt[vi + 2u], lt[vi + 3u]);
+    } else {
+      if (k < a.nlabk) kq = a.sel_km[k];
+      if (v < a.nlabv) vq = a.sel_vm[v];
+    }
     const uint64_t km = kq.x | (uint64_t)kq.y << 32, kok = kq.z | (uint64_t)kq.w << 32;
     const uint64_t vm = vq.x | (uint64_t)vq.y << 32, vok = vq.z | (uint64_t)vq.w << 32;
     const uint64_t f = km & (nwild | vm);  // this label is the requirement's first match
@@ -539,7 +551,7 @@ __device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC) {
          (notyet & a.sm_dne);
 }
 
-__device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC) {
+__device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC, const uint32_t* dyn) {
   uint32_t lo = 0, hi = 0;
   if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = live ? a.lab_off[rc + 1] : lo;
   LC.lo = lo, LC.hi = hi;
@@ -553,7 +565,7 @@ __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabC
 #if KPE_DIAG & 4  // diagnostic build: no label fold
   LC.selq = LC.lo ^ LC.hi;
 #else
-  if (a.selm & 1u) LC.selq = sel_fold(a, LC);
+  if (a.selm & 1u) LC.selq = sel_fold(a, LC, dyn);
 #endif
 }
 
@@ -762,6 +774,11 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
 #pragma unroll 1
       for (uint32_t i = t; i < a.blob_words; i += kBlock) dyn[i] = 0;
     }
+    if (a.selt_lds != PRED_NONE) {  // label-selector requirement tables (sel_km, then sel_vm)
+      uint4* d = reinterpret_cast<uint4*>(dyn + a.selt_lds);
+#pragma unroll 1
+      for (uint32_t i = t; i < a.nlabk + a.nlabv; i += kBlock) d[i] = i < a.nlabk ? a.sel_km[i] : a.sel_vm[i - a.nlabk];
+    }
     if (!NARROW && a.filt_lds != PRED_NONE) {  // program filters + filter terms for the rule lanes
       const uint32_t nw = a.fterm_lds + a.nfterms - a.filt_lds;
       const uint32_t* src = reinterpret_cast<const uint32_t*>(a.filters);
@@ -914,7 +931,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       uint32_t tb = 0;
       if constexpr (!LEAN) {
         LabCache LC;
-        lab_cache(a, rc, live, LC);
+        lab_cache(a, rc, live, LC, dyn);
 #pragma unroll 1
         for (uint32_t ti = 0; ti < a.nterms; ++ti) {
           const KpeTerm tm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u};
@@ -938,6 +955,16 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       }
       // ---- rules, in program order, for this lane's resource ----
       bool applied = false;
+#ifdef KPE_NARROW_FV
+      // every filter once per lane into a bit vector (a filter holds when all of its terms hold);
+      // a block is then one mask test over its filters [f0, f0 + nf)
+      uint64_t fv = 0;
+#pragma unroll 1
+      for (uint32_t f = 0; f < a.nfilters; ++f) {
+        const uint32_t fm = hw(fm_lane, f);
+        fv |= (uint64_t)((tb & fm) == fm) << f;
+      }
+#endif
 #pragma unroll 1
       for (uint32_t ri = 0; ri < R; ++ri) {
         const uint4 nr = make_uint4(hw(myrule.x, ri), hw(myrule.y, ri), hw(myrule.z, ri), hw(myrule.w, ri));
@@ -945,6 +972,10 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         // a block is an OR (any / legacy) or AND (all) of filters; a filter holds when
         // all of its terms hold: (tb & mask) == mask
         auto block = [&](uint32_t mode, uint32_t f0, uint32_t nf) -> bool {
+#ifdef KPE_NARROW_FV
+          const uint64_t M = (nf >= 64u ? ~0ull : ((1ull << nf) - 1ull)) << f0;
+          return mode == MODE_ALL ? (fv & M) == M : (fv & M) != 0ull;
+#else
           const bool all = mode == MODE_ALL;
           bool acc = all;
 #pragma unroll 1
@@ -954,6 +985,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
             acc = all ? (acc && h) : (acc || h);
           }
           return acc;
+#endif
         };
         const uint32_t pol = NR_POLTERM(x);
         bool m = live && (pol == 0u || ((tb >> (pol - 1u)) & 1u));
@@ -990,7 +1022,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
     LabCache LC;
-    lab_cache(a, rc, live, LC);
+    lab_cache(a, rc, live, LC, dyn);
 #if KPE_DIAG & 2  // diagnostic build: no term evaluation
     if (lane < a.nterms) tmk[lane] = LC.selq ^ gvk ^ nsa;
 #else
@@ -1099,15 +1131,25 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         }
         __builtin_amdgcn_wave_barrier();
       }
-      // (b) verdict bytes (resource lanes)
+      // (b) verdict bytes (resource lanes): the cell's (p, f, e) bits index a nibble table --
+      // NA, ERROR, FAIL, PENDING, PASS, SKIP, XFAIL, SKIP -- and four cells go to LDS as one dword
+      // when the row segments are dword aligned
+      constexpr uint32_t kVt = KPE_NA_ | KPE_ERROR_ << 4 | KPE_FAIL_ << 8 | KPE_PENDING_ << 12 | KPE_PASS_ << 16 |
+                               KPE_SKIP_ << 20 | (uint32_t)KPE_XFAIL_ << 24 | (uint32_t)KPE_SKIP_ << 28;
+      auto cell = [&](uint32_t j) -> uint32_t {
+        const uint32_t idx = (uint32_t)((rmk[j * 4] >> lane) & 1u) << 2 | (uint32_t)((rmk[j * 4 + 1] >> lane) & 1u) << 1 |
+                             (uint32_t)((rmk[j * 4 + 2] >> lane) & 1u);
+        const uint32_t v = (kVt >> (idx << 2)) & 0xFu;
+        return v | (((uint32_t)(rmk[j * 4 + 3] >> lane) & 1u) && v ? (uint32_t)KPE_XDEFER_ : 0u);
+      };
+      if ((nc & 3u) == 0u) {
+        uint32_t* sv32 = reinterpret_cast<uint32_t*>(sv + lane * nc);
+#pragma unroll 2
+        for (uint32_t j = 0; j < nc; j += 4)
+          sv32[j >> 2] = cell(j) | cell(j + 1) << 8 | cell(j + 2) << 16 | cell(j + 3) << 24;
+      } else {
 #pragma unroll 4
-      for (uint32_t j = 0; j < nc; ++j) {
-        const uint64_t pm = rmk[j * 4], fm = rmk[j * 4 + 1], em = rmk[j * 4 + 2], dm = rmk[j * 4 + 3];
-        const uint32_t f = (fm >> lane) & 1u, e = (em >> lane) & 1u;
-        const uint32_t p = (pm >> lane) & 1u;
-        const uint32_t v = p ? (e ? KPE_SKIP_ : f ? KPE_XFAIL_ : KPE_PASS_) : (f && e) ? KPE_PENDING_ : f ? KPE_FAIL_
-                                                                   : e ? KPE_ERROR_ : KPE_NA_;
-        sv[lane * nc + j] = (uint8_t)(v | (((dm >> lane) & 1u) && v != KPE_NA_ ? (uint32_t)KPE_XDEFER_ : 0u));
+        for (uint32_t j = 0; j < nc; ++j) sv[lane * nc + j] = (uint8_t)cell(j);
       }
       if (a.masks && live) {
 #pragma unroll 1

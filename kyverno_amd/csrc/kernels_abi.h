@@ -174,6 +174,9 @@ struct ScanArgs {
   const uint4* sel_vm;
   const uint64_t* ns_q;
   uint32_t selm, ns_none, nlabk, nlabv;
+  // sel_km then sel_vm staged in each scan block's LDS at this word offset (the label fold then
+  // reads LDS, not L2), or PRED_NONE
+  uint32_t selt_lds, selt_pad;
   uint64_t sm_pos, sm_wild, sm_notin, sm_exists, sm_dne;
   // outputs
   uint8_t* verdicts;  // n x nrules

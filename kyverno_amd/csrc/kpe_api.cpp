@@ -111,7 +111,8 @@ hipError_t upload(DevBuf& b, const std::vector<T>& v, hipStream_t s) {
 constexpr uint32_t kMaxLocalWords = 8192;  // 32 KiB of small-domain predicate bitsets
 constexpr uint32_t kMaxDynWords = 13312;   // dynamic LDS per scan block (52 KiB)
 constexpr uint32_t kMaxTerms = 1024;       // distinct match terms (term masks: 8 B x 4 waves each)
-constexpr uint32_t kMaxProgLds = 4096;     // filters + filter terms staged in LDS
+constexpr uint32_t kMaxProgLds = 4096;
+constexpr uint32_t kMaxSelLds = 2048;  // label-selector requirement tables staged in LDS (8 KiB)     // filters + filter terms staged in LDS
 constexpr uint32_t kMaxLocalPairs = 2048;  // domain size limit for an LDS-resident bitset
 constexpr uint32_t kMaxFuseWords = 4096;   // fuse image <= 16 KiB of LDS
 constexpr uint32_t kLeanBatchKinds = 4096; // kind table words a LEAN6 block stages
@@ -240,6 +241,7 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint64_t sm[5] = {};  // pos (EQ / In), wild, NotIn, Exists, DoesNotExist
   uint32_t pp[10] = {};  // fixed PSS predicate locations
   uint32_t wave_lds = 0, wave_words = 0, filt_lds = PRED_NONE, fterm_lds = 0, tt_lds = PRED_NONE;
+  uint32_t selt_lds = PRED_NONE;  // ScanArgs::selt_lds
   size_t dyn_bytes = 0;
   uint32_t nblocks = 0, njobs = 0, blob_words = 0, scan_blocks = 0;
   uint32_t need = 0;
@@ -982,6 +984,15 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
                                       : 2 * nterms + 2 * ncv + 2 * 4 * KPE_RULE_CHUNK + 64 * KPE_RULE_CHUNK / 4);
   const uint32_t prog_words = 2 * (uint32_t)P.filters.size() + (uint32_t)P.fterms.size();
   const bool stage_prog = !narrow && prog_words <= kMaxProgLds;
+  // the label-selector requirement tables (sel_km, sel_vm: 4 words per label key / value id) in
+  // LDS when they are small: the per-row label fold then reads LDS instead of L2
+  const bool sel_lbl = std::any_of(P.terms.begin(), P.terms.end(), [](const KpeTerm& t) { return t.type == T_SELECTOR; });
+  const uint64_t selt_need = 4ull * ((uint64_t)C.dict[D_LABK].size() + C.dict[D_LABV].size());
+  static const bool selt_off = [] {
+    const char* e = getenv("KPE_SELT");
+    return e && atoi(e) == 0;
+  }();
+  const uint32_t selt_words = sel_lbl && !selt_off && selt_need <= kMaxSelLds ? (uint32_t)selt_need : 0u;
   // LEAN scan candidate: prepped, NARROW truth-table program of kind-only terms (a kind table
   // replaces the per-resource term loop); confirmed below once predicate placement is known
   bool lean = narrow && PD.tt && P.any_pss &&
@@ -991,7 +1002,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const uint32_t kt_words = lean ? (C.dict[D_KIND].size() + 3) & ~3u : 0u;
   const uint32_t capb_words = P.any_pss ? ((uint32_t)C.capset_add.size() + 15) / 16 * 4 : 0u;  // 1 byte per set
   const int64_t budget =
-      (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 -
+      (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 - selt_words - 4 -
       (PD.tt ? (1 << KPE_TT_TERMS) : 0) - kt_words - capb_words;
   if (budget < 0) return fail(KPE_E_LIMIT, "program does not fit the scan kernel's LDS budget");
   const uint32_t local_budget = (uint32_t)std::min<int64_t>(kMaxLocalWords, budget);
@@ -1038,7 +1049,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const uint32_t capb_at = kt_at + kt_words;
   const uint32_t img_end = capb_at + capb_words;
   const uint32_t prog_at = img_end;
-  const uint32_t wave_at = (prog_at + (stage_prog ? prog_words : 0) + 1) & ~1u;
+  const uint32_t selt_at = (prog_at + (stage_prog ? prog_words : 0) + 3) & ~3u;
+  const uint32_t wave_at = (selt_at + selt_words + 1) & ~1u;
   const uint32_t scan_end = wave_at + 4 * wave_words;
   const uint32_t fuse_at = (scan_end + 3) & ~3u;
   std::vector<uint32_t> dir(npreds);
@@ -1289,6 +1301,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.filt_lds = stage_prog ? prog_at : PRED_NONE;
   B.fterm_lds = prog_at + 2 * (uint32_t)P.filters.size();
   B.wave_lds = wave_at;
+  B.selt_lds = selt_words ? selt_at : PRED_NONE;
   B.wave_words = wave_words;
   B.prep_dyn_bytes = (size_t)(fuse_at + fuse_words) * 4;
   B.pimg_words = img_end;  // prologue image: LDS [0, img_end)
@@ -1477,10 +1490,12 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.kt_lds = B.kt_lds, sa.nkinds = B.nkinds;
   sa.psum = psum_go ? D.psum.as<uint32_t>() : nullptr;
   sa.selm = B.selm;
+  sa.selt_lds = PRED_NONE;
   if (B.selm) {
     sa.sel_km = B.sel_km.as<uint4>(), sa.sel_vm = B.sel_vm.as<uint4>(), sa.ns_q = B.sel_nsq.as<uint64_t>();
     sa.ns_none = (uint32_t)C.nsl_off.size() - 1;
     sa.nlabk = C.dict[D_LABK].size(), sa.nlabv = C.dict[D_LABV].size();
+    sa.selt_lds = (B.selm & 1u) ? B.selt_lds : PRED_NONE;
     sa.sm_pos = B.sm[0], sa.sm_wild = B.sm[1], sa.sm_notin = B.sm[2], sa.sm_exists = B.sm[3], sa.sm_dne = B.sm[4];
   }
   sa.verdicts = B.verdicts.as<uint8_t>();
