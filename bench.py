@@ -353,6 +353,10 @@ def main(argv=None):
     dict_ms = st.dict_kernel_ms / L
     pat_ms = st.pattern_kernel_ms / L
     scan_achieved = acct["achieved_gbs"]
+    # spread of the timed region's scan launches (HIP events, one stream): mean, std, min, max
+    scan_std = math.sqrt(max(0.0, st.pss_kernel_ms_sq / L - scan_ms * scan_ms)) if st.launches else 0.0
+    scan_spread = {"launches": st.launches, "mean_ms": scan_ms, "std_ms": scan_std, "min_ms": st.pss_kernel_ms_min,
+                   "max_ms": st.pss_kernel_ms_max, "std_over_mean": scan_std / scan_ms if scan_ms > 0 else 0.0}
 
     # ---- the masks-producing instantiation (what a report needs for each FAIL cell's PSS
     # checks) and a cold step (per-corpus prologue re-run: dictionary predicate pass + prologue
@@ -450,7 +454,7 @@ def main(argv=None):
                      "frac": scan_achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": scan_kernel,
                      "kernel_ms": scan_ms, "alg_bytes_per_launch": acct["alg_bytes_per_launch"],
-                     "dict_kernel_ms": dict_ms,
+                     "kernel_spread": scan_spread, "dict_kernel_ms": dict_ms,
                      "pattern_kernel_ms": pat_ms,
                      # the same bytes over the timed region's step time (launches of different
                      # shards overlap on two streams there) and the isolated single-stream step
@@ -480,6 +484,7 @@ def main(argv=None):
                          "frac": pat_achieved / HBM_PEAK_GBS, "traffic": pat_traffic, "kernel": "kpe_pattern_kernel",
                          "kernel_ms": pat_ms, "alg_bytes_per_launch": pat_sum / L,
                          "scan_kernel": {"kernel_ms": scan_ms, "alg_bytes_per_launch": acct["alg_bytes_per_launch"],
+                                         "kernel_spread": scan_spread,
                                          "frac": scan_achieved / HBM_PEAK_GBS},
                          "single_stream_step_ms": single_stream_ms}
         # end-to-end ingestion of shard 0's NDJSON again (generated untimed, nothing else running):

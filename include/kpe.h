@@ -398,6 +398,8 @@ typedef struct kpe_kernel_stats {
                                summed (multi-shard launches differ in size: the mean launch carries
                                scan_bytes_sum / launches, not the last launch's scan_bytes) */
   double pattern_bytes_sum; /* the same for the pattern kernel's algorithmic bytes */
+  double pss_kernel_ms_min, pss_kernel_ms_max, pss_kernel_ms_sq;  /* the scan launches' shortest and
+                               longest duration and the sum of squared durations (spread) */
 } kpe_kernel_stats;
 kpe_status kpe_device_set_timing(kpe_device* dev, int enabled);
 kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program* prog, const kpe_corpus* c,

@@ -28,7 +28,9 @@ class KernelStats(ctypes.Structure):
                 ("dict_kernel_ms", ctypes.c_double), ("scan_bytes", ctypes.c_double),
                 ("pattern_kernel_ms", ctypes.c_double), ("pattern_bytes", ctypes.c_double),
                 ("scan_kernel", ctypes.c_int32), ("pad_", ctypes.c_int32),
-                ("scan_bytes_sum", ctypes.c_double), ("pattern_bytes_sum", ctypes.c_double)]
+                ("scan_bytes_sum", ctypes.c_double), ("pattern_bytes_sum", ctypes.c_double),
+                ("pss_kernel_ms_min", ctypes.c_double), ("pss_kernel_ms_max", ctypes.c_double),
+                ("pss_kernel_ms_sq", ctypes.c_double)]
 
 
 def lib_path():

@@ -502,7 +502,21 @@ struct LabCache {
   uint32_t lo, hi;    // the resource's labels
   uint32_t nlo, nhi;  // its namespace's labels (namespaceSelector), read from memory
   uint64_t selq, nsq;  // ScanArgs::selm: requirements that hold on its labels / its namespace's
+  uint64_t kmask;      // T_KSLOT: the kind terms that hold for its GVK
 };
+// The row's kind-term mask: binary search of its GVK in the block's LDS table (ScanArgs::kslot_lds)
+__device__ __forceinline__ uint64_t kslot_mask(const CArgs& a, const uint32_t* dyn, uint32_t gvk) {
+  const LdsPtr g = (LdsPtr)(dyn + a.kslot_lds);
+  uint32_t lo = 0, n = a.nkslot_g;
+  while (n > 1u) {  // uniform trip count
+    const uint32_t h = n >> 1;
+    lo = g[lo + h] <= gvk ? lo + h : lo;
+    n -= h;
+  }
+  if (g[lo] != gvk) return 0ull;
+  const uint32_t m = (a.nkslot_g + 1u) & ~1u;
+  return (uint64_t)g[m + 2u * lo] | (uint64_t)g[m + 2u * lo + 1u] << 32;
+}
 
 // the resource's label cache (label selectors; a namespace's labels are shared by its
 // resources and stay cache-resident, so namespaceSelector terms read them from memory)
@@ -557,6 +571,7 @@ __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabC
   LC.lo = lo, LC.hi = hi;
   LC.nlo = LC.nhi = 0;
   LC.selq = LC.nsq = 0;
+  LC.kmask = 0;
   if (a.need & NEED_NSL) {  // the namespace row's bounds, once per resource instead of per term
     const uint32_t row = a.r_nsl[rc];
     if (live && row != KPE_NO_STR) LC.nlo = a.nsl_off[row], LC.nhi = a.nsl_off[row + 1];
@@ -574,7 +589,9 @@ __device__ __forceinline__ bool eval_term(CArgs& a, const Bits& B, const KpeTerm
                                           uint32_t nsa, uint32_t name_col, uint32_t mns_col, uint32_t rc,
                                           bool live, const LabCache& LC) {
   bool ok = true;
-  if (tm.type == T_SELQ || tm.type == T_NSSELQ) {  // requirement-mask selectors (binding form)
+  if (tm.type == T_KSLOT) {
+    ok = (LC.kmask >> tm.a) & 1ull;
+  } else if (tm.type == T_SELQ || tm.type == T_NSSELQ) {  // requirement-mask selectors (binding form)
     const uint32_t q = tm.a & 0xFFu, nq = (tm.a >> 8) & 0xFFu, f = tm.a >> 16;
     const uint64_t need = (nq >= 64u ? ~0ull : ((1ull << nq) - 1ull)) << q;
     if (tm.type == T_SELQ) {
@@ -673,6 +690,14 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
 #pragma unroll 1
     for (uint32_t i = lane; i < nw; i += 64) dst[i] = src[i];
     if (lane < (nb & 3u)) base[(nw << 2) + lane] = sv[(nw << 2) + lane];
+  } else if (((R | c0 | nc) & 3u) == 0u) {  // dword-aligned row segments: nc / 4 dwords per row
+    const uint32_t nw = nc >> 2, tot = nrows * nw;
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(sv);
+#pragma clang loop vectorize(disable) unroll(disable)
+    for (uint32_t i = lane; i < tot; i += 64) {
+      const uint32_t row = i / nw, w = i - row * nw;
+      *reinterpret_cast<uint32_t*>(base + (size_t)row * R + 4u * w) = src[i];
+    }
   } else {
 #pragma clang loop vectorize(disable) unroll(disable)
     for (uint32_t i = lane; i < nrows * nc; i += 64) {
@@ -773,6 +798,11 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     if (fused) {
 #pragma unroll 1
       for (uint32_t i = t; i < a.blob_words; i += kBlock) dyn[i] = 0;
+    }
+    if (a.kslot_lds != PRED_NONE) {  // the GVK kind-term table
+      const uint32_t nw = ((a.nkslot_g + 1u) & ~1u) * 3u;
+#pragma unroll 1
+      for (uint32_t i = t; i < nw; i += kBlock) dyn[a.kslot_lds + i] = a.kslot_tab[i];
     }
     if (a.selt_lds != PRED_NONE) {  // label-selector requirement tables (sel_km, then sel_vm)
       uint4* d = reinterpret_cast<uint4*>(dyn + a.selt_lds);
@@ -932,6 +962,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       if constexpr (!LEAN) {
         LabCache LC;
         lab_cache(a, rc, live, LC, dyn);
+        if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #pragma unroll 1
         for (uint32_t ti = 0; ti < a.nterms; ++ti) {
           const KpeTerm tm{hw(tm_type, ti), hw(tm_a, ti), hw(tm_b, ti), 0u};
@@ -1023,6 +1054,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
     LabCache LC;
     lab_cache(a, rc, live, LC, dyn);
+        if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #if KPE_DIAG & 2  // diagnostic build: no term evaluation
     if (lane < a.nterms) tmk[lane] = LC.selq ^ gvk ^ nsa;
 #else

@@ -177,6 +177,10 @@ struct ScanArgs {
   // sel_km then sel_vm staged in each scan block's LDS at this word offset (the label fold then
   // reads LDS, not L2), or PRED_NONE
   uint32_t selt_lds, selt_pad;
+  // kind terms (T_KSLOT): LDS word offset of the corpus's distinct GVKs (ascending, nkslot_g of
+  // them, padded to an even count) followed by each one's 64-bit kind-term mask; PRED_NONE: none
+  uint32_t kslot_lds, nkslot_g;
+  const uint32_t* kslot_tab;  // the table in HBM (copied by every scan block)
   uint64_t sm_pos, sm_wild, sm_notin, sm_exists, sm_dne;
   // outputs
   uint8_t* verdicts;  // n x nrules

@@ -144,6 +144,7 @@ struct kpe_device {
   std::vector<hipEvent_t> pool;
   uint64_t launches = 0;
   double pss_ms = 0, dict_ms = 0, pat_ms = 0, last_bytes = 0, last_pbytes = 0, sum_bytes = 0, sum_pbytes = 0;
+  double pss_min = 0, pss_max = 0, pss_sq = 0;  // spread of the scan launches' durations
   int last_kind = 0;
   // knobs, read once at kpe_device_open: KPE_NO_BIND_CACHE (recompute per-binding products every
   // evaluation), KPE_PATVM_ERR (report a KPE_PATVM_CHECK build's bounds flags), KPE_LEAN6_MINW /
@@ -242,6 +243,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   uint32_t pp[10] = {};  // fixed PSS predicate locations
   uint32_t wave_lds = 0, wave_words = 0, filt_lds = PRED_NONE, fterm_lds = 0, tt_lds = PRED_NONE;
   uint32_t selt_lds = PRED_NONE;  // ScanArgs::selt_lds
+  uint32_t kslot_lds = PRED_NONE, nkslot_g = 0;  // ScanArgs::kslot_lds / nkslot_g
+  DevBuf kslot_tab;
   size_t dyn_bytes = 0;
   uint32_t nblocks = 0, njobs = 0, blob_words = 0, scan_blocks = 0;
   uint32_t need = 0;
@@ -960,6 +963,74 @@ double psum_bytes(const kpe::Corpus& C, const kpe::DeviceCorpus& D, uint32_t nee
   return lean_bytes(C, D, need, 0, false) - 4.0 * (double)D.bind.nkinds + 12.0 * (double)C.n;
 }
 
+// Kind terms (T_KINDS, T_KIND_PRED) of a wide-path program as one table over the corpus's
+// distinct GVKs: per GVK, bit s of its mask = kind term slot_of^-1(s) holds (CheckKind over the
+// group / version / kind strings with the same go-wildcard predicates the device evaluates). The
+// scan then looks the row's mask up once instead of evaluating each kind term from its selector
+// records. Only for <= 64 kind terms and <= 64 distinct GVKs; tab = [GVKs ascending, padded to
+// an even count][masks, 2 words each].
+static void kind_table(const kpe::Program& P, const kpe::Corpus& C, std::vector<uint32_t>& tab,
+                       std::vector<int32_t>& slot_of, uint32_t* ng) {
+  std::vector<uint32_t> kt;
+  for (size_t t = 0; t < P.terms.size(); ++t)
+    if (P.terms[t].type == T_KINDS || P.terms[t].type == T_KIND_PRED) kt.push_back((uint32_t)t);
+  if (kt.empty() || kt.size() > 64) return;
+  auto plain = [&](int32_t p) { return p < 0 || (p < (int32_t)P.preds.size() && P.preds[p].special == PRED_SPECIAL_NONE); };
+  for (uint32_t t : kt) {
+    const KpeTerm& tm = P.terms[t];
+    if (tm.type == T_KIND_PRED && !plain((int32_t)tm.a)) return;
+    if (tm.type == T_KINDS)
+      for (uint32_t k = 0; k < tm.b; ++k) {
+        const KpeKindSel& ks = P.kindsels[tm.a + k];
+        if (!plain(ks.pg) || !plain(ks.pv) || !plain(ks.pk)) return;
+      }
+  }
+  std::vector<uint32_t> G;
+  uint32_t last = 0xFFFFFFFFu;
+  for (uint32_t g : C.r_gvk) {
+    if (g == last) continue;
+    last = g;
+    if (std::find(G.begin(), G.end(), g) == G.end()) {
+      G.push_back(g);
+      if (G.size() > 64) return;
+    }
+  }
+  if (G.empty()) return;
+  std::sort(G.begin(), G.end());
+  auto pred = [&](int32_t p, std::string_view s) {
+    if (p < 0) return true;
+    for (auto& g : P.preds[p].globs)
+      if (kpe::go_wildcard(g, std::string(s))) return true;
+    return false;
+  };
+  const uint32_t m = ((uint32_t)G.size() + 1u) & ~1u;
+  tab.assign(m * 3u, 0u);
+  for (size_t i = 0; i < G.size(); ++i) {
+    const uint32_t g = G[i];
+    tab[i] = g;
+    const std::string_view kind = C.dict[D_KIND].at(GVK_KIND(g)), ver = C.dict[D_VERSION].at(GVK_VER(g)),
+                           grp = C.dict[D_GROUP].at(GVK_GRP(g));
+    uint64_t mask = 0;
+    for (size_t s = 0; s < kt.size(); ++s) {
+      const KpeTerm& tm = P.terms[kt[s]];
+      bool ok = false;
+      if (tm.type == T_KIND_PRED) {
+        ok = pred((int32_t)tm.a, kind);
+      } else {
+        for (uint32_t k = 0; k < tm.b && !ok; ++k) {
+          const KpeKindSel& ks = P.kindsels[tm.a + k];
+          ok = ks.sub_ok && pred(ks.pg, grp) && pred(ks.pv, ver) && pred(ks.pk, kind);
+        }
+      }
+      if (ok) mask |= 1ull << s;
+    }
+    tab[m + 2 * i] = (uint32_t)mask, tab[m + 2 * i + 1] = (uint32_t)(mask >> 32);
+  }
+  for (uint32_t i = (uint32_t)G.size(); i < m; ++i) tab[i] = 0xFFFFFFFFu;
+  for (size_t s = 0; s < kt.size(); ++s) slot_of[kt[s]] = (int32_t)s;
+  *ng = (uint32_t)G.size();
+}
+
 kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool want_masks) {
   auto& P = *pp->p;
   auto& C = *cc->c;
@@ -993,6 +1064,15 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
     return e && atoi(e) == 0;
   }();
   const uint32_t selt_words = sel_lbl && !selt_off && selt_need <= kMaxSelLds ? (uint32_t)selt_need : 0u;
+  static const bool kslot_off = [] {
+    const char* e = getenv("KPE_KSLOT");
+    return e && atoi(e) == 0;
+  }();
+  std::vector<uint32_t> kslot_tab;
+  std::vector<int32_t> kslot_of(P.terms.size(), -1);
+  uint32_t kslot_ng = 0;
+  if (!narrow && !kslot_off) kind_table(P, C, kslot_tab, kslot_of, &kslot_ng);
+  const uint32_t kslot_words = (uint32_t)kslot_tab.size();
   // LEAN scan candidate: prepped, NARROW truth-table program of kind-only terms (a kind table
   // replaces the per-resource term loop); confirmed below once predicate placement is known
   bool lean = narrow && PD.tt && P.any_pss &&
@@ -1003,6 +1083,7 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const uint32_t capb_words = P.any_pss ? ((uint32_t)C.capset_add.size() + 15) / 16 * 4 : 0u;  // 1 byte per set
   const int64_t budget =
       (int64_t)kMaxDynWords - 4 * (int64_t)wave_words - (stage_prog ? prog_words : 0) - 8 - selt_words - 4 -
+      kslot_words - 2 -
       (PD.tt ? (1 << KPE_TT_TERMS) : 0) - kt_words - capb_words;
   if (budget < 0) return fail(KPE_E_LIMIT, "program does not fit the scan kernel's LDS budget");
   const uint32_t local_budget = (uint32_t)std::min<int64_t>(kMaxLocalWords, budget);
@@ -1050,7 +1131,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   const uint32_t img_end = capb_at + capb_words;
   const uint32_t prog_at = img_end;
   const uint32_t selt_at = (prog_at + (stage_prog ? prog_words : 0) + 3) & ~3u;
-  const uint32_t wave_at = (selt_at + selt_words + 1) & ~1u;
+  const uint32_t kslot_at = (selt_at + selt_words + 1) & ~1u;
+  const uint32_t wave_at = (kslot_at + kslot_words + 1) & ~1u;
   const uint32_t scan_end = wave_at + 4 * wave_words;
   const uint32_t fuse_at = (scan_end + 3) & ~3u;
   std::vector<uint32_t> dir(npreds);
@@ -1181,6 +1263,8 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
       t.type = ns ? T_NSSELQ : T_SELQ;
     }
   }
+  for (size_t t = 0; t < terms.size(); ++t)  // kind terms answered by the GVK table (kind_table)
+    if (kslot_words && kslot_of[t] >= 0) terms[t] = KpeTerm{T_KSLOT, (uint32_t)kslot_of[t], 0u, 0u};
   HIPCHK(upload(B.terms_r, terms, s));
   HIPCHK(upload(B.kindsels_r, kindsels, s));
   HIPCHK(upload(B.annpairs_r, annpairs, s));
@@ -1302,6 +1386,9 @@ kpe_status ensure_binding(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc
   B.fterm_lds = prog_at + 2 * (uint32_t)P.filters.size();
   B.wave_lds = wave_at;
   B.selt_lds = selt_words ? selt_at : PRED_NONE;
+  B.kslot_lds = kslot_words ? kslot_at : PRED_NONE;
+  B.nkslot_g = kslot_ng;
+  if (kslot_words) HIPCHK(upload(B.kslot_tab, kslot_tab, s));
   B.wave_words = wave_words;
   B.prep_dyn_bytes = (size_t)(fuse_at + fuse_words) * 4;
   B.pimg_words = img_end;  // prologue image: LDS [0, img_end)
@@ -1491,6 +1578,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   sa.psum = psum_go ? D.psum.as<uint32_t>() : nullptr;
   sa.selm = B.selm;
   sa.selt_lds = PRED_NONE;
+  sa.kslot_lds = B.kslot_lds, sa.nkslot_g = B.nkslot_g;
+  sa.kslot_tab = B.kslot_lds != PRED_NONE ? B.kslot_tab.as<uint32_t>() : nullptr;
   if (B.selm) {
     sa.sel_km = B.sel_km.as<uint4>(), sa.sel_vm = B.sel_vm.as<uint4>(), sa.ns_q = B.sel_nsq.as<uint64_t>();
     sa.ns_none = (uint32_t)C.nsl_off.size() - 1;
@@ -2662,6 +2751,9 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
     HIPCHK(hipEventElapsedTime(&d3, p.c, p.d));
     dev->dict_ms += p.pre ? d1 : 0.0f;  // an empty event interval is not a kernel (kpe.h)
     dev->pss_ms += d2;
+    dev->pss_min = dev->launches == 0 ? d2 : std::min(dev->pss_min, (double)d2);
+    dev->pss_max = dev->launches == 0 ? d2 : std::max(dev->pss_max, (double)d2);
+    dev->pss_sq += (double)d2 * d2;
     dev->pat_ms += p.post ? d3 : 0.0f;
     dev->last_bytes = p.bytes;
     dev->last_pbytes = p.pbytes;
@@ -2684,10 +2776,12 @@ kpe_status kpe_device_kernel_stats(kpe_device* dev, const kpe_program*, const kp
   out->scan_kernel = dev->last_kind;
   out->pad_ = 0;
   out->scan_bytes_sum = dev->sum_bytes;
+  out->pss_kernel_ms_min = dev->pss_min, out->pss_kernel_ms_max = dev->pss_max, out->pss_kernel_ms_sq = dev->pss_sq;
   out->pattern_bytes_sum = dev->sum_pbytes;
   if (reset) {
     dev->launches = 0;
     dev->pss_ms = dev->dict_ms = dev->pat_ms = dev->sum_bytes = dev->sum_pbytes = 0;
+    dev->pss_min = dev->pss_max = dev->pss_sq = 0;
   }
   return KPE_OK;
 }

@@ -341,7 +341,10 @@ enum KpeTermType {
   // D_KIND ids of "Namespace" | "" << 16 (0xFFFF: not in the corpus). One mask compare per lane,
   // no selector record load in the tile loop.
   T_SELQ = 7,
-  T_NSSELQ = 8
+  T_NSSELQ = 8,
+  // binding-time form of T_KINDS / T_KIND_PRED on the wide path: bit a of the row's kind-term
+  // mask, looked up once per row in a table over the corpus's distinct GVKs (ScanArgs::kslot_lds)
+  T_KSLOT = 9
 };
 #define TSQ_EXC 1u      // KpeSelector::exc
 #define TSQ_STAR 2u     // KpeSelector::star_kind
