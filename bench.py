@@ -127,38 +127,6 @@ def spawn_check():
         dist.destroy_process_group()
 
 
-def e2e_pipelined(K, eng, ps, nd, nsl, docs, chunks=8):
-    """Ingestion pipelined over `chunks` row ranges of one shard's NDJSON: chunk k+1 is flattened
-    (the flattener's own threads, on a worker thread: ctypes releases the GIL) while chunk k is
-    uploaded and its evaluation enqueued; wall clock from the first flatten to the last
-    evaluation's completion. Each chunk is a corpus of its own (its own dictionaries), as a
-    scanner streaming its resources in batches would build them."""
-    from concurrent.futures import ThreadPoolExecutor
-
-    cuts, n = [0], len(nd)
-    for k in range(1, chunks):
-        p = nd.find(b"\n", max(cuts[-1], n * k // chunks))
-        cuts.append(n if p < 0 else p + 1)
-    cuts.append(n)
-    parts = [nd[cuts[k]:cuts[k + 1]] for k in range(chunks) if cuts[k + 1] > cuts[k]]
-    live, rows = [], 0
-    t0 = time.perf_counter()
-    with ThreadPoolExecutor(max_workers=1) as ex:
-        fut = ex.submit(K.Corpus, parts[0], namespace_labels=nsl, docs=docs)
-        for k in range(len(parts)):
-            c = fut.result()
-            if k + 1 < len(parts):
-                fut = ex.submit(K.Corpus, parts[k + 1], namespace_labels=nsl, docs=docs)
-            c.upload(eng.device)
-            eng.evaluate_async(ps, c)
-            live.append(c)
-            rows += c.n
-    eng.device.sync()
-    dt = time.perf_counter() - t0
-    return {"e2e_evals_per_s": rows * ps.num_rules / dt, "wall_s": dt, "chunks": len(parts), "rows": rows,
-            "note": "flatten of chunk k+1 overlapped with H2D and evaluation of chunk k; not in value"}
-
-
 def launch_ranks(world, argv):
     """`--gpus N` without an external launcher: N rank processes on this node, one per GPU, started
     with the spawn method before this process makes any GPU call (a child process each, never an
@@ -501,12 +469,6 @@ def main(argv=None):
         del c0
         e2e_flat, e2e_up, t_eval1 = t1 - t0, t2 - t1, t3 - t2
         e2e_s = t3 - t0
-        pipe = None
-        if cfg == "c2":  # (its chunks' launches would enter the pattern configs' kernel statistics)
-            try:
-                pipe = e2e_pipelined(K, eng, ps, nd0, nsl, docs)
-            except Exception as ex:  # a report field: never fails the bench line
-                pipe = {"error": str(ex)[:200]}
         del nd0
         line = {
             "metric": "resource-rule evals/sec, 1M Pods × PSS restricted, 1/8 GPU; % HBM BW",
@@ -541,7 +503,10 @@ def main(argv=None):
                     "upload_s": e2e_up, "first_eval_s": t_eval1,
                     "setup_flatten_s": t_flatten / replicas, "setup_upload_s": t_upload / replicas,
                     "note": "one shard, after the timed region: host flatten (NDJSON -> columns) + H2D + one evaluation (a new binding), not in value; setup_*: the setup's per-shard means (NDJSON generation ran beside them)",
-                    "pipelined": pipe},
+                    # (round 6: the 8-chunk pipelined leg is gone: with the upload and the
+                    # evaluation at ~6 ms of a ~0.25 s shard there is nothing for the flatten to hide
+                    # behind, and it measured the same as this serial leg, profiles/r06_d)
+                    },
         }
         print(json.dumps(line))
     if world > 1:

@@ -549,17 +549,30 @@ __device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC, const
     notyet &= ~f;
   };
   uint32_t k[kLabCache], v[kLabCache];  // the first labels with independent loads
+#if KPE_DIAG & 16  // diagnostic build: the fold without the label loads
+#pragma unroll
+  for (uint32_t j = 0; j < kLabCache; ++j) k[j] = (LC.lo + j) % 37u, v[j] = (LC.hi ^ j) % 11u;
+#else
 #pragma unroll
   for (uint32_t j = 0; j < kLabCache; ++j) {
     const bool in = LC.lo + j < LC.hi;
     k[j] = in ? a.lab_k[LC.lo + j] : KPE_NO_STR;
     v[j] = in ? a.lab_v[LC.lo + j] : KPE_NO_STR;
   }
+#endif
+#if KPE_DIAG & 8  // diagnostic build: the label loads without the fold
+  uint64_t acc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kLabCache; ++j) acc ^= (uint64_t)k[j] << (j & 31u) ^ v[j];
+#pragma unroll 1
+  for (uint32_t j = LC.lo + kLabCache; j < LC.hi; ++j) acc ^= (uint64_t)a.lab_k[j] << 3 ^ a.lab_v[j];
+  return acc;
+#endif
 #pragma unroll
   for (uint32_t j = 0; j < kLabCache; ++j)
     if (LC.lo + j < LC.hi) fold(k[j], v[j]);
 #pragma unroll 1
-  for (uint32_t j = LC.lo + kLabCache; j < LC.hi; ++j) fold(a.lab_k[j], a.lab_v[j]);
+  for (uint32_t j = LC.lo + kLabCache; j < LC.hi; ++j) fold(KPE_DIAG & 16 ? j % 37u : a.lab_k[j], KPE_DIAG & 16 ? j % 11u : a.lab_v[j]);
   const uint64_t found = ~notyet;
   return (found & okacc & (a.sm_pos | a.sm_wild)) | ((notyet | okacc) & a.sm_notin) | (found & a.sm_exists) |
          (notyet & a.sm_dne);
