@@ -1257,6 +1257,24 @@ __device__ __forceinline__ uint32_t pv_store(CondVM& vm, CV x, uint32_t flags, u
   return 0u;
 }
 
+// A substituted key equal to another substituted key of its map (PVF_GROUP: the map's keys with
+// variables, resolved in slot order): jsonutils/traverse.go:104-114 renames them in Go's random
+// map order, so which value the shared key keeps is not defined (the cell is undecided)
+__device__ __forceinline__ bool pv_key_collides(const CondArgs& a, const uint2* pvrow, uint32_t k0, uint32_t k) {
+  const uint32_t g = PVF_GROUP(a.pvars[k].flags);
+  auto view = [&](uint2 x) {
+    const KpeScalar* s = x.x == PVK_SCAL ? a.scal + x.y : a.ctab + x.y;
+    return SView{(x.x == PVK_SCAL ? a.scal_text : a.ctext) + s->text_off, (int)s->text_len};
+  };
+  const SView v = view(pvrow[k]);
+  for (uint32_t j = k0; j < k; ++j)
+    if (PVF_GROUP(a.pvars[j].flags) == g) {
+      const SView w = view(pvrow[j]);
+      if (w.n == v.n && bytes_eq(w.s, v.s, v.n)) return true;
+    }
+  return false;
+}
+
 template <bool FEPAT>
 __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16], uint8_t* tx) {
   const uint64_t im = a.img_off ? a.img_off[r] : ~0ull;
@@ -1283,7 +1301,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
     FeFrame fr[KPE_FE_DEPTH];
     vm.dep = -1;
     uint32_t ev = 0;            // the current element's verdict (PH_FE_RES) / a level's result (PH_FE_POP)
-    uint32_t pk = 0, pend = 0;  // pattern variable slots being resolved
+    uint32_t pk = 0, pk0 = 0, pend = 0;  // pattern variable slots being resolved
     // a foreach element whose verdict may decide the cell (FAIL / ERROR): its path, what decided
     // it and its tape entries (schema.h FT_*); a later candidate replaces it, and the one that
     // propagates to the cell is always the last
@@ -1309,7 +1327,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
           fr[0].f = cr.fe0, fr[0].fend = cr.fe0 + cr.nfe, fr[0].applied = 0, fr[0].scoped = kNoNode;
           ph = PH_FE_LIST;
         } else if (cr.npv) {
-          pk = cr.pv0, pend = cr.pv0 + cr.npv;
+          pk = pk0 = cr.pv0, pend = cr.pv0 + cr.npv;
           ph = PH_PV;
         } else {
           if (cr.kind == CR_NONE) v = KPE_NA_;  // no handler: no response
@@ -1358,6 +1376,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         }
         if (ph == PH_PV) {
           uint32_t bad = st != CS_OK ? (uint32_t)KPE_ERROR_ : pv_store(vm, res, a.pvars[pk].flags, pvrow + pk);
+          if (!bad && PVF_GROUP(a.pvars[pk].flags) && pv_key_collides(a, pvrow, pk0, pk)) bad = KPE_UNDECIDED_;
           ++pk;
           if (bad == KPE_UNDECIDED_) {
             v = KPE_UNDECIDED_;
@@ -1422,7 +1441,7 @@ __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char
         if (F.fe.kind == FE_DENY) {
           ph = PH_FE_DENY;
         } else if (F.fe.kind == FE_PAT && FEPAT) {
-          pk = F.fe.c & 0xFFFFu, pend = pk + (F.fe.c >> 16);
+          pk = pk0 = F.fe.c & 0xFFFFu, pend = pk + (F.fe.c >> 16);
           ph = PH_PV;
         } else if (F.fe.kind == FE_NEST && vm.dep + 1 < KPE_FE_DEPTH) {
           FeFrame& G = fr[vm.dep + 1];

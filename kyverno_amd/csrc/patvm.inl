@@ -324,7 +324,11 @@ __device__ __forceinline__ uint32_t pat_lookup_vkey(const PatArgs& a, DocView do
       return kNoNode;
     }
   }
-  if (L.bval) {  // ExpandInMetadata target: a substituted glob would be expanded
+  if (ORDER && (L.bval & 2u)) {  // the map has other keys with variables: their walk order is not kept
+    *und = 1u;
+    return kNoNode;
+  }
+  if (L.bval & 1u) {  // ExpandInMetadata target: a substituted glob would be expanded
     for (int i = 0; i < n; ++i) {
       const uint8_t c = tp_at(pc, np, i);
       if (c == '*' || c == '?') {

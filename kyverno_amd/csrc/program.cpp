@@ -835,7 +835,7 @@ class PatCompiler {
           }
     const bool expanding = expand_.count(&v) > 0;
     std::vector<std::string> first, front, back;
-    std::string vkey;  // the map's one key with variables, if any
+    std::vector<std::string> vkeys;  // the map's keys with variables
     for (auto& kv : v.o) {
       const Anc a = anchor_of(kv.first);
       if (kv.first.find("$(") != std::string::npos)
@@ -843,10 +843,9 @@ class PatCompiler {
       if (kv.first.find("{{") != std::string::npos) {
         if (!key_leaf) throw CompileError("variables in pattern keys are not supported here");
         if (a.k != AK_NONE) throw CompileError("anchored pattern keys with variables are not supported");
-        if (!vkey.empty()) throw CompileError("more than one pattern key with variables in one map");
         if (expanding && has_glob(kv.first)) throw CompileError("wildcard metadata keys with variables");
         if (expanding && repeated) throw CompileError("metadata keys with variables under an array pattern");
-        vkey = kv.first;
+        vkeys.push_back(kv.first);
       }
       if (expanding && has_glob(kv.first) && repeated)  // the reference rewrites the shared pattern per element
         throw CompileError("wildcard metadata keys under an array pattern are not supported");
@@ -869,6 +868,18 @@ class PatCompiler {
         }
       }
     }
+    // several keys with variables in one map: each must be one whole-string variable, whose
+    // substituted value kpe_cond_kernel compares with the map's other substituted keys (a rename
+    // of one onto another, traverse.go:108-114, depends on Go's map order: the cell is undecided)
+    if (vkeys.size() > 1)
+      for (auto& k : vkeys) {
+        const bool whole = k.size() >= 4 && k.compare(0, 2, "{{") == 0 && k.find("{{", 2) == std::string::npos &&
+                           k.find("}}") == k.size() - 2;
+        if (!whole)
+          throw CompileError("several pattern keys with variables in one map, one of them a partial string");
+      }
+    const uint32_t vgroup = vkeys.size() > 1 ? ++PP.vkey_groups : 0u;
+    auto is_vkey = [&](const std::string& k) { return std::find(vkeys.begin(), vkeys.end(), k) != vkeys.end(); };
     std::sort(first.begin(), first.end());
     std::vector<std::string> rest;
     for (auto& kv : v.o)
@@ -876,7 +887,7 @@ class PatCompiler {
     // a key with variables takes the place of its text before the first variable (any place is
     // correct: the device checks per row that the substituted key sorts between the same
     // neighbours, else the cell is undecided)
-    auto sort_text = [&](const std::string& k) { return k == vkey ? k.substr(0, k.find("{{")) : k; };
+    auto sort_text = [&](const std::string& k) { return is_vkey(k) ? k.substr(0, k.find("{{")) : k; };
     std::sort(rest.begin(), rest.end(),
               [&](const std::string& x, const std::string& y) { return sort_text(x) < sort_text(y); });
     for (auto& k : rest) {
@@ -909,7 +920,7 @@ class PatCompiler {
         else flags |= PMF_XSLOT;
       }
       if (h == PM_DEFAULT && val.t == JV::Str && val.s == "*") flags |= PMF_STAR;
-      if (k == vkey) {
+      if (is_vkey(k)) {
         // validateMap walks the plain keys without nested anchors in sorted order and returns the
         // first error; such members can only fail plainly, so the verdict does not depend on where
         // the substituted key sorts (only the failure path of a message does: checked per row by
@@ -918,6 +929,10 @@ class PatCompiler {
         KpeLeaf kl{};
         if (!key_leaf(k, kl)) throw CompileError("pattern key template");
         kl.bval = expanding ? 1u : 0u;
+        if (vgroup) {  // bit 1: other keys of the map have variables too (their order is not tracked)
+          kl.bval |= 2u;
+          PP.vars[kl.c0].flags |= (vgroup & 0xFFFFFFu) << PVF_GROUP_SH;
+        }
         // the map's other plain keys in walk order, [u16 length][bytes] each, and this key's place
         kl.pad[0] = (uint32_t)PP.ttext.size();
         uint32_t nsib = 0, at = 0;

@@ -36,6 +36,7 @@ struct PatProgram {
   std::vector<KpePVar> vars;           // pattern variable slots (PL_VAR / PT_VAR)
   std::vector<uint32_t> tpieces;       // 2 words per template piece (PT_*)
   std::vector<uint8_t> ttext;          // template texts
+  uint32_t vkey_groups = 0;            // maps with several keys with variables (PVF_GROUP ids)
 };
 // Compiled preconditions / deny / foreach-deny programs (schema.h QO_* / KpeC*), evaluated per
 // resource by kpe_cond_kernel. Field names are kept as text: a binding resolves them to corpus

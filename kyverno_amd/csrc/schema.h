@@ -618,6 +618,8 @@ typedef struct KpePNode {
 #define PVF_TEXT 2u   // inside a template: numbers must print as json.Marshal does
 #define PVF_KEY 4u    // a whole-string variable naming a map key: a string (traverse.go:101-103:
                       // another type is an error; null keeps the key as written: undecided)
+#define PVF_GROUP_SH 8u       // bits 8..31: the map's key group when it has several keys with variables
+#define PVF_GROUP(f) ((f) >> PVF_GROUP_SH)  // (each one whole-string variable; 0: the only one)
 typedef struct KpePVar {
   uint32_t tmpl, flags;
 } KpePVar;

@@ -458,6 +458,12 @@ def var_policy_set():
         rule("vk-collide", {"pattern": {"metadata": {"labels": {"app": "?*", "{{request.object.metadata.labels.kind || 'app'}}": "x"}}}}),
         rule("vk-number", {"pattern": {"spec": {"{{request.object.spec.containers[0].ports[0].containerPort}}": "x"}}}),
         rule("vk-spec", {"pattern": {"spec": {"{{request.object.metadata.labels.field || 'containers'}}": [{"name": "c-*"}]}}}),
+        # several whole-string key variables in one map; equal substituted keys collide (undecided)
+        rule("vk-two", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.kind || 'team'}}": "team-?",
+                                                            "{{request.object.metadata.labels.zone || 'tier'}}": "back*",
+                                                            "app": "?*"}}}}),
+        rule("vk-two-collide", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.kind || 'x1'}}": "?*",
+                                                                    "{{request.object.metadata.labels.kind || 'x2'}}": "?*"}}}}),
         # foreach entries
         rule("fe-pat", {"foreach": [{"list": ctr, "pattern": {"securityContext": {"=(privileged)": False}}}]}),
         rule("fe-pat-var", {"foreach": [{"list": ctr, "pattern": {"name": "c-{{elementIndex}}"}}]}),
@@ -486,7 +492,7 @@ def var_policy_set():
 
 # rules of var_policy_set whose cells the device may leave KPE_UNDECIDED (a variable resolving
 # to a map is a pattern subtree; documented device limit)
-VAR_UNDECIDED_OK = {"v-map", "vk-collide"}  # vk-collide: a key renamed onto another key of the map
+VAR_UNDECIDED_OK = {"v-map", "vk-collide", "vk-two-collide"}  # vk-*collide: a key renamed onto another key
 
 
 def foreach_message_policy_set():

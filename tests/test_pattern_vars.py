@@ -52,7 +52,7 @@ def test_var_policy_set_compiles(oracle):
 
 @pytest.mark.parametrize("pattern", [
     {"metadata": {"labels": {"=({{request.object.metadata.name}})": "x"}}},  # a variable in an anchored key
-    {"metadata": {"labels": {"{{request.object.metadata.name}}": "x", "{{request.object.kind}}": "y"}}},  # two
+    {"metadata": {"labels": {"a-{{request.object.metadata.name}}": "x", "{{request.object.kind}}": "y"}}},  # two, one partial
     {"metadata": {"name": "$(./namespace)"}},                              # a reference
     {"metadata": {"name": "{{ @ }}"}},                                     # {{@}}
     {"metadata": {"name": "{{ to_upper(request.object.metadata.name) }}"}},  # a function
