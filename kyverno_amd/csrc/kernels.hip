@@ -266,6 +266,7 @@ struct Tile<true> {
 template <>
 struct Tile<false> {
   uint32_t gvk, nsa, name, mns;
+  uint32_t lo, hi;  // the resource's label bounds (lab_off), one step ahead of the label loads
 };
 
 // Tile header words: lane k (< 8) holds word k of hdr[tile], hdr[tile + 1]
@@ -288,7 +289,9 @@ __device__ __forceinline__ void pin_tile(Tile<true>& d) {
   pin(d.rec), pin(d.c0), pin(d.c1), pin(d.v0), pin(d.v1), pin(d.s0), pin(d.q0), pin(d.sa0), pin(d.sa1), pin(d.name),
       pin(d.mns);
 }
-__device__ __forceinline__ void pin_tile(Tile<false>& d) { pin(d.gvk), pin(d.nsa), pin(d.name), pin(d.mns); }
+__device__ __forceinline__ void pin_tile(Tile<false>& d) {
+  pin(d.gvk), pin(d.nsa), pin(d.name), pin(d.mns), pin(d.lo), pin(d.hi);
+}
 
 // Every load of a tile is issued on every path (an unneeded column is read from the
 // binding's zero page instead: one broadcast cache line), so the number of loads a
@@ -368,6 +371,10 @@ __device__ __forceinline__ Tile<false> load_match_tile(CArgs& a, uint32_t tile, 
   d.nsa = col<uint32_t>(on_a, a.r_nsa, zp)[on_a ? rc : 0u];
   d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
   d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+  const bool on_l = need & NEED_LAB;
+  const uint32_t* lo = col<uint32_t>(on_l, a.lab_off, zp) + (on_l ? rc : 0u);
+  d.lo = lo[0];
+  d.hi = lo[on_l ? 1u : 0u];
   return d;
 }
 
@@ -498,6 +505,7 @@ __device__ __forceinline__ uint32_t pss_tile(CArgs& a, const Bits& B, const uint
 // masks (ScanArgs::selm) once per tile: every selector term is then one mask test. Without masks
 // (more than 64 requirements in a space) a term walks the labels per requirement.
 constexpr uint32_t kLabCache = 8;
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));  // a dword-aligned 16-byte load
 struct LabCache {
   uint32_t lo, hi;    // the resource's labels
   uint32_t nlo, nhi;  // its namespace's labels (namespaceSelector), read from memory
@@ -553,11 +561,14 @@ __device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC, const
 #pragma unroll
   for (uint32_t j = 0; j < kLabCache; ++j) k[j] = (LC.lo + j) % 37u, v[j] = (LC.hi ^ j) % 11u;
 #else
+  // dword-aligned 16-byte loads: the label arrays carry 128 bytes of slack past their end
+  // (upload_staged), and words past the resource's labels are never folded
 #pragma unroll
-  for (uint32_t j = 0; j < kLabCache; ++j) {
-    const bool in = LC.lo + j < LC.hi;
-    k[j] = in ? a.lab_k[LC.lo + j] : KPE_NO_STR;
-    v[j] = in ? a.lab_v[LC.lo + j] : KPE_NO_STR;
+  for (uint32_t j = 0; j < kLabCache; j += 4u) {
+    const u32x4a kk = *reinterpret_cast<const u32x4a*>(a.lab_k + LC.lo + j);
+    const u32x4a vv = *reinterpret_cast<const u32x4a*>(a.lab_v + LC.lo + j);
+    k[j] = kk.x, k[j + 1] = kk.y, k[j + 2] = kk.z, k[j + 3] = kk.w;
+    v[j] = vv.x, v[j + 1] = vv.y, v[j + 2] = vv.z, v[j + 3] = vv.w;
   }
 #endif
 #if KPE_DIAG & 8  // diagnostic build: the label loads without the fold
@@ -578,10 +589,14 @@ __device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC, const
          (notyet & a.sm_dne);
 }
 
-__device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC, const uint32_t* dyn) {
-  uint32_t lo = 0, hi = 0;
-  if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = live ? a.lab_off[rc + 1] : lo;
-  LC.lo = lo, LC.hi = hi;
+// lo / hi: the resource's lab_off bounds when the tile prefetched them (Tile<false>), else ~0u
+__device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC, const uint32_t* dyn,
+                                          uint32_t lo = ~0u, uint32_t hi = 0u) {
+  if (lo == ~0u) {
+    lo = hi = 0;
+    if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = a.lab_off[rc + 1];
+  }
+  LC.lo = lo, LC.hi = live ? hi : lo;
   LC.nlo = LC.nhi = 0;
   LC.selq = LC.nsq = 0;
   LC.kmask = 0;
@@ -974,7 +989,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       uint32_t tb = 0;
       if constexpr (!LEAN) {
         LabCache LC;
-        lab_cache(a, rc, live, LC, dyn);
+        if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
+        else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi);
         if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #pragma unroll 1
         for (uint32_t ti = 0; ti < a.nterms; ++ti) {
@@ -1066,8 +1082,9 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
     LabCache LC;
-    lab_cache(a, rc, live, LC, dyn);
-        if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
+    if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
+    else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi);
+    if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #if KPE_DIAG & 2  // diagnostic build: no term evaluation
     if (lane < a.nterms) tmk[lane] = LC.selq ^ gvk ^ nsa;
 #else
