@@ -23,7 +23,8 @@ constexpr int kCvBufs = 6 + KPE_FE_DEPTH;  // key: 0,1 (+2 list template); value
                                            // lists: 6 + nesting level
 
 constexpr uint32_t VK_NULL = 0, VK_NODE = 1, VK_CONST = 2, VK_LIST = 3, VK_KEY = 4, VK_NUM = 5,
-                   VK_TXT = 6;  // a string built by substitution (VT_TMPL) in the lane's LDS text slot p
+                   VK_TXT = 6;  // a string built by substitution (VT_TMPL) in the lane's LDS text area:
+                                // p = byte offset | length << 8
 #ifndef KPE_TXT_CAP
 #define KPE_TXT_CAP 120  // bytes of one substituted string (key / value slot); longer: undecided
 #endif
@@ -55,7 +56,6 @@ struct CondVM {
                    // no generic pointer ever reaches the lane's private memory
   uint8_t* tx;       // 2 x KPE_TXT_CAP bytes of LDS: substituted key / value strings (VK_TXT), or
                      // null when the program has no partial-string variables
-  uint32_t tlen[2];
   uint32_t bt;  // where the last block() stopped: first true `any` | first false `all` << 7
 
   // ---- value access ----------------------------------------------------------------------
@@ -108,7 +108,7 @@ struct CondVM {
   }
   __device__ __forceinline__ SView str(CV v) const {  // a JT_STR value's text
     if (v.k == VK_KEY) return SView{a.key_bytes + a.key_off[v.p], (int)(a.key_off[v.p + 1] - a.key_off[v.p])};
-    if (v.k == VK_TXT) return SView{tx + v.p * KPE_TXT_CAP, (int)tlen[v.p]};
+    if (v.k == VK_TXT) return SView{tx + (v.p & 0xFFu), (int)(v.p >> 8)};
     const uint8_t* t;
     const KpeScalar* s = scalar(v, &t);
     return SView{t + s->text_off, (int)s->text_len};
@@ -429,12 +429,15 @@ struct CondVM {
   // every {{ }} replaced by its value (substituteVarInPattern :403-420: a string as is, anything
   // else json.Marshal-ed), into the lane's LDS text slot `slot`. Undecided: a substituted text
   // holding "{{" (vars.go substitutes again), a map / list value, a number whose json.Marshal text
-  // the device does not hold (an exponent, an integer past 2^53), a result past KPE_TXT_CAP.
-  __device__ __forceinline__ int substitute(const KpeVTmpl& t, uint32_t b0, uint32_t b1, uint32_t slot, CV* out) {
-    uint8_t* d = tx + slot * KPE_TXT_CAP;
+  // the device does not hold (an exponent, an integer past 2^53), a slot's strings past KPE_TXT_CAP
+  // bytes together (the list elements of one side share its slot: `base` bytes are taken).
+  static_assert(2 * KPE_TXT_CAP <= 256, "VK_TXT offsets are one byte");
+  __device__ __forceinline__ int substitute(const KpeVTmpl& t, uint32_t b0, uint32_t b1, uint32_t slot, uint32_t base,
+                                            CV* out) {
+    uint8_t* d = tx + slot * KPE_TXT_CAP + base;
     uint32_t len = 0;
     auto put = [&](const uint8_t* p, uint32_t n) -> bool {
-      if (len + n > (uint32_t)KPE_TXT_CAP) return false;
+      if (base + len + n > (uint32_t)KPE_TXT_CAP) return false;
       for (uint32_t i = 0; i < n; ++i) d[len + i] = p[i];
       len += n;
       return true;
@@ -489,29 +492,30 @@ struct CondVM {
         default: return CS_UNDEC;  // json.Marshal of a map / list
       }
     }
-    tlen[slot] = len;
-    *out = cv(VK_TXT, slot);
+    *out = cv(VK_TXT, (slot * KPE_TXT_CAP + base) | len << 8);
     return CS_OK;
   }
   // A condition key / value after substitution (template `ti`); lists go to buffer bl. One
   // query() call site: a single query is a one-element template walk that returns its value. A
-  // string with variables inside it (alone, or the one such element of a list: program.cpp
-  // CondCompiler::tmpl) is built in the side's lane text slot (key 0, value 1).
+  // string with variables inside it (alone, or elements of a list: program.cpp CondCompiler::tmpl)
+  // is built in the side's lane text slot (key 0, value 1), a list's elements one after another.
   __device__ __forceinline__ int value(uint32_t ti, uint32_t b0, uint32_t b1, uint32_t bl, CV* out) {
     const KpeVTmpl t = a.tmpls[ti];
     const uint32_t slot = b0 == 3u ? 1u : 0u;
-    if (t.kind == VT_TMPL) return substitute(t, b0, b1, slot, out);
+    if (t.kind == VT_TMPL) return substitute(t, b0, b1, slot, 0u, out);
     const bool arr = t.kind == VT_ARRAY;
     const uint32_t n = arr ? t.b : 1u;
     blen[bl] = 0;
-    for (uint32_t k = 0; k < n; ++k) {  // list elements: constants, queries or one template
+    uint32_t fill = 0;                  // bytes of the slot taken by earlier template elements
+    for (uint32_t k = 0; k < n; ++k) {  // list elements: constants, queries or templates
       const KpeVTmpl te = arr ? a.tmpls[t.a + k] : t;
       CV x;
       if (te.kind == VT_CONST) {
         x = SC_TYPE(a.ctab[te.a].flags) == SC_T_NULL ? cv(VK_NULL, 0) : cv(VK_CONST, te.a);
       } else if (te.kind == VT_TMPL) {
-        const int st = substitute(te, b0, b1, slot, &x);
+        const int st = substitute(te, b0, b1, slot, fill, &x);
         if (st != CS_OK) return st;
+        fill += x.p >> 8;
       } else {
         const int st = query(te.a, b0, b1, &x);
         if (st != CS_OK) return st;
@@ -1279,7 +1283,7 @@ template <bool FEPAT>
 __device__ __forceinline__ void cond_eval_row(const CondArgs& a, int64_t r, char (*nb)[16], uint8_t* tx) {
   const uint64_t im = a.img_off ? a.img_off[r] : ~0ull;
   CondVM vm{a, reinterpret_cast<const uint2*>(a.doc), (uint32_t)a.doc_off[r], im == ~0ull ? kNoNode : (uint32_t)im,
-            {}, {}, -1, {}, {}, nb, tx, {}, 0u};
+            {}, {}, -1, {}, {}, nb, tx, 0u};
   uint8_t* row = a.verdicts + (size_t)r * a.R;
   uint2* pvrow = a.pvals ? a.pvals + (size_t)r * a.nvars : nullptr;
   for (uint32_t i = 0; i < a.ncr; ++i) {

@@ -754,10 +754,40 @@ class Flattener {
   const PodView& view() const { return pod; }
 
   void add(const char* p, const char* e) {
+    // The class (typed decode target) needs the resource's last top-level "kind". When "kind"
+    // leads the object (after an optional "apiVersion"), the walk starts with its class and
+    // checks at the end that no later "kind" changed it (else it walks again); otherwise a
+    // pre-scan of the top-level members finds it first.
+    std::string kind;
+    if (!lead_kind(p, e, &kind)) kind = top_kind(p, e);
+    uint32_t cls = class_of(kind);
+    if (!walk(p, e, cls) && walk(p, e, class_of(u.kind))) throw std::logic_error("resource class changed twice");
+  }
+
+ private:
+  // the leading "kind" string member of the object (at most one "apiVersion" string before it)
+  static bool lead_kind(const char* p, const char* e, std::string* kind) {
+    JCur c(p, e);
+    if (!c.obj_begin()) return false;
+    bool f = true;
+    std::string_view k;
+    std::string ks, vs;
+    for (int i = 0; i < 2 && c.obj_next(f, &k, ks); ++i) {
+      if (c.peek() != JK::Str || (k != "kind" && k != "apiVersion")) return false;
+      std::string_view v;
+      if (!c.str(&v, vs)) return false;
+      if (k == "kind") {
+        kind->assign(v);
+        return true;
+      }
+    }
+    return false;
+  }
+  // one walk of the resource with class `cls`; false: the last top-level "kind" is of another
+  // class (nothing was emitted)
+  bool walk(const char* p, const char* e, uint32_t cls) {
     u.reset();
     pod.reset();
-    std::string kind = top_kind(p, e);
-    uint32_t cls = class_of(kind);
     JCur cur(p, e);
     Typed t(cur);
     bool typed = cls != R_CLASS_OTHER;
@@ -794,15 +824,16 @@ class Flattener {
       }
     }
     if (!cur.ok()) throw std::invalid_argument("malformed resource JSON");
+    if (class_of(u.kind) != cls) return false;
     if (no_emit) {
       last_cls = cls;
       last_err = typed && t.err;
-      return;
+      return true;
     }
     emit(cls, typed && t.err);
+    return true;
   }
 
- private:
   Corpus& C;
   UView u;
   PodView pod;
@@ -1592,8 +1623,8 @@ void flatten_range(Corpus& C, const char* buf, size_t i, size_t len, bool docs) 
   std::unique_ptr<DocBuilder> db;
   if (docs) db = std::make_unique<DocBuilder>(C), C.has_docs = true;
   while (i < len) {
-    size_t j = i;
-    while (j < len && buf[j] != '\n') ++j;
+    const void* nl = memchr(buf + i, '\n', len - i);
+    const size_t j = nl ? (size_t)(static_cast<const char*>(nl) - buf) : len;
     size_t a = i, b = j;
     while (a < b && (buf[a] == ' ' || buf[a] == '\t' || buf[a] == '\r')) ++a;
     while (b > a && (buf[b - 1] == ' ' || buf[b - 1] == '\t' || buf[b - 1] == '\r')) --b;

@@ -267,6 +267,7 @@ template <>
 struct Tile<false> {
   uint32_t gvk, nsa, name, mns;
   uint32_t lo, hi;  // the resource's label bounds (lab_off), one step ahead of the label loads
+  uint32_t nsl;     // its namespace's row in the namespace-label table (r_nsl)
 };
 
 // Tile header words: lane k (< 8) holds word k of hdr[tile], hdr[tile + 1]
@@ -290,7 +291,7 @@ __device__ __forceinline__ void pin_tile(Tile<true>& d) {
       pin(d.mns);
 }
 __device__ __forceinline__ void pin_tile(Tile<false>& d) {
-  pin(d.gvk), pin(d.nsa), pin(d.name), pin(d.mns), pin(d.lo), pin(d.hi);
+  pin(d.gvk), pin(d.nsa), pin(d.name), pin(d.mns), pin(d.lo), pin(d.hi), pin(d.nsl);
 }
 
 // Every load of a tile is issued on every path (an unneeded column is read from the
@@ -375,6 +376,8 @@ __device__ __forceinline__ Tile<false> load_match_tile(CArgs& a, uint32_t tile, 
   const uint32_t* lo = col<uint32_t>(on_l, a.lab_off, zp) + (on_l ? rc : 0u);
   d.lo = lo[0];
   d.hi = lo[on_l ? 1u : 0u];
+  const bool on_s = need & NEED_NSL;
+  d.nsl = col<uint32_t>(on_s, a.r_nsl, zp)[on_s ? rc : 0u];
   return d;
 }
 
@@ -589,10 +592,12 @@ __device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC, const
          (notyet & a.sm_dne);
 }
 
-// lo / hi: the resource's lab_off bounds when the tile prefetched them (Tile<false>), else ~0u
+// lo / hi / nsl: the resource's lab_off bounds and r_nsl row when the tile prefetched them
+// (Tile<false>), else kNotFetched
+constexpr uint32_t kNotFetched = 0xFFFFFFFEu;  // r_nsl rows and label offsets stay below it
 __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC, const uint32_t* dyn,
-                                          uint32_t lo = ~0u, uint32_t hi = 0u) {
-  if (lo == ~0u) {
+                                          uint32_t lo = kNotFetched, uint32_t hi = 0u, uint32_t nsl = kNotFetched) {
+  if (lo == kNotFetched) {
     lo = hi = 0;
     if (a.need & NEED_LAB) lo = a.lab_off[rc], hi = a.lab_off[rc + 1];
   }
@@ -601,7 +606,7 @@ __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabC
   LC.selq = LC.nsq = 0;
   LC.kmask = 0;
   if (a.need & NEED_NSL) {  // the namespace row's bounds, once per resource instead of per term
-    const uint32_t row = a.r_nsl[rc];
+    const uint32_t row = nsl != kNotFetched ? nsl : a.r_nsl[rc];
     if (live && row != KPE_NO_STR) LC.nlo = a.nsl_off[row], LC.nhi = a.nsl_off[row + 1];
     if (a.selm & 2u) LC.nsq = a.ns_q[live && row != KPE_NO_STR ? row : a.ns_none];
   }
@@ -990,7 +995,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       if constexpr (!LEAN) {
         LabCache LC;
         if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
-        else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi);
+        else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi, cur.nsl);
         if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #pragma unroll 1
         for (uint32_t ti = 0; ti < a.nterms; ++ti) {
@@ -1083,7 +1088,7 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
     LabCache LC;
     if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
-    else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi);
+    else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi, cur.nsl);
     if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #if KPE_DIAG & 2  // diagnostic build: no term evaluation
     if (lane < a.nterms) tmk[lane] = LC.selq ^ gvk ^ nsa;
@@ -1267,6 +1272,13 @@ namespace {
 }  // namespace
 
 #ifndef KPE_SCAN_ONLY
+// The VM side builds as three objects in parallel (KPE_VM_PART 1: pattern kernels, 2: condition
+// kernel without the pattern VM, pssx, pack3, traces; 3: the condition kernel with it); undefined:
+// all of them in one object.
+#ifndef KPE_VM_PART
+#define KPE_VM_PART 0
+#endif
+#define KPE_IN_PART(p) (KPE_VM_PART == 0 || KPE_VM_PART == (p))
 // grid: 256-row blocks, one lane per row running every pattern rule
 #ifndef KPE_PAT_BLOCK
 #define KPE_PAT_BLOCK 128  // C5 / C3 pattern kernel (events, profiles/r03_c_ldsframes): 256 x 8 frames 20.7 / 9.2 ms,
@@ -1276,6 +1288,7 @@ namespace {
 #define KPE_PAT_MINW 3  // the leaf-table instance takes 111 VGPRs (4 waves/SIMD, as many as the 8 LDS-bound
                         // blocks per CU hold), the one without 166; the inline map path spills at 128 (r03_e_inline)
 #endif
+#if KPE_IN_PART(1)
 // LT: the leaf-table instance (PatVMT LT), for programs whose leaves all have table slots.
 template <bool LT>
 __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kernel(const PatArgs* __restrict__ ap) {
@@ -1323,6 +1336,7 @@ extern "C" hipError_t kpe_launch_leaf_table(const PatArgs* dargs, const uint32_t
                      slot_leaf);
   return hipGetLastError();
 }
+#endif  // KPE_IN_PART(1)
 
 // ===========================================================================
 // Preconditions / deny / foreach-deny conditions (condvm.inl): one lane per resource resolves
@@ -1347,11 +1361,21 @@ __global__ void __launch_bounds__(128) kpe_cond_kernel(const CondArgs* __restric
   if (i < ap->n) cond_eval_row<FEPAT>(*ap, ap->perm ? (int64_t)ap->perm[i] : i, nb[threadIdx.x], tx);
 }
 
+#if KPE_IN_PART(3)
+extern "C" hipError_t kpe_launch_cond_fepat(const CondArgs* dargs, int64_t n, int txt, hipStream_t s) {
+  const size_t lds = txt ? 128u * 2u * KPE_TXT_CAP : 0u;
+  hipLaunchKernelGGL(kpe_cond_kernel<true>, dim3((unsigned)((n + 127) / 128)), dim3(128), lds, s, dargs);
+  return hipGetLastError();
+}
+#endif
+
+#if KPE_IN_PART(2)
+extern "C" hipError_t kpe_launch_cond_fepat(const CondArgs* dargs, int64_t n, int txt, hipStream_t s);
 extern "C" hipError_t kpe_launch_cond(const CondArgs* dargs, int64_t n, int fepat, int txt, hipStream_t s) {
   if (n <= 0) return hipSuccess;
+  if (fepat) return kpe_launch_cond_fepat(dargs, n, txt, s);
   const size_t lds = txt ? 128u * 2u * KPE_TXT_CAP : 0u;
-  if (fepat) hipLaunchKernelGGL(kpe_cond_kernel<true>, dim3((unsigned)((n + 127) / 128)), dim3(128), lds, s, dargs);
-  else hipLaunchKernelGGL(kpe_cond_kernel<false>, dim3((unsigned)((n + 127) / 128)), dim3(128), lds, s, dargs);
+  hipLaunchKernelGGL(kpe_cond_kernel<false>, dim3((unsigned)((n + 127) / 128)), dim3(128), lds, s, dargs);
   return hipGetLastError();
 }
 
@@ -1445,6 +1469,9 @@ extern "C" hipError_t kpe_launch_pattern_trace(const PatArgs* dargs, const uint6
   return hipGetLastError();
 }
 
+#endif  // KPE_IN_PART(2)
+
+#if KPE_IN_PART(1)
 extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32_t npr, int lt, hipStream_t s) {
   if (n <= 0 || npr == 0) return hipSuccess;
   // one lane per row running every pattern rule (a rows x rules grid measured no faster on C5 and
@@ -1464,6 +1491,7 @@ extern "C" hipError_t kpe_launch_pattern(const PatArgs* dargs, int64_t n, uint32
   }
   return hipGetLastError();
 }
+#endif  // KPE_IN_PART(1)
 
 #endif  // !KPE_SCAN_ONLY
 

@@ -9,6 +9,11 @@ constexpr uint32_t kNoNode = 0xFFFFFFFFu;
 #endif
 constexpr int kPatStack = KPE_PAT_STACK;  // frames of one lane; deeper walks give KPE_UNDECIDED
 constexpr uint32_t PF_MAP = 0, PF_AMAPS = 1, PF_APOS = 2;
+#ifndef KPE_PAT_LCACHE
+#define KPE_PAT_LCACHE 0  // member lookups a lane remembers across the rules of its row (0: off; 4 entries
+                          // measured C5 9.25 / C3 3.06 ms against 6.15 / 2.08: 135 VGPRs, one wave per
+                          // SIMD fewer, profiles/r06_h)
+#endif
 #ifndef KPE_PAT_FLAT
 #define KPE_PAT_FLAT 2  // maps of inline depth <= this resolve in their BEGIN step (0: all through frames;
                         // C5 / C3 ms, profiles/r03_e_inline: 0 14.2 / 5.3, 1 12.9 / 5.6, 2 at 4 waves 15.1 / 7.1
@@ -295,7 +300,10 @@ __device__ __forceinline__ bool pat_var_star(const PatArgs& a, uint32_t li, cons
 // key that parses as an anchor (anchor.Parse: TrimSpace, then `^([+<=X^])?\((.+)\)$`), that
 // equals another key of the map (a rename onto it, traverse.go:108-114, depends on Go's map
 // order), that holds a glob under ExpandInMetadata, or (ORDER: the failure-path walk) that sorts
-// to another place among the map's plain keys than the compiled walk order gives it.
+// to another place among the map's plain keys than the compiled walk order gives it. An anchored
+// key (bval bit 2: the template is the whole written key, "=(" + key + ")", pad[2] = the anchor
+// text's lengths before | after the key) keeps its anchor, needs a non-empty key, and its place
+// among the map's anchors is checked in every walk; the member is looked up by the key inside.
 template <bool ORDER>
 __device__ __forceinline__ uint32_t pat_lookup_vkey(const PatArgs& a, DocView doc, uint32_t m, uint32_t li,
                                                     const uint2* pv, uint32_t* und) {
@@ -311,17 +319,25 @@ __device__ __forceinline__ uint32_t pat_lookup_vkey(const PatArgs& a, DocView do
     np = (int)(L.nc < (uint32_t)kTPieces ? L.nc : (uint32_t)kTPieces);
     n = tmpl_pieces(a, &L, pv, pc);
   }
-  // anchor.Parse of the substituted key
-  int b = 0, e = n;
-  auto ws = [](uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); };
-  while (b < e && ws(tp_at(pc, np, b))) ++b;
-  while (e > b && ws(tp_at(pc, np, e - 1))) --e;
-  if (e - b >= 3 && tp_at(pc, np, e - 1) == ')') {
-    const uint8_t c0 = tp_at(pc, np, b);
-    const bool mod = c0 == '+' || c0 == '<' || c0 == '=' || c0 == 'X' || c0 == '^';
-    if (c0 == '(' || (mod && e - b >= 4 && tp_at(pc, np, b + 1) == '(')) {
+  const bool anc = (L.bval & 4u) != 0u;
+  const int pre = anc ? (int)(L.pad[2] & 0xFFFFu) : 0, kn = anc ? n - pre - (int)(L.pad[2] >> 16) : n;
+  if (anc) {
+    if (kn < 1) {  // "=()" is no anchor (`.+`): a plain key the device does not track
       *und = 1u;
       return kNoNode;
+    }
+  } else {  // anchor.Parse of the substituted key
+    int b = 0, e = n;
+    auto ws = [](uint8_t c) { return c == ' ' || (c >= '\t' && c <= '\r'); };
+    while (b < e && ws(tp_at(pc, np, b))) ++b;
+    while (e > b && ws(tp_at(pc, np, e - 1))) --e;
+    if (e - b >= 3 && tp_at(pc, np, e - 1) == ')') {
+      const uint8_t c0 = tp_at(pc, np, b);
+      const bool mod = c0 == '+' || c0 == '<' || c0 == '=' || c0 == 'X' || c0 == '^';
+      if (c0 == '(' || (mod && e - b >= 4 && tp_at(pc, np, b + 1) == '(')) {
+        *und = 1u;
+        return kNoNode;
+      }
     }
   }
   if (ORDER && (L.bval & 2u)) {  // the map has other keys with variables: their walk order is not kept
@@ -337,20 +353,20 @@ __device__ __forceinline__ uint32_t pat_lookup_vkey(const PatArgs& a, DocView do
       }
     }
   }
-  // Go string order against the neighbours: -1 / 0 / 1
-  auto cmp = [&](const uint8_t* t, int tn) -> int {
-    for (int i = 0; i < n && i < tn; ++i) {
-      const uint8_t x = tp_at(pc, np, i);
+  // Go string order of the substituted text [o, o + len) against t: -1 / 0 / 1
+  auto cmp = [&](int o, int len, const uint8_t* t, int tn) -> int {
+    for (int i = 0; i < len && i < tn; ++i) {
+      const uint8_t x = tp_at(pc, np, o + i);
       if (x != t[i]) return x < t[i] ? -1 : 1;
     }
-    return n == tn ? 0 : (n < tn ? -1 : 1);
+    return len == tn ? 0 : (len < tn ? -1 : 1);
   };
   const uint8_t* sib = a.ttext + L.pad[0];
   const uint32_t nsib = L.pad[1] & 0xFFFFu, at = L.pad[1] >> 16;
   for (uint32_t k = 0; k < nsib; ++k) {
     const int tn = (int)sib[0] | (int)sib[1] << 8;
-    const int c = cmp(sib + 2, tn);
-    if (c == 0 || (ORDER && (k < at ? c < 0 : c > 0))) {
+    const int c = cmp(0, n, sib + 2, tn);
+    if (c == 0 || ((ORDER || anc) && (k < at ? c < 0 : c > 0))) {
       *und = 1u;
       return kNoNode;
     }
@@ -361,7 +377,7 @@ __device__ __forceinline__ uint32_t pat_lookup_vkey(const PatArgs& a, DocView do
     const uint32_t k1 = DN_KEY(doc[PVD(c)].x);
     if (!k1 || k1 > a.nkeyd) continue;
     const uint32_t o0 = a.key_off[k1 - 1u], o1 = a.key_off[k1];
-    if ((int)(o1 - o0) == n && cmp(a.key_bytes + o0, n) == 0) return c;
+    if ((int)(o1 - o0) == kn && cmp(pre, kn, a.key_bytes + o0, kn) == 0) return c;
   }
   return kNoNode;
 }
@@ -591,6 +607,30 @@ struct PatVMT {
   int sp;
   FS fs;
   uint32_t* tr;  // TRACE walks: the path record of the last failure (KPE_TRACE_WORDS words)
+#if KPE_PAT_LCACHE
+  // The lane's last KPE_PAT_LCACHE plain member lookups (tape entry, key) -> member entry: the
+  // rules of a row walk the same spine (root -> spec -> containers) one after another, and each
+  // lookup there is a chain of dependent body loads. Tape entries are absolute, so entries of an
+  // earlier row never match a later one; the aggregate initialisers of the VM leave the entries
+  // zero, and key 0 (a name absent from the corpus) is never cached.
+  uint32_t lcm[KPE_PAT_LCACHE], lck[KPE_PAT_LCACHE], lcr[KPE_PAT_LCACHE];
+  uint32_t lcn;
+  __device__ __forceinline__ uint32_t mlookup(uint32_t m, uint32_t key1) {
+    if (key1 == 0u) return kNoNode;
+#pragma unroll
+    for (int i = 0; i < KPE_PAT_LCACHE; ++i)
+      if (lcm[i] == m && lck[i] == key1) return lcr[i];
+    const uint32_t c = pat_lookup(a, doc, m, key1);
+    const uint32_t at = lcn % (uint32_t)KPE_PAT_LCACHE;
+#pragma unroll
+    for (int i = 0; i < KPE_PAT_LCACHE; ++i)
+      if (at == (uint32_t)i) lcm[i] = m, lck[i] = key1, lcr[i] = c;
+    ++lcn;
+    return c;
+  }
+#else
+  __device__ __forceinline__ uint32_t mlookup(uint32_t m, uint32_t key1) { return pat_lookup(a, doc, m, key1); }
+#endif
 
   // ---- failing paths (TRACE walks only; kpe_pattern_trace_kernel) ----
   // PatternError.Path (validate.go:31-56): the reference returns the path of the element where
@@ -612,7 +652,7 @@ struct PatVMT {
   __device__ __forceinline__ uint32_t lookup(const uint4& m, uint32_t r) {
     if (m.x & PMF_GLOB) return pat_lookup_glob(a, doc, r, m.w);
     if (m.x & PMF_VKEY) return pat_lookup_vkey<TRACE>(a, doc, r, m.w, pv, &und);
-    return pat_lookup(a, doc, r, m.y);
+    return TRACE ? pat_lookup(a, doc, r, m.y) : mlookup(r, m.y);
   }
   __device__ __forceinline__ void tput(uint32_t& n, uint32_t c) {
     if (n < KPE_TRACE_WORDS - 1u) tr[1u + n] = c;
@@ -759,7 +799,7 @@ struct PatVMT {
             // one plain member: its value's verdict is the map's (no frame; TRACE walks keep the
             // frame for the member's path component)
             const uint4 m = PU(a.members, pn.y, a.nmembers, 2);
-            br = pat_lookup(a, doc, br, m.y), bpi = m.z, state = VM_BEGIN;
+            br = mlookup(br, m.y), bpi = m.z, state = VM_BEGIN;
             continue;
           } else if (KPE_PAT_FLAT && !TRACE && pw && pw <= (uint32_t)KPE_PAT_FLAT &&
                      (v = flat_map<KPE_PAT_FLAT>(doc[PVD(br)].y, pn)) != PE_NONE) {

@@ -842,7 +842,14 @@ class PatCompiler {
         throw CompileError("$(...) references in pattern keys are not supported on the device");
       if (kv.first.find("{{") != std::string::npos) {
         if (!key_leaf) throw CompileError("variables in pattern keys are not supported here");
-        if (a.k != AK_NONE) throw CompileError("anchored pattern keys with variables are not supported");
+        if (a.k != AK_NONE) {
+          // an anchor whose key has variables: traverse.go:90-117 renames "=({{x}})" to "=(value)"
+          // before validateMap parses the anchor, so the anchor is the written one and its key the
+          // substituted text inside the parentheses (kpe: PMF_VKEY with the anchor's handler)
+          if (!phase1(a.k)) throw CompileError("global / add anchors with variables in their key are not supported");
+          if (trim_ws(kv.first) != kv.first || kv.first.find("{{") < kv.first.find('('))
+            throw CompileError("an anchored pattern key with variables outside its parentheses");
+        }
         if (expanding && has_glob(kv.first)) throw CompileError("wildcard metadata keys with variables");
         if (expanding && repeated) throw CompileError("metadata keys with variables under an array pattern");
         vkeys.push_back(kv.first);
@@ -873,6 +880,8 @@ class PatCompiler {
     // of one onto another, traverse.go:108-114, depends on Go's map order: the cell is undecided)
     if (vkeys.size() > 1)
       for (auto& k : vkeys) {
+        if (anchor_of(k).k != AK_NONE)
+          throw CompileError("an anchored pattern key with variables beside another key with variables");
         const bool whole = k.size() >= 4 && k.compare(0, 2, "{{") == 0 && k.find("{{", 2) == std::string::npos &&
                            k.find("}}") == k.size() - 2;
         if (!whole)
@@ -925,10 +934,19 @@ class PatCompiler {
         // first error; such members can only fail plainly, so the verdict does not depend on where
         // the substituted key sorts (only the failure path of a message does: checked per row by
         // the trace walk). A key whose value holds anchors would move among members that skip.
-        if (nested_anchor(val)) throw CompileError("a pattern key with variables whose value holds anchors");
+        // An anchored key (phase 1, validate.go:118-175) is walked in the sorted order of the
+        // substituted anchor keys, and the first non-skip error decides: its place among the map's
+        // anchors is checked per row in every walk (bit 2), else the cell is undecided.
+        const bool anc = a.k != AK_NONE;
+        if (!anc && nested_anchor(val)) throw CompileError("a pattern key with variables whose value holds anchors");
         KpeLeaf kl{};
         if (!key_leaf(k, kl)) throw CompileError("pattern key template");
         kl.bval = expanding ? 1u : 0u;
+        if (anc) {
+          if (kl.type != PL_TMPL) throw CompileError("pattern key template");
+          kl.bval |= 4u;
+          kl.pad[2] = (uint32_t)(k.find('(') + 1u) | 1u << 16;  // anchor text before / after the key
+        }
         if (vgroup) {  // bit 1: other keys of the map have variables too (their order is not tracked)
           kl.bval |= 2u;
           PP.vars[kl.c0].flags |= (vgroup & 0xFFFFFFu) << PVF_GROUP_SH;
@@ -936,7 +954,7 @@ class PatCompiler {
         // the map's other plain keys in walk order, [u16 length][bytes] each, and this key's place
         kl.pad[0] = (uint32_t)PP.ttext.size();
         uint32_t nsib = 0, at = 0;
-        for (auto& t : rest) {
+        for (auto& t : anc ? first : rest) {
           if (t == k) {
             at = nsib;
             continue;
@@ -1675,9 +1693,8 @@ class CondCompiler {
         if (q == "@" || q.find("{{") != std::string::npos) throw CompileError("{{@}} / nested variables");
         t.kind = VT_QUERY, t.a = Q.compile(q);
       } else {  // variables inside a string (vars.go:311-389): text and variable pieces
-        // a list element is substituted into the side's one lane text slot (condvm.inl value())
-        if (depth > 0 && ++list_tmpls_ > 1)
-          throw CompileError("more than one partial-string variable element in a condition list");
+        // list elements are substituted one after another into the side's lane text slot
+        // (condvm.inl value(): KPE_TXT_CAP bytes together, else the cell is undecided)
         if (v.s.find("\\{{") != std::string::npos) throw CompileError("escaped variables in conditions");
         t.kind = VT_TMPL, t.a = (uint32_t)CP.tpieces.size() / 2;
         auto text = [&](size_t b, size_t e) {
@@ -1703,7 +1720,6 @@ class CondCompiler {
       }
     } else if (v.t == JV::Arr && depth == 0 && has_var(v)) {
       std::vector<uint32_t> el;
-      list_tmpls_ = 0;
       for (auto& x : v.a) {
         if (x.t == JV::Arr || x.t == JV::Obj) throw CompileError("nested lists with variables");
         el.push_back(tmpl(x, 1));
@@ -1808,7 +1824,6 @@ class CondCompiler {
   CondProgram& CP;
   Consts K;
   QueryParser Q;
-  uint32_t list_tmpls_ = 0;  // partial-string elements of the list being compiled
   static bool has_var(const JV& v) {
     size_t a, b;
     if (v.t == JV::Str) return next_var(v.s, 0, &a, &b);

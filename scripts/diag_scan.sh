@@ -11,6 +11,6 @@ for d in "$@"; do
   $ROCM/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-result -munsafe-fp-atomics -fno-vectorize \
     -fno-slp-vectorize -DKPE_SCAN_ONLY -DKPE_DIAG=$d -c csrc/kernels.hip -o build/var/kernels_scan_d$d.o
   $ROCM/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/var/libkpe_d$d.so build/flatten.o build/program.o \
-    build/synth.o build/pss_msg.o build/rhash.o build/kpe_api.o build/var/kernels_scan_d$d.o build/kernels_vm.o -lpthread
+    build/synth.o build/pss_msg.o build/rhash.o build/kpe_api.o build/var/kernels_scan_d$d.o build/kernels_vm1.o build/kernels_vm2.o build/kernels_vm3.o -lpthread
   echo "built build/var/libkpe_d$d.so"
 done

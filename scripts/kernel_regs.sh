@@ -2,7 +2,7 @@
 # Register / spill / scratch summary of every kernel in the built code object (gfx950).
 set -e
 T=$(mktemp -d)
-for O in ${1:-kyverno_amd/build/kernels_scan.o kyverno_amd/build/kernels_vm.o}; do
+for O in ${1:-kyverno_amd/build/kernels_scan.o kyverno_amd/build/kernels_vm1.o kyverno_amd/build/kernels_vm2.o kyverno_amd/build/kernels_vm3.o}; do
 B=/opt/rocm/lib/llvm/bin
 $B/llvm-objcopy --dump-section=.hip_fatbin=$T/fb.bin "$O"
 $B/clang-offload-bundler --type=o --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --input=$T/fb.bin --output=$T/k.co --unbundle

@@ -284,6 +284,11 @@ def cond_policy_set():
                                        ["{{ " + obj + ".metadata.namespace }}-x", "res-1*", "web"]))),
         rule("list-tmpl-key", deny(c(["{{ " + obj + ".metadata.namespace }}/{{ " + obj + ".metadata.name }}",
                                       "{{ " + obj + ".kind }}"], "AnyIn", ["ns-000?/res-2*", "Service"]))),
+        # several partial-string elements, one after another in the side's lane text slot
+        rule("list-tmpl-two", deny(c(["{{ " + obj + ".metadata.namespace }}/{{ " + obj + ".metadata.name }}",
+                                      "k-{{ " + obj + ".kind }}", "{{ " + obj + ".metadata.name }}"], "AnyIn",
+                                     ["ns-000?/res-2*", "k-Service", "x-{{ " + obj + ".metadata.namespace }}",
+                                      "{{ " + obj + ".kind }}-{{ " + obj + ".metadata.name }}"]))),
         rule("vol-keys", deny(c("{{ " + obj + ".spec.volumes[].keys(@)[] || '' }}", "AnyNotIn",
                                 ["name", "configMap", "emptyDir", ""]))),
         rule("caps-add", deny(c("{{ " + obj + ".spec.[ephemeralContainers, initContainers, containers][]."
@@ -459,11 +464,17 @@ def var_policy_set():
         rule("vk-number", {"pattern": {"spec": {"{{request.object.spec.containers[0].ports[0].containerPort}}": "x"}}}),
         rule("vk-spec", {"pattern": {"spec": {"{{request.object.metadata.labels.field || 'containers'}}": [{"name": "c-*"}]}}}),
         # several whole-string key variables in one map; equal substituted keys collide (undecided)
-        rule("vk-two", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.kind || 'team'}}": "team-?",
-                                                            "{{request.object.metadata.labels.zone || 'tier'}}": "back*",
-                                                            "app": "?*"}}}}),
-        rule("vk-two-collide", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.kind || 'x1'}}": "?*",
-                                                                    "{{request.object.metadata.labels.kind || 'x2'}}": "?*"}}}}),
+        rule("vk-two", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.labels.zone || 'tier'}}": "back*",
+                                                            "{{request.object.metadata.annotations.owner || 'app'}}": "?*"}}}}),
+        # anchored keys with variables: renamed first (traverse.go:90-117), then parsed as anchors
+        rule("vk-anchor-eq", {"pattern": {"metadata": {"labels": {"=({{request.object.metadata.labels.zone || 'tier'}})": "back*"}}}}),
+        rule("vk-anchor-cond", {"pattern": {"metadata": {"labels": {
+            "({{request.object.metadata.annotations.owner || 'tier'}})": "front*", "app": "app-1*"}}}}),
+        rule("vk-anchor-neg", {"pattern": {"metadata": {"labels": {"X({{request.object.metadata.annotations.owner || 'tier'}})": "null"}}}}),
+        rule("vk-anchor-order", {"pattern": {"metadata": {"labels": {"=(c)": "x",
+                                                                     "=({{request.object.metadata.labels.tier}})": "x*"}}}}),
+        rule("vk-two-collide", {"pattern": {"metadata": {"labels": {"{{request.object.metadata.annotations.owner || 'x1'}}": "?*",
+                                                                    "{{request.object.metadata.annotations.owner || 'x2'}}": "?*"}}}}),
         # foreach entries
         rule("fe-pat", {"foreach": [{"list": ctr, "pattern": {"securityContext": {"=(privileged)": False}}}]}),
         rule("fe-pat-var", {"foreach": [{"list": ctr, "pattern": {"name": "c-{{elementIndex}}"}}]}),
@@ -492,7 +503,8 @@ def var_policy_set():
 
 # rules of var_policy_set whose cells the device may leave KPE_UNDECIDED (a variable resolving
 # to a map is a pattern subtree; documented device limit)
-VAR_UNDECIDED_OK = {"v-map", "vk-collide", "vk-two-collide"}  # vk-*collide: a key renamed onto another key
+# vk-*collide: a key renamed onto another key; vk-anchor-order: an anchor key that sorts elsewhere
+VAR_UNDECIDED_OK = {"v-map", "vk-collide", "vk-two-collide", "vk-anchor-order"}
 
 
 def foreach_message_policy_set():

@@ -51,7 +51,8 @@ def test_var_policy_set_compiles(oracle):
 
 
 @pytest.mark.parametrize("pattern", [
-    {"metadata": {"labels": {"=({{request.object.metadata.name}})": "x"}}},  # a variable in an anchored key
+    {"metadata": {"labels": {"<({{request.object.metadata.name}})": "x"}}},  # a variable in a global anchor key
+    {"metadata": {"labels": {"=({{request.object.metadata.name}})": "x", "{{request.object.kind}}": "y"}}},  # + another
     {"metadata": {"labels": {"a-{{request.object.metadata.name}}": "x", "{{request.object.kind}}": "y"}}},  # two, one partial
     {"metadata": {"name": "$(./namespace)"}},                              # a reference
     {"metadata": {"name": "{{ @ }}"}},                                     # {{@}}
