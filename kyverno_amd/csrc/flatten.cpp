@@ -561,7 +561,7 @@ class Typed {
             return true;
           }
           for (int i = 0; i < KPE_NUM_VOLUME_SOURCES; ++i) {
-            if (keq(k, kVolSrc[i])) {
+            if (keq_n(k, kVolSrc[i], strlen(kVolSrc[i]))) {
               JK t = c_.peek();
               if (t == JK::Null) {
                 c_.null();

@@ -349,8 +349,7 @@ class JCur {
 };
 
 // ASCII case fold compare: `key` (any case) equals `lower` (already lower case).
-inline bool keq(std::string_view key, const char* lower) {
-  size_t n = strlen(lower);
+inline bool keq_n(std::string_view key, const char* lower, size_t n) {
   if (key.size() != n) return false;
   for (size_t i = 0; i < n; ++i) {
     char c = key[i];
@@ -359,5 +358,11 @@ inline bool keq(std::string_view key, const char* lower) {
   }
   return true;
 }
+// a literal name: the length test is inlined at the call site (most keys differ in length)
+template <size_t N>
+__attribute__((always_inline)) inline bool keq(std::string_view key, const char (&lower)[N]) {
+  return key.size() == N - 1 && keq_n(key, lower, N - 1);
+}
+inline bool keq(std::string_view key, const std::string& lower) { return keq_n(key, lower.data(), lower.size()); }
 
 }  // namespace kpe
