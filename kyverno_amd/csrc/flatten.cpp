@@ -797,7 +797,7 @@ class Flattener {
     std::string_view key;
     std::string ks;
     while (cur.obj_next(f, &key, ks)) {
-      std::string k(key);
+      const std::string_view k = key;  // valid until the next member
       if (k == "kind" || k == "apiVersion") {
         if (cur.peek() == JK::Str) {
           std::string_view v;
@@ -856,7 +856,7 @@ class Flattener {
     std::string_view key;
     std::string ks;
     while (cur.obj_next(f, &key, ks)) {
-      std::string k(key);
+      const std::string_view k = key;  // valid until the next member
       // unstructured accessors
       if (k == "name" || k == "generateName" || k == "namespace") {
         if (cur.peek() == JK::Str) {
@@ -894,18 +894,17 @@ class Flattener {
         std::string_view k2;
         std::string ks2;
         std::vector<std::pair<std::string, std::string>> typed_ann;
-        while (cur.obj_next(f2, &k2, ks2)) {
-          std::string kk2(k2);
+        std::string vsc;
+        while (cur.obj_next(f2, &k2, ks2)) {  // k2 stays valid until the next member
           if (cur.peek() == JK::Str) {
             std::string_view v;
-            std::string sc;
-            cur.str(&v, sc);
-            upsert(dst, kk2, std::string(v));
-            upsert(typed_ann, kk2, std::string(v));
+            cur.str(&v, vsc);
+            upsert(dst, k2, v);
+            if (!is_lab) upsert(typed_ann, k2, v);  // the typed view is kept for annotations only
           } else if (cur.peek() == JK::Null) {
             cur.null();
             ok = false;  // NestedStringMap: non-string value => error => nil
-            upsert(typed_ann, kk2, std::string());
+            if (!is_lab) upsert(typed_ann, k2, std::string_view());
           } else {
             ok = false;
             if (typed) t.err = true;
@@ -932,14 +931,13 @@ class Flattener {
       else t.member(sid("ObjectMeta"), k);
     }
   }
-  static void upsert(std::vector<std::pair<std::string, std::string>>& v, const std::string& k,
-                     const std::string& val) {
+  static void upsert(std::vector<std::pair<std::string, std::string>>& v, std::string_view k, std::string_view val) {
     for (auto& e : v)
       if (e.first == k) {
-        e.second = val;
+        e.second.assign(val);
         return;
       }
-    v.emplace_back(k, val);
+    v.emplace_back(std::string(k), std::string(val));
   }
 
   void spec(Typed& t, uint32_t cls) {

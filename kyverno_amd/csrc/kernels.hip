@@ -720,16 +720,38 @@ __device__ __forceinline__ void store_rows(uint8_t* verdicts, const uint8_t* sv,
     const uint32_t nb = nrows * R, nw = nb >> 2;
     uint32_t* dst = reinterpret_cast<uint32_t*>(base);
     const uint32_t* src = reinterpret_cast<const uint32_t*>(sv);
+    uint32_t i = lane;
 #pragma unroll 1
-    for (uint32_t i = lane; i < nw; i += 64) dst[i] = src[i];
+    for (; 4u * i + 3u < nw; i += 64) {  // 16 bytes per lane and store
+      const uint32_t* s4 = src + 4u * i;
+      *reinterpret_cast<u32x4a*>(dst + 4u * i) = u32x4a{s4[0], s4[1], s4[2], s4[3]};
+    }
+#pragma unroll 1
+    for (i = (nw & ~3u) + lane; i < nw; i += 64) dst[i] = src[i];
     if (lane < (nb & 3u)) base[(nw << 2) + lane] = sv[(nw << 2) + lane];
-  } else if (((R | c0 | nc) & 3u) == 0u) {  // dword-aligned row segments: nc / 4 dwords per row
-    const uint32_t nw = nc >> 2, tot = nrows * nw;
+  } else if (((R | c0 | nc) & 3u) == 0u) {  // dword-aligned row segments (nc bytes of each row)
     const uint32_t* src = reinterpret_cast<const uint32_t*>(sv);
+    // unit u of the chunk is row u / n, piece u % n: one division per lane, then steps of 64 units
+    // (no integer division per store)
+    auto walk = [&](uint32_t n, uint32_t tot, auto&& put) {
+      uint32_t row = lane / n, q = lane - row * n;
+      const uint32_t drow = 64u / n, dq = 64u - drow * n;
 #pragma clang loop vectorize(disable) unroll(disable)
-    for (uint32_t i = lane; i < tot; i += 64) {
-      const uint32_t row = i / nw, w = i - row * nw;
-      *reinterpret_cast<uint32_t*>(base + (size_t)row * R + 4u * w) = src[i];
+      for (uint32_t i = lane; i < tot; i += 64) {
+        put(i, row, q);
+        row += drow, q += dq;
+        if (q >= n) q -= n, ++row;
+      }
+    };
+    if ((nc & 15u) == 0u) {  // 16 bytes per lane and store (dword-aligned addresses)
+      walk(nc >> 4, nrows * (nc >> 4), [&](uint32_t i, uint32_t row, uint32_t q) {
+        const uint32_t* s4 = src + 4u * i;
+        *reinterpret_cast<u32x4a*>(base + (size_t)row * R + 16u * q) = u32x4a{s4[0], s4[1], s4[2], s4[3]};
+      });
+    } else {
+      walk(nc >> 2, nrows * (nc >> 2), [&](uint32_t i, uint32_t row, uint32_t q) {
+        *reinterpret_cast<uint32_t*>(base + (size_t)row * R + 4u * q) = src[i];
+      });
     }
   } else {
 #pragma clang loop vectorize(disable) unroll(disable)
