@@ -444,7 +444,7 @@ def main(argv=None):
             pat_traffic = None
             try:  # FETCH_SIZE / WRITE_SIZE of the pattern kernel (scripts/gpu_pass.sh traffic:<cfg>:kpe_pattern_kernel)
                 tj = json.load(open(traffic_json))
-                if tj.get("kernel") == "kpe_pattern_kernel":
+                if tj.get("kernel", "").split("<")[0] == "kpe_pattern_kernel":  # either LT instance
                     pat_traffic = tj.get("scan_bytes_per_launch")
             except Exception:
                 pat_traffic = None
