@@ -31,6 +31,10 @@
 namespace {
 #include "strmatch.inl"
 
+#ifndef KPE_PSUM_LABPRE
+#define KPE_PSUM_LABPRE 0  // 1: PSUM tiles carry the label bounds and namespace row (C4 0.420 / 0.427 against
+                           // 0.415 / 0.416 ms, 6 spills; profiles/r06_l)
+#endif
 // Wave-uniform table read: the address is uniform, so this is a scalar (SMEM) load
 // through the constant cache — no LDS round trip and no readfirstlane to branch on it.
 #ifndef KPE_DIAG
@@ -329,6 +333,14 @@ __device__ __forceinline__ Tile<true> load_pss_tile(CArgs& a, uint32_t tile, uin
     const bool on_n = need & NEED_NAME, on_m = need & NEED_MNS;
     d.name = col<uint32_t>(on_n, a.r_name, zp)[on_n ? rc : 0u];
     d.mns = col<uint32_t>(on_m, a.r_mns, zp)[on_m ? rc : 0u];
+#if KPE_PSUM_LABPRE
+    // the list slots the records replace carry the label bounds and the namespace row one step
+    // ahead of the label loads (lab_cache)
+    const bool on_l = need & NEED_LAB, on_s = need & NEED_NSL;
+    const uint32_t* lo = col<uint32_t>(on_l, a.lab_off, zp) + (on_l ? rc : 0u);
+    d.v0 = lo[0], d.v1 = lo[on_l ? 1u : 0u];
+    d.s0 = col<uint32_t>(on_s, a.r_nsl, zp)[on_s ? rc : 0u];
+#endif
     return d;
   }
   const bool on_c = a.nctr_total, on_sa = on_c && (need & NEED_SANN);
@@ -593,7 +605,7 @@ __device__ __forceinline__ uint64_t sel_fold(CArgs& a, const LabCache& LC, const
 }
 
 // lo / hi / nsl: the resource's lab_off bounds and r_nsl row when the tile prefetched them
-// (Tile<false>), else kNotFetched
+// (Tile<false>, or PSUM tiles' list slots), else kNotFetched
 constexpr uint32_t kNotFetched = 0xFFFFFFFEu;  // r_nsl rows and label offsets stay below it
 __device__ __forceinline__ void lab_cache(CArgs& a, uint32_t rc, bool live, LabCache& LC, const uint32_t* dyn,
                                           uint32_t lo = kNotFetched, uint32_t hi = 0u, uint32_t nsl = kNotFetched) {
@@ -1016,7 +1028,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
       uint32_t tb = 0;
       if constexpr (!LEAN) {
         LabCache LC;
-        if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
+        if constexpr (PSS && PSUM && KPE_PSUM_LABPRE) lab_cache(a, rc, live, LC, dyn, cur.v0, cur.v1, cur.s0);
+        else if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
         else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi, cur.nsl);
         if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #pragma unroll 1
@@ -1109,7 +1122,8 @@ __global__ void __launch_bounds__(kBlock, LEAN ? KPE_LEAN_WAVES : KPE_SCAN_WAVES
         a.filt_lds != PRED_NONE ? reinterpret_cast<const KpeFilter*>(dyn + a.filt_lds) : a.filters;
     const uint32_t* fterm = a.filt_lds != PRED_NONE ? dyn + a.fterm_lds : a.fterms;
     LabCache LC;
-    if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
+    if constexpr (PSS && PSUM && KPE_PSUM_LABPRE) lab_cache(a, rc, live, LC, dyn, cur.v0, cur.v1, cur.s0);
+    else if constexpr (PSS) lab_cache(a, rc, live, LC, dyn);
     else lab_cache(a, rc, live, LC, dyn, cur.lo, cur.hi, cur.nsl);
     if (a.kslot_lds != PRED_NONE) LC.kmask = kslot_mask(a, dyn, gvk);
 #if KPE_DIAG & 2  // diagnostic build: no term evaluation
