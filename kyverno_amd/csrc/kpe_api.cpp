@@ -150,10 +150,11 @@ struct kpe_device {
   // evaluation), KPE_PATVM_ERR (report a KPE_PATVM_CHECK build's bounds flags), KPE_LEAN6_MINW /
   // KPE_LEAN6_TPW (waves a LEAN6 launch keeps / tiles per wave, for A/B runs)
   bool no_cache = false, patvm_err = false;
-  // the general scan of a podSecurity program reads per-pod records kpe_psum_kernel builds right
-  // before it; KPE_PSUM=0: it walks each pod's lists itself (C4 0.546 vs 0.566 ms per step, but 1.98x
-  // its algorithmic bytes against 0.92x; C3 2.66 vs 2.64 ms: profiles/r05_psA, r05_psB, r05_final5)
-  bool no_psum = false;
+  // the general scan of a podSecurity program walks each pod's lists itself; KPE_PSUM=1: it reads
+  // per-pod records kpe_psum_kernel builds right before it on the second stream (round 6: C4 step
+  // 0.393 ms without them against 0.416 ms with them, C3 unchanged, profiles/r06_n; round 5 kept the
+  // records for their 0.92x traffic against 1.98x: profiles/r05_psA, r05_psB, r05_final5)
+  bool no_psum = true;
   uint64_t lean_min_waves = 16384;  // 256 CUs x 4 SIMDs x 16 waves
   uint32_t lean_tpw = 0;
   // pinned staging for corpus uploads (two halves, double-buffered; allocated on first use): a

@@ -141,6 +141,31 @@ def test_c4_selectors_bit_exact(engine, oracle, n, seed):
         assert cnt[r]["pass"] == int((v[:, r] == 1).sum()) and cnt[r]["na"] == int((v[:, r] == 0).sum())
 
 
+@pytest.mark.parametrize("psum", ["1", "0"])
+def test_general_scan_both_pss_forms_bit_exact(oracle, psum):
+    """The general scan of a podSecurity program in both forms (KPE_PSUM, read at device open):
+    walking each pod's lists itself (the default) and reading kpe_psum_kernel's per-pod records;
+    verdicts and check masks equal the oracle's on the C4 mix and the C1 mixes."""
+    from tests.policies import c4_policy_set
+
+    old = os.environ.get("KPE_PSUM")
+    os.environ["KPE_PSUM"] = psum
+    try:
+        eng = K.Engine(ordinal=0)
+        for pols, mix, seed in ((c4_policy_set(), 3, 0x41), (parity_policy_set(), 2, 0x42)):
+            nd = K.synth_resources(seed, 20000, mix=mix)
+            nsl = K.synth_ns_labels(seed, 10000, mix=3) if mix == 3 else None
+            v, _, _ = _gpu(eng, pols, nd, nsl)
+            ref = oracle.validate(pols, nd, ns_labels=nsl, nthreads=16)
+            bad = np.argwhere(v != ref)
+            assert bad.size == 0, f"KPE_PSUM={psum}: {len(bad)} mismatching cells, first {bad[:5].tolist()}"
+    finally:
+        if old is None:
+            os.environ.pop("KPE_PSUM", None)
+        else:
+            os.environ["KPE_PSUM"] = old
+
+
 @pytest.mark.parametrize("copies", [1, 4, 8, 9])
 def test_selector_requirement_masks_and_fallback(engine, oracle, copies):
     """Selector terms decided from the per-binding requirement masks (<= 64 requirements per
