@@ -330,6 +330,9 @@ struct PatArgs {
   uint32_t nnodes, nmembers, nlists, nleaves, nconds, npats, nroots, npbuf;
   uint64_t nscal, ndoc;
   uint32_t* err;
+  // memo slot s's representative pattern rule (any rule of the slot: they share the pattern), or
+  // ~0u for an unused slot; kpe_pattern_kernel evaluates a row's slots in slot order
+  uint32_t slot_rule[KPE_PAT_MEMO];
 };
 
 // kpe_cond_kernel arguments (device-resident, one copy per binding)

@@ -1648,6 +1648,11 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       pa.roots = PD.proots.as<uint32_t>();
       pa.rules = PD.prules.as<KpePatRule>();
       pa.col2pr = PD.pcol2pr.as<uint32_t>();
+      for (uint32_t k = 0; k < KPE_PAT_MEMO; ++k) pa.slot_rule[k] = ~0u;
+      for (uint32_t i = 0; i < (uint32_t)P.pat.rules.size(); ++i) {
+        const uint32_t sl = P.pat.rules[i].flags >> PR_MEMO_SH;
+        if (sl < KPE_PAT_MEMO && pa.slot_rule[sl] == ~0u) pa.slot_rule[sl] = i;
+      }
       pa.pbuf = B.pbuf.as<uint32_t>();
       pa.pvals = P.pat.vars.empty() ? nullptr : B.pvals.as<uint2>();
       pa.nvars = (uint32_t)P.pat.vars.size();

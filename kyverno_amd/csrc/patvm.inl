@@ -1027,7 +1027,8 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
   // run the VM for the same pattern rule together.
   const uint64_t start = (uint64_t)r * a.R;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(a.verdicts);
-  for (uint32_t c00 = 0; c00 < a.R; c00 += 64u) {
+  // the pending cells of the row's 64 columns from c00
+  auto pending = [&](uint32_t c00) -> uint64_t {
     const uint64_t p0 = start + c00;
     const uint32_t sh = (uint32_t)(p0 & 3u);
     uint32_t w[17];
@@ -1043,6 +1044,43 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       pend |= (uint64_t)(((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4u * j);
     }
     if (a.R - c00 < 64u) pend &= (1ull << (a.R - c00)) - 1ull;  // past the row
+    return pend;
+  };
+  // Memo slots first, in slot order: each lane evaluates the slots its pending cells need, so the
+  // lanes of a wave that need slot s walk its pattern together (in column order, a lane whose first
+  // cell of slot s comes later than its neighbours' walked it alone: C3's rows differ in which
+  // rules their names and namespaces select). The cells then take their slot's verdict.
+  if (memo && KPE_PAT_SLOT_ORDER) {
+    uint32_t need = 0;
+    for (uint32_t c00 = 0; c00 < a.R; c00 += 64u) {
+      uint64_t pend = pending(c00);
+      while (pend) {
+        const uint32_t cq = c00 + (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1ull;
+        const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
+        if (pi == 0u) continue;
+        const uint32_t slot = a.rules[pi - 1u].flags >> PR_MEMO_SH;
+        if (slot < KPE_PAT_MEMO) need |= 1u << slot;
+      }
+    }
+#pragma unroll 1
+    for (uint32_t s = 0; s < KPE_PAT_MEMO; ++s) {
+      if (!((need >> s) & 1u)) continue;
+      uint32_t v = pat_eval_cell(vm, a.slot_rule[s]);
+      if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
+        if constexpr (DEFER) {
+          v = KPE_DEEP_;  // every cell of the slot goes to kpe_pattern_deep_kernel
+        } else {
+          PatVMT<FramesPriv, LT> deep{a, vm.doc, vm.root, vm.pv, 0u};
+          v = pat_eval_cell(deep, a.slot_rule[s]);
+        }
+      }
+      memo[s * memo_stride] = (uint8_t)v;
+    }
+    memo_ok = need;
+  }
+  for (uint32_t c00 = 0; c00 < a.R; c00 += 64u) {
+    uint64_t pend = pending(c00);
     while (pend) {
       const uint32_t q = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1ull;

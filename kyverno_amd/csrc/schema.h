@@ -661,6 +661,9 @@ typedef struct KpeCond {
 #define PR_NO_MEMO 0xFFFFu
 // 16 slots: 2 KiB of LDS per 128-lane block, so 8 blocks fit a CU's 160 KiB with the frame stacks
 // (32 slots allowed 7; C5 6.97 -> 6.59 ms, C3 3.23 -> 3.05 ms, profiles/r04_o)
+#ifndef KPE_PAT_SLOT_ORDER
+#define KPE_PAT_SLOT_ORDER 1  // kpe_pattern_kernel evaluates a row's memo slots in slot order first
+#endif
 #ifndef KPE_PAT_MEMO
 #define KPE_PAT_MEMO 16
 #endif

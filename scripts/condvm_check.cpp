@@ -141,6 +141,11 @@ int main(int argc, char** argv) {
   pa.nodes = PP.nodes.data(), pa.members = mem.data(), pa.lists = PP.lists.data(), pa.leaves = PP.leaves.data();
   pa.conds = PP.conds.data(), pa.pats = pp.data(), pa.pat_bytes = pb.data(), pa.roots = PP.roots.data();
   pa.rules = PP.rules.data(), pa.col2pr = col2pr.data(), pa.pbuf = pbuf.data(), pa.verdicts = verdicts.data();
+  for (uint32_t k = 0; k < KPE_PAT_MEMO; ++k) pa.slot_rule[k] = ~0u;
+  for (uint32_t i = 0; i < (uint32_t)PP.rules.size(); ++i) {
+    const uint32_t sl = PP.rules[i].flags >> PR_MEMO_SH;
+    if (sl < KPE_PAT_MEMO && pa.slot_rule[sl] == ~0u) pa.slot_rule[sl] = i;
+  }
   pa.pvals = pvals.data(), pa.nvars = (uint32_t)PP.vars.size(), pa.ptmpl = tp.data(), pa.ttext = tt.data();
   pa.ctab = CP.consts.data(), pa.ctext = ctext.data();
   pa.nnodes = (uint32_t)PP.nodes.size(), pa.nmembers = (uint32_t)mem.size(), pa.nlists = (uint32_t)PP.lists.size();

@@ -124,6 +124,11 @@ int main(int argc, char** argv) {
   std::vector<uint32_t> col2pr(R + 4, 0u);
   for (size_t i = 0; i < PP.rules.size(); ++i) col2pr[PP.rules[i].col] = (uint32_t)i + 1u;
   a.col2pr = col2pr.data();
+  for (uint32_t k = 0; k < KPE_PAT_MEMO; ++k) a.slot_rule[k] = ~0u;  // memo slots' representative rules
+  for (uint32_t i = 0; i < (uint32_t)PP.rules.size(); ++i) {
+    const uint32_t sl = PP.rules[i].flags >> PR_MEMO_SH;
+    if (sl < KPE_PAT_MEMO && a.slot_rule[sl] == ~0u) a.slot_rule[sl] = i;
+  }
   uint32_t err = 0;
   a.nnodes = (uint32_t)PP.nodes.size(), a.nmembers = (uint32_t)mem.size(), a.nlists = (uint32_t)PP.lists.size();
   a.nleaves = (uint32_t)PP.leaves.size(), a.nconds = (uint32_t)PP.conds.size(), a.npats = (uint32_t)pats.size();
