@@ -1481,8 +1481,8 @@ __global__ void __launch_bounds__(128) kpe_pattern_trace_kernel(const PatArgs* _
     pr.r0 = job.x, pr.nr = job.y & 0xFFFFu, pr.flags = job.y >> 16;
     if (job.z != kNoNode) start = job.z;
   } else {
-    if (!a.col2pr || a.col2pr[col] == 0u) return;
-    pr = a.rules[a.col2pr[col] - 1u];
+    if (!a.col2pr || C2P_RULE(a.col2pr[col]) == 0u) return;
+    pr = a.rules[C2P_RULE(a.col2pr[col]) - 1u];
   }
   PatVM vm{a, PV_DOCVIEW(a, reinterpret_cast<const uint2*>(a.doc), 0u, a.ndoc), start,
            a.pvals + (size_t)row * a.nvars, 0u};

@@ -305,7 +305,7 @@ struct PatArgs {
   const uint8_t* pat_bytes;
   const uint32_t* roots;           // (node, anchor slots) pairs
   const KpePatRule* rules;
-  const uint32_t* col2pr;          // verdict column -> pattern rule index + 1 (0: none), or null
+  const uint32_t* col2pr;          // verdict column -> C2P_MAKE(pattern rule index + 1, memo slot), or null
   const uint32_t* pbuf;            // glob member-name bitsets (HBM)
   // pattern variables: per-row values written by kpe_cond_kernel (pvals[row * nvars + slot]),
   // template pieces / texts, and the condition-program constants a value may name

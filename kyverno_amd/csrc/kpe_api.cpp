@@ -743,7 +743,8 @@ kpe_status ensure_program(kpe_device* dev, const kpe_program* pp) {
     HIPCHK(upload(D.ttext, PP.ttext, s0));
     {
       std::vector<uint32_t> c2p(P.rules.size() + 4, 0u);  // + slack: the kernel reads whole words
-      for (size_t i = 0; i < PP.rules.size(); ++i) c2p[PP.rules[i].col] = (uint32_t)i + 1u;
+      for (size_t i = 0; i < PP.rules.size(); ++i)
+        c2p[PP.rules[i].col] = C2P_MAKE((uint32_t)i + 1u, PP.rules[i].flags >> PR_MEMO_SH);
       HIPCHK(upload(D.pcol2pr, c2p, s0));
     }
     const auto& CP = P.cond;

@@ -1028,16 +1028,18 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
   const uint64_t start = (uint64_t)r * a.R;
   const uint32_t* words = reinterpret_cast<const uint32_t*>(a.verdicts);
   // the pending cells of the row's 64 columns from c00
+  // (a rolling pair of words, not a 17-word array: an array here is put in scratch memory)
   auto pending = [&](uint32_t c00) -> uint64_t {
     const uint64_t p0 = start + c00;
     const uint32_t sh = (uint32_t)(p0 & 3u);
-    uint32_t w[17];
-#pragma unroll
-    for (uint32_t j = 0; j < 17u; ++j) w[j] = words[(p0 >> 2) + j];  // the buffer carries slack past the matrix
+    const uint32_t* wp = words + (p0 >> 2);  // the buffer carries slack past the matrix
     uint64_t pend = 0;
+    uint32_t lo = wp[0];
 #pragma unroll
     for (uint32_t j = 0; j < 16u; ++j) {
-      uint32_t x = sh ? (uint32_t)((((uint64_t)w[j + 1u] << 32) | w[j]) >> (8u * sh)) : w[j];  // cells 4j .. 4j + 3
+      const uint32_t hi = wp[j + 1u];
+      uint32_t x = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh)) : lo;  // cells 4j .. 4j + 3
+      lo = hi;
       const uint32_t t = x ^ 0x06060606u;  // KPE_PENDING_ cells -> 0
       // exact zero-byte test (no borrow between bytes): bit 8q + 7 set iff byte q was pending
       const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
@@ -1057,10 +1059,9 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       while (pend) {
         const uint32_t cq = c00 + (uint32_t)__builtin_ctzll(pend);
         pend &= pend - 1ull;
-        const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
-        if (pi == 0u) continue;
-        const uint32_t slot = a.rules[pi - 1u].flags >> PR_MEMO_SH;
-        if (slot < KPE_PAT_MEMO) need |= 1u << slot;
+        const uint32_t e = a.col2pr ? a.col2pr[cq] : 0u;
+        const uint32_t slot = C2P_SLOT(e);
+        if (C2P_RULE(e) != 0u && slot < KPE_PAT_MEMO) need |= 1u << slot;
       }
     }
 #pragma unroll 1
@@ -1085,9 +1086,10 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       const uint32_t q = (uint32_t)__builtin_ctzll(pend);
       pend &= pend - 1ull;
       const uint32_t cq = c00 + q;
-      const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
+      const uint32_t e = a.col2pr ? a.col2pr[cq] : 0u;
+      const uint32_t pi = C2P_RULE(e);
       if (pi == 0u) continue;
-      const uint32_t slot = memo ? a.rules[pi - 1u].flags >> PR_MEMO_SH : PR_NO_MEMO;
+      const uint32_t slot = memo ? C2P_SLOT(e) : PR_NO_MEMO;
       if (slot < KPE_PAT_MEMO && ((memo_ok >> slot) & 1u)) {
         row[cq] = memo[slot * memo_stride];
         continue;
@@ -1120,13 +1122,14 @@ __device__ __forceinline__ void pat_deep_row(const PatArgs& a, int64_t r, FS fs 
   for (uint32_t c00 = 0; c00 < a.R; c00 += 64u) {
     const uint64_t p0 = start + c00;
     const uint32_t sh = (uint32_t)(p0 & 3u);
-    uint32_t w[17];
-#pragma unroll
-    for (uint32_t j = 0; j < 17u; ++j) w[j] = words[(p0 >> 2) + j];
+    const uint32_t* wp = words + (p0 >> 2);
     uint64_t mark = 0;
+    uint32_t lo = wp[0];
 #pragma unroll
     for (uint32_t j = 0; j < 16u; ++j) {
-      const uint32_t x = sh ? (uint32_t)((((uint64_t)w[j + 1u] << 32) | w[j]) >> (8u * sh)) : w[j];
+      const uint32_t hi = wp[j + 1u];
+      const uint32_t x = sh ? (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * sh)) : lo;
+      lo = hi;
       const uint32_t t = x ^ 0x26262626u;  // KPE_DEEP_ cells -> 0
       const uint32_t z = ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t | 0x7F7F7F7Fu);
       mark |= (uint64_t)(((z >> 7) & 1u) | ((z >> 14) & 2u) | ((z >> 21) & 4u) | ((z >> 28) & 8u)) << (4u * j);
@@ -1139,7 +1142,7 @@ __device__ __forceinline__ void pat_deep_row(const PatArgs& a, int64_t r, FS fs 
       const uint32_t q = (uint32_t)__builtin_ctzll(mark);
       mark &= mark - 1ull;
       const uint32_t cq = c00 + q;
-      const uint32_t pi = a.col2pr ? a.col2pr[cq] : 0u;
+      const uint32_t pi = a.col2pr ? C2P_RULE(a.col2pr[cq]) : 0u;
       row[cq] = (uint8_t)(pi ? pat_eval_cell(vm, pi - 1u) : KPE_UNDECIDED_);
     }
   }

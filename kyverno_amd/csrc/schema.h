@@ -661,6 +661,11 @@ typedef struct KpeCond {
 #define PR_NO_MEMO 0xFFFFu
 // 16 slots: 2 KiB of LDS per 128-lane block, so 8 blocks fit a CU's 160 KiB with the frame stacks
 // (32 slots allowed 7; C5 6.97 -> 6.59 ms, C3 3.23 -> 3.05 ms, profiles/r04_o)
+// PatArgs::col2pr entry: pattern rule index + 1 in the low 24 bits (0: not a pattern column), the
+// rule's memo slot + 1 in the high 8 (0: none), so a cell's slot needs no rule-record load
+#define C2P_RULE(e) ((e) & 0xFFFFFFu)
+#define C2P_SLOT(e) (((e) >> 24) - 1u)  // >= KPE_PAT_MEMO: none
+#define C2P_MAKE(pi1, slot) ((pi1) | (((slot) < KPE_PAT_MEMO ? (slot) + 1u : 0u) << 24))
 #ifndef KPE_PAT_SLOT_ORDER
 #define KPE_PAT_SLOT_ORDER 1  // kpe_pattern_kernel evaluates a row's memo slots in slot order first
 #endif

@@ -133,7 +133,8 @@ int main(int argc, char** argv) {
   std::vector<uint8_t> tt(PP.ttext.begin(), PP.ttext.end());
   tt.resize(tt.size() + 17, 0);
   std::vector<uint32_t> col2pr(R + 4, 0u);
-  for (size_t i = 0; i < PP.rules.size(); ++i) col2pr[PP.rules[i].col] = (uint32_t)i + 1u;
+  for (size_t i = 0; i < PP.rules.size(); ++i)
+    col2pr[PP.rules[i].col] = C2P_MAKE((uint32_t)i + 1u, PP.rules[i].flags >> PR_MEMO_SH);
   uint32_t perr = 0;
   PatArgs pa{};
   pa.n = C.n, pa.R = R, pa.npr = (uint32_t)PP.rules.size();

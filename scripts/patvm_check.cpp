@@ -122,7 +122,8 @@ int main(int argc, char** argv) {
   a.conds = PP.conds.data(), a.pats = pats.data(), a.pat_bytes = pb.data(), a.roots = PP.roots.data();
   a.rules = PP.rules.data(), a.pbuf = pbuf.data(), a.verdicts = verdicts.data();
   std::vector<uint32_t> col2pr(R + 4, 0u);
-  for (size_t i = 0; i < PP.rules.size(); ++i) col2pr[PP.rules[i].col] = (uint32_t)i + 1u;
+  for (size_t i = 0; i < PP.rules.size(); ++i)
+    col2pr[PP.rules[i].col] = C2P_MAKE((uint32_t)i + 1u, PP.rules[i].flags >> PR_MEMO_SH);
   a.col2pr = col2pr.data();
   for (uint32_t k = 0; k < KPE_PAT_MEMO; ++k) a.slot_rule[k] = ~0u;  // memo slots' representative rules
   for (uint32_t i = 0; i < (uint32_t)PP.rules.size(); ++i) {
