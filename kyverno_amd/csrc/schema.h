@@ -588,11 +588,15 @@ typedef struct KpePNode {
 #define PM_SLOT(x) (((x) >> 8) & 31u)
 #define PMF_XSLOT (1u << 13)  // condition / existence anchor past the 32 AnchorMap slots: a map
                               // holding it makes the cell KPE_UNDECIDED
-#define PMF_VKEY (1u << 14)   // a plain key with {{ }} variables (substitutePatterns renames it per
-                              // row, jsonutils/traverse.go:90-117): w = the key's template leaf
-                              // (PL_VAR / PL_TMPL; bval 1: under ExpandInMetadata; pad[0] = template-
-                              // text offset of the map's other plain keys in walk order, [u16 length]
-                              // [bytes] each; pad[1] = their count | this key's place << 16)
+#define PMF_VKEY (1u << 14)   // a key with {{ }} variables (substitutePatterns renames it per row,
+                              // jsonutils/traverse.go:90-117): w = the key's template leaf (PL_VAR /
+                              // PL_TMPL; bval bit 0: under ExpandInMetadata, bit 1: the map has other
+                              // keys with variables (PVF_GROUP), bit 2: an anchored key, the template
+                              // being the whole written key and pad[2] = the anchor text's lengths
+                              // before | after the key << 16; pad[0] = template-text offset of the
+                              // map's other plain keys (anchored: its other phase-1 anchor keys) in
+                              // walk order, [u16 length][bytes] each; pad[1] = their count | this
+                              // key's place << 16)
 // Leaf
 #define PL_BOOL 0u
 #define PL_INT 1u
