@@ -1616,6 +1616,9 @@ int64_t Corpus::bytes() const {
 namespace {
 
 void flatten_range(Corpus& C, const char* buf, size_t i, size_t len, bool docs) {
+  // resource names are mostly distinct: size their dictionary for the range up front (one row per
+  // ~400 bytes at most), so it does not rehash every name at each doubling
+  if (C.dict[D_NAME].size() == 0) C.dict[D_NAME].reserve(std::min<size_t>((len - i) / 400 + 64, (size_t)1 << 24));
   Flattener fl(C);
   fl.check_images = !docs;
   std::unique_ptr<DocBuilder> db;
