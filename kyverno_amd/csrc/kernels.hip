@@ -1342,6 +1342,7 @@ __global__ void __launch_bounds__(KPE_PAT_BLOCK, KPE_PAT_MINW) kpe_pattern_kerne
 template <bool LT>
 __global__ void __launch_bounds__(64) kpe_pattern_deep_kernel(const PatArgs* __restrict__ ap) {
   __shared__ uint32_t s_fs[FramesLdsDeep::kWords * FramesLdsDeep::kDepth * 64u];
+  if (ap->deep_any && *ap->deep_any == 0u) return;  // kpe_pattern_kernel marked no cell
   const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
   if (i >= ap->n) return;
   // rows through doc_perm (grouped by kind, then tape size) like the main kernel: the rows with deep

@@ -333,6 +333,9 @@ struct PatArgs {
   // memo slot s's representative pattern rule (any rule of the slot: they share the pattern), or
   // ~0u for an unused slot; kpe_pattern_kernel evaluates a row's slots in slot order
   uint32_t slot_rule[KPE_PAT_MEMO];
+  // set to 1 by kpe_pattern_kernel when it marks a cell KPE_DEEP_ (cleared before every launch);
+  // kpe_pattern_deep_kernel returns at once while it is 0 (no 1-byte-per-cell rescan); null: none
+  uint32_t* deep_any;
 };
 
 // kpe_cond_kernel arguments (device-resident, one copy per binding)

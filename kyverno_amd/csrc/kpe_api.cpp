@@ -211,7 +211,8 @@ struct Binding {  // program x corpus (dictionary sizes decide predicate placeme
   DevBuf zero_page;    // 256 zero bytes (loads of columns a program does not read)
   DevBuf fuse;         // fused dictionary pass image (pairs, patterns, small dictionaries)
   uint32_t fuse_lds = 0, fuse_words = 0, npairs = 0, fuse_pats = 0, fuse_patb = 0;
-  DevBuf pmembers, pargs, perr;  // pattern rules: resolved members, PatArgs copy, check flags
+  DevBuf pmembers, pargs, perr, pdeep;  // pattern rules: resolved members, PatArgs copy, check flags,
+                                        // PatArgs::deep_any
   bool pargs_valid = false;
   DevBuf pvals;  // pattern variables: per-row values (kpe_cond_kernel -> kpe_pattern_kernel)
   DevBuf cfkeys, cargs;  // condition rules: resolved field names, CondArgs copy
@@ -1675,6 +1676,8 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
       PCHK(B.perr.ensure(4));
       PCHK(hipMemsetAsync(B.perr.p, 0, 4, s));
       pa.err = B.perr.as<uint32_t>();
+      PCHK(B.pdeep.ensure(4));
+      pa.deep_any = B.pdeep.as<uint32_t>();
       PCHK(B.pargs.ensure(sizeof(PatArgs)));
       PCHK(hipMemcpyAsync(B.pargs.p, &pa, sizeof(PatArgs), hipMemcpyHostToDevice, s));
       PCHK(hipStreamSynchronize(s));
@@ -1788,6 +1791,7 @@ kpe_status launch(kpe_device* dev, const kpe_program* pp, kpe_corpus* cc, bool m
   }
   if (!P.pat.rules.empty()) {
     HIPCHK(ensure_pargs());
+    HIPCHK(hipMemsetAsync(B.pdeep.p, 0, 4, s));  // PatArgs::deep_any
     HIPCHK(kpe_launch_pattern(B.pargs.as<PatArgs>(), C.n, (uint32_t)P.pat.rules.size(), PD.ltab_all ? 1 : 0, s));
     if (dev->patvm_err) {  // bounds flags of a KPE_PATVM_CHECK build (scripts/pvchk.py)
       uint32_t e = 0;

@@ -1071,6 +1071,7 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
       if (FS::kDepth < kPatStack && v == KPE_UNDECIDED_) {
         if constexpr (DEFER) {
           v = KPE_DEEP_;  // every cell of the slot goes to kpe_pattern_deep_kernel
+        if (a.deep_any) a.deep_any[0] = 1u;
         } else {
           PatVMT<FramesPriv, LT> deep{a, vm.doc, vm.root, vm.pv, 0u};
           v = pat_eval_cell(deep, a.slot_rule[s]);
@@ -1099,6 +1100,7 @@ __device__ __forceinline__ void pat_eval_row(const PatArgs& a, int64_t r, FS fs,
         // a shallow (LDS) stack may have overflowed: the lane-private kPatStack-deep one decides
         if constexpr (DEFER) {
           row[cq] = (uint8_t)KPE_DEEP_;
+          if (a.deep_any) a.deep_any[0] = 1u;
           continue;
         } else {
           PatVMT<FramesPriv, LT> deep{a, vm.doc, vm.root, vm.pv, 0u};
