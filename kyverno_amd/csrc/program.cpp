@@ -2240,16 +2240,31 @@ class Lowerer {
         } else if (kind_only) {
           push({T_KIND_PRED, (uint32_t)pred(D_KIND, kpats), 0, 0});
         } else {
-          uint32_t k0 = (uint32_t)P.kindsels.size();
+          std::vector<KpeKindSel> run;
           for (auto& s : sels) {
-            KpeKindSel ks;
+            KpeKindSel ks{};
             ks.pg = s.g == "*" ? -1 : pred(D_GROUP, {s.g});
             ks.pv = s.v == "*" ? -1 : pred(D_VERSION, {s.v});
             ks.pk = s.k == "*" ? -1 : pred(D_KIND, {s.k});
             ks.sub_ok = glob_host(s.sub, "") ? 1u : 0u;
-            P.kindsels.push_back(ks);
+            run.push_back(ks);
           }
-          push({T_KINDS, k0, (uint32_t)kinds.size(), 0});
+          // an identical selector list already in the table is reused, so filters with the same
+          // kinds share one term (C3's 200 policies draw their kinds from 15 lists)
+          auto same = [](const KpeKindSel& x, const KpeKindSel& y) {
+            return x.pg == y.pg && x.pv == y.pv && x.pk == y.pk && x.sub_ok == y.sub_ok;
+          };
+          uint32_t k0 = (uint32_t)P.kindsels.size();
+          for (size_t i = 0; i + run.size() <= P.kindsels.size(); ++i) {
+            size_t j = 0;
+            while (j < run.size() && same(P.kindsels[i + j], run[j])) ++j;
+            if (j == run.size()) {
+              k0 = (uint32_t)i;
+              break;
+            }
+          }
+          if (k0 == (uint32_t)P.kindsels.size()) P.kindsels.insert(P.kindsels.end(), run.begin(), run.end());
+          push({T_KINDS, k0, (uint32_t)run.size(), 0});
         }
       }
       std::string name = sv(rd->get("name"));
