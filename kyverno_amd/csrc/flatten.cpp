@@ -1042,15 +1042,16 @@ class Flattener {
   void emit(uint32_t cls, bool derr) {
     if (C.n >= 0x7FFFFFC0) throw LimitError("more than 2^31 - 64 resources in one corpus (32-bit row ids)");
     // ---- resource row (unstructured view) ----
-    std::string group, version;
-    size_t sl = u.api_version.find('/');
-    if (sl == std::string::npos) version = u.api_version;
+    std::string_view group, version;  // views into u.api_version
+    const std::string_view av = u.api_version;
+    const size_t sl = av.find('/');
+    if (sl == std::string_view::npos) version = av;
     else {
-      group = u.api_version.substr(0, sl);
-      version = u.api_version.substr(sl + 1);
+      group = av.substr(0, sl);
+      version = av.substr(sl + 1);
     }
     bool limit = false;  // a per-resource limit: the row is kept, its cells are undecided
-    auto small_id = [&](int d, const std::string& v, uint32_t cap) -> uint32_t {
+    auto small_id = [&](int d, std::string_view v, uint32_t cap) -> uint32_t {
       const int64_t id = C.dict[d].find(v);
       if (id >= 0) return (uint32_t)id;
       if (C.dict[d].size() >= cap) return limit = true, 0u;
